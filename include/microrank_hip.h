@@ -1,0 +1,184 @@
+/*
+ * microrank_hip.h -- C-ABI of libmicrorank_hip.so, the MI355X (gfx950) implementation of
+ * MicroRank's ranking hot path.  Plain pointers and sizes only; every entry point returns
+ * an MR_* status (0 = ok) and mr_last_error(ctx) describes the failure.
+ *
+ * Each entry point names the reference interface it replaces (file:line in
+ * CUHK-SE-Group/MicroRank @ 2025-02-14).  The Python drop-in modules in
+ * microrank_amd/ (pagerank.py, preprocess_data.py, anormaly_detector.py, online_rca.py)
+ * bind these with ctypes; INTEGRATION.md shows the binding a maintainer would add.
+ *
+ * Conventions
+ *   - "host" pointers are caller-owned CPU memory, copied in/out inside the call.
+ *   - "device" handles (mr_graph, mr_spans) own HBM; they belong to one mr_ctx.
+ *   - Node order, trace order and every tie-break follow the reference.
+ *   - Calls on distinct contexts are thread-safe; one context is not re-entrant.
+ */
+#ifndef MICRORANK_HIP_H
+#define MICRORANK_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes (the Python layer maps them onto the reference's exception types) ---- */
+enum {
+    MR_OK = 0,
+    MR_ERR_ARG = 1,       /* bad argument / shape                        -> ValueError/TypeError */
+    MR_ERR_HIP = 2,       /* HIP runtime failure                          -> RuntimeError */
+    MR_ERR_VALUE = 3,     /* reference raises ValueError (empty graph, list.index miss) */
+    MR_ERR_ZERODIV = 4,   /* reference raises ZeroDivisionError (1.0/len of an empty pr list) */
+    MR_ERR_OOM = 5,       /* device allocation failed */
+    MR_ERR_COMM = 6,      /* RCCL failure */
+    MR_ERR_STATE = 7      /* handle used with the wrong context / before setup */
+};
+
+enum { MR_FP64 = 0, MR_FP32 = 1 };      /* precision of the rank vectors */
+
+/* mr_pagerank flags */
+enum {
+    MR_PR_EXACT_SUMS = 1u   /* sequential fp64 sums in reference order for the one-time scalars
+                               (pagerank.py:71-78, 95-96; T7) instead of a fixed-order tree */
+};
+
+typedef struct mr_ctx mr_ctx;
+typedef struct mr_graph mr_graph;
+typedef struct mr_spans mr_spans;
+
+/* ------------------------------------------------------------------ context */
+int         mr_version(void);
+int         mr_device_count(int* n);
+int         mr_ctx_create(int device, uint32_t flags, mr_ctx** out);
+void        mr_ctx_destroy(mr_ctx* ctx);
+const char* mr_last_error(const mr_ctx* ctx);
+int         mr_ctx_sync(mr_ctx* ctx);
+/* stream the context launches on (a hipStream_t), for callers that time with HIP events */
+void*       mr_ctx_stream(mr_ctx* ctx);
+
+/* ------------------------------------------------------------------ graph from index arrays
+ * Replaces the dense matrix fill of pagerank.trace_pagerank (pagerank.py:16-52): the four
+ * dicts become incidence lists.  Node ids follow the operation_operation key order, trace
+ * ids the operation_trace key order.
+ */
+typedef struct mr_graph_desc {
+    int32_t n_nodes;          /* N = len(operation_operation)                        */
+    int32_t n_traces;         /* T = len(operation_trace)                            */
+    int64_t nnz_sr;           /* distinct (trace, op) pairs of P_sr                  */
+    const int64_t* sr_off;    /* [T+1] trace-major P_sr incidence (op in operation_trace[t]) */
+    const int32_t* sr_ops;    /* [nnz_sr] node ids, ascending within a trace          */
+    int64_t nnz_rs;           /* distinct pairs of P_rs; 0 with rs_* NULL = same as sr */
+    const int64_t* rs_off;    /* [T+1] trace-major P_rs incidence (t in trace_operation[o]) */
+    const int32_t* rs_ops;
+    const int32_t* len_t;     /* [T] len(operation_trace[t])  -> P_sr value fp32(1/len_t) */
+    const int32_t* len_o;     /* [N] len(trace_operation[o])  -> P_rs value fp32(1/len_o) */
+    int64_t n_edges;          /* distinct (child, parent) pairs of P_ss               */
+    const int64_t* ss_off;    /* [N+1] by child                                       */
+    const int32_t* ss_par;    /* [n_edges] parent node ids, ascending within a child   */
+    const int32_t* nchild;    /* [N] len(operation_operation[p]) -> P_ss value fp32(1/nchild) */
+    int32_t n_pr;             /* len(pr_trace)                                        */
+    const int32_t* pr_trace;  /* [n_pr] trace id of each pr_trace key, in pr_trace order */
+    const int32_t* pr_len;    /* [n_pr] len(pr_trace[key])                            */
+} mr_graph_desc;
+
+int mr_graph_upload(mr_ctx* ctx, const mr_graph_desc* desc, mr_graph** out);
+int mr_graph_free(mr_graph* g);
+int mr_graph_info(const mr_graph* g, int32_t* n_nodes, int32_t* n_traces, int64_t* nnz,
+                  int64_t* n_edges);
+
+/* ------------------------------------------------------------------ K2: personalised PageRank
+ * pagerank.trace_pagerank (pagerank.py:15-112) + pageRank (pagerank.py:116-130):
+ * kinds (:54-66), preference vector (:68-85), `iters` Jacobi power iterations with max
+ * normalisation (:121-129), weight = s*sum(s)/N and trace coverage (:93-107).
+ * Results stay on the device; mr_graph_fetch copies them out.
+ */
+int mr_pagerank(mr_ctx* ctx, mr_graph* g, int anomaly, double d, double alpha, int iters,
+                int precision, uint32_t flags);
+int mr_graph_fetch(mr_graph* g, double* weight /*[N] host*/, int32_t* coverage /*[N] host*/,
+                   double* kind /*[T] host or NULL*/, float* pref /*[T] host or NULL*/);
+
+/* ------------------------------------------------------------------ spans (int-coded columns)
+ * The DataFrame of online_rca.py:377-404 after factorisation (microrank_amd/spans.py).
+ */
+typedef struct mr_span_cols {
+    int64_t n_spans;
+    int32_t n_traces, n_podops, n_svcops;
+    const int32_t* trace;     /* trace code (rank of traceID in sorted order)       */
+    const int32_t* podop;     /* podName_op code (sorted name order)                */
+    const int32_t* svcop;     /* serviceName_op code (sorted name order)            */
+    const int64_t* span;      /* spanID code                                        */
+    const int64_t* parent;    /* ParentSpanId as a spanID code, -1 if absent        */
+    const int64_t* duration;  /* span duration (reference units)                   */
+    const int64_t* tstart;    /* trace-level start, ns (NULL if absent)             */
+    const int64_t* tend;      /* trace-level end, ns                                */
+} mr_span_cols;
+
+int mr_spans_upload(mr_ctx* ctx, const mr_span_cols* cols, mr_spans** out);
+int mr_spans_free(mr_spans* s);
+
+/* K1: preprocess_data.get_pagerank_graph (preprocess_data.py:358-383) on the device.
+ * trace_mask[n_traces] (host, 0/1) selects the trace_list.  Node order = sorted parent ops,
+ * then never-parent ops in first-appearance row order (T10).  The parent join ignores
+ * traceID (T11). */
+int mr_graph_build(mr_ctx* ctx, const mr_spans* s, const uint8_t* trace_mask, mr_graph** out);
+/* node order (podop codes) and trace codes of a built graph */
+int mr_graph_nodes(const mr_graph* g, int32_t* node_podop /*[N]*/, int32_t* trace_code /*[T]*/);
+/* structure export for parity tests: any pointer may be NULL */
+int mr_graph_export(const mr_graph* g, int64_t* sr_off /*[T+1]*/, int32_t* sr_ops /*[nnz]*/,
+                    int32_t* len_t /*[T]*/, int32_t* len_o /*[N]*/, int64_t* ss_off /*[N+1]*/,
+                    int32_t* ss_par /*[E]*/, int32_t* nchild /*[N]*/);
+
+/* ------------------------------------------------------------------ K3: spectrum + top-k
+ * online_rca.calculate_spectrum_without_delay_list (online_rca.py:189-308).  Inputs are in the
+ * reference's iteration order: the anomaly_result nodes first, then normal-only nodes.
+ * has_a/has_n mark membership; method is an index into
+ * {dstar2, ochiai, jaccard, sorensendice, m1, m2, goodman, tarantula, russellrao, hamann,
+ *  dice, simplematcing, rogers}.  Output: the first min(n, top) indices of the stable
+ * descending sort and their scores.  A division by zero sets *zerodiv (the reference
+ * raises ZeroDivisionError). */
+int mr_spectrum(mr_ctx* ctx, int32_t n, const uint8_t* has_a, const double* a_w, const int64_t* a_num,
+                const uint8_t* has_n, const double* n_w, const int64_t* n_num, int64_t a_len,
+                int64_t n_len, int method, int32_t top, int32_t* out_idx, double* out_score,
+                int32_t* n_out, int32_t* zerodiv);
+
+/* ------------------------------------------------------------------ K4: SLO
+ * preprocess_data.get_operation_slo (preprocess_data.py:262-290), the semantic body of the
+ * broken anormaly_detector.get_slo (anormaly_detector.py:22-27, T16): per svcop code,
+ * round(mean/1000, 4) and round(std/1000, 4) (population std, numpy pairwise order, T13).
+ * count[o] = 0 marks an op with no spans. */
+int mr_slo(mr_ctx* ctx, const mr_spans* s, double* mean /*[n_svcops]*/, double* std_ /*[n_svcops]*/,
+           int64_t* count /*[n_svcops]*/);
+
+/* ------------------------------------------------------------------ K5: detector
+ * anormaly_detector.system_anomaly_detect (anormaly_detector.py:44-84) with
+ * get_operation_duration_data (preprocess_data.py:309-334): window [t0, t1] on trace-level
+ * times (inclusive), real = max duration/1000, expect = sum over ops (sorted order) of
+ * count*a3[op] with a3 = mean+3*std, ops without SLO (a3_valid=0) contribute 0.
+ * state[n_traces] (host): 0 not in window / dropped, 1 normal, 2 abnormal.
+ * Returns MR_ERR_VALUE with *n_spans_in_window = 0 for an empty window (the reference
+ * returns False, T2). */
+int mr_detect(mr_ctx* ctx, const mr_spans* s, int64_t t0, int64_t t1, const double* a3,
+              const uint8_t* a3_valid, uint8_t* state, int32_t* n_abnormal, int32_t* n_normal,
+              int64_t* n_spans_in_window);
+
+/* ------------------------------------------------------------------ whole RCA window on device
+ * online_rca.online_anomaly_detect_RCA body for one window (online_rca.py:320-371):
+ * detect -> (swapped, T1) two graph builds -> two PageRanks -> spectrum -> top list, with
+ * all intermediates resident in HBM.  out_idx are podop codes. */
+int mr_rca_window(mr_ctx* ctx, const mr_spans* s, int64_t t0, int64_t t1, const double* a3,
+                  const uint8_t* a3_valid, int method, int32_t top_max, int precision,
+                  int32_t* out_podop, double* out_score, int32_t* n_out, int64_t* edges_traversed,
+                  int32_t* n_abnormal, int32_t* n_normal);
+
+/* ------------------------------------------------------------------ multi-GPU (RCCL over xGMI)
+ * One process per GPU.  The unique id (128 bytes) is produced by rank 0 and broadcast by the
+ * caller (torch.distributed / any host channel).  Used by the trace-sharded PageRank. */
+int mr_comm_unique_id(uint8_t id[128]);
+int mr_comm_init(mr_ctx* ctx, int nranks, int rank, const uint8_t id[128]);
+int mr_comm_allreduce_f64(mr_ctx* ctx, double* dev_buf, int64_t n, int op /*0 sum, 1 max*/);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MICRORANK_HIP_H */

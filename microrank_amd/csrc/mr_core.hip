@@ -1,0 +1,180 @@
+// Context, error reporting, graph upload from host index arrays, result fetch.
+#include <algorithm>
+#include <cstring>
+
+#include "mr_internal.h"
+#include "mr_prim.h"
+
+int mr_fail(mr_ctx* ctx, int code, const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    if (ctx) ctx->err = buf;
+    return code;
+}
+
+extern "C" int mr_version(void) { return 100; }
+
+extern "C" int mr_device_count(int* n) {
+    int c = 0;
+    hipError_t e = hipGetDeviceCount(&c);
+    if (e != hipSuccess) c = 0;
+    if (n) *n = c;
+    return MR_OK;
+}
+
+extern "C" int mr_ctx_create(int device, uint32_t flags, mr_ctx** out) {
+    if (!out) return MR_ERR_ARG;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return MR_ERR_HIP;
+    if (device < 0 || device >= n) return MR_ERR_ARG;
+    if (hipSetDevice(device) != hipSuccess) return MR_ERR_HIP;
+    auto* c = new mr_ctx();
+    c->device = device;
+    c->flags = flags;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return MR_ERR_HIP;
+    }
+    *out = c;
+    return MR_OK;
+}
+
+void mr_comm_destroy(mr_ctx* ctx);  // mr_comm.cpp
+
+extern "C" void mr_ctx_destroy(mr_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    mr_comm_destroy(ctx);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+extern "C" const char* mr_last_error(const mr_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+extern "C" int mr_ctx_sync(mr_ctx* ctx) {
+    if (!ctx) return MR_ERR_ARG;
+    MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return MR_OK;
+}
+
+extern "C" void* mr_ctx_stream(mr_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+// ------------------------------------------------------------------------------ upload
+extern "C" int mr_graph_upload(mr_ctx* ctx, const mr_graph_desc* d, mr_graph** out) {
+    if (!ctx || !d || !out) return mr_fail(ctx, MR_ERR_ARG, "mr_graph_upload: null argument");
+    *out = nullptr;
+    const int32_t N = d->n_nodes, T = d->n_traces;
+    if (N < 0 || T < 0) return mr_fail(ctx, MR_ERR_ARG, "negative sizes");
+    if (!d->sr_off || (d->nnz_sr && !d->sr_ops) || !d->len_t || !d->len_o || !d->ss_off || !d->nchild)
+        return mr_fail(ctx, MR_ERR_ARG, "mr_graph_upload: missing array");
+    if (d->sr_off[0] != 0 || d->sr_off[T] != d->nnz_sr)
+        return mr_fail(ctx, MR_ERR_ARG, "sr_off inconsistent with nnz_sr");
+    for (int64_t e = 0; e < d->nnz_sr; ++e)
+        if (d->sr_ops[e] < 0 || d->sr_ops[e] >= N) return mr_fail(ctx, MR_ERR_ARG, "sr_ops out of range");
+    if (d->ss_off[0] != 0 || d->ss_off[N] != d->n_edges)
+        return mr_fail(ctx, MR_ERR_ARG, "ss_off inconsistent with n_edges");
+    for (int64_t e = 0; e < d->n_edges; ++e)
+        if (d->ss_par[e] < 0 || d->ss_par[e] >= N) return mr_fail(ctx, MR_ERR_ARG, "ss_par out of range");
+    MR_TRY_HIP(ctx, hipSetDevice(ctx->device));
+    auto* g = new mr_graph();
+    g->ctx = ctx;
+    g->N = N;
+    g->T = T;
+    g->nnz_sr = d->nnz_sr;
+    g->E = d->n_edges;
+    g->rs_is_sr = d->rs_off == nullptr;
+    g->nnz_rs = g->rs_is_sr ? d->nnz_sr : d->nnz_rs;
+    int rc = MR_OK;
+    auto fail = [&](int code) {
+        delete g;
+        return code;
+    };
+    // op-major transpose of P_sr (stable: traces ascending within an op)
+    std::vector<int64_t> op_off((size_t)N + 1, 0);
+    for (int64_t e = 0; e < d->nnz_sr; ++e) op_off[(size_t)d->sr_ops[e] + 1]++;
+    for (int32_t o = 0; o < N; ++o) op_off[(size_t)o + 1] += op_off[(size_t)o];
+    std::vector<int32_t> op_trs((size_t)d->nnz_sr);
+    {
+        std::vector<int64_t> pos(op_off.begin(), op_off.end() - 1);
+        for (int32_t t = 0; t < T; ++t)
+            for (int64_t e = d->sr_off[t]; e < d->sr_off[t + 1]; ++e) op_trs[(size_t)pos[(size_t)d->sr_ops[e]]++] = t;
+    }
+    if ((rc = g->sr_off.upload(ctx, op_off.data(), op_off.size())) ||
+        (rc = g->sr_trs.upload(ctx, op_trs.data(), op_trs.size())) ||
+        (rc = g->len_t.upload(ctx, d->len_t, (size_t)T)) || (rc = g->len_o.upload(ctx, d->len_o, (size_t)N)) ||
+        (rc = g->ss_off.upload(ctx, d->ss_off, (size_t)N + 1)) ||
+        (rc = g->ss_par.upload(ctx, d->ss_par, (size_t)d->n_edges)) ||
+        (rc = g->nchild.upload(ctx, d->nchild, (size_t)N)))
+        return fail(rc);
+    if (g->rs_is_sr) {
+        if ((rc = g->rs_off.upload(ctx, d->sr_off, (size_t)T + 1)) ||
+            (rc = g->rs_ops.upload(ctx, d->sr_ops, (size_t)d->nnz_sr)))
+            return fail(rc);
+    } else {
+        if (!d->rs_ops || d->rs_off[0] != 0 || d->rs_off[T] != d->nnz_rs) return fail(mr_fail(ctx, MR_ERR_ARG, "rs arrays"));
+        for (int64_t e = 0; e < d->nnz_rs; ++e)
+            if (d->rs_ops[e] < 0 || d->rs_ops[e] >= N) return fail(mr_fail(ctx, MR_ERR_ARG, "rs_ops out of range"));
+        if ((rc = g->rs_off.upload(ctx, d->rs_off, (size_t)T + 1)) ||
+            (rc = g->rs_ops.upload(ctx, d->rs_ops, (size_t)d->nnz_rs)) ||
+            (rc = g->srt_off.upload(ctx, d->sr_off, (size_t)T + 1)) ||
+            (rc = g->srt_ops.upload(ctx, d->sr_ops, (size_t)d->nnz_sr)))
+            return fail(rc);
+    }
+    // pr_trace: identity when it is operation_trace itself (graph-builder output)
+    g->n_pr = d->n_pr;
+    bool ident = d->pr_trace == nullptr;
+    if (!ident && d->n_pr == T) {
+        ident = true;
+        for (int32_t i = 0; i < T && ident; ++i) ident = d->pr_trace[i] == i && d->pr_len[i] == d->len_t[i];
+    }
+    g->pr_identity = ident;
+    if (!ident) {
+        for (int32_t i = 0; i < d->n_pr; ++i)
+            if (d->pr_trace[i] < 0 || d->pr_trace[i] >= T) return fail(mr_fail(ctx, MR_ERR_ARG, "pr_trace out of range"));
+        if ((rc = g->pr_trace.upload(ctx, d->pr_trace, (size_t)d->n_pr)) ||
+            (rc = g->pr_len.upload(ctx, d->pr_len, (size_t)d->n_pr)))
+            return fail(rc);
+    } else {
+        g->n_pr = T;
+    }
+    if ((rc = mr_graph_prepare(ctx, g))) return fail(rc);
+    MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));  // host vectors go out of scope
+    *out = g;
+    return MR_OK;
+}
+
+extern "C" int mr_graph_free(mr_graph* g) {
+    if (!g) return MR_OK;
+    (void)hipSetDevice(g->ctx->device);
+    (void)hipStreamSynchronize(g->ctx->stream);
+    delete g;
+    return MR_OK;
+}
+
+extern "C" int mr_graph_info(const mr_graph* g, int32_t* n, int32_t* t, int64_t* nnz, int64_t* e) {
+    if (!g) return MR_ERR_ARG;
+    if (n) *n = g->N;
+    if (t) *t = g->T;
+    if (nnz) *nnz = g->nnz_sr;
+    if (e) *e = g->E;
+    return MR_OK;
+}
+
+extern "C" int mr_graph_fetch(mr_graph* g, double* weight, int32_t* cov, double* kind, float* pref) {
+    if (!g) return MR_ERR_ARG;
+    mr_ctx* ctx = g->ctx;
+    MR_TRY_HIP(ctx, hipSetDevice(ctx->device));
+    if (weight) {
+        if (!g->weight.p) return mr_fail(ctx, MR_ERR_STATE, "mr_graph_fetch: mr_pagerank has not run");
+        MR_TRY(g->weight.download(ctx, weight, (size_t)g->N));
+    }
+    if (cov) MR_TRY(g->cov.download(ctx, cov, (size_t)g->N));
+    if (kind && g->kind.p) MR_TRY(g->kind.download(ctx, kind, (size_t)g->T));
+    if (pref && g->pref.p) MR_TRY(g->pref.download(ctx, pref, (size_t)g->T));
+    MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return MR_OK;
+}

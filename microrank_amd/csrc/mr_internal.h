@@ -1,0 +1,146 @@
+// Internal state of libmicrorank_hip.so.  gfx950 only: 64-lane wavefronts, 160 KiB LDS/CU.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "../../include/microrank_hip.h"
+
+constexpr int WAVE = 64;
+
+struct mr_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    uint32_t flags = 0;
+    std::string err;
+    // RCCL (loaded lazily with dlopen so the library loads without it)
+    void* comm = nullptr;
+    int rank = 0, nranks = 1;
+};
+
+int mr_fail(mr_ctx* ctx, int code, const char* fmt, ...);
+
+#define MR_TRY_HIP(ctx, call)                                                                  \
+    do {                                                                                       \
+        hipError_t e_ = (call);                                                                \
+        if (e_ != hipSuccess)                                                                  \
+            return mr_fail((ctx), MR_ERR_HIP, "%s: %s (%s:%d)", #call, hipGetErrorString(e_),  \
+                           __FILE__, __LINE__);                                                \
+    } while (0)
+
+#define MR_TRY(expr)                \
+    do {                            \
+        int rc_ = (expr);           \
+        if (rc_ != MR_OK) return rc_; \
+    } while (0)
+
+// Owned device allocation.
+template <class T>
+struct DBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    DBuf() = default;
+    DBuf(const DBuf&) = delete;
+    DBuf& operator=(const DBuf&) = delete;
+    ~DBuf() { reset(); }
+    void reset() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    int alloc(mr_ctx* ctx, size_t count) {
+        if (count <= n && p) return MR_OK;
+        reset();
+        size_t bytes = (count ? count : 1) * sizeof(T);
+        hipError_t e = hipMalloc(&p, bytes);
+        if (e != hipSuccess) {
+            p = nullptr;
+            return mr_fail(ctx, MR_ERR_OOM, "hipMalloc(%zu bytes): %s", bytes, hipGetErrorString(e));
+        }
+        n = count;
+        return MR_OK;
+    }
+    int upload(mr_ctx* ctx, const T* host, size_t count) {
+        MR_TRY(alloc(ctx, count));
+        if (count)
+            MR_TRY_HIP(ctx, hipMemcpyAsync(p, host, count * sizeof(T), hipMemcpyHostToDevice, ctx->stream));
+        return MR_OK;
+    }
+    int download(mr_ctx* ctx, T* host, size_t count) const {
+        if (count)
+            MR_TRY_HIP(ctx, hipMemcpyAsync(host, p, count * sizeof(T), hipMemcpyDeviceToHost, ctx->stream));
+        return MR_OK;
+    }
+    int zero(mr_ctx* ctx, size_t count) {
+        MR_TRY(alloc(ctx, count));
+        if (count) MR_TRY_HIP(ctx, hipMemsetAsync(p, 0, count * sizeof(T), ctx->stream));
+        return MR_OK;
+    }
+};
+
+// Device graph: the four reference dicts as incidence lists.
+struct mr_graph {
+    mr_ctx* ctx = nullptr;
+    int32_t N = 0, T = 0;
+    int64_t nnz_sr = 0, nnz_rs = 0, E = 0;
+    bool rs_is_sr = true;
+    // trace-major P_rs incidence (r' pass) and P_sr incidence (kinds)
+    DBuf<int64_t> rs_off;
+    DBuf<int32_t> rs_ops;
+    DBuf<int64_t> srt_off;   // only when !rs_is_sr
+    DBuf<int32_t> srt_ops;
+    // op-major P_sr incidence (s' pass), split into fixed-size segments
+    DBuf<int64_t> sr_off;    // [N+1]
+    DBuf<int32_t> sr_trs;    // [nnz_sr]
+    int32_t nseg = 0;
+    DBuf<int32_t> seg_op;    // [nseg]
+    DBuf<int64_t> seg_beg;   // [nseg]
+    DBuf<int32_t> op_seg;    // [N+1] first segment of op
+    // per-trace / per-op constants
+    DBuf<int32_t> len_t, len_o, nchild, cov;
+    DBuf<float> w_t, u_o, pw;    // fp32(1/len_t), fp32(1/len_o), fp32(1/nchild)
+    DBuf<int64_t> ss_off;        // P_ss by child
+    DBuf<int32_t> ss_par;
+    int32_t n_pr = 0;
+    bool pr_identity = true;     // pr_trace keys == operation_trace keys in order
+    DBuf<int32_t> pr_trace, pr_len;
+    // node order / trace codes (graphs built from spans)
+    DBuf<int32_t> node_podop, trace_code;
+    // iteration state and outputs
+    DBuf<double> kind;           // [T]
+    DBuf<float> pref;            // [T] preference vector v (fp32, as the reference)
+    DBuf<float> c_t;             // [T] fp32((1-d) * v)
+    DBuf<double> q64[2];         // [T] w_t * r'_t (fp64 mode)
+    DBuf<float> q32[2];          // [T] (fp32 mode)
+    DBuf<double> part;           // [nseg] segment partial sums of the s' pass
+    DBuf<double> bmax;           // [n trace-pass blocks] block maxima of r'
+    DBuf<double> sn, su, sp;     // [N] normalised s, u_o*s, unnormalised s'
+    DBuf<double> scal;           // [8] M_s, M_r, sums
+    DBuf<double> weight;         // [N]
+    DBuf<uint64_t> ht_key;       // kinds hash table
+    DBuf<uint32_t> ht_cnt;
+    DBuf<int32_t> ht_rep, slot_of;
+    DBuf<int32_t> flag;          // [4] error flags written by kernels
+};
+
+struct mr_spans {
+    mr_ctx* ctx = nullptr;
+    int64_t S = 0;
+    int32_t n_traces = 0, n_podops = 0, n_svcops = 0;
+    DBuf<int32_t> trace, podop, svcop;
+    DBuf<int64_t> span, parent, duration, tstart, tend;
+    bool has_times = false;
+    // spanID -> rows multimap over the whole table (static; built at upload)
+    int64_t n_span_codes = 0;
+    DBuf<int64_t> id_off;   // [n_span_codes+1]
+    DBuf<int32_t> id_rows;  // [S]
+};
+
+// Launch helpers
+inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
+
+int mr_graph_prepare(mr_ctx* ctx, mr_graph* g);   // derived arrays + segments after structure upload

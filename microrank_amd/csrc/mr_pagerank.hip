@@ -1,0 +1,423 @@
+// K2: personalised PageRank of pagerank.trace_pagerank (pagerank.py:15-130) on gfx950.
+//
+// Sparse, HBM-bound: no MFMA.  Per Jacobi iteration k (T8) two block roles share ONE launch:
+//   trace role  r'_{k+1}[t] = d * sum_{o in rs(t)} u_o * s_k[o] + fp32((1-d) v_t)   (pagerank.py:125)
+//               q'_{k+1}[t] = w_t * r'_{k+1}[t]                                      (P_sr weight, kept for s')
+//               s_k*u lives in LDS (su), one thread per trace, sequential in node order
+//   op role     part[seg]   = sum_{t in segment of sr(o)} q'_k[t]                    (pagerank.py:123)
+//               one wave per fixed 1024-entry segment of an op's trace list, fixed butterfly
+// then a one-block finish kernel:
+//   s'_{k+1}[o] = d * (sum_seg part / M_r(k) + alpha * sum_{p in ss(o)} pw_p * s_k[p])
+//   M_s = max s', s_{k+1} = s'/M_s, M_r(k+1) = max over trace-role block maxima   (pagerank.py:126-127)
+// Normalisation of r is deferred: sum_t w_t (r'_t / M_r) is computed as (sum_t w_t r'_t) / M_r.
+// Every reduction has a fixed order, so results are bitwise reproducible (no float atomics).
+#include <cmath>
+
+#include "mr_internal.h"
+#include "mr_prim.h"
+
+namespace {
+
+constexpr int SEG = 1024;           // op-list segment length (entries)
+constexpr int TB = 256;             // trace-role block size (one trace per thread)
+constexpr int OPB = 256;            // op-role block size (4 waves, one segment per wave)
+constexpr int LDS_NODES = 8192;     // su staged in LDS up to this many nodes (64 KiB)
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+// ---------------------------------------------------------------- graph constants
+__global__ void k_trace_consts(const int32_t* len_t, float* w_t, int32_t T) {
+    int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < T) w_t[t] = len_t[t] > 0 ? (float)(1.0 / (double)len_t[t]) : 0.0f;   // fp64 1/n -> fp32
+}
+
+__global__ void k_op_consts(const int32_t* len_o, const int32_t* nchild, const int64_t* sr_off,
+                            float* u_o, float* pw, int32_t* cov, int32_t* nseg_of, int32_t N) {
+    int32_t o = blockIdx.x * blockDim.x + threadIdx.x;
+    if (o >= N) return;
+    u_o[o] = len_o[o] > 0 ? (float)(1.0 / (double)len_o[o]) : 0.0f;
+    pw[o] = nchild[o] > 0 ? (float)(1.0 / (double)nchild[o]) : 0.0f;
+    int64_t c = sr_off[o + 1] - sr_off[o];
+    cov[o] = (int32_t)c;                                  // trace_num_list (pagerank.py:98-104)
+    nseg_of[o] = (int32_t)((c + SEG - 1) / SEG);
+}
+
+__global__ void k_fill_segments(const int64_t* op_seg64, const int64_t* sr_off, int32_t* op_seg,
+                                int32_t* seg_op, int64_t* seg_beg, int32_t N) {
+    int32_t o = blockIdx.x * blockDim.x + threadIdx.x;
+    if (o > N) return;
+    op_seg[o] = (int32_t)op_seg64[o];
+    if (o == N) return;
+    int64_t s0 = op_seg64[o], s1 = op_seg64[o + 1];
+    for (int64_t s = s0; s < s1; ++s) {
+        seg_op[s] = o;
+        seg_beg[s] = sr_off[o] + (s - s0) * SEG;
+    }
+}
+
+// ---------------------------------------------------------------- kinds (pagerank.py:54-66)
+// kind[t] = size of the class of traces with an equal P_sr column: key = (op set, fp32(1/len_t)).
+// Open-addressing hash table of 64-bit keys; a second pass verifies every member against the
+// slot's representative, so a hash collision is detected (flag) rather than miscounted.
+__global__ void k_kind_insert(const int64_t* off, const int32_t* ops, const float* w_t, int32_t T,
+                              uint64_t* keys, uint32_t* cnt, int32_t* rep, int32_t* slot_of,
+                              uint64_t mask, uint64_t seed) {
+    int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= T) return;
+    int64_t e0 = off[t], e1 = off[t + 1];
+    uint32_t wb = e1 > e0 ? __float_as_uint(w_t[t]) : 0u;
+    uint64_t h = mix64(seed ^ (uint64_t)wb);
+    for (int64_t e = e0; e < e1; ++e) h = mix64(h ^ (uint64_t)(uint32_t)ops[e]);
+    if (h == 0) h = 1;
+    uint64_t slot = h & mask;
+    for (;;) {
+        uint64_t k = atomicCAS((unsigned long long*)&keys[slot], 0ull, (unsigned long long)h);
+        if (k == 0 || k == h) break;
+        slot = (slot + 1) & mask;
+    }
+    atomicAdd(&cnt[slot], 1u);
+    atomicCAS(&rep[slot], -1, t);
+    slot_of[t] = (int32_t)slot;
+}
+
+__global__ void k_kind_verify(const int64_t* off, const int32_t* ops, const float* w_t, int32_t T,
+                              const uint32_t* cnt, const int32_t* rep, const int32_t* slot_of,
+                              double* kind, int32_t* flag) {
+    int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= T) return;
+    int32_t s = slot_of[t];
+    int32_t r = rep[s];
+    kind[t] = (double)cnt[s];
+    if (r == t) return;
+    int64_t a0 = off[t], a1 = off[t + 1], b0 = off[r], b1 = off[r + 1];
+    bool eq = (a1 - a0) == (b1 - b0);
+    if (eq && a1 > a0) eq = __float_as_uint(w_t[t]) == __float_as_uint(w_t[r]);
+    for (int64_t i = 0; eq && i < a1 - a0; ++i) eq = ops[a0 + i] == ops[b0 + i];
+    if (!eq) atomicOr(flag, 1);
+}
+
+// ---------------------------------------------------------------- preference (pagerank.py:68-85)
+// sums over pr_trace entries: [0] sum 1/k, [1] sum 1/len; block partials then one fixed-order pass
+__global__ void k_pref_partial(const double* kind, const int32_t* pr_trace, const int32_t* pr_len,
+                               const int32_t* len_t, int32_t n_pr, double* part, int32_t* flag) {
+    __shared__ double red[TB / WAVE];
+    double a = 0.0, b = 0.0;
+    int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n_pr) {
+        int32_t t = pr_trace ? pr_trace[i] : i;
+        int32_t ln = pr_len ? pr_len[i] : len_t[t];
+        a = 1.0 / kind[t];
+        if (ln == 0) atomicOr(flag, 2);   // 1.0/len(pr_trace[t]) -> ZeroDivisionError
+        b = ln ? 1.0 / (double)ln : 0.0;
+    }
+    a = block_sum(a, red);
+    b = block_sum(b, red);
+    if (threadIdx.x == 0) {
+        part[2 * blockIdx.x] = a;
+        part[2 * blockIdx.x + 1] = b;
+    }
+}
+
+__global__ void k_pref_total(const double* part, int32_t nb, double* scal) {
+    __shared__ double red[1024 / WAVE];
+    double a = 0.0, b = 0.0;
+    for (int32_t i = threadIdx.x; i < nb; i += blockDim.x) {
+        a += part[2 * i];
+        b += part[2 * i + 1];
+    }
+    a = block_sum(a, red);
+    b = block_sum(b, red);
+    if (threadIdx.x == 0) {
+        scal[2] = a;
+        scal[3] = b;
+    }
+}
+
+// reference order, one thread (MR_PR_EXACT_SUMS, T7)
+__global__ void k_pref_total_exact(const double* kind, const int32_t* pr_trace, const int32_t* pr_len,
+                                   const int32_t* len_t, int32_t n_pr, double* scal) {
+    if (threadIdx.x || blockIdx.x) return;
+    double a = 0.0, b = 0.0;
+    for (int32_t i = 0; i < n_pr; ++i) {
+        int32_t t = pr_trace ? pr_trace[i] : i;
+        int32_t ln = pr_len ? pr_len[i] : len_t[t];
+        a += 1.0 / kind[t];
+        b += ln ? 1.0 / (double)ln : 0.0;
+    }
+    scal[2] = a;
+    scal[3] = b;
+}
+
+__global__ void k_pref_apply(const double* kind, const int32_t* pr_trace, const int32_t* pr_len,
+                             const int32_t* len_t, int32_t n_pr, const double* scal, int anomaly,
+                             float cd, float* pref, float* c_t) {
+    int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_pr) return;
+    int32_t t = pr_trace ? pr_trace[i] : i;
+    int32_t ln = pr_len ? pr_len[i] : len_t[t];
+    double k = kind[t];
+    double v;
+    if (!anomaly) {
+        v = 1.0 / k / scal[2];                                               // :74
+    } else {
+        v = 1.0 / (k / scal[2] * 0.5 + 1.0 / (double)ln) / scal[3] * 0.5;   // :80-85
+    }
+    float vf = (float)v;
+    pref[t] = vf;
+    c_t[t] = cd * vf;   // (1.0 - d) * v: float32 array times a Python float stays float32 (T4)
+}
+
+// ---------------------------------------------------------------- iteration
+__global__ void k_iter_init(const float* u_o, const float* w_t, int32_t N, int32_t T, double* sn,
+                            double* su, double* q64, float* q32, int fp32, double* scal) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const double v0 = 1.0 / (double)(N + T);                   // pagerank.py:118-119
+    if (i < N) {
+        sn[i] = v0;
+        su[i] = (double)u_o[i] * v0;
+    }
+    if (i < T) {
+        double q = (double)w_t[i] * v0;
+        if (fp32) q32[i] = (float)q; else q64[i] = q;
+    }
+    if (i == 0) {
+        scal[0] = 1.0;   // M_s(0): s_0 is used unnormalised
+        scal[1] = 1.0;   // M_r(0)
+    }
+}
+
+template <class Q>
+__global__ void __launch_bounds__(TB) k_iter_pass(
+    // trace role
+    const int64_t* __restrict__ rs_off, const int32_t* __restrict__ rs_ops, const double* __restrict__ su,
+    const float* __restrict__ c_t, const float* __restrict__ w_t, Q* __restrict__ q_next,
+    double* __restrict__ bmax, int32_t T, int32_t N, int32_t n_tblocks, double d, int lds_su,
+    // op role
+    const int64_t* __restrict__ sr_off, const int32_t* __restrict__ sr_trs, const int32_t* __restrict__ seg_op,
+    const int64_t* __restrict__ seg_beg, const Q* __restrict__ q_cur, double* __restrict__ part, int32_t nseg) {
+    extern __shared__ double lds[];
+    if ((int32_t)blockIdx.x < n_tblocks) {
+        const double* s = su;
+        if (lds_su) {
+            for (int32_t o = threadIdx.x; o < N; o += TB) lds[o] = su[o];
+            __syncthreads();
+            s = lds;
+        }
+        int32_t t = blockIdx.x * TB + threadIdx.x;
+        double rp = -__builtin_huge_val();
+        if (t < T) {
+            double acc = 0.0;
+            const int64_t e1 = rs_off[t + 1];
+            for (int64_t e = rs_off[t]; e < e1; ++e) acc += s[rs_ops[e]];
+            rp = d * acc + (double)c_t[t];
+            q_next[t] = (Q)((double)w_t[t] * rp);
+        }
+        __shared__ double red[TB / WAVE];
+        rp = block_max(rp, red);
+        if (threadIdx.x == 0) bmax[blockIdx.x] = rp;
+        return;
+    }
+    // op role: one wave per segment
+    const int32_t seg = ((int32_t)blockIdx.x - n_tblocks) * (OPB / WAVE) + (int32_t)(threadIdx.x / WAVE);
+    if (seg >= nseg) return;
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int32_t o = seg_op[seg];
+    const int64_t b = seg_beg[seg];
+    const int64_t end = min(b + (int64_t)SEG, sr_off[o + 1]);
+    double acc = 0.0;
+    for (int64_t e = b + lane; e < end; e += WAVE) acc += (double)q_cur[sr_trs[e]];
+    acc = wave_sum(acc);
+    if (lane == 0) part[seg] = acc;
+}
+
+// one block: finish s'_{k+1}, both maxima, normalised s and u*s for the next pass
+__global__ void __launch_bounds__(1024) k_iter_finish(
+    const double* part, const int32_t* op_seg, const int64_t* ss_off, const int32_t* ss_par,
+    const float* pw, const float* u_o, const double* bmax, int32_t n_tblocks, int32_t N, double d,
+    double alpha, double* sp, double* sn, double* su, double* scal) {
+    __shared__ double red[1024 / WAVE];
+    const double Mr = scal[1];
+    double m = -__builtin_huge_val();
+    for (int32_t o = threadIdx.x; o < N; o += blockDim.x) {
+        double a = 0.0;
+        for (int32_t s = op_seg[o]; s < op_seg[o + 1]; ++s) a += part[s];
+        double b = 0.0;
+        for (int64_t e = ss_off[o]; e < ss_off[o + 1]; ++e) {
+            int32_t p = ss_par[e];
+            b += (double)pw[p] * sn[p];
+        }
+        double v = d * (a / Mr + alpha * b);     // pagerank.py:122-124
+        sp[o] = v;
+        m = nmax(m, v);
+    }
+    const double Ms = block_max(m, red);         // includes a __syncthreads: every sn read is done
+    double mr = -__builtin_huge_val();
+    for (int32_t i = threadIdx.x; i < n_tblocks; i += blockDim.x) mr = nmax(mr, bmax[i]);
+    mr = block_max(mr, red);
+    for (int32_t o = threadIdx.x; o < N; o += blockDim.x) {
+        double s = sp[o] / Ms;                   // pagerank.py:126
+        sn[o] = s;
+        su[o] = (double)u_o[o] * s;
+    }
+    if (threadIdx.x == 0) {
+        scal[0] = Ms;
+        scal[1] = mr;                            // M_r(k+1), used by the next finish
+    }
+}
+
+// weight = s * sum(s) / N (pagerank.py:93-107); the final s is already max-normalised (:129)
+__global__ void __launch_bounds__(1024) k_weights(const double* sn, int32_t N, int exact, double* weight,
+                                                  double* scal) {
+    __shared__ double red[1024 / WAVE];
+    __shared__ double tot;
+    if (exact) {
+        if (threadIdx.x == 0) {
+            double s = 0.0;
+            for (int32_t o = 0; o < N; ++o) s += sn[o];
+            tot = s;
+        }
+        __syncthreads();
+    } else {
+        // fixed-order: contiguous chunk per thread, then block tree
+        int32_t per = (N + blockDim.x - 1) / blockDim.x;
+        int32_t a = threadIdx.x * per, b = min(a + per, N);
+        double s = 0.0;
+        for (int32_t o = a; o < b; ++o) s += sn[o];
+        s = block_sum(s, red);
+        if (threadIdx.x == 0) tot = s;
+        __syncthreads();
+    }
+    const double total = tot;
+    for (int32_t o = threadIdx.x; o < N; o += blockDim.x) weight[o] = sn[o] * total / (double)N;
+    if (threadIdx.x == 0) scal[4] = total;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------ host side
+int mr_graph_prepare(mr_ctx* ctx, mr_graph* g) {
+    const int32_t N = g->N, T = g->T;
+    MR_TRY(g->w_t.alloc(ctx, (size_t)T));
+    MR_TRY(g->u_o.alloc(ctx, (size_t)N));
+    MR_TRY(g->pw.alloc(ctx, (size_t)N));
+    MR_TRY(g->cov.alloc(ctx, (size_t)N));
+    DBuf<int32_t> nseg_of;
+    DBuf<int64_t> op_seg64, tmp;
+    MR_TRY(nseg_of.alloc(ctx, (size_t)N));
+    MR_TRY(op_seg64.alloc(ctx, (size_t)N + 1));
+    MR_TRY(tmp.alloc(ctx, (size_t)scan_tmp_elems(N)));
+    if (T) hipLaunchKernelGGL(k_trace_consts, dim3(cdiv(T, 256)), dim3(256), 0, ctx->stream, g->len_t.p, g->w_t.p, T);
+    if (N)
+        hipLaunchKernelGGL(k_op_consts, dim3(cdiv(N, 256)), dim3(256), 0, ctx->stream, g->len_o.p, g->nchild.p,
+                           g->sr_off.p, g->u_o.p, g->pw.p, g->cov.p, nseg_of.p, N);
+    MR_TRY(mr_exclusive_scan_i32(ctx, nseg_of.p, op_seg64.p, N, tmp.p));
+    int64_t nseg = 0;
+    MR_TRY_HIP(ctx, hipMemcpyAsync(&nseg, op_seg64.p + N, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+    MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    g->nseg = (int32_t)nseg;
+    MR_TRY(g->op_seg.alloc(ctx, (size_t)N + 1));
+    MR_TRY(g->seg_op.alloc(ctx, (size_t)nseg));
+    MR_TRY(g->seg_beg.alloc(ctx, (size_t)nseg));
+    hipLaunchKernelGGL(k_fill_segments, dim3(cdiv(N + 1, 256)), dim3(256), 0, ctx->stream, op_seg64.p, g->sr_off.p,
+                       g->op_seg.p, g->seg_op.p, g->seg_beg.p, N);
+    MR_TRY_HIP(ctx, hipGetLastError());
+    MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));  // scratch buffers die here
+    return MR_OK;
+}
+
+extern "C" int mr_pagerank(mr_ctx* ctx, mr_graph* g, int anomaly, double d, double alpha, int iters,
+                           int precision, uint32_t flags) {
+    if (!ctx || !g || g->ctx != ctx) return mr_fail(ctx, MR_ERR_STATE, "mr_pagerank: bad handles");
+    if (iters < 0) return mr_fail(ctx, MR_ERR_ARG, "iters < 0");
+    const int32_t N = g->N, T = g->T;
+    if (N == 0 || T == 0)   // np.amax of an empty vector (pagerank.py:126-127)
+        return mr_fail(ctx, MR_ERR_VALUE, "zero-size array to reduction operation maximum which has no identity");
+    MR_TRY_HIP(ctx, hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    const bool fp32 = precision == MR_FP32;
+    const int n_tblocks = cdiv(T, TB);
+    MR_TRY(g->kind.alloc(ctx, (size_t)T));
+    MR_TRY(g->pref.zero(ctx, (size_t)T));
+    MR_TRY(g->c_t.zero(ctx, (size_t)T));
+    MR_TRY(g->flag.zero(ctx, 4));
+    MR_TRY(g->scal.zero(ctx, 8));
+    MR_TRY(g->sn.alloc(ctx, (size_t)N));
+    MR_TRY(g->su.alloc(ctx, (size_t)N));
+    MR_TRY(g->sp.alloc(ctx, (size_t)N));
+    MR_TRY(g->weight.alloc(ctx, (size_t)N));
+    MR_TRY(g->part.alloc(ctx, (size_t)g->nseg));
+    MR_TRY(g->bmax.alloc(ctx, (size_t)n_tblocks));
+    for (int i = 0; i < 2; ++i) {
+        if (fp32) MR_TRY(g->q32[i].alloc(ctx, (size_t)T));
+        else MR_TRY(g->q64[i].alloc(ctx, (size_t)T));
+    }
+    // ---- kinds
+    uint64_t cap = 1;
+    while (cap < 2ull * (uint64_t)T) cap <<= 1;
+    MR_TRY(g->ht_key.zero(ctx, cap));
+    MR_TRY(g->ht_cnt.zero(ctx, cap));
+    MR_TRY(g->ht_rep.alloc(ctx, cap));
+    MR_TRY_HIP(ctx, hipMemsetAsync(g->ht_rep.p, 0xFF, cap * sizeof(int32_t), st));
+    MR_TRY(g->slot_of.alloc(ctx, (size_t)T));
+    const int64_t* koff = g->rs_is_sr ? g->rs_off.p : g->srt_off.p;
+    const int32_t* kops = g->rs_is_sr ? g->rs_ops.p : g->srt_ops.p;
+    hipLaunchKernelGGL(k_kind_insert, dim3(cdiv(T, 256)), dim3(256), 0, st, koff, kops, g->w_t.p, T, g->ht_key.p,
+                       g->ht_cnt.p, g->ht_rep.p, g->slot_of.p, (uint64_t)(cap - 1), 0x5eed5eedull);
+    hipLaunchKernelGGL(k_kind_verify, dim3(cdiv(T, 256)), dim3(256), 0, st, koff, kops, g->w_t.p, T, g->ht_cnt.p,
+                       g->ht_rep.p, g->slot_of.p, g->kind.p, g->flag.p);
+    // ---- preference
+    const int32_t* prt = g->pr_identity ? nullptr : g->pr_trace.p;
+    const int32_t* prl = g->pr_identity ? nullptr : g->pr_len.p;
+    const int32_t n_pr = g->n_pr;
+    const int nbp = cdiv(n_pr > 0 ? n_pr : 1, TB);
+    DBuf<double> ppart;
+    MR_TRY(ppart.zero(ctx, 2 * (size_t)nbp));
+    if (n_pr > 0)
+        hipLaunchKernelGGL(k_pref_partial, dim3(nbp), dim3(TB), 0, st, g->kind.p, prt, prl, g->len_t.p, n_pr, ppart.p,
+                           g->flag.p);
+    if (flags & MR_PR_EXACT_SUMS)
+        hipLaunchKernelGGL(k_pref_total_exact, dim3(1), dim3(64), 0, st, g->kind.p, prt, prl, g->len_t.p, n_pr,
+                           g->scal.p);
+    else
+        hipLaunchKernelGGL(k_pref_total, dim3(1), dim3(1024), 0, st, ppart.p, nbp, g->scal.p);
+    int32_t hflag[4] = {0, 0, 0, 0};
+    MR_TRY_HIP(ctx, hipMemcpyAsync(hflag, g->flag.p, sizeof hflag, hipMemcpyDeviceToHost, st));
+    MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+    if (hflag[0] & 1) return mr_fail(ctx, MR_ERR_STATE, "trace-kind hash collision (retry with another seed)");
+    if (anomaly && (hflag[0] & 2)) return mr_fail(ctx, MR_ERR_ZERODIV, "float division by zero");
+    const float cd = (float)(1.0 - d);
+    if (n_pr > 0)
+        hipLaunchKernelGGL(k_pref_apply, dim3(nbp), dim3(TB), 0, st, g->kind.p, prt, prl, g->len_t.p, n_pr,
+                           g->scal.p, anomaly, cd, g->pref.p, g->c_t.p);
+    // ---- power iteration
+    hipLaunchKernelGGL(k_iter_init, dim3(cdiv(N > T ? N : T, 256)), dim3(256), 0, st, g->u_o.p, g->w_t.p, N, T,
+                       g->sn.p, g->su.p, g->q64[0].p, g->q32[0].p, (int)fp32, g->scal.p);
+    const int lds_su = N <= LDS_NODES;
+    const size_t lds = lds_su ? (size_t)N * sizeof(double) : 0;
+    const int n_oblocks = cdiv(g->nseg, OPB / WAVE);
+    for (int it = 0; it < iters; ++it) {
+        const int cur = it & 1, nxt = cur ^ 1;
+        if (fp32)
+            hipLaunchKernelGGL(k_iter_pass<float>, dim3(n_tblocks + n_oblocks), dim3(TB), lds, st, g->rs_off.p,
+                               g->rs_ops.p, g->su.p, g->c_t.p, g->w_t.p, g->q32[nxt].p, g->bmax.p, T, N, n_tblocks, d,
+                               lds_su, g->sr_off.p, g->sr_trs.p, g->seg_op.p, g->seg_beg.p, g->q32[cur].p, g->part.p,
+                               g->nseg);
+        else
+            hipLaunchKernelGGL(k_iter_pass<double>, dim3(n_tblocks + n_oblocks), dim3(TB), lds, st, g->rs_off.p,
+                               g->rs_ops.p, g->su.p, g->c_t.p, g->w_t.p, g->q64[nxt].p, g->bmax.p, T, N, n_tblocks, d,
+                               lds_su, g->sr_off.p, g->sr_trs.p, g->seg_op.p, g->seg_beg.p, g->q64[cur].p, g->part.p,
+                               g->nseg);
+        hipLaunchKernelGGL(k_iter_finish, dim3(1), dim3(1024), 0, st, g->part.p, g->op_seg.p, g->ss_off.p,
+                           g->ss_par.p, g->pw.p, g->u_o.p, g->bmax.p, n_tblocks, N, d, alpha, g->sp.p, g->sn.p,
+                           g->su.p, g->scal.p);
+    }
+    hipLaunchKernelGGL(k_weights, dim3(1), dim3(1024), 0, st, g->sn.p, N, (int)((flags & MR_PR_EXACT_SUMS) != 0),
+                       g->weight.p, g->scal.p);
+    MR_TRY_HIP(ctx, hipGetLastError());
+    return MR_OK;
+}

@@ -1,0 +1,267 @@
+"""Drop-in for the reference module ``preprocess_data`` (preprocess_data.py).
+
+* ``get_pagerank_graph`` builds the op<->trace graph on the GPU (K1,
+  csrc/mr_graph_build.hip) from the int-coded span table and returns four lazy mappings
+  with the reference's key order and list contents.  Passing them straight to
+  ``pagerank.trace_pagerank`` (what ``online_anomaly_detect_RCA`` does) keeps the graph in
+  HBM: no dict is ever materialised.
+* ``get_operation_slo`` runs the SLO reduction on the GPU (K4, csrc/mr_slo.hip).
+* ``get_span``, ``get_service_operation_list`` and ``get_operation_duration_data`` are
+  DataFrame utilities with the reference's behaviour (including the added ``operation``
+  column side effect).
+
+A DataFrame is factorised into a :class:`SpanTable` once and uploaded once; the result is
+cached per DataFrame object (see :func:`span_table`).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import weakref
+from collections.abc import Mapping
+
+import numpy as np
+import pandas as pd
+
+from . import _lib
+from ._lib import SpanCols, ptr
+from .spans import UI_SERVICE, SpanTable, op_display
+
+ROOT_INDEX = "root"   # preprocess_data.py:219
+
+
+# ------------------------------------------------------------------------ span table cache
+class DeviceSpans:
+    """An mr_spans handle: the span columns resident in HBM."""
+
+    def __init__(self, ctx, table: SpanTable):
+        lib = _lib.load()
+        table.check()
+        cols = SpanCols()
+        cols.n_spans = table.n_spans
+        cols.n_traces, cols.n_podops, cols.n_svcops = table.n_traces, table.n_podops, table.n_svcops
+        keep = {}
+        for name, ct in (("trace", C.c_int32), ("podop", C.c_int32), ("svcop", C.c_int32), ("span", C.c_int64),
+                         ("parent", C.c_int64), ("duration", C.c_int64), ("tstart", C.c_int64), ("tend", C.c_int64)):
+            a = getattr(table, name)
+            if a is None:
+                continue
+            a = np.ascontiguousarray(a, dtype=np.int32 if ct is C.c_int32 else np.int64)
+            keep[name] = a
+            setattr(cols, name, ptr(a, ct))
+        h = _lib.P()
+        ctx.check(lib.mr_spans_upload(ctx.h, C.byref(cols), C.byref(h)), "mr_spans_upload")
+        self.ctx, self.h, self.table = ctx, h, table
+
+    def close(self):
+        if getattr(self, "h", None):
+            _lib.load().mr_spans_free(self.h)
+            self.h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+_CACHE: dict = {}
+
+
+def _fingerprint(df: pd.DataFrame):
+    n = len(df)
+    if n == 0:
+        return (0,)
+    pick = [0, n // 2, n - 1]
+    sample = tuple(str(df["traceID"].iat[i]) + "|" + str(df["spanID"].iat[i]) for i in pick)
+    return (n, sample, int(df["duration"].to_numpy().sum()))
+
+
+def span_table(df: pd.DataFrame, ctx=None):
+    """(SpanTable, DeviceSpans) for a DataFrame, built once per DataFrame object."""
+    ctx = ctx or _lib.default_context()
+    key = (id(df), ctx.device)
+    fp = _fingerprint(df)
+    hit = _CACHE.get(key)
+    if hit is not None and hit[0]() is df and hit[1] == fp:
+        return hit[2], hit[3]
+    table = SpanTable.from_dataframe(df)
+    dev = DeviceSpans(ctx, table)
+    try:
+        ref = weakref.ref(df, lambda _r, k=key: _CACHE.pop(k, None))
+    except TypeError:  # pragma: no cover - DataFrames are weak-referenceable
+        ref = lambda: df
+    _CACHE[key] = (ref, fp, table, dev)
+    return table, dev
+
+
+# ------------------------------------------------------------------------ reference utilities
+def get_span(df, start=None, end=None):
+    """preprocess_data.py:222-226 -- inclusive trace-level window (T15)."""
+    if start and end:
+        df = df[(df["startTime"] >= start) & (df["endTime"] <= end)]
+    return df
+
+
+def _svc_op_names(span_df: pd.DataFrame) -> np.ndarray:
+    svc = span_df["serviceName"].to_numpy(dtype=object)
+    op = op_display(svc, span_df["operationName"].to_numpy(dtype=object))
+    return np.array([f"{a}_{b}" for a, b in zip(svc, op)], dtype=object)
+
+
+def get_service_operation_list(span_df: pd.DataFrame):
+    """preprocess_data.py:238-245: adds the ``operation`` column, returns its distinct values in
+    first-appearance order."""
+    span_df["operation"] = _svc_op_names(span_df)
+    return span_df["operation"].drop_duplicates().tolist()
+
+
+def get_operation_slo(service_operation_list, span_df: pd.DataFrame, *, ctx=None):
+    """preprocess_data.py:262-290 on the GPU (K4): {svc_op: [round(mean/1000,4), round(std/1000,4)]}
+    for the ops of the DataFrame that are in ``service_operation_list``, keys in sorted order."""
+    span_df["operation"] = _svc_op_names(span_df)
+    ctx = ctx or _lib.default_context()
+    table, dev = span_table(span_df, ctx)
+    n = table.n_svcops
+    mean = np.empty(n, np.float64)
+    std = np.empty(n, np.float64)
+    cnt = np.empty(n, np.int64)
+    ctx.check(_lib.load().mr_slo(ctx.h, dev.h, ptr(mean, C.c_double), ptr(std, C.c_double), ptr(cnt, C.c_int64)),
+              "mr_slo")
+    keep = set(service_operation_list)
+    out = {}
+    for code, name in enumerate(table.svcop_names):   # codes are in sorted name order
+        if cnt[code] > 0 and name in keep:
+            out[name] = [np.float64(mean[code]), np.float64(std[code])]
+    return out
+
+
+def get_operation_duration_data(operation_list, span_df: pd.DataFrame):
+    """preprocess_data.py:309-334 -- {traceID: {svc_op: count, ..., 'duration': max}} (sorted
+    keys, traces with max duration <= 0 dropped).  Mutates ``operationName`` of ``span_df``
+    like the reference.  The detector itself runs on the GPU (anormaly_detector.py)."""
+    span_df["operationName"] = _svc_op_names(span_df)
+    counts = span_df.groupby(["traceID", "operationName"]).size().unstack(fill_value=0)
+    counts["duration"] = span_df.groupby("traceID")["duration"].max()
+    counts = counts.dropna(subset=["duration"])
+    counts = counts[counts["duration"] > 0]
+    return counts.to_dict(orient="index")
+
+
+# ------------------------------------------------------------------------ K1 graph + lazy dicts
+class PagerankGraph:
+    """Device graph of one ``get_pagerank_graph`` call and its four reference-shaped views."""
+
+    def __init__(self, ctx, table: SpanTable, dev: DeviceSpans, trace_mask: np.ndarray):
+        lib = _lib.load()
+        mask = np.ascontiguousarray(trace_mask, dtype=np.uint8)
+        h = _lib.P()
+        ctx.check(lib.mr_graph_build(ctx.h, dev.h, ptr(mask, C.c_uint8), C.byref(h)), "mr_graph_build")
+        from .graph import DeviceGraph
+
+        n, t, nnz, e = C.c_int32(), C.c_int32(), C.c_int64(), C.c_int64()
+        lib.mr_graph_info(h, C.byref(n), C.byref(t), C.byref(nnz), C.byref(e))
+        self.N, self.T = n.value, t.value
+        self.node_podop = np.empty(self.N, np.int32)
+        self.trace_code = np.empty(self.T, np.int32)
+        ctx.check(lib.mr_graph_nodes(h, ptr(self.node_podop, C.c_int32), ptr(self.trace_code, C.c_int32)),
+                  "mr_graph_nodes")
+        self.table, self.mask = table, mask.astype(bool)
+        nodes = [table.podop_names[c] for c in self.node_podop]
+        traces = [table.trace_names[c] for c in self.trace_code]
+        self._dg = DeviceGraph(ctx, h, nodes, traces, self.N, self.T)
+        self.nodes, self.traces = nodes, traces
+        self._lists = None
+        self.operation_operation = GraphDicts(self, "operation_operation")
+        self.operation_trace = GraphDicts(self, "operation_trace")
+        self.trace_operation = GraphDicts(self, "trace_operation")
+        self.pr_trace = GraphDicts(self, "pr_trace")
+
+    def device_graph(self):
+        return self._dg
+
+    def as_tuple(self):
+        return self.operation_operation, self.operation_trace, self.trace_operation, self.pr_trace
+
+    def _materialise(self):
+        """List contents (one entry per span, DataFrame row order) for code that inspects the
+        dicts; the key order comes from the device graph."""
+        if self._lists is not None:
+            return self._lists
+        tb = self.table
+        rows = np.flatnonzero(self.mask[tb.trace])
+        node_of = {int(c): i for i, c in enumerate(self.node_podop)}
+        rn = np.array([node_of[int(c)] for c in tb.podop[rows]], dtype=np.int64)
+        tr_of = {int(c): i for i, c in enumerate(self.trace_code)}
+        rt = np.array([tr_of[int(c)] for c in tb.trace[rows]], dtype=np.int64)
+        ot = {k: [] for k in self.traces}
+        tnames, nnames = self.traces, self.nodes
+        for t, n in zip(rt, rn):
+            ot[tnames[t]].append(nnames[n])
+        to = {k: [] for k in sorted(nnames)}
+        for t, n in zip(rt, rn):
+            to[nnames[n]].append(tnames[t])
+        # children: merge of ParentSpanId == spanID, left (child) row order, then right row order
+        oo = {k: [] for k in nnames}
+        sp = tb.span[rows]
+        order = np.argsort(sp, kind="stable")
+        srt = sp[order]
+        par = tb.parent[rows]
+        lo = np.searchsorted(srt, par, "left")
+        hi = np.searchsorted(srt, par, "right")
+        for i in range(rows.size):
+            if par[i] < 0:
+                continue
+            for j in order[lo[i]:hi[i]]:
+                oo[nnames[rn[j]]].append(nnames[rn[i]])
+        self._lists = {"operation_operation": oo, "operation_trace": ot, "trace_operation": to, "pr_trace": ot}
+        return self._lists
+
+
+class GraphDicts(Mapping):
+    """Read-only mapping with the reference's key order; list values materialise on demand."""
+
+    def __init__(self, owner: PagerankGraph, kind: str):
+        self.owner = owner
+        self.kind = kind
+
+    def _keys(self):
+        o = self.owner
+        if self.kind == "operation_operation":
+            return o.nodes
+        if self.kind == "trace_operation":
+            return sorted(o.nodes)
+        return o.traces
+
+    def __iter__(self):
+        return iter(self._keys())
+
+    def __len__(self):
+        return len(self._keys())
+
+    def __getitem__(self, k):
+        return self.owner._materialise()[self.kind][k]
+
+    def __contains__(self, k):
+        return k in self.owner._materialise()[self.kind]
+
+    def keys(self):
+        return list(self._keys())
+
+    def __repr__(self):
+        return f"<GraphDicts {self.kind}: {len(self)} keys on {self.owner._dg.ctx.device}>"
+
+
+def get_pagerank_graph(trace_list, span_df: pd.DataFrame, *, ctx=None):
+    """preprocess_data.py:358-383 on the GPU (K1).  Returns (operation_operation,
+    operation_trace, trace_operation, pr_trace) as lazy mappings backed by the device graph."""
+    ctx = ctx or _lib.default_context()
+    table, dev = span_table(span_df, ctx)
+    index = table.meta.get("trace_index")
+    if index is None:
+        index = table.meta["trace_index"] = {n: i for i, n in enumerate(table.trace_names)}
+    mask = np.zeros(table.n_traces, np.uint8)
+    for t in trace_list:
+        i = index.get(t)
+        if i is not None:
+            mask[i] = 1
+    return PagerankGraph(ctx, table, dev, mask).as_tuple()

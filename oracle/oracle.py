@@ -288,24 +288,31 @@ def span_graph(trace: np.ndarray, podop: np.ndarray, span: np.ndarray, parent: n
                      nchild.astype(np.int64), int(parent_ops.size), rows, node, tidx)
 
 
-def span_graph_dicts(sg: SpanGraph, podop_names, trace_names):
-    """The four dicts of preprocess_data.py:370-383 from a SpanGraph (list contents in row
-    order; children lists as multisets in merge order is not reproduced -- compare sorted)."""
+def span_graph_dicts(sg: SpanGraph, span: np.ndarray, parent: np.ndarray, podop_names, trace_names):
+    """The four dicts of preprocess_data.py:370-383 from a SpanGraph: list entries one per span
+    in row order; children in merge order (child row order, then matching parent rows)."""
     nodes = [podop_names[c] for c in sg.node_podop]
-    oo = {n: [] for n in nodes}
-    # children multiset per parent
-    for c, p in zip(sg.ss_c, sg.ss_p):
-        pass
-    ot, to = {}, {}
     tn = [trace_names[c] for c in sg.trace_codes]
-    for t in tn:
-        ot[t] = []
-    for n in sorted(nodes):
-        to[n] = []
+    rows = sg.rows
+    ot = {t: [] for t in tn}
     for ti, ni in zip(sg.tidx_of_row, sg.node_of_row):
         ot[tn[ti]].append(nodes[ni])
+    to = {n: [] for n in sorted(nodes)}
+    for ti, ni in zip(sg.tidx_of_row, sg.node_of_row):
         to[nodes[ni]].append(tn[ti])
-    return nodes, ot, to
+    oo = {n: [] for n in nodes}
+    sp = span[rows]
+    order = np.argsort(sp, kind="stable")
+    srt = sp[order]
+    par = parent[rows]
+    lo = np.searchsorted(srt, par, "left")
+    hi = np.searchsorted(srt, par, "right")
+    for i in range(rows.size):
+        if par[i] < 0:
+            continue
+        for j in order[lo[i]:hi[i]]:
+            oo[nodes[sg.node_of_row[j]]].append(nodes[sg.node_of_row[i]])
+    return oo, ot, to, dict(ot)
 
 
 # ----------------------------------------------------------------------------- spectrum

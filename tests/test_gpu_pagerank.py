@@ -1,0 +1,102 @@
+"""GPU parity of K2 (trace_pagerank) against the reference fixtures and the oracle.
+
+Tolerances (BASELINE.json north star): fp64 scores within 1e-6 relative (we assert 1e-10:
+the only difference from the reference is the summation order of its dense dgemv),
+fp32 within 1e-4; coverage counts, key order and kinds exact.
+"""
+import numpy as np
+import pytest
+
+import oracle as orc
+from conftest import load_golden, unhex
+from gpu_util import c2_graph, golden_graph_dicts, host_graph_from_oracle
+
+pytestmark = pytest.mark.gpu
+
+RTOL64 = 1e-10
+RTOL32 = 1e-4
+
+
+def _check(got, exp, rtol):
+    w, num = got
+    assert list(w.keys()) == exp["keys"]
+    assert list(num.keys()) == exp["num_keys"]
+    assert [int(v) for v in num.values()] == exp["num"]
+    assert all(isinstance(v, np.float64) for v in w.values())
+    np.testing.assert_allclose(np.array(list(w.values())), unhex(exp["weight"]), rtol=rtol, atol=0)
+
+
+@pytest.mark.parametrize("case", ["fig3", "multiset_selfloop", "pr_subset", "single", "asym_incidence"])
+@pytest.mark.parametrize("anomaly", [False, True])
+@pytest.mark.parametrize("precision", ["fp64", "fp32"])
+def test_dict_cases(case, anomaly, precision):
+    from microrank_amd.pagerank import trace_pagerank
+
+    d = load_golden("dict_cases.json")[case]
+    inp = d["input"]
+    got = trace_pagerank(inp["operation_operation"], inp["operation_trace"], inp["trace_operation"],
+                         inp["pr_trace"], anomaly, precision=precision)
+    _check(got, d[f"anomaly={anomaly}"], RTOL64 if precision == "fp64" else RTOL32)
+
+
+def test_unknown_key_raises_value_error():
+    from microrank_amd.pagerank import trace_pagerank
+
+    with pytest.raises(ValueError):
+        trace_pagerank({"a": ["zz"]}, {"t": ["a"]}, {"a": ["t"]}, {"t": ["a"]}, False)
+    with pytest.raises(ValueError):
+        trace_pagerank({}, {}, {}, {}, False)
+    with pytest.raises(ZeroDivisionError):
+        trace_pagerank({"a": []}, {"t": ["a"], "u": ["a"]}, {"a": ["t", "u"]}, {"t": ["a"], "u": []}, True)
+
+
+@pytest.mark.parametrize("name", ["c1", "pods_dup_broken", "ops200"])
+def test_span_case_graphs(name):
+    """The reference's own graph dicts for each window -> trace_pagerank on the GPU."""
+    from microrank_amd.pagerank import trace_pagerank
+
+    case = load_golden(f"{name}.json")
+    from conftest import regen_window
+
+    _, adf = regen_window(case)
+    tnames = sorted(adf["traceID"].unique())
+    for gkey, anomaly, pkey in (("graph_swapped_normal", False, "pr_normal"),
+                                ("graph_swapped_anomaly", True, "pr_anomaly")):
+        dicts = golden_graph_dicts(case[gkey], tnames)
+        _check(trace_pagerank(*dicts, anomaly), case[pkey], RTOL64)
+        _check(trace_pagerank(*dicts, anomaly, precision="fp32"), case[pkey], RTOL32)
+
+
+@pytest.fixture(scope="module")
+def c2():
+    return c2_graph()
+
+
+@pytest.mark.parametrize("anomaly", [False, True])
+def test_c2_scale_against_oracle(c2, anomaly):
+    """1k ops / 200k traces: GPU vs oracle; kinds exact, weights 1e-10 (fp64) / 1e-4 (fp32),
+    and bitwise-identical reruns (fixed-order reductions)."""
+    from microrank_amd import _lib
+    from microrank_amd.graph import DeviceGraph
+
+    st, sg = c2
+    g = sg.as_graph()
+    kind = orc.trace_kinds(g) if g.T <= 300_000 else None
+    v = orc.preference(g, kind, anomaly)
+    s = orc.power_iteration(g, v)
+    w_ref, cov_ref = orc.weights(g, s)
+    ctx = _lib.default_context()
+    dg = DeviceGraph.upload(ctx, host_graph_from_oracle(g))
+    dg.pagerank(anomaly)
+    w, cov, k, pref = dg.fetch(kinds=True)
+    np.testing.assert_array_equal(k, kind)
+    np.testing.assert_allclose(pref, v, rtol=1.2e-7, atol=0)   # tree vs sequential sum: <=1 fp32 ulp
+    np.testing.assert_array_equal(cov, np.array(list(cov_ref.values())))
+    np.testing.assert_allclose(w, np.array(list(w_ref.values())), rtol=RTOL64, atol=0)
+    dg.pagerank(anomaly)
+    w2, _ = dg.fetch()
+    assert w2.tobytes() == w.tobytes(), "rerun not bitwise identical"
+    dg.pagerank(anomaly, precision="fp32")
+    w3, _ = dg.fetch()
+    np.testing.assert_allclose(w3, np.array(list(w_ref.values())), rtol=RTOL32, atol=0)
+    dg.close()
