@@ -1,0 +1,554 @@
+// K1: preprocess_data.get_pagerank_graph (preprocess_data.py:358-383) on gfx950.
+//
+// From HBM-resident int-coded span columns and a trace mask (the trace_list, :360):
+//   1. compact the selected rows, keeping row order (first appearance, T10)
+//   2. per row: span counts per trace (len_t, :377) and per pod-op (len_o, :379), first
+//      appearance row per pod-op, and the parent join ParentSpanId == spanID over the selected
+//      rows regardless of traceID (:370, T11) -> distinct (parent op, child op) edges with
+//      multiplicity (children multiset size, :371).  Hot keys (the root op is in every trace)
+//      are aggregated in LDS per block before any global atomic.
+//   3. node order: parent ops sorted by name (= code), then the other ops by first appearance
+//      (:371-375, T10)
+//   4. (trace, node) pairs -> stable radix sort -> distinct pairs = trace-major CSR; a second
+//      stable sort by node gives the op-major CSC (traces ascending); call edges sorted by
+//      (child, parent) give P_ss by child.
+#include <algorithm>
+
+#include "mr_prim.h"
+#include "mr_sort.h"
+
+namespace {
+constexpr int BT = 256;
+constexpr int LDS_HIST = 8192;     // pod-op histograms in LDS up to this many codes
+constexpr int ESET = 1024;         // per-block LDS edge set slots
+constexpr uint64_t EMPTY = ~0ull;
+
+__device__ __forceinline__ uint64_t hmix(uint64_t z) {
+    z ^= z >> 33;
+    z *= 0xff51afd7ed558ccdull;
+    z ^= z >> 33;
+    z *= 0xc4ceb9fe1a85ec53ull;
+    return z ^ (z >> 33);
+}
+
+// ---------------------------------------------------------------- spans upload: spanID multimap
+__global__ void k_count_codes(const int64_t* span, int64_t S, int32_t* cnt) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < S) atomicAdd(&cnt[span[i]], 1);
+}
+__global__ void k_fill_ids(const int64_t* span, int64_t S, const int64_t* off, int32_t* cur, int32_t* rows) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < S) {
+        int64_t c = span[i];
+        rows[off[c] + atomicAdd(&cur[c], 1)] = (int32_t)i;
+    }
+}
+// rows inside a spanID bucket ascending (buckets hold duplicates only: tiny)
+__global__ void k_sort_buckets(const int64_t* off, int64_t n_codes, int32_t* rows) {
+    int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n_codes) return;
+    int64_t a = off[c], b = off[c + 1];
+    for (int64_t i = a + 1; i < b; ++i) {
+        int32_t v = rows[i];
+        int64_t j = i - 1;
+        while (j >= a && rows[j] > v) {
+            rows[j + 1] = rows[j];
+            --j;
+        }
+        rows[j + 1] = v;
+    }
+}
+
+// ---------------------------------------------------------------- selection
+__global__ void k_sel_flags(const int32_t* trace, int64_t S, const uint8_t* mask, int32_t* flag) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < S) flag[i] = mask[trace[i]] ? 1 : 0;
+}
+__global__ void k_compact_rows(const int32_t* flag, const int64_t* pos, int64_t S, int32_t* rows) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < S && flag[i]) rows[pos[i]] = (int32_t)i;
+}
+
+// ---------------------------------------------------------------- per-row statistics + join
+__device__ __forceinline__ void global_edge_add(uint64_t key, uint32_t c, uint64_t* gk, uint32_t* gc, uint64_t gmask) {
+    uint64_t s = hmix(key) & gmask;
+    for (;;) {
+        unsigned long long k = atomicCAS((unsigned long long*)&gk[s], (unsigned long long)EMPTY, (unsigned long long)key);
+        if (k == EMPTY || k == key) break;
+        s = (s + 1) & gmask;
+    }
+    atomicAdd(&gc[s], c);
+}
+
+__global__ void __launch_bounds__(BT) k_rows(const int32_t* rows, int64_t Ssel, const int32_t* trace,
+                                             const int32_t* podop, const int64_t* parent, const int32_t* selflag,
+                                             const int64_t* id_off, const int32_t* id_rows, int64_t n_codes,
+                                             int32_t n_podops, int use_lds_hist, int32_t* tcnt, int32_t* ocnt,
+                                             int32_t* ofirst, uint64_t* gk, uint32_t* gc, uint64_t gmask) {
+    extern __shared__ int32_t lh[];   // [2*n_podops] counts, first rows (when use_lds_hist)
+    __shared__ unsigned long long ek[ESET];
+    __shared__ uint32_t ec[ESET];
+    int32_t* lcnt = lh;
+    int32_t* lfirst = lh + n_podops;
+    if (use_lds_hist)
+        for (int32_t i = threadIdx.x; i < n_podops; i += BT) {
+            lcnt[i] = 0;
+            lfirst[i] = 0x7fffffff;
+        }
+    for (int i = threadIdx.x; i < ESET; i += BT) {
+        ek[i] = EMPTY;
+        ec[i] = 0;
+    }
+    __syncthreads();
+    const int64_t base = (int64_t)blockIdx.x * BT * 8;
+    for (int c = 0; c < 8; ++c) {
+        const int64_t li = base + (int64_t)c * BT + threadIdx.x;   // local (selected) row index
+        if (li >= Ssel) break;
+        const int32_t r = rows[li];
+        const int32_t op = podop[r];
+        atomicAdd(&tcnt[trace[r]], 1);
+        if (use_lds_hist) {
+            atomicAdd(&lcnt[op], 1);
+            atomicMin(&lfirst[op], (int32_t)li);
+        } else {
+            atomicAdd(&ocnt[op], 1);
+            atomicMin(&ofirst[op], (int32_t)li);
+        }
+        const int64_t p = parent[r];
+        if (p < 0 || p >= n_codes) continue;
+        for (int64_t e = id_off[p]; e < id_off[p + 1]; ++e) {
+            const int32_t j = id_rows[e];
+            if (!selflag[j]) continue;
+            const uint64_t key = ((uint64_t)(uint32_t)podop[j] << 32) | (uint32_t)op;   // (parent, child)
+            uint32_t s = (uint32_t)(hmix(key) & (ESET - 1));
+            bool done = false;
+            for (int probe = 0; probe < 32; ++probe) {
+                unsigned long long k = atomicCAS(&ek[s], (unsigned long long)EMPTY, (unsigned long long)key);
+                if (k == EMPTY || k == key) {
+                    atomicAdd(&ec[s], 1u);
+                    done = true;
+                    break;
+                }
+                s = (s + 1) & (ESET - 1);
+            }
+            if (!done) global_edge_add(key, 1u, gk, gc, gmask);   // LDS set crowded: go global
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < ESET; i += BT)
+        if (ek[i] != EMPTY) global_edge_add(ek[i], ec[i], gk, gc, gmask);
+    if (use_lds_hist)
+        for (int32_t i = threadIdx.x; i < n_podops; i += BT)
+            if (lcnt[i]) {
+                atomicAdd(&ocnt[i], lcnt[i]);
+                atomicMin(&ofirst[i], lfirst[i]);
+            }
+}
+
+// ---------------------------------------------------------------- node order
+__global__ void k_edge_flags(const uint64_t* gk, int64_t cap, int32_t* flag) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < cap) flag[i] = gk[i] != EMPTY;
+}
+__global__ void k_edge_compact(const uint64_t* gk, const uint32_t* gc, const int32_t* flag, const int64_t* pos,
+                               int64_t cap, uint64_t* ekey, uint32_t* ecnt, int32_t* is_par, int32_t* nchild_code) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= cap || !flag[i]) return;
+    const uint64_t k = gk[i];
+    ekey[pos[i]] = k;
+    ecnt[pos[i]] = gc[i];
+    const int32_t par = (int32_t)(k >> 32);
+    is_par[par] = 1;
+    atomicAdd(&nchild_code[par], (int32_t)gc[i]);
+}
+// flags: parent codes (sorted by code) and present non-parents keyed by first row
+__global__ void k_node_flags(const int32_t* ocnt, const int32_t* is_par, int32_t n, int32_t* pflag, int32_t* qflag) {
+    int32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n) return;
+    pflag[c] = is_par[c] ? 1 : 0;
+    qflag[c] = (ocnt[c] > 0 && !is_par[c]) ? 1 : 0;
+}
+__global__ void k_node_parents(const int32_t* pflag, const int64_t* ppos, const int32_t* qflag, const int64_t* qpos,
+                               const int32_t* ofirst, int32_t n, int32_t* node_of_code, int32_t* node_podop,
+                               uint64_t* qkey, uint32_t* qval) {
+    int32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n) return;
+    if (pflag[c]) {
+        node_of_code[c] = (int32_t)ppos[c];
+        node_podop[ppos[c]] = c;
+    }
+    if (qflag[c]) {
+        qkey[qpos[c]] = (uint64_t)(uint32_t)ofirst[c];
+        qval[qpos[c]] = (uint32_t)c;
+    }
+}
+__global__ void k_node_rest(const uint32_t* qval, int64_t nq, int32_t P, int32_t* node_of_code, int32_t* node_podop) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nq) return;
+    const int32_t c = (int32_t)qval[i];
+    node_of_code[c] = P + (int32_t)i;
+    node_podop[P + i] = c;
+}
+
+// ---------------------------------------------------------------- traces
+__global__ void k_trace_flags(const int32_t* tcnt, int32_t n, int32_t* flag) {
+    int32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c < n) flag[c] = tcnt[c] > 0;
+}
+__global__ void k_trace_index(const int32_t* flag, const int64_t* pos, const int32_t* tcnt, int32_t n,
+                              int32_t* tidx_of_code, int32_t* trace_code, int32_t* len_t) {
+    int32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n || !flag[c]) return;
+    const int32_t t = (int32_t)pos[c];
+    tidx_of_code[c] = t;
+    trace_code[t] = c;
+    len_t[t] = tcnt[c];
+}
+
+// ---------------------------------------------------------------- pairs
+__global__ void k_pair_keys(const int32_t* rows, int64_t Ssel, const int32_t* trace, const int32_t* podop,
+                            const int32_t* tidx_of_code, const int32_t* node_of_code, int nb, uint64_t* keys) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= Ssel) return;
+    const int32_t r = rows[i];
+    keys[i] = ((uint64_t)(uint32_t)tidx_of_code[trace[r]] << nb) | (uint32_t)node_of_code[podop[r]];
+}
+__global__ void k_run_heads(const uint64_t* keys, int64_t n, int32_t* flag) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) flag[i] = (i == 0 || keys[i] != keys[i - 1]) ? 1 : 0;
+}
+// distinct pairs in (trace, node) order; every present trace has >= 1 pair, so its CSR offset is
+// the position of its first pair (no per-trace counting atomics)
+__global__ void k_pairs_out(const uint64_t* keys, const int32_t* flag, const int64_t* pos, int64_t n, int nb,
+                            int64_t* rs_off, uint64_t* ckey, uint32_t* cval) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || !flag[i]) return;
+    const uint64_t k = keys[i];
+    const uint32_t t = (uint32_t)(k >> nb), node = (uint32_t)(k & ((1ull << nb) - 1));
+    const int64_t e = pos[i];
+    ckey[e] = node;      // re-sorted by node for the CSC; value carries the trace
+    cval[e] = t;
+    if (i == 0 || (keys[i - 1] >> nb) != t) rs_off[t] = e;
+}
+__global__ void k_pairs_csr(const uint64_t* ckey, int64_t nnz, int32_t* sr_ops) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < nnz) sr_ops[i] = (int32_t)ckey[i];
+}
+// every present node has >= 1 pair: its CSC offset is the position of its first pair
+__global__ void k_csc_out(const uint64_t* key_sorted, const uint32_t* val_sorted, int64_t nnz, int64_t* sr_off,
+                          int32_t* sr_trs) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nnz) return;
+    sr_trs[i] = (int32_t)val_sorted[i];
+    if (i == 0 || key_sorted[i] != key_sorted[i - 1]) sr_off[key_sorted[i]] = i;
+}
+__global__ void k_set_last(int64_t* off, int32_t n, int64_t v) { off[n] = v; }
+
+// ---------------------------------------------------------------- per-node arrays
+__global__ void k_node_arrays(const int32_t* node_podop, int32_t N, const int32_t* ocnt, const int32_t* nchild_code,
+                              int32_t* len_o, int32_t* nchild) {
+    int32_t n = blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= N) return;
+    const int32_t c = node_podop[n];
+    len_o[n] = ocnt[c];
+    nchild[n] = nchild_code[c];
+}
+__global__ void k_edge_nodes(const uint64_t* ekey, int64_t E, const int32_t* node_of_code, int nb, uint64_t* skey) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= E) return;
+    const uint64_t k = ekey[i];
+    const uint32_t par = (uint32_t)node_of_code[(int32_t)(k >> 32)];
+    const uint32_t ch = (uint32_t)node_of_code[(int32_t)(k & 0xffffffffu)];
+    skey[i] = ((uint64_t)ch << nb) | par;    // sort by (child, parent)
+}
+__global__ void k_edge_csr(const uint64_t* skey, int64_t E, int nb, int32_t* ss_par, int32_t* ccount) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= E) return;
+    ss_par[i] = (int32_t)(skey[i] & ((1ull << nb) - 1));
+    atomicAdd(&ccount[skey[i] >> nb], 1);
+}
+}  // namespace
+
+// ------------------------------------------------------------------------------ host
+extern "C" int mr_spans_upload(mr_ctx* ctx, const mr_span_cols* c, mr_spans** out) {
+    if (!ctx || !c || !out) return mr_fail(ctx, MR_ERR_ARG, "mr_spans_upload: null argument");
+    *out = nullptr;
+    const int64_t S = c->n_spans;
+    if (S < 0 || S >= (1ll << 31)) return mr_fail(ctx, MR_ERR_ARG, "n_spans out of range (int32 row ids)");
+    if (S && (!c->trace || !c->podop || !c->svcop || !c->span || !c->parent || !c->duration))
+        return mr_fail(ctx, MR_ERR_ARG, "mr_spans_upload: missing column");
+    MR_TRY_HIP(ctx, hipSetDevice(ctx->device));
+    int64_t max_code = -1;
+    for (int64_t i = 0; i < S; ++i) {
+        if (c->span[i] < 0) return mr_fail(ctx, MR_ERR_ARG, "negative span code at row %lld", (long long)i);
+        if (c->trace[i] < 0 || c->trace[i] >= c->n_traces || c->podop[i] < 0 || c->podop[i] >= c->n_podops ||
+            c->svcop[i] < 0 || c->svcop[i] >= c->n_svcops)
+            return mr_fail(ctx, MR_ERR_ARG, "code out of range at row %lld", (long long)i);
+        max_code = std::max(max_code, c->span[i]);
+    }
+    auto* s = new mr_spans();
+    s->ctx = ctx;
+    s->S = S;
+    s->n_traces = c->n_traces;
+    s->n_podops = c->n_podops;
+    s->n_svcops = c->n_svcops;
+    s->n_span_codes = max_code + 1;
+    s->has_times = c->tstart && c->tend;
+    int rc = MR_OK;
+    auto fail = [&](int code) {
+        delete s;
+        return code;
+    };
+    if ((rc = s->trace.upload(ctx, c->trace, S)) || (rc = s->podop.upload(ctx, c->podop, S)) ||
+        (rc = s->svcop.upload(ctx, c->svcop, S)) || (rc = s->span.upload(ctx, c->span, S)) ||
+        (rc = s->parent.upload(ctx, c->parent, S)) || (rc = s->duration.upload(ctx, c->duration, S)))
+        return fail(rc);
+    if (s->has_times && ((rc = s->tstart.upload(ctx, c->tstart, S)) || (rc = s->tend.upload(ctx, c->tend, S))))
+        return fail(rc);
+    // spanID -> rows multimap (counting sort by code)
+    const int64_t U = s->n_span_codes;
+    DBuf<int32_t> cnt;
+    DBuf<int64_t> tmp;
+    if ((rc = cnt.zero(ctx, (size_t)U)) || (rc = s->id_off.alloc(ctx, (size_t)U + 1)) ||
+        (rc = s->id_rows.alloc(ctx, (size_t)S)) || (rc = tmp.alloc(ctx, (size_t)scan_tmp_elems(U))))
+        return fail(rc);
+    if (S) hipLaunchKernelGGL(k_count_codes, dim3(cdiv(S, 256)), dim3(256), 0, ctx->stream, s->span.p, S, cnt.p);
+    if ((rc = mr_exclusive_scan_i32(ctx, cnt.p, s->id_off.p, U, tmp.p))) return fail(rc);
+    if (U && hipMemsetAsync(cnt.p, 0, U * sizeof(int32_t), ctx->stream) != hipSuccess) return fail(MR_ERR_HIP);
+    if (S)
+        hipLaunchKernelGGL(k_fill_ids, dim3(cdiv(S, 256)), dim3(256), 0, ctx->stream, s->span.p, S, s->id_off.p, cnt.p,
+                           s->id_rows.p);
+    if (U) hipLaunchKernelGGL(k_sort_buckets, dim3(cdiv(U, 256)), dim3(256), 0, ctx->stream, s->id_off.p, U, s->id_rows.p);
+    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(ctx->stream) != hipSuccess)
+        return fail(mr_fail(ctx, MR_ERR_HIP, "mr_spans_upload: kernel failure"));
+    *out = s;
+    return MR_OK;
+}
+
+extern "C" int mr_spans_free(mr_spans* s) {
+    if (!s) return MR_OK;
+    (void)hipSetDevice(s->ctx->device);
+    (void)hipStreamSynchronize(s->ctx->stream);
+    delete s;
+    return MR_OK;
+}
+
+static int read_i64(mr_ctx* ctx, const int64_t* dev, int64_t* host) {
+    MR_TRY_HIP(ctx, hipMemcpyAsync(host, dev, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+    MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return MR_OK;
+}
+
+int mr_graph_build_dev(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d_mask, mr_graph** out) {
+    hipStream_t st = ctx->stream;
+    const int64_t S = sp->S;
+    const int32_t NT = sp->n_traces, NP = sp->n_podops;
+    auto g = new mr_graph();
+    g->ctx = ctx;
+    int rc = MR_OK;
+    auto fail = [&](int code) {
+        delete g;
+        return code;
+    };
+#define TRY(x)                          \
+    do {                                \
+        if ((rc = (x))) return fail(rc); \
+    } while (0)
+#define TRY_HIP_(x)                                                                              \
+    do {                                                                                         \
+        hipError_t e_ = (x);                                                                     \
+        if (e_ != hipSuccess) return fail(mr_fail(ctx, MR_ERR_HIP, "%s: %s", #x, hipGetErrorString(e_))); \
+    } while (0)
+    // 1. selected rows
+    DBuf<int32_t> selflag, rows;
+    DBuf<int64_t> pos, tmp;
+    const int64_t tmpn = std::max<int64_t>({scan_tmp_elems(S), scan_tmp_elems(NT), scan_tmp_elems(NP), 1});
+    TRY(selflag.alloc(ctx, S));
+    TRY(pos.alloc(ctx, S + 1));
+    TRY(tmp.alloc(ctx, tmpn));
+    if (S) hipLaunchKernelGGL(k_sel_flags, dim3(cdiv(S, 256)), dim3(256), 0, st, sp->trace.p, S, d_mask, selflag.p);
+    TRY(mr_exclusive_scan_i32(ctx, selflag.p, pos.p, S, tmp.p));
+    int64_t Ssel = 0;
+    TRY(read_i64(ctx, pos.p + S, &Ssel));
+    TRY(rows.alloc(ctx, Ssel));
+    if (S) hipLaunchKernelGGL(k_compact_rows, dim3(cdiv(S, 256)), dim3(256), 0, st, selflag.p, pos.p, S, rows.p);
+    // 2. statistics + join
+    DBuf<int32_t> tcnt, ocnt, ofirst;
+    TRY(tcnt.zero(ctx, NT));
+    TRY(ocnt.zero(ctx, NP));
+    TRY(ofirst.alloc(ctx, NP));
+    if (NP) TRY_HIP_(hipMemsetAsync(ofirst.p, 0x7f, NP * sizeof(int32_t), st));
+    uint64_t ecap_want = (uint64_t)std::min<int64_t>(std::max<int64_t>(Ssel, 1), (int64_t)NP * NP + 1);
+    uint64_t ecap = 1024;
+    while (ecap < 2 * ecap_want) ecap <<= 1;
+    DBuf<uint64_t> gk;
+    DBuf<uint32_t> gc;
+    TRY(gk.alloc(ctx, ecap));
+    TRY(gc.zero(ctx, ecap));
+    TRY_HIP_(hipMemsetAsync(gk.p, 0xff, ecap * sizeof(uint64_t), st));
+    const int use_lds = NP <= LDS_HIST;
+    const size_t lds = use_lds ? 2 * (size_t)NP * sizeof(int32_t) : 0;
+    if (Ssel)
+        hipLaunchKernelGGL(k_rows, dim3(cdiv(Ssel, BT * 8)), dim3(BT), lds, st, rows.p, Ssel, sp->trace.p, sp->podop.p,
+                           sp->parent.p, selflag.p, sp->id_off.p, sp->id_rows.p, sp->n_span_codes, NP, use_lds, tcnt.p,
+                           ocnt.p, ofirst.p, gk.p, gc.p, ecap - 1);
+    // edges
+    DBuf<int32_t> eflag, is_par, nchild_code;
+    DBuf<int64_t> epos, etmp;
+    TRY(eflag.alloc(ctx, ecap));
+    TRY(epos.alloc(ctx, ecap + 1));
+    TRY(etmp.alloc(ctx, scan_tmp_elems(ecap)));
+    TRY(is_par.zero(ctx, NP));
+    TRY(nchild_code.zero(ctx, NP));
+    hipLaunchKernelGGL(k_edge_flags, dim3(cdiv(ecap, 256)), dim3(256), 0, st, gk.p, (int64_t)ecap, eflag.p);
+    TRY(mr_exclusive_scan_i32(ctx, eflag.p, epos.p, ecap, etmp.p));
+    int64_t E = 0;
+    TRY(read_i64(ctx, epos.p + ecap, &E));
+    DBuf<uint64_t> ekey;
+    DBuf<uint32_t> ecnt;
+    TRY(ekey.alloc(ctx, E));
+    TRY(ecnt.alloc(ctx, E));
+    hipLaunchKernelGGL(k_edge_compact, dim3(cdiv(ecap, 256)), dim3(256), 0, st, gk.p, gc.p, eflag.p, epos.p,
+                       (int64_t)ecap, ekey.p, ecnt.p, is_par.p, nchild_code.p);
+    // 3. node order
+    DBuf<int32_t> pflag, qflag, node_of_code;
+    DBuf<int64_t> ppos, qpos;
+    TRY(pflag.alloc(ctx, NP));
+    TRY(qflag.alloc(ctx, NP));
+    TRY(ppos.alloc(ctx, NP + 1));
+    TRY(qpos.alloc(ctx, NP + 1));
+    TRY(node_of_code.alloc(ctx, NP));
+    if (NP) hipLaunchKernelGGL(k_node_flags, dim3(cdiv(NP, 256)), dim3(256), 0, st, ocnt.p, is_par.p, NP, pflag.p, qflag.p);
+    TRY(mr_exclusive_scan_i32(ctx, pflag.p, ppos.p, NP, tmp.p));
+    TRY(mr_exclusive_scan_i32(ctx, qflag.p, qpos.p, NP, tmp.p));
+    int64_t P = 0, Q = 0;
+    TRY(read_i64(ctx, ppos.p + NP, &P));
+    TRY(read_i64(ctx, qpos.p + NP, &Q));
+    const int32_t N = (int32_t)(P + Q);
+    TRY(g->node_podop.alloc(ctx, N));
+    DBuf<uint64_t> qkey;
+    DBuf<uint32_t> qval;
+    TRY(qkey.alloc(ctx, Q));
+    TRY(qval.alloc(ctx, Q));
+    if (NP)
+        hipLaunchKernelGGL(k_node_parents, dim3(cdiv(NP, 256)), dim3(256), 0, st, pflag.p, ppos.p, qflag.p, qpos.p,
+                           ofirst.p, NP, node_of_code.p, g->node_podop.p, qkey.p, qval.p);
+    SortScratch ws;
+    TRY(mr_radix_sort(ctx, qkey.p, qval.p, Q, bits_for((uint64_t)std::max<int64_t>(Ssel, 1)), ws));
+    if (Q)
+        hipLaunchKernelGGL(k_node_rest, dim3(cdiv(Q, 256)), dim3(256), 0, st, qval.p, Q, (int32_t)P, node_of_code.p,
+                           g->node_podop.p);
+    // traces
+    DBuf<int32_t> tflag, tidx_of_code;
+    DBuf<int64_t> tpos;
+    TRY(tflag.alloc(ctx, NT));
+    TRY(tpos.alloc(ctx, NT + 1));
+    TRY(tidx_of_code.alloc(ctx, NT));
+    if (NT) hipLaunchKernelGGL(k_trace_flags, dim3(cdiv(NT, 256)), dim3(256), 0, st, tcnt.p, NT, tflag.p);
+    TRY(mr_exclusive_scan_i32(ctx, tflag.p, tpos.p, NT, tmp.p));
+    int64_t T64 = 0;
+    TRY(read_i64(ctx, tpos.p + NT, &T64));
+    const int32_t T = (int32_t)T64;
+    TRY(g->trace_code.alloc(ctx, T));
+    TRY(g->len_t.alloc(ctx, T));
+    if (NT)
+        hipLaunchKernelGGL(k_trace_index, dim3(cdiv(NT, 256)), dim3(256), 0, st, tflag.p, tpos.p, tcnt.p, NT,
+                           tidx_of_code.p, g->trace_code.p, g->len_t.p);
+    // 4. pairs -> CSR, CSC
+    const int nb = std::max(1, bits_for((uint64_t)std::max(N - 1, 0)));
+    DBuf<uint64_t> keys;
+    TRY(keys.alloc(ctx, Ssel));
+    if (Ssel)
+        hipLaunchKernelGGL(k_pair_keys, dim3(cdiv(Ssel, 256)), dim3(256), 0, st, rows.p, Ssel, sp->trace.p, sp->podop.p,
+                           tidx_of_code.p, node_of_code.p, nb, keys.p);
+    TRY(mr_radix_sort(ctx, keys.p, nullptr, Ssel, nb + bits_for((uint64_t)std::max(T - 1, 0)), ws));
+    DBuf<int32_t> head;
+    DBuf<int64_t> hpos;
+    TRY(head.alloc(ctx, Ssel));
+    TRY(hpos.alloc(ctx, Ssel + 1));
+    if (Ssel) hipLaunchKernelGGL(k_run_heads, dim3(cdiv(Ssel, 256)), dim3(256), 0, st, keys.p, Ssel, head.p);
+    TRY(mr_exclusive_scan_i32(ctx, head.p, hpos.p, Ssel, tmp.p));
+    int64_t nnz = 0;
+    TRY(read_i64(ctx, hpos.p + Ssel, &nnz));
+    DBuf<uint64_t> ckey;
+    DBuf<uint32_t> cval;
+    TRY(ckey.alloc(ctx, nnz));
+    TRY(cval.alloc(ctx, nnz));
+    TRY(g->rs_ops.alloc(ctx, nnz));
+    TRY(g->rs_off.alloc(ctx, T + 1));
+    if (Ssel)
+        hipLaunchKernelGGL(k_pairs_out, dim3(cdiv(Ssel, 256)), dim3(256), 0, st, keys.p, head.p, hpos.p, Ssel, nb,
+                           g->rs_off.p, ckey.p, cval.p);
+    hipLaunchKernelGGL(k_set_last, dim3(1), dim3(1), 0, st, g->rs_off.p, T, nnz);
+    if (nnz) hipLaunchKernelGGL(k_pairs_csr, dim3(cdiv(nnz, 256)), dim3(256), 0, st, ckey.p, nnz, g->rs_ops.p);
+    // CSC: stable sort of the (trace-ordered) pairs by node
+    TRY(mr_radix_sort(ctx, ckey.p, cval.p, nnz, nb, ws));
+    TRY(g->sr_trs.alloc(ctx, nnz));
+    TRY(g->sr_off.alloc(ctx, N + 1));
+    if (nnz) hipLaunchKernelGGL(k_csc_out, dim3(cdiv(nnz, 256)), dim3(256), 0, st, ckey.p, cval.p, nnz, g->sr_off.p, g->sr_trs.p);
+    hipLaunchKernelGGL(k_set_last, dim3(1), dim3(1), 0, st, g->sr_off.p, N, nnz);
+    DBuf<int64_t> ntmp;
+    TRY(ntmp.alloc(ctx, scan_tmp_elems(std::max(N, 1))));
+    // per-node arrays and P_ss
+    TRY(g->len_o.alloc(ctx, N));
+    TRY(g->nchild.alloc(ctx, N));
+    if (N)
+        hipLaunchKernelGGL(k_node_arrays, dim3(cdiv(N, 256)), dim3(256), 0, st, g->node_podop.p, N, ocnt.p,
+                           nchild_code.p, g->len_o.p, g->nchild.p);
+    DBuf<uint64_t> skey;
+    TRY(skey.alloc(ctx, E));
+    if (E) hipLaunchKernelGGL(k_edge_nodes, dim3(cdiv(E, 256)), dim3(256), 0, st, ekey.p, E, node_of_code.p, nb, skey.p);
+    TRY(mr_radix_sort(ctx, skey.p, nullptr, E, 2 * nb, ws));
+    DBuf<int32_t> ccount;
+    TRY(ccount.zero(ctx, N));
+    TRY(g->ss_par.alloc(ctx, E));
+    TRY(g->ss_off.alloc(ctx, N + 1));
+    if (E) hipLaunchKernelGGL(k_edge_csr, dim3(cdiv(E, 256)), dim3(256), 0, st, skey.p, E, nb, g->ss_par.p, ccount.p);
+    TRY(mr_exclusive_scan_i32(ctx, ccount.p, g->ss_off.p, N, ntmp.p));
+    TRY_HIP_(hipGetLastError());
+    g->N = N;
+    g->T = T;
+    g->nnz_sr = g->nnz_rs = nnz;
+    g->E = E;
+    g->rs_is_sr = true;
+    g->pr_identity = true;
+    g->n_pr = T;
+    TRY(mr_graph_prepare(ctx, g));
+#undef TRY
+#undef TRY_HIP_
+    *out = g;
+    return MR_OK;
+}
+
+extern "C" int mr_graph_build(mr_ctx* ctx, const mr_spans* sp, const uint8_t* trace_mask, mr_graph** out) {
+    if (!ctx || !sp || !trace_mask || !out || sp->ctx != ctx) return mr_fail(ctx, MR_ERR_ARG, "mr_graph_build: bad arguments");
+    MR_TRY_HIP(ctx, hipSetDevice(ctx->device));
+    DBuf<uint8_t> mask;
+    MR_TRY(mask.upload(ctx, trace_mask, (size_t)sp->n_traces));
+    return mr_graph_build_dev(ctx, sp, mask.p, out);
+}
+
+extern "C" int mr_graph_nodes(const mr_graph* g, int32_t* node_podop, int32_t* trace_code) {
+    if (!g) return MR_ERR_ARG;
+    mr_ctx* ctx = g->ctx;
+    if (!g->node_podop.p && g->N) return mr_fail(ctx, MR_ERR_STATE, "graph was not built from spans");
+    if (node_podop && g->N) MR_TRY(g->node_podop.download(ctx, node_podop, g->N));
+    if (trace_code && g->T) MR_TRY(g->trace_code.download(ctx, trace_code, g->T));
+    MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return MR_OK;
+}
+
+extern "C" int mr_graph_export(const mr_graph* g, int64_t* sr_off, int32_t* sr_ops, int32_t* len_t, int32_t* len_o,
+                               int64_t* ss_off, int32_t* ss_par, int32_t* nchild) {
+    if (!g) return MR_ERR_ARG;
+    mr_ctx* ctx = g->ctx;
+    if (sr_off) MR_TRY(g->rs_off.download(ctx, sr_off, (size_t)g->T + 1));
+    if (sr_ops) MR_TRY(g->rs_ops.download(ctx, sr_ops, (size_t)g->nnz_rs));
+    if (len_t) MR_TRY(g->len_t.download(ctx, len_t, (size_t)g->T));
+    if (len_o) MR_TRY(g->len_o.download(ctx, len_o, (size_t)g->N));
+    if (ss_off) MR_TRY(g->ss_off.download(ctx, ss_off, (size_t)g->N + 1));
+    if (ss_par) MR_TRY(g->ss_par.download(ctx, ss_par, (size_t)g->E));
+    if (nchild) MR_TRY(g->nchild.download(ctx, nchild, (size_t)g->N));
+    MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return MR_OK;
+}

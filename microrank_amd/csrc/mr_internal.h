@@ -117,8 +117,11 @@ struct mr_graph {
     DBuf<double> q64[2];         // [T] w_t * r'_t (fp64 mode)
     DBuf<float> q32[2];          // [T] (fp32 mode)
     DBuf<double> part;           // [nseg] segment partial sums of the s' pass
-    DBuf<double> bmax;           // [n trace-pass blocks] block maxima of r'
-    DBuf<double> sn, su, sp;     // [N] normalised s, u_o*s, unnormalised s'
+    DBuf<uint32_t> op_cnt;       // [N] monotone per-op arrival counters (last arriver finishes s')
+    DBuf<unsigned long long> mslot;  // [6] bits of (M_s, M_r) for iterations k%3
+    DBuf<double> spb[2];         // [N] unnormalised s' (double-buffered)
+    DBuf<double> sub[2];         // [N] u_o * s'[o]
+    DBuf<double> sn;             // [N] final normalised s
     DBuf<double> scal;           // [8] M_s, M_r, sums
     DBuf<double> weight;         // [N]
     DBuf<uint64_t> ht_key;       // kinds hash table

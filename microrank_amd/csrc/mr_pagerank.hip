@@ -1,16 +1,19 @@
 // K2: personalised PageRank of pagerank.trace_pagerank (pagerank.py:15-130) on gfx950.
 //
-// Sparse, HBM-bound: no MFMA.  Per Jacobi iteration k (T8) two block roles share ONE launch:
-//   trace role  r'_{k+1}[t] = d * sum_{o in rs(t)} u_o * s_k[o] + fp32((1-d) v_t)   (pagerank.py:125)
-//               q'_{k+1}[t] = w_t * r'_{k+1}[t]                                      (P_sr weight, kept for s')
-//               s_k*u lives in LDS (su), one thread per trace, sequential in node order
-//   op role     part[seg]   = sum_{t in segment of sr(o)} q'_k[t]                    (pagerank.py:123)
-//               one wave per fixed 1024-entry segment of an op's trace list, fixed butterfly
-// then a one-block finish kernel:
-//   s'_{k+1}[o] = d * (sum_seg part / M_r(k) + alpha * sum_{p in ss(o)} pw_p * s_k[p])
-//   M_s = max s', s_{k+1} = s'/M_s, M_r(k+1) = max over trace-role block maxima   (pagerank.py:126-127)
-// Normalisation of r is deferred: sum_t w_t (r'_t / M_r) is computed as (sum_t w_t r'_t) / M_r.
-// Every reduction has a fixed order, so results are bitwise reproducible (no float atomics).
+// Sparse, HBM-bound: no MFMA.  Each Jacobi iteration k -> k+1 (T8) is ONE launch with two
+// block roles that both read only iteration-k state:
+//   trace role  r'[t] = d * sum_{o in rs(t)} u_o * s_k[o] + fp32((1-d) v_t)      (pagerank.py:125)
+//               q'[t] = w_t * r'[t]      (the P_sr-weighted value the op role sums next time)
+//               s_k*u is staged in LDS; the block's contiguous id range is read coalesced into
+//               LDS, then each thread sums its trace in node order.
+//   op role     one wave per fixed 1024-entry segment of an op's trace list sums q'_k; the
+//               LAST segment of an op to finish (agent-scope acq_rel counter) combines the
+//               partials in segment order and adds the call-graph term:
+//               s'[o] = d * (sum q'_k / M_r(k) + alpha * sum_{p in ss(o)} pw_p * s_k[p])  (:122-124)
+// Maxima M_s, M_r (np.amax, :126-127) travel as bit patterns of non-negative doubles through
+// atomicMax, which is exact and order-independent.  Normalisation of r is deferred:
+// sum_t w_t (r'_t / M_r) is evaluated as (sum_t w_t r'_t) / M_r.  Every float reduction has a
+// fixed order (no float atomics), so results are bitwise reproducible run to run.
 #include <cmath>
 
 #include "mr_internal.h"
@@ -20,8 +23,8 @@ namespace {
 
 constexpr int SEG = 1024;           // op-list segment length (entries)
 constexpr int TB = 256;             // trace-role block size (one trace per thread)
-constexpr int OPB = 256;            // op-role block size (4 waves, one segment per wave)
 constexpr int LDS_NODES = 8192;     // su staged in LDS up to this many nodes (64 KiB)
+constexpr int VCAP = 2048;          // trace-role ids staged per round in LDS (16 KiB of values)
 
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     z += 0x9E3779B97F4A7C15ull;
@@ -44,7 +47,7 @@ __global__ void k_op_consts(const int32_t* len_o, const int32_t* nchild, const i
     pw[o] = nchild[o] > 0 ? (float)(1.0 / (double)nchild[o]) : 0.0f;
     int64_t c = sr_off[o + 1] - sr_off[o];
     cov[o] = (int32_t)c;                                  // trace_num_list (pagerank.py:98-104)
-    nseg_of[o] = (int32_t)((c + SEG - 1) / SEG);
+    nseg_of[o] = c > 0 ? (int32_t)((c + SEG - 1) / SEG) : 1;   // >= 1: every op gets a finisher
 }
 
 __global__ void k_fill_segments(const int64_t* op_seg64, const int64_t* sr_off, int32_t* op_seg,
@@ -64,25 +67,63 @@ __global__ void k_fill_segments(const int64_t* op_seg64, const int64_t* sr_off, 
 // kind[t] = size of the class of traces with an equal P_sr column: key = (op set, fp32(1/len_t)).
 // Open-addressing hash table of 64-bit keys; a second pass verifies every member against the
 // slot's representative, so a hash collision is detected (flag) rather than miscounted.
-__global__ void k_kind_insert(const int64_t* off, const int32_t* ops, const float* w_t, int32_t T,
-                              uint64_t* keys, uint32_t* cnt, int32_t* rep, int32_t* slot_of,
-                              uint64_t mask, uint64_t seed) {
-    int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= T) return;
+constexpr int KB = 256, KLDS = 512;   // kinds: block size, LDS table slots
+
+__device__ __forceinline__ uint64_t kind_hash(const int64_t* off, const int32_t* ops, const float* w_t,
+                                              int32_t t, uint64_t seed) {
     int64_t e0 = off[t], e1 = off[t + 1];
     uint32_t wb = e1 > e0 ? __float_as_uint(w_t[t]) : 0u;
     uint64_t h = mix64(seed ^ (uint64_t)wb);
     for (int64_t e = e0; e < e1; ++e) h = mix64(h ^ (uint64_t)(uint32_t)ops[e]);
-    if (h == 0) h = 1;
-    uint64_t slot = h & mask;
-    for (;;) {
-        uint64_t k = atomicCAS((unsigned long long*)&keys[slot], 0ull, (unsigned long long)h);
-        if (k == 0 || k == h) break;
-        slot = (slot + 1) & mask;
+    return h ? h : 1;
+}
+
+// Two-level insertion: traces of a block are first counted in an LDS table (hot kinds -- the
+// same few call paths in thousands of traces -- would otherwise serialise on one global
+// counter), then each distinct key of the block does ONE global insert + add.
+__global__ void __launch_bounds__(KB) k_kind_insert(const int64_t* off, const int32_t* ops, const float* w_t,
+                                                    int32_t T, uint64_t* keys, uint32_t* cnt, int32_t* rep,
+                                                    int32_t* slot_of, uint64_t mask, uint64_t seed) {
+    __shared__ unsigned long long lkey[KLDS];
+    __shared__ uint32_t lcnt[KLDS];
+    __shared__ int32_t lrep[KLDS];
+    __shared__ int32_t lglob[KLDS];
+    for (int i = threadIdx.x; i < KLDS; i += KB) {
+        lkey[i] = 0ull;
+        lcnt[i] = 0u;
+        lrep[i] = -1;
     }
-    atomicAdd(&cnt[slot], 1u);
-    atomicCAS(&rep[slot], -1, t);
-    slot_of[t] = (int32_t)slot;
+    __syncthreads();
+    const int32_t t = blockIdx.x * KB + threadIdx.x;
+    int myslot = -1;
+    if (t < T) {
+        const uint64_t h = kind_hash(off, ops, w_t, t, seed);
+        int s = (int)(h & (KLDS - 1));
+        for (;;) {
+            unsigned long long k = atomicCAS(&lkey[s], 0ull, (unsigned long long)h);
+            if (k == 0ull || k == h) break;
+            s = (s + 1) & (KLDS - 1);
+        }
+        atomicAdd(&lcnt[s], 1u);
+        atomicCAS(&lrep[s], -1, t);
+        myslot = s;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < KLDS; i += KB) {
+        const uint64_t h = lkey[i];
+        if (!h) continue;
+        uint64_t slot = h & mask;
+        for (;;) {
+            uint64_t k = atomicCAS((unsigned long long*)&keys[slot], 0ull, (unsigned long long)h);
+            if (k == 0 || k == h) break;
+            slot = (slot + 1) & mask;
+        }
+        atomicAdd(&cnt[slot], lcnt[i]);
+        atomicCAS(&rep[slot], -1, lrep[i]);
+        lglob[i] = (int32_t)slot;
+    }
+    __syncthreads();
+    if (t < T) slot_of[t] = lglob[myslot];
 }
 
 __global__ void k_kind_verify(const int64_t* off, const int32_t* ops, const float* w_t, int32_t T,
@@ -173,57 +214,88 @@ __global__ void k_pref_apply(const double* kind, const int32_t* pr_trace, const 
 }
 
 // ---------------------------------------------------------------- iteration
-__global__ void k_iter_init(const float* u_o, const float* w_t, int32_t N, int32_t T, double* sn,
-                            double* su, double* q64, float* q32, int fp32, double* scal) {
+__device__ __forceinline__ double bits2d(unsigned long long b) { return __longlong_as_double((long long)b); }
+__device__ __forceinline__ unsigned long long d2bits(double v) {
+    return (unsigned long long)__double_as_longlong(v);
+}
+
+__global__ void k_iter_init(const float* w_t, const float* u_o, int32_t N, int32_t T, double* sp0, double* su0,
+                            double* q64, float* q32, int fp32, unsigned long long* mslot) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const double v0 = 1.0 / (double)(N + T);                   // pagerank.py:118-119
     if (i < N) {
-        sn[i] = v0;
-        su[i] = (double)u_o[i] * v0;
+        sp0[i] = v0;
+        su0[i] = (double)u_o[i] * v0;
     }
     if (i < T) {
         double q = (double)w_t[i] * v0;
         if (fp32) q32[i] = (float)q; else q64[i] = q;
     }
-    if (i == 0) {
-        scal[0] = 1.0;   // M_s(0): s_0 is used unnormalised
-        scal[1] = 1.0;   // M_r(0)
-    }
+    if (i < 6) mslot[i] = i < 2 ? d2bits(1.0) : 0ull;   // M_s(0) = M_r(0) = 1: s_0, r_0 used as is
 }
 
+// One Jacobi iteration k -> k+1 in ONE launch.  Maxima are exchanged as the bit patterns of
+// non-negative doubles through atomicMax (exact and order-independent); slot k%3 holds
+// (M_s(k), M_r(k)), slot (k+1)%3 collects iteration k+1, slot (k+2)%3 is cleared here for k+2.
+// s' is carried unnormalised together with su'[o] = u_o * s'[o]; the division by M_s(k) is
+// applied to each finished sum instead of to every term.
 template <class Q>
-__global__ void __launch_bounds__(TB) k_iter_pass(
+__global__ void __launch_bounds__(TB) k_iter(
     // trace role
-    const int64_t* __restrict__ rs_off, const int32_t* __restrict__ rs_ops, const double* __restrict__ su,
-    const float* __restrict__ c_t, const float* __restrict__ w_t, Q* __restrict__ q_next,
-    double* __restrict__ bmax, int32_t T, int32_t N, int32_t n_tblocks, double d, int lds_su,
+    const int64_t* __restrict__ rs_off, const int32_t* __restrict__ rs_ops, const double* __restrict__ su_cur,
+    const float* __restrict__ c_t, const float* __restrict__ w_t, Q* __restrict__ q_next, int32_t T, int32_t N,
+    int32_t n_tblocks, double d, double alpha, int lds_su,
     // op role
     const int64_t* __restrict__ sr_off, const int32_t* __restrict__ sr_trs, const int32_t* __restrict__ seg_op,
-    const int64_t* __restrict__ seg_beg, const Q* __restrict__ q_cur, double* __restrict__ part, int32_t nseg) {
+    const int64_t* __restrict__ seg_beg, const int32_t* __restrict__ op_seg, const Q* __restrict__ q_cur,
+    double* part, int32_t nseg, uint32_t* op_cnt, uint32_t epoch, const int64_t* __restrict__ ss_off,
+    const int32_t* __restrict__ ss_par, const float* __restrict__ pw, const float* __restrict__ u_o,
+    const double* __restrict__ sp_cur, double* __restrict__ sp_next, double* __restrict__ su_next,
+    unsigned long long* mslot, int k3) {
     extern __shared__ double lds[];
+    __shared__ double red[TB / WAVE];
+    const double Ms = bits2d(mslot[2 * k3]), Mr = bits2d(mslot[2 * k3 + 1]);
+    unsigned long long* Mnext = mslot + 2 * ((k3 + 1) % 3);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        mslot[2 * ((k3 + 2) % 3)] = 0ull;
+        mslot[2 * ((k3 + 2) % 3) + 1] = 0ull;
+    }
     if ((int32_t)blockIdx.x < n_tblocks) {
-        const double* s = su;
+        // ---- trace role: r'[t] = d * (sum_o u_o s'_k[o]) / M_s(k) + c_t  (pagerank.py:125)
+        const double* su = su_cur;
+        double* vals = lds + (lds_su ? N : 0);
         if (lds_su) {
-            for (int32_t o = threadIdx.x; o < N; o += TB) lds[o] = su[o];
-            __syncthreads();
-            s = lds;
+            for (int32_t o = threadIdx.x; o < N; o += TB) lds[o] = su_cur[o];
+            su = lds;
         }
-        int32_t t = blockIdx.x * TB + threadIdx.x;
+        const int32_t t0 = blockIdx.x * TB;
+        const int32_t t1 = min(t0 + TB, T);
+        const int64_t e0 = rs_off[t0], e1 = rs_off[t1];
+        const int32_t t = t0 + threadIdx.x;
+        const bool own = t < T;
+        const int64_t a = own ? rs_off[t] : 0, b = own ? rs_off[t + 1] : 0;
+        double acc = 0.0;
+        // the block's contiguous id range in rounds of VCAP: coalesced id reads, LDS gather of
+        // su', then every thread continues its own trace's sum in node order
+        for (int64_t lo = e0; lo < e1; lo += VCAP) {
+            const int64_t hi = min(lo + (int64_t)VCAP, e1);
+            __syncthreads();
+            for (int64_t e = lo + threadIdx.x; e < hi; e += TB) vals[e - lo] = su[rs_ops[e]];
+            __syncthreads();
+            const int64_t x0 = max(a, lo), x1 = min(b, hi);
+            for (int64_t e = x0; e < x1; ++e) acc += vals[e - lo];
+        }
         double rp = -__builtin_huge_val();
-        if (t < T) {
-            double acc = 0.0;
-            const int64_t e1 = rs_off[t + 1];
-            for (int64_t e = rs_off[t]; e < e1; ++e) acc += s[rs_ops[e]];
-            rp = d * acc + (double)c_t[t];
+        if (own) {
+            rp = d * (acc / Ms) + (double)c_t[t];
             q_next[t] = (Q)((double)w_t[t] * rp);
         }
-        __shared__ double red[TB / WAVE];
         rp = block_max(rp, red);
-        if (threadIdx.x == 0) bmax[blockIdx.x] = rp;
+        if (threadIdx.x == 0) atomicMax(&Mnext[1], d2bits(rp));
         return;
     }
-    // op role: one wave per segment
-    const int32_t seg = ((int32_t)blockIdx.x - n_tblocks) * (OPB / WAVE) + (int32_t)(threadIdx.x / WAVE);
+    // ---- op role: one wave per fixed segment of an op's trace list  (pagerank.py:122-124)
+    const int32_t seg = ((int32_t)blockIdx.x - n_tblocks) * (TB / WAVE) + (int32_t)(threadIdx.x / WAVE);
     if (seg >= nseg) return;
     const int lane = threadIdx.x & (WAVE - 1);
     const int32_t o = seg_op[seg];
@@ -232,49 +304,58 @@ __global__ void __launch_bounds__(TB) k_iter_pass(
     double acc = 0.0;
     for (int64_t e = b + lane; e < end; e += WAVE) acc += (double)q_cur[sr_trs[e]];
     acc = wave_sum(acc);
-    if (lane == 0) part[seg] = acc;
-}
-
-// one block: finish s'_{k+1}, both maxima, normalised s and u*s for the next pass
-__global__ void __launch_bounds__(1024) k_iter_finish(
-    const double* part, const int32_t* op_seg, const int64_t* ss_off, const int32_t* ss_par,
-    const float* pw, const float* u_o, const double* bmax, int32_t n_tblocks, int32_t N, double d,
-    double alpha, double* sp, double* sn, double* su, double* scal) {
-    __shared__ double red[1024 / WAVE];
-    const double Mr = scal[1];
-    double m = -__builtin_huge_val();
-    for (int32_t o = threadIdx.x; o < N; o += blockDim.x) {
-        double a = 0.0;
-        for (int32_t s = op_seg[o]; s < op_seg[o + 1]; ++s) a += part[s];
-        double b = 0.0;
-        for (int64_t e = ss_off[o]; e < ss_off[o + 1]; ++e) {
-            int32_t p = ss_par[e];
-            b += (double)pw[p] * sn[p];
+    const int32_t s0 = op_seg[o], s1 = op_seg[o + 1];
+    uint32_t old = 0;
+    if (lane == 0) {
+        if (s1 - s0 > 1) {
+            // hand-off without L2 write-back: write-through (sc1) payload, drain, relaxed counter
+            __hip_atomic_store(&part[seg], acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            old = __hip_atomic_fetch_add(&op_cnt[o], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            old = epoch - 1u;   // single segment: this wave finishes the op
         }
-        double v = d * (a / Mr + alpha * b);     // pagerank.py:122-124
-        sp[o] = v;
-        m = nmax(m, v);
     }
-    const double Ms = block_max(m, red);         // includes a __syncthreads: every sn read is done
-    double mr = -__builtin_huge_val();
-    for (int32_t i = threadIdx.x; i < n_tblocks; i += blockDim.x) mr = nmax(mr, bmax[i]);
-    mr = block_max(mr, red);
-    for (int32_t o = threadIdx.x; o < N; o += blockDim.x) {
-        double s = sp[o] / Ms;                   // pagerank.py:126
-        sn[o] = s;
-        su[o] = (double)u_o[o] * s;
+    old = __shfl(old, 0, WAVE);
+    if (old != epoch * (uint32_t)(s1 - s0) - 1u) return;
+    // last segment of op o to finish: combine the partials (sc1 loads) in a fixed order
+    double sum = 0.0;
+    if (s1 - s0 > 1) {
+        for (int32_t s = s0 + lane; s < s1; s += WAVE)
+            sum += __hip_atomic_load(&part[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sum = wave_sum(sum);
+    } else {
+        sum = acc;
     }
-    if (threadIdx.x == 0) {
-        scal[0] = Ms;
-        scal[1] = mr;                            // M_r(k+1), used by the next finish
+    double bb = 0.0;
+    for (int64_t e = ss_off[o] + lane; e < ss_off[o + 1]; e += WAVE) {
+        const int32_t p = ss_par[e];
+        bb += (double)pw[p] * sp_cur[p];
+    }
+    bb = wave_sum(bb);
+    if (lane == 0) {
+        const double v = d * (sum / Mr + alpha * (bb / Ms));      // pagerank.py:122-124
+        sp_next[o] = v;
+        su_next[o] = (double)u_o[o] * v;
+        atomicMax(&Mnext[0], d2bits(v));
     }
 }
 
-// weight = s * sum(s) / N (pagerank.py:93-107); the final s is already max-normalised (:129)
-__global__ void __launch_bounds__(1024) k_weights(const double* sn, int32_t N, int exact, double* weight,
-                                                  double* scal) {
+// result = s/max(s) (pagerank.py:126,129); weight = result * sum(result) / N (:93-107)
+__global__ void __launch_bounds__(1024) k_weights(const double* sp, const unsigned long long* mslot, int k3,
+                                                  int32_t N, int exact, double* sn, double* weight, double* scal) {
     __shared__ double red[1024 / WAVE];
     __shared__ double tot;
+    const double Ms = bits2d(mslot[2 * k3]);
+    double m = -__builtin_huge_val();
+    for (int32_t o = threadIdx.x; o < N; o += blockDim.x) {
+        double v = sp[o] / Ms;
+        sn[o] = v;
+        m = nmax(m, v);
+    }
+    m = block_max(m, red);
+    for (int32_t o = threadIdx.x; o < N; o += blockDim.x) sn[o] = sn[o] / m;
+    __syncthreads();
     if (exact) {
         if (threadIdx.x == 0) {
             double s = 0.0;
@@ -283,7 +364,6 @@ __global__ void __launch_bounds__(1024) k_weights(const double* sn, int32_t N, i
         }
         __syncthreads();
     } else {
-        // fixed-order: contiguous chunk per thread, then block tree
         int32_t per = (N + blockDim.x - 1) / blockDim.x;
         int32_t a = threadIdx.x * per, b = min(a + per, N);
         double s = 0.0;
@@ -347,11 +427,12 @@ extern "C" int mr_pagerank(mr_ctx* ctx, mr_graph* g, int anomaly, double d, doub
     MR_TRY(g->flag.zero(ctx, 4));
     MR_TRY(g->scal.zero(ctx, 8));
     MR_TRY(g->sn.alloc(ctx, (size_t)N));
-    MR_TRY(g->su.alloc(ctx, (size_t)N));
-    MR_TRY(g->sp.alloc(ctx, (size_t)N));
+    MR_TRY(g->spb[0].alloc(ctx, (size_t)N));
+    MR_TRY(g->spb[1].alloc(ctx, (size_t)N));
+    MR_TRY(g->sub[0].alloc(ctx, (size_t)N));
+    MR_TRY(g->sub[1].alloc(ctx, (size_t)N));
     MR_TRY(g->weight.alloc(ctx, (size_t)N));
     MR_TRY(g->part.alloc(ctx, (size_t)g->nseg));
-    MR_TRY(g->bmax.alloc(ctx, (size_t)n_tblocks));
     for (int i = 0; i < 2; ++i) {
         if (fp32) MR_TRY(g->q32[i].alloc(ctx, (size_t)T));
         else MR_TRY(g->q64[i].alloc(ctx, (size_t)T));
@@ -366,7 +447,7 @@ extern "C" int mr_pagerank(mr_ctx* ctx, mr_graph* g, int anomaly, double d, doub
     MR_TRY(g->slot_of.alloc(ctx, (size_t)T));
     const int64_t* koff = g->rs_is_sr ? g->rs_off.p : g->srt_off.p;
     const int32_t* kops = g->rs_is_sr ? g->rs_ops.p : g->srt_ops.p;
-    hipLaunchKernelGGL(k_kind_insert, dim3(cdiv(T, 256)), dim3(256), 0, st, koff, kops, g->w_t.p, T, g->ht_key.p,
+    hipLaunchKernelGGL(k_kind_insert, dim3(cdiv(T, KB)), dim3(KB), 0, st, koff, kops, g->w_t.p, T, g->ht_key.p,
                        g->ht_cnt.p, g->ht_rep.p, g->slot_of.p, (uint64_t)(cap - 1), 0x5eed5eedull);
     hipLaunchKernelGGL(k_kind_verify, dim3(cdiv(T, 256)), dim3(256), 0, st, koff, kops, g->w_t.p, T, g->ht_cnt.p,
                        g->ht_rep.p, g->slot_of.p, g->kind.p, g->flag.p);
@@ -395,29 +476,30 @@ extern "C" int mr_pagerank(mr_ctx* ctx, mr_graph* g, int anomaly, double d, doub
         hipLaunchKernelGGL(k_pref_apply, dim3(nbp), dim3(TB), 0, st, g->kind.p, prt, prl, g->len_t.p, n_pr,
                            g->scal.p, anomaly, cd, g->pref.p, g->c_t.p);
     // ---- power iteration
-    hipLaunchKernelGGL(k_iter_init, dim3(cdiv(N > T ? N : T, 256)), dim3(256), 0, st, g->u_o.p, g->w_t.p, N, T,
-                       g->sn.p, g->su.p, g->q64[0].p, g->q32[0].p, (int)fp32, g->scal.p);
+    MR_TRY(g->op_cnt.zero(ctx, (size_t)N));
+    MR_TRY(g->mslot.alloc(ctx, 6));
+    hipLaunchKernelGGL(k_iter_init, dim3(cdiv(N > T ? N : T, 256)), dim3(256), 0, st, g->w_t.p, g->u_o.p, N, T,
+                       g->spb[0].p, g->sub[0].p, g->q64[0].p, g->q32[0].p, (int)fp32, g->mslot.p);
     const int lds_su = N <= LDS_NODES;
-    const size_t lds = lds_su ? (size_t)N * sizeof(double) : 0;
-    const int n_oblocks = cdiv(g->nseg, OPB / WAVE);
+    const size_t lds = ((lds_su ? (size_t)N : 0) + VCAP) * sizeof(double);
+    const int n_oblocks = cdiv(g->nseg, TB / WAVE);
     for (int it = 0; it < iters; ++it) {
         const int cur = it & 1, nxt = cur ^ 1;
         if (fp32)
-            hipLaunchKernelGGL(k_iter_pass<float>, dim3(n_tblocks + n_oblocks), dim3(TB), lds, st, g->rs_off.p,
-                               g->rs_ops.p, g->su.p, g->c_t.p, g->w_t.p, g->q32[nxt].p, g->bmax.p, T, N, n_tblocks, d,
-                               lds_su, g->sr_off.p, g->sr_trs.p, g->seg_op.p, g->seg_beg.p, g->q32[cur].p, g->part.p,
-                               g->nseg);
+            hipLaunchKernelGGL(k_iter<float>, dim3(n_tblocks + n_oblocks), dim3(TB), lds, st, g->rs_off.p, g->rs_ops.p,
+                               g->sub[cur].p, g->c_t.p, g->w_t.p, g->q32[nxt].p, T, N, n_tblocks, d, alpha, lds_su,
+                               g->sr_off.p, g->sr_trs.p, g->seg_op.p, g->seg_beg.p, g->op_seg.p, g->q32[cur].p,
+                               g->part.p, g->nseg, g->op_cnt.p, (uint32_t)(it + 1), g->ss_off.p, g->ss_par.p, g->pw.p,
+                               g->u_o.p, g->spb[cur].p, g->spb[nxt].p, g->sub[nxt].p, g->mslot.p, it % 3);
         else
-            hipLaunchKernelGGL(k_iter_pass<double>, dim3(n_tblocks + n_oblocks), dim3(TB), lds, st, g->rs_off.p,
-                               g->rs_ops.p, g->su.p, g->c_t.p, g->w_t.p, g->q64[nxt].p, g->bmax.p, T, N, n_tblocks, d,
-                               lds_su, g->sr_off.p, g->sr_trs.p, g->seg_op.p, g->seg_beg.p, g->q64[cur].p, g->part.p,
-                               g->nseg);
-        hipLaunchKernelGGL(k_iter_finish, dim3(1), dim3(1024), 0, st, g->part.p, g->op_seg.p, g->ss_off.p,
-                           g->ss_par.p, g->pw.p, g->u_o.p, g->bmax.p, n_tblocks, N, d, alpha, g->sp.p, g->sn.p,
-                           g->su.p, g->scal.p);
+            hipLaunchKernelGGL(k_iter<double>, dim3(n_tblocks + n_oblocks), dim3(TB), lds, st, g->rs_off.p, g->rs_ops.p,
+                               g->sub[cur].p, g->c_t.p, g->w_t.p, g->q64[nxt].p, T, N, n_tblocks, d, alpha, lds_su,
+                               g->sr_off.p, g->sr_trs.p, g->seg_op.p, g->seg_beg.p, g->op_seg.p, g->q64[cur].p,
+                               g->part.p, g->nseg, g->op_cnt.p, (uint32_t)(it + 1), g->ss_off.p, g->ss_par.p, g->pw.p,
+                               g->u_o.p, g->spb[cur].p, g->spb[nxt].p, g->sub[nxt].p, g->mslot.p, it % 3);
     }
-    hipLaunchKernelGGL(k_weights, dim3(1), dim3(1024), 0, st, g->sn.p, N, (int)((flags & MR_PR_EXACT_SUMS) != 0),
-                       g->weight.p, g->scal.p);
+    hipLaunchKernelGGL(k_weights, dim3(1), dim3(1024), 0, st, g->spb[iters & 1].p, g->mslot.p, iters % 3, N,
+                       (int)((flags & MR_PR_EXACT_SUMS) != 0), g->sn.p, g->weight.p, g->scal.p);
     MR_TRY_HIP(ctx, hipGetLastError());
     return MR_OK;
 }

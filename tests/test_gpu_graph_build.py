@@ -1,0 +1,149 @@
+"""GPU parity of K1 (get_pagerank_graph on the device) against the oracle and the reference
+fixtures: node order, trace order, incidence, span counts and call edges bit-exact."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import oracle as orc
+from conftest import load_golden, regen_window, unhex
+
+pytestmark = pytest.mark.gpu
+
+
+def _export(pg):
+    from microrank_amd import _lib
+    from microrank_amd._lib import ptr
+
+    info = pg.device_graph().info()
+    N, T, nnz, E = info["N"], info["T"], info["nnz"], info["E"]
+    sr_off = np.empty(T + 1, np.int64)
+    sr_ops = np.empty(nnz, np.int32)
+    len_t = np.empty(T, np.int32)
+    len_o = np.empty(N, np.int32)
+    ss_off = np.empty(N + 1, np.int64)
+    ss_par = np.empty(E, np.int32)
+    nchild = np.empty(N, np.int32)
+    dg = pg.device_graph()
+    dg.ctx.check(_lib.load().mr_graph_export(dg.h, ptr(sr_off, C.c_int64), ptr(sr_ops, C.c_int32),
+                                             ptr(len_t, C.c_int32), ptr(len_o, C.c_int32), ptr(ss_off, C.c_int64),
+                                             ptr(ss_par, C.c_int32), ptr(nchild, C.c_int32)))
+    return dict(sr_off=sr_off, sr_ops=sr_ops, len_t=len_t, len_o=len_o, ss_off=ss_off, ss_par=ss_par, nchild=nchild)
+
+
+def _check_against_oracle(table, dev, sel):
+    from microrank_amd import _lib
+    from microrank_amd.preprocess_data import PagerankGraph
+
+    ctx = _lib.default_context()
+    pg = PagerankGraph(ctx, table, dev, sel.astype(np.uint8))
+    sg = orc.span_graph(table.trace, table.podop, table.span, table.parent, sel)
+    np.testing.assert_array_equal(pg.node_podop, sg.node_podop)
+    np.testing.assert_array_equal(pg.trace_code, sg.trace_codes)
+    ex = _export(pg)
+    np.testing.assert_array_equal(ex["len_t"], sg.len_t)
+    np.testing.assert_array_equal(ex["len_o"], sg.len_o)
+    np.testing.assert_array_equal(ex["nchild"], sg.nchild)
+    t_of = np.repeat(np.arange(sg.trace_codes.size), np.diff(ex["sr_off"]))
+    np.testing.assert_array_equal(t_of, sg.sr_t)
+    np.testing.assert_array_equal(ex["sr_ops"], sg.sr_o)
+    c_of = np.repeat(np.arange(sg.node_podop.size), np.diff(ex["ss_off"]))
+    np.testing.assert_array_equal(c_of, sg.ss_c)
+    np.testing.assert_array_equal(ex["ss_par"], sg.ss_p)
+    return pg, sg
+
+
+@pytest.mark.parametrize("name", ["c1", "pods_dup_broken", "ops200"])
+def test_graph_build_matches_reference(name):
+    from microrank_amd import _lib
+    from microrank_amd.pagerank import trace_pagerank
+    from microrank_amd.preprocess_data import get_pagerank_graph, span_table
+
+    case = load_golden(f"{name}.json")
+    _, adf = regen_window(case)
+    table, dev = span_table(adf, _lib.default_context())
+    for lst_key, gkey, anomaly, pkey in (("abnormal", "graph_swapped_normal", False, "pr_normal"),
+                                         ("normal", "graph_swapped_anomaly", True, "pr_anomaly")):
+        sel = np.zeros(table.n_traces, bool)
+        sel[case["detect"][lst_key]] = True
+        _check_against_oracle(table, dev, sel)
+        tnames = sorted(adf["traceID"].unique())
+        g = get_pagerank_graph([tnames[i] for i in case["detect"][lst_key]], adf)
+        assert list(g[0].keys()) == case[gkey]["nodes"]
+        w, num = trace_pagerank(*g, anomaly)
+        exp = case[pkey]
+        assert list(w) == exp["keys"] and list(num.values()) == exp["num"]
+        np.testing.assert_allclose(list(w.values()), unhex(exp["weight"]), rtol=1e-10)
+
+
+def test_graph_views_materialise_like_reference():
+    """The lazy dicts, when read, hold the reference's lists (row order, merge order)."""
+    from microrank_amd.preprocess_data import get_pagerank_graph
+
+    case = load_golden("pods_dup_broken.json")
+    _, adf = regen_window(case)
+    tnames = sorted(adf["traceID"].unique())
+    g = get_pagerank_graph([tnames[i] for i in case["detect"]["abnormal"]], adf)
+    exp = case["graph_swapped_normal"]
+    nodes = exp["nodes"]
+    d = exp["operation_operation"]
+    pos = 0
+    for k, ln in zip(d["keys"], d["len"]):
+        assert g[0][nodes[k]] == [nodes[v] for v in d["vals"][pos:pos + ln]]
+        pos += ln
+    d = exp["operation_trace"]
+    pos = 0
+    for k, ln in zip(d["keys"], d["len"]):
+        assert g[1][tnames[k]] == [nodes[v] for v in d["vals"][pos:pos + ln]]
+        pos += ln
+    assert list(g[2].keys()) == [nodes[k] for k in exp["trace_operation"]["keys"]]
+
+
+def test_edge_spans_graph():
+    import pandas as pd
+
+    from conftest import GOLDEN
+    from microrank_amd.pagerank import trace_pagerank
+    from microrank_amd.preprocess_data import get_pagerank_graph
+
+    e = load_golden("edges.json")
+    df = pd.read_parquet(f"{GOLDEN}/edges_spans.parquet")
+    all_tr = sorted(df.traceID.unique())
+    for key, lst in (("all", all_tr), ("subset", all_tr[::2] + ["not-a-trace"])):
+        g = get_pagerank_graph(lst, df)
+        exp = e[f"graph_{key}"]
+        assert list(g[0].keys()) == list(exp["operation_operation"].keys())
+        for p, ch in exp["operation_operation"].items():
+            assert g[0][p] == ch
+        for flag_ in (False, True):
+            w, num = trace_pagerank(*g, flag_)
+            ex = e[f"pr_{key}_{flag_}"]
+            assert list(w) == ex["keys"] and list(num.values()) == ex["num"]
+            np.testing.assert_allclose(list(w.values()), unhex(ex["weight"]), rtol=1e-10)
+
+
+def test_empty_selection_raises_like_reference():
+    from microrank_amd.pagerank import trace_pagerank
+    from microrank_amd.preprocess_data import get_pagerank_graph
+
+    case = load_golden("c1.json")
+    _, adf = regen_window(case)
+    g = get_pagerank_graph([], adf)
+    assert len(g[0]) == 0 and len(g[1]) == 0
+    with pytest.raises(ValueError):
+        trace_pagerank(*g, False)
+
+
+@pytest.mark.parametrize("dup,broken,pods", [(0.0, 0.0, 1), (0.02, 0.05, 3)])
+def test_c2_scale_graph_build(dup, broken, pods):
+    """1k ops / 200k traces (C2), with and without duplicated spanIDs / broken traces."""
+    from microrank_amd import _lib, synth
+    from microrank_amd.preprocess_data import DeviceSpans
+
+    topo = synth.make_topology(1000, 11, pods_per_service=pods)
+    st = synth.gen_spans(topo, 200_000, 12, branch=1.9, p_max=0.8, dup_span_frac=dup, broken_frac=broken, names=False)
+    st.trace_names = [str(i) for i in range(st.meta["n_gen_traces"])]
+    dev = DeviceSpans(_lib.default_context(), st)
+    rng = np.random.default_rng(5)
+    sel = rng.random(st.n_traces) < 0.6
+    _check_against_oracle(st, dev, sel)
