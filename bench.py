@@ -1,0 +1,212 @@
+"""Benchmark: MicroRank RCA windows on MI355X (one process per GPU).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--precision fp64|fp32] [--no-cpu]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (driver, N > 1)
+
+Workload (BASELINE.json configs[1], "C2"): one RCA window of 1k operations / 200k traces
+(~22 spans/trace, Train-Ticket-like synthetic call tree with one faulty operation), fp64.
+The span columns are generated, factorised and uploaded BEFORE the timed region; a "step" is
+one full window ranked on the device: detector -> two graph builds (T1 swap) -> two
+25-iteration PageRanks -> DStar2 spectrum + top list (mr_rca_window).
+
+N > 1: every rank ranks its own independent window (different seed): data-parallel windows,
+no collective on the data path -> "scaling": "weak".
+
+value = edges traversed by all PageRank iterations of all ranks (25 * (2 nnz + E_c) per graph)
+/ max-over-ranks wall time of the K steps  [GTEPS].  Every other part of the window (detector,
+graph builds, spectrum) is inside that time.  windows_per_s is reported beside it.
+roofline: the power-iteration kernel (k_iter), algorithmic bytes (SURVEY §8(d) B_iter) per
+launch over its live HIP-event duration on the library's stream.
+cpu_baseline: the C restatement (oracle/, OpenMP) of the same window on this host's cores.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+import numpy as np  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s HBM3E spec
+
+
+def make_window(seed: int, n_ops: int, n_traces: int):
+    """Synthetic C2 window: (SpanTable of the window, SpanTable of the normal SLO period)."""
+    from microrank_amd import synth
+
+    topo, normal, abnormal = synth.window_pair(n_ops, n_traces, seed, branch=1.9, p_max=0.8, fault_ms=6000.0,
+                                               names=False)
+    for st in (normal, abnormal):
+        st.trace_names = None
+    return topo, normal, abnormal
+
+
+def slo_from_gpu(ctx, normal):
+    """SLO of the normal period with K4 (get_operation_slo's kernel), as {svcop code: a3}."""
+    import ctypes as C
+
+    from microrank_amd import _lib
+    from microrank_amd._lib import ptr
+    from microrank_amd.preprocess_data import DeviceSpans
+
+    dev = DeviceSpans(ctx, normal)
+    n = normal.n_svcops
+    mean, std, cnt = np.empty(n), np.empty(n), np.empty(n, np.int64)
+    ctx.check(_lib.load().mr_slo(ctx.h, dev.h, ptr(mean, C.c_double), ptr(std, C.c_double), ptr(cnt, C.c_int64)))
+    dev.close()
+    a3 = mean + 3 * std
+    ok = (cnt > 0).astype(np.uint8)
+    return a3, ok
+
+
+def run_window(ctx, dev, t0, t1, a3, ok, prec):
+    import ctypes as C
+
+    from microrank_amd import _lib
+    from microrank_amd._lib import ptr
+
+    codes = np.zeros(11, np.int32)
+    scores = np.zeros(11, np.float64)
+    n_out, na, nn, edges = C.c_int32(), C.c_int32(), C.c_int32(), C.c_int64()
+    ctx.check(_lib.load().mr_rca_window(ctx.h, dev.h, t0, t1, ptr(a3, C.c_double), ptr(ok, C.c_uint8), 0, 5, prec,
+                                        ptr(codes, C.c_int32), ptr(scores, C.c_double), C.byref(n_out),
+                                        C.byref(edges), C.byref(na), C.byref(nn)), "mr_rca_window")
+    return edges.value, codes[:n_out.value].copy(), scores[:n_out.value].copy(), na.value, nn.value
+
+
+def cpu_baseline(abnormal, t0, t1, a3, ok, target_s=12.0):
+    """The oracle's C restatement of the same window, timed on this host (bounded sample)."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import c_oracle
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    res = c_oracle.rca_window(abnormal, t0, t1, a3, ok, nthreads=threads)   # warm-up + correctness handle
+    n, t_start, edges = 0, time.perf_counter(), 0
+    while True:
+        r = c_oracle.rca_window(abnormal, t0, t1, a3, ok, nthreads=threads)
+        edges += r[4]
+        n += 1
+        el = time.perf_counter() - t_start
+        if el >= target_s or n >= 20:
+            break
+    return {"value": round(edges / el / 1e9, 4), "unit": "GTEPS", "cores": threads, "kind": "port",
+            "sample": f"{n} full C2 windows (detect + 2 graph builds + 2x25 PageRank iterations + spectrum), "
+                      f"oracle/mr_oracle.c OpenMP, {el:.1f} s",
+            "windows_per_s": round(n / el, 4)}, res
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--precision", choices=["fp64", "fp32"], default="fp64")
+    ap.add_argument("--ops", type=int, default=1000)
+    ap.add_argument("--traces", type=int, default=200_000)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # control plane only: barrier + max over ranks (gloo, host)
+
+        dist.init_process_group("gloo")
+    os.environ.setdefault("MICRORANK_DEVICE", str(local))
+
+    from microrank_amd import _lib
+    from microrank_amd.preprocess_data import DeviceSpans
+
+    ctx = _lib.default_context()
+    topo, normal, abnormal = make_window(1234 + 7919 * rank, args.ops, args.traces)
+    a3, ok = slo_from_gpu(ctx, normal)
+    dev = DeviceSpans(ctx, abnormal)              # window spans resident in HBM from here on
+    t0 = int(abnormal.tstart.min())
+    t1 = t0 + 5 * 60 * 10**9
+    prec = _lib.MR_FP32 if args.precision == "fp32" else _lib.MR_FP64
+
+    def barrier():
+        ctx.sync()
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        run_window(ctx, dev, t0, t1, a3, ok, prec)
+    load = _lib.load()
+    load.mr_ctx_profile(ctx.h, 1)
+    barrier()
+    t_start = time.perf_counter()
+    edges = 0
+    for _ in range(args.steps):
+        e, top, scores, na, nn = run_window(ctx, dev, t0, t1, a3, ok, prec)
+        edges += e
+    barrier()
+    elapsed = time.perf_counter() - t_start
+    import ctypes as C
+
+    launches, kms, kbytes = C.c_int64(), C.c_double(), C.c_double()
+    load.mr_ctx_prof_read(ctx.h, C.byref(launches), C.byref(kms), C.byref(kbytes))
+    load.mr_ctx_profile(ctx.h, 0)
+    if dist is not None:
+        import torch
+
+        t = torch.tensor([elapsed, float(edges)], dtype=torch.float64)
+        mx = t.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        sm = t.clone()
+        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        elapsed, edges_all = float(mx[0]), float(sm[1])
+    else:
+        edges_all = float(edges)
+    if rank != 0:
+        if dist is not None:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+    avg_ms = kms.value / max(launches.value, 1)
+    achieved = (kbytes.value / max(launches.value, 1)) / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+    out = {
+        "metric": "PageRank GTEPS + RCA windows ranked/sec at 1/2/4/8 MI355X; % HBM roofline",
+        "value": round(edges_all / elapsed / 1e9, 3),
+        "unit": "GTEPS",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64" if args.precision == "fp64" else "f32",
+        "data": "synthetic (seeded Train-Ticket-like spans, int-coded, resident in HBM)",
+        "config": {"workload": f"C2 RCA window: {args.ops} ops / {args.traces} traces per rank, "
+                               f"detect + 2 graph builds + 2x25 PageRank iterations + DStar2 top-11",
+                   "n_spans": int(abnormal.n_spans), "n_abnormal": na, "n_normal": nn,
+                   "edges_per_window": int(edges // max(args.steps, 1)), "parallelism": f"windows x{world}"},
+        "windows_per_s": round(world * args.steps / elapsed, 3),
+        "roofline": {"bound": "hbm", "kernel": "k_iter (one Jacobi iteration)", "achieved": round(achieved, 1),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": None, "avg_launch_us": round(avg_ms * 1e3, 3), "launches": launches.value,
+                     "bytes_per_launch": round(kbytes.value / max(launches.value, 1))},
+    }
+    if not args.no_cpu:
+        try:
+            cb, cres = cpu_baseline(abnormal, t0, t1, a3, ok)
+            out["cpu_baseline"] = cb
+            out["cpu_top_matches"] = bool(cres is not None and list(cres[0]) == list(top))
+        except Exception as e:  # the baseline must never sink the GPU line
+            out["cpu_baseline"] = {"value": None, "error": f"{type(e).__name__}: {e}"}
+    print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -56,6 +56,11 @@ const char* mr_last_error(const mr_ctx* ctx);
 int         mr_ctx_sync(mr_ctx* ctx);
 /* stream the context launches on (a hipStream_t), for callers that time with HIP events */
 void*       mr_ctx_stream(mr_ctx* ctx);
+/* live timing of the power-iteration kernel: while enabled every launch is bracketed by HIP
+ * events on the context stream; mr_ctx_prof_read syncs, returns the launch count, the summed
+ * kernel time and the summed algorithmic bytes (SURVEY §8(d) B_iter), and clears the record */
+int         mr_ctx_profile(mr_ctx* ctx, int enable);
+int         mr_ctx_prof_read(mr_ctx* ctx, int64_t* launches, double* total_ms, double* total_bytes);
 
 /* ------------------------------------------------------------------ graph from index arrays
  * Replaces the dense matrix fill of pagerank.trace_pagerank (pagerank.py:16-52): the four

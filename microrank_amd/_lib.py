@@ -51,6 +51,8 @@ SIGNATURES = {
     "mr_last_error": (C.c_char_p, [P]),
     "mr_ctx_sync": (C.c_int, [P]),
     "mr_ctx_stream": (P, [P]),
+    "mr_ctx_profile": (C.c_int, [P, C.c_int]),
+    "mr_ctx_prof_read": (C.c_int, [P, i64p, f64p, f64p]),
     "mr_graph_upload": (C.c_int, [P, C.POINTER(GraphDesc), C.POINTER(P)]),
     "mr_graph_free": (C.c_int, [P]),
     "mr_graph_info": (C.c_int, [P, i32p, i32p, i64p, i64p]),

@@ -45,10 +45,59 @@ extern "C" int mr_ctx_create(int device, uint32_t flags, mr_ctx** out) {
 
 void mr_comm_destroy(mr_ctx* ctx);  // mr_comm.cpp
 
+static void prof_clear(mr_ctx* ctx) {
+    for (hipEvent_t e : ctx->prof_ev) (void)hipEventDestroy(e);
+    ctx->prof_ev.clear();
+    ctx->prof_bytes.clear();
+}
+
+extern "C" int mr_ctx_profile(mr_ctx* ctx, int enable) {
+    if (!ctx) return MR_ERR_ARG;
+    (void)hipStreamSynchronize(ctx->stream);
+    prof_clear(ctx);
+    ctx->prof = enable != 0;
+    return MR_OK;
+}
+
+extern "C" int mr_ctx_prof_read(mr_ctx* ctx, int64_t* launches, double* total_ms, double* total_bytes) {
+    if (!ctx) return MR_ERR_ARG;
+    MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    double ms = 0.0, by = 0.0;
+    for (size_t i = 0; i + 1 < ctx->prof_ev.size(); i += 2) {
+        float t = 0.0f;
+        MR_TRY_HIP(ctx, hipEventElapsedTime(&t, ctx->prof_ev[i], ctx->prof_ev[i + 1]));
+        ms += t;
+        by += ctx->prof_bytes[i / 2];
+    }
+    if (launches) *launches = (int64_t)(ctx->prof_ev.size() / 2);
+    if (total_ms) *total_ms = ms;
+    if (total_bytes) *total_bytes = by;
+    prof_clear(ctx);
+    return MR_OK;
+}
+
+// bracket a launch with events when profiling (called by the power iteration)
+void mr_prof_begin(mr_ctx* ctx) {
+    if (!ctx->prof) return;
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return;
+    (void)hipEventRecord(e, ctx->stream);
+    ctx->prof_ev.push_back(e);
+}
+void mr_prof_end(mr_ctx* ctx, double bytes) {
+    if (!ctx->prof) return;
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return;
+    (void)hipEventRecord(e, ctx->stream);
+    ctx->prof_ev.push_back(e);
+    ctx->prof_bytes.push_back(bytes);
+}
+
 extern "C" void mr_ctx_destroy(mr_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     mr_comm_destroy(ctx);
+    prof_clear(ctx);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }

@@ -1,0 +1,286 @@
+// K5: anormaly_detector.system_anomaly_detect (anormaly_detector.py:44-84) with
+// preprocess_data.get_operation_duration_data (preprocess_data.py:309-334), and the whole
+// RCA window of online_rca.online_anomaly_detect_RCA (online_rca.py:320-371) on the device.
+//
+// Detector: spans whose trace-level [start, end] lies in [t0, t1] (inclusive, T15) are sorted
+// by (trace, service-op); per trace, expect = sum over its ops in name order of
+// count * (mean + 3 std), ops without an SLO adding nothing (the reference's bare except),
+// real = max duration / 1000, abnormal iff real > expect (strict), traces with max <= 0
+// dropped (:329).  The sum is sequential per trace with separate multiply and add (T14), so
+// the partition is bit-exact.
+#include <algorithm>
+
+#include "mr_prim.h"
+#include "mr_sort.h"
+
+int mr_graph_build_dev(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d_mask, mr_graph** out);
+int mr_spectrum_dev(mr_ctx* ctx, int32_t n, const uint8_t* flags, const double* a_w, const int64_t* a_num,
+                    const double* n_w, const int64_t* n_num, int64_t A, int64_t Nl, int method, int32_t top,
+                    int32_t* d_out_idx, double* d_out_score, uint8_t* d_out_np, int32_t* d_zflag);
+
+namespace {
+__global__ void k_win_flags(const int64_t* ts, const int64_t* te, int64_t S, int64_t t0, int64_t t1, int32_t* flag) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < S) flag[i] = (ts[i] >= t0 && te[i] <= t1) ? 1 : 0;
+}
+__global__ void k_win_keys(const int32_t* flag, const int64_t* pos, int64_t S, const int32_t* trace, const int32_t* svcop,
+                           const int64_t* dur, int nb, uint64_t* keys, long long* tmax) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= S || !flag[i]) return;
+    keys[pos[i]] = ((uint64_t)(uint32_t)trace[i] << nb) | (uint32_t)svcop[i];
+    atomicMax(&tmax[trace[i]], (long long)dur[i]);
+}
+__global__ void k_win_runs(const uint64_t* keys, int64_t n, int32_t* head) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) head[i] = (i == 0 || keys[i] != keys[i - 1]) ? 1 : 0;
+}
+// runs -> (key, count); first run of each trace
+__global__ void k_win_run_out(const uint64_t* keys, const int32_t* head, const int64_t* hpos, int64_t n, int nb,
+                              uint64_t* rkey, int64_t* rstart, int64_t* tfirst) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || !head[i]) return;
+    const int64_t r = hpos[i];
+    rkey[r] = keys[i];
+    rstart[r] = i;
+    const uint64_t t = keys[i] >> nb;
+    if (i == 0 || (keys[i - 1] >> nb) != t) tfirst[t] = r;
+}
+__global__ void k_win_traces(const uint64_t* rkey, const int64_t* rstart, int64_t nruns, int64_t nspan, int nb,
+                             const int64_t* tfirst, const long long* tmax, const double* a3, const uint8_t* a3v,
+                             int32_t n_traces, uint8_t* state, int32_t* counts) {
+    const int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n_traces) return;
+    const int64_t r0 = tfirst[t];
+    if (r0 < 0) {
+        state[t] = 0;
+        return;
+    }
+    const long long mx = tmax[t];
+    if (!(mx > 0)) {   // grouped[grouped['duration'] > 0] (preprocess_data.py:329)
+        state[t] = 0;
+        return;
+    }
+    double expect = 0.0;
+    const uint64_t mask = (1ull << nb) - 1ull;
+    for (int64_t r = r0; r < nruns && (rkey[r] >> nb) == (uint64_t)t; ++r) {
+        const int32_t op = (int32_t)(rkey[r] & mask);
+        const int64_t end = r + 1 < nruns ? rstart[r + 1] : nspan;
+        const int64_t cnt = end - rstart[r];
+        if (a3v[op]) expect += (double)cnt * a3[op];   // anormaly_detector.py:64-65
+    }
+    const double real = (double)mx / 1000.0;           // :58
+    const bool ab = real > expect;                     // :69
+    state[t] = ab ? 2 : 1;
+    atomicAdd(&counts[ab ? 0 : 1], 1);
+}
+__global__ void k_fill_i64(int64_t* p, int64_t n, int64_t v) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = v;
+}
+
+// union of the two graphs' nodes in the reference's spectrum order (online_rca.py:201-225)
+__global__ void k_union_a(const int32_t* a_podop, int32_t Na, const double* a_w, const int32_t* a_cov, int32_t* pos_of_code,
+                          uint8_t* flags, double* ua_w, int64_t* ua_num, int32_t* uc) {
+    int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= Na) return;
+    pos_of_code[a_podop[i]] = i;
+    flags[i] = 1 | 4 | 8;   // in anomaly_result; np.float64 weights on both sides
+    ua_w[i] = a_w[i];
+    ua_num[i] = a_cov[i];
+    uc[i] = a_podop[i];
+}
+__global__ void k_union_n_flags(const int32_t* n_podop, int32_t Nn, const int32_t* pos_of_code, int32_t* only) {
+    int32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < Nn) only[j] = pos_of_code[n_podop[j]] < 0 ? 1 : 0;
+}
+__global__ void k_union_n(const int32_t* n_podop, int32_t Nn, const double* n_w, const int32_t* n_cov,
+                          const int32_t* pos_of_code, const int32_t* only, const int64_t* opos, int32_t Na,
+                          uint8_t* flags, double* ua_w, int64_t* ua_num, double* un_w, int64_t* un_num, int32_t* uc) {
+    int32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= Nn) return;
+    const int32_t c = n_podop[j];
+    int32_t p;
+    if (only[j]) {
+        p = Na + (int32_t)opos[j];
+        flags[p] = 2 | 8;
+        ua_w[p] = 0.0;
+        ua_num[p] = 0;
+        uc[p] = c;
+    } else {
+        p = pos_of_code[c];
+        flags[p] = 1 | 2 | 4 | 8;
+    }
+    un_w[p] = n_w[j];
+    un_num[p] = n_cov[j];
+}
+}  // namespace
+
+// Detector on the device; d_state[n_traces] receives 0/1/2.  Returns MR_ERR_VALUE for an empty window.
+static int detect_dev(mr_ctx* ctx, const mr_spans* s, int64_t t0, int64_t t1, const double* d_a3, const uint8_t* d_a3v,
+                      uint8_t* d_state, int32_t* n_abn, int32_t* n_nor, int64_t* n_in) {
+    hipStream_t st = ctx->stream;
+    const int64_t S = s->S;
+    const int32_t NT = s->n_traces, NO = s->n_svcops;
+    if (!s->has_times) return mr_fail(ctx, MR_ERR_ARG, "spans have no startTime/endTime columns");
+    DBuf<int32_t> flag;
+    DBuf<int64_t> pos, tmp;
+    MR_TRY(flag.alloc(ctx, S));
+    MR_TRY(pos.alloc(ctx, S + 1));
+    MR_TRY(tmp.alloc(ctx, std::max<int64_t>(scan_tmp_elems(S), 1)));
+    if (S) hipLaunchKernelGGL(k_win_flags, dim3(cdiv(S, 256)), dim3(256), 0, st, s->tstart.p, s->tend.p, S, t0, t1, flag.p);
+    MR_TRY(mr_exclusive_scan_i32(ctx, flag.p, pos.p, S, tmp.p));
+    int64_t W = 0;
+    MR_TRY_HIP(ctx, hipMemcpyAsync(&W, pos.p + S, sizeof W, hipMemcpyDeviceToHost, st));
+    MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+    *n_in = W;
+    if (W == 0) return mr_fail(ctx, MR_ERR_VALUE, "Current span list is empty");
+    const int nb = std::max(1, bits_for((uint64_t)std::max(NO - 1, 0)));
+    DBuf<uint64_t> keys;
+    DBuf<long long> tmax;
+    MR_TRY(keys.alloc(ctx, W));
+    MR_TRY(tmax.alloc(ctx, NT));
+    MR_TRY_HIP(ctx, hipMemsetAsync(tmax.p, 0x80, NT * sizeof(long long), st));   // very negative
+    hipLaunchKernelGGL(k_win_keys, dim3(cdiv(S, 256)), dim3(256), 0, st, flag.p, pos.p, S, s->trace.p, s->svcop.p,
+                       s->duration.p, nb, keys.p, tmax.p);
+    SortScratch ws;
+    MR_TRY(mr_radix_sort(ctx, keys.p, nullptr, W, nb + bits_for((uint64_t)std::max(NT - 1, 0)), ws));
+    DBuf<int32_t> head;
+    DBuf<int64_t> hpos;
+    MR_TRY(head.alloc(ctx, W));
+    MR_TRY(hpos.alloc(ctx, W + 1));
+    hipLaunchKernelGGL(k_win_runs, dim3(cdiv(W, 256)), dim3(256), 0, st, keys.p, W, head.p);
+    MR_TRY(mr_exclusive_scan_i32(ctx, head.p, hpos.p, W, tmp.p));
+    int64_t R = 0;
+    MR_TRY_HIP(ctx, hipMemcpyAsync(&R, hpos.p + W, sizeof R, hipMemcpyDeviceToHost, st));
+    MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+    DBuf<uint64_t> rkey;
+    DBuf<int64_t> rstart, tfirst;
+    DBuf<int32_t> counts;
+    MR_TRY(rkey.alloc(ctx, R));
+    MR_TRY(rstart.alloc(ctx, R));
+    MR_TRY(tfirst.alloc(ctx, NT));
+    MR_TRY(counts.zero(ctx, 2));
+    hipLaunchKernelGGL(k_fill_i64, dim3(cdiv(NT, 256)), dim3(256), 0, st, tfirst.p, (int64_t)NT, (int64_t)-1);
+    hipLaunchKernelGGL(k_win_run_out, dim3(cdiv(W, 256)), dim3(256), 0, st, keys.p, head.p, hpos.p, W, nb, rkey.p,
+                       rstart.p, tfirst.p);
+    hipLaunchKernelGGL(k_win_traces, dim3(cdiv(NT, 256)), dim3(256), 0, st, rkey.p, rstart.p, R, W, nb, tfirst.p, tmax.p,
+                       d_a3, d_a3v, NT, d_state, counts.p);
+    MR_TRY_HIP(ctx, hipGetLastError());
+    int32_t hc[2];
+    MR_TRY(counts.download(ctx, hc, 2));
+    MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+    *n_abn = hc[0];
+    *n_nor = hc[1];
+    return MR_OK;
+}
+
+extern "C" int mr_detect(mr_ctx* ctx, const mr_spans* s, int64_t t0, int64_t t1, const double* a3, const uint8_t* a3_valid,
+                         uint8_t* state, int32_t* n_abnormal, int32_t* n_normal, int64_t* n_spans_in_window) {
+    if (!ctx || !s || s->ctx != ctx || !a3 || !a3_valid || !state || !n_abnormal || !n_normal || !n_spans_in_window)
+        return mr_fail(ctx, MR_ERR_ARG, "mr_detect: bad arguments");
+    MR_TRY_HIP(ctx, hipSetDevice(ctx->device));
+    DBuf<double> da3;
+    DBuf<uint8_t> dv, dst;
+    MR_TRY(da3.upload(ctx, a3, s->n_svcops));
+    MR_TRY(dv.upload(ctx, a3_valid, s->n_svcops));
+    MR_TRY(dst.zero(ctx, s->n_traces));
+    *n_abnormal = *n_normal = 0;
+    MR_TRY(detect_dev(ctx, s, t0, t1, da3.p, dv.p, dst.p, n_abnormal, n_normal, n_spans_in_window));
+    MR_TRY(dst.download(ctx, state, s->n_traces));
+    MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return MR_OK;
+}
+
+namespace {
+__global__ void k_masks(const uint8_t* state, int32_t n, uint8_t* m_abn, uint8_t* m_nor) {
+    int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    m_abn[t] = state[t] == 2;
+    m_nor[t] = state[t] == 1;
+}
+__global__ void k_top_codes(const int32_t* idx, const int32_t* uc, int32_t k, int32_t* out) {
+    int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < k) out[i] = uc[idx[i]];
+}
+}  // namespace
+
+// One RCA window (online_rca.py:320-371) with every intermediate in HBM.
+extern "C" int mr_rca_window(mr_ctx* ctx, const mr_spans* s, int64_t t0, int64_t t1, const double* a3,
+                             const uint8_t* a3_valid, int method, int32_t top_max, int precision, int32_t* out_podop,
+                             double* out_score, int32_t* n_out, int64_t* edges_traversed, int32_t* n_abnormal,
+                             int32_t* n_normal) {
+    if (!ctx || !s || s->ctx != ctx || !a3 || !a3_valid || !n_out) return mr_fail(ctx, MR_ERR_ARG, "mr_rca_window: bad arguments");
+    MR_TRY_HIP(ctx, hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    *n_out = 0;
+    if (edges_traversed) *edges_traversed = 0;
+    const int32_t NT = s->n_traces, NP = s->n_podops;
+    DBuf<double> da3;
+    DBuf<uint8_t> dv, dst, m_abn, m_nor;
+    MR_TRY(da3.upload(ctx, a3, s->n_svcops));
+    MR_TRY(dv.upload(ctx, a3_valid, s->n_svcops));
+    MR_TRY(dst.zero(ctx, NT));
+    int32_t na = 0, nn = 0;
+    int64_t nin = 0;
+    MR_TRY(detect_dev(ctx, s, t0, t1, da3.p, dv.p, dst.p, &na, &nn, &nin));
+    if (n_abnormal) *n_abnormal = na;
+    if (n_normal) *n_normal = nn;
+    // T1: the driver unpacks (flag, normal_list, abnormal_list) from (flag, abnormal, normal)
+    if (na == 0 || nn == 0) return MR_OK;   // no anomaly, or one list empty: nothing is ranked
+    MR_TRY(m_abn.alloc(ctx, NT));
+    MR_TRY(m_nor.alloc(ctx, NT));
+    hipLaunchKernelGGL(k_masks, dim3(cdiv(NT, 256)), dim3(256), 0, st, dst.p, NT, m_abn.p, m_nor.p);
+    mr_graph *gn = nullptr, *ga = nullptr;
+    int rc = mr_graph_build_dev(ctx, s, m_abn.p, &gn);   // "normal" graph = detector's abnormal traces
+    if (rc == MR_OK) rc = mr_graph_build_dev(ctx, s, m_nor.p, &ga);
+    if (rc == MR_OK) rc = mr_pagerank(ctx, gn, 0, 0.85, 0.01, 25, precision, 0);
+    if (rc == MR_OK) rc = mr_pagerank(ctx, ga, 1, 0.85, 0.01, 25, precision, 0);
+    if (rc != MR_OK) {
+        delete gn;
+        delete ga;
+        return rc;
+    }
+    if (edges_traversed) *edges_traversed = 25 * (2 * (gn->nnz_sr + ga->nnz_sr) + gn->E + ga->E);
+    // spectrum over the union (anomaly nodes, then normal-only nodes)
+    const int32_t Na = ga->N, Nn = gn->N;
+    DBuf<int32_t> pos_of_code, only, uc, idx, zf;
+    DBuf<int64_t> opos, tmp, ua_num, un_num;
+    DBuf<uint8_t> fl;
+    DBuf<double> ua_w, un_w, sc;
+    const int32_t U = Na + Nn;   // upper bound
+    auto cleanup = [&](int code) {
+        delete gn;
+        delete ga;
+        return code;
+    };
+    if ((rc = pos_of_code.alloc(ctx, NP)) || (rc = only.alloc(ctx, Nn)) || (rc = uc.alloc(ctx, U)) ||
+        (rc = opos.alloc(ctx, Nn + 1)) || (rc = tmp.alloc(ctx, scan_tmp_elems(Nn))) || (rc = ua_num.zero(ctx, U)) ||
+        (rc = un_num.zero(ctx, U)) || (rc = fl.zero(ctx, U)) || (rc = ua_w.zero(ctx, U)) || (rc = un_w.zero(ctx, U)) ||
+        (rc = zf.zero(ctx, 1)))
+        return cleanup(rc);
+    if (hipMemsetAsync(pos_of_code.p, 0xff, NP * sizeof(int32_t), st) != hipSuccess) return cleanup(MR_ERR_HIP);
+    hipLaunchKernelGGL(k_union_a, dim3(cdiv(Na, 256)), dim3(256), 0, st, ga->node_podop.p, Na, ga->weight.p, ga->cov.p,
+                       pos_of_code.p, fl.p, ua_w.p, ua_num.p, uc.p);
+    hipLaunchKernelGGL(k_union_n_flags, dim3(cdiv(Nn, 256)), dim3(256), 0, st, gn->node_podop.p, Nn, pos_of_code.p, only.p);
+    if ((rc = mr_exclusive_scan_i32(ctx, only.p, opos.p, Nn, tmp.p))) return cleanup(rc);
+    int64_t nonly = 0;
+    if (hipMemcpyAsync(&nonly, opos.p + Nn, sizeof nonly, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+        return cleanup(MR_ERR_HIP);
+    hipLaunchKernelGGL(k_union_n, dim3(cdiv(Nn, 256)), dim3(256), 0, st, gn->node_podop.p, Nn, gn->weight.p, gn->cov.p,
+                       pos_of_code.p, only.p, opos.p, Na, fl.p, ua_w.p, ua_num.p, un_w.p, un_num.p, uc.p);
+    const int32_t n = Na + (int32_t)nonly;
+    const int32_t k = std::min(n, std::max(0, top_max + 6));   // online_rca.py:304
+    if ((rc = idx.alloc(ctx, std::max(k, 1))) || (rc = sc.alloc(ctx, std::max(k, 1)))) return cleanup(rc);
+    // A = len(abnormal_list) = detector normal count, N = len(normal_list) = detector abnormal count
+    rc = mr_spectrum_dev(ctx, n, fl.p, ua_w.p, ua_num.p, un_w.p, un_num.p, nn, na, method, k, idx.p, sc.p, nullptr, zf.p);
+    if (rc) return cleanup(rc);
+    DBuf<int32_t> codes;
+    if ((rc = codes.alloc(ctx, std::max(k, 1)))) return cleanup(rc);
+    if (k) hipLaunchKernelGGL(k_top_codes, dim3(cdiv(k, 256)), dim3(256), 0, st, idx.p, uc.p, k, codes.p);
+    if (k && out_podop && (rc = codes.download(ctx, out_podop, k))) return cleanup(rc);
+    if (k && out_score && (rc = sc.download(ctx, out_score, k))) return cleanup(rc);
+    if (hipStreamSynchronize(st) != hipSuccess) return cleanup(MR_ERR_HIP);
+    *n_out = k;
+    return cleanup(MR_OK);
+}

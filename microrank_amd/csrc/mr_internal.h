@@ -20,6 +20,11 @@ struct mr_ctx {
     // RCCL (loaded lazily with dlopen so the library loads without it)
     void* comm = nullptr;
     int rank = 0, nranks = 1;
+    // live kernel timing of the power-iteration launches (mr_ctx_profile): event pairs on the
+    // context stream plus the algorithmic bytes of each launch
+    bool prof = false;
+    std::vector<hipEvent_t> prof_ev;
+    std::vector<double> prof_bytes;
 };
 
 int mr_fail(mr_ctx* ctx, int code, const char* fmt, ...);
@@ -123,6 +128,7 @@ struct mr_graph {
     DBuf<double> sub[2];         // [N] u_o * s'[o]
     DBuf<double> sn;             // [N] final normalised s
     DBuf<double> scal;           // [8] M_s, M_r, sums
+    DBuf<double> ppart;          // preference-sum block partials
     DBuf<double> weight;         // [N]
     DBuf<uint64_t> ht_key;       // kinds hash table
     DBuf<uint32_t> ht_cnt;

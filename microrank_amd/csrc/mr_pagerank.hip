@@ -14,7 +14,9 @@
 // atomicMax, which is exact and order-independent.  Normalisation of r is deferred:
 // sum_t w_t (r'_t / M_r) is evaluated as (sum_t w_t r'_t) / M_r.  Every float reduction has a
 // fixed order (no float atomics), so results are bitwise reproducible run to run.
+#include <algorithm>
 #include <cmath>
+#include <cstdlib>
 
 #include "mr_internal.h"
 #include "mr_prim.h"
@@ -31,6 +33,23 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     return z ^ (z >> 31);
+}
+
+__global__ void k_pr_reset(int32_t T, int64_t cap, int32_t N, float* pref, float* c_t, uint64_t* hk, uint32_t* hc,
+                           int32_t* hr, uint32_t* op_cnt, int32_t* flag, double* scal) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < T) {
+        pref[i] = 0.0f;
+        c_t[i] = 0.0f;
+    }
+    if (i < cap) {
+        hk[i] = 0ull;
+        hc[i] = 0u;
+        hr[i] = -1;
+    }
+    if (i < N) op_cnt[i] = 0u;
+    if (i < 4) flag[i] = 0;
+    if (i < 8) scal[i] = 0.0;
 }
 
 // ---------------------------------------------------------------- graph constants
@@ -214,6 +233,9 @@ __global__ void k_pref_apply(const double* kind, const int32_t* pr_trace, const 
 }
 
 // ---------------------------------------------------------------- iteration
+// M_s / M_r per iteration live in MSH shards (an atomicMax per block or op on ONE word would
+// serialise ~2k same-address atomics per iteration); readers reduce the shards.
+constexpr int MSH = 64;
 __device__ __forceinline__ double bits2d(unsigned long long b) { return __longlong_as_double((long long)b); }
 __device__ __forceinline__ unsigned long long d2bits(double v) {
     return (unsigned long long)__double_as_longlong(v);
@@ -231,7 +253,8 @@ __global__ void k_iter_init(const float* w_t, const float* u_o, int32_t N, int32
         double q = (double)w_t[i] * v0;
         if (fp32) q32[i] = (float)q; else q64[i] = q;
     }
-    if (i < 6) mslot[i] = i < 2 ? d2bits(1.0) : 0ull;   // M_s(0) = M_r(0) = 1: s_0, r_0 used as is
+    // M_s(0) = M_r(0) = 1: s_0, r_0 are used as they are; slots 1, 2 start cleared
+    if (i < 6 * MSH) mslot[i] = i < 2 * MSH ? d2bits(1.0) : 0ull;
 }
 
 // One Jacobi iteration k -> k+1 in ONE launch.  Maxima are exchanged as the bit patterns of
@@ -239,7 +262,7 @@ __global__ void k_iter_init(const float* w_t, const float* u_o, int32_t N, int32
 // (M_s(k), M_r(k)), slot (k+1)%3 collects iteration k+1, slot (k+2)%3 is cleared here for k+2.
 // s' is carried unnormalised together with su'[o] = u_o * s'[o]; the division by M_s(k) is
 // applied to each finished sum instead of to every term.
-template <class Q>
+template <class Q, int VW>
 __global__ void __launch_bounds__(TB) k_iter(
     // trace role
     const int64_t* __restrict__ rs_off, const int32_t* __restrict__ rs_ops, const double* __restrict__ su_cur,
@@ -254,44 +277,96 @@ __global__ void __launch_bounds__(TB) k_iter(
     unsigned long long* mslot, int k3) {
     extern __shared__ double lds[];
     __shared__ double red[TB / WAVE];
-    const double Ms = bits2d(mslot[2 * k3]), Mr = bits2d(mslot[2 * k3 + 1]);
-    unsigned long long* Mnext = mslot + 2 * ((k3 + 1) % 3);
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        mslot[2 * ((k3 + 2) % 3)] = 0ull;
-        mslot[2 * ((k3 + 2) % 3) + 1] = 0ull;
+    __shared__ double msr[2];
+    // slot layout: [k%3][s|r][MSH]
+    const unsigned long long* Mcur = mslot + (size_t)2 * MSH * k3;
+    unsigned long long* Mnext = mslot + (size_t)2 * MSH * ((k3 + 1) % 3);
+    if (blockIdx.x == 0 && threadIdx.x < 2 * MSH) mslot[(size_t)2 * MSH * ((k3 + 2) % 3) + threadIdx.x] = 0ull;
+    if (threadIdx.x < WAVE) {
+        double ms = bits2d(Mcur[threadIdx.x]), mr = bits2d(Mcur[MSH + threadIdx.x]);
+        ms = wave_max(ms);
+        mr = wave_max(mr);
+        if (threadIdx.x == 0) {
+            msr[0] = ms;
+            msr[1] = mr;
+        }
     }
+    __syncthreads();
+    const double Ms = msr[0], Mr = msr[1];
+    const int shard = blockIdx.x % MSH;
     if ((int32_t)blockIdx.x < n_tblocks) {
         // ---- trace role: r'[t] = d * (sum_o u_o s'_k[o]) / M_s(k) + c_t  (pagerank.py:125)
         const double* su = su_cur;
-        double* vals = lds + (lds_su ? N : 0);
         if (lds_su) {
             for (int32_t o = threadIdx.x; o < N; o += TB) lds[o] = su_cur[o];
             su = lds;
         }
-        const int32_t t0 = blockIdx.x * TB;
-        const int32_t t1 = min(t0 + TB, T);
-        const int64_t e0 = rs_off[t0], e1 = rs_off[t1];
-        const int32_t t = t0 + threadIdx.x;
-        const bool own = t < T;
-        const int64_t a = own ? rs_off[t] : 0, b = own ? rs_off[t + 1] : 0;
-        double acc = 0.0;
-        // the block's contiguous id range in rounds of VCAP: coalesced id reads, LDS gather of
-        // su', then every thread continues its own trace's sum in node order
-        for (int64_t lo = e0; lo < e1; lo += VCAP) {
-            const int64_t hi = min(lo + (int64_t)VCAP, e1);
-            __syncthreads();
-            for (int64_t e = lo + threadIdx.x; e < hi; e += TB) vals[e - lo] = su[rs_ops[e]];
-            __syncthreads();
-            const int64_t x0 = max(a, lo), x1 = min(b, hi);
-            for (int64_t e = x0; e < x1; ++e) acc += vals[e - lo];
+        double rmax = -__builtin_huge_val();
+        if (VW == 0) {
+            // LDS-staged: the block's contiguous id range is read coalesced in rounds of VCAP ids
+            // (all loads in flight before any gather), su' gathered into LDS, then each thread
+            // continues its own trace's sum in node order
+            double* vals = lds + (lds_su ? N : 0);
+            const int32_t t0 = blockIdx.x * TB;
+            const int32_t t1 = min(t0 + TB, T);
+            const int64_t e0 = rs_off[t0], e1 = rs_off[t1];
+            const int32_t t = t0 + threadIdx.x;
+            const bool own = t < T;
+            const int64_t a = own ? rs_off[t] : 0, b = own ? rs_off[t + 1] : 0;
+            double acc = 0.0;
+            for (int64_t lo = e0; lo < e1; lo += VCAP) {
+                const int64_t hi = min(lo + (int64_t)VCAP, e1);
+                __syncthreads();
+                int32_t id[VCAP / TB];
+#pragma unroll
+                for (int j = 0; j < VCAP / TB; ++j) id[j] = rs_ops[min(lo + threadIdx.x + (int64_t)j * TB, hi - 1)];
+#pragma unroll
+                for (int j = 0; j < VCAP / TB; ++j) {
+                    const int64_t e = lo + threadIdx.x + (int64_t)j * TB;
+                    if (e < hi) vals[e - lo] = su[id[j]];
+                }
+                __syncthreads();
+                const int64_t x0 = max(a, lo), x1 = min(b, hi);
+                int64_t e = x0;
+                for (; e + 4 <= x1; e += 4) {
+                    const double v0 = vals[e - lo], v1 = vals[e + 1 - lo], v2 = vals[e + 2 - lo], v3 = vals[e + 3 - lo];
+                    acc += v0;
+                    acc += v1;
+                    acc += v2;
+                    acc += v3;
+                }
+                for (; e < x1; ++e) acc += vals[e - lo];
+            }
+            if (own) {
+                const double rp = d * (acc / Ms) + (double)c_t[t];
+                q_next[t] = (Q)((double)w_t[t] * rp);
+                rmax = rp;
+            }
+        } else {
+            // CSR-vector: VW lanes per trace, coalesced ids, LDS gather, fixed butterfly
+            if (lds_su) __syncthreads();
+            constexpr int VWE = VW > 0 ? VW : 1;
+            constexpr int G = TB / VWE;
+            const int grp = threadIdx.x / VWE, gl = threadIdx.x % VWE;
+#pragma unroll 4
+            for (int step = 0; step < VWE; ++step) {
+                const int32_t t = (int32_t)blockIdx.x * TB + step * G + grp;
+                double acc = 0.0;
+                if (t < T) {
+                    const int64_t a = rs_off[t], b = rs_off[t + 1];
+                    for (int64_t e = a + gl; e < b; e += VWE) acc += su[rs_ops[e]];
+                }
+#pragma unroll
+                for (int m = VWE / 2; m >= 1; m >>= 1) acc += __shfl_xor(acc, m, WAVE);
+                if (gl == 0 && t < T) {
+                    const double rp = d * (acc / Ms) + (double)c_t[t];
+                    q_next[t] = (Q)((double)w_t[t] * rp);
+                    rmax = nmax(rmax, rp);
+                }
+            }
         }
-        double rp = -__builtin_huge_val();
-        if (own) {
-            rp = d * (acc / Ms) + (double)c_t[t];
-            q_next[t] = (Q)((double)w_t[t] * rp);
-        }
-        rp = block_max(rp, red);
-        if (threadIdx.x == 0) atomicMax(&Mnext[1], d2bits(rp));
+        rmax = block_max(rmax, red);
+        if (threadIdx.x == 0) atomicMax(&Mnext[MSH + shard], d2bits(rmax));
         return;
     }
     // ---- op role: one wave per fixed segment of an op's trace list  (pagerank.py:122-124)
@@ -302,7 +377,17 @@ __global__ void __launch_bounds__(TB) k_iter(
     const int64_t b = seg_beg[seg];
     const int64_t end = min(b + (int64_t)SEG, sr_off[o + 1]);
     double acc = 0.0;
-    for (int64_t e = b + lane; e < end; e += WAVE) acc += (double)q_cur[sr_trs[e]];
+    if (end > b) {   // ids first, then every gather, then the sum in element order
+        int32_t id[SEG / WAVE];
+#pragma unroll
+        for (int j = 0; j < SEG / WAVE; ++j) id[j] = sr_trs[min(b + lane + (int64_t)j * WAVE, end - 1)];
+        double v[SEG / WAVE];
+#pragma unroll
+        for (int j = 0; j < SEG / WAVE; ++j) v[j] = (double)q_cur[id[j]];
+#pragma unroll
+        for (int j = 0; j < SEG / WAVE; ++j)
+            if (b + lane + (int64_t)j * WAVE < end) acc += v[j];
+    }
     acc = wave_sum(acc);
     const int32_t s0 = op_seg[o], s1 = op_seg[o + 1];
     uint32_t old = 0;
@@ -337,7 +422,7 @@ __global__ void __launch_bounds__(TB) k_iter(
         const double v = d * (sum / Mr + alpha * (bb / Ms));      // pagerank.py:122-124
         sp_next[o] = v;
         su_next[o] = (double)u_o[o] * v;
-        atomicMax(&Mnext[0], d2bits(v));
+        atomicMax(&Mnext[o % MSH], d2bits(v));
     }
 }
 
@@ -346,7 +431,9 @@ __global__ void __launch_bounds__(1024) k_weights(const double* sp, const unsign
                                                   int32_t N, int exact, double* sn, double* weight, double* scal) {
     __shared__ double red[1024 / WAVE];
     __shared__ double tot;
-    const double Ms = bits2d(mslot[2 * k3]);
+    double ms = -__builtin_huge_val();
+    for (int i = threadIdx.x; i < MSH; i += blockDim.x) ms = nmax(ms, bits2d(mslot[(size_t)2 * MSH * k3 + i]));
+    const double Ms = block_max(ms, red);
     double m = -__builtin_huge_val();
     for (int32_t o = threadIdx.x; o < N; o += blockDim.x) {
         double v = sp[o] / Ms;
@@ -377,9 +464,50 @@ __global__ void __launch_bounds__(1024) k_weights(const double* sp, const unsign
     if (threadIdx.x == 0) scal[4] = total;
 }
 
+template <class Q> Q* qbuf(mr_graph* g, int i);
+template <> double* qbuf<double>(mr_graph* g, int i) { return g->q64[i].p; }
+template <> float* qbuf<float>(mr_graph* g, int i) { return g->q32[i].p; }
+
+template <class Q, int VW>
+void launch_iter_vw(mr_ctx* ctx, mr_graph* g, int n_tb, int n_oblocks, size_t lds, double d, double alpha,
+                    int lds_su, int cur, int nxt, int it) {
+    hipLaunchKernelGGL((k_iter<Q, VW>), dim3(n_tb + n_oblocks), dim3(TB), lds, ctx->stream, g->rs_off.p, g->rs_ops.p,
+                       g->sub[cur].p, g->c_t.p, g->w_t.p, qbuf<Q>(g, nxt), g->T, g->N, n_tb, d, alpha, lds_su,
+                       g->sr_off.p, g->sr_trs.p, g->seg_op.p, g->seg_beg.p, g->op_seg.p, qbuf<Q>(g, cur), g->part.p,
+                       g->nseg, g->op_cnt.p, (uint32_t)(it + 1), g->ss_off.p, g->ss_par.p, g->pw.p, g->u_o.p,
+                       g->spb[cur].p, g->spb[nxt].p, g->sub[nxt].p, g->mslot.p, it % 3);
+}
+
+template <class Q>
+int launch_iter(mr_ctx* ctx, mr_graph* g, int vw, int n_tb, int n_oblocks, size_t lds, double d, double alpha,
+                int lds_su, int cur, int nxt, int it) {
+    switch (vw) {
+        case 4: launch_iter_vw<Q, 4>(ctx, g, n_tb, n_oblocks, lds, d, alpha, lds_su, cur, nxt, it); break;
+        case 8: launch_iter_vw<Q, 8>(ctx, g, n_tb, n_oblocks, lds, d, alpha, lds_su, cur, nxt, it); break;
+        case 16: launch_iter_vw<Q, 16>(ctx, g, n_tb, n_oblocks, lds, d, alpha, lds_su, cur, nxt, it); break;
+        case 32: launch_iter_vw<Q, 32>(ctx, g, n_tb, n_oblocks, lds, d, alpha, lds_su, cur, nxt, it); break;
+        case 64: launch_iter_vw<Q, 64>(ctx, g, n_tb, n_oblocks, lds, d, alpha, lds_su, cur, nxt, it); break;
+        default: launch_iter_vw<Q, 0>(ctx, g, n_tb, n_oblocks, lds, d, alpha, lds_su, cur, nxt, it); break;
+    }
+    return MR_OK;
+}
 }  // namespace
 
 // ------------------------------------------------------------------------------ host side
+// MR_DEBUG=1: check every launch (names the failing kernel instead of a later sticky error)
+static const bool g_debug = getenv("MR_DEBUG") != nullptr;
+#define MR_DEBUG_CHECK(ctx, name)                                                                          \
+    do {                                                                                                   \
+        if (g_debug) {                                                                                     \
+            hipError_t e_ = hipGetLastError();                                                             \
+            if (e_ == hipSuccess) e_ = hipStreamSynchronize((ctx)->stream);                                \
+            if (e_ != hipSuccess) return mr_fail((ctx), MR_ERR_HIP, "%s: %s", name, hipGetErrorString(e_)); \
+        }                                                                                                  \
+    } while (0)
+
+void mr_prof_begin(mr_ctx* ctx);
+void mr_prof_end(mr_ctx* ctx, double bytes);
+
 int mr_graph_prepare(mr_ctx* ctx, mr_graph* g) {
     const int32_t N = g->N, T = g->T;
     MR_TRY(g->w_t.alloc(ctx, (size_t)T));
@@ -421,11 +549,22 @@ extern "C" int mr_pagerank(mr_ctx* ctx, mr_graph* g, int anomaly, double d, doub
     hipStream_t st = ctx->stream;
     const bool fp32 = precision == MR_FP32;
     const int n_tblocks = cdiv(T, TB);
+    uint64_t cap = 1;
+    while (cap < 2ull * (uint64_t)T) cap <<= 1;
+    const int32_t n_pr = g->n_pr;
+    const int nbp = cdiv(n_pr > 0 ? n_pr : 1, TB);
     MR_TRY(g->kind.alloc(ctx, (size_t)T));
-    MR_TRY(g->pref.zero(ctx, (size_t)T));
-    MR_TRY(g->c_t.zero(ctx, (size_t)T));
-    MR_TRY(g->flag.zero(ctx, 4));
-    MR_TRY(g->scal.zero(ctx, 8));
+    MR_TRY(g->pref.alloc(ctx, (size_t)T));
+    MR_TRY(g->c_t.alloc(ctx, (size_t)T));
+    MR_TRY(g->flag.alloc(ctx, 4));
+    MR_TRY(g->scal.alloc(ctx, 8));
+    MR_TRY(g->ppart.alloc(ctx, 2 * (size_t)nbp));
+    MR_TRY(g->ht_key.alloc(ctx, cap));
+    MR_TRY(g->ht_cnt.alloc(ctx, cap));
+    MR_TRY(g->ht_rep.alloc(ctx, cap));
+    MR_TRY(g->slot_of.alloc(ctx, (size_t)T));
+    MR_TRY(g->op_cnt.alloc(ctx, (size_t)N));
+    MR_TRY(g->mslot.alloc(ctx, 6 * MSH));
     MR_TRY(g->sn.alloc(ctx, (size_t)N));
     MR_TRY(g->spb[0].alloc(ctx, (size_t)N));
     MR_TRY(g->spb[1].alloc(ctx, (size_t)N));
@@ -437,69 +576,78 @@ extern "C" int mr_pagerank(mr_ctx* ctx, mr_graph* g, int anomaly, double d, doub
         if (fp32) MR_TRY(g->q32[i].alloc(ctx, (size_t)T));
         else MR_TRY(g->q64[i].alloc(ctx, (size_t)T));
     }
+    // one launch clears every per-call word (instead of a memset per buffer)
+    hipLaunchKernelGGL(k_pr_reset, dim3(cdiv(std::max<int64_t>({(int64_t)T, (int64_t)cap, (int64_t)N, 16}), 256)),
+                       dim3(256), 0, st, T, (int64_t)cap, N, g->pref.p, g->c_t.p, g->ht_key.p, g->ht_cnt.p, g->ht_rep.p,
+                       g->op_cnt.p, g->flag.p, g->scal.p);
+    MR_DEBUG_CHECK(ctx, "k_pr_reset");
     // ---- kinds
-    uint64_t cap = 1;
-    while (cap < 2ull * (uint64_t)T) cap <<= 1;
-    MR_TRY(g->ht_key.zero(ctx, cap));
-    MR_TRY(g->ht_cnt.zero(ctx, cap));
-    MR_TRY(g->ht_rep.alloc(ctx, cap));
-    MR_TRY_HIP(ctx, hipMemsetAsync(g->ht_rep.p, 0xFF, cap * sizeof(int32_t), st));
-    MR_TRY(g->slot_of.alloc(ctx, (size_t)T));
     const int64_t* koff = g->rs_is_sr ? g->rs_off.p : g->srt_off.p;
     const int32_t* kops = g->rs_is_sr ? g->rs_ops.p : g->srt_ops.p;
     hipLaunchKernelGGL(k_kind_insert, dim3(cdiv(T, KB)), dim3(KB), 0, st, koff, kops, g->w_t.p, T, g->ht_key.p,
                        g->ht_cnt.p, g->ht_rep.p, g->slot_of.p, (uint64_t)(cap - 1), 0x5eed5eedull);
+    MR_DEBUG_CHECK(ctx, "k_kind_insert");
     hipLaunchKernelGGL(k_kind_verify, dim3(cdiv(T, 256)), dim3(256), 0, st, koff, kops, g->w_t.p, T, g->ht_cnt.p,
                        g->ht_rep.p, g->slot_of.p, g->kind.p, g->flag.p);
+    MR_DEBUG_CHECK(ctx, "k_kind_verify");
     // ---- preference
     const int32_t* prt = g->pr_identity ? nullptr : g->pr_trace.p;
     const int32_t* prl = g->pr_identity ? nullptr : g->pr_len.p;
-    const int32_t n_pr = g->n_pr;
-    const int nbp = cdiv(n_pr > 0 ? n_pr : 1, TB);
-    DBuf<double> ppart;
-    MR_TRY(ppart.zero(ctx, 2 * (size_t)nbp));
     if (n_pr > 0)
-        hipLaunchKernelGGL(k_pref_partial, dim3(nbp), dim3(TB), 0, st, g->kind.p, prt, prl, g->len_t.p, n_pr, ppart.p,
-                           g->flag.p);
+        hipLaunchKernelGGL(k_pref_partial, dim3(nbp), dim3(TB), 0, st, g->kind.p, prt, prl, g->len_t.p, n_pr,
+                           g->ppart.p, g->flag.p);
     if (flags & MR_PR_EXACT_SUMS)
         hipLaunchKernelGGL(k_pref_total_exact, dim3(1), dim3(64), 0, st, g->kind.p, prt, prl, g->len_t.p, n_pr,
                            g->scal.p);
     else
-        hipLaunchKernelGGL(k_pref_total, dim3(1), dim3(1024), 0, st, ppart.p, nbp, g->scal.p);
+        hipLaunchKernelGGL(k_pref_total, dim3(1), dim3(1024), 0, st, g->ppart.p, nbp, g->scal.p);
+    MR_DEBUG_CHECK(ctx, "k_pref");
+    const float cd = (float)(1.0 - d);
+    if (n_pr > 0)
+        hipLaunchKernelGGL(k_pref_apply, dim3(nbp), dim3(TB), 0, st, g->kind.p, prt, prl, g->len_t.p, n_pr,
+                           g->scal.p, anomaly, cd, g->pref.p, g->c_t.p);
+    MR_DEBUG_CHECK(ctx, "k_pref_apply");
+    // ---- power iteration
+    hipLaunchKernelGGL(k_iter_init, dim3(cdiv(std::max<int64_t>({N, T, 6 * MSH}), 256)), dim3(256), 0, st, g->w_t.p, g->u_o.p, N, T,
+                       g->spb[0].p, g->sub[0].p, g->q64[0].p, g->q32[0].p, (int)fp32, g->mslot.p);
+    MR_DEBUG_CHECK(ctx, "k_iter_init");
+    const int lds_su = N <= LDS_NODES;
+    const size_t lds = ((lds_su ? (size_t)N : 0) + VCAP) * sizeof(double);
+    int n_oblocks = cdiv(g->nseg, TB / WAVE);
+    int n_tb = n_tblocks;
+    if (const char* rm = getenv("MR_ROLE_MASK")) {   // profiling knob: 1 = trace role only, 2 = op role only
+        const int m = atoi(rm);
+        if (!(m & 1)) n_tb = 0;
+        if (!(m & 2)) n_oblocks = 0;
+    }
+    // lanes per trace for the trace role: the average distinct ops per trace, rounded up to 2^k
+    const double avgdeg = (double)g->nnz_rs / (double)T;
+    int vw = avgdeg <= 4 ? 4 : avgdeg <= 8 ? 8 : avgdeg <= 16 ? 16 : avgdeg <= 32 ? 32 : 64;
+    int staged = 1;   // LDS-staged trace role by default (measured faster than CSR-vector at C2)
+    if (const char* tm = getenv("MR_TRACE_MODE")) staged = atoi(tm) == 0;
+    if (staged) vw = 0;
+    // algorithmic bytes of one iteration: op ids once, offsets, the r/v/len_t
+    // streams, call edges and three N-vectors; o = 4-byte offsets below 2^31 nonzeros
+    const double w = fp32 ? 4.0 : 8.0, o = g->nnz_sr < (1ll << 31) ? 4.0 : 8.0;
+    const double b_iter = 4.0 * (double)g->nnz_sr + o * ((double)T + 1) + 4.0 * w * (double)T + (8.0 + w) * (double)g->E +
+                          3.0 * w * (double)N;
+    for (int it = 0; it < iters; ++it) {
+        const int cur = it & 1, nxt = cur ^ 1;
+        mr_prof_begin(ctx);
+        if (fp32) MR_TRY(launch_iter<float>(ctx, g, vw, n_tb, n_oblocks, lds, d, alpha, lds_su, cur, nxt, it));
+        else MR_TRY(launch_iter<double>(ctx, g, vw, n_tb, n_oblocks, lds, d, alpha, lds_su, cur, nxt, it));
+        MR_DEBUG_CHECK(ctx, "k_iter");
+        mr_prof_end(ctx, b_iter);
+    }
+    hipLaunchKernelGGL(k_weights, dim3(1), dim3(1024), 0, st, g->spb[iters & 1].p, g->mslot.p, iters % 3, N,
+                       (int)((flags & MR_PR_EXACT_SUMS) != 0), g->sn.p, g->weight.p, g->scal.p);
+    MR_DEBUG_CHECK(ctx, "k_weights");
+    MR_TRY_HIP(ctx, hipGetLastError());
+    // the only host round trip of the call: error words raised by the kernels
     int32_t hflag[4] = {0, 0, 0, 0};
     MR_TRY_HIP(ctx, hipMemcpyAsync(hflag, g->flag.p, sizeof hflag, hipMemcpyDeviceToHost, st));
     MR_TRY_HIP(ctx, hipStreamSynchronize(st));
     if (hflag[0] & 1) return mr_fail(ctx, MR_ERR_STATE, "trace-kind hash collision (retry with another seed)");
     if (anomaly && (hflag[0] & 2)) return mr_fail(ctx, MR_ERR_ZERODIV, "float division by zero");
-    const float cd = (float)(1.0 - d);
-    if (n_pr > 0)
-        hipLaunchKernelGGL(k_pref_apply, dim3(nbp), dim3(TB), 0, st, g->kind.p, prt, prl, g->len_t.p, n_pr,
-                           g->scal.p, anomaly, cd, g->pref.p, g->c_t.p);
-    // ---- power iteration
-    MR_TRY(g->op_cnt.zero(ctx, (size_t)N));
-    MR_TRY(g->mslot.alloc(ctx, 6));
-    hipLaunchKernelGGL(k_iter_init, dim3(cdiv(N > T ? N : T, 256)), dim3(256), 0, st, g->w_t.p, g->u_o.p, N, T,
-                       g->spb[0].p, g->sub[0].p, g->q64[0].p, g->q32[0].p, (int)fp32, g->mslot.p);
-    const int lds_su = N <= LDS_NODES;
-    const size_t lds = ((lds_su ? (size_t)N : 0) + VCAP) * sizeof(double);
-    const int n_oblocks = cdiv(g->nseg, TB / WAVE);
-    for (int it = 0; it < iters; ++it) {
-        const int cur = it & 1, nxt = cur ^ 1;
-        if (fp32)
-            hipLaunchKernelGGL(k_iter<float>, dim3(n_tblocks + n_oblocks), dim3(TB), lds, st, g->rs_off.p, g->rs_ops.p,
-                               g->sub[cur].p, g->c_t.p, g->w_t.p, g->q32[nxt].p, T, N, n_tblocks, d, alpha, lds_su,
-                               g->sr_off.p, g->sr_trs.p, g->seg_op.p, g->seg_beg.p, g->op_seg.p, g->q32[cur].p,
-                               g->part.p, g->nseg, g->op_cnt.p, (uint32_t)(it + 1), g->ss_off.p, g->ss_par.p, g->pw.p,
-                               g->u_o.p, g->spb[cur].p, g->spb[nxt].p, g->sub[nxt].p, g->mslot.p, it % 3);
-        else
-            hipLaunchKernelGGL(k_iter<double>, dim3(n_tblocks + n_oblocks), dim3(TB), lds, st, g->rs_off.p, g->rs_ops.p,
-                               g->sub[cur].p, g->c_t.p, g->w_t.p, g->q64[nxt].p, T, N, n_tblocks, d, alpha, lds_su,
-                               g->sr_off.p, g->sr_trs.p, g->seg_op.p, g->seg_beg.p, g->op_seg.p, g->q64[cur].p,
-                               g->part.p, g->nseg, g->op_cnt.p, (uint32_t)(it + 1), g->ss_off.p, g->ss_par.p, g->pw.p,
-                               g->u_o.p, g->spb[cur].p, g->spb[nxt].p, g->sub[nxt].p, g->mslot.p, it % 3);
-    }
-    hipLaunchKernelGGL(k_weights, dim3(1), dim3(1024), 0, st, g->spb[iters & 1].p, g->mslot.p, iters % 3, N,
-                       (int)((flags & MR_PR_EXACT_SUMS) != 0), g->sn.p, g->weight.p, g->scal.p);
-    MR_TRY_HIP(ctx, hipGetLastError());
     return MR_OK;
 }

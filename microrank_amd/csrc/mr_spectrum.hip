@@ -1,0 +1,222 @@
+// K3: online_rca.calculate_spectrum_without_delay_list (online_rca.py:189-308) on gfx950.
+//
+// One thread per node computes (ef, nf, ep, np) from the two PageRank weight/coverage vectors
+// (:201-225) and applies one of the 13 formulas (:231-298) with the reference's operation
+// order (no FMA contraction).  The stable descending sort (:303) is a sort on the composite
+// key (score, position): positions break ties exactly like Python's stable `sorted`.  Nodes
+// are in the reference's iteration order: anomaly_result nodes, then normal-only nodes.
+//
+// Python raises ZeroDivisionError only when BOTH operands of a division are Python scalars
+// (an np.float64 operand gives inf/nan instead).  Each node carries the "numpy-typed" bits of
+// its inputs, the kernel propagates them through the formula and flags a division by zero
+// between two Python-typed values.
+#include <algorithm>
+
+#include "mr_prim.h"
+#include "mr_sort.h"
+
+namespace {
+enum Method { DSTAR2, OCHIAI, JACCARD, SORENSEN, M1, M2, GOODMAN, TARANTULA, RUSSELLRAO, HAMANN, DICE, SIMPLE, ROGERS };
+
+struct TV {   // typed value: v and whether it is numpy-typed (np.float64) in the reference
+    double v;
+    bool np;
+};
+__device__ __forceinline__ TV add(TV a, TV b) { return {a.v + b.v, a.np || b.np}; }
+__device__ __forceinline__ TV sub(TV a, TV b) { return {a.v - b.v, a.np || b.np}; }
+__device__ __forceinline__ TV mul(TV a, TV b) { return {a.v * b.v, a.np || b.np}; }
+__device__ __forceinline__ TV dv(TV a, TV b, bool& zd) {
+    if (!a.np && !b.np && b.v == 0.0) zd = true;
+    return {a.v / b.v, a.np || b.np};
+}
+
+__device__ double spectrum_score(int method, TV ef, TV nf, TV ep, TV np_, bool& zd, bool& res_np) {
+    const TV two{2.0, false};
+    TV r{0.0, false};
+    switch (method) {
+        case DSTAR2: r = dv(mul(ef, ef), add(ep, nf), zd); break;                                     // :234
+        case OCHIAI: r = dv(ef, TV{sqrt(add(ep, ef).v * add(ef, nf).v), false}, zd); break;           // :237
+        case JACCARD: r = dv(ef, add(add(ef, ep), nf), zd); break;                                     // :242
+        case SORENSEN: r = dv(mul(two, ef), add(add(mul(two, ef), ep), nf), zd); break;                // :245
+        case M1: r = dv(add(ef, np_), add(ep, nf), zd); break;                                         // :250
+        case M2: r = dv(ef, add(add(add(mul(two, ep), mul(two, nf)), ef), np_), zd); break;            // :253
+        case GOODMAN: r = dv(sub(sub(mul(two, ef), nf), ep), add(add(mul(two, ef), nf), ep), zd); break;  // :257
+        case TARANTULA: {                                                                              // :262
+            TV a = dv(ef, add(ef, nf), zd);
+            TV b = dv(ef, add(ef, nf), zd);
+            TV c = dv(ep, add(ep, np_), zd);
+            r = dv(a, add(b, c), zd);
+        } break;
+        case RUSSELLRAO: r = dv(ef, add(add(add(ef, nf), ep), np_), zd); break;                        // :272
+        case HAMANN: r = dv(sub(sub(add(ef, np_), ep), nf), add(add(add(ef, nf), ep), np_), zd); break;  // :278
+        case DICE: r = dv(mul(two, ef), add(add(ef, nf), ep), zd); break;                              // :285
+        case SIMPLE: r = dv(add(ef, np_), add(add(add(ef, np_), nf), ep), zd); break;                  // :290
+        case ROGERS: r = dv(add(ef, np_), add(add(add(ef, np_), mul(two, nf)), mul(two, ep)), zd); break;  // :296
+    }
+    res_np = r.np;
+    return r.v;
+}
+
+// order-preserving bits for a DESCENDING sort (ascending key = descending score); -0 == +0
+__device__ __forceinline__ uint64_t desc_key(double v) {
+    if (v == 0.0) v = 0.0;
+    uint64_t b = (uint64_t)__double_as_longlong(v);
+    b = (b >> 63) ? ~b : (b | 0x8000000000000000ull);   // ascending-orderable
+    return ~b;
+}
+
+// flags per node: bit0 in anomaly_result, bit1 in normal_result, bit2 a_w numpy-typed,
+// bit3 n_w numpy-typed
+__global__ void k_spectrum(int32_t n, const uint8_t* flags, const double* a_w, const int64_t* a_num, const double* n_w,
+                           const int64_t* n_num, int64_t A, int64_t Nl, int method, double* score, uint8_t* res_np,
+                           uint64_t* key, uint32_t* idx, int32_t* zflag) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint8_t f = flags[i];
+    const bool ha = f & 1, hn = f & 2, ta = f & 4, tn = f & 8;
+    const TV eps{0.0000001, false};
+    TV ef, nf, ep, np_;
+    if (ha) {   // :201-214
+        ef = TV{a_w[i] * (double)a_num[i], ta};
+        nf = TV{a_w[i] * (double)(A - a_num[i]), ta};
+        if (hn) {
+            ep = TV{n_w[i] * (double)n_num[i], tn};
+            np_ = TV{n_w[i] * (double)(Nl - n_num[i]), tn};
+        } else {
+            ep = eps;
+            np_ = eps;
+        }
+    } else {    // :216-225 normal-only
+        ep = TV{(1.0 + n_w[i]) * (double)n_num[i], tn};
+        np_ = TV{(double)(Nl - n_num[i]), false};
+        ef = eps;
+        nf = eps;
+    }
+    bool zd = false, rnp = false;
+    const double s = spectrum_score(method, ef, nf, ep, np_, zd, rnp);
+    score[i] = s;
+    res_np[i] = rnp;
+    key[i] = desc_key(s);
+    idx[i] = (uint32_t)i;
+    if (zd) atomicOr(zflag, 1);
+}
+
+// small n: one block sorts (key, idx) pairs in LDS with a bitonic network; (key, idx) pairs are
+// unique, so the unstable network still yields the stable order
+constexpr int SB = 4096;
+__global__ void __launch_bounds__(1024) k_sort_small(uint64_t* key, uint32_t* idx, int32_t n) {
+    __shared__ uint64_t k[SB];
+    __shared__ uint32_t v[SB];
+    int32_t m = 1;
+    while (m < n) m <<= 1;
+    for (int32_t i = threadIdx.x; i < m; i += blockDim.x) {
+        k[i] = i < n ? key[i] : ~0ull;
+        v[i] = i < n ? idx[i] : 0xffffffffu;
+    }
+    __syncthreads();
+    for (int32_t size = 2; size <= m; size <<= 1) {
+        for (int32_t stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int32_t i = threadIdx.x; i < m; i += blockDim.x) {
+                const int32_t j = i ^ stride;
+                if (j > i) {
+                    const bool up = (i & size) == 0;
+                    const bool gt = k[i] > k[j] || (k[i] == k[j] && v[i] > v[j]);
+                    if (gt == up) {
+                        uint64_t tk = k[i];
+                        k[i] = k[j];
+                        k[j] = tk;
+                        uint32_t tv = v[i];
+                        v[i] = v[j];
+                        v[j] = tv;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (int32_t i = threadIdx.x; i < n; i += blockDim.x) {
+        key[i] = k[i];
+        idx[i] = v[i];
+    }
+}
+
+__global__ void k_gather_top(const uint32_t* idx, const double* score, const uint8_t* res_np, int32_t top,
+                             int32_t* out_idx, double* out_score, uint8_t* out_np) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= top) return;
+    const uint32_t j = idx[i];
+    out_idx[i] = (int32_t)j;
+    out_score[i] = score[j];
+    if (out_np) out_np[i] = res_np[j];
+}
+}  // namespace
+
+// Device-side spectrum over n nodes whose inputs are already in HBM.  Writes the first `top`
+// sorted positions / scores to device buffers.
+int mr_spectrum_dev(mr_ctx* ctx, int32_t n, const uint8_t* flags, const double* a_w, const int64_t* a_num,
+                    const double* n_w, const int64_t* n_num, int64_t A, int64_t Nl, int method, int32_t top,
+                    int32_t* d_out_idx, double* d_out_score, uint8_t* d_out_np, int32_t* d_zflag) {
+    hipStream_t st = ctx->stream;
+    DBuf<double> score;
+    DBuf<uint8_t> rnp;
+    DBuf<uint64_t> key;
+    DBuf<uint32_t> idx;
+    MR_TRY(score.alloc(ctx, n));
+    MR_TRY(rnp.alloc(ctx, n));
+    MR_TRY(key.alloc(ctx, n));
+    MR_TRY(idx.alloc(ctx, n));
+    hipLaunchKernelGGL(k_spectrum, dim3(cdiv(n, 256)), dim3(256), 0, st, n, flags, a_w, a_num, n_w, n_num, A, Nl,
+                       method, score.p, rnp.p, key.p, idx.p, d_zflag);
+    if (n <= SB) {
+        hipLaunchKernelGGL(k_sort_small, dim3(1), dim3(1024), 0, st, key.p, idx.p, n);
+    } else {
+        SortScratch ws;
+        MR_TRY(mr_radix_sort(ctx, key.p, idx.p, n, 64, ws));   // LSD radix is stable: ties keep position order
+        MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+    }
+    if (top > 0)
+        hipLaunchKernelGGL(k_gather_top, dim3(cdiv(top, 256)), dim3(256), 0, st, idx.p, score.p, rnp.p, top, d_out_idx,
+                           d_out_score, d_out_np);
+    MR_TRY_HIP(ctx, hipGetLastError());
+    MR_TRY_HIP(ctx, hipStreamSynchronize(st));   // local buffers die here
+    return MR_OK;
+}
+
+extern "C" int mr_spectrum(mr_ctx* ctx, int32_t n, const uint8_t* has_a, const double* a_w, const int64_t* a_num,
+                           const uint8_t* has_n, const double* n_w, const int64_t* n_num, int64_t a_len, int64_t n_len,
+                           int method, int32_t top, int32_t* out_idx, double* out_score, int32_t* n_out,
+                           int32_t* zerodiv) {
+    if (!ctx || n < 0 || !n_out || !zerodiv) return mr_fail(ctx, MR_ERR_ARG, "mr_spectrum: bad arguments");
+    *n_out = 0;
+    *zerodiv = 0;
+    if (method < 0 || method > ROGERS) return MR_OK;   // unknown method: the reference returns empty lists
+    if (n == 0) return MR_OK;
+    MR_TRY_HIP(ctx, hipSetDevice(ctx->device));
+    // has_a/has_n carry the membership bit in bit 0 and the numpy-typed bit in bit 1
+    std::vector<uint8_t> fl((size_t)n);
+    for (int32_t i = 0; i < n; ++i)
+        fl[i] = (uint8_t)((has_a[i] & 1) | ((has_n[i] & 1) << 1) | ((has_a[i] & 2) << 1) | ((has_n[i] & 2) << 2));
+    const int32_t k = std::min(n, std::max(top, 0));
+    DBuf<uint8_t> dfl;
+    DBuf<double> daw, dnw, dsc;
+    DBuf<int64_t> dan, dnn;
+    DBuf<int32_t> didx, dz;
+    MR_TRY(dfl.upload(ctx, fl.data(), n));
+    MR_TRY(daw.upload(ctx, a_w, n));
+    MR_TRY(dan.upload(ctx, a_num, n));
+    MR_TRY(dnw.upload(ctx, n_w, n));
+    MR_TRY(dnn.upload(ctx, n_num, n));
+    MR_TRY(didx.alloc(ctx, std::max(k, 1)));
+    MR_TRY(dsc.alloc(ctx, std::max(k, 1)));
+    MR_TRY(dz.zero(ctx, 1));
+    MR_TRY(mr_spectrum_dev(ctx, n, dfl.p, daw.p, dan.p, dnw.p, dnn.p, a_len, n_len, method, k, didx.p, dsc.p, nullptr,
+                           dz.p));
+    if (k) {
+        MR_TRY(didx.download(ctx, out_idx, k));
+        MR_TRY(dsc.download(ctx, out_score, k));
+    }
+    MR_TRY(dz.download(ctx, zerodiv, 1));
+    MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    *n_out = k;
+    return MR_OK;
+}

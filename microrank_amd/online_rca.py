@@ -1,0 +1,161 @@
+"""Drop-in for the reference module ``online_rca`` (online_rca.py).
+
+* ``calculate_spectrum_without_delay_list`` -- the weighted spectrum scores and the stable
+  top list (online_rca.py:189-308), computed on the GPU (K3, csrc/mr_spectrum.hip); printing,
+  argument names and return types as in the reference.
+* ``online_anomaly_detect_RCA`` -- the sliding-window driver (online_rca.py:311-372), line for
+  line the same control flow, with every ranking step on the GPU.
+* ``rca_window`` -- one whole window (detect -> 2 graphs -> 2 PageRanks -> spectrum) in a
+  single C-ABI call with every intermediate resident in HBM (used by bench.py).
+"""
+from __future__ import annotations
+
+import csv
+import ctypes as C
+import math
+import time
+
+import numpy as np
+import pandas as pd
+
+from . import _lib
+from ._lib import SPECTRUM_METHODS, ptr
+from .anormaly_detector import slo_arrays, system_anomaly_detect, trace_list_partition  # noqa: F401
+from .pagerank import trace_pagerank
+from .preprocess_data import (get_operation_duration_data, get_operation_slo, get_pagerank_graph,  # noqa: F401
+                              get_service_operation_list, get_span, span_table)
+from .spans import to_ns
+
+
+def timestamp(datetime):
+    """online_rca.py:182-186."""
+    return int(time.mktime(time.strptime(str(datetime), "%Y-%m-%d %H:%M:%S"))) * 1000
+
+
+def _is_np(v) -> bool:
+    return isinstance(v, np.generic)
+
+
+def calculate_spectrum_without_delay_list(anomaly_result, normal_result, anomaly_list_len, normal_list_len, top_max,
+                                          normal_num_list, anomaly_num_list, spectrum_method, *, ctx=None):
+    """online_rca.calculate_spectrum_without_delay_list on MI355X."""
+    nodes = list(anomaly_result)
+    nodes += [k for k in normal_result if k not in anomaly_result]
+    n = len(nodes)
+    has_a = np.zeros(n, np.uint8)
+    has_n = np.zeros(n, np.uint8)
+    a_w = np.zeros(n, np.float64)
+    n_w = np.zeros(n, np.float64)
+    a_num = np.zeros(n, np.int64)
+    n_num = np.zeros(n, np.int64)
+    kinds = []   # (a numpy-typed, n numpy-typed) per node, for the result type
+    for i, node in enumerate(nodes):
+        ta = tn = False
+        if node in anomaly_result:
+            w = anomaly_result[node]
+            a_w[i] = w
+            a_num[i] = anomaly_num_list[node]          # KeyError as in the reference (:205)
+            ta = _is_np(w)
+            has_a[i] = 1 | (2 if ta else 0)
+        if node in normal_result:
+            w = normal_result[node]
+            n_w[i] = w
+            n_num[i] = normal_num_list[node]
+            tn = _is_np(w)
+            has_n[i] = 1 | (2 if tn else 0)
+        kinds.append((ta, tn))
+    try:
+        method = SPECTRUM_METHODS.index(spectrum_method)
+    except ValueError:
+        return [], []                                  # no branch matched: empty result (:231-298)
+    if n == 0:
+        return [], []
+    ctx = ctx or _lib.default_context()
+    k = max(0, min(n, top_max + 6))
+    idx = np.zeros(max(k, 1), np.int32)
+    sc = np.zeros(max(k, 1), np.float64)
+    n_out, zd = C.c_int32(), C.c_int32()
+    ctx.check(_lib.load().mr_spectrum(ctx.h, n, ptr(has_a, C.c_uint8), ptr(a_w, C.c_double), ptr(a_num, C.c_int64),
+                                      ptr(has_n, C.c_uint8), ptr(n_w, C.c_double), ptr(n_num, C.c_int64),
+                                      int(anomaly_list_len), int(normal_list_len), method, k, ptr(idx, C.c_int32),
+                                      ptr(sc, C.c_double), C.byref(n_out), C.byref(zd)), "mr_spectrum")
+    if zd.value:
+        raise ZeroDivisionError("float division by zero")
+    top_list, score_list = [], []
+    for j in range(n_out.value):
+        i = int(idx[j])
+        ta, tn = kinds[i]
+        ha, hn = bool(has_a[i] & 1), bool(has_n[i] & 1)
+        if spectrum_method == "ochiai":          # ef / math.sqrt(...): the type of ef decides
+            res_np = ta if ha else False
+        else:
+            res_np = (ta or (tn and hn)) if ha else tn
+        s = np.float64(sc[j]) if res_np else float(sc[j])
+        top_list.append(nodes[i])
+        score_list.append(s)
+        print("%-50s: %.8f" % (nodes[i], s))
+    return top_list, score_list
+
+
+def online_anomaly_detect_RCA(data, slo, operation_list):
+    """online_rca.online_anomaly_detect_RCA (online_rca.py:311-372): 5-minute windows, a triggered
+    window advances by 9 minutes; the detector's lists are unpacked swapped (T1), an empty
+    window makes the unpacking raise TypeError (T2); result.csv is rewritten per trigger."""
+    window_normal = pd.Timedelta(minutes=5)
+    window_abnormal = pd.Timedelta(minutes=4)
+    start = data["startTime"].min()
+    end = data["endTime"].max()
+    current_time = start
+    while current_time < end:
+        start_time = current_time
+        end_time = current_time + window_normal
+        anomaly_flag, normal_list, abnormal_list = system_anomaly_detect(
+            data, start_time=start_time, end_time=end_time, slo=slo, operation_list=operation_list)
+        if anomaly_flag:
+            print("anomaly_list", len(abnormal_list))
+            print("normal_list", len(normal_list))
+            print("total", len(normal_list) + len(abnormal_list))
+            if not abnormal_list or not normal_list:
+                current_time += window_normal
+                continue
+            n_graph = get_pagerank_graph(normal_list, data)
+            normal_trace_result, normal_num_list = trace_pagerank(*n_graph, False)
+            a_graph = get_pagerank_graph(abnormal_list, data)
+            anomaly_trace_result, anomaly_num_list = trace_pagerank(*a_graph, True)
+            top_list, score_list = calculate_spectrum_without_delay_list(
+                anomaly_result=anomaly_trace_result, normal_result=normal_trace_result,
+                anomaly_list_len=len(abnormal_list), normal_list_len=len(normal_list), top_max=5,
+                anomaly_num_list=anomaly_num_list, normal_num_list=normal_num_list, spectrum_method="dstar2")
+            print(top_list, score_list)
+            ranked = sorted(zip(top_list, score_list), key=lambda x: x[1], reverse=True)
+            with open("result.csv", "w", newline="") as f:
+                w = csv.writer(f)
+                w.writerow(["level", "result", "rank", "confidence"])
+                for rank, (service, score) in enumerate(ranked, start=1):
+                    w.writerow(["span", service, rank, float(score)])
+            current_time += window_abnormal
+        current_time += window_normal
+
+
+def rca_window(data, start_time, end_time, slo, *, top_max=5, spectrum_method="dstar2", precision="fp64", ctx=None,
+               table=None, dev=None):
+    """One RCA window entirely on the device (mr_rca_window).  Returns a dict with the top list
+    (pod-op names), scores, the detector counts and the edges traversed by the two PageRanks."""
+    ctx = ctx or _lib.default_context()
+    if table is None or dev is None:
+        table, dev = span_table(data, ctx)
+    a3, ok = slo_arrays(table, slo)
+    k = max(top_max + 6, 1)
+    codes = np.zeros(k, np.int32)
+    scores = np.zeros(k, np.float64)
+    n_out, na, nn, edges = C.c_int32(), C.c_int32(), C.c_int32(), C.c_int64()
+    method = SPECTRUM_METHODS.index(spectrum_method)
+    prec = _lib.MR_FP32 if precision == "fp32" else _lib.MR_FP64
+    ctx.check(_lib.load().mr_rca_window(ctx.h, dev.h, to_ns(start_time), to_ns(end_time), ptr(a3, C.c_double),
+                                        ptr(ok, C.c_uint8), method, top_max, prec, ptr(codes, C.c_int32),
+                                        ptr(scores, C.c_double), C.byref(n_out), C.byref(edges), C.byref(na),
+                                        C.byref(nn)), "mr_rca_window")
+    m = n_out.value
+    names = table.podop_names
+    return {"top": [names[c] for c in codes[:m]] if names is not None else codes[:m].tolist(),
+            "score": scores[:m].tolist(), "n_abnormal": na.value, "n_normal": nn.value, "edges": edges.value}

@@ -32,3 +32,14 @@ for prec in ("fp64", "fp32"):
     t = float(np.median(ts))
     edges = 25 * (2 * g.sr_t.size + g.ss_c.size)
     print(f"{prec}: trace_pagerank median {t*1e3:.3f} ms  -> {edges/t/1e9:.2f} GTEPS (whole call incl. kinds)")
+if os.environ.get("ROLE_AB"):
+    for mask in ("1", "2", "3", "1", "2", "3"):
+        os.environ["MR_ROLE_MASK"] = mask
+        ts = []
+        for _ in range(reps):
+            t = time.perf_counter()
+            dg.pagerank(True)
+            ctx.sync()
+            ts.append(time.perf_counter() - t)
+        print(f"role mask {mask}: median {np.median(ts)*1e3:.3f} ms")
+    os.environ.pop("MR_ROLE_MASK")

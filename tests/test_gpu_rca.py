@@ -1,0 +1,195 @@
+"""GPU parity of K3 (spectrum), K4 (SLO), K5 (detector) and the whole driver against the
+reference's own outputs (tests/golden).  Spectrum scores, SLO values and the detector's
+partition are bit-exact; the driver's stdout is identical except the full-precision repr line
+(online_rca.py:358) and result.csv, whose scores are compared at 1e-10 relative."""
+import contextlib
+import io
+import math
+import os
+
+import numpy as np
+import pandas as pd
+import pytest
+
+from conftest import GOLDEN, load_golden, regen_window, unhex
+
+pytestmark = pytest.mark.gpu
+SPAN_CASES = ["c1", "pods_dup_broken", "ops200"]
+
+
+def _spectrum_inputs(case):
+    a, n = case["pr_anomaly"], case["pr_normal"]
+    a_w = {k: np.float64(v) for k, v in zip(a["keys"], unhex(a["weight"]))}
+    n_w = {k: np.float64(v) for k, v in zip(n["keys"], unhex(n["weight"]))}
+    return (a_w, n_w, len(case["detect"]["normal"]), len(case["detect"]["abnormal"]),
+            dict(zip(n["num_keys"], n["num"])), dict(zip(a["num_keys"], a["num"])))
+
+
+@pytest.mark.parametrize("name", SPAN_CASES)
+def test_spectrum_all_methods(name):
+    from microrank_amd.online_rca import calculate_spectrum_without_delay_list as spec
+
+    case = load_golden(f"{name}.json")
+    a_w, n_w, A, Nn, n_num, a_num = _spectrum_inputs(case)
+    for m, exp in case["spectrum"].items():
+        buf = io.StringIO()
+        with contextlib.redirect_stdout(buf):
+            top, score = spec(anomaly_result=a_w, normal_result=n_w, anomaly_list_len=A, normal_list_len=Nn,
+                              top_max=5, normal_num_list=n_num, anomaly_num_list=a_num, spectrum_method=m)
+        if "error" in exp:
+            pytest.fail(f"reference raised {exp['error']} for {m}")
+        assert top == exp["top"], m
+        assert [float(s).hex() for s in score] == exp["score"], m
+        assert buf.getvalue() == exp["stdout"], m
+        assert all(isinstance(s, np.float64) for s in score)
+
+
+def test_spectrum_python_scalar_edges():
+    """Python-float inputs: the reference raises ZeroDivisionError where both operands of a
+    division are Python scalars; numpy scalars give inf/nan instead."""
+    from microrank_amd.online_rca import calculate_spectrum_without_delay_list as spec
+
+    d = load_golden("dict_cases.json")["spectrum_edges"]
+    i = d["input"]
+    for m, exp in d["out"].items():
+        args = dict(anomaly_result=i["a_w"], normal_result=i["n_w"], anomaly_list_len=i["A"], normal_list_len=i["N"],
+                    top_max=5, normal_num_list=i["n_n"], anomaly_num_list=i["a_n"], spectrum_method=m)
+        buf = io.StringIO()
+        if "error" in exp:
+            with pytest.raises(ZeroDivisionError), contextlib.redirect_stdout(buf):
+                spec(**args)
+            continue
+        with contextlib.redirect_stdout(buf):
+            top, score = spec(**args)
+        assert top == exp["top"], m
+        assert [float(s).hex() for s in score] == exp["score"], m
+        assert buf.getvalue() == exp["stdout"], m
+
+
+@pytest.mark.parametrize("name", SPAN_CASES)
+def test_slo_bit_exact(name):
+    from microrank_amd.anormaly_detector import get_slo
+    from microrank_amd.preprocess_data import get_operation_slo, get_service_operation_list
+
+    case = load_golden(f"{name}.json")
+    ndf, _ = regen_window(case)
+    df = ndf.copy()
+    ol = get_service_operation_list(df)
+    assert ol == case["operation_list"]
+    slo = get_operation_slo(ol, df)
+    assert list(slo) == list(case["slo"])
+    for k, v in slo.items():
+        assert [float(v[0]).hex(), float(v[1]).hex()] == case["slo"][k], k
+        assert isinstance(v[0], np.float64)
+    slo2 = get_slo(ndf.copy())   # T16: the working form of get_slo
+    assert {k: [float(x).hex() for x in v] for k, v in slo2.items()} == case["slo"]
+
+
+@pytest.mark.parametrize("name", SPAN_CASES)
+def test_detector_partition(name):
+    from microrank_amd.anormaly_detector import system_anomaly_detect
+
+    case = load_golden(f"{name}.json")
+    _, adf = regen_window(case)
+    slo = {k: [np.float64(float.fromhex(a)), np.float64(float.fromhex(b))] for k, (a, b) in case["slo"].items()}
+    det = case["detect"]
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        flag, ab, no = system_anomaly_detect(adf, start_time=pd.Timestamp(det["start_ns"]),
+                                             end_time=pd.Timestamp(det["end_ns"]), slo=slo,
+                                             operation_list=case["operation_list"])
+    tnames = sorted(adf["traceID"].unique())
+    assert ab == [tnames[i] for i in det["abnormal"]]
+    assert no == [tnames[i] for i in det["normal"]]
+    assert flag == det["flag"]
+    assert buf.getvalue() == det["stdout"]
+
+
+def test_edge_spans_slo_and_detector():
+    from microrank_amd.anormaly_detector import system_anomaly_detect
+    from microrank_amd.preprocess_data import get_operation_slo, get_service_operation_list
+
+    e = load_golden("edges.json")
+    df = pd.read_parquet(os.path.join(GOLDEN, "edges_spans.parquet"))
+    sdf = df.copy()
+    ol = get_service_operation_list(sdf)
+    slo = get_operation_slo(ol[:-1], sdf)
+    assert {k: [float(v[0]).hex(), float(v[1]).hex()] for k, v in slo.items()} == e["slo"]
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        flag, ab, no = system_anomaly_detect(df, start_time=df.startTime.min(),
+                                             end_time=df.startTime.min() + pd.Timedelta(minutes=5), slo=slo,
+                                             operation_list=ol)
+    assert (flag, ab, no) == (e["detect"]["flag"], e["detect"]["abnormal"], e["detect"]["normal"])
+    assert buf.getvalue() == e["detect"]["stdout"]
+
+
+def test_empty_window_returns_false_and_driver_raises():
+    from microrank_amd.anormaly_detector import system_anomaly_detect
+
+    df = pd.read_parquet(os.path.join(GOLDEN, "edges_spans.parquet"))
+    t = df.startTime.min() - pd.Timedelta(days=1)
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        assert system_anomaly_detect(df, t, t + pd.Timedelta(minutes=5), {}, []) is False
+    assert buf.getvalue() == "Error: Current span list is empty \n"
+    # T2: every trace outlasts the first 5-minute window -> the detector returns False and the
+    # driver's 3-way unpacking raises TypeError, as in the reference
+    from microrank_amd.online_rca import online_anomaly_detect_RCA
+
+    long = df.copy()
+    long["endTime"] = long["startTime"] + pd.Timedelta(minutes=10)
+    with pytest.raises(TypeError), contextlib.redirect_stdout(io.StringIO()):
+        online_anomaly_detect_RCA(long, {}, [])
+
+
+@pytest.mark.parametrize("name", ["c1", "pods_dup_broken"])
+def test_driver_matches_reference(name, tmp_path, monkeypatch):
+    from microrank_amd.online_rca import online_anomaly_detect_RCA
+
+    case = load_golden(f"{name}.json")
+    _, adf = regen_window(case)
+    slo = {k: [np.float64(float.fromhex(a)), np.float64(float.fromhex(b))] for k, (a, b) in case["slo"].items()}
+    monkeypatch.chdir(tmp_path)
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        online_anomaly_detect_RCA(adf.copy(), slo, case["operation_list"])
+    got = buf.getvalue().splitlines()
+    exp = case["driver_stdout"].splitlines()
+    assert len(got) == len(exp)
+    for g, x in zip(got, exp):
+        if g.startswith("[") and x.startswith("["):    # print(top_list, score_list): full repr
+            gl, xl = g.split("] [", 1), x.split("] [", 1)
+            assert gl[0] == xl[0]
+            gs = [float(v.split("(")[-1].rstrip(")]")) for v in gl[1].split(", ")]
+            xs = [float(v.split("(")[-1].rstrip(")]")) for v in xl[1].split(", ")]
+            np.testing.assert_allclose(gs, xs, rtol=1e-10)
+        else:
+            assert g == x
+    got_csv = open("result.csv").read().splitlines()
+    exp_csv = case["result_csv"].splitlines()
+    assert len(got_csv) == len(exp_csv)
+    for g, x in zip(got_csv, exp_csv):
+        gp, xp = g.split(","), x.split(",")
+        assert gp[:-1] == xp[:-1]
+        if gp[-1] != "confidence":
+            assert math.isclose(float(gp[-1]), float(xp[-1]), rel_tol=1e-10)
+
+
+@pytest.mark.parametrize("name", ["c1", "pods_dup_broken", "ops200"])
+def test_rca_window_device_pipeline(name):
+    """mr_rca_window (all intermediates in HBM) ranks like the reference driver's window."""
+    from microrank_amd.online_rca import rca_window
+
+    case = load_golden(f"{name}.json")
+    _, adf = regen_window(case)
+    slo = {k: [np.float64(float.fromhex(a)), np.float64(float.fromhex(b))] for k, (a, b) in case["slo"].items()}
+    det = case["detect"]
+    out = rca_window(adf, pd.Timestamp(det["start_ns"]), pd.Timestamp(det["end_ns"]), slo)
+    exp = case["spectrum"]["dstar2"]
+    assert out["n_abnormal"] == len(det["abnormal"]) and out["n_normal"] == len(det["normal"])
+    assert out["top"] == exp["top"]
+    np.testing.assert_allclose(out["score"], unhex(exp["score"]), rtol=1e-10)
+    out32 = rca_window(adf, pd.Timestamp(det["start_ns"]), pd.Timestamp(det["end_ns"]), slo, precision="fp32")
+    assert out32["top"][:5] == exp["top"][:5]
+    np.testing.assert_allclose(out32["score"], unhex(exp["score"]), rtol=1e-4)
