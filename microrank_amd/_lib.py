@@ -5,6 +5,7 @@ There is no CPU fallback: if the library or a GPU is missing every entry point r
 from __future__ import annotations
 
 import ctypes as C
+import sys
 import os
 import threading
 from typing import Optional
@@ -157,6 +158,8 @@ class Context:
             self.h = None
 
     def __del__(self):  # pragma: no cover - interpreter teardown order
+        if sys.is_finalizing():   # device handles may already be gone; the process exit frees all
+            return
         try:
             self.close()
         except Exception:

@@ -45,6 +45,52 @@ extern "C" int mr_ctx_create(int device, uint32_t flags, mr_ctx** out) {
 
 void mr_comm_destroy(mr_ctx* ctx);  // mr_comm.cpp
 
+// ------------------------------------------------------------------------------ pool
+static size_t pool_round(size_t b) {
+    if (b <= 4096) return (b + 255) & ~(size_t)255;
+    if (b <= (1u << 20)) return (b + 4095) & ~(size_t)4095;
+    return (b + (1u << 20) - 1) & ~(size_t)((1u << 20) - 1);
+}
+
+void* mr_pool_alloc(mr_ctx* ctx, size_t bytes) {
+    const size_t want = pool_round(bytes);
+    auto it = ctx->pool_free.lower_bound(want);
+    if (it != ctx->pool_free.end() && it->first <= 2 * want) {   // reuse a block at most 2x too big
+        void* p = it->second;
+        ctx->pool_live[p] = it->first;
+        ctx->pool_free.erase(it);
+        return p;
+    }
+    void* p = nullptr;
+    if (hipMalloc(&p, want) != hipSuccess) {
+        // give the cached blocks back and retry once
+        (void)hipStreamSynchronize(ctx->stream);
+        for (auto& kv : ctx->pool_free) {
+            (void)hipFree(kv.second);
+            ctx->pool_bytes -= kv.first;
+        }
+        ctx->pool_free.clear();
+        if (hipMalloc(&p, want) != hipSuccess) return nullptr;
+    }
+    ctx->pool_bytes += want;
+    ctx->pool_live[p] = want;
+    return p;
+}
+
+void mr_pool_free(mr_ctx* ctx, void* p) {
+    if (!ctx || !p) return;
+    auto it = ctx->pool_live.find(p);
+    if (it == ctx->pool_live.end()) return;
+    ctx->pool_free.emplace(it->second, p);   // stream-ordered reuse: no sync needed
+    ctx->pool_live.erase(it);
+}
+
+void mr_pool_release(mr_ctx* ctx) {
+    (void)hipStreamSynchronize(ctx->stream);
+    for (auto& kv : ctx->pool_free) (void)hipFree(kv.second);
+    ctx->pool_free.clear();
+}
+
 static void prof_clear(mr_ctx* ctx) {
     for (hipEvent_t e : ctx->prof_ev) (void)hipEventDestroy(e);
     ctx->prof_ev.clear();
@@ -98,6 +144,9 @@ extern "C" void mr_ctx_destroy(mr_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     mr_comm_destroy(ctx);
     prof_clear(ctx);
+    mr_pool_release(ctx);
+    for (auto& kv : ctx->pool_live) (void)hipFree(kv.first);   // handles the caller leaked
+    ctx->pool_live.clear();
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }

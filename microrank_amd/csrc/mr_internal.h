@@ -5,6 +5,7 @@
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -25,7 +26,17 @@ struct mr_ctx {
     bool prof = false;
     std::vector<hipEvent_t> prof_ev;
     std::vector<double> prof_bytes;
+    // stream-ordered caching allocator: every buffer of this context is used on `stream` only,
+    // so a block released by one call can be handed to the next without a hipFree/hipMalloc
+    // (each of which synchronises the device and costs tens of microseconds)
+    std::multimap<size_t, void*> pool_free;
+    std::map<void*, size_t> pool_live;
+    size_t pool_bytes = 0;
 };
+
+void* mr_pool_alloc(mr_ctx* ctx, size_t bytes);
+void mr_pool_free(mr_ctx* ctx, void* p);
+void mr_pool_release(mr_ctx* ctx);
 
 int mr_fail(mr_ctx* ctx, int code, const char* fmt, ...);
 
@@ -48,12 +59,13 @@ template <class T>
 struct DBuf {
     T* p = nullptr;
     size_t n = 0;
+    mr_ctx* owner = nullptr;
     DBuf() = default;
     DBuf(const DBuf&) = delete;
     DBuf& operator=(const DBuf&) = delete;
     ~DBuf() { reset(); }
     void reset() {
-        if (p) (void)hipFree(p);
+        if (p) mr_pool_free(owner, p);
         p = nullptr;
         n = 0;
     }
@@ -61,11 +73,9 @@ struct DBuf {
         if (count <= n && p) return MR_OK;
         reset();
         size_t bytes = (count ? count : 1) * sizeof(T);
-        hipError_t e = hipMalloc(&p, bytes);
-        if (e != hipSuccess) {
-            p = nullptr;
-            return mr_fail(ctx, MR_ERR_OOM, "hipMalloc(%zu bytes): %s", bytes, hipGetErrorString(e));
-        }
+        p = (T*)mr_pool_alloc(ctx, bytes);
+        if (!p) return mr_fail(ctx, MR_ERR_OOM, "device allocation of %zu bytes failed", bytes);
+        owner = ctx;
         n = count;
         return MR_OK;
     }

@@ -12,6 +12,7 @@
 from __future__ import annotations
 
 import ctypes as C
+import sys
 from collections.abc import Mapping
 from dataclasses import dataclass
 from typing import Optional
@@ -185,6 +186,8 @@ class DeviceGraph:
             self.h = None
 
     def __del__(self):  # pragma: no cover
+        if sys.is_finalizing():   # the owning context may already be destroyed
+            return
         try:
             self.close()
         except Exception:

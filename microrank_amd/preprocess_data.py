@@ -16,6 +16,7 @@ cached per DataFrame object (see :func:`span_table`).
 from __future__ import annotations
 
 import ctypes as C
+import sys
 import weakref
 from collections.abc import Mapping
 
@@ -58,6 +59,8 @@ class DeviceSpans:
             self.h = None
 
     def __del__(self):  # pragma: no cover
+        if sys.is_finalizing():   # the owning context may already be destroyed
+            return
         try:
             self.close()
         except Exception:
