@@ -468,3 +468,57 @@ def detect(trace: np.ndarray, svcop: np.ndarray, duration: np.ndarray, tstart, t
                 exp += c * slo_mean_plus3std[o]
         (ab if real > exp else no).append(t)
     return bool(ab), ab, no
+
+
+# ----------------------------------------------------------------------------- trace sharding
+def sharded_pagerank(g: Graph, comm, anomaly: bool, d: float = D_DEFAULT, alpha: float = ALPHA_DEFAULT,
+                     iters: int = ITERS_DEFAULT):
+    """The multi-GPU decomposition restated on CPU: ``g`` holds THIS rank's
+    traces (every span of a trace on one rank) over the GLOBAL node index space.  ``comm`` offers
+    sum(np.ndarray) / max(float) / gather(obj) across ranks.  Per iteration one SUM of the N-length
+    partial P_sr.r vector and one MAX of r'; everything else (len_o, nchild, coverage, kind classes,
+    preference sums) is reduced once.  Returns (s, coverage) identical on every rank."""
+    N = g.N
+    len_o = comm.sum(g.len_o.astype(np.float64)).astype(np.int64)
+    nchild = comm.sum(g.nchild.astype(np.float64)).astype(np.int64)
+    cov = comm.sum(np.bincount(g.sr_o, minlength=N).astype(np.float64)).astype(np.int64)
+    edges = set()
+    for part in comm.gather(list(zip(g.ss_c.tolist(), g.ss_p.tolist()))):
+        edges.update(map(tuple, part))
+    ss = np.array(sorted(edges), dtype=np.int64).reshape(-1, 2)
+    # kinds: global class sizes of the (op set, fp32(1/len)) keys
+    w32 = (1.0 / np.maximum(g.len_t, 1)).astype(np.float32)
+    sets = [[] for _ in range(g.T)]
+    for t, o in zip(g.sr_t, g.sr_o):
+        sets[t].append(int(o))
+    keys = [(tuple(sorted(sets[t])), w32[t].view(np.uint32).item() if sets[t] else 0) for t in range(g.T)]
+    counts = {}
+    for part in comm.gather(keys):
+        for k in part:
+            counts[k] = counts.get(k, 0) + 1
+    kind = np.array([counts[k] for k in keys], dtype=np.float64)
+    # preference sums: global
+    if not anomaly:
+        S = comm.sum(np.array([np.sum(1.0 / kind)]))[0]
+        v = (1.0 / kind / S).astype(np.float32)
+    else:
+        KS, NS = comm.sum(np.array([np.sum(1.0 / kind), np.sum(1.0 / g.len_t)]))
+        v = (1.0 / (kind / KS * 0.5 + 1.0 / g.len_t) / NS * 0.5).astype(np.float32)
+    T_global = int(comm.sum(np.array([float(g.T)]))[0])
+    w_sr = (1.0 / np.maximum(g.len_t, 1)).astype(np.float32).astype(np.float64)[g.sr_t]
+    w_rs = (1.0 / np.maximum(len_o, 1)).astype(np.float32).astype(np.float64)[g.sr_o]
+    w_ss = (1.0 / np.maximum(nchild, 1)).astype(np.float32).astype(np.float64)[ss[:, 1]]
+    s = np.ones(N) / float(N + T_global)
+    r = np.ones(g.T) / float(N + T_global)
+    c = ((1.0 - d) * v).astype(np.float64)
+    for _ in range(iters):
+        part = np.bincount(g.sr_o, weights=w_sr * r[g.sr_t], minlength=N)
+        sr = comm.sum(part)
+        ssv = np.bincount(ss[:, 0], weights=w_ss * s[ss[:, 1]], minlength=N)
+        rs = np.bincount(g.sr_t, weights=w_rs * s[g.sr_o], minlength=g.T)
+        s_new = d * (sr + alpha * ssv)
+        r_new = d * rs + c
+        mr = comm.max(float(np.max(r_new)) if r_new.size else -np.inf)
+        s = s_new / np.max(s_new)
+        r = r_new / mr
+    return s / np.max(s), cov
