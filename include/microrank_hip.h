@@ -100,6 +100,10 @@ int mr_graph_info(const mr_graph* g, int32_t* n_nodes, int32_t* n_traces, int64_
  */
 int mr_pagerank(mr_ctx* ctx, mr_graph* g, int anomaly, double d, double alpha, int iters,
                 int precision, uint32_t flags);
+/* several independent graphs (e.g. the normal and anomaly graphs of a window, or many windows)
+ * ranked together: one launch per Jacobi iteration covers every graph */
+int mr_pagerank_batch(mr_ctx* ctx, mr_graph* const* graphs, const int* anomaly, int n_graphs, double d,
+                      double alpha, int iters, int precision, uint32_t flags);
 int mr_graph_fetch(mr_graph* g, double* weight /*[N] host*/, int32_t* coverage /*[N] host*/,
                    double* kind /*[T] host or NULL*/, float* pref /*[T] host or NULL*/);
 

@@ -233,8 +233,11 @@ extern "C" int mr_rca_window(mr_ctx* ctx, const mr_spans* s, int64_t t0, int64_t
     mr_graph *gn = nullptr, *ga = nullptr;
     int rc = mr_graph_build_dev(ctx, s, m_abn.p, &gn);   // "normal" graph = detector's abnormal traces
     if (rc == MR_OK) rc = mr_graph_build_dev(ctx, s, m_nor.p, &ga);
-    if (rc == MR_OK) rc = mr_pagerank(ctx, gn, 0, 0.85, 0.01, 25, precision, 0);
-    if (rc == MR_OK) rc = mr_pagerank(ctx, ga, 1, 0.85, 0.01, 25, precision, 0);
+    if (rc == MR_OK) {   // both PageRanks in one batched launch per iteration
+        mr_graph* both[2] = {gn, ga};
+        const int anom[2] = {0, 1};
+        rc = mr_pagerank_batch(ctx, both, anom, 2, 0.85, 0.01, 25, precision, 0);
+    }
     if (rc != MR_OK) {
         delete gn;
         delete ga;

@@ -257,31 +257,62 @@ __global__ void k_iter_init(const float* w_t, const float* u_o, int32_t N, int32
     if (i < 6 * MSH) mslot[i] = i < 2 * MSH ? d2bits(1.0) : 0ull;
 }
 
-// One Jacobi iteration k -> k+1 in ONE launch.  Maxima are exchanged as the bit patterns of
-// non-negative doubles through atomicMax (exact and order-independent); slot k%3 holds
-// (M_s(k), M_r(k)), slot (k+1)%3 collects iteration k+1, slot (k+2)%3 is cleared here for k+2.
-// s' is carried unnormalised together with su'[o] = u_o * s'[o]; the division by M_s(k) is
-// applied to each finished sum instead of to every term.
-template <class Q, int VW>
-__global__ void __launch_bounds__(TB) k_iter(
-    // trace role
-    const int64_t* __restrict__ rs_off, const int32_t* __restrict__ rs_ops, const double* __restrict__ su_cur,
-    const float* __restrict__ c_t, const float* __restrict__ w_t, Q* __restrict__ q_next, int32_t T, int32_t N,
-    int32_t n_tblocks, double d, double alpha, int lds_su,
-    // op role
-    const int64_t* __restrict__ sr_off, const int32_t* __restrict__ sr_trs, const int32_t* __restrict__ seg_op,
-    const int64_t* __restrict__ seg_beg, const int32_t* __restrict__ op_seg, const Q* __restrict__ q_cur,
-    double* part, int32_t nseg, uint32_t* op_cnt, uint32_t epoch, const int64_t* __restrict__ ss_off,
-    const int32_t* __restrict__ ss_par, const float* __restrict__ pw, const float* __restrict__ u_o,
-    const double* __restrict__ sp_cur, double* __restrict__ sp_next, double* __restrict__ su_next,
-    unsigned long long* mslot, int k3) {
+// Per-graph view for the batched iteration: one launch per Jacobi iteration covers every graph
+// of a batch (the two graphs of an RCA window, or many windows), each graph owning a contiguous
+// range of blocks [blk0, blk0 + n_tb + n_ob).
+struct GDev {
+    const int64_t* rs_off;
+    const int32_t* rs_ops;
+    const float* c_t;
+    const float* w_t;
+    const float* u_o;
+    const float* pw;
+    const int64_t* sr_off;
+    const int32_t* sr_trs;
+    const int32_t* seg_op;
+    const int64_t* seg_beg;
+    const int32_t* op_seg;
+    const int64_t* ss_off;
+    const int32_t* ss_par;
+    void* q[2];
+    double* sub[2];
+    double* spb[2];
+    double* part;
+    uint32_t* op_cnt;
+    unsigned long long* mslot;
+    int32_t T, N, nseg, n_tb, lds_su, blk0;
+};
+
+// One Jacobi iteration k -> k+1.  Maxima are exchanged as the bit patterns of non-negative
+// doubles through atomicMax (exact and order-independent); slot k%3 holds (M_s(k), M_r(k)),
+// slot (k+1)%3 collects iteration k+1, slot (k+2)%3 is cleared here for k+2.  s' is carried
+// unnormalised together with su'[o] = u_o * s'[o]; the division by M_s(k) is applied to each
+// finished sum instead of to every term.
+template <class Q>
+__global__ void __launch_bounds__(TB) k_iter(const GDev* __restrict__ gs, int32_t ng, double d, double alpha, int it) {
     extern __shared__ double lds[];
     __shared__ double red[TB / WAVE];
     __shared__ double msr[2];
+    __shared__ int32_t sg;
+    if (threadIdx.x == 0) {   // this block's graph: the last one whose blk0 <= blockIdx.x
+        int32_t lo = 0, hi = ng - 1;
+        while (lo < hi) {
+            const int32_t mid = (lo + hi + 1) >> 1;
+            if (gs[mid].blk0 <= (int32_t)blockIdx.x) lo = mid; else hi = mid - 1;
+        }
+        sg = lo;
+    }
+    __syncthreads();
+    const GDev& G = gs[sg];
+    const int32_t lb = (int32_t)blockIdx.x - G.blk0;
+    const int cur = it & 1, nxt = cur ^ 1, k3 = it % 3;
+    const uint32_t epoch = (uint32_t)it + 1u;
+    const int32_t T = G.T, N = G.N;
+    unsigned long long* mslot = G.mslot;
     // slot layout: [k%3][s|r][MSH]
     const unsigned long long* Mcur = mslot + (size_t)2 * MSH * k3;
     unsigned long long* Mnext = mslot + (size_t)2 * MSH * ((k3 + 1) % 3);
-    if (blockIdx.x == 0 && threadIdx.x < 2 * MSH) mslot[(size_t)2 * MSH * ((k3 + 2) % 3) + threadIdx.x] = 0ull;
+    if (lb == 0 && threadIdx.x < 2 * MSH) mslot[(size_t)2 * MSH * ((k3 + 2) % 3) + threadIdx.x] = 0ull;
     if (threadIdx.x < WAVE) {
         double ms = bits2d(Mcur[threadIdx.x]), mr = bits2d(Mcur[MSH + threadIdx.x]);
         ms = wave_max(ms);
@@ -294,88 +325,68 @@ __global__ void __launch_bounds__(TB) k_iter(
     __syncthreads();
     const double Ms = msr[0], Mr = msr[1];
     const int shard = blockIdx.x % MSH;
-    if ((int32_t)blockIdx.x < n_tblocks) {
+    if (lb < G.n_tb) {
         // ---- trace role: r'[t] = d * (sum_o u_o s'_k[o]) / M_s(k) + c_t  (pagerank.py:125)
-        const double* su = su_cur;
-        if (lds_su) {
-            for (int32_t o = threadIdx.x; o < N; o += TB) lds[o] = su_cur[o];
+        // The block's contiguous id range is read coalesced in rounds of VCAP ids (all loads in
+        // flight before any gather), su' gathered from LDS into LDS, then each thread continues
+        // its own trace's sum in node order.
+        const int64_t* __restrict__ rs_off = G.rs_off;
+        const int32_t* __restrict__ rs_ops = G.rs_ops;
+        const double* su = G.sub[cur];
+        if (G.lds_su) {
+            for (int32_t o = threadIdx.x; o < N; o += TB) lds[o] = su[o];
             su = lds;
         }
+        double* vals = lds + (G.lds_su ? N : 0);
+        const int32_t t0 = lb * TB;
+        const int32_t t1 = min(t0 + TB, T);
+        const int64_t e0 = rs_off[t0], e1 = rs_off[t1];
+        const int32_t t = t0 + threadIdx.x;
+        const bool own = t < T;
+        const int64_t a = own ? rs_off[t] : 0, b = own ? rs_off[t + 1] : 0;
+        double acc = 0.0;
+        for (int64_t lo = e0; lo < e1; lo += VCAP) {
+            const int64_t hi = min(lo + (int64_t)VCAP, e1);
+            __syncthreads();
+            int32_t id[VCAP / TB];
+#pragma unroll
+            for (int j = 0; j < VCAP / TB; ++j) id[j] = rs_ops[min(lo + threadIdx.x + (int64_t)j * TB, hi - 1)];
+#pragma unroll
+            for (int j = 0; j < VCAP / TB; ++j) {
+                const int64_t e = lo + threadIdx.x + (int64_t)j * TB;
+                if (e < hi) vals[e - lo] = su[id[j]];
+            }
+            __syncthreads();
+            const int64_t x0 = max(a, lo), x1 = min(b, hi);
+            int64_t e = x0;
+            for (; e + 4 <= x1; e += 4) {
+                const double v0 = vals[e - lo], v1 = vals[e + 1 - lo], v2 = vals[e + 2 - lo], v3 = vals[e + 3 - lo];
+                acc += v0;
+                acc += v1;
+                acc += v2;
+                acc += v3;
+            }
+            for (; e < x1; ++e) acc += vals[e - lo];
+        }
         double rmax = -__builtin_huge_val();
-        if (VW == 0) {
-            // LDS-staged: the block's contiguous id range is read coalesced in rounds of VCAP ids
-            // (all loads in flight before any gather), su' gathered into LDS, then each thread
-            // continues its own trace's sum in node order
-            double* vals = lds + (lds_su ? N : 0);
-            const int32_t t0 = blockIdx.x * TB;
-            const int32_t t1 = min(t0 + TB, T);
-            const int64_t e0 = rs_off[t0], e1 = rs_off[t1];
-            const int32_t t = t0 + threadIdx.x;
-            const bool own = t < T;
-            const int64_t a = own ? rs_off[t] : 0, b = own ? rs_off[t + 1] : 0;
-            double acc = 0.0;
-            for (int64_t lo = e0; lo < e1; lo += VCAP) {
-                const int64_t hi = min(lo + (int64_t)VCAP, e1);
-                __syncthreads();
-                int32_t id[VCAP / TB];
-#pragma unroll
-                for (int j = 0; j < VCAP / TB; ++j) id[j] = rs_ops[min(lo + threadIdx.x + (int64_t)j * TB, hi - 1)];
-#pragma unroll
-                for (int j = 0; j < VCAP / TB; ++j) {
-                    const int64_t e = lo + threadIdx.x + (int64_t)j * TB;
-                    if (e < hi) vals[e - lo] = su[id[j]];
-                }
-                __syncthreads();
-                const int64_t x0 = max(a, lo), x1 = min(b, hi);
-                int64_t e = x0;
-                for (; e + 4 <= x1; e += 4) {
-                    const double v0 = vals[e - lo], v1 = vals[e + 1 - lo], v2 = vals[e + 2 - lo], v3 = vals[e + 3 - lo];
-                    acc += v0;
-                    acc += v1;
-                    acc += v2;
-                    acc += v3;
-                }
-                for (; e < x1; ++e) acc += vals[e - lo];
-            }
-            if (own) {
-                const double rp = d * (acc / Ms) + (double)c_t[t];
-                q_next[t] = (Q)((double)w_t[t] * rp);
-                rmax = rp;
-            }
-        } else {
-            // CSR-vector: VW lanes per trace, coalesced ids, LDS gather, fixed butterfly
-            if (lds_su) __syncthreads();
-            constexpr int VWE = VW > 0 ? VW : 1;
-            constexpr int G = TB / VWE;
-            const int grp = threadIdx.x / VWE, gl = threadIdx.x % VWE;
-#pragma unroll 4
-            for (int step = 0; step < VWE; ++step) {
-                const int32_t t = (int32_t)blockIdx.x * TB + step * G + grp;
-                double acc = 0.0;
-                if (t < T) {
-                    const int64_t a = rs_off[t], b = rs_off[t + 1];
-                    for (int64_t e = a + gl; e < b; e += VWE) acc += su[rs_ops[e]];
-                }
-#pragma unroll
-                for (int m = VWE / 2; m >= 1; m >>= 1) acc += __shfl_xor(acc, m, WAVE);
-                if (gl == 0 && t < T) {
-                    const double rp = d * (acc / Ms) + (double)c_t[t];
-                    q_next[t] = (Q)((double)w_t[t] * rp);
-                    rmax = nmax(rmax, rp);
-                }
-            }
+        if (own) {
+            const double rp = d * (acc / Ms) + (double)G.c_t[t];
+            ((Q*)G.q[nxt])[t] = (Q)((double)G.w_t[t] * rp);
+            rmax = rp;
         }
         rmax = block_max(rmax, red);
         if (threadIdx.x == 0) atomicMax(&Mnext[MSH + shard], d2bits(rmax));
         return;
     }
     // ---- op role: one wave per fixed segment of an op's trace list  (pagerank.py:122-124)
-    const int32_t seg = ((int32_t)blockIdx.x - n_tblocks) * (TB / WAVE) + (int32_t)(threadIdx.x / WAVE);
-    if (seg >= nseg) return;
+    const int32_t seg = (lb - G.n_tb) * (TB / WAVE) + (int32_t)(threadIdx.x / WAVE);
+    if (seg >= G.nseg) return;
     const int lane = threadIdx.x & (WAVE - 1);
-    const int32_t o = seg_op[seg];
-    const int64_t b = seg_beg[seg];
-    const int64_t end = min(b + (int64_t)SEG, sr_off[o + 1]);
+    const int32_t o = G.seg_op[seg];
+    const int64_t b = G.seg_beg[seg];
+    const int64_t end = min(b + (int64_t)SEG, G.sr_off[o + 1]);
+    const Q* __restrict__ q_cur = (const Q*)G.q[cur];
+    const int32_t* __restrict__ sr_trs = G.sr_trs;
     double acc = 0.0;
     if (end > b) {   // ids first, then every gather, then the sum in element order
         int32_t id[SEG / WAVE];
@@ -389,14 +400,14 @@ __global__ void __launch_bounds__(TB) k_iter(
             if (b + lane + (int64_t)j * WAVE < end) acc += v[j];
     }
     acc = wave_sum(acc);
-    const int32_t s0 = op_seg[o], s1 = op_seg[o + 1];
+    const int32_t s0 = G.op_seg[o], s1 = G.op_seg[o + 1];
     uint32_t old = 0;
     if (lane == 0) {
         if (s1 - s0 > 1) {
             // hand-off without L2 write-back: write-through (sc1) payload, drain, relaxed counter
-            __hip_atomic_store(&part[seg], acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&G.part[seg], acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            old = __hip_atomic_fetch_add(&op_cnt[o], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            old = __hip_atomic_fetch_add(&G.op_cnt[o], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
             old = epoch - 1u;   // single segment: this wave finishes the op
         }
@@ -407,21 +418,22 @@ __global__ void __launch_bounds__(TB) k_iter(
     double sum = 0.0;
     if (s1 - s0 > 1) {
         for (int32_t s = s0 + lane; s < s1; s += WAVE)
-            sum += __hip_atomic_load(&part[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            sum += __hip_atomic_load(&G.part[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         sum = wave_sum(sum);
     } else {
         sum = acc;
     }
+    const double* sp_cur = G.spb[cur];
     double bb = 0.0;
-    for (int64_t e = ss_off[o] + lane; e < ss_off[o + 1]; e += WAVE) {
-        const int32_t p = ss_par[e];
-        bb += (double)pw[p] * sp_cur[p];
+    for (int64_t e = G.ss_off[o] + lane; e < G.ss_off[o + 1]; e += WAVE) {
+        const int32_t p = G.ss_par[e];
+        bb += (double)G.pw[p] * sp_cur[p];
     }
     bb = wave_sum(bb);
     if (lane == 0) {
         const double v = d * (sum / Mr + alpha * (bb / Ms));      // pagerank.py:122-124
-        sp_next[o] = v;
-        su_next[o] = (double)u_o[o] * v;
+        G.spb[nxt][o] = v;
+        G.sub[nxt][o] = (double)G.u_o[o] * v;
         atomicMax(&Mnext[o % MSH], d2bits(v));
     }
 }
@@ -462,34 +474,6 @@ __global__ void __launch_bounds__(1024) k_weights(const double* sp, const unsign
     const double total = tot;
     for (int32_t o = threadIdx.x; o < N; o += blockDim.x) weight[o] = sn[o] * total / (double)N;
     if (threadIdx.x == 0) scal[4] = total;
-}
-
-template <class Q> Q* qbuf(mr_graph* g, int i);
-template <> double* qbuf<double>(mr_graph* g, int i) { return g->q64[i].p; }
-template <> float* qbuf<float>(mr_graph* g, int i) { return g->q32[i].p; }
-
-template <class Q, int VW>
-void launch_iter_vw(mr_ctx* ctx, mr_graph* g, int n_tb, int n_oblocks, size_t lds, double d, double alpha,
-                    int lds_su, int cur, int nxt, int it) {
-    hipLaunchKernelGGL((k_iter<Q, VW>), dim3(n_tb + n_oblocks), dim3(TB), lds, ctx->stream, g->rs_off.p, g->rs_ops.p,
-                       g->sub[cur].p, g->c_t.p, g->w_t.p, qbuf<Q>(g, nxt), g->T, g->N, n_tb, d, alpha, lds_su,
-                       g->sr_off.p, g->sr_trs.p, g->seg_op.p, g->seg_beg.p, g->op_seg.p, qbuf<Q>(g, cur), g->part.p,
-                       g->nseg, g->op_cnt.p, (uint32_t)(it + 1), g->ss_off.p, g->ss_par.p, g->pw.p, g->u_o.p,
-                       g->spb[cur].p, g->spb[nxt].p, g->sub[nxt].p, g->mslot.p, it % 3);
-}
-
-template <class Q>
-int launch_iter(mr_ctx* ctx, mr_graph* g, int vw, int n_tb, int n_oblocks, size_t lds, double d, double alpha,
-                int lds_su, int cur, int nxt, int it) {
-    switch (vw) {
-        case 4: launch_iter_vw<Q, 4>(ctx, g, n_tb, n_oblocks, lds, d, alpha, lds_su, cur, nxt, it); break;
-        case 8: launch_iter_vw<Q, 8>(ctx, g, n_tb, n_oblocks, lds, d, alpha, lds_su, cur, nxt, it); break;
-        case 16: launch_iter_vw<Q, 16>(ctx, g, n_tb, n_oblocks, lds, d, alpha, lds_su, cur, nxt, it); break;
-        case 32: launch_iter_vw<Q, 32>(ctx, g, n_tb, n_oblocks, lds, d, alpha, lds_su, cur, nxt, it); break;
-        case 64: launch_iter_vw<Q, 64>(ctx, g, n_tb, n_oblocks, lds, d, alpha, lds_su, cur, nxt, it); break;
-        default: launch_iter_vw<Q, 0>(ctx, g, n_tb, n_oblocks, lds, d, alpha, lds_su, cur, nxt, it); break;
-    }
-    return MR_OK;
 }
 }  // namespace
 
@@ -534,21 +518,13 @@ int mr_graph_prepare(mr_ctx* ctx, mr_graph* g) {
     hipLaunchKernelGGL(k_fill_segments, dim3(cdiv(N + 1, 256)), dim3(256), 0, ctx->stream, op_seg64.p, g->sr_off.p,
                        g->op_seg.p, g->seg_op.p, g->seg_beg.p, N);
     MR_TRY_HIP(ctx, hipGetLastError());
-    MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));  // scratch buffers die here
-    return MR_OK;
+    return MR_OK;   // scratch returns to the stream-ordered pool: no sync needed
 }
 
-extern "C" int mr_pagerank(mr_ctx* ctx, mr_graph* g, int anomaly, double d, double alpha, int iters,
-                           int precision, uint32_t flags) {
-    if (!ctx || !g || g->ctx != ctx) return mr_fail(ctx, MR_ERR_STATE, "mr_pagerank: bad handles");
-    if (iters < 0) return mr_fail(ctx, MR_ERR_ARG, "iters < 0");
-    const int32_t N = g->N, T = g->T;
-    if (N == 0 || T == 0)   // np.amax of an empty vector (pagerank.py:126-127)
-        return mr_fail(ctx, MR_ERR_VALUE, "zero-size array to reduction operation maximum which has no identity");
-    MR_TRY_HIP(ctx, hipSetDevice(ctx->device));
+// kinds, preference vector and iteration state of one graph (everything before the iterations)
+static int pagerank_setup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool fp32, uint32_t flags) {
     hipStream_t st = ctx->stream;
-    const bool fp32 = precision == MR_FP32;
-    const int n_tblocks = cdiv(T, TB);
+    const int32_t N = g->N, T = g->T;
     uint64_t cap = 1;
     while (cap < 2ull * (uint64_t)T) cap <<= 1;
     const int32_t n_pr = g->n_pr;
@@ -607,47 +583,108 @@ extern "C" int mr_pagerank(mr_ctx* ctx, mr_graph* g, int anomaly, double d, doub
         hipLaunchKernelGGL(k_pref_apply, dim3(nbp), dim3(TB), 0, st, g->kind.p, prt, prl, g->len_t.p, n_pr,
                            g->scal.p, anomaly, cd, g->pref.p, g->c_t.p);
     MR_DEBUG_CHECK(ctx, "k_pref_apply");
-    // ---- power iteration
-    hipLaunchKernelGGL(k_iter_init, dim3(cdiv(std::max<int64_t>({N, T, 6 * MSH}), 256)), dim3(256), 0, st, g->w_t.p, g->u_o.p, N, T,
-                       g->spb[0].p, g->sub[0].p, g->q64[0].p, g->q32[0].p, (int)fp32, g->mslot.p);
+    hipLaunchKernelGGL(k_iter_init, dim3(cdiv(std::max<int64_t>({N, T, 6 * MSH}), 256)), dim3(256), 0, st, g->w_t.p,
+                       g->u_o.p, N, T, g->spb[0].p, g->sub[0].p, g->q64[0].p, g->q32[0].p, (int)fp32, g->mslot.p);
     MR_DEBUG_CHECK(ctx, "k_iter_init");
-    const int lds_su = N <= LDS_NODES;
-    const size_t lds = ((lds_su ? (size_t)N : 0) + VCAP) * sizeof(double);
-    int n_oblocks = cdiv(g->nseg, TB / WAVE);
-    int n_tb = n_tblocks;
-    if (const char* rm = getenv("MR_ROLE_MASK")) {   // profiling knob: 1 = trace role only, 2 = op role only
-        const int m = atoi(rm);
-        if (!(m & 1)) n_tb = 0;
-        if (!(m & 2)) n_oblocks = 0;
-    }
-    // lanes per trace for the trace role: the average distinct ops per trace, rounded up to 2^k
-    const double avgdeg = (double)g->nnz_rs / (double)T;
-    int vw = avgdeg <= 4 ? 4 : avgdeg <= 8 ? 8 : avgdeg <= 16 ? 16 : avgdeg <= 32 ? 32 : 64;
-    int staged = 1;   // LDS-staged trace role by default (measured faster than CSR-vector at C2)
-    if (const char* tm = getenv("MR_TRACE_MODE")) staged = atoi(tm) == 0;
-    if (staged) vw = 0;
-    // algorithmic bytes of one iteration: op ids once, offsets, the r/v/len_t
-    // streams, call edges and three N-vectors; o = 4-byte offsets below 2^31 nonzeros
+    return MR_OK;
+}
+
+// algorithmic bytes of one iteration of one graph: op ids once, offsets, the
+// r/v/len_t streams, call edges and three N-vectors; o = 4-byte offsets below 2^31 nonzeros
+static double iter_bytes(const mr_graph* g, bool fp32) {
     const double w = fp32 ? 4.0 : 8.0, o = g->nnz_sr < (1ll << 31) ? 4.0 : 8.0;
-    const double b_iter = 4.0 * (double)g->nnz_sr + o * ((double)T + 1) + 4.0 * w * (double)T + (8.0 + w) * (double)g->E +
-                          3.0 * w * (double)N;
-    for (int it = 0; it < iters; ++it) {
-        const int cur = it & 1, nxt = cur ^ 1;
-        mr_prof_begin(ctx);
-        if (fp32) MR_TRY(launch_iter<float>(ctx, g, vw, n_tb, n_oblocks, lds, d, alpha, lds_su, cur, nxt, it));
-        else MR_TRY(launch_iter<double>(ctx, g, vw, n_tb, n_oblocks, lds, d, alpha, lds_su, cur, nxt, it));
-        MR_DEBUG_CHECK(ctx, "k_iter");
-        mr_prof_end(ctx, b_iter);
+    return 4.0 * (double)g->nnz_sr + o * ((double)g->T + 1) + 4.0 * w * (double)g->T + (8.0 + w) * (double)g->E +
+           3.0 * w * (double)g->N;
+}
+
+int mr_pagerank_batch_impl(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly, int ng, double d, double alpha,
+                           int iters, int precision, uint32_t flags) {
+    if (!ctx || ng <= 0 || !gs || !anomaly) return mr_fail(ctx, MR_ERR_ARG, "mr_pagerank: bad arguments");
+    if (iters < 0) return mr_fail(ctx, MR_ERR_ARG, "iters < 0");
+    for (int i = 0; i < ng; ++i) {
+        if (!gs[i] || gs[i]->ctx != ctx) return mr_fail(ctx, MR_ERR_STATE, "mr_pagerank: bad handles");
+        if (gs[i]->N == 0 || gs[i]->T == 0)   // np.amax of an empty vector (pagerank.py:126-127)
+            return mr_fail(ctx, MR_ERR_VALUE, "zero-size array to reduction operation maximum which has no identity");
     }
-    hipLaunchKernelGGL(k_weights, dim3(1), dim3(1024), 0, st, g->spb[iters & 1].p, g->mslot.p, iters % 3, N,
-                       (int)((flags & MR_PR_EXACT_SUMS) != 0), g->sn.p, g->weight.p, g->scal.p);
-    MR_DEBUG_CHECK(ctx, "k_weights");
+    MR_TRY_HIP(ctx, hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    const bool fp32 = precision == MR_FP32;
+    for (int i = 0; i < ng; ++i) MR_TRY(pagerank_setup(ctx, gs[i], anomaly[i], d, fp32, flags));
+    // ---- batched power iteration: one launch per iteration for every graph
+    int mask = 3;
+    if (const char* rm = getenv("MR_ROLE_MASK")) mask = atoi(rm);   // profiling knob: 1 trace / 2 op role
+    std::vector<GDev> hv((size_t)ng);
+    int32_t blocks = 0;
+    size_t lds = VCAP * sizeof(double);
+    double bytes = 0.0;
+    for (int i = 0; i < ng; ++i) {
+        mr_graph* g = gs[i];
+        GDev& v = hv[(size_t)i];
+        v.rs_off = g->rs_off.p;
+        v.rs_ops = g->rs_ops.p;
+        v.c_t = g->c_t.p;
+        v.w_t = g->w_t.p;
+        v.u_o = g->u_o.p;
+        v.pw = g->pw.p;
+        v.sr_off = g->sr_off.p;
+        v.sr_trs = g->sr_trs.p;
+        v.seg_op = g->seg_op.p;
+        v.seg_beg = g->seg_beg.p;
+        v.op_seg = g->op_seg.p;
+        v.ss_off = g->ss_off.p;
+        v.ss_par = g->ss_par.p;
+        for (int j = 0; j < 2; ++j) {
+            v.q[j] = fp32 ? (void*)g->q32[j].p : (void*)g->q64[j].p;
+            v.sub[j] = g->sub[j].p;
+            v.spb[j] = g->spb[j].p;
+        }
+        v.part = g->part.p;
+        v.op_cnt = g->op_cnt.p;
+        v.mslot = g->mslot.p;
+        v.T = g->T;
+        v.N = g->N;
+        v.nseg = (mask & 2) ? g->nseg : 0;
+        v.n_tb = (mask & 1) ? cdiv(g->T, TB) : 0;
+        v.lds_su = g->N <= LDS_NODES;
+        v.blk0 = blocks;
+        blocks += v.n_tb + cdiv(v.nseg, TB / WAVE);
+        if (v.lds_su) lds = std::max(lds, ((size_t)g->N + VCAP) * sizeof(double));
+        bytes += iter_bytes(g, fp32);
+    }
+    DBuf<GDev> dv;
+    MR_TRY(dv.upload(ctx, hv.data(), hv.size()));
+    for (int it = 0; it < iters && blocks > 0; ++it) {
+        mr_prof_begin(ctx);
+        if (fp32) hipLaunchKernelGGL(k_iter<float>, dim3(blocks), dim3(TB), lds, st, dv.p, ng, d, alpha, it);
+        else hipLaunchKernelGGL(k_iter<double>, dim3(blocks), dim3(TB), lds, st, dv.p, ng, d, alpha, it);
+        MR_DEBUG_CHECK(ctx, "k_iter");
+        mr_prof_end(ctx, bytes);
+    }
+    for (int i = 0; i < ng; ++i) {
+        mr_graph* g = gs[i];
+        hipLaunchKernelGGL(k_weights, dim3(1), dim3(1024), 0, st, g->spb[iters & 1].p, g->mslot.p, iters % 3, g->N,
+                           (int)((flags & MR_PR_EXACT_SUMS) != 0), g->sn.p, g->weight.p, g->scal.p);
+        MR_DEBUG_CHECK(ctx, "k_weights");
+    }
     MR_TRY_HIP(ctx, hipGetLastError());
     // the only host round trip of the call: error words raised by the kernels
-    int32_t hflag[4] = {0, 0, 0, 0};
-    MR_TRY_HIP(ctx, hipMemcpyAsync(hflag, g->flag.p, sizeof hflag, hipMemcpyDeviceToHost, st));
+    std::vector<int32_t> hflag((size_t)4 * ng, 0);
+    for (int i = 0; i < ng; ++i)
+        MR_TRY_HIP(ctx, hipMemcpyAsync(&hflag[(size_t)4 * i], gs[i]->flag.p, 4 * sizeof(int32_t), hipMemcpyDeviceToHost, st));
     MR_TRY_HIP(ctx, hipStreamSynchronize(st));
-    if (hflag[0] & 1) return mr_fail(ctx, MR_ERR_STATE, "trace-kind hash collision (retry with another seed)");
-    if (anomaly && (hflag[0] & 2)) return mr_fail(ctx, MR_ERR_ZERODIV, "float division by zero");
+    for (int i = 0; i < ng; ++i) {
+        if (hflag[(size_t)4 * i] & 1) return mr_fail(ctx, MR_ERR_STATE, "trace-kind hash collision (retry with another seed)");
+        if (anomaly[i] && (hflag[(size_t)4 * i] & 2)) return mr_fail(ctx, MR_ERR_ZERODIV, "float division by zero");
+    }
     return MR_OK;
+}
+
+extern "C" int mr_pagerank(mr_ctx* ctx, mr_graph* g, int anomaly, double d, double alpha, int iters,
+                           int precision, uint32_t flags) {
+    return mr_pagerank_batch_impl(ctx, &g, &anomaly, 1, d, alpha, iters, precision, flags);
+}
+
+extern "C" int mr_pagerank_batch(mr_ctx* ctx, mr_graph* const* graphs, const int* anomaly, int n_graphs, double d,
+                                 double alpha, int iters, int precision, uint32_t flags) {
+    return mr_pagerank_batch_impl(ctx, graphs, anomaly, n_graphs, d, alpha, iters, precision, flags);
 }
