@@ -108,7 +108,7 @@ int mr_graph_fetch(mr_graph* g, double* weight /*[N] host*/, int32_t* coverage /
                    double* kind /*[T] host or NULL*/, float* pref /*[T] host or NULL*/);
 
 /* ------------------------------------------------------------------ spans (int-coded columns)
- * The DataFrame of online_rca.py:377-404 after factorisation (microrank_amd/spans.py).
+ * The DataFrame of online_rca.py:221-248 after factorisation (microrank_amd/spans.py).
  */
 typedef struct mr_span_cols {
     int64_t n_spans;
@@ -126,7 +126,7 @@ typedef struct mr_span_cols {
 int mr_spans_upload(mr_ctx* ctx, const mr_span_cols* cols, mr_spans** out);
 int mr_spans_free(mr_spans* s);
 
-/* K1: preprocess_data.get_pagerank_graph (preprocess_data.py:358-383) on the device.
+/* K1: preprocess_data.get_pagerank_graph (preprocess_data.py:146-171) on the device.
  * trace_mask[n_traces] (host, 0/1) selects the trace_list.  Node order = sorted parent ops,
  * then never-parent ops in first-appearance row order (T10).  The parent join ignores
  * traceID (T11). */
@@ -139,7 +139,7 @@ int mr_graph_export(const mr_graph* g, int64_t* sr_off /*[T+1]*/, int32_t* sr_op
                     int32_t* ss_par /*[E]*/, int32_t* nchild /*[N]*/);
 
 /* ------------------------------------------------------------------ K3: spectrum + top-k
- * online_rca.calculate_spectrum_without_delay_list (online_rca.py:189-308).  Inputs are in the
+ * online_rca.calculate_spectrum_without_delay_list (online_rca.py:33-152).  Inputs are in the
  * reference's iteration order: the anomaly_result nodes first, then normal-only nodes.
  * has_a/has_n mark membership; method is an index into
  * {dstar2, ochiai, jaccard, sorensendice, m1, m2, goodman, tarantula, russellrao, hamann,
@@ -152,7 +152,7 @@ int mr_spectrum(mr_ctx* ctx, int32_t n, const uint8_t* has_a, const double* a_w,
                 int32_t* n_out, int32_t* zerodiv);
 
 /* ------------------------------------------------------------------ K4: SLO
- * preprocess_data.get_operation_slo (preprocess_data.py:262-290), the semantic body of the
+ * preprocess_data.get_operation_slo (preprocess_data.py:50-78), the semantic body of the
  * broken anormaly_detector.get_slo (anormaly_detector.py:22-27, T16): per svcop code,
  * round(mean/1000, 4) and round(std/1000, 4) (population std, numpy pairwise order, T13).
  * count[o] = 0 marks an op with no spans. */
@@ -161,7 +161,7 @@ int mr_slo(mr_ctx* ctx, const mr_spans* s, double* mean /*[n_svcops]*/, double* 
 
 /* ------------------------------------------------------------------ K5: detector
  * anormaly_detector.system_anomaly_detect (anormaly_detector.py:44-84) with
- * get_operation_duration_data (preprocess_data.py:309-334): window [t0, t1] on trace-level
+ * get_operation_duration_data (preprocess_data.py:97-122): window [t0, t1] on trace-level
  * times (inclusive), real = max duration/1000, expect = sum over ops (sorted order) of
  * count*a3[op] with a3 = mean+3*std, ops without SLO (a3_valid=0) contribute 0.
  * state[n_traces] (host): 0 not in window / dropped, 1 normal, 2 abnormal.
@@ -172,7 +172,7 @@ int mr_detect(mr_ctx* ctx, const mr_spans* s, int64_t t0, int64_t t1, const doub
               int64_t* n_spans_in_window);
 
 /* ------------------------------------------------------------------ whole RCA window on device
- * online_rca.online_anomaly_detect_RCA body for one window (online_rca.py:320-371):
+ * online_rca.online_anomaly_detect_RCA body for one window (online_rca.py:164-215):
  * detect -> (swapped, T1) two graph builds -> two PageRanks -> spectrum -> top list, with
  * all intermediates resident in HBM.  out_idx are podop codes. */
 int mr_rca_window(mr_ctx* ctx, const mr_spans* s, int64_t t0, int64_t t1, const double* a3,

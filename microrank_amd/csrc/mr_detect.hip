@@ -1,6 +1,6 @@
 // K5: anormaly_detector.system_anomaly_detect (anormaly_detector.py:44-84) with
-// preprocess_data.get_operation_duration_data (preprocess_data.py:309-334), and the whole
-// RCA window of online_rca.online_anomaly_detect_RCA (online_rca.py:320-371) on the device.
+// preprocess_data.get_operation_duration_data (preprocess_data.py:97-122), and the whole
+// RCA window of online_rca.online_anomaly_detect_RCA (online_rca.py:164-215) on the device.
 //
 // Detector: spans whose trace-level [start, end] lies in [t0, t1] (inclusive, T15) are sorted
 // by (trace, service-op); per trace, expect = sum over its ops in name order of
@@ -9,6 +9,7 @@
 // dropped (:329).  The sum is sequential per trace with separate multiply and add (T14), so
 // the partition is bit-exact.
 #include <algorithm>
+#include <climits>
 
 #include "mr_prim.h"
 #include "mr_sort.h"
@@ -23,12 +24,27 @@ __global__ void k_win_flags(const int64_t* ts, const int64_t* te, int64_t S, int
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < S) flag[i] = (ts[i] >= t0 && te[i] <= t1) ? 1 : 0;
 }
+// Spans of a trace are mostly adjacent in DataFrame order, so a per-span atomicMax on
+// tmax[trace] serialises lanes on one address.  A segmented max over the wave (combine with
+// lane-off when it belongs to the same trace; max is idempotent, so non-adjacent runs of one
+// trace merging is harmless) leaves the run maximum in the run's last lane, which alone issues
+// the atomic.
 __global__ void k_win_keys(const int32_t* flag, const int64_t* pos, int64_t S, const int32_t* trace, const int32_t* svcop,
                            const int64_t* dur, int nb, uint64_t* keys, long long* tmax) {
-    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= S || !flag[i]) return;
-    keys[pos[i]] = ((uint64_t)(uint32_t)trace[i] << nb) | (uint32_t)svcop[i];
-    atomicMax(&tmax[trace[i]], (long long)dur[i]);
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool in = i < S && flag[i];
+    const int32_t t = in ? trace[i] : -1;
+    long long v = in ? (long long)dur[i] : LLONG_MIN;
+    if (in) keys[pos[i]] = ((uint64_t)(uint32_t)t << nb) | (uint32_t)svcop[i];
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int32_t to = __shfl_up(t, off, 64);
+        const long long vo = __shfl_up(v, off, 64);
+        if (lane >= off && to == t && vo > v) v = vo;
+    }
+    const int32_t tn = __shfl_down(t, 1, 64);
+    if (in && (lane == 63 || tn != t)) atomicMax(&tmax[t], v);
 }
 __global__ void k_win_runs(const uint64_t* keys, int64_t n, int32_t* head) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -49,36 +65,37 @@ __global__ void k_win_traces(const uint64_t* rkey, const int64_t* rstart, int64_
                              const int64_t* tfirst, const long long* tmax, const double* a3, const uint8_t* a3v,
                              int32_t n_traces, uint8_t* state, int32_t* counts) {
     const int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n_traces) return;
-    const int64_t r0 = tfirst[t];
-    if (r0 < 0) {
-        state[t] = 0;
-        return;
+    int st = 0;
+    if (t < n_traces) {
+        const int64_t r0 = tfirst[t];
+        const long long mx = r0 < 0 ? 0 : tmax[t];
+        if (r0 >= 0 && mx > 0) {   // grouped[grouped['duration'] > 0] (preprocess_data.py:117)
+            double expect = 0.0;
+            const uint64_t mask = (1ull << nb) - 1ull;
+            for (int64_t r = r0; r < nruns && (rkey[r] >> nb) == (uint64_t)t; ++r) {
+                const int32_t op = (int32_t)(rkey[r] & mask);
+                const int64_t end = r + 1 < nruns ? rstart[r + 1] : nspan;
+                const int64_t cnt = end - rstart[r];
+                if (a3v[op]) expect += (double)cnt * a3[op];   // anormaly_detector.py:64-65
+            }
+            const double real = (double)mx / 1000.0;           // :58
+            st = real > expect ? 2 : 1;                        // :69
+        }
+        state[t] = (uint8_t)st;
     }
-    const long long mx = tmax[t];
-    if (!(mx > 0)) {   // grouped[grouped['duration'] > 0] (preprocess_data.py:329)
-        state[t] = 0;
-        return;
+    // one counter update per wave (200k same-address atomics cost ~2 ms)
+    const uint64_t ab = __ballot(st == 2), nr = __ballot(st == 1);
+    if ((threadIdx.x & 63) == 0) {
+        if (ab) atomicAdd(&counts[0], (int32_t)__popcll(ab));
+        if (nr) atomicAdd(&counts[1], (int32_t)__popcll(nr));
     }
-    double expect = 0.0;
-    const uint64_t mask = (1ull << nb) - 1ull;
-    for (int64_t r = r0; r < nruns && (rkey[r] >> nb) == (uint64_t)t; ++r) {
-        const int32_t op = (int32_t)(rkey[r] & mask);
-        const int64_t end = r + 1 < nruns ? rstart[r + 1] : nspan;
-        const int64_t cnt = end - rstart[r];
-        if (a3v[op]) expect += (double)cnt * a3[op];   // anormaly_detector.py:64-65
-    }
-    const double real = (double)mx / 1000.0;           // :58
-    const bool ab = real > expect;                     // :69
-    state[t] = ab ? 2 : 1;
-    atomicAdd(&counts[ab ? 0 : 1], 1);
 }
 __global__ void k_fill_i64(int64_t* p, int64_t n, int64_t v) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) p[i] = v;
 }
 
-// union of the two graphs' nodes in the reference's spectrum order (online_rca.py:201-225)
+// union of the two graphs' nodes in the reference's spectrum order (online_rca.py:45-69)
 __global__ void k_union_a(const int32_t* a_podop, int32_t Na, const double* a_w, const int32_t* a_cov, int32_t* pos_of_code,
                           uint8_t* flags, double* ua_w, int64_t* ua_num, int32_t* uc) {
     int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -204,7 +221,7 @@ __global__ void k_top_codes(const int32_t* idx, const int32_t* uc, int32_t k, in
 }
 }  // namespace
 
-// One RCA window (online_rca.py:320-371) with every intermediate in HBM.
+// One RCA window (online_rca.py:164-215) with every intermediate in HBM.
 extern "C" int mr_rca_window(mr_ctx* ctx, const mr_spans* s, int64_t t0, int64_t t1, const double* a3,
                              const uint8_t* a3_valid, int method, int32_t top_max, int precision, int32_t* out_podop,
                              double* out_score, int32_t* n_out, int64_t* edges_traversed, int32_t* n_abnormal,
@@ -273,7 +290,7 @@ extern "C" int mr_rca_window(mr_ctx* ctx, const mr_spans* s, int64_t t0, int64_t
     hipLaunchKernelGGL(k_union_n, dim3(cdiv(Nn, 256)), dim3(256), 0, st, gn->node_podop.p, Nn, gn->weight.p, gn->cov.p,
                        pos_of_code.p, only.p, opos.p, Na, fl.p, ua_w.p, ua_num.p, un_w.p, un_num.p, uc.p);
     const int32_t n = Na + (int32_t)nonly;
-    const int32_t k = std::min(n, std::max(0, top_max + 6));   // online_rca.py:304
+    const int32_t k = std::min(n, std::max(0, top_max + 6));   // online_rca.py:148
     if ((rc = idx.alloc(ctx, std::max(k, 1))) || (rc = sc.alloc(ctx, std::max(k, 1)))) return cleanup(rc);
     // A = len(abnormal_list) = detector normal count, N = len(normal_list) = detector abnormal count
     rc = mr_spectrum_dev(ctx, n, fl.p, ua_w.p, ua_num.p, un_w.p, un_num.p, nn, na, method, k, idx.p, sc.p, nullptr, zf.p);

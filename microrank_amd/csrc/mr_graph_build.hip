@@ -1,4 +1,4 @@
-// K1: preprocess_data.get_pagerank_graph (preprocess_data.py:358-383) on gfx950.
+// K1: preprocess_data.get_pagerank_graph (preprocess_data.py:146-171) on gfx950.
 //
 // From HBM-resident int-coded span columns and a trace mask (the trace_list, :360):
 //   1. compact the selected rows, keeping row order (first appearance, T10)

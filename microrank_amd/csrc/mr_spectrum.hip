@@ -1,4 +1,4 @@
-// K3: online_rca.calculate_spectrum_without_delay_list (online_rca.py:189-308) on gfx950.
+// K3: online_rca.calculate_spectrum_without_delay_list (online_rca.py:33-152) on gfx950.
 //
 // One thread per node computes (ef, nf, ep, np) from the two PageRank weight/coverage vectors
 // (:201-225) and applies one of the 13 formulas (:231-298) with the reference's operation

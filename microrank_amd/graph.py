@@ -1,7 +1,7 @@
 """Host side of the PageRank graph: dicts <-> incidence arrays <-> device handle.
 
 ``trace_pagerank`` receives the four dicts of ``get_pagerank_graph``
-(preprocess_data.py:358-383).  Two ways in:
+(preprocess_data.py:146-171).  Two ways in:
 
 * the dicts are :class:`GraphDicts` views produced by this package's
   ``get_pagerank_graph`` -- they carry the device graph built by K1, nothing is converted;

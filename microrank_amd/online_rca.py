@@ -1,9 +1,9 @@
 """Drop-in for the reference module ``online_rca`` (online_rca.py).
 
 * ``calculate_spectrum_without_delay_list`` -- the weighted spectrum scores and the stable
-  top list (online_rca.py:189-308), computed on the GPU (K3, csrc/mr_spectrum.hip); printing,
+  top list (online_rca.py:33-152), computed on the GPU (K3, csrc/mr_spectrum.hip); printing,
   argument names and return types as in the reference.
-* ``online_anomaly_detect_RCA`` -- the sliding-window driver (online_rca.py:311-372), line for
+* ``online_anomaly_detect_RCA`` -- the sliding-window driver (online_rca.py:155-216), line for
   line the same control flow, with every ranking step on the GPU.
 * ``rca_window`` -- one whole window (detect -> 2 graphs -> 2 PageRanks -> spectrum) in a
   single C-ABI call with every intermediate resident in HBM (used by bench.py).
@@ -28,7 +28,7 @@ from .spans import to_ns
 
 
 def timestamp(datetime):
-    """online_rca.py:182-186."""
+    """online_rca.py:26-30."""
     return int(time.mktime(time.strptime(str(datetime), "%Y-%m-%d %H:%M:%S"))) * 1000
 
 
@@ -98,7 +98,7 @@ def calculate_spectrum_without_delay_list(anomaly_result, normal_result, anomaly
 
 
 def online_anomaly_detect_RCA(data, slo, operation_list):
-    """online_rca.online_anomaly_detect_RCA (online_rca.py:311-372): 5-minute windows, a triggered
+    """online_rca.online_anomaly_detect_RCA (online_rca.py:155-216): 5-minute windows, a triggered
     window advances by 9 minutes; the detector's lists are unpacked swapped (T1), an empty
     window makes the unpacking raise TypeError (T2); result.csv is rewritten per trigger."""
     window_normal = pd.Timedelta(minutes=5)

@@ -27,7 +27,7 @@ from . import _lib
 from ._lib import SpanCols, ptr
 from .spans import UI_SERVICE, SpanTable, op_display
 
-ROOT_INDEX = "root"   # preprocess_data.py:219
+ROOT_INDEX = "root"   # preprocess_data.py:7
 
 
 # ------------------------------------------------------------------------ span table cache
@@ -99,7 +99,7 @@ def span_table(df: pd.DataFrame, ctx=None):
 
 # ------------------------------------------------------------------------ reference utilities
 def get_span(df, start=None, end=None):
-    """preprocess_data.py:222-226 -- inclusive trace-level window (T15)."""
+    """preprocess_data.py:10-14 -- inclusive trace-level window (T15)."""
     if start and end:
         df = df[(df["startTime"] >= start) & (df["endTime"] <= end)]
     return df
@@ -112,14 +112,14 @@ def _svc_op_names(span_df: pd.DataFrame) -> np.ndarray:
 
 
 def get_service_operation_list(span_df: pd.DataFrame):
-    """preprocess_data.py:238-245: adds the ``operation`` column, returns its distinct values in
+    """preprocess_data.py:26-33: adds the ``operation`` column, returns its distinct values in
     first-appearance order."""
     span_df["operation"] = _svc_op_names(span_df)
     return span_df["operation"].drop_duplicates().tolist()
 
 
 def get_operation_slo(service_operation_list, span_df: pd.DataFrame, *, ctx=None):
-    """preprocess_data.py:262-290 on the GPU (K4): {svc_op: [round(mean/1000,4), round(std/1000,4)]}
+    """preprocess_data.py:50-78 on the GPU (K4): {svc_op: [round(mean/1000,4), round(std/1000,4)]}
     for the ops of the DataFrame that are in ``service_operation_list``, keys in sorted order."""
     span_df["operation"] = _svc_op_names(span_df)
     ctx = ctx or _lib.default_context()
@@ -139,7 +139,7 @@ def get_operation_slo(service_operation_list, span_df: pd.DataFrame, *, ctx=None
 
 
 def get_operation_duration_data(operation_list, span_df: pd.DataFrame):
-    """preprocess_data.py:309-334 -- {traceID: {svc_op: count, ..., 'duration': max}} (sorted
+    """preprocess_data.py:97-122 -- {traceID: {svc_op: count, ..., 'duration': max}} (sorted
     keys, traces with max duration <= 0 dropped).  Mutates ``operationName`` of ``span_df``
     like the reference.  The detector itself runs on the GPU (anormaly_detector.py)."""
     span_df["operationName"] = _svc_op_names(span_df)
@@ -255,7 +255,7 @@ class GraphDicts(Mapping):
 
 
 def get_pagerank_graph(trace_list, span_df: pd.DataFrame, *, ctx=None):
-    """preprocess_data.py:358-383 on the GPU (K1).  Returns (operation_operation,
+    """preprocess_data.py:146-171 on the GPU (K1).  Returns (operation_operation,
     operation_trace, trace_operation, pr_trace) as lazy mappings backed by the device graph."""
     ctx = ctx or _lib.default_context()
     table, dev = span_table(span_df, ctx)

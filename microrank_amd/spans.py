@@ -1,9 +1,9 @@
 """Int-coded columnar span table: the wire format between pandas and the HIP kernels.
 
 The reference keeps spans in a pandas DataFrame of strings (schema renamed at
-``online_rca.py:377-400`` from the OTel export of ``collect_data.py:35-46``) and
+``online_rca.py:221-244`` from the OTel export of ``collect_data.py:35-46``) and
 re-derives operation names with string concatenation in every function
-(``preprocess_data.py:238-244, 265-269, 312-316, 363-367``).  Here that work is
+(``preprocess_data.py:26-32, 53-57, 100-104, 151-155``).  Here that work is
 done ONCE per DataFrame: every string column becomes an int32/int64 code whose
 integer order equals the code-point (Python ``str``) order of the strings, so
 "sorted by name" in the reference (pandas ``groupby`` sort, T10) is "sorted by
@@ -11,7 +11,7 @@ code" on the device.
 
 Two operation namespaces exist (T10):
   * ``svcop`` = ``serviceName + '_' + op``  -- SLO / detector (preprocess_data.py:29-30,55-56,102-103)
-  * ``podop`` = ``podName + '_' + op``      -- PageRank graph    (preprocess_data.py:363-367)
+  * ``podop`` = ``podName + '_' + op``      -- PageRank graph    (preprocess_data.py:151-155)
 where ``op`` drops the last ``/segment`` for service ``ts-ui-dashboard``.
 """
 from __future__ import annotations
@@ -26,7 +26,7 @@ UI_SERVICE = "ts-ui-dashboard"
 
 def op_display(service: np.ndarray, operation: np.ndarray) -> np.ndarray:
     """Operation part of a name: ``rsplit('/', 1)[0]`` for ts-ui-dashboard spans
-    (preprocess_data.py:240-242), the raw operationName otherwise."""
+    (preprocess_data.py:28-30), the raw operationName otherwise."""
     out = np.array(operation, dtype=object, copy=True)
     ui = np.asarray(service, dtype=object) == UI_SERVICE
     if ui.any():

@@ -2,7 +2,7 @@
 
 A Train-Ticket-like call tree whose root service is ``ts-ui-dashboard`` (REST op
 names ending in an id segment, to exercise the ``rsplit('/')`` naming rule of
-preprocess_data.py:240-242).  Every trace is a random walk down the tree from the
+preprocess_data.py:28-30).  Every trace is a random walk down the tree from the
 root: each child is visited with probability ``min(p_max, branch/fanout)`` and a
 visited child is called a second time with probability ``p_repeat`` (span
 multiplicity, T5).  A span's duration is its own work plus its children's, so the
@@ -193,7 +193,7 @@ def gen_spans(topo: Topology, n_traces: int, seed: int = 0, *, t0_ns: int = 1_70
 
 
 def to_dataframe(st: SpanTable, topo: Topology, seed: int = 0):
-    """Materialise the reference string schema (online_rca.py:377-404 after rename)."""
+    """Materialise the reference string schema (online_rca.py:221-248 after rename)."""
     import pandas as pd
 
     rng = np.random.default_rng([seed, 0x33])
@@ -264,3 +264,33 @@ def frame_digest(df) -> str:
     for c in ("duration", "startTime", "endTime"):
         h.update(np.ascontiguousarray(df[c].to_numpy().astype(np.int64)).tobytes())
     return h.hexdigest()
+
+
+SLO_SIZES = (1, 7, 8, 9, 127, 128, 129, 1000, 8191, 8192, 8193, 16384, 16385, 24577, 50001, 131075)
+
+
+def slo_frame(seed: int = 7, sizes=SLO_SIZES):
+    """Spans of ops sized around numpy's 8192-element reduction buffer and its pairwise
+    block (128), rows interleaved at random: the SLO variance depends on the row order inside
+    each op and on the buffer chunking of np.std (preprocess_data.py:66-73)."""
+    import pandas as pd
+
+    rng = np.random.default_rng(seed)
+    op = np.repeat(np.arange(len(sizes)), sizes)
+    rng.shuffle(op)
+    n = op.size
+    # heavy-tailed integer durations (microseconds), large enough that rounding matters
+    dur = (rng.lognormal(8.0, 1.5, n) + rng.integers(0, 1000, n)).astype(np.int64)
+    t0 = np.int64(1_700_000_000_000_000_000)
+    start = t0 + np.arange(n, dtype=np.int64) * 1000
+    return pd.DataFrame({
+        "traceID": [f"s{i // 4:07d}" for i in range(n)],
+        "spanID": [f"x{i:08d}" for i in range(n)],
+        "ParentSpanId": [None] * n,
+        "serviceName": [f"svc{o % 3}" for o in op],
+        "operationName": [f"op{o:02d}" for o in op],
+        "podName": [f"svc{o % 3}-pod" for o in op],
+        "duration": dur,
+        "startTime": pd.to_datetime(start),
+        "endTime": pd.to_datetime(start + dur * 1000),
+    })

@@ -4,10 +4,10 @@
  * parallelised with OpenMP where the reference's algorithm allows it:
  *
  *   detect   anormaly_detector.system_anomaly_detect          anormaly_detector.py:44-84
- *            + preprocess_data.get_operation_duration_data    preprocess_data.py:309-334
- *   graph    preprocess_data.get_pagerank_graph               preprocess_data.py:358-383
+ *            + preprocess_data.get_operation_duration_data    preprocess_data.py:97-122
+ *   graph    preprocess_data.get_pagerank_graph               preprocess_data.py:146-171
  *   rank     pagerank.trace_pagerank / pageRank               pagerank.py:15-130
- *   score    online_rca.calculate_spectrum_without_delay_list online_rca.py:189-308
+ *   score    online_rca.calculate_spectrum_without_delay_list online_rca.py:33-152
  *
  * Semantics follow SURVEY.md §8.1 (T1-T15) exactly as the numpy oracle (oracle/oracle.py),
  * which is pinned to the reference's golden vectors; tests check this C port against both.
@@ -68,7 +68,7 @@ static void ograph_free(ograph* g) {
     memset(g, 0, sizeof *g);
 }
 
-/* preprocess_data.py:358-383 */
+/* preprocess_data.py:146-171 */
 static void build_graph(int64_t S, const int32_t* trace, const int32_t* podop, const int64_t* span, const int64_t* parent,
                         int32_t NT, int32_t NP, const uint8_t* tmask, const int64_t* id_off, const int32_t* id_rows,
                         int64_t n_codes, ograph* g) {
@@ -271,7 +271,7 @@ int oracle_pagerank(const ograph* g, int anomaly, int iters, double* weight, int
     return 0;
 }
 
-/* ---------------------------------------------------------------- spectrum (online_rca.py:189-308) */
+/* ---------------------------------------------------------------- spectrum (online_rca.py:33-152) */
 static double spec(int m, double ef, double nf, double ep, double np_) {
     switch (m) {
         case 0: return ef * ef / (ep + nf);

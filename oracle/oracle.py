@@ -215,7 +215,7 @@ def trace_pagerank(operation_operation, operation_trace, trace_operation, pr_tra
 # ----------------------------------------------------------------------------- spans -> graph
 @dataclass
 class SpanGraph:
-    """get_pagerank_graph restated on int codes (preprocess_data.py:358-383)."""
+    """get_pagerank_graph restated on int codes (preprocess_data.py:146-171)."""
     node_podop: np.ndarray      # podop code per node, node order (T10)
     trace_codes: np.ndarray     # sorted trace codes present
     sr_t: np.ndarray            # distinct (trace idx, node idx) pairs sorted by (t, o)
@@ -289,7 +289,7 @@ def span_graph(trace: np.ndarray, podop: np.ndarray, span: np.ndarray, parent: n
 
 
 def span_graph_dicts(sg: SpanGraph, span: np.ndarray, parent: np.ndarray, podop_names, trace_names):
-    """The four dicts of preprocess_data.py:370-383 from a SpanGraph: list entries one per span
+    """The four dicts of preprocess_data.py:158-171 from a SpanGraph: list entries one per span
     in row order; children in merge order (child row order, then matching parent rows)."""
     nodes = [podop_names[c] for c in sg.node_podop]
     tn = [trace_names[c] for c in sg.trace_codes]
@@ -322,7 +322,7 @@ SPECTRUM_METHODS = ("dstar2", "ochiai", "jaccard", "sorensendice", "m1", "m2", "
 
 def spectrum(anomaly_result, normal_result, anomaly_list_len, normal_list_len, top_max,
              normal_num_list, anomaly_num_list, spectrum_method):
-    """online_rca.py:189-308 -- returns (top_list, score_list, printed_lines)."""
+    """online_rca.py:33-152 -- returns (top_list, score_list, printed_lines)."""
     sp = {}
     for node in anomaly_result:                       # :201-214
         a = anomaly_result[node]
@@ -408,6 +408,21 @@ def numpy_pairwise_sum(x: np.ndarray) -> float:
     return numpy_pairwise_sum(x[:n2]) + numpy_pairwise_sum(x[n2:])
 
 
+NPY_BUFSIZE = 8192   # numpy's default ufunc buffer (numpy/_core/include/numpy/ndarraytypes.h)
+
+
+def numpy_reduce_sum(x: np.ndarray) -> float:
+    """np.add.reduce of a 1-D float64 array as numpy runs it: the reduction loop is handed the
+    array in NPY_BUFSIZE-element pieces, each piece summed pairwise (numpy_pairwise_sum) into the
+    running accumulator (DOUBLE_add's ``io1 += pairwise_sum(...)``).  For n <= 8192 this is the
+    plain pairwise sum; np.var / np.std use it for the squared deviations (pinned by
+    tests/golden/slo_large.json, produced by the reference's get_operation_slo)."""
+    acc = 0.0
+    for i in range(0, x.size, NPY_BUFSIZE):
+        acc += numpy_pairwise_sum(x[i:i + NPY_BUFSIZE])
+    return acc
+
+
 def np_round4(x: float) -> float:
     """round(np.float64, 4) == rint(x*1e4)/1e4 (T13)."""
     return float(np.rint(x * 10000.0) / 10000.0)
@@ -430,7 +445,7 @@ def operation_slo(svcop: np.ndarray, duration: np.ndarray, svcop_names, operatio
         d = duration[seg].astype(np.int64)
         mean = float(d.sum()) / d.size
         dev = d.astype(np.float64) - mean
-        var = numpy_pairwise_sum(dev * dev) / d.size
+        var = numpy_reduce_sum(dev * dev) / d.size
         out[name] = [np.float64(np_round4(mean / 1000.0)), np.float64(np_round4(math.sqrt(var) / 1000.0))]
     return dict(sorted(out.items()))
 

@@ -12,6 +12,9 @@ from microrank_amd.preprocess_data import DeviceSpans  # noqa: E402
 ctx = _lib.default_context()
 topo, normal, abnormal = bench.make_window(1234, 1000, 200_000)
 a3, ok = bench.slo_from_gpu(ctx, normal)
+t = time.perf_counter()
+bench.slo_from_gpu(ctx, normal)
+print(f"slo (upload + K4, {normal.n_spans} spans): {(time.perf_counter()-t)*1e3:.2f} ms", flush=True)
 dev = DeviceSpans(ctx, abnormal)
 t0 = int(abnormal.tstart.min())
 t1 = t0 + 5 * 60 * 10**9

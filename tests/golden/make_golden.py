@@ -217,13 +217,28 @@ def edge_span_df():
             r["spanID"] = "tr000-a"
         if r["traceID"] == "tr001" and r["ParentSpanId"] == "tr001-a":
             r["ParentSpanId"] = "tr000-a"
-    # zero-duration trace is dropped by the detector (preprocess_data.py:329)
+    # zero-duration trace is dropped by the detector (preprocess_data.py:117)
     add("trzero", "z-r", None, ui, "GET /api/orders/1", "ui-pod-0", 0, 3)
     return pd.DataFrame(rows)
 
 
+def slo_large(outdir):
+    """get_operation_slo on ops straddling numpy's 8192-element reduction buffer."""
+    df = synth.slo_frame()
+    sdf = df.copy()
+    ol = ref_pp.get_service_operation_list(sdf)
+    slo = ref_pp.get_operation_slo(ol, sdf)
+    out = {"seed": 7, "sizes": list(synth.SLO_SIZES), "digest": synth.frame_digest(df), "operation_list": ol,
+           "slo": {k: [fhex(v[0]), fhex(v[1])] for k, v in slo.items()}}
+    with open(os.path.join(outdir, "slo_large.json"), "w") as f:
+        json.dump(out, f, indent=0)
+
+
 def main():
     outdir = HERE
+    if sys.argv[1:] == ["slo_large"]:
+        slo_large(outdir)
+        return
     man = {"numpy": np.__version__, "pandas": pd.__version__, "python": sys.version.split()[0]}
     try:
         cfg = np.show_config(mode="dicts")
@@ -284,6 +299,7 @@ def main():
     # synthetic windows
     span_case("c1", dict(n_ops=40, n_traces=2000, seed=100), outdir)
     span_case("pods_dup_broken", dict(n_ops=30, n_traces=600, seed=200, pods=2, dup=0.01, broken=0.05), outdir)
+    slo_large(outdir)
     span_case("ops200", dict(n_ops=200, n_traces=1500, seed=300, branch=1.9, p_max=0.8, fault_ms=6000.0), outdir, driver=False)
     with open(os.path.join(outdir, "manifest.json"), "w") as f:
         json.dump(man, f, indent=1, sort_keys=True)

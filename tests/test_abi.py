@@ -49,7 +49,7 @@ def test_no_gpu_fails_loudly():
 
 def test_python_surface_matches_reference_signatures():
     """Argument names of the drop-in functions are the reference's (the driver passes several
-    by keyword: online_rca.py:323-357)."""
+    by keyword: online_rca.py:167-201)."""
     from microrank_amd import anormaly_detector, online_rca, pagerank, preprocess_data
 
     def names(fn):

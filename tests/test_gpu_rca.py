@@ -1,7 +1,7 @@
 """GPU parity of K3 (spectrum), K4 (SLO), K5 (detector) and the whole driver against the
 reference's own outputs (tests/golden).  Spectrum scores, SLO values and the detector's
 partition are bit-exact; the driver's stdout is identical except the full-precision repr line
-(online_rca.py:358) and result.csv, whose scores are compared at 1e-10 relative."""
+(online_rca.py:202) and result.csv, whose scores are compared at 1e-10 relative."""
 import contextlib
 import io
 import math
@@ -83,6 +83,22 @@ def test_slo_bit_exact(name):
         assert isinstance(v[0], np.float64)
     slo2 = get_slo(ndf.copy())   # T16: the working form of get_slo
     assert {k: [float(x).hex() for x in v] for k, v in slo2.items()} == case["slo"]
+
+
+def test_slo_large_ops_bit_exact():
+    """Ops of 1..131075 spans around numpy's 8192-element reduction buffer (golden from the
+    reference's get_operation_slo)."""
+    from microrank_amd import synth
+    from microrank_amd.preprocess_data import get_operation_slo, get_service_operation_list
+
+    case = load_golden("slo_large.json")
+    df = synth.slo_frame(case["seed"], tuple(case["sizes"]))
+    assert synth.frame_digest(df) == case["digest"]
+    ol = get_service_operation_list(df)
+    assert ol == case["operation_list"]
+    slo = get_operation_slo(ol, df)
+    assert {k: [float(v[0]).hex(), float(v[1]).hex()] for k, v in slo.items()} == case["slo"]
+    assert list(slo) == list(case["slo"])
 
 
 @pytest.mark.parametrize("name", SPAN_CASES)
@@ -193,3 +209,32 @@ def test_rca_window_device_pipeline(name):
     out32 = rca_window(adf, pd.Timestamp(det["start_ns"]), pd.Timestamp(det["end_ns"]), slo, precision="fp32")
     assert out32["top"][:5] == exp["top"][:5]
     np.testing.assert_allclose(out32["score"], unhex(exp["score"]), rtol=1e-4)
+
+
+def test_slo_bench_scale_matches_oracle():
+    """K4 on the bench's normal period (1k ops, ~1.4M spans, hot ops of >8192 spans) against the
+    oracle's np.std restatement: bit-exact."""
+    import ctypes as C
+
+    import bench
+    import oracle as orc
+    from microrank_amd import _lib
+    from microrank_amd._lib import ptr
+    from microrank_amd.preprocess_data import DeviceSpans
+
+    _, normal, _ = bench.make_window(1234, 1000, 100_000)
+    ctx = _lib.default_context()
+    dev = DeviceSpans(ctx, normal)
+    n = normal.n_svcops
+    mean, std, cnt = np.empty(n), np.empty(n), np.empty(n, np.int64)
+    ctx.check(_lib.load().mr_slo(ctx.h, dev.h, ptr(mean, C.c_double), ptr(std, C.c_double), ptr(cnt, C.c_int64)))
+    dev.close()
+    assert cnt.max() > 8192
+    names = [str(i) for i in range(n)]
+    exp = orc.operation_slo(normal.svcop, normal.duration, names, names)
+    for code in range(n):
+        if cnt[code] == 0:
+            assert str(code) not in exp
+            continue
+        e = exp[str(code)]
+        assert (mean[code], std[code]) == (float(e[0]), float(e[1])), code

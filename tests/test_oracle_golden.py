@@ -201,3 +201,18 @@ def test_edge_spans():
             g.nodes = nodes
             w = orc.weights(g, orc.power_iteration(g, orc.preference(g, orc.trace_kinds(g), flag_)))
             check_pr(w, e[f"pr_{key}_{flag_}"])
+
+
+def test_slo_large_ops_numpy_buffering():
+    """Ops larger than numpy's 8192-element reduction buffer: np.std sums the buffers
+    sequentially (oracle.numpy_reduce_sum); plain pairwise summation over the whole op differs
+    in the last bits for some of them."""
+    from microrank_amd import synth
+
+    case = load_golden("slo_large.json")
+    df = synth.slo_frame(case["seed"], tuple(case["sizes"]))
+    assert synth.frame_digest(df) == case["digest"]
+    st = _spans(df)
+    slo = orc.operation_slo(st.svcop, st.duration, st.svcop_names, case["operation_list"])
+    assert {k: [float(v[0]).hex(), float(v[1]).hex()] for k, v in slo.items()} == case["slo"]
+    assert list(slo) == sorted(case["slo"])
