@@ -191,19 +191,8 @@ extern "C" int mr_graph_upload(mr_ctx* ctx, const mr_graph_desc* d, mr_graph** o
         delete g;
         return code;
     };
-    // op-major transpose of P_sr (stable: traces ascending within an op)
-    std::vector<int64_t> op_off((size_t)N + 1, 0);
-    for (int64_t e = 0; e < d->nnz_sr; ++e) op_off[(size_t)d->sr_ops[e] + 1]++;
-    for (int32_t o = 0; o < N; ++o) op_off[(size_t)o + 1] += op_off[(size_t)o];
-    std::vector<int32_t> op_trs((size_t)d->nnz_sr);
-    {
-        std::vector<int64_t> pos(op_off.begin(), op_off.end() - 1);
-        for (int32_t t = 0; t < T; ++t)
-            for (int64_t e = d->sr_off[t]; e < d->sr_off[t + 1]; ++e) op_trs[(size_t)pos[(size_t)d->sr_ops[e]]++] = t;
-    }
-    if ((rc = g->sr_off.upload(ctx, op_off.data(), op_off.size())) ||
-        (rc = g->sr_trs.upload(ctx, op_trs.data(), op_trs.size())) ||
-        (rc = g->len_t.upload(ctx, d->len_t, (size_t)T)) || (rc = g->len_o.upload(ctx, d->len_o, (size_t)N)) ||
+    // the op-major side (tiles of P_sr) is derived on the device by mr_graph_prepare
+    if ((rc = g->len_t.upload(ctx, d->len_t, (size_t)T)) || (rc = g->len_o.upload(ctx, d->len_o, (size_t)N)) ||
         (rc = g->ss_off.upload(ctx, d->ss_off, (size_t)N + 1)) ||
         (rc = g->ss_par.upload(ctx, d->ss_par, (size_t)d->n_edges)) ||
         (rc = g->nchild.upload(ctx, d->nchild, (size_t)N)))

@@ -9,8 +9,8 @@
 //      are aggregated in LDS per block before any global atomic.
 //   3. node order: parent ops sorted by name (= code), then the other ops by first appearance
 //      (:371-375, T10)
-//   4. (trace, node) pairs -> stable radix sort -> distinct pairs = trace-major CSR; a second
-//      stable sort by node gives the op-major CSC (traces ascending); call edges sorted by
+//   4. (trace, node) pairs -> stable radix sort -> distinct pairs = trace-major CSR (the
+//      op-major side is derived by mr_graph_prepare as tiles); call edges sorted by
 //      (child, parent) give P_ss by child.
 #include <algorithm>
 
@@ -220,27 +220,14 @@ __global__ void k_run_heads(const uint64_t* keys, int64_t n, int32_t* flag) {
 // distinct pairs in (trace, node) order; every present trace has >= 1 pair, so its CSR offset is
 // the position of its first pair (no per-trace counting atomics)
 __global__ void k_pairs_out(const uint64_t* keys, const int32_t* flag, const int64_t* pos, int64_t n, int nb,
-                            int64_t* rs_off, uint64_t* ckey, uint32_t* cval) {
+                            int64_t* rs_off, int32_t* rs_ops) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n || !flag[i]) return;
     const uint64_t k = keys[i];
-    const uint32_t t = (uint32_t)(k >> nb), node = (uint32_t)(k & ((1ull << nb) - 1));
+    const uint32_t t = (uint32_t)(k >> nb);
     const int64_t e = pos[i];
-    ckey[e] = node;      // re-sorted by node for the CSC; value carries the trace
-    cval[e] = t;
+    rs_ops[e] = (int32_t)(k & ((1ull << nb) - 1));
     if (i == 0 || (keys[i - 1] >> nb) != t) rs_off[t] = e;
-}
-__global__ void k_pairs_csr(const uint64_t* ckey, int64_t nnz, int32_t* sr_ops) {
-    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < nnz) sr_ops[i] = (int32_t)ckey[i];
-}
-// every present node has >= 1 pair: its CSC offset is the position of its first pair
-__global__ void k_csc_out(const uint64_t* key_sorted, const uint32_t* val_sorted, int64_t nnz, int64_t* sr_off,
-                          int32_t* sr_trs) {
-    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nnz) return;
-    sr_trs[i] = (int32_t)val_sorted[i];
-    if (i == 0 || key_sorted[i] != key_sorted[i - 1]) sr_off[key_sorted[i]] = i;
 }
 __global__ void k_set_last(int64_t* off, int32_t n, int64_t v) { off[n] = v; }
 
@@ -470,23 +457,12 @@ int mr_graph_build_dev(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d_mask, m
     TRY(mr_exclusive_scan_i32(ctx, head.p, hpos.p, Ssel, tmp.p));
     int64_t nnz = 0;
     TRY(read_i64(ctx, hpos.p + Ssel, &nnz));
-    DBuf<uint64_t> ckey;
-    DBuf<uint32_t> cval;
-    TRY(ckey.alloc(ctx, nnz));
-    TRY(cval.alloc(ctx, nnz));
     TRY(g->rs_ops.alloc(ctx, nnz));
     TRY(g->rs_off.alloc(ctx, T + 1));
     if (Ssel)
         hipLaunchKernelGGL(k_pairs_out, dim3(cdiv(Ssel, 256)), dim3(256), 0, st, keys.p, head.p, hpos.p, Ssel, nb,
-                           g->rs_off.p, ckey.p, cval.p);
+                           g->rs_off.p, g->rs_ops.p);
     hipLaunchKernelGGL(k_set_last, dim3(1), dim3(1), 0, st, g->rs_off.p, T, nnz);
-    if (nnz) hipLaunchKernelGGL(k_pairs_csr, dim3(cdiv(nnz, 256)), dim3(256), 0, st, ckey.p, nnz, g->rs_ops.p);
-    // CSC: stable sort of the (trace-ordered) pairs by node
-    TRY(mr_radix_sort(ctx, ckey.p, cval.p, nnz, nb, ws));
-    TRY(g->sr_trs.alloc(ctx, nnz));
-    TRY(g->sr_off.alloc(ctx, N + 1));
-    if (nnz) hipLaunchKernelGGL(k_csc_out, dim3(cdiv(nnz, 256)), dim3(256), 0, st, ckey.p, cval.p, nnz, g->sr_off.p, g->sr_trs.p);
-    hipLaunchKernelGGL(k_set_last, dim3(1), dim3(1), 0, st, g->sr_off.p, N, nnz);
     DBuf<int64_t> ntmp;
     TRY(ntmp.alloc(ctx, scan_tmp_elems(std::max(N, 1))));
     // per-node arrays and P_ss

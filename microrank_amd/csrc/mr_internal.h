@@ -108,13 +108,21 @@ struct mr_graph {
     DBuf<int32_t> rs_ops;
     DBuf<int64_t> srt_off;   // only when !rs_is_sr
     DBuf<int32_t> srt_ops;
-    // op-major P_sr incidence (s' pass), split into fixed-size segments
-    DBuf<int64_t> sr_off;    // [N+1]
-    DBuf<int32_t> sr_trs;    // [nnz_sr]
-    int32_t nseg = 0;
-    DBuf<int32_t> seg_op;    // [nseg]
-    DBuf<int64_t> seg_beg;   // [nseg]
-    DBuf<int32_t> op_seg;    // [N+1] first segment of op
+    // trace-major P_rs node ids as u16 when N <= 65536 (the r' pass reads half the bytes)
+    DBuf<uint16_t> rs16;
+    // P_sr in compressed sparse blocks for the s' pass: traces cut in tiles of 2^tshift; within a
+    // tile the distinct (op, trace) entries sorted by (op, trace) as u16 tile-local trace
+    // indices; a "pair" is the run of one op inside one tile.
+    int32_t tshift = 0, n_tiles = 0;
+    int64_t n_pairs = 0;
+    DBuf<uint16_t> tl_ltr;    // [nnz_sr] tile-local trace index, (tile, op, trace) order
+    DBuf<int32_t> pr_op;      // [n_pairs] op of the pair
+    DBuf<int64_t> pr_beg;     // [n_pairs+1] first entry in tl_ltr
+    DBuf<int32_t> tile_pr0;   // [n_tiles+1] first pair of a tile
+    DBuf<int32_t> lp;         // [<= n_pairs] long pairs (summed by a whole wave), tile order
+    DBuf<int32_t> tile_lp0;   // [n_tiles+1]
+    DBuf<int32_t> op_pr_off;  // [N+1] pairs of an op ...
+    DBuf<int32_t> op_pr;      // [n_pairs] ... in tile order (the s' reduction order)
     // per-trace / per-op constants
     DBuf<int32_t> len_t, len_o, nchild, cov;
     DBuf<float> w_t, u_o, pw;    // fp32(1/len_t), fp32(1/len_o), fp32(1/nchild)
@@ -131,8 +139,7 @@ struct mr_graph {
     DBuf<float> c_t;             // [T] fp32((1-d) * v)
     DBuf<double> q64[2];         // [T] w_t * r'_t (fp64 mode)
     DBuf<float> q32[2];          // [T] (fp32 mode)
-    DBuf<double> part;           // [nseg] segment partial sums of the s' pass
-    DBuf<uint32_t> op_cnt;       // [N] monotone per-op arrival counters (last arriver finishes s')
+    DBuf<double> part;           // [n_pairs] per-(tile, op) partial sums of the s' pass
     DBuf<unsigned long long> mslot;  // [6] bits of (M_s, M_r) for iterations k%3
     DBuf<double> spb[2];         // [N] unnormalised s' (double-buffered)
     DBuf<double> sub[2];         // [N] u_o * s'[o]

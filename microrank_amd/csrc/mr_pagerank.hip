@@ -1,17 +1,20 @@
 // K2: personalised PageRank of pagerank.trace_pagerank (pagerank.py:15-130) on gfx950.
 //
-// Sparse, HBM-bound: no MFMA.  Each Jacobi iteration k -> k+1 (T8) is ONE launch with two
-// block roles that both read only iteration-k state:
-//   trace role  r'[t] = d * sum_{o in rs(t)} u_o * s_k[o] + fp32((1-d) v_t)      (pagerank.py:125)
-//               q'[t] = w_t * r'[t]      (the P_sr-weighted value the op role sums next time)
-//               s_k*u is staged in LDS; the block's contiguous id range is read coalesced into
-//               LDS, then each thread sums its trace in node order.
-//   op role     one wave per fixed 1024-entry segment of an op's trace list sums q'_k; the
-//               LAST segment of an op to finish (agent-scope acq_rel counter) combines the
-//               partials in segment order and adds the call-graph term:
-//               s'[o] = d * (sum q'_k / M_r(k) + alpha * sum_{p in ss(o)} pw_p * s_k[p])  (:122-124)
-// Maxima M_s, M_r (np.amax, :126-127) travel as bit patterns of non-negative doubles through
-// atomicMax, which is exact and order-independent.  Normalisation of r is deferred:
+// Sparse, HBM-bound: no MFMA.  Each Jacobi iteration k -> k+1 (T8) is two launches:
+//   k_iter_a, two block roles reading only iteration-k state:
+//     trace role  r'[t] = d * sum_{o in rs(t)} u_o * s_k[o] + fp32((1-d) v_t)     (pagerank.py:125)
+//                 q'[t] = w_t * r'[t]   (the P_sr-weighted value the op side sums next time)
+//                 s_k*u staged in LDS; the block's contiguous id range (u16 ids when N <= 65536)
+//                 read coalesced into LDS, then each thread sums its trace in node order.
+//     tile role   P_sr in compressed sparse blocks: traces cut in tiles of 2^tshift, the tile's
+//                 q_k staged in LDS with coalesced loads, and each (tile, op) pair -- the op's
+//                 traces inside the tile as u16 tile-local indices -- summed in trace order
+//                 (a thread per short pair, a wave per long one) into part[pair].
+//   k_iter_b, a wave per op: s'[o] = d * (sum of the op's pair partials in tile order / M_r(k)
+//                 + alpha * sum_{p in ss(o)} pw_p * s_k[p] / M_s(k))                 (:122-124)
+// The op side never gathers q from HBM at random (an op-major CSC did: 5% of HBM at 10M
+// traces).  Maxima M_s, M_r (np.amax, :126-127) travel as bit patterns of non-negative doubles
+// through atomicMax (exact, order-independent).  Normalisation of r is deferred:
 // sum_t w_t (r'_t / M_r) is evaluated as (sum_t w_t r'_t) / M_r.  Every float reduction has a
 // fixed order (no float atomics), so results are bitwise reproducible run to run.
 #include <algorithm>
@@ -20,13 +23,15 @@
 
 #include "mr_internal.h"
 #include "mr_prim.h"
+#include "mr_sort.h"
 
 namespace {
 
-constexpr int SEG = 1024;           // op-list segment length (entries)
 constexpr int TB = 256;             // trace-role block size (one trace per thread)
 constexpr int LDS_NODES = 8192;     // su staged in LDS up to this many nodes (64 KiB)
 constexpr int VCAP = 2048;          // trace-role ids staged per round in LDS (16 KiB of values)
+constexpr int LONG_PAIR = 32;       // tile pairs longer than this are summed by a whole wave
+constexpr int TSHIFT_MIN = 8, TSHIFT_MAX = 12;   // tiles of 256 .. 4096 traces
 
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     z += 0x9E3779B97F4A7C15ull;
@@ -36,7 +41,7 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
 }
 
 __global__ void k_pr_reset(int32_t T, int64_t cap, int32_t N, float* pref, float* c_t, uint64_t* hk, uint32_t* hc,
-                           int32_t* hr, uint32_t* op_cnt, int32_t* flag, double* scal) {
+                           int32_t* hr, int32_t* flag, double* scal) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < T) {
         pref[i] = 0.0f;
@@ -47,7 +52,6 @@ __global__ void k_pr_reset(int32_t T, int64_t cap, int32_t N, float* pref, float
         hc[i] = 0u;
         hr[i] = -1;
     }
-    if (i < N) op_cnt[i] = 0u;
     if (i < 4) flag[i] = 0;
     if (i < 8) scal[i] = 0.0;
 }
@@ -58,28 +62,91 @@ __global__ void k_trace_consts(const int32_t* len_t, float* w_t, int32_t T) {
     if (t < T) w_t[t] = len_t[t] > 0 ? (float)(1.0 / (double)len_t[t]) : 0.0f;   // fp64 1/n -> fp32
 }
 
-__global__ void k_op_consts(const int32_t* len_o, const int32_t* nchild, const int64_t* sr_off,
-                            float* u_o, float* pw, int32_t* cov, int32_t* nseg_of, int32_t N) {
+__global__ void k_op_consts(const int32_t* len_o, const int32_t* nchild, float* u_o, float* pw, int32_t N) {
     int32_t o = blockIdx.x * blockDim.x + threadIdx.x;
     if (o >= N) return;
     u_o[o] = len_o[o] > 0 ? (float)(1.0 / (double)len_o[o]) : 0.0f;
     pw[o] = nchild[o] > 0 ? (float)(1.0 / (double)nchild[o]) : 0.0f;
-    int64_t c = sr_off[o + 1] - sr_off[o];
-    cov[o] = (int32_t)c;                                  // trace_num_list (pagerank.py:98-104)
-    nseg_of[o] = c > 0 ? (int32_t)((c + SEG - 1) / SEG) : 1;   // >= 1: every op gets a finisher
+}
+__global__ void k_ids16(const int32_t* ops, int64_t n, uint16_t* o16) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) o16[i] = (uint16_t)ops[i];
 }
 
-__global__ void k_fill_segments(const int64_t* op_seg64, const int64_t* sr_off, int32_t* op_seg,
-                                int32_t* seg_op, int64_t* seg_beg, int32_t N) {
-    int32_t o = blockIdx.x * blockDim.x + threadIdx.x;
-    if (o > N) return;
-    op_seg[o] = (int32_t)op_seg64[o];
-    if (o == N) return;
-    int64_t s0 = op_seg64[o], s1 = op_seg64[o + 1];
-    for (int64_t s = s0; s < s1; ++s) {
-        seg_op[s] = o;
-        seg_beg[s] = sr_off[o] + (s - s0) * SEG;
+// ---------------------------------------------------------------- P_sr tiles (compressed sparse blocks)
+// entry (t, o) of the trace-major P_sr incidence -> key (tile(t), o), value t mod tile; a stable
+// sort by key leaves every tile's entries in (op, trace) order
+__global__ void k_tile_keys(const int64_t* off, const int32_t* ops, int32_t T, int tshift, int nb, uint64_t* key,
+                            uint32_t* val) {
+    const int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= T) return;
+    const uint64_t hi = (uint64_t)(uint32_t)(t >> tshift) << nb;
+    const uint32_t lt = (uint32_t)t & ((1u << tshift) - 1u);
+    for (int64_t e = off[t]; e < off[t + 1]; ++e) {
+        key[e] = hi | (uint32_t)ops[e];
+        val[e] = lt;
     }
+}
+__global__ void k_key_heads(const uint64_t* key, int64_t n, int32_t* head) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) head[i] = (i == 0 || key[i] != key[i - 1]) ? 1 : 0;
+}
+__global__ void k_tile_pairs(const uint64_t* key, const uint32_t* val, const int32_t* head, const int64_t* hpos,
+                             int64_t n, int nb, uint16_t* ltr, int32_t* pr_op, int64_t* pr_beg, int32_t* pr_tile) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n) return;
+    ltr[e] = (uint16_t)val[e];
+    if (head[e]) {
+        const int64_t p = hpos[e];
+        const uint64_t k = key[e];
+        pr_op[p] = (int32_t)(k & ((1ull << nb) - 1ull));
+        pr_beg[p] = e;
+        pr_tile[p] = (int32_t)(k >> nb);
+    }
+    if (e == n - 1) pr_beg[hpos[n]] = n;
+}
+// out[q] = first i in [0, n) with a[i] >= q (a sorted), q in [0, nq]; n from the device when d_n
+template <class K>
+__global__ void k_lower_bound(const K* a, int64_t n, const int64_t* d_n, int32_t nq, int32_t* out) {
+    const int32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q > nq) return;
+    int64_t lo = 0, hi = d_n ? *d_n : n;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if ((int64_t)a[mid] < (int64_t)q) lo = mid + 1; else hi = mid;
+    }
+    out[q] = (int32_t)lo;
+}
+__global__ void k_pair_op_keys(const int32_t* pr_op, int64_t np, uint64_t* key, uint32_t* val) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= np) return;
+    key[p] = (uint64_t)(uint32_t)pr_op[p];
+    val[p] = (uint32_t)p;
+}
+__global__ void k_long_flags(const int64_t* pr_beg, int64_t np, int32_t* flag) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < np) flag[p] = (pr_beg[p + 1] - pr_beg[p]) > LONG_PAIR ? 1 : 0;
+}
+__global__ void k_long_list(const int32_t* flag, const int64_t* pos, const int32_t* pr_tile, int64_t np, int32_t* lp,
+                            int32_t* lp_tile) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= np || !flag[p]) return;
+    lp[pos[p]] = (int32_t)p;
+    lp_tile[pos[p]] = pr_tile[p];
+}
+__global__ void k_op_pairs(const uint64_t* skey, const uint32_t* sval, int64_t np, int32_t* op_pr, int32_t* op_key) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= np) return;
+    op_pr[i] = (int32_t)sval[i];
+    op_key[i] = (int32_t)skey[i];
+}
+// coverage = traces containing the op (trace_num_list, pagerank.py:98-104) = its pair lengths
+__global__ void k_cov(const int32_t* op_pr_off, const int32_t* op_pr, const int64_t* pr_beg, int32_t N, int32_t* cov) {
+    const int32_t o = blockIdx.x * blockDim.x + threadIdx.x;
+    if (o >= N) return;
+    int64_t c = 0;
+    for (int32_t i = op_pr_off[o]; i < op_pr_off[o + 1]; ++i) c += pr_beg[op_pr[i] + 1] - pr_beg[op_pr[i]];
+    cov[o] = (int32_t)c;
 }
 
 // ---------------------------------------------------------------- kinds (pagerank.py:54-66)
@@ -257,172 +324,174 @@ __global__ void k_iter_init(const float* w_t, const float* u_o, int32_t N, int32
     if (i < 6 * MSH) mslot[i] = i < 2 * MSH ? d2bits(1.0) : 0ull;
 }
 
-// Per-graph view for the batched iteration: one launch per Jacobi iteration covers every graph
-// of a batch (the two graphs of an RCA window, or many windows), each graph owning a contiguous
-// range of blocks [blk0, blk0 + n_tb + n_ob).
+// Per-graph view for the batched iteration: one k_iter_a / k_iter_b pair per Jacobi iteration
+// covers every graph of a batch (the two graphs of an RCA window, or many windows); graph i owns
+// blocks [blk0, blk0 + n_tb + n_tiles) of k_iter_a and [blk0b, blk0b + n_ob) of k_iter_b.
 struct GDev {
     const int64_t* rs_off;
     const int32_t* rs_ops;
+    const uint16_t* rs16;       // u16 copy of rs_ops (N <= 65536) or null
     const float* c_t;
     const float* w_t;
     const float* u_o;
     const float* pw;
-    const int64_t* sr_off;
-    const int32_t* sr_trs;
-    const int32_t* seg_op;
-    const int64_t* seg_beg;
-    const int32_t* op_seg;
+    const uint16_t* ltr;
+    const int64_t* pr_beg;
+    const int32_t* tile_pr0;
+    const int32_t* lp;
+    const int32_t* tile_lp0;
+    const int32_t* op_pr_off;
+    const int32_t* op_pr;
     const int64_t* ss_off;
     const int32_t* ss_par;
     void* q[2];
     double* sub[2];
     double* spb[2];
     double* part;
-    uint32_t* op_cnt;
     unsigned long long* mslot;
-    int32_t T, N, nseg, n_tb, lds_su, blk0;
+    int32_t T, N, n_tb, n_tiles, tshift, lds_su, blk0, n_ob, blk0b;
 };
 
-// One Jacobi iteration k -> k+1.  Maxima are exchanged as the bit patterns of non-negative
-// doubles through atomicMax (exact and order-independent); slot k%3 holds (M_s(k), M_r(k)),
-// slot (k+1)%3 collects iteration k+1, slot (k+2)%3 is cleared here for k+2.  s' is carried
-// unnormalised together with su'[o] = u_o * s'[o]; the division by M_s(k) is applied to each
-// finished sum instead of to every term.
+__device__ __forceinline__ int32_t graph_of(const GDev* gs, int32_t ng, int32_t blk, bool b_launch) {
+    int32_t lo = 0, hi = ng - 1;
+    while (lo < hi) {
+        const int32_t mid = (lo + hi + 1) >> 1;
+        if ((b_launch ? gs[mid].blk0b : gs[mid].blk0) <= blk) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+
+// trace role inner loop: the block's id range in rounds of VCAP ids, all loads in flight before
+// the LDS gathers, then each thread continues its own trace's sum in node order
+template <class ID>
+__device__ __forceinline__ double trace_sums(const ID* __restrict__ ids, int64_t e0, int64_t e1, int64_t a, int64_t b,
+                                             const double* su, double* vals) {
+    double acc = 0.0;
+    for (int64_t lo = e0; lo < e1; lo += VCAP) {
+        const int64_t hi = min(lo + (int64_t)VCAP, e1);
+        __syncthreads();
+        int32_t id[VCAP / TB];
+#pragma unroll
+        for (int j = 0; j < VCAP / TB; ++j) id[j] = (int32_t)ids[min(lo + threadIdx.x + (int64_t)j * TB, hi - 1)];
+#pragma unroll
+        for (int j = 0; j < VCAP / TB; ++j) {
+            const int64_t e = lo + threadIdx.x + (int64_t)j * TB;
+            if (e < hi) vals[e - lo] = su[id[j]];
+        }
+        __syncthreads();
+        const int64_t x0 = max(a, lo), x1 = min(b, hi);
+        int64_t e = x0;
+        for (; e + 4 <= x1; e += 4) {
+            const double v0 = vals[e - lo], v1 = vals[e + 1 - lo], v2 = vals[e + 2 - lo], v3 = vals[e + 3 - lo];
+            acc += v0;
+            acc += v1;
+            acc += v2;
+            acc += v3;
+        }
+        for (; e < x1; ++e) acc += vals[e - lo];
+    }
+    return acc;
+}
+
+// Iteration k, first half.  Maxima are exchanged as the bit patterns of non-negative doubles
+// through atomicMax; slot k%3 holds (M_s(k), M_r(k)), slot (k+1)%3 collects iteration k+1, slot
+// (k+2)%3 is cleared here for k+2.  s' is carried unnormalised together with su'[o] = u_o*s'[o];
+// the division by M_s(k) is applied to each finished sum instead of to every term.
 template <class Q>
-__global__ void __launch_bounds__(TB) k_iter(const GDev* __restrict__ gs, int32_t ng, double d, double alpha, int it) {
+__global__ void __launch_bounds__(TB) k_iter_a(const GDev* __restrict__ gs, int32_t ng, double d, int it) {
     extern __shared__ double lds[];
     __shared__ double red[TB / WAVE];
-    __shared__ double msr[2];
+    __shared__ double msr;
     __shared__ int32_t sg;
-    if (threadIdx.x == 0) {   // this block's graph: the last one whose blk0 <= blockIdx.x
-        int32_t lo = 0, hi = ng - 1;
-        while (lo < hi) {
-            const int32_t mid = (lo + hi + 1) >> 1;
-            if (gs[mid].blk0 <= (int32_t)blockIdx.x) lo = mid; else hi = mid - 1;
-        }
-        sg = lo;
-    }
+    if (threadIdx.x == 0) sg = graph_of(gs, ng, (int32_t)blockIdx.x, false);
     __syncthreads();
     const GDev& G = gs[sg];
     const int32_t lb = (int32_t)blockIdx.x - G.blk0;
     const int cur = it & 1, nxt = cur ^ 1, k3 = it % 3;
-    const uint32_t epoch = (uint32_t)it + 1u;
     const int32_t T = G.T, N = G.N;
     unsigned long long* mslot = G.mslot;
-    // slot layout: [k%3][s|r][MSH]
-    const unsigned long long* Mcur = mslot + (size_t)2 * MSH * k3;
+    const unsigned long long* Mcur = mslot + (size_t)2 * MSH * k3;   // [k%3][s|r][MSH]
     unsigned long long* Mnext = mslot + (size_t)2 * MSH * ((k3 + 1) % 3);
     if (lb == 0 && threadIdx.x < 2 * MSH) mslot[(size_t)2 * MSH * ((k3 + 2) % 3) + threadIdx.x] = 0ull;
-    if (threadIdx.x < WAVE) {
-        double ms = bits2d(Mcur[threadIdx.x]), mr = bits2d(Mcur[MSH + threadIdx.x]);
-        ms = wave_max(ms);
-        mr = wave_max(mr);
-        if (threadIdx.x == 0) {
-            msr[0] = ms;
-            msr[1] = mr;
-        }
-    }
-    __syncthreads();
-    const double Ms = msr[0], Mr = msr[1];
-    const int shard = blockIdx.x % MSH;
     if (lb < G.n_tb) {
-        // ---- trace role: r'[t] = d * (sum_o u_o s'_k[o]) / M_s(k) + c_t  (pagerank.py:125)
-        // The block's contiguous id range is read coalesced in rounds of VCAP ids (all loads in
-        // flight before any gather), su' gathered from LDS into LDS, then each thread continues
-        // its own trace's sum in node order.
-        const int64_t* __restrict__ rs_off = G.rs_off;
-        const int32_t* __restrict__ rs_ops = G.rs_ops;
+        // ---- trace role (pagerank.py:125)
+        const int32_t t0 = lb * TB;
+        const int32_t t1 = min(t0 + TB, T);
+        const int32_t t = t0 + threadIdx.x;
+        const bool own = t < T;
+        const int64_t e0 = G.rs_off[t0], e1 = G.rs_off[t1];
+        const int64_t a = own ? G.rs_off[t] : 0, b = own ? G.rs_off[t + 1] : 0;
         const double* su = G.sub[cur];
         if (G.lds_su) {
             for (int32_t o = threadIdx.x; o < N; o += TB) lds[o] = su[o];
             su = lds;
         }
-        double* vals = lds + (G.lds_su ? N : 0);
-        const int32_t t0 = lb * TB;
-        const int32_t t1 = min(t0 + TB, T);
-        const int64_t e0 = rs_off[t0], e1 = rs_off[t1];
-        const int32_t t = t0 + threadIdx.x;
-        const bool own = t < T;
-        const int64_t a = own ? rs_off[t] : 0, b = own ? rs_off[t + 1] : 0;
-        double acc = 0.0;
-        for (int64_t lo = e0; lo < e1; lo += VCAP) {
-            const int64_t hi = min(lo + (int64_t)VCAP, e1);
-            __syncthreads();
-            int32_t id[VCAP / TB];
-#pragma unroll
-            for (int j = 0; j < VCAP / TB; ++j) id[j] = rs_ops[min(lo + threadIdx.x + (int64_t)j * TB, hi - 1)];
-#pragma unroll
-            for (int j = 0; j < VCAP / TB; ++j) {
-                const int64_t e = lo + threadIdx.x + (int64_t)j * TB;
-                if (e < hi) vals[e - lo] = su[id[j]];
-            }
-            __syncthreads();
-            const int64_t x0 = max(a, lo), x1 = min(b, hi);
-            int64_t e = x0;
-            for (; e + 4 <= x1; e += 4) {
-                const double v0 = vals[e - lo], v1 = vals[e + 1 - lo], v2 = vals[e + 2 - lo], v3 = vals[e + 3 - lo];
-                acc += v0;
-                acc += v1;
-                acc += v2;
-                acc += v3;
-            }
-            for (; e < x1; ++e) acc += vals[e - lo];
+        if (threadIdx.x < WAVE) {
+            const double ms = wave_max(bits2d(Mcur[threadIdx.x]));
+            if (threadIdx.x == 0) msr = ms;
         }
+        double* vals = lds + (G.lds_su ? N : 0);
+        const double acc = G.rs16 ? trace_sums(G.rs16, e0, e1, a, b, su, vals) : trace_sums(G.rs_ops, e0, e1, a, b, su, vals);
+        __syncthreads();   // msr (also when the block's id range is empty)
         double rmax = -__builtin_huge_val();
         if (own) {
-            const double rp = d * (acc / Ms) + (double)G.c_t[t];
+            const double rp = d * (acc / msr) + (double)G.c_t[t];
             ((Q*)G.q[nxt])[t] = (Q)((double)G.w_t[t] * rp);
             rmax = rp;
         }
         rmax = block_max(rmax, red);
-        if (threadIdx.x == 0) atomicMax(&Mnext[MSH + shard], d2bits(rmax));
+        if (threadIdx.x == 0) atomicMax(&Mnext[MSH + blockIdx.x % MSH], d2bits(rmax));
         return;
     }
-    // ---- op role: one wave per fixed segment of an op's trace list  (pagerank.py:122-124)
-    const int32_t seg = (lb - G.n_tb) * (TB / WAVE) + (int32_t)(threadIdx.x / WAVE);
-    if (seg >= G.nseg) return;
+    // ---- tile role: partial sums of q_k over each (tile, op) pair  (pagerank.py:122-124, P_sr r)
+    const int32_t tile = lb - G.n_tb;
+    if (tile >= G.n_tiles) return;
+    Q* qs = (Q*)lds;
+    const Q* __restrict__ qg = (const Q*)G.q[cur];
+    const int32_t tb0 = tile << G.tshift;
+    const int32_t nt = min(1 << G.tshift, T - tb0);
+    const int32_t p0 = G.tile_pr0[tile], p1 = G.tile_pr0[tile + 1];
+    const int32_t l0 = G.tile_lp0[tile], l1 = G.tile_lp0[tile + 1];
+    for (int32_t i = threadIdx.x; i < nt; i += TB) qs[i] = qg[tb0 + i];
+    __syncthreads();
+    const uint16_t* __restrict__ ltr = G.ltr;
+    const int64_t* __restrict__ pr_beg = G.pr_beg;
+    double* part = G.part;
+    for (int32_t p = p0 + (int32_t)threadIdx.x; p < p1; p += TB) {   // short pairs: one thread each
+        const int64_t b = pr_beg[p], e = pr_beg[p + 1];
+        if (e - b > LONG_PAIR) continue;
+        double sum = 0.0;
+        for (int64_t j = b; j < e; ++j) sum += (double)qs[ltr[j]];
+        part[p] = sum;
+    }
     const int lane = threadIdx.x & (WAVE - 1);
-    const int32_t o = G.seg_op[seg];
-    const int64_t b = G.seg_beg[seg];
-    const int64_t end = min(b + (int64_t)SEG, G.sr_off[o + 1]);
-    const Q* __restrict__ q_cur = (const Q*)G.q[cur];
-    const int32_t* __restrict__ sr_trs = G.sr_trs;
-    double acc = 0.0;
-    if (end > b) {   // ids first, then every gather, then the sum in element order
-        int32_t id[SEG / WAVE];
-#pragma unroll
-        for (int j = 0; j < SEG / WAVE; ++j) id[j] = sr_trs[min(b + lane + (int64_t)j * WAVE, end - 1)];
-        double v[SEG / WAVE];
-#pragma unroll
-        for (int j = 0; j < SEG / WAVE; ++j) v[j] = (double)q_cur[id[j]];
-#pragma unroll
-        for (int j = 0; j < SEG / WAVE; ++j)
-            if (b + lane + (int64_t)j * WAVE < end) acc += v[j];
-    }
-    acc = wave_sum(acc);
-    const int32_t s0 = G.op_seg[o], s1 = G.op_seg[o + 1];
-    uint32_t old = 0;
-    if (lane == 0) {
-        if (s1 - s0 > 1) {
-            // hand-off without L2 write-back: write-through (sc1) payload, drain, relaxed counter
-            __hip_atomic_store(&G.part[seg], acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            old = __hip_atomic_fetch_add(&G.op_cnt[o], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            old = epoch - 1u;   // single segment: this wave finishes the op
-        }
-    }
-    old = __shfl(old, 0, WAVE);
-    if (old != epoch * (uint32_t)(s1 - s0) - 1u) return;
-    // last segment of op o to finish: combine the partials (sc1 loads) in a fixed order
-    double sum = 0.0;
-    if (s1 - s0 > 1) {
-        for (int32_t s = s0 + lane; s < s1; s += WAVE)
-            sum += __hip_atomic_load(&G.part[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int32_t i = l0 + (int32_t)(threadIdx.x / WAVE); i < l1; i += TB / WAVE) {   // long pairs: one wave each
+        const int32_t p = G.lp[i];
+        const int64_t b = pr_beg[p], e = pr_beg[p + 1];
+        double sum = 0.0;
+        for (int64_t j = b + lane; j < e; j += WAVE) sum += (double)qs[ltr[j]];
         sum = wave_sum(sum);
-    } else {
-        sum = acc;
+        if (lane == 0) part[p] = sum;
     }
+}
+
+// Iteration k, second half: a wave per op combines the op's pair partials in tile order and adds
+// the call-graph term: s'[o] = d * (sum / M_r(k) + alpha * sum_p pw_p s_k[p] / M_s(k))  (:122-124)
+__global__ void __launch_bounds__(TB) k_iter_b(const GDev* __restrict__ gs, int32_t ng, double d, double alpha, int it) {
+    __shared__ int32_t sg;
+    if (threadIdx.x == 0) sg = graph_of(gs, ng, (int32_t)blockIdx.x, true);
+    __syncthreads();
+    const GDev& G = gs[sg];
+    const int32_t o = ((int32_t)blockIdx.x - G.blk0b) * (TB / WAVE) + (int32_t)(threadIdx.x / WAVE);
+    if (o >= G.N) return;
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int cur = it & 1, nxt = cur ^ 1, k3 = it % 3;
+    const unsigned long long* Mcur = G.mslot + (size_t)2 * MSH * k3;
+    unsigned long long* Mnext = G.mslot + (size_t)2 * MSH * ((k3 + 1) % 3);
+    const double Ms = wave_max(bits2d(Mcur[lane])), Mr = wave_max(bits2d(Mcur[MSH + lane]));
+    double sum = 0.0;
+    for (int32_t i = G.op_pr_off[o] + lane; i < G.op_pr_off[o + 1]; i += WAVE) sum += G.part[G.op_pr[i]];
+    sum = wave_sum(sum);
     const double* sp_cur = G.spb[cur];
     double bb = 0.0;
     for (int64_t e = G.ss_off[o] + lane; e < G.ss_off[o + 1]; e += WAVE) {
@@ -492,31 +561,101 @@ static const bool g_debug = getenv("MR_DEBUG") != nullptr;
 void mr_prof_begin(mr_ctx* ctx);
 void mr_prof_end(mr_ctx* ctx, double bytes);
 
+// Derived per-graph arrays: fp32 reciprocals, u16 ids, and the P_sr tiles.  One host round trip
+// (the number of (tile, op) pairs sizes the pair arrays).
 int mr_graph_prepare(mr_ctx* ctx, mr_graph* g) {
+    hipStream_t st = ctx->stream;
     const int32_t N = g->N, T = g->T;
+    const int64_t nnz = g->nnz_sr;
+    if (nnz >= (1ll << 31)) return mr_fail(ctx, MR_ERR_ARG, "more than 2^31 (trace, op) pairs on one device: shard the traces");
     MR_TRY(g->w_t.alloc(ctx, (size_t)T));
     MR_TRY(g->u_o.alloc(ctx, (size_t)N));
     MR_TRY(g->pw.alloc(ctx, (size_t)N));
     MR_TRY(g->cov.alloc(ctx, (size_t)N));
-    DBuf<int32_t> nseg_of;
-    DBuf<int64_t> op_seg64, tmp;
-    MR_TRY(nseg_of.alloc(ctx, (size_t)N));
-    MR_TRY(op_seg64.alloc(ctx, (size_t)N + 1));
-    MR_TRY(tmp.alloc(ctx, (size_t)scan_tmp_elems(N)));
-    if (T) hipLaunchKernelGGL(k_trace_consts, dim3(cdiv(T, 256)), dim3(256), 0, ctx->stream, g->len_t.p, g->w_t.p, T);
-    if (N)
-        hipLaunchKernelGGL(k_op_consts, dim3(cdiv(N, 256)), dim3(256), 0, ctx->stream, g->len_o.p, g->nchild.p,
-                           g->sr_off.p, g->u_o.p, g->pw.p, g->cov.p, nseg_of.p, N);
-    MR_TRY(mr_exclusive_scan_i32(ctx, nseg_of.p, op_seg64.p, N, tmp.p));
-    int64_t nseg = 0;
-    MR_TRY_HIP(ctx, hipMemcpyAsync(&nseg, op_seg64.p + N, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
-    MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    g->nseg = (int32_t)nseg;
-    MR_TRY(g->op_seg.alloc(ctx, (size_t)N + 1));
-    MR_TRY(g->seg_op.alloc(ctx, (size_t)nseg));
-    MR_TRY(g->seg_beg.alloc(ctx, (size_t)nseg));
-    hipLaunchKernelGGL(k_fill_segments, dim3(cdiv(N + 1, 256)), dim3(256), 0, ctx->stream, op_seg64.p, g->sr_off.p,
-                       g->op_seg.p, g->seg_op.p, g->seg_beg.p, N);
+    if (T) hipLaunchKernelGGL(k_trace_consts, dim3(cdiv(T, 256)), dim3(256), 0, st, g->len_t.p, g->w_t.p, T);
+    if (N) hipLaunchKernelGGL(k_op_consts, dim3(cdiv(N, 256)), dim3(256), 0, st, g->len_o.p, g->nchild.p, g->u_o.p, g->pw.p, N);
+    if (N <= 65536 && g->nnz_rs) {
+        MR_TRY(g->rs16.alloc(ctx, (size_t)g->nnz_rs));
+        hipLaunchKernelGGL(k_ids16, dim3(cdiv(g->nnz_rs, 256)), dim3(256), 0, st, g->rs_ops.p, g->nnz_rs, g->rs16.p);
+    }
+    // tiles: ~256 of them when T allows, 256..4096 traces each
+    int ts = TSHIFT_MIN;
+    while (ts < TSHIFT_MAX && ((int64_t)T >> ts) > 256) ++ts;
+    g->tshift = ts;
+    g->n_tiles = T ? cdiv(T, (int64_t)1 << ts) : 0;
+    const int32_t NTL = g->n_tiles;
+    const int nb = std::max(1, bits_for((uint64_t)std::max(N - 1, 0)));
+    const int64_t* off = g->rs_is_sr ? g->rs_off.p : g->srt_off.p;
+    const int32_t* ops = g->rs_is_sr ? g->rs_ops.p : g->srt_ops.p;
+    MR_TRY(g->tl_ltr.alloc(ctx, (size_t)nnz));
+    MR_TRY(g->tile_pr0.alloc(ctx, (size_t)NTL + 1));
+    MR_TRY(g->tile_lp0.alloc(ctx, (size_t)NTL + 1));
+    MR_TRY(g->op_pr_off.alloc(ctx, (size_t)N + 1));
+    int64_t np = 0;
+    DBuf<int32_t> pr_tile;
+    {
+        DBuf<uint64_t> key;
+        DBuf<uint32_t> val;
+        DBuf<int32_t> head;
+        DBuf<int64_t> hpos, tmp;
+        MR_TRY(key.alloc(ctx, (size_t)nnz));
+        MR_TRY(val.alloc(ctx, (size_t)nnz));
+        MR_TRY(head.alloc(ctx, (size_t)nnz));
+        MR_TRY(hpos.alloc(ctx, (size_t)nnz + 1));
+        MR_TRY(tmp.alloc(ctx, (size_t)scan_tmp_elems(std::max<int64_t>(nnz, 1))));
+        if (T) hipLaunchKernelGGL(k_tile_keys, dim3(cdiv(T, 256)), dim3(256), 0, st, off, ops, T, ts, nb, key.p, val.p);
+        SortScratch ws;
+        MR_TRY(mr_radix_sort(ctx, key.p, val.p, nnz, nb + bits_for((uint64_t)std::max(NTL - 1, 0)), ws));
+        if (nnz) hipLaunchKernelGGL(k_key_heads, dim3(cdiv(nnz, 256)), dim3(256), 0, st, key.p, nnz, head.p);
+        MR_TRY(mr_exclusive_scan_i32(ctx, head.p, hpos.p, nnz, tmp.p));
+        MR_TRY_HIP(ctx, hipMemcpyAsync(&np, hpos.p + nnz, sizeof np, hipMemcpyDeviceToHost, st));
+        MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+        g->n_pairs = np;
+        MR_TRY(g->pr_op.alloc(ctx, (size_t)np));
+        MR_TRY(g->pr_beg.alloc(ctx, (size_t)np + 1));
+        MR_TRY(pr_tile.alloc(ctx, (size_t)np));
+        if (nnz)
+            hipLaunchKernelGGL(k_tile_pairs, dim3(cdiv(nnz, 256)), dim3(256), 0, st, key.p, val.p, head.p, hpos.p, nnz, nb,
+                               g->tl_ltr.p, g->pr_op.p, g->pr_beg.p, pr_tile.p);
+        else
+            MR_TRY_HIP(ctx, hipMemsetAsync(g->pr_beg.p, 0, sizeof(int64_t), st));
+    }
+    hipLaunchKernelGGL(k_lower_bound<int32_t>, dim3(cdiv(NTL + 1, 256)), dim3(256), 0, st, pr_tile.p, np,
+                       (const int64_t*)nullptr, NTL, g->tile_pr0.p);
+    // long pairs (> LONG_PAIR entries) get a whole wave; listed per tile
+    MR_TRY(g->lp.alloc(ctx, (size_t)std::max<int64_t>(np, 1)));
+    {
+        DBuf<int32_t> lflag, lp_tile;
+        DBuf<int64_t> lpos, tmp;
+        MR_TRY(lflag.alloc(ctx, (size_t)np));
+        MR_TRY(lpos.alloc(ctx, (size_t)np + 1));
+        MR_TRY(lp_tile.alloc(ctx, (size_t)std::max<int64_t>(np, 1)));
+        MR_TRY(tmp.alloc(ctx, (size_t)scan_tmp_elems(std::max<int64_t>(np, 1))));
+        if (np) hipLaunchKernelGGL(k_long_flags, dim3(cdiv(np, 256)), dim3(256), 0, st, g->pr_beg.p, np, lflag.p);
+        MR_TRY(mr_exclusive_scan_i32(ctx, lflag.p, lpos.p, np, tmp.p));
+        if (np)
+            hipLaunchKernelGGL(k_long_list, dim3(cdiv(np, 256)), dim3(256), 0, st, lflag.p, lpos.p, pr_tile.p, np, g->lp.p,
+                               lp_tile.p);
+        hipLaunchKernelGGL(k_lower_bound<int32_t>, dim3(cdiv(NTL + 1, 256)), dim3(256), 0, st, lp_tile.p, (int64_t)0,
+                           lpos.p + np, NTL, g->tile_lp0.p);
+    }
+    // op-major order of the pairs (tile order within an op): the s' reduction order
+    MR_TRY(g->op_pr.alloc(ctx, (size_t)np));
+    {
+        DBuf<uint64_t> key;
+        DBuf<uint32_t> val;
+        DBuf<int32_t> okey;
+        MR_TRY(key.alloc(ctx, (size_t)np));
+        MR_TRY(val.alloc(ctx, (size_t)np));
+        MR_TRY(okey.alloc(ctx, (size_t)np));
+        if (np) hipLaunchKernelGGL(k_pair_op_keys, dim3(cdiv(np, 256)), dim3(256), 0, st, g->pr_op.p, np, key.p, val.p);
+        SortScratch ws;
+        MR_TRY(mr_radix_sort(ctx, key.p, val.p, np, nb, ws));
+        if (np) hipLaunchKernelGGL(k_op_pairs, dim3(cdiv(np, 256)), dim3(256), 0, st, key.p, val.p, np, g->op_pr.p, okey.p);
+        hipLaunchKernelGGL(k_lower_bound<int32_t>, dim3(cdiv(N + 1, 256)), dim3(256), 0, st, okey.p, np,
+                           (const int64_t*)nullptr, N, g->op_pr_off.p);
+    }
+    if (N) hipLaunchKernelGGL(k_cov, dim3(cdiv(N, 256)), dim3(256), 0, st, g->op_pr_off.p, g->op_pr.p, g->pr_beg.p, N, g->cov.p);
     MR_TRY_HIP(ctx, hipGetLastError());
     return MR_OK;   // scratch returns to the stream-ordered pool: no sync needed
 }
@@ -539,7 +678,6 @@ static int pagerank_setup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool 
     MR_TRY(g->ht_cnt.alloc(ctx, cap));
     MR_TRY(g->ht_rep.alloc(ctx, cap));
     MR_TRY(g->slot_of.alloc(ctx, (size_t)T));
-    MR_TRY(g->op_cnt.alloc(ctx, (size_t)N));
     MR_TRY(g->mslot.alloc(ctx, 6 * MSH));
     MR_TRY(g->sn.alloc(ctx, (size_t)N));
     MR_TRY(g->spb[0].alloc(ctx, (size_t)N));
@@ -547,7 +685,7 @@ static int pagerank_setup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool 
     MR_TRY(g->sub[0].alloc(ctx, (size_t)N));
     MR_TRY(g->sub[1].alloc(ctx, (size_t)N));
     MR_TRY(g->weight.alloc(ctx, (size_t)N));
-    MR_TRY(g->part.alloc(ctx, (size_t)g->nseg));
+    MR_TRY(g->part.alloc(ctx, (size_t)std::max<int64_t>(g->n_pairs, 1)));
     for (int i = 0; i < 2; ++i) {
         if (fp32) MR_TRY(g->q32[i].alloc(ctx, (size_t)T));
         else MR_TRY(g->q64[i].alloc(ctx, (size_t)T));
@@ -555,7 +693,7 @@ static int pagerank_setup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool 
     // one launch clears every per-call word (instead of a memset per buffer)
     hipLaunchKernelGGL(k_pr_reset, dim3(cdiv(std::max<int64_t>({(int64_t)T, (int64_t)cap, (int64_t)N, 16}), 256)),
                        dim3(256), 0, st, T, (int64_t)cap, N, g->pref.p, g->c_t.p, g->ht_key.p, g->ht_cnt.p, g->ht_rep.p,
-                       g->op_cnt.p, g->flag.p, g->scal.p);
+                       g->flag.p, g->scal.p);
     MR_DEBUG_CHECK(ctx, "k_pr_reset");
     // ---- kinds
     const int64_t* koff = g->rs_is_sr ? g->rs_off.p : g->srt_off.p;
@@ -610,11 +748,11 @@ int mr_pagerank_batch_impl(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly,
     hipStream_t st = ctx->stream;
     const bool fp32 = precision == MR_FP32;
     for (int i = 0; i < ng; ++i) MR_TRY(pagerank_setup(ctx, gs[i], anomaly[i], d, fp32, flags));
-    // ---- batched power iteration: one launch per iteration for every graph
+    // ---- batched power iteration: one k_iter_a + k_iter_b pair per iteration for every graph
     int mask = 3;
-    if (const char* rm = getenv("MR_ROLE_MASK")) mask = atoi(rm);   // profiling knob: 1 trace / 2 op role
+    if (const char* rm = getenv("MR_ROLE_MASK")) mask = atoi(rm);   // profiling knob: 1 trace / 2 op side
     std::vector<GDev> hv((size_t)ng);
-    int32_t blocks = 0;
+    int32_t blocks_a = 0, blocks_b = 0;
     size_t lds = VCAP * sizeof(double);
     double bytes = 0.0;
     for (int i = 0; i < ng; ++i) {
@@ -622,15 +760,18 @@ int mr_pagerank_batch_impl(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly,
         GDev& v = hv[(size_t)i];
         v.rs_off = g->rs_off.p;
         v.rs_ops = g->rs_ops.p;
+        v.rs16 = g->rs16.p;
         v.c_t = g->c_t.p;
         v.w_t = g->w_t.p;
         v.u_o = g->u_o.p;
         v.pw = g->pw.p;
-        v.sr_off = g->sr_off.p;
-        v.sr_trs = g->sr_trs.p;
-        v.seg_op = g->seg_op.p;
-        v.seg_beg = g->seg_beg.p;
-        v.op_seg = g->op_seg.p;
+        v.ltr = g->tl_ltr.p;
+        v.pr_beg = g->pr_beg.p;
+        v.tile_pr0 = g->tile_pr0.p;
+        v.lp = g->lp.p;
+        v.tile_lp0 = g->tile_lp0.p;
+        v.op_pr_off = g->op_pr_off.p;
+        v.op_pr = g->op_pr.p;
         v.ss_off = g->ss_off.p;
         v.ss_par = g->ss_par.p;
         for (int j = 0; j < 2; ++j) {
@@ -639,25 +780,35 @@ int mr_pagerank_batch_impl(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly,
             v.spb[j] = g->spb[j].p;
         }
         v.part = g->part.p;
-        v.op_cnt = g->op_cnt.p;
         v.mslot = g->mslot.p;
         v.T = g->T;
         v.N = g->N;
-        v.nseg = (mask & 2) ? g->nseg : 0;
         v.n_tb = (mask & 1) ? cdiv(g->T, TB) : 0;
+        v.n_tiles = (mask & 2) ? g->n_tiles : 0;
+        v.tshift = g->tshift;
         v.lds_su = g->N <= LDS_NODES;
-        v.blk0 = blocks;
-        blocks += v.n_tb + cdiv(v.nseg, TB / WAVE);
+        v.blk0 = blocks_a;
+        blocks_a += v.n_tb + v.n_tiles;
+        v.n_ob = (mask & 2) ? cdiv(g->N, TB / WAVE) : 0;
+        v.blk0b = blocks_b;
+        blocks_b += v.n_ob;
         if (v.lds_su) lds = std::max(lds, ((size_t)g->N + VCAP) * sizeof(double));
+        lds = std::max(lds, ((size_t)1 << g->tshift) * (fp32 ? sizeof(float) : sizeof(double)));
         bytes += iter_bytes(g, fp32);
     }
     DBuf<GDev> dv;
     MR_TRY(dv.upload(ctx, hv.data(), hv.size()));
-    for (int it = 0; it < iters && blocks > 0; ++it) {
+    for (int it = 0; it < iters; ++it) {
         mr_prof_begin(ctx);
-        if (fp32) hipLaunchKernelGGL(k_iter<float>, dim3(blocks), dim3(TB), lds, st, dv.p, ng, d, alpha, it);
-        else hipLaunchKernelGGL(k_iter<double>, dim3(blocks), dim3(TB), lds, st, dv.p, ng, d, alpha, it);
-        MR_DEBUG_CHECK(ctx, "k_iter");
+        if (blocks_a) {
+            if (fp32) hipLaunchKernelGGL(k_iter_a<float>, dim3(blocks_a), dim3(TB), lds, st, dv.p, ng, d, it);
+            else hipLaunchKernelGGL(k_iter_a<double>, dim3(blocks_a), dim3(TB), lds, st, dv.p, ng, d, it);
+            MR_DEBUG_CHECK(ctx, "k_iter_a");
+        }
+        if (blocks_b) {
+            hipLaunchKernelGGL(k_iter_b, dim3(blocks_b), dim3(TB), 0, st, dv.p, ng, d, alpha, it);
+            MR_DEBUG_CHECK(ctx, "k_iter_b");
+        }
         mr_prof_end(ctx, bytes);
     }
     for (int i = 0; i < ng; ++i) {

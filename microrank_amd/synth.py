@@ -294,3 +294,44 @@ def slo_frame(seed: int = 7, sizes=SLO_SIZES):
         "startTime": pd.to_datetime(start),
         "endTime": pd.to_datetime(start + dur * 1000),
     })
+
+
+def big_graph(n_ops: int, n_traces: int, seed: int = 11, spans_mean: float = 19.0, zipf_s: float = 1.1,
+              fp_dup: float = 0.25):
+    """A C4/C5-scale op<->trace graph generated directly as incidence lists (no span table):
+    per trace ~Poisson(spans_mean) spans whose ops follow a power law (zipf_s) over n_ops, the
+    root op in every trace, duplicates within a trace allowed (len_t counts spans, the incidence
+    keeps distinct ops); a random call tree over the ops.  Returns a graph.HostGraph with
+    ``nodes``/``traces`` as ranges (names are not needed for timing)."""
+    from .graph import HostGraph
+
+    rng = np.random.default_rng(seed)
+    T, N = int(n_traces), int(n_ops)
+    k = np.maximum(rng.poisson(spans_mean - 1.0, T), 1).astype(np.int64) + 1        # spans per trace
+    S = int(k.sum())
+    trace = np.repeat(np.arange(T, dtype=np.int64), k)
+    w = 1.0 / np.arange(1, N + 1, dtype=np.float64) ** zipf_s
+    cdf = np.cumsum(w / w.sum())
+    op = np.searchsorted(cdf, rng.random(S), side="right").clip(0, N - 1).astype(np.int64)
+    first = np.zeros(S, bool)
+    first[np.r_[0, np.cumsum(k)[:-1]]] = True
+    op[first] = 0                                                                    # root span
+    len_t = k.astype(np.int32)
+    len_o = np.bincount(op, minlength=N).astype(np.int32)
+    key = np.unique(trace * N + op)
+    del trace, op
+    tr = key // N
+    sr_ops = (key % N).astype(np.int32)
+    sr_off = np.zeros(T + 1, np.int64)
+    np.cumsum(np.bincount(tr, minlength=T), out=sr_off[1:])
+    del key, tr
+    # call tree: every op but the root has one parent of smaller index
+    child = np.arange(1, N, dtype=np.int64)
+    parent = (rng.random(N - 1) * child).astype(np.int64)
+    order = np.lexsort((parent, child))
+    ss_off = np.zeros(N + 1, np.int64)
+    np.cumsum(np.bincount(child[order], minlength=N), out=ss_off[1:])
+    ss_par = parent[order].astype(np.int32)
+    nchild = np.bincount(parent, minlength=N).astype(np.int32)
+    return HostGraph(range(N), range(T), sr_off, sr_ops, None, None, len_t, len_o, ss_off, ss_par, nchild,
+                     None, None)
