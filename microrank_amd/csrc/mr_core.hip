@@ -186,6 +186,7 @@ extern "C" int mr_graph_upload(mr_ctx* ctx, const mr_graph_desc* d, mr_graph** o
     g->E = d->n_edges;
     g->rs_is_sr = d->rs_off == nullptr;
     g->nnz_rs = g->rs_is_sr ? d->nnz_sr : d->nnz_rs;
+    for (int32_t t = 0; t < T && g->traces_nonempty; ++t) g->traces_nonempty = d->sr_off[t + 1] > d->sr_off[t];
     int rc = MR_OK;
     auto fail = [&](int code) {
         delete g;

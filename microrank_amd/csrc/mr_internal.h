@@ -123,6 +123,13 @@ struct mr_graph {
     DBuf<int32_t> tile_lp0;   // [n_tiles+1]
     DBuf<int32_t> op_pr_off;  // [N+1] pairs of an op ...
     DBuf<int32_t> op_pr;      // [n_pairs] ... in tile order (the s' reduction order)
+    // fused single-pass iteration (N <= FX_NMAX, P_rs == P_sr): one read of the trace-major ids
+    // per iteration; the s' side accumulates per trace block in LDS as 64-bit fixed point and
+    // leaves one dense row of N partials per block (exact integer sums: order-free)
+    bool fused = false;
+    bool traces_nonempty = true;   // every trace has an op (span-built graphs; checked at upload)
+    DBuf<uint64_t> fx_part;   // [n_blocks * N]
+    DBuf<double> fx_ssv;      // [N] alpha * (P_ss s_k)[o] / M_s(k), from k_fx_a for k_fx_b
     // per-trace / per-op constants
     DBuf<int32_t> len_t, len_o, nchild, cov;
     DBuf<float> w_t, u_o, pw;    // fp32(1/len_t), fp32(1/len_o), fp32(1/nchild)

@@ -149,6 +149,20 @@ __global__ void k_cov(const int32_t* op_pr_off, const int32_t* op_pr, const int6
     cov[o] = (int32_t)c;
 }
 
+// fused-path coverage: histogram of the distinct (trace, op) incidence's op ids (N <= FX_NMAX:
+// LDS counters per block, one global add per touched op)
+__global__ void __launch_bounds__(256) k_cov_hist(const uint16_t* ids, int64_t n, int32_t N, int32_t* cov) {
+    extern __shared__ int32_t hcnt[];
+    for (int32_t o = threadIdx.x; o < N; o += 256) hcnt[o] = 0;
+    __syncthreads();
+    const int64_t per = (int64_t)256 * 64;
+    const int64_t b0 = (int64_t)blockIdx.x * per;
+    for (int64_t e = b0 + threadIdx.x; e < min(b0 + per, n); e += 256) atomicAdd(&hcnt[ids[e]], 1);
+    __syncthreads();
+    for (int32_t o = threadIdx.x; o < N; o += 256)
+        if (hcnt[o]) atomicAdd(&cov[o], hcnt[o]);
+}
+
 // ---------------------------------------------------------------- kinds (pagerank.py:54-66)
 // kind[t] = size of the class of traces with an equal P_sr column: key = (op set, fp32(1/len_t)).
 // Open-addressing hash table of 64-bit keys; a second pass verifies every member against the
@@ -349,14 +363,24 @@ struct GDev {
     double* spb[2];
     double* part;
     unsigned long long* mslot;
+    unsigned long long* fx_part;
+    double* fx_ssv;
+    int32_t probe;               // diagnostics (MR_FX_PROBE): 1 skip atomics, 2 skip gathers
+    unsigned long long* stamp;   // diagnostics (MR_FX_STAMP): per-block phase clocks, else null
+    double fx_scale, fx_iscale;
     int32_t T, N, n_tb, n_tiles, tshift, lds_su, blk0, n_ob, blk0b;
+    int32_t blk0f, n_fa, blk0fb, n_fb;   // fused path: k_fx_a / k_fx_b block ranges
 };
 
-__device__ __forceinline__ int32_t graph_of(const GDev* gs, int32_t ng, int32_t blk, bool b_launch) {
+// graph owning block `blk` of launch kind `which` (0 k_iter_a, 1 k_iter_b, 2 k_fx_a, 3 k_fx_b);
+// the start offsets are non-decreasing over graphs (graphs without blocks in a launch repeat it)
+__device__ __forceinline__ int32_t graph_of(const GDev* gs, int32_t ng, int32_t blk, int which) {
     int32_t lo = 0, hi = ng - 1;
     while (lo < hi) {
         const int32_t mid = (lo + hi + 1) >> 1;
-        if ((b_launch ? gs[mid].blk0b : gs[mid].blk0) <= blk) lo = mid; else hi = mid - 1;
+        const GDev& g = gs[mid];
+        const int32_t s = which == 0 ? g.blk0 : which == 1 ? g.blk0b : which == 2 ? g.blk0f : g.blk0fb;
+        if (s <= blk) lo = mid; else hi = mid - 1;
     }
     return lo;
 }
@@ -403,7 +427,7 @@ __global__ void __launch_bounds__(TB) k_iter_a(const GDev* __restrict__ gs, int3
     __shared__ double red[TB / WAVE];
     __shared__ double msr;
     __shared__ int32_t sg;
-    if (threadIdx.x == 0) sg = graph_of(gs, ng, (int32_t)blockIdx.x, false);
+    if (threadIdx.x == 0) sg = graph_of(gs, ng, (int32_t)blockIdx.x, 0);
     __syncthreads();
     const GDev& G = gs[sg];
     const int32_t lb = (int32_t)blockIdx.x - G.blk0;
@@ -479,7 +503,7 @@ __global__ void __launch_bounds__(TB) k_iter_a(const GDev* __restrict__ gs, int3
 // the call-graph term: s'[o] = d * (sum / M_r(k) + alpha * sum_p pw_p s_k[p] / M_s(k))  (:122-124)
 __global__ void __launch_bounds__(TB) k_iter_b(const GDev* __restrict__ gs, int32_t ng, double d, double alpha, int it) {
     __shared__ int32_t sg;
-    if (threadIdx.x == 0) sg = graph_of(gs, ng, (int32_t)blockIdx.x, true);
+    if (threadIdx.x == 0) sg = graph_of(gs, ng, (int32_t)blockIdx.x, 1);
     __syncthreads();
     const GDev& G = gs[sg];
     const int32_t o = ((int32_t)blockIdx.x - G.blk0b) * (TB / WAVE) + (int32_t)(threadIdx.x / WAVE);
@@ -503,6 +527,290 @@ __global__ void __launch_bounds__(TB) k_iter_b(const GDev* __restrict__ gs, int3
         const double v = d * (sum / Mr + alpha * (bb / Ms));      // pagerank.py:122-124
         G.spb[nxt][o] = v;
         G.sub[nxt][o] = (double)G.u_o[o] * v;
+        atomicMax(&Mnext[o % MSH], d2bits(v));
+    }
+}
+
+// ---------------------------------------------------------------- fused single-pass iteration
+// For graphs with N <= FX_NMAX and P_rs == P_sr (every graph built from spans): ONE read of the
+// trace-major u16 ids per iteration serves both products of pagerank.py:122-125.
+//   k_fx_a  block = TT consecutive traces (a thread each):
+//     r'[t]   = d * sum_{o in ops(t)} su_k[o] / M_s(k) + fp32((1-d) v_t)        (node order)
+//     lacc[o] += X_t for o in ops(t),   X_t = rint(w_t r'_k[t] / M_r(k) * 2^SC)   (LDS, u64)
+//   The block's N accumulators go out as one dense row part[block][0..N).  Because X_t <= 2^SC
+//   (w_t <= 1, r'_k <= M_r(k)) and SC = 63 - log2(TT), a row entry never exceeds 2^63.
+//   k_fx_b  wave per op: S_o = sum over blocks of part[.][o] as two exact 32-bit-limb sums, one
+//   rounding to double, then s'[o] = d * (S_o 2^-SC + alpha * sum_p pw_p s_k[p] / M_s(k)).
+// Integer sums are exact, so the result does not depend on atomic or reduction order: runs are
+// bitwise reproducible, and the quantisation (2^-SC absolute per term, SC >= 53) sits below
+// fp64's own rounding of the reference's dot products.
+constexpr int FX_NMAX = 8192;
+constexpr int FX_CAP = 24;   // staged ids per thread: blocks with more entries take the long path
+
+// graph of a fused-launch block: ng <= 2 resolves from the scalar split (no memory hop)
+__device__ __forceinline__ int32_t fx_graph(const GDev* gs, int32_t ng, int32_t split, int which) {
+    if (ng == 1) return 0;
+    if (ng == 2) return (int32_t)blockIdx.x >= split ? 1 : 0;
+    return graph_of(gs, ng, (int32_t)blockIdx.x, which);
+}
+
+// LDS layout of k_fx_a (byte offsets), shared by kernel and host
+struct FxLds {
+    size_t su, lacc, head, tail, tsum, xl, toff, owner, hbits, ids, total;
+    __host__ __device__ FxLds(int32_t N, int32_t TT) {
+        su = 0;
+        lacc = su + ((size_t)N + 1) * 8;
+        head = lacc + ((size_t)N + 1) * 8;
+        tail = head + (size_t)TT * 8;
+        tsum = tail + (size_t)TT * 8;
+        xl = tsum + (size_t)TT * 8;
+        toff = xl + ((size_t)TT + 1) * 8;
+        owner = toff + ((size_t)TT + 1) * 4;
+        hbits = owner + (size_t)TT * 4;
+        ids = (hbits + ((size_t)FX_CAP * TT / 32 + 2) * 4 + 15) / 16 * 16;
+        total = ids + ((size_t)FX_CAP * TT + 16) * 2;
+    }
+};
+
+// Balanced walk (blocks whose id range fits FX_CAP*TT - 8 entries): the block's ids are staged
+// in LDS from a 16-B aligned base (positions q = entry - base; the entry range starts at `shift`)
+// and cut into TT equal segments of L positions (L a multiple of 8); lane s walks segment s in
+// order.  Trace starts are bits of an LDS bitmap.  Per trace the walk yields pieces: a whole
+// trace inside one segment -> tsum[t]; a trace crossing segments -> tail[first segment] +
+// head[each later segment], combined in segment order by the trace's own thread.  Sums stay
+// sequential within a piece: fixed order, deterministic.  Requires non-empty traces (every
+// graph built from spans; uploaded graphs are checked on the host).
+template <class Q>
+__global__ void __launch_bounds__(1024) k_fx_a(const GDev* __restrict__ gs, int32_t ng, int32_t split, double d,
+                                               double alpha, int it) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lraw[];
+    __shared__ double red[1024 / WAVE];
+    __shared__ double msh[2];
+    const unsigned long long ts0 = __builtin_amdgcn_s_memrealtime();
+    const GDev& G = gs[fx_graph(gs, ng, split, 2)];
+    const int32_t TT = (int32_t)blockDim.x;
+    const int32_t lb = (int32_t)blockIdx.x - G.blk0f;
+    const int cur = it & 1, nxt = cur ^ 1, k3 = it % 3;
+    const int32_t T = G.T, N = G.N;
+    const int32_t t0 = lb * TT;
+    const int32_t nt = min(TT, T - t0);
+    const int32_t i = (int32_t)threadIdx.x;
+    const int32_t t = t0 + i;
+    const bool own = i < nt;
+    const FxLds L_(N, TT);
+    double* su = (double*)(lraw + L_.su);
+    unsigned long long* lacc = (unsigned long long*)(lraw + L_.lacc);
+    double* head = (double*)(lraw + L_.head);
+    double* tail = (double*)(lraw + L_.tail);
+    double* tsum = (double*)(lraw + L_.tsum);
+    unsigned long long* xl = (unsigned long long*)(lraw + L_.xl);   // xl[c + 1] = X of trace c; xl[0] = 0
+    int32_t* toff = (int32_t*)(lraw + L_.toff);
+    int32_t* owner = (int32_t*)(lraw + L_.owner);
+    uint32_t* hbits = (uint32_t*)(lraw + L_.hbits);
+    uint16_t* ids = (uint16_t*)(lraw + L_.ids);
+    // every independent load of the block goes out before the first barrier
+    const int64_t e0 = G.rs_off[t0], e1 = G.rs_off[t0 + nt];
+    const int64_t a = own ? G.rs_off[t] : 0, b = own ? G.rs_off[t + 1] : 0;
+    const double qk = own ? (double)((const Q*)G.q[cur])[t] : 0.0;
+    const float ct = own ? G.c_t[t] : 0.0f, wt = own ? G.w_t[t] : 0.0f;
+    unsigned long long* mslot = G.mslot;
+    const unsigned long long* Mcur = mslot + (size_t)2 * MSH * k3;
+    unsigned long long* Mnext = mslot + (size_t)2 * MSH * ((k3 + 1) % 3);
+    if (lb == 0 && i < 2 * MSH) mslot[(size_t)2 * MSH * ((k3 + 2) % 3) + i] = 0ull;
+    const int64_t base = e0 & ~(int64_t)7;
+    const int32_t shift = (int32_t)(e0 - base);
+    const int64_t np_ = e1 - base;                 // positions [shift, np_) hold the block's entries
+    const bool bal = np_ <= (int64_t)FX_CAP * TT;
+    if (bal) {   // stage the id range: 16-B loads of 8 ids (the buffer is padded past nnz)
+        const uint4* src = (const uint4*)(G.rs16 + base);
+        const int32_t nch = (int32_t)((np_ + 7) >> 3);
+        uint4 v[FX_CAP / 8];
+#pragma unroll
+        for (int j = 0; j < FX_CAP / 8; ++j) v[j] = src[min(i + j * TT, nch - 1)];
+#pragma unroll
+        for (int j = 0; j < FX_CAP / 8; ++j)
+            if (i + j * TT < nch) *(uint4*)(ids + (size_t)(i + j * TT) * 8) = v[j];
+        for (int32_t w = i; w < FX_CAP * TT / 32 + 2; w += TT) hbits[w] = 0u;
+        if (i == 0) {
+            owner[0] = -1;   // positions before `shift` belong to the previous block
+            xl[0] = 0ull;
+        }
+    }
+    const double* sug = G.sub[cur];
+    for (int32_t o = i; o <= N; o += TT) {
+        su[o] = o < N ? sug[o] : 0.0;
+        lacc[o] = 0ull;
+    }
+    if (i < WAVE) {
+        const double ms = wave_max(bits2d(Mcur[i]));
+        const double mr = wave_max(bits2d(Mcur[MSH + i]));
+        if (i == 0) {
+            msh[0] = ms;
+            msh[1] = mr;
+        }
+    }
+    if (own) toff[i] = (int32_t)(a - base);
+    if (i == 0) toff[nt] = (int32_t)np_;
+    __syncthreads();
+    const unsigned long long X = own ? (unsigned long long)__double2ull_rn(qk / msh[1] * G.fx_scale) : 0ull;
+    if (G.stamp && i == 0) G.stamp[(size_t)blockIdx.x * 8 + 1] = __builtin_amdgcn_s_memrealtime();
+    double acc = 0.0;
+    if (bal) {
+        int32_t L = (int32_t)((np_ + 8 * TT - 1) / (8 * TT)) * 8;
+        if (L == 0) L = 8;
+        const int32_t ra = (int32_t)(a - base), rb = (int32_t)(b - base);
+        if (own) {
+            xl[i + 1] = X;
+            atomicOr(&hbits[ra >> 5], 1u << (ra & 31));
+            for (int32_t sg = (ra + L - 1) / L; sg * L < rb; ++sg) owner[sg] = i;   // segments starting in t
+        }
+        __syncthreads();
+        if (G.stamp && i == 0) G.stamp[(size_t)blockIdx.x * 8 + 2] = __builtin_amdgcn_s_memrealtime();
+        const int32_t p = i * L;
+        if (p < np_) {
+            const int32_t qe = (int32_t)min((int64_t)p + L, np_);
+            const unsigned long long bits =
+                (((unsigned long long)hbits[(p >> 5) + 1] << 32) | hbits[p >> 5]) >> (p & 31);
+            int32_t c = owner[i];
+            bool st = bits & 1ull;                   // the segment's first piece starts a trace
+            unsigned long long Xc = xl[c + 1];
+            for (int32_t ch = p; ch < qe; ch += 8) {
+                const uint4 w = *(const uint4*)(ids + ch);   // 8 ids, 16-B aligned (ch % 8 == 0)
+                int32_t o[8];
+                o[0] = (int32_t)(w.x & 0xffffu); o[1] = (int32_t)(w.x >> 16);
+                o[2] = (int32_t)(w.y & 0xffffu); o[3] = (int32_t)(w.y >> 16);
+                o[4] = (int32_t)(w.z & 0xffffu); o[5] = (int32_t)(w.z >> 16);
+                o[6] = (int32_t)(w.w & 0xffffu); o[7] = (int32_t)(w.w >> 16);
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    if (ch + j < shift || ch + j >= qe) o[j] = N;   // outside the block: the zero slot
+                double g[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) g[j] = su[o[j]];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int32_t e = ch + j;
+                    if (e > p && e < qe && ((bits >> (e - p)) & 1ull)) {   // a new trace starts at e
+                        if (st) tsum[c] = acc; else head[i] = acc;
+                        acc = 0.0;
+                        st = true;
+                        ++c;
+                        Xc = xl[c + 1];
+                    }
+                    acc += g[j];
+                    atomicAdd(&lacc[o[j]], Xc);
+                }
+            }
+            const bool ends = qe == np_ || ((bits >> (qe - p)) & 1ull);
+            if (st) {
+                if (ends) tsum[c] = acc; else tail[i] = acc;
+            } else {
+                head[i] = acc;
+            }
+        }
+        __syncthreads();
+        if (G.stamp && i == 0) G.stamp[(size_t)blockIdx.x * 8 + 3] = __builtin_amdgcn_s_memrealtime();
+        if (own && rb > ra) {
+            const int32_t sa = ra / L, sb = (rb - 1) / L;
+            if (sa == sb) {
+                acc = tsum[i];
+            } else {
+                acc = tail[sa];
+                for (int32_t sg = sa + 1; sg <= sb; ++sg) acc += head[sg];
+            }
+        } else {
+            acc = 0.0;
+        }
+    } else {
+        // long block (rare): thread per trace in rounds of FX_CAP*TT staged ids, 8-entry chunks
+        const int32_t cap = FX_CAP * TT;
+        const int lane = i & (WAVE - 1);
+        for (int64_t lo = e0; lo < e1; lo += cap) {
+            const int64_t hi = min(lo + (int64_t)cap, e1);
+            __syncthreads();
+            for (int64_t e = lo + i; e < hi; e += TT) ids[e - lo] = G.rs16[e];
+            __syncthreads();
+            const int32_t x0 = (int32_t)(max(a, lo) - lo), x1 = (int32_t)(min(b, hi) - lo);
+            for (int32_t c = x0; c < x1; c += 8) {
+                int32_t o[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) o[j] = c + j < x1 ? (int32_t)ids[c + j] : N;
+                double g[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) g[j] = su[o[j]];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) acc += g[j];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) atomicAdd(&lacc[o[(j + lane) & 7]], X);
+            }
+        }
+    }
+    // call-graph term for the next s' (pagerank.py:122-124, alpha P_ss s_k), a thread per op
+    for (int32_t oss = lb * TT + i; oss < N; oss += G.n_fa * TT) {
+        const double* sp_cur = G.spb[cur];
+        double bb = 0.0;
+        for (int64_t e = G.ss_off[oss]; e < G.ss_off[oss + 1]; ++e) {
+            const int32_t pp = G.ss_par[e];
+            bb += (double)G.pw[pp] * sp_cur[pp];
+        }
+        G.fx_ssv[oss] = alpha * (bb / msh[0]);
+    }
+    if (G.stamp && i == 0) G.stamp[(size_t)blockIdx.x * 8 + 4] = __builtin_amdgcn_s_memrealtime();
+    __syncthreads();
+    if (G.stamp && i == 0) G.stamp[(size_t)blockIdx.x * 8 + 5] = __builtin_amdgcn_s_memrealtime();
+    unsigned long long* prow = G.fx_part + (size_t)lb * N;
+    for (int32_t o = i; o < N; o += TT) prow[o] = lacc[o];
+    double rmax = -__builtin_huge_val();
+    if (own) {
+        const double rp = d * (acc / msh[0]) + (double)ct;   // pagerank.py:125
+        ((Q*)G.q[nxt])[t] = (Q)((double)wt * rp);
+        rmax = rp;
+    }
+    rmax = block_max(rmax, red);
+    if (i == 0) {
+        atomicMax(&Mnext[MSH + blockIdx.x % MSH], d2bits(rmax));
+        if (G.stamp) {
+            G.stamp[(size_t)blockIdx.x * 8] = ts0;
+            G.stamp[(size_t)blockIdx.x * 8 + 6] = __builtin_amdgcn_s_memrealtime();
+        }
+    }
+}
+
+__global__ void __launch_bounds__(TB) k_fx_b(const GDev* __restrict__ gs, int32_t ng, int32_t split, double d, int it) {
+    const GDev& G = gs[fx_graph(gs, ng, split, 3)];
+    const int32_t o = ((int32_t)blockIdx.x - G.blk0fb) * (TB / WAVE) + (int32_t)(threadIdx.x / WAVE);
+    if (o >= G.N) return;
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int nxt = (it & 1) ^ 1, k3 = it % 3;
+    unsigned long long* Mnext = G.mslot + (size_t)2 * MSH * ((k3 + 1) % 3);
+    const int32_t nb = G.n_fa, N = G.N;
+    const double ssv = G.fx_ssv[o];
+    const float uo = G.u_o[o];
+    const unsigned long long* __restrict__ col = G.fx_part + o;
+    unsigned long long lo = 0ull, hi = 0ull;
+    int32_t i = lane;
+    for (; i + 3 * WAVE < nb; i += 4 * WAVE) {
+        const unsigned long long v0 = col[(size_t)i * N], v1 = col[(size_t)(i + WAVE) * N],
+                                 v2 = col[(size_t)(i + 2 * WAVE) * N], v3 = col[(size_t)(i + 3 * WAVE) * N];
+        lo += (v0 & 0xffffffffull) + (v1 & 0xffffffffull) + (v2 & 0xffffffffull) + (v3 & 0xffffffffull);
+        hi += (v0 >> 32) + (v1 >> 32) + (v2 >> 32) + (v3 >> 32);
+    }
+    for (; i < nb; i += WAVE) {
+        const unsigned long long v = col[(size_t)i * N];
+        lo += v & 0xffffffffull;
+        hi += v >> 32;
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        lo += __shfl_xor(lo, m, WAVE);
+        hi += __shfl_xor(hi, m, WAVE);
+    }
+    // hi, lo < 2^53 (fewer than 2^21 blocks): both conversions exact, one rounding in the add
+    const double sum = ((double)hi * 4294967296.0 + (double)lo) * G.fx_iscale;
+    if (lane == 0) {
+        const double v = d * (sum + ssv);      // pagerank.py:122-124
+        G.spb[nxt][o] = v;
+        G.sub[nxt][o] = (double)uo * v;
         atomicMax(&Mnext[o % MSH], d2bits(v));
     }
 }
@@ -575,8 +883,20 @@ int mr_graph_prepare(mr_ctx* ctx, mr_graph* g) {
     if (T) hipLaunchKernelGGL(k_trace_consts, dim3(cdiv(T, 256)), dim3(256), 0, st, g->len_t.p, g->w_t.p, T);
     if (N) hipLaunchKernelGGL(k_op_consts, dim3(cdiv(N, 256)), dim3(256), 0, st, g->len_o.p, g->nchild.p, g->u_o.p, g->pw.p, N);
     if (N <= 65536 && g->nnz_rs) {
-        MR_TRY(g->rs16.alloc(ctx, (size_t)g->nnz_rs));
+        MR_TRY(g->rs16.alloc(ctx, (size_t)g->nnz_rs + 8));
         hipLaunchKernelGGL(k_ids16, dim3(cdiv(g->nnz_rs, 256)), dim3(256), 0, st, g->rs_ops.p, g->nnz_rs, g->rs16.p);
+    }
+    static const bool no_fused = getenv("MR_NO_FUSED") != nullptr;   // A/B knob: force the tile path
+    g->fused = !no_fused && g->rs_is_sr && g->traces_nonempty && N <= FX_NMAX;
+    if (g->fused) {   // no P_sr tiles: the fused iteration reads the trace-major ids only
+        MR_TRY_HIP(ctx, hipMemsetAsync(g->cov.p, 0, (size_t)std::max(N, 1) * sizeof(int32_t), st));
+        if (nnz && N)
+            hipLaunchKernelGGL(k_cov_hist, dim3(cdiv(nnz, 256 * 64)), dim3(256), (size_t)N * sizeof(int32_t), st,
+                               g->rs16.p, nnz, N, g->cov.p);
+        g->n_tiles = 0;
+        g->n_pairs = 0;
+        MR_TRY_HIP(ctx, hipGetLastError());
+        return MR_OK;
     }
     // tiles: ~256 of them when T allows, 256..4096 traces each
     int ts = TSHIFT_MIN;
@@ -660,6 +980,16 @@ int mr_graph_prepare(mr_ctx* ctx, mr_graph* g) {
     return MR_OK;   // scratch returns to the stream-ordered pool: no sync needed
 }
 
+// traces per k_fx_a block (= its block size; MR_TT overrides for measurements)
+static int fx_tt() {
+    static const int tt = [] {
+        const char* e = getenv("MR_TT");
+        const int v = e ? atoi(e) : 512;
+        return (v == 256 || v == 512 || v == 1024) ? v : 512;
+    }();
+    return tt;
+}
+
 // kinds, preference vector and iteration state of one graph (everything before the iterations)
 static int pagerank_setup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool fp32, uint32_t flags) {
     hipStream_t st = ctx->stream;
@@ -685,7 +1015,11 @@ static int pagerank_setup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool 
     MR_TRY(g->sub[0].alloc(ctx, (size_t)N));
     MR_TRY(g->sub[1].alloc(ctx, (size_t)N));
     MR_TRY(g->weight.alloc(ctx, (size_t)N));
-    MR_TRY(g->part.alloc(ctx, (size_t)std::max<int64_t>(g->n_pairs, 1)));
+    if (g->fused) {
+        MR_TRY(g->fx_part.alloc(ctx, (size_t)cdiv(T, fx_tt()) * (size_t)N));
+        MR_TRY(g->fx_ssv.alloc(ctx, (size_t)N));
+    }
+    else MR_TRY(g->part.alloc(ctx, (size_t)std::max<int64_t>(g->n_pairs, 1)));
     for (int i = 0; i < 2; ++i) {
         if (fp32) MR_TRY(g->q32[i].alloc(ctx, (size_t)T));
         else MR_TRY(g->q64[i].alloc(ctx, (size_t)T));
@@ -752,8 +1086,10 @@ int mr_pagerank_batch_impl(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly,
     int mask = 3;
     if (const char* rm = getenv("MR_ROLE_MASK")) mask = atoi(rm);   // profiling knob: 1 trace / 2 op side
     std::vector<GDev> hv((size_t)ng);
-    int32_t blocks_a = 0, blocks_b = 0;
-    size_t lds = VCAP * sizeof(double);
+    int32_t blocks_a = 0, blocks_b = 0, blocks_fa = 0, blocks_fb = 0;
+    size_t lds = VCAP * sizeof(double), lds_f = 0;
+    const int TT = fx_tt();
+    const int sc = 63 - (TT == 256 ? 8 : TT == 512 ? 9 : 10);
     double bytes = 0.0;
     for (int i = 0; i < ng; ++i) {
         mr_graph* g = gs[i];
@@ -781,25 +1117,55 @@ int mr_pagerank_batch_impl(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly,
         }
         v.part = g->part.p;
         v.mslot = g->mslot.p;
+        v.fx_part = (unsigned long long*)g->fx_part.p;
+        v.fx_ssv = g->fx_ssv.p;
+        v.stamp = nullptr;
+        v.probe = getenv("MR_FX_PROBE") ? atoi(getenv("MR_FX_PROBE")) : 0;
+        v.fx_scale = std::ldexp(1.0, sc);
+        v.fx_iscale = std::ldexp(1.0, -sc);
         v.T = g->T;
         v.N = g->N;
+        v.blk0f = blocks_fa;
+        v.n_fa = g->fused ? cdiv(g->T, TT) : 0;
+        blocks_fa += v.n_fa;
+        v.blk0fb = blocks_fb;
+        v.n_fb = g->fused ? cdiv(g->N, TB / WAVE) : 0;
+        blocks_fb += v.n_fb;
+        v.blk0 = blocks_a;
+        v.blk0b = blocks_b;
+        bytes += iter_bytes(g, fp32);
+        if (g->fused) {
+            lds_f = std::max(lds_f, FxLds(g->N, TT).total);
+            continue;   // no tile-path blocks (n_tb = n_tiles = n_ob = 0)
+        }
         v.n_tb = (mask & 1) ? cdiv(g->T, TB) : 0;
         v.n_tiles = (mask & 2) ? g->n_tiles : 0;
         v.tshift = g->tshift;
         v.lds_su = g->N <= LDS_NODES;
-        v.blk0 = blocks_a;
         blocks_a += v.n_tb + v.n_tiles;
         v.n_ob = (mask & 2) ? cdiv(g->N, TB / WAVE) : 0;
-        v.blk0b = blocks_b;
         blocks_b += v.n_ob;
         if (v.lds_su) lds = std::max(lds, ((size_t)g->N + VCAP) * sizeof(double));
         lds = std::max(lds, ((size_t)1 << g->tshift) * (fp32 ? sizeof(float) : sizeof(double)));
-        bytes += iter_bytes(g, fp32);
+    }
+    static const bool stamps = getenv("MR_FX_STAMP") != nullptr;
+    DBuf<unsigned long long> dstamp;
+    if (stamps && blocks_fa) {
+        MR_TRY(dstamp.zero(ctx, (size_t)blocks_fa * 8));
+        for (auto& v : hv) v.stamp = dstamp.p;
     }
     DBuf<GDev> dv;
     MR_TRY(dv.upload(ctx, hv.data(), hv.size()));
+    const int32_t split_fa = ng == 2 ? hv[1].blk0f : 0, split_fb = ng == 2 ? hv[1].blk0fb : 0;
     for (int it = 0; it < iters; ++it) {
         mr_prof_begin(ctx);
+        if (blocks_fa) {
+            if (fp32) hipLaunchKernelGGL(k_fx_a<float>, dim3(blocks_fa), dim3(TT), lds_f, st, dv.p, ng, split_fa, d, alpha, it);
+            else hipLaunchKernelGGL(k_fx_a<double>, dim3(blocks_fa), dim3(TT), lds_f, st, dv.p, ng, split_fa, d, alpha, it);
+            MR_DEBUG_CHECK(ctx, "k_fx_a");
+            hipLaunchKernelGGL(k_fx_b, dim3(blocks_fb), dim3(TB), 0, st, dv.p, ng, split_fb, d, it);
+            MR_DEBUG_CHECK(ctx, "k_fx_b");
+        }
         if (blocks_a) {
             if (fp32) hipLaunchKernelGGL(k_iter_a<float>, dim3(blocks_a), dim3(TB), lds, st, dv.p, ng, d, it);
             else hipLaunchKernelGGL(k_iter_a<double>, dim3(blocks_a), dim3(TB), lds, st, dv.p, ng, d, it);
@@ -818,6 +1184,30 @@ int mr_pagerank_batch_impl(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly,
         MR_DEBUG_CHECK(ctx, "k_weights");
     }
     MR_TRY_HIP(ctx, hipGetLastError());
+    if (dstamp.p) {   // diagnostics: phase times of the last k_fx_a launch, in 10 ns ticks
+        std::vector<unsigned long long> h((size_t)blocks_fa * 8);
+        MR_TRY(dstamp.download(ctx, h.data(), h.size()));
+        MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+        unsigned long long t0 = ~0ull, t6 = 0;
+        double sum[6] = {0}, mx[6] = {0};
+        int nb = 0;
+        for (int32_t b = 0; b < blocks_fa; ++b) {
+            const unsigned long long* x = &h[(size_t)b * 8];
+            if (!x[2]) continue;   // long-path blocks have no walk stamps
+            ++nb;
+            t0 = std::min(t0, x[0]);
+            t6 = std::max(t6, x[6]);
+            for (int k = 0; k < 6; ++k) {
+                const double dt = (double)(x[k + 1] - x[k]) * 0.01;
+                sum[k] += dt;
+                mx[k] = std::max(mx[k], dt);
+            }
+        }
+        fprintf(stderr, "[stamp] k_fx_a %d blocks span %.2f us; avg/max us: stage %.2f/%.2f mark %.2f/%.2f "
+                "walk %.2f/%.2f combine+ss %.2f/%.2f bar %.2f/%.2f tail %.2f/%.2f\n", nb, (t6 - t0) * 0.01,
+                sum[0] / nb, mx[0], sum[1] / nb, mx[1], sum[2] / nb, mx[2], sum[3] / nb, mx[3], sum[4] / nb, mx[4],
+                sum[5] / nb, mx[5]);
+    }
     // the only host round trip of the call: error words raised by the kernels
     std::vector<int32_t> hflag((size_t)4 * ng, 0);
     for (int i = 0; i < ng; ++i)
