@@ -9,12 +9,17 @@
 // dropped (:329).  The sum is sequential per trace with separate multiply and add (T14), so
 // the partition is bit-exact.
 #include <algorithm>
+#include <chrono>
+#include <utility>
+#include <vector>
 #include <climits>
 
 #include "mr_prim.h"
 #include "mr_sort.h"
 
-int mr_graph_build_dev(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d_mask, mr_graph** out);
+int mr_graph_build_dev(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d_mask, mr_graph** out, const int64_t* win);
+int mr_detect_indexed(mr_ctx* ctx, const mr_spans* s, int64_t t0, int64_t t1, const double* d_a3, const uint8_t* d_a3v,
+                      uint8_t* d_state, int32_t* n_abn, int32_t* n_nor, int64_t* n_in);
 int mr_spectrum_dev(mr_ctx* ctx, int32_t n, const uint8_t* flags, const double* a_w, const int64_t* a_num,
                     const double* n_w, const int64_t* n_num, int64_t A, int64_t Nl, int method, int32_t top,
                     int32_t* d_out_idx, double* d_out_score, uint8_t* d_out_np, int32_t* d_zflag);
@@ -139,6 +144,9 @@ static int detect_dev(mr_ctx* ctx, const mr_spans* s, int64_t t0, int64_t t1, co
     const int64_t S = s->S;
     const int32_t NT = s->n_traces, NO = s->n_svcops;
     if (!s->has_times) return mr_fail(ctx, MR_ERR_ARG, "spans have no startTime/endTime columns");
+    static const bool no_index = getenv("MR_NO_INDEX") != nullptr;   // A/B knob: force the row-level path
+    if (s->indexed && s->uniform_times && !no_index)   // the window selects whole traces: per-trace pass
+        return mr_detect_indexed(ctx, s, t0, t1, d_a3, d_a3v, d_state, n_abn, n_nor, n_in);
     DBuf<int32_t> flag;
     DBuf<int64_t> pos, tmp;
     MR_TRY(flag.alloc(ctx, S));
@@ -231,6 +239,26 @@ extern "C" int mr_rca_window(mr_ctx* ctx, const mr_spans* s, int64_t t0, int64_t
     hipStream_t st = ctx->stream;
     *n_out = 0;
     if (edges_traversed) *edges_traversed = 0;
+    // MR_WIN_TIMING: wall time of each phase (a stream sync at each mark; diagnostics only)
+    static const bool timing = getenv("MR_WIN_TIMING") != nullptr;
+    std::vector<std::pair<const char*, std::chrono::steady_clock::time_point>> marks;
+    auto mark = [&](const char* name) {
+        if (!timing) return;
+        (void)hipStreamSynchronize(st);
+        marks.emplace_back(name, std::chrono::steady_clock::now());
+    };
+    struct Report {
+        decltype(marks)& m;
+        ~Report() {
+            if (m.size() < 2) return;
+            fprintf(stderr, "[window]");
+            for (size_t i = 1; i < m.size(); ++i)
+                fprintf(stderr, " %s %.1f", m[i].first,
+                        std::chrono::duration<double, std::micro>(m[i].second - m[i - 1].second).count());
+            fprintf(stderr, " us\n");
+        }
+    } report{marks};
+    mark("start");
     const int32_t NT = s->n_traces, NP = s->n_podops;
     DBuf<double> da3;
     DBuf<uint8_t> dv, dst, m_abn, m_nor;
@@ -240,6 +268,7 @@ extern "C" int mr_rca_window(mr_ctx* ctx, const mr_spans* s, int64_t t0, int64_t
     int32_t na = 0, nn = 0;
     int64_t nin = 0;
     MR_TRY(detect_dev(ctx, s, t0, t1, da3.p, dv.p, dst.p, &na, &nn, &nin));
+    mark("detect");
     if (n_abnormal) *n_abnormal = na;
     if (n_normal) *n_normal = nn;
     // T1: the driver unpacks (flag, normal_list, abnormal_list) from (flag, abnormal, normal)
@@ -248,13 +277,18 @@ extern "C" int mr_rca_window(mr_ctx* ctx, const mr_spans* s, int64_t t0, int64_t
     MR_TRY(m_nor.alloc(ctx, NT));
     hipLaunchKernelGGL(k_masks, dim3(cdiv(NT, 256)), dim3(256), 0, st, dst.p, NT, m_abn.p, m_nor.p);
     mr_graph *gn = nullptr, *ga = nullptr;
-    int rc = mr_graph_build_dev(ctx, s, m_abn.p, &gn);   // "normal" graph = detector's abnormal traces
-    if (rc == MR_OK) rc = mr_graph_build_dev(ctx, s, m_nor.p, &ga);
+    // the graphs see the window's rows only (get_pagerank_graph(.., span_list), online_rca.py:180,185)
+    const int64_t win[2] = {t0, t1};
+    int rc = mr_graph_build_dev(ctx, s, m_abn.p, &gn, win);   // "normal" graph = detector's abnormal traces
+    mark("build_n");
+    if (rc == MR_OK) rc = mr_graph_build_dev(ctx, s, m_nor.p, &ga, win);
+    mark("build_a");
     if (rc == MR_OK) {   // both PageRanks in one batched launch per iteration
         mr_graph* both[2] = {gn, ga};
         const int anom[2] = {0, 1};
         rc = mr_pagerank_batch(ctx, both, anom, 2, 0.85, 0.01, 25, precision, 0);
     }
+    mark("pagerank");
     if (rc != MR_OK) {
         delete gn;
         delete ga;
@@ -301,6 +335,7 @@ extern "C" int mr_rca_window(mr_ctx* ctx, const mr_spans* s, int64_t t0, int64_t
     if (k && out_podop && (rc = codes.download(ctx, out_podop, k))) return cleanup(rc);
     if (k && out_score && (rc = sc.download(ctx, out_score, k))) return cleanup(rc);
     if (hipStreamSynchronize(st) != hipSuccess) return cleanup(MR_ERR_HIP);
+    mark("spectrum");
     *n_out = k;
     return cleanup(MR_OK);
 }

@@ -13,6 +13,7 @@
 //      op-major side is derived by mr_graph_prepare as tiles); call edges sorted by
 //      (child, parent) give P_ss by child.
 #include <algorithm>
+#include <vector>
 
 #include "mr_prim.h"
 #include "mr_sort.h"
@@ -60,9 +61,11 @@ __global__ void k_sort_buckets(const int64_t* off, int64_t n_codes, int32_t* row
 }
 
 // ---------------------------------------------------------------- selection
-__global__ void k_sel_flags(const int32_t* trace, int64_t S, const uint8_t* mask, int32_t* flag) {
+// rows of masked traces; with a window (ts non-null) also inside it (the window's span_df)
+__global__ void k_sel_flags(const int32_t* trace, int64_t S, const uint8_t* mask, const int64_t* ts, const int64_t* te,
+                            int64_t t0, int64_t t1, int32_t* flag) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < S) flag[i] = mask[trace[i]] ? 1 : 0;
+    if (i < S) flag[i] = (mask[trace[i]] && (!ts || (ts[i] >= t0 && te[i] <= t1))) ? 1 : 0;
 }
 __global__ void k_compact_rows(const int32_t* flag, const int64_t* pos, int64_t S, int32_t* rows) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -254,6 +257,135 @@ __global__ void k_edge_csr(const uint64_t* skey, int64_t E, int nb, int32_t* ss_
     ss_par[i] = (int32_t)(skey[i] & ((1ull << nb) - 1));
     atomicAdd(&ccount[skey[i] >> nb], 1);
 }
+
+// ---------------------------------------------------------------- indexed build (whole traces)
+constexpr int IX_EPT = 16;  // index entries per thread in k_ix_stats (fewer blocks: fewer global flushes)
+constexpr int IX_B = 8;     // entries per thread whose loads are batched
+__global__ void k_ix_sel(const uint8_t* mask, const int32_t* tlen, const int64_t* po_off, int32_t NT, int32_t* tflag,
+                         int32_t* zc) {
+    const int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= NT) return;
+    const bool on = mask[t] && tlen[t] > 0;
+    tflag[t] = on ? 1 : 0;
+    zc[t] = on ? (int32_t)(po_off[t + 1] - po_off[t]) : 0;
+}
+// entry-parallel over the index: span counts and first rows per pod-op of the selected traces
+// (LDS-aggregated per block), and their join keys with multiplicity into the block's LDS edge
+// set (hot keys aggregated before global atomics).  Block b takes a 1/gridDim share of each list.
+__global__ void __launch_bounds__(BT) k_ix_stats(const int32_t* tflag, int64_t n_po, const int32_t* po_tr,
+                                                 const int32_t* po_op, const int32_t* po_cnt, const int32_t* po_first,
+                                                 int64_t n_ed, const int32_t* ed_tr, const uint64_t* ed_key,
+                                                 const int32_t* ed_cnt, int32_t n_podops, int use_lds_hist,
+                                                 int32_t* ocnt, int32_t* ofirst, uint64_t* gk, uint32_t* gc,
+                                                 uint64_t gmask) {
+    extern __shared__ int32_t lh[];
+    __shared__ unsigned long long ek[ESET];
+    __shared__ uint32_t ec[ESET];
+    int32_t* lcnt = lh;
+    int32_t* lfirst = lh + n_podops;
+    if (use_lds_hist)
+        for (int32_t i = threadIdx.x; i < n_podops; i += BT) {
+            lcnt[i] = 0;
+            lfirst[i] = 0x7fffffff;
+        }
+    for (int i = threadIdx.x; i < ESET; i += BT) {
+        ek[i] = EMPTY;
+        ec[i] = 0;
+    }
+    __syncthreads();
+    const int64_t pper = (n_po + gridDim.x - 1) / gridDim.x, eper = (n_ed + gridDim.x - 1) / gridDim.x;
+    // loads of a round of IX_B entries per thread go out together, then the trace flags
+    const int64_t p0 = (int64_t)blockIdx.x * pper, p1 = min(p0 + pper, n_po);
+    for (int64_t rb = p0; rb < p1; rb += (int64_t)BT * IX_B) {
+        int32_t tr[IX_B], op[IX_B], cn[IX_B], fr[IX_B];
+        bool on[IX_B];
+#pragma unroll
+        for (int j = 0; j < IX_B; ++j) {
+            const int64_t r = min(rb + threadIdx.x + (int64_t)j * BT, p1 - 1);
+            tr[j] = po_tr[r];
+            op[j] = po_op[r];
+            cn[j] = po_cnt[r];
+            fr[j] = po_first[r];
+        }
+#pragma unroll
+        for (int j = 0; j < IX_B; ++j) on[j] = rb + threadIdx.x + (int64_t)j * BT < p1 && tflag[tr[j]];
+#pragma unroll
+        for (int j = 0; j < IX_B; ++j) {
+            if (!on[j]) continue;
+            if (use_lds_hist) {
+                atomicAdd(&lcnt[op[j]], cn[j]);
+                atomicMin(&lfirst[op[j]], fr[j]);
+            } else {
+                atomicAdd(&ocnt[op[j]], cn[j]);
+                atomicMin(&ofirst[op[j]], fr[j]);
+            }
+        }
+    }
+    const int64_t q0 = (int64_t)blockIdx.x * eper, q1 = min(q0 + eper, n_ed);
+    for (int64_t rb = q0; rb < q1; rb += (int64_t)BT * IX_B) {
+        int32_t tr[IX_B], cn[IX_B];
+        uint64_t ky[IX_B];
+        bool on[IX_B];
+#pragma unroll
+        for (int j = 0; j < IX_B; ++j) {
+            const int64_t r = min(rb + threadIdx.x + (int64_t)j * BT, q1 - 1);
+            tr[j] = ed_tr[r];
+            ky[j] = ed_key[r];
+            cn[j] = ed_cnt[r];
+        }
+#pragma unroll
+        for (int j = 0; j < IX_B; ++j) on[j] = rb + threadIdx.x + (int64_t)j * BT < q1 && tflag[tr[j]];
+        for (int j = 0; j < IX_B; ++j) {
+            if (!on[j]) continue;
+            const uint64_t key = ky[j];
+            uint32_t s = (uint32_t)(hmix(key) & (ESET - 1));
+            bool done = false;
+            for (int probe = 0; probe < 32; ++probe) {
+                unsigned long long kk = atomicCAS(&ek[s], (unsigned long long)EMPTY, (unsigned long long)key);
+                if (kk == EMPTY || kk == key) {
+                    atomicAdd(&ec[s], (uint32_t)cn[j]);
+                    done = true;
+                    break;
+                }
+                s = (s + 1) & (ESET - 1);
+            }
+            if (!done) global_edge_add(key, (uint32_t)cn[j], gk, gc, gmask);
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < ESET; i += BT)
+        if (ek[i] != EMPTY) global_edge_add(ek[i], ec[i], gk, gc, gmask);
+    if (use_lds_hist)
+        for (int32_t i = threadIdx.x; i < n_podops; i += BT)
+            if (lcnt[i]) {
+                atomicAdd(&ocnt[i], lcnt[i]);
+                atomicMin(&ofirst[i], lfirst[i]);
+            }
+}
+// join pairs whose rows lie in different traces count when both traces are selected (T11)
+__global__ void k_ix_cross(const uint8_t* mask, const int32_t* tc, const int32_t* tp, const uint64_t* key, int64_t n,
+                           uint64_t* gk, uint32_t* gc, uint64_t gmask) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n && mask[tc[i]] && mask[tp[i]]) global_edge_add(key[i], 1u, gk, gc, gmask);
+}
+__global__ void k_ix_trace_rows(const int32_t* tflag, const int64_t* tpos, const int64_t* zoff, int32_t NT,
+                                const int32_t* tlen, int32_t* trace_code, int32_t* len_t, int64_t* rs_off) {
+    const int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= NT || !tflag[t]) return;
+    const int32_t p = (int32_t)tpos[t];
+    trace_code[p] = t;
+    len_t[p] = tlen[t];
+    rs_off[p] = zoff[t];
+}
+// the selected traces' op lists (entry-parallel): rs_ops[zoff[t] + k] = node of the k-th pod-op
+__global__ void k_ix_trace_ops(const int32_t* tflag, const int64_t* zoff, int64_t n_po, const int32_t* po_tr,
+                               const int64_t* po_off, const int32_t* po_op, const int32_t* node_of_code, int32_t* rs_ops) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n_po) return;
+    const int32_t t = po_tr[r];
+    if (!tflag[t]) return;
+    rs_ops[zoff[t] + (r - po_off[t])] = node_of_code[po_op[r]];
+}
 }  // namespace
 
 // ------------------------------------------------------------------------------ host
@@ -308,6 +440,7 @@ extern "C" int mr_spans_upload(mr_ctx* ctx, const mr_span_cols* c, mr_spans** ou
     if (U) hipLaunchKernelGGL(k_sort_buckets, dim3(cdiv(U, 256)), dim3(256), 0, ctx->stream, s->id_off.p, U, s->id_rows.p);
     if (hipGetLastError() != hipSuccess || hipStreamSynchronize(ctx->stream) != hipSuccess)
         return fail(mr_fail(ctx, MR_ERR_HIP, "mr_spans_upload: kernel failure"));
+    if ((rc = mr_spans_index(ctx, s))) return fail(rc);
     *out = s;
     return MR_OK;
 }
@@ -326,172 +459,264 @@ static int read_i64(mr_ctx* ctx, const int64_t* dev, int64_t* host) {
     return MR_OK;
 }
 
-int mr_graph_build_dev(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d_mask, mr_graph** out) {
+// Shared by both builds, after the per-pod-op statistics and the call-edge hash are complete:
+// call edges -> node order (sorted parent ops, then the others by first appearance, T10) ->
+// per-node arrays (len_o, nchild) and P_ss by child.  ofirst holds a key per pod-op that orders
+// first appearances like the DataFrame rows (row_bits wide).
+static int build_nodes(mr_ctx* ctx, mr_graph* g, int32_t NP, const int32_t* ocnt, const int32_t* ofirst, int row_bits,
+                       const uint64_t* gk, const uint32_t* gc, uint64_t ecap, DBuf<int32_t>& node_of_code) {
+    hipStream_t st = ctx->stream;
+    DBuf<int32_t> eflag, is_par, nchild_code;
+    DBuf<int64_t> epos, etmp, tmp;
+    MR_TRY(eflag.alloc(ctx, ecap));
+    MR_TRY(epos.alloc(ctx, ecap + 1));
+    MR_TRY(etmp.alloc(ctx, scan_tmp_elems(ecap)));
+    MR_TRY(tmp.alloc(ctx, std::max<int64_t>(scan_tmp_elems(NP), 1)));
+    MR_TRY(is_par.zero(ctx, NP));
+    MR_TRY(nchild_code.zero(ctx, NP));
+    hipLaunchKernelGGL(k_edge_flags, dim3(cdiv(ecap, 256)), dim3(256), 0, st, gk, (int64_t)ecap, eflag.p);
+    MR_TRY(mr_exclusive_scan_i32(ctx, eflag.p, epos.p, ecap, etmp.p));
+    int64_t E = 0;
+    MR_TRY(read_i64(ctx, epos.p + ecap, &E));
+    DBuf<uint64_t> ekey;
+    DBuf<uint32_t> ecnt;
+    MR_TRY(ekey.alloc(ctx, E));
+    MR_TRY(ecnt.alloc(ctx, E));
+    hipLaunchKernelGGL(k_edge_compact, dim3(cdiv(ecap, 256)), dim3(256), 0, st, gk, gc, eflag.p, epos.p, (int64_t)ecap,
+                       ekey.p, ecnt.p, is_par.p, nchild_code.p);
+    // node order
+    DBuf<int32_t> pflag, qflag;
+    DBuf<int64_t> ppos, qpos;
+    MR_TRY(pflag.alloc(ctx, NP));
+    MR_TRY(qflag.alloc(ctx, NP));
+    MR_TRY(ppos.alloc(ctx, NP + 1));
+    MR_TRY(qpos.alloc(ctx, NP + 1));
+    MR_TRY(node_of_code.alloc(ctx, NP));
+    if (NP) hipLaunchKernelGGL(k_node_flags, dim3(cdiv(NP, 256)), dim3(256), 0, st, ocnt, is_par.p, NP, pflag.p, qflag.p);
+    MR_TRY(mr_exclusive_scan_i32(ctx, pflag.p, ppos.p, NP, tmp.p));
+    MR_TRY(mr_exclusive_scan_i32(ctx, qflag.p, qpos.p, NP, tmp.p));
+    int64_t PQ[2] = {0, 0};
+    MR_TRY_HIP(ctx, hipMemcpyAsync(&PQ[0], ppos.p + NP, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    MR_TRY_HIP(ctx, hipMemcpyAsync(&PQ[1], qpos.p + NP, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+    const int64_t P = PQ[0], Q = PQ[1];
+    const int32_t N = (int32_t)(P + Q);
+    MR_TRY(g->node_podop.alloc(ctx, N));
+    DBuf<uint64_t> qkey;
+    DBuf<uint32_t> qval;
+    MR_TRY(qkey.alloc(ctx, Q));
+    MR_TRY(qval.alloc(ctx, Q));
+    if (NP)
+        hipLaunchKernelGGL(k_node_parents, dim3(cdiv(NP, 256)), dim3(256), 0, st, pflag.p, ppos.p, qflag.p, qpos.p, ofirst,
+                           NP, node_of_code.p, g->node_podop.p, qkey.p, qval.p);
+    SortScratch ws;
+    MR_TRY(mr_radix_sort(ctx, qkey.p, qval.p, Q, row_bits, ws));
+    if (Q)
+        hipLaunchKernelGGL(k_node_rest, dim3(cdiv(Q, 256)), dim3(256), 0, st, qval.p, Q, (int32_t)P, node_of_code.p,
+                           g->node_podop.p);
+    // per-node arrays and P_ss
+    const int nb = std::max(1, bits_for((uint64_t)std::max(N - 1, 0)));
+    MR_TRY(g->len_o.alloc(ctx, N));
+    MR_TRY(g->nchild.alloc(ctx, N));
+    if (N)
+        hipLaunchKernelGGL(k_node_arrays, dim3(cdiv(N, 256)), dim3(256), 0, st, g->node_podop.p, N, ocnt, nchild_code.p,
+                           g->len_o.p, g->nchild.p);
+    DBuf<uint64_t> skey;
+    MR_TRY(skey.alloc(ctx, E));
+    if (E) hipLaunchKernelGGL(k_edge_nodes, dim3(cdiv(E, 256)), dim3(256), 0, st, ekey.p, E, node_of_code.p, nb, skey.p);
+    MR_TRY(mr_radix_sort(ctx, skey.p, nullptr, E, 2 * nb, ws));
+    DBuf<int32_t> ccount;
+    DBuf<int64_t> ntmp;
+    MR_TRY(ccount.zero(ctx, N));
+    MR_TRY(ntmp.alloc(ctx, scan_tmp_elems(std::max(N, 1))));
+    MR_TRY(g->ss_par.alloc(ctx, E));
+    MR_TRY(g->ss_off.alloc(ctx, N + 1));
+    if (E) hipLaunchKernelGGL(k_edge_csr, dim3(cdiv(E, 256)), dim3(256), 0, st, skey.p, E, nb, g->ss_par.p, ccount.p);
+    MR_TRY(mr_exclusive_scan_i32(ctx, ccount.p, g->ss_off.p, N, ntmp.p));
+    MR_TRY_HIP(ctx, hipGetLastError());
+    g->N = N;
+    g->E = E;
+    return MR_OK;
+}
+
+static uint64_t edge_capacity(int64_t want, int32_t NP) {
+    const uint64_t w = (uint64_t)std::min<int64_t>(std::max<int64_t>(want, 1), (int64_t)NP * NP + 1);
+    uint64_t cap = 1024;
+    while (cap < 2 * w) cap <<= 1;
+    return cap;
+}
+
+// Row-level build: any span table (rows selected by trace mask and, when `win`, by the
+// trace-level time window of each row).
+static int graph_build_rows(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d_mask, const int64_t* win, mr_graph* g) {
     hipStream_t st = ctx->stream;
     const int64_t S = sp->S;
     const int32_t NT = sp->n_traces, NP = sp->n_podops;
-    auto g = new mr_graph();
-    g->ctx = ctx;
-    int rc = MR_OK;
-    auto fail = [&](int code) {
-        delete g;
-        return code;
-    };
-#define TRY(x)                          \
-    do {                                \
-        if ((rc = (x))) return fail(rc); \
-    } while (0)
-#define TRY_HIP_(x)                                                                              \
-    do {                                                                                         \
-        hipError_t e_ = (x);                                                                     \
-        if (e_ != hipSuccess) return fail(mr_fail(ctx, MR_ERR_HIP, "%s: %s", #x, hipGetErrorString(e_))); \
-    } while (0)
     // 1. selected rows
     DBuf<int32_t> selflag, rows;
     DBuf<int64_t> pos, tmp;
     const int64_t tmpn = std::max<int64_t>({scan_tmp_elems(S), scan_tmp_elems(NT), scan_tmp_elems(NP), 1});
-    TRY(selflag.alloc(ctx, S));
-    TRY(pos.alloc(ctx, S + 1));
-    TRY(tmp.alloc(ctx, tmpn));
-    if (S) hipLaunchKernelGGL(k_sel_flags, dim3(cdiv(S, 256)), dim3(256), 0, st, sp->trace.p, S, d_mask, selflag.p);
-    TRY(mr_exclusive_scan_i32(ctx, selflag.p, pos.p, S, tmp.p));
+    MR_TRY(selflag.alloc(ctx, S));
+    MR_TRY(pos.alloc(ctx, S + 1));
+    MR_TRY(tmp.alloc(ctx, tmpn));
+    if (S)
+        hipLaunchKernelGGL(k_sel_flags, dim3(cdiv(S, 256)), dim3(256), 0, st, sp->trace.p, S, d_mask, win ? sp->tstart.p : nullptr,
+                           win ? sp->tend.p : nullptr, win ? win[0] : 0, win ? win[1] : 0, selflag.p);
+    MR_TRY(mr_exclusive_scan_i32(ctx, selflag.p, pos.p, S, tmp.p));
     int64_t Ssel = 0;
-    TRY(read_i64(ctx, pos.p + S, &Ssel));
-    TRY(rows.alloc(ctx, Ssel));
+    MR_TRY(read_i64(ctx, pos.p + S, &Ssel));
+    MR_TRY(rows.alloc(ctx, Ssel));
     if (S) hipLaunchKernelGGL(k_compact_rows, dim3(cdiv(S, 256)), dim3(256), 0, st, selflag.p, pos.p, S, rows.p);
     // 2. statistics + join
     DBuf<int32_t> tcnt, ocnt, ofirst;
-    TRY(tcnt.zero(ctx, NT));
-    TRY(ocnt.zero(ctx, NP));
-    TRY(ofirst.alloc(ctx, NP));
-    if (NP) TRY_HIP_(hipMemsetAsync(ofirst.p, 0x7f, NP * sizeof(int32_t), st));
-    uint64_t ecap_want = (uint64_t)std::min<int64_t>(std::max<int64_t>(Ssel, 1), (int64_t)NP * NP + 1);
-    uint64_t ecap = 1024;
-    while (ecap < 2 * ecap_want) ecap <<= 1;
+    MR_TRY(tcnt.zero(ctx, NT));
+    MR_TRY(ocnt.zero(ctx, NP));
+    MR_TRY(ofirst.alloc(ctx, NP));
+    if (NP) MR_TRY_HIP(ctx, hipMemsetAsync(ofirst.p, 0x7f, NP * sizeof(int32_t), st));
+    const uint64_t ecap = edge_capacity(Ssel, NP);
     DBuf<uint64_t> gk;
     DBuf<uint32_t> gc;
-    TRY(gk.alloc(ctx, ecap));
-    TRY(gc.zero(ctx, ecap));
-    TRY_HIP_(hipMemsetAsync(gk.p, 0xff, ecap * sizeof(uint64_t), st));
+    MR_TRY(gk.alloc(ctx, ecap));
+    MR_TRY(gc.zero(ctx, ecap));
+    MR_TRY_HIP(ctx, hipMemsetAsync(gk.p, 0xff, ecap * sizeof(uint64_t), st));
     const int use_lds = NP <= LDS_HIST;
     const size_t lds = use_lds ? 2 * (size_t)NP * sizeof(int32_t) : 0;
     if (Ssel)
         hipLaunchKernelGGL(k_rows, dim3(cdiv(Ssel, BT * 8)), dim3(BT), lds, st, rows.p, Ssel, sp->trace.p, sp->podop.p,
                            sp->parent.p, selflag.p, sp->id_off.p, sp->id_rows.p, sp->n_span_codes, NP, use_lds, tcnt.p,
                            ocnt.p, ofirst.p, gk.p, gc.p, ecap - 1);
-    // edges
-    DBuf<int32_t> eflag, is_par, nchild_code;
-    DBuf<int64_t> epos, etmp;
-    TRY(eflag.alloc(ctx, ecap));
-    TRY(epos.alloc(ctx, ecap + 1));
-    TRY(etmp.alloc(ctx, scan_tmp_elems(ecap)));
-    TRY(is_par.zero(ctx, NP));
-    TRY(nchild_code.zero(ctx, NP));
-    hipLaunchKernelGGL(k_edge_flags, dim3(cdiv(ecap, 256)), dim3(256), 0, st, gk.p, (int64_t)ecap, eflag.p);
-    TRY(mr_exclusive_scan_i32(ctx, eflag.p, epos.p, ecap, etmp.p));
-    int64_t E = 0;
-    TRY(read_i64(ctx, epos.p + ecap, &E));
-    DBuf<uint64_t> ekey;
-    DBuf<uint32_t> ecnt;
-    TRY(ekey.alloc(ctx, E));
-    TRY(ecnt.alloc(ctx, E));
-    hipLaunchKernelGGL(k_edge_compact, dim3(cdiv(ecap, 256)), dim3(256), 0, st, gk.p, gc.p, eflag.p, epos.p,
-                       (int64_t)ecap, ekey.p, ecnt.p, is_par.p, nchild_code.p);
-    // 3. node order
-    DBuf<int32_t> pflag, qflag, node_of_code;
-    DBuf<int64_t> ppos, qpos;
-    TRY(pflag.alloc(ctx, NP));
-    TRY(qflag.alloc(ctx, NP));
-    TRY(ppos.alloc(ctx, NP + 1));
-    TRY(qpos.alloc(ctx, NP + 1));
-    TRY(node_of_code.alloc(ctx, NP));
-    if (NP) hipLaunchKernelGGL(k_node_flags, dim3(cdiv(NP, 256)), dim3(256), 0, st, ocnt.p, is_par.p, NP, pflag.p, qflag.p);
-    TRY(mr_exclusive_scan_i32(ctx, pflag.p, ppos.p, NP, tmp.p));
-    TRY(mr_exclusive_scan_i32(ctx, qflag.p, qpos.p, NP, tmp.p));
-    int64_t P = 0, Q = 0;
-    TRY(read_i64(ctx, ppos.p + NP, &P));
-    TRY(read_i64(ctx, qpos.p + NP, &Q));
-    const int32_t N = (int32_t)(P + Q);
-    TRY(g->node_podop.alloc(ctx, N));
-    DBuf<uint64_t> qkey;
-    DBuf<uint32_t> qval;
-    TRY(qkey.alloc(ctx, Q));
-    TRY(qval.alloc(ctx, Q));
-    if (NP)
-        hipLaunchKernelGGL(k_node_parents, dim3(cdiv(NP, 256)), dim3(256), 0, st, pflag.p, ppos.p, qflag.p, qpos.p,
-                           ofirst.p, NP, node_of_code.p, g->node_podop.p, qkey.p, qval.p);
-    SortScratch ws;
-    TRY(mr_radix_sort(ctx, qkey.p, qval.p, Q, bits_for((uint64_t)std::max<int64_t>(Ssel, 1)), ws));
-    if (Q)
-        hipLaunchKernelGGL(k_node_rest, dim3(cdiv(Q, 256)), dim3(256), 0, st, qval.p, Q, (int32_t)P, node_of_code.p,
-                           g->node_podop.p);
+    // 3. edges, node order, per-node arrays, P_ss
+    DBuf<int32_t> node_of_code;
+    MR_TRY(build_nodes(ctx, g, NP, ocnt.p, ofirst.p, bits_for((uint64_t)std::max<int64_t>(Ssel, 1)), gk.p, gc.p, ecap,
+                       node_of_code));
+    const int32_t N = g->N;
     // traces
     DBuf<int32_t> tflag, tidx_of_code;
     DBuf<int64_t> tpos;
-    TRY(tflag.alloc(ctx, NT));
-    TRY(tpos.alloc(ctx, NT + 1));
-    TRY(tidx_of_code.alloc(ctx, NT));
+    MR_TRY(tflag.alloc(ctx, NT));
+    MR_TRY(tpos.alloc(ctx, NT + 1));
+    MR_TRY(tidx_of_code.alloc(ctx, NT));
     if (NT) hipLaunchKernelGGL(k_trace_flags, dim3(cdiv(NT, 256)), dim3(256), 0, st, tcnt.p, NT, tflag.p);
-    TRY(mr_exclusive_scan_i32(ctx, tflag.p, tpos.p, NT, tmp.p));
+    MR_TRY(mr_exclusive_scan_i32(ctx, tflag.p, tpos.p, NT, tmp.p));
     int64_t T64 = 0;
-    TRY(read_i64(ctx, tpos.p + NT, &T64));
+    MR_TRY(read_i64(ctx, tpos.p + NT, &T64));
     const int32_t T = (int32_t)T64;
-    TRY(g->trace_code.alloc(ctx, T));
-    TRY(g->len_t.alloc(ctx, T));
+    MR_TRY(g->trace_code.alloc(ctx, T));
+    MR_TRY(g->len_t.alloc(ctx, T));
     if (NT)
         hipLaunchKernelGGL(k_trace_index, dim3(cdiv(NT, 256)), dim3(256), 0, st, tflag.p, tpos.p, tcnt.p, NT,
                            tidx_of_code.p, g->trace_code.p, g->len_t.p);
-    // 4. pairs -> CSR, CSC
+    // 4. pairs -> trace-major CSR
     const int nb = std::max(1, bits_for((uint64_t)std::max(N - 1, 0)));
     DBuf<uint64_t> keys;
-    TRY(keys.alloc(ctx, Ssel));
+    MR_TRY(keys.alloc(ctx, Ssel));
     if (Ssel)
         hipLaunchKernelGGL(k_pair_keys, dim3(cdiv(Ssel, 256)), dim3(256), 0, st, rows.p, Ssel, sp->trace.p, sp->podop.p,
                            tidx_of_code.p, node_of_code.p, nb, keys.p);
-    TRY(mr_radix_sort(ctx, keys.p, nullptr, Ssel, nb + bits_for((uint64_t)std::max(T - 1, 0)), ws));
+    SortScratch ws;
+    MR_TRY(mr_radix_sort(ctx, keys.p, nullptr, Ssel, nb + bits_for((uint64_t)std::max(T - 1, 0)), ws));
     DBuf<int32_t> head;
     DBuf<int64_t> hpos;
-    TRY(head.alloc(ctx, Ssel));
-    TRY(hpos.alloc(ctx, Ssel + 1));
+    MR_TRY(head.alloc(ctx, Ssel));
+    MR_TRY(hpos.alloc(ctx, Ssel + 1));
     if (Ssel) hipLaunchKernelGGL(k_run_heads, dim3(cdiv(Ssel, 256)), dim3(256), 0, st, keys.p, Ssel, head.p);
-    TRY(mr_exclusive_scan_i32(ctx, head.p, hpos.p, Ssel, tmp.p));
+    MR_TRY(mr_exclusive_scan_i32(ctx, head.p, hpos.p, Ssel, tmp.p));
     int64_t nnz = 0;
-    TRY(read_i64(ctx, hpos.p + Ssel, &nnz));
-    TRY(g->rs_ops.alloc(ctx, nnz));
-    TRY(g->rs_off.alloc(ctx, T + 1));
+    MR_TRY(read_i64(ctx, hpos.p + Ssel, &nnz));
+    MR_TRY(g->rs_ops.alloc(ctx, nnz));
+    MR_TRY(g->rs_off.alloc(ctx, T + 1));
     if (Ssel)
         hipLaunchKernelGGL(k_pairs_out, dim3(cdiv(Ssel, 256)), dim3(256), 0, st, keys.p, head.p, hpos.p, Ssel, nb,
                            g->rs_off.p, g->rs_ops.p);
     hipLaunchKernelGGL(k_set_last, dim3(1), dim3(1), 0, st, g->rs_off.p, T, nnz);
-    DBuf<int64_t> ntmp;
-    TRY(ntmp.alloc(ctx, scan_tmp_elems(std::max(N, 1))));
-    // per-node arrays and P_ss
-    TRY(g->len_o.alloc(ctx, N));
-    TRY(g->nchild.alloc(ctx, N));
-    if (N)
-        hipLaunchKernelGGL(k_node_arrays, dim3(cdiv(N, 256)), dim3(256), 0, st, g->node_podop.p, N, ocnt.p,
-                           nchild_code.p, g->len_o.p, g->nchild.p);
-    DBuf<uint64_t> skey;
-    TRY(skey.alloc(ctx, E));
-    if (E) hipLaunchKernelGGL(k_edge_nodes, dim3(cdiv(E, 256)), dim3(256), 0, st, ekey.p, E, node_of_code.p, nb, skey.p);
-    TRY(mr_radix_sort(ctx, skey.p, nullptr, E, 2 * nb, ws));
-    DBuf<int32_t> ccount;
-    TRY(ccount.zero(ctx, N));
-    TRY(g->ss_par.alloc(ctx, E));
-    TRY(g->ss_off.alloc(ctx, N + 1));
-    if (E) hipLaunchKernelGGL(k_edge_csr, dim3(cdiv(E, 256)), dim3(256), 0, st, skey.p, E, nb, g->ss_par.p, ccount.p);
-    TRY(mr_exclusive_scan_i32(ctx, ccount.p, g->ss_off.p, N, ntmp.p));
-    TRY_HIP_(hipGetLastError());
-    g->N = N;
+    MR_TRY_HIP(ctx, hipGetLastError());
     g->T = T;
     g->nnz_sr = g->nnz_rs = nnz;
-    g->E = E;
-    g->rs_is_sr = true;
-    g->pr_identity = true;
-    g->n_pr = T;
-    TRY(mr_graph_prepare(ctx, g));
-#undef TRY
-#undef TRY_HIP_
+    return MR_OK;
+}
+
+// Indexed build (mr_span_index.hip): whole traces selected by the mask; every per-row fact comes
+// from the per-trace index, so no row is sorted.  Each trace's op list is written in pod-op code
+// order (a fixed order for the kind keys; mr_graph_export sorts by node id for inspection).
+static int graph_build_indexed(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d_mask, mr_graph* g) {
+    hipStream_t st = ctx->stream;
+    const int32_t NT = sp->n_traces, NP = sp->n_podops;
+    DBuf<int32_t> tflag, zc;
+    DBuf<int64_t> tpos, zoff, tmp;
+    MR_TRY(tflag.alloc(ctx, NT));
+    MR_TRY(zc.alloc(ctx, NT));
+    MR_TRY(tpos.alloc(ctx, NT + 1));
+    MR_TRY(zoff.alloc(ctx, NT + 1));
+    MR_TRY(tmp.alloc(ctx, std::max<int64_t>({scan_tmp_elems(NT), scan_tmp_elems(NP), 1})));
+    DBuf<int32_t> ocnt, ofirst;
+    MR_TRY(ocnt.zero(ctx, NP));
+    MR_TRY(ofirst.alloc(ctx, NP));
+    if (NP) MR_TRY_HIP(ctx, hipMemsetAsync(ofirst.p, 0x7f, NP * sizeof(int32_t), st));
+    const uint64_t ecap = edge_capacity(sp->n_ed + sp->n_xj, NP);
+    DBuf<uint64_t> gk;
+    DBuf<uint32_t> gc;
+    MR_TRY(gk.alloc(ctx, ecap));
+    MR_TRY(gc.zero(ctx, ecap));
+    MR_TRY_HIP(ctx, hipMemsetAsync(gk.p, 0xff, ecap * sizeof(uint64_t), st));
+    if (NT) {
+        hipLaunchKernelGGL(k_ix_sel, dim3(cdiv(NT, 256)), dim3(256), 0, st, d_mask, sp->tlen.p, sp->po_off.p, NT, tflag.p,
+                           zc.p);
+        const int use_lds = NP <= LDS_HIST;
+        const size_t lds = use_lds ? 2 * (size_t)NP * sizeof(int32_t) : 0;
+        const int nblk = std::max(1, std::min(1024, cdiv(std::max(sp->n_po, sp->n_ed), BT * IX_EPT)));
+        hipLaunchKernelGGL(k_ix_stats, dim3(nblk), dim3(BT), lds, st, tflag.p, sp->n_po, sp->po_tr.p, sp->po_op.p,
+                           sp->po_cnt.p, sp->po_first.p, sp->n_ed, sp->ed_tr.p, sp->ed_key.p, sp->ed_cnt.p, NP, use_lds,
+                           ocnt.p, ofirst.p, gk.p, gc.p, ecap - 1);
+    }
+    if (sp->n_xj)
+        hipLaunchKernelGGL(k_ix_cross, dim3(cdiv(sp->n_xj, 256)), dim3(256), 0, st, d_mask, sp->xj_tc.p, sp->xj_tp.p,
+                           sp->xj_key.p, sp->n_xj, gk.p, gc.p, ecap - 1);
+    MR_TRY(mr_exclusive_scan_i32(ctx, tflag.p, tpos.p, NT, tmp.p));
+    MR_TRY(mr_exclusive_scan_i32(ctx, zc.p, zoff.p, NT, tmp.p));
+    DBuf<int32_t> node_of_code;
+    MR_TRY(build_nodes(ctx, g, NP, ocnt.p, ofirst.p, bits_for((uint64_t)std::max<int64_t>(sp->S, 1)), gk.p, gc.p, ecap,
+                       node_of_code));
+    int64_t h[2] = {0, 0};   // T, nnz (their scans ran before build_nodes' syncs)
+    MR_TRY_HIP(ctx, hipMemcpyAsync(&h[0], tpos.p + NT, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    MR_TRY_HIP(ctx, hipMemcpyAsync(&h[1], zoff.p + NT, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+    const int32_t T = (int32_t)h[0];
+    const int64_t nnz = h[1];
+    MR_TRY(g->trace_code.alloc(ctx, T));
+    MR_TRY(g->len_t.alloc(ctx, T));
+    MR_TRY(g->rs_ops.alloc(ctx, nnz));
+    MR_TRY(g->rs_off.alloc(ctx, T + 1));
+    if (NT)
+        hipLaunchKernelGGL(k_ix_trace_rows, dim3(cdiv(NT, 256)), dim3(256), 0, st, tflag.p, tpos.p, zoff.p, NT, sp->tlen.p,
+                           g->trace_code.p, g->len_t.p, g->rs_off.p);
+    if (sp->n_po)
+        hipLaunchKernelGGL(k_ix_trace_ops, dim3(cdiv(sp->n_po, 256)), dim3(256), 0, st, tflag.p, zoff.p, sp->n_po,
+                           sp->po_tr.p, sp->po_off.p, sp->po_op.p, node_of_code.p, g->rs_ops.p);
+    hipLaunchKernelGGL(k_set_last, dim3(1), dim3(1), 0, st, g->rs_off.p, T, nnz);
+    MR_TRY_HIP(ctx, hipGetLastError());
+    g->T = T;
+    g->nnz_sr = g->nnz_rs = nnz;
+    return MR_OK;
+}
+
+// win (nullable): [t0, t1] restricts rows to the time window on the row-level path; the indexed
+// path is taken only when the window selects whole traces (uniform trace times) or is absent.
+int mr_graph_build_dev(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d_mask, mr_graph** out, const int64_t* win) {
+    auto g = new mr_graph();
+    g->ctx = ctx;
+    static const bool no_index = getenv("MR_NO_INDEX") != nullptr;   // A/B knob: force the row-level path
+    const bool indexed = sp->indexed && !no_index && (!win || sp->uniform_times);
+    int rc = indexed ? graph_build_indexed(ctx, sp, d_mask, g) : graph_build_rows(ctx, sp, d_mask, win, g);
+    if (rc == MR_OK) {
+        g->rs_is_sr = true;
+        g->pr_identity = true;
+        g->n_pr = g->T;
+        rc = mr_graph_prepare(ctx, g);
+    }
+    if (rc != MR_OK) {
+        delete g;
+        return rc;
+    }
     *out = g;
     return MR_OK;
 }
@@ -501,7 +726,7 @@ extern "C" int mr_graph_build(mr_ctx* ctx, const mr_spans* sp, const uint8_t* tr
     MR_TRY_HIP(ctx, hipSetDevice(ctx->device));
     DBuf<uint8_t> mask;
     MR_TRY(mask.upload(ctx, trace_mask, (size_t)sp->n_traces));
-    return mr_graph_build_dev(ctx, sp, mask.p, out);
+    return mr_graph_build_dev(ctx, sp, mask.p, out, nullptr);
 }
 
 extern "C" int mr_graph_nodes(const mr_graph* g, int32_t* node_podop, int32_t* trace_code) {
@@ -520,6 +745,12 @@ extern "C" int mr_graph_export(const mr_graph* g, int64_t* sr_off, int32_t* sr_o
     mr_ctx* ctx = g->ctx;
     if (sr_off) MR_TRY(g->rs_off.download(ctx, sr_off, (size_t)g->T + 1));
     if (sr_ops) MR_TRY(g->rs_ops.download(ctx, sr_ops, (size_t)g->nnz_rs));
+    if (sr_ops) {   // op lists in node order (the indexed build keeps pod-op code order)
+        std::vector<int64_t> off((size_t)g->T + 1);
+        MR_TRY(g->rs_off.download(ctx, off.data(), off.size()));
+        MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        for (int32_t t = 0; t < g->T; ++t) std::sort(sr_ops + off[t], sr_ops + off[t + 1]);
+    }
     if (len_t) MR_TRY(g->len_t.download(ctx, len_t, (size_t)g->T));
     if (len_o) MR_TRY(g->len_o.download(ctx, len_o, (size_t)g->N));
     if (ss_off) MR_TRY(g->ss_off.download(ctx, ss_off, (size_t)g->N + 1));

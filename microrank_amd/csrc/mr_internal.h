@@ -171,7 +171,25 @@ struct mr_spans {
     int64_t n_span_codes = 0;
     DBuf<int64_t> id_off;   // [n_span_codes+1]
     DBuf<int32_t> id_rows;  // [S]
+    // Per-trace index (mr_span_index.hip), built once at upload: everything a window needs from
+    // a trace, so detector and graph builds of a window are per-trace gathers with no row sort.
+    bool indexed = false;        // index built (key bits fit)
+    bool uniform_times = false;  // tstart/tend constant within every trace (window = trace set)
+    DBuf<int32_t> tlen;                  // [NT] rows of the trace
+    DBuf<long long> tmaxd, tts, tte;     // [NT] max duration, trace-level start / end
+    int64_t n_po = 0, n_sv = 0, n_ed = 0, n_xj = 0;
+    DBuf<int64_t> po_off;                // [NT+1] distinct pod-ops of a trace (code order) ...
+    DBuf<int32_t> po_op, po_cnt, po_first, po_tr;   // ... with span count, first row and trace
+    DBuf<int64_t> sv_off;                // [NT+1] distinct service-ops of a trace (code order) ...
+    DBuf<int32_t> sv_op, sv_cnt;         // ... with span count
+    DBuf<int64_t> ed_off;                // [NT+1] distinct (parent pod-op, child pod-op) join keys
+    DBuf<uint64_t> ed_key;               //        inside the trace, (parent << 32 | child) ...
+    DBuf<int32_t> ed_cnt, ed_tr;         // ... with multiplicity and trace
+    DBuf<int32_t> xj_tc, xj_tp;          // [n_xj] join pairs across traces (T11): child / parent trace
+    DBuf<uint64_t> xj_key;               //        and key
 };
+
+int mr_spans_index(mr_ctx* ctx, mr_spans* s);
 
 // Launch helpers
 inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }

@@ -79,8 +79,55 @@ __global__ void __launch_bounds__(SCAN_T) k_scan_tiles(const In* in, int64_t* ou
     }
 }
 
+// small n: one launch, one 1024-thread block walking tiles of 8192 with a running carry
+constexpr int SS_T = 1024, SS_I = 8;
+constexpr int64_t SCAN_SINGLE_MAX = 2 * SS_T * SS_I;
+template <class In>
+__global__ void __launch_bounds__(SS_T) k_scan_single(const In* in, int64_t* out, int64_t n) {
+    __shared__ int64_t wsum[SS_T / WAVE];
+    const int tid = threadIdx.x, lane = tid & (WAVE - 1), w = tid / WAVE;
+    int64_t carry = 0;
+    for (int64_t base = 0; base < n; base += (int64_t)SS_T * SS_I) {
+        int64_t v[SS_I], s = 0;
+#pragma unroll
+        for (int j = 0; j < SS_I; ++j) {
+            const int64_t idx = base + (int64_t)tid * SS_I + j;
+            v[j] = idx < n ? (int64_t)in[idx] : 0;
+            s += v[j];
+        }
+        int64_t inc = s;   // inclusive scan over the wave
+#pragma unroll
+        for (int off = 1; off < WAVE; off <<= 1) {
+            const int64_t o = __shfl_up(inc, off, WAVE);
+            if (lane >= off) inc += o;
+        }
+        if (lane == WAVE - 1) wsum[w] = inc;
+        __syncthreads();
+        int64_t wpre = 0, tot = 0;
+        for (int k = 0; k < SS_T / WAVE; ++k) {
+            if (k < w) wpre += wsum[k];
+            tot += wsum[k];
+        }
+        int64_t run = carry + wpre + inc - s;
+#pragma unroll
+        for (int j = 0; j < SS_I; ++j) {
+            const int64_t idx = base + (int64_t)tid * SS_I + j;
+            if (idx < n) out[idx] = run;
+            run += v[j];
+        }
+        carry += tot;
+        __syncthreads();   // wsum reused by the next tile
+    }
+    if (tid == 0) out[n] = carry;
+}
+
 template <class In>
 int scan_impl(mr_ctx* ctx, const In* in, int64_t* out, int64_t n, int64_t* tmp) {
+    if (n > 0 && n <= SCAN_SINGLE_MAX) {
+        hipLaunchKernelGGL(k_scan_single<In>, dim3(1), dim3(SS_T), 0, ctx->stream, in, out, n);
+        MR_TRY_HIP(ctx, hipGetLastError());
+        return MR_OK;
+    }
     int64_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
     if (nb == 0) {
         MR_TRY_HIP(ctx, hipMemsetAsync(out, 0, sizeof(int64_t), ctx->stream));

@@ -81,10 +81,69 @@ __global__ void k_copy_u32(const uint32_t* a, uint32_t* b, int64_t n) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) b[i] = a[i];
 }
+// small n: one launch, one block; bitonic sort in LDS of (masked key, position) pairs, so equal
+// keys keep their input order (stable, like the radix path)
+constexpr int SL_MAX = 4096, SL_T = 1024;
+__global__ void __launch_bounds__(SL_T) k_sort_lds(uint64_t* keys, uint32_t* vals, int32_t n, uint64_t mask) {
+    __shared__ uint64_t sk[SL_MAX];
+    __shared__ uint32_t sp[SL_MAX];
+    int32_t m = 1;
+    while (m < n) m <<= 1;
+    for (int32_t i = threadIdx.x; i < m; i += SL_T) {
+        sk[i] = i < n ? (keys[i] & mask) : ~0ull;
+        sp[i] = (uint32_t)i;
+    }
+    __syncthreads();
+    for (int32_t k = 2; k <= m; k <<= 1) {
+        for (int32_t j = k >> 1; j > 0; j >>= 1) {
+            for (int32_t i = threadIdx.x; i < m; i += SL_T) {
+                const int32_t l = i ^ j;
+                if (l > i) {
+                    const uint64_t a = sk[i], b = sk[l];
+                    const uint32_t pa = sp[i], pb = sp[l];
+                    const bool gt = a > b || (a == b && pa > pb);
+                    if (((i & k) == 0) == gt) {   // ascending in the lower half of each k-run
+                        sk[i] = b;
+                        sk[l] = a;
+                        sp[i] = pb;
+                        sp[l] = pa;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    // gather the originals in sorted order (keys keep their unmasked bits)
+    uint64_t ok[SL_MAX / SL_T];
+    uint32_t ov[SL_MAX / SL_T];
+#pragma unroll
+    for (int r = 0; r < SL_MAX / SL_T; ++r) {
+        const int32_t i = threadIdx.x + r * SL_T;
+        if (i < n) {
+            ok[r] = keys[sp[i]];
+            if (vals) ov[r] = vals[sp[i]];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < SL_MAX / SL_T; ++r) {
+        const int32_t i = threadIdx.x + r * SL_T;
+        if (i < n) {
+            keys[i] = ok[r];
+            if (vals) vals[i] = ov[r];
+        }
+    }
+}
 }  // namespace
 
 int mr_radix_sort(mr_ctx* ctx, uint64_t* keys, uint32_t* vals, int64_t n, int bits, SortScratch& ws) {
     if (n <= 1 || bits <= 0) return MR_OK;
+    if (n <= SL_MAX) {
+        const uint64_t mask = bits >= 64 ? ~0ull : ((1ull << bits) - 1ull);
+        hipLaunchKernelGGL(k_sort_lds, dim3(1), dim3(SL_T), 0, ctx->stream, keys, vals, (int32_t)n, mask);
+        MR_TRY_HIP(ctx, hipGetLastError());
+        return MR_OK;
+    }
     const int64_t nb = (n + RTILE - 1) / RTILE;
     MR_TRY(ws.k2.alloc(ctx, (size_t)n));
     if (vals) MR_TRY(ws.v2.alloc(ctx, (size_t)n));

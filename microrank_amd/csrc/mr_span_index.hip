@@ -1,0 +1,394 @@
+// Per-trace index of an uploaded span table, built once per table (mr_spans_upload) so that the
+// per-window work of online_rca.online_anomaly_detect_RCA (online_rca.py:164-215) never sorts
+// span rows again.  From one stable sort of the rows by (trace, code) it keeps, per trace:
+//   * distinct pod-ops (podName_operationName, preprocess_data.py:151-155) with span count and
+//     first row -> len_o, trace_num_list, node order and the trace-major incidence of
+//     get_pagerank_graph (:146-171) for any trace subset;
+//   * distinct service-ops with span count -> the detector's expect sum in name order
+//     (anormaly_detector.py:56-67, preprocess_data.py:97-122);
+//   * the parent join ParentSpanId == spanID (:157-159) resolved once: distinct (parent op,
+//     child op) keys with multiplicity for pairs inside the trace, and the rare pairs whose
+//     rows lie in different traces (T11) kept as a flat list;
+//   * span count, max duration, trace-level start/end, and whether start/end are constant over
+//     the trace's rows (then a time window selects whole traces and the window detector is a
+//     per-trace pass; otherwise the row-level path runs).
+// The index is a derived view of the uploaded columns: no result depends on it being present.
+#include <algorithm>
+#include <climits>
+
+#include "mr_prim.h"
+#include "mr_sort.h"
+
+namespace {
+constexpr int XB = 256;
+
+__global__ void k_ix_keys(const int32_t* trace, const int32_t* code, int64_t S, int nbc, uint64_t* key, uint32_t* val) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= S) return;
+    key[i] = ((uint64_t)(uint32_t)trace[i] << nbc) | (uint32_t)code[i];
+    val[i] = (uint32_t)i;
+}
+__global__ void k_ix_heads(const uint64_t* key, int64_t n, int32_t* head) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) head[i] = (i == 0 || key[i] != key[i - 1]) ? 1 : 0;
+}
+// run r = (trace, code): code, first row (stable sort: the smallest), start position; one
+// per-trace run count for the trace offsets
+__global__ void k_ix_runs(const uint64_t* key, const uint32_t* val, const int32_t* head, const int64_t* hpos, int64_t n,
+                          int nbc, int32_t* r_code, int32_t* r_first, int32_t* r_tr, int64_t* r_start, int32_t* truns) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || !head[i]) return;
+    const int64_t r = hpos[i];
+    const uint64_t k = key[i];
+    const int32_t t = (int32_t)(k >> nbc);
+    r_code[r] = (int32_t)(k & ((1ull << nbc) - 1ull));
+    if (r_first) r_first[r] = (int32_t)val[i];
+    if (r_tr) r_tr[r] = t;
+    r_start[r] = i;
+    atomicAdd(&truns[t], 1);
+}
+__global__ void k_ix_cnt(const int64_t* r_start, int64_t R, int64_t n, int32_t* r_cnt) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < R) r_cnt[r] = (int32_t)((r + 1 < R ? r_start[r + 1] : n) - r_start[r]);
+}
+// per-trace scalars: rows, max duration, min/max of trace-level start and end
+// (rows of a trace are mostly adjacent: lanes of one trace are combined over the wave first and
+// the run's last lane alone updates the trace; runs of one trace split over waves merge exactly)
+__global__ void k_ix_trace_stats(const int32_t* trace, const int64_t* dur, const int64_t* ts, const int64_t* te, int64_t S,
+                                 int32_t* tlen, long long* tmaxd, long long* tsmin, long long* tsmax, long long* temin,
+                                 long long* temax) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool in = i < S;
+    const int32_t t = in ? trace[i] : -1;
+    int32_t n = in ? 1 : 0;
+    long long md = in ? (long long)dur[i] : LLONG_MIN;
+    long long s0 = in && ts ? (long long)ts[i] : LLONG_MAX, s1 = in && ts ? (long long)ts[i] : LLONG_MIN;
+    long long e0 = in && ts ? (long long)te[i] : LLONG_MAX, e1 = in && ts ? (long long)te[i] : LLONG_MIN;
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {   // inclusive segmented scan over runs of equal t
+        const int32_t to = __shfl_up(t, off, 64);
+        const int32_t no = __shfl_up(n, off, 64);
+        const long long mo = __shfl_up(md, off, 64), a0 = __shfl_up(s0, off, 64), a1 = __shfl_up(s1, off, 64),
+                        b0 = __shfl_up(e0, off, 64), b1 = __shfl_up(e1, off, 64);
+        if (lane >= off && to == t) {
+            n += no;
+            md = max(md, mo);
+            s0 = min(s0, a0);
+            s1 = max(s1, a1);
+            e0 = min(e0, b0);
+            e1 = max(e1, b1);
+        }
+    }
+    const int32_t tn = __shfl_down(t, 1, 64);
+    if (!in || (lane != 63 && tn == t)) return;
+    atomicAdd(&tlen[t], n);
+    atomicMax(&tmaxd[t], md);
+    if (ts) {
+        atomicMin(&tsmin[t], s0);
+        atomicMax(&tsmax[t], s1);
+        atomicMin(&temin[t], e0);
+        atomicMax(&temax[t], e1);
+    }
+}
+__global__ void k_ix_uniform(const int32_t* tlen, const long long* tsmin, const long long* tsmax, const long long* temin,
+                             const long long* temax, int32_t NT, int32_t* bad) {
+    const int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < NT && tlen[t] > 0 && (tsmin[t] != tsmax[t] || temin[t] != temax[t])) atomicOr(bad, 1);
+}
+// parent join, pass 1: number of internal / cross-trace (child row, parent row) pairs per row
+__global__ void k_ix_join_count(const int32_t* trace, const int64_t* parent, int64_t S, const int64_t* id_off,
+                                const int32_t* id_rows, int64_t n_codes, int32_t* nin, int32_t* nx) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= S) return;
+    int32_t a = 0, b = 0;
+    const int64_t p = parent[c];
+    if (p >= 0 && p < n_codes) {
+        const int32_t tc = trace[c];
+        for (int64_t e = id_off[p]; e < id_off[p + 1]; ++e) {
+            if (trace[id_rows[e]] == tc) ++a; else ++b;
+        }
+    }
+    nin[c] = a;
+    nx[c] = b;
+}
+// pass 2: internal pairs as sort keys (trace, parent op, child op); cross pairs listed
+__global__ void k_ix_join_fill(const int32_t* trace, const int32_t* podop, const int64_t* parent, int64_t S,
+                               const int64_t* id_off, const int32_t* id_rows, int64_t n_codes, const int64_t* pin,
+                               const int64_t* px, int nbp, uint64_t* ikey, int32_t* xtc, int32_t* xtp, uint64_t* xkey) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= S) return;
+    const int64_t p = parent[c];
+    if (p < 0 || p >= n_codes) return;
+    const int32_t tc = trace[c];
+    const uint32_t oc = (uint32_t)podop[c];
+    int64_t a = pin[c], b = px[c];
+    for (int64_t e = id_off[p]; e < id_off[p + 1]; ++e) {
+        const int32_t j = id_rows[e];
+        const uint32_t op = (uint32_t)podop[j];
+        if (trace[j] == tc) {
+            ikey[a++] = ((uint64_t)(uint32_t)tc << (2 * nbp)) | ((uint64_t)op << nbp) | oc;
+        } else {
+            xtc[b] = tc;
+            xtp[b] = trace[j];
+            xkey[b] = ((uint64_t)op << 32) | oc;
+            ++b;
+        }
+    }
+}
+__global__ void k_ix_edge_runs(const uint64_t* key, const int32_t* head, const int64_t* hpos, int64_t n, int nbp,
+                               uint64_t* ed_key, int32_t* ed_tr, int64_t* r_start, int32_t* truns) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || !head[i]) return;
+    const int64_t r = hpos[i];
+    const uint64_t k = key[i];
+    const uint64_t m = (1ull << nbp) - 1ull;
+    const int32_t t = (int32_t)(k >> (2 * nbp));
+    ed_key[r] = (((k >> nbp) & m) << 32) | (k & m);
+    ed_tr[r] = t;
+    r_start[r] = i;
+    atomicAdd(&truns[t], 1);
+}
+
+// ---------------------------------------------------------------- window detector (uniform times)
+// anormaly_detector.system_anomaly_detect on whole traces: in window iff the trace-level
+// [start, end] lies in [t0, t1] (T15); expect = sum over the trace's service-ops in name order of
+// count * (mean + 3 std) (sequential, no FMA: T14); abnormal iff max duration / 1000 > expect.
+constexpr int DB = 256, DCAP = 16;   // detector: traces per block, staged entries per thread
+constexpr int CSH = 64;              // counter shards
+__global__ void __launch_bounds__(DB) k_ix_detect(int32_t NT, const int32_t* tlen, const long long* tts,
+                                                  const long long* tte, const long long* tmaxd, const int64_t* sv_off,
+                                                  const int32_t* sv_op, const int32_t* sv_cnt, const double* a3,
+                                                  const uint8_t* a3v, int64_t t0, int64_t t1, uint8_t* state,
+                                                  unsigned long long* counts) {
+    __shared__ double term[DB * DCAP];
+    const int32_t tb = blockIdx.x * DB, te_ = min(tb + DB, NT);
+    const int32_t t = tb + threadIdx.x;
+    const int64_t r0 = sv_off[tb], r1 = sv_off[te_];
+    const bool fits = r1 - r0 <= (int64_t)DB * DCAP;
+    // the block's (count * (mean + 3 std)) terms, entry-parallel: one product per entry as the
+    // reference rounds it; ops without an SLO contribute +0.0 (an exact no-op on the sum)
+    if (fits) {   // all loads of a thread in flight together: ids and counts, then the SLO gathers
+        int32_t op[DCAP], cn[DCAP];
+#pragma unroll
+        for (int j = 0; j < DCAP; ++j) {
+            const int64_t r = min(r0 + threadIdx.x + (int64_t)j * DB, max(r1 - 1, r0));
+            op[j] = sv_op[r];
+            cn[j] = sv_cnt[r];
+        }
+        double av[DCAP];
+        uint8_t vv[DCAP];
+#pragma unroll
+        for (int j = 0; j < DCAP; ++j) {
+            av[j] = a3[op[j]];
+            vv[j] = a3v[op[j]];
+        }
+#pragma unroll
+        for (int j = 0; j < DCAP; ++j) {
+            const int64_t r = r0 + threadIdx.x + (int64_t)j * DB;
+            if (r < r1) term[r - r0] = vv[j] ? (double)cn[j] * av[j] : 0.0;
+        }
+    }
+    __syncthreads();
+    int st = 0;
+    int64_t rows = 0;
+    if (t < NT) {
+        const bool in = tlen[t] > 0 && tts[t] >= t0 && tte[t] <= t1;
+        if (in) {
+            rows = tlen[t];
+            const long long mx = tmaxd[t];
+            if (mx > 0) {   // grouped[grouped['duration'] > 0] (preprocess_data.py:117)
+                double expect = 0.0;
+                const int64_t a = sv_off[t], b = sv_off[t + 1];
+                if (fits) {
+                    for (int64_t r = a; r < b; ++r) expect += term[r - r0];   // name order (T14)
+                } else {
+                    for (int64_t r = a; r < b; ++r) {
+                        const int32_t op = sv_op[r];
+                        if (a3v[op]) expect += (double)sv_cnt[r] * a3[op];   // anormaly_detector.py:64-65
+                    }
+                }
+                st = (double)mx / 1000.0 > expect ? 2 : 1;                   // :58, :69
+            }
+        }
+        state[t] = (uint8_t)st;
+    }
+    // counts: per wave, per block, then one add per block into one of CSH shards (~200k traces
+    // on three same-address counters had cost ~0.1 ms of serialised atomics)
+    __shared__ unsigned long long bc[3][DB / 64];
+    const uint64_t ab = __ballot(st == 2), nr = __ballot(st == 1);
+    int64_t rw = rows;
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) rw += __shfl_xor(rw, m, 64);
+    const int w = threadIdx.x / 64;
+    if ((threadIdx.x & 63) == 0) {
+        bc[0][w] = (unsigned long long)__popcll(ab);
+        bc[1][w] = (unsigned long long)__popcll(nr);
+        bc[2][w] = (unsigned long long)rw;
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        unsigned long long v = 0;
+        for (int k = 0; k < DB / 64; ++k) v += bc[threadIdx.x][k];
+        if (v) atomicAdd(&counts[(size_t)(blockIdx.x % CSH) * 3 + threadIdx.x], v);
+    }
+}
+}  // namespace
+
+// (trace, code) runs of the rows: offsets per trace, code, count and (optionally) first row
+static int trace_runs(mr_ctx* ctx, const mr_spans* s, const int32_t* code, int32_t n_codes, DBuf<int64_t>& off,
+                      DBuf<int32_t>& r_code, DBuf<int32_t>& r_cnt, DBuf<int32_t>* r_first, DBuf<int32_t>* r_tr,
+                      int64_t* n_runs) {
+    hipStream_t st = ctx->stream;
+    const int64_t S = s->S;
+    const int32_t NT = s->n_traces;
+    const int nbc = std::max(1, bits_for((uint64_t)std::max(n_codes - 1, 0)));
+    DBuf<uint64_t> key;
+    DBuf<uint32_t> val;
+    DBuf<int32_t> head, truns;
+    DBuf<int64_t> hpos, tmp, r_start;
+    MR_TRY(key.alloc(ctx, S));
+    MR_TRY(val.alloc(ctx, S));
+    MR_TRY(head.alloc(ctx, S));
+    MR_TRY(hpos.alloc(ctx, S + 1));
+    MR_TRY(tmp.alloc(ctx, std::max(scan_tmp_elems(S), scan_tmp_elems(NT))));
+    MR_TRY(truns.zero(ctx, NT));
+    hipLaunchKernelGGL(k_ix_keys, dim3(cdiv(S, XB)), dim3(XB), 0, st, s->trace.p, code, S, nbc, key.p, val.p);
+    SortScratch ws;
+    MR_TRY(mr_radix_sort(ctx, key.p, val.p, S, nbc + bits_for((uint64_t)std::max(NT - 1, 0)), ws));
+    hipLaunchKernelGGL(k_ix_heads, dim3(cdiv(S, XB)), dim3(XB), 0, st, key.p, S, head.p);
+    MR_TRY(mr_exclusive_scan_i32(ctx, head.p, hpos.p, S, tmp.p));
+    int64_t R = 0;
+    MR_TRY_HIP(ctx, hipMemcpyAsync(&R, hpos.p + S, sizeof R, hipMemcpyDeviceToHost, st));
+    MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+    MR_TRY(r_code.alloc(ctx, R));
+    MR_TRY(r_cnt.alloc(ctx, R));
+    MR_TRY(r_start.alloc(ctx, R));
+    if (r_first) MR_TRY(r_first->alloc(ctx, R));
+    if (r_tr) MR_TRY(r_tr->alloc(ctx, R));
+    hipLaunchKernelGGL(k_ix_runs, dim3(cdiv(S, XB)), dim3(XB), 0, st, key.p, val.p, head.p, hpos.p, S, nbc, r_code.p,
+                       r_first ? r_first->p : nullptr, r_tr ? r_tr->p : nullptr, r_start.p, truns.p);
+    hipLaunchKernelGGL(k_ix_cnt, dim3(cdiv(std::max<int64_t>(R, 1), XB)), dim3(XB), 0, st, r_start.p, R, S, r_cnt.p);
+    MR_TRY(off.alloc(ctx, (size_t)NT + 1));
+    MR_TRY(mr_exclusive_scan_i32(ctx, truns.p, off.p, NT, tmp.p));
+    MR_TRY_HIP(ctx, hipGetLastError());
+    MR_TRY_HIP(ctx, hipStreamSynchronize(st));   // scratch is freed on return
+    *n_runs = R;
+    return MR_OK;
+}
+
+int mr_spans_index(mr_ctx* ctx, mr_spans* s) {
+    hipStream_t st = ctx->stream;
+    const int64_t S = s->S;
+    const int32_t NT = s->n_traces, NP = s->n_podops;
+    s->indexed = false;
+    const int nbt = bits_for((uint64_t)std::max(NT - 1, 0));
+    const int nbp = std::max(1, bits_for((uint64_t)std::max(NP - 1, 0)));
+    const int nbs = std::max(1, bits_for((uint64_t)std::max(s->n_svcops - 1, 0)));
+    if (S == 0 || NT == 0 || nbt + 2 * nbp > 64 || nbt + nbs > 64 || nbp > 32) return MR_OK;   // row-level paths only
+    // per-trace scalars
+    MR_TRY(s->tlen.zero(ctx, NT));
+    MR_TRY(s->tmaxd.alloc(ctx, NT));
+    MR_TRY(s->tts.alloc(ctx, NT));
+    MR_TRY(s->tte.alloc(ctx, NT));
+    DBuf<long long> tsmax, temax;
+    MR_TRY(tsmax.alloc(ctx, NT));
+    MR_TRY(temax.alloc(ctx, NT));
+    DBuf<int32_t> bad;
+    MR_TRY(bad.zero(ctx, 1));
+    MR_TRY_HIP(ctx, hipMemsetAsync(s->tmaxd.p, 0x80, NT * sizeof(long long), st));   // very negative
+    MR_TRY_HIP(ctx, hipMemsetAsync(tsmax.p, 0x80, NT * sizeof(long long), st));
+    MR_TRY_HIP(ctx, hipMemsetAsync(temax.p, 0x80, NT * sizeof(long long), st));
+    MR_TRY_HIP(ctx, hipMemsetAsync(s->tts.p, 0x7f, NT * sizeof(long long), st));     // very positive
+    MR_TRY_HIP(ctx, hipMemsetAsync(s->tte.p, 0x7f, NT * sizeof(long long), st));
+    hipLaunchKernelGGL(k_ix_trace_stats, dim3(cdiv(S, XB)), dim3(XB), 0, st, s->trace.p, s->duration.p,
+                       s->has_times ? s->tstart.p : nullptr, s->has_times ? s->tend.p : nullptr, S, s->tlen.p,
+                       s->tmaxd.p, s->tts.p, tsmax.p, s->tte.p, temax.p);
+    if (s->has_times)
+        hipLaunchKernelGGL(k_ix_uniform, dim3(cdiv(NT, XB)), dim3(XB), 0, st, s->tlen.p, s->tts.p, tsmax.p, s->tte.p,
+                           temax.p, NT, bad.p);
+    // distinct pod-ops and service-ops per trace
+    MR_TRY(trace_runs(ctx, s, s->podop.p, NP, s->po_off, s->po_op, s->po_cnt, &s->po_first, &s->po_tr, &s->n_po));
+    MR_TRY(trace_runs(ctx, s, s->svcop.p, s->n_svcops, s->sv_off, s->sv_op, s->sv_cnt, nullptr, nullptr, &s->n_sv));
+    // parent join resolved once
+    {
+        DBuf<int32_t> nin, nx;
+        DBuf<int64_t> pin, px, tmp;
+        MR_TRY(nin.alloc(ctx, S));
+        MR_TRY(nx.alloc(ctx, S));
+        MR_TRY(pin.alloc(ctx, S + 1));
+        MR_TRY(px.alloc(ctx, S + 1));
+        MR_TRY(tmp.alloc(ctx, std::max(scan_tmp_elems(S), scan_tmp_elems(NT))));
+        hipLaunchKernelGGL(k_ix_join_count, dim3(cdiv(S, XB)), dim3(XB), 0, st, s->trace.p, s->parent.p, S, s->id_off.p,
+                           s->id_rows.p, s->n_span_codes, nin.p, nx.p);
+        MR_TRY(mr_exclusive_scan_i32(ctx, nin.p, pin.p, S, tmp.p));
+        MR_TRY(mr_exclusive_scan_i32(ctx, nx.p, px.p, S, tmp.p));
+        int64_t h[2] = {0, 0};
+        MR_TRY_HIP(ctx, hipMemcpyAsync(&h[0], pin.p + S, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+        MR_TRY_HIP(ctx, hipMemcpyAsync(&h[1], px.p + S, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+        MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+        const int64_t J = h[0];
+        s->n_xj = h[1];
+        DBuf<uint64_t> ikey;
+        MR_TRY(ikey.alloc(ctx, J));
+        MR_TRY(s->xj_tc.alloc(ctx, s->n_xj));
+        MR_TRY(s->xj_tp.alloc(ctx, s->n_xj));
+        MR_TRY(s->xj_key.alloc(ctx, s->n_xj));
+        hipLaunchKernelGGL(k_ix_join_fill, dim3(cdiv(S, XB)), dim3(XB), 0, st, s->trace.p, s->podop.p, s->parent.p, S,
+                           s->id_off.p, s->id_rows.p, s->n_span_codes, pin.p, px.p, nbp, ikey.p, s->xj_tc.p, s->xj_tp.p,
+                           s->xj_key.p);
+        SortScratch ws;
+        MR_TRY(mr_radix_sort(ctx, ikey.p, nullptr, J, nbt + 2 * nbp, ws));
+        DBuf<int32_t> head, truns;
+        DBuf<int64_t> hpos, r_start;
+        MR_TRY(head.alloc(ctx, J));
+        MR_TRY(hpos.alloc(ctx, J + 1));
+        MR_TRY(truns.zero(ctx, NT));
+        MR_TRY(tmp.alloc(ctx, std::max({scan_tmp_elems(J), scan_tmp_elems(NT), (int64_t)1})));
+        if (J) hipLaunchKernelGGL(k_ix_heads, dim3(cdiv(J, XB)), dim3(XB), 0, st, ikey.p, J, head.p);
+        MR_TRY(mr_exclusive_scan_i32(ctx, head.p, hpos.p, J, tmp.p));
+        int64_t R = 0;
+        MR_TRY_HIP(ctx, hipMemcpyAsync(&R, hpos.p + J, sizeof R, hipMemcpyDeviceToHost, st));
+        MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+        s->n_ed = R;
+        MR_TRY(s->ed_key.alloc(ctx, R));
+        MR_TRY(s->ed_cnt.alloc(ctx, R));
+        MR_TRY(s->ed_tr.alloc(ctx, R));
+        MR_TRY(r_start.alloc(ctx, R));
+        if (J)
+            hipLaunchKernelGGL(k_ix_edge_runs, dim3(cdiv(J, XB)), dim3(XB), 0, st, ikey.p, head.p, hpos.p, J, nbp,
+                               s->ed_key.p, s->ed_tr.p, r_start.p, truns.p);
+        if (R) hipLaunchKernelGGL(k_ix_cnt, dim3(cdiv(R, XB)), dim3(XB), 0, st, r_start.p, R, J, s->ed_cnt.p);
+        MR_TRY(s->ed_off.alloc(ctx, (size_t)NT + 1));
+        MR_TRY(mr_exclusive_scan_i32(ctx, truns.p, s->ed_off.p, NT, tmp.p));
+        MR_TRY_HIP(ctx, hipGetLastError());
+        MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+    }
+    int32_t hb = 0;
+    MR_TRY(bad.download(ctx, &hb, 1));
+    MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+    s->uniform_times = s->has_times && hb == 0;
+    s->indexed = true;
+    return MR_OK;
+}
+
+// Window detector on the index (uniform trace times): state[t] 0 out / 1 normal / 2 abnormal.
+int mr_detect_indexed(mr_ctx* ctx, const mr_spans* s, int64_t t0, int64_t t1, const double* d_a3, const uint8_t* d_a3v,
+                      uint8_t* d_state, int32_t* n_abn, int32_t* n_nor, int64_t* n_in) {
+    hipStream_t st = ctx->stream;
+    const int32_t NT = s->n_traces;
+    DBuf<unsigned long long> counts;
+    MR_TRY(counts.zero(ctx, 3 * CSH));
+    hipLaunchKernelGGL(k_ix_detect, dim3(cdiv(NT, DB)), dim3(DB), 0, st, NT, s->tlen.p, s->tts.p, s->tte.p, s->tmaxd.p,
+                       s->sv_off.p, s->sv_op.p, s->sv_cnt.p, d_a3, d_a3v, t0, t1, d_state, counts.p);
+    MR_TRY_HIP(ctx, hipGetLastError());
+    unsigned long long sh[3 * CSH], hc[3] = {0, 0, 0};
+    MR_TRY(counts.download(ctx, sh, 3 * CSH));
+    MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+    for (int k = 0; k < 3 * CSH; ++k) hc[k % 3] += sh[k];
+    *n_in = (int64_t)hc[2];
+    if (hc[2] == 0) return mr_fail(ctx, MR_ERR_VALUE, "Current span list is empty");
+    *n_abn = (int32_t)hc[0];
+    *n_nor = (int32_t)hc[1];
+    return MR_OK;
+}
