@@ -15,8 +15,10 @@ no collective on the data path -> "scaling": "weak".
 value = edges traversed by all PageRank iterations of all ranks (25 * (2 nnz + E_c) per graph)
 / max-over-ranks wall time of the K steps  [GTEPS].  Every other part of the window (detector,
 graph builds, spectrum) is inside that time.  windows_per_s is reported beside it.
-roofline: the power-iteration kernel (k_iter), algorithmic bytes (SURVEY §8(d) B_iter) per
-launch over its live HIP-event duration on the library's stream.
+roofline: one power iteration (the k_fx_a + k_fx_b launch pair), algorithmic bytes (SURVEY §8(d)
+B_iter, both graphs of the window) over its live HIP-event duration on the library's stream;
+traffic = FETCH_SIZE (x2, gfx950) + WRITE_SIZE of the same launches per iteration from two
+rocprofv3 --pmc child runs made before this process touches the GPU (--no-traffic skips them).
 cpu_baseline: the C restatement (oracle/, OpenMP) of the same window on this host's cores.
 """
 from __future__ import annotations
@@ -79,6 +81,49 @@ def run_window(ctx, dev, t0, t1, a3, ok, prec):
     return edges.value, codes[:n_out.value].copy(), scores[:n_out.value].copy(), na.value, nn.value
 
 
+ITER_KERNELS = ("k_fx_a", "k_fx_b", "k_iter_a", "k_iter_b")
+
+
+def pmc_traffic(args, timeout_s=240):
+    """HBM bytes per power iteration (all kernels of one iteration: k_fx_a + k_fx_b, or the tile
+    path's k_iter_a + k_iter_b) from two rocprofv3 --pmc child runs of this bench (FETCH_SIZE and
+    WRITE_SIZE in separate passes, MI355X_MICROARCH.md 'HBM': FETCH_SIZE reads half the bytes of
+    wide streaming loads on gfx950 -> x2).  Child processes only: this process has not touched
+    the GPU yet when it runs them.  None when rocprofv3 is unavailable or a pass fails."""
+    import csv
+    import glob
+    import shutil
+    import subprocess
+    import tempfile
+
+    prof = shutil.which("rocprofv3") or ("/opt/rocm/bin/rocprofv3" if os.path.exists("/opt/rocm/bin/rocprofv3") else None)
+    if prof is None:
+        return None
+    env = dict(os.environ, TMPDIR="/tmp")
+    vals = {}
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        with tempfile.TemporaryDirectory(dir="/tmp") as d:
+            cmd = [prof, "--pmc", ctr, "-d", d, "-o", "run", "--output-format", "csv", "--",
+                   sys.executable, os.path.abspath(__file__), "--pmc-child", "--steps", "2", "--warmup", "1",
+                   "--no-cpu", "--ops", str(args.ops), "--traces", str(args.traces), "--precision", args.precision]
+            try:
+                subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
+                               timeout=timeout_s, check=True)
+            except Exception:
+                return None
+            per_iter, n_a = 0.0, 0
+            for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+                for r in csv.DictReader(open(f)):
+                    name = r["Kernel_Name"]
+                    if r["Counter_Name"] == ctr and any(k in name for k in ITER_KERNELS):
+                        per_iter += float(r["Counter_Value"])
+                        n_a += any(k in name for k in ("k_fx_a", "k_iter_a"))
+            if n_a == 0:
+                return None
+            vals[ctr] = per_iter / n_a * 1024.0   # KB -> bytes, per iteration
+    return {"fetch": 2.0 * vals["FETCH_SIZE"], "write": vals["WRITE_SIZE"]}
+
+
 def cpu_baseline(abnormal, t0, t1, a3, ok, target_s=12.0):
     """The oracle's C restatement of the same window, timed on this host (bounded sample)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
@@ -109,11 +154,17 @@ def main():
     ap.add_argument("--ops", type=int, default=1000)
     ap.add_argument("--traces", type=int, default=200_000)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC passes for roofline.traffic")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # PMC passes first, in child processes, before this process initialises the GPU
+    traffic = None
+    if world == 1 and not args.pmc_child and not args.no_traffic:
+        traffic = pmc_traffic(args)
     dist = None
     if world > 1:
         import torch.distributed as dist  # control plane only: barrier + max over ranks (gloo, host)
@@ -190,11 +241,19 @@ def main():
                    "n_spans": int(abnormal.n_spans), "n_abnormal": na, "n_normal": nn,
                    "edges_per_window": int(edges // max(args.steps, 1)), "parallelism": f"windows x{world}"},
         "windows_per_s": round(world * args.steps / elapsed, 3),
-        "roofline": {"bound": "hbm", "kernel": "k_iter (one Jacobi iteration)", "achieved": round(achieved, 1),
+        "roofline": {"bound": "hbm", "kernel": "one Jacobi iteration: k_fx_a + k_fx_b (fused path, N <= 8192)",
+                     "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": None, "avg_launch_us": round(avg_ms * 1e3, 3), "launches": launches.value,
+                     "traffic": None if traffic is None else round(traffic["fetch"] + traffic["write"]),
+                     "traffic_detail": traffic and {"fetch_bytes": round(traffic["fetch"]),
+                                                    "write_bytes": round(traffic["write"]),
+                                                    "source": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950) / WRITE_SIZE, "
+                                                              "per iteration (A + B launches)"},
+                     "avg_launch_us": round(avg_ms * 1e3, 3), "launches": launches.value,
                      "bytes_per_launch": round(kbytes.value / max(launches.value, 1))},
     }
+    if args.pmc_child:
+        return
     if not args.no_cpu:
         try:
             cb, cres = cpu_baseline(abnormal, t0, t1, a3, ok)

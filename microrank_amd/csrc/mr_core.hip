@@ -1,5 +1,7 @@
 // Context, error reporting, graph upload from host index arrays, result fetch.
 #include <algorithm>
+#include <chrono>
+#include <cstdlib>
 #include <cstring>
 
 #include "mr_internal.h"
@@ -13,6 +15,22 @@ int mr_fail(mr_ctx* ctx, int code, const char* fmt, ...) {
     va_end(ap);
     if (ctx) ctx->err = buf;
     return code;
+}
+
+PhaseTimer::PhaseTimer(hipStream_t s, const char* t) : st(s), tag(t), on(getenv("MR_WIN_TIMING") != nullptr) {
+    mark("start");
+}
+void PhaseTimer::mark(const char* name) {
+    if (!on) return;
+    (void)hipStreamSynchronize(st);
+    marks.emplace_back(name, std::chrono::duration<double, std::micro>(
+                                 std::chrono::steady_clock::now().time_since_epoch()).count());
+}
+PhaseTimer::~PhaseTimer() {
+    if (!on || marks.size() < 2) return;
+    fprintf(stderr, "[%s]", tag);
+    for (size_t i = 1; i < marks.size(); ++i) fprintf(stderr, " %s %.1f", marks[i].first, marks[i].second - marks[i - 1].second);
+    fprintf(stderr, " us\n");
 }
 
 extern "C" int mr_version(void) { return 100; }

@@ -464,7 +464,8 @@ static int read_i64(mr_ctx* ctx, const int64_t* dev, int64_t* host) {
 // per-node arrays (len_o, nchild) and P_ss by child.  ofirst holds a key per pod-op that orders
 // first appearances like the DataFrame rows (row_bits wide).
 static int build_nodes(mr_ctx* ctx, mr_graph* g, int32_t NP, const int32_t* ocnt, const int32_t* ofirst, int row_bits,
-                       const uint64_t* gk, const uint32_t* gc, uint64_t ecap, DBuf<int32_t>& node_of_code) {
+                       const uint64_t* gk, const uint32_t* gc, uint64_t ecap, DBuf<int32_t>& node_of_code,
+                       PhaseTimer* pt = nullptr) {
     hipStream_t st = ctx->stream;
     DBuf<int32_t> eflag, is_par, nchild_code;
     DBuf<int64_t> epos, etmp, tmp;
@@ -484,6 +485,7 @@ static int build_nodes(mr_ctx* ctx, mr_graph* g, int32_t NP, const int32_t* ocnt
     MR_TRY(ecnt.alloc(ctx, E));
     hipLaunchKernelGGL(k_edge_compact, dim3(cdiv(ecap, 256)), dim3(256), 0, st, gk, gc, eflag.p, epos.p, (int64_t)ecap,
                        ekey.p, ecnt.p, is_par.p, nchild_code.p);
+    if (pt) pt->mark("edges");
     // node order
     DBuf<int32_t> pflag, qflag;
     DBuf<int64_t> ppos, qpos;
@@ -514,6 +516,7 @@ static int build_nodes(mr_ctx* ctx, mr_graph* g, int32_t NP, const int32_t* ocnt
     if (Q)
         hipLaunchKernelGGL(k_node_rest, dim3(cdiv(Q, 256)), dim3(256), 0, st, qval.p, Q, (int32_t)P, node_of_code.p,
                            g->node_podop.p);
+    if (pt) pt->mark("order");
     // per-node arrays and P_ss
     const int nb = std::max(1, bits_for((uint64_t)std::max(N - 1, 0)));
     MR_TRY(g->len_o.alloc(ctx, N));
@@ -640,6 +643,7 @@ static int graph_build_rows(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d_ma
 // order (a fixed order for the kind keys; mr_graph_export sorts by node id for inspection).
 static int graph_build_indexed(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d_mask, mr_graph* g) {
     hipStream_t st = ctx->stream;
+    PhaseTimer pt(st, "build");
     const int32_t NT = sp->n_traces, NP = sp->n_podops;
     DBuf<int32_t> tflag, zc;
     DBuf<int64_t> tpos, zoff, tmp;
@@ -652,7 +656,7 @@ static int graph_build_indexed(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d
     MR_TRY(ocnt.zero(ctx, NP));
     MR_TRY(ofirst.alloc(ctx, NP));
     if (NP) MR_TRY_HIP(ctx, hipMemsetAsync(ofirst.p, 0x7f, NP * sizeof(int32_t), st));
-    const uint64_t ecap = edge_capacity(sp->n_ed + sp->n_xj, NP);
+    const uint64_t ecap = edge_capacity(sp->n_edge_keys, NP);
     DBuf<uint64_t> gk;
     DBuf<uint32_t> gc;
     MR_TRY(gk.alloc(ctx, ecap));
@@ -671,11 +675,14 @@ static int graph_build_indexed(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d
     if (sp->n_xj)
         hipLaunchKernelGGL(k_ix_cross, dim3(cdiv(sp->n_xj, 256)), dim3(256), 0, st, d_mask, sp->xj_tc.p, sp->xj_tp.p,
                            sp->xj_key.p, sp->n_xj, gk.p, gc.p, ecap - 1);
+    pt.mark("stats");
     MR_TRY(mr_exclusive_scan_i32(ctx, tflag.p, tpos.p, NT, tmp.p));
     MR_TRY(mr_exclusive_scan_i32(ctx, zc.p, zoff.p, NT, tmp.p));
+    pt.mark("scans");
     DBuf<int32_t> node_of_code;
     MR_TRY(build_nodes(ctx, g, NP, ocnt.p, ofirst.p, bits_for((uint64_t)std::max<int64_t>(sp->S, 1)), gk.p, gc.p, ecap,
-                       node_of_code));
+                       node_of_code, &pt));
+    pt.mark("nodes");
     int64_t h[2] = {0, 0};   // T, nnz (their scans ran before build_nodes' syncs)
     MR_TRY_HIP(ctx, hipMemcpyAsync(&h[0], tpos.p + NT, sizeof(int64_t), hipMemcpyDeviceToHost, st));
     MR_TRY_HIP(ctx, hipMemcpyAsync(&h[1], zoff.p + NT, sizeof(int64_t), hipMemcpyDeviceToHost, st));
@@ -696,6 +703,7 @@ static int graph_build_indexed(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d
     MR_TRY_HIP(ctx, hipGetLastError());
     g->T = T;
     g->nnz_sr = g->nnz_rs = nnz;
+    pt.mark("traces");
     return MR_OK;
 }
 
@@ -711,7 +719,9 @@ int mr_graph_build_dev(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d_mask, m
         g->rs_is_sr = true;
         g->pr_identity = true;
         g->n_pr = g->T;
+        PhaseTimer pt(ctx->stream, "prepare");
         rc = mr_graph_prepare(ctx, g);
+        pt.mark("done");
     }
     if (rc != MR_OK) {
         delete g;

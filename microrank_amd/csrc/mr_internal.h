@@ -7,6 +7,7 @@
 #include <cstdio>
 #include <map>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../../include/microrank_hip.h"
@@ -178,6 +179,7 @@ struct mr_spans {
     DBuf<int32_t> tlen;                  // [NT] rows of the trace
     DBuf<long long> tmaxd, tts, tte;     // [NT] max duration, trace-level start / end
     int64_t n_po = 0, n_sv = 0, n_ed = 0, n_xj = 0;
+    int64_t n_edge_keys = 0;             // distinct (parent op, child op) over the table: edge-set bound
     DBuf<int64_t> po_off;                // [NT+1] distinct pod-ops of a trace (code order) ...
     DBuf<int32_t> po_op, po_cnt, po_first, po_tr;   // ... with span count, first row and trace
     DBuf<int64_t> sv_off;                // [NT+1] distinct service-ops of a trace (code order) ...
@@ -190,6 +192,17 @@ struct mr_spans {
 };
 
 int mr_spans_index(mr_ctx* ctx, mr_spans* s);
+
+// MR_WIN_TIMING diagnostics: wall-clock phase marks (each mark synchronises the stream)
+struct PhaseTimer {
+    hipStream_t st;
+    const char* tag;
+    bool on;
+    std::vector<std::pair<const char*, double>> marks;
+    PhaseTimer(hipStream_t s, const char* t);
+    void mark(const char* name);
+    ~PhaseTimer();
+};
 
 // Launch helpers
 inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }

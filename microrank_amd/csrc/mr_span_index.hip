@@ -136,6 +136,14 @@ __global__ void k_ix_join_fill(const int32_t* trace, const int32_t* podop, const
         }
     }
 }
+// (parent << 32 | child) -> (parent << nbp | child), internal keys then cross keys
+__global__ void k_ix_pack_keys(const uint64_t* ed_key, int64_t n_ed, const uint64_t* xj_key, int64_t n_xj, int nbp,
+                               uint64_t* out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_ed + n_xj) return;
+    const uint64_t k = i < n_ed ? ed_key[i] : xj_key[i - n_ed];
+    out[i] = ((k >> 32) << nbp) | (k & 0xffffffffull);
+}
 __global__ void k_ix_edge_runs(const uint64_t* key, const int32_t* head, const int64_t* hpos, int64_t n, int nbp,
                                uint64_t* ed_key, int32_t* ed_tr, int64_t* r_start, int32_t* truns) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -362,6 +370,24 @@ int mr_spans_index(mr_ctx* ctx, mr_spans* s) {
         MR_TRY(s->ed_off.alloc(ctx, (size_t)NT + 1));
         MR_TRY(mr_exclusive_scan_i32(ctx, truns.p, s->ed_off.p, NT, tmp.p));
         MR_TRY_HIP(ctx, hipGetLastError());
+        MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+    }
+    {   // distinct call-edge keys over the whole table: a bound for any subset's edge set
+        const int64_t K = s->n_ed + s->n_xj;
+        DBuf<uint64_t> k2;
+        DBuf<int32_t> head;
+        DBuf<int64_t> hpos, tmp;
+        MR_TRY(k2.alloc(ctx, K));
+        MR_TRY(head.alloc(ctx, K));
+        MR_TRY(hpos.alloc(ctx, K + 1));
+        MR_TRY(tmp.alloc(ctx, std::max<int64_t>(scan_tmp_elems(K), 1)));
+        if (K) hipLaunchKernelGGL(k_ix_pack_keys, dim3(cdiv(K, XB)), dim3(XB), 0, st, s->ed_key.p, s->n_ed, s->xj_key.p,
+                                  s->n_xj, nbp, k2.p);
+        SortScratch ws;
+        MR_TRY(mr_radix_sort(ctx, k2.p, nullptr, K, 2 * nbp, ws));
+        if (K) hipLaunchKernelGGL(k_ix_heads, dim3(cdiv(K, XB)), dim3(XB), 0, st, k2.p, K, head.p);
+        MR_TRY(mr_exclusive_scan_i32(ctx, head.p, hpos.p, K, tmp.p));
+        MR_TRY_HIP(ctx, hipMemcpyAsync(&s->n_edge_keys, hpos.p + K, sizeof(int64_t), hipMemcpyDeviceToHost, st));
         MR_TRY_HIP(ctx, hipStreamSynchronize(st));
     }
     int32_t hb = 0;
