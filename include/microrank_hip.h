@@ -187,6 +187,25 @@ int mr_comm_unique_id(uint8_t id[128]);
 int mr_comm_init(mr_ctx* ctx, int nranks, int rank, const uint8_t id[128]);
 int mr_comm_allreduce_f64(mr_ctx* ctx, double* dev_buf, int64_t n, int op /*0 sum, 1 max*/);
 
+/* Host-staged collectives instead of RCCL (ranks sharing one GPU, CPU-side transports, tests):
+ * the library copies the operand to host memory, calls fn, and copies the result back.
+ *   coll 0 allreduce: buf[n] in/out, op 0 sum / 1 max
+ *   coll 1 allgather: buf[nranks * n]; this rank's n elements are at rank * n on entry
+ * dtype: 0 float64, 1 int32, 2 uint64, 3 int64.  fn returns 0 on success. */
+typedef int (*mr_host_coll_fn)(void* user, int coll, void* buf, int64_t n, int dtype, int op);
+int mr_comm_set_host(mr_ctx* ctx, mr_host_coll_fn fn, void* user, int nranks, int rank);
+
+/* Trace-sharded PageRank: g holds THIS rank's traces (every span of
+ * a trace on one rank) over the GLOBAL node index space, with this rank's partial len_o and
+ * nchild and its local call edges.  Once per graph the library sums len_o / nchild / coverage,
+ * unites the call edges, merges the trace-kind classes and the preference sums over the ranks;
+ * per iteration it sums the exact fixed-point P_sr r partials (uint64 limbs) and takes the max of
+ * r'.  Afterwards every rank holds the same weight and coverage vectors (mr_graph_fetch).
+ * Requires a collective backend (mr_comm_init or mr_comm_set_host) and the fused iteration
+ * (N <= 16384). */
+int mr_pagerank_sharded(mr_ctx* ctx, mr_graph* g, int anomaly, double d, double alpha, int iters,
+                        int precision, uint32_t flags);
+
 #ifdef __cplusplus
 }
 #endif

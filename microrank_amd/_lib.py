@@ -75,6 +75,8 @@ SIGNATURES = {
     "mr_comm_unique_id": (C.c_int, [C.POINTER(C.c_uint8)]),
     "mr_comm_init": (C.c_int, [P, C.c_int, C.c_int, C.POINTER(C.c_uint8)]),
     "mr_comm_allreduce_f64": (C.c_int, [P, P, C.c_int64, C.c_int]),
+    "mr_comm_set_host": (C.c_int, [P, C.c_void_p, C.c_void_p, C.c_int, C.c_int]),
+    "mr_pagerank_sharded": (C.c_int, [P, P, C.c_int, C.c_double, C.c_double, C.c_int, C.c_int, C.c_uint32]),
 }
 
 _lib = None

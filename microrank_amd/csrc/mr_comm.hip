@@ -1,8 +1,9 @@
-// RCCL (over xGMI) for the trace-sharded PageRank: one process per GPU, the score-vector
-// all-reduce per iteration.  librccl is dlopen'ed on first use so the library itself loads on
-// machines (and CPU test containers) without it.
+// Collectives of the trace-sharded PageRank (mr_shard.hip): RCCL over xGMI, one process per GPU
+// (librccl is dlopen'ed on first use so the library loads on machines without it), or a
+// host-staged callback (ranks that share a GPU, CPU transports such as gloo in the tests).
 #include <dlfcn.h>
 #include <cstring>
+#include <vector>
 #include <rccl/rccl.h>
 
 #include "mr_internal.h"
@@ -93,4 +94,49 @@ int mr_comm_allgather(mr_ctx* ctx, const void* send, void* recv, size_t n, ncclD
 extern "C" int mr_comm_allreduce_f64(mr_ctx* ctx, double* buf, int64_t n, int op) {
     if (!ctx || !buf || n < 0) return MR_ERR_ARG;
     return mr_comm_allreduce(ctx, buf, buf, (size_t)n, ncclFloat64, op ? ncclMax : ncclSum);
+}
+
+extern "C" int mr_comm_set_host(mr_ctx* ctx, mr_host_coll_fn fn, void* user, int nranks, int rank) {
+    if (!ctx || nranks < 1 || rank < 0 || rank >= nranks) return MR_ERR_ARG;
+    ctx->host_coll = fn;
+    ctx->host_user = user;
+    ctx->nranks = fn ? nranks : 1;
+    ctx->rank = fn ? rank : 0;
+    return MR_OK;
+}
+
+static size_t dt_size(int dt) { return dt == MR_DT_I32 ? 4 : 8; }
+static ncclDataType_t dt_nccl(int dt) {
+    return dt == MR_DT_F64 ? ncclFloat64 : dt == MR_DT_I32 ? ncclInt32 : dt == MR_DT_U64 ? ncclUint64 : ncclInt64;
+}
+
+int mr_coll_allreduce(mr_ctx* ctx, void* dbuf, int64_t n, int dtype, int op) {
+    if (n <= 0 || (ctx->nranks == 1 && !ctx->comm && !ctx->host_coll)) return MR_OK;
+    if (ctx->comm) return mr_comm_allreduce(ctx, dbuf, dbuf, (size_t)n, dt_nccl(dtype), op ? ncclMax : ncclSum);
+    if (!ctx->host_coll) return mr_fail(ctx, MR_ERR_COMM, "no collective backend (mr_comm_init / mr_comm_set_host)");
+    std::vector<unsigned char> h((size_t)n * dt_size(dtype));
+    MR_TRY_HIP(ctx, hipMemcpyAsync(h.data(), dbuf, h.size(), hipMemcpyDeviceToHost, ctx->stream));
+    MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (ctx->host_coll(ctx->host_user, 0, h.data(), n, dtype, op))
+        return mr_fail(ctx, MR_ERR_COMM, "host allreduce callback failed");
+    MR_TRY_HIP(ctx, hipMemcpyAsync(dbuf, h.data(), h.size(), hipMemcpyHostToDevice, ctx->stream));
+    MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return MR_OK;
+}
+
+int mr_coll_allgather(mr_ctx* ctx, const void* dsend, void* drecv, int64_t n, int dtype) {
+    const size_t bytes = (size_t)n * dt_size(dtype);
+    if (ctx->comm) return n > 0 ? mr_comm_allgather(ctx, dsend, drecv, (size_t)n, dt_nccl(dtype)) : MR_OK;
+    if (!ctx->host_coll) {   // a single rank: the gather is the send buffer
+        if (bytes) MR_TRY_HIP(ctx, hipMemcpyAsync(drecv, dsend, bytes, hipMemcpyDeviceToDevice, ctx->stream));
+        return MR_OK;
+    }
+    if (n <= 0) return MR_OK;
+    std::vector<unsigned char> h(bytes * (size_t)ctx->nranks);
+    MR_TRY_HIP(ctx, hipMemcpyAsync(h.data() + bytes * (size_t)ctx->rank, dsend, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (ctx->host_coll(ctx->host_user, 1, h.data(), n, dtype, 0)) return mr_fail(ctx, MR_ERR_COMM, "host allgather callback failed");
+    MR_TRY_HIP(ctx, hipMemcpyAsync(drecv, h.data(), h.size(), hipMemcpyHostToDevice, ctx->stream));
+    MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return MR_OK;
 }

@@ -22,6 +22,9 @@ struct mr_ctx {
     // RCCL (loaded lazily with dlopen so the library loads without it)
     void* comm = nullptr;
     int rank = 0, nranks = 1;
+    // host-staged collective backend (mr_comm_set_host), used when no RCCL communicator is set
+    mr_host_coll_fn host_coll = nullptr;
+    void* host_user = nullptr;
     // live kernel timing of the power-iteration launches (mr_ctx_profile): event pairs on the
     // context stream plus the algorithmic bytes of each launch
     bool prof = false;
@@ -129,8 +132,11 @@ struct mr_graph {
     // leaves one dense row of N partials per block (exact integer sums: order-free)
     bool fused = false;
     bool traces_nonempty = true;   // every trace has an op (span-built graphs; checked at upload)
+    int64_t T_all = 0;             // traces over all shards (0: this graph is whole)
+    bool sharded_done = false;     // mr_pagerank_sharded's graph-level exchange has run
     DBuf<uint64_t> fx_part;   // [n_blocks * N]
     DBuf<double> fx_ssv;      // [N] alpha * (P_ss s_k)[o] / M_s(k), from k_fx_a for k_fx_b
+    DBuf<uint64_t> fx_limb;   // [2N] sharded graphs: exact limb sums per op, all-reduced per iteration
     // per-trace / per-op constants
     DBuf<int32_t> len_t, len_o, nchild, cov;
     DBuf<float> w_t, u_o, pw;    // fp32(1/len_t), fp32(1/len_o), fp32(1/nchild)
@@ -192,6 +198,12 @@ struct mr_spans {
 };
 
 int mr_spans_index(mr_ctx* ctx, mr_spans* s);
+
+// collectives over the context's backend (RCCL communicator or host callback); device buffers
+enum { MR_DT_F64 = 0, MR_DT_I32 = 1, MR_DT_U64 = 2, MR_DT_I64 = 3 };
+int mr_coll_allreduce(mr_ctx* ctx, void* dbuf, int64_t n, int dtype, int op /*0 sum, 1 max*/);
+int mr_coll_allgather(mr_ctx* ctx, const void* dsend, void* drecv, int64_t n, int dtype);
+inline bool mr_coll_ready(const mr_ctx* ctx) { return ctx->comm || ctx->host_coll; }
 
 // MR_WIN_TIMING diagnostics: wall-clock phase marks (each mark synchronises the stream)
 struct PhaseTimer {

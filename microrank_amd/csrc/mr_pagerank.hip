@@ -322,14 +322,16 @@ __device__ __forceinline__ unsigned long long d2bits(double v) {
     return (unsigned long long)__double_as_longlong(v);
 }
 
-__global__ void k_iter_init(const float* w_t, const float* u_o, int32_t N, int32_t T, double* sp0, double* su0,
-                            double* q64, float* q32, int fp32, unsigned long long* mslot) {
+// T_all: traces of the whole graph (all shards) for the initial value
+__global__ void k_iter_init(const float* w_t, const float* u_o, int32_t N, int32_t T, int64_t T_all, double* sp0,
+                            double* su0, double* su1, double* q64, float* q32, int fp32, unsigned long long* mslot) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const double v0 = 1.0 / (double)(N + T);                   // pagerank.py:118-119
+    const double v0 = 1.0 / (double)((int64_t)N + T_all);      // pagerank.py:118-119
     if (i < N) {
         sp0[i] = v0;
         su0[i] = (double)u_o[i] * v0;
     }
+    if (i == N) su0[N] = su1[N] = 0.0;   // the fused walk's pad slot
     if (i < T) {
         double q = (double)w_t[i] * v0;
         if (fp32) q32[i] = (float)q; else q64[i] = q;
@@ -365,6 +367,7 @@ struct GDev {
     unsigned long long* mslot;
     unsigned long long* fx_part;
     double* fx_ssv;
+    unsigned long long* fx_limb;   // sharded: [2N] (lo, hi) limb sums per op
     int32_t probe;               // diagnostics (MR_FX_PROBE): 1 skip atomics, 2 skip gathers
     unsigned long long* stamp;   // diagnostics (MR_FX_STAMP): per-block phase clocks, else null
     double fx_scale, fx_iscale;
@@ -544,7 +547,8 @@ __global__ void __launch_bounds__(TB) k_iter_b(const GDev* __restrict__ gs, int3
 // Integer sums are exact, so the result does not depend on atomic or reduction order: runs are
 // bitwise reproducible, and the quantisation (2^-SC absolute per term, SC >= 53) sits below
 // fp64's own rounding of the reference's dot products.
-constexpr int FX_NMAX = 8192;
+constexpr int FX_NMAX = 16384;
+constexpr size_t FX_LDS_BUDGET = 150 * 1024;   // su joins lacc in LDS while both fit this budget
 constexpr int FX_CAP = 24;   // staged ids per thread: blocks with more entries take the long path
 
 // graph of a fused-launch block: ng <= 2 resolves from the scalar split (no memory hop)
@@ -557,9 +561,13 @@ __device__ __forceinline__ int32_t fx_graph(const GDev* gs, int32_t ng, int32_t 
 // LDS layout of k_fx_a (byte offsets), shared by kernel and host
 struct FxLds {
     size_t su, lacc, head, tail, tsum, xl, toff, owner, hbits, ids, total;
+    bool su_lds;   // su staged in LDS; otherwise gathered from its global copy (L2-resident)
     __host__ __device__ FxLds(int32_t N, int32_t TT) {
+        size_t rest = ((size_t)N + 1) * 8 + 4 * (size_t)TT * 8 + 8 + ((size_t)TT + 1) * 4 + (size_t)TT * 4 +
+                      ((size_t)FX_CAP * TT / 32 + 2) * 4 + 16 + ((size_t)FX_CAP * TT + 16) * 2;
+        su_lds = ((size_t)N + 1) * 8 + rest <= FX_LDS_BUDGET;
         su = 0;
-        lacc = su + ((size_t)N + 1) * 8;
+        lacc = su + (su_lds ? ((size_t)N + 1) * 8 : 0);
         head = lacc + ((size_t)N + 1) * 8;
         tail = head + (size_t)TT * 8;
         tsum = tail + (size_t)TT * 8;
@@ -598,7 +606,9 @@ __global__ void __launch_bounds__(1024) k_fx_a(const GDev* __restrict__ gs, int3
     const int32_t t = t0 + i;
     const bool own = i < nt;
     const FxLds L_(N, TT);
-    double* su = (double*)(lraw + L_.su);
+    const double* sug = G.sub[cur];   // N + 1 entries, sub[N] = 0 (the pad slot)
+    double* su_l = (double*)(lraw + L_.su);
+    const double* su = L_.su_lds ? su_l : sug;
     unsigned long long* lacc = (unsigned long long*)(lraw + L_.lacc);
     double* head = (double*)(lraw + L_.head);
     double* tail = (double*)(lraw + L_.tail);
@@ -636,9 +646,8 @@ __global__ void __launch_bounds__(1024) k_fx_a(const GDev* __restrict__ gs, int3
             xl[0] = 0ull;
         }
     }
-    const double* sug = G.sub[cur];
     for (int32_t o = i; o <= N; o += TT) {
-        su[o] = o < N ? sug[o] : 0.0;
+        if (L_.su_lds) su_l[o] = o < N ? sug[o] : 0.0;
         lacc[o] = 0ull;
     }
     if (i < WAVE) {
@@ -776,7 +785,10 @@ __global__ void __launch_bounds__(1024) k_fx_a(const GDev* __restrict__ gs, int3
     }
 }
 
-__global__ void __launch_bounds__(TB) k_fx_b(const GDev* __restrict__ gs, int32_t ng, int32_t split, double d, int it) {
+// mode 0: whole graph; sharded graphs split it around the limb all-reduce: mode 1 writes this
+// rank's limbs (lo, hi) per op to fx_limb, mode 2 finishes from the reduced limbs
+__global__ void __launch_bounds__(TB) k_fx_b(const GDev* __restrict__ gs, int32_t ng, int32_t split, double d, int it,
+                                             int mode) {
     const GDev& G = gs[fx_graph(gs, ng, split, 3)];
     const int32_t o = ((int32_t)blockIdx.x - G.blk0fb) * (TB / WAVE) + (int32_t)(threadIdx.x / WAVE);
     if (o >= G.N) return;
@@ -788,7 +800,7 @@ __global__ void __launch_bounds__(TB) k_fx_b(const GDev* __restrict__ gs, int32_
     const float uo = G.u_o[o];
     const unsigned long long* __restrict__ col = G.fx_part + o;
     unsigned long long lo = 0ull, hi = 0ull;
-    int32_t i = lane;
+    int32_t i = mode == 2 ? nb : lane;
     for (; i + 3 * WAVE < nb; i += 4 * WAVE) {
         const unsigned long long v0 = col[(size_t)i * N], v1 = col[(size_t)(i + WAVE) * N],
                                  v2 = col[(size_t)(i + 2 * WAVE) * N], v3 = col[(size_t)(i + 3 * WAVE) * N];
@@ -805,7 +817,18 @@ __global__ void __launch_bounds__(TB) k_fx_b(const GDev* __restrict__ gs, int32_
         lo += __shfl_xor(lo, m, WAVE);
         hi += __shfl_xor(hi, m, WAVE);
     }
-    // hi, lo < 2^53 (fewer than 2^21 blocks): both conversions exact, one rounding in the add
+    if (mode == 1) {
+        if (lane == 0) {
+            G.fx_limb[2 * o] = lo;
+            G.fx_limb[2 * o + 1] = hi;
+        }
+        return;
+    }
+    if (mode == 2) {
+        lo = G.fx_limb[2 * o];
+        hi = G.fx_limb[2 * o + 1];
+    }
+    // hi, lo < 2^53 (fewer than 2^21 blocks over all ranks): both conversions exact, one rounding
     const double sum = ((double)hi * 4294967296.0 + (double)lo) * G.fx_iscale;
     if (lane == 0) {
         const double v = d * (sum + ssv);      // pagerank.py:122-124
@@ -851,6 +874,83 @@ __global__ void __launch_bounds__(1024) k_weights(const double* sp, const unsign
     const double total = tot;
     for (int32_t o = threadIdx.x; o < N; o += blockDim.x) weight[o] = sn[o] * total / (double)N;
     if (threadIdx.x == 0) scal[4] = total;
+}
+// ---------------------------------------------------------------- trace-sharded graphs
+// local call edges (child, parent) as sort keys c << nb | p
+__global__ void k_sh_edge_keys(const int64_t* ss_off, const int32_t* ss_par, int32_t N, int nb, uint64_t* key) {
+    const int32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= N) return;
+    for (int64_t e = ss_off[c]; e < ss_off[c + 1]; ++e) key[e] = ((uint64_t)c << nb) | (uint32_t)ss_par[e];
+}
+__global__ void k_sh_pad(uint64_t* key, int64_t from, int64_t to, uint64_t pad) {
+    const int64_t i = from + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < to) key[i] = pad;
+}
+// heads of distinct real keys in the sorted union (pads sort last and are dropped)
+__global__ void k_sh_edge_heads(const uint64_t* key, int64_t n, uint64_t pad, int32_t* head) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) head[i] = key[i] != pad && (i == 0 || key[i] != key[i - 1]) ? 1 : 0;
+}
+__global__ void k_sh_edge_out(const uint64_t* key, const int32_t* head, const int64_t* pos, int64_t n, int nb,
+                              int32_t* ss_par, int32_t* ccount) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || !head[i]) return;
+    ss_par[pos[i]] = (int32_t)(key[i] & ((1ull << nb) - 1ull));
+    atomicAdd(&ccount[(int32_t)(key[i] >> nb)], 1);
+}
+// this rank's kind classes as (key, check hash of the representative, count); empty slots skipped
+__global__ void k_sh_kind_list(const uint64_t* hk, const uint32_t* hc, const int32_t* hr, int64_t cap,
+                               const int32_t* flag, const int64_t* pos, const int64_t* off, const int32_t* ops,
+                               const float* w_t, uint64_t* out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= cap || !flag[i]) return;
+    const int64_t p = pos[i];
+    out[3 * p] = hk[i];
+    out[3 * p + 1] = kind_hash(off, ops, w_t, hr[i], 0x0ddba11cafeull);
+    out[3 * p + 2] = hc[i];
+}
+__global__ void k_sh_kind_flags(const uint64_t* hk, int64_t cap, int32_t* flag) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < cap) flag[i] = hk[i] != 0ull;
+}
+// all ranks' lists into one table: counts summed per key; a key whose check hash differs
+// between ranks is a 64-bit collision across ranks -> flag
+__global__ void k_sh_kind_merge(const uint64_t* in, int64_t n, uint64_t* gk, uint64_t* gh, unsigned long long* gc,
+                                uint64_t mask, int32_t* flag) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t k = in[3 * i];
+    if (!k) return;
+    uint64_t s = mix64(k) & mask;
+    for (;;) {
+        const unsigned long long old = atomicCAS((unsigned long long*)&gk[s], 0ull, (unsigned long long)k);
+        if (old == 0ull) {
+            gh[s] = in[3 * i + 1];   // first writer; later writers compare after the table settles
+            break;
+        }
+        if (old == k) break;
+        s = (s + 1) & mask;
+    }
+    atomicAdd(&gc[s], (unsigned long long)in[3 * i + 2]);
+}
+__global__ void k_sh_kind_check(const uint64_t* in, int64_t n, const uint64_t* gk, const uint64_t* gh, uint64_t mask,
+                                int32_t* flag) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || !in[3 * i]) return;
+    const uint64_t k = in[3 * i];
+    uint64_t s = mix64(k) & mask;
+    while (gk[s] != k) s = (s + 1) & mask;
+    if (gh[s] != in[3 * i + 1]) atomicOr(flag, 1);
+}
+// kind[t] = the class size over all ranks
+__global__ void k_sh_kind_apply(const uint64_t* hk, const int32_t* slot_of, int32_t T, const uint64_t* gk,
+                                const unsigned long long* gc, uint64_t mask, double* kind) {
+    const int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= T) return;
+    const uint64_t k = hk[slot_of[t]];
+    uint64_t s = mix64(k) & mask;
+    while (gk[s] != k) s = (s + 1) & mask;
+    kind[t] = (double)gc[s];
 }
 }  // namespace
 
@@ -991,7 +1091,10 @@ static int fx_tt() {
 }
 
 // kinds, preference vector and iteration state of one graph (everything before the iterations)
-static int pagerank_setup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool fp32, uint32_t flags) {
+static int shard_kinds(mr_ctx* ctx, mr_graph* g, uint64_t cap);
+
+static int pagerank_setup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool fp32, uint32_t flags,
+                          bool sharded = false) {
     hipStream_t st = ctx->stream;
     const int32_t N = g->N, T = g->T;
     uint64_t cap = 1;
@@ -1012,8 +1115,8 @@ static int pagerank_setup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool 
     MR_TRY(g->sn.alloc(ctx, (size_t)N));
     MR_TRY(g->spb[0].alloc(ctx, (size_t)N));
     MR_TRY(g->spb[1].alloc(ctx, (size_t)N));
-    MR_TRY(g->sub[0].alloc(ctx, (size_t)N));
-    MR_TRY(g->sub[1].alloc(ctx, (size_t)N));
+    MR_TRY(g->sub[0].alloc(ctx, (size_t)N + 1));   // [N] = 0: the fused walk's pad slot
+    MR_TRY(g->sub[1].alloc(ctx, (size_t)N + 1));
     MR_TRY(g->weight.alloc(ctx, (size_t)N));
     if (g->fused) {
         MR_TRY(g->fx_part.alloc(ctx, (size_t)cdiv(T, fx_tt()) * (size_t)N));
@@ -1038,25 +1141,28 @@ static int pagerank_setup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool 
     hipLaunchKernelGGL(k_kind_verify, dim3(cdiv(T, 256)), dim3(256), 0, st, koff, kops, g->w_t.p, T, g->ht_cnt.p,
                        g->ht_rep.p, g->slot_of.p, g->kind.p, g->flag.p);
     MR_DEBUG_CHECK(ctx, "k_kind_verify");
+    if (sharded) MR_TRY(shard_kinds(ctx, g, cap));   // class sizes over all ranks
     // ---- preference
     const int32_t* prt = g->pr_identity ? nullptr : g->pr_trace.p;
     const int32_t* prl = g->pr_identity ? nullptr : g->pr_len.p;
     if (n_pr > 0)
         hipLaunchKernelGGL(k_pref_partial, dim3(nbp), dim3(TB), 0, st, g->kind.p, prt, prl, g->len_t.p, n_pr,
                            g->ppart.p, g->flag.p);
-    if (flags & MR_PR_EXACT_SUMS)
+    if ((flags & MR_PR_EXACT_SUMS) && !sharded)
         hipLaunchKernelGGL(k_pref_total_exact, dim3(1), dim3(64), 0, st, g->kind.p, prt, prl, g->len_t.p, n_pr,
                            g->scal.p);
     else
         hipLaunchKernelGGL(k_pref_total, dim3(1), dim3(1024), 0, st, g->ppart.p, nbp, g->scal.p);
     MR_DEBUG_CHECK(ctx, "k_pref");
+    if (sharded) MR_TRY(mr_coll_allreduce(ctx, g->scal.p + 2, 2, MR_DT_F64, 0));   // sum(1/k), sum(1/len)
     const float cd = (float)(1.0 - d);
     if (n_pr > 0)
         hipLaunchKernelGGL(k_pref_apply, dim3(nbp), dim3(TB), 0, st, g->kind.p, prt, prl, g->len_t.p, n_pr,
                            g->scal.p, anomaly, cd, g->pref.p, g->c_t.p);
     MR_DEBUG_CHECK(ctx, "k_pref_apply");
-    hipLaunchKernelGGL(k_iter_init, dim3(cdiv(std::max<int64_t>({N, T, 6 * MSH}), 256)), dim3(256), 0, st, g->w_t.p,
-                       g->u_o.p, N, T, g->spb[0].p, g->sub[0].p, g->q64[0].p, g->q32[0].p, (int)fp32, g->mslot.p);
+    hipLaunchKernelGGL(k_iter_init, dim3(cdiv(std::max<int64_t>({(int64_t)N + 1, T, 6 * MSH}), 256)), dim3(256), 0, st,
+                       g->w_t.p, g->u_o.p, N, T, g->T_all > 0 ? g->T_all : (int64_t)T, g->spb[0].p, g->sub[0].p,
+                       g->sub[1].p, g->q64[0].p, g->q32[0].p, (int)fp32, g->mslot.p);
     MR_DEBUG_CHECK(ctx, "k_iter_init");
     return MR_OK;
 }
@@ -1070,7 +1176,7 @@ static double iter_bytes(const mr_graph* g, bool fp32) {
 }
 
 int mr_pagerank_batch_impl(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly, int ng, double d, double alpha,
-                           int iters, int precision, uint32_t flags) {
+                           int iters, int precision, uint32_t flags, bool sharded = false) {
     if (!ctx || ng <= 0 || !gs || !anomaly) return mr_fail(ctx, MR_ERR_ARG, "mr_pagerank: bad arguments");
     if (iters < 0) return mr_fail(ctx, MR_ERR_ARG, "iters < 0");
     for (int i = 0; i < ng; ++i) {
@@ -1081,7 +1187,7 @@ int mr_pagerank_batch_impl(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly,
     MR_TRY_HIP(ctx, hipSetDevice(ctx->device));
     hipStream_t st = ctx->stream;
     const bool fp32 = precision == MR_FP32;
-    for (int i = 0; i < ng; ++i) MR_TRY(pagerank_setup(ctx, gs[i], anomaly[i], d, fp32, flags));
+    for (int i = 0; i < ng; ++i) MR_TRY(pagerank_setup(ctx, gs[i], anomaly[i], d, fp32, flags, sharded));
     // ---- batched power iteration: one k_iter_a + k_iter_b pair per iteration for every graph
     int mask = 3;
     if (const char* rm = getenv("MR_ROLE_MASK")) mask = atoi(rm);   // profiling knob: 1 trace / 2 op side
@@ -1119,6 +1225,7 @@ int mr_pagerank_batch_impl(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly,
         v.mslot = g->mslot.p;
         v.fx_part = (unsigned long long*)g->fx_part.p;
         v.fx_ssv = g->fx_ssv.p;
+        v.fx_limb = (unsigned long long*)g->fx_limb.p;
         v.stamp = nullptr;
         v.probe = getenv("MR_FX_PROBE") ? atoi(getenv("MR_FX_PROBE")) : 0;
         v.fx_scale = std::ldexp(1.0, sc);
@@ -1163,7 +1270,14 @@ int mr_pagerank_batch_impl(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly,
             if (fp32) hipLaunchKernelGGL(k_fx_a<float>, dim3(blocks_fa), dim3(TT), lds_f, st, dv.p, ng, split_fa, d, alpha, it);
             else hipLaunchKernelGGL(k_fx_a<double>, dim3(blocks_fa), dim3(TT), lds_f, st, dv.p, ng, split_fa, d, alpha, it);
             MR_DEBUG_CHECK(ctx, "k_fx_a");
-            hipLaunchKernelGGL(k_fx_b, dim3(blocks_fb), dim3(TB), 0, st, dv.p, ng, split_fb, d, it);
+            if (!sharded) {
+                hipLaunchKernelGGL(k_fx_b, dim3(blocks_fb), dim3(TB), 0, st, dv.p, ng, split_fb, d, it, 0);
+            } else {   // r' max and the P_sr r limbs over all ranks (exact: integers, max)
+                MR_TRY(mr_coll_allreduce(ctx, gs[0]->mslot.p + (size_t)2 * MSH * ((it + 1) % 3) + MSH, MSH, MR_DT_U64, 1));
+                hipLaunchKernelGGL(k_fx_b, dim3(blocks_fb), dim3(TB), 0, st, dv.p, ng, split_fb, d, it, 1);
+                MR_TRY(mr_coll_allreduce(ctx, gs[0]->fx_limb.p, 2 * (int64_t)gs[0]->N, MR_DT_U64, 0));
+                hipLaunchKernelGGL(k_fx_b, dim3(blocks_fb), dim3(TB), 0, st, dv.p, ng, split_fb, d, it, 2);
+            }
             MR_DEBUG_CHECK(ctx, "k_fx_b");
         }
         if (blocks_a) {
@@ -1228,4 +1342,119 @@ extern "C" int mr_pagerank(mr_ctx* ctx, mr_graph* g, int anomaly, double d, doub
 extern "C" int mr_pagerank_batch(mr_ctx* ctx, mr_graph* const* graphs, const int* anomaly, int n_graphs, double d,
                                  double alpha, int iters, int precision, uint32_t flags) {
     return mr_pagerank_batch_impl(ctx, graphs, anomaly, n_graphs, d, alpha, iters, precision, flags);
+}
+
+// ------------------------------------------------------------------------------ sharded graphs
+static int shard_kinds(mr_ctx* ctx, mr_graph* g, uint64_t cap) {
+    hipStream_t st = ctx->stream;
+    const int32_t T = g->T;
+    const int64_t* koff = g->rs_is_sr ? g->rs_off.p : g->srt_off.p;
+    const int32_t* kops = g->rs_is_sr ? g->rs_ops.p : g->srt_ops.p;
+    DBuf<int32_t> fl;
+    DBuf<int64_t> pos, tmp;
+    MR_TRY(fl.alloc(ctx, cap));
+    MR_TRY(pos.alloc(ctx, cap + 1));
+    MR_TRY(tmp.alloc(ctx, scan_tmp_elems((int64_t)cap)));
+    hipLaunchKernelGGL(k_sh_kind_flags, dim3(cdiv(cap, 256)), dim3(256), 0, st, g->ht_key.p, (int64_t)cap, fl.p);
+    MR_TRY(mr_exclusive_scan_i32(ctx, fl.p, pos.p, (int64_t)cap, tmp.p));
+    DBuf<int64_t> kn;
+    MR_TRY(kn.alloc(ctx, 1));
+    MR_TRY_HIP(ctx, hipMemcpyAsync(kn.p, pos.p + cap, sizeof(int64_t), hipMemcpyDeviceToDevice, st));
+    int64_t Kl = 0;
+    MR_TRY(kn.download(ctx, &Kl, 1));
+    MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+    MR_TRY(mr_coll_allreduce(ctx, kn.p, 1, MR_DT_I64, 1));
+    int64_t Kmax = 0;
+    MR_TRY(kn.download(ctx, &Kmax, 1));
+    MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+    const int R = ctx->nranks;
+    DBuf<uint64_t> send, recv;
+    MR_TRY(send.zero(ctx, (size_t)3 * std::max<int64_t>(Kmax, 1)));
+    MR_TRY(recv.alloc(ctx, (size_t)3 * std::max<int64_t>(Kmax, 1) * R));
+    hipLaunchKernelGGL(k_sh_kind_list, dim3(cdiv(cap, 256)), dim3(256), 0, st, g->ht_key.p, g->ht_cnt.p, g->ht_rep.p,
+                       (int64_t)cap, fl.p, pos.p, koff, kops, g->w_t.p, send.p);
+    MR_TRY(mr_coll_allgather(ctx, send.p, recv.p, 3 * std::max<int64_t>(Kmax, 1), MR_DT_U64));
+    const int64_t n = std::max<int64_t>(Kmax, 1) * R;
+    uint64_t gcap = 1;
+    while (gcap < 2 * (uint64_t)n) gcap <<= 1;
+    DBuf<uint64_t> gk, gh;
+    DBuf<unsigned long long> gc;
+    MR_TRY(gk.zero(ctx, gcap));
+    MR_TRY(gh.zero(ctx, gcap));
+    MR_TRY(gc.zero(ctx, gcap));
+    hipLaunchKernelGGL(k_sh_kind_merge, dim3(cdiv(n, 256)), dim3(256), 0, st, recv.p, n, gk.p, gh.p, gc.p, gcap - 1,
+                       g->flag.p);
+    hipLaunchKernelGGL(k_sh_kind_check, dim3(cdiv(n, 256)), dim3(256), 0, st, recv.p, n, gk.p, gh.p, gcap - 1, g->flag.p);
+    if (T)
+        hipLaunchKernelGGL(k_sh_kind_apply, dim3(cdiv(T, 256)), dim3(256), 0, st, g->ht_key.p, g->slot_of.p, T, gk.p,
+                           gc.p, gcap - 1, g->kind.p);
+    MR_TRY_HIP(ctx, hipGetLastError());
+    MR_TRY_HIP(ctx, hipStreamSynchronize(st));   // scratch leaves scope
+    return MR_OK;
+}
+
+// once per graph: per-op sums, the union of the call edges, the number of traces
+static int shard_exchange(mr_ctx* ctx, mr_graph* g) {
+    hipStream_t st = ctx->stream;
+    const int32_t N = g->N;
+    MR_TRY(mr_coll_allreduce(ctx, g->len_o.p, N, MR_DT_I32, 0));
+    MR_TRY(mr_coll_allreduce(ctx, g->nchild.p, N, MR_DT_I32, 0));
+    MR_TRY(mr_coll_allreduce(ctx, g->cov.p, N, MR_DT_I32, 0));
+    if (N) hipLaunchKernelGGL(k_op_consts, dim3(cdiv(N, 256)), dim3(256), 0, st, g->len_o.p, g->nchild.p, g->u_o.p, g->pw.p, N);
+    DBuf<int64_t> sc;
+    MR_TRY(sc.alloc(ctx, 2));
+    int64_t h[2] = {(int64_t)g->T, g->E};
+    MR_TRY(sc.upload(ctx, h, 2));
+    MR_TRY(mr_coll_allreduce(ctx, sc.p, 1, MR_DT_I64, 0));       // traces over all ranks
+    MR_TRY(mr_coll_allreduce(ctx, sc.p + 1, 1, MR_DT_I64, 1));   // largest local edge list
+    MR_TRY(sc.download(ctx, h, 2));
+    MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+    g->T_all = h[0];
+    const int64_t Emax = std::max<int64_t>(h[1], 1);
+    const int R = ctx->nranks;
+    const int nb = std::max(1, bits_for((uint64_t)std::max(N - 1, 0)));
+    const uint64_t pad = 1ull << (2 * nb);   // above every real key
+    DBuf<uint64_t> send, recv;
+    MR_TRY(send.alloc(ctx, (size_t)Emax));
+    MR_TRY(recv.alloc(ctx, (size_t)Emax * R));
+    if (N) hipLaunchKernelGGL(k_sh_edge_keys, dim3(cdiv(N, 256)), dim3(256), 0, st, g->ss_off.p, g->ss_par.p, N, nb, send.p);
+    if (Emax > g->E) hipLaunchKernelGGL(k_sh_pad, dim3(cdiv(Emax - g->E, 256)), dim3(256), 0, st, send.p, g->E, Emax, pad);
+    MR_TRY(mr_coll_allgather(ctx, send.p, recv.p, Emax, MR_DT_U64));
+    const int64_t n = Emax * R;
+    SortScratch ws;
+    MR_TRY(mr_radix_sort(ctx, recv.p, nullptr, n, 2 * nb + 1, ws));
+    DBuf<int32_t> head, ccount;
+    DBuf<int64_t> pos, tmp;
+    MR_TRY(head.alloc(ctx, n));
+    MR_TRY(pos.alloc(ctx, n + 1));
+    MR_TRY(tmp.alloc(ctx, std::max(scan_tmp_elems(n), scan_tmp_elems(std::max(N, 1)))));
+    hipLaunchKernelGGL(k_sh_edge_heads, dim3(cdiv(n, 256)), dim3(256), 0, st, recv.p, n, pad, head.p);
+    MR_TRY(mr_exclusive_scan_i32(ctx, head.p, pos.p, n, tmp.p));
+    int64_t E = 0;
+    MR_TRY_HIP(ctx, hipMemcpyAsync(&E, pos.p + n, sizeof E, hipMemcpyDeviceToHost, st));
+    MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+    MR_TRY(ccount.zero(ctx, N));
+    g->ss_par.reset();
+    MR_TRY(g->ss_par.alloc(ctx, (size_t)std::max<int64_t>(E, 1)));
+    hipLaunchKernelGGL(k_sh_edge_out, dim3(cdiv(n, 256)), dim3(256), 0, st, recv.p, head.p, pos.p, n, nb, g->ss_par.p,
+                       ccount.p);
+    MR_TRY(mr_exclusive_scan_i32(ctx, ccount.p, g->ss_off.p, N, tmp.p));
+    g->E = E;
+    MR_TRY_HIP(ctx, hipGetLastError());
+    MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+    return MR_OK;
+}
+
+extern "C" int mr_pagerank_sharded(mr_ctx* ctx, mr_graph* g, int anomaly, double d, double alpha, int iters,
+                                   int precision, uint32_t flags) {
+    if (!ctx || !g || g->ctx != ctx) return mr_fail(ctx, MR_ERR_ARG, "mr_pagerank_sharded: bad handles");
+    if (!mr_coll_ready(ctx) && ctx->nranks != 1) return mr_fail(ctx, MR_ERR_COMM, "no collective backend");
+    if (!g->fused) return mr_fail(ctx, MR_ERR_ARG, "mr_pagerank_sharded needs the fused iteration (N <= %d)", FX_NMAX);
+    MR_TRY_HIP(ctx, hipSetDevice(ctx->device));
+    if (!g->sharded_done) {   // the graph-level exchange happens once per graph
+        MR_TRY(shard_exchange(ctx, g));
+        g->sharded_done = true;
+    }
+    MR_TRY(g->fx_limb.alloc(ctx, 2 * (size_t)std::max(g->N, 1)));
+    return mr_pagerank_batch_impl(ctx, &g, &anomaly, 1, d, alpha, iters, precision, flags, true);
 }

@@ -1,0 +1,95 @@
+"""Trace-sharded PageRank over several processes.
+
+One process per GPU holds a shard of the traces (every span of a trace on one rank) over the
+global node index space.  ``mr_pagerank_sharded`` (csrc/mr_pagerank.hip) exchanges, once per
+graph, the per-op span counts / children counts / coverage, the call edges and the trace-kind
+classes, and per iteration the exact fixed-point P_sr r limbs (uint64 SUM) and max r' (MAX), so
+every rank ends with the weights the whole graph would give.
+
+Collectives run over RCCL (:func:`use_rccl`, xGMI between GPUs) or, for ranks that share a GPU
+or have no RCCL, over a host-staged callback on a ``torch.distributed`` process group
+(:func:`use_host`; gloo in the tests).  torch is the control plane only.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from ._lib import ptr
+
+HOST_COLL = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_int64, C.c_int, C.c_int)
+_NP = {0: np.float64, 1: np.int32, 2: np.int64, 3: np.int64}   # uint64 reduced as int64: same bits
+                                                                 # for sums mod 2^64 and for the
+                                                                 # max of non-negative values
+
+
+class _HostCollectives:
+    """mr_host_coll_fn over a torch.distributed group; keeps the ctypes callback alive."""
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+
+        self.dist, self.group = dist, group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.fn = HOST_COLL(self._call)
+
+    def _call(self, user, coll, buf, n, dtype, op):
+        import torch
+
+        try:
+            dt = _NP[dtype]
+            if coll == 0:
+                a = np.ctypeslib.as_array((C.c_byte * (n * np.dtype(dt).itemsize)).from_address(buf)).view(dt)
+                t = torch.from_numpy(a.copy())
+                self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX if op else self.dist.ReduceOp.SUM, group=self.group)
+                a[:] = t.numpy()
+            else:
+                a = np.ctypeslib.as_array(
+                    (C.c_byte * (n * self.world * np.dtype(dt).itemsize)).from_address(buf)).view(dt)
+                mine = torch.from_numpy(a[self.rank * n:(self.rank + 1) * n].copy())
+                parts = [torch.empty_like(mine) for _ in range(self.world)]
+                self.dist.all_gather(parts, mine, group=self.group)
+                a[:] = torch.cat(parts).numpy()
+            return 0
+        except Exception:   # never raise through C
+            return 1
+
+
+def use_host(ctx: "_lib.Context", group=None):
+    """Host-staged collectives over a torch.distributed group (any backend, e.g. gloo)."""
+    hc = _HostCollectives(group)
+    ctx.check(_lib.load().mr_comm_set_host(ctx.h, C.cast(hc.fn, C.c_void_p), None, hc.world, hc.rank),
+              "mr_comm_set_host")
+    ctx._host_coll = hc
+    return hc
+
+
+def use_rccl(ctx: "_lib.Context", group=None):
+    """RCCL communicator for this context: rank 0's unique id travels over the torch group."""
+    import torch
+    import torch.distributed as dist
+
+    lib = _lib.load()
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    uid = np.zeros(128, np.uint8)
+    if rank == 0:
+        ctx.check(lib.mr_comm_unique_id(ptr(uid, C.c_uint8)), "mr_comm_unique_id")
+    t = torch.from_numpy(uid.copy())
+    dist.broadcast(t, src=0, group=group)
+    uid[:] = t.numpy()
+    ctx.check(lib.mr_comm_init(ctx.h, world, rank, ptr(uid, C.c_uint8)), "mr_comm_init")
+
+
+def sharded_pagerank(dg, anomaly: bool, d: float = 0.85, alpha: float = 0.01, iters: int = 25,
+                     precision: str = "fp64"):
+    """PageRank of the whole graph from this rank's shard ``dg`` (a DeviceGraph whose len_o /
+    nchild are this rank's partial counts and whose call edges are its local ones).  Returns
+    (weights, coverage) of the whole graph, identical on every rank."""
+    lib = _lib.load()
+    prec = _lib.MR_FP32 if precision == "fp32" else _lib.MR_FP64
+    dg.ctx.check(lib.mr_pagerank_sharded(dg.ctx.h, dg.h, int(bool(anomaly)), d, alpha, iters, prec, 0),
+                 "mr_pagerank_sharded")
+    return dg.fetch()
