@@ -368,7 +368,6 @@ struct GDev {
     unsigned long long* fx_part;
     double* fx_ssv;
     unsigned long long* fx_limb;   // sharded: [2N] (lo, hi) limb sums per op
-    int32_t probe;               // diagnostics (MR_FX_PROBE): 1 skip atomics, 2 skip gathers
     unsigned long long* stamp;   // diagnostics (MR_FX_STAMP): per-block phase clocks, else null
     double fx_scale, fx_iscale;
     int32_t T, N, n_tb, n_tiles, tshift, lds_su, blk0, n_ob, blk0b;
@@ -969,6 +968,20 @@ static const bool g_debug = getenv("MR_DEBUG") != nullptr;
 void mr_prof_begin(mr_ctx* ctx);
 void mr_prof_end(mr_ctx* ctx, double bytes);
 
+// traces per k_fx_a block (= its block size): the largest of 1024/512/256 whose LDS image fits
+// (MR_TT caps it for measurements); 0 when none fits
+constexpr size_t FX_LDS_MAX = 160 * 1024 - 512;   // minus the kernel's static LDS
+static int fx_tt(int32_t N) {
+    static const int cap = [] {
+        const char* e = getenv("MR_TT");
+        const int v = e ? atoi(e) : 1024;
+        return (v == 256 || v == 512 || v == 1024) ? v : 1024;
+    }();
+    for (int tt = cap; tt >= 256; tt >>= 1)
+        if (FxLds(N, tt).total <= FX_LDS_MAX) return tt;
+    return 0;
+}
+
 // Derived per-graph arrays: fp32 reciprocals, u16 ids, and the P_sr tiles.  One host round trip
 // (the number of (tile, op) pairs sizes the pair arrays).
 int mr_graph_prepare(mr_ctx* ctx, mr_graph* g) {
@@ -987,7 +1000,7 @@ int mr_graph_prepare(mr_ctx* ctx, mr_graph* g) {
         hipLaunchKernelGGL(k_ids16, dim3(cdiv(g->nnz_rs, 256)), dim3(256), 0, st, g->rs_ops.p, g->nnz_rs, g->rs16.p);
     }
     static const bool no_fused = getenv("MR_NO_FUSED") != nullptr;   // A/B knob: force the tile path
-    g->fused = !no_fused && g->rs_is_sr && g->traces_nonempty && N <= FX_NMAX;
+    g->fused = !no_fused && g->rs_is_sr && g->traces_nonempty && N <= FX_NMAX && fx_tt(N) > 0;
     if (g->fused) {   // no P_sr tiles: the fused iteration reads the trace-major ids only
         MR_TRY_HIP(ctx, hipMemsetAsync(g->cov.p, 0, (size_t)std::max(N, 1) * sizeof(int32_t), st));
         if (nnz && N)
@@ -1080,20 +1093,11 @@ int mr_graph_prepare(mr_ctx* ctx, mr_graph* g) {
     return MR_OK;   // scratch returns to the stream-ordered pool: no sync needed
 }
 
-// traces per k_fx_a block (= its block size; MR_TT overrides for measurements)
-static int fx_tt() {
-    static const int tt = [] {
-        const char* e = getenv("MR_TT");
-        const int v = e ? atoi(e) : 512;
-        return (v == 256 || v == 512 || v == 1024) ? v : 512;
-    }();
-    return tt;
-}
 
 // kinds, preference vector and iteration state of one graph (everything before the iterations)
 static int shard_kinds(mr_ctx* ctx, mr_graph* g, uint64_t cap);
 
-static int pagerank_setup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool fp32, uint32_t flags,
+static int pagerank_setup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool fp32, uint32_t flags, int TT,
                           bool sharded = false) {
     hipStream_t st = ctx->stream;
     const int32_t N = g->N, T = g->T;
@@ -1119,7 +1123,7 @@ static int pagerank_setup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool 
     MR_TRY(g->sub[1].alloc(ctx, (size_t)N + 1));
     MR_TRY(g->weight.alloc(ctx, (size_t)N));
     if (g->fused) {
-        MR_TRY(g->fx_part.alloc(ctx, (size_t)cdiv(T, fx_tt()) * (size_t)N));
+        MR_TRY(g->fx_part.alloc(ctx, (size_t)cdiv(T, TT) * (size_t)N));
         MR_TRY(g->fx_ssv.alloc(ctx, (size_t)N));
     }
     else MR_TRY(g->part.alloc(ctx, (size_t)std::max<int64_t>(g->n_pairs, 1)));
@@ -1187,14 +1191,16 @@ int mr_pagerank_batch_impl(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly,
     MR_TRY_HIP(ctx, hipSetDevice(ctx->device));
     hipStream_t st = ctx->stream;
     const bool fp32 = precision == MR_FP32;
-    for (int i = 0; i < ng; ++i) MR_TRY(pagerank_setup(ctx, gs[i], anomaly[i], d, fp32, flags, sharded));
+    int TT = 1024;   // one block size for the batch: the largest that fits every fused graph
+    for (int i = 0; i < ng; ++i)
+        if (gs[i]->fused) TT = std::min(TT, fx_tt(gs[i]->N));
+    for (int i = 0; i < ng; ++i) MR_TRY(pagerank_setup(ctx, gs[i], anomaly[i], d, fp32, flags, TT, sharded));
     // ---- batched power iteration: one k_iter_a + k_iter_b pair per iteration for every graph
     int mask = 3;
     if (const char* rm = getenv("MR_ROLE_MASK")) mask = atoi(rm);   // profiling knob: 1 trace / 2 op side
     std::vector<GDev> hv((size_t)ng);
     int32_t blocks_a = 0, blocks_b = 0, blocks_fa = 0, blocks_fb = 0;
     size_t lds = VCAP * sizeof(double), lds_f = 0;
-    const int TT = fx_tt();
     const int sc = 63 - (TT == 256 ? 8 : TT == 512 ? 9 : 10);
     double bytes = 0.0;
     for (int i = 0; i < ng; ++i) {
@@ -1227,7 +1233,6 @@ int mr_pagerank_batch_impl(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly,
         v.fx_ssv = g->fx_ssv.p;
         v.fx_limb = (unsigned long long*)g->fx_limb.p;
         v.stamp = nullptr;
-        v.probe = getenv("MR_FX_PROBE") ? atoi(getenv("MR_FX_PROBE")) : 0;
         v.fx_scale = std::ldexp(1.0, sc);
         v.fx_iscale = std::ldexp(1.0, -sc);
         v.T = g->T;

@@ -1,8 +1,8 @@
 // K3: online_rca.calculate_spectrum_without_delay_list (online_rca.py:33-152) on gfx950.
 //
 // One thread per node computes (ef, nf, ep, np) from the two PageRank weight/coverage vectors
-// (:201-225) and applies one of the 13 formulas (:231-298) with the reference's operation
-// order (no FMA contraction).  The stable descending sort (:303) is a sort on the composite
+// (:45-69) and applies one of the 13 formulas (:77-142) with the reference's operation
+// order (no FMA contraction).  The stable descending sort (:147) is a sort on the composite
 // key (score, position): positions break ties exactly like Python's stable `sorted`.  Nodes
 // are in the reference's iteration order: anomaly_result nodes, then normal-only nodes.
 //
@@ -34,24 +34,24 @@ __device__ double spectrum_score(int method, TV ef, TV nf, TV ep, TV np_, bool& 
     const TV two{2.0, false};
     TV r{0.0, false};
     switch (method) {
-        case DSTAR2: r = dv(mul(ef, ef), add(ep, nf), zd); break;                                     // :234
-        case OCHIAI: r = dv(ef, TV{sqrt(add(ep, ef).v * add(ef, nf).v), false}, zd); break;           // :237
-        case JACCARD: r = dv(ef, add(add(ef, ep), nf), zd); break;                                     // :242
-        case SORENSEN: r = dv(mul(two, ef), add(add(mul(two, ef), ep), nf), zd); break;                // :245
-        case M1: r = dv(add(ef, np_), add(ep, nf), zd); break;                                         // :250
-        case M2: r = dv(ef, add(add(add(mul(two, ep), mul(two, nf)), ef), np_), zd); break;            // :253
-        case GOODMAN: r = dv(sub(sub(mul(two, ef), nf), ep), add(add(mul(two, ef), nf), ep), zd); break;  // :257
-        case TARANTULA: {                                                                              // :262
+        case DSTAR2: r = dv(mul(ef, ef), add(ep, nf), zd); break;                                     // :78
+        case OCHIAI: r = dv(ef, TV{sqrt(add(ep, ef).v * add(ef, nf).v), false}, zd); break;           // :81
+        case JACCARD: r = dv(ef, add(add(ef, ep), nf), zd); break;                                     // :86
+        case SORENSEN: r = dv(mul(two, ef), add(add(mul(two, ef), ep), nf), zd); break;                // :89
+        case M1: r = dv(add(ef, np_), add(ep, nf), zd); break;                                         // :94
+        case M2: r = dv(ef, add(add(add(mul(two, ep), mul(two, nf)), ef), np_), zd); break;            // :97
+        case GOODMAN: r = dv(sub(sub(mul(two, ef), nf), ep), add(add(mul(two, ef), nf), ep), zd); break;  // :101
+        case TARANTULA: {                                                                              // :106
             TV a = dv(ef, add(ef, nf), zd);
             TV b = dv(ef, add(ef, nf), zd);
             TV c = dv(ep, add(ep, np_), zd);
             r = dv(a, add(b, c), zd);
         } break;
-        case RUSSELLRAO: r = dv(ef, add(add(add(ef, nf), ep), np_), zd); break;                        // :272
-        case HAMANN: r = dv(sub(sub(add(ef, np_), ep), nf), add(add(add(ef, nf), ep), np_), zd); break;  // :278
-        case DICE: r = dv(mul(two, ef), add(add(ef, nf), ep), zd); break;                              // :285
-        case SIMPLE: r = dv(add(ef, np_), add(add(add(ef, np_), nf), ep), zd); break;                  // :290
-        case ROGERS: r = dv(add(ef, np_), add(add(add(ef, np_), mul(two, nf)), mul(two, ep)), zd); break;  // :296
+        case RUSSELLRAO: r = dv(ef, add(add(add(ef, nf), ep), np_), zd); break;                        // :116
+        case HAMANN: r = dv(sub(sub(add(ef, np_), ep), nf), add(add(add(ef, nf), ep), np_), zd); break;  // :122
+        case DICE: r = dv(mul(two, ef), add(add(ef, nf), ep), zd); break;                              // :128
+        case SIMPLE: r = dv(add(ef, np_), add(add(add(ef, np_), nf), ep), zd); break;                  // :134
+        case ROGERS: r = dv(add(ef, np_), add(add(add(ef, np_), mul(two, nf)), mul(two, ep)), zd); break;  // :140
     }
     res_np = r.np;
     return r.v;
@@ -76,7 +76,7 @@ __global__ void k_spectrum(int32_t n, const uint8_t* flags, const double* a_w, c
     const bool ha = f & 1, hn = f & 2, ta = f & 4, tn = f & 8;
     const TV eps{0.0000001, false};
     TV ef, nf, ep, np_;
-    if (ha) {   // :201-214
+    if (ha) {   // :45-58
         ef = TV{a_w[i] * (double)a_num[i], ta};
         nf = TV{a_w[i] * (double)(A - a_num[i]), ta};
         if (hn) {
@@ -86,7 +86,7 @@ __global__ void k_spectrum(int32_t n, const uint8_t* flags, const double* a_w, c
             ep = eps;
             np_ = eps;
         }
-    } else {    // :216-225 normal-only
+    } else {    // :60-69 normal-only
         ep = TV{(1.0 + n_w[i]) * (double)n_num[i], tn};
         np_ = TV{(double)(Nl - n_num[i]), false};
         ef = eps;

@@ -54,7 +54,7 @@ def calculate_spectrum_without_delay_list(anomaly_result, normal_result, anomaly
         if node in anomaly_result:
             w = anomaly_result[node]
             a_w[i] = w
-            a_num[i] = anomaly_num_list[node]          # KeyError as in the reference (:205)
+            a_num[i] = anomaly_num_list[node]          # KeyError as in the reference (:49)
             ta = _is_np(w)
             has_a[i] = 1 | (2 if ta else 0)
         if node in normal_result:
@@ -67,7 +67,7 @@ def calculate_spectrum_without_delay_list(anomaly_result, normal_result, anomaly
     try:
         method = SPECTRUM_METHODS.index(spectrum_method)
     except ValueError:
-        return [], []                                  # no branch matched: empty result (:231-298)
+        return [], []                                  # no branch matched: empty result (:77-142)
     if n == 0:
         return [], []
     ctx = ctx or _lib.default_context()

@@ -297,15 +297,21 @@ def slo_frame(seed: int = 7, sizes=SLO_SIZES):
 
 
 def big_graph(n_ops: int, n_traces: int, seed: int = 11, spans_mean: float = 19.0, zipf_s: float = 1.1,
-              fp_dup: float = 0.25):
+              fp_dup: float = 0.25, shard: tuple | None = None):
     """A C4/C5-scale op<->trace graph generated directly as incidence lists (no span table):
     per trace ~Poisson(spans_mean) spans whose ops follow a power law (zipf_s) over n_ops, the
     root op in every trace, duplicates within a trace allowed (len_t counts spans, the incidence
     keeps distinct ops); a random call tree over the ops.  Returns a graph.HostGraph with
-    ``nodes``/``traces`` as ranges (names are not needed for timing)."""
+    ``nodes``/``traces`` as ranges (names are not needed for timing).
+
+    ``shard=(rank, world)``: this rank's n_traces traces of a trace-sharded graph:
+    traces from a per-rank stream, the call tree from ``seed`` (the same on every rank); len_o is
+    this rank's partial span count and the call edges / children counts sit on rank 0, which is
+    what mr_pagerank_sharded expects."""
     from .graph import HostGraph
 
-    rng = np.random.default_rng(seed)
+    rank, world = shard if shard is not None else (0, 1)
+    rng = np.random.default_rng(seed if shard is None else (seed, rank, world))
     T, N = int(n_traces), int(n_ops)
     k = np.maximum(rng.poisson(spans_mean - 1.0, T), 1).astype(np.int64) + 1        # spans per trace
     S = int(k.sum())
@@ -326,8 +332,11 @@ def big_graph(n_ops: int, n_traces: int, seed: int = 11, spans_mean: float = 19.
     np.cumsum(np.bincount(tr, minlength=T), out=sr_off[1:])
     del key, tr
     # call tree: every op but the root has one parent of smaller index
+    trng = rng if shard is None else np.random.default_rng(seed)
     child = np.arange(1, N, dtype=np.int64)
-    parent = (rng.random(N - 1) * child).astype(np.int64)
+    parent = (trng.random(N - 1) * child).astype(np.int64)
+    if rank != 0:
+        child, parent = child[:0], parent[:0]
     order = np.lexsort((parent, child))
     ss_off = np.zeros(N + 1, np.int64)
     np.cumsum(np.bincount(child[order], minlength=N), out=ss_off[1:])
