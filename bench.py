@@ -145,6 +145,110 @@ def cpu_baseline(abnormal, t0, t1, a3, ok, target_s=12.0):
             "windows_per_s": round(n / el, 4)}, res
 
 
+def c4_cpu_baseline(n_ops, n_traces, target_s=15.0):
+    """25 power iterations of a C4-shaped graph of n_traces traces on the host: the oracle's numpy
+    restatement (bincount SpMV per product), one core.  Preference = uniform (the iteration cost
+    does not depend on it); kinds are not part of this timing."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as orc
+
+    from microrank_amd import synth
+
+    hg = synth.big_graph(n_ops, n_traces, seed=5)
+    T, N = hg.T, hg.N
+    sr_t = np.repeat(np.arange(T, dtype=np.int64), np.diff(hg.sr_off))
+    sr_o = hg.sr_ops.astype(np.int64)
+    ss_c = np.repeat(np.arange(N, dtype=np.int64), np.diff(hg.ss_off))
+    g = orc.Graph(list(range(N)), list(range(T)), sr_t, sr_o, sr_t, sr_o, hg.len_t, hg.len_o, ss_c,
+                  hg.ss_par.astype(np.int64), hg.nchild, np.arange(T), hg.len_t.copy())
+    v = np.full(T, 1.0 / T, np.float32)
+    n, edges, t_start = 0, 0, time.perf_counter()
+    while True:
+        orc.power_iteration(g, v)
+        n += 1
+        edges += 25 * (2 * sr_o.size + ss_c.size)
+        el = time.perf_counter() - t_start
+        if el >= target_s or n >= 5:
+            break
+    return {"value": round(edges / el / 1e9, 4), "unit": "GTEPS", "cores": 1, "kind": "port",
+            "sample": f"{n} x 25 power iterations of a {T}-trace / {N}-op graph (same generator), "
+                      f"oracle numpy restatement, {el:.1f} s"}
+
+
+def run_c4(args, world, rank, dist):
+    """C4: one 10k-op / 10M-trace graph sharded by trace over the ranks (strong scaling); a step is
+    one whole trace_pagerank of the graph (kinds, preference, 25 iterations with the per-iteration
+    exact limb all-reduce over RCCL)."""
+    import ctypes as C
+
+    from microrank_amd import _lib, shard, synth
+    from microrank_amd.graph import DeviceGraph
+
+    t_local = args.c4_traces // world + (1 if rank < args.c4_traces % world else 0)
+    hg = synth.big_graph(args.c4_ops, t_local, seed=11, shard=(rank, world))
+    nnz_local = int(hg.sr_ops.size)
+    ctx = _lib.default_context()
+    if world > 1:
+        shard.use_rccl(ctx)
+    dg = DeviceGraph.upload(ctx, hg)
+    del hg
+    prec = args.precision
+    for _ in range(max(args.warmup, 1)):   # the first call also runs the once-per-graph exchange
+        shard.sharded_pagerank(dg, True, precision=prec)
+    E = dg.info()["E"]
+    load = _lib.load()
+    load.mr_ctx_profile(ctx.h, 1)
+    ctx.sync()
+    if dist is not None:
+        dist.barrier()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        w, cov = shard.sharded_pagerank(dg, True, precision=prec)
+    ctx.sync()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    launches, kms, kbytes = C.c_int64(), C.c_double(), C.c_double()
+    load.mr_ctx_prof_read(ctx.h, C.byref(launches), C.byref(kms), C.byref(kbytes))
+    nnz_all = float(nnz_local)
+    if dist is not None:
+        import torch
+
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t[0])
+        t = torch.tensor([nnz_all], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        nnz_all = float(t[0])
+    if rank != 0:
+        return None
+    avg_ms = kms.value / max(launches.value, 1)
+    achieved = (kbytes.value / max(launches.value, 1)) / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+    edges = 25.0 * (2.0 * nnz_all + E) * args.steps
+    out = {
+        "metric": "PageRank GTEPS + RCA windows ranked/sec at 1/2/4/8 MI355X; % HBM roofline",
+        "value": round(edges / elapsed / 1e9, 3), "unit": "GTEPS", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "f64" if prec == "fp64" else "f32",
+        "data": "synthetic (power-law op popularity, root op in every trace, random call tree; per-rank shards)",
+        "config": {"workload": f"C4 sharded trace_pagerank: {args.c4_ops} ops / {args.c4_traces} traces over "
+                               f"{world} GPU(s), anomaly preference, 25 iterations", "nnz": int(nnz_all), "call_edges": E,
+                   "parallelism": f"trace shards x{world}, RCCL limb all-reduce per iteration"},
+        "roofline": {"bound": "hbm", "kernel": "one Jacobi iteration on this rank (k_fx_a + k_fx_b"
+                                               + (" + 2 all-reduces)" if world > 1 else ")"),
+                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "avg_launch_us": round(avg_ms * 1e3, 3), "launches": launches.value,
+                     "bytes_per_launch": round(kbytes.value / max(launches.value, 1))},
+    }
+    if not args.no_cpu and world == 1:
+        try:
+            out["cpu_baseline"] = c4_cpu_baseline(args.c4_ops, 1_000_000)
+        except Exception as e:
+            out["cpu_baseline"] = {"value": None, "error": f"{type(e).__name__}: {e}"}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -156,6 +260,10 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC passes for roofline.traffic")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--config", choices=["c2", "c4"], default="c2",
+                    help="c2: RCA windows (default, weak scaling); c4: one trace-sharded graph (strong scaling)")
+    ap.add_argument("--c4-ops", type=int, default=10_000)
+    ap.add_argument("--c4-traces", type=int, default=10_000_000)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -163,7 +271,7 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # PMC passes first, in child processes, before this process initialises the GPU
     traffic = None
-    if world == 1 and not args.pmc_child and not args.no_traffic:
+    if world == 1 and not args.pmc_child and not args.no_traffic and args.config == "c2":
         traffic = pmc_traffic(args)
     dist = None
     if world > 1:
@@ -171,6 +279,14 @@ def main():
 
         dist.init_process_group("gloo")
     os.environ.setdefault("MICRORANK_DEVICE", str(local))
+    if args.config == "c4":
+        out = run_c4(args, world, rank, dist)
+        if out is not None:
+            print(json.dumps(out), flush=True)
+        if dist is not None:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
 
     from microrank_amd import _lib
     from microrank_amd.preprocess_data import DeviceSpans
@@ -241,7 +357,7 @@ def main():
                    "n_spans": int(abnormal.n_spans), "n_abnormal": na, "n_normal": nn,
                    "edges_per_window": int(edges // max(args.steps, 1)), "parallelism": f"windows x{world}"},
         "windows_per_s": round(world * args.steps / elapsed, 3),
-        "roofline": {"bound": "hbm", "kernel": "one Jacobi iteration: k_fx_a + k_fx_b (fused path, N <= 8192)",
+        "roofline": {"bound": "hbm", "kernel": "one Jacobi iteration: k_fx_a + k_fx_b (fused path)",
                      "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": None if traffic is None else round(traffic["fetch"] + traffic["write"]),

@@ -372,6 +372,7 @@ struct GDev {
     double fx_scale, fx_iscale;
     int32_t T, N, n_tb, n_tiles, tshift, lds_su, blk0, n_ob, blk0b;
     int32_t blk0f, n_fa, blk0fb, n_fb;   // fused path: k_fx_a / k_fx_b block ranges
+    int32_t fx_k;                        // tiles of TT traces per k_fx_a block
 };
 
 // graph owning block `blk` of launch kind `which` (0 k_iter_a, 1 k_iter_b, 2 k_fx_a, 3 k_fx_b);
@@ -599,11 +600,7 @@ __global__ void __launch_bounds__(1024) k_fx_a(const GDev* __restrict__ gs, int3
     const int32_t lb = (int32_t)blockIdx.x - G.blk0f;
     const int cur = it & 1, nxt = cur ^ 1, k3 = it % 3;
     const int32_t T = G.T, N = G.N;
-    const int32_t t0 = lb * TT;
-    const int32_t nt = min(TT, T - t0);
     const int32_t i = (int32_t)threadIdx.x;
-    const int32_t t = t0 + i;
-    const bool own = i < nt;
     const FxLds L_(N, TT);
     const double* sug = G.sub[cur];   // N + 1 entries, sub[N] = 0 (the pad slot)
     double* su_l = (double*)(lraw + L_.su);
@@ -617,35 +614,11 @@ __global__ void __launch_bounds__(1024) k_fx_a(const GDev* __restrict__ gs, int3
     int32_t* owner = (int32_t*)(lraw + L_.owner);
     uint32_t* hbits = (uint32_t*)(lraw + L_.hbits);
     uint16_t* ids = (uint16_t*)(lraw + L_.ids);
-    // every independent load of the block goes out before the first barrier
-    const int64_t e0 = G.rs_off[t0], e1 = G.rs_off[t0 + nt];
-    const int64_t a = own ? G.rs_off[t] : 0, b = own ? G.rs_off[t + 1] : 0;
-    const double qk = own ? (double)((const Q*)G.q[cur])[t] : 0.0;
-    const float ct = own ? G.c_t[t] : 0.0f, wt = own ? G.w_t[t] : 0.0f;
     unsigned long long* mslot = G.mslot;
     const unsigned long long* Mcur = mslot + (size_t)2 * MSH * k3;
     unsigned long long* Mnext = mslot + (size_t)2 * MSH * ((k3 + 1) % 3);
     if (lb == 0 && i < 2 * MSH) mslot[(size_t)2 * MSH * ((k3 + 2) % 3) + i] = 0ull;
-    const int64_t base = e0 & ~(int64_t)7;
-    const int32_t shift = (int32_t)(e0 - base);
-    const int64_t np_ = e1 - base;                 // positions [shift, np_) hold the block's entries
-    const bool bal = np_ <= (int64_t)FX_CAP * TT;
-    if (bal) {   // stage the id range: 16-B loads of 8 ids (the buffer is padded past nnz)
-        const uint4* src = (const uint4*)(G.rs16 + base);
-        const int32_t nch = (int32_t)((np_ + 7) >> 3);
-        uint4 v[FX_CAP / 8];
-#pragma unroll
-        for (int j = 0; j < FX_CAP / 8; ++j) v[j] = src[min(i + j * TT, nch - 1)];
-#pragma unroll
-        for (int j = 0; j < FX_CAP / 8; ++j)
-            if (i + j * TT < nch) *(uint4*)(ids + (size_t)(i + j * TT) * 8) = v[j];
-        for (int32_t w = i; w < FX_CAP * TT / 32 + 2; w += TT) hbits[w] = 0u;
-        if (i == 0) {
-            owner[0] = -1;   // positions before `shift` belong to the previous block
-            xl[0] = 0ull;
-        }
-    }
-    for (int32_t o = i; o <= N; o += TT) {
+    for (int32_t o = i; o <= N; o += TT) {   // once per block: the accumulator spans all its tiles
         if (L_.su_lds) su_l[o] = o < N ? sug[o] : 0.0;
         lacc[o] = 0ull;
     }
@@ -657,100 +630,140 @@ __global__ void __launch_bounds__(1024) k_fx_a(const GDev* __restrict__ gs, int3
             msh[1] = mr;
         }
     }
-    if (own) toff[i] = (int32_t)(a - base);
-    if (i == 0) toff[nt] = (int32_t)np_;
-    __syncthreads();
-    const unsigned long long X = own ? (unsigned long long)__double2ull_rn(qk / msh[1] * G.fx_scale) : 0ull;
-    if (G.stamp && i == 0) G.stamp[(size_t)blockIdx.x * 8 + 1] = __builtin_amdgcn_s_memrealtime();
-    double acc = 0.0;
-    if (bal) {
-        int32_t L = (int32_t)((np_ + 8 * TT - 1) / (8 * TT)) * 8;
-        if (L == 0) L = 8;
-        const int32_t ra = (int32_t)(a - base), rb = (int32_t)(b - base);
-        if (own) {
-            xl[i + 1] = X;
-            atomicOr(&hbits[ra >> 5], 1u << (ra & 31));
-            for (int32_t sg = (ra + L - 1) / L; sg * L < rb; ++sg) owner[sg] = i;   // segments starting in t
+    const int32_t n_tiles = (T + TT - 1) / TT;
+    const int32_t tb = lb * G.fx_k, te = min(tb + G.fx_k, n_tiles);
+    double rmax = -__builtin_huge_val();
+    for (int32_t tile = tb; tile < te; ++tile) {
+        const bool first = tile == tb;
+        const int32_t t0 = tile * TT;
+        const int32_t nt = min(TT, T - t0);
+        const int32_t t = t0 + i;
+        const bool own = i < nt;
+        // every independent load of the tile goes out before its first barrier
+        const int64_t e0 = G.rs_off[t0], e1 = G.rs_off[t0 + nt];
+        const int64_t a = own ? G.rs_off[t] : 0, b = own ? G.rs_off[t + 1] : 0;
+        const double qk = own ? (double)((const Q*)G.q[cur])[t] : 0.0;
+        const float ct = own ? G.c_t[t] : 0.0f, wt = own ? G.w_t[t] : 0.0f;
+        const int64_t base = e0 & ~(int64_t)7;
+        const int32_t shift = (int32_t)(e0 - base);
+        const int64_t np_ = e1 - base;                 // positions [shift, np_) hold the tile's entries
+        const bool bal = np_ <= (int64_t)FX_CAP * TT;
+        if (!first) __syncthreads();                   // the previous tile's readers are done
+        if (bal) {   // stage the id range: 16-B loads of 8 ids (the buffer is padded past nnz)
+            const uint4* src = (const uint4*)(G.rs16 + base);
+            const int32_t nch = (int32_t)((np_ + 7) >> 3);
+            uint4 v[FX_CAP / 8];
+#pragma unroll
+            for (int j = 0; j < FX_CAP / 8; ++j) v[j] = src[min(i + j * TT, nch - 1)];
+#pragma unroll
+            for (int j = 0; j < FX_CAP / 8; ++j)
+                if (i + j * TT < nch) *(uint4*)(ids + (size_t)(i + j * TT) * 8) = v[j];
+            for (int32_t w = i; w < FX_CAP * TT / 32 + 2; w += TT) hbits[w] = 0u;
+            if (i == 0) {
+                owner[0] = -1;   // positions before `shift` belong to the previous tile
+                xl[0] = 0ull;
+            }
         }
+        if (own) toff[i] = (int32_t)(a - base);
+        if (i == 0) toff[nt] = (int32_t)np_;
         __syncthreads();
-        if (G.stamp && i == 0) G.stamp[(size_t)blockIdx.x * 8 + 2] = __builtin_amdgcn_s_memrealtime();
-        const int32_t p = i * L;
-        if (p < np_) {
-            const int32_t qe = (int32_t)min((int64_t)p + L, np_);
-            const unsigned long long bits =
-                (((unsigned long long)hbits[(p >> 5) + 1] << 32) | hbits[p >> 5]) >> (p & 31);
-            int32_t c = owner[i];
-            bool st = bits & 1ull;                   // the segment's first piece starts a trace
-            unsigned long long Xc = xl[c + 1];
-            for (int32_t ch = p; ch < qe; ch += 8) {
-                const uint4 w = *(const uint4*)(ids + ch);   // 8 ids, 16-B aligned (ch % 8 == 0)
-                int32_t o[8];
-                o[0] = (int32_t)(w.x & 0xffffu); o[1] = (int32_t)(w.x >> 16);
-                o[2] = (int32_t)(w.y & 0xffffu); o[3] = (int32_t)(w.y >> 16);
-                o[4] = (int32_t)(w.z & 0xffffu); o[5] = (int32_t)(w.z >> 16);
-                o[6] = (int32_t)(w.w & 0xffffu); o[7] = (int32_t)(w.w >> 16);
+        const unsigned long long X = own ? (unsigned long long)__double2ull_rn(qk / msh[1] * G.fx_scale) : 0ull;
+        if (G.stamp && i == 0 && first) G.stamp[(size_t)blockIdx.x * 8 + 1] = __builtin_amdgcn_s_memrealtime();
+        double acc = 0.0;
+        if (bal) {
+            int32_t L = (int32_t)((np_ + 8 * TT - 1) / (8 * TT)) * 8;
+            if (L == 0) L = 8;
+            const int32_t ra = (int32_t)(a - base), rb = (int32_t)(b - base);
+            if (own) {
+                xl[i + 1] = X;
+                atomicOr(&hbits[ra >> 5], 1u << (ra & 31));
+                for (int32_t sg = (ra + L - 1) / L; sg * L < rb; ++sg) owner[sg] = i;   // segments starting in t
+            }
+            __syncthreads();
+            if (G.stamp && i == 0 && first) G.stamp[(size_t)blockIdx.x * 8 + 2] = __builtin_amdgcn_s_memrealtime();
+            const int32_t p = i * L;
+            if (p < np_) {
+                const int32_t qe = (int32_t)min((int64_t)p + L, np_);
+                const unsigned long long bits =
+                    (((unsigned long long)hbits[(p >> 5) + 1] << 32) | hbits[p >> 5]) >> (p & 31);
+                int32_t c = owner[i];
+                bool st = bits & 1ull;                   // the segment's first piece starts a trace
+                unsigned long long Xc = xl[c + 1];
+                for (int32_t ch = p; ch < qe; ch += 8) {
+                    const uint4 w = *(const uint4*)(ids + ch);   // 8 ids, 16-B aligned (ch % 8 == 0)
+                    int32_t o[8];
+                    o[0] = (int32_t)(w.x & 0xffffu); o[1] = (int32_t)(w.x >> 16);
+                    o[2] = (int32_t)(w.y & 0xffffu); o[3] = (int32_t)(w.y >> 16);
+                    o[4] = (int32_t)(w.z & 0xffffu); o[5] = (int32_t)(w.z >> 16);
+                    o[6] = (int32_t)(w.w & 0xffffu); o[7] = (int32_t)(w.w >> 16);
 #pragma unroll
-                for (int j = 0; j < 8; ++j)
-                    if (ch + j < shift || ch + j >= qe) o[j] = N;   // outside the block: the zero slot
-                double g[8];
+                    for (int j = 0; j < 8; ++j)
+                        if (ch + j < shift || ch + j >= qe) o[j] = N;   // outside the tile: the zero slot
+                    double g[8];
 #pragma unroll
-                for (int j = 0; j < 8; ++j) g[j] = su[o[j]];
+                    for (int j = 0; j < 8; ++j) g[j] = su[o[j]];
 #pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const int32_t e = ch + j;
-                    if (e > p && e < qe && ((bits >> (e - p)) & 1ull)) {   // a new trace starts at e
-                        if (st) tsum[c] = acc; else head[i] = acc;
-                        acc = 0.0;
-                        st = true;
-                        ++c;
-                        Xc = xl[c + 1];
+                    for (int j = 0; j < 8; ++j) {
+                        const int32_t e = ch + j;
+                        if (e > p && e < qe && ((bits >> (e - p)) & 1ull)) {   // a new trace starts at e
+                            if (st) tsum[c] = acc; else head[i] = acc;
+                            acc = 0.0;
+                            st = true;
+                            ++c;
+                            Xc = xl[c + 1];
+                        }
+                        acc += g[j];
+                        atomicAdd(&lacc[o[j]], Xc);
                     }
-                    acc += g[j];
-                    atomicAdd(&lacc[o[j]], Xc);
+                }
+                const bool ends = qe == np_ || ((bits >> (qe - p)) & 1ull);
+                if (st) {
+                    if (ends) tsum[c] = acc; else tail[i] = acc;
+                } else {
+                    head[i] = acc;
                 }
             }
-            const bool ends = qe == np_ || ((bits >> (qe - p)) & 1ull);
-            if (st) {
-                if (ends) tsum[c] = acc; else tail[i] = acc;
+            __syncthreads();
+            if (G.stamp && i == 0 && first) G.stamp[(size_t)blockIdx.x * 8 + 3] = __builtin_amdgcn_s_memrealtime();
+            if (own && rb > ra) {
+                const int32_t sa = ra / L, sb = (rb - 1) / L;
+                if (sa == sb) {
+                    acc = tsum[i];
+                } else {
+                    acc = tail[sa];
+                    for (int32_t sg = sa + 1; sg <= sb; ++sg) acc += head[sg];
+                }
             } else {
-                head[i] = acc;
-            }
-        }
-        __syncthreads();
-        if (G.stamp && i == 0) G.stamp[(size_t)blockIdx.x * 8 + 3] = __builtin_amdgcn_s_memrealtime();
-        if (own && rb > ra) {
-            const int32_t sa = ra / L, sb = (rb - 1) / L;
-            if (sa == sb) {
-                acc = tsum[i];
-            } else {
-                acc = tail[sa];
-                for (int32_t sg = sa + 1; sg <= sb; ++sg) acc += head[sg];
+                acc = 0.0;
             }
         } else {
-            acc = 0.0;
-        }
-    } else {
-        // long block (rare): thread per trace in rounds of FX_CAP*TT staged ids, 8-entry chunks
-        const int32_t cap = FX_CAP * TT;
-        const int lane = i & (WAVE - 1);
-        for (int64_t lo = e0; lo < e1; lo += cap) {
-            const int64_t hi = min(lo + (int64_t)cap, e1);
-            __syncthreads();
-            for (int64_t e = lo + i; e < hi; e += TT) ids[e - lo] = G.rs16[e];
-            __syncthreads();
-            const int32_t x0 = (int32_t)(max(a, lo) - lo), x1 = (int32_t)(min(b, hi) - lo);
-            for (int32_t c = x0; c < x1; c += 8) {
-                int32_t o[8];
+            // long tile (rare): thread per trace in rounds of FX_CAP*TT staged ids, 8-entry chunks
+            const int32_t cap = FX_CAP * TT;
+            const int lane = i & (WAVE - 1);
+            for (int64_t lo = e0; lo < e1; lo += cap) {
+                const int64_t hi = min(lo + (int64_t)cap, e1);
+                __syncthreads();
+                for (int64_t e = lo + i; e < hi; e += TT) ids[e - lo] = G.rs16[e];
+                __syncthreads();
+                const int32_t x0 = (int32_t)(max(a, lo) - lo), x1 = (int32_t)(min(b, hi) - lo);
+                for (int32_t c = x0; c < x1; c += 8) {
+                    int32_t o[8];
 #pragma unroll
-                for (int j = 0; j < 8; ++j) o[j] = c + j < x1 ? (int32_t)ids[c + j] : N;
-                double g[8];
+                    for (int j = 0; j < 8; ++j) o[j] = c + j < x1 ? (int32_t)ids[c + j] : N;
+                    double g[8];
 #pragma unroll
-                for (int j = 0; j < 8; ++j) g[j] = su[o[j]];
+                    for (int j = 0; j < 8; ++j) g[j] = su[o[j]];
 #pragma unroll
-                for (int j = 0; j < 8; ++j) acc += g[j];
+                    for (int j = 0; j < 8; ++j) acc += g[j];
 #pragma unroll
-                for (int j = 0; j < 8; ++j) atomicAdd(&lacc[o[(j + lane) & 7]], X);
+                    for (int j = 0; j < 8; ++j) atomicAdd(&lacc[o[(j + lane) & 7]], X);
+                }
             }
+        }
+        if (own) {
+            const double rp = d * (acc / msh[0]) + (double)ct;   // pagerank.py:125
+            ((Q*)G.q[nxt])[t] = (Q)((double)wt * rp);
+            rmax = nmax(rmax, rp);
         }
     }
     // call-graph term for the next s' (pagerank.py:122-124, alpha P_ss s_k), a thread per op
@@ -768,12 +781,6 @@ __global__ void __launch_bounds__(1024) k_fx_a(const GDev* __restrict__ gs, int3
     if (G.stamp && i == 0) G.stamp[(size_t)blockIdx.x * 8 + 5] = __builtin_amdgcn_s_memrealtime();
     unsigned long long* prow = G.fx_part + (size_t)lb * N;
     for (int32_t o = i; o < N; o += TT) prow[o] = lacc[o];
-    double rmax = -__builtin_huge_val();
-    if (own) {
-        const double rp = d * (acc / msh[0]) + (double)ct;   // pagerank.py:125
-        ((Q*)G.q[nxt])[t] = (Q)((double)wt * rp);
-        rmax = rp;
-    }
     rmax = block_max(rmax, red);
     if (i == 0) {
         atomicMax(&Mnext[MSH + blockIdx.x % MSH], d2bits(rmax));
@@ -784,57 +791,62 @@ __global__ void __launch_bounds__(1024) k_fx_a(const GDev* __restrict__ gs, int3
     }
 }
 
-// mode 0: whole graph; sharded graphs split it around the limb all-reduce: mode 1 writes this
-// rank's limbs (lo, hi) per op to fx_limb, mode 2 finishes from the reduced limbs
-__global__ void __launch_bounds__(TB) k_fx_b(const GDev* __restrict__ gs, int32_t ng, int32_t split, double d, int it,
-                                             int mode) {
+// Column sums of the partial rows: a block per chunk of FB_OPS consecutive ops (lane = op, so
+// every row read is one coalesced 512-B segment), its FB_W waves splitting the rows; the waves'
+// limb sums meet in LDS (integers: order-free).  mode 0: whole graph; sharded graphs split it
+// around the limb all-reduce: mode 1 writes this rank's limbs (lo, hi) per op to fx_limb, mode 2
+// finishes from the reduced limbs.
+constexpr int FB_OPS = WAVE, FB_W = 16;
+__global__ void __launch_bounds__(FB_OPS * FB_W) k_fx_b(const GDev* __restrict__ gs, int32_t ng, int32_t split,
+                                                       double d, int it, int mode) {
+    __shared__ unsigned long long slo[FB_W][FB_OPS], shi[FB_W][FB_OPS];
     const GDev& G = gs[fx_graph(gs, ng, split, 3)];
-    const int32_t o = ((int32_t)blockIdx.x - G.blk0fb) * (TB / WAVE) + (int32_t)(threadIdx.x / WAVE);
-    if (o >= G.N) return;
-    const int lane = threadIdx.x & (WAVE - 1);
-    const int nxt = (it & 1) ^ 1, k3 = it % 3;
-    unsigned long long* Mnext = G.mslot + (size_t)2 * MSH * ((k3 + 1) % 3);
-    const int32_t nb = G.n_fa, N = G.N;
-    const double ssv = G.fx_ssv[o];
-    const float uo = G.u_o[o];
-    const unsigned long long* __restrict__ col = G.fx_part + o;
+    const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
+    const int32_t o = ((int32_t)blockIdx.x - G.blk0fb) * FB_OPS + lane;
+    const int32_t N = G.N, nb = G.n_fa;
+    const bool on = o < N;
     unsigned long long lo = 0ull, hi = 0ull;
-    int32_t i = mode == 2 ? nb : lane;
-    for (; i + 3 * WAVE < nb; i += 4 * WAVE) {
-        const unsigned long long v0 = col[(size_t)i * N], v1 = col[(size_t)(i + WAVE) * N],
-                                 v2 = col[(size_t)(i + 2 * WAVE) * N], v3 = col[(size_t)(i + 3 * WAVE) * N];
-        lo += (v0 & 0xffffffffull) + (v1 & 0xffffffffull) + (v2 & 0xffffffffull) + (v3 & 0xffffffffull);
-        hi += (v0 >> 32) + (v1 >> 32) + (v2 >> 32) + (v3 >> 32);
+    if (on && mode != 2) {
+        const unsigned long long* __restrict__ col = G.fx_part + o;
+        int32_t r = w;
+        for (; r + 3 * FB_W < nb; r += 4 * FB_W) {
+            const unsigned long long v0 = col[(size_t)r * N], v1 = col[(size_t)(r + FB_W) * N],
+                                     v2 = col[(size_t)(r + 2 * FB_W) * N], v3 = col[(size_t)(r + 3 * FB_W) * N];
+            lo += (v0 & 0xffffffffull) + (v1 & 0xffffffffull) + (v2 & 0xffffffffull) + (v3 & 0xffffffffull);
+            hi += (v0 >> 32) + (v1 >> 32) + (v2 >> 32) + (v3 >> 32);
+        }
+        for (; r < nb; r += FB_W) {
+            const unsigned long long v = col[(size_t)r * N];
+            lo += v & 0xffffffffull;
+            hi += v >> 32;
+        }
     }
-    for (; i < nb; i += WAVE) {
-        const unsigned long long v = col[(size_t)i * N];
-        lo += v & 0xffffffffull;
-        hi += v >> 32;
-    }
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) {
-        lo += __shfl_xor(lo, m, WAVE);
-        hi += __shfl_xor(hi, m, WAVE);
+    slo[w][lane] = lo;
+    shi[w][lane] = hi;
+    __syncthreads();
+    if (w != 0 || !on) return;
+    lo = hi = 0ull;
+    for (int k = 0; k < FB_W; ++k) {
+        lo += slo[k][lane];
+        hi += shi[k][lane];
     }
     if (mode == 1) {
-        if (lane == 0) {
-            G.fx_limb[2 * o] = lo;
-            G.fx_limb[2 * o + 1] = hi;
-        }
+        G.fx_limb[2 * o] = lo;
+        G.fx_limb[2 * o + 1] = hi;
         return;
     }
     if (mode == 2) {
         lo = G.fx_limb[2 * o];
         hi = G.fx_limb[2 * o + 1];
     }
-    // hi, lo < 2^53 (fewer than 2^21 blocks over all ranks): both conversions exact, one rounding
+    const int nxt = (it & 1) ^ 1, k3 = it % 3;
+    unsigned long long* Mnext = G.mslot + (size_t)2 * MSH * ((k3 + 1) % 3);
+    // hi, lo < 2^53 (fewer than 2^21 rows over all ranks): both conversions exact, one rounding
     const double sum = ((double)hi * 4294967296.0 + (double)lo) * G.fx_iscale;
-    if (lane == 0) {
-        const double v = d * (sum + ssv);      // pagerank.py:122-124
-        G.spb[nxt][o] = v;
-        G.sub[nxt][o] = (double)uo * v;
-        atomicMax(&Mnext[o % MSH], d2bits(v));
-    }
+    const double v = d * (sum + G.fx_ssv[o]);      // pagerank.py:122-124
+    G.spb[nxt][o] = v;
+    G.sub[nxt][o] = (double)G.u_o[o] * v;
+    atomicMax(&Mnext[o % MSH], d2bits(v));
 }
 
 // result = s/max(s) (pagerank.py:126,129); weight = result * sum(result) / N (:93-107)
@@ -982,6 +994,15 @@ static int fx_tt(int32_t N) {
     return 0;
 }
 
+// tiles of TT traces per k_fx_a block: about 1024 blocks, so the dense partial rows (N per block)
+// stay a small fraction of the iteration's bytes; k*TT <= 2^15 keeps the fixed-point scale >= 2^48
+static int fx_k(int32_t T, int TT) {
+    const int64_t tiles = (T + TT - 1) / TT;
+    int k = 1;
+    while (k * 2 * (int64_t)TT <= 32768 && tiles / (k * 2) >= 1024) k *= 2;
+    return k;
+}
+
 // Derived per-graph arrays: fp32 reciprocals, u16 ids, and the P_sr tiles.  One host round trip
 // (the number of (tile, op) pairs sizes the pair arrays).
 int mr_graph_prepare(mr_ctx* ctx, mr_graph* g) {
@@ -1123,7 +1144,7 @@ static int pagerank_setup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool 
     MR_TRY(g->sub[1].alloc(ctx, (size_t)N + 1));
     MR_TRY(g->weight.alloc(ctx, (size_t)N));
     if (g->fused) {
-        MR_TRY(g->fx_part.alloc(ctx, (size_t)cdiv(T, TT) * (size_t)N));
+        MR_TRY(g->fx_part.alloc(ctx, (size_t)cdiv(cdiv(T, TT), fx_k(T, TT)) * (size_t)N));
         MR_TRY(g->fx_ssv.alloc(ctx, (size_t)N));
     }
     else MR_TRY(g->part.alloc(ctx, (size_t)std::max<int64_t>(g->n_pairs, 1)));
@@ -1201,7 +1222,6 @@ int mr_pagerank_batch_impl(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly,
     std::vector<GDev> hv((size_t)ng);
     int32_t blocks_a = 0, blocks_b = 0, blocks_fa = 0, blocks_fb = 0;
     size_t lds = VCAP * sizeof(double), lds_f = 0;
-    const int sc = 63 - (TT == 256 ? 8 : TT == 512 ? 9 : 10);
     double bytes = 0.0;
     for (int i = 0; i < ng; ++i) {
         mr_graph* g = gs[i];
@@ -1233,15 +1253,19 @@ int mr_pagerank_batch_impl(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly,
         v.fx_ssv = g->fx_ssv.p;
         v.fx_limb = (unsigned long long*)g->fx_limb.p;
         v.stamp = nullptr;
+        v.fx_k = fx_k(g->T, TT);
+        // a row entry stays below 2^63; shards of one graph hold different trace counts, and their
+        // limbs are summed, so they share the scale of the largest block (2^15 traces)
+        const int sc = 63 - (sharded ? 15 : bits_for((uint64_t)v.fx_k * TT - 1));
         v.fx_scale = std::ldexp(1.0, sc);
         v.fx_iscale = std::ldexp(1.0, -sc);
         v.T = g->T;
         v.N = g->N;
         v.blk0f = blocks_fa;
-        v.n_fa = g->fused ? cdiv(g->T, TT) : 0;
+        v.n_fa = g->fused ? cdiv(cdiv(g->T, TT), v.fx_k) : 0;
         blocks_fa += v.n_fa;
         v.blk0fb = blocks_fb;
-        v.n_fb = g->fused ? cdiv(g->N, TB / WAVE) : 0;
+        v.n_fb = g->fused ? cdiv(g->N, FB_OPS) : 0;
         blocks_fb += v.n_fb;
         v.blk0 = blocks_a;
         v.blk0b = blocks_b;
@@ -1276,12 +1300,12 @@ int mr_pagerank_batch_impl(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly,
             else hipLaunchKernelGGL(k_fx_a<double>, dim3(blocks_fa), dim3(TT), lds_f, st, dv.p, ng, split_fa, d, alpha, it);
             MR_DEBUG_CHECK(ctx, "k_fx_a");
             if (!sharded) {
-                hipLaunchKernelGGL(k_fx_b, dim3(blocks_fb), dim3(TB), 0, st, dv.p, ng, split_fb, d, it, 0);
+                hipLaunchKernelGGL(k_fx_b, dim3(blocks_fb), dim3(FB_OPS * FB_W), 0, st, dv.p, ng, split_fb, d, it, 0);
             } else {   // r' max and the P_sr r limbs over all ranks (exact: integers, max)
                 MR_TRY(mr_coll_allreduce(ctx, gs[0]->mslot.p + (size_t)2 * MSH * ((it + 1) % 3) + MSH, MSH, MR_DT_U64, 1));
-                hipLaunchKernelGGL(k_fx_b, dim3(blocks_fb), dim3(TB), 0, st, dv.p, ng, split_fb, d, it, 1);
+                hipLaunchKernelGGL(k_fx_b, dim3(blocks_fb), dim3(FB_OPS * FB_W), 0, st, dv.p, ng, split_fb, d, it, 1);
                 MR_TRY(mr_coll_allreduce(ctx, gs[0]->fx_limb.p, 2 * (int64_t)gs[0]->N, MR_DT_U64, 0));
-                hipLaunchKernelGGL(k_fx_b, dim3(blocks_fb), dim3(TB), 0, st, dv.p, ng, split_fb, d, it, 2);
+                hipLaunchKernelGGL(k_fx_b, dim3(blocks_fb), dim3(FB_OPS * FB_W), 0, st, dv.p, ng, split_fb, d, it, 2);
             }
             MR_DEBUG_CHECK(ctx, "k_fx_b");
         }
