@@ -372,7 +372,7 @@ struct GDev {
     double fx_scale, fx_iscale;
     int32_t T, N, n_tb, n_tiles, tshift, lds_su, blk0, n_ob, blk0b;
     int32_t blk0f, n_fa, blk0fb, n_fb;   // fused path: k_fx_a / k_fx_b block ranges
-    int32_t fx_k;                        // tiles of TT traces per k_fx_a block
+    int32_t fb_ops;                      // k_fx_b ops per block
 };
 
 // graph owning block `blk` of launch kind `which` (0 k_iter_a, 1 k_iter_b, 2 k_fx_a, 3 k_fx_b);
@@ -549,6 +549,24 @@ __global__ void __launch_bounds__(TB) k_iter_b(const GDev* __restrict__ gs, int3
 // fp64's own rounding of the reference's dot products.
 constexpr int FX_NMAX = 16384;
 constexpr size_t FX_LDS_BUDGET = 150 * 1024;   // su joins lacc in LDS while both fit this budget
+// global-memory views of pointers read from GDev: loads through them compile to global_load
+// (vmcnt only) instead of flat_load, whose lgkmcnt share would make every LDS wait also wait
+// for outstanding HBM loads
+#define GLB __attribute__((address_space(1)))
+__device__ __forceinline__ int64_t rfl64(int64_t v) {   // a wave-uniform value held in VGPRs -> SGPRs
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)v);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)((uint64_t)v >> 32));
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+template <class T>
+__device__ __forceinline__ const GLB T* gp(const T* p) { return (const GLB T*)p; }
+template <class T>
+__device__ __forceinline__ GLB T* gpw(T* p) { return (GLB T*)p; }
+
+// k_fx_a block size cap: 512 threads leave each wave 256 VGPRs for the pipelined walk (1024 would
+// cap it at 128 and spill); small graphs still fill the chip with two resident blocks per CU
+constexpr int FX_TMAX = 512;
 constexpr int FX_CAP = 24;   // staged ids per thread: blocks with more entries take the long path
 
 // graph of a fused-launch block: ng <= 2 resolves from the scalar split (no memory hop)
@@ -560,20 +578,21 @@ __device__ __forceinline__ int32_t fx_graph(const GDev* gs, int32_t ng, int32_t 
 
 // LDS layout of k_fx_a (byte offsets), shared by kernel and host
 struct FxLds {
-    size_t su, lacc, head, tail, tsum, xl, toff, owner, hbits, ids, total;
+    size_t su, lacc, head, tail, tsum, xl, owner, hbits, ids, total;
     bool su_lds;   // su staged in LDS; otherwise gathered from its global copy (L2-resident)
-    __host__ __device__ FxLds(int32_t N, int32_t TT) {
-        size_t rest = ((size_t)N + 1) * 8 + 4 * (size_t)TT * 8 + 8 + ((size_t)TT + 1) * 4 + (size_t)TT * 4 +
+    __host__ __device__ FxLds(int32_t N, int32_t TT, bool allow_su = true) {
+        size_t rest = ((size_t)N + 1) * 8 + 4 * (size_t)TT * 8 + 8 + (size_t)TT * 4 +
                       ((size_t)FX_CAP * TT / 32 + 2) * 4 + 16 + ((size_t)FX_CAP * TT + 16) * 2;
-        su_lds = ((size_t)N + 1) * 8 + rest <= FX_LDS_BUDGET;
+        su_lds = allow_su && ((size_t)N + 1) * 8 + rest <= FX_LDS_BUDGET;
+        // with su in LDS, su and the accumulator interleave (16 B per op: one address for the
+        // gather and the atomic of an entry)
         su = 0;
-        lacc = su + (su_lds ? ((size_t)N + 1) * 8 : 0);
-        head = lacc + ((size_t)N + 1) * 8;
+        lacc = su_lds ? 8 : 0;
+        head = ((size_t)N + 1) * (su_lds ? 16 : 8);
         tail = head + (size_t)TT * 8;
         tsum = tail + (size_t)TT * 8;
         xl = tsum + (size_t)TT * 8;
-        toff = xl + ((size_t)TT + 1) * 8;
-        owner = toff + ((size_t)TT + 1) * 4;
+        owner = xl + ((size_t)TT + 1) * 8;
         hbits = owner + (size_t)TT * 4;
         ids = (hbits + ((size_t)FX_CAP * TT / 32 + 2) * 4 + 15) / 16 * 16;
         total = ids + ((size_t)FX_CAP * TT + 16) * 2;
@@ -588,12 +607,34 @@ struct FxLds {
 // head[each later segment], combined in segment order by the trace's own thread.  Sums stay
 // sequential within a piece: fixed order, deterministic.  Requires non-empty traces (every
 // graph built from spans; uploaded graphs are checked on the host).
-template <class Q>
-__global__ void __launch_bounds__(1024) k_fx_a(const GDev* __restrict__ gs, int32_t ng, int32_t split, double d,
-                                               double alpha, int it) {
+// staged id chunk `cidx` (positions 8*cidx .. 8*cidx+7): positions outside the tile's entries
+// [shift, np) become N, the zero slot, so the walk needs no per-entry bounds tests
+__device__ __forceinline__ u32x4 fx_pad(u32x4 v, int32_t cidx, int32_t shift, int64_t np, int32_t N) {
+    // keep positions k (0..7) of the chunk with kb <= k < ke; 32-bit, only k is a constant
+    const int32_t q0 = cidx * 8;
+    const int32_t kb = shift - q0, ke = (int32_t)min(np - (int64_t)q0, (int64_t)8);
+    if (kb <= 0 && ke >= 8) return v;
+    const uint32_t n = (uint32_t)N;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        uint32_t x = v[k];
+        if (2 * k < kb || 2 * k >= ke) x = (x & 0xffff0000u) | n;
+        if (2 * k + 1 < kb || 2 * k + 1 >= ke) x = (x & 0x0000ffffu) | (n << 16);
+        v[k] = x;
+    }
+    return v;
+}
+
+// PF: blocks walk several tiles with the next tile's loads in flight; without PF every block
+// has one tile.  Both fit 128 VGPRs: two 512-thread blocks per CU where the LDS image allows.
+template <class Q, bool SUL, int MAXT, bool PF>
+__global__ void __launch_bounds__(MAXT, 4) k_fx_a(const GDev* __restrict__ gs, int32_t ng, int32_t split,
+                                                           double d, double alpha, int it) {
+    static_assert(FX_CAP == 24, "three 16-B id chunks per thread");
     extern __shared__ __attribute__((aligned(16))) unsigned char lraw[];
-    __shared__ double red[1024 / WAVE];
+    __shared__ double red[MAXT / WAVE];
     __shared__ double msh[2];
+    __shared__ int64_t nxe[2];   // the next tile's id range
     const unsigned long long ts0 = __builtin_amdgcn_s_memrealtime();
     const GDev& G = gs[fx_graph(gs, ng, split, 2)];
     const int32_t TT = (int32_t)blockDim.x;
@@ -601,26 +642,33 @@ __global__ void __launch_bounds__(1024) k_fx_a(const GDev* __restrict__ gs, int3
     const int cur = it & 1, nxt = cur ^ 1, k3 = it % 3;
     const int32_t T = G.T, N = G.N;
     const int32_t i = (int32_t)threadIdx.x;
-    const FxLds L_(N, TT);
-    const double* sug = G.sub[cur];   // N + 1 entries, sub[N] = 0 (the pad slot)
+    const FxLds L_(N, TT, SUL);
+    // global operands through addrspace(1) pointers: global_load (vmcnt only), never flat
+    const GLB int64_t* rs_off = gp(G.rs_off);
+    const GLB u32x4* rs16 = gp((const u32x4*)G.rs16);   // 8 ids per 16 B; padded past nnz
+    const GLB uint16_t* rs16s = gp(G.rs16);
+    const GLB Q* qc = gp((const Q*)G.q[cur]);
+    GLB Q* qn = gpw((Q*)G.q[nxt]);
+    const GLB float* c_t = gp(G.c_t);
+    const GLB float* w_t = gp(G.w_t);
+    const GLB double* sug = gp(G.sub[cur]);   // N + 1 entries, sub[N] = 0 (the pad slot)
+    constexpr int AS = SUL ? 2 : 1;   // word stride of su / lacc in LDS (interleaved when SUL)
     double* su_l = (double*)(lraw + L_.su);
-    const double* su = L_.su_lds ? su_l : sug;
     unsigned long long* lacc = (unsigned long long*)(lraw + L_.lacc);
     double* head = (double*)(lraw + L_.head);
     double* tail = (double*)(lraw + L_.tail);
     double* tsum = (double*)(lraw + L_.tsum);
     unsigned long long* xl = (unsigned long long*)(lraw + L_.xl);   // xl[c + 1] = X of trace c; xl[0] = 0
-    int32_t* toff = (int32_t*)(lraw + L_.toff);
     int32_t* owner = (int32_t*)(lraw + L_.owner);
     uint32_t* hbits = (uint32_t*)(lraw + L_.hbits);
     uint16_t* ids = (uint16_t*)(lraw + L_.ids);
-    unsigned long long* mslot = G.mslot;
-    const unsigned long long* Mcur = mslot + (size_t)2 * MSH * k3;
-    unsigned long long* Mnext = mslot + (size_t)2 * MSH * ((k3 + 1) % 3);
+    GLB unsigned long long* mslot = gpw(G.mslot);
+    const GLB unsigned long long* Mcur = mslot + (size_t)2 * MSH * k3;
+    GLB unsigned long long* Mnext = mslot + (size_t)2 * MSH * ((k3 + 1) % 3);
     if (lb == 0 && i < 2 * MSH) mslot[(size_t)2 * MSH * ((k3 + 2) % 3) + i] = 0ull;
     for (int32_t o = i; o <= N; o += TT) {   // once per block: the accumulator spans all its tiles
-        if (L_.su_lds) su_l[o] = o < N ? sug[o] : 0.0;
-        lacc[o] = 0ull;
+        if (SUL) su_l[AS * o] = sug[o];
+        lacc[AS * o] = 0ull;
     }
     if (i < WAVE) {
         const double ms = wave_max(bits2d(Mcur[i]));
@@ -630,45 +678,119 @@ __global__ void __launch_bounds__(1024) k_fx_a(const GDev* __restrict__ gs, int3
             msh[1] = mr;
         }
     }
-    const int32_t n_tiles = (T + TT - 1) / TT;
-    const int32_t tb = lb * G.fx_k, te = min(tb + G.fx_k, n_tiles);
+    const int32_t n_tiles = (T + TT - 1) / TT;   // this block's tiles: an even share of the graph's
+    const int32_t tb = (int32_t)((int64_t)lb * n_tiles / G.n_fa), te = (int32_t)((int64_t)(lb + 1) * n_tiles / G.n_fa);
+    // Software pipeline over the block's tiles: trace offsets run two tiles ahead, ids and
+    // per-trace words one tile ahead, so their HBM latency hides behind the current tile's walk.
+    // gfx9 counts loads and stores in one in-order vmcnt, so every global access in the loop is
+    // unconditional (clamped indices, a pad slot for the store) -- the compiler can then wait for
+    // exactly the load it needs -- and loaded values are consumed at the end of an iteration.
+    // A tile's id range [e0, e1) comes from its first and last traces' offsets through LDS.
+    int64_t e0 = 0, e1 = 0, p_a = 0, p_b = 0, o_a = 0, o_b = 0;
+    double p_qk = 0.0;
+    float p_ct = 0.0f, p_wt = 0.0f;
+    u32x4 pv0 = {0u, 0u, 0u, 0u}, pv1 = pv0, pv2 = pv0;
+#define FX_OFFS(tile_, a_, b_)                                          \
+    do {                                                                \
+        const int32_t t0_ = (tile_) * TT, tc_ = t0_ + min(i, T - t0_ - 1); \
+        a_ = rs_off[tc_];                                               \
+        b_ = rs_off[tc_ + 1];                                           \
+    } while (0)
+    // ids chunks clamped in-bounds (the buffer is padded past nnz; a long tile ignores them)
+#define FX_BODY(tile_, e0s_, e1s_, qk_, ct_, wt_, v0_, v1_, v2_)                                   \
+    do {                                                                                           \
+        const int32_t tc_ = (tile_) * TT + min(i, T - (tile_) * TT - 1);                           \
+        qk_ = (double)qc[tc_];                                                                     \
+        ct_ = c_t[tc_];                                                                            \
+        wt_ = w_t[tc_];                                                                            \
+        const int64_t base_ = (e0s_) & ~(int64_t)7;                                                \
+        const GLB u32x4* src_ = rs16 + (base_ >> 3);                                               \
+        const int32_t nch_ = (int32_t)min((((e1s_) - base_) + 7) >> 3, (int64_t)FX_CAP / 8 * TT);  \
+        v0_ = src_[min(i, nch_ - 1)];                                                              \
+        v1_ = src_[min(i + TT, nch_ - 1)];                                                         \
+        v2_ = src_[min(i + 2 * TT, nch_ - 1)];                                                     \
+    } while (0)
+#define FX_BOUNDS(tile_, e0_, e1_)                                            \
+    do {                                                                      \
+        e0_ = rs_off[(tile_) * TT];                                           \
+        e1_ = rs_off[min((tile_) * TT + TT, T)];                              \
+    } while (0)
+    if (tb < te) {
+        FX_BOUNDS(tb, e0, e1);
+        FX_OFFS(tb, p_a, p_b);
+        FX_BODY(tb, e0, e1, p_qk, p_ct, p_wt, pv0, pv1, pv2);
+        if (PF) {
+            const int32_t t1 = min(tb + 1, te - 1), nt1 = min(TT, T - t1 * TT);
+            FX_OFFS(t1, o_a, o_b);
+            if (i == 0) nxe[0] = o_a;   // tile tb + 1's id range, from its first and last traces
+            if (i == nt1 - 1) nxe[1] = o_b;
+        }
+    }
     double rmax = -__builtin_huge_val();
+    // diagnostics (MR_FX_STAMP): thread 0 sums its clock per tile phase
+    // (sums in LDS: no registers held across the walk)
+    __shared__ unsigned long long ph[7];   // [6]: the last clock
+    const unsigned long long t_init = G.stamp ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    if (G.stamp && i == 0) {
+        for (int k = 0; k < 6; ++k) ph[k] = 0ull;
+        ph[6] = t_init;
+    }
+#define FX_MARK(slot)                                                        \
+    do {                                                                     \
+        if (G.stamp && i == 0) {                                             \
+            const unsigned long long nw_ = __builtin_amdgcn_s_memrealtime(); \
+            ph[slot] += nw_ - ph[6];                                         \
+            ph[6] = nw_;                                                     \
+        }                                                                    \
+    } while (0)
     for (int32_t tile = tb; tile < te; ++tile) {
         const bool first = tile == tb;
+        if (!PF && !first) {
+            FX_BOUNDS(tile, e0, e1);
+            FX_OFFS(tile, p_a, p_b);
+            FX_BODY(tile, e0, e1, p_qk, p_ct, p_wt, pv0, pv1, pv2);
+        }
         const int32_t t0 = tile * TT;
         const int32_t nt = min(TT, T - t0);
         const int32_t t = t0 + i;
         const bool own = i < nt;
-        // every independent load of the tile goes out before its first barrier
-        const int64_t e0 = G.rs_off[t0], e1 = G.rs_off[t0 + nt];
-        const int64_t a = own ? G.rs_off[t] : 0, b = own ? G.rs_off[t + 1] : 0;
-        const double qk = own ? (double)((const Q*)G.q[cur])[t] : 0.0;
-        const float ct = own ? G.c_t[t] : 0.0f, wt = own ? G.w_t[t] : 0.0f;
+        const int64_t a = p_a, b = p_b;
+        const double qk = p_qk;
+        const float ct = p_ct, wt = p_wt;
         const int64_t base = e0 & ~(int64_t)7;
         const int32_t shift = (int32_t)(e0 - base);
         const int64_t np_ = e1 - base;                 // positions [shift, np_) hold the tile's entries
         const bool bal = np_ <= (int64_t)FX_CAP * TT;
         if (!first) __syncthreads();                   // the previous tile's readers are done
-        if (bal) {   // stage the id range: 16-B loads of 8 ids (the buffer is padded past nnz)
-            const uint4* src = (const uint4*)(G.rs16 + base);
+        FX_MARK(4);
+        if (bal) {   // stage the id range
             const int32_t nch = (int32_t)((np_ + 7) >> 3);
-            uint4 v[FX_CAP / 8];
-#pragma unroll
-            for (int j = 0; j < FX_CAP / 8; ++j) v[j] = src[min(i + j * TT, nch - 1)];
-#pragma unroll
-            for (int j = 0; j < FX_CAP / 8; ++j)
-                if (i + j * TT < nch) *(uint4*)(ids + (size_t)(i + j * TT) * 8) = v[j];
+            if (i < nch) *(u32x4*)(ids + (size_t)i * 8) = fx_pad(pv0, i, shift, np_, N);
+            if (i + TT < nch) *(u32x4*)(ids + (size_t)(i + TT) * 8) = fx_pad(pv1, i + TT, shift, np_, N);
+            if (i + 2 * TT < nch) *(u32x4*)(ids + (size_t)(i + 2 * TT) * 8) = fx_pad(pv2, i + 2 * TT, shift, np_, N);
             for (int32_t w = i; w < FX_CAP * TT / 32 + 2; w += TT) hbits[w] = 0u;
             if (i == 0) {
                 owner[0] = -1;   // positions before `shift` belong to the previous tile
                 xl[0] = 0ull;
             }
         }
-        if (own) toff[i] = (int32_t)(a - base);
-        if (i == 0) toff[nt] = (int32_t)np_;
+        FX_MARK(5);
         __syncthreads();
+        // prefetch: tile + 1's ids and words, tile + 2's offsets (the last tiles reload themselves)
+        int64_t m_a = 0, m_b = 0, e0n = e0, e1n = e1;
+        double n_qk = 0.0;
+        float n_ct = 0.0f, n_wt = 0.0f;
+        u32x4 nv0 = pv0, nv1 = pv1, nv2 = pv2;
+        if (PF) {
+            if (tile + 1 < te) {
+                e0n = nxe[0];
+                e1n = nxe[1];
+            }
+            FX_BODY(min(tile + 1, te - 1), e0n, e1n, n_qk, n_ct, n_wt, nv0, nv1, nv2);
+            FX_OFFS(min(tile + 2, te - 1), m_a, m_b);
+        }
         const unsigned long long X = own ? (unsigned long long)__double2ull_rn(qk / msh[1] * G.fx_scale) : 0ull;
-        if (G.stamp && i == 0 && first) G.stamp[(size_t)blockIdx.x * 8 + 1] = __builtin_amdgcn_s_memrealtime();
+        FX_MARK(0);
         double acc = 0.0;
         if (bal) {
             int32_t L = (int32_t)((np_ + 8 * TT - 1) / (8 * TT)) * 8;
@@ -680,40 +802,47 @@ __global__ void __launch_bounds__(1024) k_fx_a(const GDev* __restrict__ gs, int3
                 for (int32_t sg = (ra + L - 1) / L; sg * L < rb; ++sg) owner[sg] = i;   // segments starting in t
             }
             __syncthreads();
-            if (G.stamp && i == 0 && first) G.stamp[(size_t)blockIdx.x * 8 + 2] = __builtin_amdgcn_s_memrealtime();
+            FX_MARK(1);
             const int32_t p = i * L;
             if (p < np_) {
                 const int32_t qe = (int32_t)min((int64_t)p + L, np_);
+                // trace starts of the segment (L <= 24 positions fit the 33+ bits left after the
+                // shift); position p's own start is `st`, the rest are tested per 8-entry chunk
                 const unsigned long long bits =
                     (((unsigned long long)hbits[(p >> 5) + 1] << 32) | hbits[p >> 5]) >> (p & 31);
                 int32_t c = owner[i];
                 bool st = bits & 1ull;                   // the segment's first piece starts a trace
-                unsigned long long Xc = xl[c + 1];
+                const unsigned long long sb = bits & ~1ull;
                 for (int32_t ch = p; ch < qe; ch += 8) {
-                    const uint4 w = *(const uint4*)(ids + ch);   // 8 ids, 16-B aligned (ch % 8 == 0)
+                    // 8 ids, 16-B aligned (ch % 8 == 0); positions outside the tile hold N (zero slot)
+                    const uint4 w = *(const uint4*)(ids + ch);
+                    const uint32_t m8 = (uint32_t)(sb >> (ch - p)) & 0xffu;
                     int32_t o[8];
                     o[0] = (int32_t)(w.x & 0xffffu); o[1] = (int32_t)(w.x >> 16);
                     o[2] = (int32_t)(w.y & 0xffffu); o[3] = (int32_t)(w.y >> 16);
                     o[4] = (int32_t)(w.z & 0xffffu); o[5] = (int32_t)(w.z >> 16);
                     o[6] = (int32_t)(w.w & 0xffffu); o[7] = (int32_t)(w.w >> 16);
+                    // all LDS reads of the chunk go out together (su and each entry's trace X),
+                    // then the 8 atomics issue back to back: an LDS wait inside the entry loop
+                    // would also wait for every atomic before it
+                    double g[8];
+                    unsigned long long xj[8];
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) g[j] = SUL ? su_l[AS * o[j]] : sug[o[j]];
 #pragma unroll
                     for (int j = 0; j < 8; ++j)
-                        if (ch + j < shift || ch + j >= qe) o[j] = N;   // outside the tile: the zero slot
-                    double g[8];
+                        xj[j] = xl[c + 1 + (int32_t)__builtin_popcount(m8 & ((2u << j) - 1u))];
 #pragma unroll
-                    for (int j = 0; j < 8; ++j) g[j] = su[o[j]];
+                    for (int j = 0; j < 8; ++j) atomicAdd(&lacc[AS * o[j]], xj[j]);
 #pragma unroll
                     for (int j = 0; j < 8; ++j) {
-                        const int32_t e = ch + j;
-                        if (e > p && e < qe && ((bits >> (e - p)) & 1ull)) {   // a new trace starts at e
+                        if (m8 & (1u << j)) {   // a new trace starts at ch + j
                             if (st) tsum[c] = acc; else head[i] = acc;
                             acc = 0.0;
                             st = true;
                             ++c;
-                            Xc = xl[c + 1];
                         }
                         acc += g[j];
-                        atomicAdd(&lacc[o[j]], Xc);
                     }
                 }
                 const bool ends = qe == np_ || ((bits >> (qe - p)) & 1ull);
@@ -724,7 +853,7 @@ __global__ void __launch_bounds__(1024) k_fx_a(const GDev* __restrict__ gs, int3
                 }
             }
             __syncthreads();
-            if (G.stamp && i == 0 && first) G.stamp[(size_t)blockIdx.x * 8 + 3] = __builtin_amdgcn_s_memrealtime();
+            FX_MARK(2);
             if (own && rb > ra) {
                 const int32_t sa = ra / L, sb = (rb - 1) / L;
                 if (sa == sb) {
@@ -743,7 +872,7 @@ __global__ void __launch_bounds__(1024) k_fx_a(const GDev* __restrict__ gs, int3
             for (int64_t lo = e0; lo < e1; lo += cap) {
                 const int64_t hi = min(lo + (int64_t)cap, e1);
                 __syncthreads();
-                for (int64_t e = lo + i; e < hi; e += TT) ids[e - lo] = G.rs16[e];
+                for (int64_t e = lo + i; e < hi; e += TT) ids[e - lo] = rs16s[e];
                 __syncthreads();
                 const int32_t x0 = (int32_t)(max(a, lo) - lo), x1 = (int32_t)(min(b, hi) - lo);
                 for (int32_t c = x0; c < x1; c += 8) {
@@ -752,41 +881,71 @@ __global__ void __launch_bounds__(1024) k_fx_a(const GDev* __restrict__ gs, int3
                     for (int j = 0; j < 8; ++j) o[j] = c + j < x1 ? (int32_t)ids[c + j] : N;
                     double g[8];
 #pragma unroll
-                    for (int j = 0; j < 8; ++j) g[j] = su[o[j]];
+                    for (int j = 0; j < 8; ++j) g[j] = SUL ? su_l[AS * o[j]] : sug[o[j]];
 #pragma unroll
                     for (int j = 0; j < 8; ++j) acc += g[j];
 #pragma unroll
-                    for (int j = 0; j < 8; ++j) atomicAdd(&lacc[o[(j + lane) & 7]], X);
+                    for (int j = 0; j < 8; ++j) atomicAdd(&lacc[AS * o[(j + lane) & 7]], X);
                 }
             }
         }
-        if (own) {
-            const double rp = d * (acc / msh[0]) + (double)ct;   // pagerank.py:125
-            ((Q*)G.q[nxt])[t] = (Q)((double)wt * rp);
-            rmax = nmax(rmax, rp);
+        const double rp = d * (acc / msh[0]) + (double)ct;   // pagerank.py:125
+        if (own) rmax = nmax(rmax, rp);
+        FX_MARK(3);
+        if (PF) {
+            // tile + 2's id range for the next iteration's prefetch (read after its first barrier)
+            const int32_t t2 = min(tile + 2, te - 1), nt2 = min(TT, T - t2 * TT);
+            if (i == 0) nxe[0] = m_a;
+            if (i == nt2 - 1) nxe[1] = m_b;
+            e0 = e0n;
+            e1 = e1n;
+            p_a = o_a;
+            p_b = o_b;
+            p_qk = n_qk;
+            p_ct = n_ct;
+            p_wt = n_wt;
+            pv0 = nv0;
+            pv1 = nv1;
+            pv2 = nv2;
+            o_a = m_a;
+            o_b = m_b;
         }
+        qn[own ? t : T] = (Q)((double)wt * rp);   // last: no wait above queues behind it (q[T]: pad slot)
     }
+#undef FX_MARK
+#undef FX_BODY
+#undef FX_OFFS
+#undef FX_BOUNDS
     // call-graph term for the next s' (pagerank.py:122-124, alpha P_ss s_k), a thread per op
-    for (int32_t oss = lb * TT + i; oss < N; oss += G.n_fa * TT) {
-        const double* sp_cur = G.spb[cur];
-        double bb = 0.0;
-        for (int64_t e = G.ss_off[oss]; e < G.ss_off[oss + 1]; ++e) {
-            const int32_t pp = G.ss_par[e];
-            bb += (double)G.pw[pp] * sp_cur[pp];
+    {
+        const GLB double* sp_cur = gp(G.spb[cur]);
+        const GLB int64_t* ss_off = gp(G.ss_off);
+        const GLB int32_t* ss_par = gp(G.ss_par);
+        const GLB float* pw = gp(G.pw);
+        GLB double* ssv = gpw(G.fx_ssv);
+        for (int32_t oss = lb * TT + i; oss < N; oss += G.n_fa * TT) {
+            double bb = 0.0;
+            for (int64_t e = ss_off[oss]; e < ss_off[oss + 1]; ++e) {
+                const int32_t pp = ss_par[e];
+                bb += (double)pw[pp] * sp_cur[pp];
+            }
+            ssv[oss] = alpha * (bb / msh[0]);
         }
-        G.fx_ssv[oss] = alpha * (bb / msh[0]);
     }
-    if (G.stamp && i == 0) G.stamp[(size_t)blockIdx.x * 8 + 4] = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long t_loop = G.stamp ? __builtin_amdgcn_s_memrealtime() : 0ull;
     __syncthreads();
-    if (G.stamp && i == 0) G.stamp[(size_t)blockIdx.x * 8 + 5] = __builtin_amdgcn_s_memrealtime();
-    unsigned long long* prow = G.fx_part + (size_t)lb * N;
-    for (int32_t o = i; o < N; o += TT) prow[o] = lacc[o];
+    GLB unsigned long long* prow = gpw(G.fx_part) + (size_t)lb * N;
+    for (int32_t o = i; o < N; o += TT) prow[o] = lacc[AS * o];
     rmax = block_max(rmax, red);
     if (i == 0) {
-        atomicMax(&Mnext[MSH + blockIdx.x % MSH], d2bits(rmax));
+        atomicMax((unsigned long long*)&Mnext[MSH + blockIdx.x % MSH], d2bits(rmax));
         if (G.stamp) {
-            G.stamp[(size_t)blockIdx.x * 8] = ts0;
-            G.stamp[(size_t)blockIdx.x * 8 + 6] = __builtin_amdgcn_s_memrealtime();
+            unsigned long long* sp = G.stamp + (size_t)blockIdx.x * 16;
+            sp[0] = ts0;
+            sp[1] = t_init - ts0;
+            for (int k = 0; k < 6; ++k) sp[2 + k] = ph[k];
+            sp[8] = t_loop;
+            sp[9] = __builtin_amdgcn_s_memrealtime();
         }
     }
 }
@@ -796,57 +955,77 @@ __global__ void __launch_bounds__(1024) k_fx_a(const GDev* __restrict__ gs, int3
 // limb sums meet in LDS (integers: order-free).  mode 0: whole graph; sharded graphs split it
 // around the limb all-reduce: mode 1 writes this rank's limbs (lo, hi) per op to fx_limb, mode 2
 // finishes from the reduced limbs.
-constexpr int FB_OPS = WAVE, FB_W = 16;
-__global__ void __launch_bounds__(FB_OPS * FB_W) k_fx_b(const GDev* __restrict__ gs, int32_t ng, int32_t split,
-                                                       double d, int it, int mode) {
-    __shared__ unsigned long long slo[FB_W][FB_OPS], shi[FB_W][FB_OPS];
+constexpr int FB_W = 16;
+// ops per k_fx_b block: a lane reads op (lane % ops) of every (64/ops)-th row of its wave's share,
+// so a row read stays one 128-B line per op group while small graphs still spread over many CUs
+static int fb_ops(int32_t N) { return N <= 8192 ? 16 : 32; }
+__global__ void __launch_bounds__(WAVE * FB_W) k_fx_b(const GDev* __restrict__ gs, int32_t ng, int32_t split,
+                                                     double d, int it, int mode) {
+    __shared__ unsigned long long slo[FB_W * WAVE], shi[FB_W * WAVE];
     const GDev& G = gs[fx_graph(gs, ng, split, 3)];
     const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
-    const int32_t o = ((int32_t)blockIdx.x - G.blk0fb) * FB_OPS + lane;
+    const int32_t OPB = G.fb_ops, GR = WAVE / OPB;
+    const int32_t ol = lane % OPB, grp = lane / OPB;
+    const int32_t o = ((int32_t)blockIdx.x - G.blk0fb) * OPB + ol;
     const int32_t N = G.N, nb = G.n_fa;
     const bool on = o < N;
+    // the finishing lanes' operands, loaded before the rows so both latencies overlap
+    const bool fin = w == 0 && lane < OPB && on;
+    const double ssv = fin ? G.fx_ssv[o] : 0.0;
+    const float uo = fin ? G.u_o[o] : 0.0f;
     unsigned long long lo = 0ull, hi = 0ull;
     if (on && mode != 2) {
-        const unsigned long long* __restrict__ col = G.fx_part + o;
-        int32_t r = w;
-        for (; r + 3 * FB_W < nb; r += 4 * FB_W) {
-            const unsigned long long v0 = col[(size_t)r * N], v1 = col[(size_t)(r + FB_W) * N],
-                                     v2 = col[(size_t)(r + 2 * FB_W) * N], v3 = col[(size_t)(r + 3 * FB_W) * N];
-            lo += (v0 & 0xffffffffull) + (v1 & 0xffffffffull) + (v2 & 0xffffffffull) + (v3 & 0xffffffffull);
-            hi += (v0 >> 32) + (v1 >> 32) + (v2 >> 32) + (v3 >> 32);
-        }
-        for (; r < nb; r += FB_W) {
-            const unsigned long long v = col[(size_t)r * N];
-            lo += v & 0xffffffffull;
-            hi += v >> 32;
+        // batches of 16 rows per lane, every load in flight before the sums (indices clamped:
+        // the repeats are cache hits and are not added)
+        const int32_t stride = FB_W * GR;
+        const GLB unsigned long long* col = gp((const unsigned long long*)G.fx_part) + o;
+        for (int32_t r0 = w * GR + grp; r0 < nb; r0 += 16 * stride) {
+            unsigned long long v[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) v[k] = col[(size_t)min(r0 + k * stride, nb - 1) * N];
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                if (r0 + k * stride < nb) {
+                    lo += v[k] & 0xffffffffull;
+                    hi += v[k] >> 32;
+                }
         }
     }
-    slo[w][lane] = lo;
-    shi[w][lane] = hi;
+    // the wave's row groups of one op meet by lane shuffles, the waves through LDS (integers:
+    // order-free)
+    for (int m = WAVE / 2; m >= OPB; m >>= 1) {
+        lo += (unsigned long long)__shfl_xor((long long)lo, m);
+        hi += (unsigned long long)__shfl_xor((long long)hi, m);
+    }
+    if (lane < OPB) {
+        slo[w * WAVE + lane] = lo;
+        shi[w * WAVE + lane] = hi;
+    }
     __syncthreads();
-    if (w != 0 || !on) return;
+    if (!fin) return;
+    const int32_t op = o;
     lo = hi = 0ull;
     for (int k = 0; k < FB_W; ++k) {
-        lo += slo[k][lane];
-        hi += shi[k][lane];
+        lo += slo[k * WAVE + lane];
+        hi += shi[k * WAVE + lane];
     }
     if (mode == 1) {
-        G.fx_limb[2 * o] = lo;
-        G.fx_limb[2 * o + 1] = hi;
+        G.fx_limb[2 * op] = lo;
+        G.fx_limb[2 * op + 1] = hi;
         return;
     }
     if (mode == 2) {
-        lo = G.fx_limb[2 * o];
-        hi = G.fx_limb[2 * o + 1];
+        lo = G.fx_limb[2 * op];
+        hi = G.fx_limb[2 * op + 1];
     }
     const int nxt = (it & 1) ^ 1, k3 = it % 3;
     unsigned long long* Mnext = G.mslot + (size_t)2 * MSH * ((k3 + 1) % 3);
     // hi, lo < 2^53 (fewer than 2^21 rows over all ranks): both conversions exact, one rounding
     const double sum = ((double)hi * 4294967296.0 + (double)lo) * G.fx_iscale;
-    const double v = d * (sum + G.fx_ssv[o]);      // pagerank.py:122-124
-    G.spb[nxt][o] = v;
-    G.sub[nxt][o] = (double)G.u_o[o] * v;
-    atomicMax(&Mnext[o % MSH], d2bits(v));
+    const double v = d * (sum + ssv);      // pagerank.py:122-124
+    G.spb[nxt][op] = v;
+    G.sub[nxt][op] = (double)uo * v;
+    atomicMax(&Mnext[op % MSH], d2bits(v));
 }
 
 // result = s/max(s) (pagerank.py:126,129); weight = result * sum(result) / N (:93-107)
@@ -980,27 +1159,49 @@ static const bool g_debug = getenv("MR_DEBUG") != nullptr;
 void mr_prof_begin(mr_ctx* ctx);
 void mr_prof_end(mr_ctx* ctx, double bytes);
 
-// traces per k_fx_a block (= its block size): the largest of 1024/512/256 whose LDS image fits
+// traces per k_fx_a block (= its block size): the larger of 512/256 whose LDS image fits
 // (MR_TT caps it for measurements); 0 when none fits
 constexpr size_t FX_LDS_MAX = 160 * 1024 - 512;   // minus the kernel's static LDS
 static int fx_tt(int32_t N) {
     static const int cap = [] {
         const char* e = getenv("MR_TT");
-        const int v = e ? atoi(e) : 1024;
-        return (v == 256 || v == 512 || v == 1024) ? v : 1024;
+        const int v = e ? atoi(e) : FX_TMAX;
+        return (v == 256 || v == FX_TMAX) ? v : FX_TMAX;
     }();
     for (int tt = cap; tt >= 256; tt >>= 1)
         if (FxLds(N, tt).total <= FX_LDS_MAX) return tt;
     return 0;
 }
 
-// tiles of TT traces per k_fx_a block: about 1024 blocks, so the dense partial rows (N per block)
-// stay a small fraction of the iteration's bytes; k*TT <= 2^15 keeps the fixed-point scale >= 2^48
-static int fx_k(int32_t T, int TT) {
-    const int64_t tiles = (T + TT - 1) / TT;
-    int k = 1;
-    while (k * 2 * (int64_t)TT <= 32768 && tiles / (k * 2) >= 1024) k *= 2;
-    return k;
+// k_fx_a blocks of a graph: one tile each while the tiles fit the resident blocks, else the
+// resident block count (times r) with an even share of the tiles each, so no tail round is
+// left; the dense partial rows (N words per block) stay a small part of an iteration's bytes.
+// At most 2^15 traces per block keeps the fixed-point scale >= 2^48.
+static int64_t fx_blocks(int32_t T, int32_t N, int TT) {
+    static const int ncu = [] {
+        int dev = 0, v = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            v = 256;
+        return std::max(v, 1);
+    }();
+    const int64_t tiles = cdiv((int64_t)T, TT);
+    // resident blocks per CU: LDS image and VGPRs (the runtime's occupancy for the variant)
+    const FxLds L(N, TT);
+    auto per_cu = [&](bool pf) {
+        int n = 0;
+        const void* kfn = pf ? (L.su_lds ? (const void*)k_fx_a<double, true, FX_TMAX, true>
+                                         : (const void*)k_fx_a<double, false, FX_TMAX, true>)
+                             : (L.su_lds ? (const void*)k_fx_a<double, true, FX_TMAX, false>
+                                         : (const void*)k_fx_a<double, false, FX_TMAX, false>);
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kfn, TT, L.total) != hipSuccess || n < 1)
+            n = std::max<int>(1, (int)(FX_LDS_MAX / L.total));
+        return (int64_t)n;
+    };
+    if (tiles <= ncu * per_cu(false)) return tiles;   // one tile per block, no pipeline
+    const int64_t resident = ncu * per_cu(true);
+    int64_t nb = resident;
+    while (cdiv(tiles, nb) * TT > 32768) nb += resident;
+    return std::min(nb, tiles);
 }
 
 // Derived per-graph arrays: fp32 reciprocals, u16 ids, and the P_sr tiles.  One host round trip
@@ -1144,13 +1345,13 @@ static int pagerank_setup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool 
     MR_TRY(g->sub[1].alloc(ctx, (size_t)N + 1));
     MR_TRY(g->weight.alloc(ctx, (size_t)N));
     if (g->fused) {
-        MR_TRY(g->fx_part.alloc(ctx, (size_t)cdiv(cdiv(T, TT), fx_k(T, TT)) * (size_t)N));
+        MR_TRY(g->fx_part.alloc(ctx, (size_t)fx_blocks(T, N, TT) * (size_t)N));
         MR_TRY(g->fx_ssv.alloc(ctx, (size_t)N));
     }
     else MR_TRY(g->part.alloc(ctx, (size_t)std::max<int64_t>(g->n_pairs, 1)));
     for (int i = 0; i < 2; ++i) {
-        if (fp32) MR_TRY(g->q32[i].alloc(ctx, (size_t)T));
-        else MR_TRY(g->q64[i].alloc(ctx, (size_t)T));
+        if (fp32) MR_TRY(g->q32[i].alloc(ctx, (size_t)T + 1));   // [T]: k_fx_a's pad slot
+        else MR_TRY(g->q64[i].alloc(ctx, (size_t)T + 1));
     }
     // one launch clears every per-call word (instead of a memset per buffer)
     hipLaunchKernelGGL(k_pr_reset, dim3(cdiv(std::max<int64_t>({(int64_t)T, (int64_t)cap, (int64_t)N, 16}), 256)),
@@ -1212,7 +1413,7 @@ int mr_pagerank_batch_impl(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly,
     MR_TRY_HIP(ctx, hipSetDevice(ctx->device));
     hipStream_t st = ctx->stream;
     const bool fp32 = precision == MR_FP32;
-    int TT = 1024;   // one block size for the batch: the largest that fits every fused graph
+    int TT = FX_TMAX;   // one block size for the batch: the largest that fits every fused graph
     for (int i = 0; i < ng; ++i)
         if (gs[i]->fused) TT = std::min(TT, fx_tt(gs[i]->N));
     for (int i = 0; i < ng; ++i) MR_TRY(pagerank_setup(ctx, gs[i], anomaly[i], d, fp32, flags, TT, sharded));
@@ -1222,6 +1423,8 @@ int mr_pagerank_batch_impl(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly,
     std::vector<GDev> hv((size_t)ng);
     int32_t blocks_a = 0, blocks_b = 0, blocks_fa = 0, blocks_fb = 0;
     size_t lds = VCAP * sizeof(double), lds_f = 0;
+    bool sul = true;   // every fused graph stages su in LDS
+    bool multi = false;   // some fused block walks several tiles (the pipelined variant)
     double bytes = 0.0;
     for (int i = 0; i < ng; ++i) {
         mr_graph* g = gs[i];
@@ -1253,25 +1456,28 @@ int mr_pagerank_batch_impl(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly,
         v.fx_ssv = g->fx_ssv.p;
         v.fx_limb = (unsigned long long*)g->fx_limb.p;
         v.stamp = nullptr;
-        v.fx_k = fx_k(g->T, TT);
+        const int64_t nfa = g->fused ? fx_blocks(g->T, g->N, TT) : 0;
         // a row entry stays below 2^63; shards of one graph hold different trace counts, and their
         // limbs are summed, so they share the scale of the largest block (2^15 traces)
-        const int sc = 63 - (sharded ? 15 : bits_for((uint64_t)v.fx_k * TT - 1));
+        const int sc = 63 - (sharded ? 15 : bits_for((uint64_t)std::max<int64_t>(cdiv(cdiv((int64_t)g->T, TT), std::max<int64_t>(nfa, 1)) * TT - 1, 1)));
         v.fx_scale = std::ldexp(1.0, sc);
         v.fx_iscale = std::ldexp(1.0, -sc);
         v.T = g->T;
         v.N = g->N;
         v.blk0f = blocks_fa;
-        v.n_fa = g->fused ? cdiv(cdiv(g->T, TT), v.fx_k) : 0;
+        v.n_fa = (int32_t)nfa;
         blocks_fa += v.n_fa;
         v.blk0fb = blocks_fb;
-        v.n_fb = g->fused ? cdiv(g->N, FB_OPS) : 0;
+        v.fb_ops = fb_ops(g->N);
+        v.n_fb = g->fused ? cdiv(g->N, v.fb_ops) : 0;
         blocks_fb += v.n_fb;
         v.blk0 = blocks_a;
         v.blk0b = blocks_b;
         bytes += iter_bytes(g, fp32);
         if (g->fused) {
             lds_f = std::max(lds_f, FxLds(g->N, TT).total);
+            sul = sul && FxLds(g->N, TT).su_lds;
+            multi = multi || v.n_fa < cdiv(g->T, TT);
             continue;   // no tile-path blocks (n_tb = n_tiles = n_ob = 0)
         }
         v.n_tb = (mask & 1) ? cdiv(g->T, TB) : 0;
@@ -1287,25 +1493,31 @@ int mr_pagerank_batch_impl(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly,
     static const bool stamps = getenv("MR_FX_STAMP") != nullptr;
     DBuf<unsigned long long> dstamp;
     if (stamps && blocks_fa) {
-        MR_TRY(dstamp.zero(ctx, (size_t)blocks_fa * 8));
+        MR_TRY(dstamp.zero(ctx, (size_t)blocks_fa * 16));
         for (auto& v : hv) v.stamp = dstamp.p;
     }
     DBuf<GDev> dv;
     MR_TRY(dv.upload(ctx, hv.data(), hv.size()));
     const int32_t split_fa = ng == 2 ? hv[1].blk0f : 0, split_fb = ng == 2 ? hv[1].blk0fb : 0;
+    using FxA = void (*)(const GDev*, int32_t, int32_t, double, double, int);
+    const FxA fx_tab[2][2][2] = {
+        {{k_fx_a<double, false, FX_TMAX, false>, k_fx_a<double, false, FX_TMAX, true>},
+         {k_fx_a<double, true, FX_TMAX, false>, k_fx_a<double, true, FX_TMAX, true>}},
+        {{k_fx_a<float, false, FX_TMAX, false>, k_fx_a<float, false, FX_TMAX, true>},
+         {k_fx_a<float, true, FX_TMAX, false>, k_fx_a<float, true, FX_TMAX, true>}}};
+    const FxA fx_a = fx_tab[fp32 ? 1 : 0][sul ? 1 : 0][multi ? 1 : 0];
     for (int it = 0; it < iters; ++it) {
         mr_prof_begin(ctx);
         if (blocks_fa) {
-            if (fp32) hipLaunchKernelGGL(k_fx_a<float>, dim3(blocks_fa), dim3(TT), lds_f, st, dv.p, ng, split_fa, d, alpha, it);
-            else hipLaunchKernelGGL(k_fx_a<double>, dim3(blocks_fa), dim3(TT), lds_f, st, dv.p, ng, split_fa, d, alpha, it);
+            hipLaunchKernelGGL(fx_a, dim3(blocks_fa), dim3(TT), lds_f, st, dv.p, ng, split_fa, d, alpha, it);
             MR_DEBUG_CHECK(ctx, "k_fx_a");
             if (!sharded) {
-                hipLaunchKernelGGL(k_fx_b, dim3(blocks_fb), dim3(FB_OPS * FB_W), 0, st, dv.p, ng, split_fb, d, it, 0);
+                hipLaunchKernelGGL(k_fx_b, dim3(blocks_fb), dim3(WAVE * FB_W), 0, st, dv.p, ng, split_fb, d, it, 0);
             } else {   // r' max and the P_sr r limbs over all ranks (exact: integers, max)
                 MR_TRY(mr_coll_allreduce(ctx, gs[0]->mslot.p + (size_t)2 * MSH * ((it + 1) % 3) + MSH, MSH, MR_DT_U64, 1));
-                hipLaunchKernelGGL(k_fx_b, dim3(blocks_fb), dim3(FB_OPS * FB_W), 0, st, dv.p, ng, split_fb, d, it, 1);
+                hipLaunchKernelGGL(k_fx_b, dim3(blocks_fb), dim3(WAVE * FB_W), 0, st, dv.p, ng, split_fb, d, it, 1);
                 MR_TRY(mr_coll_allreduce(ctx, gs[0]->fx_limb.p, 2 * (int64_t)gs[0]->N, MR_DT_U64, 0));
-                hipLaunchKernelGGL(k_fx_b, dim3(blocks_fb), dim3(FB_OPS * FB_W), 0, st, dv.p, ng, split_fb, d, it, 2);
+                hipLaunchKernelGGL(k_fx_b, dim3(blocks_fb), dim3(WAVE * FB_W), 0, st, dv.p, ng, split_fb, d, it, 2);
             }
             MR_DEBUG_CHECK(ctx, "k_fx_b");
         }
@@ -1328,28 +1540,29 @@ int mr_pagerank_batch_impl(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly,
     }
     MR_TRY_HIP(ctx, hipGetLastError());
     if (dstamp.p) {   // diagnostics: phase times of the last k_fx_a launch, in 10 ns ticks
-        std::vector<unsigned long long> h((size_t)blocks_fa * 8);
+        std::vector<unsigned long long> h((size_t)blocks_fa * 16);
         MR_TRY(dstamp.download(ctx, h.data(), h.size()));
         MR_TRY_HIP(ctx, hipStreamSynchronize(st));
-        unsigned long long t0 = ~0ull, t6 = 0;
-        double sum[6] = {0}, mx[6] = {0};
+        unsigned long long t0 = ~0ull, t9 = 0;
+        const char* nm[8] = {"init", "bar-in", "stage", "bar+pf", "mark", "walk", "rest", "ss+rows"};
+        const int slot[8] = {1, 6, 7, 2, 3, 4, 5, -1};
+        double sum[8] = {0}, mx[8] = {0};
         int nb = 0;
         for (int32_t b = 0; b < blocks_fa; ++b) {
-            const unsigned long long* x = &h[(size_t)b * 8];
-            if (!x[2]) continue;   // long-path blocks have no walk stamps
+            const unsigned long long* x = &h[(size_t)b * 16];
+            if (!x[9]) continue;
             ++nb;
             t0 = std::min(t0, x[0]);
-            t6 = std::max(t6, x[6]);
-            for (int k = 0; k < 6; ++k) {
-                const double dt = (double)(x[k + 1] - x[k]) * 0.01;
+            t9 = std::max(t9, x[9]);
+            for (int k = 0; k < 8; ++k) {
+                const double dt = (slot[k] < 0 ? (double)(x[9] - x[8]) : (double)x[slot[k]]) * 0.01;
                 sum[k] += dt;
                 mx[k] = std::max(mx[k], dt);
             }
         }
-        fprintf(stderr, "[stamp] k_fx_a %d blocks span %.2f us; avg/max us: stage %.2f/%.2f mark %.2f/%.2f "
-                "walk %.2f/%.2f combine+ss %.2f/%.2f bar %.2f/%.2f tail %.2f/%.2f\n", nb, (t6 - t0) * 0.01,
-                sum[0] / nb, mx[0], sum[1] / nb, mx[1], sum[2] / nb, mx[2], sum[3] / nb, mx[3], sum[4] / nb, mx[4],
-                sum[5] / nb, mx[5]);
+        fprintf(stderr, "[stamp] k_fx_a %d blocks span %.2f us; per block avg/max us:", nb, (t9 - t0) * 0.01);
+        for (int k = 0; k < 8; ++k) fprintf(stderr, " %s %.2f/%.2f", nm[k], sum[k] / std::max(nb, 1), mx[k]);
+        fprintf(stderr, "\n");
     }
     // the only host round trip of the call: error words raised by the kernels
     std::vector<int32_t> hflag((size_t)4 * ng, 0);
