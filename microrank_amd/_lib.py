@@ -12,7 +12,8 @@ from typing import Optional
 
 import numpy as np
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libmicrorank_hip.so")
+# MR_LIB_PATH: an alternative build of the same library (timing experiments)
+LIB_PATH = os.environ.get("MR_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libmicrorank_hip.so")
 
 MR_OK, MR_ERR_ARG, MR_ERR_HIP, MR_ERR_VALUE, MR_ERR_ZERODIV, MR_ERR_OOM, MR_ERR_COMM, MR_ERR_STATE = range(8)
 MR_FP64, MR_FP32 = 0, 1

@@ -580,21 +580,22 @@ __device__ __forceinline__ int32_t fx_graph(const GDev* gs, int32_t ng, int32_t 
 struct FxLds {
     size_t su, lacc, head, tail, tsum, xl, owner, hbits, ids, total;
     bool su_lds;   // su staged in LDS; otherwise gathered from its global copy (L2-resident)
-    __host__ __device__ FxLds(int32_t N, int32_t TT, bool allow_su = true) {
-        size_t rest = ((size_t)N + 1) * 8 + 4 * (size_t)TT * 8 + 8 + (size_t)TT * 4 +
-                      ((size_t)FX_CAP * TT / 32 + 2) * 4 + 16 + ((size_t)FX_CAP * TT + 16) * 2;
+    // TT traces per tile, NS walk segments (the block size, a multiple of TT)
+    __host__ __device__ FxLds(int32_t N, int32_t TT, int32_t NS, bool allow_su = true) {
+        size_t rest = ((size_t)N + 1) * 8 + 2 * (size_t)NS * 8 + (size_t)TT * 8 + (size_t)TT * 8 + 8 +
+                      (size_t)NS * 4 + ((size_t)FX_CAP * TT / 32 + 2) * 8 + 16 + ((size_t)FX_CAP * TT + 16) * 2;
         su_lds = allow_su && ((size_t)N + 1) * 8 + rest <= FX_LDS_BUDGET;
         // with su in LDS, su and the accumulator interleave (16 B per op: one address for the
         // gather and the atomic of an entry)
         su = 0;
         lacc = su_lds ? 8 : 0;
         head = ((size_t)N + 1) * (su_lds ? 16 : 8);
-        tail = head + (size_t)TT * 8;
-        tsum = tail + (size_t)TT * 8;
+        tail = head + (size_t)NS * 8;
+        tsum = tail + (size_t)NS * 8;
         xl = tsum + (size_t)TT * 8;
         owner = xl + ((size_t)TT + 1) * 8;
-        hbits = owner + (size_t)TT * 4;
-        ids = (hbits + ((size_t)FX_CAP * TT / 32 + 2) * 4 + 15) / 16 * 16;
+        hbits = owner + (size_t)NS * 4;
+        ids = (hbits + ((size_t)FX_CAP * TT / 32 + 2) * 8 + 15) / 16 * 16;   // hbits: two buffers
         total = ids + ((size_t)FX_CAP * TT + 16) * 2;
     }
 };
@@ -626,23 +627,24 @@ __device__ __forceinline__ u32x4 fx_pad(u32x4 v, int32_t cidx, int32_t shift, in
 }
 
 // PF: blocks walk several tiles with the next tile's loads in flight; without PF every block
-// has one tile.  Both fit 128 VGPRs: two 512-thread blocks per CU where the LDS image allows.
-template <class Q, bool SUL, int MAXT, bool PF>
-__global__ void __launch_bounds__(MAXT, 4) k_fx_a(const GDev* __restrict__ gs, int32_t ng, int32_t split,
-                                                           double d, double alpha, int it) {
-    static_assert(FX_CAP == 24, "three 16-B id chunks per thread");
+// has one tile.  S: walk segments (threads) per trace of a tile -- S = 2 doubles the waves that
+// hide the gathers' latency at the same LDS image.  All variants fit 128 VGPRs.
+template <class Q, bool SUL, bool PF, int S>
+__global__ void __launch_bounds__(S * FX_TMAX, 4) k_fx_a(const GDev* __restrict__ gs, int32_t ng, int32_t split,
+                                                         double d, double alpha, int it, int32_t TT) {
+    static_assert(FX_CAP == 24, "at most three 16-B id chunks per thread");
     extern __shared__ __attribute__((aligned(16))) unsigned char lraw[];
-    __shared__ double red[MAXT / WAVE];
+    __shared__ double red[S * FX_TMAX / WAVE];
     __shared__ double msh[2];
     __shared__ int64_t nxe[2];   // the next tile's id range
     const unsigned long long ts0 = __builtin_amdgcn_s_memrealtime();
     const GDev& G = gs[fx_graph(gs, ng, split, 2)];
-    const int32_t TT = (int32_t)blockDim.x;
+    const int32_t NS = S * TT;   // == blockDim.x
     const int32_t lb = (int32_t)blockIdx.x - G.blk0f;
     const int cur = it & 1, nxt = cur ^ 1, k3 = it % 3;
     const int32_t T = G.T, N = G.N;
     const int32_t i = (int32_t)threadIdx.x;
-    const FxLds L_(N, TT, SUL);
+    const FxLds L_(N, TT, NS, SUL);
     // global operands through addrspace(1) pointers: global_load (vmcnt only), never flat
     const GLB int64_t* rs_off = gp(G.rs_off);
     const GLB u32x4* rs16 = gp((const u32x4*)G.rs16);   // 8 ids per 16 B; padded past nnz
@@ -666,10 +668,13 @@ __global__ void __launch_bounds__(MAXT, 4) k_fx_a(const GDev* __restrict__ gs, i
     const GLB unsigned long long* Mcur = mslot + (size_t)2 * MSH * k3;
     GLB unsigned long long* Mnext = mslot + (size_t)2 * MSH * ((k3 + 1) % 3);
     if (lb == 0 && i < 2 * MSH) mslot[(size_t)2 * MSH * ((k3 + 2) % 3) + i] = 0ull;
-    for (int32_t o = i; o <= N; o += TT) {   // once per block: the accumulator spans all its tiles
+    for (int32_t o = i; o <= N; o += NS) {   // once per block: the accumulator spans all its tiles
         if (SUL) su_l[AS * o] = sug[o];
         lacc[AS * o] = 0ull;
     }
+    const int32_t HW = FX_CAP * TT / 32 + 2;   // words of one trace-start bitmap (tile parity)
+    for (int32_t w = i; w < 2 * HW; w += NS) hbits[w] = 0u;
+    if (i == 0) xl[0] = 0ull;
     if (i < WAVE) {
         const double ms = wave_max(bits2d(Mcur[i]));
         const double mr = wave_max(bits2d(Mcur[MSH + i]));
@@ -692,14 +697,14 @@ __global__ void __launch_bounds__(MAXT, 4) k_fx_a(const GDev* __restrict__ gs, i
     u32x4 pv0 = {0u, 0u, 0u, 0u}, pv1 = pv0, pv2 = pv0;
 #define FX_OFFS(tile_, a_, b_)                                          \
     do {                                                                \
-        const int32_t t0_ = (tile_) * TT, tc_ = t0_ + min(i, T - t0_ - 1); \
+        const int32_t t0_ = (tile_) * TT, tc_ = t0_ + min(min(i, TT - 1), T - t0_ - 1); \
         a_ = rs_off[tc_];                                               \
         b_ = rs_off[tc_ + 1];                                           \
     } while (0)
     // ids chunks clamped in-bounds (the buffer is padded past nnz; a long tile ignores them)
 #define FX_BODY(tile_, e0s_, e1s_, qk_, ct_, wt_, v0_, v1_, v2_)                                   \
     do {                                                                                           \
-        const int32_t tc_ = (tile_) * TT + min(i, T - (tile_) * TT - 1);                           \
+        const int32_t tc_ = (tile_) * TT + min(min(i, TT - 1), T - (tile_) * TT - 1);              \
         qk_ = (double)qc[tc_];                                                                     \
         ct_ = c_t[tc_];                                                                            \
         wt_ = w_t[tc_];                                                                            \
@@ -707,8 +712,8 @@ __global__ void __launch_bounds__(MAXT, 4) k_fx_a(const GDev* __restrict__ gs, i
         const GLB u32x4* src_ = rs16 + (base_ >> 3);                                               \
         const int32_t nch_ = (int32_t)min((((e1s_) - base_) + 7) >> 3, (int64_t)FX_CAP / 8 * TT);  \
         v0_ = src_[min(i, nch_ - 1)];                                                              \
-        v1_ = src_[min(i + TT, nch_ - 1)];                                                         \
-        v2_ = src_[min(i + 2 * TT, nch_ - 1)];                                                     \
+        if (S < 3) v1_ = src_[min(i + NS, nch_ - 1)];                                              \
+        if (S < 2) v2_ = src_[min(i + 2 * NS, nch_ - 1)];                                          \
     } while (0)
 #define FX_BOUNDS(tile_, e0_, e1_)                                            \
     do {                                                                      \
@@ -730,19 +735,22 @@ __global__ void __launch_bounds__(MAXT, 4) k_fx_a(const GDev* __restrict__ gs, i
     // diagnostics (MR_FX_STAMP): thread 0 sums its clock per tile phase
     // (sums in LDS: no registers held across the walk)
     __shared__ unsigned long long ph[7];   // [6]: the last clock
-    const unsigned long long t_init = G.stamp ? __builtin_amdgcn_s_memrealtime() : 0ull;
-    if (G.stamp && i == 0) {
+    const bool stamp = G.stamp != nullptr;
+    const unsigned long long t_init = stamp ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    if (stamp && i == 0) {
         for (int k = 0; k < 6; ++k) ph[k] = 0ull;
         ph[6] = t_init;
     }
 #define FX_MARK(slot)                                                        \
     do {                                                                     \
-        if (G.stamp && i == 0) {                                             \
+        if (stamp && i == 0) {                                               \
             const unsigned long long nw_ = __builtin_amdgcn_s_memrealtime(); \
             ph[slot] += nw_ - ph[6];                                         \
             ph[6] = nw_;                                                     \
         }                                                                    \
     } while (0)
+    __syncthreads();   // accumulator, bitmaps and maxima ready
+    const double xsc = G.fx_scale / msh[1];   // X = rint(q / M_r * 2^SC), as one multiply
     for (int32_t tile = tb; tile < te; ++tile) {
         const bool first = tile == tb;
         if (!PF && !first) {
@@ -761,21 +769,37 @@ __global__ void __launch_bounds__(MAXT, 4) k_fx_a(const GDev* __restrict__ gs, i
         const int32_t shift = (int32_t)(e0 - base);
         const int64_t np_ = e1 - base;                 // positions [shift, np_) hold the tile's entries
         const bool bal = np_ <= (int64_t)FX_CAP * TT;
-        if (!first) __syncthreads();                   // the previous tile's readers are done
-        FX_MARK(4);
-        if (bal) {   // stage the id range
+        // No barrier opens the tile: the previous tile's walk barrier already orders its readers
+        // of ids/owner/xl before this staging, its combine reads of tsum/head/tail come before
+        // this tile's stage barrier in every thread, and the trace-start bitmaps alternate by
+        // tile parity (the other one is cleared here, for the next tile).
+        uint32_t* hb = hbits + (tile & 1) * HW;
+        // segment length L = 8, 16 or 32 positions (a power of two: divisions become shifts;
+        // 32 still fits the 64-bit start window read at a segment's first position)
+        const int32_t lgL = np_ <= 8 * (int64_t)NS ? 3 : np_ <= 16 * (int64_t)NS ? 4 : 5;
+        const int32_t L = 1 << lgL;
+        const int32_t ra = (int32_t)(a - base), rb = (int32_t)(b - base);
+        const unsigned long long X = own ? (unsigned long long)__double2ull_rn(qk * xsc) : 0ull;
+        {
+            uint32_t* hb_next = hbits + ((tile + 1) & 1) * HW;
+            for (int32_t w = i; w < HW; w += NS) hb_next[w] = 0u;
+        }
+        if (bal) {   // stage the id range and mark the trace starts / segment owners
             const int32_t nch = (int32_t)((np_ + 7) >> 3);
             if (i < nch) *(u32x4*)(ids + (size_t)i * 8) = fx_pad(pv0, i, shift, np_, N);
-            if (i + TT < nch) *(u32x4*)(ids + (size_t)(i + TT) * 8) = fx_pad(pv1, i + TT, shift, np_, N);
-            if (i + 2 * TT < nch) *(u32x4*)(ids + (size_t)(i + 2 * TT) * 8) = fx_pad(pv2, i + 2 * TT, shift, np_, N);
-            for (int32_t w = i; w < FX_CAP * TT / 32 + 2; w += TT) hbits[w] = 0u;
-            if (i == 0) {
-                owner[0] = -1;   // positions before `shift` belong to the previous tile
-                xl[0] = 0ull;
+            if (S < 3 && i + NS < nch) *(u32x4*)(ids + (size_t)(i + NS) * 8) = fx_pad(pv1, i + NS, shift, np_, N);
+            if (S < 2 && i + 2 * NS < nch)
+                *(u32x4*)(ids + (size_t)(i + 2 * NS) * 8) = fx_pad(pv2, i + 2 * NS, shift, np_, N);
+            if (i == 0) owner[0] = -1;   // positions before `shift` belong to the previous tile
+            if (own) {
+                xl[i + 1] = X;
+                atomicOr(&hb[ra >> 5], 1u << (ra & 31));
+                for (int32_t sg = (ra + L - 1) >> lgL; (sg << lgL) < rb; ++sg) owner[sg] = i;   // segments starting in t
             }
         }
-        FX_MARK(5);
+        FX_MARK(4);
         __syncthreads();
+        FX_MARK(5);
         // prefetch: tile + 1's ids and words, tile + 2's offsets (the last tiles reload themselves)
         int64_t m_a = 0, m_b = 0, e0n = e0, e1n = e1;
         double n_qk = 0.0;
@@ -789,27 +813,16 @@ __global__ void __launch_bounds__(MAXT, 4) k_fx_a(const GDev* __restrict__ gs, i
             FX_BODY(min(tile + 1, te - 1), e0n, e1n, n_qk, n_ct, n_wt, nv0, nv1, nv2);
             FX_OFFS(min(tile + 2, te - 1), m_a, m_b);
         }
-        const unsigned long long X = own ? (unsigned long long)__double2ull_rn(qk / msh[1] * G.fx_scale) : 0ull;
         FX_MARK(0);
         double acc = 0.0;
         if (bal) {
-            int32_t L = (int32_t)((np_ + 8 * TT - 1) / (8 * TT)) * 8;
-            if (L == 0) L = 8;
-            const int32_t ra = (int32_t)(a - base), rb = (int32_t)(b - base);
-            if (own) {
-                xl[i + 1] = X;
-                atomicOr(&hbits[ra >> 5], 1u << (ra & 31));
-                for (int32_t sg = (ra + L - 1) / L; sg * L < rb; ++sg) owner[sg] = i;   // segments starting in t
-            }
-            __syncthreads();
-            FX_MARK(1);
             const int32_t p = i * L;
             if (p < np_) {
                 const int32_t qe = (int32_t)min((int64_t)p + L, np_);
-                // trace starts of the segment (L <= 24 positions fit the 33+ bits left after the
+                // trace starts of the segment (L <= 32 positions fit the 33+ bits left after the
                 // shift); position p's own start is `st`, the rest are tested per 8-entry chunk
                 const unsigned long long bits =
-                    (((unsigned long long)hbits[(p >> 5) + 1] << 32) | hbits[p >> 5]) >> (p & 31);
+                    (((unsigned long long)hb[(p >> 5) + 1] << 32) | hb[p >> 5]) >> (p & 31);
                 int32_t c = owner[i];
                 bool st = bits & 1ull;                   // the segment's first piece starts a trace
                 const unsigned long long sb = bits & ~1ull;
@@ -827,13 +840,18 @@ __global__ void __launch_bounds__(MAXT, 4) k_fx_a(const GDev* __restrict__ gs, i
                     // would also wait for every atomic before it
                     double g[8];
                     unsigned long long xj[8];
+#ifndef MR_EXP
+#define MR_EXP 0   // timing experiments only: 1 drops the atomics, 2 the gathers, 3 both
+#endif
 #pragma unroll
-                    for (int j = 0; j < 8; ++j) g[j] = SUL ? su_l[AS * o[j]] : sug[o[j]];
+                    for (int j = 0; j < 8; ++j) g[j] = (MR_EXP & 2) ? (double)o[j] : SUL ? su_l[AS * o[j]] : sug[o[j]];
+                    if (!(MR_EXP & 1)) {
 #pragma unroll
-                    for (int j = 0; j < 8; ++j)
-                        xj[j] = xl[c + 1 + (int32_t)__builtin_popcount(m8 & ((2u << j) - 1u))];
+                        for (int j = 0; j < 8; ++j)
+                            xj[j] = xl[c + 1 + (int32_t)__builtin_popcount(m8 & ((2u << j) - 1u))];
 #pragma unroll
-                    for (int j = 0; j < 8; ++j) atomicAdd(&lacc[AS * o[j]], xj[j]);
+                        for (int j = 0; j < 8; ++j) atomicAdd(&lacc[AS * o[j]], xj[j]);
+                    }
 #pragma unroll
                     for (int j = 0; j < 8; ++j) {
                         if (m8 & (1u << j)) {   // a new trace starts at ch + j
@@ -855,7 +873,7 @@ __global__ void __launch_bounds__(MAXT, 4) k_fx_a(const GDev* __restrict__ gs, i
             __syncthreads();
             FX_MARK(2);
             if (own && rb > ra) {
-                const int32_t sa = ra / L, sb = (rb - 1) / L;
+                const int32_t sa = ra >> lgL, sb = (rb - 1) >> lgL;
                 if (sa == sb) {
                     acc = tsum[i];
                 } else {
@@ -872,7 +890,7 @@ __global__ void __launch_bounds__(MAXT, 4) k_fx_a(const GDev* __restrict__ gs, i
             for (int64_t lo = e0; lo < e1; lo += cap) {
                 const int64_t hi = min(lo + (int64_t)cap, e1);
                 __syncthreads();
-                for (int64_t e = lo + i; e < hi; e += TT) ids[e - lo] = rs16s[e];
+                for (int64_t e = lo + i; e < hi; e += NS) ids[e - lo] = rs16s[e];
                 __syncthreads();
                 const int32_t x0 = (int32_t)(max(a, lo) - lo), x1 = (int32_t)(min(b, hi) - lo);
                 for (int32_t c = x0; c < x1; c += 8) {
@@ -888,6 +906,7 @@ __global__ void __launch_bounds__(MAXT, 4) k_fx_a(const GDev* __restrict__ gs, i
                     for (int j = 0; j < 8; ++j) atomicAdd(&lacc[AS * o[(j + lane) & 7]], X);
                 }
             }
+            __syncthreads();   // the next tile's staging overwrites ids
         }
         const double rp = d * (acc / msh[0]) + (double)ct;   // pagerank.py:125
         if (own) rmax = nmax(rmax, rp);
@@ -923,7 +942,7 @@ __global__ void __launch_bounds__(MAXT, 4) k_fx_a(const GDev* __restrict__ gs, i
         const GLB int32_t* ss_par = gp(G.ss_par);
         const GLB float* pw = gp(G.pw);
         GLB double* ssv = gpw(G.fx_ssv);
-        for (int32_t oss = lb * TT + i; oss < N; oss += G.n_fa * TT) {
+        for (int32_t oss = lb * NS + i; oss < N; oss += G.n_fa * NS) {
             double bb = 0.0;
             for (int64_t e = ss_off[oss]; e < ss_off[oss + 1]; ++e) {
                 const int32_t pp = ss_par[e];
@@ -932,10 +951,10 @@ __global__ void __launch_bounds__(MAXT, 4) k_fx_a(const GDev* __restrict__ gs, i
             ssv[oss] = alpha * (bb / msh[0]);
         }
     }
-    const unsigned long long t_loop = G.stamp ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    const unsigned long long t_loop = stamp ? __builtin_amdgcn_s_memrealtime() : 0ull;
     __syncthreads();
     GLB unsigned long long* prow = gpw(G.fx_part) + (size_t)lb * N;
-    for (int32_t o = i; o < N; o += TT) prow[o] = lacc[AS * o];
+    for (int32_t o = i; o < N; o += NS) prow[o] = lacc[AS * o];
     rmax = block_max(rmax, red);
     if (i == 0) {
         atomicMax((unsigned long long*)&Mnext[MSH + blockIdx.x % MSH], d2bits(rmax));
@@ -1162,6 +1181,31 @@ void mr_prof_end(mr_ctx* ctx, double bytes);
 // traces per k_fx_a block (= its block size): the larger of 512/256 whose LDS image fits
 // (MR_TT caps it for measurements); 0 when none fits
 constexpr size_t FX_LDS_MAX = 160 * 1024 - 512;   // minus the kernel's static LDS
+// walk segments per trace of a tile (k_fx_a's S): one-tile blocks take S = 1 (two 512-thread
+// blocks per CU), pipelined multi-tile blocks S = 2 (16 waves per CU on one LDS image);
+// MR_FX_S = 1 or 2 forces it for measurements
+static int fx_s(bool multi) {
+    static const int v = [] {
+        const char* e = getenv("MR_FX_S");
+        return e ? (atoi(e) == 1 ? 1 : 2) : 0;
+    }();
+    return v ? v : (multi ? 2 : 1);
+}
+
+using FxA = void (*)(const GDev*, int32_t, int32_t, double, double, int, int32_t);
+static FxA fx_kernel(bool fp32, bool sul, bool pf, int S) {
+    static const FxA tab[2][2][2][2] = {
+        {{{k_fx_a<double, false, false, 1>, k_fx_a<double, false, false, 2>},
+          {k_fx_a<double, false, true, 1>, k_fx_a<double, false, true, 2>}},
+         {{k_fx_a<double, true, false, 1>, k_fx_a<double, true, false, 2>},
+          {k_fx_a<double, true, true, 1>, k_fx_a<double, true, true, 2>}}},
+        {{{k_fx_a<float, false, false, 1>, k_fx_a<float, false, false, 2>},
+          {k_fx_a<float, false, true, 1>, k_fx_a<float, false, true, 2>}},
+         {{k_fx_a<float, true, false, 1>, k_fx_a<float, true, false, 2>},
+          {k_fx_a<float, true, true, 1>, k_fx_a<float, true, true, 2>}}}};
+    return tab[fp32 ? 1 : 0][sul ? 1 : 0][pf ? 1 : 0][S == 2 ? 1 : 0];
+}
+
 static int fx_tt(int32_t N) {
     static const int cap = [] {
         const char* e = getenv("MR_TT");
@@ -1169,7 +1213,7 @@ static int fx_tt(int32_t N) {
         return (v == 256 || v == FX_TMAX) ? v : FX_TMAX;
     }();
     for (int tt = cap; tt >= 256; tt >>= 1)
-        if (FxLds(N, tt).total <= FX_LDS_MAX) return tt;
+        if (FxLds(N, tt, 2 * tt).total <= FX_LDS_MAX) return tt;   // fits either S
     return 0;
 }
 
@@ -1186,14 +1230,12 @@ static int64_t fx_blocks(int32_t T, int32_t N, int TT) {
     }();
     const int64_t tiles = cdiv((int64_t)T, TT);
     // resident blocks per CU: LDS image and VGPRs (the runtime's occupancy for the variant)
-    const FxLds L(N, TT);
     auto per_cu = [&](bool pf) {
+        const int S = fx_s(pf);
+        const FxLds L(N, TT, S * TT);
         int n = 0;
-        const void* kfn = pf ? (L.su_lds ? (const void*)k_fx_a<double, true, FX_TMAX, true>
-                                         : (const void*)k_fx_a<double, false, FX_TMAX, true>)
-                             : (L.su_lds ? (const void*)k_fx_a<double, true, FX_TMAX, false>
-                                         : (const void*)k_fx_a<double, false, FX_TMAX, false>);
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kfn, TT, L.total) != hipSuccess || n < 1)
+        const void* kfn = (const void*)fx_kernel(false, L.su_lds, pf, S);
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kfn, S * TT, L.total) != hipSuccess || n < 1)
             n = std::max<int>(1, (int)(FX_LDS_MAX / L.total));
         return (int64_t)n;
     };
@@ -1475,8 +1517,7 @@ int mr_pagerank_batch_impl(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly,
         v.blk0b = blocks_b;
         bytes += iter_bytes(g, fp32);
         if (g->fused) {
-            lds_f = std::max(lds_f, FxLds(g->N, TT).total);
-            sul = sul && FxLds(g->N, TT).su_lds;
+            sul = sul && FxLds(g->N, TT, 2 * TT).su_lds;   // (fits either S)
             multi = multi || v.n_fa < cdiv(g->T, TT);
             continue;   // no tile-path blocks (n_tb = n_tiles = n_ob = 0)
         }
@@ -1499,17 +1540,14 @@ int mr_pagerank_batch_impl(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly,
     DBuf<GDev> dv;
     MR_TRY(dv.upload(ctx, hv.data(), hv.size()));
     const int32_t split_fa = ng == 2 ? hv[1].blk0f : 0, split_fb = ng == 2 ? hv[1].blk0fb : 0;
-    using FxA = void (*)(const GDev*, int32_t, int32_t, double, double, int);
-    const FxA fx_tab[2][2][2] = {
-        {{k_fx_a<double, false, FX_TMAX, false>, k_fx_a<double, false, FX_TMAX, true>},
-         {k_fx_a<double, true, FX_TMAX, false>, k_fx_a<double, true, FX_TMAX, true>}},
-        {{k_fx_a<float, false, FX_TMAX, false>, k_fx_a<float, false, FX_TMAX, true>},
-         {k_fx_a<float, true, FX_TMAX, false>, k_fx_a<float, true, FX_TMAX, true>}}};
-    const FxA fx_a = fx_tab[fp32 ? 1 : 0][sul ? 1 : 0][multi ? 1 : 0];
+    const int fx_S = fx_s(multi);
+    const FxA fx_a = fx_kernel(fp32, sul, multi, fx_S);
+    for (int i = 0; i < ng; ++i)
+        if (gs[i]->fused) lds_f = std::max(lds_f, FxLds(gs[i]->N, TT, fx_S * TT, sul).total);
     for (int it = 0; it < iters; ++it) {
         mr_prof_begin(ctx);
         if (blocks_fa) {
-            hipLaunchKernelGGL(fx_a, dim3(blocks_fa), dim3(TT), lds_f, st, dv.p, ng, split_fa, d, alpha, it);
+            hipLaunchKernelGGL(fx_a, dim3(blocks_fa), dim3(fx_S * TT), lds_f, st, dv.p, ng, split_fa, d, alpha, it, TT);
             MR_DEBUG_CHECK(ctx, "k_fx_a");
             if (!sharded) {
                 hipLaunchKernelGGL(k_fx_b, dim3(blocks_fb), dim3(WAVE * FB_W), 0, st, dv.p, ng, split_fb, d, it, 0);
@@ -1544,7 +1582,7 @@ int mr_pagerank_batch_impl(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly,
         MR_TRY(dstamp.download(ctx, h.data(), h.size()));
         MR_TRY_HIP(ctx, hipStreamSynchronize(st));
         unsigned long long t0 = ~0ull, t9 = 0;
-        const char* nm[8] = {"init", "bar-in", "stage", "bar+pf", "mark", "walk", "rest", "ss+rows"};
+        const char* nm[8] = {"init", "stage", "bar", "pf", "-", "walk", "rest", "ss+rows"};
         const int slot[8] = {1, 6, 7, 2, 3, 4, 5, -1};
         double sum[8] = {0}, mx[8] = {0};
         int nb = 0;

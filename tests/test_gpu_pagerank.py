@@ -100,3 +100,55 @@ def test_c2_scale_against_oracle(c2, anomaly):
     w3, _ = dg.fetch()
     np.testing.assert_allclose(w3, np.array(list(w_ref.values())), rtol=RTOL32, atol=0)
     dg.close()
+
+
+def _oracle_graph_from_host(hg) -> "orc.Graph":
+    T, N = hg.T, hg.N
+    sr_t = np.repeat(np.arange(T, dtype=np.int64), np.diff(hg.sr_off))
+    ss_c = np.repeat(np.arange(N, dtype=np.int64), np.diff(hg.ss_off))
+    return orc.Graph(list(range(N)), list(range(T)), sr_t, hg.sr_ops.astype(np.int64), sr_t,
+                     hg.sr_ops.astype(np.int64), hg.len_t.astype(np.int64), hg.len_o.astype(np.int64), ss_c,
+                     hg.ss_par.astype(np.int64), hg.nchild.astype(np.int64), np.arange(T, dtype=np.int64),
+                     hg.len_t.astype(np.int64))
+
+
+def _with_long_traces(hg, n_long, width, seed):
+    """Append n_long traces of `width` distinct ops each: their tiles exceed the staged-id cap and
+    take the fused kernel's long-tile path."""
+    from microrank_amd.graph import HostGraph
+
+    rng = np.random.default_rng(seed)
+    ops = np.sort(np.stack([rng.choice(hg.N, width, replace=False) for _ in range(n_long)]), axis=1)
+    sr_ops = np.concatenate([hg.sr_ops, ops.ravel().astype(np.int32)])
+    sr_off = np.concatenate([hg.sr_off, hg.sr_off[-1] + width * np.arange(1, n_long + 1, dtype=np.int64)])
+    len_t = np.concatenate([hg.len_t, np.full(n_long, width, np.int32)])
+    len_o = hg.len_o + np.bincount(ops.ravel(), minlength=hg.N).astype(np.int32)
+    T = hg.T + n_long
+    return HostGraph(range(hg.N), range(T), sr_off, sr_ops, None, None, len_t, len_o, hg.ss_off, hg.ss_par,
+                     hg.nchild, None, None)
+
+
+@pytest.mark.parametrize("anomaly", [False, True])
+def test_large_op_count_multi_tile_long_tiles(anomaly):
+    """9k ops (su gathered from L2, not LDS), 250k traces (several tiles per block: the pipelined
+    variant) plus 3k 60-op traces (tiles past the staged-id cap: the long-tile path), ragged last
+    tile: GPU vs oracle at 1e-10, coverage exact, bitwise reruns."""
+    from microrank_amd import _lib, synth
+    from microrank_amd.graph import DeviceGraph
+
+    hg = _with_long_traces(synth.big_graph(9000, 250_000, seed=5), 3000, 60, seed=6)
+    g = _oracle_graph_from_host(hg)
+    kind = orc.trace_kinds(g)
+    v = orc.preference(g, kind, anomaly)
+    s = orc.power_iteration(g, v)
+    w_ref, cov_ref = orc.weights(g, s)
+    ctx = _lib.default_context()
+    dg = DeviceGraph.upload(ctx, hg)
+    dg.pagerank(anomaly)
+    w, cov = dg.fetch()
+    np.testing.assert_array_equal(cov, np.array(list(cov_ref.values())))
+    np.testing.assert_allclose(w, np.array(list(w_ref.values())), rtol=RTOL64, atol=0)
+    dg.pagerank(anomaly)
+    w2, _ = dg.fetch()
+    assert w2.tobytes() == w.tobytes(), "rerun not bitwise identical"
+    dg.close()
