@@ -185,7 +185,10 @@ def run_c4(args, world, rank, dist):
     from microrank_amd.graph import DeviceGraph
 
     t_local = args.c4_traces // world + (1 if rank < args.c4_traces % world else 0)
+    t_gen = time.perf_counter()
     hg = synth.big_graph(args.c4_ops, t_local, seed=11, shard=(rank, world))
+    print(f"[bench] rank {rank}: generated {t_local} traces / {hg.sr_ops.size} pairs in "
+          f"{time.perf_counter() - t_gen:.1f} s", file=sys.stderr, flush=True)
     nnz_local = int(hg.sr_ops.size)
     ctx = _lib.default_context()
     if world > 1:
@@ -193,6 +196,7 @@ def run_c4(args, world, rank, dist):
     dg = DeviceGraph.upload(ctx, hg)
     del hg
     prec = args.precision
+    fused = args.c4_ops <= 16384   # N <= FX_NMAX: fused k_fx_a/k_fx_b, else the tile path
     for _ in range(max(args.warmup, 1)):   # the first call also runs the once-per-graph exchange
         shard.sharded_pagerank(dg, True, precision=prec)
     E = dg.info()["E"]
@@ -231,10 +235,13 @@ def run_c4(args, world, rank, dist):
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "f64" if prec == "fp64" else "f32",
         "data": "synthetic (power-law op popularity, root op in every trace, random call tree; per-rank shards)",
-        "config": {"workload": f"C4 sharded trace_pagerank: {args.c4_ops} ops / {args.c4_traces} traces over "
-                               f"{world} GPU(s), anomaly preference, 25 iterations", "nnz": int(nnz_all), "call_edges": E,
-                   "parallelism": f"trace shards x{world}, RCCL limb all-reduce per iteration"},
-        "roofline": {"bound": "hbm", "kernel": "one Jacobi iteration on this rank (k_fx_a + k_fx_b"
+        "config": {"workload": f"{args.config.upper()} sharded trace_pagerank: {args.c4_ops} ops / {args.c4_traces} "
+                               f"traces over {world} GPU(s), anomaly preference, 25 iterations", "nnz": int(nnz_all),
+                   "call_edges": E,
+                   "parallelism": f"trace shards x{world}, RCCL " + ("limb" if fused else "fp64 op-sum")
+                                  + " all-reduce per iteration"},
+        "roofline": {"bound": "hbm", "kernel": "one Jacobi iteration on this rank ("
+                                               + ("k_fx_a + k_fx_b" if fused else "k_iter_a + k_iter_b")
                                                + (" + 2 all-reduces)" if world > 1 else ")"),
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
@@ -254,17 +261,25 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--precision", choices=["fp64", "fp32"], default="fp64")
+    ap.add_argument("--precision", choices=["fp64", "fp32"], default=None,
+                    help="default fp64 (c2, c4), fp32 (c5: BASELINE configs[4])")
     ap.add_argument("--ops", type=int, default=1000)
     ap.add_argument("--traces", type=int, default=200_000)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC passes for roofline.traffic")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
-    ap.add_argument("--config", choices=["c2", "c4"], default="c2",
-                    help="c2: RCA windows (default, weak scaling); c4: one trace-sharded graph (strong scaling)")
-    ap.add_argument("--c4-ops", type=int, default=10_000)
-    ap.add_argument("--c4-traces", type=int, default=10_000_000)
+    ap.add_argument("--config", choices=["c2", "c4", "c5"], default="c2",
+                    help="c2: RCA windows (default, weak scaling); c4 / c5: one trace-sharded graph (strong "
+                         "scaling; c5 = 100k ops / 100M traces fp32, the tile-path iteration)")
+    ap.add_argument("--c4-ops", type=int, default=None, help="c4/c5 op count (default 10k / 100k)")
+    ap.add_argument("--c4-traces", type=int, default=None, help="c4/c5 trace count over all ranks (10M / 100M)")
     args = ap.parse_args()
+    if args.precision is None:
+        args.precision = "fp32" if args.config == "c5" else "fp64"
+    if args.c4_ops is None:
+        args.c4_ops = 100_000 if args.config == "c5" else 10_000
+    if args.c4_traces is None:
+        args.c4_traces = 100_000_000 if args.config == "c5" else 10_000_000
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -279,7 +294,7 @@ def main():
 
         dist.init_process_group("gloo")
     os.environ.setdefault("MICRORANK_DEVICE", str(local))
-    if args.config == "c4":
+    if args.config in ("c4", "c5"):
         out = run_c4(args, world, rank, dist)
         if out is not None:
             print(json.dumps(out), flush=True)

@@ -199,10 +199,10 @@ int mr_comm_set_host(mr_ctx* ctx, mr_host_coll_fn fn, void* user, int nranks, in
  * a trace on one rank) over the GLOBAL node index space, with this rank's partial len_o and
  * nchild and its local call edges.  Once per graph the library sums len_o / nchild / coverage,
  * unites the call edges, merges the trace-kind classes and the preference sums over the ranks;
- * per iteration it sums the exact fixed-point P_sr r partials (uint64 limbs) and takes the max of
- * r'.  Afterwards every rank holds the same weight and coverage vectors (mr_graph_fetch).
- * Requires a collective backend (mr_comm_init or mr_comm_set_host) and the fused iteration
- * (N <= 16384). */
+ * per iteration it takes the max of r' and sums the P_sr r partials: exact fixed-point uint64
+ * limbs on the fused iteration (N <= 16384), fp64 per-op sums on the tile path (larger N, C5).
+ * Afterwards every rank holds the same weight and coverage vectors (mr_graph_fetch).
+ * Requires a collective backend (mr_comm_init or mr_comm_set_host). */
 int mr_pagerank_sharded(mr_ctx* ctx, mr_graph* g, int anomaly, double d, double alpha, int iters,
                         int precision, uint32_t flags);
 

@@ -137,6 +137,7 @@ struct mr_graph {
     DBuf<uint64_t> fx_part;   // [n_blocks * N]
     DBuf<double> fx_ssv;      // [N] alpha * (P_ss s_k)[o] / M_s(k), from k_fx_a for k_fx_b
     DBuf<uint64_t> fx_limb;   // [2N] sharded graphs: exact limb sums per op, all-reduced per iteration
+    DBuf<double> op_sum;      // [N] sharded tile-path graphs: this rank's P_sr r per op, all-reduced
     // per-trace / per-op constants
     DBuf<int32_t> len_t, len_o, nchild, cov;
     DBuf<float> w_t, u_o, pw;    // fp32(1/len_t), fp32(1/len_o), fp32(1/nchild)

@@ -368,6 +368,7 @@ struct GDev {
     unsigned long long* fx_part;
     double* fx_ssv;
     unsigned long long* fx_limb;   // sharded: [2N] (lo, hi) limb sums per op
+    double* op_sum;                // sharded tile path: [N] pair-partial sums per op
     unsigned long long* stamp;   // diagnostics (MR_FX_STAMP): per-block phase clocks, else null
     double fx_scale, fx_iscale;
     int32_t T, N, n_tb, n_tiles, tshift, lds_su, blk0, n_ob, blk0b;
@@ -504,7 +505,10 @@ __global__ void __launch_bounds__(TB) k_iter_a(const GDev* __restrict__ gs, int3
 
 // Iteration k, second half: a wave per op combines the op's pair partials in tile order and adds
 // the call-graph term: s'[o] = d * (sum / M_r(k) + alpha * sum_p pw_p s_k[p] / M_s(k))  (:122-124)
-__global__ void __launch_bounds__(TB) k_iter_b(const GDev* __restrict__ gs, int32_t ng, double d, double alpha, int it) {
+// Sharded graphs (traces split over ranks) run it twice around an fp64 SUM all-reduce of the
+// per-op sums: mode 1 writes this rank's sum to op_sum, mode 2 finishes from the reduced op_sum.
+__global__ void __launch_bounds__(TB) k_iter_b(const GDev* __restrict__ gs, int32_t ng, double d, double alpha, int it,
+                                               int mode) {
     __shared__ int32_t sg;
     if (threadIdx.x == 0) sg = graph_of(gs, ng, (int32_t)blockIdx.x, 1);
     __syncthreads();
@@ -515,10 +519,18 @@ __global__ void __launch_bounds__(TB) k_iter_b(const GDev* __restrict__ gs, int3
     const int cur = it & 1, nxt = cur ^ 1, k3 = it % 3;
     const unsigned long long* Mcur = G.mslot + (size_t)2 * MSH * k3;
     unsigned long long* Mnext = G.mslot + (size_t)2 * MSH * ((k3 + 1) % 3);
-    const double Ms = wave_max(bits2d(Mcur[lane])), Mr = wave_max(bits2d(Mcur[MSH + lane]));
     double sum = 0.0;
-    for (int32_t i = G.op_pr_off[o] + lane; i < G.op_pr_off[o + 1]; i += WAVE) sum += G.part[G.op_pr[i]];
-    sum = wave_sum(sum);
+    if (mode != 2) {
+        for (int32_t i = G.op_pr_off[o] + lane; i < G.op_pr_off[o + 1]; i += WAVE) sum += G.part[G.op_pr[i]];
+        sum = wave_sum(sum);
+        if (mode == 1) {
+            if (lane == 0) G.op_sum[o] = sum;
+            return;
+        }
+    } else {
+        sum = G.op_sum[o];
+    }
+    const double Ms = wave_max(bits2d(Mcur[lane])), Mr = wave_max(bits2d(Mcur[MSH + lane]));
     const double* sp_cur = G.spb[cur];
     double bb = 0.0;
     for (int64_t e = G.ss_off[o] + lane; e < G.ss_off[o + 1]; e += WAVE) {
@@ -1497,6 +1509,7 @@ int mr_pagerank_batch_impl(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly,
         v.fx_part = (unsigned long long*)g->fx_part.p;
         v.fx_ssv = g->fx_ssv.p;
         v.fx_limb = (unsigned long long*)g->fx_limb.p;
+        v.op_sum = g->op_sum.p;
         v.stamp = nullptr;
         const int64_t nfa = g->fused ? fx_blocks(g->T, g->N, TT) : 0;
         // a row entry stays below 2^63; shards of one graph hold different trace counts, and their
@@ -1565,7 +1578,14 @@ int mr_pagerank_batch_impl(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly,
             MR_DEBUG_CHECK(ctx, "k_iter_a");
         }
         if (blocks_b) {
-            hipLaunchKernelGGL(k_iter_b, dim3(blocks_b), dim3(TB), 0, st, dv.p, ng, d, alpha, it);
+            if (!sharded) {
+                hipLaunchKernelGGL(k_iter_b, dim3(blocks_b), dim3(TB), 0, st, dv.p, ng, d, alpha, it, 0);
+            } else {   // r' max over ranks, then the per-op P_sr r sums over ranks (fp64 SUM)
+                MR_TRY(mr_coll_allreduce(ctx, gs[0]->mslot.p + (size_t)2 * MSH * ((it + 1) % 3) + MSH, MSH, MR_DT_U64, 1));
+                hipLaunchKernelGGL(k_iter_b, dim3(blocks_b), dim3(TB), 0, st, dv.p, ng, d, alpha, it, 1);
+                MR_TRY(mr_coll_allreduce(ctx, gs[0]->op_sum.p, (int64_t)gs[0]->N, MR_DT_F64, 0));
+                hipLaunchKernelGGL(k_iter_b, dim3(blocks_b), dim3(TB), 0, st, dv.p, ng, d, alpha, it, 2);
+            }
             MR_DEBUG_CHECK(ctx, "k_iter_b");
         }
         mr_prof_end(ctx, bytes);
@@ -1729,12 +1749,12 @@ extern "C" int mr_pagerank_sharded(mr_ctx* ctx, mr_graph* g, int anomaly, double
                                    int precision, uint32_t flags) {
     if (!ctx || !g || g->ctx != ctx) return mr_fail(ctx, MR_ERR_ARG, "mr_pagerank_sharded: bad handles");
     if (!mr_coll_ready(ctx) && ctx->nranks != 1) return mr_fail(ctx, MR_ERR_COMM, "no collective backend");
-    if (!g->fused) return mr_fail(ctx, MR_ERR_ARG, "mr_pagerank_sharded needs the fused iteration (N <= %d)", FX_NMAX);
     MR_TRY_HIP(ctx, hipSetDevice(ctx->device));
     if (!g->sharded_done) {   // the graph-level exchange happens once per graph
         MR_TRY(shard_exchange(ctx, g));
         g->sharded_done = true;
     }
-    MR_TRY(g->fx_limb.alloc(ctx, 2 * (size_t)std::max(g->N, 1)));
+    if (g->fused) MR_TRY(g->fx_limb.alloc(ctx, 2 * (size_t)std::max(g->N, 1)));   // fixed-point limbs
+    else MR_TRY(g->op_sum.alloc(ctx, (size_t)std::max(g->N, 1)));                    // tile path: fp64 sums
     return mr_pagerank_batch_impl(ctx, &g, &anomaly, 1, d, alpha, iters, precision, flags, true);
 }

@@ -20,6 +20,8 @@ from __future__ import annotations
 from dataclasses import dataclass
 from typing import Optional
 
+import os
+
 import numpy as np
 
 from .spans import UI_SERVICE, SpanTable
@@ -296,6 +298,25 @@ def slo_frame(seed: int = 7, sizes=SLO_SIZES):
     })
 
 
+_BIG_CHUNK = 1 << 21   # traces per generation chunk of big_graph
+
+
+def _big_chunk(job):
+    """Traces of one big_graph chunk: (len_t, len_o partial, distinct ops per trace, sorted ops)."""
+    rng, T, N, cdf, spans_mean = job
+    if not isinstance(rng, np.random.Generator):
+        rng = np.random.default_rng(rng)
+    k = np.maximum(rng.poisson(spans_mean - 1.0, T), 1).astype(np.int64) + 1        # spans per trace
+    S = int(k.sum())
+    trace = np.repeat(np.arange(T, dtype=np.int64), k)
+    op = np.searchsorted(cdf, rng.random(S), side="right").clip(0, N - 1).astype(np.int64)
+    op[np.r_[0, np.cumsum(k)[:-1]]] = 0                                              # root span
+    len_o = np.bincount(op, minlength=N)
+    key = np.unique(trace * N + op)
+    del trace, op
+    return k.astype(np.int32), len_o, np.bincount(key // N, minlength=T), (key % N).astype(np.int32)
+
+
 def big_graph(n_ops: int, n_traces: int, seed: int = 11, spans_mean: float = 19.0, zipf_s: float = 1.1,
               fp_dup: float = 0.25, shard: tuple | None = None):
     """A C4/C5-scale op<->trace graph generated directly as incidence lists (no span table):
@@ -313,24 +334,23 @@ def big_graph(n_ops: int, n_traces: int, seed: int = 11, spans_mean: float = 19.
     rank, world = shard if shard is not None else (0, 1)
     rng = np.random.default_rng(seed if shard is None else (seed, rank, world))
     T, N = int(n_traces), int(n_ops)
-    k = np.maximum(rng.poisson(spans_mean - 1.0, T), 1).astype(np.int64) + 1        # spans per trace
-    S = int(k.sum())
-    trace = np.repeat(np.arange(T, dtype=np.int64), k)
     w = 1.0 / np.arange(1, N + 1, dtype=np.float64) ** zipf_s
     cdf = np.cumsum(w / w.sum())
-    op = np.searchsorted(cdf, rng.random(S), side="right").clip(0, N - 1).astype(np.int64)
-    first = np.zeros(S, bool)
-    first[np.r_[0, np.cumsum(k)[:-1]]] = True
-    op[first] = 0                                                                    # root span
-    len_t = k.astype(np.int32)
-    len_o = np.bincount(op, minlength=N).astype(np.int32)
-    key = np.unique(trace * N + op)
-    del trace, op
-    tr = key // N
-    sr_ops = (key % N).astype(np.int32)
+    if T <= _BIG_CHUNK:
+        parts = [_big_chunk((rng, T, N, cdf, spans_mean))]
+    else:   # C5-sized graphs (10^8 traces, 2x10^9 spans): chunks with their own streams, in parallel
+        from concurrent.futures import ProcessPoolExecutor
+
+        jobs = [((seed, rank, world, c), min(_BIG_CHUNK, T - c0), N, cdf, spans_mean)
+                for c, c0 in enumerate(range(0, T, _BIG_CHUNK))]
+        with ProcessPoolExecutor(max_workers=min(16, os.cpu_count() or 1)) as ex:
+            parts = list(ex.map(_big_chunk, jobs))
+    len_t = np.concatenate([p[0] for p in parts])
+    len_o = np.sum([p[1] for p in parts], axis=0).astype(np.int32)
     sr_off = np.zeros(T + 1, np.int64)
-    np.cumsum(np.bincount(tr, minlength=T), out=sr_off[1:])
-    del key, tr
+    np.cumsum(np.concatenate([p[2] for p in parts]), out=sr_off[1:])
+    sr_ops = np.concatenate([p[3] for p in parts])
+    del parts
     # call tree: every op but the root has one parent of smaller index
     trng = rng if shard is None else np.random.default_rng(seed)
     child = np.arange(1, N, dtype=np.int64)

@@ -2,7 +2,9 @@
 of a window's traces; collectives go through the host-staged backend over gloo.  The weights
 must equal the whole graph's on one GPU (the per-iteration P_sr r sums are exact integers, so
 only the once-per-graph preference sums may round differently), coverage exactly, and both
-ranks bitwise.  A one-rank RCCL communicator exercises the RCCL plumbing of the same path."""
+ranks bitwise.  A one-rank RCCL communicator exercises the RCCL plumbing of the same path.
+The tile path (N > 16384, config C5; or forced with MR_NO_FUSED) sums fp64 per-op partials over
+the ranks instead: equal to the whole graph within 1e-10, ranks bitwise."""
 import os
 import socket
 
@@ -36,8 +38,10 @@ def _whole(anomaly):
     return w, cov
 
 
-def _worker(rank, world, port, anomaly, backend, q):
+def _worker(rank, world, port, anomaly, backend, q, big=None, tile=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if tile:
+        os.environ["MR_NO_FUSED"] = "1"   # read once, at this process's first graph prepare
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from gpu_util import host_graph_from_oracle
@@ -49,8 +53,13 @@ def _worker(rank, world, port, anomaly, backend, q):
             shard.use_host(ctx)
         else:
             shard.use_rccl(ctx)
-        dg = DeviceGraph.upload(ctx, host_graph_from_oracle(_shard(_window_graph(), rank, world)))
-        w, cov = shard.sharded_pagerank(dg, anomaly)
+        if big is None:
+            hg = host_graph_from_oracle(_shard(_window_graph(), rank, world))
+        else:
+            from microrank_amd import synth
+            hg = synth.big_graph(big[0], big[1], seed=3, shard=(rank, world))
+        dg = DeviceGraph.upload(ctx, hg)
+        w, cov = shard.sharded_pagerank(dg, anomaly, precision=big[2] if big else "fp64")
         info = dg.info()
         dg.close()
         ctx.close()
@@ -61,11 +70,11 @@ def _worker(rank, world, port, anomaly, backend, q):
         dist.destroy_process_group()
 
 
-def _run(world, anomaly, backend):
+def _run(world, anomaly, backend, big=None, tile=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, anomaly, backend, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, anomaly, backend, q, big, tile)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=180) for _ in procs]
@@ -93,3 +102,62 @@ def test_one_rank_rccl_matches_whole_graph():
     (rank, w, cov, info), = _run(1, True, "rccl")
     np.testing.assert_allclose(w, w_ref, rtol=1e-12, atol=0)
     np.testing.assert_array_equal(cov, cov_ref)
+
+
+def test_two_tile_path_shards_match_whole_graph():
+    """Small window, both ranks forced onto the tile path: fp64 op-sum all-reduce."""
+    w_ref, cov_ref = _whole(True)
+    res = _run(2, True, "host", tile=True)
+    for rank, w, cov, info in res:
+        np.testing.assert_allclose(w, w_ref, rtol=1e-10, atol=0)
+        np.testing.assert_array_equal(cov, cov_ref)
+    assert res[0][1].tobytes() == res[1][1].tobytes(), "ranks disagree"
+
+
+def _union_of_shards(n_ops, n_traces, world):
+    """The whole graph the shards of synth.big_graph(shard=(r, world)) make up."""
+    from microrank_amd import synth
+    from microrank_amd.graph import HostGraph
+
+    parts = [synth.big_graph(n_ops, n_traces, seed=3, shard=(r, world)) for r in range(world)]
+    sr_ops = np.concatenate([p.sr_ops for p in parts])
+    offs = [parts[0].sr_off]
+    for p in parts[1:]:
+        offs.append(offs[-1][-1] + p.sr_off[1:])
+    T = sum(p.T for p in parts)
+    return HostGraph(range(n_ops), range(T), np.concatenate(offs), sr_ops, None, None,
+                     np.concatenate([p.len_t for p in parts]), sum(p.len_o for p in parts), parts[0].ss_off,
+                     parts[0].ss_par, parts[0].nchild, None, None)
+
+
+@pytest.mark.parametrize("precision", ["fp64", "fp32"])
+def test_large_op_count_shards_match_whole_graph(precision):
+    """C5-shaped (N = 20000 > the fused path's 16384: tile path), power-law ops, 2 ranks x 30k
+    traces on one GPU vs the union graph on one GPU and vs the oracle."""
+    from microrank_amd import _lib
+    from microrank_amd.graph import DeviceGraph
+
+    n_ops, n_tr = 20_000, 30_000
+    hg = _union_of_shards(n_ops, n_tr, 2)
+    ctx = _lib.Context(0)
+    dg = DeviceGraph.upload(ctx, hg)
+    dg.pagerank(True, precision=precision)
+    w_ref, cov_ref = dg.fetch()
+    dg.close()
+    ctx.close()
+    res = _run(2, True, "host", big=(n_ops, n_tr, precision))
+    rtol = 1e-10 if precision == "fp64" else 1e-5
+    for rank, w, cov, info in res:
+        np.testing.assert_allclose(w, w_ref, rtol=rtol, atol=0)
+        np.testing.assert_array_equal(cov, cov_ref)
+    assert res[0][1].tobytes() == res[1][1].tobytes(), "ranks disagree"
+    if precision == "fp64":   # the union graph against the oracle
+        from test_gpu_pagerank import _oracle_graph_from_host
+        import oracle as orc
+
+        g = _oracle_graph_from_host(hg)
+        kind = orc.trace_kinds(g)
+        s = orc.power_iteration(g, orc.preference(g, kind, True))
+        w_o, cov_o = orc.weights(g, s)
+        np.testing.assert_allclose(w_ref, np.array(list(w_o.values())), rtol=1e-10, atol=0)
+        np.testing.assert_array_equal(cov_ref, np.array(list(cov_o.values())))
