@@ -5,11 +5,15 @@
 
 Workload (BASELINE.json configs[1], "C2"): one RCA window of 1k operations / 200k traces
 (~22 spans/trace, Train-Ticket-like synthetic call tree with one faulty operation), fp64.
-The span columns are generated, factorised and uploaded BEFORE the timed region; a "step" is
-one full window ranked on the device: detector -> two graph builds (T1 swap) -> two
-25-iteration PageRanks -> DStar2 spectrum + top list (mr_rca_window).
+The span columns are generated, factorised and uploaded BEFORE the timed region; a window is
+ranked on the device: detector -> two graph builds (T1 swap) -> two 25-iteration PageRanks ->
+DStar2 spectrum + top list (mr_rca_window).  A "step" ranks --streams W (default 4) copies of
+that window concurrently, each on its own library context (HIP stream) driven by its own host
+thread: one window alone leaves the GPU idle between its small dependent launches, W windows
+fill those gaps (independent windows are data-parallel, no collective).
+W matches the box's 4 hardware queues (GPU_MAX_HW_QUEUES).
 
-N > 1: every rank ranks its own independent window (different seed): data-parallel windows,
+N > 1: every rank ranks its own independent windows (different seed): data-parallel windows,
 no collective on the data path -> "scaling": "weak".
 
 value = edges traversed by all PageRank iterations of all ranks (25 * (2 nnz + E_c) per graph)
@@ -105,7 +109,7 @@ def pmc_traffic(args, timeout_s=240):
         with tempfile.TemporaryDirectory(dir="/tmp") as d:
             cmd = [prof, "--pmc", ctr, "-d", d, "-o", "run", "--output-format", "csv", "--",
                    sys.executable, os.path.abspath(__file__), "--pmc-child", "--steps", "2", "--warmup", "1",
-                   "--no-cpu", "--ops", str(args.ops), "--traces", str(args.traces), "--precision", args.precision]
+                   "--no-cpu", "--streams", "1", "--ops", str(args.ops), "--traces", str(args.traces), "--precision", args.precision]
             try:
                 subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
                                timeout=timeout_s, check=True)
@@ -266,6 +270,8 @@ def main():
     ap.add_argument("--ops", type=int, default=1000)
     ap.add_argument("--traces", type=int, default=200_000)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--streams", type=int, default=4,
+                    help="c2: independent windows ranked concurrently per GPU, one context/stream/host thread each")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC passes for roofline.traffic")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--config", choices=["c2", "c4", "c5"], default="c2",
@@ -306,31 +312,56 @@ def main():
     from microrank_amd import _lib
     from microrank_amd.preprocess_data import DeviceSpans
 
-    ctx = _lib.default_context()
+    # W independent windows per rank, each on its own context (HIP stream) and host thread: the
+    # windows' small launches and host round trips overlap on the GPU (C3's data-parallel windows
+    # within one device).  A step ranks all W windows.
+    W = max(1, args.streams)
+    dev_id = int(os.environ["MICRORANK_DEVICE"])
+    ctxs = [_lib.default_context()] + [_lib.Context(dev_id) for _ in range(W - 1)]
+    # the same window's spans on every context (separate HBM copies): every window of a step is
+    # the configured C2 window, so GTEPS and windows/s stay comparable across W
     topo, normal, abnormal = make_window(1234 + 7919 * rank, args.ops, args.traces)
-    a3, ok = slo_from_gpu(ctx, normal)
-    dev = DeviceSpans(ctx, abnormal)              # window spans resident in HBM from here on
     t0 = int(abnormal.tstart.min())
-    t1 = t0 + 5 * 60 * 10**9
+    wins = []
+    for cx in ctxs:
+        a3, ok = slo_from_gpu(cx, normal)
+        dev = DeviceSpans(cx, abnormal)              # window spans resident in HBM from here on
+        wins.append((cx, dev, t0, t0 + 5 * 60 * 10**9, a3, ok, abnormal))
+    del topo, normal
+    ctx = ctxs[0]
+    cx0, dev0, t0, t1, a3, ok, abnormal = wins[0]
     prec = _lib.MR_FP32 if args.precision == "fp32" else _lib.MR_FP64
 
     def barrier():
-        ctx.sync()
+        for cx in ctxs:
+            cx.sync()
         if dist is not None:
             dist.barrier()
 
-    for _ in range(args.warmup):
-        run_window(ctx, dev, t0, t1, a3, ok, prec)
+    def run_all(n):
+        """n windows on every context; (edges, the first context's last result)."""
+        if W == 1:
+            res = [run_window(cx0, dev0, t0, t1, a3, ok, prec) for _ in range(n)]
+            return sum(r[0] for r in res), res[-1] if res else None
+        from concurrent.futures import ThreadPoolExecutor
+
+        def one(win):
+            cx, dv, a, b, s3, sok, _ = win
+            return [run_window(cx, dv, a, b, s3, sok, prec) for _ in range(n)]
+
+        with ThreadPoolExecutor(max_workers=W) as ex:
+            outs = list(ex.map(one, wins))
+        return sum(r[0] for o in outs for r in o), outs[0][-1] if outs[0] else None
+
+    run_all(args.warmup)
     load = _lib.load()
     load.mr_ctx_profile(ctx.h, 1)
     barrier()
     t_start = time.perf_counter()
-    edges = 0
-    for _ in range(args.steps):
-        e, top, scores, na, nn = run_window(ctx, dev, t0, t1, a3, ok, prec)
-        edges += e
+    edges, last = run_all(args.steps)
     barrier()
     elapsed = time.perf_counter() - t_start
+    e, top, scores, na, nn = last
     import ctypes as C
 
     launches, kms, kbytes = C.c_int64(), C.c_double(), C.c_double()
@@ -370,9 +401,11 @@ def main():
         "config": {"workload": f"C2 RCA window: {args.ops} ops / {args.traces} traces per rank, "
                                f"detect + 2 graph builds + 2x25 PageRank iterations + DStar2 top-11",
                    "n_spans": int(abnormal.n_spans), "n_abnormal": na, "n_normal": nn,
-                   "edges_per_window": int(edges // max(args.steps, 1)), "parallelism": f"windows x{world}"},
-        "windows_per_s": round(world * args.steps / elapsed, 3),
-        "roofline": {"bound": "hbm", "kernel": "one Jacobi iteration: k_fx_a + k_fx_b (fused path)",
+                   "edges_per_window": int(edges // max(args.steps * W, 1)), "windows_per_step": W,
+                   "parallelism": f"windows x{world} ranks x{W} streams"},
+        "windows_per_s": round(world * W * args.steps / elapsed, 3),
+        "roofline": {"bound": "hbm", "kernel": "one Jacobi iteration: k_fx_a + k_fx_b (fused path)"
+                                               + (f", stream 0 of {W} concurrent windows" if W > 1 else ""),
                      "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": None if traffic is None else round(traffic["fetch"] + traffic["write"]),

@@ -238,3 +238,42 @@ def test_slo_bench_scale_matches_oracle():
             continue
         e = exp[str(code)]
         assert (mean[code], std[code]) == (float(e[0]), float(e[1])), code
+
+
+def test_concurrent_contexts_rank_like_one():
+    """bench.py's --streams: four contexts (streams) ranking copies of one window from four host
+    threads at once give bitwise the same top list, scores and edge counts as one context alone,
+    and the oracle's C restatement ranks the same top list."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    import bench
+    import c_oracle
+    from microrank_amd import _lib
+    from microrank_amd.preprocess_data import DeviceSpans
+
+    _, normal, abnormal = bench.make_window(1234, 300, 30_000)
+    t0 = int(abnormal.tstart.min())
+    t1 = t0 + 5 * 60 * 10**9
+    ctxs = [_lib.Context(0) for _ in range(4)]
+    wins = []
+    for cx in ctxs:
+        a3, ok = bench.slo_from_gpu(cx, normal)
+        wins.append((cx, DeviceSpans(cx, abnormal), a3, ok))
+    ref = bench.run_window(wins[0][0], wins[0][1], t0, t1, wins[0][2], wins[0][3], _lib.MR_FP64)
+
+    def go(w):
+        return [bench.run_window(w[0], w[1], t0, t1, w[2], w[3], _lib.MR_FP64) for _ in range(3)]
+
+    with ThreadPoolExecutor(max_workers=4) as ex:
+        outs = list(ex.map(go, wins))
+    for o in outs:
+        for e, top, scores, na, nn in o:
+            assert (e, na, nn) == (ref[0], ref[3], ref[4])
+            assert list(top) == list(ref[1])
+            assert scores.tobytes() == ref[2].tobytes()
+    cres = c_oracle.rca_window(abnormal, t0, t1, wins[0][2], wins[0][3], nthreads=4)
+    assert list(cres[0]) == list(ref[1])
+    for w in wins:
+        w[1].close()
+    for cx in ctxs:
+        cx.close()
