@@ -144,7 +144,7 @@ def cpu_baseline(abnormal, t0, t1, a3, ok, target_s=12.0):
         if el >= target_s or n >= 20:
             break
     return {"value": round(edges / el / 1e9, 4), "unit": "GTEPS", "cores": threads, "kind": "port",
-            "sample": f"{n} full C2 windows (detect + 2 graph builds + 2x25 PageRank iterations + spectrum), "
+            "sample": f"{n} full windows of this config (detect + 2 graph builds + 2x25 PageRank iterations + spectrum), "
                       f"oracle/mr_oracle.c OpenMP, {el:.1f} s",
             "windows_per_s": round(n / el, 4)}, res
 
@@ -274,9 +274,13 @@ def main():
                     help="c2: independent windows ranked concurrently per GPU, one context/stream/host thread each")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC passes for roofline.traffic")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
-    ap.add_argument("--config", choices=["c2", "c4", "c5"], default="c2",
-                    help="c2: RCA windows (default, weak scaling); c4 / c5: one trace-sharded graph (strong "
+    ap.add_argument("--config", choices=["c2", "c3", "c4", "c5"], default="c2",
+                    help="c2: RCA windows (default, weak scaling); c3: a batch of --c3-windows 500-op / 20k-trace "
+                         "windows split over the ranks (strong scaling); c4 / c5: one trace-sharded graph (strong "
                          "scaling; c5 = 100k ops / 100M traces fp32, the tile-path iteration)")
+    ap.add_argument("--c3-windows", type=int, default=4096, help="c3: windows in the whole batch (all ranks)")
+    ap.add_argument("--c3-distinct", type=int, default=4,
+                    help="c3: distinct seeded windows resident per stream (the batch cycles through them)")
     ap.add_argument("--c4-ops", type=int, default=None, help="c4/c5 op count (default 10k / 100k)")
     ap.add_argument("--c4-traces", type=int, default=None, help="c4/c5 trace count over all ranks (10M / 100M)")
     args = ap.parse_args()
@@ -286,13 +290,19 @@ def main():
         args.c4_ops = 100_000 if args.config == "c5" else 10_000
     if args.c4_traces is None:
         args.c4_traces = 100_000_000 if args.config == "c5" else 10_000_000
+    if args.config == "c3":   # BASELINE configs[2]: 500 ops / 20k traces per window
+        args.ops, args.traces = 500, 20_000
+        if "--steps" not in sys.argv:
+            args.steps = 3
+        if "--warmup" not in sys.argv:
+            args.warmup = 1
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # PMC passes first, in child processes, before this process initialises the GPU
     traffic = None
-    if world == 1 and not args.pmc_child and not args.no_traffic and args.config == "c2":
+    if world == 1 and not args.pmc_child and not args.no_traffic and args.config in ("c2", "c3"):
         traffic = pmc_traffic(args)
     dist = None
     if world > 1:
@@ -318,19 +328,35 @@ def main():
     W = max(1, args.streams)
     dev_id = int(os.environ["MICRORANK_DEVICE"])
     ctxs = [_lib.default_context()] + [_lib.Context(dev_id) for _ in range(W - 1)]
-    # the same window's spans on every context (separate HBM copies): every window of a step is
-    # the configured C2 window, so GTEPS and windows/s stay comparable across W
-    topo, normal, abnormal = make_window(1234 + 7919 * rank, args.ops, args.traces)
-    t0 = int(abnormal.tstart.min())
-    wins = []
-    for cx in ctxs:
-        a3, ok = slo_from_gpu(cx, normal)
-        dev = DeviceSpans(cx, abnormal)              # window spans resident in HBM from here on
-        wins.append((cx, dev, t0, t0 + 5 * 60 * 10**9, a3, ok, abnormal))
+    # c2: the same window's spans on every context (separate HBM copies): every window of a step is
+    # the configured C2 window, so GTEPS and windows/s stay comparable across W.
+    # c3: D distinct seeded windows per context; the rank's share of the batch cycles through them.
+    D = max(1, args.c3_distinct) if args.config == "c3" else 1
+    wins = [[] for _ in ctxs]   # per context: [(dev, t0, t1, a3, ok, abnormal)]
+    for d in range(D):
+        seed = 1234 + 7919 * rank + 104729 * d
+        if d == 0 or args.config == "c3":
+            topo, normal, abnormal = make_window(seed, args.ops, args.traces)
+        t0 = int(abnormal.tstart.min())
+        for ci, cx in enumerate(ctxs):
+            if args.config == "c3" and D * W > 1:
+                # distinct windows on every context too (one generator call per (context, d))
+                if ci > 0:
+                    topo, normal, abnormal = make_window(seed + 31 * ci, args.ops, args.traces)
+                    t0 = int(abnormal.tstart.min())
+            a3, ok = slo_from_gpu(cx, normal)
+            dev = DeviceSpans(cx, abnormal)          # window spans resident in HBM from here on
+            wins[ci].append((dev, t0, t0 + 5 * 60 * 10**9, a3, ok, abnormal))
     del topo, normal
     ctx = ctxs[0]
-    cx0, dev0, t0, t1, a3, ok, abnormal = wins[0]
+    dev0, t0, t1, a3, ok, abnormal = wins[0][0]
     prec = _lib.MR_FP32 if args.precision == "fp32" else _lib.MR_FP64
+    if args.config == "c3":
+        # this rank's share of the batch, dealt round-robin over its contexts
+        share = args.c3_windows // world + (1 if rank < args.c3_windows % world else 0)
+        per_ctx = [len(range(ci, share, W)) for ci in range(W)]
+    else:
+        share, per_ctx = None, None
 
     def barrier():
         for cx in ctxs:
@@ -339,26 +365,32 @@ def main():
             dist.barrier()
 
     def run_all(n):
-        """n windows on every context; (edges, the first context's last result)."""
+        """n steps on every context; (edges, the first context's last result).  c2: a step is one
+        window per context; c3: a step is the rank's share of the batch."""
+        def one(ci):
+            cx, res = ctxs[ci], []
+            cnt = n * (per_ctx[ci] if per_ctx is not None else 1)
+            for j in range(cnt):
+                dv, a, b, s3, sok, _ = wins[ci][j % len(wins[ci])]
+                res.append(run_window(cx, dv, a, b, s3, sok, prec))
+            return res
         if W == 1:
-            res = [run_window(cx0, dev0, t0, t1, a3, ok, prec) for _ in range(n)]
-            return sum(r[0] for r in res), res[-1] if res else None
-        from concurrent.futures import ThreadPoolExecutor
+            outs = [one(0)]
+        else:
+            from concurrent.futures import ThreadPoolExecutor
 
-        def one(win):
-            cx, dv, a, b, s3, sok, _ = win
-            return [run_window(cx, dv, a, b, s3, sok, prec) for _ in range(n)]
-
-        with ThreadPoolExecutor(max_workers=W) as ex:
-            outs = list(ex.map(one, wins))
-        return sum(r[0] for o in outs for r in o), outs[0][-1] if outs[0] else None
+            with ThreadPoolExecutor(max_workers=W) as ex:
+                outs = list(ex.map(one, range(W)))
+        # the last result of context 0's first window (the one the CPU baseline re-ranks)
+        last0 = outs[0][(len(outs[0]) - 1) // len(wins[0]) * len(wins[0])] if outs[0] else None
+        return sum(r[0] for o in outs for r in o), sum(len(o) for o in outs), last0
 
     run_all(args.warmup)
     load = _lib.load()
     load.mr_ctx_profile(ctx.h, 1)
     barrier()
     t_start = time.perf_counter()
-    edges, last = run_all(args.steps)
+    edges, n_win, last = run_all(args.steps)
     barrier()
     elapsed = time.perf_counter() - t_start
     e, top, scores, na, nn = last
@@ -370,14 +402,14 @@ def main():
     if dist is not None:
         import torch
 
-        t = torch.tensor([elapsed, float(edges)], dtype=torch.float64)
+        t = torch.tensor([elapsed, float(edges), float(n_win)], dtype=torch.float64)
         mx = t.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         sm = t.clone()
         dist.all_reduce(sm, op=dist.ReduceOp.SUM)
-        elapsed, edges_all = float(mx[0]), float(sm[1])
+        elapsed, edges_all, win_all = float(mx[0]), float(sm[1]), int(sm[2])
     else:
-        edges_all = float(edges)
+        edges_all, win_all = float(edges), n_win
     if rank != 0:
         if dist is not None:
             dist.barrier()
@@ -385,6 +417,7 @@ def main():
         return
     avg_ms = kms.value / max(launches.value, 1)
     achieved = (kbytes.value / max(launches.value, 1)) / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+    c3 = args.config == "c3"
     out = {
         "metric": "PageRank GTEPS + RCA windows ranked/sec at 1/2/4/8 MI355X; % HBM roofline",
         "value": round(edges_all / elapsed / 1e9, 3),
@@ -394,16 +427,20 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if c3 else "weak",
         "vs_baseline": None,
         "dtype": "f64" if args.precision == "fp64" else "f32",
-        "data": "synthetic (seeded Train-Ticket-like spans, int-coded, resident in HBM)",
-        "config": {"workload": f"C2 RCA window: {args.ops} ops / {args.traces} traces per rank, "
-                               f"detect + 2 graph builds + 2x25 PageRank iterations + DStar2 top-11",
+        "data": "synthetic (seeded Train-Ticket-like spans, int-coded, resident in HBM)"
+                + (f"; {D * W} distinct windows per rank, the batch cycles through them" if c3 else ""),
+        "config": {"workload": (f"C3 batch of {args.c3_windows} RCA windows ({args.ops} ops / {args.traces} traces "
+                                f"each) over {world} GPU(s)" if c3 else
+                                f"C2 RCA window: {args.ops} ops / {args.traces} traces per rank")
+                               + ", detect + 2 graph builds + 2x25 PageRank iterations + DStar2 top-11",
                    "n_spans": int(abnormal.n_spans), "n_abnormal": na, "n_normal": nn,
-                   "edges_per_window": int(edges // max(args.steps * W, 1)), "windows_per_step": W,
+                   "edges_per_window": int(edges // max(n_win, 1)),
+                   "windows_per_step": (win_all // args.steps) if c3 else W,
                    "parallelism": f"windows x{world} ranks x{W} streams"},
-        "windows_per_s": round(world * W * args.steps / elapsed, 3),
+        "windows_per_s": round(win_all / elapsed, 3),
         "roofline": {"bound": "hbm", "kernel": "one Jacobi iteration: k_fx_a + k_fx_b (fused path)"
                                                + (f", stream 0 of {W} concurrent windows" if W > 1 else ""),
                      "achieved": round(achieved, 1),
