@@ -102,6 +102,14 @@ struct DBuf {
 };
 
 // Device graph: the four reference dicts as incidence lists.
+// the kinds hash table (mr_pagerank.hip): 64-bit keys in one array (the CAS-probed one, half the
+// footprint of a packed slot -- it stays MALL-resident longer), class size + representative in a
+// second 8 B array (one line for k_kind_verify's read)
+struct alignas(8) KCnt {
+    uint32_t cnt;
+    int32_t rep;
+};
+
 struct mr_graph {
     mr_ctx* ctx = nullptr;
     int32_t N = 0, T = 0;
@@ -162,9 +170,10 @@ struct mr_graph {
     DBuf<double> scal;           // [8] M_s, M_r, sums
     DBuf<double> ppart;          // preference-sum block partials
     DBuf<double> weight;         // [N]
-    DBuf<uint64_t> ht_key;       // kinds hash table
-    DBuf<uint32_t> ht_cnt;
-    DBuf<int32_t> ht_rep, slot_of;
+    DBuf<unsigned long long> ht_key;   // kinds hash table keys
+    DBuf<KCnt> ht_cr;                  // per slot: class size, representative
+    DBuf<int32_t> slot_of;
+    DBuf<uint64_t> ht_chk;   // sharded on >1 rank: check hash of each class's representative
     DBuf<int32_t> flag;          // [4] error flags written by kernels
 };
 

@@ -40,8 +40,8 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     return z ^ (z >> 31);
 }
 
-__global__ void k_pr_reset(int32_t T, int64_t cap, int32_t N, float* pref, float* c_t, uint64_t* hk, uint32_t* hc,
-                           int32_t* hr, int32_t* flag, double* scal) {
+__global__ void k_pr_reset(int32_t T, int64_t cap, int32_t N, float* pref, float* c_t, unsigned long long* hk, KCnt* cr, int32_t* flag,
+                           double* scal) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < T) {
         pref[i] = 0.0f;
@@ -49,8 +49,7 @@ __global__ void k_pr_reset(int32_t T, int64_t cap, int32_t N, float* pref, float
     }
     if (i < cap) {
         hk[i] = 0ull;
-        hc[i] = 0u;
-        hr[i] = -1;
+        cr[i] = KCnt{0u, -1};
     }
     if (i < 4) flag[i] = 0;
     if (i < 8) scal[i] = 0.0;
@@ -169,35 +168,120 @@ __global__ void __launch_bounds__(256) k_cov_hist(const uint16_t* ids, int64_t n
 // slot's representative, so a hash collision is detected (flag) rather than miscounted.
 constexpr int KB = 256, KLDS = 512;   // kinds: block size, LDS table slots
 
-__device__ __forceinline__ uint64_t kind_hash(const int64_t* off, const int32_t* ops, const float* w_t,
-                                              int32_t t, uint64_t seed) {
-    int64_t e0 = off[t], e1 = off[t + 1];
-    uint32_t wb = e1 > e0 ? __float_as_uint(w_t[t]) : 0u;
-    uint64_t h = mix64(seed ^ (uint64_t)wb);
-    for (int64_t e = e0; e < e1; ++e) h = mix64(h ^ (uint64_t)(uint32_t)ops[e]);
+// Set hash of a trace's key (its distinct ascending op ids, fp32(1/len_t), the id count):
+// mix64(mix64(seed ^ wb ^ n << 32) + sum_op mix64(op ^ seed)).  Order-free, so the per-thread
+// walk below and k_kind_insert's cooperative u16 form give the same key for the same trace (a
+// requirement across ranks of a sharded graph).  CHK: a second, independently seeded hash of
+// the same words, which travels with the key between ranks to catch a 64-bit key collision.
+__device__ __forceinline__ uint64_t kind_fold(uint64_t seed, uint64_t wb, int64_t n, uint64_t acc) {
+    const uint64_t h = mix64(mix64(seed ^ wb ^ ((uint64_t)n << 32)) + acc);
     return h ? h : 1;
 }
+template <bool CHK>
+__device__ __forceinline__ uint64_t kind_hash2(const int64_t* off, const int32_t* ops, const float* w_t,
+                                               int32_t t, uint64_t seed, uint64_t seed2, uint64_t* h2) {
+    const int64_t e0 = off[t], e1 = off[t + 1];
+    const uint64_t wb = e1 > e0 ? (uint64_t)__float_as_uint(w_t[t]) : 0ull;
+    uint64_t a = 0, a2 = 0;
+    for (int64_t e = e0; e < e1; ++e) {
+        const uint64_t o = (uint64_t)(uint32_t)ops[e];
+        a += mix64(o ^ seed);
+        if (CHK) a2 += mix64(o ^ seed2);
+    }
+    if (CHK) *h2 = kind_fold(seed2, wb, e1 - e0, a2);
+    return kind_fold(seed, wb, e1 - e0, a);
+}
+constexpr uint64_t KCHK_SEED = 0x0ddba11cafeull;
 
 // Two-level insertion: traces of a block are first counted in an LDS table (hot kinds -- the
 // same few call paths in thousands of traces -- would otherwise serialise on one global
 // counter), then each distinct key of the block does ONE global insert + add.
-__global__ void __launch_bounds__(KB) k_kind_insert(const int64_t* off, const int32_t* ops, const float* w_t,
-                                                    int32_t T, uint64_t* keys, uint32_t* cnt, int32_t* rep,
-                                                    int32_t* slot_of, uint64_t mask, uint64_t seed) {
+// CHK (sharded graphs on >1 rank): the representative's check hash is stored per global slot
+// (chk) for the cross-rank merge, computed in the same walk instead of a later re-read.
+// U16 (u16 trace-major ids, N <= 65536): the block's 256 traces are hashed cooperatively -- the
+// threads stream the block's contiguous id range in aligned 8-id (16 B) chunks, coalesced across
+// the wave, and add mix64(op) into per-trace LDS sums (an order-free SET hash: the ids of a
+// trace are distinct and ascending, so the set is the list).  The walk-per-thread form (int32
+// ids) reads one trace per lane, ~60 B apart.  Either hash only buckets traces; membership is
+// decided by k_kind_verify's exact comparison.
+template <bool CHK, bool U16>
+__global__ void __launch_bounds__(KB) k_kind_insert(const int64_t* off, const int32_t* ops, const uint16_t* o16,
+                                                    const float* w_t, int32_t T, unsigned long long* hk, KCnt* cr, int32_t* slot_of,
+                                                    uint64_t mask, uint64_t seed, uint64_t* chk) {
     __shared__ unsigned long long lkey[KLDS];
     __shared__ uint32_t lcnt[KLDS];
     __shared__ int32_t lrep[KLDS];
     __shared__ int32_t lglob[KLDS];
+    __shared__ uint64_t lchk[CHK ? KLDS : 1];
+    __shared__ int64_t loff[U16 ? KB + 1 : 1];
+    __shared__ unsigned long long lacc[U16 ? KB : 1], lacc2[U16 && CHK ? KB : 1];
     for (int i = threadIdx.x; i < KLDS; i += KB) {
         lkey[i] = 0ull;
         lcnt[i] = 0u;
         lrep[i] = -1;
     }
+    const int32_t tb = blockIdx.x * KB;
+    const int32_t t = tb + threadIdx.x;
+    if (U16) {
+        const int nt = min(KB, T - tb);
+        if ((int)threadIdx.x < nt) {
+            loff[threadIdx.x] = off[t];
+            lacc[threadIdx.x] = 0ull;
+            if (CHK) lacc2[threadIdx.x] = 0ull;
+        }
+        if (threadIdx.x == 0) loff[nt] = off[tb + nt];
+        __syncthreads();
+        const int64_t b = loff[0], e = loff[nt];
+        for (int64_t c = (b & ~7ll) + 8ll * threadIdx.x; c < e; c += 8ll * KB) {
+            const uint4 v = *reinterpret_cast<const uint4*>(o16 + c);   // rs16 holds nnz + 8 ids
+            const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+            const int64_t p0 = c > b ? c : b;
+            int lo = 0, hi = nt - 1;   // the trace holding p0: last lt with loff[lt] <= p0
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (loff[mid] <= p0) lo = mid;
+                else hi = mid - 1;
+            }
+            int lt = lo;
+            int64_t nb = loff[lt + 1];
+            unsigned long long a = 0ull, a2 = 0ull;
+            bool any = false;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int64_t idx = c + k;
+                if (idx < b || idx >= e) continue;
+                while (idx >= nb) {
+                    if (any) {
+                        atomicAdd(&lacc[lt], a);
+                        if (CHK) atomicAdd(&lacc2[lt], a2);
+                    }
+                    a = a2 = 0ull;
+                    any = false;
+                    ++lt;
+                    nb = loff[lt + 1];
+                }
+                const uint64_t op = (wd[k >> 1] >> ((k & 1) * 16)) & 0xffffu;
+                a += mix64(op ^ seed);
+                if (CHK) a2 += mix64(op ^ KCHK_SEED);
+                any = true;
+            }
+            if (any) {
+                atomicAdd(&lacc[lt], a);
+                if (CHK) atomicAdd(&lacc2[lt], a2);
+            }
+        }
+    }
     __syncthreads();
-    const int32_t t = blockIdx.x * KB + threadIdx.x;
     int myslot = -1;
     if (t < T) {
-        const uint64_t h = kind_hash(off, ops, w_t, t, seed);
+        uint64_t h2 = 0, h;
+        if (U16) {
+            const int64_t n = loff[threadIdx.x + 1] - loff[threadIdx.x];
+            const uint64_t wb = n > 0 ? (uint64_t)__float_as_uint(w_t[t]) : 0ull;
+            h = kind_fold(seed, wb, n, lacc[threadIdx.x]);
+            if (CHK) h2 = kind_fold(KCHK_SEED, wb, n, lacc2[threadIdx.x]);
+        } else
+            h = kind_hash2<CHK>(off, ops, w_t, t, seed, KCHK_SEED, &h2);
         int s = (int)(h & (KLDS - 1));
         for (;;) {
             unsigned long long k = atomicCAS(&lkey[s], 0ull, (unsigned long long)h);
@@ -205,7 +289,7 @@ __global__ void __launch_bounds__(KB) k_kind_insert(const int64_t* off, const in
             s = (s + 1) & (KLDS - 1);
         }
         atomicAdd(&lcnt[s], 1u);
-        atomicCAS(&lrep[s], -1, t);
+        if (atomicCAS(&lrep[s], -1, t) == -1 && CHK) lchk[s] = h2;
         myslot = s;
     }
     __syncthreads();
@@ -214,26 +298,30 @@ __global__ void __launch_bounds__(KB) k_kind_insert(const int64_t* off, const in
         if (!h) continue;
         uint64_t slot = h & mask;
         for (;;) {
-            uint64_t k = atomicCAS((unsigned long long*)&keys[slot], 0ull, (unsigned long long)h);
-            if (k == 0 || k == h) break;
+            const uint64_t k = atomicCAS(&hk[slot], 0ull, (unsigned long long)h);
+            if (k == 0) {   // the class's first block names its representative (read after this kernel)
+                cr[slot].rep = lrep[i];
+                if (CHK) chk[slot] = lchk[i];
+                break;
+            }
+            if (k == h) break;
             slot = (slot + 1) & mask;
         }
-        atomicAdd(&cnt[slot], lcnt[i]);
-        atomicCAS(&rep[slot], -1, lrep[i]);
+        atomicAdd(&cr[slot].cnt, lcnt[i]);
         lglob[i] = (int32_t)slot;
     }
     __syncthreads();
     if (t < T) slot_of[t] = lglob[myslot];
 }
 
-__global__ void k_kind_verify(const int64_t* off, const int32_t* ops, const float* w_t, int32_t T,
-                              const uint32_t* cnt, const int32_t* rep, const int32_t* slot_of,
-                              double* kind, int32_t* flag) {
+template <typename ID>   // int32 ids, or their u16 copy (rs16)
+__global__ void k_kind_verify(const int64_t* off, const ID* ops, const float* w_t, int32_t T,
+                              const KCnt* cr, const int32_t* slot_of, double* kind, int32_t* flag) {
     int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= T) return;
-    int32_t s = slot_of[t];
-    int32_t r = rep[s];
-    kind[t] = (double)cnt[s];
+    const KCnt ks = cr[slot_of[t]];
+    const int32_t r = ks.rep;
+    kind[t] = (double)ks.cnt;
     if (r == t) return;
     int64_t a0 = off[t], a1 = off[t + 1], b0 = off[r], b1 = off[r + 1];
     bool eq = (a1 - a0) == (b1 - b0);
@@ -1120,17 +1208,16 @@ __global__ void k_sh_edge_out(const uint64_t* key, const int32_t* head, const in
     atomicAdd(&ccount[(int32_t)(key[i] >> nb)], 1);
 }
 // this rank's kind classes as (key, check hash of the representative, count); empty slots skipped
-__global__ void k_sh_kind_list(const uint64_t* hk, const uint32_t* hc, const int32_t* hr, int64_t cap,
-                               const int32_t* flag, const int64_t* pos, const int64_t* off, const int32_t* ops,
-                               const float* w_t, uint64_t* out) {
+__global__ void k_sh_kind_list(const unsigned long long* hk, const KCnt* cr, const uint64_t* hchk, int64_t cap, const int32_t* flag,
+                               const int64_t* pos, uint64_t* out) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= cap || !flag[i]) return;
     const int64_t p = pos[i];
     out[3 * p] = hk[i];
-    out[3 * p + 1] = kind_hash(off, ops, w_t, hr[i], 0x0ddba11cafeull);
-    out[3 * p + 2] = hc[i];
+    out[3 * p + 1] = hchk[i];   // k_kind_insert<true>: the representative's check hash
+    out[3 * p + 2] = cr[i].cnt;
 }
-__global__ void k_sh_kind_flags(const uint64_t* hk, int64_t cap, int32_t* flag) {
+__global__ void k_sh_kind_flags(const unsigned long long* hk, int64_t cap, int32_t* flag) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < cap) flag[i] = hk[i] != 0ull;
 }
@@ -1164,7 +1251,7 @@ __global__ void k_sh_kind_check(const uint64_t* in, int64_t n, const uint64_t* g
     if (gh[s] != in[3 * i + 1]) atomicOr(flag, 1);
 }
 // kind[t] = the class size over all ranks
-__global__ void k_sh_kind_apply(const uint64_t* hk, const int32_t* slot_of, int32_t T, const uint64_t* gk,
+__global__ void k_sh_kind_apply(const unsigned long long* hk, const int32_t* slot_of, int32_t T, const uint64_t* gk,
                                 const unsigned long long* gc, uint64_t mask, double* kind) {
     const int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= T) return;
@@ -1388,8 +1475,7 @@ static int pagerank_setup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool 
     MR_TRY(g->scal.alloc(ctx, 8));
     MR_TRY(g->ppart.alloc(ctx, 2 * (size_t)nbp));
     MR_TRY(g->ht_key.alloc(ctx, cap));
-    MR_TRY(g->ht_cnt.alloc(ctx, cap));
-    MR_TRY(g->ht_rep.alloc(ctx, cap));
+    MR_TRY(g->ht_cr.alloc(ctx, cap));
     MR_TRY(g->slot_of.alloc(ctx, (size_t)T));
     MR_TRY(g->mslot.alloc(ctx, 6 * MSH));
     MR_TRY(g->sn.alloc(ctx, (size_t)N));
@@ -1409,19 +1495,32 @@ static int pagerank_setup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool 
     }
     // one launch clears every per-call word (instead of a memset per buffer)
     hipLaunchKernelGGL(k_pr_reset, dim3(cdiv(std::max<int64_t>({(int64_t)T, (int64_t)cap, (int64_t)N, 16}), 256)),
-                       dim3(256), 0, st, T, (int64_t)cap, N, g->pref.p, g->c_t.p, g->ht_key.p, g->ht_cnt.p, g->ht_rep.p,
+                       dim3(256), 0, st, T, (int64_t)cap, N, g->pref.p, g->c_t.p, g->ht_key.p, g->ht_cr.p,
                        g->flag.p, g->scal.p);
     MR_DEBUG_CHECK(ctx, "k_pr_reset");
     // ---- kinds
     const int64_t* koff = g->rs_is_sr ? g->rs_off.p : g->srt_off.p;
     const int32_t* kops = g->rs_is_sr ? g->rs_ops.p : g->srt_ops.p;
-    hipLaunchKernelGGL(k_kind_insert, dim3(cdiv(T, KB)), dim3(KB), 0, st, koff, kops, g->w_t.p, T, g->ht_key.p,
-                       g->ht_cnt.p, g->ht_rep.p, g->slot_of.p, (uint64_t)(cap - 1), 0x5eed5eedull);
+    // one shard of a multi-rank graph: the cross-rank merge needs a check hash per class
+    const bool chk = sharded && ctx->nranks > 1;
+    if (chk) MR_TRY(g->ht_chk.alloc(ctx, cap));
+    static const bool no_u16 = getenv("MR_KIND_WALK") != nullptr;   // A/B knob: per-thread int32 walk
+    const bool u16 = !no_u16 && g->rs_is_sr && g->rs16.p != nullptr;   // rs16 = u16 copy of rs_ops
+    auto kins = chk ? (u16 ? k_kind_insert<true, true> : k_kind_insert<true, false>)
+                    : (u16 ? k_kind_insert<false, true> : k_kind_insert<false, false>);
+    if (T)
+        hipLaunchKernelGGL(kins, dim3(cdiv(T, KB)), dim3(KB), 0, st, koff, kops, (const uint16_t*)g->rs16.p, g->w_t.p,
+                           T, g->ht_key.p, g->ht_cr.p, g->slot_of.p, (uint64_t)(cap - 1), 0x5eed5eedull,
+                           chk ? g->ht_chk.p : (uint64_t*)nullptr);
     MR_DEBUG_CHECK(ctx, "k_kind_insert");
-    hipLaunchKernelGGL(k_kind_verify, dim3(cdiv(T, 256)), dim3(256), 0, st, koff, kops, g->w_t.p, T, g->ht_cnt.p,
-                       g->ht_rep.p, g->slot_of.p, g->kind.p, g->flag.p);
+    if (u16)
+        hipLaunchKernelGGL(k_kind_verify<uint16_t>, dim3(cdiv(T, 256)), dim3(256), 0, st, koff,
+                           (const uint16_t*)g->rs16.p, g->w_t.p, T, g->ht_cr.p, g->slot_of.p, g->kind.p, g->flag.p);
+    else
+        hipLaunchKernelGGL(k_kind_verify<int32_t>, dim3(cdiv(T, 256)), dim3(256), 0, st, koff, kops, g->w_t.p, T,
+                           g->ht_cr.p, g->slot_of.p, g->kind.p, g->flag.p);
     MR_DEBUG_CHECK(ctx, "k_kind_verify");
-    if (sharded) MR_TRY(shard_kinds(ctx, g, cap));   // class sizes over all ranks
+    if (chk) MR_TRY(shard_kinds(ctx, g, cap));   // class sizes over all ranks (one rank: already global)
     // ---- preference
     const int32_t* prt = g->pr_identity ? nullptr : g->pr_trace.p;
     const int32_t* prl = g->pr_identity ? nullptr : g->pr_len.p;
@@ -1648,8 +1747,6 @@ extern "C" int mr_pagerank_batch(mr_ctx* ctx, mr_graph* const* graphs, const int
 static int shard_kinds(mr_ctx* ctx, mr_graph* g, uint64_t cap) {
     hipStream_t st = ctx->stream;
     const int32_t T = g->T;
-    const int64_t* koff = g->rs_is_sr ? g->rs_off.p : g->srt_off.p;
-    const int32_t* kops = g->rs_is_sr ? g->rs_ops.p : g->srt_ops.p;
     DBuf<int32_t> fl;
     DBuf<int64_t> pos, tmp;
     MR_TRY(fl.alloc(ctx, cap));
@@ -1671,8 +1768,8 @@ static int shard_kinds(mr_ctx* ctx, mr_graph* g, uint64_t cap) {
     DBuf<uint64_t> send, recv;
     MR_TRY(send.zero(ctx, (size_t)3 * std::max<int64_t>(Kmax, 1)));
     MR_TRY(recv.alloc(ctx, (size_t)3 * std::max<int64_t>(Kmax, 1) * R));
-    hipLaunchKernelGGL(k_sh_kind_list, dim3(cdiv(cap, 256)), dim3(256), 0, st, g->ht_key.p, g->ht_cnt.p, g->ht_rep.p,
-                       (int64_t)cap, fl.p, pos.p, koff, kops, g->w_t.p, send.p);
+    hipLaunchKernelGGL(k_sh_kind_list, dim3(cdiv(cap, 256)), dim3(256), 0, st, g->ht_key.p, g->ht_cr.p, g->ht_chk.p,
+                       (int64_t)cap, fl.p, pos.p, send.p);
     MR_TRY(mr_coll_allgather(ctx, send.p, recv.p, 3 * std::max<int64_t>(Kmax, 1), MR_DT_U64));
     const int64_t n = std::max<int64_t>(Kmax, 1) * R;
     uint64_t gcap = 1;
