@@ -1656,12 +1656,15 @@ int mr_pagerank_batch_impl(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly,
     const FxA fx_a = fx_kernel(fp32, sul, multi, fx_S);
     for (int i = 0; i < ng; ++i)
         if (gs[i]->fused) lds_f = std::max(lds_f, FxLds(gs[i]->N, TT, fx_S * TT, sul).total);
+    // a sharded graph with no collective backend is one whole shard: the split launches around the
+    // (no-op) all-reduces would compute the same integers / sums in two halves
+    const bool coll = sharded && mr_coll_ready(ctx);
     for (int it = 0; it < iters; ++it) {
         mr_prof_begin(ctx);
         if (blocks_fa) {
             hipLaunchKernelGGL(fx_a, dim3(blocks_fa), dim3(fx_S * TT), lds_f, st, dv.p, ng, split_fa, d, alpha, it, TT);
             MR_DEBUG_CHECK(ctx, "k_fx_a");
-            if (!sharded) {
+            if (!coll) {
                 hipLaunchKernelGGL(k_fx_b, dim3(blocks_fb), dim3(WAVE * FB_W), 0, st, dv.p, ng, split_fb, d, it, 0);
             } else {   // r' max and the P_sr r limbs over all ranks (exact: integers, max)
                 MR_TRY(mr_coll_allreduce(ctx, gs[0]->mslot.p + (size_t)2 * MSH * ((it + 1) % 3) + MSH, MSH, MR_DT_U64, 1));
@@ -1677,7 +1680,7 @@ int mr_pagerank_batch_impl(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly,
             MR_DEBUG_CHECK(ctx, "k_iter_a");
         }
         if (blocks_b) {
-            if (!sharded) {
+            if (!coll) {
                 hipLaunchKernelGGL(k_iter_b, dim3(blocks_b), dim3(TB), 0, st, dv.p, ng, d, alpha, it, 0);
             } else {   // r' max over ranks, then the per-op P_sr r sums over ranks (fp64 SUM)
                 MR_TRY(mr_coll_allreduce(ctx, gs[0]->mslot.p + (size_t)2 * MSH * ((it + 1) % 3) + MSH, MSH, MR_DT_U64, 1));

@@ -38,10 +38,12 @@ def _whole(anomaly):
     return w, cov
 
 
-def _worker(rank, world, port, anomaly, backend, q, big=None, tile=False):
+def _worker(rank, world, port, anomaly, backend, q, big=None, tile=False, walk_ranks=()):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     if tile:
         os.environ["MR_NO_FUSED"] = "1"   # read once, at this process's first graph prepare
+    if rank in walk_ranks:
+        os.environ["MR_KIND_WALK"] = "1"   # kinds hashed by the per-thread int32 walk (read once)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from gpu_util import host_graph_from_oracle
@@ -70,11 +72,12 @@ def _worker(rank, world, port, anomaly, backend, q, big=None, tile=False):
         dist.destroy_process_group()
 
 
-def _run(world, anomaly, backend, big=None, tile=False):
+def _run(world, anomaly, backend, big=None, tile=False, walk_ranks=()):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, anomaly, backend, q, big, tile)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, anomaly, backend, q, big, tile, walk_ranks))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=180) for _ in procs]
@@ -161,3 +164,44 @@ def test_large_op_count_shards_match_whole_graph(precision):
         w_o, cov_o = orc.weights(g, s)
         np.testing.assert_allclose(w_ref, np.array(list(w_o.values())), rtol=1e-10, atol=0)
         np.testing.assert_array_equal(cov_ref, np.array(list(cov_o.values())))
+
+
+def test_kind_hash_forms_agree_across_ranks():
+    """Rank 0 hashes kinds with the cooperative u16 form, rank 1 with the per-thread int32 walk:
+    the set hash is the same function, so the cross-rank class merge still finds every class
+    (a mismatch would split classes and change the preference vector)."""
+    w_ref, cov_ref = _whole(True)
+    res = _run(2, True, "host", walk_ranks=(1,))
+    for rank, w, cov, info in res:
+        np.testing.assert_allclose(w, w_ref, rtol=1e-12, atol=0)
+        np.testing.assert_array_equal(cov, cov_ref)
+    assert res[0][1].tobytes() == res[1][1].tobytes(), "ranks disagree"
+
+
+def test_wide_op_space_int32_ids_shards():
+    """N = 70000 > 65535: no u16 ids, so kinds take the int32 walk and the iteration the tile
+    path; 2 ranks x 10k traces vs the union graph on one GPU and vs the oracle."""
+    from microrank_amd import _lib
+    from microrank_amd.graph import DeviceGraph
+    from test_gpu_pagerank import _oracle_graph_from_host
+    import oracle as orc
+
+    n_ops, n_tr = 70_000, 10_000
+    hg = _union_of_shards(n_ops, n_tr, 2)
+    ctx = _lib.Context(0)
+    dg = DeviceGraph.upload(ctx, hg)
+    dg.pagerank(True)
+    w_ref, cov_ref = dg.fetch()
+    dg.close()
+    ctx.close()
+    g = _oracle_graph_from_host(hg)
+    kind = orc.trace_kinds(g)
+    s = orc.power_iteration(g, orc.preference(g, kind, True))
+    w_o, cov_o = orc.weights(g, s)
+    np.testing.assert_allclose(w_ref, np.array(list(w_o.values())), rtol=1e-10, atol=0)
+    np.testing.assert_array_equal(cov_ref, np.array(list(cov_o.values())))
+    res = _run(2, True, "host", big=(n_ops, n_tr, "fp64"))
+    for rank, w, cov, info in res:
+        np.testing.assert_allclose(w, w_ref, rtol=1e-10, atol=0)
+        np.testing.assert_array_equal(cov, cov_ref)
+    assert res[0][1].tobytes() == res[1][1].tobytes(), "ranks disagree"
