@@ -7,11 +7,12 @@ Workload (BASELINE.json configs[1], "C2"): one RCA window of 1k operations / 200
 (~22 spans/trace, Train-Ticket-like synthetic call tree with one faulty operation), fp64.
 The span columns are generated, factorised and uploaded BEFORE the timed region; a window is
 ranked on the device: detector -> two graph builds (T1 swap) -> two 25-iteration PageRanks ->
-DStar2 spectrum + top list (mr_rca_window).  A "step" ranks --streams W (default 4) copies of
+DStar2 spectrum + top list (mr_rca_window).  A "step" ranks --streams W (default 8) copies of
 that window concurrently, each on its own library context (HIP stream) driven by its own host
-thread: one window alone leaves the GPU idle between its small dependent launches, W windows
-fill those gaps (independent windows are data-parallel, no collective).
-W matches the box's 4 hardware queues (GPU_MAX_HW_QUEUES).
+thread: one window alone leaves the GPU idle between its small dependent launches and host
+round trips, W windows fill those gaps (independent windows are data-parallel,
+no collective).  W = 8 (measured r01: W=4 172, 6 166, 8 195, 12 200 GTEPS; the 8 streams share
+the box's 4 hardware queues).
 
 N > 1: every rank ranks its own independent windows (different seed): data-parallel windows,
 no collective on the data path -> "scaling": "weak".
@@ -270,7 +271,7 @@ def main():
     ap.add_argument("--ops", type=int, default=1000)
     ap.add_argument("--traces", type=int, default=200_000)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--streams", type=int, default=4,
+    ap.add_argument("--streams", type=int, default=8,
                     help="c2: independent windows ranked concurrently per GPU, one context/stream/host thread each")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC passes for roofline.traffic")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
