@@ -667,7 +667,13 @@ static int graph_build_indexed(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d
                            zc.p);
         const int use_lds = NP <= LDS_HIST;
         const size_t lds = use_lds ? 2 * (size_t)NP * sizeof(int32_t) : 0;
-        const int nblk = std::max(1, std::min(1024, cdiv(std::max(sp->n_po, sp->n_ed), BT * IX_EPT)));
+        // block cap 256 (one per CU): measured on the C2 window (scripts/ab_ix.sh) 1024 -> 101 us,
+        // 512 -> 103, 256 -> 83, 128 -> 106 avg; MR_IX_BLOCKS overrides it for measurements
+        static const int ix_cap = [] {
+            const char* e = getenv("MR_IX_BLOCKS");
+            return e ? std::max(1, atoi(e)) : 256;
+        }();
+        const int nblk = std::max(1, std::min(ix_cap, cdiv(std::max(sp->n_po, sp->n_ed), BT * IX_EPT)));
         hipLaunchKernelGGL(k_ix_stats, dim3(nblk), dim3(BT), lds, st, tflag.p, sp->n_po, sp->po_tr.p, sp->po_op.p,
                            sp->po_cnt.p, sp->po_first.p, sp->n_ed, sp->ed_tr.p, sp->ed_key.p, sp->ed_cnt.p, NP, use_lds,
                            ocnt.p, ofirst.p, gk.p, gc.p, ecap - 1);
