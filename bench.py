@@ -110,7 +110,11 @@ def pmc_traffic(args, timeout_s=240):
         with tempfile.TemporaryDirectory(dir="/tmp") as d:
             cmd = [prof, "--pmc", ctr, "-d", d, "-o", "run", "--output-format", "csv", "--",
                    sys.executable, os.path.abspath(__file__), "--pmc-child", "--steps", "2", "--warmup", "1",
-                   "--no-cpu", "--streams", "1", "--ops", str(args.ops), "--traces", str(args.traces), "--precision", args.precision]
+                   "--no-cpu", "--precision", args.precision]
+            if args.config in ("c4", "c5"):
+                cmd += ["--config", args.config, "--c4-ops", str(args.c4_ops), "--c4-traces", str(args.c4_traces)]
+            else:
+                cmd += ["--streams", "1", "--ops", str(args.ops), "--traces", str(args.traces)]
             try:
                 subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
                                timeout=timeout_s, check=True)
@@ -303,8 +307,8 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # PMC passes first, in child processes, before this process initialises the GPU
     traffic = None
-    if world == 1 and not args.pmc_child and not args.no_traffic and args.config in ("c2", "c3"):
-        traffic = pmc_traffic(args)
+    if world == 1 and not args.pmc_child and not args.no_traffic:
+        traffic = pmc_traffic(args, timeout_s=240 if args.config in ("c2", "c3") else 400)
     dist = None
     if world > 1:
         import torch.distributed as dist  # control plane only: barrier + max over ranks (gloo, host)
@@ -313,7 +317,12 @@ def main():
     os.environ.setdefault("MICRORANK_DEVICE", str(local))
     if args.config in ("c4", "c5"):
         out = run_c4(args, world, rank, dist)
-        if out is not None:
+        if out is not None and traffic is not None:
+            out["roofline"]["traffic"] = round(traffic["fetch"] + traffic["write"])
+            out["roofline"]["traffic_detail"] = {
+                "fetch_bytes": round(traffic["fetch"]), "write_bytes": round(traffic["write"]),
+                "source": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950) / WRITE_SIZE, per iteration (A + B launches)"}
+        if out is not None and not args.pmc_child:
             print(json.dumps(out), flush=True)
         if dist is not None:
             dist.barrier()
