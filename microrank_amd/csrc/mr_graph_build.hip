@@ -261,6 +261,19 @@ __global__ void k_edge_csr(const uint64_t* skey, int64_t E, int nb, int32_t* ss_
 // ---------------------------------------------------------------- indexed build (whole traces)
 constexpr int IX_EPT = 16;  // index entries per thread in k_ix_stats (fewer blocks: fewer global flushes)
 constexpr int IX_B = 8;     // entries per thread whose loads are batched
+// one launch for the indexed build's four initialisations (was four memsets: each a separate
+// ~3 us fill launch, twice per window): per-op counts / first rows, edge keys (EMPTY) / counts
+__global__ void k_ix_init(int32_t* ocnt, int32_t* ofirst, int32_t NP, uint64_t* gk, uint32_t* gc, int64_t ecap) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < NP) {
+        ocnt[i] = 0;
+        ofirst[i] = 0x7f7f7f7f;   // the old memset's byte pattern: larger than any row
+    }
+    if (i < ecap) {
+        gk[i] = ~0ull;
+        gc[i] = 0u;
+    }
+}
 __global__ void k_ix_sel(const uint8_t* mask, const int32_t* tlen, const int64_t* po_off, int32_t NT, int32_t* tflag,
                          int32_t* zc) {
     const int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -653,15 +666,16 @@ static int graph_build_indexed(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d
     MR_TRY(zoff.alloc(ctx, NT + 1));
     MR_TRY(tmp.alloc(ctx, std::max<int64_t>({scan_tmp_elems(NT), scan_tmp_elems(NP), 1})));
     DBuf<int32_t> ocnt, ofirst;
-    MR_TRY(ocnt.zero(ctx, NP));
+    MR_TRY(ocnt.alloc(ctx, NP));
     MR_TRY(ofirst.alloc(ctx, NP));
-    if (NP) MR_TRY_HIP(ctx, hipMemsetAsync(ofirst.p, 0x7f, NP * sizeof(int32_t), st));
     const uint64_t ecap = edge_capacity(sp->n_edge_keys, NP);
     DBuf<uint64_t> gk;
     DBuf<uint32_t> gc;
     MR_TRY(gk.alloc(ctx, ecap));
-    MR_TRY(gc.zero(ctx, ecap));
-    MR_TRY_HIP(ctx, hipMemsetAsync(gk.p, 0xff, ecap * sizeof(uint64_t), st));
+    MR_TRY(gc.alloc(ctx, ecap));
+    if (NP || ecap)
+        hipLaunchKernelGGL(k_ix_init, dim3(cdiv(std::max<int64_t>(NP, (int64_t)ecap), 256)), dim3(256), 0, st, ocnt.p,
+                           ofirst.p, NP, gk.p, gc.p, (int64_t)ecap);
     if (NT) {
         hipLaunchKernelGGL(k_ix_sel, dim3(cdiv(NT, 256)), dim3(256), 0, st, d_mask, sp->tlen.p, sp->po_off.p, NT, tflag.p,
                            zc.p);
