@@ -100,6 +100,19 @@ __global__ void k_fill_i64(int64_t* p, int64_t n, int64_t v) {
     if (i < n) p[i] = v;
 }
 
+__global__ void k_union_init(int32_t* pos_of_code, int32_t NP, int64_t* ua_num, int64_t* un_num, uint8_t* fl,
+                             double* ua_w, double* un_w, int32_t U, int32_t* zf) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < NP) pos_of_code[i] = -1;
+    if (i < U) {
+        ua_num[i] = 0;
+        un_num[i] = 0;
+        fl[i] = 0;
+        ua_w[i] = 0.0;
+        un_w[i] = 0.0;
+    }
+    if (i == 0) zf[0] = 0;
+}
 // union of the two graphs' nodes in the reference's spectrum order (online_rca.py:45-69)
 __global__ void k_union_a(const int32_t* a_podop, int32_t Na, const double* a_w, const int32_t* a_cov, int32_t* pos_of_code,
                           uint8_t* flags, double* ua_w, int64_t* ua_num, int32_t* uc) {
@@ -308,11 +321,13 @@ extern "C" int mr_rca_window(mr_ctx* ctx, const mr_spans* s, int64_t t0, int64_t
         return code;
     };
     if ((rc = pos_of_code.alloc(ctx, NP)) || (rc = only.alloc(ctx, Nn)) || (rc = uc.alloc(ctx, U)) ||
-        (rc = opos.alloc(ctx, Nn + 1)) || (rc = tmp.alloc(ctx, scan_tmp_elems(Nn))) || (rc = ua_num.zero(ctx, U)) ||
-        (rc = un_num.zero(ctx, U)) || (rc = fl.zero(ctx, U)) || (rc = ua_w.zero(ctx, U)) || (rc = un_w.zero(ctx, U)) ||
-        (rc = zf.zero(ctx, 1)))
+        (rc = opos.alloc(ctx, Nn + 1)) || (rc = tmp.alloc(ctx, scan_tmp_elems(Nn))) || (rc = ua_num.alloc(ctx, U)) ||
+        (rc = un_num.alloc(ctx, U)) || (rc = fl.alloc(ctx, U)) || (rc = ua_w.alloc(ctx, U)) || (rc = un_w.alloc(ctx, U)) ||
+        (rc = zf.alloc(ctx, 1)))
         return cleanup(rc);
-    if (hipMemsetAsync(pos_of_code.p, 0xff, NP * sizeof(int32_t), st) != hipSuccess) return cleanup(MR_ERR_HIP);
+    // one launch clears the union's arrays (was seven memsets per window)
+    hipLaunchKernelGGL(k_union_init, dim3(cdiv(std::max<int64_t>({(int64_t)NP, (int64_t)U, 1}), 256)), dim3(256), 0, st,
+                       pos_of_code.p, NP, ua_num.p, un_num.p, fl.p, ua_w.p, un_w.p, U, zf.p);
     hipLaunchKernelGGL(k_union_a, dim3(cdiv(Na, 256)), dim3(256), 0, st, ga->node_podop.p, Na, ga->weight.p, ga->cov.p,
                        pos_of_code.p, fl.p, ua_w.p, ua_num.p, uc.p);
     hipLaunchKernelGGL(k_union_n_flags, dim3(cdiv(Nn, 256)), dim3(256), 0, st, gn->node_podop.p, Nn, pos_of_code.p, only.p);
