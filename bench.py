@@ -133,25 +133,43 @@ def pmc_traffic(args, timeout_s=240):
     return {"fetch": 2.0 * vals["FETCH_SIZE"], "write": vals["WRITE_SIZE"]}
 
 
-def cpu_baseline(abnormal, t0, t1, a3, ok, target_s=12.0):
-    """The oracle's C restatement of the same window, timed on this host (bounded sample)."""
+def host_cores():
+    """(threads this process may use, CPUs of the machine): the CPU affinity / OMP_NUM_THREADS share
+    (16 per GPU on the GPU box, whose nproc shows the whole machine) and os.cpu_count()."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return (min(aff, omp) if omp > 0 else aff), (os.cpu_count() or 1)
+
+
+def cpu_baseline(abnormal, t0, t1, a3, ok, target_s=10.0, one_core_s=8.0):
+    """The oracle's C restatement of the same window, timed on this host (bounded samples): on
+    every core this process may use, and on one core (SURVEY §8(d) CPU baseline timing)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import c_oracle
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    threads, machine = host_cores()
     res = c_oracle.rca_window(abnormal, t0, t1, a3, ok, nthreads=threads)   # warm-up + correctness handle
-    n, t_start, edges = 0, time.perf_counter(), 0
-    while True:
-        r = c_oracle.rca_window(abnormal, t0, t1, a3, ok, nthreads=threads)
-        edges += r[4]
-        n += 1
-        el = time.perf_counter() - t_start
-        if el >= target_s or n >= 20:
-            break
+
+    def timed(nthreads, budget, cap):
+        n, t_start, edges = 0, time.perf_counter(), 0
+        while True:
+            r = c_oracle.rca_window(abnormal, t0, t1, a3, ok, nthreads=nthreads)
+            edges += r[4]
+            n += 1
+            el = time.perf_counter() - t_start
+            if el >= budget or n >= cap:
+                return n, el, edges
+
+    n, el, edges = timed(threads, target_s, 20)
+    n1, el1, edges1 = timed(1, one_core_s, 8)
     return {"value": round(edges / el / 1e9, 4), "unit": "GTEPS", "cores": threads, "kind": "port",
             "sample": f"{n} full windows of this config (detect + 2 graph builds + 2x25 PageRank iterations + spectrum), "
-                      f"oracle/mr_oracle.c OpenMP, {el:.1f} s",
-            "windows_per_s": round(n / el, 4)}, res
+                      f"oracle/mr_oracle.c OpenMP on {threads} threads, {el:.1f} s; one core: {n1} windows, {el1:.1f} s",
+            "windows_per_s": round(n / el, 4), "nproc": machine,
+            "one_core": {"value": round(edges1 / el1 / 1e9, 4), "windows_per_s": round(n1 / el1, 4), "cores": 1}}, res
 
 
 def c4_cpu_baseline(n_ops, n_traces, target_s=15.0):

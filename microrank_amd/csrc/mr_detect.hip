@@ -6,7 +6,7 @@
 // by (trace, service-op); per trace, expect = sum over its ops in name order of
 // count * (mean + 3 std), ops without an SLO adding nothing (the reference's bare except),
 // real = max duration / 1000, abnormal iff real > expect (strict), traces with max <= 0
-// dropped (:329).  The sum is sequential per trace with separate multiply and add (T14), so
+// dropped (preprocess_data.py:117).  The sum is sequential per trace with separate multiply and add (T14), so
 // the partition is bit-exact.
 #include <algorithm>
 #include <chrono>
@@ -290,11 +290,12 @@ extern "C" int mr_rca_window(mr_ctx* ctx, const mr_spans* s, int64_t t0, int64_t
     MR_TRY(m_nor.alloc(ctx, NT));
     hipLaunchKernelGGL(k_masks, dim3(cdiv(NT, 256)), dim3(256), 0, st, dst.p, NT, m_abn.p, m_nor.p);
     mr_graph *gn = nullptr, *ga = nullptr;
-    // the graphs see the window's rows only (get_pagerank_graph(.., span_list), online_rca.py:180,185)
-    const int64_t win[2] = {t0, t1};
-    int rc = mr_graph_build_dev(ctx, s, m_abn.p, &gn, win);   // "normal" graph = detector's abnormal traces
+    // the graphs take EVERY row of the selected traces: the driver passes the whole DataFrame,
+    // get_pagerank_graph(normal_list, data) (online_rca.py:180,185), which filters by traceID
+    // only (preprocess_data.py:148) -- not the detector's window rows
+    int rc = mr_graph_build_dev(ctx, s, m_abn.p, &gn, nullptr);   // "normal" graph = detector's abnormal traces
     mark("build_n");
-    if (rc == MR_OK) rc = mr_graph_build_dev(ctx, s, m_nor.p, &ga, win);
+    if (rc == MR_OK) rc = mr_graph_build_dev(ctx, s, m_nor.p, &ga, nullptr);
     mark("build_a");
     if (rc == MR_OK) {   // both PageRanks in one batched launch per iteration
         mr_graph* both[2] = {gn, ga};

@@ -1,14 +1,14 @@
 // K1: preprocess_data.get_pagerank_graph (preprocess_data.py:146-171) on gfx950.
 //
-// From HBM-resident int-coded span columns and a trace mask (the trace_list, :360):
+// From HBM-resident int-coded span columns and a trace mask (the trace_list, :148):
 //   1. compact the selected rows, keeping row order (first appearance, T10)
-//   2. per row: span counts per trace (len_t, :377) and per pod-op (len_o, :379), first
+//   2. per row: span counts per trace (len_t, :165) and per pod-op (len_o, :167), first
 //      appearance row per pod-op, and the parent join ParentSpanId == spanID over the selected
-//      rows regardless of traceID (:370, T11) -> distinct (parent op, child op) edges with
-//      multiplicity (children multiset size, :371).  Hot keys (the root op is in every trace)
+//      rows regardless of traceID (preprocess_data.py:157-158, T11) -> distinct (parent op, child op) edges with
+//      multiplicity (children multiset size, :159).  Hot keys (the root op is in every trace)
 //      are aggregated in LDS per block before any global atomic.
 //   3. node order: parent ops sorted by name (= code), then the other ops by first appearance
-//      (:371-375, T10)
+//      (preprocess_data.py:159-163, T10)
 //   4. (trace, node) pairs -> stable radix sort -> distinct pairs = trace-major CSR (the
 //      op-major side is derived by mr_graph_prepare as tiles); call edges sorted by
 //      (child, parent) give P_ss by child.

@@ -140,6 +140,7 @@ struct mr_graph {
     // leaves one dense row of N partials per block (exact integer sums: order-free)
     bool fused = false;
     bool traces_nonempty = true;   // every trace has an op (span-built graphs; checked at upload)
+    bool force_tile = false;       // the ranks of a sharded graph agreed on the tile path
     int64_t T_all = 0;             // traces over all shards (0: this graph is whole)
     bool sharded_done = false;     // mr_pagerank_sharded's graph-level exchange has run
     DBuf<uint64_t> fx_part;   // [n_blocks * N]

@@ -207,7 +207,7 @@ constexpr uint64_t KCHK_SEED = 0x0ddba11cafeull;
 template <bool CHK, bool U16>
 __global__ void __launch_bounds__(KB) k_kind_insert(const int64_t* off, const int32_t* ops, const uint16_t* o16,
                                                     const float* w_t, int32_t T, unsigned long long* hk, KCnt* cr, int32_t* slot_of,
-                                                    uint64_t mask, uint64_t seed, uint64_t* chk) {
+                                                    uint64_t mask, uint64_t seed, uint64_t* chk, uint64_t hmask) {
     __shared__ unsigned long long lkey[KLDS];
     __shared__ uint32_t lcnt[KLDS];
     __shared__ int32_t lrep[KLDS];
@@ -282,6 +282,8 @@ __global__ void __launch_bounds__(KB) k_kind_insert(const int64_t* off, const in
             if (CHK) h2 = kind_fold(KCHK_SEED, wb, n, lacc2[threadIdx.x]);
         } else
             h = kind_hash2<CHK>(off, ops, w_t, t, seed, KCHK_SEED, &h2);
+        h &= hmask;   // ~0 (tests narrow it to force collisions)
+        if (!h) h = 1;
         int s = (int)(h & (KLDS - 1));
         for (;;) {
             unsigned long long k = atomicCAS(&lkey[s], 0ull, (unsigned long long)h);
@@ -341,7 +343,7 @@ __global__ void k_pref_partial(const double* kind, const int32_t* pr_trace, cons
         int32_t t = pr_trace ? pr_trace[i] : i;
         int32_t ln = pr_len ? pr_len[i] : len_t[t];
         a = 1.0 / kind[t];
-        if (ln == 0) atomicOr(flag, 2);   // 1.0/len(pr_trace[t]) -> ZeroDivisionError
+        if (ln == 0) atomicOr(flag + 1, 1);   // 1.0/len(pr_trace[t]) -> ZeroDivisionError (word 1)
         b = ln ? 1.0 / (double)ln : 0.0;
     }
     a = block_sum(a, red);
@@ -556,7 +558,8 @@ __global__ void __launch_bounds__(TB) k_iter_a(const GDev* __restrict__ gs, int3
             rmax = rp;
         }
         rmax = block_max(rmax, red);
-        if (threadIdx.x == 0) atomicMax(&Mnext[MSH + blockIdx.x % MSH], d2bits(rmax));
+        // a block with no trace (an empty shard's placeholder) leaves -inf: no bits to max in
+        if (threadIdx.x == 0 && rmax >= 0.0) atomicMax(&Mnext[MSH + blockIdx.x % MSH], d2bits(rmax));
         return;
     }
     // ---- tile role: partial sums of q_k over each (tile, op) pair  (pagerank.py:122-124, P_sr r)
@@ -1057,7 +1060,8 @@ __global__ void __launch_bounds__(S * FX_TMAX, 4) k_fx_a(const GDev* __restrict_
     for (int32_t o = i; o < N; o += NS) prow[o] = lacc[AS * o];
     rmax = block_max(rmax, red);
     if (i == 0) {
-        atomicMax((unsigned long long*)&Mnext[MSH + blockIdx.x % MSH], d2bits(rmax));
+        if (rmax >= 0.0)   // -inf: a block without traces (an empty shard's placeholder)
+            atomicMax((unsigned long long*)&Mnext[MSH + blockIdx.x % MSH], d2bits(rmax));
         if (G.stamp) {
             unsigned long long* sp = G.stamp + (size_t)blockIdx.x * 16;
             sp[0] = ts0;
@@ -1363,7 +1367,7 @@ int mr_graph_prepare(mr_ctx* ctx, mr_graph* g) {
         hipLaunchKernelGGL(k_ids16, dim3(cdiv(g->nnz_rs, 256)), dim3(256), 0, st, g->rs_ops.p, g->nnz_rs, g->rs16.p);
     }
     static const bool no_fused = getenv("MR_NO_FUSED") != nullptr;   // A/B knob: force the tile path
-    g->fused = !no_fused && g->rs_is_sr && g->traces_nonempty && N <= FX_NMAX && fx_tt(N) > 0;
+    g->fused = !no_fused && !g->force_tile && g->rs_is_sr && g->traces_nonempty && N <= FX_NMAX && fx_tt(N) > 0;
     if (g->fused) {   // no P_sr tiles: the fused iteration reads the trace-major ids only
         MR_TRY_HIP(ctx, hipMemsetAsync(g->cov.p, 0, (size_t)std::max(N, 1) * sizeof(int32_t), st));
         if (nnz && N)
@@ -1461,7 +1465,7 @@ int mr_graph_prepare(mr_ctx* ctx, mr_graph* g) {
 static int shard_kinds(mr_ctx* ctx, mr_graph* g, uint64_t cap);
 
 static int pagerank_setup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool fp32, uint32_t flags, int TT,
-                          bool sharded = false) {
+                          bool sharded, uint64_t seed, uint64_t hmask) {
     hipStream_t st = ctx->stream;
     const int32_t N = g->N, T = g->T;
     uint64_t cap = 1;
@@ -1485,7 +1489,7 @@ static int pagerank_setup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool 
     MR_TRY(g->sub[1].alloc(ctx, (size_t)N + 1));
     MR_TRY(g->weight.alloc(ctx, (size_t)N));
     if (g->fused) {
-        MR_TRY(g->fx_part.alloc(ctx, (size_t)fx_blocks(T, N, TT) * (size_t)N));
+        MR_TRY(g->fx_part.alloc(ctx, (size_t)std::max<int64_t>(fx_blocks(T, N, TT), 1) * (size_t)N));
         MR_TRY(g->fx_ssv.alloc(ctx, (size_t)N));
     }
     else MR_TRY(g->part.alloc(ctx, (size_t)std::max<int64_t>(g->n_pairs, 1)));
@@ -1510,13 +1514,13 @@ static int pagerank_setup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool 
                     : (u16 ? k_kind_insert<false, true> : k_kind_insert<false, false>);
     if (T)
         hipLaunchKernelGGL(kins, dim3(cdiv(T, KB)), dim3(KB), 0, st, koff, kops, (const uint16_t*)g->rs16.p, g->w_t.p,
-                           T, g->ht_key.p, g->ht_cr.p, g->slot_of.p, (uint64_t)(cap - 1), 0x5eed5eedull,
-                           chk ? g->ht_chk.p : (uint64_t*)nullptr);
+                           T, g->ht_key.p, g->ht_cr.p, g->slot_of.p, (uint64_t)(cap - 1), seed,
+                           chk ? g->ht_chk.p : (uint64_t*)nullptr, hmask);
     MR_DEBUG_CHECK(ctx, "k_kind_insert");
-    if (u16)
+    if (T && u16)
         hipLaunchKernelGGL(k_kind_verify<uint16_t>, dim3(cdiv(T, 256)), dim3(256), 0, st, koff,
                            (const uint16_t*)g->rs16.p, g->w_t.p, T, g->ht_cr.p, g->slot_of.p, g->kind.p, g->flag.p);
-    else
+    else if (T)
         hipLaunchKernelGGL(k_kind_verify<int32_t>, dim3(cdiv(T, 256)), dim3(256), 0, st, koff, kops, g->w_t.p, T,
                            g->ht_cr.p, g->slot_of.p, g->kind.p, g->flag.p);
     MR_DEBUG_CHECK(ctx, "k_kind_verify");
@@ -1524,8 +1528,8 @@ static int pagerank_setup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool 
     // ---- preference
     const int32_t* prt = g->pr_identity ? nullptr : g->pr_trace.p;
     const int32_t* prl = g->pr_identity ? nullptr : g->pr_len.p;
-    if (n_pr > 0)
-        hipLaunchKernelGGL(k_pref_partial, dim3(nbp), dim3(TB), 0, st, g->kind.p, prt, prl, g->len_t.p, n_pr,
+    // also with n_pr == 0 (an empty shard): the one block writes the zero partials the sums read
+    hipLaunchKernelGGL(k_pref_partial, dim3(nbp), dim3(TB), 0, st, g->kind.p, prt, prl, g->len_t.p, n_pr,
                            g->ppart.p, g->flag.p);
     if ((flags & MR_PR_EXACT_SUMS) && !sharded)
         hipLaunchKernelGGL(k_pref_total_exact, dim3(1), dim3(64), 0, st, g->kind.p, prt, prl, g->len_t.p, n_pr,
@@ -1554,13 +1558,20 @@ static double iter_bytes(const mr_graph* g, bool fp32) {
            3.0 * w * (double)g->N;
 }
 
-int mr_pagerank_batch_impl(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly, int ng, double d, double alpha,
-                           int iters, int precision, uint32_t flags, bool sharded = false) {
+// one attempt with kind-hash seed `seed`; *collided reports a 64-bit key collision found by the
+// exact verification (k_kind_verify / k_sh_kind_check), after which the caller retries
+static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly, int ng, double d, double alpha,
+                            int iters, int precision, uint32_t flags, bool sharded, uint64_t seed, uint64_t hmask,
+                            bool* collided) {
+    *collided = false;
     if (!ctx || ng <= 0 || !gs || !anomaly) return mr_fail(ctx, MR_ERR_ARG, "mr_pagerank: bad arguments");
     if (iters < 0) return mr_fail(ctx, MR_ERR_ARG, "iters < 0");
     for (int i = 0; i < ng; ++i) {
         if (!gs[i] || gs[i]->ctx != ctx) return mr_fail(ctx, MR_ERR_STATE, "mr_pagerank: bad handles");
-        if (gs[i]->N == 0 || gs[i]->T == 0)   // np.amax of an empty vector (pagerank.py:126-127)
+        // np.amax of an empty vector (pagerank.py:126-127); a shard tests the whole graph's traces,
+        // so a rank whose shard is empty still joins every collective of the call
+        const int64_t T = sharded ? gs[i]->T_all : (int64_t)gs[i]->T;
+        if (gs[i]->N == 0 || T == 0)
             return mr_fail(ctx, MR_ERR_VALUE, "zero-size array to reduction operation maximum which has no identity");
     }
     MR_TRY_HIP(ctx, hipSetDevice(ctx->device));
@@ -1569,7 +1580,7 @@ int mr_pagerank_batch_impl(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly,
     int TT = FX_TMAX;   // one block size for the batch: the largest that fits every fused graph
     for (int i = 0; i < ng; ++i)
         if (gs[i]->fused) TT = std::min(TT, fx_tt(gs[i]->N));
-    for (int i = 0; i < ng; ++i) MR_TRY(pagerank_setup(ctx, gs[i], anomaly[i], d, fp32, flags, TT, sharded));
+    for (int i = 0; i < ng; ++i) MR_TRY(pagerank_setup(ctx, gs[i], anomaly[i], d, fp32, flags, TT, sharded, seed, hmask));
     // ---- batched power iteration: one k_iter_a + k_iter_b pair per iteration for every graph
     int mask = 3;
     if (const char* rm = getenv("MR_ROLE_MASK")) mask = atoi(rm);   // profiling knob: 1 trace / 2 op side
@@ -1610,7 +1621,9 @@ int mr_pagerank_batch_impl(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly,
         v.fx_limb = (unsigned long long*)g->fx_limb.p;
         v.op_sum = g->op_sum.p;
         v.stamp = nullptr;
-        const int64_t nfa = g->fused ? fx_blocks(g->T, g->N, TT) : 0;
+        // a shard without traces still runs one (empty) block: it clears the maxima slot and
+        // writes a zero partial row, and the collectives after the launch need every rank
+        const int64_t nfa = g->fused ? std::max<int64_t>(fx_blocks(g->T, g->N, TT), sharded ? 1 : 0) : 0;
         // a row entry stays below 2^63; shards of one graph hold different trace counts, and their
         // limbs are summed, so they share the scale of the largest block (2^15 traces)
         const int sc = 63 - (sharded ? 15 : bits_for((uint64_t)std::max<int64_t>(cdiv(cdiv((int64_t)g->T, TT), std::max<int64_t>(nfa, 1)) * TT - 1, 1)));
@@ -1633,7 +1646,7 @@ int mr_pagerank_batch_impl(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly,
             multi = multi || v.n_fa < cdiv(g->T, TT);
             continue;   // no tile-path blocks (n_tb = n_tiles = n_ob = 0)
         }
-        v.n_tb = (mask & 1) ? cdiv(g->T, TB) : 0;
+        v.n_tb = (mask & 1) ? std::max(cdiv(g->T, TB), sharded ? 1 : 0) : 0;   // (empty shard: see nfa)
         v.n_tiles = (mask & 2) ? g->n_tiles : 0;
         v.tshift = g->tshift;
         v.lds_su = g->N <= LDS_NODES;
@@ -1724,16 +1737,45 @@ int mr_pagerank_batch_impl(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly,
         for (int k = 0; k < 8; ++k) fprintf(stderr, " %s %.2f/%.2f", nm[k], sum[k] / std::max(nb, 1), mx[k]);
         fprintf(stderr, "\n");
     }
+    // a shard's local collision must make every rank retry: the error words meet in a MAX
+    if (coll) MR_TRY(mr_coll_allreduce(ctx, gs[0]->flag.p, 4, MR_DT_I32, 1));
     // the only host round trip of the call: error words raised by the kernels
     std::vector<int32_t> hflag((size_t)4 * ng, 0);
     for (int i = 0; i < ng; ++i)
         MR_TRY_HIP(ctx, hipMemcpyAsync(&hflag[(size_t)4 * i], gs[i]->flag.p, 4 * sizeof(int32_t), hipMemcpyDeviceToHost, st));
     MR_TRY_HIP(ctx, hipStreamSynchronize(st));
     for (int i = 0; i < ng; ++i) {
-        if (hflag[(size_t)4 * i] & 1) return mr_fail(ctx, MR_ERR_STATE, "trace-kind hash collision (retry with another seed)");
-        if (anomaly[i] && (hflag[(size_t)4 * i] & 2)) return mr_fail(ctx, MR_ERR_ZERODIV, "float division by zero");
+        if (hflag[(size_t)4 * i] & 1) {
+            *collided = true;
+            return MR_OK;
+        }
+        if (anomaly[i] && (hflag[(size_t)4 * i + 1] & 1)) return mr_fail(ctx, MR_ERR_ZERODIV, "float division by zero");
     }
     return MR_OK;
+}
+
+// A 64-bit set-hash collision between two different trace kinds is caught by the exact
+// verification; the whole call then reruns with the next seed (independent hash functions), so
+// an input that collides under one seed is still ranked.  Seeds are a fixed sequence: every rank
+// of a sharded graph takes the same one.
+int mr_pagerank_batch_impl(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly, int ng, double d, double alpha,
+                           int iters, int precision, uint32_t flags, bool sharded = false) {
+    static const uint64_t seed0 = [] {   // MR_KIND_SEED: test knob (start the sequence elsewhere)
+        const char* e = getenv("MR_KIND_SEED");
+        return e ? (uint64_t)strtoull(e, nullptr, 0) : 0x5eed5eedull;
+    }();
+    // MR_KIND_TEST_COLLIDE: test knob -- the first attempt keeps 2 bits of every key, so distinct
+    // kinds collide and the verification + retry path runs
+    const bool force = getenv("MR_KIND_TEST_COLLIDE") != nullptr;   // read per call (tests set it)
+    constexpr int ATTEMPTS = 4;
+    for (int a = 0; a < ATTEMPTS; ++a) {
+        bool collided = false;
+        MR_TRY(pagerank_attempt(ctx, gs, anomaly, ng, d, alpha, iters, precision, flags, sharded,
+                                seed0 + 0x9E3779B97F4A7C15ull * (uint64_t)a, (force && a == 0) ? 3ull : ~0ull,
+                                &collided));
+        if (!collided) return MR_OK;
+    }
+    return mr_fail(ctx, MR_ERR_STATE, "trace-kind hash collision under %d seeds", ATTEMPTS);
 }
 
 extern "C" int mr_pagerank(mr_ctx* ctx, mr_graph* g, int anomaly, double d, double alpha, int iters,
@@ -1851,6 +1893,21 @@ extern "C" int mr_pagerank_sharded(mr_ctx* ctx, mr_graph* g, int anomaly, double
     if (!mr_coll_ready(ctx) && ctx->nranks != 1) return mr_fail(ctx, MR_ERR_COMM, "no collective backend");
     MR_TRY_HIP(ctx, hipSetDevice(ctx->device));
     if (!g->sharded_done) {   // the graph-level exchange happens once per graph
+        if (mr_coll_ready(ctx) && ctx->nranks > 1) {
+            // every rank must run the same iteration (the fused path's u64 limb all-reduce or the
+            // tile path's fp64 op sums): the fused choice depends on this shard (e.g. a trace
+            // without ops), so the ranks agree on it -- fused only if fused everywhere
+            DBuf<int32_t> f;
+            int32_t tile = g->fused ? 0 : 1;   // MAX over ranks: 1 if any rank takes the tile path
+            MR_TRY(f.upload(ctx, &tile, 1));
+            MR_TRY(mr_coll_allreduce(ctx, f.p, 1, MR_DT_I32, 1));
+            MR_TRY(f.download(ctx, &tile, 1));
+            MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));
+            if (g->fused && tile) {
+                g->force_tile = true;
+                MR_TRY(mr_graph_prepare(ctx, g));   // the P_sr tiles (before the per-op sums below)
+            }
+        }
         MR_TRY(shard_exchange(ctx, g));
         g->sharded_done = true;
     }

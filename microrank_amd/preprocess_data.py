@@ -68,32 +68,41 @@ class DeviceSpans:
 
 
 _CACHE: dict = {}
+# every column SpanTable.from_dataframe reads: an in-place edit of any of them (the reference's own
+# get_operation_duration_data rewrites operationName, preprocess_data.py:100) must rebuild the table
+_TABLE_COLUMNS = ("traceID", "spanID", "ParentSpanId", "serviceName", "operationName", "podName", "duration",
+                  "startTime", "endTime")
 
 
 def _fingerprint(df: pd.DataFrame):
-    n = len(df)
-    if n == 0:
-        return (0,)
-    pick = [0, n // 2, n - 1]
-    sample = tuple(str(df["traceID"].iat[i]) + "|" + str(df["spanID"].iat[i]) for i in pick)
-    return (n, sample, int(df["duration"].to_numpy().sum()))
+    """Content hash of the columns the span table is built from (row order included)."""
+    cols = [c for c in _TABLE_COLUMNS if c in df.columns]
+    if len(df) == 0:
+        return (0, tuple(cols))
+    h = pd.util.hash_pandas_object(df[cols], index=False).to_numpy()
+    # order-sensitive fold: row i's hash weighted by an odd multiplier of its position
+    w = (np.arange(h.size, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15)) | np.uint64(1)
+    return (len(df), tuple(cols), int(np.bitwise_xor.reduce(h * w)), int(h.sum(dtype=np.uint64)))
 
 
 def span_table(df: pd.DataFrame, ctx=None):
-    """(SpanTable, DeviceSpans) for a DataFrame, built once per DataFrame object."""
+    """(SpanTable, DeviceSpans) for a DataFrame, built once per (DataFrame, Context) and rebuilt
+    when any column it reads changed.  The device table belongs to the context that uploaded it
+    (mr_spans handles are per mr_ctx), so two contexts sharing a DataFrame get a handle each."""
     ctx = ctx or _lib.default_context()
-    key = (id(df), ctx.device)
+    key = (id(df), id(ctx))
     fp = _fingerprint(df)
     hit = _CACHE.get(key)
-    if hit is not None and hit[0]() is df and hit[1] == fp:
-        return hit[2], hit[3]
+    if hit is not None and hit[0]() is df and hit[1]() is ctx and hit[2] == fp:
+        return hit[3], hit[4]
     table = SpanTable.from_dataframe(df)
     dev = DeviceSpans(ctx, table)
     try:
         ref = weakref.ref(df, lambda _r, k=key: _CACHE.pop(k, None))
-    except TypeError:  # pragma: no cover - DataFrames are weak-referenceable
-        ref = lambda: df
-    _CACHE[key] = (ref, fp, table, dev)
+        cref = weakref.ref(ctx, lambda _r, k=key: _CACHE.pop(k, None))
+    except TypeError:  # pragma: no cover - DataFrames and Contexts are weak-referenceable
+        ref, cref = (lambda: df), (lambda: ctx)
+    _CACHE[key] = (ref, cref, fp, table, dev)
     return table, dev
 
 

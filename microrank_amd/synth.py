@@ -117,8 +117,15 @@ def _walk(topo: Topology, n_traces: int, rng, branch: float, p_max: float, p_rep
 def gen_spans(topo: Topology, n_traces: int, seed: int = 0, *, t0_ns: int = 1_700_000_000 * 10**9,
               minutes: float = 5.0, branch: float = 1.6, p_max: float = 0.7, p_repeat: float = 0.1,
               fault_op: Optional[int] = None, fault_frac: float = 0.0, fault_ms: float = 2500.0,
-              dup_span_frac: float = 0.0, broken_frac: float = 0.0, names: bool = True) -> SpanTable:
-    """Generate ``n_traces`` traces.  Trace codes are assigned in sorted traceID order."""
+              dup_span_frac: float = 0.0, broken_frac: float = 0.0, names: bool = True,
+              span_times: bool = False) -> SpanTable:
+    """Generate ``n_traces`` traces.  Trace codes are assigned in sorted traceID order.
+
+    ``span_times``: startTime / endTime per SPAN (a child starts after its parent, ends after
+    its own duration) instead of the trace-level TraceStart / TraceEnd the reference's CSVs
+    carry (online_rca.py:229-230), so traces near a window edge straddle it: the detector's
+    window (preprocess_data.py:13) then keeps only some rows of a trace, while the graph of the
+    trace takes all of them (online_rca.py:180,185)."""
     rng = np.random.default_rng([seed, 0x5A])
     tr, op, par, lvl = _walk(topo, n_traces, rng, branch, p_max, p_repeat)
     S = tr.size
@@ -148,6 +155,15 @@ def gen_spans(topo: Topology, n_traces: int, seed: int = 0, *, t0_ns: int = 1_70
     root_dur = np.zeros(n_traces, dtype=np.int64)
     root_dur[tr[lvl == 0]] = dur_us[lvl == 0]
     tend_tr = tstart_tr + root_dur * 1000
+    if span_times:
+        # per span: the parent's start + a 0..2 ms offset per level, end = start + duration
+        off = np.zeros(S, dtype=np.int64)
+        jit = rng.integers(0, 2_000_000, size=S)
+        for level in range(1, int(lvl.max()) + 1):
+            m = lvl == level
+            off[m] = off[par[m]] + jit[m]
+        sp_start = tstart_tr[tr] + off
+        sp_end = sp_start + dur_us * 1000
     # traceIDs: random 128-bit hex; code = rank in sorted order
     hi = rng.integers(0, 2**63, size=n_traces, dtype=np.int64)
     trace_rank = np.argsort(np.argsort(hi, kind="stable"), kind="stable").astype(np.int32)
@@ -171,7 +187,8 @@ def gen_spans(topo: Topology, n_traces: int, seed: int = 0, *, t0_ns: int = 1_70
     # podop / svcop codes via the name dictionaries (sorted string order)
     st = SpanTable(trace=trace_rank[tr[row]], podop=None, svcop=None, span=span_code.astype(np.int64),
                    parent=parent_code.astype(np.int64), duration=dur_us[row],
-                   tstart=tstart_tr[tr[row]], tend=tend_tr[tr[row]])
+                   tstart=sp_start[row] if span_times else tstart_tr[tr[row]],
+                   tend=sp_end[row] if span_times else tend_tr[tr[row]])
     svc_of = topo.service[op_r]
     svcop_str = np.array([f"{topo.svc_names[s]}_{topo.op_names[o]}" for s, o in
                           zip(topo.service, range(topo.n_ops))], dtype=object)
@@ -239,14 +256,16 @@ def fault_op_of(topo: Topology) -> int:
 
 def window_pair(n_ops: int, n_traces: int, seed: int, *, pods: int = 1, dup: float = 0.0,
                 broken: float = 0.0, branch: float = 4.0, p_max: float = 0.7, zipf_s: float = 0.0,
-                fault_frac: float = 0.4, fault_ms: float = 4000.0, names: bool = True):
+                fault_frac: float = 0.4, fault_ms: float = 4000.0, names: bool = True, span_times: bool = False,
+                minutes: float = 5.0):
     """(topology, normal SpanTable for the SLO, abnormal SpanTable with a fault) -- SURVEY §8.2."""
     topo = make_topology(n_ops, seed, pods_per_service=pods, zipf_s=zipf_s)
-    normal = gen_spans(topo, n_traces, seed + 1, branch=branch, p_max=p_max, names=names)
+    normal = gen_spans(topo, n_traces, seed + 1, branch=branch, p_max=p_max, names=names, span_times=span_times,
+                       minutes=minutes)
     abnormal = gen_spans(topo, n_traces, seed + 2, branch=branch, p_max=p_max,
                          fault_op=fault_op_of(topo), fault_frac=fault_frac, fault_ms=fault_ms,
                          dup_span_frac=dup,
-                         broken_frac=broken, names=names)
+                         broken_frac=broken, names=names, span_times=span_times, minutes=minutes)
     return topo, normal, abnormal
 
 

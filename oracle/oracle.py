@@ -238,13 +238,13 @@ class SpanGraph:
 
 def span_graph(trace: np.ndarray, podop: np.ndarray, span: np.ndarray, parent: np.ndarray,
                selected: np.ndarray) -> SpanGraph:
-    """``selected``: bool per trace code (the trace_list membership, :360).
+    """``selected``: bool per trace code (the trace_list membership, preprocess_data.py:148).
 
-    * :370 merge ParentSpanId == spanID over the filtered spans, traceID ignored (T11):
-      duplicated spanIDs fan out, orphans give no edge.
-    * :371 groupby(parent op) sorts parents by name; :372-375 never-parent ops follow in
+    * preprocess_data.py:157-158 merge ParentSpanId == spanID over the filtered spans, traceID
+      ignored (T11): duplicated spanIDs fan out, orphans give no edge.
+    * :159 groupby(parent op) sorts parents by name; :160-163 never-parent ops follow in
       first-appearance row order (T10).
-    * :377-381 trace keys sorted; list entries one per span.
+    * :165-169 trace keys sorted; list entries one per span.
     """
     rows = np.flatnonzero(selected[trace])
     op = podop[rows].astype(np.int64)
@@ -324,7 +324,7 @@ def spectrum(anomaly_result, normal_result, anomaly_list_len, normal_list_len, t
              normal_num_list, anomaly_num_list, spectrum_method):
     """online_rca.py:33-152 -- returns (top_list, score_list, printed_lines)."""
     sp = {}
-    for node in anomaly_result:                       # :201-214
+    for node in anomaly_result:                       # online_rca.py:45-58
         a = anomaly_result[node]
         e = {"ef": a * anomaly_num_list[node], "nf": a * (anomaly_list_len - anomaly_num_list[node])}
         if node in normal_result:
@@ -335,14 +335,14 @@ def spectrum(anomaly_result, normal_result, anomaly_list_len, normal_list_len, t
             e["ep"] = 0.0000001
             e["np"] = 0.0000001
         sp[node] = e
-    for node in normal_result:                        # :216-225
+    for node in normal_result:                        # online_rca.py:60-69
         if node not in sp:
             n = normal_result[node]
             sp[node] = {"ep": (1 + n) * normal_num_list[node], "np": normal_list_len - normal_num_list[node],
                         "ef": 0.0000001, "nf": 0.0000001}
     res = {}
     m = spectrum_method
-    for node, e in sp.items():                        # :231-298
+    for node, e in sp.items():                        # online_rca.py:75-142
         ef, nf, ep, np_ = e["ef"], e["nf"], e["ep"], e["np"]
         if m == "dstar2":
             res[node] = ef * ef / (ep + nf)
@@ -371,7 +371,7 @@ def spectrum(anomaly_result, normal_result, anomaly_list_len, normal_list_len, t
         elif m == "rogers":
             res[node] = (ef + np_) / (ef + np_ + 2 * nf + 2 * ep)
     top, score, lines = [], [], []
-    for i, (k, v) in enumerate(sorted(res.items(), key=lambda x: x[1], reverse=True)):  # :303 stable
+    for i, (k, v) in enumerate(sorted(res.items(), key=lambda x: x[1], reverse=True)):  # :147-150, stable
         if i < top_max + 6:
             top.append(k)
             score.append(v)
@@ -429,7 +429,7 @@ def np_round4(x: float) -> float:
 
 
 def operation_slo(svcop: np.ndarray, duration: np.ndarray, svcop_names, operation_list) -> dict:
-    """preprocess_data.get_operation_slo (:262-290): per service-op [round(mean/1000,4),
+    """preprocess_data.get_operation_slo (preprocess_data.py:50-78): per service-op [round(mean/1000,4),
     round(std/1000,4)], population std, keys in sorted name order filtered by operation_list."""
     keep = set(operation_list)
     out = {}
@@ -452,7 +452,8 @@ def operation_slo(svcop: np.ndarray, duration: np.ndarray, svcop_names, operatio
 
 def detect(trace: np.ndarray, svcop: np.ndarray, duration: np.ndarray, tstart, tend, t0: int, t1: int,
            slo_mean_plus3std: Dict[int, float]):
-    """anormaly_detector.system_anomaly_detect (:44-84) + get_operation_duration_data (:309-334):
+    """anormaly_detector.system_anomaly_detect (anormaly_detector.py:44-84) + get_operation_duration_data
+    (preprocess_data.py:97-122):
     window on trace-level times (inclusive, T15); per trace real = max duration / 1000,
     expect = sum over ops in sorted name order of count * (mean + 3 std) (T14); traces with
     max duration <= 0 dropped.  Returns (flag, abnormal codes, normal codes) in sorted order,

@@ -234,10 +234,20 @@ def slo_large(outdir):
         json.dump(out, f, indent=0)
 
 
+def span_times_case(outdir):
+    """Per-span startTime / endTime (synth span_times): traces at the window's end straddle it, so
+    the detector sees some of their rows (get_span, preprocess_data.py:10-14) while the driver's
+    graphs take all rows of the selected traces (online_rca.py:180,185 pass the whole frame)."""
+    span_case("span_times", dict(n_ops=40, n_traces=1500, seed=400, span_times=True, minutes=5.2), outdir)
+
+
 def main():
     outdir = HERE
     if sys.argv[1:] == ["slo_large"]:
         slo_large(outdir)
+        return
+    if sys.argv[1:] == ["span_times"]:
+        span_times_case(outdir)
         return
     man = {"numpy": np.__version__, "pandas": pd.__version__, "python": sys.version.split()[0]}
     try:
@@ -301,6 +311,7 @@ def main():
     span_case("pods_dup_broken", dict(n_ops=30, n_traces=600, seed=200, pods=2, dup=0.01, broken=0.05), outdir)
     slo_large(outdir)
     span_case("ops200", dict(n_ops=200, n_traces=1500, seed=300, branch=1.9, p_max=0.8, fault_ms=6000.0), outdir, driver=False)
+    span_times_case(outdir)
     with open(os.path.join(outdir, "manifest.json"), "w") as f:
         json.dump(man, f, indent=1, sort_keys=True)
 

@@ -40,9 +40,13 @@ def _window_graph():
     return sg.as_graph()
 
 
-def _shard(g, rank, world):
-    """Traces [lo, hi) of the global graph, over the global node space."""
-    lo, hi = rank * g.T // world, (rank + 1) * g.T // world
+def _shard(g, rank, world, bounds=None):
+    """Traces [lo, hi) of the global graph, over the global node space (``bounds``: the ranks'
+    first traces, world + 1 ascending cut points; default an even split)."""
+    if bounds is None:
+        lo, hi = rank * g.T // world, (rank + 1) * g.T // world
+    else:
+        lo, hi = bounds[rank], bounds[rank + 1]
     m = (g.sr_t >= lo) & (g.sr_t < hi)
     sr_t, sr_o = g.sr_t[m] - lo, g.sr_o[m]
     len_t = g.len_t[lo:hi]
@@ -59,12 +63,13 @@ def _shard(g, rank, world):
                      nchild, np.arange(hi - lo), len_t.copy())
 
 
-def _worker(rank, world, port, anomaly, q):
+def _worker(rank, world, port, anomaly, q, empty_last=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         g = _window_graph()
-        s, cov = orc.sharded_pagerank(_shard(g, rank, world), GlooComm(), anomaly)
+        bounds = [0] + [g.T] * world if empty_last else None   # rank 0 all traces, the rest none
+        s, cov = orc.sharded_pagerank(_shard(g, rank, world, bounds), GlooComm(), anomaly)
         q.put((rank, s, cov))
     finally:
         dist.destroy_process_group()
@@ -76,14 +81,15 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("anomaly", [False, True])
-def test_two_rank_sharded_pagerank_matches_single(anomaly):
+@pytest.mark.parametrize("anomaly,empty_last", [(False, False), (True, False), (True, True)])
+def test_two_rank_sharded_pagerank_matches_single(anomaly, empty_last):
+    """empty_last: rank 1 holds no trace at all -- it still takes part in every reduction."""
     g = _window_graph()
     s_ref = orc.power_iteration(g, orc.preference(g, orc.trace_kinds(g), anomaly))
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, anomaly, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, anomaly, q, empty_last)) for r in range(2)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in procs]

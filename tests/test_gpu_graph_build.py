@@ -53,7 +53,7 @@ def _check_against_oracle(table, dev, sel):
     return pg, sg
 
 
-@pytest.mark.parametrize("name", ["c1", "pods_dup_broken", "ops200"])
+@pytest.mark.parametrize("name", ["c1", "pods_dup_broken", "ops200", "span_times"])
 def test_graph_build_matches_reference(name):
     from microrank_amd import _lib
     from microrank_amd.pagerank import trace_pagerank
@@ -147,3 +147,55 @@ def test_c2_scale_graph_build(dup, broken, pods):
     rng = np.random.default_rng(5)
     sel = rng.random(st.n_traces) < 0.6
     _check_against_oracle(st, dev, sel)
+
+
+def test_graph_sees_in_place_column_edits():
+    """The reference's get_operation_duration_data rewrites operationName on the frame it gets
+    (preprocess_data.py:100); a later get_pagerank_graph on that frame names its nodes from the
+    rewritten column.  The device span table must be rebuilt, not served from the cache."""
+    from microrank_amd.preprocess_data import get_operation_duration_data, get_pagerank_graph
+
+    case = load_golden("c1.json")
+    _, adf = regen_window(case)
+    df = adf.copy()
+    tnames = sorted(df["traceID"].unique())
+    lst = [tnames[i] for i in case["detect"]["normal"]]
+    before = list(get_pagerank_graph(lst, df)[0].keys())
+    assert before == case["graph_swapped_anomaly"]["nodes"]
+    get_operation_duration_data(case["operation_list"], df)   # mutates df["operationName"]
+    after = list(get_pagerank_graph(lst, df)[0].keys())
+    assert after != before
+    # the oracle on the rewritten frame (ts-ui-dashboard names lose one more '/segment', so some
+    # nodes merge -- as in the reference, whose get_pagerank_graph re-applies the rsplit rule)
+    from microrank_amd.spans import SpanTable
+
+    st = SpanTable.from_dataframe(df)
+    sel = np.isin(np.array(st.trace_names, dtype=object), lst)
+    sg = orc.span_graph(st.trace, st.podop, st.span, st.parent, sel)
+    assert after == [st.podop_names[c] for c in sg.node_podop]
+    from microrank_amd.preprocess_data import _fingerprint
+
+    fp = _fingerprint(df)
+    df.loc[df.index[0], "duration"] += 1   # any used column, in place
+    assert _fingerprint(df) != fp
+
+
+def test_two_contexts_share_one_dataframe():
+    """One Context per thread (the bench's streams): each context gets its own device span table
+    for the same DataFrame (mr_spans handles belong to the context that uploaded them)."""
+    from microrank_amd import _lib
+    from microrank_amd.pagerank import trace_pagerank
+    from microrank_amd.preprocess_data import get_pagerank_graph, span_table
+
+    case = load_golden("c1.json")
+    _, adf = regen_window(case)
+    tnames = sorted(adf["traceID"].unique())
+    lst = [tnames[i] for i in case["detect"]["abnormal"]]
+    c1, c2 = _lib.Context(0), _lib.Context(0)
+    t1, d1 = span_table(adf, c1)
+    t2, d2 = span_table(adf, c2)
+    assert d1 is not d2 and d1.ctx is c1 and d2.ctx is c2
+    w1, _ = trace_pagerank(*get_pagerank_graph(lst, adf, ctx=c1), False, ctx=c1)
+    w2, _ = trace_pagerank(*get_pagerank_graph(lst, adf, ctx=c2), False, ctx=c2)
+    assert list(w1) == list(w2) and [float(x) for x in w1.values()] == [float(x) for x in w2.values()]
+    np.testing.assert_allclose(list(w1.values()), unhex(case["pr_normal"]["weight"]), rtol=1e-10)

@@ -50,7 +50,7 @@ def test_unknown_key_raises_value_error():
         trace_pagerank({"a": []}, {"t": ["a"], "u": ["a"]}, {"a": ["t", "u"]}, {"t": ["a"], "u": []}, True)
 
 
-@pytest.mark.parametrize("name", ["c1", "pods_dup_broken", "ops200"])
+@pytest.mark.parametrize("name", ["c1", "pods_dup_broken", "ops200", "span_times"])
 def test_span_case_graphs(name):
     """The reference's own graph dicts for each window -> trace_pagerank on the GPU."""
     from microrank_amd.pagerank import trace_pagerank
@@ -152,3 +152,23 @@ def test_large_op_count_multi_tile_long_tiles(anomaly):
     w2, _ = dg.fetch()
     assert w2.tobytes() == w.tobytes(), "rerun not bitwise identical"
     dg.close()
+
+
+def test_kind_hash_collision_retries_with_next_seed(monkeypatch):
+    """MR_KIND_TEST_COLLIDE narrows the first attempt's kind keys to 2 bits, so distinct trace
+    kinds share keys: the exact verification must catch it and the call must rerun with the next
+    seed, giving the same kinds and weights as an uncollided run (pagerank.py:54-66)."""
+    from microrank_amd.pagerank import trace_pagerank
+
+    case = load_golden("c1.json")
+    from conftest import regen_window
+
+    _, adf = regen_window(case)
+    tnames = sorted(adf["traceID"].unique())
+    oo, ot, to, pt = golden_graph_dicts(case["graph_swapped_anomaly"], tnames)
+    ref = trace_pagerank(oo, ot, to, pt, True)
+    monkeypatch.setenv("MR_KIND_TEST_COLLIDE", "1")
+    got = trace_pagerank(oo, ot, to, pt, True)
+    assert list(got[0]) == list(ref[0]) and got[1] == ref[1]
+    assert [float(x) for x in got[0].values()] == [float(x) for x in ref[0].values()]
+    _check(got, case["pr_anomaly"], RTOL64)

@@ -14,7 +14,7 @@ import pytest
 from conftest import GOLDEN, load_golden, regen_window, unhex
 
 pytestmark = pytest.mark.gpu
-SPAN_CASES = ["c1", "pods_dup_broken", "ops200"]
+SPAN_CASES = ["c1", "pods_dup_broken", "ops200", "span_times"]
 
 
 def _spectrum_inputs(case):
@@ -159,7 +159,7 @@ def test_empty_window_returns_false_and_driver_raises():
         online_anomaly_detect_RCA(long, {}, [])
 
 
-@pytest.mark.parametrize("name", ["c1", "pods_dup_broken"])
+@pytest.mark.parametrize("name", ["c1", "pods_dup_broken", "span_times"])
 def test_driver_matches_reference(name, tmp_path, monkeypatch):
     from microrank_amd.online_rca import online_anomaly_detect_RCA
 
@@ -192,7 +192,7 @@ def test_driver_matches_reference(name, tmp_path, monkeypatch):
             assert math.isclose(float(gp[-1]), float(xp[-1]), rel_tol=1e-10)
 
 
-@pytest.mark.parametrize("name", ["c1", "pods_dup_broken", "ops200"])
+@pytest.mark.parametrize("name", ["c1", "pods_dup_broken", "ops200", "span_times"])
 def test_rca_window_device_pipeline(name):
     """mr_rca_window (all intermediates in HBM) ranks like the reference driver's window."""
     from microrank_amd.online_rca import rca_window

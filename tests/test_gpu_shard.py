@@ -38,9 +38,9 @@ def _whole(anomaly):
     return w, cov
 
 
-def _worker(rank, world, port, anomaly, backend, q, big=None, tile=False, walk_ranks=()):
+def _worker(rank, world, port, anomaly, backend, q, big=None, tile=False, walk_ranks=(), empty_last=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    if tile:
+    if tile is True or (tile and rank in tile):   # True: every rank; a tuple: those ranks
         os.environ["MR_NO_FUSED"] = "1"   # read once, at this process's first graph prepare
     if rank in walk_ranks:
         os.environ["MR_KIND_WALK"] = "1"   # kinds hashed by the per-thread int32 walk (read once)
@@ -56,7 +56,9 @@ def _worker(rank, world, port, anomaly, backend, q, big=None, tile=False, walk_r
         else:
             shard.use_rccl(ctx)
         if big is None:
-            hg = host_graph_from_oracle(_shard(_window_graph(), rank, world))
+            g = _window_graph()
+            bounds = [0] + [g.T] * world if empty_last else None   # rank 0 all traces, the rest none
+            hg = host_graph_from_oracle(_shard(g, rank, world, bounds))
         else:
             from microrank_amd import synth
             hg = synth.big_graph(big[0], big[1], seed=3, shard=(rank, world))
@@ -72,11 +74,12 @@ def _worker(rank, world, port, anomaly, backend, q, big=None, tile=False, walk_r
         dist.destroy_process_group()
 
 
-def _run(world, anomaly, backend, big=None, tile=False, walk_ranks=()):
+def _run(world, anomaly, backend, big=None, tile=False, walk_ranks=(), empty_last=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, anomaly, backend, q, big, tile, walk_ranks))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, anomaly, backend, q, big, tile, walk_ranks,
+                                               empty_last))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -178,9 +181,11 @@ def test_kind_hash_forms_agree_across_ranks():
     assert res[0][1].tobytes() == res[1][1].tobytes(), "ranks disagree"
 
 
-def test_wide_op_space_int32_ids_shards():
+@pytest.mark.parametrize("precision", ["fp64", "fp32"])
+def test_wide_op_space_int32_ids_shards(precision):
     """N = 70000 > 65535: no u16 ids, so kinds take the int32 walk and the iteration the tile
-    path; 2 ranks x 10k traces vs the union graph on one GPU and vs the oracle."""
+    path (fp32: config C5's precision); 2 ranks x 10k traces vs the union graph on one GPU and vs
+    the oracle (fp64 restatement: 1e-10; the fp32 vectors: 1e-4, BASELINE north star)."""
     from microrank_amd import _lib
     from microrank_amd.graph import DeviceGraph
     from test_gpu_pagerank import _oracle_graph_from_host
@@ -190,7 +195,7 @@ def test_wide_op_space_int32_ids_shards():
     hg = _union_of_shards(n_ops, n_tr, 2)
     ctx = _lib.Context(0)
     dg = DeviceGraph.upload(ctx, hg)
-    dg.pagerank(True)
+    dg.pagerank(True, precision=precision)
     w_ref, cov_ref = dg.fetch()
     dg.close()
     ctx.close()
@@ -198,9 +203,35 @@ def test_wide_op_space_int32_ids_shards():
     kind = orc.trace_kinds(g)
     s = orc.power_iteration(g, orc.preference(g, kind, True))
     w_o, cov_o = orc.weights(g, s)
-    np.testing.assert_allclose(w_ref, np.array(list(w_o.values())), rtol=1e-10, atol=0)
+    tol = 1e-10 if precision == "fp64" else 1e-4
+    np.testing.assert_allclose(w_ref, np.array(list(w_o.values())), rtol=tol, atol=0)
     np.testing.assert_array_equal(cov_ref, np.array(list(cov_o.values())))
-    res = _run(2, True, "host", big=(n_ops, n_tr, "fp64"))
+    res = _run(2, True, "host", big=(n_ops, n_tr, precision))
+    for rank, w, cov, info in res:
+        np.testing.assert_allclose(w, w_ref, rtol=1e-10 if precision == "fp64" else 1e-5, atol=0)
+        np.testing.assert_array_equal(cov, cov_ref)
+    assert res[0][1].tobytes() == res[1][1].tobytes(), "ranks disagree"
+
+
+@pytest.mark.parametrize("tile", [False, True])
+def test_empty_shard_joins_every_collective(tile):
+    """Rank 1 holds no trace: it must still run every per-graph and per-iteration collective (a
+    rank that returned early would leave rank 0 blocked), and both end with the whole graph's
+    weights -- on the fused path and on the tile path."""
+    w_ref, cov_ref = _whole(True)
+    res = _run(2, True, "host", tile=tile, empty_last=True)
+    for rank, w, cov, info in res:
+        np.testing.assert_allclose(w, w_ref, rtol=1e-10, atol=0)
+        np.testing.assert_array_equal(cov, cov_ref)
+    assert res[1][3]["T"] == 0
+    assert res[0][1].tobytes() == res[1][1].tobytes(), "ranks disagree"
+
+
+def test_ranks_agree_on_the_iteration_path():
+    """Rank 1 alone is forced onto the tile path: rank 0 must follow it (one collective protocol
+    per iteration), and the result still equals the whole graph's."""
+    w_ref, cov_ref = _whole(True)
+    res = _run(2, True, "host", tile=(1,))
     for rank, w, cov, info in res:
         np.testing.assert_allclose(w, w_ref, rtol=1e-10, atol=0)
         np.testing.assert_array_equal(cov, cov_ref)

@@ -16,7 +16,7 @@ import oracle as orc
 from conftest import load_golden, regen_window, unhex
 from microrank_amd.spans import SpanTable
 
-SPAN_CASES = ["c1", "pods_dup_broken", "ops200"]
+SPAN_CASES = ["c1", "pods_dup_broken", "ops200", "span_times"]
 
 
 def check_pr(got, exp, rtol=1e-12):
