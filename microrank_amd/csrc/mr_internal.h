@@ -122,6 +122,12 @@ struct mr_graph {
     DBuf<int32_t> srt_ops;
     // trace-major P_rs node ids as u16 when N <= 65536 (the r' pass reads half the bytes)
     DBuf<uint16_t> rs16;
+    // fused iteration with N too large for su in LDS beside the accumulators: ops relabelled by
+    // descending coverage (perm[new] = old), the kernel's id stream rsp in the new labels, and
+    // su of the n_hot most covered ops staged in LDS (the rest gathered from HBM/L2)
+    DBuf<int32_t> perm;
+    DBuf<uint16_t> rsp;
+    bool relabeled = false;
     // P_sr in compressed sparse blocks for the s' pass: traces cut in tiles of 2^tshift; within a
     // tile the distinct (op, trace) entries sorted by (op, trace) as u16 tile-local trace
     // indices; a "pair" is the run of one op inside one tile.

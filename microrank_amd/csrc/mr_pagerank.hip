@@ -162,6 +162,24 @@ __global__ void __launch_bounds__(256) k_cov_hist(const uint16_t* ids, int64_t n
         if (hcnt[o]) atomicAdd(&cov[o], hcnt[o]);
 }
 
+// ---------------------------------------------------------------- op relabelling (fused, large N)
+// ops by descending coverage (ties by op): key = ~cov << 14 | op (N <= 16384)
+__global__ void k_relabel_keys(const int32_t* cov, int32_t N, uint64_t* key) {
+    const int32_t o = blockIdx.x * blockDim.x + threadIdx.x;
+    if (o < N) key[o] = ((uint64_t)(~(uint32_t)cov[o]) << 14) | (uint32_t)o;
+}
+__global__ void k_relabel_perm(const uint64_t* key, int32_t N, int32_t* perm, int32_t* inv) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    const int32_t o = (int32_t)(key[i] & 0x3fffu);
+    perm[i] = o;
+    inv[o] = i;
+}
+__global__ void k_relabel_ids(const uint16_t* ids, int64_t n, const int32_t* inv, uint16_t* out) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < n) out[e] = (uint16_t)inv[ids[e]];
+}
+
 // ---------------------------------------------------------------- kinds (pagerank.py:54-66)
 // kind[t] = size of the class of traces with an equal P_sr column: key = (op set, fp32(1/len_t)).
 // Open-addressing hash table of 64-bit keys; a second pass verifies every member against the
@@ -413,13 +431,15 @@ __device__ __forceinline__ unsigned long long d2bits(double v) {
 }
 
 // T_all: traces of the whole graph (all shards) for the initial value
+// perm (relabelled fused graphs): su is kept in the kernel's op labels, su[new] = u_o[perm[new]] s
 __global__ void k_iter_init(const float* w_t, const float* u_o, int32_t N, int32_t T, int64_t T_all, double* sp0,
-                            double* su0, double* su1, double* q64, float* q32, int fp32, unsigned long long* mslot) {
+                            double* su0, double* su1, double* q64, float* q32, int fp32, unsigned long long* mslot,
+                            const int32_t* perm) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const double v0 = 1.0 / (double)((int64_t)N + T_all);      // pagerank.py:118-119
     if (i < N) {
         sp0[i] = v0;
-        su0[i] = (double)u_o[i] * v0;
+        su0[i] = (double)u_o[perm ? perm[i] : i] * v0;
     }
     if (i == N) su0[N] = su1[N] = 0.0;   // the fused walk's pad slot
     if (i < T) {
@@ -437,6 +457,9 @@ struct GDev {
     const int64_t* rs_off;
     const int32_t* rs_ops;
     const uint16_t* rs16;       // u16 copy of rs_ops (N <= 65536) or null
+    const uint16_t* rsw;        // the fused kernel's ids: rs16, or rsp in relabelled ops
+    const int32_t* perm;        // relabelled ops: perm[new] = old (null: identity)
+    int32_t n_hot;              // k_wv_a: su of ops [0, n_hot) in LDS (relabelled graphs)
     const float* c_t;
     const float* w_t;
     const float* u_o;
@@ -1073,6 +1096,330 @@ __global__ void __launch_bounds__(S * FX_TMAX, 4) k_fx_a(const GDev* __restrict_
     }
 }
 
+// ---------------------------------------------------------------- fused iteration, wave-autonomous (k_wv_a)
+// The single-pass iteration of k_fx_a (same sums in the same order: bitwise the same results)
+// with no block barrier inside the trace loop.  Every wave streams its own WAVE TILES of 64
+// consecutive traces:
+//   * lane i owns trace i of the wave tile (X_t, the combine, the q store) AND the contiguous
+//     position segment [i*L, i*L + L) of the tile's 16-B aligned id range (L = 8 or 16: wave
+//     tiles of up to 1024 positions; larger ones take the thread-per-trace path);
+//   * the segment's ids come straight into registers (two 16-B chunks), the tile's offsets two
+//     tiles ahead and its ids / per-trace words one tile ahead, so 16 independent waves per CU
+//     keep their loads in flight while others walk;
+//   * trace starts, segment owners, X values and the walk's pieces live in a per-wave LDS
+//     scratch: written and read by the same wave, so in order with no barrier;
+//   * the block's waves share the per-op accumulator (LDS u64 atomics: integers, order-free)
+//     and su (LDS when it fits beside the accumulator; otherwise gathered from its global copy
+//     right after the tile's ids arrive, before the bitmap staging).
+// The block synchronises only to clear the accumulator and to write its partial row.
+constexpr int WV_POS = 1024;                 // positions of a wave tile's fast path (64 x 16)
+struct WvScratch {                           // per-wave LDS scratch (byte offsets)
+    static constexpr size_t hb = 0;          // 34 words: trace starts of 1024 positions (+2 read-ahead)
+    static constexpr size_t owner = 144;     // int32[64]: trace (in the tile) of a segment's first position
+    static constexpr size_t xl = 400;        // u64[66]: xl[c + 1] = X of trace c, xl[0] = 0
+    static constexpr size_t tsum = 928;      // double[64]
+    static constexpr size_t head = 1440;     // double[64]
+    static constexpr size_t tail = 1952;     // double[64]
+    static constexpr size_t bytes = 2464;    // (the long path's staged ids, u16[1024], alias it)
+};
+constexpr size_t WV_LDS_MAX = 160 * 1024 - 512;
+// su modes of k_wv_a: global gathers only / every op's su in LDS (interleaved with the
+// accumulator: one address for the gather and the atomic) / the n_hot most covered ops' su in
+// LDS (relabelled graphs, ops [0, n_hot)), the rest gathered
+enum { WV_SU_GLOBAL = 0, WV_SU_ALL = 1, WV_SU_HOT = 2 };
+struct WvLds {
+    size_t su, lacc, wave, total;
+    bool su_lds;       // every op's su fits beside the accumulator
+    int32_t n_hot;     // WV_SU_HOT: ops whose su fits
+    __host__ __device__ WvLds(int32_t N, int32_t NT, int mode = WV_SU_ALL) {
+        const size_t scratch = (size_t)(NT / WAVE) * WvScratch::bytes;
+        su_lds = ((size_t)N + 1) * 16 + scratch <= WV_LDS_MAX;
+        const bool all = mode == WV_SU_ALL && su_lds;
+        const size_t accb = ((size_t)N + 1) * (all ? 16 : 8);
+        n_hot = 0;
+        if (mode == WV_SU_HOT) {
+            const size_t room = WV_LDS_MAX - scratch - (accb + 15) / 16 * 16;
+            n_hot = (int32_t)std::min<size_t>((size_t)N, room / 8 / 64 * 64);
+        }
+        lacc = all ? 8 : 0;
+        su = all ? 0 : (accb + 15) / 16 * 16;   // WV_SU_HOT: su_hot[n_hot] after the accumulator
+        wave = su + (mode == WV_SU_HOT ? ((size_t)n_hot * 8 + 15) / 16 * 16 : all ? 0 : 0);
+        if (all) wave = (accb + 15) / 16 * 16;
+        total = wave + scratch;
+    }
+};
+
+template <class Q, int SUM, int NT>
+__global__ void __launch_bounds__(NT) k_wv_a(const GDev* __restrict__ gs, int32_t ng, int32_t split, double d,
+                                             double alpha, int it, int32_t unused) {
+    constexpr bool SUL = SUM == WV_SU_ALL, HOT = SUM == WV_SU_HOT;
+    constexpr int NW = NT / WAVE;
+    extern __shared__ __attribute__((aligned(16))) unsigned char lraw[];
+    __shared__ double red[NW];
+    __shared__ double msh[2];
+    const GDev& G = gs[fx_graph(gs, ng, split, 2)];
+    const int32_t lb = (int32_t)blockIdx.x - G.blk0f;
+    const int cur = it & 1, nxt = cur ^ 1, k3 = it % 3;
+    const int32_t T = G.T, N = G.N;
+    const int32_t tid = (int32_t)threadIdx.x, lane = tid & (WAVE - 1), wv = tid / WAVE;
+    const WvLds L_(N, NT, SUM);
+    const int32_t NH = HOT ? G.n_hot : 0;   // <= L_.n_hot (the host sizes both alike)
+    const GLB int32_t* rs_off = gp((const int32_t*)G.rs_off);   // low words (offsets < 2^31)
+    const GLB u32x4* rs16 = gp((const u32x4*)G.rsw);           // 8 ids per 16 B; padded past nnz
+    const GLB uint16_t* rs16s = gp(G.rsw);
+    const GLB Q* qc = gp((const Q*)G.q[cur]);
+    GLB Q* qn = gpw((Q*)G.q[nxt]);
+    const GLB float* c_t = gp(G.c_t);
+    const GLB float* w_t = gp(G.w_t);
+    const GLB double* sug = gp(G.sub[cur]);   // N + 1 entries, sub[N] = 0 (the pad slot)
+    constexpr int AS = SUL ? 2 : 1;
+    double* su_l = (double*)(lraw + L_.su);
+    unsigned long long* lacc = (unsigned long long*)(lraw + L_.lacc);
+    unsigned char* ws = lraw + L_.wave + (size_t)wv * WvScratch::bytes;
+    uint32_t* hb = (uint32_t*)(ws + WvScratch::hb);
+    int32_t* owner = (int32_t*)(ws + WvScratch::owner);
+    unsigned long long* xl = (unsigned long long*)(ws + WvScratch::xl);
+    double* tsum = (double*)(ws + WvScratch::tsum);
+    double* head = (double*)(ws + WvScratch::head);
+    double* tail = (double*)(ws + WvScratch::tail);
+    uint16_t* lids = (uint16_t*)ws;
+    GLB unsigned long long* mslot = gpw(G.mslot);
+    const GLB unsigned long long* Mcur = mslot + (size_t)2 * MSH * k3;
+    GLB unsigned long long* Mnext = mslot + (size_t)2 * MSH * ((k3 + 1) % 3);
+    if (lb == 0 && tid < 2 * MSH) mslot[(size_t)2 * MSH * ((k3 + 2) % 3) + tid] = 0ull;
+    for (int32_t o = tid; o <= N; o += NT) {
+        if (SUL) su_l[AS * o] = sug[o];
+        lacc[AS * o] = 0ull;
+    }
+    if (HOT)
+        for (int32_t o = tid; o < NH; o += NT) su_l[o] = sug[o];
+    if (tid < WAVE) {
+        const double ms = wave_max(bits2d(Mcur[tid]));
+        const double mr = wave_max(bits2d(Mcur[MSH + tid]));
+        if (tid == 0) {
+            msh[0] = ms;
+            msh[1] = mr;
+        }
+    }
+    __syncthreads();   // accumulator and maxima ready
+    const double xsc = G.fx_scale / msh[1], Ms = msh[0];
+    // this block's wave tiles [kb, ke); wave wv takes kb + wv, kb + wv + NW, ...
+    const int32_t W = (T + WAVE - 1) / WAVE;
+    const int32_t kb = (int32_t)((int64_t)lb * W / G.n_fa), ke = (int32_t)((int64_t)(lb + 1) * W / G.n_fa);
+    // per-lane trace of wave tile k (clamped into the graph: lanes past T repeat the last trace)
+    auto tr_of = [&](int32_t k) { return min(k * WAVE + lane, T - 1); };
+    // pipeline: offsets two tiles ahead, ids + per-trace words one tile ahead; every global load
+    // in the loop is unconditional (clamped), so each use waits for exactly its own load
+    int32_t k = kb + wv;
+    const int32_t kl = max(ke - 1, kb);   // clamp target of the look-ahead
+    int32_t a0 = 0, b0 = 0, a1 = 0, b1 = 0;   // offsets of tiles k and k + NW
+    double qk = 0.0;
+    float ct = 0.0f, wt = 0.0f;
+    u32x4 v0 = {0u, 0u, 0u, 0u}, v1 = v0;
+    if (k < ke) {   // (a wave without tiles -- e.g. an empty shard -- loads nothing)
+        const int32_t t = tr_of(min(k, kl));
+        a0 = rs_off[2 * t];
+        b0 = rs_off[2 * t + 2];
+        const int32_t t1 = tr_of(min(k + NW, kl));
+        a1 = rs_off[2 * t1];
+        b1 = rs_off[2 * t1 + 2];
+    // words + ids of the tile whose offsets are (a_, b_)
+#define WV_LOAD(kk_, a_, b_, qk_, ct_, wt_, v0_, v1_)                                               \
+    do {                                                                                            \
+        const int32_t t_ = tr_of(min((kk_), kl));                                                   \
+        qk_ = (double)qc[t_];                                                                       \
+        ct_ = c_t[t_];                                                                              \
+        wt_ = w_t[t_];                                                                              \
+        const int32_t e0_ = __builtin_amdgcn_readfirstlane(a_);                                     \
+        const int32_t e1_ = __builtin_amdgcn_readlane(b_, WAVE - 1);                                \
+        const int32_t base_ = e0_ & ~7, np_ = e1_ - base_;                                          \
+        const int32_t nch_ = (np_ + 7) >> 3, cpl_ = np_ <= 8 * WAVE ? 1 : 2;                        \
+        const GLB u32x4* src_ = rs16 + (base_ >> 3);                                                \
+        v0_ = src_[min(lane * cpl_, nch_ - 1)];                                                     \
+        v1_ = src_[min(lane * cpl_ + 1, nch_ - 1)];                                                 \
+    } while (0)
+        WV_LOAD(k, a0, b0, qk, ct, wt, v0, v1);
+    }
+    double rmax = -__builtin_huge_val();
+    for (; k < ke; k += NW) {
+        // ---- this tile's state (loaded one tile ago)
+        const int32_t t = k * WAVE + lane;
+        const bool own = t < T;
+        const int32_t a = a0, b = b0;
+        const int32_t e0 = __builtin_amdgcn_readfirstlane(a), e1 = __builtin_amdgcn_readlane(b, WAVE - 1);
+        const double q_k = qk;
+        const float c_k = ct, w_k = wt;
+        u32x4 c0 = v0, c1 = v1;
+        const int32_t base = e0 & ~7, shift = e0 - base, np_ = e1 - base;
+        const int lgL = np_ <= 8 * WAVE ? 3 : np_ <= WV_POS ? 4 : 0;   // 0: long tile
+        const int32_t L = 1 << lgL, p = lane * L, cpl = L >> 3;
+        const int32_t qe = lgL ? min(p + L, np_) : 0;
+        const int32_t ra = a - base, rb = b - base;
+        const unsigned long long X = own ? (unsigned long long)__double2ull_rn(q_k * xsc) : 0ull;
+        c0 = fx_pad(c0, lane * cpl, shift, np_, N);
+        c1 = fx_pad(c1, lane * cpl + 1, shift, np_, N);
+        // !SUL: the segment's su values from the global copy, in flight during the staging; HOT:
+        // only the cold ops' -- a hot entry loads the pad slot sug[N] instead (every hot lane the
+        // same line: no L2 traffic, and the load stays unconditional for exact vmcnt waits)
+        double gv0[8], gv1[8];
+        if (!SUL && !(MR_EXP & 2)) {
+            const uint32_t w0[4] = {c0.x, c0.y, c0.z, c0.w}, w1[4] = {c1.x, c1.y, c1.z, c1.w};
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int32_t o = (int32_t)((w0[j >> 1] >> ((j & 1) * 16)) & 0xffffu);
+                gv0[j] = sug[HOT && o < NH ? N : o];
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int32_t o = (int32_t)((w1[j >> 1] >> ((j & 1) * 16)) & 0xffffu);
+                gv1[j] = sug[HOT && o < NH ? N : o];
+            }
+        }
+        // ---- look-ahead: tile k + NW's words and ids, tile k + 2NW's offsets -- issued AFTER
+        // the gathers (compiler barrier): loads complete in issue order (one vmcnt), so the walk
+        // then waits for its L2 gathers only, not for these HBM loads
+        asm volatile("" ::: "memory");
+        WV_LOAD(k + NW, a1, b1, qk, ct, wt, v0, v1);
+        a0 = a1;
+        b0 = b1;
+        {
+            const int32_t t2 = tr_of(min(k + 2 * NW, kl));
+            a1 = rs_off[2 * t2];
+            b1 = rs_off[2 * t2 + 2];
+        }
+        double acc = 0.0;
+        if (lgL) {
+            // ---- staging (per-wave scratch): trace starts, segment owners, X
+            if (lane < 34) hb[lane] = 0u;
+            owner[lane] = -1;
+            __builtin_amdgcn_wave_barrier();
+            if (own) {
+                xl[lane + 1] = X;
+                atomicOr(&hb[ra >> 5], 1u << (ra & 31));
+                for (int32_t sg = (ra + L - 1) >> lgL; (sg << lgL) < rb; ++sg) owner[sg] = lane;
+            }
+            if (lane == 0) xl[0] = 0ull;
+            __builtin_amdgcn_wave_barrier();
+            // ---- walk
+            if (p < qe) {
+                const unsigned long long bits =
+                    (((unsigned long long)hb[(p >> 5) + 1] << 32) | hb[p >> 5]) >> (p & 31);
+                int32_t c = owner[lane];
+                bool st = bits & 1ull;
+                const unsigned long long sb = bits & ~1ull;
+#pragma unroll
+                for (int kc = 0; kc < 2; ++kc) {
+                    if (kc >= cpl || p + 8 * kc >= qe) break;
+                    const u32x4 w = kc ? c1 : c0;
+                    const uint32_t m8 = (uint32_t)(sb >> (8 * kc)) & 0xffu;
+                    int32_t o[8];
+                    o[0] = (int32_t)(w.x & 0xffffu); o[1] = (int32_t)(w.x >> 16);
+                    o[2] = (int32_t)(w.y & 0xffffu); o[3] = (int32_t)(w.y >> 16);
+                    o[4] = (int32_t)(w.z & 0xffffu); o[5] = (int32_t)(w.z >> 16);
+                    o[6] = (int32_t)(w.w & 0xffffu); o[7] = (int32_t)(w.w >> 16);
+                    double g[8];
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const double gg = kc ? gv1[j] : gv0[j];
+                        g[j] = (MR_EXP & 2) ? (double)o[j]
+                               : SUL      ? su_l[AS * o[j]]
+                               : HOT      ? (o[j] < NH ? su_l[min(o[j], NH - 1)] : gg)
+                                          : gg;
+                    }
+                    unsigned long long xj[8];
+#pragma unroll
+                    for (int j = 0; j < 8; ++j)
+                        xj[j] = (MR_EXP & 4) ? X : xl[c + 1 + (int32_t)__builtin_popcount(m8 & ((2u << j) - 1u))];
+                    if (!(MR_EXP & 1)) {
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) atomicAdd(&lacc[AS * o[j]], xj[j]);
+                    }
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        if (m8 & (1u << j)) {   // a new trace starts at p + 8 kc + j
+                            if (st) tsum[c] = acc; else head[lane] = acc;
+                            acc = 0.0;
+                            st = true;
+                            ++c;
+                        }
+                        acc += g[j];
+                    }
+                }
+                const bool ends = qe == np_ || ((bits >> (qe - p)) & 1ull);
+                if (st) {
+                    if (ends) tsum[c] = acc; else tail[lane] = acc;
+                } else {
+                    head[lane] = acc;
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            // ---- combine: trace = its pieces in segment order
+            if (own && rb > ra) {
+                const int32_t sa = ra >> lgL, sbg = (rb - 1) >> lgL;
+                if (sa == sbg) {
+                    acc = tsum[lane];
+                } else {
+                    acc = tail[sa];
+                    for (int32_t sg = sa + 1; sg <= sbg; ++sg) acc += head[sg];
+                }
+            } else {
+                acc = 0.0;
+            }
+            __builtin_amdgcn_wave_barrier();   // the scratch is rewritten by the next tile
+        } else {
+            // ---- long wave tile (rare): thread per trace in rounds of 1024 staged ids
+            for (int32_t lo = e0; lo < e1; lo += WV_POS) {
+                const int32_t hi = min(lo + WV_POS, e1);
+                __builtin_amdgcn_wave_barrier();
+                for (int32_t e = lo + lane; e < hi; e += WAVE) lids[e - lo] = rs16s[e];
+                __builtin_amdgcn_wave_barrier();
+                const int32_t x0 = max(a, lo) - lo, x1 = min(b, hi) - lo;
+                for (int32_t cc = x0; cc < x1; cc += 8) {
+                    int32_t o[8];
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) o[j] = cc + j < x1 ? (int32_t)lids[cc + j] : N;
+                    double g[8];
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) g[j] = SUL ? su_l[AS * o[j]] : (HOT && o[j] < NH) ? su_l[o[j]] : sug[o[j]];
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) acc += g[j];
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) atomicAdd(&lacc[AS * o[(j + lane) & 7]], X);
+                }
+            }
+            if (!own) acc = 0.0;
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this rare path's loads: none pending at the merge
+        }
+        const double rp = d * (acc / Ms) + (double)c_k;   // pagerank.py:125
+        if (own) rmax = nmax(rmax, rp);
+        qn[own ? t : T] = (Q)((double)w_k * rp);          // q[T]: pad slot
+    }
+#undef WV_LOAD
+    // call-graph term for the next s' (pagerank.py:122-124, alpha P_ss s_k), a thread per op
+    {
+        const GLB double* sp_cur = gp(G.spb[cur]);
+        const GLB int64_t* ss_off = gp(G.ss_off);
+        const GLB int32_t* ss_par = gp(G.ss_par);
+        const GLB float* pw = gp(G.pw);
+        GLB double* ssv = gpw(G.fx_ssv);
+        for (int32_t oss = lb * NT + tid; oss < N; oss += G.n_fa * NT) {
+            double bb = 0.0;
+            for (int64_t e = ss_off[oss]; e < ss_off[oss + 1]; ++e) {
+                const int32_t pp = ss_par[e];
+                bb += (double)pw[pp] * sp_cur[pp];
+            }
+            ssv[oss] = alpha * (bb / Ms);
+        }
+    }
+    __syncthreads();
+    GLB unsigned long long* prow = gpw(G.fx_part) + (size_t)lb * N;
+    for (int32_t o = tid; o < N; o += NT) prow[o] = lacc[AS * o];
+    rmax = block_max(rmax, red);
+    if (tid == 0 && rmax >= 0.0)   // -inf: a block without traces (an empty shard's placeholder)
+        atomicMax((unsigned long long*)&Mnext[MSH + blockIdx.x % MSH], d2bits(rmax));
+}
+
 // Column sums of the partial rows: a block per chunk of FB_OPS consecutive ops (lane = op, so
 // every row read is one coalesced 512-B segment), its FB_W waves splitting the rows; the waves'
 // limb sums meet in LDS (integers: order-free).  mode 0: whole graph; sharded graphs split it
@@ -1089,13 +1436,15 @@ __global__ void __launch_bounds__(WAVE * FB_W) k_fx_b(const GDev* __restrict__ g
     const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
     const int32_t OPB = G.fb_ops, GR = WAVE / OPB;
     const int32_t ol = lane % OPB, grp = lane / OPB;
+    // o: the column (the fused kernel's op label); op: the graph's op (perm: relabelled graphs)
     const int32_t o = ((int32_t)blockIdx.x - G.blk0fb) * OPB + ol;
     const int32_t N = G.N, nb = G.n_fa;
     const bool on = o < N;
     // the finishing lanes' operands, loaded before the rows so both latencies overlap
     const bool fin = w == 0 && lane < OPB && on;
-    const double ssv = fin ? G.fx_ssv[o] : 0.0;
-    const float uo = fin ? G.u_o[o] : 0.0f;
+    const int32_t op = fin && G.perm ? G.perm[o] : o;
+    const double ssv = fin ? G.fx_ssv[op] : 0.0;
+    const float uo = fin ? G.u_o[op] : 0.0f;
     unsigned long long lo = 0ull, hi = 0ull;
     if (on && mode != 2) {
         // batches of 16 rows per lane, every load in flight before the sums (indices clamped:
@@ -1126,7 +1475,6 @@ __global__ void __launch_bounds__(WAVE * FB_W) k_fx_b(const GDev* __restrict__ g
     }
     __syncthreads();
     if (!fin) return;
-    const int32_t op = o;
     lo = hi = 0ull;
     for (int k = 0; k < FB_W; ++k) {
         lo += slo[k * WAVE + lane];
@@ -1147,7 +1495,7 @@ __global__ void __launch_bounds__(WAVE * FB_W) k_fx_b(const GDev* __restrict__ g
     const double sum = ((double)hi * 4294967296.0 + (double)lo) * G.fx_iscale;
     const double v = d * (sum + ssv);      // pagerank.py:122-124
     G.spb[nxt][op] = v;
-    G.sub[nxt][op] = (double)uo * v;
+    G.sub[nxt][o] = (double)uo * v;   // su in the kernel's labels
     atomicMax(&Mnext[op % MSH], d2bits(v));
 }
 
@@ -1349,6 +1697,85 @@ static int64_t fx_blocks(int32_t T, int32_t N, int TT) {
     return std::min(nb, tiles);
 }
 
+// ---- k_wv_a (default fused kernel; MR_FX_V1 selects k_fx_a for A/B measurements)
+static bool fx_v1() {
+    static const bool v = getenv("MR_FX_V1") != nullptr;
+    return v;
+}
+using WvA = void (*)(const GDev*, int32_t, int32_t, double, double, int, int32_t);
+static WvA wv_kernel(bool fp32, int mode, int NT) {
+    static const WvA tab[2][3][2] = {
+        {{k_wv_a<double, 0, 512>, k_wv_a<double, 0, 1024>},
+         {k_wv_a<double, 1, 512>, k_wv_a<double, 1, 1024>},
+         {k_wv_a<double, 2, 512>, k_wv_a<double, 2, 1024>}},
+        {{k_wv_a<float, 0, 512>, k_wv_a<float, 0, 1024>},
+         {k_wv_a<float, 1, 512>, k_wv_a<float, 1, 1024>},
+         {k_wv_a<float, 2, 512>, k_wv_a<float, 2, 1024>}}};
+    return tab[fp32 ? 1 : 0][mode][NT == 1024 ? 1 : 0];
+}
+static int num_cus() {
+    static const int ncu = [] {
+        int dev = 0, v = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            v = 256;
+        return std::max(v, 1);
+    }();
+    return ncu;
+}
+
+// Launch plan of the fused iteration for a batch of graphs (one kernel variant per launch).
+struct FxPlan {
+    bool v2 = true;     // k_wv_a
+    int NT = 1024;      // block size (16 waves; 512 when the graphs are small)
+    int mode = WV_SU_ALL;   // su in LDS for every fused graph of the batch / hot ops / none
+    bool sul = true;    // mode == WV_SU_ALL
+};
+static FxPlan fx_plan(mr_graph* const* gs, int ng) {
+    FxPlan P;
+    P.v2 = !fx_v1();
+    if (!P.v2) return P;
+    int32_t nmax = 0;
+    int64_t tmax = 0;
+    for (int i = 0; i < ng; ++i)
+        if (gs[i]->fused) {
+            nmax = std::max(nmax, gs[i]->N);
+            tmax = std::max<int64_t>(tmax, gs[i]->T);
+        }
+    static const int force_nt = [] {
+        const char* e = getenv("MR_WV_NT");
+        return e ? atoi(e) : 0;
+    }();
+    // 1024-thread blocks when the largest graph has a wave tile for every wave of the chip
+    P.NT = force_nt == 512 || force_nt == 1024 ? force_nt : (cdiv(tmax, WAVE) >= (int64_t)num_cus() * 16 ? 1024 : 512);
+    bool relabeled = false;
+    for (int i = 0; i < ng; ++i) relabeled = relabeled || (gs[i]->fused && gs[i]->relabeled);
+    P.sul = WvLds(nmax, P.NT, WV_SU_ALL).su_lds;
+    P.mode = P.sul ? WV_SU_ALL : relabeled ? WV_SU_HOT : WV_SU_GLOBAL;
+    if (P.mode == WV_SU_HOT)   // every graph of the launch must be relabelled (hot ops = low labels)
+        for (int i = 0; i < ng; ++i)
+            if (gs[i]->fused && !gs[i]->relabeled) P.mode = WV_SU_GLOBAL;
+    return P;
+}
+
+// blocks of one graph: a resident block per CU (its waves stream the wave tiles), fewer when the
+// graph has fewer wave tiles than waves, more when a block would exceed 65535 traces (the
+// fixed-point scale 2^48 keeps a block's per-op sums below 2^64)
+static int64_t wv_blocks(int32_t T, int32_t N, const FxPlan& P) {
+    const int64_t W = cdiv((int64_t)T, WAVE), NW = P.NT / WAVE;
+    const WvLds L(N, P.NT, P.mode);
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, (const void*)wv_kernel(false, P.mode, P.NT), P.NT, L.total) !=
+            hipSuccess || n < 1)
+        n = std::max<int>(1, (int)(WV_LDS_MAX / L.total));
+    const int64_t resident = (int64_t)num_cus() * n;
+    int64_t nb = std::min<int64_t>(resident, cdiv(W, NW));
+    nb = std::max<int64_t>(nb, (int64_t)cdiv(W, 1023));   // <= 1023 wave tiles (65472 traces) per block
+    return std::max<int64_t>(std::min(nb, W), W ? 1 : 0);
+}
+static int64_t fused_blocks(int32_t T, int32_t N, const FxPlan& P, int TT_v1) {
+    return P.v2 ? wv_blocks(T, N, P) : fx_blocks(T, N, TT_v1);
+}
+
 // Derived per-graph arrays: fp32 reciprocals, u16 ids, and the P_sr tiles.  One host round trip
 // (the number of (tile, op) pairs sizes the pair arrays).
 int mr_graph_prepare(mr_ctx* ctx, mr_graph* g) {
@@ -1366,6 +1793,7 @@ int mr_graph_prepare(mr_ctx* ctx, mr_graph* g) {
         MR_TRY(g->rs16.alloc(ctx, (size_t)g->nnz_rs + 8));
         hipLaunchKernelGGL(k_ids16, dim3(cdiv(g->nnz_rs, 256)), dim3(256), 0, st, g->rs_ops.p, g->nnz_rs, g->rs16.p);
     }
+    g->relabeled = false;   // (set below for fused graphs that need it)
     static const bool no_fused = getenv("MR_NO_FUSED") != nullptr;   // A/B knob: force the tile path
     g->fused = !no_fused && !g->force_tile && g->rs_is_sr && g->traces_nonempty && N <= FX_NMAX && fx_tt(N) > 0;
     if (g->fused) {   // no P_sr tiles: the fused iteration reads the trace-major ids only
@@ -1373,6 +1801,27 @@ int mr_graph_prepare(mr_ctx* ctx, mr_graph* g) {
         if (nnz && N)
             hipLaunchKernelGGL(k_cov_hist, dim3(cdiv(nnz, 256 * 64)), dim3(256), (size_t)N * sizeof(int32_t), st,
                                g->rs16.p, nnz, N, g->cov.p);
+        // su does not fit in LDS beside the accumulators: relabel ops by descending coverage so
+        // k_wv_a stages the su of the most covered ops (ops [0, n_hot)) and gathers the rest.
+        // The kinds keep rs16 (original labels, the same hash on every rank); only the
+        // iteration's id stream (rsp), su and the partial rows use the new labels.
+        g->relabeled = !fx_v1() && !WvLds(N, 1024, WV_SU_ALL).su_lds;
+        if (g->relabeled) {
+            DBuf<uint64_t> key;
+            DBuf<int32_t> inv;
+            MR_TRY(key.alloc(ctx, (size_t)N));
+            MR_TRY(inv.alloc(ctx, (size_t)N));
+            MR_TRY(g->perm.alloc(ctx, (size_t)N));
+            MR_TRY(g->rsp.alloc(ctx, (size_t)nnz + 8));
+            hipLaunchKernelGGL(k_relabel_keys, dim3(cdiv(N, 256)), dim3(256), 0, st, g->cov.p, N, key.p);
+            SortScratch ws;
+            MR_TRY(mr_radix_sort(ctx, key.p, nullptr, N, 46, ws));
+            hipLaunchKernelGGL(k_relabel_perm, dim3(cdiv(N, 256)), dim3(256), 0, st, key.p, N, g->perm.p, inv.p);
+            if (nnz) hipLaunchKernelGGL(k_relabel_ids, dim3(cdiv(nnz, 256)), dim3(256), 0, st, g->rs16.p, nnz, inv.p, g->rsp.p);
+        } else {
+            g->perm.reset();
+            g->rsp.reset();
+        }
         g->n_tiles = 0;
         g->n_pairs = 0;
         MR_TRY_HIP(ctx, hipGetLastError());
@@ -1465,7 +1914,7 @@ int mr_graph_prepare(mr_ctx* ctx, mr_graph* g) {
 static int shard_kinds(mr_ctx* ctx, mr_graph* g, uint64_t cap);
 
 static int pagerank_setup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool fp32, uint32_t flags, int TT,
-                          bool sharded, uint64_t seed, uint64_t hmask) {
+                          const FxPlan& plan, bool sharded, uint64_t seed, uint64_t hmask) {
     hipStream_t st = ctx->stream;
     const int32_t N = g->N, T = g->T;
     uint64_t cap = 1;
@@ -1489,7 +1938,7 @@ static int pagerank_setup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool 
     MR_TRY(g->sub[1].alloc(ctx, (size_t)N + 1));
     MR_TRY(g->weight.alloc(ctx, (size_t)N));
     if (g->fused) {
-        MR_TRY(g->fx_part.alloc(ctx, (size_t)std::max<int64_t>(fx_blocks(T, N, TT), 1) * (size_t)N));
+        MR_TRY(g->fx_part.alloc(ctx, (size_t)std::max<int64_t>(fused_blocks(T, N, plan, TT), 1) * (size_t)N));
         MR_TRY(g->fx_ssv.alloc(ctx, (size_t)N));
     }
     else MR_TRY(g->part.alloc(ctx, (size_t)std::max<int64_t>(g->n_pairs, 1)));
@@ -1545,7 +1994,8 @@ static int pagerank_setup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool 
     MR_DEBUG_CHECK(ctx, "k_pref_apply");
     hipLaunchKernelGGL(k_iter_init, dim3(cdiv(std::max<int64_t>({(int64_t)N + 1, T, 6 * MSH}), 256)), dim3(256), 0, st,
                        g->w_t.p, g->u_o.p, N, T, g->T_all > 0 ? g->T_all : (int64_t)T, g->spb[0].p, g->sub[0].p,
-                       g->sub[1].p, g->q64[0].p, g->q32[0].p, (int)fp32, g->mslot.p);
+                       g->sub[1].p, g->q64[0].p, g->q32[0].p, (int)fp32, g->mslot.p,
+                       g->relabeled ? (const int32_t*)g->perm.p : nullptr);
     MR_DEBUG_CHECK(ctx, "k_iter_init");
     return MR_OK;
 }
@@ -1580,7 +2030,9 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
     int TT = FX_TMAX;   // one block size for the batch: the largest that fits every fused graph
     for (int i = 0; i < ng; ++i)
         if (gs[i]->fused) TT = std::min(TT, fx_tt(gs[i]->N));
-    for (int i = 0; i < ng; ++i) MR_TRY(pagerank_setup(ctx, gs[i], anomaly[i], d, fp32, flags, TT, sharded, seed, hmask));
+    const FxPlan plan = fx_plan(gs, ng);
+    if (plan.v2) TT = WAVE;   // wave tiles
+    for (int i = 0; i < ng; ++i) MR_TRY(pagerank_setup(ctx, gs[i], anomaly[i], d, fp32, flags, TT, plan, sharded, seed, hmask));
     // ---- batched power iteration: one k_iter_a + k_iter_b pair per iteration for every graph
     int mask = 3;
     if (const char* rm = getenv("MR_ROLE_MASK")) mask = atoi(rm);   // profiling knob: 1 trace / 2 op side
@@ -1596,6 +2048,9 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         v.rs_off = g->rs_off.p;
         v.rs_ops = g->rs_ops.p;
         v.rs16 = g->rs16.p;
+        v.rsw = g->relabeled ? g->rsp.p : g->rs16.p;
+        v.perm = g->relabeled ? g->perm.p : nullptr;
+        v.n_hot = plan.v2 && plan.mode == WV_SU_HOT ? WvLds(g->N, plan.NT, WV_SU_HOT).n_hot : 0;
         v.c_t = g->c_t.p;
         v.w_t = g->w_t.p;
         v.u_o = g->u_o.p;
@@ -1623,10 +2078,16 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         v.stamp = nullptr;
         // a shard without traces still runs one (empty) block: it clears the maxima slot and
         // writes a zero partial row, and the collectives after the launch need every rank
-        const int64_t nfa = g->fused ? std::max<int64_t>(fx_blocks(g->T, g->N, TT), sharded ? 1 : 0) : 0;
+        const int64_t nfa = g->fused ? std::max<int64_t>(fused_blocks(g->T, g->N, plan, TT), sharded ? 1 : 0) : 0;
         // a row entry stays below 2^63; shards of one graph hold different trace counts, and their
         // limbs are summed, so they share the scale of the largest block (2^15 traces)
-        const int sc = 63 - (sharded ? 15 : bits_for((uint64_t)std::max<int64_t>(cdiv(cdiv((int64_t)g->T, TT), std::max<int64_t>(nfa, 1)) * TT - 1, 1)));
+        // v1: a row entry stays below 2^63; v2: below 2^64 (traces per block < 2^(64-sc)).
+        // Shards of one graph hold different trace counts and their limbs are summed, so they
+        // share one scale, 2^48 (<= 65535 traces per block: wv_blocks / fx_blocks)
+        const int64_t tpb = cdiv(cdiv((int64_t)g->T, TT), std::max<int64_t>(nfa, 1)) * TT;
+        const int sc = sharded ? 48
+                               : plan.v2 ? 64 - bits_for((uint64_t)std::max<int64_t>(tpb, 1))
+                                         : 63 - bits_for((uint64_t)std::max<int64_t>(tpb - 1, 1));
         v.fx_scale = std::ldexp(1.0, sc);
         v.fx_iscale = std::ldexp(1.0, -sc);
         v.T = g->T;
@@ -1642,7 +2103,7 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         v.blk0b = blocks_b;
         bytes += iter_bytes(g, fp32);
         if (g->fused) {
-            sul = sul && FxLds(g->N, TT, 2 * TT).su_lds;   // (fits either S)
+            sul = sul && (plan.v2 ? plan.sul : FxLds(g->N, TT, 2 * TT).su_lds);   // (v1: fits either S)
             multi = multi || v.n_fa < cdiv(g->T, TT);
             continue;   // no tile-path blocks (n_tb = n_tiles = n_ob = 0)
         }
@@ -1668,14 +2129,18 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
     const int fx_S = fx_s(multi);
     const FxA fx_a = fx_kernel(fp32, sul, multi, fx_S);
     for (int i = 0; i < ng; ++i)
-        if (gs[i]->fused) lds_f = std::max(lds_f, FxLds(gs[i]->N, TT, fx_S * TT, sul).total);
+        if (gs[i]->fused)
+            lds_f = std::max(lds_f, plan.v2 ? WvLds(gs[i]->N, plan.NT, plan.mode).total : FxLds(gs[i]->N, TT, fx_S * TT, sul).total);
+    const WvA sg_a = plan.v2 ? wv_kernel(fp32, plan.mode, plan.NT) : nullptr;
+    const int fx_bs = plan.v2 ? plan.NT : fx_S * TT;
     // a sharded graph with no collective backend is one whole shard: the split launches around the
     // (no-op) all-reduces would compute the same integers / sums in two halves
     const bool coll = sharded && mr_coll_ready(ctx);
     for (int it = 0; it < iters; ++it) {
         mr_prof_begin(ctx);
         if (blocks_fa) {
-            hipLaunchKernelGGL(fx_a, dim3(blocks_fa), dim3(fx_S * TT), lds_f, st, dv.p, ng, split_fa, d, alpha, it, TT);
+            if (sg_a) hipLaunchKernelGGL(sg_a, dim3(blocks_fa), dim3(fx_bs), lds_f, st, dv.p, ng, split_fa, d, alpha, it, TT);
+            else hipLaunchKernelGGL(fx_a, dim3(blocks_fa), dim3(fx_bs), lds_f, st, dv.p, ng, split_fa, d, alpha, it, TT);
             MR_DEBUG_CHECK(ctx, "k_fx_a");
             if (!coll) {
                 hipLaunchKernelGGL(k_fx_b, dim3(blocks_fb), dim3(WAVE * FB_W), 0, st, dv.p, ng, split_fb, d, it, 0);
