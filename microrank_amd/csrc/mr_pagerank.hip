@@ -1112,15 +1112,16 @@ __global__ void __launch_bounds__(S * FX_TMAX, 4) k_fx_a(const GDev* __restrict_
 //     and su (LDS when it fits beside the accumulator; otherwise gathered from its global copy
 //     right after the tile's ids arrive, before the bitmap staging).
 // The block synchronises only to clear the accumulator and to write its partial row.
-constexpr int WV_POS = 1024;                 // positions of a wave tile's fast path (64 x 16)
+constexpr int WV_POS = 1024;                 // positions of a wave tile's pipelined path (64 x 16)
+constexpr int WV_POS_MAX = 4096;             // segment path up to 64 positions per lane
 struct WvScratch {                           // per-wave LDS scratch (byte offsets)
-    static constexpr size_t hb = 0;          // 34 words: trace starts of 1024 positions (+2 read-ahead)
-    static constexpr size_t owner = 144;     // int32[64]: trace (in the tile) of a segment's first position
-    static constexpr size_t xl = 400;        // u64[66]: xl[c + 1] = X of trace c, xl[0] = 0
-    static constexpr size_t tsum = 928;      // double[64]
-    static constexpr size_t head = 1440;     // double[64]
-    static constexpr size_t tail = 1952;     // double[64]
-    static constexpr size_t bytes = 2464;    // (the long path's staged ids, u16[1024], alias it)
+    static constexpr size_t hb = 0;          // 130 words: trace starts of 4096 positions (+2 read-ahead)
+    static constexpr size_t owner = 528;     // int32[64]: trace (in the tile) of a segment's first position
+    static constexpr size_t xl = 784;        // u64[66]: xl[c + 1] = X of trace c, xl[0] = 0
+    static constexpr size_t tsum = 1312;     // double[64]
+    static constexpr size_t head = 1824;     // double[64]
+    static constexpr size_t tail = 2336;     // double[64]
+    static constexpr size_t bytes = 2848;    // (the long path's staged ids, u16[1024], alias it)
 };
 constexpr size_t WV_LDS_MAX = 160 * 1024 - 512;
 // su modes of k_wv_a: global gathers only / every op's su in LDS (interleaved with the
@@ -1214,7 +1215,6 @@ __global__ void __launch_bounds__(NT) k_wv_a(const GDev* __restrict__ gs, int32_
     const int32_t kl = max(ke - 1, kb);   // clamp target of the look-ahead
     int32_t a0 = 0, b0 = 0, a1 = 0, b1 = 0;   // offsets of tiles k and k + NW
     double qk = 0.0;
-    float ct = 0.0f, wt = 0.0f;
     u32x4 v0 = {0u, 0u, 0u, 0u}, v1 = v0;
     if (k < ke) {   // (a wave without tiles -- e.g. an empty shard -- loads nothing)
         const int32_t t = tr_of(min(k, kl));
@@ -1224,21 +1224,20 @@ __global__ void __launch_bounds__(NT) k_wv_a(const GDev* __restrict__ gs, int32_
         a1 = rs_off[2 * t1];
         b1 = rs_off[2 * t1 + 2];
     // words + ids of the tile whose offsets are (a_, b_)
-#define WV_LOAD(kk_, a_, b_, qk_, ct_, wt_, v0_, v1_)                                               \
+#define WV_LOAD(kk_, a_, b_, qk_, v0_, v1_)                                                         \
     do {                                                                                            \
         const int32_t t_ = tr_of(min((kk_), kl));                                                   \
         qk_ = (double)qc[t_];                                                                       \
-        ct_ = c_t[t_];                                                                              \
-        wt_ = w_t[t_];                                                                              \
         const int32_t e0_ = __builtin_amdgcn_readfirstlane(a_);                                     \
         const int32_t e1_ = __builtin_amdgcn_readlane(b_, WAVE - 1);                                \
         const int32_t base_ = e0_ & ~7, np_ = e1_ - base_;                                          \
-        const int32_t nch_ = (np_ + 7) >> 3, cpl_ = np_ <= 8 * WAVE ? 1 : 2;                        \
+        const int32_t nch_ = (np_ + 7) >> 3;                                                        \
+        const int32_t cpl_ = np_ <= 8 * WAVE ? 1 : np_ <= WV_POS ? 2 : np_ <= 2 * WV_POS ? 4 : 8;   \
         const GLB u32x4* src_ = rs16 + (base_ >> 3);                                                \
         v0_ = src_[min(lane * cpl_, nch_ - 1)];                                                     \
         v1_ = src_[min(lane * cpl_ + 1, nch_ - 1)];                                                 \
     } while (0)
-        WV_LOAD(k, a0, b0, qk, ct, wt, v0, v1);
+        WV_LOAD(k, a0, b0, qk, v0, v1);
     }
     double rmax = -__builtin_huge_val();
     for (; k < ke; k += NW) {
@@ -1248,10 +1247,10 @@ __global__ void __launch_bounds__(NT) k_wv_a(const GDev* __restrict__ gs, int32_
         const int32_t a = a0, b = b0;
         const int32_t e0 = __builtin_amdgcn_readfirstlane(a), e1 = __builtin_amdgcn_readlane(b, WAVE - 1);
         const double q_k = qk;
-        const float c_k = ct, w_k = wt;
         u32x4 c0 = v0, c1 = v1;
         const int32_t base = e0 & ~7, shift = e0 - base, np_ = e1 - base;
-        const int lgL = np_ <= 8 * WAVE ? 3 : np_ <= WV_POS ? 4 : 0;   // 0: long tile
+        // segment length 8 / 16 (ids prefetched) or 32 / 64 positions; 0: long tile
+        const int lgL = np_ <= 8 * WAVE ? 3 : np_ <= WV_POS ? 4 : np_ <= 2 * WV_POS ? 5 : np_ <= WV_POS_MAX ? 6 : 0;
         const int32_t L = 1 << lgL, p = lane * L, cpl = L >> 3;
         const int32_t qe = lgL ? min(p + L, np_) : 0;
         const int32_t ra = a - base, rb = b - base;
@@ -1279,7 +1278,7 @@ __global__ void __launch_bounds__(NT) k_wv_a(const GDev* __restrict__ gs, int32_
         // the gathers (compiler barrier): loads complete in issue order (one vmcnt), so the walk
         // then waits for its L2 gathers only, not for these HBM loads
         asm volatile("" ::: "memory");
-        WV_LOAD(k + NW, a1, b1, qk, ct, wt, v0, v1);
+        WV_LOAD(k + NW, a1, b1, qk, v0, v1);
         a0 = a1;
         b0 = b1;
         {
@@ -1287,10 +1286,12 @@ __global__ void __launch_bounds__(NT) k_wv_a(const GDev* __restrict__ gs, int32_
             a1 = rs_off[2 * t2];
             b1 = rs_off[2 * t2 + 2];
         }
+        // this tile's (1-d) v_t and w_t, needed only after the walk (their latency hides behind it)
+        const float c_k = c_t[tr_of(k)], w_k = w_t[tr_of(k)];
         double acc = 0.0;
         if (lgL) {
             // ---- staging (per-wave scratch): trace starts, segment owners, X
-            if (lane < 34) hb[lane] = 0u;
+            for (int32_t w = lane; w < 130; w += WAVE) hb[w] = 0u;
             owner[lane] = -1;
             __builtin_amdgcn_wave_barrier();
             if (own) {
@@ -1302,16 +1303,21 @@ __global__ void __launch_bounds__(NT) k_wv_a(const GDev* __restrict__ gs, int32_
             __builtin_amdgcn_wave_barrier();
             // ---- walk
             if (p < qe) {
+                // trace starts of the segment: L <= 64 bits from position p, and whether a trace
+                // starts right after it (the segment's last piece is then complete)
+                const int32_t w0 = p >> 5;
                 const unsigned long long bits =
-                    (((unsigned long long)hb[(p >> 5) + 1] << 32) | hb[p >> 5]) >> (p & 31);
+                    (((unsigned long long)hb[w0 + 1] << 32) | hb[w0]) >> (p & 31);
                 int32_t c = owner[lane];
                 bool st = bits & 1ull;
-                const unsigned long long sb = bits & ~1ull;
-#pragma unroll
-                for (int kc = 0; kc < 2; ++kc) {
-                    if (kc >= cpl || p + 8 * kc >= qe) break;
-                    const u32x4 w = kc ? c1 : c0;
-                    const uint32_t m8 = (uint32_t)(sb >> (8 * kc)) & 0xffu;
+                // one chunk of 8 positions: op-side atomics (X of each entry's trace) and the
+                // trace side's sequential sums restarted at each trace start; a finished piece
+                // goes to tsum[c] (a trace inside the segment) or head[lane] (the segment's first
+                // piece, continuing a trace from an earlier segment).  Only the store is
+                // predicated (one address select, one masked ds_write).
+                auto chunk = [&](const u32x4 w, const double* gsrc, int kc) {
+                    // starts after the segment's first position (that one is `st`)
+                    const uint32_t m8 = (uint32_t)(bits >> (8 * kc)) & (kc ? 0xffu : 0xfeu);
                     int32_t o[8];
                     o[0] = (int32_t)(w.x & 0xffffu); o[1] = (int32_t)(w.x >> 16);
                     o[2] = (int32_t)(w.y & 0xffffu); o[3] = (int32_t)(w.y >> 16);
@@ -1320,7 +1326,7 @@ __global__ void __launch_bounds__(NT) k_wv_a(const GDev* __restrict__ gs, int32_
                     double g[8];
 #pragma unroll
                     for (int j = 0; j < 8; ++j) {
-                        const double gg = kc ? gv1[j] : gv0[j];
+                        const double gg = gsrc[j];
                         g[j] = (MR_EXP & 2) ? (double)o[j]
                                : SUL      ? su_l[AS * o[j]]
                                : HOT      ? (o[j] < NH ? su_l[min(o[j], NH - 1)] : gg)
@@ -1336,21 +1342,39 @@ __global__ void __launch_bounds__(NT) k_wv_a(const GDev* __restrict__ gs, int32_
                     }
 #pragma unroll
                     for (int j = 0; j < 8; ++j) {
-                        if (m8 & (1u << j)) {   // a new trace starts at p + 8 kc + j
-                            if (st) tsum[c] = acc; else head[lane] = acc;
-                            acc = 0.0;
-                            st = true;
-                            ++c;
-                        }
-                        acc += g[j];
+                        const bool sj = (m8 >> j) & 1u;   // a new trace starts at p + 8 kc + j
+                        double* dst = st ? tsum + c : head + lane;
+                        if (sj) *dst = acc;
+                        c += sj ? 1 : 0;
+                        st = st || sj;
+                        acc = (sj ? 0.0 : acc) + g[j];
                     }
+                };
+                chunk(c0, gv0, 0);
+                if (cpl > 1 && p + 8 < qe) chunk(c1, gv1, 1);
+                if (cpl > 2) {
+                    // segments of 32 / 64 positions (wave tiles of heavy traces): chunks 2.. are
+                    // loaded here, latency exposed; the wait below leaves nothing of this rare
+                    // path pending where it rejoins the pipelined one
+                    const GLB u32x4* src = rs16 + (base >> 3);
+                    for (int kc = 2; kc < cpl; ++kc) {
+                        if (p + 8 * kc >= qe) break;
+                        const u32x4 w = fx_pad(src[lane * cpl + kc], lane * cpl + kc, shift, np_, N);
+                        if (!SUL) {   // the su gathers land in gv0's registers (chunk 0 is done)
+                            const uint32_t wd[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+                            for (int j = 0; j < 8; ++j) {
+                                const int32_t o = (int32_t)((wd[j >> 1] >> ((j & 1) * 16)) & 0xffffu);
+                                gv0[j] = sug[HOT && o < NH ? N : o];
+                            }
+                        }
+                        chunk(w, gv0, kc);
+                    }
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 }
-                const bool ends = qe == np_ || ((bits >> (qe - p)) & 1ull);
-                if (st) {
-                    if (ends) tsum[c] = acc; else tail[lane] = acc;
-                } else {
-                    head[lane] = acc;
-                }
+                const bool ends = qe == np_ || (qe - p < L ? ((bits >> (qe - p)) & 1ull)
+                                                           : lgL == 6 ? (hb[w0 + 2] & 1u) : ((bits >> L) & 1ull));
+                *(st ? (ends ? tsum + c : tail + lane) : head + lane) = acc;
             }
             __builtin_amdgcn_wave_barrier();
             // ---- combine: trace = its pieces in segment order
