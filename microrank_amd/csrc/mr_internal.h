@@ -128,6 +128,19 @@ struct mr_graph {
     DBuf<int32_t> perm;
     DBuf<uint16_t> rsp;
     bool relabeled = false;
+    // trace-parallel layout of the fused iteration (k_tr_a): traces sorted by op count (tperm[p]
+    // = trace at position p), wave tiles of 64 consecutive positions, each tile's ids in chunks
+    // of 4 per lane stored lane-interleaved ([chunk][lane] x 8 B: one 512-B load per chunk),
+    // each trace's ids rotated by (lane mod len) and padded with N + lane
+    int32_t n_wt = 0;                // wave tiles
+    DBuf<int32_t> tperm;             // [T]
+    DBuf<uint16_t> tids;             // [coff[n_wt] * 256]
+    DBuf<int32_t> coff;              // [n_wt+1] first chunk of a tile
+    std::vector<int32_t> coff_h;     // host copy (the per-wave tile split of a launch)
+    DBuf<float> w_tp, c_tp;          // [T] w_t, c_t in position order
+    DBuf<int32_t> wtile;             // [waves+1] first tile of each wave of the last launch plan
+    int32_t wtile_nw = 0;            // waves that wtile was cut for
+    int32_t wtile_tpb = 0;           // most tiles of one block under that cut
     // P_sr in compressed sparse blocks for the s' pass: traces cut in tiles of 2^tshift; within a
     // tile the distinct (op, trace) entries sorted by (op, trace) as u16 tile-local trace
     // indices; a "pair" is the run of one op inside one tile.

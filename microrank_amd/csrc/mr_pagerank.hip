@@ -20,6 +20,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <cstring>
 
 #include "mr_internal.h"
 #include "mr_prim.h"
@@ -178,6 +179,54 @@ __global__ void k_relabel_perm(const uint64_t* key, int32_t N, int32_t* perm, in
 __global__ void k_relabel_ids(const uint16_t* ids, int64_t n, const int32_t* inv, uint16_t* out) {
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e < n) out[e] = (uint16_t)inv[ids[e]];
+}
+
+// ---------------------------------------------------------------- trace-parallel layout (k_tr_a)
+// traces by op count: key = len << 32 | trace
+__global__ void k_tr_keys(const int64_t* off, int32_t T, uint64_t* key) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < T) key[t] = ((uint64_t)(off[t + 1] - off[t]) << 32) | (uint32_t)t;
+}
+__global__ void k_tr_perm(const uint64_t* key, int32_t T, const float* w_t, int32_t* tperm, float* w_tp) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= T) return;
+    const int32_t t = (int32_t)(uint32_t)key[p];
+    tperm[p] = t;
+    w_tp[p] = w_t[t];
+}
+// chunks of 4 ids per tile: its last position holds its longest trace (ascending sort)
+__global__ void k_tr_chunks(const uint64_t* key, int32_t T, int32_t n_wt, int64_t* nch) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < n_wt) nch[k] = (int64_t)(((key[min(k * WAVE + WAVE - 1, (int64_t)T - 1)] >> 32) + 3) >> 2);
+}
+__global__ void k_tr_coff(const int64_t* c64, int32_t n, int32_t* coff) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i <= n) coff[i] = (int32_t)c64[i];
+}
+// thread per (tile, lane): the lane's trace rotated by (lane mod len), then pads N + lane
+__global__ void k_tr_fill(const uint64_t* key, const int64_t* off, const uint16_t* ids, const int64_t* c64, int32_t T,
+                          int32_t N, int32_t n_wt, uint16_t* tids) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)n_wt * WAVE) return;
+    const int32_t k = (int32_t)(i / WAVE), lane = (int32_t)(i % WAVE);
+    const int64_t p = (int64_t)k * WAVE + lane;
+    int64_t a = 0, len = 0;
+    if (p < T) {
+        const int32_t t = (int32_t)(uint32_t)key[p];
+        a = off[t];
+        len = off[t + 1] - a;
+    }
+    const int64_t rot = len ? lane % len : 0, n4 = (c64[k + 1] - c64[k]) * 4;
+    uint16_t* dst = tids + (size_t)c64[k] * (WAVE * 4) + (size_t)lane * 4;
+    for (int64_t j = 0; j < n4; ++j) {
+        int64_t jj = j + rot;
+        if (jj >= len) jj -= len;
+        dst[(size_t)(j >> 2) * (WAVE * 4) + (j & 3)] = j < len ? ids[a + jj] : (uint16_t)(N + lane);
+    }
+}
+__global__ void k_tr_gather(const float* src, const int32_t* tperm, int32_t T, float* dst) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < T) dst[p] = src[tperm[p]];
 }
 
 // ---------------------------------------------------------------- kinds (pagerank.py:54-66)
@@ -430,8 +479,11 @@ __device__ __forceinline__ unsigned long long d2bits(double v) {
     return (unsigned long long)__double_as_longlong(v);
 }
 
+constexpr int TR_PAD = WAVE;   // k_tr_a's pad ids N .. N + 63 (su = 0)
+
 // T_all: traces of the whole graph (all shards) for the initial value
 // perm (relabelled fused graphs): su is kept in the kernel's op labels, su[new] = u_o[perm[new]] s
+// w_t: in position order for k_tr_a (w_tp: q is then indexed by position), else by trace
 __global__ void k_iter_init(const float* w_t, const float* u_o, int32_t N, int32_t T, int64_t T_all, double* sp0,
                             double* su0, double* su1, double* q64, float* q32, int fp32, unsigned long long* mslot,
                             const int32_t* perm) {
@@ -441,7 +493,7 @@ __global__ void k_iter_init(const float* w_t, const float* u_o, int32_t N, int32
         sp0[i] = v0;
         su0[i] = (double)u_o[perm ? perm[i] : i] * v0;
     }
-    if (i == N) su0[N] = su1[N] = 0.0;   // the fused walk's pad slot
+    if (i >= N && i < N + TR_PAD) su0[i] = su1[i] = 0.0;   // the fused walks' pad slots
     if (i < T) {
         double q = (double)w_t[i] * v0;
         if (fp32) q32[i] = (float)q; else q64[i] = q;
@@ -459,7 +511,12 @@ struct GDev {
     const uint16_t* rs16;       // u16 copy of rs_ops (N <= 65536) or null
     const uint16_t* rsw;        // the fused kernel's ids: rs16, or rsp in relabelled ops
     const int32_t* perm;        // relabelled ops: perm[new] = old (null: identity)
-    int32_t n_hot;              // k_wv_a: su of ops [0, n_hot) in LDS (relabelled graphs)
+    int32_t n_hot;              // k_wv_a / k_tr_a: su of ops [0, n_hot) in LDS (relabelled graphs)
+    const uint16_t* tids;       // k_tr_a: lane-interleaved id chunks of the wave tiles
+    const int32_t* coff;        // [n_wt+1] first chunk of a tile
+    const int32_t* wtile;       // [waves+1] first tile of each wave of the launch
+    const float* c_tp;          // c_t, w_t in position order (tperm)
+    const float* w_tp;
     const float* c_t;
     const float* w_t;
     const float* u_o;
@@ -685,6 +742,7 @@ __device__ __forceinline__ int64_t rfl64(int64_t v) {   // a wave-uniform value 
     return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 template <class T>
 __device__ __forceinline__ const GLB T* gp(const T* p) { return (const GLB T*)p; }
 template <class T>
@@ -1444,6 +1502,176 @@ __global__ void __launch_bounds__(NT) k_wv_a(const GDev* __restrict__ gs, int32_
         atomicMax((unsigned long long*)&Mnext[MSH + blockIdx.x % MSH], d2bits(rmax));
 }
 
+// ---------------------------------------------------------------- fused iteration, trace-parallel (k_tr_a)
+// The single-pass iteration with lane = trace.  At prepare a graph's traces are sorted by op
+// count (tperm: position -> trace) and cut into wave tiles of 64 positions; a tile stores its
+// traces' ids lane-interleaved in chunks of 4 (chunk c = 64 lanes x 4 u16: one coalesced 512-B
+// load), padded to the tile's longest trace with N + lane (a zero su slot and a dummy
+// accumulator per lane, so pads neither branch nor collide), and each trace rotated by
+// (lane mod len): a trace's first op is often a root shared by the whole tile, and rotation
+// spreads those atomics over the chunk's four instructions and many lanes' addresses.
+// Each wave streams a contiguous run of tiles as ONE chunk stream -- ids three chunks ahead,
+// the su of cold ops (WV_SU_HOT / GLOBAL) one chunk ahead, a tile's q, (1-d) v and w one tile
+// ahead -- with every load unconditional (clamped), so each use waits for exactly its own load.
+// Per entry: one su read (LDS, or the prefetched gather), one add into the lane's own trace sum
+// (sequential: deterministic), one LDS u64 atomic of the lane's X_t (integers: order-free).  The
+// block synchronises only to clear the accumulator and to write its partial row.
+struct TrLds {
+    size_t su, lacc, total;
+    bool su_lds;      // every op's su fits beside the accumulator (interleaved: 16 B per op)
+    int32_t n_hot;    // WV_SU_HOT: su of ops [0, n_hot) in LDS
+    __host__ __device__ TrLds(int32_t N, int mode) {
+        const size_t ns = (size_t)N + TR_PAD;
+        su_lds = ns * 16 <= WV_LDS_MAX;
+        const bool all = mode == WV_SU_ALL && su_lds;
+        const size_t accb = (ns * (all ? 16 : 8) + 15) / 16 * 16;
+        n_hot = 0;
+        if (mode == WV_SU_HOT && accb < WV_LDS_MAX)
+            n_hot = (int32_t)std::min<size_t>((size_t)N, (WV_LDS_MAX - accb) / 8 / 64 * 64);
+        lacc = all ? 8 : 0;
+        su = all ? 0 : accb;
+        total = all ? accb : accb + (size_t)n_hot * 8;
+    }
+};
+
+template <class Q, int SUM, int NT>
+__global__ void __launch_bounds__(NT) k_tr_a(const GDev* __restrict__ gs, int32_t ng, int32_t split, double d,
+                                             double alpha, int it, int32_t unused) {
+    constexpr bool SUL = SUM == WV_SU_ALL, HOT = SUM == WV_SU_HOT;
+    constexpr int NW = NT / WAVE, AS = SUL ? 2 : 1;
+    extern __shared__ __attribute__((aligned(16))) unsigned char lraw[];
+    __shared__ double red[NW];
+    __shared__ double msh[2];
+    const GDev& G = gs[fx_graph(gs, ng, split, 2)];
+    const int32_t lb = (int32_t)blockIdx.x - G.blk0f;
+    const int cur = it & 1, nxt = cur ^ 1, k3 = it % 3;
+    const int32_t T = G.T, N = G.N;
+    const int32_t tid = (int32_t)threadIdx.x, lane = tid & (WAVE - 1), wv = tid / WAVE;
+    const TrLds L_(N, SUM);
+    const int32_t NH = HOT ? G.n_hot : 0;   // <= L_.n_hot (the host sizes both alike), >= 64
+    const GLB u32x2* ids = gp((const u32x2*)G.tids) + lane;   // chunk c of this lane: ids[c * WAVE]
+    const GLB int32_t* coff = gp(G.coff);
+    const GLB Q* qc = gp((const Q*)G.q[cur]);
+    GLB Q* qn = gpw((Q*)G.q[nxt]);
+    const GLB float* c_tp = gp(G.c_tp);
+    const GLB float* w_tp = gp(G.w_tp);
+    const GLB double* sug = gp(G.sub[cur]);   // N + TR_PAD entries, [N, N + TR_PAD) = 0
+    double* su_l = (double*)(lraw + L_.su);
+    unsigned long long* lacc = (unsigned long long*)(lraw + L_.lacc);
+    GLB unsigned long long* mslot = gpw(G.mslot);
+    const GLB unsigned long long* Mcur = mslot + (size_t)2 * MSH * k3;
+    GLB unsigned long long* Mnext = mslot + (size_t)2 * MSH * ((k3 + 1) % 3);
+    if (lb == 0 && tid < 2 * MSH) mslot[(size_t)2 * MSH * ((k3 + 2) % 3) + tid] = 0ull;
+    // this wave's tiles [k, ke) (a contiguous run: the host cuts them by chunk count)
+    const GLB int32_t* wt = gp(G.wtile) + ((size_t)lb * NW + wv);
+    int32_t k = __builtin_amdgcn_readfirstlane(wt[0]);
+    const int32_t ke = __builtin_amdgcn_readfirstlane(wt[1]);
+    for (int32_t o = tid; o < N + TR_PAD; o += NT) {
+        if (SUL) su_l[AS * o] = sug[o];
+        lacc[AS * o] = 0ull;
+    }
+    if (HOT)
+        for (int32_t o = tid; o < NH; o += NT) su_l[o] = sug[o];
+    if (tid < WAVE) {
+        const double ms = wave_max(bits2d(Mcur[tid]));
+        const double mr = wave_max(bits2d(Mcur[MSH + tid]));
+        if (tid == 0) {
+            msh[0] = ms;
+            msh[1] = mr;
+        }
+    }
+    __syncthreads();   // accumulator and maxima ready
+    const double xsc = G.fx_scale / msh[1], Ms = msh[0];
+    double rmax = -__builtin_huge_val();
+    if (k < ke) {
+        auto pos = [&](int32_t kk) { return min(kk * WAVE + lane, T - 1); };
+        // cold-op su of a chunk (hot ops load the pad slot sug[N]: one line, no traffic)
+        auto gather = [&](const u32x2 w, double* g) {
+            const int32_t o[4] = {(int32_t)(w.x & 0xffffu), (int32_t)(w.x >> 16), (int32_t)(w.y & 0xffffu),
+                                  (int32_t)(w.y >> 16)};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) g[j] = SUL ? 0.0 : sug[HOT && o[j] < NH ? N : o[j]];
+        };
+        int32_t c = __builtin_amdgcn_readfirstlane(coff[k]);
+        int32_t ce = __builtin_amdgcn_readfirstlane(coff[k + 1]);   // end of tile k
+        const int32_t cl = __builtin_amdgcn_readfirstlane(coff[ke]) - 1;   // the run's last chunk
+        // tile k's words; tile k + 1's q and end chunk (one tile ahead, clamped into the run)
+        const int32_t kn = min(k + 1, ke - 1);
+        double q_cur = (double)qc[pos(k)];
+        float c_cur = c_tp[pos(k)], w_cur = w_tp[pos(k)];
+        double q_nx = (double)qc[pos(kn)];
+        int32_t ce_nx = coff[kn + 1];
+        u32x2 w0 = ids[(size_t)c * WAVE];
+        u32x2 w1 = ids[(size_t)min(c + 1, cl) * WAVE];
+        u32x2 w2 = ids[(size_t)min(c + 2, cl) * WAVE];
+        double g0[4], g1[4];
+        if (!SUL) gather(w0, g0);
+        unsigned long long X = k * WAVE + lane < T ? (unsigned long long)__double2ull_rn(q_cur * xsc) : 0ull;
+        double acc = 0.0;
+        for (;;) {
+            // chunk c: ids w0 (here), cold su g0 (in flight); ids w1, w2 in flight
+            const u32x2 w3 = ids[(size_t)min(c + 3, cl) * WAVE];
+            if (!SUL) gather(w1, g1);
+            const int32_t o[4] = {(int32_t)(w0.x & 0xffffu), (int32_t)(w0.x >> 16), (int32_t)(w0.y & 0xffffu),
+                                  (int32_t)(w0.y >> 16)};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const double g = SUL ? su_l[AS * o[j]] : HOT ? (o[j] < NH ? su_l[min(o[j], NH - 1)] : g0[j]) : g0[j];
+                acc += g;
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) atomicAdd(&lacc[AS * o[j]], X);
+            w0 = w1;
+            w1 = w2;
+            w2 = w3;
+            if (!SUL) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) g0[j] = g1[j];
+            }
+            if (++c == ce) {
+                // ---- tile k done: r' of its traces (pagerank.py:125) and the next q
+                const int32_t p = k * WAVE + lane;
+                const bool own = p < T;
+                const double rp = d * (acc / Ms) + (double)c_cur;
+                if (own) rmax = nmax(rmax, rp);
+                qn[own ? p : T] = (Q)((double)w_cur * rp);   // q[T]: pad slot
+                if (++k == ke) break;
+                ce = __builtin_amdgcn_readfirstlane(ce_nx);
+                q_cur = q_nx;
+                const int32_t kk = min(k + 1, ke - 1);
+                c_cur = c_tp[pos(k)];
+                w_cur = w_tp[pos(k)];
+                q_nx = (double)qc[pos(kk)];
+                ce_nx = coff[kk + 1];
+                X = k * WAVE + lane < T ? (unsigned long long)__double2ull_rn(q_cur * xsc) : 0ull;
+                acc = 0.0;
+            }
+        }
+    }
+    // call-graph term for the next s' (pagerank.py:122-124, alpha P_ss s_k), a thread per op
+    {
+        const GLB double* sp_cur = gp(G.spb[cur]);
+        const GLB int64_t* ss_off = gp(G.ss_off);
+        const GLB int32_t* ss_par = gp(G.ss_par);
+        const GLB float* pw = gp(G.pw);
+        GLB double* ssv = gpw(G.fx_ssv);
+        for (int32_t oss = lb * NT + tid; oss < N; oss += G.n_fa * NT) {
+            double bb = 0.0;
+            for (int64_t e = ss_off[oss]; e < ss_off[oss + 1]; ++e) {
+                const int32_t pp = ss_par[e];
+                bb += (double)pw[pp] * sp_cur[pp];
+            }
+            ssv[oss] = alpha * (bb / Ms);
+        }
+    }
+    __syncthreads();
+    GLB unsigned long long* prow = gpw(G.fx_part) + (size_t)lb * N;
+    for (int32_t o = tid; o < N; o += NT) prow[o] = lacc[AS * o];
+    rmax = block_max(rmax, red);
+    if (tid == 0 && rmax >= 0.0)   // -inf: a block without traces (an empty shard's placeholder)
+        atomicMax((unsigned long long*)&Mnext[MSH + blockIdx.x % MSH], d2bits(rmax));
+}
+
 // Column sums of the partial rows: a block per chunk of FB_OPS consecutive ops (lane = op, so
 // every row read is one coalesced 512-B segment), its FB_W waves splitting the rows; the waves'
 // limb sums meet in LDS (integers: order-free).  mode 0: whole graph; sharded graphs split it
@@ -1721,11 +1949,19 @@ static int64_t fx_blocks(int32_t T, int32_t N, int TT) {
     return std::min(nb, tiles);
 }
 
-// ---- k_wv_a (default fused kernel; MR_FX_V1 selects k_fx_a for A/B measurements)
-static bool fx_v1() {
-    static const bool v = getenv("MR_FX_V1") != nullptr;
+// ---- fused iteration kernel: k_tr_a (default); MR_FX_KERNEL=wv / v1 selects k_wv_a / k_fx_a
+// for A/B measurements
+enum { FXK_V1 = 1, FXK_WV = 2, FXK_TR = 3 };
+static int fx_kind() {
+    static const int v = [] {
+        const char* e = getenv("MR_FX_KERNEL");
+        if (e && !strcmp(e, "v1")) return (int)FXK_V1;
+        if (e && !strcmp(e, "wv")) return (int)FXK_WV;
+        return (int)FXK_TR;
+    }();
     return v;
 }
+static bool fx_v1() { return fx_kind() == FXK_V1; }
 using WvA = void (*)(const GDev*, int32_t, int32_t, double, double, int, int32_t);
 static WvA wv_kernel(bool fp32, int mode, int NT) {
     static const WvA tab[2][3][2] = {
@@ -1735,6 +1971,16 @@ static WvA wv_kernel(bool fp32, int mode, int NT) {
         {{k_wv_a<float, 0, 512>, k_wv_a<float, 0, 1024>},
          {k_wv_a<float, 1, 512>, k_wv_a<float, 1, 1024>},
          {k_wv_a<float, 2, 512>, k_wv_a<float, 2, 1024>}}};
+    return tab[fp32 ? 1 : 0][mode][NT == 1024 ? 1 : 0];
+}
+static WvA tr_kernel(bool fp32, int mode, int NT) {
+    static const WvA tab[2][3][2] = {
+        {{k_tr_a<double, 0, 512>, k_tr_a<double, 0, 1024>},
+         {k_tr_a<double, 1, 512>, k_tr_a<double, 1, 1024>},
+         {k_tr_a<double, 2, 512>, k_tr_a<double, 2, 1024>}},
+        {{k_tr_a<float, 0, 512>, k_tr_a<float, 0, 1024>},
+         {k_tr_a<float, 1, 512>, k_tr_a<float, 1, 1024>},
+         {k_tr_a<float, 2, 512>, k_tr_a<float, 2, 1024>}}};
     return tab[fp32 ? 1 : 0][mode][NT == 1024 ? 1 : 0];
 }
 static int num_cus() {
@@ -1749,7 +1995,8 @@ static int num_cus() {
 
 // Launch plan of the fused iteration for a batch of graphs (one kernel variant per launch).
 struct FxPlan {
-    bool v2 = true;     // k_wv_a
+    bool v2 = true;     // wave tiles (k_tr_a / k_wv_a), else k_fx_a
+    bool tr = true;     // k_tr_a
     int NT = 1024;      // block size (16 waves; 512 when the graphs are small)
     int mode = WV_SU_ALL;   // su in LDS for every fused graph of the batch / hot ops / none
     bool sul = true;    // mode == WV_SU_ALL
@@ -1757,6 +2004,7 @@ struct FxPlan {
 static FxPlan fx_plan(mr_graph* const* gs, int ng) {
     FxPlan P;
     P.v2 = !fx_v1();
+    P.tr = fx_kind() == FXK_TR;
     if (!P.v2) return P;
     int32_t nmax = 0;
     int64_t tmax = 0;
@@ -1773,12 +2021,30 @@ static FxPlan fx_plan(mr_graph* const* gs, int ng) {
     P.NT = force_nt == 512 || force_nt == 1024 ? force_nt : (cdiv(tmax, WAVE) >= (int64_t)num_cus() * 16 ? 1024 : 512);
     bool relabeled = false;
     for (int i = 0; i < ng; ++i) relabeled = relabeled || (gs[i]->fused && gs[i]->relabeled);
-    P.sul = WvLds(nmax, P.NT, WV_SU_ALL).su_lds;
+    P.sul = P.tr ? TrLds(nmax, WV_SU_ALL).su_lds : WvLds(nmax, P.NT, WV_SU_ALL).su_lds;
     P.mode = P.sul ? WV_SU_ALL : relabeled ? WV_SU_HOT : WV_SU_GLOBAL;
     if (P.mode == WV_SU_HOT)   // every graph of the launch must be relabelled (hot ops = low labels)
         for (int i = 0; i < ng; ++i)
             if (gs[i]->fused && !gs[i]->relabeled) P.mode = WV_SU_GLOBAL;
+    if (P.tr && P.mode == WV_SU_HOT && TrLds(nmax, WV_SU_HOT).n_hot < 64) P.mode = WV_SU_GLOBAL;
     return P;
+}
+static int32_t plan_n_hot(int32_t N, const FxPlan& P) {
+    if (!P.v2 || P.mode != WV_SU_HOT) return 0;
+    return P.tr ? TrLds(N, WV_SU_HOT).n_hot : WvLds(N, P.NT, WV_SU_HOT).n_hot;
+}
+static size_t plan_lds(int32_t N, const FxPlan& P) {
+    return P.tr ? TrLds(N, P.mode).total : WvLds(N, P.NT, P.mode).total;
+}
+
+// resident blocks of the plan's kernel on the chip (occupancy by LDS image and VGPRs)
+static int64_t plan_resident(int32_t N, const FxPlan& P) {
+    const size_t lds = plan_lds(N, P);
+    const WvA kfn = P.tr ? tr_kernel(false, P.mode, P.NT) : wv_kernel(false, P.mode, P.NT);
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, (const void*)kfn, P.NT, lds) != hipSuccess || n < 1)
+        n = std::max<int>(1, (int)(WV_LDS_MAX / std::max<size_t>(lds, 1)));
+    return (int64_t)num_cus() * n;
 }
 
 // blocks of one graph: a resident block per CU (its waves stream the wave tiles), fewer when the
@@ -1786,18 +2052,91 @@ static FxPlan fx_plan(mr_graph* const* gs, int ng) {
 // fixed-point scale 2^48 keeps a block's per-op sums below 2^64)
 static int64_t wv_blocks(int32_t T, int32_t N, const FxPlan& P) {
     const int64_t W = cdiv((int64_t)T, WAVE), NW = P.NT / WAVE;
-    const WvLds L(N, P.NT, P.mode);
-    int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, (const void*)wv_kernel(false, P.mode, P.NT), P.NT, L.total) !=
-            hipSuccess || n < 1)
-        n = std::max<int>(1, (int)(WV_LDS_MAX / L.total));
-    const int64_t resident = (int64_t)num_cus() * n;
+    const int64_t resident = plan_resident(N, P);
     int64_t nb = std::min<int64_t>(resident, cdiv(W, NW));
     nb = std::max<int64_t>(nb, (int64_t)cdiv(W, 1023));   // <= 1023 wave tiles (65472 traces) per block
     return std::max<int64_t>(std::min(nb, W), W ? 1 : 0);
 }
-static int64_t fused_blocks(int32_t T, int32_t N, const FxPlan& P, int TT_v1) {
-    return P.v2 ? wv_blocks(T, N, P) : fx_blocks(T, N, TT_v1);
+
+// k_tr_a: blocks of one graph and the cut of its tiles into contiguous per-wave runs of about
+// equal cost (chunks + 2 per tile: a tile's q/r words weigh about two chunks).  Cached per
+// graph for the wave count; at most 1023 tiles (65472 traces) per block.
+static int tr_split(mr_ctx* ctx, mr_graph* g, const FxPlan& P, int64_t* nfa) {
+    const int64_t W = g->n_wt, NW = P.NT / WAVE;
+    const int64_t resident = plan_resident(g->N, P);
+    int64_t nb = std::max<int64_t>(std::min<int64_t>(resident, cdiv(W, NW)), 1);
+    const std::vector<int32_t>& co = g->coff_h;
+    for (;;) {
+        const int64_t nw = nb * NW;
+        if (g->wtile.p && g->wtile_nw == nw) break;
+        std::vector<int32_t> cut((size_t)nw + 1);
+        const double total = W ? (double)co[(size_t)W] + 2.0 * (double)W : 0.0;
+        int64_t k = 0;
+        for (int64_t i = 0; i <= nw; ++i) {   // first tile whose cost prefix reaches the target
+            const double target = total * (double)i / (double)nw;
+            while (k < W && (double)co[(size_t)k] + 2.0 * (double)k < target) ++k;
+            cut[(size_t)i] = (int32_t)k;
+        }
+        cut[(size_t)nw] = (int32_t)W;
+        int32_t tpb = 0;
+        for (int64_t b = 0; b < nb; ++b) tpb = std::max(tpb, cut[(size_t)((b + 1) * NW)] - cut[(size_t)(b * NW)]);
+        if (tpb > 1023) {
+            nb += resident;
+            continue;
+        }
+        MR_TRY(g->wtile.upload(ctx, cut.data(), cut.size()));
+        MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));   // (the host vector leaves scope)
+        g->wtile_nw = (int32_t)nw;
+        g->wtile_tpb = tpb;
+        break;
+    }
+    *nfa = nb;
+    return MR_OK;
+}
+
+static int fused_blocks(mr_ctx* ctx, mr_graph* g, const FxPlan& P, int TT_v1, int64_t* nfa) {
+    if (P.tr) return tr_split(ctx, g, P, nfa);
+    *nfa = P.v2 ? wv_blocks(g->T, g->N, P) : fx_blocks(g->T, g->N, TT_v1);
+    return MR_OK;
+}
+
+// k_tr_a's layout of a fused graph (after w_t and the kernel's ids rs16 / rsp): traces sorted by
+// op count, tiles of 64 positions, ids lane-interleaved in chunks of 4.  One host round trip (the
+// chunk count sizes the id array; the chunk offsets stay on the host for the per-wave cut).
+static int tr_layout(mr_ctx* ctx, mr_graph* g) {
+    hipStream_t st = ctx->stream;
+    const int32_t T = g->T, N = g->N;
+    const int32_t W = cdiv(T, WAVE);
+    g->n_wt = W;
+    g->wtile_nw = 0;
+    DBuf<uint64_t> key;
+    DBuf<int64_t> c64, tmp;
+    MR_TRY(key.alloc(ctx, (size_t)std::max(T, 1)));
+    MR_TRY(c64.alloc(ctx, (size_t)W + 1));
+    MR_TRY(tmp.alloc(ctx, (size_t)scan_tmp_elems(std::max<int64_t>(W, 1))));
+    MR_TRY(g->tperm.alloc(ctx, (size_t)std::max(T, 1)));
+    MR_TRY(g->w_tp.alloc(ctx, (size_t)std::max(T, 1)));
+    MR_TRY(g->coff.alloc(ctx, (size_t)W + 1));
+    if (T) {
+        hipLaunchKernelGGL(k_tr_keys, dim3(cdiv(T, 256)), dim3(256), 0, st, g->rs_off.p, T, key.p);
+        SortScratch ws;
+        MR_TRY(mr_radix_sort(ctx, key.p, nullptr, T, 32 + bits_for((uint64_t)std::max(N, 1)), ws));
+        hipLaunchKernelGGL(k_tr_perm, dim3(cdiv(T, 256)), dim3(256), 0, st, key.p, T, g->w_t.p, g->tperm.p, g->w_tp.p);
+        hipLaunchKernelGGL(k_tr_chunks, dim3(cdiv(W, 256)), dim3(256), 0, st, key.p, T, W, c64.p);
+    }
+    MR_TRY(mr_exclusive_scan(ctx, c64.p, c64.p, W, tmp.p));
+    hipLaunchKernelGGL(k_tr_coff, dim3(cdiv((int64_t)W + 1, 256)), dim3(256), 0, st, c64.p, W, g->coff.p);
+    g->coff_h.assign((size_t)W + 1, 0);
+    MR_TRY(g->coff.download(ctx, g->coff_h.data(), (size_t)W + 1));
+    MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+    const int64_t nch = g->coff_h[(size_t)W];
+    MR_TRY(g->tids.alloc(ctx, (size_t)std::max<int64_t>(nch, 1) * WAVE * 4));
+    const uint16_t* src = g->relabeled ? g->rsp.p : g->rs16.p;
+    if (W)
+        hipLaunchKernelGGL(k_tr_fill, dim3(cdiv((int64_t)W * WAVE, 256)), dim3(256), 0, st, key.p, g->rs_off.p, src, c64.p,
+                           T, N, W, g->tids.p);
+    MR_TRY_HIP(ctx, hipGetLastError());
+    return MR_OK;   // (scratch returns to the stream-ordered pool)
 }
 
 // Derived per-graph arrays: fp32 reciprocals, u16 ids, and the P_sr tiles.  One host round trip
@@ -1829,7 +2168,7 @@ int mr_graph_prepare(mr_ctx* ctx, mr_graph* g) {
         // k_wv_a stages the su of the most covered ops (ops [0, n_hot)) and gathers the rest.
         // The kinds keep rs16 (original labels, the same hash on every rank); only the
         // iteration's id stream (rsp), su and the partial rows use the new labels.
-        g->relabeled = !fx_v1() && !WvLds(N, 1024, WV_SU_ALL).su_lds;
+        g->relabeled = fx_kind() == FXK_TR ? !TrLds(N, WV_SU_ALL).su_lds : fx_kind() == FXK_WV && !WvLds(N, 1024, WV_SU_ALL).su_lds;
         if (g->relabeled) {
             DBuf<uint64_t> key;
             DBuf<int32_t> inv;
@@ -1846,6 +2185,7 @@ int mr_graph_prepare(mr_ctx* ctx, mr_graph* g) {
             g->perm.reset();
             g->rsp.reset();
         }
+        MR_TRY(tr_layout(ctx, g));
         g->n_tiles = 0;
         g->n_pairs = 0;
         MR_TRY_HIP(ctx, hipGetLastError());
@@ -1958,11 +2298,15 @@ static int pagerank_setup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool 
     MR_TRY(g->sn.alloc(ctx, (size_t)N));
     MR_TRY(g->spb[0].alloc(ctx, (size_t)N));
     MR_TRY(g->spb[1].alloc(ctx, (size_t)N));
-    MR_TRY(g->sub[0].alloc(ctx, (size_t)N + 1));   // [N] = 0: the fused walk's pad slot
-    MR_TRY(g->sub[1].alloc(ctx, (size_t)N + 1));
+    MR_TRY(g->sub[0].alloc(ctx, (size_t)N + TR_PAD));   // [N, N + TR_PAD) = 0: the fused walks' pad slots
+    MR_TRY(g->sub[1].alloc(ctx, (size_t)N + TR_PAD));
     MR_TRY(g->weight.alloc(ctx, (size_t)N));
+    const bool tr = g->fused && plan.tr;
+    if (tr) MR_TRY(g->c_tp.alloc(ctx, (size_t)std::max(T, 1)));
     if (g->fused) {
-        MR_TRY(g->fx_part.alloc(ctx, (size_t)std::max<int64_t>(fused_blocks(T, N, plan, TT), 1) * (size_t)N));
+        int64_t nfa = 0;
+        MR_TRY(fused_blocks(ctx, g, plan, TT, &nfa));
+        MR_TRY(g->fx_part.alloc(ctx, (size_t)std::max<int64_t>(nfa, 1) * (size_t)N));
         MR_TRY(g->fx_ssv.alloc(ctx, (size_t)N));
     }
     else MR_TRY(g->part.alloc(ctx, (size_t)std::max<int64_t>(g->n_pairs, 1)));
@@ -2016,8 +2360,9 @@ static int pagerank_setup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool 
         hipLaunchKernelGGL(k_pref_apply, dim3(nbp), dim3(TB), 0, st, g->kind.p, prt, prl, g->len_t.p, n_pr,
                            g->scal.p, anomaly, cd, g->pref.p, g->c_t.p);
     MR_DEBUG_CHECK(ctx, "k_pref_apply");
-    hipLaunchKernelGGL(k_iter_init, dim3(cdiv(std::max<int64_t>({(int64_t)N + 1, T, 6 * MSH}), 256)), dim3(256), 0, st,
-                       g->w_t.p, g->u_o.p, N, T, g->T_all > 0 ? g->T_all : (int64_t)T, g->spb[0].p, g->sub[0].p,
+    if (tr && T) hipLaunchKernelGGL(k_tr_gather, dim3(cdiv(T, 256)), dim3(256), 0, st, g->c_t.p, g->tperm.p, T, g->c_tp.p);
+    hipLaunchKernelGGL(k_iter_init, dim3(cdiv(std::max<int64_t>({(int64_t)N + TR_PAD, T, 6 * MSH}), 256)), dim3(256), 0, st,
+                       tr ? g->w_tp.p : g->w_t.p, g->u_o.p, N, T, g->T_all > 0 ? g->T_all : (int64_t)T, g->spb[0].p, g->sub[0].p,
                        g->sub[1].p, g->q64[0].p, g->q32[0].p, (int)fp32, g->mslot.p,
                        g->relabeled ? (const int32_t*)g->perm.p : nullptr);
     MR_DEBUG_CHECK(ctx, "k_iter_init");
@@ -2074,7 +2419,12 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         v.rs16 = g->rs16.p;
         v.rsw = g->relabeled ? g->rsp.p : g->rs16.p;
         v.perm = g->relabeled ? g->perm.p : nullptr;
-        v.n_hot = plan.v2 && plan.mode == WV_SU_HOT ? WvLds(g->N, plan.NT, WV_SU_HOT).n_hot : 0;
+        v.n_hot = plan_n_hot(g->N, plan);
+        v.tids = g->tids.p;
+        v.coff = g->coff.p;
+        v.wtile = g->wtile.p;
+        v.c_tp = g->c_tp.p;
+        v.w_tp = g->w_tp.p;
         v.c_t = g->c_t.p;
         v.w_t = g->w_t.p;
         v.u_o = g->u_o.p;
@@ -2102,13 +2452,16 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         v.stamp = nullptr;
         // a shard without traces still runs one (empty) block: it clears the maxima slot and
         // writes a zero partial row, and the collectives after the launch need every rank
-        const int64_t nfa = g->fused ? std::max<int64_t>(fused_blocks(g->T, g->N, plan, TT), sharded ? 1 : 0) : 0;
+        int64_t nfa = 0;
+        if (g->fused) MR_TRY(fused_blocks(ctx, g, plan, TT, &nfa));
+        nfa = g->fused ? std::max<int64_t>(nfa, sharded ? 1 : 0) : 0;
         // a row entry stays below 2^63; shards of one graph hold different trace counts, and their
         // limbs are summed, so they share the scale of the largest block (2^15 traces)
         // v1: a row entry stays below 2^63; v2: below 2^64 (traces per block < 2^(64-sc)).
         // Shards of one graph hold different trace counts and their limbs are summed, so they
         // share one scale, 2^48 (<= 65535 traces per block: wv_blocks / fx_blocks)
-        const int64_t tpb = cdiv(cdiv((int64_t)g->T, TT), std::max<int64_t>(nfa, 1)) * TT;
+        const int64_t tpb = plan.tr && g->fused ? (int64_t)g->wtile_tpb * WAVE
+                                                : cdiv(cdiv((int64_t)g->T, TT), std::max<int64_t>(nfa, 1)) * TT;
         const int sc = sharded ? 48
                                : plan.v2 ? 64 - bits_for((uint64_t)std::max<int64_t>(tpb, 1))
                                          : 63 - bits_for((uint64_t)std::max<int64_t>(tpb - 1, 1));
@@ -2154,8 +2507,8 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
     const FxA fx_a = fx_kernel(fp32, sul, multi, fx_S);
     for (int i = 0; i < ng; ++i)
         if (gs[i]->fused)
-            lds_f = std::max(lds_f, plan.v2 ? WvLds(gs[i]->N, plan.NT, plan.mode).total : FxLds(gs[i]->N, TT, fx_S * TT, sul).total);
-    const WvA sg_a = plan.v2 ? wv_kernel(fp32, plan.mode, plan.NT) : nullptr;
+            lds_f = std::max(lds_f, plan.v2 ? plan_lds(gs[i]->N, plan) : FxLds(gs[i]->N, TT, fx_S * TT, sul).total);
+    const WvA sg_a = plan.tr ? tr_kernel(fp32, plan.mode, plan.NT) : plan.v2 ? wv_kernel(fp32, plan.mode, plan.NT) : nullptr;
     const int fx_bs = plan.v2 ? plan.NT : fx_S * TT;
     // a sharded graph with no collective backend is one whole shard: the split launches around the
     // (no-op) all-reduces would compute the same integers / sums in two halves
