@@ -271,23 +271,14 @@ constexpr uint64_t KCHK_SEED = 0x0ddba11cafeull;
 // trace are distinct and ascending, so the set is the list).  The walk-per-thread form (int32
 // ids) reads one trace per lane, ~60 B apart.  Either hash only buckets traces; membership is
 // decided by k_kind_verify's exact comparison.
+// Set hashes of the block's KB traces (tb = first trace): U16 -- the cooperative walk below,
+// through per-trace LDS sums (loff, lacc, lacc2: KB + 1 / KB / KB entries); else a walk per
+// thread.  Every thread of the block must call it; *h (and *h2 with CHK) is set for t < T.
 template <bool CHK, bool U16>
-__global__ void __launch_bounds__(KB) k_kind_insert(const int64_t* off, const int32_t* ops, const uint16_t* o16,
-                                                    const float* w_t, int32_t T, unsigned long long* hk, KCnt* cr, int32_t* slot_of,
-                                                    uint64_t mask, uint64_t seed, uint64_t* chk, uint64_t hmask) {
-    __shared__ unsigned long long lkey[KLDS];
-    __shared__ uint32_t lcnt[KLDS];
-    __shared__ int32_t lrep[KLDS];
-    __shared__ int32_t lglob[KLDS];
-    __shared__ uint64_t lchk[CHK ? KLDS : 1];
-    __shared__ int64_t loff[U16 ? KB + 1 : 1];
-    __shared__ unsigned long long lacc[U16 ? KB : 1], lacc2[U16 && CHK ? KB : 1];
-    for (int i = threadIdx.x; i < KLDS; i += KB) {
-        lkey[i] = 0ull;
-        lcnt[i] = 0u;
-        lrep[i] = -1;
-    }
-    const int32_t tb = blockIdx.x * KB;
+__device__ __forceinline__ void kind_block_hash(const int64_t* off, const int32_t* ops, const uint16_t* o16,
+                                                const float* w_t, int32_t T, int32_t tb, uint64_t seed, int64_t* loff,
+                                                unsigned long long* lacc, unsigned long long* lacc2, uint64_t* h,
+                                                uint64_t* h2) {
     const int32_t t = tb + threadIdx.x;
     if (U16) {
         const int nt = min(KB, T - tb);
@@ -337,18 +328,43 @@ __global__ void __launch_bounds__(KB) k_kind_insert(const int64_t* off, const in
                 if (CHK) atomicAdd(&lacc2[lt], a2);
             }
         }
+        __syncthreads();
     }
-    __syncthreads();
-    int myslot = -1;
     if (t < T) {
-        uint64_t h2 = 0, h;
         if (U16) {
             const int64_t n = loff[threadIdx.x + 1] - loff[threadIdx.x];
             const uint64_t wb = n > 0 ? (uint64_t)__float_as_uint(w_t[t]) : 0ull;
-            h = kind_fold(seed, wb, n, lacc[threadIdx.x]);
-            if (CHK) h2 = kind_fold(KCHK_SEED, wb, n, lacc2[threadIdx.x]);
-        } else
-            h = kind_hash2<CHK>(off, ops, w_t, t, seed, KCHK_SEED, &h2);
+            *h = kind_fold(seed, wb, n, lacc[threadIdx.x]);
+            if (CHK) *h2 = kind_fold(KCHK_SEED, wb, n, lacc2[threadIdx.x]);
+        } else {
+            *h = kind_hash2<CHK>(off, ops, w_t, t, seed, KCHK_SEED, h2);
+        }
+    }
+}
+
+template <bool CHK, bool U16>
+__global__ void __launch_bounds__(KB) k_kind_insert(const int64_t* off, const int32_t* ops, const uint16_t* o16,
+                                                    const float* w_t, int32_t T, unsigned long long* hk, KCnt* cr, int32_t* slot_of,
+                                                    uint64_t mask, uint64_t seed, uint64_t* chk, uint64_t hmask) {
+    __shared__ unsigned long long lkey[KLDS];
+    __shared__ uint32_t lcnt[KLDS];
+    __shared__ int32_t lrep[KLDS];
+    __shared__ int32_t lglob[KLDS];
+    __shared__ uint64_t lchk[CHK ? KLDS : 1];
+    __shared__ int64_t loff[U16 ? KB + 1 : 1];
+    __shared__ unsigned long long lacc[U16 ? KB : 1], lacc2[U16 && CHK ? KB : 1];
+    for (int i = threadIdx.x; i < KLDS; i += KB) {
+        lkey[i] = 0ull;
+        lcnt[i] = 0u;
+        lrep[i] = -1;
+    }
+    const int32_t tb = blockIdx.x * KB;
+    const int32_t t = tb + threadIdx.x;
+    uint64_t h = 0, h2 = 0;
+    kind_block_hash<CHK, U16>(off, ops, o16, w_t, T, tb, seed, loff, lacc, lacc2, &h, &h2);
+    __syncthreads();
+    int myslot = -1;
+    if (t < T) {
         h &= hmask;   // ~0 (tests narrow it to force collisions)
         if (!h) h = 1;
         int s = (int)(h & (KLDS - 1));
@@ -396,6 +412,141 @@ __global__ void k_kind_verify(const int64_t* off, const ID* ops, const float* w_
     bool eq = (a1 - a0) == (b1 - b0);
     if (eq && a1 > a0) eq = __float_as_uint(w_t[t]) == __float_as_uint(w_t[r]);
     for (int64_t i = 0; eq && i < a1 - a0; ++i) eq = ops[a0 + i] == ops[b0 + i];
+    if (!eq) atomicOr(flag, 1);
+}
+
+// Kinds by partition (graphs on one rank), no global hash table:
+//   k_kind_rec     per block of KB traces: set hashes, equal keys merged in an LDS table into
+//                  RECORDS (key, count, first trace) -- a hot kind (thousands of traces on one
+//                  call path) leaves one record per block, so no later atomic serialises on it --
+//                  and the records counted per partition (the key's top bits);
+//   k_kind_rscatter a counting sort of the records into partitions of ~KP_MEAN;
+//   k_kind_part    a block per partition merges its records in an LDS table (count sum, first
+//                  trace min): every record then holds its class's size and representative;
+//   k_kind_final   per trace: kind = its record's class size; every member is checked against
+//                  the representative (ops and fp32(1/len_t), exactly): a hash collision raises
+//                  flag word 0 (retry with the next seed), never a miscount.
+constexpr int KP_MEAN = 1024;   // mean records per partition (at most)
+constexpr int KP_LDS = 4096;    // LDS table slots of a partition block
+constexpr int KP_B = 256;
+__device__ __forceinline__ int32_t kind_part(uint64_t h, int pb) { return pb ? (int32_t)(h >> (64 - pb)) : 0; }
+template <bool U16>
+__global__ void __launch_bounds__(KB) k_kind_rec(const int64_t* off, const int32_t* ops, const uint16_t* o16,
+                                                 const float* w_t, int32_t T, uint64_t seed, uint64_t hmask, int pb,
+                                                 uint64_t* rh, uint32_t* rc, int32_t* rr, int32_t* nrec, int32_t* rec_of,
+                                                 int32_t* hist) {
+    __shared__ unsigned long long lkey[KLDS];
+    __shared__ uint32_t lcnt[KLDS];
+    __shared__ int32_t lrep[KLDS];
+    __shared__ int32_t lidx[KLDS];
+    __shared__ int32_t ln;
+    __shared__ int64_t loff[U16 ? KB + 1 : 1];
+    __shared__ unsigned long long lacc[U16 ? KB : 1], lacc2[1];
+    for (int i = threadIdx.x; i < KLDS; i += KB) {
+        lkey[i] = 0ull;
+        lcnt[i] = 0u;
+        lrep[i] = 0x7fffffff;
+    }
+    if (threadIdx.x == 0) ln = 0;
+    const int32_t tb = blockIdx.x * KB, t = tb + threadIdx.x;
+    uint64_t h = 0, h2 = 0;
+    kind_block_hash<false, U16>(off, ops, o16, w_t, T, tb, seed, loff, lacc, lacc2, &h, &h2);
+    __syncthreads();
+    int s = -1;
+    if (t < T) {
+        h &= hmask;   // ~0 (tests narrow it to force collisions)
+        if (!h) h = 1;
+        s = (int)(h & (KLDS - 1));
+        for (;;) {   // <= KB distinct keys in KLDS = 2 KB slots: always a free slot
+            const unsigned long long k = atomicCAS(&lkey[s], 0ull, (unsigned long long)h);
+            if (k == 0ull || k == h) break;
+            s = (s + 1) & (KLDS - 1);
+        }
+        atomicAdd(&lcnt[s], 1u);
+        atomicMin(&lrep[s], t);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < KLDS; i += KB) {
+        const uint64_t k = lkey[i];
+        if (!k) continue;
+        const int32_t r = atomicAdd(&ln, 1);   // record order within the block: free (sums / mins)
+        lidx[i] = r;
+        const int64_t rec = (int64_t)tb + r;
+        rh[rec] = k;
+        rc[rec] = lcnt[i];
+        rr[rec] = lrep[i];
+        atomicAdd(&hist[kind_part(k, pb)], 1);
+    }
+    __syncthreads();
+    if (t < T) rec_of[t] = tb + lidx[s];
+    if (threadIdx.x == 0) nrec[blockIdx.x] = ln;
+}
+__global__ void k_kind_rscatter(const uint64_t* rh, const uint32_t* rc, const int32_t* rr, const int32_t* nrec,
+                                int32_t T, int pb, unsigned long long* cur, uint64_t* eh, uint32_t* ec, int32_t* er,
+                                int32_t* rpos) {
+    const int32_t rec = blockIdx.x * blockDim.x + threadIdx.x;
+    if (rec >= T || (rec % KB) >= nrec[rec / KB]) return;
+    const uint64_t k = rh[rec];
+    const int32_t pos = (int32_t)atomicAdd(&cur[kind_part(k, pb)], 1ull);
+    eh[pos] = k;
+    ec[pos] = rc[rec];
+    er[pos] = rr[rec];
+    rpos[rec] = pos;
+}
+__global__ void __launch_bounds__(KP_B) k_kind_part(const int64_t* pstart, const uint64_t* eh, uint32_t* ec, int32_t* er,
+                                                    int32_t* flag) {
+    __shared__ unsigned long long tkey[KP_LDS];
+    __shared__ uint32_t tcnt[KP_LDS];
+    __shared__ int32_t trep[KP_LDS];
+    const int64_t b = pstart[blockIdx.x], e = pstart[blockIdx.x + 1];
+    for (int i = threadIdx.x; i < KP_LDS; i += KP_B) {
+        tkey[i] = 0ull;
+        tcnt[i] = 0u;
+        trep[i] = 0x7fffffff;
+    }
+    __syncthreads();
+    for (int64_t i = b + threadIdx.x; i < e; i += KP_B) {
+        const uint64_t h = eh[i];
+        int s = (int)(h & (KP_LDS - 1));
+        for (int probe = 0;; ++probe) {
+            if (probe == KP_LDS) {   // more distinct keys than slots: not with hashed partitions
+                atomicOr(flag + 2, 1);
+                break;
+            }
+            const unsigned long long k = atomicCAS(&tkey[s], 0ull, (unsigned long long)h);
+            if (k == 0ull || k == h) {
+                atomicAdd(&tcnt[s], ec[i]);
+                atomicMin(&trep[s], er[i]);   // the class's first trace (deterministic)
+                break;
+            }
+            s = (s + 1) & (KP_LDS - 1);
+        }
+    }
+    __syncthreads();
+    for (int64_t i = b + threadIdx.x; i < e; i += KP_B) {
+        const uint64_t h = eh[i];
+        int s = (int)(h & (KP_LDS - 1));
+        for (int probe = 0; probe < KP_LDS && tkey[s] != h; ++probe) s = (s + 1) & (KP_LDS - 1);
+        if (tkey[s] != h) continue;   // (overflowed: flagged above)
+        ec[i] = tcnt[s];
+        er[i] = trep[s];
+    }
+}
+template <typename ID>
+__global__ void k_kind_final(const int32_t* rec_of, const int32_t* rpos, const uint32_t* ec, const int32_t* er,
+                             const int64_t* off, const ID* ops, const float* w_t, int32_t T, double* kind,
+                             int32_t* flag) {
+    const int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= T) return;
+    const int32_t pos = rpos[rec_of[t]];
+    kind[t] = (double)ec[pos];
+    const int32_t r = er[pos];
+    if (r == t) return;
+    // exact membership: same ids and the same fp32(1/len_t) as the representative
+    const int64_t a0 = off[t], a1 = off[t + 1], b0 = off[r], b1 = off[r + 1];
+    bool eq = (a1 - a0) == (b1 - b0);
+    if (eq && a1 > a0) eq = __float_as_uint(w_t[t]) == __float_as_uint(w_t[r]);
+    for (int64_t j = 0; eq && j < a1 - a0; ++j) eq = ops[a0 + j] == ops[b0 + j];
     if (!eq) atomicOr(flag, 1);
 }
 
@@ -1503,6 +1654,9 @@ __global__ void __launch_bounds__(NT) k_wv_a(const GDev* __restrict__ gs, int32_
 }
 
 // ---------------------------------------------------------------- fused iteration, trace-parallel (k_tr_a)
+#ifndef MR_TREXP
+#define MR_TREXP 0   // timing experiments only: 1 atomics / 2 su reads at conflict-free addresses
+#endif
 // The single-pass iteration with lane = trace.  At prepare a graph's traces are sorted by op
 // count (tperm: position -> trace) and cut into wave tiles of 64 positions; a tile stores its
 // traces' ids lane-interleaved in chunks of 4 (chunk c = 64 lanes x 4 u16: one coalesced 512-B
@@ -1520,17 +1674,19 @@ struct TrLds {
     size_t su, lacc, total;
     bool su_lds;      // every op's su fits beside the accumulator (interleaved: 16 B per op)
     int32_t n_hot;    // WV_SU_HOT: su of ops [0, n_hot) in LDS
+    // the accumulator first, then su (8-B strides: a 32-lane read group spreads over 32 bank
+    // pairs, a 16-lane atomic group over 16)
     __host__ __device__ TrLds(int32_t N, int mode) {
         const size_t ns = (size_t)N + TR_PAD;
         su_lds = ns * 16 <= WV_LDS_MAX;
         const bool all = mode == WV_SU_ALL && su_lds;
-        const size_t accb = (ns * (all ? 16 : 8) + 15) / 16 * 16;
+        const size_t accb = (ns * 8 + 15) / 16 * 16;
         n_hot = 0;
         if (mode == WV_SU_HOT && accb < WV_LDS_MAX)
             n_hot = (int32_t)std::min<size_t>((size_t)N, (WV_LDS_MAX - accb) / 8 / 64 * 64);
-        lacc = all ? 8 : 0;
-        su = all ? 0 : accb;
-        total = all ? accb : accb + (size_t)n_hot * 8;
+        lacc = 0;
+        su = accb;
+        total = all ? 2 * accb : accb + (size_t)n_hot * 8;
     }
 };
 
@@ -1538,7 +1694,7 @@ template <class Q, int SUM, int NT>
 __global__ void __launch_bounds__(NT) k_tr_a(const GDev* __restrict__ gs, int32_t ng, int32_t split, double d,
                                              double alpha, int it, int32_t unused) {
     constexpr bool SUL = SUM == WV_SU_ALL, HOT = SUM == WV_SU_HOT;
-    constexpr int NW = NT / WAVE, AS = SUL ? 2 : 1;
+    constexpr int NW = NT / WAVE;
     extern __shared__ __attribute__((aligned(16))) unsigned char lraw[];
     __shared__ double red[NW];
     __shared__ double msh[2];
@@ -1567,8 +1723,8 @@ __global__ void __launch_bounds__(NT) k_tr_a(const GDev* __restrict__ gs, int32_
     int32_t k = __builtin_amdgcn_readfirstlane(wt[0]);
     const int32_t ke = __builtin_amdgcn_readfirstlane(wt[1]);
     for (int32_t o = tid; o < N + TR_PAD; o += NT) {
-        if (SUL) su_l[AS * o] = sug[o];
-        lacc[AS * o] = 0ull;
+        if (SUL) su_l[o] = sug[o];
+        lacc[o] = 0ull;
     }
     if (HOT)
         for (int32_t o = tid; o < NH; o += NT) su_l[o] = sug[o];
@@ -1595,58 +1751,76 @@ __global__ void __launch_bounds__(NT) k_tr_a(const GDev* __restrict__ gs, int32_
         int32_t c = __builtin_amdgcn_readfirstlane(coff[k]);
         int32_t ce = __builtin_amdgcn_readfirstlane(coff[k + 1]);   // end of tile k
         const int32_t cl = __builtin_amdgcn_readfirstlane(coff[ke]) - 1;   // the run's last chunk
-        // tile k's words; tile k + 1's q and end chunk (one tile ahead, clamped into the run)
+        // tile k's words; tile k + 1's q and end chunk (one tile ahead, clamped into the run).  The
+        // end chunk is loaded per lane (lane-varying address: a vector load -- a scalar load would
+        // share lgkmcnt with the LDS traffic and force full drains)
         const int32_t kn = min(k + 1, ke - 1);
         double q_cur = (double)qc[pos(k)];
         float c_cur = c_tp[pos(k)], w_cur = w_tp[pos(k)];
         double q_nx = (double)qc[pos(kn)];
-        int32_t ce_nx = coff[kn + 1];
-        u32x2 w0 = ids[(size_t)c * WAVE];
-        u32x2 w1 = ids[(size_t)min(c + 1, cl) * WAVE];
-        u32x2 w2 = ids[(size_t)min(c + 2, cl) * WAVE];
-        double g0[4], g1[4];
-        if (!SUL) gather(w0, g0);
-        unsigned long long X = k * WAVE + lane < T ? (unsigned long long)__double2ull_rn(q_cur * xsc) : 0ull;
-        double acc = 0.0;
-        for (;;) {
-            // chunk c: ids w0 (here), cold su g0 (in flight); ids w1, w2 in flight
-            const u32x2 w3 = ids[(size_t)min(c + 3, cl) * WAVE];
-            if (!SUL) gather(w1, g1);
-            const int32_t o[4] = {(int32_t)(w0.x & 0xffffu), (int32_t)(w0.x >> 16), (int32_t)(w0.y & 0xffffu),
-                                  (int32_t)(w0.y >> 16)};
+        int32_t ce_nx = coff[min(kn + 1 + lane, ke)];
+        // su of a chunk's ops from LDS (HOT: the hot part; the cold part comes from gather)
+        auto lds_su = [&](const u32x2 w, double* sv) {
+            const int32_t o[4] = {(int32_t)(w.x & 0xffffu), (int32_t)(w.x >> 16), (int32_t)(w.y & 0xffffu),
+                                  (int32_t)(w.y >> 16)};
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const double g = SUL ? su_l[AS * o[j]] : HOT ? (o[j] < NH ? su_l[min(o[j], NH - 1)] : g0[j]) : g0[j];
-                acc += g;
+                const int32_t orr = (MR_TREXP & 2) ? N + lane : o[j];   // (timing experiment: no conflicts)
+                sv[j] = SUL ? su_l[orr] : HOT ? su_l[min(orr, NH - 1)] : 0.0;
             }
-#pragma unroll
-            for (int j = 0; j < 4; ++j) atomicAdd(&lacc[AS * o[j]], X);
-            w0 = w1;
-            w1 = w2;
-            w2 = w3;
-            if (!SUL) {
-#pragma unroll
-                for (int j = 0; j < 4; ++j) g0[j] = g1[j];
-            }
-            if (++c == ce) {
-                // ---- tile k done: r' of its traces (pagerank.py:125) and the next q
-                const int32_t p = k * WAVE + lane;
-                const bool own = p < T;
-                const double rp = d * (acc / Ms) + (double)c_cur;
-                if (own) rmax = nmax(rmax, rp);
-                qn[own ? p : T] = (Q)((double)w_cur * rp);   // q[T]: pad slot
-                if (++k == ke) break;
-                ce = __builtin_amdgcn_readfirstlane(ce_nx);
-                q_cur = q_nx;
-                const int32_t kk = min(k + 1, ke - 1);
-                c_cur = c_tp[pos(k)];
-                w_cur = w_tp[pos(k)];
-                q_nx = (double)qc[pos(kk)];
-                ce_nx = coff[kk + 1];
-                X = k * WAVE + lane < T ? (unsigned long long)__double2ull_rn(q_cur * xsc) : 0ull;
-                acc = 0.0;
-            }
+        };
+        // ids ring (4 chunks: the current one and three ahead), su ping-pong (current, next)
+        u32x2 wa = ids[(size_t)c * WAVE];
+        u32x2 wb = ids[(size_t)min(c + 1, cl) * WAVE];
+        u32x2 wc = ids[(size_t)min(c + 2, cl) * WAVE];
+        u32x2 wd;
+        double gA[4], gB[4], sA[4], sB[4];
+        if (!SUL) gather(wa, gA);
+        if (SUL || HOT) lds_su(wa, sA);
+        unsigned long long X = k * WAVE + lane < T ? (unsigned long long)__double2ull_rn(q_cur * xsc) : 0ull;
+        double acc = 0.0;
+        // One chunk: ids CUR (here), su SC / GC (LDS here, cold gathers in flight); NXT's cold
+        // gathers and LDS reads go out before CUR's atomics (their latency, bank conflicts
+        // included, overlaps a whole chunk), and the ids three chunks ahead land in LD.  The loop
+        // is unrolled 4x so the ring rotates by renaming, not by register moves (a move of an
+        // in-flight register would wait for it).
+#define TR_STEP(CUR, NXT, LD, GC, SC, GN, SN)                                                              \
+        {                                                                                                  \
+            LD = ids[(size_t)min(c + 3, cl) * WAVE];                                                       \
+            if (!SUL) gather(NXT, GN);                                                                     \
+            if (SUL || HOT) lds_su(NXT, SN);                                                               \
+            const int32_t o_[4] = {(int32_t)(CUR.x & 0xffffu), (int32_t)(CUR.x >> 16),                     \
+                                   (int32_t)(CUR.y & 0xffffu), (int32_t)(CUR.y >> 16)};                    \
+            _Pragma("unroll") for (int j = 0; j < 4; ++j) atomicAdd(&lacc[(MR_TREXP & 1) ? N + lane : o_[j]], X); \
+            _Pragma("unroll") for (int j = 0; j < 4; ++j)                                                  \
+                acc += SUL ? SC[j] : HOT ? (o_[j] < NH ? SC[j] : GC[j]) : GC[j];                          \
+            if (++c == ce) {                                                                               \
+                /* tile k done: r' of its traces (pagerank.py:125) and the next q */                      \
+                const int32_t p_ = k * WAVE + lane;                                                        \
+                const bool own_ = p_ < T;                                                                  \
+                const double rp_ = d * (acc / Ms) + (double)c_cur;                                         \
+                if (own_) rmax = nmax(rmax, rp_);                                                          \
+                qn[own_ ? p_ : T] = (Q)((double)w_cur * rp_);   /* q[T]: pad slot */                      \
+                if (++k == ke) goto tr_done;                                                               \
+                ce = __builtin_amdgcn_readfirstlane(ce_nx);                                                \
+                q_cur = q_nx;                                                                              \
+                const int32_t kk_ = min(k + 1, ke - 1);                                                    \
+                c_cur = c_tp[pos(k)];                                                                      \
+                w_cur = w_tp[pos(k)];                                                                      \
+                q_nx = (double)qc[pos(kk_)];                                                               \
+                ce_nx = coff[min(kk_ + 1 + lane, ke)];                                                     \
+                X = p_ + WAVE < T ? (unsigned long long)__double2ull_rn(q_cur * xsc) : 0ull;               \
+                acc = 0.0;                                                                                 \
+            }                                                                                              \
         }
+        for (;;) {
+            TR_STEP(wa, wb, wd, gA, sA, gB, sB)
+            TR_STEP(wb, wc, wa, gB, sB, gA, sA)
+            TR_STEP(wc, wd, wb, gA, sA, gB, sB)
+            TR_STEP(wd, wa, wc, gB, sB, gA, sA)
+        }
+#undef TR_STEP
+    tr_done:;
     }
     // call-graph term for the next s' (pagerank.py:122-124, alpha P_ss s_k), a thread per op
     {
@@ -1666,7 +1840,7 @@ __global__ void __launch_bounds__(NT) k_tr_a(const GDev* __restrict__ gs, int32_
     }
     __syncthreads();
     GLB unsigned long long* prow = gpw(G.fx_part) + (size_t)lb * N;
-    for (int32_t o = tid; o < N; o += NT) prow[o] = lacc[AS * o];
+    for (int32_t o = tid; o < N; o += NT) prow[o] = lacc[o];
     rmax = block_max(rmax, red);
     if (tid == 0 && rmax >= 0.0)   // -inf: a block without traces (an empty shard's placeholder)
         atomicMax((unsigned long long*)&Mnext[MSH + blockIdx.x % MSH], d2bits(rmax));
@@ -2281,8 +2455,16 @@ static int pagerank_setup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool 
                           const FxPlan& plan, bool sharded, uint64_t seed, uint64_t hmask) {
     hipStream_t st = ctx->stream;
     const int32_t N = g->N, T = g->T;
+    // Kinds through a global hash table (k_kind_insert) while it stays cache-resident, and for one
+    // shard of a multi-rank graph (the cross-rank merge needs its classes and a check hash per
+    // class); larger graphs by partition (k_kind_rec .. k_kind_final: no table of random atomics)
+    const bool chk = sharded && ctx->nranks > 1;
     uint64_t cap = 1;
     while (cap < 2ull * (uint64_t)T) cap <<= 1;
+    const char* kpe = getenv("MR_KIND_PART_MIN");   // test knob (read per call): traces from which the partition path runs
+    const int64_t kp_min = kpe ? (int64_t)atoll(kpe) : (int64_t)(1 << 21);
+    const bool ktab = chk || (int64_t)T < kp_min;
+    if (!ktab) cap = 0;
     const int32_t n_pr = g->n_pr;
     const int nbp = cdiv(n_pr > 0 ? n_pr : 1, TB);
     MR_TRY(g->kind.alloc(ctx, (size_t)T));
@@ -2291,9 +2473,11 @@ static int pagerank_setup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool 
     MR_TRY(g->flag.alloc(ctx, 4));
     MR_TRY(g->scal.alloc(ctx, 8));
     MR_TRY(g->ppart.alloc(ctx, 2 * (size_t)nbp));
-    MR_TRY(g->ht_key.alloc(ctx, cap));
-    MR_TRY(g->ht_cr.alloc(ctx, cap));
-    MR_TRY(g->slot_of.alloc(ctx, (size_t)T));
+    if (ktab) {
+        MR_TRY(g->ht_key.alloc(ctx, cap));
+        MR_TRY(g->ht_cr.alloc(ctx, cap));
+        MR_TRY(g->slot_of.alloc(ctx, (size_t)T));
+    }
     MR_TRY(g->mslot.alloc(ctx, 6 * MSH));
     MR_TRY(g->sn.alloc(ctx, (size_t)N));
     MR_TRY(g->spb[0].alloc(ctx, (size_t)N));
@@ -2322,25 +2506,64 @@ static int pagerank_setup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool 
     // ---- kinds
     const int64_t* koff = g->rs_is_sr ? g->rs_off.p : g->srt_off.p;
     const int32_t* kops = g->rs_is_sr ? g->rs_ops.p : g->srt_ops.p;
-    // one shard of a multi-rank graph: the cross-rank merge needs a check hash per class
-    const bool chk = sharded && ctx->nranks > 1;
-    if (chk) MR_TRY(g->ht_chk.alloc(ctx, cap));
     static const bool no_u16 = getenv("MR_KIND_WALK") != nullptr;   // A/B knob: per-thread int32 walk
     const bool u16 = !no_u16 && g->rs_is_sr && g->rs16.p != nullptr;   // rs16 = u16 copy of rs_ops
-    auto kins = chk ? (u16 ? k_kind_insert<true, true> : k_kind_insert<true, false>)
-                    : (u16 ? k_kind_insert<false, true> : k_kind_insert<false, false>);
-    if (T)
-        hipLaunchKernelGGL(kins, dim3(cdiv(T, KB)), dim3(KB), 0, st, koff, kops, (const uint16_t*)g->rs16.p, g->w_t.p,
-                           T, g->ht_key.p, g->ht_cr.p, g->slot_of.p, (uint64_t)(cap - 1), seed,
-                           chk ? g->ht_chk.p : (uint64_t*)nullptr, hmask);
-    MR_DEBUG_CHECK(ctx, "k_kind_insert");
-    if (T && u16)
-        hipLaunchKernelGGL(k_kind_verify<uint16_t>, dim3(cdiv(T, 256)), dim3(256), 0, st, koff,
-                           (const uint16_t*)g->rs16.p, g->w_t.p, T, g->ht_cr.p, g->slot_of.p, g->kind.p, g->flag.p);
-    else if (T)
-        hipLaunchKernelGGL(k_kind_verify<int32_t>, dim3(cdiv(T, 256)), dim3(256), 0, st, koff, kops, g->w_t.p, T,
-                           g->ht_cr.p, g->slot_of.p, g->kind.p, g->flag.p);
-    MR_DEBUG_CHECK(ctx, "k_kind_verify");
+    if (ktab) {
+        if (chk) MR_TRY(g->ht_chk.alloc(ctx, cap));
+        auto kins = chk ? (u16 ? k_kind_insert<true, true> : k_kind_insert<true, false>)
+                        : (u16 ? k_kind_insert<false, true> : k_kind_insert<false, false>);
+        if (T)
+            hipLaunchKernelGGL(kins, dim3(cdiv(T, KB)), dim3(KB), 0, st, koff, kops, (const uint16_t*)g->rs16.p, g->w_t.p,
+                               T, g->ht_key.p, g->ht_cr.p, g->slot_of.p, (uint64_t)(cap - 1), seed,
+                               chk ? g->ht_chk.p : (uint64_t*)nullptr, hmask);
+        MR_DEBUG_CHECK(ctx, "k_kind_insert");
+        if (T && u16)
+            hipLaunchKernelGGL(k_kind_verify<uint16_t>, dim3(cdiv(T, 256)), dim3(256), 0, st, koff,
+                               (const uint16_t*)g->rs16.p, g->w_t.p, T, g->ht_cr.p, g->slot_of.p, g->kind.p, g->flag.p);
+        else if (T)
+            hipLaunchKernelGGL(k_kind_verify<int32_t>, dim3(cdiv(T, 256)), dim3(256), 0, st, koff, kops, g->w_t.p, T,
+                               g->ht_cr.p, g->slot_of.p, g->kind.p, g->flag.p);
+        MR_DEBUG_CHECK(ctx, "k_kind_verify");
+    } else if (T) {
+        // partitions P = 2^pb >= T / KP_MEAN by the hash's top bits (records <= T)
+        const int pb = bits_for((uint64_t)(cdiv(T, KP_MEAN) - 1));
+        const int64_t P = (int64_t)1 << pb;
+        const int32_t nb = cdiv(T, KB);
+        const size_t R = (size_t)nb * KB;
+        DBuf<uint64_t> rh, eh;
+        DBuf<uint32_t> rc, ec;
+        DBuf<int32_t> rr, er, nrec, rec_of, rpos, hist;
+        DBuf<int64_t> pstart, tmp;
+        DBuf<unsigned long long> cur;
+        MR_TRY(rh.alloc(ctx, R));
+        MR_TRY(rc.alloc(ctx, R));
+        MR_TRY(rr.alloc(ctx, R));
+        MR_TRY(rpos.alloc(ctx, R));
+        MR_TRY(eh.alloc(ctx, (size_t)T));
+        MR_TRY(ec.alloc(ctx, (size_t)T));
+        MR_TRY(er.alloc(ctx, (size_t)T));
+        MR_TRY(nrec.alloc(ctx, (size_t)nb));
+        MR_TRY(rec_of.alloc(ctx, (size_t)T));
+        MR_TRY(hist.zero(ctx, (size_t)P));
+        MR_TRY(pstart.alloc(ctx, (size_t)P + 1));
+        MR_TRY(cur.alloc(ctx, (size_t)P));
+        MR_TRY(tmp.alloc(ctx, (size_t)scan_tmp_elems(P)));
+        auto krec = u16 ? k_kind_rec<true> : k_kind_rec<false>;
+        hipLaunchKernelGGL(krec, dim3(nb), dim3(KB), 0, st, koff, kops, (const uint16_t*)g->rs16.p, g->w_t.p, T, seed,
+                           hmask, pb, rh.p, rc.p, rr.p, nrec.p, rec_of.p, hist.p);
+        MR_TRY(mr_exclusive_scan_i32(ctx, hist.p, pstart.p, P, tmp.p));
+        MR_TRY_HIP(ctx, hipMemcpyAsync(cur.p, pstart.p, (size_t)P * sizeof(int64_t), hipMemcpyDeviceToDevice, st));
+        hipLaunchKernelGGL(k_kind_rscatter, dim3(cdiv((int64_t)R, 256)), dim3(256), 0, st, rh.p, rc.p, rr.p, nrec.p,
+                           (int32_t)std::min<size_t>(R, 0x7fffffff), pb, cur.p, eh.p, ec.p, er.p, rpos.p);
+        hipLaunchKernelGGL(k_kind_part, dim3((uint32_t)P), dim3(KP_B), 0, st, pstart.p, eh.p, ec.p, er.p, g->flag.p);
+        if (u16)
+            hipLaunchKernelGGL(k_kind_final<uint16_t>, dim3(cdiv(T, 256)), dim3(256), 0, st, rec_of.p, rpos.p, ec.p, er.p,
+                               koff, (const uint16_t*)g->rs16.p, g->w_t.p, T, g->kind.p, g->flag.p);
+        else
+            hipLaunchKernelGGL(k_kind_final<int32_t>, dim3(cdiv(T, 256)), dim3(256), 0, st, rec_of.p, rpos.p, ec.p, er.p,
+                               koff, kops, g->w_t.p, T, g->kind.p, g->flag.p);
+        MR_DEBUG_CHECK(ctx, "k_kind_part");
+    }
     if (chk) MR_TRY(shard_kinds(ctx, g, cap));   // class sizes over all ranks (one rank: already global)
     // ---- preference
     const int32_t* prt = g->pr_identity ? nullptr : g->pr_trace.p;
@@ -2591,6 +2814,7 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
             *collided = true;
             return MR_OK;
         }
+        if (hflag[(size_t)4 * i + 2] & 1) return mr_fail(ctx, MR_ERR_STATE, "trace kinds: a partition exceeded its table");
         if (anomaly[i] && (hflag[(size_t)4 * i + 1] & 1)) return mr_fail(ctx, MR_ERR_ZERODIV, "float division by zero");
     }
     return MR_OK;

@@ -102,6 +102,30 @@ def test_c2_scale_against_oracle(c2, anomaly):
     dg.close()
 
 
+@pytest.mark.parametrize("part_min", ["0", "1000000000"])
+def test_kinds_partition_and_table_paths(c2, part_min, monkeypatch):
+    """Both kinds paths (the per-partition LDS tables of large graphs, forced here with
+    MR_KIND_PART_MIN=0, and the global hash table) give the oracle's kinds exactly on the C2
+    graph (hot kinds: thousands of traces on one call path), and the same weights bitwise."""
+    from microrank_amd import _lib
+    from microrank_amd.graph import DeviceGraph
+
+    monkeypatch.setenv("MR_KIND_PART_MIN", part_min)
+    st, sg = c2
+    g = sg.as_graph()
+    kind = orc.trace_kinds(g)
+    ctx = _lib.default_context()
+    dg = DeviceGraph.upload(ctx, host_graph_from_oracle(g))
+    dg.pagerank(True)
+    w, cov, k, pref = dg.fetch(kinds=True)
+    np.testing.assert_array_equal(k, kind)
+    monkeypatch.setenv("MR_KIND_PART_MIN", "1000000000" if part_min == "0" else "0")
+    dg.pagerank(True)
+    w2, _ = dg.fetch()
+    assert w2.tobytes() == w.tobytes()
+    dg.close()
+
+
 def _oracle_graph_from_host(hg) -> "orc.Graph":
     T, N = hg.T, hg.N
     sr_t = np.repeat(np.arange(T, dtype=np.int64), np.diff(hg.sr_off))
@@ -154,7 +178,8 @@ def test_large_op_count_multi_tile_long_tiles(anomaly):
     dg.close()
 
 
-def test_kind_hash_collision_retries_with_next_seed(monkeypatch):
+@pytest.mark.parametrize("part_min", [None, "0"])
+def test_kind_hash_collision_retries_with_next_seed(monkeypatch, part_min):
     """MR_KIND_TEST_COLLIDE narrows the first attempt's kind keys to 2 bits, so distinct trace
     kinds share keys: the exact verification must catch it and the call must rerun with the next
     seed, giving the same kinds and weights as an uncollided run (pagerank.py:54-66)."""
@@ -167,6 +192,8 @@ def test_kind_hash_collision_retries_with_next_seed(monkeypatch):
     tnames = sorted(adf["traceID"].unique())
     oo, ot, to, pt = golden_graph_dicts(case["graph_swapped_anomaly"], tnames)
     ref = trace_pagerank(oo, ot, to, pt, True)
+    if part_min is not None:   # the partition path's verification (k_kind_final)
+        monkeypatch.setenv("MR_KIND_PART_MIN", part_min)
     monkeypatch.setenv("MR_KIND_TEST_COLLIDE", "1")
     got = trace_pagerank(oo, ot, to, pt, True)
     assert list(got[0]) == list(ref[0]) and got[1] == ref[1]
