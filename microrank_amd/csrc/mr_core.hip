@@ -3,6 +3,8 @@
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 
 #include "mr_internal.h"
 #include "mr_prim.h"
@@ -157,9 +159,36 @@ void mr_prof_end(mr_ctx* ctx, double bytes) {
     ctx->prof_bytes.push_back(bytes);
 }
 
+static std::mutex g_handles_mu;
+static std::map<void*, std::pair<mr_ctx*, void (*)(void*)>> g_handles;
+void mr_handle_add(mr_ctx* ctx, void* h, void (*del)(void*)) {
+    std::lock_guard<std::mutex> lk(g_handles_mu);
+    g_handles[h] = {ctx, del};
+}
+bool mr_handle_take(void* h) {
+    std::lock_guard<std::mutex> lk(g_handles_mu);
+    return g_handles.erase(h) > 0;
+}
+
 extern "C" void mr_ctx_destroy(mr_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    {   // the context's live handles go first (their buffers return to its pool)
+        std::vector<std::pair<void*, void (*)(void*)>> mine;
+        {
+            std::lock_guard<std::mutex> lk(g_handles_mu);
+            for (auto it = g_handles.begin(); it != g_handles.end();) {
+                if (it->second.first == ctx) {
+                    mine.emplace_back(it->first, it->second.second);
+                    it = g_handles.erase(it);
+                } else {
+                    ++it;
+                }
+            }
+        }
+        for (auto& m : mine) m.second(m.first);
+    }
     mr_comm_destroy(ctx);
     prof_clear(ctx);
     mr_pool_release(ctx);
@@ -249,12 +278,13 @@ extern "C" int mr_graph_upload(mr_ctx* ctx, const mr_graph_desc* d, mr_graph** o
     }
     if ((rc = mr_graph_prepare(ctx, g))) return fail(rc);
     MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));  // host vectors go out of scope
+    mr_handle_add(ctx, g, [](void* h) { delete (mr_graph*)h; });
     *out = g;
     return MR_OK;
 }
 
 extern "C" int mr_graph_free(mr_graph* g) {
-    if (!g) return MR_OK;
+    if (!g || !mr_handle_take(g)) return MR_OK;   // (freed with its context)
     (void)hipSetDevice(g->ctx->device);
     (void)hipStreamSynchronize(g->ctx->stream);
     delete g;

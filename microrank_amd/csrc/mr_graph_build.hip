@@ -454,12 +454,13 @@ extern "C" int mr_spans_upload(mr_ctx* ctx, const mr_span_cols* c, mr_spans** ou
     if (hipGetLastError() != hipSuccess || hipStreamSynchronize(ctx->stream) != hipSuccess)
         return fail(mr_fail(ctx, MR_ERR_HIP, "mr_spans_upload: kernel failure"));
     if ((rc = mr_spans_index(ctx, s))) return fail(rc);
+    mr_handle_add(ctx, s, [](void* h) { delete (mr_spans*)h; });
     *out = s;
     return MR_OK;
 }
 
 extern "C" int mr_spans_free(mr_spans* s) {
-    if (!s) return MR_OK;
+    if (!s || !mr_handle_take(s)) return MR_OK;   // (freed with its context)
     (void)hipSetDevice(s->ctx->device);
     (void)hipStreamSynchronize(s->ctx->stream);
     delete s;
@@ -765,7 +766,9 @@ extern "C" int mr_graph_build(mr_ctx* ctx, const mr_spans* sp, const uint8_t* tr
     MR_TRY_HIP(ctx, hipSetDevice(ctx->device));
     DBuf<uint8_t> mask;
     MR_TRY(mask.upload(ctx, trace_mask, (size_t)sp->n_traces));
-    return mr_graph_build_dev(ctx, sp, mask.p, out, nullptr);
+    MR_TRY(mr_graph_build_dev(ctx, sp, mask.p, out, nullptr));
+    mr_handle_add(ctx, *out, [](void* h) { delete (mr_graph*)h; });
+    return MR_OK;
 }
 
 extern "C" int mr_graph_nodes(const mr_graph* g, int32_t* node_podop, int32_t* trace_code) {

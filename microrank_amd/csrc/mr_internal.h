@@ -229,6 +229,12 @@ struct mr_spans {
 
 int mr_spans_index(mr_ctx* ctx, mr_spans* s);
 
+// Handles given out across the ABI (graphs, span tables) are registered with their context:
+// mr_ctx_destroy frees the ones still live, and freeing a handle that is not registered (its
+// context already destroyed it) does nothing.
+void mr_handle_add(mr_ctx* ctx, void* h, void (*del)(void*));
+bool mr_handle_take(void* h);   // unregister; false when h is not live
+
 // collectives over the context's backend (RCCL communicator or host callback); device buffers
 enum { MR_DT_F64 = 0, MR_DT_I32 = 1, MR_DT_U64 = 2, MR_DT_I64 = 3 };
 int mr_coll_allreduce(mr_ctx* ctx, void* dbuf, int64_t n, int dtype, int op /*0 sum, 1 max*/);

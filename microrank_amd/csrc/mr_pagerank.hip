@@ -688,7 +688,8 @@ struct GDev {
     unsigned long long* mslot;
     unsigned long long* fx_part;
     double* fx_ssv;
-    unsigned long long* fx_limb;   // sharded: [2N] (lo, hi) limb sums per op
+    unsigned long long* fx_limb;   // sharded: [2N] (lo, hi) limb sums per op, then [nranks] r' maxima
+    int32_t rank, nranks;          // sharded: this rank's slot of the r' maxima appended to the sum
     double* op_sum;                // sharded tile path: [N] pair-partial sums per op
     unsigned long long* stamp;   // diagnostics (MR_FX_STAMP): per-block phase clocks, else null
     double fx_scale, fx_iscale;
@@ -708,6 +709,31 @@ __device__ __forceinline__ int32_t graph_of(const GDev* gs, int32_t ng, int32_t 
         if (s <= blk) lo = mid; else hi = mid - 1;
     }
     return lo;
+}
+
+// One collective per sharded iteration: the r' maximum of this rank travels with the per-op sums
+// in a one-hot slot per rank (its bit pattern, or the double itself in an fp64 sum: x + 0 = x),
+// so the SUM all-reduce also delivers every rank's maximum.  put: a wave reduces this rank's MSH
+// shards into slot[rank] and zeroes the other slots; take: the max over the slots joins the shards.
+template <class W>
+__device__ __forceinline__ void rmax_put(const GDev& G, const unsigned long long* Mnext, W* slots, int lane) {
+    const double m = wave_max(bits2d(Mnext[MSH + lane]));
+    for (int j = lane; j < G.nranks; j += WAVE) {
+        if constexpr (sizeof(W) == 8 && (W)0.5 == (W)0) slots[j] = j == G.rank ? (W)d2bits(m) : (W)0;
+        else slots[j] = j == G.rank ? (W)m : (W)0;
+    }
+}
+__device__ __forceinline__ void rmax_take_bits(const unsigned long long* slots, int n, unsigned long long* Mnext, int lane) {
+    unsigned long long b = 0ull;
+    for (int j = lane; j < n; j += WAVE) b = max(b, slots[j]);
+    const double m = wave_max(bits2d(b));
+    if (lane == 0) atomicMax(&Mnext[MSH], d2bits(m));
+}
+__device__ __forceinline__ void rmax_take_f64(const double* slots, int n, unsigned long long* Mnext, int lane) {
+    double b = 0.0;
+    for (int j = lane; j < n; j += WAVE) b = nmax(b, slots[j]);
+    const double m = wave_max(b);
+    if (lane == 0) atomicMax(&Mnext[MSH], d2bits(m));
 }
 
 // trace role inner loop: the block's id range in rounds of VCAP ids, all loads in flight before
@@ -847,10 +873,12 @@ __global__ void __launch_bounds__(TB) k_iter_b(const GDev* __restrict__ gs, int3
         sum = wave_sum(sum);
         if (mode == 1) {
             if (lane == 0) G.op_sum[o] = sum;
+            if (o == 0) rmax_put(G, Mnext, G.op_sum + G.N, lane);   // this rank's r' max, one-hot
             return;
         }
     } else {
         sum = G.op_sum[o];
+        if (o == 0) rmax_take_f64(G.op_sum + G.N, G.nranks, Mnext, lane);
     }
     const double Ms = wave_max(bits2d(Mcur[lane])), Mr = wave_max(bits2d(Mcur[MSH + lane]));
     const double* sp_cur = G.spb[cur];
@@ -1871,6 +1899,11 @@ __global__ void __launch_bounds__(WAVE * FB_W) k_fx_b(const GDev* __restrict__ g
     const int32_t op = fin && G.perm ? G.perm[o] : o;
     const double ssv = fin ? G.fx_ssv[op] : 0.0;
     const float uo = fin ? G.u_o[op] : 0.0f;
+    if ((int32_t)blockIdx.x == G.blk0fb && w == 1 && mode) {   // r' maxima riding on the limb sum
+        unsigned long long* Mn = G.mslot + (size_t)2 * MSH * ((it % 3 + 1) % 3);
+        if (mode == 1) rmax_put(G, Mn, G.fx_limb + 2 * (size_t)N, lane);
+        else rmax_take_bits(G.fx_limb + 2 * (size_t)N, G.nranks, Mn, lane);
+    }
     unsigned long long lo = 0ull, hi = 0ull;
     if (on && mode != 2) {
         // batches of 16 rows per lane, every load in flight before the sums (indices clamped:
@@ -2672,6 +2705,8 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         v.fx_ssv = g->fx_ssv.p;
         v.fx_limb = (unsigned long long*)g->fx_limb.p;
         v.op_sum = g->op_sum.p;
+        v.rank = ctx->rank;
+        v.nranks = ctx->nranks;
         v.stamp = nullptr;
         // a shard without traces still runs one (empty) block: it clears the maxima slot and
         // writes a zero partial row, and the collectives after the launch need every rank
@@ -2744,10 +2779,9 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
             MR_DEBUG_CHECK(ctx, "k_fx_a");
             if (!coll) {
                 hipLaunchKernelGGL(k_fx_b, dim3(blocks_fb), dim3(WAVE * FB_W), 0, st, dv.p, ng, split_fb, d, it, 0);
-            } else {   // r' max and the P_sr r limbs over all ranks (exact: integers, max)
-                MR_TRY(mr_coll_allreduce(ctx, gs[0]->mslot.p + (size_t)2 * MSH * ((it + 1) % 3) + MSH, MSH, MR_DT_U64, 1));
+            } else {   // ONE all-reduce: the P_sr r limbs and every rank's r' max (exact: integers)
                 hipLaunchKernelGGL(k_fx_b, dim3(blocks_fb), dim3(WAVE * FB_W), 0, st, dv.p, ng, split_fb, d, it, 1);
-                MR_TRY(mr_coll_allreduce(ctx, gs[0]->fx_limb.p, 2 * (int64_t)gs[0]->N, MR_DT_U64, 0));
+                MR_TRY(mr_coll_allreduce(ctx, gs[0]->fx_limb.p, 2 * (int64_t)gs[0]->N + ctx->nranks, MR_DT_U64, 0));
                 hipLaunchKernelGGL(k_fx_b, dim3(blocks_fb), dim3(WAVE * FB_W), 0, st, dv.p, ng, split_fb, d, it, 2);
             }
             MR_DEBUG_CHECK(ctx, "k_fx_b");
@@ -2760,10 +2794,9 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         if (blocks_b) {
             if (!coll) {
                 hipLaunchKernelGGL(k_iter_b, dim3(blocks_b), dim3(TB), 0, st, dv.p, ng, d, alpha, it, 0);
-            } else {   // r' max over ranks, then the per-op P_sr r sums over ranks (fp64 SUM)
-                MR_TRY(mr_coll_allreduce(ctx, gs[0]->mslot.p + (size_t)2 * MSH * ((it + 1) % 3) + MSH, MSH, MR_DT_U64, 1));
+            } else {   // ONE all-reduce: the per-op P_sr r sums (fp64 SUM) and every rank's r' max
                 hipLaunchKernelGGL(k_iter_b, dim3(blocks_b), dim3(TB), 0, st, dv.p, ng, d, alpha, it, 1);
-                MR_TRY(mr_coll_allreduce(ctx, gs[0]->op_sum.p, (int64_t)gs[0]->N, MR_DT_F64, 0));
+                MR_TRY(mr_coll_allreduce(ctx, gs[0]->op_sum.p, (int64_t)gs[0]->N + ctx->nranks, MR_DT_F64, 0));
                 hipLaunchKernelGGL(k_iter_b, dim3(blocks_b), dim3(TB), 0, st, dv.p, ng, d, alpha, it, 2);
             }
             MR_DEBUG_CHECK(ctx, "k_iter_b");
@@ -2977,7 +3010,8 @@ extern "C" int mr_pagerank_sharded(mr_ctx* ctx, mr_graph* g, int anomaly, double
         MR_TRY(shard_exchange(ctx, g));
         g->sharded_done = true;
     }
-    if (g->fused) MR_TRY(g->fx_limb.alloc(ctx, 2 * (size_t)std::max(g->N, 1)));   // fixed-point limbs
-    else MR_TRY(g->op_sum.alloc(ctx, (size_t)std::max(g->N, 1)));                    // tile path: fp64 sums
+    // the per-iteration all-reduce buffer: the per-op sums, then one r' max slot per rank
+    if (g->fused) MR_TRY(g->fx_limb.alloc(ctx, 2 * (size_t)g->N + (size_t)ctx->nranks));   // fixed-point limbs
+    else MR_TRY(g->op_sum.alloc(ctx, (size_t)g->N + (size_t)ctx->nranks));                  // tile path: fp64 sums
     return mr_pagerank_batch_impl(ctx, &g, &anomaly, 1, d, alpha, iters, precision, flags, true);
 }

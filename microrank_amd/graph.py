@@ -181,9 +181,10 @@ class DeviceGraph:
         return dict(N=n.value, T=t.value, nnz=nnz.value, E=e.value)
 
     def close(self):
-        if getattr(self, "h", None):
+        # a destroyed context has freed its handles already (mr_ctx_destroy)
+        if getattr(self, "h", None) and getattr(getattr(self, "ctx", None), "h", None):
             _lib.load().mr_graph_free(self.h)
-            self.h = None
+        self.h = None
 
     def __del__(self):  # pragma: no cover
         if sys.is_finalizing():   # the owning context may already be destroyed

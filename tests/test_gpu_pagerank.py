@@ -199,3 +199,26 @@ def test_kind_hash_collision_retries_with_next_seed(monkeypatch, part_min):
     assert list(got[0]) == list(ref[0]) and got[1] == ref[1]
     assert [float(x) for x in got[0].values()] == [float(x) for x in ref[0].values()]
     _check(got, case["pr_anomaly"], RTOL64)
+
+
+def test_context_destroy_frees_its_handles():
+    """A context destroyed before its graphs / span tables (garbage-collection order of a
+    reference cycle) frees them itself; freeing the stale handles afterwards is a no-op."""
+    from microrank_amd import _lib
+    from microrank_amd.graph import DeviceGraph
+    from microrank_amd.preprocess_data import DeviceSpans
+    from conftest import regen_window
+    from microrank_amd.spans import SpanTable
+
+    d = load_golden("dict_cases.json")["fig3"]["input"]
+    cx = _lib.Context(0)
+    g = orc.graph_from_dicts(d["operation_operation"], d["operation_trace"], d["trace_operation"], d["pr_trace"])
+    dg = DeviceGraph.upload(cx, host_graph_from_oracle(g))
+    _, adf = regen_window(load_golden("c1.json"))
+    sp = DeviceSpans(cx, SpanTable.from_dataframe(adf))
+    h_graph, h_spans = dg.h, sp.h
+    cx.close()
+    lib = _lib.load()
+    assert lib.mr_graph_free(h_graph) == 0 and lib.mr_spans_free(h_spans) == 0   # stale: no-op
+    dg.close()
+    sp.close()

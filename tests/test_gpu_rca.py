@@ -277,3 +277,54 @@ def test_concurrent_contexts_rank_like_one():
         w[1].close()
     for cx in ctxs:
         cx.close()
+
+
+def _oracle_rca(st, t0, t1, a3, ok, top_max=5):
+    """The driver's window (online_rca.py:164-201) on the numpy oracle: detector (T1 swap), the
+    two span graphs (preprocess_data.py:146-171), both PageRanks (pagerank.py:15-112), DStar2."""
+    import oracle as orc
+
+    a3map = {i: float(a3[i]) for i in range(len(a3)) if ok[i]}
+    _, ab, no = orc.detect(st.trace, st.svcop, st.duration, st.tstart, st.tend, t0, t1, a3map)
+    res = {}
+    for lst, anomaly in ((ab, False), (no, True)):   # normal_list = the detector's abnormal traces
+        sel = np.zeros(st.n_traces, bool)
+        sel[lst] = True
+        g = orc.span_graph(st.trace, st.podop, st.span, st.parent, sel).as_graph()
+        s = orc.power_iteration(g, orc.preference(g, orc.trace_kinds(g), anomaly))
+        res[anomaly] = orc.weights(g, s)
+    top, score, _ = orc.spectrum(res[True][0], res[False][0], len(no), len(ab), top_max, res[False][1], res[True][1],
+                                 "dstar2")
+    return top, score, len(ab), len(no)
+
+
+@pytest.fixture(scope="module")
+def c3_window():
+    import bench
+
+    _, normal, abnormal = bench.make_window(4242, 500, 20_000)   # BASELINE configs[2]: 500 ops / 20k traces
+    t0 = int(abnormal.tstart.min())
+    return normal, abnormal, t0, t0 + 5 * 60 * 10**9
+
+
+def test_c3_window_against_oracle(c3_window):
+    """C3-shaped window (500 ops / 20k traces): mr_rca_window's top-11 and DStar2 scores against
+    the numpy oracle's whole window at 1e-10 (fp64), the top-5 and 1e-4 in fp32."""
+    import bench
+    from microrank_amd import _lib
+    from microrank_amd.preprocess_data import DeviceSpans
+
+    normal, abnormal, t0, t1 = c3_window
+    ctx = _lib.default_context()
+    a3, ok = bench.slo_from_gpu(ctx, normal)
+    dev = DeviceSpans(ctx, abnormal)
+    top, score, na, nn = _oracle_rca(abnormal, t0, t1, a3, ok)
+    assert na > 0 and nn > 0 and len(top) == 11
+    e, codes, scores, gna, gnn = bench.run_window(ctx, dev, t0, t1, a3, ok, _lib.MR_FP64)
+    assert (gna, gnn) == (na, nn)
+    assert list(codes) == list(top)
+    np.testing.assert_allclose(scores, score, rtol=1e-10, atol=0)
+    e32, c32, s32, _, _ = bench.run_window(ctx, dev, t0, t1, a3, ok, _lib.MR_FP32)
+    assert list(c32[:5]) == list(top[:5])
+    np.testing.assert_allclose(s32, score, rtol=1e-4, atol=0)
+    dev.close()
