@@ -121,6 +121,9 @@ typedef struct mr_span_cols {
     const int64_t* duration;  /* span duration (reference units)                   */
     const int64_t* tstart;    /* trace-level start, ns (NULL if absent)             */
     const int64_t* tend;      /* trace-level end, ns                                */
+    const int32_t* row;       /* global row index (NULL: the rows are the whole table) --
+                                 a shard of a table split over ranks keeps the table's
+                                 row order here for first appearance (T10)           */
 } mr_span_cols;
 
 int mr_spans_upload(mr_ctx* ctx, const mr_span_cols* cols, mr_spans** out);
@@ -131,6 +134,15 @@ int mr_spans_free(mr_spans* s);
  * then never-parent ops in first-appearance row order (T10).  The parent join ignores
  * traceID (T11). */
 int mr_graph_build(mr_ctx* ctx, const mr_spans* s, const uint8_t* trace_mask, mr_graph** out);
+/* K1 over a trace-sharded span table (one process per GPU, every span of a trace on one
+ * rank, span / pod-op / trace codes global, cols.row set): this rank's graph over the GLOBAL
+ * node order -- pod-op counts, first appearances and parent flags reduced over the ranks
+ * (preprocess_data.py:159-163, T10), and the ParentSpanId == spanID join resolved across ranks
+ * too (:157-158, T11: a child's parent rows may lie in traces of another rank).  len_o, nchild
+ * and the call edges stay this rank's parts: mr_pagerank_sharded combines them.  Collectives
+ * over the context's backend (mr_comm_init / mr_comm_set_host); replaces the per-rank
+ * get_pagerank_graph(trace_list, span_df) of a sharded deployment. */
+int mr_graph_build_sharded(mr_ctx* ctx, const mr_spans* s, const uint8_t* trace_mask, mr_graph** out);
 /* node order (podop codes) and trace codes of a built graph */
 int mr_graph_nodes(const mr_graph* g, int32_t* node_podop /*[N]*/, int32_t* trace_code /*[T]*/);
 /* structure export for parity tests: any pointer may be NULL */

@@ -41,7 +41,8 @@ class GraphDesc(C.Structure):
 class SpanCols(C.Structure):
     _fields_ = [("n_spans", C.c_int64), ("n_traces", C.c_int32), ("n_podops", C.c_int32),
                 ("n_svcops", C.c_int32), ("trace", i32p), ("podop", i32p), ("svcop", i32p),
-                ("span", i64p), ("parent", i64p), ("duration", i64p), ("tstart", i64p), ("tend", i64p)]
+                ("span", i64p), ("parent", i64p), ("duration", i64p), ("tstart", i64p), ("tend", i64p),
+                ("row", i32p)]
 
 
 # name -> (restype, argtypes); every symbol here must be exported (tests check it)
@@ -63,6 +64,7 @@ SIGNATURES = {
                                     C.c_int, C.c_uint32]),
     "mr_graph_fetch": (C.c_int, [P, f64p, i32p, f64p, f32p]),
     "mr_spans_upload": (C.c_int, [P, C.POINTER(SpanCols), C.POINTER(P)]),
+    "mr_graph_build_sharded": (C.c_int, [P, P, C.POINTER(C.c_uint8), C.POINTER(P)]),
     "mr_spans_free": (C.c_int, [P]),
     "mr_graph_build": (C.c_int, [P, P, u8p, C.POINTER(P)]),
     "mr_graph_nodes": (C.c_int, [P, i32p, i32p]),

@@ -399,6 +399,83 @@ __global__ void k_ix_trace_ops(const int32_t* tflag, const int64_t* zoff, int64_
     if (!tflag[t]) return;
     rs_ops[zoff[t] + (r - po_off[t])] = node_of_code[po_op[r]];
 }
+// ---------------------------------------------------------------- sharded build: the join across ranks
+// A child row's parent rows may lie in traces of another rank (T11).  Each rank publishes a
+// Bloom filter of the ParentSpanIds of its selected rows; a rank exports the selected rows whose
+// spanID may be a parent on another rank (both filter bits set there); every rank joins its
+// children against the other ranks' exports (exact spanID compare), counting edges at the child.
+__device__ __forceinline__ uint32_t bloom_bit(uint64_t k, int i, int fb) {
+    return (uint32_t)(hmix(k + (i ? 0x9E3779B97F4A7C15ull : 0ull)) >> 20) & ((1u << fb) - 1u);
+}
+__global__ void k_bloom_set(const int32_t* trace, const int64_t* parent, int64_t S, const uint8_t* mask, int fb,
+                            uint32_t* F) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= S || !mask[trace[i]] || parent[i] < 0) return;
+    for (int h = 0; h < 2; ++h) {
+        const uint32_t b = bloom_bit((uint64_t)parent[i], h, fb);
+        atomicOr(&F[b >> 5], 1u << (b & 31));
+    }
+}
+__global__ void k_export_flags(const int32_t* trace, const int64_t* span, int64_t S, const uint8_t* mask, int fb,
+                               const uint32_t* Fall, int64_t words, int R, int me, int32_t* flag) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= S) return;
+    int32_t hit = 0;
+    if (mask[trace[i]]) {
+        const uint32_t b0 = bloom_bit((uint64_t)span[i], 0, fb), b1 = bloom_bit((uint64_t)span[i], 1, fb);
+        for (int r = 0; r < R && !hit; ++r) {
+            if (r == me) continue;
+            const uint32_t* F = Fall + (size_t)r * words;
+            hit = ((F[b0 >> 5] >> (b0 & 31)) & (F[b1 >> 5] >> (b1 & 31)) & 1u) ? 1 : 0;
+        }
+    }
+    flag[i] = hit;
+}
+// export record: (spanID code, pod-op | rank << 32); pads (~0, ~0) sort last
+__global__ void k_export_fill(const int32_t* flag, const int64_t* pos, int64_t S, const int64_t* span,
+                              const int32_t* podop, int me, int64_t cap, uint64_t* out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < S && flag[i]) {
+        out[2 * pos[i]] = (uint64_t)span[i];
+        out[2 * pos[i] + 1] = (uint64_t)(uint32_t)podop[i] | ((uint64_t)(uint32_t)me << 32);
+    }
+    const int64_t n = pos[S];
+    if (i >= n && i < cap) out[2 * i] = out[2 * i + 1] = ~0ull;
+}
+__global__ void k_export_keys(const uint64_t* rec, int64_t n, uint64_t* key, uint32_t* val) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        key[i] = rec[2 * i];
+        val[i] = (uint32_t)i;
+    }
+}
+// per selected child row: the other ranks' export records with spanID == its parent
+template <bool ADD>
+__global__ void k_cross_join(const int32_t* trace, const int64_t* parent, const int32_t* podop, int64_t S,
+                             const uint8_t* mask, const uint64_t* skey, const uint32_t* sval, const uint64_t* rec,
+                             int64_t n, int me, unsigned long long* count, uint64_t* gk, uint32_t* gc, uint64_t gmask) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= S || !mask[trace[i]] || parent[i] < 0) return;
+    const uint64_t p = (uint64_t)parent[i];
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (skey[mid] < p) lo = mid + 1;
+        else hi = mid;
+    }
+    uint32_t c = 0;
+    for (int64_t j = lo; j < n && skey[j] == p; ++j) {
+        const uint64_t w = rec[2 * (size_t)sval[j] + 1];
+        if ((int)(w >> 32) == me) continue;   // this rank's own rows: joined locally
+        ++c;
+        if (ADD) global_edge_add(((w & 0xffffffffull) << 32) | (uint32_t)podop[i], 1u, gk, gc, gmask);
+    }
+    if (!ADD && c) atomicAdd(count, (unsigned long long)c);
+}
+__global__ void k_neg_i32(int32_t* a, int32_t n) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) a[i] = -a[i];
+}
 }  // namespace
 
 // ------------------------------------------------------------------------------ host
@@ -426,6 +503,16 @@ extern "C" int mr_spans_upload(mr_ctx* ctx, const mr_span_cols* c, mr_spans** ou
     s->n_svcops = c->n_svcops;
     s->n_span_codes = max_code + 1;
     s->has_times = c->tstart && c->tend;
+    int64_t row_max = S;
+    if (c->row) {
+        row_max = 0;
+        for (int64_t i = 0; i < S; ++i) {
+            if (c->row[i] < 0 || (i && c->row[i] <= c->row[i - 1]))
+                return mr_fail(ctx, MR_ERR_ARG, "row: global row indices must be non-negative and ascending");
+            row_max = std::max<int64_t>(row_max, c->row[i]);
+        }
+    }
+    s->row_bits = bits_for((uint64_t)std::max<int64_t>(row_max, 1));
     int rc = MR_OK;
     auto fail = [&](int code) {
         delete s;
@@ -437,6 +524,7 @@ extern "C" int mr_spans_upload(mr_ctx* ctx, const mr_span_cols* c, mr_spans** ou
         return fail(rc);
     if (s->has_times && ((rc = s->tstart.upload(ctx, c->tstart, S)) || (rc = s->tend.upload(ctx, c->tend, S))))
         return fail(rc);
+    if (c->row && (rc = s->grow.upload(ctx, c->row, S))) return fail(rc);
     // spanID -> rows multimap (counting sort by code)
     const int64_t U = s->n_span_codes;
     DBuf<int32_t> cnt;
@@ -485,9 +573,11 @@ __global__ void k_zero2_i32(int32_t* a, int32_t* b, int32_t n) {
         b[i] = 0;
     }
 }
+// sharded: node presence (span counts), first appearances and parent flags are reduced over the
+// ranks for the node order (every rank the same N and order); len_o / nchild stay this rank's.
 static int build_nodes(mr_ctx* ctx, mr_graph* g, int32_t NP, const int32_t* ocnt, const int32_t* ofirst, int row_bits,
                        const uint64_t* gk, const uint32_t* gc, uint64_t ecap, DBuf<int32_t>& node_of_code,
-                       PhaseTimer* pt = nullptr) {
+                       PhaseTimer* pt = nullptr, bool sharded = false) {
     hipStream_t st = ctx->stream;
     DBuf<int32_t> eflag, is_par, nchild_code;
     DBuf<int64_t> epos, etmp, tmp;
@@ -509,6 +599,22 @@ static int build_nodes(mr_ctx* ctx, mr_graph* g, int32_t NP, const int32_t* ocnt
     hipLaunchKernelGGL(k_edge_compact, dim3(cdiv(ecap, 256)), dim3(256), 0, st, gk, gc, eflag.p, epos.p, (int64_t)ecap,
                        ekey.p, ecnt.p, is_par.p, nchild_code.p);
     if (pt) pt->mark("edges");
+    DBuf<int32_t> ocnt_g, ofirst_g;
+    const int32_t* ocnt_o = ocnt;     // the node order's presence counts and first rows
+    const int32_t* ofirst_o = ofirst;
+    if (sharded && NP) {
+        MR_TRY(ocnt_g.alloc(ctx, NP));
+        MR_TRY(ofirst_g.alloc(ctx, NP));
+        MR_TRY_HIP(ctx, hipMemcpyAsync(ocnt_g.p, ocnt, NP * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
+        MR_TRY_HIP(ctx, hipMemcpyAsync(ofirst_g.p, ofirst, NP * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
+        hipLaunchKernelGGL(k_neg_i32, dim3(cdiv(NP, 256)), dim3(256), 0, st, ofirst_g.p, NP);
+        MR_TRY(mr_coll_allreduce(ctx, is_par.p, NP, MR_DT_I32, 1));
+        MR_TRY(mr_coll_allreduce(ctx, ocnt_g.p, NP, MR_DT_I32, 0));
+        MR_TRY(mr_coll_allreduce(ctx, ofirst_g.p, NP, MR_DT_I32, 1));   // max of -first = min first
+        hipLaunchKernelGGL(k_neg_i32, dim3(cdiv(NP, 256)), dim3(256), 0, st, ofirst_g.p, NP);
+        ocnt_o = ocnt_g.p;
+        ofirst_o = ofirst_g.p;
+    }
     // node order
     DBuf<int32_t> pflag, qflag;
     DBuf<int64_t> ppos, qpos;
@@ -517,7 +623,7 @@ static int build_nodes(mr_ctx* ctx, mr_graph* g, int32_t NP, const int32_t* ocnt
     MR_TRY(ppos.alloc(ctx, NP + 1));
     MR_TRY(qpos.alloc(ctx, NP + 1));
     MR_TRY(node_of_code.alloc(ctx, NP));
-    if (NP) hipLaunchKernelGGL(k_node_flags, dim3(cdiv(NP, 256)), dim3(256), 0, st, ocnt, is_par.p, NP, pflag.p, qflag.p);
+    if (NP) hipLaunchKernelGGL(k_node_flags, dim3(cdiv(NP, 256)), dim3(256), 0, st, ocnt_o, is_par.p, NP, pflag.p, qflag.p);
     MR_TRY(mr_exclusive_scan_i32(ctx, pflag.p, ppos.p, NP, tmp.p));
     MR_TRY(mr_exclusive_scan_i32(ctx, qflag.p, qpos.p, NP, tmp.p));
     int64_t PQ[2] = {0, 0};
@@ -532,7 +638,7 @@ static int build_nodes(mr_ctx* ctx, mr_graph* g, int32_t NP, const int32_t* ocnt
     MR_TRY(qkey.alloc(ctx, Q));
     MR_TRY(qval.alloc(ctx, Q));
     if (NP)
-        hipLaunchKernelGGL(k_node_parents, dim3(cdiv(NP, 256)), dim3(256), 0, st, pflag.p, ppos.p, qflag.p, qpos.p, ofirst,
+        hipLaunchKernelGGL(k_node_parents, dim3(cdiv(NP, 256)), dim3(256), 0, st, pflag.p, ppos.p, qflag.p, qpos.p, ofirst_o,
                            NP, node_of_code.p, g->node_podop.p, qkey.p, qval.p);
     SortScratch ws;
     MR_TRY(mr_radix_sort(ctx, qkey.p, qval.p, Q, row_bits, ws));
@@ -664,10 +770,77 @@ static int graph_build_rows(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d_ma
 // Indexed build (mr_span_index.hip): whole traces selected by the mask; every per-row fact comes
 // from the per-trace index, so no row is sorted.  Each trace's op list is written in pod-op code
 // order (a fixed order for the kind keys; mr_graph_export sorts by node id for inspection).
-static int graph_build_indexed(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d_mask, mr_graph* g) {
+// The sharded build's cross-rank exchange (see k_bloom_set): the other ranks' export records
+// sorted by spanID (keys / record index) and the number of cross-rank (child, parent) matches.
+struct CrossJoin {
+    DBuf<uint64_t> rec, key;
+    DBuf<uint32_t> val;
+    int64_t n = 0;
+    int64_t matches = 0;
+};
+static int cross_exchange(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d_mask, CrossJoin& X) {
+    hipStream_t st = ctx->stream;
+    const int64_t S = sp->S;
+    const int R = ctx->nranks, me = ctx->rank;
+    DBuf<int64_t> sc;
+    int64_t h = S;
+    MR_TRY(sc.upload(ctx, &h, 1));
+    MR_TRY(mr_coll_allreduce(ctx, sc.p, 1, MR_DT_I64, 1));   // the largest shard sizes the filters
+    MR_TRY(sc.download(ctx, &h, 1));
+    MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+    const int fb = std::min(28, std::max(16, bits_for((uint64_t)std::max<int64_t>(h, 1)) + 4));   // >= 16 bits per row
+    const int64_t words = ((int64_t)1 << fb) / 32;
+    DBuf<uint32_t> F, Fall;
+    MR_TRY(F.zero(ctx, (size_t)words));
+    MR_TRY(Fall.alloc(ctx, (size_t)words * R));
+    if (S) hipLaunchKernelGGL(k_bloom_set, dim3(cdiv(S, 256)), dim3(256), 0, st, sp->trace.p, sp->parent.p, S, d_mask, fb, F.p);
+    MR_TRY(mr_coll_allgather(ctx, F.p, Fall.p, words, MR_DT_I32));
+    DBuf<int32_t> flag;
+    DBuf<int64_t> pos, tmp;
+    MR_TRY(flag.alloc(ctx, (size_t)std::max<int64_t>(S, 1)));
+    MR_TRY(pos.alloc(ctx, (size_t)S + 1));
+    MR_TRY(tmp.alloc(ctx, (size_t)std::max<int64_t>(scan_tmp_elems(S), 1)));
+    if (S)
+        hipLaunchKernelGGL(k_export_flags, dim3(cdiv(S, 256)), dim3(256), 0, st, sp->trace.p, sp->span.p, S, d_mask, fb,
+                           Fall.p, words, R, me, flag.p);
+    MR_TRY(mr_exclusive_scan_i32(ctx, flag.p, pos.p, S, tmp.p));
+    MR_TRY_HIP(ctx, hipMemcpyAsync(sc.p, pos.p + S, sizeof(int64_t), hipMemcpyDeviceToDevice, st));
+    MR_TRY(mr_coll_allreduce(ctx, sc.p, 1, MR_DT_I64, 1));   // the largest export list sizes the gather
+    MR_TRY(sc.download(ctx, &h, 1));
+    MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+    const int64_t cap = std::max<int64_t>(h, 1);
+    DBuf<uint64_t> send;
+    MR_TRY(send.alloc(ctx, 2 * (size_t)cap));
+    hipLaunchKernelGGL(k_export_fill, dim3(cdiv(std::max<int64_t>(S, cap), 256)), dim3(256), 0, st, flag.p, pos.p, S,
+                       sp->span.p, sp->podop.p, me, cap, send.p);
+    X.n = cap * R;
+    MR_TRY(X.rec.alloc(ctx, 2 * (size_t)X.n));
+    MR_TRY(mr_coll_allgather(ctx, send.p, X.rec.p, 2 * cap, MR_DT_U64));
+    MR_TRY(X.key.alloc(ctx, (size_t)X.n));
+    MR_TRY(X.val.alloc(ctx, (size_t)X.n));
+    hipLaunchKernelGGL(k_export_keys, dim3(cdiv(X.n, 256)), dim3(256), 0, st, X.rec.p, X.n, X.key.p, X.val.p);
+    SortScratch ws;
+    MR_TRY(mr_radix_sort(ctx, X.key.p, X.val.p, X.n, 64, ws));
+    DBuf<unsigned long long> cnt;
+    MR_TRY(cnt.zero(ctx, 1));
+    if (S)
+        hipLaunchKernelGGL(k_cross_join<false>, dim3(cdiv(S, 256)), dim3(256), 0, st, sp->trace.p, sp->parent.p,
+                           sp->podop.p, S, d_mask, X.key.p, X.val.p, X.rec.p, X.n, me, cnt.p, (uint64_t*)nullptr,
+                           (uint32_t*)nullptr, (uint64_t)0);
+    unsigned long long m = 0;
+    MR_TRY(cnt.download(ctx, &m, 1));
+    MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+    X.matches = (int64_t)m;
+    return MR_OK;
+}
+
+static int graph_build_indexed(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d_mask, mr_graph* g,
+                               bool sharded = false) {
     hipStream_t st = ctx->stream;
     PhaseTimer pt(st, "build");
     const int32_t NT = sp->n_traces, NP = sp->n_podops;
+    CrossJoin X;
+    if (sharded) MR_TRY(cross_exchange(ctx, sp, d_mask, X));
     DBuf<int32_t> tflag, zc;
     DBuf<int64_t> tpos, zoff, tmp;
     MR_TRY(tflag.alloc(ctx, NT));
@@ -678,7 +851,7 @@ static int graph_build_indexed(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d
     DBuf<int32_t> ocnt, ofirst;
     MR_TRY(ocnt.alloc(ctx, NP));
     MR_TRY(ofirst.alloc(ctx, NP));
-    const uint64_t ecap = edge_capacity(sp->n_edge_keys, NP);
+    const uint64_t ecap = edge_capacity(sp->n_edge_keys + X.matches, NP);
     DBuf<uint64_t> gk;
     DBuf<uint32_t> gc;
     MR_TRY(gk.alloc(ctx, ecap));
@@ -705,13 +878,16 @@ static int graph_build_indexed(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d
     if (sp->n_xj)
         hipLaunchKernelGGL(k_ix_cross, dim3(cdiv(sp->n_xj, 256)), dim3(256), 0, st, d_mask, sp->xj_tc.p, sp->xj_tp.p,
                            sp->xj_key.p, sp->n_xj, gk.p, gc.p, ecap - 1);
+    if (X.matches && sp->S)   // cross-rank parent joins, counted at the child's rank
+        hipLaunchKernelGGL(k_cross_join<true>, dim3(cdiv(sp->S, 256)), dim3(256), 0, st, sp->trace.p, sp->parent.p,
+                           sp->podop.p, sp->S, d_mask, X.key.p, X.val.p, X.rec.p, X.n, ctx->rank,
+                           (unsigned long long*)nullptr, gk.p, gc.p, ecap - 1);
     pt.mark("stats");
     MR_TRY(mr_exclusive_scan_i32(ctx, tflag.p, tpos.p, NT, tmp.p));
     MR_TRY(mr_exclusive_scan_i32(ctx, zc.p, zoff.p, NT, tmp.p));
     pt.mark("scans");
     DBuf<int32_t> node_of_code;
-    MR_TRY(build_nodes(ctx, g, NP, ocnt.p, ofirst.p, bits_for((uint64_t)std::max<int64_t>(sp->S, 1)), gk.p, gc.p, ecap,
-                       node_of_code, &pt));
+    MR_TRY(build_nodes(ctx, g, NP, ocnt.p, ofirst.p, sp->row_bits, gk.p, gc.p, ecap, node_of_code, &pt, sharded));
     pt.mark("nodes");
     int64_t h[2] = {0, 0};   // T, nnz (their scans ran before build_nodes' syncs)
     MR_TRY_HIP(ctx, hipMemcpyAsync(&h[0], tpos.p + NT, sizeof(int64_t), hipMemcpyDeviceToHost, st));
@@ -768,6 +944,34 @@ extern "C" int mr_graph_build(mr_ctx* ctx, const mr_spans* sp, const uint8_t* tr
     MR_TRY(mask.upload(ctx, trace_mask, (size_t)sp->n_traces));
     MR_TRY(mr_graph_build_dev(ctx, sp, mask.p, out, nullptr));
     mr_handle_add(ctx, *out, [](void* h) { delete (mr_graph*)h; });
+    return MR_OK;
+}
+
+extern "C" int mr_graph_build_sharded(mr_ctx* ctx, const mr_spans* sp, const uint8_t* trace_mask, mr_graph** out) {
+    if (!ctx || !sp || !trace_mask || !out || sp->ctx != ctx)
+        return mr_fail(ctx, MR_ERR_ARG, "mr_graph_build_sharded: bad arguments");
+    if (!mr_coll_ready(ctx) && ctx->nranks != 1) return mr_fail(ctx, MR_ERR_COMM, "no collective backend");
+    if (!sp->indexed) return mr_fail(ctx, MR_ERR_STATE, "span table has no per-trace index (sharded build needs it)");
+    MR_TRY_HIP(ctx, hipSetDevice(ctx->device));
+    *out = nullptr;
+    DBuf<uint8_t> mask;
+    MR_TRY(mask.upload(ctx, trace_mask, (size_t)sp->n_traces));
+    auto g = new mr_graph();
+    g->ctx = ctx;
+    int rc = graph_build_indexed(ctx, sp, mask.p, g, true);
+    if (rc == MR_OK) {
+        g->rs_is_sr = true;
+        g->pr_identity = true;
+        g->n_pr = g->T;
+        rc = mr_graph_prepare(ctx, g);
+    }
+    if (rc == MR_OK) rc = hipStreamSynchronize(ctx->stream) == hipSuccess ? MR_OK : mr_fail(ctx, MR_ERR_HIP, "sync");
+    if (rc != MR_OK) {
+        delete g;
+        return rc;
+    }
+    mr_handle_add(ctx, g, [](void* h) { delete (mr_graph*)h; });
+    *out = g;
     return MR_OK;
 }
 

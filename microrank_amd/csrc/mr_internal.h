@@ -204,6 +204,8 @@ struct mr_spans {
     DBuf<int32_t> trace, podop, svcop;
     DBuf<int64_t> span, parent, duration, tstart, tend;
     bool has_times = false;
+    DBuf<int32_t> grow;          // global row index per row (a shard of a larger table), or empty
+    int row_bits = 0;            // bits of the largest (global) row index + 1
     // spanID -> rows multimap over the whole table (static; built at upload)
     int64_t n_span_codes = 0;
     DBuf<int64_t> id_off;   // [n_span_codes+1]

@@ -47,6 +47,10 @@ __global__ void k_ix_runs(const uint64_t* key, const uint32_t* val, const int32_
     r_start[r] = i;
     atomicAdd(&truns[t], 1);
 }
+__global__ void k_ix_map_rows(int32_t* first, int64_t n, const int32_t* grow) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < n) first[r] = grow[first[r]];
+}
 __global__ void k_ix_cnt(const int64_t* r_start, int64_t R, int64_t n, int32_t* r_cnt) {
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r < R) r_cnt[r] = (int32_t)((r + 1 < R ? r_start[r + 1] : n) - r_start[r]);
@@ -317,6 +321,8 @@ int mr_spans_index(mr_ctx* ctx, mr_spans* s) {
                            temax.p, NT, bad.p);
     // distinct pod-ops and service-ops per trace
     MR_TRY(trace_runs(ctx, s, s->podop.p, NP, s->po_off, s->po_op, s->po_cnt, &s->po_first, &s->po_tr, &s->n_po));
+    if (s->grow.p && s->n_po)   // a shard: first appearances in the whole table's row order
+        hipLaunchKernelGGL(k_ix_map_rows, dim3(cdiv(s->n_po, XB)), dim3(XB), 0, st, s->po_first.p, s->n_po, s->grow.p);
     MR_TRY(trace_runs(ctx, s, s->svcop.p, s->n_svcops, s->sv_off, s->sv_op, s->sv_cnt, nullptr, nullptr, &s->n_sv));
     // parent join resolved once
     {

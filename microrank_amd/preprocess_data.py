@@ -42,8 +42,9 @@ class DeviceSpans:
         cols.n_traces, cols.n_podops, cols.n_svcops = table.n_traces, table.n_podops, table.n_svcops
         keep = {}
         for name, ct in (("trace", C.c_int32), ("podop", C.c_int32), ("svcop", C.c_int32), ("span", C.c_int64),
-                         ("parent", C.c_int64), ("duration", C.c_int64), ("tstart", C.c_int64), ("tend", C.c_int64)):
-            a = getattr(table, name)
+                         ("parent", C.c_int64), ("duration", C.c_int64), ("tstart", C.c_int64), ("tend", C.c_int64),
+                         ("row", C.c_int32)):
+            a = getattr(table, name, None)
             if a is None:
                 continue
             a = np.ascontiguousarray(a, dtype=np.int32 if ct is C.c_int32 else np.int64)

@@ -3,8 +3,10 @@
 One process per GPU holds a shard of the traces (every span of a trace on one rank) over the
 global node index space.  ``mr_pagerank_sharded`` (csrc/mr_pagerank.hip) exchanges, once per
 graph, the per-op span counts / children counts / coverage, the call edges and the trace-kind
-classes, and per iteration the exact fixed-point P_sr r limbs (uint64 SUM) and max r' (MAX), so
-every rank ends with the weights the whole graph would give.
+classes, and per iteration ONE all-reduce: the exact fixed-point P_sr r limbs (uint64 SUM) with
+every rank's max r' in a one-hot slot, so every rank ends with the weights the whole graph would
+give.  :func:`build_graph` builds a rank's graph from its span shard (K1 over the ranks: global
+node order, cross-rank parent joins).
 
 Collectives run over RCCL (:func:`use_rccl`, xGMI between GPUs) or, for ranks that share a GPU
 or have no RCCL, over a host-staged callback on a ``torch.distributed`` process group
@@ -93,3 +95,25 @@ def sharded_pagerank(dg, anomaly: bool, d: float = 0.85, alpha: float = 0.01, it
     dg.ctx.check(lib.mr_pagerank_sharded(dg.ctx.h, dg.h, int(bool(anomaly)), d, alpha, iters, prec, 0),
                  "mr_pagerank_sharded")
     return dg.fetch()
+
+
+def build_graph(dev_spans, trace_mask) -> "DeviceGraph":
+    """K1 on this rank's span shard (mr_graph_build_sharded): ``dev_spans`` holds every span of
+    this rank's traces with global codes and global row indices (SpanTable.shard);
+    ``trace_mask`` selects the trace_list over the global trace codes.  The graph has the whole
+    graph's node order (T10) and its cross-rank parent joins (T11); its len_o / nchild / edges are
+    this rank's parts, which :func:`sharded_pagerank` combines."""
+    from .graph import DeviceGraph
+
+    lib = _lib.load()
+    ctx = dev_spans.ctx
+    mask = np.ascontiguousarray(trace_mask, dtype=np.uint8)
+    h = _lib.P()
+    ctx.check(lib.mr_graph_build_sharded(ctx.h, dev_spans.h, ptr(mask, C.c_uint8), C.byref(h)),
+              "mr_graph_build_sharded")
+    n, t, nnz, e = C.c_int32(), C.c_int32(), C.c_int64(), C.c_int64()
+    lib.mr_graph_info(h, C.byref(n), C.byref(t), C.byref(nnz), C.byref(e))
+    node_podop = np.empty(n.value, np.int32)
+    trace_code = np.empty(t.value, np.int32)
+    ctx.check(lib.mr_graph_nodes(h, ptr(node_podop, C.c_int32), ptr(trace_code, C.c_int32)), "mr_graph_nodes")
+    return DeviceGraph(ctx, h, node_podop, trace_code, n.value, t.value)

@@ -58,6 +58,7 @@ class SpanTable:
     podop_names: Optional[Sequence[str]] = None
     svcop_names: Optional[Sequence[str]] = None
     meta: dict = field(default_factory=dict)
+    row: Optional[np.ndarray] = None      # int32 global row index (a shard of a larger table), else None
 
     @property
     def n_spans(self) -> int:
@@ -89,7 +90,19 @@ class SpanTable:
         pick = lambda a: None if a is None else a[rows]
         return SpanTable(self.trace[rows], self.podop[rows], self.svcop[rows], self.span[rows],
                          self.parent[rows], self.duration[rows], pick(self.tstart), pick(self.tend),
-                         self.trace_names, self.podop_names, self.svcop_names, dict(self.meta))
+                         self.trace_names, self.podop_names, self.svcop_names, dict(self.meta), pick(self.row))
+
+    def shard(self, rank: int, world: int) -> "SpanTable":
+        """This rank's traces (trace code % world == rank) with every span of each, codes and
+        dictionaries global, and the global row index of each row (first appearance, T10): the
+        per-rank table of a trace-sharded deployment (mr_graph_build_sharded)."""
+        rows = np.flatnonzero(self.trace % world == rank)
+        sub = self.take(rows)
+        sub.row = (self.row[rows] if self.row is not None else rows).astype(np.int32)
+        for attr, n in (("trace_names", self.n_traces), ("podop_names", self.n_podops), ("svcop_names", self.n_svcops)):
+            if getattr(sub, attr) is None:   # code spaces stay the whole table's
+                setattr(sub, attr, range(n))
+        return sub
 
     # ------------------------------------------------------------------ ingest
     @classmethod

@@ -238,3 +238,103 @@ def test_ranks_agree_on_the_iteration_path():
         np.testing.assert_allclose(w, w_ref, rtol=1e-10, atol=0)
         np.testing.assert_array_equal(cov, cov_ref)
     assert res[0][1].tobytes() == res[1][1].tobytes(), "ranks disagree"
+
+
+# ------------------------------------------------------------------ K1 over the ranks (spans)
+def _span_table():
+    """Spans with cross-trace duplicated spanIDs (T11 joins across the shards) and broken traces
+    (orphans), 3 pods per service (pod-ops != service-ops), names=False (codes only)."""
+    from microrank_amd import synth
+
+    topo = synth.make_topology(120, 5, pods_per_service=3)
+    return synth.gen_spans(topo, 6000, 9, branch=1.9, p_max=0.8, dup_span_frac=0.03, broken_frac=0.05, names=False)
+
+
+def _span_mask(st):
+    rng = np.random.default_rng(4)
+    return (rng.random(st.n_traces) < 0.7).astype(np.uint8)
+
+
+def _span_worker(rank, world, port, anomaly, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from microrank_amd import _lib, shard
+        from microrank_amd.preprocess_data import DeviceSpans
+
+        st = _span_table()
+        ctx = _lib.Context(0)
+        shard.use_host(ctx)
+        dev = DeviceSpans(ctx, st.shard(rank, world))
+        dg = shard.build_graph(dev, _span_mask(st))
+        nodes = np.array(dg.nodes)
+        w, cov = shard.sharded_pagerank(dg, anomaly)
+        info = dg.info()
+        dg.close()
+        dev.close()
+        ctx.close()
+        q.put((rank, w, cov, (nodes, info)))
+    except Exception as e:
+        q.put((rank, repr(e), None, None))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("anomaly", [False, True])
+def test_sharded_build_from_spans_matches_single_gpu(anomaly):
+    """Two ranks each build their graph from their own span shard (mr_graph_build_sharded: global
+    node order over the ranks, T10; parent joins across the shards, T11) and rank it with
+    mr_pagerank_sharded: node order equal to the single-GPU K1 graph of the whole table,
+    weights within 1e-10, coverage exact, ranks bitwise, and the call-edge count of the whole
+    graph.  The table has joins whose parent row lies on the other rank (counted below)."""
+    import ctypes as C
+
+    from microrank_amd import _lib
+    from microrank_amd.graph import DeviceGraph
+    from microrank_amd.preprocess_data import DeviceSpans
+    from microrank_amd._lib import ptr
+
+    st = _span_table()
+    mask = _span_mask(st)
+    sel = mask[st.trace].astype(bool)
+    child_rank = st.trace[sel] % 2
+    par = st.parent[sel]
+    spans_by_rank = [set(st.span[sel & (st.trace % 2 == r)].tolist()) for r in range(2)]
+    cross = sum(1 for p, r in zip(par.tolist(), child_rank.tolist()) if p >= 0 and p in spans_by_rank[1 - r])
+    assert cross > 0, "no cross-rank parent joins in the test table"
+    ctx = _lib.Context(0)
+    dev = DeviceSpans(ctx, st)
+    lib = _lib.load()
+    h = _lib.P()
+    ctx.check(lib.mr_graph_build(ctx.h, dev.h, ptr(mask, C.c_uint8), C.byref(h)))
+    info = {}
+    n, t, nnz, e = C.c_int32(), C.c_int32(), C.c_int64(), C.c_int64()
+    lib.mr_graph_info(h, C.byref(n), C.byref(t), C.byref(nnz), C.byref(e))
+    nodes = np.empty(n.value, np.int32)
+    lib.mr_graph_nodes(h, ptr(nodes, C.c_int32), ptr(np.empty(t.value, np.int32), C.c_int32))
+    whole = DeviceGraph(ctx, h, nodes, None, n.value, t.value)
+    whole.pagerank(anomaly)
+    w_ref, cov_ref = whole.fetch()
+    E_whole = e.value
+    whole.close()
+    dev.close()
+    ctx.close()
+
+    mpc = mp.get_context("spawn")
+    q = mpc.Queue()
+    port = _free_port()
+    procs = [mpc.Process(target=_span_worker, args=(r, 2, port, anomaly, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=180) for _ in procs], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, w, cov, extra in res:
+        assert cov is not None, f"rank {rank} failed: {w}"
+        np.testing.assert_array_equal(extra[0], nodes)
+        np.testing.assert_allclose(w, w_ref, rtol=1e-10, atol=0)
+        np.testing.assert_array_equal(cov, cov_ref)
+    assert res[0][1].tobytes() == res[1][1].tobytes(), "ranks disagree"
+    assert res[0][3][1]["T"] + res[1][3][1]["T"] == t.value
+    assert res[0][3][1]["E"] == E_whole   # after the exchange: the whole graph's call edges
