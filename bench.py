@@ -213,28 +213,58 @@ def run_c4(args, world, rank, dist):
 
     t_local = args.c4_traces // world + (1 if rank < args.c4_traces % world else 0)
     t_gen = time.perf_counter()
-    hg = synth.big_graph(args.c4_ops, t_local, seed=11, shard=(rank, world))
-    print(f"[bench] rank {rank}: generated {t_local} traces / {hg.sr_ops.size} pairs in "
-          f"{time.perf_counter() - t_gen:.1f} s", file=sys.stderr, flush=True)
-    nnz_local = int(hg.sr_ops.size)
     ctx = _lib.default_context()
     if world > 1:
         shard.use_rccl(ctx)
-    dg = DeviceGraph.upload(ctx, hg)
-    del hg
     prec = args.precision
     fused = args.c4_ops <= 16384   # N <= FX_NMAX: fused k_fx_a/k_fx_b, else the tile path
+    dev = None
+    if args.from_spans:
+        # K1 inside the timed step: this rank's span shard is resident in HBM (ingest), a step
+        # builds the rank's graph from it (mr_graph_build_sharded: global node order and
+        # cross-rank parent joins over the collectives) and ranks it
+        from microrank_amd.preprocess_data import DeviceSpans
+
+        st = synth.big_spans(args.c4_ops, args.c4_traces, seed=11, shard=(rank, world))
+        print(f"[bench] rank {rank}: generated {t_local} traces / {st.n_spans} spans in "
+              f"{time.perf_counter() - t_gen:.1f} s", file=sys.stderr, flush=True)
+        dev = DeviceSpans(ctx, st)
+        mask = np.ones(st.n_traces, np.uint8)
+        n_spans_local = st.n_spans
+        del st
+        dg = None
+    else:
+        hg = synth.big_graph(args.c4_ops, t_local, seed=11, shard=(rank, world))
+        print(f"[bench] rank {rank}: generated {t_local} traces / {hg.sr_ops.size} pairs in "
+              f"{time.perf_counter() - t_gen:.1f} s", file=sys.stderr, flush=True)
+        dg = DeviceGraph.upload(ctx, hg)
+        del hg
+    build_s = [0.0]
+
+    def step():
+        nonlocal dg
+        if dev is not None:
+            if dg is not None:
+                dg.close()
+            tb = time.perf_counter()
+            dg = shard.build_graph(dev, mask)
+            ctx.sync()
+            build_s[0] += time.perf_counter() - tb
+        return shard.sharded_pagerank(dg, True, precision=prec)
+
     for _ in range(max(args.warmup, 1)):   # the first call also runs the once-per-graph exchange
-        shard.sharded_pagerank(dg, True, precision=prec)
+        step()
     E = dg.info()["E"]
+    nnz_local = dg.info()["nnz"]
     load = _lib.load()
     load.mr_ctx_profile(ctx.h, 1)
     ctx.sync()
     if dist is not None:
         dist.barrier()
+    build_s[0] = 0.0
     t_start = time.perf_counter()
     for _ in range(args.steps):
-        w, cov = shard.sharded_pagerank(dg, True, precision=prec)
+        w, cov = step()
     ctx.sync()
     if dist is not None:
         dist.barrier()
@@ -262,7 +292,9 @@ def run_c4(args, world, rank, dist):
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "f64" if prec == "fp64" else "f32",
         "data": "synthetic (power-law op popularity, root op in every trace, random call tree; per-rank shards)",
-        "config": {"workload": f"{args.config.upper()} sharded trace_pagerank: {args.c4_ops} ops / {args.c4_traces} "
+        "config": {"workload": f"{args.config.upper()} sharded "
+                               + ("K1 graph build from span shards + " if dev is not None else "")
+                               + f"trace_pagerank: {args.c4_ops} ops / {args.c4_traces} "
                                f"traces over {world} GPU(s), anomaly preference, 25 iterations", "nnz": int(nnz_all),
                    "call_edges": E,
                    "parallelism": f"trace shards x{world}, RCCL " + ("limb" if fused else "fp64 op-sum")
@@ -275,6 +307,11 @@ def run_c4(args, world, rank, dist):
                      "avg_launch_us": round(avg_ms * 1e3, 3), "launches": launches.value,
                      "bytes_per_launch": round(kbytes.value / max(launches.value, 1))},
     }
+    if dev is not None:
+        out["data"] = ("synthetic span shards (power-law ops, root op in every trace, random parent per span, "
+                       "5% broken traces, 1% duplicated root spanIDs across ranks), int-coded, resident in HBM")
+        out["config"]["n_spans_rank0"] = int(n_spans_local)
+        out["build_ms"] = round(build_s[0] / args.steps * 1e3, 3)   # rank 0's K1 share of a step
     if not args.no_cpu and world == 1:
         try:
             out["cpu_baseline"] = c4_cpu_baseline(args.c4_ops, 1_000_000)
@@ -306,6 +343,8 @@ def main():
                     help="c3: distinct seeded windows resident per stream (the batch cycles through them)")
     ap.add_argument("--c4-ops", type=int, default=None, help="c4/c5 op count (default 10k / 100k)")
     ap.add_argument("--c4-traces", type=int, default=None, help="c4/c5 trace count over all ranks (10M / 100M)")
+    ap.add_argument("--from-spans", action="store_true",
+                    help="c4: each rank holds a span shard and a step includes the K1 graph build (mr_graph_build_sharded)")
     args = ap.parse_args()
     if args.precision is None:
         args.precision = "fp32" if args.config == "c5" else "fp64"

@@ -260,6 +260,11 @@ __global__ void k_edge_csr(const uint64_t* skey, int64_t E, int nb, int32_t* ss_
 
 // ---------------------------------------------------------------- indexed build (whole traces)
 constexpr int IX_EPT = 16;  // index entries per thread in k_ix_stats (fewer blocks: fewer global flushes)
+// k_ix_stats: 16-wave blocks (one per CU) whose LDS holds the per-pod-op counts and first rows
+// of up to IX_HIST codes (128 KB) beside the edge set: the C4 graph's 10k ops aggregate in LDS
+// instead of a global atomic pair per index entry
+constexpr int IX_BT = 1024;
+constexpr int IX_HIST = 16384;
 constexpr int IX_B = 8;     // entries per thread whose loads are batched
 // one launch for the indexed build's four initialisations (was four memsets: each a separate
 // ~3 us fill launch, twice per window): per-op counts / first rows, edge keys (EMPTY) / counts
@@ -285,7 +290,7 @@ __global__ void k_ix_sel(const uint8_t* mask, const int32_t* tlen, const int64_t
 // entry-parallel over the index: span counts and first rows per pod-op of the selected traces
 // (LDS-aggregated per block), and their join keys with multiplicity into the block's LDS edge
 // set (hot keys aggregated before global atomics).  Block b takes a 1/gridDim share of each list.
-__global__ void __launch_bounds__(BT) k_ix_stats(const int32_t* tflag, int64_t n_po, const int32_t* po_tr,
+__global__ void __launch_bounds__(IX_BT) k_ix_stats(const int32_t* tflag, int64_t n_po, const int32_t* po_tr,
                                                  const int32_t* po_op, const int32_t* po_cnt, const int32_t* po_first,
                                                  int64_t n_ed, const int32_t* ed_tr, const uint64_t* ed_key,
                                                  const int32_t* ed_cnt, int32_t n_podops, int use_lds_hist,
@@ -297,11 +302,11 @@ __global__ void __launch_bounds__(BT) k_ix_stats(const int32_t* tflag, int64_t n
     int32_t* lcnt = lh;
     int32_t* lfirst = lh + n_podops;
     if (use_lds_hist)
-        for (int32_t i = threadIdx.x; i < n_podops; i += BT) {
+        for (int32_t i = threadIdx.x; i < n_podops; i += IX_BT) {
             lcnt[i] = 0;
             lfirst[i] = 0x7fffffff;
         }
-    for (int i = threadIdx.x; i < ESET; i += BT) {
+    for (int i = threadIdx.x; i < ESET; i += IX_BT) {
         ek[i] = EMPTY;
         ec[i] = 0;
     }
@@ -309,19 +314,19 @@ __global__ void __launch_bounds__(BT) k_ix_stats(const int32_t* tflag, int64_t n
     const int64_t pper = (n_po + gridDim.x - 1) / gridDim.x, eper = (n_ed + gridDim.x - 1) / gridDim.x;
     // loads of a round of IX_B entries per thread go out together, then the trace flags
     const int64_t p0 = (int64_t)blockIdx.x * pper, p1 = min(p0 + pper, n_po);
-    for (int64_t rb = p0; rb < p1; rb += (int64_t)BT * IX_B) {
+    for (int64_t rb = p0; rb < p1; rb += (int64_t)IX_BT * IX_B) {
         int32_t tr[IX_B], op[IX_B], cn[IX_B], fr[IX_B];
         bool on[IX_B];
 #pragma unroll
         for (int j = 0; j < IX_B; ++j) {
-            const int64_t r = min(rb + threadIdx.x + (int64_t)j * BT, p1 - 1);
+            const int64_t r = min(rb + threadIdx.x + (int64_t)j * IX_BT, p1 - 1);
             tr[j] = po_tr[r];
             op[j] = po_op[r];
             cn[j] = po_cnt[r];
             fr[j] = po_first[r];
         }
 #pragma unroll
-        for (int j = 0; j < IX_B; ++j) on[j] = rb + threadIdx.x + (int64_t)j * BT < p1 && tflag[tr[j]];
+        for (int j = 0; j < IX_B; ++j) on[j] = rb + threadIdx.x + (int64_t)j * IX_BT < p1 && tflag[tr[j]];
 #pragma unroll
         for (int j = 0; j < IX_B; ++j) {
             if (!on[j]) continue;
@@ -335,19 +340,19 @@ __global__ void __launch_bounds__(BT) k_ix_stats(const int32_t* tflag, int64_t n
         }
     }
     const int64_t q0 = (int64_t)blockIdx.x * eper, q1 = min(q0 + eper, n_ed);
-    for (int64_t rb = q0; rb < q1; rb += (int64_t)BT * IX_B) {
+    for (int64_t rb = q0; rb < q1; rb += (int64_t)IX_BT * IX_B) {
         int32_t tr[IX_B], cn[IX_B];
         uint64_t ky[IX_B];
         bool on[IX_B];
 #pragma unroll
         for (int j = 0; j < IX_B; ++j) {
-            const int64_t r = min(rb + threadIdx.x + (int64_t)j * BT, q1 - 1);
+            const int64_t r = min(rb + threadIdx.x + (int64_t)j * IX_BT, q1 - 1);
             tr[j] = ed_tr[r];
             ky[j] = ed_key[r];
             cn[j] = ed_cnt[r];
         }
 #pragma unroll
-        for (int j = 0; j < IX_B; ++j) on[j] = rb + threadIdx.x + (int64_t)j * BT < q1 && tflag[tr[j]];
+        for (int j = 0; j < IX_B; ++j) on[j] = rb + threadIdx.x + (int64_t)j * IX_BT < q1 && tflag[tr[j]];
         for (int j = 0; j < IX_B; ++j) {
             if (!on[j]) continue;
             const uint64_t key = ky[j];
@@ -366,10 +371,10 @@ __global__ void __launch_bounds__(BT) k_ix_stats(const int32_t* tflag, int64_t n
         }
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < ESET; i += BT)
+    for (int i = threadIdx.x; i < ESET; i += IX_BT)
         if (ek[i] != EMPTY) global_edge_add(ek[i], ec[i], gk, gc, gmask);
     if (use_lds_hist)
-        for (int32_t i = threadIdx.x; i < n_podops; i += BT)
+        for (int32_t i = threadIdx.x; i < n_podops; i += IX_BT)
             if (lcnt[i]) {
                 atomicAdd(&ocnt[i], lcnt[i]);
                 atomicMin(&ofirst[i], lfirst[i]);
@@ -840,7 +845,7 @@ static int graph_build_indexed(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d
     PhaseTimer pt(st, "build");
     const int32_t NT = sp->n_traces, NP = sp->n_podops;
     CrossJoin X;
-    if (sharded) MR_TRY(cross_exchange(ctx, sp, d_mask, X));
+    if (sharded && ctx->nranks > 1) MR_TRY(cross_exchange(ctx, sp, d_mask, X));   // (one rank: all joins local)
     DBuf<int32_t> tflag, zc;
     DBuf<int64_t> tpos, zoff, tmp;
     MR_TRY(tflag.alloc(ctx, NT));
@@ -862,16 +867,15 @@ static int graph_build_indexed(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d
     if (NT) {
         hipLaunchKernelGGL(k_ix_sel, dim3(cdiv(NT, 256)), dim3(256), 0, st, d_mask, sp->tlen.p, sp->po_off.p, NT, tflag.p,
                            zc.p);
-        const int use_lds = NP <= LDS_HIST;
+        const int use_lds = NP <= IX_HIST;
         const size_t lds = use_lds ? 2 * (size_t)NP * sizeof(int32_t) : 0;
-        // block cap 256 (one per CU): measured on the C2 window (scripts/ab_ix.sh) 1024 -> 101 us,
-        // 512 -> 103, 256 -> 83, 128 -> 106 avg; MR_IX_BLOCKS overrides it for measurements
+        // block cap 256 (one per CU); MR_IX_BLOCKS overrides it for measurements
         static const int ix_cap = [] {
             const char* e = getenv("MR_IX_BLOCKS");
             return e ? std::max(1, atoi(e)) : 256;
         }();
-        const int nblk = std::max(1, std::min(ix_cap, cdiv(std::max(sp->n_po, sp->n_ed), BT * IX_EPT)));
-        hipLaunchKernelGGL(k_ix_stats, dim3(nblk), dim3(BT), lds, st, tflag.p, sp->n_po, sp->po_tr.p, sp->po_op.p,
+        const int nblk = std::max(1, std::min(ix_cap, cdiv(std::max(sp->n_po, sp->n_ed), IX_BT * IX_EPT)));
+        hipLaunchKernelGGL(k_ix_stats, dim3(nblk), dim3(IX_BT), lds, st, tflag.p, sp->n_po, sp->po_tr.p, sp->po_op.p,
                            sp->po_cnt.p, sp->po_first.p, sp->n_ed, sp->ed_tr.p, sp->ed_key.p, sp->ed_cnt.p, NP, use_lds,
                            ocnt.p, ofirst.p, gk.p, gc.p, ecap - 1);
     }

@@ -182,46 +182,90 @@ __global__ void k_relabel_ids(const uint16_t* ids, int64_t n, const int32_t* inv
 }
 
 // ---------------------------------------------------------------- trace-parallel layout (k_tr_a)
-// traces by op count: key = len << 32 | trace
-__global__ void k_tr_keys(const int64_t* off, int32_t T, uint64_t* key) {
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t < T) key[t] = ((uint64_t)(off[t + 1] - off[t]) << 32) | (uint32_t)t;
+// Traces by op count: a counting sort (lengths <= N <= FX_NMAX), order within a length free --
+// nothing numeric depends on it (a trace's ids are rotated by trace mod len, not by position;
+// the accumulator is integer).  Blocks of TRB threads take TRB * TR_PER traces each.
+constexpr int TRB = 1024, TR_PER = 16;
+__global__ void __launch_bounds__(TRB) k_tr_hist(const int64_t* off, int32_t T, int32_t nbin, int32_t* hist) {
+    extern __shared__ int32_t lh[];
+    for (int32_t i = threadIdx.x; i < nbin; i += TRB) lh[i] = 0;
+    __syncthreads();
+    const int64_t t0 = (int64_t)blockIdx.x * TRB * TR_PER;
+    for (int32_t j = 0; j < TR_PER; ++j) {
+        const int64_t t = t0 + (int64_t)j * TRB + threadIdx.x;
+        if (t < T) atomicAdd(&lh[off[t + 1] - off[t]], 1);
+    }
+    __syncthreads();
+    for (int32_t i = threadIdx.x; i < nbin; i += TRB)
+        if (lh[i]) atomicAdd(&hist[i], lh[i]);
 }
-__global__ void k_tr_perm(const uint64_t* key, int32_t T, const float* w_t, int32_t* tperm, float* w_tp) {
-    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= T) return;
-    const int32_t t = (int32_t)(uint32_t)key[p];
-    tperm[p] = t;
-    w_tp[p] = w_t[t];
+// positions: bin start (cursor, claimed per block and bin) + the trace's rank in its block's bin
+__global__ void __launch_bounds__(TRB) k_tr_place(const int64_t* off, int32_t T, int32_t nbin,
+                                                  unsigned long long* cursor, const float* w_t, int32_t* tperm,
+                                                  float* w_tp) {
+    extern __shared__ int32_t lh[];
+    int32_t* lbase = lh + nbin;
+    for (int32_t i = threadIdx.x; i < nbin; i += TRB) lh[i] = 0;
+    __syncthreads();
+    const int64_t t0 = (int64_t)blockIdx.x * TRB * TR_PER;
+    int32_t rk[TR_PER], ln[TR_PER];
+#pragma unroll
+    for (int32_t j = 0; j < TR_PER; ++j) {
+        const int64_t t = t0 + (int64_t)j * TRB + threadIdx.x;
+        ln[j] = t < T ? (int32_t)(off[t + 1] - off[t]) : -1;
+        rk[j] = ln[j] >= 0 ? atomicAdd(&lh[ln[j]], 1) : 0;
+    }
+    __syncthreads();
+    for (int32_t i = threadIdx.x; i < nbin; i += TRB)
+        if (lh[i]) lbase[i] = (int32_t)atomicAdd(&cursor[i], (unsigned long long)lh[i]);
+    __syncthreads();
+#pragma unroll
+    for (int32_t j = 0; j < TR_PER; ++j) {
+        if (ln[j] < 0) continue;
+        const int32_t t = (int32_t)(t0 + (int64_t)j * TRB + threadIdx.x);
+        const int32_t p = lbase[ln[j]] + rk[j];
+        tperm[p] = t;
+        w_tp[p] = w_t[t];
+    }
 }
-// chunks of 4 ids per tile: its last position holds its longest trace (ascending sort)
-__global__ void k_tr_chunks(const uint64_t* key, int32_t T, int32_t n_wt, int64_t* nch) {
+// chunks of 4 ids per tile: its last position holds its longest trace (ascending lengths)
+__global__ void k_tr_chunks(const int32_t* tperm, const int64_t* off, int32_t T, int32_t n_wt, int64_t* nch) {
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k < n_wt) nch[k] = (int64_t)(((key[min(k * WAVE + WAVE - 1, (int64_t)T - 1)] >> 32) + 3) >> 2);
+    if (k >= n_wt) return;
+    const int32_t t = tperm[min(k * WAVE + WAVE - 1, (int64_t)T - 1)];
+    nch[k] = (off[t + 1] - off[t] + 3) >> 2;
 }
 __global__ void k_tr_coff(const int64_t* c64, int32_t n, int32_t* coff) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i <= n) coff[i] = (int32_t)c64[i];
 }
-// thread per (tile, lane): the lane's trace rotated by (lane mod len), then pads N + lane
-__global__ void k_tr_fill(const uint64_t* key, const int64_t* off, const uint16_t* ids, const int64_t* c64, int32_t T,
+// thread per (tile, lane): the lane's trace rotated by (trace mod len), then pads N + lane
+__global__ void k_tr_fill(const int32_t* tperm, const int64_t* off, const uint16_t* ids, const int64_t* c64, int32_t T,
                           int32_t N, int32_t n_wt, uint16_t* tids) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (int64_t)n_wt * WAVE) return;
     const int32_t k = (int32_t)(i / WAVE), lane = (int32_t)(i % WAVE);
     const int64_t p = (int64_t)k * WAVE + lane;
-    int64_t a = 0, len = 0;
+    int64_t a = 0, len = 0, rot = 0;
     if (p < T) {
-        const int32_t t = (int32_t)(uint32_t)key[p];
+        const int32_t t = tperm[p];
         a = off[t];
         len = off[t + 1] - a;
+        rot = len ? t % len : 0;
     }
-    const int64_t rot = len ? lane % len : 0, n4 = (c64[k + 1] - c64[k]) * 4;
-    uint16_t* dst = tids + (size_t)c64[k] * (WAVE * 4) + (size_t)lane * 4;
-    for (int64_t j = 0; j < n4; ++j) {
-        int64_t jj = j + rot;
-        if (jj >= len) jj -= len;
-        dst[(size_t)(j >> 2) * (WAVE * 4) + (j & 3)] = j < len ? ids[a + jj] : (uint16_t)(N + lane);
+    const int64_t nc = c64[k + 1] - c64[k];
+    unsigned long long* dst = (unsigned long long*)tids + (size_t)c64[k] * WAVE + lane;   // 4 ids per 8-B store
+    int64_t jj = rot;
+    for (int64_t c = 0; c < nc; ++c) {
+        unsigned long long v = 0ull;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int64_t j = 4 * c + q;
+            const uint16_t id = j < len ? ids[a + jj] : (uint16_t)(N + lane);
+            if (j < len && ++jj == len) jj = 0;
+            v |= (unsigned long long)id << (16 * q);
+        }
+        dst[(size_t)c * WAVE] = v;
     }
 }
 __global__ void k_tr_gather(const float* src, const int32_t* tperm, int32_t T, float* dst) {
@@ -693,6 +737,7 @@ struct GDev {
     double* op_sum;                // sharded tile path: [N] pair-partial sums per op
     unsigned long long* stamp;   // diagnostics (MR_FX_STAMP): per-block phase clocks, else null
     double fx_scale, fx_iscale;
+    double alpha;                  // P_ss weight (k_fx_b's call-graph term)
     int32_t T, N, n_tb, n_tiles, tshift, lds_su, blk0, n_ob, blk0b;
     int32_t blk0f, n_fa, blk0fb, n_fb;   // fused path: k_fx_a / k_fx_b block ranges
     int32_t fb_ops;                      // k_fx_b ops per block
@@ -1850,22 +1895,7 @@ __global__ void __launch_bounds__(NT) k_tr_a(const GDev* __restrict__ gs, int32_
 #undef TR_STEP
     tr_done:;
     }
-    // call-graph term for the next s' (pagerank.py:122-124, alpha P_ss s_k), a thread per op
-    {
-        const GLB double* sp_cur = gp(G.spb[cur]);
-        const GLB int64_t* ss_off = gp(G.ss_off);
-        const GLB int32_t* ss_par = gp(G.ss_par);
-        const GLB float* pw = gp(G.pw);
-        GLB double* ssv = gpw(G.fx_ssv);
-        for (int32_t oss = lb * NT + tid; oss < N; oss += G.n_fa * NT) {
-            double bb = 0.0;
-            for (int64_t e = ss_off[oss]; e < ss_off[oss + 1]; ++e) {
-                const int32_t pp = ss_par[e];
-                bb += (double)pw[pp] * sp_cur[pp];
-            }
-            ssv[oss] = alpha * (bb / Ms);
-        }
-    }
+    // (the call-graph term alpha P_ss s_k is k_fx_b's: a wave per op)
     __syncthreads();
     GLB unsigned long long* prow = gpw(G.fx_part) + (size_t)lb * N;
     for (int32_t o = tid; o < N; o += NT) prow[o] = lacc[o];
@@ -1886,18 +1916,43 @@ static int fb_ops(int32_t N) { return N <= 8192 ? 16 : 32; }
 __global__ void __launch_bounds__(WAVE * FB_W) k_fx_b(const GDev* __restrict__ gs, int32_t ng, int32_t split,
                                                      double d, int it, int mode) {
     __shared__ unsigned long long slo[FB_W * WAVE], shi[FB_W * WAVE];
+    __shared__ double lssv[WAVE];
     const GDev& G = gs[fx_graph(gs, ng, split, 3)];
     const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
     const int32_t OPB = G.fb_ops, GR = WAVE / OPB;
     const int32_t ol = lane % OPB, grp = lane / OPB;
     // o: the column (the fused kernel's op label); op: the graph's op (perm: relabelled graphs)
-    const int32_t o = ((int32_t)blockIdx.x - G.blk0fb) * OPB + ol;
+    const int32_t o0 = ((int32_t)blockIdx.x - G.blk0fb) * OPB;
+    const int32_t o = o0 + ol;
     const int32_t N = G.N, nb = G.n_fa;
     const bool on = o < N;
+    const int k3c = it % 3;
+    // the call-graph term alpha (P_ss s_k)[op] / M_s(k) (pagerank.py:122-124) of the block's ops: a
+    // wave per op, its lanes striding the op's parents, one fixed-order wave sum (a hub op with
+    // thousands of parents costs one wave, not one thread)
+    {
+        const double Ms = wave_max(bits2d(G.mslot[(size_t)2 * MSH * k3c + lane]));
+        const GLB double* sp_cur = gp(G.spb[it & 1]);
+        const GLB int64_t* ss_off = gp(G.ss_off);
+        const GLB int32_t* ss_par = gp(G.ss_par);
+        const GLB float* pw = gp(G.pw);
+        for (int32_t j = w; j < OPB; j += FB_W) {
+            const int32_t oj = o0 + j;
+            if (oj >= N) break;
+            const int32_t opj = G.perm ? G.perm[oj] : oj;
+            const int64_t e0 = ss_off[opj], e1 = ss_off[opj + 1];
+            double bb = 0.0;
+            for (int64_t e = e0 + lane; e < e1; e += WAVE) {
+                const int32_t pp = ss_par[e];
+                bb += (double)pw[pp] * sp_cur[pp];
+            }
+            bb = wave_sum(bb);
+            if (lane == 0) lssv[j] = G.alpha * (bb / Ms);
+        }
+    }
     // the finishing lanes' operands, loaded before the rows so both latencies overlap
     const bool fin = w == 0 && lane < OPB && on;
     const int32_t op = fin && G.perm ? G.perm[o] : o;
-    const double ssv = fin ? G.fx_ssv[op] : 0.0;
     const float uo = fin ? G.u_o[op] : 0.0f;
     if ((int32_t)blockIdx.x == G.blk0fb && w == 1 && mode) {   // r' maxima riding on the limb sum
         unsigned long long* Mn = G.mslot + (size_t)2 * MSH * ((it % 3 + 1) % 3);
@@ -1950,6 +2005,7 @@ __global__ void __launch_bounds__(WAVE * FB_W) k_fx_b(const GDev* __restrict__ g
     }
     const int nxt = (it & 1) ^ 1, k3 = it % 3;
     unsigned long long* Mnext = G.mslot + (size_t)2 * MSH * ((k3 + 1) % 3);
+    const double ssv = lssv[lane];   // (written before the barrier above)
     // hi, lo < 2^53 (fewer than 2^21 rows over all ranks): both conversions exact, one rounding
     const double sum = ((double)hi * 4294967296.0 + (double)lo) * G.fx_iscale;
     const double v = d * (sum + ssv);      // pagerank.py:122-124
@@ -2316,20 +2372,27 @@ static int tr_layout(mr_ctx* ctx, mr_graph* g) {
     const int32_t W = cdiv(T, WAVE);
     g->n_wt = W;
     g->wtile_nw = 0;
-    DBuf<uint64_t> key;
-    DBuf<int64_t> c64, tmp;
-    MR_TRY(key.alloc(ctx, (size_t)std::max(T, 1)));
+    const int32_t nbin = N + 1;   // trace lengths 1..N (distinct ops)
+    DBuf<int32_t> hist;
+    DBuf<int64_t> boff, c64, tmp;
+    DBuf<unsigned long long> cursor;
+    MR_TRY(hist.zero(ctx, (size_t)nbin));
+    MR_TRY(boff.alloc(ctx, (size_t)nbin + 1));
     MR_TRY(c64.alloc(ctx, (size_t)W + 1));
-    MR_TRY(tmp.alloc(ctx, (size_t)scan_tmp_elems(std::max<int64_t>(W, 1))));
+    MR_TRY(tmp.alloc(ctx, (size_t)std::max(scan_tmp_elems(std::max<int64_t>(W, 1)), scan_tmp_elems(nbin))));
     MR_TRY(g->tperm.alloc(ctx, (size_t)std::max(T, 1)));
     MR_TRY(g->w_tp.alloc(ctx, (size_t)std::max(T, 1)));
     MR_TRY(g->coff.alloc(ctx, (size_t)W + 1));
     if (T) {
-        hipLaunchKernelGGL(k_tr_keys, dim3(cdiv(T, 256)), dim3(256), 0, st, g->rs_off.p, T, key.p);
-        SortScratch ws;
-        MR_TRY(mr_radix_sort(ctx, key.p, nullptr, T, 32 + bits_for((uint64_t)std::max(N, 1)), ws));
-        hipLaunchKernelGGL(k_tr_perm, dim3(cdiv(T, 256)), dim3(256), 0, st, key.p, T, g->w_t.p, g->tperm.p, g->w_tp.p);
-        hipLaunchKernelGGL(k_tr_chunks, dim3(cdiv(W, 256)), dim3(256), 0, st, key.p, T, W, c64.p);
+        const int nb = cdiv(T, (int64_t)TRB * TR_PER);
+        hipLaunchKernelGGL(k_tr_hist, dim3(nb), dim3(TRB), (size_t)nbin * sizeof(int32_t), st, g->rs_off.p, T, nbin,
+                           hist.p);
+        MR_TRY(mr_exclusive_scan_i32(ctx, hist.p, boff.p, nbin, tmp.p));
+        MR_TRY(cursor.alloc(ctx, (size_t)nbin));
+        MR_TRY_HIP(ctx, hipMemcpyAsync(cursor.p, boff.p, (size_t)nbin * sizeof(int64_t), hipMemcpyDeviceToDevice, st));
+        hipLaunchKernelGGL(k_tr_place, dim3(nb), dim3(TRB), 2 * (size_t)nbin * sizeof(int32_t), st, g->rs_off.p, T,
+                           nbin, cursor.p, g->w_t.p, g->tperm.p, g->w_tp.p);
+        hipLaunchKernelGGL(k_tr_chunks, dim3(cdiv(W, 256)), dim3(256), 0, st, g->tperm.p, g->rs_off.p, T, W, c64.p);
     }
     MR_TRY(mr_exclusive_scan(ctx, c64.p, c64.p, W, tmp.p));
     hipLaunchKernelGGL(k_tr_coff, dim3(cdiv((int64_t)W + 1, 256)), dim3(256), 0, st, c64.p, W, g->coff.p);
@@ -2340,8 +2403,8 @@ static int tr_layout(mr_ctx* ctx, mr_graph* g) {
     MR_TRY(g->tids.alloc(ctx, (size_t)std::max<int64_t>(nch, 1) * WAVE * 4));
     const uint16_t* src = g->relabeled ? g->rsp.p : g->rs16.p;
     if (W)
-        hipLaunchKernelGGL(k_tr_fill, dim3(cdiv((int64_t)W * WAVE, 256)), dim3(256), 0, st, key.p, g->rs_off.p, src, c64.p,
-                           T, N, W, g->tids.p);
+        hipLaunchKernelGGL(k_tr_fill, dim3(cdiv((int64_t)W * WAVE, 256)), dim3(256), 0, st, g->tperm.p, g->rs_off.p, src,
+                           c64.p, T, N, W, g->tids.p);
     MR_TRY_HIP(ctx, hipGetLastError());
     return MR_OK;   // (scratch returns to the stream-ordered pool)
 }
@@ -2723,6 +2786,7 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         const int sc = sharded ? 48
                                : plan.v2 ? 64 - bits_for((uint64_t)std::max<int64_t>(tpb, 1))
                                          : 63 - bits_for((uint64_t)std::max<int64_t>(tpb - 1, 1));
+        v.alpha = alpha;
         v.fx_scale = std::ldexp(1.0, sc);
         v.fx_iscale = std::ldexp(1.0, -sc);
         v.T = g->T;

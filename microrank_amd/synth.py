@@ -383,3 +383,73 @@ def big_graph(n_ops: int, n_traces: int, seed: int = 11, spans_mean: float = 19.
     nchild = np.bincount(parent, minlength=N).astype(np.int32)
     return HostGraph(range(N), range(T), sr_off, sr_ops, None, None, len_t, len_o, ss_off, ss_par, nchild,
                      None, None)
+
+
+_SPAN_SLOTS = 32   # C4 span tables: at most this many spans per trace (global row = trace * 32 + j)
+
+
+def big_spans(n_ops: int, n_traces: int, seed: int = 11, spans_mean: float = 19.0,
+              dup_frac: float = 0.01, broken_frac: float = 0.05, shard: tuple | None = None) -> SpanTable:
+    """A C4-scale SPAN table (codes only), generated vectorised for K1-inclusive benchmarks.
+    Ops form a random call tree (op o > 0 has one parent op < o, the same tree on every rank);
+    per trace ~Poisson(spans_mean) spans (capped at 32): the first is the root op, each later
+    span picks a uniformly chosen earlier span of the trace as its parent and one of the parent
+    op's child ops (a leaf op's child: the next op code -- edges off the tree, at most n_ops).
+    ``broken_frac`` of the traces lose one non-root span (orphans, T11) and ``dup_frac`` of the
+    rows reuse the spanID of a random trace's root span -- often a trace of another rank, so the
+    ParentSpanId join crosses shards (T11).  Pod-op = service-op = op.
+
+    ``shard=(rank, world)``: this rank's share of the n_traces traces (a contiguous trace-code
+    range) with global codes; rows are trace-major and ``row`` = trace * 32 + span slot (a
+    monotone global row index: first appearance, T10)."""
+    rank, world = shard if shard is not None else (0, 1)
+    base, rem = divmod(n_traces, world)
+    t_lo = rank * base + min(rank, rem)
+    T = base + (1 if rank < rem else 0)
+    N = int(n_ops)
+    trng = np.random.default_rng(seed)                                 # the op tree: every rank alike
+    child = np.arange(1, N, dtype=np.int64)
+    par_op = (trng.random(N - 1) * child).astype(np.int64)
+    order = np.argsort(par_op, kind="stable")
+    ch_list = child[order]
+    ch_off = np.zeros(N + 1, np.int64)
+    np.cumsum(np.bincount(par_op, minlength=N), out=ch_off[1:])
+    rng = np.random.default_rng((seed, rank, world))
+    k = np.clip(rng.poisson(spans_mean - 1.0, T) + 1, 1, _SPAN_SLOTS).astype(np.int64)
+    M = np.zeros((T, _SPAN_SLOTS), np.int32)                           # op of slot j of each trace
+    P = np.full((T, _SPAN_SLOTS), -1, np.int8)                         # parent slot
+    for j in range(1, _SPAN_SLOTS):
+        live = np.flatnonzero(k > j)
+        if live.size == 0:
+            break
+        pj = (rng.random(live.size) * j).astype(np.int64)
+        po = M[live, pj].astype(np.int64)
+        nch = ch_off[po + 1] - ch_off[po]
+        pick = ch_off[po] + (rng.random(live.size) * np.maximum(nch, 1)).astype(np.int64)
+        M[live, j] = np.where(nch > 0, ch_list[np.minimum(pick, ch_list.size - 1)], (po + 1) % N).astype(np.int32)
+        P[live, j] = pj.astype(np.int8)
+    S0 = int(k.sum())
+    valid = np.arange(_SPAN_SLOTS)[None, :] < k[:, None]
+    tr = np.repeat(np.arange(T, dtype=np.int64), k)
+    j = np.nonzero(valid)[1].astype(np.int64)
+    gtr = tr + t_lo
+    op = M[valid]
+    pslot = P[valid].astype(np.int64)
+    del M, P, valid
+    code = gtr * _SPAN_SLOTS + j                                       # spanID code = global row slot
+    parent = np.where(pslot >= 0, gtr * _SPAN_SLOTS + pslot, -1)
+    start = np.zeros(T + 1, np.int64)
+    np.cumsum(k, out=start[1:])
+    keep = np.ones(S0, bool)
+    bt = np.flatnonzero((rng.random(T) < broken_frac) & (k > 1))
+    keep[start[bt] + 1 + (rng.random(bt.size) * (k[bt] - 1)).astype(np.int64)] = False
+    if dup_frac > 0:
+        d = np.flatnonzero(rng.random(S0) < dup_frac)
+        code[d] = rng.integers(0, n_traces, d.size) * _SPAN_SLOTS      # a root spanID, any rank
+    dur = rng.integers(1_000, 2_000_000, S0)
+    t_start = (1_700_000_000 * 10**9 + gtr * 1000).astype(np.int64)
+    sl = keep
+    return SpanTable(trace=gtr[sl].astype(np.int32), podop=op[sl], svcop=op[sl], span=code[sl],
+                     parent=parent[sl], duration=dur[sl], tstart=t_start[sl], tend=t_start[sl] + dur[sl] * 1000,
+                     trace_names=range(n_traces), podop_names=range(N), svcop_names=range(N),
+                     row=(gtr[sl] * _SPAN_SLOTS + j[sl]).astype(np.int32))
