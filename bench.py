@@ -86,7 +86,7 @@ def run_window(ctx, dev, t0, t1, a3, ok, prec):
     return edges.value, codes[:n_out.value].copy(), scores[:n_out.value].copy(), na.value, nn.value
 
 
-ITER_KERNELS = ("k_fx_a", "k_fx_b", "k_iter_a", "k_iter_b")
+ITER_KERNELS = ("k_tr_a", "k_wv_a", "k_fx_a", "k_fx_b", "k_iter_a", "k_iter_b")
 
 
 def pmc_traffic(args, timeout_s=240):
@@ -114,7 +114,7 @@ def pmc_traffic(args, timeout_s=240):
             if args.config in ("c4", "c5"):
                 cmd += ["--config", args.config, "--c4-ops", str(args.c4_ops), "--c4-traces", str(args.c4_traces)]
             else:
-                cmd += ["--streams", "1", "--ops", str(args.ops), "--traces", str(args.traces)]
+                cmd += ["--streams", str(args.streams), "--ops", str(args.ops), "--traces", str(args.traces)]
             try:
                 subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
                                timeout=timeout_s, check=True)
@@ -126,7 +126,7 @@ def pmc_traffic(args, timeout_s=240):
                     name = r["Kernel_Name"]
                     if r["Counter_Name"] == ctr and any(k in name for k in ITER_KERNELS):
                         per_iter += float(r["Counter_Value"])
-                        n_a += any(k in name for k in ("k_fx_a", "k_iter_a"))
+                        n_a += any(k in name for k in ("k_tr_a", "k_wv_a", "k_fx_a", "k_iter_a"))
             if n_a == 0:
                 return None
             vals[ctr] = per_iter / n_a * 1024.0   # KB -> bytes, per iteration
@@ -333,6 +333,8 @@ def main():
     ap.add_argument("--streams", type=int, default=8,
                     help="c2: independent windows ranked concurrently per GPU, one context/stream/host thread each")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC passes for roofline.traffic")
+    ap.add_argument("--streams-mode", action="store_true",
+                    help="c2/c3: W contexts + W host threads, one mr_rca_window per window (instead of mr_windows_batch)")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--config", choices=["c2", "c3", "c4", "c5"], default="c2",
                     help="c2: RCA windows (default, weak scaling); c3: a batch of --c3-windows 500-op / 20k-trace "
@@ -394,18 +396,27 @@ def main():
     # within one device).  A step ranks all W windows.
     W = max(1, args.streams)
     dev_id = int(os.environ["MICRORANK_DEVICE"])
-    ctxs = [_lib.default_context()] + [_lib.Context(dev_id) for _ in range(W - 1)]
+    batch = not args.streams_mode
+    # batch (default): one context; a step is ONE mr_windows_batch call over W windows (their
+    # detectors / builds / spectra on the library's auxiliary streams, their PageRanks sharing
+    # each iteration's launches).  --streams-mode: W contexts driven by W host threads, one
+    # mr_rca_window call per window (round-1 design, kept for A/B).
+    ctxs = [_lib.default_context()] + ([] if batch else [_lib.Context(dev_id) for _ in range(W - 1)])
     # c2: the same window's spans on every context (separate HBM copies): every window of a step is
     # the configured C2 window, so GTEPS and windows/s stay comparable across W.
     # c3: D distinct seeded windows per context; the rank's share of the batch cycles through them.
     D = max(1, args.c3_distinct) if args.config == "c3" else 1
-    wins = [[] for _ in ctxs]   # per context: [(dev, t0, t1, a3, ok, abnormal)]
+    wins = [[] for _ in range(1 if batch else W)]   # per context: [(dev, t0, t1, a3, ok, abnormal)]
     for d in range(D):
         seed = 1234 + 7919 * rank + 104729 * d
         if d == 0 or args.config == "c3":
             topo, normal, abnormal = make_window(seed, args.ops, args.traces)
         t0 = int(abnormal.tstart.min())
-        for ci, cx in enumerate(ctxs):
+        for ci in range(W):
+            cx = ctxs[0] if batch else ctxs[ci]
+            if batch and ci > 0 and args.config != "c3":   # c2: W copies of the one window
+                wins[0].append(wins[0][0])
+                continue
             if args.config == "c3" and D * W > 1:
                 # distinct windows on every context too (one generator call per (context, d))
                 if ci > 0:
@@ -413,7 +424,7 @@ def main():
                     t0 = int(abnormal.tstart.min())
             a3, ok = slo_from_gpu(cx, normal)
             dev = DeviceSpans(cx, abnormal)          # window spans resident in HBM from here on
-            wins[ci].append((dev, t0, t0 + 5 * 60 * 10**9, a3, ok, abnormal))
+            wins[0 if batch else ci].append((dev, t0, t0 + 5 * 60 * 10**9, a3, ok, abnormal))
     del topo, normal
     ctx = ctxs[0]
     dev0, t0, t1, a3, ok, abnormal = wins[0][0]
@@ -421,7 +432,7 @@ def main():
     if args.config == "c3":
         # this rank's share of the batch, dealt round-robin over its contexts
         share = args.c3_windows // world + (1 if rank < args.c3_windows % world else 0)
-        per_ctx = [len(range(ci, share, W)) for ci in range(W)]
+        per_ctx = [len(range(ci, share, W)) for ci in range(W)] if not batch else None
     else:
         share, per_ctx = None, None
 
@@ -432,8 +443,27 @@ def main():
             dist.barrier()
 
     def run_all(n):
-        """n steps on every context; (edges, the first context's last result).  c2: a step is one
-        window per context; c3: a step is the rank's share of the batch."""
+        """n steps; (edges, windows, the first window's last result).  c2: a step is W windows;
+        c3: a step is the rank's share of the batch."""
+        if batch:
+            from microrank_amd.online_rca import rank_windows
+
+            pool = wins[0]
+            per_step = share if share is not None else W
+            res, first = [], None
+            for _ in range(n):
+                for c0 in range(0, per_step, 64):   # c3: calls of <= 64 windows
+                    idx = range(c0, min(per_step, c0 + 64))
+                    out = rank_windows(ctx, [pool[j % len(pool)][:5] for j in idx],
+                                       precision="fp32" if prec == _lib.MR_FP32 else "fp64")
+                    for j, (codes, scores, na_, nn_, e_, st_) in zip(idx, out):
+                        if st_ != 0:
+                            raise RuntimeError(f"window {j}: status {st_}")
+                        res.append(e_)
+                        if j % len(pool) == 0:
+                            first = (e_, codes, scores, na_, nn_)
+            return sum(res), len(res), first
+
         def one(ci):
             cx, res = ctxs[ci], []
             cnt = n * (per_ctx[ci] if per_ctx is not None else 1)
@@ -506,10 +536,14 @@ def main():
                    "n_spans": int(abnormal.n_spans), "n_abnormal": na, "n_normal": nn,
                    "edges_per_window": int(edges // max(n_win, 1)),
                    "windows_per_step": (win_all // args.steps) if c3 else W,
-                   "parallelism": f"windows x{world} ranks x{W} streams"},
+                   "parallelism": (f"windows x{world} ranks, mr_windows_batch of {W} windows per call "
+                                   f"(PageRanks of all {2 * W} graphs share each iteration's launches)") if batch
+                                  else f"windows x{world} ranks x{W} streams"},
         "windows_per_s": round(win_all / elapsed, 3),
-        "roofline": {"bound": "hbm", "kernel": "one Jacobi iteration: k_fx_a + k_fx_b (fused path)"
-                                               + (f", stream 0 of {W} concurrent windows" if W > 1 else ""),
+        "roofline": {"bound": "hbm", "kernel": ("one Jacobi iteration of the batch's graphs: k_tr_a + k_fx_b "
+                                                f"launches over {2 * W} graphs") if batch else
+                                               ("one Jacobi iteration: k_tr_a + k_fx_b (fused path)"
+                                                + (f", stream 0 of {W} concurrent windows" if W > 1 else "")),
                      "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": None if traffic is None else round(traffic["fetch"] + traffic["write"]),

@@ -192,6 +192,20 @@ int mr_rca_window(mr_ctx* ctx, const mr_spans* s, int64_t t0, int64_t t1, const 
                   int32_t* out_podop, double* out_score, int32_t* n_out, int64_t* edges_traversed,
                   int32_t* n_abnormal, int32_t* n_normal);
 
+/* C3: rank n_windows RCA windows in one call -- each as mr_rca_window.  Window i:
+ * spans[i] (a span table of this context; windows may share one), [t0[i], t1[i]], the SLO
+ * a3[i] / a3_valid[i] (n_svcops of spans[i]).  The windows' detectors and graph builds run
+ * concurrently on auxiliary streams of this context, the PageRanks of all their graphs share
+ * each power iteration's launches, then the spectra run concurrently.  Per window i:
+ * out_podop / out_score[i * (top_max + 6) ..], n_out[i], edges_traversed[i], n_abnormal[i],
+ * n_normal[i], status[i] (MR_OK, or MR_ERR_VALUE for an empty window -- the reference's
+ * unpack of False, T2).  Replaces a loop of online_anomaly_detect_RCA windows
+ * (online_rca.py:161-216) over independent windows. */
+int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* const* spans, const int64_t* t0,
+                     const int64_t* t1, const double* const* a3, const uint8_t* const* a3_valid, int method,
+                     int32_t top_max, int precision, int32_t* out_podop, double* out_score, int32_t* n_out,
+                     int64_t* edges_traversed, int32_t* n_abnormal, int32_t* n_normal, int32_t* status);
+
 /* ------------------------------------------------------------------ multi-GPU (RCCL over xGMI)
  * One process per GPU.  The unique id (128 bytes) is produced by rank 0 and broadcast by the
  * caller (torch.distributed / any host channel).  Used by the trace-sharded PageRank. */

@@ -73,6 +73,9 @@ SIGNATURES = {
                               C.c_int, C.c_int32, i32p, f64p, i32p, i32p]),
     "mr_slo": (C.c_int, [P, P, f64p, f64p, i64p]),
     "mr_detect": (C.c_int, [P, P, C.c_int64, C.c_int64, f64p, u8p, u8p, i32p, i32p, i64p]),
+    "mr_windows_batch": (C.c_int, [P, C.c_int32, C.POINTER(P), i64p, i64p, C.POINTER(C.c_void_p),
+                                   C.POINTER(C.c_void_p), C.c_int, C.c_int32, C.c_int, i32p, f64p, i32p, i64p, i32p,
+                                   i32p, i32p]),
     "mr_rca_window": (C.c_int, [P, P, C.c_int64, C.c_int64, f64p, u8p, C.c_int, C.c_int32, C.c_int,
                                 i32p, f64p, i32p, i64p, i32p, i32p]),
     "mr_comm_unique_id": (C.c_int, [C.POINTER(C.c_uint8)]),

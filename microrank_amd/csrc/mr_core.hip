@@ -174,6 +174,8 @@ extern "C" void mr_ctx_destroy(mr_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
+    for (mr_ctx* a : ctx->aux) mr_ctx_destroy(a);
+    ctx->aux.clear();
     {   // the context's live handles go first (their buffers return to its pool)
         std::vector<std::pair<void*, void (*)(void*)>> mine;
         {

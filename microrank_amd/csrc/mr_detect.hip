@@ -13,6 +13,11 @@
 #include <utility>
 #include <vector>
 #include <climits>
+#include <condition_variable>
+#include <deque>
+#include <mutex>
+#include <string>
+#include <thread>
 
 #include "mr_prim.h"
 #include "mr_sort.h"
@@ -242,116 +247,268 @@ __global__ void k_top_codes(const int32_t* idx, const int32_t* uc, int32_t k, in
 }
 }  // namespace
 
-// One RCA window (online_rca.py:164-215) with every intermediate in HBM.
-extern "C" int mr_rca_window(mr_ctx* ctx, const mr_spans* s, int64_t t0, int64_t t1, const double* a3,
-                             const uint8_t* a3_valid, int method, int32_t top_max, int precision, int32_t* out_podop,
-                             double* out_score, int32_t* n_out, int64_t* edges_traversed, int32_t* n_abnormal,
-                             int32_t* n_normal) {
-    if (!ctx || !s || s->ctx != ctx || !a3 || !a3_valid || !n_out) return mr_fail(ctx, MR_ERR_ARG, "mr_rca_window: bad arguments");
-    MR_TRY_HIP(ctx, hipSetDevice(ctx->device));
-    hipStream_t st = ctx->stream;
-    *n_out = 0;
-    if (edges_traversed) *edges_traversed = 0;
-    // MR_WIN_TIMING: wall time of each phase (a stream sync at each mark; diagnostics only)
-    static const bool timing = getenv("MR_WIN_TIMING") != nullptr;
-    std::vector<std::pair<const char*, std::chrono::steady_clock::time_point>> marks;
-    auto mark = [&](const char* name) {
-        if (!timing) return;
+// One RCA window (online_rca.py:164-215) with every intermediate in HBM, in three phases so a
+// batch of windows can overlap them: detect + both graph builds (any context), the two
+// PageRanks (batched with other windows' graphs), the spectrum over the union.
+struct WinRun {
+    int rc = MR_OK;
+    int32_t na = 0, nn = 0;
+    int64_t nin = 0;
+    mr_graph *gn = nullptr, *ga = nullptr;   // "normal" graph (detector's abnormal traces), "anomaly" graph
+    ~WinRun() {
+        delete gn;
+        delete ga;
+    }
+};
+
+// MR_WIN_TIMING: wall time of each phase (a stream sync at each mark; diagnostics only)
+struct WinMarks {
+    hipStream_t st;
+    bool on;
+    std::vector<std::pair<const char*, std::chrono::steady_clock::time_point>> m;
+    explicit WinMarks(hipStream_t s) : st(s), on(getenv("MR_WIN_TIMING") != nullptr) {}
+    void mark(const char* name) {
+        if (!on) return;
         (void)hipStreamSynchronize(st);
-        marks.emplace_back(name, std::chrono::steady_clock::now());
-    };
-    struct Report {
-        decltype(marks)& m;
-        ~Report() {
-            if (m.size() < 2) return;
-            fprintf(stderr, "[window]");
-            for (size_t i = 1; i < m.size(); ++i)
-                fprintf(stderr, " %s %.1f", m[i].first,
-                        std::chrono::duration<double, std::micro>(m[i].second - m[i - 1].second).count());
-            fprintf(stderr, " us\n");
-        }
-    } report{marks};
-    mark("start");
-    const int32_t NT = s->n_traces, NP = s->n_podops;
+        m.emplace_back(name, std::chrono::steady_clock::now());
+    }
+    ~WinMarks() {
+        if (m.size() < 2) return;
+        fprintf(stderr, "[window]");
+        for (size_t i = 1; i < m.size(); ++i)
+            fprintf(stderr, " %s %.1f", m[i].first, std::chrono::duration<double, std::micro>(m[i].second - m[i - 1].second).count());
+        fprintf(stderr, " us\n");
+    }
+};
+
+static int win_detect_build(mr_ctx* ctx, const mr_spans* s, int64_t t0, int64_t t1, const double* a3,
+                            const uint8_t* a3_valid, WinRun& w, WinMarks* mk) {
+    hipStream_t st = ctx->stream;
+    const int32_t NT = s->n_traces;
     DBuf<double> da3;
     DBuf<uint8_t> dv, dst, m_abn, m_nor;
     MR_TRY(da3.upload(ctx, a3, s->n_svcops));
     MR_TRY(dv.upload(ctx, a3_valid, s->n_svcops));
     MR_TRY(dst.zero(ctx, NT));
-    int32_t na = 0, nn = 0;
-    int64_t nin = 0;
-    MR_TRY(detect_dev(ctx, s, t0, t1, da3.p, dv.p, dst.p, &na, &nn, &nin));
-    mark("detect");
-    if (n_abnormal) *n_abnormal = na;
-    if (n_normal) *n_normal = nn;
+    MR_TRY(detect_dev(ctx, s, t0, t1, da3.p, dv.p, dst.p, &w.na, &w.nn, &w.nin));
+    if (mk) mk->mark("detect");
     // T1: the driver unpacks (flag, normal_list, abnormal_list) from (flag, abnormal, normal)
-    if (na == 0 || nn == 0) return MR_OK;   // no anomaly, or one list empty: nothing is ranked
+    if (w.na == 0 || w.nn == 0) return MR_OK;   // no anomaly, or one list empty: nothing is ranked
     MR_TRY(m_abn.alloc(ctx, NT));
     MR_TRY(m_nor.alloc(ctx, NT));
     hipLaunchKernelGGL(k_masks, dim3(cdiv(NT, 256)), dim3(256), 0, st, dst.p, NT, m_abn.p, m_nor.p);
-    mr_graph *gn = nullptr, *ga = nullptr;
     // the graphs take EVERY row of the selected traces: the driver passes the whole DataFrame,
     // get_pagerank_graph(normal_list, data) (online_rca.py:180,185), which filters by traceID
     // only (preprocess_data.py:148) -- not the detector's window rows
-    int rc = mr_graph_build_dev(ctx, s, m_abn.p, &gn, nullptr);   // "normal" graph = detector's abnormal traces
-    mark("build_n");
-    if (rc == MR_OK) rc = mr_graph_build_dev(ctx, s, m_nor.p, &ga, nullptr);
-    mark("build_a");
-    if (rc == MR_OK) {   // both PageRanks in one batched launch per iteration
-        mr_graph* both[2] = {gn, ga};
-        const int anom[2] = {0, 1};
-        rc = mr_pagerank_batch(ctx, both, anom, 2, 0.85, 0.01, 25, precision, 0);
-    }
-    mark("pagerank");
-    if (rc != MR_OK) {
-        delete gn;
-        delete ga;
-        return rc;
-    }
-    if (edges_traversed) *edges_traversed = 25 * (2 * (gn->nnz_sr + ga->nnz_sr) + gn->E + ga->E);
-    // spectrum over the union (anomaly nodes, then normal-only nodes)
+    MR_TRY(mr_graph_build_dev(ctx, s, m_abn.p, &w.gn, nullptr));   // "normal" graph = detector's abnormal traces
+    if (mk) mk->mark("build_n");
+    MR_TRY(mr_graph_build_dev(ctx, s, m_nor.p, &w.ga, nullptr));
+    if (mk) mk->mark("build_a");
+    MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+    return MR_OK;
+}
+
+// spectrum over the union (anomaly nodes, then normal-only nodes) -> top codes / scores (host)
+static int win_spectrum(mr_ctx* ctx, const mr_spans* s, const WinRun& w, int method, int32_t top_max,
+                        int32_t* out_podop, double* out_score, int32_t* n_out) {
+    hipStream_t st = ctx->stream;
+    const int32_t NP = s->n_podops;
+    const mr_graph *gn = w.gn, *ga = w.ga;
     const int32_t Na = ga->N, Nn = gn->N;
     DBuf<int32_t> pos_of_code, only, uc, idx, zf;
     DBuf<int64_t> opos, tmp, ua_num, un_num;
     DBuf<uint8_t> fl;
     DBuf<double> ua_w, un_w, sc;
     const int32_t U = Na + Nn;   // upper bound
-    auto cleanup = [&](int code) {
-        delete gn;
-        delete ga;
-        return code;
-    };
-    if ((rc = pos_of_code.alloc(ctx, NP)) || (rc = only.alloc(ctx, Nn)) || (rc = uc.alloc(ctx, U)) ||
-        (rc = opos.alloc(ctx, Nn + 1)) || (rc = tmp.alloc(ctx, scan_tmp_elems(Nn))) || (rc = ua_num.alloc(ctx, U)) ||
-        (rc = un_num.alloc(ctx, U)) || (rc = fl.alloc(ctx, U)) || (rc = ua_w.alloc(ctx, U)) || (rc = un_w.alloc(ctx, U)) ||
-        (rc = zf.alloc(ctx, 1)))
-        return cleanup(rc);
+    MR_TRY(pos_of_code.alloc(ctx, NP));
+    MR_TRY(only.alloc(ctx, Nn));
+    MR_TRY(uc.alloc(ctx, U));
+    MR_TRY(opos.alloc(ctx, Nn + 1));
+    MR_TRY(tmp.alloc(ctx, scan_tmp_elems(Nn)));
+    MR_TRY(ua_num.alloc(ctx, U));
+    MR_TRY(un_num.alloc(ctx, U));
+    MR_TRY(fl.alloc(ctx, U));
+    MR_TRY(ua_w.alloc(ctx, U));
+    MR_TRY(un_w.alloc(ctx, U));
+    MR_TRY(zf.alloc(ctx, 1));
     // one launch clears the union's arrays (was seven memsets per window)
     hipLaunchKernelGGL(k_union_init, dim3(cdiv(std::max<int64_t>({(int64_t)NP, (int64_t)U, 1}), 256)), dim3(256), 0, st,
                        pos_of_code.p, NP, ua_num.p, un_num.p, fl.p, ua_w.p, un_w.p, U, zf.p);
     hipLaunchKernelGGL(k_union_a, dim3(cdiv(Na, 256)), dim3(256), 0, st, ga->node_podop.p, Na, ga->weight.p, ga->cov.p,
                        pos_of_code.p, fl.p, ua_w.p, ua_num.p, uc.p);
     hipLaunchKernelGGL(k_union_n_flags, dim3(cdiv(Nn, 256)), dim3(256), 0, st, gn->node_podop.p, Nn, pos_of_code.p, only.p);
-    if ((rc = mr_exclusive_scan_i32(ctx, only.p, opos.p, Nn, tmp.p))) return cleanup(rc);
+    MR_TRY(mr_exclusive_scan_i32(ctx, only.p, opos.p, Nn, tmp.p));
     int64_t nonly = 0;
-    if (hipMemcpyAsync(&nonly, opos.p + Nn, sizeof nonly, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipStreamSynchronize(st) != hipSuccess)
-        return cleanup(MR_ERR_HIP);
+    MR_TRY_HIP(ctx, hipMemcpyAsync(&nonly, opos.p + Nn, sizeof nonly, hipMemcpyDeviceToHost, st));
+    MR_TRY_HIP(ctx, hipStreamSynchronize(st));
     hipLaunchKernelGGL(k_union_n, dim3(cdiv(Nn, 256)), dim3(256), 0, st, gn->node_podop.p, Nn, gn->weight.p, gn->cov.p,
                        pos_of_code.p, only.p, opos.p, Na, fl.p, ua_w.p, ua_num.p, un_w.p, un_num.p, uc.p);
     const int32_t n = Na + (int32_t)nonly;
     const int32_t k = std::min(n, std::max(0, top_max + 6));   // online_rca.py:148
-    if ((rc = idx.alloc(ctx, std::max(k, 1))) || (rc = sc.alloc(ctx, std::max(k, 1)))) return cleanup(rc);
+    MR_TRY(idx.alloc(ctx, std::max(k, 1)));
+    MR_TRY(sc.alloc(ctx, std::max(k, 1)));
     // A = len(abnormal_list) = detector normal count, N = len(normal_list) = detector abnormal count
-    rc = mr_spectrum_dev(ctx, n, fl.p, ua_w.p, ua_num.p, un_w.p, un_num.p, nn, na, method, k, idx.p, sc.p, nullptr, zf.p);
-    if (rc) return cleanup(rc);
+    MR_TRY(mr_spectrum_dev(ctx, n, fl.p, ua_w.p, ua_num.p, un_w.p, un_num.p, w.nn, w.na, method, k, idx.p, sc.p, nullptr,
+                           zf.p));
     DBuf<int32_t> codes;
-    if ((rc = codes.alloc(ctx, std::max(k, 1)))) return cleanup(rc);
+    MR_TRY(codes.alloc(ctx, std::max(k, 1)));
     if (k) hipLaunchKernelGGL(k_top_codes, dim3(cdiv(k, 256)), dim3(256), 0, st, idx.p, uc.p, k, codes.p);
-    if (k && out_podop && (rc = codes.download(ctx, out_podop, k))) return cleanup(rc);
-    if (k && out_score && (rc = sc.download(ctx, out_score, k))) return cleanup(rc);
-    if (hipStreamSynchronize(st) != hipSuccess) return cleanup(MR_ERR_HIP);
-    mark("spectrum");
+    if (k && out_podop) MR_TRY(codes.download(ctx, out_podop, k));
+    if (k && out_score) MR_TRY(sc.download(ctx, out_score, k));
+    MR_TRY_HIP(ctx, hipStreamSynchronize(st));
     *n_out = k;
-    return cleanup(MR_OK);
+    return MR_OK;
+}
+
+static int64_t win_edges(const WinRun& w) {
+    return w.gn ? 25 * (2 * (w.gn->nnz_sr + w.ga->nnz_sr) + w.gn->E + w.ga->E) : 0;
+}
+
+extern "C" int mr_rca_window(mr_ctx* ctx, const mr_spans* s, int64_t t0, int64_t t1, const double* a3,
+                             const uint8_t* a3_valid, int method, int32_t top_max, int precision, int32_t* out_podop,
+                             double* out_score, int32_t* n_out, int64_t* edges_traversed, int32_t* n_abnormal,
+                             int32_t* n_normal) {
+    if (!ctx || !s || s->ctx != ctx || !a3 || !a3_valid || !n_out) return mr_fail(ctx, MR_ERR_ARG, "mr_rca_window: bad arguments");
+    MR_TRY_HIP(ctx, hipSetDevice(ctx->device));
+    *n_out = 0;
+    if (edges_traversed) *edges_traversed = 0;
+    WinMarks mk(ctx->stream);
+    mk.mark("start");
+    WinRun w;
+    MR_TRY(win_detect_build(ctx, s, t0, t1, a3, a3_valid, w, &mk));
+    if (n_abnormal) *n_abnormal = w.na;
+    if (n_normal) *n_normal = w.nn;
+    if (!w.gn) return MR_OK;
+    mr_graph* both[2] = {w.gn, w.ga};   // both PageRanks in one batched launch per iteration
+    const int anom[2] = {0, 1};
+    MR_TRY(mr_pagerank_batch(ctx, both, anom, 2, 0.85, 0.01, 25, precision, 0));
+    mk.mark("pagerank");
+    if (edges_traversed) *edges_traversed = win_edges(w);
+    MR_TRY(win_spectrum(ctx, s, w, method, top_max, out_podop, out_score, n_out));
+    mk.mark("spectrum");
+    return MR_OK;
+}
+
+// C3: many windows per call, pipelined over GROUPS of windows.  Auxiliary
+// contexts (own stream and pool each) driven by host threads run the windows' detector + graph
+// builds and, later, their spectra; this context runs the PageRanks of one group's graphs at a
+// time (all of the group's graphs share each iteration's k_tr_a + k_fx_b launches) while the
+// auxiliary streams already build the next group's graphs.
+static int win_aux(mr_ctx* ctx, int n) {
+    while ((int)ctx->aux.size() < n) {
+        mr_ctx* a = nullptr;
+        const int rc = mr_ctx_create(ctx->device, ctx->flags, &a);
+        if (rc != MR_OK) return mr_fail(ctx, rc, "mr_windows_batch: auxiliary context creation failed");
+        ctx->aux.push_back(a);
+    }
+    return MR_OK;
+}
+
+extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* const* spans, const int64_t* t0,
+                                const int64_t* t1, const double* const* a3, const uint8_t* const* a3_valid, int method,
+                                int32_t top_max, int precision, int32_t* out_podop, double* out_score, int32_t* n_out,
+                                int64_t* edges_traversed, int32_t* n_abnormal, int32_t* n_normal, int32_t* status) {
+    if (!ctx || n_windows < 0 || (n_windows && (!spans || !t0 || !t1 || !a3 || !a3_valid || !n_out || !status)))
+        return mr_fail(ctx, MR_ERR_ARG, "mr_windows_batch: bad arguments");
+    for (int32_t i = 0; i < n_windows; ++i)
+        if (!spans[i] || spans[i]->ctx != ctx || !a3[i] || !a3_valid[i])
+            return mr_fail(ctx, MR_ERR_ARG, "mr_windows_batch: bad window %d", i);
+    MR_TRY_HIP(ctx, hipSetDevice(ctx->device));
+    if (n_windows == 0) return MR_OK;
+    const int32_t K = std::max(0, top_max + 6);
+    static const int max_streams = [] {   // MR_WIN_STREAMS: auxiliary streams of a batch
+        const char* e = getenv("MR_WIN_STREAMS");
+        return e ? std::max(1, atoi(e)) : 8;
+    }();
+    static const int group_size = [] {    // MR_WIN_GROUP: windows whose PageRanks share launches
+        const char* e = getenv("MR_WIN_GROUP");
+        return e ? std::max(1, atoi(e)) : 4;
+    }();
+    const int nthr = std::min<int>(n_windows, max_streams);
+    const int gsz = std::min<int>(n_windows, group_size);
+    const int ngroups = (n_windows + gsz - 1) / gsz;
+    MR_TRY(win_aux(ctx, nthr));
+    std::vector<WinRun> w((size_t)n_windows);
+    std::vector<std::string> err((size_t)nthr);
+    // task queue: phase-1 tasks (window i -> i) first, phase-3 tasks (~i) appended per group
+    std::mutex mu;
+    std::condition_variable cv_task, cv_done;
+    std::deque<int32_t> q;
+    bool closed = false;
+    std::vector<int> built((size_t)ngroups, 0);
+    for (int32_t i = 0; i < n_windows; ++i) q.push_back(i);
+    std::vector<std::thread> th;
+    for (int k = 0; k < nthr; ++k)
+        th.emplace_back([&, k] {
+            mr_ctx* a = ctx->aux[(size_t)k];
+            (void)hipSetDevice(a->device);
+            for (;;) {
+                int32_t task;
+                {
+                    std::unique_lock<std::mutex> lk(mu);
+                    cv_task.wait(lk, [&] { return closed || !q.empty(); });
+                    if (q.empty()) return;
+                    task = q.front();
+                    q.pop_front();
+                }
+                if (task >= 0) {   // detect + both builds
+                    const int32_t i = task;
+                    WinRun& r = w[(size_t)i];
+                    r.rc = win_detect_build(a, spans[i], t0[i], t1[i], a3[i], a3_valid[i], r, nullptr);
+                    if (r.rc != MR_OK && r.rc != MR_ERR_VALUE) err[(size_t)k] = a->err;
+                    std::lock_guard<std::mutex> lk(mu);
+                    ++built[(size_t)(i / gsz)];
+                    cv_done.notify_all();
+                } else {           // spectrum
+                    const int32_t i = ~task;
+                    WinRun& r = w[(size_t)i];
+                    r.rc = win_spectrum(a, spans[i], r, method, top_max, out_podop ? out_podop + (size_t)i * K : nullptr,
+                                        out_score ? out_score + (size_t)i * K : nullptr, &n_out[i]);
+                    if (r.rc != MR_OK) err[(size_t)k] = a->err;
+                }
+            }
+        });
+    int rc = MR_OK;
+    for (int g = 0; g < ngroups && rc == MR_OK; ++g) {
+        const int32_t i0 = g * gsz, i1 = std::min<int32_t>(n_windows, i0 + gsz);
+        {
+            std::unique_lock<std::mutex> lk(mu);
+            cv_done.wait(lk, [&] { return built[(size_t)g] == i1 - i0; });
+        }
+        std::vector<mr_graph*> gs;
+        std::vector<int> anom;
+        for (int32_t i = i0; i < i1; ++i) {
+            WinRun& r = w[(size_t)i];
+            n_out[i] = 0;
+            if (r.rc == MR_OK && r.gn) {
+                r.gn->ctx = r.ga->ctx = ctx;   // (built and synced on an auxiliary context)
+                gs.push_back(r.gn);
+                gs.push_back(r.ga);
+                anom.push_back(0);
+                anom.push_back(1);
+            }
+        }
+        if (!gs.empty()) rc = mr_pagerank_batch(ctx, gs.data(), anom.data(), (int)gs.size(), 0.85, 0.01, 25, precision, 0);
+        std::lock_guard<std::mutex> lk(mu);
+        for (int32_t i = i0; i < i1; ++i)
+            if (rc == MR_OK && w[(size_t)i].rc == MR_OK && w[(size_t)i].gn) q.push_back(~i);
+        cv_task.notify_all();
+    }
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        closed = true;
+        cv_task.notify_all();
+    }
+    for (auto& t : th) t.join();
+    MR_TRY(rc);
+    for (auto& e : err)
+        if (!e.empty()) return mr_fail(ctx, MR_ERR_HIP, "mr_windows_batch: %s", e.c_str());
+    for (int32_t i = 0; i < n_windows; ++i) {
+        const WinRun& r = w[(size_t)i];
+        status[i] = r.rc;
+        if (edges_traversed) edges_traversed[i] = r.rc == MR_OK ? win_edges(r) : 0;
+        if (n_abnormal) n_abnormal[i] = r.na;
+        if (n_normal) n_normal[i] = r.nn;
+    }
+    return MR_OK;   // (the graphs go back to their contexts' pools: every stream is idle here)
 }

@@ -36,6 +36,9 @@ struct mr_ctx {
     std::multimap<size_t, void*> pool_free;
     std::map<void*, size_t> pool_live;
     size_t pool_bytes = 0;
+    // mr_windows_batch: auxiliary contexts (own stream + pool) for the windows' concurrent
+    // detector / graph-build / spectrum phases; created on first use, destroyed with this one
+    std::vector<mr_ctx*> aux;
 };
 
 void* mr_pool_alloc(mr_ctx* ctx, size_t bytes);

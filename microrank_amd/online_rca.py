@@ -159,3 +159,30 @@ def rca_window(data, start_time, end_time, slo, *, top_max=5, spectrum_method="d
     names = table.podop_names
     return {"top": [names[c] for c in codes[:m]] if names is not None else codes[:m].tolist(),
             "score": scores[:m].tolist(), "n_abnormal": na.value, "n_normal": nn.value, "edges": edges.value}
+
+
+def rank_windows(ctx, windows, *, top_max=5, spectrum_method="dstar2", precision="fp64"):
+    """C3: many RCA windows in one call (mr_windows_batch).  ``windows``: a list of
+    (DeviceSpans, t0_ns, t1_ns, a3, a3_valid) (the SLO arrays over the table's service-op
+    codes).  Returns per window (top pod-op codes, scores, n_abnormal, n_normal, edges, status);
+    status MR_ERR_VALUE marks an empty window (the reference raises TypeError there, T2)."""
+    n = len(windows)
+    k = max(top_max + 6, 1)
+    keep = [np.ascontiguousarray(w[3], np.float64) for w in windows] + \
+           [np.ascontiguousarray(w[4], np.uint8) for w in windows]
+    spans = (_lib.P * max(n, 1))(*[w[0].h for w in windows])
+    t0 = np.array([int(w[1]) for w in windows], np.int64)
+    t1 = np.array([int(w[2]) for w in windows], np.int64)
+    a3 = (C.c_void_p * max(n, 1))(*[a.ctypes.data for a in keep[:n]])
+    ok = (C.c_void_p * max(n, 1))(*[a.ctypes.data for a in keep[n:]])
+    codes = np.zeros(max(n, 1) * k, np.int32)
+    scores = np.zeros(max(n, 1) * k, np.float64)
+    n_out, edges, na, nn, status = (np.zeros(max(n, 1), t) for t in (np.int32, np.int64, np.int32, np.int32, np.int32))
+    method = SPECTRUM_METHODS.index(spectrum_method)
+    prec = _lib.MR_FP32 if precision == "fp32" else _lib.MR_FP64
+    ctx.check(_lib.load().mr_windows_batch(ctx.h, n, spans, ptr(t0, C.c_int64), ptr(t1, C.c_int64), a3, ok, method,
+                                           top_max, prec, ptr(codes, C.c_int32), ptr(scores, C.c_double),
+                                           ptr(n_out, C.c_int32), ptr(edges, C.c_int64), ptr(na, C.c_int32),
+                                           ptr(nn, C.c_int32), ptr(status, C.c_int32)), "mr_windows_batch")
+    return [(codes[i * k:i * k + n_out[i]].copy(), scores[i * k:i * k + n_out[i]].copy(), int(na[i]), int(nn[i]),
+             int(edges[i]), int(status[i])) for i in range(n)]

@@ -328,3 +328,42 @@ def test_c3_window_against_oracle(c3_window):
     assert list(c32[:5]) == list(top[:5])
     np.testing.assert_allclose(s32, score, rtol=1e-4, atol=0)
     dev.close()
+
+
+def test_windows_batch_matches_standalone(c3_window):
+    """mr_windows_batch: four C3-shaped windows (three distinct span tables, one of them twice)
+    plus an empty window in one call -- every window's top list equals its standalone
+    mr_rca_window run, scores within 1e-12 (the batch shares the PageRank launches: only the
+    fixed-point scale of a block may differ), the empty window flagged MR_ERR_VALUE."""
+    import bench
+    from microrank_amd import _lib
+    from microrank_amd.online_rca import rank_windows
+    from microrank_amd.preprocess_data import DeviceSpans
+
+    ctx = _lib.default_context()
+    wins = []
+    normal, abnormal, t0, t1 = c3_window
+    a3, ok = bench.slo_from_gpu(ctx, normal)
+    dev0 = DeviceSpans(ctx, abnormal)
+    wins.append((dev0, t0, t1, a3, ok))
+    devs = [dev0]
+    for seed in (77, 78):
+        _, nrm, ab = bench.make_window(seed, 500, 20_000)
+        s3, sok = bench.slo_from_gpu(ctx, nrm)
+        d = DeviceSpans(ctx, ab)
+        devs.append(d)
+        u0 = int(ab.tstart.min())
+        wins.append((d, u0, u0 + 5 * 60 * 10**9, s3, sok))
+    wins.append(wins[0])
+    wins.append((dev0, 0, 1, a3, ok))   # no trace in [0, 1] ns: empty window
+    got = rank_windows(ctx, wins)
+    for w, (codes, scores, na, nn, edges, status) in zip(wins[:4], got[:4]):
+        assert status == 0
+        e, c1, s1, na1, nn1 = bench.run_window(ctx, w[0], w[1], w[2], w[3], w[4], _lib.MR_FP64)
+        assert (na, nn, edges) == (na1, nn1, e)
+        assert list(codes) == list(c1)
+        np.testing.assert_allclose(scores, s1, rtol=1e-12, atol=0)
+    assert got[0][0].tolist() == got[3][0].tolist() and got[0][1].tobytes() == got[3][1].tobytes()
+    assert got[4][5] == _lib.MR_ERR_VALUE
+    for d in devs:
+        d.close()
