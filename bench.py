@@ -89,6 +89,47 @@ def run_window(ctx, dev, t0, t1, a3, ok, prec):
 ITER_KERNELS = ("k_tr_a", "k_wv_a", "k_fx_a", "k_fx_b", "k_iter_a", "k_iter_b")
 
 
+def kind_compressed_probe(ctx, dev, t0, t1, a3, ok, reps=5):
+    """§8(f) f4, reported beside (not in) GTEPS: the window's larger graph (the detector's normal
+    traces) ranked uncompressed and kind-compressed (MR_PR_KIND_COMPRESS: one representative per
+    trace kind, multiplicities carried): time per trace_pagerank call, kinds vs traces, and the
+    largest relative weight difference."""
+    import ctypes as C
+
+    from microrank_amd import _lib
+    from microrank_amd._lib import ptr
+    from microrank_amd.graph import DeviceGraph
+
+    lib = _lib.load()
+    n_tr = dev.table.n_traces
+    state = np.zeros(n_tr, np.uint8)
+    na, nn, nin = C.c_int32(), C.c_int32(), C.c_int64()
+    ctx.check(lib.mr_detect(ctx.h, dev.h, t0, t1, ptr(a3, C.c_double), ptr(ok, C.c_uint8), ptr(state, C.c_uint8),
+                            C.byref(na), C.byref(nn), C.byref(nin)), "mr_detect")
+    mask = (state == 1).astype(np.uint8)
+    h = _lib.P()
+    ctx.check(lib.mr_graph_build(ctx.h, dev.h, ptr(mask, C.c_uint8), C.byref(h)), "mr_graph_build")
+    n, t, nnz, e = C.c_int32(), C.c_int32(), C.c_int64(), C.c_int64()
+    lib.mr_graph_info(h, C.byref(n), C.byref(t), C.byref(nnz), C.byref(e))
+    g = DeviceGraph(ctx, h, None, None, n.value, t.value)
+    res = {}
+    for comp in (False, True):
+        g.pagerank(True, compress_kinds=comp)
+        ctx.sync()
+        ts = time.perf_counter()
+        for _ in range(reps):
+            g.pagerank(True, compress_kinds=comp)
+        ctx.sync()
+        res[comp] = ((time.perf_counter() - ts) / reps * 1e3, *g.fetch(kinds=True)[:3])
+    w0, w1, kind = res[False][1], res[True][1], res[True][3]
+    g.close()
+    return {"graph": f"C2 window, detector-normal traces: {t.value} traces / {n.value} ops / {nnz.value} pairs",
+            "kinds": int(round(float((1.0 / kind).sum()))), "traces": int(t.value),
+            "ms_per_call": round(res[True][0], 3), "ms_per_call_uncompressed": round(res[False][0], 3),
+            "speedup": round(res[False][0] / res[True][0], 3),
+            "max_rel_diff": float(np.max(np.abs(w1 - w0) / np.maximum(np.abs(w0), 1e-300)))}
+
+
 def pmc_traffic(args, timeout_s=240):
     """HBM bytes per power iteration (all kernels of one iteration: k_fx_a + k_fx_b, or the tile
     path's k_iter_a + k_iter_b) from two rocprofv3 --pmc child runs of this bench (FETCH_SIZE and
@@ -556,6 +597,10 @@ def main():
     }
     if args.pmc_child:
         return
+    try:
+        out["kind_compressed"] = kind_compressed_probe(ctx, dev0, t0, t1, a3, ok)
+    except Exception as e:  # a side metric never sinks the line
+        out["kind_compressed"] = {"error": f"{type(e).__name__}: {e}"}
     if not args.no_cpu:
         try:
             cb, cres = cpu_baseline(abnormal, t0, t1, a3, ok)

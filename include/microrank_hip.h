@@ -39,8 +39,12 @@ enum { MR_FP64 = 0, MR_FP32 = 1 };      /* precision of the rank vectors */
 
 /* mr_pagerank flags */
 enum {
-    MR_PR_EXACT_SUMS = 1u   /* sequential fp64 sums in reference order for the one-time scalars
+    MR_PR_EXACT_SUMS = 1u,  /* sequential fp64 sums in reference order for the one-time scalars
                                (pagerank.py:71-78, 95-96; T7) instead of a fixed-order tree */
+    MR_PR_KIND_COMPRESS = 2u /* mr_pagerank only: iterate over one
+                               representative trace per kind with its multiplicity -- traces of
+                               one kind (pagerank.py:54-66) have identical r; same weights
+                               within fp64 rounding, work proportional to the kinds */
 };
 
 typedef struct mr_ctx mr_ctx;

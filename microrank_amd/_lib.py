@@ -18,6 +18,7 @@ LIB_PATH = os.environ.get("MR_LIB_PATH") or os.path.join(os.path.dirname(os.path
 MR_OK, MR_ERR_ARG, MR_ERR_HIP, MR_ERR_VALUE, MR_ERR_ZERODIV, MR_ERR_OOM, MR_ERR_COMM, MR_ERR_STATE = range(8)
 MR_FP64, MR_FP32 = 0, 1
 MR_PR_EXACT_SUMS = 1
+MR_PR_KIND_COMPRESS = 2   # mr_pagerank: iterate over one representative per trace kind (§8(f) f4)
 
 SPECTRUM_METHODS = ("dstar2", "ochiai", "jaccard", "sorensendice", "m1", "m2", "goodman", "tarantula",
                     "russellrao", "hamann", "dice", "simplematcing", "rogers")

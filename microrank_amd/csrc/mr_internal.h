@@ -141,9 +141,17 @@ struct mr_graph {
     DBuf<int32_t> coff;              // [n_wt+1] first chunk of a tile
     std::vector<int32_t> coff_h;     // host copy (the per-wave tile split of a launch)
     DBuf<float> w_tp, c_tp;          // [T] w_t, c_t in position order
+    // kind compression (MR_PR_KIND_COMPRESS): a graph of one representative trace per kind whose
+    // q carries the kind's multiplicity (mw_tp = w_t * mult in position order); kind = mult
+    bool kinds_given = false;
+    DBuf<double> mult, mw_tp;
+    std::vector<int64_t> tile_mult_h;   // per wave tile: the multiplicity its traces stand for
+    DBuf<int32_t> krep;              // [T] class representative of each trace (when allocated)
+    int64_t kc_kinds = 0;            // kinds of the last kind-compressed ranking (0: none)
     DBuf<int32_t> wtile;             // [waves+1] first tile of each wave of the last launch plan
     int32_t wtile_nw = 0;            // waves that wtile was cut for
     int32_t wtile_tpb = 0;           // most tiles of one block under that cut
+    int64_t wtile_msum = 0;          // most traces one block stands for (x multiplicity when compressed)
     // P_sr in compressed sparse blocks for the s' pass: traces cut in tiles of 2^tshift; within a
     // tile the distinct (op, trace) entries sorted by (op, trace) as u16 tile-local trace
     // indices; a "pair" is the run of one op inside one tile.

@@ -21,6 +21,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 
 #include "mr_internal.h"
 #include "mr_prim.h"
@@ -445,12 +446,13 @@ __global__ void __launch_bounds__(KB) k_kind_insert(const int64_t* off, const in
 
 template <typename ID>   // int32 ids, or their u16 copy (rs16)
 __global__ void k_kind_verify(const int64_t* off, const ID* ops, const float* w_t, int32_t T,
-                              const KCnt* cr, const int32_t* slot_of, double* kind, int32_t* flag) {
+                              const KCnt* cr, const int32_t* slot_of, double* kind, int32_t* flag, int32_t* krep) {
     int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= T) return;
     const KCnt ks = cr[slot_of[t]];
     const int32_t r = ks.rep;
     kind[t] = (double)ks.cnt;
+    if (krep) krep[t] = r;   // (kind compression: the class representative)
     if (r == t) return;
     int64_t a0 = off[t], a1 = off[t + 1], b0 = off[r], b1 = off[r + 1];
     bool eq = (a1 - a0) == (b1 - b0);
@@ -579,12 +581,13 @@ __global__ void __launch_bounds__(KP_B) k_kind_part(const int64_t* pstart, const
 template <typename ID>
 __global__ void k_kind_final(const int32_t* rec_of, const int32_t* rpos, const uint32_t* ec, const int32_t* er,
                              const int64_t* off, const ID* ops, const float* w_t, int32_t T, double* kind,
-                             int32_t* flag) {
+                             int32_t* flag, int32_t* krep) {
     const int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= T) return;
     const int32_t pos = rpos[rec_of[t]];
     kind[t] = (double)ec[pos];
     const int32_t r = er[pos];
+    if (krep) krep[t] = r;   // (kind compression: the class representative)
     if (r == t) return;
     // exact membership: same ids and the same fp32(1/len_t) as the representative
     const int64_t a0 = off[t], a1 = off[t + 1], b0 = off[r], b1 = off[r + 1];
@@ -594,10 +597,48 @@ __global__ void k_kind_final(const int32_t* rec_of, const int32_t* rpos, const u
     if (!eq) atomicOr(flag, 1);
 }
 
+// ---------------------------------------------------------------- kind compression (§8(f) f4)
+// Traces of one kind have identical r (same op set and len_t, hence the same v_t): the iteration
+// runs over one representative per kind whose q carries the kind's multiplicity.
+__global__ void k_kc_flags(const int32_t* krep, int32_t T, int32_t* flag) {
+    const int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < T) flag[t] = krep[t] == t ? 1 : 0;
+}
+__global__ void k_kc_reps(const int32_t* flag, const int64_t* pos, int32_t T, const int64_t* off, const int32_t* len_t,
+                          const double* kind, int32_t* rep, int32_t* len_c, double* mult, int32_t* cnt) {
+    const int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= T || !flag[t]) return;
+    const int64_t k = pos[t];
+    rep[k] = t;
+    len_c[k] = len_t[t];
+    mult[k] = kind[t];
+    cnt[k] = (int32_t)(off[t + 1] - off[t]);
+}
+__global__ void k_kc_ops(const int32_t* rep, const int64_t* off_c, int32_t K, const int64_t* off, const int32_t* ops,
+                         int32_t* ops_c) {
+    const int32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= K) return;
+    const int32_t t = rep[k];
+    const int64_t a = off[t], n = off[t + 1] - a, b = off_c[k];
+    for (int64_t j = 0; j < n; ++j) ops_c[b + j] = ops[a + j];
+}
+__global__ void k_kc_mw(const int32_t* tperm, const float* w_tp, const double* mult, int32_t T, double* mw_tp) {
+    const int32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < T) mw_tp[p] = (double)w_tp[p] * mult[tperm[p]];   // exact: a 24-bit mantissa times an integer < 2^29
+}
+__global__ void k_kc_tile_mult(const int32_t* tperm, const double* mult, int32_t T, int32_t n_wt, int64_t* out) {
+    const int32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n_wt) return;
+    int64_t m = 0;
+    for (int32_t p = k * WAVE; p < min(k * WAVE + WAVE, T); ++p) m += (int64_t)mult[tperm[p]];
+    out[k] = m;
+}
+
 // ---------------------------------------------------------------- preference (pagerank.py:68-85)
 // sums over pr_trace entries: [0] sum 1/k, [1] sum 1/len; block partials then one fixed-order pass
+// mult (kind-compressed graphs): trace i stands for mult[i] traces of its kind
 __global__ void k_pref_partial(const double* kind, const int32_t* pr_trace, const int32_t* pr_len,
-                               const int32_t* len_t, int32_t n_pr, double* part, int32_t* flag) {
+                               const int32_t* len_t, int32_t n_pr, const double* mult, double* part, int32_t* flag) {
     __shared__ double red[TB / WAVE];
     double a = 0.0, b = 0.0;
     int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -607,6 +648,10 @@ __global__ void k_pref_partial(const double* kind, const int32_t* pr_trace, cons
         a = 1.0 / kind[t];
         if (ln == 0) atomicOr(flag + 1, 1);   // 1.0/len(pr_trace[t]) -> ZeroDivisionError (word 1)
         b = ln ? 1.0 / (double)ln : 0.0;
+        if (mult) {
+            a *= mult[t];
+            b *= mult[t];
+        }
     }
     a = block_sum(a, red);
     b = block_sum(b, red);
@@ -679,9 +724,9 @@ constexpr int TR_PAD = WAVE;   // k_tr_a's pad ids N .. N + 63 (su = 0)
 // T_all: traces of the whole graph (all shards) for the initial value
 // perm (relabelled fused graphs): su is kept in the kernel's op labels, su[new] = u_o[perm[new]] s
 // w_t: in position order for k_tr_a (w_tp: q is then indexed by position), else by trace
-__global__ void k_iter_init(const float* w_t, const float* u_o, int32_t N, int32_t T, int64_t T_all, double* sp0,
-                            double* su0, double* su1, double* q64, float* q32, int fp32, unsigned long long* mslot,
-                            const int32_t* perm) {
+__global__ void k_iter_init(const float* w_t, const double* mw, const float* u_o, int32_t N, int32_t T, int64_t T_all,
+                            double* sp0, double* su0, double* su1, double* q64, float* q32, int fp32,
+                            unsigned long long* mslot, const int32_t* perm) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const double v0 = 1.0 / (double)((int64_t)N + T_all);      // pagerank.py:118-119
     if (i < N) {
@@ -690,7 +735,7 @@ __global__ void k_iter_init(const float* w_t, const float* u_o, int32_t N, int32
     }
     if (i >= N && i < N + TR_PAD) su0[i] = su1[i] = 0.0;   // the fused walks' pad slots
     if (i < T) {
-        double q = (double)w_t[i] * v0;
+        double q = (mw ? mw[i] : (double)w_t[i]) * v0;   // mw: w_t times the kind's multiplicity
         if (fp32) q32[i] = (float)q; else q64[i] = q;
     }
     // M_s(0) = M_r(0) = 1: s_0, r_0 are used as they are; slots 1, 2 start cleared
@@ -712,6 +757,7 @@ struct GDev {
     const int32_t* wtile;       // [waves+1] first tile of each wave of the launch
     const float* c_tp;          // c_t, w_t in position order (tperm)
     const float* w_tp;
+    const double* mw_tp;        // kind-compressed graphs: w_t * multiplicity (position order), else null
     const float* c_t;
     const float* w_t;
     const float* u_o;
@@ -1828,8 +1874,12 @@ __global__ void __launch_bounds__(NT) k_tr_a(const GDev* __restrict__ gs, int32_
         // end chunk is loaded per lane (lane-varying address: a vector load -- a scalar load would
         // share lgkmcnt with the LDS traffic and force full drains)
         const int32_t kn = min(k + 1, ke - 1);
+        // w_t of a position: times the kind's multiplicity on a kind-compressed graph (uniform branch)
+        const GLB double* mw_tp = gp(G.mw_tp);
+        auto wq = [&](int32_t kk) { return mw_tp ? mw_tp[pos(kk)] : (double)w_tp[pos(kk)]; };
         double q_cur = (double)qc[pos(k)];
-        float c_cur = c_tp[pos(k)], w_cur = w_tp[pos(k)];
+        float c_cur = c_tp[pos(k)];
+        double w_cur = wq(k);
         double q_nx = (double)qc[pos(kn)];
         int32_t ce_nx = coff[min(kn + 1 + lane, ke)];
         // su of a chunk's ops from LDS (HOT: the hot part; the cold part comes from gather)
@@ -1873,13 +1923,13 @@ __global__ void __launch_bounds__(NT) k_tr_a(const GDev* __restrict__ gs, int32_
                 const bool own_ = p_ < T;                                                                  \
                 const double rp_ = d * (acc / Ms) + (double)c_cur;                                         \
                 if (own_) rmax = nmax(rmax, rp_);                                                          \
-                qn[own_ ? p_ : T] = (Q)((double)w_cur * rp_);   /* q[T]: pad slot */                      \
+                qn[own_ ? p_ : T] = (Q)(w_cur * rp_);   /* q[T]: pad slot */                              \
                 if (++k == ke) goto tr_done;                                                               \
                 ce = __builtin_amdgcn_readfirstlane(ce_nx);                                                \
                 q_cur = q_nx;                                                                              \
                 const int32_t kk_ = min(k + 1, ke - 1);                                                    \
                 c_cur = c_tp[pos(k)];                                                                      \
-                w_cur = w_tp[pos(k)];                                                                      \
+                w_cur = wq(k);                                                                             \
                 q_nx = (double)qc[pos(kk_)];                                                               \
                 ce_nx = coff[min(kk_ + 1 + lane, ke)];                                                     \
                 X = p_ + WAVE < T ? (unsigned long long)__double2ull_rn(q_cur * xsc) : 0ull;               \
@@ -2225,6 +2275,7 @@ static int fx_kind() {
     return v;
 }
 static bool fx_v1() { return fx_kind() == FXK_V1; }
+static bool plan_is_tr() { return fx_kind() == FXK_TR; }
 using WvA = void (*)(const GDev*, int32_t, int32_t, double, double, int, int32_t);
 static WvA wv_kernel(bool fp32, int mode, int NT) {
     static const WvA tab[2][3][2] = {
@@ -2342,11 +2393,22 @@ static int tr_split(mr_ctx* ctx, mr_graph* g, const FxPlan& P, int64_t* nfa) {
         }
         cut[(size_t)nw] = (int32_t)W;
         int32_t tpb = 0;
-        for (int64_t b = 0; b < nb; ++b) tpb = std::max(tpb, cut[(size_t)((b + 1) * NW)] - cut[(size_t)(b * NW)]);
+        int64_t msum = 0;   // traces a block stands for (kind-compressed graphs: with multiplicity)
+        for (int64_t b = 0; b < nb; ++b) {
+            const int32_t k0 = cut[(size_t)(b * NW)], k1 = cut[(size_t)((b + 1) * NW)];
+            tpb = std::max(tpb, k1 - k0);
+            int64_t m = (int64_t)(k1 - k0) * WAVE;
+            if (!g->tile_mult_h.empty()) {
+                m = 0;
+                for (int32_t k = k0; k < k1; ++k) m += g->tile_mult_h[(size_t)k];
+            }
+            msum = std::max(msum, m);
+        }
         if (tpb > 1023) {
             nb += resident;
             continue;
         }
+        g->wtile_msum = msum;
         MR_TRY(g->wtile.upload(ctx, cut.data(), cut.size()));
         MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));   // (the host vector leaves scope)
         g->wtile_nw = (int32_t)nw;
@@ -2546,6 +2608,7 @@ int mr_graph_prepare(mr_ctx* ctx, mr_graph* g) {
 
 // kinds, preference vector and iteration state of one graph (everything before the iterations)
 static int shard_kinds(mr_ctx* ctx, mr_graph* g, uint64_t cap);
+static int graph_kinds(mr_ctx* ctx, mr_graph* g, bool chk, bool ktab, uint64_t cap, uint64_t seed, uint64_t hmask);
 
 static int pagerank_setup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool fp32, uint32_t flags, int TT,
                           const FxPlan& plan, bool sharded, uint64_t seed, uint64_t hmask) {
@@ -2599,7 +2662,42 @@ static int pagerank_setup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool 
                        dim3(256), 0, st, T, (int64_t)cap, N, g->pref.p, g->c_t.p, g->ht_key.p, g->ht_cr.p,
                        g->flag.p, g->scal.p);
     MR_DEBUG_CHECK(ctx, "k_pr_reset");
-    // ---- kinds
+    // ---- kinds (a kind-compressed graph carries its class sizes: kinds_given)
+    if (!g->kinds_given) MR_TRY(graph_kinds(ctx, g, chk, ktab, cap, seed, hmask));
+    if (chk) MR_TRY(shard_kinds(ctx, g, cap));   // class sizes over all ranks (one rank: already global)
+    // ---- preference
+    const int32_t* prt = g->pr_identity ? nullptr : g->pr_trace.p;
+    const int32_t* prl = g->pr_identity ? nullptr : g->pr_len.p;
+    // also with n_pr == 0 (an empty shard): the one block writes the zero partials the sums read
+    hipLaunchKernelGGL(k_pref_partial, dim3(nbp), dim3(TB), 0, st, g->kind.p, prt, prl, g->len_t.p, n_pr,
+                       g->mult.p, g->ppart.p, g->flag.p);
+    if ((flags & MR_PR_EXACT_SUMS) && !sharded && !g->mult.p)
+        hipLaunchKernelGGL(k_pref_total_exact, dim3(1), dim3(64), 0, st, g->kind.p, prt, prl, g->len_t.p, n_pr,
+                           g->scal.p);
+    else
+        hipLaunchKernelGGL(k_pref_total, dim3(1), dim3(1024), 0, st, g->ppart.p, nbp, g->scal.p);
+    MR_DEBUG_CHECK(ctx, "k_pref");
+    if (sharded) MR_TRY(mr_coll_allreduce(ctx, g->scal.p + 2, 2, MR_DT_F64, 0));   // sum(1/k), sum(1/len)
+    const float cd = (float)(1.0 - d);
+    if (n_pr > 0)
+        hipLaunchKernelGGL(k_pref_apply, dim3(nbp), dim3(TB), 0, st, g->kind.p, prt, prl, g->len_t.p, n_pr,
+                           g->scal.p, anomaly, cd, g->pref.p, g->c_t.p);
+    MR_DEBUG_CHECK(ctx, "k_pref_apply");
+    if (tr && T) hipLaunchKernelGGL(k_tr_gather, dim3(cdiv(T, 256)), dim3(256), 0, st, g->c_t.p, g->tperm.p, T, g->c_tp.p);
+    hipLaunchKernelGGL(k_iter_init, dim3(cdiv(std::max<int64_t>({(int64_t)N + TR_PAD, T, 6 * MSH}), 256)), dim3(256), 0, st,
+                       tr ? g->w_tp.p : g->w_t.p, tr ? g->mw_tp.p : nullptr, g->u_o.p, N, T,
+                       g->T_all > 0 ? g->T_all : (int64_t)T, g->spb[0].p, g->sub[0].p,
+                       g->sub[1].p, g->q64[0].p, g->q32[0].p, (int)fp32, g->mslot.p,
+                       g->relabeled ? (const int32_t*)g->perm.p : nullptr);
+    MR_DEBUG_CHECK(ctx, "k_iter_init");
+    return MR_OK;
+}
+
+// Kinds of g (pagerank.py:54-66) into g->kind, the class representative of each trace into
+// g->krep when that is allocated; a 64-bit key collision sets flag word 0.
+static int graph_kinds(mr_ctx* ctx, mr_graph* g, bool chk, bool ktab, uint64_t cap, uint64_t seed, uint64_t hmask) {
+    hipStream_t st = ctx->stream;
+    const int32_t T = g->T;
     const int64_t* koff = g->rs_is_sr ? g->rs_off.p : g->srt_off.p;
     const int32_t* kops = g->rs_is_sr ? g->rs_ops.p : g->srt_ops.p;
     static const bool no_u16 = getenv("MR_KIND_WALK") != nullptr;   // A/B knob: per-thread int32 walk
@@ -2615,10 +2713,11 @@ static int pagerank_setup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool 
         MR_DEBUG_CHECK(ctx, "k_kind_insert");
         if (T && u16)
             hipLaunchKernelGGL(k_kind_verify<uint16_t>, dim3(cdiv(T, 256)), dim3(256), 0, st, koff,
-                               (const uint16_t*)g->rs16.p, g->w_t.p, T, g->ht_cr.p, g->slot_of.p, g->kind.p, g->flag.p);
+                               (const uint16_t*)g->rs16.p, g->w_t.p, T, g->ht_cr.p, g->slot_of.p, g->kind.p, g->flag.p,
+                               g->krep.p);
         else if (T)
             hipLaunchKernelGGL(k_kind_verify<int32_t>, dim3(cdiv(T, 256)), dim3(256), 0, st, koff, kops, g->w_t.p, T,
-                               g->ht_cr.p, g->slot_of.p, g->kind.p, g->flag.p);
+                               g->ht_cr.p, g->slot_of.p, g->kind.p, g->flag.p, g->krep.p);
         MR_DEBUG_CHECK(ctx, "k_kind_verify");
     } else if (T) {
         // partitions P = 2^pb >= T / KP_MEAN by the hash's top bits (records <= T)
@@ -2654,37 +2753,12 @@ static int pagerank_setup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool 
         hipLaunchKernelGGL(k_kind_part, dim3((uint32_t)P), dim3(KP_B), 0, st, pstart.p, eh.p, ec.p, er.p, g->flag.p);
         if (u16)
             hipLaunchKernelGGL(k_kind_final<uint16_t>, dim3(cdiv(T, 256)), dim3(256), 0, st, rec_of.p, rpos.p, ec.p, er.p,
-                               koff, (const uint16_t*)g->rs16.p, g->w_t.p, T, g->kind.p, g->flag.p);
+                               koff, (const uint16_t*)g->rs16.p, g->w_t.p, T, g->kind.p, g->flag.p, g->krep.p);
         else
             hipLaunchKernelGGL(k_kind_final<int32_t>, dim3(cdiv(T, 256)), dim3(256), 0, st, rec_of.p, rpos.p, ec.p, er.p,
-                               koff, kops, g->w_t.p, T, g->kind.p, g->flag.p);
+                               koff, kops, g->w_t.p, T, g->kind.p, g->flag.p, g->krep.p);
         MR_DEBUG_CHECK(ctx, "k_kind_part");
     }
-    if (chk) MR_TRY(shard_kinds(ctx, g, cap));   // class sizes over all ranks (one rank: already global)
-    // ---- preference
-    const int32_t* prt = g->pr_identity ? nullptr : g->pr_trace.p;
-    const int32_t* prl = g->pr_identity ? nullptr : g->pr_len.p;
-    // also with n_pr == 0 (an empty shard): the one block writes the zero partials the sums read
-    hipLaunchKernelGGL(k_pref_partial, dim3(nbp), dim3(TB), 0, st, g->kind.p, prt, prl, g->len_t.p, n_pr,
-                           g->ppart.p, g->flag.p);
-    if ((flags & MR_PR_EXACT_SUMS) && !sharded)
-        hipLaunchKernelGGL(k_pref_total_exact, dim3(1), dim3(64), 0, st, g->kind.p, prt, prl, g->len_t.p, n_pr,
-                           g->scal.p);
-    else
-        hipLaunchKernelGGL(k_pref_total, dim3(1), dim3(1024), 0, st, g->ppart.p, nbp, g->scal.p);
-    MR_DEBUG_CHECK(ctx, "k_pref");
-    if (sharded) MR_TRY(mr_coll_allreduce(ctx, g->scal.p + 2, 2, MR_DT_F64, 0));   // sum(1/k), sum(1/len)
-    const float cd = (float)(1.0 - d);
-    if (n_pr > 0)
-        hipLaunchKernelGGL(k_pref_apply, dim3(nbp), dim3(TB), 0, st, g->kind.p, prt, prl, g->len_t.p, n_pr,
-                           g->scal.p, anomaly, cd, g->pref.p, g->c_t.p);
-    MR_DEBUG_CHECK(ctx, "k_pref_apply");
-    if (tr && T) hipLaunchKernelGGL(k_tr_gather, dim3(cdiv(T, 256)), dim3(256), 0, st, g->c_t.p, g->tperm.p, T, g->c_tp.p);
-    hipLaunchKernelGGL(k_iter_init, dim3(cdiv(std::max<int64_t>({(int64_t)N + TR_PAD, T, 6 * MSH}), 256)), dim3(256), 0, st,
-                       tr ? g->w_tp.p : g->w_t.p, g->u_o.p, N, T, g->T_all > 0 ? g->T_all : (int64_t)T, g->spb[0].p, g->sub[0].p,
-                       g->sub[1].p, g->q64[0].p, g->q32[0].p, (int)fp32, g->mslot.p,
-                       g->relabeled ? (const int32_t*)g->perm.p : nullptr);
-    MR_DEBUG_CHECK(ctx, "k_iter_init");
     return MR_OK;
 }
 
@@ -2744,6 +2818,7 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         v.wtile = g->wtile.p;
         v.c_tp = g->c_tp.p;
         v.w_tp = g->w_tp.p;
+        v.mw_tp = g->mw_tp.p;
         v.c_t = g->c_t.p;
         v.w_t = g->w_t.p;
         v.u_o = g->u_o.p;
@@ -2781,7 +2856,7 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         // v1: a row entry stays below 2^63; v2: below 2^64 (traces per block < 2^(64-sc)).
         // Shards of one graph hold different trace counts and their limbs are summed, so they
         // share one scale, 2^48 (<= 65535 traces per block: wv_blocks / fx_blocks)
-        const int64_t tpb = plan.tr && g->fused ? (int64_t)g->wtile_tpb * WAVE
+        const int64_t tpb = plan.tr && g->fused ? g->wtile_msum
                                                 : cdiv(cdiv((int64_t)g->T, TT), std::max<int64_t>(nfa, 1)) * TT;
         const int sc = sharded ? 48
                                : plan.v2 ? 64 - bits_for((uint64_t)std::max<int64_t>(tpb, 1))
@@ -2941,8 +3016,124 @@ int mr_pagerank_batch_impl(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly,
     return mr_fail(ctx, MR_ERR_STATE, "trace-kind hash collision under %d seeds", ATTEMPTS);
 }
 
+// MR_PR_KIND_COMPRESS (§8(f) f4): kinds of g with each trace's class representative, then a graph
+// of the K representatives (multiplicities carried in q and in the preference sums), ranked
+// by the same fused iteration; its weights are g's.  Graphs off the fused path (or with
+// pr_trace != operation_trace) rank uncompressed.
+static int kind_compressed_pagerank(mr_ctx* ctx, mr_graph* g, int anomaly, double d, double alpha, int iters,
+                                    int precision, uint32_t flags) {
+    const uint32_t plain = flags & ~(uint32_t)MR_PR_KIND_COMPRESS;
+    if (!ctx || !g || g->ctx != ctx) return mr_fail(ctx, MR_ERR_ARG, "mr_pagerank: bad arguments");
+    const int32_t T = g->T, N = g->N;
+    if (!g->fused || !g->rs_is_sr || !g->pr_identity || T == 0 || N == 0)
+        return mr_pagerank_batch_impl(ctx, &g, &anomaly, 1, d, alpha, iters, precision, plain);
+    MR_TRY_HIP(ctx, hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    // ---- kinds with representatives (the seed sequence of mr_pagerank_batch_impl)
+    uint64_t cap = 1;
+    while (cap < 2ull * (uint64_t)T) cap <<= 1;
+    const char* kpe = getenv("MR_KIND_PART_MIN");
+    const bool ktab = (int64_t)T < (kpe ? (int64_t)atoll(kpe) : (int64_t)(1 << 21));
+    if (!ktab) cap = 0;
+    MR_TRY(g->kind.alloc(ctx, (size_t)T));
+    MR_TRY(g->krep.alloc(ctx, (size_t)T));
+    MR_TRY(g->pref.alloc(ctx, (size_t)T));
+    MR_TRY(g->c_t.alloc(ctx, (size_t)T));
+    MR_TRY(g->flag.alloc(ctx, 4));
+    MR_TRY(g->scal.alloc(ctx, 8));
+    if (ktab) {
+        MR_TRY(g->ht_key.alloc(ctx, cap));
+        MR_TRY(g->ht_cr.alloc(ctx, cap));
+        MR_TRY(g->slot_of.alloc(ctx, (size_t)T));
+    }
+    const bool force = getenv("MR_KIND_TEST_COLLIDE") != nullptr;
+    bool ok = false;
+    for (int a = 0; a < 4 && !ok; ++a) {
+        hipLaunchKernelGGL(k_pr_reset, dim3(cdiv(std::max<int64_t>({(int64_t)T, (int64_t)cap, 16}), 256)), dim3(256), 0,
+                           st, T, (int64_t)cap, N, g->pref.p, g->c_t.p, g->ht_key.p, g->ht_cr.p, g->flag.p, g->scal.p);
+        MR_TRY(graph_kinds(ctx, g, false, ktab, cap, 0x5eed5eedull + 0x9E3779B97F4A7C15ull * (uint64_t)a,
+                           (force && a == 0) ? 3ull : ~0ull));
+        int32_t hf[4];
+        MR_TRY(g->flag.download(ctx, hf, 4));
+        MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+        if (hf[2] & 1) return mr_fail(ctx, MR_ERR_STATE, "trace kinds: a partition exceeded its table");
+        ok = !(hf[0] & 1);
+    }
+    if (!ok) return mr_fail(ctx, MR_ERR_STATE, "trace-kind hash collision under 4 seeds");
+    // ---- the representatives' graph
+    DBuf<int32_t> fl, rep, cnt;
+    DBuf<int64_t> pos, tmp;
+    MR_TRY(fl.alloc(ctx, (size_t)T));
+    MR_TRY(pos.alloc(ctx, (size_t)T + 1));
+    MR_TRY(tmp.alloc(ctx, (size_t)scan_tmp_elems(T)));
+    hipLaunchKernelGGL(k_kc_flags, dim3(cdiv(T, 256)), dim3(256), 0, st, g->krep.p, T, fl.p);
+    MR_TRY(mr_exclusive_scan_i32(ctx, fl.p, pos.p, T, tmp.p));
+    int64_t K = 0;
+    MR_TRY_HIP(ctx, hipMemcpyAsync(&K, pos.p + T, sizeof K, hipMemcpyDeviceToHost, st));
+    MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+    std::unique_ptr<mr_graph> gc(new mr_graph());
+    gc->ctx = ctx;
+    gc->N = N;
+    gc->T = (int32_t)K;
+    gc->T_all = T;   // v0 = 1 / (N + T) over every trace (pagerank.py:118-119)
+    gc->E = g->E;
+    MR_TRY(rep.alloc(ctx, (size_t)K));
+    MR_TRY(cnt.alloc(ctx, (size_t)K));
+    MR_TRY(gc->len_t.alloc(ctx, (size_t)K));
+    MR_TRY(gc->mult.alloc(ctx, (size_t)K));
+    hipLaunchKernelGGL(k_kc_reps, dim3(cdiv(T, 256)), dim3(256), 0, st, fl.p, pos.p, T, g->rs_off.p, g->len_t.p,
+                       g->kind.p, rep.p, gc->len_t.p, gc->mult.p, cnt.p);
+    MR_TRY(gc->rs_off.alloc(ctx, (size_t)K + 1));
+    MR_TRY(tmp.alloc(ctx, (size_t)scan_tmp_elems(K)));
+    MR_TRY(mr_exclusive_scan_i32(ctx, cnt.p, gc->rs_off.p, K, tmp.p));
+    int64_t nnz = 0;
+    MR_TRY_HIP(ctx, hipMemcpyAsync(&nnz, gc->rs_off.p + K, sizeof nnz, hipMemcpyDeviceToHost, st));
+    MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+    MR_TRY(gc->rs_ops.alloc(ctx, (size_t)nnz));
+    hipLaunchKernelGGL(k_kc_ops, dim3(cdiv(K, 256)), dim3(256), 0, st, rep.p, gc->rs_off.p, (int32_t)K, g->rs_off.p,
+                       g->rs_ops.p, gc->rs_ops.p);
+    MR_TRY(gc->len_o.alloc(ctx, (size_t)N));
+    MR_TRY(gc->nchild.alloc(ctx, (size_t)N));
+    MR_TRY(gc->ss_off.alloc(ctx, (size_t)N + 1));
+    MR_TRY(gc->ss_par.alloc(ctx, (size_t)std::max<int64_t>(g->E, 1)));
+    MR_TRY_HIP(ctx, hipMemcpyAsync(gc->len_o.p, g->len_o.p, (size_t)N * 4, hipMemcpyDeviceToDevice, st));
+    MR_TRY_HIP(ctx, hipMemcpyAsync(gc->nchild.p, g->nchild.p, (size_t)N * 4, hipMemcpyDeviceToDevice, st));
+    MR_TRY_HIP(ctx, hipMemcpyAsync(gc->ss_off.p, g->ss_off.p, ((size_t)N + 1) * 8, hipMemcpyDeviceToDevice, st));
+    if (g->E) MR_TRY_HIP(ctx, hipMemcpyAsync(gc->ss_par.p, g->ss_par.p, (size_t)g->E * 4, hipMemcpyDeviceToDevice, st));
+    gc->rs_is_sr = true;
+    gc->pr_identity = true;
+    gc->n_pr = (int32_t)K;
+    gc->nnz_sr = gc->nnz_rs = nnz;
+    MR_TRY(mr_graph_prepare(ctx, gc.get()));
+    if (!gc->fused || !plan_is_tr())
+        return mr_pagerank_batch_impl(ctx, &g, &anomaly, 1, d, alpha, iters, precision, plain);
+    MR_TRY(gc->mw_tp.alloc(ctx, (size_t)K));
+    hipLaunchKernelGGL(k_kc_mw, dim3(cdiv(K, 256)), dim3(256), 0, st, gc->tperm.p, gc->w_tp.p, gc->mult.p, (int32_t)K,
+                       gc->mw_tp.p);
+    DBuf<int64_t> tm;
+    MR_TRY(tm.alloc(ctx, (size_t)std::max(gc->n_wt, 1)));
+    hipLaunchKernelGGL(k_kc_tile_mult, dim3(cdiv(gc->n_wt, 256)), dim3(256), 0, st, gc->tperm.p, gc->mult.p, (int32_t)K,
+                       gc->n_wt, tm.p);
+    gc->tile_mult_h.assign((size_t)gc->n_wt, 0);
+    MR_TRY(tm.download(ctx, gc->tile_mult_h.data(), (size_t)gc->n_wt));
+    MR_TRY(gc->kind.alloc(ctx, (size_t)K));   // the class sizes, as the preference reads them
+    MR_TRY_HIP(ctx, hipMemcpyAsync(gc->kind.p, gc->mult.p, (size_t)K * 8, hipMemcpyDeviceToDevice, st));
+    MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+    gc->kinds_given = true;
+    mr_graph* gcp = gc.get();
+    MR_TRY(mr_pagerank_batch_impl(ctx, &gcp, &anomaly, 1, d, alpha, iters, precision, plain));
+    MR_TRY(g->weight.alloc(ctx, (size_t)N));
+    MR_TRY(g->sn.alloc(ctx, (size_t)N));
+    MR_TRY_HIP(ctx, hipMemcpyAsync(g->weight.p, gc->weight.p, (size_t)N * 8, hipMemcpyDeviceToDevice, st));
+    MR_TRY_HIP(ctx, hipMemcpyAsync(g->sn.p, gc->sn.p, (size_t)N * 8, hipMemcpyDeviceToDevice, st));
+    MR_TRY_HIP(ctx, hipStreamSynchronize(st));   // gc's buffers return to the pool
+    g->kc_kinds = K;
+    return MR_OK;
+}
+
 extern "C" int mr_pagerank(mr_ctx* ctx, mr_graph* g, int anomaly, double d, double alpha, int iters,
                            int precision, uint32_t flags) {
+    if (flags & MR_PR_KIND_COMPRESS) return kind_compressed_pagerank(ctx, g, anomaly, d, alpha, iters, precision, flags);
     return mr_pagerank_batch_impl(ctx, &g, &anomaly, 1, d, alpha, iters, precision, flags);
 }
 

@@ -32,12 +32,14 @@ def _device_graph(operation_operation, operation_trace, trace_operation, pr_trac
 
 
 def trace_pagerank(operation_operation, operation_trace, trace_operation, pr_trace, anomaly, *,
-                   precision: str = "fp64", ctx=None):
-    """pagerank.trace_pagerank on MI355X (pagerank.py:15-112)."""
+                   precision: str = "fp64", ctx=None, compress_kinds: bool = False):
+    """pagerank.trace_pagerank on MI355X (pagerank.py:15-112).  compress_kinds: rank one
+    representative per trace kind with its multiplicity (same weights within
+    fp64 rounding)."""
     ctx = ctx or _lib.default_context()
     g, owned = _device_graph(operation_operation, operation_trace, trace_operation, pr_trace, ctx)
     try:
-        g.pagerank(bool(anomaly), D, ALPHA, ITERATIONS, precision)
+        g.pagerank(bool(anomaly), D, ALPHA, ITERATIONS, precision, compress_kinds=compress_kinds)
         w, cov = g.fetch()
     finally:
         if owned:

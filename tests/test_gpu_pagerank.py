@@ -222,3 +222,45 @@ def test_context_destroy_frees_its_handles():
     assert lib.mr_graph_free(h_graph) == 0 and lib.mr_spans_free(h_spans) == 0   # stale: no-op
     dg.close()
     sp.close()
+
+
+@pytest.mark.parametrize("name", ["c1", "pods_dup_broken", "ops200", "span_times"])
+def test_kind_compressed_matches_reference(name):
+    """§8(f) f4: the kind-compressed ranking (one representative per kind, multiplicities in q
+    and the preference sums) gives the reference fixtures' weights at 1e-10."""
+    from microrank_amd.pagerank import trace_pagerank
+
+    case = load_golden(f"{name}.json")
+    from conftest import regen_window
+
+    _, adf = regen_window(case)
+    tnames = sorted(adf["traceID"].unique())
+    for gkey, anomaly, pkey in (("graph_swapped_normal", False, "pr_normal"),
+                                ("graph_swapped_anomaly", True, "pr_anomaly")):
+        dicts = golden_graph_dicts(case[gkey], tnames)
+        _check(trace_pagerank(*dicts, anomaly, compress_kinds=True), case[pkey], RTOL64)
+
+
+@pytest.mark.parametrize("anomaly", [False, True])
+@pytest.mark.parametrize("part_min", [None, "0"])
+def test_kind_compressed_c2_matches_uncompressed(c2, anomaly, part_min, monkeypatch):
+    """C2 graph (hot kinds): compressed weights within 1e-10 of the uncompressed ranking and of
+    the oracle, coverage exact, for both kinds paths; far fewer kinds than traces."""
+    from microrank_amd import _lib
+    from microrank_amd.graph import DeviceGraph
+
+    if part_min is not None:
+        monkeypatch.setenv("MR_KIND_PART_MIN", part_min)
+    st, sg = c2
+    g = sg.as_graph()
+    ctx = _lib.default_context()
+    dg = DeviceGraph.upload(ctx, host_graph_from_oracle(g))
+    dg.pagerank(anomaly)
+    w0, cov0, k0, _ = dg.fetch(kinds=True)
+    dg.pagerank(anomaly, compress_kinds=True)
+    w1, cov1, k1, _ = dg.fetch(kinds=True)
+    np.testing.assert_array_equal(cov1, cov0)
+    np.testing.assert_array_equal(k1, k0)
+    np.testing.assert_allclose(w1, w0, rtol=1e-10, atol=0)
+    assert (1.0 / k0).sum() < 0.6 * g.T   # the C2 window repeats call paths (113k kinds of 200k traces)
+    dg.close()
