@@ -371,8 +371,9 @@ def main():
     ap.add_argument("--ops", type=int, default=1000)
     ap.add_argument("--traces", type=int, default=200_000)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--streams", type=int, default=8,
-                    help="c2: independent windows ranked concurrently per GPU, one context/stream/host thread each")
+    ap.add_argument("--streams", type=int, default=None,
+                    help="c2: windows per step (default 64: one mr_windows_batch call; --streams-mode: 8 contexts "
+                         "/ streams / host threads, one window each); c3: windows per batch call")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC passes for roofline.traffic")
     ap.add_argument("--streams-mode", action="store_true",
                     help="c2/c3: W contexts + W host threads, one mr_rca_window per window (instead of mr_windows_batch)")
@@ -389,6 +390,8 @@ def main():
     ap.add_argument("--from-spans", action="store_true",
                     help="c4: each rank holds a span shard and a step includes the K1 graph build (mr_graph_build_sharded)")
     args = ap.parse_args()
+    if args.streams is None:
+        args.streams = 8 if args.streams_mode else 64
     if args.precision is None:
         args.precision = "fp32" if args.config == "c5" else "fp64"
     if args.c4_ops is None:
@@ -453,7 +456,7 @@ def main():
         if d == 0 or args.config == "c3":
             topo, normal, abnormal = make_window(seed, args.ops, args.traces)
         t0 = int(abnormal.tstart.min())
-        for ci in range(W):
+        for ci in range(min(W, 8) if batch and args.config == "c3" else W):   # c3 batch: 8 x D distinct windows
             cx = ctxs[0] if batch else ctxs[ci]
             if batch and ci > 0 and args.config != "c3":   # c2: W copies of the one window
                 wins[0].append(wins[0][0])
@@ -493,8 +496,8 @@ def main():
             per_step = share if share is not None else W
             res, first = [], None
             for _ in range(n):
-                for c0 in range(0, per_step, 64):   # c3: calls of <= 64 windows
-                    idx = range(c0, min(per_step, c0 + 64))
+                for c0 in range(0, per_step, W):   # c3: calls of <= W windows
+                    idx = range(c0, min(per_step, c0 + W))
                     out = rank_windows(ctx, [pool[j % len(pool)][:5] for j in idx],
                                        precision="fp32" if prec == _lib.MR_FP32 else "fp64")
                     for j, (codes, scores, na_, nn_, e_, st_) in zip(idx, out):

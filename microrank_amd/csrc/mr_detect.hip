@@ -282,7 +282,7 @@ struct WinMarks {
 };
 
 static int win_detect_build(mr_ctx* ctx, const mr_spans* s, int64_t t0, int64_t t1, const double* a3,
-                            const uint8_t* a3_valid, WinRun& w, WinMarks* mk) {
+                            const uint8_t* a3_valid, WinRun& w, WinMarks* mk, int precision = -1) {
     hipStream_t st = ctx->stream;
     const int32_t NT = s->n_traces;
     DBuf<double> da3;
@@ -304,6 +304,10 @@ static int win_detect_build(mr_ctx* ctx, const mr_spans* s, int64_t t0, int64_t 
     if (mk) mk->mark("build_n");
     MR_TRY(mr_graph_build_dev(ctx, s, m_nor.p, &w.ga, nullptr));
     if (mk) mk->mark("build_a");
+    if (precision >= 0) {   // batch: kinds / preference / iteration state on this stream too
+        MR_TRY(mr_pagerank_presetup(ctx, w.gn, 0, 0.85, precision, 0));
+        MR_TRY(mr_pagerank_presetup(ctx, w.ga, 1, 0.85, precision, 0));
+    }
     MR_TRY_HIP(ctx, hipStreamSynchronize(st));
     return MR_OK;
 }
@@ -418,11 +422,11 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
     const int32_t K = std::max(0, top_max + 6);
     static const int max_streams = [] {   // MR_WIN_STREAMS: auxiliary streams of a batch
         const char* e = getenv("MR_WIN_STREAMS");
-        return e ? std::max(1, atoi(e)) : 8;
+        return e ? std::max(1, atoi(e)) : 16;
     }();
     static const int group_size = [] {    // MR_WIN_GROUP: windows whose PageRanks share launches
         const char* e = getenv("MR_WIN_GROUP");
-        return e ? std::max(1, atoi(e)) : 4;
+        return e ? std::max(1, atoi(e)) : 16;
     }();
     const int nthr = std::min<int>(n_windows, max_streams);
     const int gsz = std::min<int>(n_windows, group_size);
@@ -454,7 +458,7 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
                 if (task >= 0) {   // detect + both builds
                     const int32_t i = task;
                     WinRun& r = w[(size_t)i];
-                    r.rc = win_detect_build(a, spans[i], t0[i], t1[i], a3[i], a3_valid[i], r, nullptr);
+                    r.rc = win_detect_build(a, spans[i], t0[i], t1[i], a3[i], a3_valid[i], r, nullptr, precision);
                     if (r.rc != MR_OK && r.rc != MR_ERR_VALUE) err[(size_t)k] = a->err;
                     std::lock_guard<std::mutex> lk(mu);
                     ++built[(size_t)(i / gsz)];

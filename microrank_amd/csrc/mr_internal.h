@@ -148,6 +148,12 @@ struct mr_graph {
     std::vector<int64_t> tile_mult_h;   // per wave tile: the multiplicity its traces stand for
     DBuf<int32_t> krep;              // [T] class representative of each trace (when allocated)
     int64_t kc_kinds = 0;            // kinds of the last kind-compressed ranking (0: none)
+    // mr_pagerank_presetup: kinds / preference / iteration state already set up for the next call
+    bool pre_ok = false, pre_fp32 = false;
+    int pre_anomaly = 0;
+    double pre_d = 0.0;
+    uint32_t pre_flags = 0;
+    uint64_t pre_seed = 0, pre_hmask = 0;
     DBuf<int32_t> wtile;             // [waves+1] first tile of each wave of the last launch plan
     int32_t wtile_nw = 0;            // waves that wtile was cut for
     int32_t wtile_tpb = 0;           // most tiles of one block under that cut
@@ -269,3 +275,4 @@ struct PhaseTimer {
 inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 
 int mr_graph_prepare(mr_ctx* ctx, mr_graph* g);   // derived arrays + segments after structure upload
+int mr_pagerank_presetup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, int precision, uint32_t flags);

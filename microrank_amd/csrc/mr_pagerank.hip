@@ -2610,8 +2610,10 @@ int mr_graph_prepare(mr_ctx* ctx, mr_graph* g) {
 static int shard_kinds(mr_ctx* ctx, mr_graph* g, uint64_t cap);
 static int graph_kinds(mr_ctx* ctx, mr_graph* g, bool chk, bool ktab, uint64_t cap, uint64_t seed, uint64_t hmask);
 
-static int pagerank_setup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool fp32, uint32_t flags, int TT,
-                          const FxPlan& plan, bool sharded, uint64_t seed, uint64_t hmask) {
+// (plan-independent: a window's graphs are set up on the stream that built them, before the
+// batch's plan exists -- mr_pagerank_presetup)
+static int pagerank_setup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool fp32, uint32_t flags, bool tr_plan,
+                          bool sharded, uint64_t seed, uint64_t hmask) {
     hipStream_t st = ctx->stream;
     const int32_t N = g->N, T = g->T;
     // Kinds through a global hash table (k_kind_insert) while it stays cache-resident, and for one
@@ -2644,14 +2646,9 @@ static int pagerank_setup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool 
     MR_TRY(g->sub[0].alloc(ctx, (size_t)N + TR_PAD));   // [N, N + TR_PAD) = 0: the fused walks' pad slots
     MR_TRY(g->sub[1].alloc(ctx, (size_t)N + TR_PAD));
     MR_TRY(g->weight.alloc(ctx, (size_t)N));
-    const bool tr = g->fused && plan.tr;
+    const bool tr = g->fused && tr_plan;
     if (tr) MR_TRY(g->c_tp.alloc(ctx, (size_t)std::max(T, 1)));
-    if (g->fused) {
-        int64_t nfa = 0;
-        MR_TRY(fused_blocks(ctx, g, plan, TT, &nfa));
-        MR_TRY(g->fx_part.alloc(ctx, (size_t)std::max<int64_t>(nfa, 1) * (size_t)N));
-        MR_TRY(g->fx_ssv.alloc(ctx, (size_t)N));
-    }
+    if (g->fused) MR_TRY(g->fx_ssv.alloc(ctx, (size_t)N));
     else MR_TRY(g->part.alloc(ctx, (size_t)std::max<int64_t>(g->n_pairs, 1)));
     for (int i = 0; i < 2; ++i) {
         if (fp32) MR_TRY(g->q32[i].alloc(ctx, (size_t)T + 1));   // [T]: k_fx_a's pad slot
@@ -2794,7 +2791,18 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         if (gs[i]->fused) TT = std::min(TT, fx_tt(gs[i]->N));
     const FxPlan plan = fx_plan(gs, ng);
     if (plan.v2) TT = WAVE;   // wave tiles
-    for (int i = 0; i < ng; ++i) MR_TRY(pagerank_setup(ctx, gs[i], anomaly[i], d, fp32, flags, TT, plan, sharded, seed, hmask));
+    for (int i = 0; i < ng; ++i) {
+        mr_graph* g = gs[i];
+        const bool pre = g->pre_ok && g->pre_anomaly == anomaly[i] && g->pre_d == d && g->pre_fp32 == fp32 &&
+                         g->pre_flags == flags && g->pre_seed == seed && g->pre_hmask == hmask && !sharded;
+        g->pre_ok = false;   // the iteration state is consumed by this call
+        if (!pre) MR_TRY(pagerank_setup(ctx, g, anomaly[i], d, fp32, flags, plan.tr, sharded, seed, hmask));
+        if (g->fused) {   // the plan's blocks: partial rows and (k_tr_a) the per-wave cut
+            int64_t nfa = 0;
+            MR_TRY(fused_blocks(ctx, g, plan, TT, &nfa));
+            MR_TRY(g->fx_part.alloc(ctx, (size_t)std::max<int64_t>(nfa, 1) * (size_t)g->N));
+        }
+    }
     // ---- batched power iteration: one k_iter_a + k_iter_b pair per iteration for every graph
     int mask = 3;
     if (const char* rm = getenv("MR_ROLE_MASK")) mask = atoi(rm);   // profiling knob: 1 trace / 2 op side
@@ -2996,21 +3004,42 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
 // verification; the whole call then reruns with the next seed (independent hash functions), so
 // an input that collides under one seed is still ranked.  Seeds are a fixed sequence: every rank
 // of a sharded graph takes the same one.
-int mr_pagerank_batch_impl(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly, int ng, double d, double alpha,
-                           int iters, int precision, uint32_t flags, bool sharded = false) {
+static uint64_t kind_seed(int a) {
     static const uint64_t seed0 = [] {   // MR_KIND_SEED: test knob (start the sequence elsewhere)
         const char* e = getenv("MR_KIND_SEED");
         return e ? (uint64_t)strtoull(e, nullptr, 0) : 0x5eed5eedull;
     }();
-    // MR_KIND_TEST_COLLIDE: test knob -- the first attempt keeps 2 bits of every key, so distinct
-    // kinds collide and the verification + retry path runs
-    const bool force = getenv("MR_KIND_TEST_COLLIDE") != nullptr;   // read per call (tests set it)
+    return seed0 + 0x9E3779B97F4A7C15ull * (uint64_t)a;
+}
+// MR_KIND_TEST_COLLIDE: test knob -- the first attempt keeps 2 bits of every key, so distinct
+// kinds collide and the verification + retry path runs
+static uint64_t kind_hmask(int a) { return (a == 0 && getenv("MR_KIND_TEST_COLLIDE") != nullptr) ? 3ull : ~0ull; }
+
+// A graph's kinds, preference and iteration state for its next mr_pagerank(_batch) call with
+// these arguments, on THIS context's stream (the one that built it): mr_windows_batch sets up a
+// window's graphs while the previous group's iterations run.  The next call on the graph skips
+// its own setup when the arguments match (first kind-hash seed; a collision retries in full).
+int mr_pagerank_presetup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, int precision, uint32_t flags) {
+    const bool fp32 = precision == MR_FP32;
+    if (g->N == 0 || g->T == 0) return MR_OK;   // (the call itself raises)
+    MR_TRY(pagerank_setup(ctx, g, anomaly, d, fp32, flags, fx_kind() == FXK_TR, false, kind_seed(0), kind_hmask(0)));
+    g->pre_ok = true;
+    g->pre_anomaly = anomaly;
+    g->pre_d = d;
+    g->pre_fp32 = fp32;
+    g->pre_flags = flags;
+    g->pre_seed = kind_seed(0);
+    g->pre_hmask = kind_hmask(0);
+    return MR_OK;
+}
+
+int mr_pagerank_batch_impl(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly, int ng, double d, double alpha,
+                           int iters, int precision, uint32_t flags, bool sharded = false) {
     constexpr int ATTEMPTS = 4;
     for (int a = 0; a < ATTEMPTS; ++a) {
         bool collided = false;
-        MR_TRY(pagerank_attempt(ctx, gs, anomaly, ng, d, alpha, iters, precision, flags, sharded,
-                                seed0 + 0x9E3779B97F4A7C15ull * (uint64_t)a, (force && a == 0) ? 3ull : ~0ull,
-                                &collided));
+        MR_TRY(pagerank_attempt(ctx, gs, anomaly, ng, d, alpha, iters, precision, flags, sharded, kind_seed(a),
+                                kind_hmask(a), &collided));
         if (!collided) return MR_OK;
     }
     return mr_fail(ctx, MR_ERR_STATE, "trace-kind hash collision under %d seeds", ATTEMPTS);
@@ -3046,13 +3075,11 @@ static int kind_compressed_pagerank(mr_ctx* ctx, mr_graph* g, int anomaly, doubl
         MR_TRY(g->ht_cr.alloc(ctx, cap));
         MR_TRY(g->slot_of.alloc(ctx, (size_t)T));
     }
-    const bool force = getenv("MR_KIND_TEST_COLLIDE") != nullptr;
     bool ok = false;
     for (int a = 0; a < 4 && !ok; ++a) {
         hipLaunchKernelGGL(k_pr_reset, dim3(cdiv(std::max<int64_t>({(int64_t)T, (int64_t)cap, 16}), 256)), dim3(256), 0,
                            st, T, (int64_t)cap, N, g->pref.p, g->c_t.p, g->ht_key.p, g->ht_cr.p, g->flag.p, g->scal.p);
-        MR_TRY(graph_kinds(ctx, g, false, ktab, cap, 0x5eed5eedull + 0x9E3779B97F4A7C15ull * (uint64_t)a,
-                           (force && a == 0) ? 3ull : ~0ull));
+        MR_TRY(graph_kinds(ctx, g, false, ktab, cap, kind_seed(a), kind_hmask(a)));
         int32_t hf[4];
         MR_TRY(g->flag.download(ctx, hf, 4));
         MR_TRY_HIP(ctx, hipStreamSynchronize(st));
