@@ -86,7 +86,7 @@ def run_window(ctx, dev, t0, t1, a3, ok, prec):
     return edges.value, codes[:n_out.value].copy(), scores[:n_out.value].copy(), na.value, nn.value
 
 
-ITER_KERNELS = ("k_tr_a", "k_wv_a", "k_fx_a", "k_fx_b", "k_iter_a", "k_iter_b")
+ITER_KERNELS = ("k_tr_a", "k_wv_a", "k_fx_a", "k_fx_b", "k_iter_a", "k_iter_b", "k_cold_trace", "k_cold_ops")
 
 
 def kind_compressed_probe(ctx, dev, t0, t1, a3, ok, reps=5):
@@ -258,7 +258,10 @@ def run_c4(args, world, rank, dist):
     if world > 1:
         shard.use_rccl(ctx)
     prec = args.precision
-    fused = args.c4_ops <= 16384   # N <= FX_NMAX: fused k_fx_a/k_fx_b, else the tile path
+    # N <= FX_NMAX: k_tr_a + k_fx_b; above it the wide fused path (hot ops through k_tr_a, cold
+    # entries through k_cold_trace / k_cold_ops); MR_NO_WIDE=1 keeps the tile path for A/B runs
+    wide = args.c4_ops > 16384
+    fused = not (wide and os.environ.get("MR_NO_WIDE"))
     dev = None
     if args.from_spans:
         # K1 inside the timed step: this rank's span shard is resident in HBM (ingest), a step
@@ -341,7 +344,8 @@ def run_c4(args, world, rank, dist):
                    "parallelism": f"trace shards x{world}, RCCL " + ("limb" if fused else "fp64 op-sum")
                                   + " all-reduce per iteration"},
         "roofline": {"bound": "hbm", "kernel": "one Jacobi iteration on this rank ("
-                                               + ("k_fx_a + k_fx_b" if fused else "k_iter_a + k_iter_b")
+                                               + (("k_cold_trace + k_cold_ops + k_tr_a + k_fx_b" if wide else
+                                                   "k_tr_a + k_fx_b") if fused else "k_iter_a + k_iter_b")
                                                + (" + 2 all-reduces)" if world > 1 else ")"),
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
@@ -381,7 +385,7 @@ def main():
     ap.add_argument("--config", choices=["c2", "c3", "c4", "c5"], default="c2",
                     help="c2: RCA windows (default, weak scaling); c3: a batch of --c3-windows 500-op / 20k-trace "
                          "windows split over the ranks (strong scaling); c4 / c5: one trace-sharded graph (strong "
-                         "scaling; c5 = 100k ops / 100M traces fp32, the tile-path iteration)")
+                         "scaling; c5 = 100k ops / 100M traces fp32, the wide fused iteration)")
     ap.add_argument("--c3-windows", type=int, default=4096, help="c3: windows in the whole batch (all ranks)")
     ap.add_argument("--c3-distinct", type=int, default=4,
                     help="c3: distinct seeded windows resident per stream (the batch cycles through them)")

@@ -144,6 +144,24 @@ struct mr_graph {
     // kind compression (MR_PR_KIND_COMPRESS): a graph of one representative trace per kind whose
     // q carries the kind's multiplicity (mw_tp = w_t * mult in position order); kind = mult
     bool kinds_given = false;
+    // wide fused graphs (N > 16384, e.g. C5's 100k ops): ops relabelled by coverage, the NA
+    // most covered ("hot") ops go through k_tr_a (their u16 ids, LDS accumulator); each trace's
+    // other ("cold") entries are summed per position by k_cold_trace (cold_acc, added to r') and
+    // accumulated per op range in LDS by k_cold_ops from (position, op) pairs sorted by range
+    bool wide = false;
+    int32_t NA = 0;                  // k_tr_a's ops (= N unless wide)
+    DBuf<int64_t> hot_off;           // [T+1] hot entries per trace (u16 ids in hot16)
+    DBuf<uint16_t> hot16;
+    DBuf<int32_t> cold_off_p, cold_ops_p;   // [T+1], [n_cold]: cold op ids per position
+    DBuf<int32_t> cp_pos;            // [n_cold] cold pairs, by (range, position): position ...
+    DBuf<uint16_t> cp_op;            // ... and op - range base
+    int32_t cold_rw = 0, n_ranges = 0, n_cb = 0;
+    int64_t n_cold = 0;
+    uint64_t cold_span = 0;          // widest position span of a k_cold_ops block (its scale)
+    DBuf<int32_t> cold_rowbase;      // [n_ranges+1] first k_cold_ops block (row) of each range
+    DBuf<int64_t> cb_beg;            // [n_cb+1] pair slice of each block
+    DBuf<uint64_t> cold_part;        // [n_cb * cold_rw] partial rows of the cold ranges
+    DBuf<double> cold_acc;           // [T] per position: sum of su over the trace's cold entries
     DBuf<double> mult, mw_tp;
     std::vector<int64_t> tile_mult_h;   // per wave tile: the multiplicity its traces stand for
     DBuf<int32_t> krep;              // [T] class representative of each trace (when allocated)

@@ -182,6 +182,117 @@ __global__ void k_relabel_ids(const uint16_t* ids, int64_t n, const int32_t* inv
     if (e < n) out[e] = (uint16_t)inv[ids[e]];
 }
 
+// ---------------------------------------------------------------- wide fused graphs (N > FX_NMAX)
+// Ops relabelled by coverage; the WIDE_NA most covered ("hot") ops keep k_tr_a's LDS walk (u16
+// ids, su and accumulator in LDS); the other ("cold") entries of each trace are summed per
+// position by k_cold_trace and accumulated per op range by k_cold_ops (LDS accumulator of one
+// range, (position, op) pairs grouped by range, position order within a range).
+constexpr int32_t WIDE_NA = 10112;      // (WIDE_NA + TR_PAD) * 16 B <= k_tr_a's LDS (su + accumulator)
+constexpr int32_t WIDE_RW_MAX = 19456;  // ops per cold range: k_cold_ops' accumulator <= 152 KB
+constexpr int WIDE_CB = 256;            // k_cold_ops blocks over all ranges (one per CU: LDS-bound)
+constexpr int WIDE_CT = 1024;           // k_cold_ops block size
+constexpr int32_t WIDE_HIST = 32768;    // coverage counters in LDS (ops above: global adds)
+constexpr int WIDE_RMAX = 255;          // ranges (8-bit sort digit)
+
+__global__ void __launch_bounds__(256) k_cov_hist_w(const int32_t* ids, int64_t n, int32_t N, int32_t* cov) {
+    extern __shared__ int32_t hcnt[];
+    const int32_t NL = min(N, WIDE_HIST);
+    for (int32_t o = threadIdx.x; o < NL; o += 256) hcnt[o] = 0;
+    __syncthreads();
+    const int64_t per = (int64_t)256 * 256;
+    const int64_t b0 = (int64_t)blockIdx.x * per;
+    for (int64_t e = b0 + threadIdx.x; e < min(b0 + per, n); e += 256) {
+        const int32_t o = ids[e];
+        if (o < NL) atomicAdd(&hcnt[o], 1);
+        else atomicAdd(&cov[o], 1);
+    }
+    __syncthreads();
+    for (int32_t o = threadIdx.x; o < NL; o += 256)
+        if (hcnt[o]) atomicAdd(&cov[o], hcnt[o]);
+}
+// key = ~cov << nbo | op (descending coverage, ties by op)
+__global__ void k_relabel_keys_w(const int32_t* cov, int32_t N, int nbo, uint64_t* key) {
+    const int32_t o = blockIdx.x * blockDim.x + threadIdx.x;
+    if (o < N) key[o] = ((uint64_t)(~(uint32_t)cov[o]) << nbo) | (uint32_t)o;
+}
+__global__ void k_relabel_perm_w(const uint64_t* key, int32_t N, uint64_t omask, int32_t* perm, int32_t* inv) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    const int32_t o = (int32_t)(key[i] & omask);
+    perm[i] = o;
+    inv[o] = i;
+}
+// per trace: hot entries (at least one: a trace without hot ops walks the pad id NA) and cold ones
+__global__ void k_wide_count(const int64_t* off, const int32_t* ops, const int32_t* inv, int32_t T, int32_t NA,
+                             int32_t* nh, int32_t* nc) {
+    const int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= T) return;
+    int32_t h = 0, c = 0;
+    for (int64_t e = off[t]; e < off[t + 1]; ++e) {
+        if (inv[ops[e]] < NA) ++h;
+        else ++c;
+    }
+    nh[t] = max(h, 1);
+    nc[t] = c;
+}
+__global__ void k_wide_hot(const int64_t* off, const int32_t* ops, const int32_t* inv, int32_t T, int32_t NA,
+                           const int64_t* hoff, uint16_t* hot16) {
+    const int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= T) return;
+    int64_t k = hoff[t];
+    const int64_t k0 = k;
+    for (int64_t e = off[t]; e < off[t + 1]; ++e) {
+        const int32_t o = inv[ops[e]];
+        if (o < NA) hot16[k++] = (uint16_t)o;
+    }
+    if (k == k0) hot16[k] = (uint16_t)NA;
+}
+__global__ void k_wide_cold_cnt(const int32_t* tperm, const int32_t* nc, int32_t T, int32_t* cnt) {
+    const int32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < T) cnt[p] = nc[tperm[p]];
+}
+// cold entries in position order: op ids for k_cold_trace, and sort keys p << 24 | (op - range
+// base) << 8 | range whose one stable 8-bit pass groups them by range (positions stay ascending)
+__global__ void k_wide_cold_fill(const int32_t* tperm, const int64_t* off, const int32_t* ops, const int32_t* inv,
+                                 int32_t T, int32_t NA, int32_t RW, const int64_t* coff, int32_t* cops, uint64_t* key) {
+    const int32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= T) return;
+    const int32_t t = tperm[p];
+    int64_t k = coff[p];
+    for (int64_t e = off[t]; e < off[t + 1]; ++e) {
+        const int32_t o = inv[ops[e]];
+        if (o < NA) continue;
+        const int32_t r = (o - NA) / RW;
+        cops[k] = o;
+        key[k] = ((uint64_t)p << 24) | ((uint64_t)(o - NA - r * RW) << 8) | (uint64_t)r;
+        ++k;
+    }
+}
+// rb[r] = first pair of range r (rb[R] = n)
+__global__ void k_wide_bounds(const uint64_t* key, int64_t n, int32_t R, int64_t* rb) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int32_t r = (int32_t)(key[i] & 0xff);
+    const int32_t rp = i ? (int32_t)(key[i - 1] & 0xff) : -1;
+    for (int32_t x = rp + 1; x <= r; ++x) rb[x] = i;
+    if (i == n - 1)
+        for (int32_t x = r + 1; x <= R; ++x) rb[x] = n;
+}
+__global__ void k_wide_unpack(const uint64_t* key, int64_t n, int32_t* cp_pos, uint16_t* cp_op) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t k = key[i];
+    cp_pos[i] = (int32_t)(k >> 24);
+    cp_op[i] = (uint16_t)((k >> 8) & 0xffff);
+}
+// the widest position span of a k_cold_ops block: an op gets at most that many adds in one row
+__global__ void k_wide_span(const int64_t* cb_beg, int32_t n_cb, const int32_t* cp_pos, unsigned long long* span) {
+    const int32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= n_cb) return;
+    const int64_t b0 = cb_beg[b], b1 = cb_beg[b + 1];
+    if (b1 > b0) atomicMax(span, (unsigned long long)(cp_pos[b1 - 1] - cp_pos[b0] + 1));
+}
+
 // ---------------------------------------------------------------- trace-parallel layout (k_tr_a)
 // Traces by op count: a counting sort (lengths <= N <= FX_NMAX), order within a length free --
 // nothing numeric depends on it (a trace's ids are rotated by trace mod len, not by position;
@@ -783,6 +894,13 @@ struct GDev {
     double* op_sum;                // sharded tile path: [N] pair-partial sums per op
     unsigned long long* stamp;   // diagnostics (MR_FX_STAMP): per-block phase clocks, else null
     double fx_scale, fx_iscale;
+    // wide fused graphs: k_tr_a's ops [0, NA) (NA = N otherwise); ops [NA, N) in ranges of
+    // cold_rw ops whose rows (cold_part, blocks cold_rowbase[r] .. [r+1]) carry scale cx_scale
+    int32_t NA, cold_rw;
+    const double* cold_acc;        // [T] per position: the cold half of the trace's su sum
+    const unsigned long long* cold_part;
+    const int32_t* cold_rowbase;
+    double cx_scale, cx_iscale;
     double alpha;                  // P_ss weight (k_fx_b's call-graph term)
     int32_t T, N, n_tb, n_tiles, tshift, lds_su, blk0, n_ob, blk0b;
     int32_t blk0f, n_fa, blk0fb, n_fb;   // fused path: k_fx_a / k_fx_b block ranges
@@ -1820,7 +1938,7 @@ __global__ void __launch_bounds__(NT) k_tr_a(const GDev* __restrict__ gs, int32_
     const GDev& G = gs[fx_graph(gs, ng, split, 2)];
     const int32_t lb = (int32_t)blockIdx.x - G.blk0f;
     const int cur = it & 1, nxt = cur ^ 1, k3 = it % 3;
-    const int32_t T = G.T, N = G.N;
+    const int32_t T = G.T, N = G.NA;   // (wide graphs: the hot ops)
     const int32_t tid = (int32_t)threadIdx.x, lane = tid & (WAVE - 1), wv = tid / WAVE;
     const TrLds L_(N, SUM);
     const int32_t NH = HOT ? G.n_hot : 0;   // <= L_.n_hot (the host sizes both alike), >= 64
@@ -1830,7 +1948,7 @@ __global__ void __launch_bounds__(NT) k_tr_a(const GDev* __restrict__ gs, int32_
     GLB Q* qn = gpw((Q*)G.q[nxt]);
     const GLB float* c_tp = gp(G.c_tp);
     const GLB float* w_tp = gp(G.w_tp);
-    const GLB double* sug = gp(G.sub[cur]);   // N + TR_PAD entries, [N, N + TR_PAD) = 0
+    const GLB double* sug = gp(G.sub[cur]);   // ids >= N are pads (su 0)
     double* su_l = (double*)(lraw + L_.su);
     unsigned long long* lacc = (unsigned long long*)(lraw + L_.lacc);
     GLB unsigned long long* mslot = gpw(G.mslot);
@@ -1842,7 +1960,7 @@ __global__ void __launch_bounds__(NT) k_tr_a(const GDev* __restrict__ gs, int32_
     int32_t k = __builtin_amdgcn_readfirstlane(wt[0]);
     const int32_t ke = __builtin_amdgcn_readfirstlane(wt[1]);
     for (int32_t o = tid; o < N + TR_PAD; o += NT) {
-        if (SUL) su_l[o] = sug[o];
+        if (SUL) su_l[o] = o < N ? sug[o] : 0.0;
         lacc[o] = 0ull;
     }
     if (HOT)
@@ -1860,12 +1978,15 @@ __global__ void __launch_bounds__(NT) k_tr_a(const GDev* __restrict__ gs, int32_
     double rmax = -__builtin_huge_val();
     if (k < ke) {
         auto pos = [&](int32_t kk) { return min(kk * WAVE + lane, T - 1); };
-        // cold-op su of a chunk (hot ops load the pad slot sug[N]: one line, no traffic)
+        // cold-op su of a chunk (hot ops load sug[0]: one line, no traffic; pads read as 0)
         auto gather = [&](const u32x2 w, double* g) {
             const int32_t o[4] = {(int32_t)(w.x & 0xffffu), (int32_t)(w.x >> 16), (int32_t)(w.y & 0xffffu),
                                   (int32_t)(w.y >> 16)};
 #pragma unroll
-            for (int j = 0; j < 4; ++j) g[j] = SUL ? 0.0 : sug[HOT && o[j] < NH ? N : o[j]];
+            for (int j = 0; j < 4; ++j) {
+                const double v = SUL ? 0.0 : sug[HOT && o[j] < NH ? 0 : min(o[j], N - 1)];
+                g[j] = o[j] < N ? v : 0.0;
+            }
         };
         int32_t c = __builtin_amdgcn_readfirstlane(coff[k]);
         int32_t ce = __builtin_amdgcn_readfirstlane(coff[k + 1]);   // end of tile k
@@ -1879,6 +2000,9 @@ __global__ void __launch_bounds__(NT) k_tr_a(const GDev* __restrict__ gs, int32_
         auto wq = [&](int32_t kk) { return mw_tp ? mw_tp[pos(kk)] : (double)w_tp[pos(kk)]; };
         double q_cur = (double)qc[pos(k)];
         float c_cur = c_tp[pos(k)];
+        // wide graphs: the cold half of the trace's sum (k_cold_trace), else 0 (acc + 0 = acc)
+        const GLB double* cacc = gp(G.cold_acc);
+        double x_cur = cacc ? cacc[pos(k)] : 0.0;
         double w_cur = wq(k);
         double q_nx = (double)qc[pos(kn)];
         int32_t ce_nx = coff[min(kn + 1 + lane, ke)];
@@ -1921,7 +2045,7 @@ __global__ void __launch_bounds__(NT) k_tr_a(const GDev* __restrict__ gs, int32_
                 /* tile k done: r' of its traces (pagerank.py:125) and the next q */                      \
                 const int32_t p_ = k * WAVE + lane;                                                        \
                 const bool own_ = p_ < T;                                                                  \
-                const double rp_ = d * (acc / Ms) + (double)c_cur;                                         \
+                const double rp_ = d * ((acc + x_cur) / Ms) + (double)c_cur;                               \
                 if (own_) rmax = nmax(rmax, rp_);                                                          \
                 qn[own_ ? p_ : T] = (Q)(w_cur * rp_);   /* q[T]: pad slot */                              \
                 if (++k == ke) goto tr_done;                                                               \
@@ -1929,6 +2053,7 @@ __global__ void __launch_bounds__(NT) k_tr_a(const GDev* __restrict__ gs, int32_
                 q_cur = q_nx;                                                                              \
                 const int32_t kk_ = min(k + 1, ke - 1);                                                    \
                 c_cur = c_tp[pos(k)];                                                                      \
+                x_cur = cacc ? cacc[pos(k)] : 0.0;                                                         \
                 w_cur = wq(k);                                                                             \
                 q_nx = (double)qc[pos(kk_)];                                                               \
                 ce_nx = coff[min(kk_ + 1 + lane, ke)];                                                     \
@@ -2014,14 +2139,27 @@ __global__ void __launch_bounds__(WAVE * FB_W) k_fx_b(const GDev* __restrict__ g
         // batches of 16 rows per lane, every load in flight before the sums (indices clamped:
         // the repeats are cache hits and are not added)
         const int32_t stride = FB_W * GR;
-        const GLB unsigned long long* col = gp((const unsigned long long*)G.fx_part) + o;
-        for (int32_t r0 = w * GR + grp; r0 < nb; r0 += 16 * stride) {
+        // the op's rows: k_tr_a's (stride NA), or on a wide graph its cold range's (stride cold_rw)
+        const GLB unsigned long long* col;
+        int32_t nbl;
+        size_t rs;
+        if (o < G.NA) {
+            col = gp((const unsigned long long*)G.fx_part) + o;
+            nbl = nb;
+            rs = (size_t)G.NA;
+        } else {
+            const int32_t oc = o - G.NA, r = oc / G.cold_rw, rb0 = G.cold_rowbase[r];
+            nbl = G.cold_rowbase[r + 1] - rb0;
+            col = gp(G.cold_part) + (size_t)rb0 * G.cold_rw + (oc - r * G.cold_rw);
+            rs = (size_t)G.cold_rw;
+        }
+        for (int32_t r0 = w * GR + grp; r0 < nbl; r0 += 16 * stride) {
             unsigned long long v[16];
 #pragma unroll
-            for (int k = 0; k < 16; ++k) v[k] = col[(size_t)min(r0 + k * stride, nb - 1) * N];
+            for (int k = 0; k < 16; ++k) v[k] = col[(size_t)min(r0 + k * stride, nbl - 1) * rs];
 #pragma unroll
             for (int k = 0; k < 16; ++k)
-                if (r0 + k * stride < nb) {
+                if (r0 + k * stride < nbl) {
                     lo += v[k] & 0xffffffffull;
                     hi += v[k] >> 32;
                 }
@@ -2057,11 +2195,74 @@ __global__ void __launch_bounds__(WAVE * FB_W) k_fx_b(const GDev* __restrict__ g
     unsigned long long* Mnext = G.mslot + (size_t)2 * MSH * ((k3 + 1) % 3);
     const double ssv = lssv[lane];   // (written before the barrier above)
     // hi, lo < 2^53 (fewer than 2^21 rows over all ranks): both conversions exact, one rounding
-    const double sum = ((double)hi * 4294967296.0 + (double)lo) * G.fx_iscale;
+    const double sum = ((double)hi * 4294967296.0 + (double)lo) * (o < G.NA ? G.fx_iscale : G.cx_iscale);
     const double v = d * (sum + ssv);      // pagerank.py:122-124
     G.spb[nxt][op] = v;
     G.sub[nxt][o] = (double)uo * v;   // su in the kernel's labels
     atomicMax(&Mnext[op % MSH], d2bits(v));
+}
+
+// ---- wide fused graphs, per iteration, before k_tr_a
+// cold half of each trace's su sum (pagerank.py:125), in position order: k_tr_a adds it to the
+// lane's hot sum before the division by M_s(k)
+__global__ void k_cold_trace(const int32_t* __restrict__ coff, const int32_t* __restrict__ cops,
+                             const double* __restrict__ su, int32_t T, double* __restrict__ cacc) {
+    const int32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= T) return;
+    const int32_t a = coff[p], b = coff[p + 1];
+    double acc = 0.0;
+    int32_t j = a;
+    for (; j + 4 <= b; j += 4) {
+        const int32_t o0 = cops[j], o1 = cops[j + 1], o2 = cops[j + 2], o3 = cops[j + 3];
+        const double v0 = su[o0], v1 = su[o1], v2 = su[o2], v3 = su[o3];
+        acc += v0;
+        acc += v1;
+        acc += v2;
+        acc += v3;
+    }
+    for (; j < b; ++j) acc += su[cops[j]];
+    cacc[p] = acc;
+}
+// cold half of P_sr r (pagerank.py:122-124): a block per slice of one range's (position, op)
+// pairs, X = rint(q_k[p] / M_r(k) * 2^SCc) added into the range's LDS accumulator; the block's row
+// goes out whole (k_fx_b sums a range's rows like k_tr_a's).  SCc leaves no overflow: an op gets
+// at most one add per position of the slice (SCc = 64 - bits(widest slice span)).
+template <class Q>
+__global__ void __launch_bounds__(WIDE_CT) k_cold_ops(const int64_t* __restrict__ cb_beg, const int32_t* __restrict__ cp_pos,
+                                                     const uint16_t* __restrict__ cp_op, const void* qv,
+                                                     const unsigned long long* mslot, int it, double cx_scale,
+                                                     int32_t RW, unsigned long long* __restrict__ cold_part) {
+    extern __shared__ unsigned long long cacc_l[];
+    __shared__ double mr;
+    const Q* __restrict__ q = (const Q*)qv;
+    const int k3 = it % 3;
+    for (int32_t i = threadIdx.x; i < RW; i += WIDE_CT) cacc_l[i] = 0ull;
+    if (threadIdx.x < WAVE) {
+        const double m = wave_max(bits2d(mslot[(size_t)2 * MSH * k3 + MSH + threadIdx.x]));
+        if (threadIdx.x == 0) mr = m;
+    }
+    __syncthreads();
+    const double xsc = cx_scale / mr;
+    const int64_t b = cb_beg[blockIdx.x], e = cb_beg[blockIdx.x + 1];
+    int64_t i = b + threadIdx.x;
+    for (; i + 3 * WIDE_CT < e; i += 4 * WIDE_CT) {   // four pairs in flight per thread
+        int32_t p[4];
+        uint16_t o[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            p[j] = cp_pos[i + j * WIDE_CT];
+            o[j] = cp_op[i + j * WIDE_CT];
+        }
+        double v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = (double)q[p[j]];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) atomicAdd(&cacc_l[o[j]], (unsigned long long)__double2ull_rn(v[j] * xsc));
+    }
+    for (; i < e; i += WIDE_CT) atomicAdd(&cacc_l[cp_op[i]], (unsigned long long)__double2ull_rn((double)q[cp_pos[i]] * xsc));
+    __syncthreads();
+    unsigned long long* row = cold_part + (size_t)blockIdx.x * RW;
+    for (int32_t o = threadIdx.x; o < RW; o += WIDE_CT) row[o] = cacc_l[o];
 }
 
 // result = s/max(s) (pagerank.py:126,129); weight = result * sum(result) / N (:93-107)
@@ -2307,6 +2508,9 @@ static int num_cus() {
     return ncu;
 }
 
+// ops of the fused kernel's walk: a wide graph's hot ops, else all
+static int32_t kern_n(const mr_graph* g) { return g->wide ? g->NA : g->N; }
+
 // Launch plan of the fused iteration for a batch of graphs (one kernel variant per launch).
 struct FxPlan {
     bool v2 = true;     // wave tiles (k_tr_a / k_wv_a), else k_fx_a
@@ -2324,7 +2528,7 @@ static FxPlan fx_plan(mr_graph* const* gs, int ng) {
     int64_t tmax = 0;
     for (int i = 0; i < ng; ++i)
         if (gs[i]->fused) {
-            nmax = std::max(nmax, gs[i]->N);
+            nmax = std::max(nmax, kern_n(gs[i]));
             tmax = std::max<int64_t>(tmax, gs[i]->T);
         }
     static const int force_nt = [] {
@@ -2377,7 +2581,7 @@ static int64_t wv_blocks(int32_t T, int32_t N, const FxPlan& P) {
 // graph for the wave count; at most 1023 tiles (65472 traces) per block.
 static int tr_split(mr_ctx* ctx, mr_graph* g, const FxPlan& P, int64_t* nfa) {
     const int64_t W = g->n_wt, NW = P.NT / WAVE;
-    const int64_t resident = plan_resident(g->N, P);
+    const int64_t resident = plan_resident(kern_n(g), P);
     int64_t nb = std::max<int64_t>(std::min<int64_t>(resident, cdiv(W, NW)), 1);
     const std::vector<int32_t>& co = g->coff_h;
     for (;;) {
@@ -2428,9 +2632,11 @@ static int fused_blocks(mr_ctx* ctx, mr_graph* g, const FxPlan& P, int TT_v1, in
 // k_tr_a's layout of a fused graph (after w_t and the kernel's ids rs16 / rsp): traces sorted by
 // op count, tiles of 64 positions, ids lane-interleaved in chunks of 4.  One host round trip (the
 // chunk count sizes the id array; the chunk offsets stay on the host for the per-wave cut).
-static int tr_layout(mr_ctx* ctx, mr_graph* g) {
+// off / ids: the trace-major incidence the kernel walks (rs_off with rs16 / rsp, or a wide graph's
+// hot entries), N: the kernel's op count (pads N + lane)
+static int tr_layout(mr_ctx* ctx, mr_graph* g, const int64_t* off, const uint16_t* src, int32_t N) {
     hipStream_t st = ctx->stream;
-    const int32_t T = g->T, N = g->N;
+    const int32_t T = g->T;
     const int32_t W = cdiv(T, WAVE);
     g->n_wt = W;
     g->wtile_nw = 0;
@@ -2447,14 +2653,14 @@ static int tr_layout(mr_ctx* ctx, mr_graph* g) {
     MR_TRY(g->coff.alloc(ctx, (size_t)W + 1));
     if (T) {
         const int nb = cdiv(T, (int64_t)TRB * TR_PER);
-        hipLaunchKernelGGL(k_tr_hist, dim3(nb), dim3(TRB), (size_t)nbin * sizeof(int32_t), st, g->rs_off.p, T, nbin,
+        hipLaunchKernelGGL(k_tr_hist, dim3(nb), dim3(TRB), (size_t)nbin * sizeof(int32_t), st, off, T, nbin,
                            hist.p);
         MR_TRY(mr_exclusive_scan_i32(ctx, hist.p, boff.p, nbin, tmp.p));
         MR_TRY(cursor.alloc(ctx, (size_t)nbin));
         MR_TRY_HIP(ctx, hipMemcpyAsync(cursor.p, boff.p, (size_t)nbin * sizeof(int64_t), hipMemcpyDeviceToDevice, st));
-        hipLaunchKernelGGL(k_tr_place, dim3(nb), dim3(TRB), 2 * (size_t)nbin * sizeof(int32_t), st, g->rs_off.p, T,
+        hipLaunchKernelGGL(k_tr_place, dim3(nb), dim3(TRB), 2 * (size_t)nbin * sizeof(int32_t), st, off, T,
                            nbin, cursor.p, g->w_t.p, g->tperm.p, g->w_tp.p);
-        hipLaunchKernelGGL(k_tr_chunks, dim3(cdiv(W, 256)), dim3(256), 0, st, g->tperm.p, g->rs_off.p, T, W, c64.p);
+        hipLaunchKernelGGL(k_tr_chunks, dim3(cdiv(W, 256)), dim3(256), 0, st, g->tperm.p, off, T, W, c64.p);
     }
     MR_TRY(mr_exclusive_scan(ctx, c64.p, c64.p, W, tmp.p));
     hipLaunchKernelGGL(k_tr_coff, dim3(cdiv((int64_t)W + 1, 256)), dim3(256), 0, st, c64.p, W, g->coff.p);
@@ -2463,12 +2669,124 @@ static int tr_layout(mr_ctx* ctx, mr_graph* g) {
     MR_TRY_HIP(ctx, hipStreamSynchronize(st));
     const int64_t nch = g->coff_h[(size_t)W];
     MR_TRY(g->tids.alloc(ctx, (size_t)std::max<int64_t>(nch, 1) * WAVE * 4));
-    const uint16_t* src = g->relabeled ? g->rsp.p : g->rs16.p;
     if (W)
-        hipLaunchKernelGGL(k_tr_fill, dim3(cdiv((int64_t)W * WAVE, 256)), dim3(256), 0, st, g->tperm.p, g->rs_off.p, src,
+        hipLaunchKernelGGL(k_tr_fill, dim3(cdiv((int64_t)W * WAVE, 256)), dim3(256), 0, st, g->tperm.p, off, src,
                            c64.p, T, N, W, g->tids.p);
     MR_TRY_HIP(ctx, hipGetLastError());
     return MR_OK;   // (scratch returns to the stream-ordered pool)
+}
+
+// A wide fused graph (N > FX_NMAX): ops relabelled by coverage, hot entries (labels < NA) laid
+// out for k_tr_a, cold entries per position for k_cold_trace and grouped by op range for
+// k_cold_ops with the blocks of each range (about WIDE_CB over all ranges, by pair count).
+static int wide_prepare(mr_ctx* ctx, mr_graph* g) {
+    hipStream_t st = ctx->stream;
+    const int32_t N = g->N, T = g->T, NA = WIDE_NA;
+    const int64_t nnz = g->nnz_sr;
+    g->wide = true;
+    g->NA = NA;
+    g->rsp.reset();
+    // ---- coverage, then labels by descending coverage (perm[new] = old)
+    MR_TRY_HIP(ctx, hipMemsetAsync(g->cov.p, 0, (size_t)N * sizeof(int32_t), st));
+    if (nnz)
+        hipLaunchKernelGGL(k_cov_hist_w, dim3(cdiv(nnz, (int64_t)256 * 256)), dim3(256),
+                           (size_t)std::min(N, WIDE_HIST) * sizeof(int32_t), st, g->rs_ops.p, nnz, N, g->cov.p);
+    const int nbo = bits_for((uint64_t)(N - 1));
+    DBuf<uint64_t> key;
+    DBuf<int32_t> inv;
+    MR_TRY(key.alloc(ctx, (size_t)N));
+    MR_TRY(inv.alloc(ctx, (size_t)N));
+    MR_TRY(g->perm.alloc(ctx, (size_t)N));
+    hipLaunchKernelGGL(k_relabel_keys_w, dim3(cdiv(N, 256)), dim3(256), 0, st, g->cov.p, N, nbo, key.p);
+    {
+        SortScratch ws;
+        MR_TRY(mr_radix_sort(ctx, key.p, nullptr, N, nbo + 32, ws));
+    }
+    hipLaunchKernelGGL(k_relabel_perm_w, dim3(cdiv(N, 256)), dim3(256), 0, st, key.p, N, (1ull << nbo) - 1ull, g->perm.p,
+                       inv.p);
+    g->relabeled = true;
+    // ---- hot entries per trace (u16, node order; a trace without any walks the pad id NA)
+    DBuf<int32_t> nh, nc;
+    DBuf<int64_t> tmp;
+    MR_TRY(nh.alloc(ctx, (size_t)T));
+    MR_TRY(nc.alloc(ctx, (size_t)T));
+    MR_TRY(g->hot_off.alloc(ctx, (size_t)T + 1));
+    MR_TRY(tmp.alloc(ctx, (size_t)scan_tmp_elems(std::max<int64_t>(T, 1))));
+    hipLaunchKernelGGL(k_wide_count, dim3(cdiv(T, 256)), dim3(256), 0, st, g->rs_off.p, g->rs_ops.p, inv.p, T, NA, nh.p,
+                       nc.p);
+    MR_TRY(mr_exclusive_scan_i32(ctx, nh.p, g->hot_off.p, T, tmp.p));
+    int64_t n_hot = 0;
+    MR_TRY_HIP(ctx, hipMemcpyAsync(&n_hot, g->hot_off.p + T, sizeof n_hot, hipMemcpyDeviceToHost, st));
+    MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+    MR_TRY(g->hot16.alloc(ctx, (size_t)n_hot + 8));
+    hipLaunchKernelGGL(k_wide_hot, dim3(cdiv(T, 256)), dim3(256), 0, st, g->rs_off.p, g->rs_ops.p, inv.p, T, NA,
+                       g->hot_off.p, g->hot16.p);
+    MR_TRY(tr_layout(ctx, g, g->hot_off.p, g->hot16.p, NA));   // tperm, w_tp, tids, coff (host copy)
+    // ---- cold entries in position order
+    DBuf<int32_t> cnt;
+    DBuf<int64_t> coff64;
+    MR_TRY(cnt.alloc(ctx, (size_t)T));
+    MR_TRY(coff64.alloc(ctx, (size_t)T + 1));
+    hipLaunchKernelGGL(k_wide_cold_cnt, dim3(cdiv(T, 256)), dim3(256), 0, st, g->tperm.p, nc.p, T, cnt.p);
+    MR_TRY(mr_exclusive_scan_i32(ctx, cnt.p, coff64.p, T, tmp.p));
+    int64_t n_cold = 0;
+    MR_TRY_HIP(ctx, hipMemcpyAsync(&n_cold, coff64.p + T, sizeof n_cold, hipMemcpyDeviceToHost, st));
+    MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+    g->n_cold = n_cold;
+    MR_TRY(g->cold_off_p.alloc(ctx, (size_t)T + 1));
+    hipLaunchKernelGGL(k_tr_coff, dim3(cdiv((int64_t)T + 1, 256)), dim3(256), 0, st, coff64.p, T, g->cold_off_p.p);
+    const int32_t R = (int32_t)cdiv((int64_t)N - NA, WIDE_RW_MAX);
+    const int32_t RW = (int32_t)(cdiv(cdiv((int64_t)N - NA, R), WAVE) * WAVE);
+    g->n_ranges = R;
+    g->cold_rw = RW;
+    MR_TRY(g->cold_ops_p.alloc(ctx, (size_t)n_cold + 1));
+    MR_TRY(g->cp_pos.alloc(ctx, (size_t)n_cold + 1));
+    MR_TRY(g->cp_op.alloc(ctx, (size_t)n_cold + 1));
+    DBuf<int64_t> rb;
+    MR_TRY(rb.zero(ctx, (size_t)R + 1));
+    {
+        DBuf<uint64_t> ck;
+        MR_TRY(ck.alloc(ctx, (size_t)n_cold + 1));
+        hipLaunchKernelGGL(k_wide_cold_fill, dim3(cdiv(T, 256)), dim3(256), 0, st, g->tperm.p, g->rs_off.p, g->rs_ops.p,
+                           inv.p, T, NA, RW, coff64.p, g->cold_ops_p.p, ck.p);
+        SortScratch ws;
+        MR_TRY(mr_radix_sort(ctx, ck.p, nullptr, n_cold, 8, ws));   // stable: positions stay ascending
+        if (n_cold) {
+            hipLaunchKernelGGL(k_wide_bounds, dim3(cdiv(n_cold, 256)), dim3(256), 0, st, ck.p, n_cold, R, rb.p);
+            hipLaunchKernelGGL(k_wide_unpack, dim3(cdiv(n_cold, 256)), dim3(256), 0, st, ck.p, n_cold, g->cp_pos.p,
+                               g->cp_op.p);
+        }
+    }
+    std::vector<int64_t> rbh((size_t)R + 1);
+    MR_TRY(rb.download(ctx, rbh.data(), rbh.size()));
+    MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+    // ---- k_cold_ops blocks: each range's pairs in equal slices, blocks proportional to its pairs
+    std::vector<int32_t> rowbase((size_t)R + 1);
+    std::vector<int64_t> beg;
+    for (int32_t r = 0; r < R; ++r) {
+        const int64_t pr = rbh[(size_t)r + 1] - rbh[(size_t)r];
+        const int64_t nbr = std::max<int64_t>(1, (int64_t)std::llround((double)WIDE_CB * (double)pr / (double)std::max<int64_t>(n_cold, 1)));
+        rowbase[(size_t)r] = (int32_t)beg.size();
+        for (int64_t j = 0; j < nbr; ++j) beg.push_back(rbh[(size_t)r] + pr * j / nbr);
+    }
+    rowbase[(size_t)R] = (int32_t)beg.size();
+    beg.push_back(rbh[(size_t)R]);
+    g->n_cb = (int32_t)beg.size() - 1;
+    MR_TRY(g->cb_beg.upload(ctx, beg.data(), beg.size()));
+    MR_TRY(g->cold_rowbase.upload(ctx, rowbase.data(), rowbase.size()));
+    MR_TRY(g->cold_part.alloc(ctx, (size_t)g->n_cb * (size_t)RW));
+    MR_TRY(g->cold_acc.alloc(ctx, (size_t)T));
+    DBuf<unsigned long long> span;
+    MR_TRY(span.zero(ctx, 1));
+    hipLaunchKernelGGL(k_wide_span, dim3(cdiv(g->n_cb, 256)), dim3(256), 0, st, g->cb_beg.p, g->n_cb, g->cp_pos.p, span.p);
+    unsigned long long sp = 0;
+    MR_TRY(span.download(ctx, &sp, 1));
+    MR_TRY_HIP(ctx, hipStreamSynchronize(st));   // (also: the host vectors leave scope)
+    g->cold_span = std::max<uint64_t>(sp, 1);
+    g->n_tiles = 0;
+    g->n_pairs = 0;
+    MR_TRY_HIP(ctx, hipGetLastError());
+    return MR_OK;
 }
 
 // Derived per-graph arrays: fp32 reciprocals, u16 ids, and the P_sr tiles.  One host round trip
@@ -2489,8 +2807,16 @@ int mr_graph_prepare(mr_ctx* ctx, mr_graph* g) {
         hipLaunchKernelGGL(k_ids16, dim3(cdiv(g->nnz_rs, 256)), dim3(256), 0, st, g->rs_ops.p, g->nnz_rs, g->rs16.p);
     }
     g->relabeled = false;   // (set below for fused graphs that need it)
+    g->wide = false;
+    g->NA = N;
     static const bool no_fused = getenv("MR_NO_FUSED") != nullptr;   // A/B knob: force the tile path
-    g->fused = !no_fused && !g->force_tile && g->rs_is_sr && g->traces_nonempty && N <= FX_NMAX && fx_tt(N) > 0;
+    static const bool no_wide = getenv("MR_NO_WIDE") != nullptr;     // A/B knob: N > FX_NMAX on the tile path
+    const bool fusable = !no_fused && !g->force_tile && g->rs_is_sr && g->traces_nonempty;
+    if (fusable && !no_wide && N > FX_NMAX && plan_is_tr() && (int64_t)N <= (int64_t)WIDE_NA + (int64_t)WIDE_RMAX * WIDE_RW_MAX) {
+        g->fused = true;
+        return wide_prepare(ctx, g);
+    }
+    g->fused = fusable && N <= FX_NMAX && fx_tt(N) > 0;
     if (g->fused) {   // no P_sr tiles: the fused iteration reads the trace-major ids only
         MR_TRY_HIP(ctx, hipMemsetAsync(g->cov.p, 0, (size_t)std::max(N, 1) * sizeof(int32_t), st));
         if (nnz && N)
@@ -2517,7 +2843,7 @@ int mr_graph_prepare(mr_ctx* ctx, mr_graph* g) {
             g->perm.reset();
             g->rsp.reset();
         }
-        MR_TRY(tr_layout(ctx, g));
+        MR_TRY(tr_layout(ctx, g, g->rs_off.p, g->relabeled ? g->rsp.p : g->rs16.p, N));
         g->n_tiles = 0;
         g->n_pairs = 0;
         MR_TRY_HIP(ctx, hipGetLastError());
@@ -2800,8 +3126,19 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         if (g->fused) {   // the plan's blocks: partial rows and (k_tr_a) the per-wave cut
             int64_t nfa = 0;
             MR_TRY(fused_blocks(ctx, g, plan, TT, &nfa));
-            MR_TRY(g->fx_part.alloc(ctx, (size_t)std::max<int64_t>(nfa, 1) * (size_t)g->N));
+            MR_TRY(g->fx_part.alloc(ctx, (size_t)std::max<int64_t>(nfa, 1) * (size_t)kern_n(g)));
         }
+    }
+    // a sharded wide graph: the widest cold slice span over the ranks (one scale for every rank)
+    uint64_t cold_span_all = 1;
+    for (int i = 0; i < ng; ++i)
+        if (gs[i]->wide) cold_span_all = std::max(cold_span_all, gs[i]->cold_span);
+    if (sharded && mr_coll_ready(ctx)) {
+        DBuf<uint64_t> csp;
+        MR_TRY(csp.upload(ctx, &cold_span_all, 1));
+        MR_TRY(mr_coll_allreduce(ctx, csp.p, 1, MR_DT_U64, 1));
+        MR_TRY(csp.download(ctx, &cold_span_all, 1));
+        MR_TRY_HIP(ctx, hipStreamSynchronize(st));
     }
     // ---- batched power iteration: one k_iter_a + k_iter_b pair per iteration for every graph
     int mask = 3;
@@ -2820,7 +3157,7 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         v.rs16 = g->rs16.p;
         v.rsw = g->relabeled ? g->rsp.p : g->rs16.p;
         v.perm = g->relabeled ? g->perm.p : nullptr;
-        v.n_hot = plan_n_hot(g->N, plan);
+        v.n_hot = plan_n_hot(kern_n(g), plan);
         v.tids = g->tids.p;
         v.coff = g->coff.p;
         v.wtile = g->wtile.p;
@@ -2874,6 +3211,27 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         v.fx_iscale = std::ldexp(1.0, -sc);
         v.T = g->T;
         v.N = g->N;
+        v.NA = kern_n(g);
+        v.cold_rw = g->cold_rw;
+        v.cold_acc = g->wide ? g->cold_acc.p : nullptr;
+        v.cold_part = (const unsigned long long*)g->cold_part.p;
+        v.cold_rowbase = g->cold_rowbase.p;
+        v.cx_scale = v.fx_scale;
+        v.cx_iscale = v.fx_iscale;
+        if (g->wide) {
+            // cold rows: at most cold_span adds per op and row; a sharded graph's ranks sum their
+            // limbs per op, and an op hot on one rank may be cold on another: one scale for both
+            // (the smaller), agreed over the ranks (cold_span_all)
+            const int scc = 64 - bits_for(sharded ? cold_span_all : g->cold_span);
+            if (sharded) {
+                const int s1 = std::min(sc, scc);
+                v.fx_scale = v.cx_scale = std::ldexp(1.0, s1);
+                v.fx_iscale = v.cx_iscale = std::ldexp(1.0, -s1);
+            } else {
+                v.cx_scale = std::ldexp(1.0, scc);
+                v.cx_iscale = std::ldexp(1.0, -scc);
+            }
+        }
         v.blk0f = blocks_fa;
         v.n_fa = (int32_t)nfa;
         blocks_fa += v.n_fa;
@@ -2912,7 +3270,7 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
     const FxA fx_a = fx_kernel(fp32, sul, multi, fx_S);
     for (int i = 0; i < ng; ++i)
         if (gs[i]->fused)
-            lds_f = std::max(lds_f, plan.v2 ? plan_lds(gs[i]->N, plan) : FxLds(gs[i]->N, TT, fx_S * TT, sul).total);
+            lds_f = std::max(lds_f, plan.v2 ? plan_lds(kern_n(gs[i]), plan) : FxLds(gs[i]->N, TT, fx_S * TT, sul).total);
     const WvA sg_a = plan.tr ? tr_kernel(fp32, plan.mode, plan.NT) : plan.v2 ? wv_kernel(fp32, plan.mode, plan.NT) : nullptr;
     const int fx_bs = plan.v2 ? plan.NT : fx_S * TT;
     // a sharded graph with no collective backend is one whole shard: the split launches around the
@@ -2920,6 +3278,24 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
     const bool coll = sharded && mr_coll_ready(ctx);
     for (int it = 0; it < iters; ++it) {
         mr_prof_begin(ctx);
+        for (int i = 0; i < ng; ++i) {   // wide graphs: the cold halves, before k_tr_a / k_fx_b
+            mr_graph* g = gs[i];
+            if (!g->wide) continue;
+            if (g->T)
+                hipLaunchKernelGGL(k_cold_trace, dim3(cdiv(g->T, 256)), dim3(256), 0, st, g->cold_off_p.p, g->cold_ops_p.p,
+                                   g->sub[it & 1].p, g->T, g->cold_acc.p);
+            const void* qc = fp32 ? (const void*)g->q32[it & 1].p : (const void*)g->q64[it & 1].p;
+            const size_t lds_c = (size_t)g->cold_rw * sizeof(unsigned long long);
+            if (fp32)
+                hipLaunchKernelGGL(k_cold_ops<float>, dim3(g->n_cb), dim3(WIDE_CT), lds_c, st, g->cb_beg.p, g->cp_pos.p,
+                                   g->cp_op.p, qc, g->mslot.p, it, hv[(size_t)i].cx_scale, g->cold_rw,
+                                   (unsigned long long*)g->cold_part.p);
+            else
+                hipLaunchKernelGGL(k_cold_ops<double>, dim3(g->n_cb), dim3(WIDE_CT), lds_c, st, g->cb_beg.p, g->cp_pos.p,
+                                   g->cp_op.p, qc, g->mslot.p, it, hv[(size_t)i].cx_scale, g->cold_rw,
+                                   (unsigned long long*)g->cold_part.p);
+            MR_DEBUG_CHECK(ctx, "k_cold");
+        }
         if (blocks_fa) {
             if (sg_a) hipLaunchKernelGGL(sg_a, dim3(blocks_fa), dim3(fx_bs), lds_f, st, dv.p, ng, split_fa, d, alpha, it, TT);
             else hipLaunchKernelGGL(fx_a, dim3(blocks_fa), dim3(fx_bs), lds_f, st, dv.p, ng, split_fa, d, alpha, it, TT);

@@ -178,6 +178,49 @@ def test_large_op_count_multi_tile_long_tiles(anomaly):
     dg.close()
 
 
+def _with_cold_traces(hg, n, lo, seed):
+    """Append n traces of 1..3 distinct ops drawn from [lo, N): traces whose ops are all outside
+    the wide path's hot set (a pad id in the LDS walk, every entry on the cold side)."""
+    from microrank_amd.graph import HostGraph
+
+    rng = np.random.default_rng(seed)
+    width = rng.integers(1, 4, n)
+    ops = [np.sort(rng.choice(np.arange(lo, hg.N), w, replace=False)) for w in width]
+    flat = np.concatenate(ops).astype(np.int32)
+    sr_ops = np.concatenate([hg.sr_ops, flat])
+    sr_off = np.concatenate([hg.sr_off, hg.sr_off[-1] + np.cumsum(width).astype(np.int64)])
+    len_t = np.concatenate([hg.len_t, width.astype(np.int32)])
+    len_o = hg.len_o + np.bincount(flat, minlength=hg.N).astype(np.int32)
+    return HostGraph(range(hg.N), range(hg.T + n), sr_off, sr_ops, None, None, len_t, len_o, hg.ss_off, hg.ss_par,
+                     hg.nchild, None, None)
+
+
+@pytest.mark.parametrize("precision", ["fp64", "fp32"])
+def test_wide_fused_path_against_oracle(precision):
+    """N = 50000 > 16384 (config C5's regime): the wide fused path -- hot ops through the LDS walk,
+    cold entries through k_cold_trace / k_cold_ops over 3 op ranges -- plus 3k traces with no hot op
+    at all.  GPU vs oracle (fp64 1e-10, fp32 1e-4), coverage exact, bitwise reruns."""
+    from microrank_amd import _lib, synth
+    from microrank_amd.graph import DeviceGraph
+
+    hg = _with_cold_traces(synth.big_graph(50_000, 40_000, seed=9), 3000, 30_000, seed=10)
+    g = _oracle_graph_from_host(hg)
+    kind = orc.trace_kinds(g)
+    s = orc.power_iteration(g, orc.preference(g, kind, True))
+    w_ref, cov_ref = orc.weights(g, s)
+    ctx = _lib.default_context()
+    dg = DeviceGraph.upload(ctx, hg)
+    dg.pagerank(True, precision=precision)
+    w, cov = dg.fetch()
+    tol = RTOL64 if precision == "fp64" else 1e-4
+    np.testing.assert_array_equal(cov, np.array(list(cov_ref.values())))
+    np.testing.assert_allclose(w, np.array(list(w_ref.values())), rtol=tol, atol=0)
+    dg.pagerank(True, precision=precision)
+    w2, _ = dg.fetch()
+    assert w2.tobytes() == w.tobytes(), "rerun not bitwise identical"
+    dg.close()
+
+
 @pytest.mark.parametrize("part_min", [None, "0"])
 def test_kind_hash_collision_retries_with_next_seed(monkeypatch, part_min):
     """MR_KIND_TEST_COLLIDE narrows the first attempt's kind keys to 2 bits, so distinct trace
