@@ -174,6 +174,7 @@ extern "C" void mr_ctx_destroy(mr_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->side) (void)hipStreamSynchronize(ctx->side);
     for (mr_ctx* a : ctx->aux) mr_ctx_destroy(a);
     ctx->aux.clear();
     {   // the context's live handles go first (their buffers return to its pool)
@@ -196,6 +197,9 @@ extern "C" void mr_ctx_destroy(mr_ctx* ctx) {
     mr_pool_release(ctx);
     for (auto& kv : ctx->pool_live) (void)hipFree(kv.first);   // handles the caller leaked
     ctx->pool_live.clear();
+    for (hipEvent_t& e : ctx->side_ev)
+        if (e) (void)hipEventDestroy(e);
+    if (ctx->side) (void)hipStreamDestroy(ctx->side);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }

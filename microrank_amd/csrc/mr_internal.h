@@ -39,6 +39,10 @@ struct mr_ctx {
     // mr_windows_batch: auxiliary contexts (own stream + pool) for the windows' concurrent
     // detector / graph-build / spectrum phases; created on first use, destroyed with this one
     std::vector<mr_ctx*> aux;
+    // a second stream for work that overlaps the main stream inside one call (wide graphs:
+    // k_cold_ops beside k_cold_trace / k_tr_a), joined back by events; created on first use
+    hipStream_t side = nullptr;
+    hipEvent_t side_ev[2] = {nullptr, nullptr};
 };
 
 void* mr_pool_alloc(mr_ctx* ctx, size_t bytes);

@@ -3276,30 +3276,49 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
     // a sharded graph with no collective backend is one whole shard: the split launches around the
     // (no-op) all-reduces would compute the same integers / sums in two halves
     const bool coll = sharded && mr_coll_ready(ctx);
+    // wide graphs: k_cold_ops (LDS-bound) runs on the side stream beside k_cold_trace (L2-gather
+    // bound) and k_tr_a on the main stream; k_fx_b waits for both
+    bool any_wide = false;
+    for (int i = 0; i < ng; ++i) any_wide = any_wide || gs[i]->wide;
+    static const bool no_side = getenv("MR_WIDE_SERIAL") != nullptr;   // A/B knob: one stream
+    hipStream_t sst = st;
+    if (any_wide && !no_side) {
+        if (!ctx->side) {
+            MR_TRY_HIP(ctx, hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
+            for (hipEvent_t& e : ctx->side_ev) MR_TRY_HIP(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        }
+        sst = ctx->side;
+    }
     for (int it = 0; it < iters; ++it) {
         mr_prof_begin(ctx);
+        if (any_wide && sst != st) {
+            MR_TRY_HIP(ctx, hipEventRecord(ctx->side_ev[0], st));   // this iteration's su and q are ready
+            MR_TRY_HIP(ctx, hipStreamWaitEvent(sst, ctx->side_ev[0], 0));
+        }
         for (int i = 0; i < ng; ++i) {   // wide graphs: the cold halves, before k_tr_a / k_fx_b
             mr_graph* g = gs[i];
             if (!g->wide) continue;
-            if (g->T)
-                hipLaunchKernelGGL(k_cold_trace, dim3(cdiv(g->T, 256)), dim3(256), 0, st, g->cold_off_p.p, g->cold_ops_p.p,
-                                   g->sub[it & 1].p, g->T, g->cold_acc.p);
             const void* qc = fp32 ? (const void*)g->q32[it & 1].p : (const void*)g->q64[it & 1].p;
             const size_t lds_c = (size_t)g->cold_rw * sizeof(unsigned long long);
             if (fp32)
-                hipLaunchKernelGGL(k_cold_ops<float>, dim3(g->n_cb), dim3(WIDE_CT), lds_c, st, g->cb_beg.p, g->cp_pos.p,
+                hipLaunchKernelGGL(k_cold_ops<float>, dim3(g->n_cb), dim3(WIDE_CT), lds_c, sst, g->cb_beg.p, g->cp_pos.p,
                                    g->cp_op.p, qc, g->mslot.p, it, hv[(size_t)i].cx_scale, g->cold_rw,
                                    (unsigned long long*)g->cold_part.p);
             else
-                hipLaunchKernelGGL(k_cold_ops<double>, dim3(g->n_cb), dim3(WIDE_CT), lds_c, st, g->cb_beg.p, g->cp_pos.p,
+                hipLaunchKernelGGL(k_cold_ops<double>, dim3(g->n_cb), dim3(WIDE_CT), lds_c, sst, g->cb_beg.p, g->cp_pos.p,
                                    g->cp_op.p, qc, g->mslot.p, it, hv[(size_t)i].cx_scale, g->cold_rw,
                                    (unsigned long long*)g->cold_part.p);
+            if (g->T)
+                hipLaunchKernelGGL(k_cold_trace, dim3(cdiv(g->T, 256)), dim3(256), 0, st, g->cold_off_p.p, g->cold_ops_p.p,
+                                   g->sub[it & 1].p, g->T, g->cold_acc.p);
             MR_DEBUG_CHECK(ctx, "k_cold");
         }
+        if (any_wide && sst != st) MR_TRY_HIP(ctx, hipEventRecord(ctx->side_ev[1], sst));
         if (blocks_fa) {
             if (sg_a) hipLaunchKernelGGL(sg_a, dim3(blocks_fa), dim3(fx_bs), lds_f, st, dv.p, ng, split_fa, d, alpha, it, TT);
             else hipLaunchKernelGGL(fx_a, dim3(blocks_fa), dim3(fx_bs), lds_f, st, dv.p, ng, split_fa, d, alpha, it, TT);
             MR_DEBUG_CHECK(ctx, "k_fx_a");
+            if (any_wide && sst != st) MR_TRY_HIP(ctx, hipStreamWaitEvent(st, ctx->side_ev[1], 0));   // k_cold_ops done
             if (!coll) {
                 hipLaunchKernelGGL(k_fx_b, dim3(blocks_fb), dim3(WAVE * FB_W), 0, st, dv.p, ng, split_fb, d, it, 0);
             } else {   // ONE all-reduce: the P_sr r limbs and every rank's r' max (exact: integers)
