@@ -236,12 +236,13 @@ __global__ void k_set_last(int64_t* off, int32_t n, int64_t v) { off[n] = v; }
 
 // ---------------------------------------------------------------- per-node arrays
 __global__ void k_node_arrays(const int32_t* node_podop, int32_t N, const int32_t* ocnt, const int32_t* nchild_code,
-                              int32_t* len_o, int32_t* nchild) {
+                              const int32_t* ocov, int32_t* len_o, int32_t* nchild, int32_t* cov) {
     int32_t n = blockIdx.x * blockDim.x + threadIdx.x;
     if (n >= N) return;
     const int32_t c = node_podop[n];
     len_o[n] = ocnt[c];
     nchild[n] = nchild_code[c];
+    if (ocov) cov[n] = ocov[c];
 }
 __global__ void k_edge_nodes(const uint64_t* ekey, int64_t E, const int32_t* node_of_code, int nb, uint64_t* skey) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -258,20 +259,167 @@ __global__ void k_edge_csr(const uint64_t* skey, int64_t E, int nb, int32_t* ss_
     atomicAdd(&ccount[skey[i] >> nb], 1);
 }
 
+// ---------------------------------------------------------------- node order of a window graph, one block
+// Windows (C2/C3: up to a few thousand pod-ops and call edges) take the whole of build_nodes in
+// ONE single-block launch -- edges out of the hash table, parent flags and child counts, the
+// node order (parents by code, the rest by first row, T10), per-node arrays, and P_ss by child --
+// instead of ~15 launches and two host round trips.  Sizes go to `out` (N, E, overflow); a graph
+// with more than NS_EMAX edges sets overflow and the caller runs build_nodes instead.
+constexpr int NS_T = 1024, NS_PMAX = 4096, NS_EMAX = 8192;
+__device__ __forceinline__ void ns_bitonic(uint64_t* a, int n) {   // n a power of two
+    for (int k = 2; k <= n; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < n; i += NS_T) {
+                const int ixj = i ^ j;
+                if (ixj > i) {
+                    const uint64_t x = a[i], y = a[ixj];
+                    if ((x > y) == ((i & k) == 0)) {
+                        a[i] = y;
+                        a[ixj] = x;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+}
+// exclusive prefix of v over the block's threads (in thread order); total in *tot
+__device__ __forceinline__ int32_t ns_scan(int32_t v, int32_t* sbuf, int32_t* tot) {
+    sbuf[threadIdx.x] = v;
+    __syncthreads();
+    for (int o = 1; o < NS_T; o <<= 1) {
+        const int32_t a = threadIdx.x >= o ? sbuf[threadIdx.x - o] : 0;
+        __syncthreads();
+        sbuf[threadIdx.x] += a;
+        __syncthreads();
+    }
+    const int32_t incl = sbuf[threadIdx.x];
+    if (threadIdx.x == NS_T - 1) *tot = incl;
+    __syncthreads();
+    return incl - v;
+}
+__global__ void __launch_bounds__(NS_T) k_nodes_small(const uint64_t* gk, const uint32_t* gc, int64_t ecap,
+                                                     const int32_t* ocnt, const int32_t* ofirst, int32_t NP,
+                                                     int32_t* node_of_code, int32_t* node_podop, int32_t* len_o,
+                                                     int32_t* nchild, const int32_t* ocov, int32_t* cov,
+                                                     int32_t* ss_par, int64_t* ss_off, const int64_t* T_dev, const int64_t* nnz_dev, int64_t* rs_off,
+                                                     int64_t* out) {
+    __shared__ int32_t is_par[NS_PMAX], nch[NS_PMAX], noc[NS_PMAX];
+    __shared__ uint64_t qb[NS_PMAX], eb[NS_EMAX];
+    __shared__ int32_t sbuf[NS_T];
+    __shared__ int32_t ecount, tot, P, Q;
+    const int tid = threadIdx.x;
+    for (int c = tid; c < NP; c += NS_T) {
+        is_par[c] = 0;
+        nch[c] = 0;
+    }
+    if (tid == 0) ecount = 0;
+    __syncthreads();
+    // call edges out of the hash table (parent code << 32 | child code): parents and child counts
+    for (int64_t i = tid; i < ecap; i += NS_T) {
+        const uint64_t k = gk[i];
+        if (k == EMPTY) continue;
+        const int32_t par = (int32_t)(k >> 32);
+        is_par[par] = 1;
+        atomicAdd(&nch[par], (int32_t)gc[i]);
+        const int32_t e = atomicAdd(&ecount, 1);
+        if (e < NS_EMAX) eb[e] = k;
+    }
+    __syncthreads();
+    const int32_t E = ecount;
+    if (tid == 0) {   // the trace side's sizes (its scans ran before this launch)
+        out[3] = *T_dev;
+        out[4] = *nnz_dev;
+        rs_off[*T_dev] = *nnz_dev;
+    }
+    if (E > NS_EMAX) {
+        if (tid == 0) out[2] = 1;
+        return;
+    }
+    // node order: parents by code, then present non-parents by first row (T10)
+    const int per = (NP + NS_T - 1) / NS_T, c0 = tid * per;   // each thread a run of codes
+    int32_t np = 0, nq = 0;
+    for (int c = c0; c < min(c0 + per, NP); ++c) {
+        np += is_par[c] ? 1 : 0;
+        nq += (!is_par[c] && ocnt[c] > 0) ? 1 : 0;
+    }
+    int32_t pp = ns_scan(np, sbuf, &tot);
+    if (tid == 0) P = tot;
+    __syncthreads();
+    int32_t qp = ns_scan(nq, sbuf, &tot);
+    if (tid == 0) Q = tot;
+    __syncthreads();
+    const int32_t nP = P, nQ = Q;
+    for (int c = c0; c < min(c0 + per, NP); ++c) {
+        if (is_par[c]) {
+            noc[c] = pp;
+            node_podop[pp] = c;
+            ++pp;
+        } else if (ocnt[c] > 0) {
+            qb[qp++] = ((uint64_t)(uint32_t)ofirst[c] << 32) | (uint32_t)c;
+        }
+    }
+    int qn = 1;
+    while (qn < nQ) qn <<= 1;
+    for (int i = nQ + tid; i < qn; i += NS_T) qb[i] = EMPTY;
+    __syncthreads();
+    if (nQ > 1) ns_bitonic(qb, qn);
+    for (int i = tid; i < nQ; i += NS_T) {
+        const int32_t c = (int32_t)(qb[i] & 0xffffffffu);
+        noc[c] = nP + i;
+        node_podop[nP + i] = c;
+    }
+    __syncthreads();
+    const int32_t N = nP + nQ;
+    for (int c = tid; c < NP; c += NS_T) node_of_code[c] = (is_par[c] || ocnt[c] > 0) ? noc[c] : -1;
+    for (int c = c0; c < min(c0 + per, NP); ++c)   // per-node arrays (node_podop's writes are this block's)
+        if (is_par[c] || ocnt[c] > 0) {
+            len_o[noc[c]] = ocnt[c];
+            nchild[noc[c]] = nch[c];
+            cov[noc[c]] = ocov[c];
+        }
+    // P_ss by child: edges as (child node << 32 | parent node), sorted; offsets by binary search
+    for (int e = tid; e < E; e += NS_T) {
+        const uint64_t k = eb[e];
+        eb[e] = ((uint64_t)(uint32_t)noc[(int32_t)(k & 0xffffffffu)] << 32) | (uint32_t)noc[(int32_t)(k >> 32)];
+    }
+    int en = 1;
+    while (en < E) en <<= 1;
+    for (int i = E + tid; i < en; i += NS_T) eb[i] = EMPTY;
+    __syncthreads();
+    if (E > 1) ns_bitonic(eb, en);
+    for (int e = tid; e < E; e += NS_T) ss_par[e] = (int32_t)(eb[e] & 0xffffffffu);
+    for (int n = tid; n <= N; n += NS_T) {
+        int32_t lo = 0, hi = E;   // first edge whose child >= n
+        while (lo < hi) {
+            const int32_t mid = (lo + hi) >> 1;
+            if ((int32_t)(eb[mid] >> 32) < n) lo = mid + 1;
+            else hi = mid;
+        }
+        ss_off[n] = lo;
+    }
+    if (tid == 0) {
+        out[0] = N;
+        out[1] = E;
+        out[2] = 0;
+    }
+}
+
 // ---------------------------------------------------------------- indexed build (whole traces)
 constexpr int IX_EPT = 16;  // index entries per thread in k_ix_stats (fewer blocks: fewer global flushes)
 // k_ix_stats: 16-wave blocks (one per CU) whose LDS holds the per-pod-op counts and first rows
 // of up to IX_HIST codes (128 KB) beside the edge set: the C4 graph's 10k ops aggregate in LDS
 // instead of a global atomic pair per index entry
 constexpr int IX_BT = 1024;
-constexpr int IX_HIST = 16384;
+constexpr int IX_HIST = 12288;   // three per-code counters (span count, first row, traces)
 constexpr int IX_B = 8;     // entries per thread whose loads are batched
 // one launch for the indexed build's four initialisations (was four memsets: each a separate
 // ~3 us fill launch, twice per window): per-op counts / first rows, edge keys (EMPTY) / counts
-__global__ void k_ix_init(int32_t* ocnt, int32_t* ofirst, int32_t NP, uint64_t* gk, uint32_t* gc, int64_t ecap) {
+__global__ void k_ix_init(int32_t* ocnt, int32_t* ofirst, int32_t* ocov, int32_t NP, uint64_t* gk, uint32_t* gc,
+                          int64_t ecap) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < NP) {
         ocnt[i] = 0;
+        ocov[i] = 0;
         ofirst[i] = 0x7f7f7f7f;   // the old memset's byte pattern: larger than any row
     }
     if (i < ecap) {
@@ -294,17 +442,19 @@ __global__ void __launch_bounds__(IX_BT) k_ix_stats(const int32_t* tflag, int64_
                                                  const int32_t* po_op, const int32_t* po_cnt, const int32_t* po_first,
                                                  int64_t n_ed, const int32_t* ed_tr, const uint64_t* ed_key,
                                                  const int32_t* ed_cnt, int32_t n_podops, int use_lds_hist,
-                                                 int32_t* ocnt, int32_t* ofirst, uint64_t* gk, uint32_t* gc,
-                                                 uint64_t gmask) {
+                                                 int32_t* ocnt, int32_t* ofirst, int32_t* ocov, uint64_t* gk,
+                                                 uint32_t* gc, uint64_t gmask) {
     extern __shared__ int32_t lh[];
     __shared__ unsigned long long ek[ESET];
     __shared__ uint32_t ec[ESET];
     int32_t* lcnt = lh;
     int32_t* lfirst = lh + n_podops;
+    int32_t* lcov = lh + 2 * n_podops;   // traces per pod-op (the graph's coverage)
     if (use_lds_hist)
         for (int32_t i = threadIdx.x; i < n_podops; i += IX_BT) {
             lcnt[i] = 0;
             lfirst[i] = 0x7fffffff;
+            lcov[i] = 0;
         }
     for (int i = threadIdx.x; i < ESET; i += IX_BT) {
         ek[i] = EMPTY;
@@ -333,9 +483,11 @@ __global__ void __launch_bounds__(IX_BT) k_ix_stats(const int32_t* tflag, int64_
             if (use_lds_hist) {
                 atomicAdd(&lcnt[op[j]], cn[j]);
                 atomicMin(&lfirst[op[j]], fr[j]);
+                atomicAdd(&lcov[op[j]], 1);
             } else {
                 atomicAdd(&ocnt[op[j]], cn[j]);
                 atomicMin(&ofirst[op[j]], fr[j]);
+                atomicAdd(&ocov[op[j]], 1);
             }
         }
     }
@@ -378,6 +530,7 @@ __global__ void __launch_bounds__(IX_BT) k_ix_stats(const int32_t* tflag, int64_
             if (lcnt[i]) {
                 atomicAdd(&ocnt[i], lcnt[i]);
                 atomicMin(&ofirst[i], lfirst[i]);
+                atomicAdd(&ocov[i], lcov[i]);
             }
 }
 // join pairs whose rows lie in different traces count when both traces are selected (T11)
@@ -580,7 +733,8 @@ __global__ void k_zero2_i32(int32_t* a, int32_t* b, int32_t n) {
 }
 // sharded: node presence (span counts), first appearances and parent flags are reduced over the
 // ranks for the node order (every rank the same N and order); len_o / nchild stay this rank's.
-static int build_nodes(mr_ctx* ctx, mr_graph* g, int32_t NP, const int32_t* ocnt, const int32_t* ofirst, int row_bits,
+static int build_nodes(mr_ctx* ctx, mr_graph* g, int32_t NP, const int32_t* ocnt, const int32_t* ofirst,
+                       const int32_t* ocov, int row_bits,
                        const uint64_t* gk, const uint32_t* gc, uint64_t ecap, DBuf<int32_t>& node_of_code,
                        PhaseTimer* pt = nullptr, bool sharded = false) {
     hipStream_t st = ctx->stream;
@@ -655,9 +809,11 @@ static int build_nodes(mr_ctx* ctx, mr_graph* g, int32_t NP, const int32_t* ocnt
     const int nb = std::max(1, bits_for((uint64_t)std::max(N - 1, 0)));
     MR_TRY(g->len_o.alloc(ctx, N));
     MR_TRY(g->nchild.alloc(ctx, N));
+    if (ocov) MR_TRY(g->cov.alloc(ctx, (size_t)std::max(N, 1)));
     if (N)
         hipLaunchKernelGGL(k_node_arrays, dim3(cdiv(N, 256)), dim3(256), 0, st, g->node_podop.p, N, ocnt, nchild_code.p,
-                           g->len_o.p, g->nchild.p);
+                           ocov, g->len_o.p, g->nchild.p, g->cov.p);
+    g->cov_ready = ocov != nullptr;
     DBuf<uint64_t> skey;
     MR_TRY(skey.alloc(ctx, E));
     if (E) hipLaunchKernelGGL(k_edge_nodes, dim3(cdiv(E, 256)), dim3(256), 0, st, ekey.p, E, node_of_code.p, nb, skey.p);
@@ -724,8 +880,8 @@ static int graph_build_rows(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d_ma
                            ocnt.p, ofirst.p, gk.p, gc.p, ecap - 1);
     // 3. edges, node order, per-node arrays, P_ss
     DBuf<int32_t> node_of_code;
-    MR_TRY(build_nodes(ctx, g, NP, ocnt.p, ofirst.p, bits_for((uint64_t)std::max<int64_t>(Ssel, 1)), gk.p, gc.p, ecap,
-                       node_of_code));
+    MR_TRY(build_nodes(ctx, g, NP, ocnt.p, ofirst.p, nullptr, bits_for((uint64_t)std::max<int64_t>(Ssel, 1)), gk.p,
+                       gc.p, ecap, node_of_code));
     const int32_t N = g->N;
     // traces
     DBuf<int32_t> tflag, tidx_of_code;
@@ -853,9 +1009,10 @@ static int graph_build_indexed(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d
     MR_TRY(tpos.alloc(ctx, NT + 1));
     MR_TRY(zoff.alloc(ctx, NT + 1));
     MR_TRY(tmp.alloc(ctx, std::max<int64_t>({scan_tmp_elems(NT), scan_tmp_elems(NP), 1})));
-    DBuf<int32_t> ocnt, ofirst;
+    DBuf<int32_t> ocnt, ofirst, ocov;
     MR_TRY(ocnt.alloc(ctx, NP));
     MR_TRY(ofirst.alloc(ctx, NP));
+    MR_TRY(ocov.alloc(ctx, NP));
     const uint64_t ecap = edge_capacity(sp->n_edge_keys + X.matches, NP);
     DBuf<uint64_t> gk;
     DBuf<uint32_t> gc;
@@ -863,12 +1020,12 @@ static int graph_build_indexed(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d
     MR_TRY(gc.alloc(ctx, ecap));
     if (NP || ecap)
         hipLaunchKernelGGL(k_ix_init, dim3(cdiv(std::max<int64_t>(NP, (int64_t)ecap), 256)), dim3(256), 0, st, ocnt.p,
-                           ofirst.p, NP, gk.p, gc.p, (int64_t)ecap);
+                           ofirst.p, ocov.p, NP, gk.p, gc.p, (int64_t)ecap);
     if (NT) {
         hipLaunchKernelGGL(k_ix_sel, dim3(cdiv(NT, 256)), dim3(256), 0, st, d_mask, sp->tlen.p, sp->po_off.p, NT, tflag.p,
                            zc.p);
         const int use_lds = NP <= IX_HIST;
-        const size_t lds = use_lds ? 2 * (size_t)NP * sizeof(int32_t) : 0;
+        const size_t lds = use_lds ? 3 * (size_t)NP * sizeof(int32_t) : 0;
         // block cap 256 (one per CU); MR_IX_BLOCKS overrides it for measurements
         static const int ix_cap = [] {
             const char* e = getenv("MR_IX_BLOCKS");
@@ -877,7 +1034,7 @@ static int graph_build_indexed(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d
         const int nblk = std::max(1, std::min(ix_cap, cdiv(std::max(sp->n_po, sp->n_ed), IX_BT * IX_EPT)));
         hipLaunchKernelGGL(k_ix_stats, dim3(nblk), dim3(IX_BT), lds, st, tflag.p, sp->n_po, sp->po_tr.p, sp->po_op.p,
                            sp->po_cnt.p, sp->po_first.p, sp->n_ed, sp->ed_tr.p, sp->ed_key.p, sp->ed_cnt.p, NP, use_lds,
-                           ocnt.p, ofirst.p, gk.p, gc.p, ecap - 1);
+                           ocnt.p, ofirst.p, ocov.p, gk.p, gc.p, ecap - 1);
     }
     if (sp->n_xj)
         hipLaunchKernelGGL(k_ix_cross, dim3(cdiv(sp->n_xj, 256)), dim3(256), 0, st, d_mask, sp->xj_tc.p, sp->xj_tp.p,
@@ -891,7 +1048,49 @@ static int graph_build_indexed(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d
     MR_TRY(mr_exclusive_scan_i32(ctx, zc.p, zoff.p, NT, tmp.p));
     pt.mark("scans");
     DBuf<int32_t> node_of_code;
-    MR_TRY(build_nodes(ctx, g, NP, ocnt.p, ofirst.p, sp->row_bits, gk.p, gc.p, ecap, node_of_code, &pt, sharded));
+    static const bool no_small = getenv("MR_NO_NODES_SMALL") != nullptr;   // A/B knob
+    if (!sharded && !no_small && NP <= NS_PMAX) {
+        // one launch for the node order and P_ss, the trace rows / op lists into upper-bound
+        // buffers right behind it, and ONE host round trip for (N, E, T, nnz)
+        DBuf<int64_t> dout;
+        MR_TRY(dout.alloc(ctx, 8));
+        MR_TRY(node_of_code.alloc(ctx, std::max(NP, 1)));
+        MR_TRY(g->node_podop.alloc(ctx, std::max(NP, 1)));
+        MR_TRY(g->len_o.alloc(ctx, std::max(NP, 1)));
+        MR_TRY(g->nchild.alloc(ctx, std::max(NP, 1)));
+        MR_TRY(g->cov.alloc(ctx, std::max(NP, 1)));
+        MR_TRY(g->ss_par.alloc(ctx, NS_EMAX));
+        MR_TRY(g->ss_off.alloc(ctx, (size_t)NP + 1));
+        MR_TRY(g->trace_code.alloc(ctx, std::max(NT, 1)));
+        MR_TRY(g->len_t.alloc(ctx, std::max(NT, 1)));
+        MR_TRY(g->rs_ops.alloc(ctx, (size_t)std::max<int64_t>(sp->n_po, 1)));
+        MR_TRY(g->rs_off.alloc(ctx, (size_t)NT + 1));
+        hipLaunchKernelGGL(k_nodes_small, dim3(1), dim3(NS_T), 0, st, gk.p, gc.p, (int64_t)ecap, ocnt.p, ofirst.p, NP,
+                           node_of_code.p, g->node_podop.p, g->len_o.p, g->nchild.p, ocov.p, g->cov.p, g->ss_par.p,
+                           g->ss_off.p,
+                           tpos.p + NT, zoff.p + NT, g->rs_off.p, dout.p);
+        if (NT)
+            hipLaunchKernelGGL(k_ix_trace_rows, dim3(cdiv(NT, 256)), dim3(256), 0, st, tflag.p, tpos.p, zoff.p, NT,
+                               sp->tlen.p, g->trace_code.p, g->len_t.p, g->rs_off.p);
+        if (sp->n_po)
+            hipLaunchKernelGGL(k_ix_trace_ops, dim3(cdiv(sp->n_po, 256)), dim3(256), 0, st, tflag.p, zoff.p, sp->n_po,
+                               sp->po_tr.p, sp->po_off.p, sp->po_op.p, node_of_code.p, g->rs_ops.p);
+        int64_t h[5] = {0, 0, 0, 0, 0};   // N, E, overflow, T, nnz
+        MR_TRY(dout.download(ctx, h, 5));
+        MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+        pt.mark("nodes+traces");
+        if (!h[2]) {
+            g->N = (int32_t)h[0];
+            g->E = h[1];
+            g->T = (int32_t)h[3];
+            g->nnz_sr = g->nnz_rs = h[4];
+            g->cov_ready = true;
+            MR_TRY_HIP(ctx, hipGetLastError());
+            return MR_OK;
+        }
+        // more call edges than the one-block path holds: the general node order below
+    }
+    MR_TRY(build_nodes(ctx, g, NP, ocnt.p, ofirst.p, ocov.p, sp->row_bits, gk.p, gc.p, ecap, node_of_code, &pt, sharded));
     pt.mark("nodes");
     int64_t h[2] = {0, 0};   // T, nnz (their scans ran before build_nodes' syncs)
     MR_TRY_HIP(ctx, hipMemcpyAsync(&h[0], tpos.p + NT, sizeof(int64_t), hipMemcpyDeviceToHost, st));

@@ -179,6 +179,7 @@ struct mr_graph {
     DBuf<int32_t> wtile;             // [waves+1] first tile of each wave of the last launch plan
     int32_t wtile_nw = 0;            // waves that wtile was cut for
     int32_t wtile_tpb = 0;           // most tiles of one block under that cut
+    DBuf<double> dscale;             // {2^SC, 2^-SC} of a device-side cut (k_tr_cut; wtile_msum < 0)
     int64_t wtile_msum = 0;          // most traces one block stands for (x multiplicity when compressed)
     // P_sr in compressed sparse blocks for the s' pass: traces cut in tiles of 2^tshift; within a
     // tile the distinct (op, trace) entries sorted by (op, trace) as u16 tile-local trace
@@ -207,6 +208,7 @@ struct mr_graph {
     DBuf<double> op_sum;      // [N] sharded tile-path graphs: this rank's P_sr r per op, all-reduced
     // per-trace / per-op constants
     DBuf<int32_t> len_t, len_o, nchild, cov;
+    bool cov_ready = false;          // cov filled by the build (the indexed K1), else by mr_graph_prepare
     DBuf<float> w_t, u_o, pw;    // fp32(1/len_t), fp32(1/len_o), fp32(1/nchild)
     DBuf<int64_t> ss_off;        // P_ss by child
     DBuf<int32_t> ss_par;

@@ -58,20 +58,23 @@ __global__ void k_pr_reset(int32_t T, int64_t cap, int32_t N, float* pref, float
 }
 
 // ---------------------------------------------------------------- graph constants
-__global__ void k_trace_consts(const int32_t* len_t, float* w_t, int32_t T) {
-    int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t < T) w_t[t] = len_t[t] > 0 ? (float)(1.0 / (double)len_t[t]) : 0.0f;   // fp64 1/n -> fp32
-}
-
 __global__ void k_op_consts(const int32_t* len_o, const int32_t* nchild, float* u_o, float* pw, int32_t N) {
     int32_t o = blockIdx.x * blockDim.x + threadIdx.x;
     if (o >= N) return;
     u_o[o] = len_o[o] > 0 ? (float)(1.0 / (double)len_o[o]) : 0.0f;
     pw[o] = nchild[o] > 0 ? (float)(1.0 / (double)nchild[o]) : 0.0f;
 }
-__global__ void k_ids16(const int32_t* ops, int64_t n, uint16_t* o16) {
-    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) o16[i] = (uint16_t)ops[i];
+// per-graph constants in one launch: w_t = fp32(1/len_t) (fp64 1/n -> fp32), u_o, pw, and the
+// u16 copy of the op ids (N <= 65536)
+__global__ void k_graph_consts(const int32_t* len_t, float* w_t, int32_t T, const int32_t* len_o, const int32_t* nchild,
+                               float* u_o, float* pw, int32_t N, const int32_t* ops, int64_t n, uint16_t* o16) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < T) w_t[i] = len_t[i] > 0 ? (float)(1.0 / (double)len_t[i]) : 0.0f;
+    if (i < N) {
+        u_o[i] = len_o[i] > 0 ? (float)(1.0 / (double)len_o[i]) : 0.0f;
+        pw[i] = nchild[i] > 0 ? (float)(1.0 / (double)nchild[i]) : 0.0f;
+    }
+    if (o16 && i < n) o16[i] = (uint16_t)ops[i];
 }
 
 // ---------------------------------------------------------------- P_sr tiles (compressed sparse blocks)
@@ -312,9 +315,9 @@ __global__ void __launch_bounds__(TRB) k_tr_hist(const int64_t* off, int32_t T, 
         if (lh[i]) atomicAdd(&hist[i], lh[i]);
 }
 // positions: bin start (cursor, claimed per block and bin) + the trace's rank in its block's bin
-__global__ void __launch_bounds__(TRB) k_tr_place(const int64_t* off, int32_t T, int32_t nbin,
-                                                  unsigned long long* cursor, const float* w_t, int32_t* tperm,
-                                                  float* w_tp) {
+// (a bin's remaining count hands out its slots from the end: hist is consumed, no cursor copy)
+__global__ void __launch_bounds__(TRB) k_tr_place(const int64_t* off, int32_t T, int32_t nbin, const int64_t* boff,
+                                                  int32_t* hist, const float* w_t, int32_t* tperm, float* w_tp) {
     extern __shared__ int32_t lh[];
     int32_t* lbase = lh + nbin;
     for (int32_t i = threadIdx.x; i < nbin; i += TRB) lh[i] = 0;
@@ -329,7 +332,7 @@ __global__ void __launch_bounds__(TRB) k_tr_place(const int64_t* off, int32_t T,
     }
     __syncthreads();
     for (int32_t i = threadIdx.x; i < nbin; i += TRB)
-        if (lh[i]) lbase[i] = (int32_t)atomicAdd(&cursor[i], (unsigned long long)lh[i]);
+        if (lh[i]) lbase[i] = (int32_t)boff[i] + atomicSub(&hist[i], lh[i]) - lh[i];
     __syncthreads();
 #pragma unroll
     for (int32_t j = 0; j < TR_PER; ++j) {
@@ -350,6 +353,47 @@ __global__ void k_tr_chunks(const int32_t* tperm, const int64_t* off, int32_t T,
 __global__ void k_tr_coff(const int64_t* c64, int32_t n, int32_t* coff) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i <= n) coff[i] = (int32_t)c64[i];
+}
+// k_tr_a's per-wave runs of tiles of about equal cost (chunks + 2 per tile: a tile's q / r words
+// weigh about two chunks), in one block on the device (no host round trip): cut[i] = first tile
+// whose cost prefix reaches total * i / nw.  A block (NW waves) must stay within 1023 tiles (65472
+// traces: the fixed-point budget); a cost cut that breaks it falls back to equal tile counts (the
+// host sizes the grid so those fit).  scale = {2^SC, 2^-SC}, SC = 64 - bits(most traces of a block).
+constexpr int TC_T = 1024, TC_MAX = 16384;
+__global__ void __launch_bounds__(TC_T) k_tr_cut(const int32_t* coff, int32_t W, int32_t nw, int32_t NW, int32_t* cut,
+                                                 double* scale) {
+    __shared__ int32_t lc[TC_MAX + 1];
+    __shared__ int32_t mx;
+    if (threadIdx.x == 0) mx = 0;
+    const double total = W ? (double)coff[W] + 2.0 * (double)W : 0.0;
+    for (int32_t i = threadIdx.x; i <= nw; i += TC_T) {
+        const double target = total * (double)i / (double)nw;
+        int32_t lo = 0, hi = W;
+        while (lo < hi) {
+            const int32_t mid = (lo + hi) >> 1;
+            if ((double)coff[mid] + 2.0 * (double)mid < target) lo = mid + 1;
+            else hi = mid;
+        }
+        lc[i] = i == nw ? W : lo;
+    }
+    __syncthreads();
+    const int32_t nb = nw / NW;
+    for (int32_t b = threadIdx.x; b < nb; b += TC_T) atomicMax(&mx, lc[(b + 1) * NW] - lc[b * NW]);
+    __syncthreads();
+    if (mx > 1023) {   // (uniform: read after the barrier)
+        __syncthreads();
+        if (threadIdx.x == 0) mx = 0;
+        for (int32_t i = threadIdx.x; i <= nw; i += TC_T) lc[i] = (int32_t)((int64_t)W * i / nw);
+        __syncthreads();
+        for (int32_t b = threadIdx.x; b < nb; b += TC_T) atomicMax(&mx, lc[(b + 1) * NW] - lc[b * NW]);
+        __syncthreads();
+    }
+    for (int32_t i = threadIdx.x; i <= nw; i += TC_T) cut[i] = lc[i];
+    if (threadIdx.x == 0) {
+        const int sc = __clzll((unsigned long long)max(mx, 1) * WAVE);   // 64 - bits(traces)
+        scale[0] = __longlong_as_double((long long)(1023 + sc) << 52);
+        scale[1] = __longlong_as_double((long long)(1023 - sc) << 52);
+    }
 }
 // thread per (tile, lane): the lane's trace rotated by (trace mod len), then pads N + lane
 __global__ void k_tr_fill(const int32_t* tperm, const int64_t* off, const uint16_t* ids, const int64_t* c64, int32_t T,
@@ -894,6 +938,7 @@ struct GDev {
     double* op_sum;                // sharded tile path: [N] pair-partial sums per op
     unsigned long long* stamp;   // diagnostics (MR_FX_STAMP): per-block phase clocks, else null
     double fx_scale, fx_iscale;
+    const double* dscale;          // k_tr_a graphs cut on the device: {2^SC, 2^-SC} (k_tr_cut), else null
     // wide fused graphs: k_tr_a's ops [0, NA) (NA = N otherwise); ops [NA, N) in ranges of
     // cold_rw ops whose rows (cold_part, blocks cold_rowbase[r] .. [r+1]) carry scale cx_scale
     int32_t NA, cold_rw;
@@ -1974,7 +2019,7 @@ __global__ void __launch_bounds__(NT) k_tr_a(const GDev* __restrict__ gs, int32_
         }
     }
     __syncthreads();   // accumulator and maxima ready
-    const double xsc = G.fx_scale / msh[1], Ms = msh[0];
+    const double xsc = (G.dscale ? G.dscale[0] : G.fx_scale) / msh[1], Ms = msh[0];
     double rmax = -__builtin_huge_val();
     if (k < ke) {
         auto pos = [&](int32_t kk) { return min(kk * WAVE + lane, T - 1); };
@@ -2195,7 +2240,7 @@ __global__ void __launch_bounds__(WAVE * FB_W) k_fx_b(const GDev* __restrict__ g
     unsigned long long* Mnext = G.mslot + (size_t)2 * MSH * ((k3 + 1) % 3);
     const double ssv = lssv[lane];   // (written before the barrier above)
     // hi, lo < 2^53 (fewer than 2^21 rows over all ranks): both conversions exact, one rounding
-    const double sum = ((double)hi * 4294967296.0 + (double)lo) * (o < G.NA ? G.fx_iscale : G.cx_iscale);
+    const double sum = ((double)hi * 4294967296.0 + (double)lo) * (o < G.NA ? (G.dscale ? G.dscale[1] : G.fx_iscale) : G.cx_iscale);
     const double v = d * (sum + ssv);      // pagerank.py:122-124
     G.spb[nxt][op] = v;
     G.sub[nxt][o] = (double)uo * v;   // su in the kernel's labels
@@ -2582,11 +2627,32 @@ static int64_t wv_blocks(int32_t T, int32_t N, const FxPlan& P) {
 static int tr_split(mr_ctx* ctx, mr_graph* g, const FxPlan& P, int64_t* nfa) {
     const int64_t W = g->n_wt, NW = P.NT / WAVE;
     const int64_t resident = plan_resident(kern_n(g), P);
-    int64_t nb = std::max<int64_t>(std::min<int64_t>(resident, cdiv(W, NW)), 1);
+    int64_t nb = std::max<int64_t>({std::min<int64_t>(resident, cdiv(W, NW)), cdiv(W, 1023), 1});
+    // on the device (k_tr_cut: no host round trip) unless a block's traces must be weighed by
+    // their kinds' multiplicities (kind-compressed graphs) or the cut table exceeds its LDS
+    if (g->tile_mult_h.empty() && nb * NW <= TC_MAX) {
+        const int64_t nw = nb * NW;
+        if (!(g->wtile.p && g->wtile_nw == nw && g->wtile_msum < 0)) {
+            MR_TRY(g->wtile.alloc(ctx, (size_t)nw + 1));
+            MR_TRY(g->dscale.alloc(ctx, 2));
+            hipLaunchKernelGGL(k_tr_cut, dim3(1), dim3(TC_T), 0, ctx->stream, g->coff.p, (int32_t)W, (int32_t)nw,
+                               (int32_t)NW, g->wtile.p, g->dscale.p);
+            MR_TRY_HIP(ctx, hipGetLastError());
+            g->wtile_nw = (int32_t)nw;
+            g->wtile_msum = -1;   // the scale is on the device
+        }
+        *nfa = nb;
+        return MR_OK;
+    }
+    if (g->coff_h.size() != (size_t)W + 1) {
+        g->coff_h.assign((size_t)W + 1, 0);
+        MR_TRY(g->coff.download(ctx, g->coff_h.data(), (size_t)W + 1));
+        MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    }
     const std::vector<int32_t>& co = g->coff_h;
     for (;;) {
         const int64_t nw = nb * NW;
-        if (g->wtile.p && g->wtile_nw == nw) break;
+        if (g->wtile.p && g->wtile_nw == nw && g->wtile_msum >= 0) break;
         std::vector<int32_t> cut((size_t)nw + 1);
         const double total = W ? (double)co[(size_t)W] + 2.0 * (double)W : 0.0;
         int64_t k = 0;
@@ -2634,7 +2700,7 @@ static int fused_blocks(mr_ctx* ctx, mr_graph* g, const FxPlan& P, int TT_v1, in
 // chunk count sizes the id array; the chunk offsets stay on the host for the per-wave cut).
 // off / ids: the trace-major incidence the kernel walks (rs_off with rs16 / rsp, or a wide graph's
 // hot entries), N: the kernel's op count (pads N + lane)
-static int tr_layout(mr_ctx* ctx, mr_graph* g, const int64_t* off, const uint16_t* src, int32_t N) {
+static int tr_layout(mr_ctx* ctx, mr_graph* g, const int64_t* off, const uint16_t* src, int32_t N, int64_t nent) {
     hipStream_t st = ctx->stream;
     const int32_t T = g->T;
     const int32_t W = cdiv(T, WAVE);
@@ -2643,7 +2709,6 @@ static int tr_layout(mr_ctx* ctx, mr_graph* g, const int64_t* off, const uint16_
     const int32_t nbin = N + 1;   // trace lengths 1..N (distinct ops)
     DBuf<int32_t> hist;
     DBuf<int64_t> boff, c64, tmp;
-    DBuf<unsigned long long> cursor;
     MR_TRY(hist.zero(ctx, (size_t)nbin));
     MR_TRY(boff.alloc(ctx, (size_t)nbin + 1));
     MR_TRY(c64.alloc(ctx, (size_t)W + 1));
@@ -2656,18 +2721,17 @@ static int tr_layout(mr_ctx* ctx, mr_graph* g, const int64_t* off, const uint16_
         hipLaunchKernelGGL(k_tr_hist, dim3(nb), dim3(TRB), (size_t)nbin * sizeof(int32_t), st, off, T, nbin,
                            hist.p);
         MR_TRY(mr_exclusive_scan_i32(ctx, hist.p, boff.p, nbin, tmp.p));
-        MR_TRY(cursor.alloc(ctx, (size_t)nbin));
-        MR_TRY_HIP(ctx, hipMemcpyAsync(cursor.p, boff.p, (size_t)nbin * sizeof(int64_t), hipMemcpyDeviceToDevice, st));
         hipLaunchKernelGGL(k_tr_place, dim3(nb), dim3(TRB), 2 * (size_t)nbin * sizeof(int32_t), st, off, T,
-                           nbin, cursor.p, g->w_t.p, g->tperm.p, g->w_tp.p);
+                           nbin, boff.p, hist.p, g->w_t.p, g->tperm.p, g->w_tp.p);
         hipLaunchKernelGGL(k_tr_chunks, dim3(cdiv(W, 256)), dim3(256), 0, st, g->tperm.p, off, T, W, c64.p);
     }
     MR_TRY(mr_exclusive_scan(ctx, c64.p, c64.p, W, tmp.p));
     hipLaunchKernelGGL(k_tr_coff, dim3(cdiv((int64_t)W + 1, 256)), dim3(256), 0, st, c64.p, W, g->coff.p);
-    g->coff_h.assign((size_t)W + 1, 0);
-    MR_TRY(g->coff.download(ctx, g->coff_h.data(), (size_t)W + 1));
-    MR_TRY_HIP(ctx, hipStreamSynchronize(st));
-    const int64_t nch = g->coff_h[(size_t)W];
+    // the id array at an upper bound of the chunk count (no host round trip): tile k holds
+    // ceil(maxlen_k / 4) chunks, and with lengths ascending maxlen_k <= every length of tile k + 1,
+    // so sum_k maxlen_k <= nent / 64 + 2 N
+    g->coff_h.clear();
+    const int64_t nch = (int64_t)W + (nent / WAVE + 2 * (int64_t)N) / 4 + 2;
     MR_TRY(g->tids.alloc(ctx, (size_t)std::max<int64_t>(nch, 1) * WAVE * 4));
     if (W)
         hipLaunchKernelGGL(k_tr_fill, dim3(cdiv((int64_t)W * WAVE, 256)), dim3(256), 0, st, g->tperm.p, off, src,
@@ -2687,8 +2751,8 @@ static int wide_prepare(mr_ctx* ctx, mr_graph* g) {
     g->NA = NA;
     g->rsp.reset();
     // ---- coverage, then labels by descending coverage (perm[new] = old)
-    MR_TRY_HIP(ctx, hipMemsetAsync(g->cov.p, 0, (size_t)N * sizeof(int32_t), st));
-    if (nnz)
+    if (!g->cov_ready) MR_TRY_HIP(ctx, hipMemsetAsync(g->cov.p, 0, (size_t)N * sizeof(int32_t), st));
+    if (nnz && !g->cov_ready)
         hipLaunchKernelGGL(k_cov_hist_w, dim3(cdiv(nnz, (int64_t)256 * 256)), dim3(256),
                            (size_t)std::min(N, WIDE_HIST) * sizeof(int32_t), st, g->rs_ops.p, nnz, N, g->cov.p);
     const int nbo = bits_for((uint64_t)(N - 1));
@@ -2721,7 +2785,7 @@ static int wide_prepare(mr_ctx* ctx, mr_graph* g) {
     MR_TRY(g->hot16.alloc(ctx, (size_t)n_hot + 8));
     hipLaunchKernelGGL(k_wide_hot, dim3(cdiv(T, 256)), dim3(256), 0, st, g->rs_off.p, g->rs_ops.p, inv.p, T, NA,
                        g->hot_off.p, g->hot16.p);
-    MR_TRY(tr_layout(ctx, g, g->hot_off.p, g->hot16.p, NA));   // tperm, w_tp, tids, coff (host copy)
+    MR_TRY(tr_layout(ctx, g, g->hot_off.p, g->hot16.p, NA, n_hot));   // tperm, w_tp, tids, coff (host copy)
     // ---- cold entries in position order
     DBuf<int32_t> cnt;
     DBuf<int64_t> coff64;
@@ -2799,13 +2863,14 @@ int mr_graph_prepare(mr_ctx* ctx, mr_graph* g) {
     MR_TRY(g->w_t.alloc(ctx, (size_t)T));
     MR_TRY(g->u_o.alloc(ctx, (size_t)N));
     MR_TRY(g->pw.alloc(ctx, (size_t)N));
-    MR_TRY(g->cov.alloc(ctx, (size_t)N));
-    if (T) hipLaunchKernelGGL(k_trace_consts, dim3(cdiv(T, 256)), dim3(256), 0, st, g->len_t.p, g->w_t.p, T);
-    if (N) hipLaunchKernelGGL(k_op_consts, dim3(cdiv(N, 256)), dim3(256), 0, st, g->len_o.p, g->nchild.p, g->u_o.p, g->pw.p, N);
-    if (N <= 65536 && g->nnz_rs) {
-        MR_TRY(g->rs16.alloc(ctx, (size_t)g->nnz_rs + 8));
-        hipLaunchKernelGGL(k_ids16, dim3(cdiv(g->nnz_rs, 256)), dim3(256), 0, st, g->rs_ops.p, g->nnz_rs, g->rs16.p);
-    }
+    if (!g->cov_ready) MR_TRY(g->cov.alloc(ctx, (size_t)N));
+    const bool u16 = N <= 65536 && g->nnz_rs;
+    if (u16) MR_TRY(g->rs16.alloc(ctx, (size_t)g->nnz_rs + 8));
+    const int64_t nc = std::max<int64_t>({(int64_t)T, (int64_t)N, u16 ? g->nnz_rs : 0});
+    if (nc)
+        hipLaunchKernelGGL(k_graph_consts, dim3(cdiv(nc, 256)), dim3(256), 0, st, g->len_t.p, g->w_t.p, T, g->len_o.p,
+                           g->nchild.p, g->u_o.p, g->pw.p, N, g->rs_ops.p, u16 ? g->nnz_rs : 0,
+                           u16 ? g->rs16.p : (uint16_t*)nullptr);
     g->relabeled = false;   // (set below for fused graphs that need it)
     g->wide = false;
     g->NA = N;
@@ -2818,8 +2883,8 @@ int mr_graph_prepare(mr_ctx* ctx, mr_graph* g) {
     }
     g->fused = fusable && N <= FX_NMAX && fx_tt(N) > 0;
     if (g->fused) {   // no P_sr tiles: the fused iteration reads the trace-major ids only
-        MR_TRY_HIP(ctx, hipMemsetAsync(g->cov.p, 0, (size_t)std::max(N, 1) * sizeof(int32_t), st));
-        if (nnz && N)
+        if (!g->cov_ready) MR_TRY_HIP(ctx, hipMemsetAsync(g->cov.p, 0, (size_t)std::max(N, 1) * sizeof(int32_t), st));
+        if (nnz && N && !g->cov_ready)
             hipLaunchKernelGGL(k_cov_hist, dim3(cdiv(nnz, 256 * 64)), dim3(256), (size_t)N * sizeof(int32_t), st,
                                g->rs16.p, nnz, N, g->cov.p);
         // su does not fit in LDS beside the accumulators: relabel ops by descending coverage so
@@ -2843,7 +2908,7 @@ int mr_graph_prepare(mr_ctx* ctx, mr_graph* g) {
             g->perm.reset();
             g->rsp.reset();
         }
-        MR_TRY(tr_layout(ctx, g, g->rs_off.p, g->relabeled ? g->rsp.p : g->rs16.p, N));
+        MR_TRY(tr_layout(ctx, g, g->rs_off.p, g->relabeled ? g->rsp.p : g->rs16.p, N, nnz));
         g->n_tiles = 0;
         g->n_pairs = 0;
         MR_TRY_HIP(ctx, hipGetLastError());
@@ -3218,6 +3283,8 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         v.cold_rowbase = g->cold_rowbase.p;
         v.cx_scale = v.fx_scale;
         v.cx_iscale = v.fx_iscale;
+        // the graph's scale on the device (k_tr_cut) unless the ranks share the fixed one
+        v.dscale = (!sharded && plan.tr && g->fused && g->wtile_msum < 0) ? g->dscale.p : nullptr;
         if (g->wide) {
             // cold rows: at most cold_span adds per op and row; a sharded graph's ranks sum their
             // limbs per op, and an op hot on one rank may be cold on another: one scale for both
