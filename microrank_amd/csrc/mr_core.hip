@@ -105,6 +105,16 @@ void mr_pool_free(mr_ctx* ctx, void* p) {
     ctx->pool_live.erase(it);
 }
 
+int mr_read_words(mr_ctx* ctx, const int64_t* dev, int n, int64_t* out) {
+    if (n <= 0) return MR_OK;
+    if (n > 64) return mr_fail(ctx, MR_ERR_ARG, "mr_read_words: %d words", n);
+    if (!ctx->pin) MR_TRY_HIP(ctx, hipHostMalloc((void**)&ctx->pin, 64 * sizeof(int64_t), hipHostMallocDefault));
+    MR_TRY_HIP(ctx, hipMemcpyAsync(ctx->pin, dev, (size_t)n * sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+    MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    for (int i = 0; i < n; ++i) out[i] = ctx->pin[i];
+    return MR_OK;
+}
+
 void mr_pool_release(mr_ctx* ctx) {
     (void)hipStreamSynchronize(ctx->stream);
     for (auto& kv : ctx->pool_free) (void)hipFree(kv.second);
@@ -200,6 +210,7 @@ extern "C" void mr_ctx_destroy(mr_ctx* ctx) {
     for (hipEvent_t& e : ctx->side_ev)
         if (e) (void)hipEventDestroy(e);
     if (ctx->side) (void)hipStreamDestroy(ctx->side);
+    if (ctx->pin) (void)hipHostFree(ctx->pin);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }

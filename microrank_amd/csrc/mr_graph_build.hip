@@ -713,11 +713,7 @@ extern "C" int mr_spans_free(mr_spans* s) {
     return MR_OK;
 }
 
-static int read_i64(mr_ctx* ctx, const int64_t* dev, int64_t* host) {
-    MR_TRY_HIP(ctx, hipMemcpyAsync(host, dev, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
-    MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    return MR_OK;
-}
+static int read_i64(mr_ctx* ctx, const int64_t* dev, int64_t* host) { return mr_read_words(ctx, dev, 1, host); }
 
 // Shared by both builds, after the per-pod-op statistics and the call-edge hash are complete:
 // call edges -> node order (sorted parent ops, then the others by first appearance, T10) ->
@@ -1076,8 +1072,7 @@ static int graph_build_indexed(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d
             hipLaunchKernelGGL(k_ix_trace_ops, dim3(cdiv(sp->n_po, 256)), dim3(256), 0, st, tflag.p, zoff.p, sp->n_po,
                                sp->po_tr.p, sp->po_off.p, sp->po_op.p, node_of_code.p, g->rs_ops.p);
         int64_t h[5] = {0, 0, 0, 0, 0};   // N, E, overflow, T, nnz
-        MR_TRY(dout.download(ctx, h, 5));
-        MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+        MR_TRY(mr_read_words(ctx, dout.p, 5, h));
         pt.mark("nodes+traces");
         if (!h[2]) {
             g->N = (int32_t)h[0];

@@ -43,11 +43,16 @@ struct mr_ctx {
     // k_cold_ops beside k_cold_trace / k_tr_a), joined back by events; created on first use
     hipStream_t side = nullptr;
     hipEvent_t side_ev[2] = {nullptr, nullptr};
+    // pinned host words for the small size read-backs of a call (a DMA straight into host memory
+    // instead of the runtime's pageable staging path); created on first use
+    int64_t* pin = nullptr;
 };
 
 void* mr_pool_alloc(mr_ctx* ctx, size_t bytes);
 void mr_pool_free(mr_ctx* ctx, void* p);
 void mr_pool_release(mr_ctx* ctx);
+// n (<= 64) int64 words from the device into out, through the context's pinned words; syncs the stream
+int mr_read_words(mr_ctx* ctx, const int64_t* dev, int n, int64_t* out);
 
 int mr_fail(mr_ctx* ctx, int code, const char* fmt, ...);
 
