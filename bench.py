@@ -604,6 +604,35 @@ def main():
     }
     if args.pmc_child:
         return
+    # SURVEY 8(d) window bytes: 52 S (the span columns once) + per graph build 24 S read + 4 nnz +
+    # 4 T written + the window's PageRank iterations (the live per-iteration byte counts above)
+    S = int(abnormal.n_spans)
+    nnz_w = max(0.0, (edges // max(n_win, 1)) / 25.0) / 2.0   # 2 nnz + E per iteration, E << nnz
+    bytes_w = 52.0 * S + 2 * 24.0 * S + 4.0 * nnz_w + 4.0 * (na + nn) + kbytes.value / max(n_win, 1)
+    out["window_roofline"] = {"bytes_per_window": round(bytes_w), "achieved": round(bytes_w * n_win / elapsed / 1e9, 1),
+                              "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                              "frac": round(bytes_w * n_win / elapsed / 1e9 / HBM_PEAK_GBS, 4),
+                              "formula": "52 S + 2 (24 S + 4 nnz + 4 T) + 25 B_iter per graph (SURVEY 8(d))"}
+    try:   # single-window latency: one window per mr_windows_batch call, nothing to overlap with
+        from microrank_amd.online_rca import rank_windows
+
+        one = [wins[0][0][:5]]
+        pr = "fp32" if prec == _lib.MR_FP32 else "fp64"
+        for _ in range(2):
+            rank_windows(ctx, one, precision=pr)
+        ctx.sync()
+        lat = []
+        for _ in range(15):
+            ts = time.perf_counter()
+            rank_windows(ctx, one, precision=pr)
+            ctx.sync()
+            lat.append((time.perf_counter() - ts) * 1e3)
+        lat.sort()
+        out["window_ms"] = {"median": round(lat[len(lat) // 2], 3), "min": round(lat[0], 3),
+                            "what": "one window alone (W=1): detect + 2 graph builds + 2x25 iterations + spectrum, "
+                                    "host wall time of one mr_windows_batch call"}
+    except Exception as e:  # a side metric never sinks the line
+        out["window_ms"] = {"error": f"{type(e).__name__}: {e}"}
     try:
         out["kind_compressed"] = kind_compressed_probe(ctx, dev0, t0, t1, a3, ok)
     except Exception as e:  # a side metric never sinks the line
