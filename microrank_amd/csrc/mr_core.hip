@@ -211,6 +211,7 @@ extern "C" void mr_ctx_destroy(mr_ctx* ctx) {
         if (e) (void)hipEventDestroy(e);
     if (ctx->side) (void)hipStreamDestroy(ctx->side);
     if (ctx->pin) (void)hipHostFree(ctx->pin);
+    if (ctx->scan_st) (void)hipFree(ctx->scan_st);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }

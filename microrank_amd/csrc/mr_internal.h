@@ -46,6 +46,10 @@ struct mr_ctx {
     // pinned host words for the small size read-backs of a call (a DMA straight into host memory
     // instead of the runtime's pageable staging path); created on first use
     int64_t* pin = nullptr;
+    // status words of the single-pass scans (mr_prim.hip k_scan_dl): per-call epochs, no clearing
+    unsigned long long* scan_st = nullptr;
+    size_t scan_cap = 0;
+    uint32_t scan_epoch = 0;
 };
 
 void* mr_pool_alloc(mr_ctx* ctx, size_t bytes);

@@ -121,6 +121,74 @@ __global__ void __launch_bounds__(SS_T) k_scan_single(const In* in, int64_t* out
     if (tid == 0) out[n] = carry;
 }
 
+// larger n: ONE launch, a tile of SCAN_TILE per block, tiles chained by decoupled look-back.  A
+// tile publishes its sum (flag 1), then -- once its exclusive prefix is known from the tiles
+// before it -- its inclusive prefix (flag 2); a block waits only on lower block indices, which
+// the dispatcher has already placed.  Status words [epoch:20 | flag:2 | value:42] live in a
+// per-context buffer; the epoch changes every call, so no clearing launch is needed (the buffer
+// is cleared once per 2^20 calls, when the epoch wraps).  Relaxed agent-scope atomics (sc1):
+// the word carries its value, no other data is published through it.
+constexpr int DL_EB = 20, DL_VB = 42;
+constexpr unsigned long long DL_VMASK = (1ull << DL_VB) - 1ull;
+__device__ __forceinline__ unsigned long long dl_word(uint64_t epoch, unsigned flag, int64_t v) {
+    return (epoch << (DL_VB + 2)) | ((unsigned long long)flag << DL_VB) | ((unsigned long long)v & DL_VMASK);
+}
+template <class In>
+__global__ void __launch_bounds__(SCAN_T) k_scan_dl(const In* in, int64_t* out, int64_t n, unsigned long long* st,
+                                                    uint64_t epoch) {
+    __shared__ int64_t tsum[SCAN_T];
+    __shared__ int64_t s_excl;
+    const int64_t tile = blockIdx.x;
+    const int64_t base = tile * SCAN_TILE + (int64_t)threadIdx.x * SCAN_I;
+    int64_t v[SCAN_I];
+    int64_t s = 0;
+#pragma unroll
+    for (int i = 0; i < SCAN_I; ++i) {
+        const int64_t j = base + i;
+        v[i] = j < n ? (int64_t)in[j] : 0;
+        s += v[i];
+    }
+    tsum[threadIdx.x] = s;
+    __syncthreads();
+    for (int off = 1; off < SCAN_T; off <<= 1) {
+        const int64_t a = threadIdx.x >= off ? tsum[threadIdx.x - off] : 0;
+        __syncthreads();
+        tsum[threadIdx.x] += a;
+        __syncthreads();
+    }
+    const int64_t agg = tsum[SCAN_T - 1];
+    if (threadIdx.x == 0) {
+        int64_t excl = 0;
+        if (tile == 0) {
+            __hip_atomic_store(&st[0], dl_word(epoch, 2, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            __hip_atomic_store(&st[tile], dl_word(epoch, 1, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (int64_t j = tile - 1; j >= 0;) {
+                const unsigned long long w = __hip_atomic_load(&st[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const unsigned flag = (unsigned)(w >> DL_VB) & 3u;
+                if ((w >> (DL_VB + 2)) != epoch || flag == 0) {
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;   // tile j has not published this call's value yet
+                }
+                excl += (int64_t)(w & DL_VMASK);
+                if (flag == 2) break;
+                --j;
+            }
+            __hip_atomic_store(&st[tile], dl_word(epoch, 2, excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        s_excl = excl;
+        if (tile == (int64_t)gridDim.x - 1) out[n] = excl + agg;
+    }
+    __syncthreads();
+    int64_t run = s_excl + (threadIdx.x ? tsum[threadIdx.x - 1] : 0);
+#pragma unroll
+    for (int i = 0; i < SCAN_I; ++i) {
+        const int64_t j = base + i;
+        if (j < n) out[j] = run;
+        run += v[i];
+    }
+}
+
 template <class In>
 int scan_impl(mr_ctx* ctx, const In* in, int64_t* out, int64_t n, int64_t* tmp) {
     if (n > 0 && n <= SCAN_SINGLE_MAX) {
@@ -131,6 +199,28 @@ int scan_impl(mr_ctx* ctx, const In* in, int64_t* out, int64_t n, int64_t* tmp) 
     int64_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
     if (nb == 0) {
         MR_TRY_HIP(ctx, hipMemsetAsync(out, 0, sizeof(int64_t), ctx->stream));
+        return MR_OK;
+    }
+    static const bool three_pass = getenv("MR_SCAN_3PASS") != nullptr;   // A/B knob
+    if (!three_pass) {
+        if ((size_t)nb > ctx->scan_cap) {   // grow the status words (stream-ordered: sync first)
+            MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));
+            if (ctx->scan_st) MR_TRY_HIP(ctx, hipFree(ctx->scan_st));
+            ctx->scan_st = nullptr;
+            const size_t cap = std::max<size_t>((size_t)nb, 4096);
+            MR_TRY_HIP(ctx, hipMalloc((void**)&ctx->scan_st, cap * sizeof(unsigned long long)));
+            MR_TRY_HIP(ctx, hipMemsetAsync(ctx->scan_st, 0, cap * sizeof(unsigned long long), ctx->stream));
+            ctx->scan_cap = cap;
+            ctx->scan_epoch = 0;
+        }
+        ctx->scan_epoch = (ctx->scan_epoch + 1) & ((1u << DL_EB) - 1u);
+        if (ctx->scan_epoch == 0) {   // wrapped: clear every word (epoch 0 marks a cleared word)
+            MR_TRY_HIP(ctx, hipMemsetAsync(ctx->scan_st, 0, ctx->scan_cap * sizeof(unsigned long long), ctx->stream));
+            ctx->scan_epoch = 1;
+        }
+        hipLaunchKernelGGL(k_scan_dl<In>, dim3((unsigned)nb), dim3(SCAN_T), 0, ctx->stream, in, out, n, ctx->scan_st,
+                           (uint64_t)ctx->scan_epoch);
+        MR_TRY_HIP(ctx, hipGetLastError());
         return MR_OK;
     }
     hipLaunchKernelGGL(k_scan_reduce<In>, dim3((unsigned)nb), dim3(SCAN_T), 0, ctx->stream, in, n, tmp);
