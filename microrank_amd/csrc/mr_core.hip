@@ -105,13 +105,20 @@ void mr_pool_free(mr_ctx* ctx, void* p) {
     ctx->pool_live.erase(it);
 }
 
+int mr_read_bytes(mr_ctx* ctx, const void* dev, size_t bytes, unsigned char** host) {
+    if (bytes > MR_PIN_BYTES) return mr_fail(ctx, MR_ERR_ARG, "mr_read_bytes: %zu bytes", bytes);
+    if (!ctx->pin) MR_TRY_HIP(ctx, hipHostMalloc((void**)&ctx->pin, MR_PIN_BYTES, hipHostMallocDefault));
+    if (bytes) MR_TRY_HIP(ctx, hipMemcpyAsync(ctx->pin, dev, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    *host = (unsigned char*)ctx->pin;
+    return MR_OK;
+}
 int mr_read_words(mr_ctx* ctx, const int64_t* dev, int n, int64_t* out) {
     if (n <= 0) return MR_OK;
     if (n > 64) return mr_fail(ctx, MR_ERR_ARG, "mr_read_words: %d words", n);
-    if (!ctx->pin) MR_TRY_HIP(ctx, hipHostMalloc((void**)&ctx->pin, 64 * sizeof(int64_t), hipHostMallocDefault));
-    MR_TRY_HIP(ctx, hipMemcpyAsync(ctx->pin, dev, (size_t)n * sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
-    MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    for (int i = 0; i < n; ++i) out[i] = ctx->pin[i];
+    unsigned char* h = nullptr;
+    MR_TRY(mr_read_bytes(ctx, dev, (size_t)n * sizeof(int64_t), &h));
+    memcpy(out, h, (size_t)n * sizeof(int64_t));
     return MR_OK;
 }
 

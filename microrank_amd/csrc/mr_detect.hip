@@ -319,6 +319,13 @@ static int win_spectrum(mr_ctx* ctx, const mr_spans* s, const WinRun& w, int met
     const int32_t NP = s->n_podops;
     const mr_graph *gn = w.gn, *ga = w.ga;
     const int32_t Na = ga->N, Nn = gn->N;
+    static const bool no_small = getenv("MR_NO_WIN_SPECTRUM_SMALL") != nullptr;   // A/B knob
+    if (!no_small) {   // one block, one read-back (k_win_spectrum) when the window fits it
+        const int rc = mr_win_spectrum_small(ctx, Na, ga->node_podop.p, ga->weight.p, ga->cov.p, Nn, gn->node_podop.p,
+                                             gn->weight.p, gn->cov.p, NP, w.nn, w.na, method,
+                                             std::max(0, top_max + 6), out_podop, out_score, n_out);
+        if (rc != MR_ERR_STATE) return rc;
+    }
     DBuf<int32_t> pos_of_code, only, uc, idx, zf;
     DBuf<int64_t> opos, tmp, ua_num, un_num;
     DBuf<uint8_t> fl;

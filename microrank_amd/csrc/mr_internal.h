@@ -57,6 +57,14 @@ void mr_pool_free(mr_ctx* ctx, void* p);
 void mr_pool_release(mr_ctx* ctx);
 // n (<= 64) int64 words from the device into out, through the context's pinned words; syncs the stream
 int mr_read_words(mr_ctx* ctx, const int64_t* dev, int n, int64_t* out);
+// up to MR_PIN_BYTES bytes from the device into the context's pinned buffer (*host points there,
+// valid until the next read-back on this context); syncs the stream
+constexpr size_t MR_PIN_BYTES = 8192;
+int mr_read_bytes(mr_ctx* ctx, const void* dev, size_t bytes, unsigned char** host);
+int mr_win_spectrum_small(mr_ctx* ctx, int32_t Na, const int32_t* a_podop, const double* a_w, const int32_t* a_cov,
+                          int32_t Nn, const int32_t* n_podop, const double* n_w, const int32_t* n_cov, int32_t NP,
+                          int64_t A, int64_t Nl, int method, int32_t k, int32_t* out_codes, double* out_score,
+                          int32_t* n_out);
 
 int mr_fail(mr_ctx* ctx, int code, const char* fmt, ...);
 

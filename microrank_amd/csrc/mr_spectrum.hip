@@ -11,6 +11,7 @@
 // its inputs, the kernel propagates them through the formula and flags a division by zero
 // between two Python-typed values.
 #include <algorithm>
+#include <cstring>
 
 #include "mr_prim.h"
 #include "mr_sort.h"
@@ -149,7 +150,133 @@ __global__ void k_gather_top(const uint32_t* idx, const double* score, const uin
     out_score[i] = score[j];
     if (out_np) out_np[i] = res_np[j];
 }
+// A window's whole spectrum step in ONE block (union sizes up to WS_MAX, pod-op codes up to
+// WS_PMAX): the union of the two graphs' nodes in the reference's order (anomaly_result nodes,
+// then normal-only nodes in normal_result order, online_rca.py:45-69), the scores (k_spectrum's
+// formula and typing), the stable descending sort and the top k -- instead of ~10 launches and
+// three host round trips.  out: [k] codes (int32, at 0), [k] scores (double, at 8 * WS_KMAX / 2)
+constexpr int WS_T = 1024, WS_MAX = 4096, WS_PMAX = 4096, WS_KMAX = 256;
+__global__ void __launch_bounds__(WS_T) k_win_spectrum(int32_t Na, const int32_t* a_podop, const double* a_w,
+                                                      const int32_t* a_cov, int32_t Nn, const int32_t* n_podop,
+                                                      const double* n_w, const int32_t* n_cov, int32_t NP, int64_t A,
+                                                      int64_t Nl, int method, int32_t k, unsigned char* out) {
+    __shared__ int32_t nidx[WS_PMAX], apos[WS_PMAX];
+    __shared__ uint64_t key[WS_MAX];
+    __shared__ uint32_t vix[WS_MAX];
+    __shared__ int32_t ucode[WS_MAX];
+    __shared__ double score[WS_MAX];
+    __shared__ int32_t sbuf[WS_T];
+    __shared__ int32_t nonly;
+    const int tid = threadIdx.x;
+    for (int c = tid; c < NP; c += WS_T) {
+        nidx[c] = -1;
+        apos[c] = -1;
+    }
+    __syncthreads();
+    for (int j = tid; j < Nn; j += WS_T) nidx[n_podop[j]] = j;
+    for (int i = tid; i < Na; i += WS_T) apos[a_podop[i]] = i;
+    __syncthreads();
+    // normal-only nodes in normal order: each thread a run of j, a block scan of the run counts
+    const int per = (Nn + WS_T - 1) / WS_T, j0 = tid * per, j1 = min(j0 + per, Nn);
+    int32_t cnt = 0;
+    for (int j = j0; j < j1; ++j) cnt += apos[n_podop[j]] < 0 ? 1 : 0;
+    sbuf[tid] = cnt;
+    __syncthreads();
+    for (int o = 1; o < WS_T; o <<= 1) {
+        const int32_t v = tid >= o ? sbuf[tid - o] : 0;
+        __syncthreads();
+        sbuf[tid] += v;
+        __syncthreads();
+    }
+    if (tid == WS_T - 1) nonly = sbuf[tid];
+    int32_t pos = Na + sbuf[tid] - cnt;
+    const TV eps{0.0000001, false};
+    for (int j = j0; j < j1; ++j) {   // normal-only entries (:60-69)
+        const int32_t c = n_podop[j];
+        if (apos[c] >= 0) continue;
+        const TV ep{(1.0 + n_w[j]) * (double)n_cov[j], true}, np_{(double)(Nl - n_cov[j]), false};
+        bool zd = false, rnp = false;
+        const double sc = spectrum_score(method, eps, eps, ep, np_, zd, rnp);
+        score[pos] = sc;
+        key[pos] = desc_key(sc);
+        vix[pos] = (uint32_t)pos;
+        ucode[pos] = c;
+        ++pos;
+    }
+    for (int i = tid; i < Na; i += WS_T) {   // anomaly_result entries (:45-58)
+        const int32_t c = a_podop[i], j = nidx[c];
+        const TV ef{a_w[i] * (double)a_cov[i], true}, nf{a_w[i] * (double)(A - a_cov[i]), true};
+        TV ep = eps, np_ = eps;
+        if (j >= 0) {
+            ep = TV{n_w[j] * (double)n_cov[j], true};
+            np_ = TV{n_w[j] * (double)(Nl - n_cov[j]), true};
+        }
+        bool zd = false, rnp = false;
+        const double sc = spectrum_score(method, ef, nf, ep, np_, zd, rnp);
+        score[i] = sc;
+        key[i] = desc_key(sc);
+        vix[i] = (uint32_t)i;
+        ucode[i] = c;
+    }
+    __syncthreads();
+    const int32_t n = Na + nonly;
+    int32_t m = 1;
+    while (m < n) m <<= 1;
+    for (int32_t i = n + tid; i < m; i += WS_T) {
+        key[i] = ~0ull;
+        vix[i] = 0xffffffffu;
+    }
+    __syncthreads();
+    for (int32_t size = 2; size <= m; size <<= 1)
+        for (int32_t stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int32_t i = tid; i < m; i += WS_T) {
+                const int32_t jj = i ^ stride;
+                if (jj > i) {
+                    const bool up = (i & size) == 0;
+                    const bool gt = key[i] > key[jj] || (key[i] == key[jj] && vix[i] > vix[jj]);
+                    if (gt == up) {
+                        const uint64_t tk = key[i];
+                        key[i] = key[jj];
+                        key[jj] = tk;
+                        const uint32_t tv = vix[i];
+                        vix[i] = vix[jj];
+                        vix[jj] = tv;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    const int32_t kk = min(k, n);
+    int32_t* oc = (int32_t*)out;
+    double* os = (double*)(out + 4 * WS_KMAX);
+    for (int32_t i = tid; i < kk; i += WS_T) {
+        oc[i] = ucode[vix[i]];
+        os[i] = score[vix[i]];
+    }
+    if (tid == 0) ((int32_t*)(out + 12 * WS_KMAX))[0] = kk;
+}
 }  // namespace
+
+// The window spectrum in one launch and one read-back (k_win_spectrum), or MR_ERR_STATE when the
+// sizes exceed its one-block limits (the caller then takes the general path).
+int mr_win_spectrum_small(mr_ctx* ctx, int32_t Na, const int32_t* a_podop, const double* a_w, const int32_t* a_cov,
+                          int32_t Nn, const int32_t* n_podop, const double* n_w, const int32_t* n_cov, int32_t NP,
+                          int64_t A, int64_t Nl, int method, int32_t k, int32_t* out_codes, double* out_score,
+                          int32_t* n_out) {
+    if (Na + Nn > WS_MAX || NP > WS_PMAX || k > WS_KMAX || k < 0) return MR_ERR_STATE;
+    DBuf<unsigned char> out;
+    MR_TRY(out.alloc(ctx, 12 * WS_KMAX + 16));
+    hipLaunchKernelGGL(k_win_spectrum, dim3(1), dim3(WS_T), 0, ctx->stream, Na, a_podop, a_w, a_cov, Nn, n_podop, n_w,
+                       n_cov, NP, A, Nl, method, k, out.p);
+    MR_TRY_HIP(ctx, hipGetLastError());
+    unsigned char* h = nullptr;
+    MR_TRY(mr_read_bytes(ctx, out.p, 12 * WS_KMAX + 16, &h));
+    const int32_t kk = ((const int32_t*)(h + 12 * WS_KMAX))[0];
+    if (out_codes) memcpy(out_codes, h, (size_t)kk * sizeof(int32_t));
+    if (out_score) memcpy(out_score, h + 4 * WS_KMAX, (size_t)kk * sizeof(double));
+    *n_out = kk;
+    return MR_OK;
+}
 
 // Device-side spectrum over n nodes whose inputs are already in HBM.  Writes the first `top`
 // sorted positions / scores to device buffers.
