@@ -13,8 +13,12 @@
 #include <utility>
 #include <vector>
 #include <climits>
+#include <cstring>
 #include <condition_variable>
 #include <deque>
+#include <map>
+#include <memory>
+#include <tuple>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -255,9 +259,12 @@ struct WinRun {
     int32_t na = 0, nn = 0;
     int64_t nin = 0;
     mr_graph *gn = nullptr, *ga = nullptr;   // "normal" graph (detector's abnormal traces), "anomaly" graph
+    hipEvent_t ev = nullptr;                 // batch: the window's graphs are ready on its stream
+    bool slot = false;                       // batch: its spectrum went to the device result slot
     ~WinRun() {
         delete gn;
         delete ga;
+        if (ev) (void)hipEventDestroy(ev);
     }
 };
 
@@ -309,6 +316,55 @@ static int win_detect_build(mr_ctx* ctx, const mr_spans* s, int64_t t0, int64_t 
         MR_TRY(mr_pagerank_presetup(ctx, w.ga, 1, 0.85, precision, 0));
     }
     MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+    return MR_OK;
+}
+
+// Batch form of win_detect_build for indexed spans with trace-level times: the detector, both
+// masks and both graph builds are enqueued first and their counters / sizes come back in ONE host
+// round trip; the graphs' prepare and PageRank set-up follow, and an event (w.ev) marks them
+// ready on this stream -- the caller's PageRank waits on it instead of on the host.
+static int win_detect_build_async(mr_ctx* ctx, const mr_spans* s, int64_t t0, int64_t t1, const double* d_a3,
+                                  const uint8_t* d_a3v, WinRun& w, int precision) {
+    hipStream_t st = ctx->stream;
+    const int32_t NT = s->n_traces;
+    constexpr size_t CW = 3 * MR_DETECT_SHARDS;   // detector counter shards, then 8 + 8 size words
+    DBuf<int64_t> wb;
+    DBuf<uint8_t> dst, m_abn, m_nor;
+    MR_TRY(wb.zero(ctx, CW + 16));
+    MR_TRY(dst.alloc(ctx, std::max(NT, 1)));
+    MR_TRY(m_abn.alloc(ctx, std::max(NT, 1)));
+    MR_TRY(m_nor.alloc(ctx, std::max(NT, 1)));
+    MR_TRY(mr_detect_indexed_launch(ctx, s, t0, t1, d_a3, d_a3v, dst.p, (unsigned long long*)wb.p));
+    if (NT) hipLaunchKernelGGL(k_masks, dim3(cdiv(NT, 256)), dim3(256), 0, st, dst.p, NT, m_abn.p, m_nor.p);
+    w.gn = new mr_graph();
+    w.gn->ctx = ctx;
+    w.ga = new mr_graph();
+    w.ga->ctx = ctx;
+    IxBuild bn, ba;
+    // (the graphs take EVERY row of the selected traces: get_pagerank_graph(list, data),
+    // online_rca.py:180,185 / preprocess_data.py:148)
+    MR_TRY(mr_ix_launch(ctx, s, m_abn.p, w.gn, bn, wb.p + CW));       // "normal" graph = detector's abnormal traces
+    MR_TRY(mr_ix_launch(ctx, s, m_nor.p, w.ga, ba, wb.p + CW + 8));
+    int64_t h[CW + 16];
+    {
+        unsigned char* hp = nullptr;
+        MR_TRY(mr_read_bytes(ctx, wb.p, (CW + 16) * sizeof(int64_t), &hp));
+        memcpy(h, hp, sizeof h);
+    }
+    mr_detect_sum((const unsigned long long*)h, &w.na, &w.nn, &w.nin);
+    if (w.nin == 0 || w.na == 0 || w.nn == 0) {   // empty window, or a list empty: nothing is ranked (T1)
+        delete w.gn;
+        delete w.ga;
+        w.gn = w.ga = nullptr;
+        if (w.nin == 0) return mr_fail(ctx, MR_ERR_VALUE, "Current span list is empty");
+        return MR_OK;
+    }
+    MR_TRY(mr_ix_finish(ctx, s, w.gn, bn, bn.small ? h + CW : nullptr));
+    MR_TRY(mr_ix_finish(ctx, s, w.ga, ba, ba.small ? h + CW + 8 : nullptr));
+    MR_TRY(mr_pagerank_presetup(ctx, w.gn, 0, 0.85, precision, 0));
+    MR_TRY(mr_pagerank_presetup(ctx, w.ga, 1, 0.85, precision, 0));
+    if (!w.ev) MR_TRY_HIP(ctx, hipEventCreateWithFlags(&w.ev, hipEventDisableTiming));
+    MR_TRY_HIP(ctx, hipEventRecord(w.ev, st));
     return MR_OK;
 }
 
@@ -439,7 +495,31 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
     const int gsz = std::min<int>(n_windows, group_size);
     const int ngroups = (n_windows + gsz - 1) / gsz;
     MR_TRY(win_aux(ctx, nthr));
+    // the SLO vectors once per distinct (a3, a3_valid, length) of the batch (windows usually share
+    // one pair), resident before any window's detector runs
+    std::map<std::tuple<const double*, const uint8_t*, int32_t>, size_t> slo_ix;
+    std::vector<std::unique_ptr<DBuf<double>>> d_a3;
+    std::vector<std::unique_ptr<DBuf<uint8_t>>> d_a3v;
+    std::vector<size_t> slo_of((size_t)n_windows);
+    for (int32_t i = 0; i < n_windows; ++i) {
+        const auto key = std::make_tuple(a3[i], a3_valid[i], spans[i]->n_svcops);
+        auto it = slo_ix.find(key);
+        if (it == slo_ix.end()) {
+            d_a3.emplace_back(new DBuf<double>());
+            d_a3v.emplace_back(new DBuf<uint8_t>());
+            MR_TRY(d_a3.back()->upload(ctx, a3[i], (size_t)std::max(spans[i]->n_svcops, 1)));
+            MR_TRY(d_a3v.back()->upload(ctx, a3_valid[i], (size_t)std::max(spans[i]->n_svcops, 1)));
+            it = slo_ix.emplace(key, d_a3.size() - 1).first;
+        }
+        slo_of[(size_t)i] = it->second;
+    }
+    // the windows' spectrum results land in device slots, read back once at the end
+    DBuf<unsigned char> slots;
+    MR_TRY(slots.alloc(ctx, (size_t)n_windows * MR_WS_SLOT));
+    MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));   // uploads done before other streams read them
+    static const bool no_index = getenv("MR_NO_INDEX") != nullptr;
     std::vector<WinRun> w((size_t)n_windows);
+    std::vector<hipEvent_t> gev((size_t)ngroups, nullptr);   // a group's PageRanks are done
     std::vector<std::string> err((size_t)nthr);
     // task queue: phase-1 tasks (window i -> i) first, phase-3 tasks (~i) appended per group
     std::mutex mu;
@@ -465,16 +545,28 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
                 if (task >= 0) {   // detect + both builds
                     const int32_t i = task;
                     WinRun& r = w[(size_t)i];
-                    r.rc = win_detect_build(a, spans[i], t0[i], t1[i], a3[i], a3_valid[i], r, nullptr, precision);
+                    const mr_spans* sp = spans[i];
+                    if (sp->indexed && sp->uniform_times && sp->has_times && !no_index)
+                        r.rc = win_detect_build_async(a, sp, t0[i], t1[i], d_a3[slo_of[(size_t)i]]->p,
+                                                      d_a3v[slo_of[(size_t)i]]->p, r, precision);
+                    else   // (synchronised at its end: no event needed)
+                        r.rc = win_detect_build(a, sp, t0[i], t1[i], a3[i], a3_valid[i], r, nullptr, precision);
                     if (r.rc != MR_OK && r.rc != MR_ERR_VALUE) err[(size_t)k] = a->err;
                     std::lock_guard<std::mutex> lk(mu);
                     ++built[(size_t)(i / gsz)];
                     cv_done.notify_all();
-                } else {           // spectrum
+                } else {           // spectrum, after the group's PageRanks (an event, not a host wait)
                     const int32_t i = ~task;
                     WinRun& r = w[(size_t)i];
-                    r.rc = win_spectrum(a, spans[i], r, method, top_max, out_podop ? out_podop + (size_t)i * K : nullptr,
-                                        out_score ? out_score + (size_t)i * K : nullptr, &n_out[i]);
+                    (void)hipStreamWaitEvent(a->stream, gev[(size_t)(i / gsz)], 0);
+                    r.rc = mr_win_spectrum_launch(a, r.ga->N, r.ga->node_podop.p, r.ga->weight.p, r.ga->cov.p, r.gn->N,
+                                                  r.gn->node_podop.p, r.gn->weight.p, r.gn->cov.p, spans[i]->n_podops,
+                                                  r.nn, r.na, method, K, slots.p + (size_t)i * MR_WS_SLOT);
+                    r.slot = r.rc == MR_OK;
+                    if (r.rc == MR_ERR_STATE)   // past the one-block limits: the general path (synchronous)
+                        r.rc = win_spectrum(a, spans[i], r, method, top_max,
+                                            out_podop ? out_podop + (size_t)i * K : nullptr,
+                                            out_score ? out_score + (size_t)i * K : nullptr, &n_out[i]);
                     if (r.rc != MR_OK) err[(size_t)k] = a->err;
                 }
             }
@@ -492,7 +584,8 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
             WinRun& r = w[(size_t)i];
             n_out[i] = 0;
             if (r.rc == MR_OK && r.gn) {
-                r.gn->ctx = r.ga->ctx = ctx;   // (built and synced on an auxiliary context)
+                if (r.ev) MR_TRY_HIP(ctx, hipStreamWaitEvent(ctx->stream, r.ev, 0));   // its graphs are ready
+                r.gn->ctx = r.ga->ctx = ctx;   // (built on an auxiliary context)
                 gs.push_back(r.gn);
                 gs.push_back(r.ga);
                 anom.push_back(0);
@@ -500,6 +593,10 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
             }
         }
         if (!gs.empty()) rc = mr_pagerank_batch(ctx, gs.data(), anom.data(), (int)gs.size(), 0.85, 0.01, 25, precision, 0);
+        if (rc == MR_OK) {
+            if (!gev[(size_t)g]) rc = hipEventCreateWithFlags(&gev[(size_t)g], hipEventDisableTiming) == hipSuccess ? MR_OK : MR_ERR_HIP;
+            if (rc == MR_OK) rc = hipEventRecord(gev[(size_t)g], ctx->stream) == hipSuccess ? MR_OK : MR_ERR_HIP;
+        }
         std::lock_guard<std::mutex> lk(mu);
         for (int32_t i = i0; i < i1; ++i)
             if (rc == MR_OK && w[(size_t)i].rc == MR_OK && w[(size_t)i].gn) q.push_back(~i);
@@ -511,9 +608,20 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
         cv_task.notify_all();
     }
     for (auto& t : th) t.join();
+    for (int k = 0; k < nthr; ++k) (void)hipStreamSynchronize(ctx->aux[(size_t)k]->stream);
+    for (hipEvent_t e : gev)
+        if (e) (void)hipEventDestroy(e);
     MR_TRY(rc);
     for (auto& e : err)
         if (!e.empty()) return mr_fail(ctx, MR_ERR_HIP, "mr_windows_batch: %s", e.c_str());
+    {   // every device-slot spectrum in one read-back
+        std::vector<unsigned char> hs((size_t)n_windows * MR_WS_SLOT);
+        MR_TRY_HIP(ctx, hipMemcpy(hs.data(), slots.p, hs.size(), hipMemcpyDeviceToHost));
+        for (int32_t i = 0; i < n_windows; ++i)
+            if (w[(size_t)i].slot)
+                mr_win_spectrum_unpack(hs.data() + (size_t)i * MR_WS_SLOT, out_podop ? out_podop + (size_t)i * K : nullptr,
+                                       out_score ? out_score + (size_t)i * K : nullptr, &n_out[i]);
+    }
     for (int32_t i = 0; i < n_windows; ++i) {
         const WinRun& r = w[(size_t)i];
         status[i] = r.rc;

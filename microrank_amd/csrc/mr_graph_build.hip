@@ -412,28 +412,75 @@ constexpr int IX_EPT = 16;  // index entries per thread in k_ix_stats (fewer blo
 constexpr int IX_BT = 1024;
 constexpr int IX_HIST = 12288;   // three per-code counters (span count, first row, traces)
 constexpr int IX_B = 8;     // entries per thread whose loads are batched
-// one launch for the indexed build's four initialisations (was four memsets: each a separate
-// ~3 us fill launch, twice per window): per-op counts / first rows, edge keys (EMPTY) / counts
-__global__ void k_ix_init(int32_t* ocnt, int32_t* ofirst, int32_t* ocov, int32_t NP, uint64_t* gk, uint32_t* gc,
-                          int64_t ecap) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < NP) {
-        ocnt[i] = 0;
-        ocov[i] = 0;
-        ofirst[i] = 0x7f7f7f7f;   // the old memset's byte pattern: larger than any row
+// The indexed build's first launch: the trace selection with BOTH exclusive scans -- tpos over
+// the selection flags, zoff over the selected traces' op-list lengths -- chained across tiles by
+// decoupled look-back (two status chains), plus the clearing of the per-code counters and the
+// edge hash (a grid-stride share per block): one launch where there were four.
+constexpr int SEL_T = 256, SEL_I = 8, SEL_TILE = SEL_T * SEL_I;
+__global__ void __launch_bounds__(SEL_T) k_ix_sel_scan(const uint8_t* mask, const int32_t* tlen, const int64_t* po_off,
+                                                      int32_t NT, int32_t* tflag, int64_t* tpos, int64_t* zoff,
+                                                      unsigned long long* st, uint64_t epoch, int32_t* ocnt,
+                                                      int32_t* ofirst, int32_t* ocov, int32_t NP, uint64_t* gk,
+                                                      uint32_t* gc, int64_t ecap) {
+    __shared__ int64_t sa[SEL_T], sb[SEL_T];
+    __shared__ int64_t ex[2];
+    const int tid = threadIdx.x;
+    const int64_t gsz = (int64_t)gridDim.x * SEL_T, gi = (int64_t)blockIdx.x * SEL_T + tid;
+    for (int64_t i = gi; i < max((int64_t)NP, ecap); i += gsz) {
+        if (i < NP) {
+            ocnt[i] = 0;
+            ofirst[i] = 0x7f7f7f7f;   // larger than any row
+            ocov[i] = 0;
+        }
+        if (i < ecap) {
+            gk[i] = ~0ull;
+            gc[i] = 0u;
+        }
     }
-    if (i < ecap) {
-        gk[i] = ~0ull;
-        gc[i] = 0u;
+    const int64_t tile = blockIdx.x, base = tile * SEL_TILE + (int64_t)tid * SEL_I;
+    int32_t f[SEL_I];
+    int64_t z[SEL_I], a = 0, b = 0;
+#pragma unroll
+    for (int i = 0; i < SEL_I; ++i) {
+        const int64_t t = base + i;
+        const bool on = t < NT && mask[t] && tlen[t] > 0;
+        f[i] = on ? 1 : 0;
+        z[i] = on ? po_off[t + 1] - po_off[t] : 0;
+        if (t < NT) tflag[t] = f[i];
+        a += f[i];
+        b += z[i];
     }
-}
-__global__ void k_ix_sel(const uint8_t* mask, const int32_t* tlen, const int64_t* po_off, int32_t NT, int32_t* tflag,
-                         int32_t* zc) {
-    const int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= NT) return;
-    const bool on = mask[t] && tlen[t] > 0;
-    tflag[t] = on ? 1 : 0;
-    zc[t] = on ? (int32_t)(po_off[t + 1] - po_off[t]) : 0;
+    sa[tid] = a;
+    sb[tid] = b;
+    __syncthreads();
+    for (int o = 1; o < SEL_T; o <<= 1) {
+        const int64_t x = tid >= o ? sa[tid - o] : 0, y = tid >= o ? sb[tid - o] : 0;
+        __syncthreads();
+        sa[tid] += x;
+        sb[tid] += y;
+        __syncthreads();
+    }
+    if (tid == 0) {
+        const int64_t aggA = sa[SEL_T - 1], aggB = sb[SEL_T - 1];
+        ex[0] = dl_lookback(st, tile, aggA, epoch);
+        ex[1] = dl_lookback(st + gridDim.x, tile, aggB, epoch);
+        if (tile == (int64_t)gridDim.x - 1) {
+            tpos[NT] = ex[0] + aggA;
+            zoff[NT] = ex[1] + aggB;
+        }
+    }
+    __syncthreads();
+    int64_t ra = ex[0] + sa[tid] - a, rb = ex[1] + sb[tid] - b;
+#pragma unroll
+    for (int i = 0; i < SEL_I; ++i) {
+        const int64_t t = base + i;
+        if (t < NT) {
+            tpos[t] = ra;
+            zoff[t] = rb;
+        }
+        ra += f[i];
+        rb += z[i];
+    }
 }
 // entry-parallel over the index: span counts and first rows per pod-op of the selected traces
 // (LDS-aggregated per block), and their join keys with multiplicity into the block's LDS edge
@@ -539,23 +586,23 @@ __global__ void k_ix_cross(const uint8_t* mask, const int32_t* tc, const int32_t
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n && mask[tc[i]] && mask[tp[i]]) global_edge_add(key[i], 1u, gk, gc, gmask);
 }
-__global__ void k_ix_trace_rows(const int32_t* tflag, const int64_t* tpos, const int64_t* zoff, int32_t NT,
-                                const int32_t* tlen, int32_t* trace_code, int32_t* len_t, int64_t* rs_off) {
-    const int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= NT || !tflag[t]) return;
-    const int32_t p = (int32_t)tpos[t];
-    trace_code[p] = t;
-    len_t[p] = tlen[t];
-    rs_off[p] = zoff[t];
-}
-// the selected traces' op lists (entry-parallel): rs_ops[zoff[t] + k] = node of the k-th pod-op
-__global__ void k_ix_trace_ops(const int32_t* tflag, const int64_t* zoff, int64_t n_po, const int32_t* po_tr,
-                               const int64_t* po_off, const int32_t* po_op, const int32_t* node_of_code, int32_t* rs_ops) {
-    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= n_po) return;
-    const int32_t t = po_tr[r];
-    if (!tflag[t]) return;
-    rs_ops[zoff[t] + (r - po_off[t])] = node_of_code[po_op[r]];
+// the selected traces' rows (trace_code, len_t, CSR offsets) and, entry-parallel, their op lists
+// rs_ops[zoff[t] + k] = node of the k-th pod-op: one launch over max(NT, n_po)
+__global__ void k_ix_traces(const int32_t* tflag, const int64_t* tpos, const int64_t* zoff, int32_t NT,
+                            const int32_t* tlen, int32_t* trace_code, int32_t* len_t, int64_t* rs_off, int64_t n_po,
+                            const int32_t* po_tr, const int64_t* po_off, const int32_t* po_op,
+                            const int32_t* node_of_code, int32_t* rs_ops) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < NT && tflag[i]) {
+        const int32_t p = (int32_t)tpos[i];
+        trace_code[p] = (int32_t)i;
+        len_t[p] = tlen[i];
+        rs_off[p] = zoff[i];
+    }
+    if (i < n_po) {
+        const int32_t t = po_tr[i];
+        if (tflag[t]) rs_ops[zoff[t] + (i - po_off[t])] = node_of_code[po_op[i]];
+    }
 }
 // ---------------------------------------------------------------- sharded build: the join across ranks
 // A child row's parent rows may lie in traces of another rank (T11).  Each rank publishes a
@@ -991,35 +1038,36 @@ static int cross_exchange(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d_mask
     return MR_OK;
 }
 
-static int graph_build_indexed(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d_mask, mr_graph* g,
-                               bool sharded = false) {
+// Split in two so a caller can read the sizes of several builds (and other counters) in ONE host
+// round trip: mr_ix_launch enqueues everything up to the one-block node order (sizes to d_out:
+// N, E, overflow, T, nnz), mr_ix_finish takes them (h, or null: read here) and completes the
+// graph -- on overflow / sharded graphs through the general node order.
+static int ix_launch(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d_mask, mr_graph* g, IxBuild& b, int64_t* d_out,
+                     bool sharded) {
     hipStream_t st = ctx->stream;
-    PhaseTimer pt(st, "build");
     const int32_t NT = sp->n_traces, NP = sp->n_podops;
     CrossJoin X;
     if (sharded && ctx->nranks > 1) MR_TRY(cross_exchange(ctx, sp, d_mask, X));   // (one rank: all joins local)
-    DBuf<int32_t> tflag, zc;
-    DBuf<int64_t> tpos, zoff, tmp;
-    MR_TRY(tflag.alloc(ctx, NT));
-    MR_TRY(zc.alloc(ctx, NT));
-    MR_TRY(tpos.alloc(ctx, NT + 1));
-    MR_TRY(zoff.alloc(ctx, NT + 1));
-    MR_TRY(tmp.alloc(ctx, std::max<int64_t>({scan_tmp_elems(NT), scan_tmp_elems(NP), 1})));
-    DBuf<int32_t> ocnt, ofirst, ocov;
-    MR_TRY(ocnt.alloc(ctx, NP));
-    MR_TRY(ofirst.alloc(ctx, NP));
-    MR_TRY(ocov.alloc(ctx, NP));
-    const uint64_t ecap = edge_capacity(sp->n_edge_keys + X.matches, NP);
-    DBuf<uint64_t> gk;
-    DBuf<uint32_t> gc;
-    MR_TRY(gk.alloc(ctx, ecap));
-    MR_TRY(gc.alloc(ctx, ecap));
-    if (NP || ecap)
-        hipLaunchKernelGGL(k_ix_init, dim3(cdiv(std::max<int64_t>(NP, (int64_t)ecap), 256)), dim3(256), 0, st, ocnt.p,
-                           ofirst.p, ocov.p, NP, gk.p, gc.p, (int64_t)ecap);
+    MR_TRY(b.tflag.alloc(ctx, NT));
+    MR_TRY(b.tpos.alloc(ctx, NT + 1));
+    MR_TRY(b.zoff.alloc(ctx, NT + 1));
+    MR_TRY(b.ocnt.alloc(ctx, NP));
+    MR_TRY(b.ofirst.alloc(ctx, NP));
+    MR_TRY(b.ocov.alloc(ctx, NP));
+    b.ecap = edge_capacity(sp->n_edge_keys + X.matches, NP);
+    const uint64_t ecap = b.ecap;
+    MR_TRY(b.gk.alloc(ctx, ecap));
+    MR_TRY(b.gc.alloc(ctx, ecap));
+    {   // selection + both trace scans + clearing, one launch
+        const int64_t nt = std::max<int64_t>(cdiv((int64_t)NT, SEL_TILE), 1);
+        unsigned long long* dst = nullptr;
+        uint64_t epoch = 0;
+        MR_TRY(mr_dl_status(ctx, 2 * nt, &dst, &epoch));
+        hipLaunchKernelGGL(k_ix_sel_scan, dim3((unsigned)nt), dim3(SEL_T), 0, st, d_mask, sp->tlen.p, sp->po_off.p, NT,
+                           b.tflag.p, b.tpos.p, b.zoff.p, dst, epoch, b.ocnt.p, b.ofirst.p, b.ocov.p, NP, b.gk.p,
+                           b.gc.p, (int64_t)ecap);
+    }
     if (NT) {
-        hipLaunchKernelGGL(k_ix_sel, dim3(cdiv(NT, 256)), dim3(256), 0, st, d_mask, sp->tlen.p, sp->po_off.p, NT, tflag.p,
-                           zc.p);
         const int use_lds = NP <= IX_HIST;
         const size_t lds = use_lds ? 3 * (size_t)NP * sizeof(int32_t) : 0;
         // block cap 256 (one per CU); MR_IX_BLOCKS overrides it for measurements
@@ -1028,29 +1076,23 @@ static int graph_build_indexed(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d
             return e ? std::max(1, atoi(e)) : 256;
         }();
         const int nblk = std::max(1, std::min(ix_cap, cdiv(std::max(sp->n_po, sp->n_ed), IX_BT * IX_EPT)));
-        hipLaunchKernelGGL(k_ix_stats, dim3(nblk), dim3(IX_BT), lds, st, tflag.p, sp->n_po, sp->po_tr.p, sp->po_op.p,
+        hipLaunchKernelGGL(k_ix_stats, dim3(nblk), dim3(IX_BT), lds, st, b.tflag.p, sp->n_po, sp->po_tr.p, sp->po_op.p,
                            sp->po_cnt.p, sp->po_first.p, sp->n_ed, sp->ed_tr.p, sp->ed_key.p, sp->ed_cnt.p, NP, use_lds,
-                           ocnt.p, ofirst.p, ocov.p, gk.p, gc.p, ecap - 1);
+                           b.ocnt.p, b.ofirst.p, b.ocov.p, b.gk.p, b.gc.p, ecap - 1);
     }
     if (sp->n_xj)
         hipLaunchKernelGGL(k_ix_cross, dim3(cdiv(sp->n_xj, 256)), dim3(256), 0, st, d_mask, sp->xj_tc.p, sp->xj_tp.p,
-                           sp->xj_key.p, sp->n_xj, gk.p, gc.p, ecap - 1);
+                           sp->xj_key.p, sp->n_xj, b.gk.p, b.gc.p, ecap - 1);
     if (X.matches && sp->S)   // cross-rank parent joins, counted at the child's rank
         hipLaunchKernelGGL(k_cross_join<true>, dim3(cdiv(sp->S, 256)), dim3(256), 0, st, sp->trace.p, sp->parent.p,
                            sp->podop.p, sp->S, d_mask, X.key.p, X.val.p, X.rec.p, X.n, ctx->rank,
-                           (unsigned long long*)nullptr, gk.p, gc.p, ecap - 1);
-    pt.mark("stats");
-    MR_TRY(mr_exclusive_scan_i32(ctx, tflag.p, tpos.p, NT, tmp.p));
-    MR_TRY(mr_exclusive_scan_i32(ctx, zc.p, zoff.p, NT, tmp.p));
-    pt.mark("scans");
-    DBuf<int32_t> node_of_code;
+                           (unsigned long long*)nullptr, b.gk.p, b.gc.p, ecap - 1);
     static const bool no_small = getenv("MR_NO_NODES_SMALL") != nullptr;   // A/B knob
-    if (!sharded && !no_small && NP <= NS_PMAX) {
+    b.small = !sharded && !no_small && NP <= NS_PMAX;
+    if (b.small) {
         // one launch for the node order and P_ss, the trace rows / op lists into upper-bound
-        // buffers right behind it, and ONE host round trip for (N, E, T, nnz)
-        DBuf<int64_t> dout;
-        MR_TRY(dout.alloc(ctx, 8));
-        MR_TRY(node_of_code.alloc(ctx, std::max(NP, 1)));
+        // buffers right behind it; the sizes (N, E, T, nnz) go to d_out
+        MR_TRY(b.node_of_code.alloc(ctx, std::max(NP, 1)));
         MR_TRY(g->node_podop.alloc(ctx, std::max(NP, 1)));
         MR_TRY(g->len_o.alloc(ctx, std::max(NP, 1)));
         MR_TRY(g->nchild.alloc(ctx, std::max(NP, 1)));
@@ -1061,53 +1103,80 @@ static int graph_build_indexed(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d
         MR_TRY(g->len_t.alloc(ctx, std::max(NT, 1)));
         MR_TRY(g->rs_ops.alloc(ctx, (size_t)std::max<int64_t>(sp->n_po, 1)));
         MR_TRY(g->rs_off.alloc(ctx, (size_t)NT + 1));
-        hipLaunchKernelGGL(k_nodes_small, dim3(1), dim3(NS_T), 0, st, gk.p, gc.p, (int64_t)ecap, ocnt.p, ofirst.p, NP,
-                           node_of_code.p, g->node_podop.p, g->len_o.p, g->nchild.p, ocov.p, g->cov.p, g->ss_par.p,
-                           g->ss_off.p,
-                           tpos.p + NT, zoff.p + NT, g->rs_off.p, dout.p);
-        if (NT)
-            hipLaunchKernelGGL(k_ix_trace_rows, dim3(cdiv(NT, 256)), dim3(256), 0, st, tflag.p, tpos.p, zoff.p, NT,
-                               sp->tlen.p, g->trace_code.p, g->len_t.p, g->rs_off.p);
-        if (sp->n_po)
-            hipLaunchKernelGGL(k_ix_trace_ops, dim3(cdiv(sp->n_po, 256)), dim3(256), 0, st, tflag.p, zoff.p, sp->n_po,
-                               sp->po_tr.p, sp->po_off.p, sp->po_op.p, node_of_code.p, g->rs_ops.p);
-        int64_t h[5] = {0, 0, 0, 0, 0};   // N, E, overflow, T, nnz
-        MR_TRY(mr_read_words(ctx, dout.p, 5, h));
-        pt.mark("nodes+traces");
-        if (!h[2]) {
-            g->N = (int32_t)h[0];
-            g->E = h[1];
-            g->T = (int32_t)h[3];
-            g->nnz_sr = g->nnz_rs = h[4];
-            g->cov_ready = true;
-            MR_TRY_HIP(ctx, hipGetLastError());
-            return MR_OK;
-        }
-        // more call edges than the one-block path holds: the general node order below
+        hipLaunchKernelGGL(k_nodes_small, dim3(1), dim3(NS_T), 0, st, b.gk.p, b.gc.p, (int64_t)ecap, b.ocnt.p,
+                           b.ofirst.p, NP, b.node_of_code.p, g->node_podop.p, g->len_o.p, g->nchild.p, b.ocov.p,
+                           g->cov.p, g->ss_par.p, g->ss_off.p, b.tpos.p + NT, b.zoff.p + NT, g->rs_off.p, d_out);
+        if (NT || sp->n_po)
+            hipLaunchKernelGGL(k_ix_traces, dim3(cdiv(std::max<int64_t>(NT, sp->n_po), 256)), dim3(256), 0, st,
+                               b.tflag.p, b.tpos.p, b.zoff.p, NT, sp->tlen.p, g->trace_code.p, g->len_t.p, g->rs_off.p,
+                               sp->n_po, sp->po_tr.p, sp->po_off.p, sp->po_op.p, b.node_of_code.p, g->rs_ops.p);
     }
-    MR_TRY(build_nodes(ctx, g, NP, ocnt.p, ofirst.p, ocov.p, sp->row_bits, gk.p, gc.p, ecap, node_of_code, &pt, sharded));
-    pt.mark("nodes");
-    int64_t h[2] = {0, 0};   // T, nnz (their scans ran before build_nodes' syncs)
-    MR_TRY_HIP(ctx, hipMemcpyAsync(&h[0], tpos.p + NT, sizeof(int64_t), hipMemcpyDeviceToHost, st));
-    MR_TRY_HIP(ctx, hipMemcpyAsync(&h[1], zoff.p + NT, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    MR_TRY_HIP(ctx, hipGetLastError());
+    return MR_OK;
+}
+
+static int ix_finish(mr_ctx* ctx, const mr_spans* sp, mr_graph* g, IxBuild& b, const int64_t* h, bool sharded) {
+    hipStream_t st = ctx->stream;
+    const int32_t NT = sp->n_traces, NP = sp->n_podops;
+    if (b.small && h && !h[2]) {
+        g->N = (int32_t)h[0];
+        g->E = h[1];
+        g->T = (int32_t)h[3];
+        g->nnz_sr = g->nnz_rs = h[4];
+        g->cov_ready = true;
+        return MR_OK;
+    }
+    // the general node order (sharded graphs; more call edges than the one-block path holds)
+    MR_TRY(build_nodes(ctx, g, NP, b.ocnt.p, b.ofirst.p, b.ocov.p, sp->row_bits, b.gk.p, b.gc.p, b.ecap, b.node_of_code,
+                       nullptr, sharded));
+    int64_t hh[2] = {0, 0};   // T, nnz (their scans ran before build_nodes' syncs)
+    MR_TRY_HIP(ctx, hipMemcpyAsync(&hh[0], b.tpos.p + NT, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    MR_TRY_HIP(ctx, hipMemcpyAsync(&hh[1], b.zoff.p + NT, sizeof(int64_t), hipMemcpyDeviceToHost, st));
     MR_TRY_HIP(ctx, hipStreamSynchronize(st));
-    const int32_t T = (int32_t)h[0];
-    const int64_t nnz = h[1];
+    const int32_t T = (int32_t)hh[0];
+    const int64_t nnz = hh[1];
     MR_TRY(g->trace_code.alloc(ctx, T));
     MR_TRY(g->len_t.alloc(ctx, T));
     MR_TRY(g->rs_ops.alloc(ctx, nnz));
     MR_TRY(g->rs_off.alloc(ctx, T + 1));
-    if (NT)
-        hipLaunchKernelGGL(k_ix_trace_rows, dim3(cdiv(NT, 256)), dim3(256), 0, st, tflag.p, tpos.p, zoff.p, NT, sp->tlen.p,
-                           g->trace_code.p, g->len_t.p, g->rs_off.p);
-    if (sp->n_po)
-        hipLaunchKernelGGL(k_ix_trace_ops, dim3(cdiv(sp->n_po, 256)), dim3(256), 0, st, tflag.p, zoff.p, sp->n_po,
-                           sp->po_tr.p, sp->po_off.p, sp->po_op.p, node_of_code.p, g->rs_ops.p);
+    if (NT || sp->n_po)
+        hipLaunchKernelGGL(k_ix_traces, dim3(cdiv(std::max<int64_t>(NT, sp->n_po), 256)), dim3(256), 0, st, b.tflag.p,
+                           b.tpos.p, b.zoff.p, NT, sp->tlen.p, g->trace_code.p, g->len_t.p, g->rs_off.p, sp->n_po,
+                           sp->po_tr.p, sp->po_off.p, sp->po_op.p, b.node_of_code.p, g->rs_ops.p);
     hipLaunchKernelGGL(k_set_last, dim3(1), dim3(1), 0, st, g->rs_off.p, T, nnz);
     MR_TRY_HIP(ctx, hipGetLastError());
     g->T = T;
     g->nnz_sr = g->nnz_rs = nnz;
-    pt.mark("traces");
+    return MR_OK;
+}
+
+static int graph_build_indexed(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d_mask, mr_graph* g,
+                               bool sharded = false) {
+    IxBuild b;
+    DBuf<int64_t> dout;
+    MR_TRY(dout.alloc(ctx, 8));
+    MR_TRY(ix_launch(ctx, sp, d_mask, g, b, dout.p, sharded));
+    int64_t h[5] = {0, 0, 0, 0, 0};   // N, E, overflow, T, nnz
+    if (b.small) MR_TRY(mr_read_words(ctx, dout.p, 5, h));
+    return ix_finish(ctx, sp, g, b, b.small ? h : nullptr, sharded);
+}
+
+int mr_ix_launch(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d_mask, mr_graph* g, IxBuild& b, int64_t* d_out) {
+    return ix_launch(ctx, sp, d_mask, g, b, d_out, false);
+}
+int mr_ix_finish(mr_ctx* ctx, const mr_spans* sp, mr_graph* g, IxBuild& b, const int64_t* h) {
+    MR_TRY(ix_finish(ctx, sp, g, b, h, false));
+    return mr_graph_post_build(ctx, g);
+}
+
+// a built graph's trace-role fields and derived arrays (the K1 result is P_rs = P_sr)
+int mr_graph_post_build(mr_ctx* ctx, mr_graph* g) {
+    g->rs_is_sr = true;
+    g->pr_identity = true;
+    g->n_pr = g->T;
+    PhaseTimer pt(ctx->stream, "prepare");
+    MR_TRY(mr_graph_prepare(ctx, g));
+    pt.mark("done");
     return MR_OK;
 }
 
@@ -1119,14 +1188,7 @@ int mr_graph_build_dev(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d_mask, m
     static const bool no_index = getenv("MR_NO_INDEX") != nullptr;   // A/B knob: force the row-level path
     const bool indexed = sp->indexed && !no_index && (!win || sp->uniform_times);
     int rc = indexed ? graph_build_indexed(ctx, sp, d_mask, g) : graph_build_rows(ctx, sp, d_mask, win, g);
-    if (rc == MR_OK) {
-        g->rs_is_sr = true;
-        g->pr_identity = true;
-        g->n_pr = g->T;
-        PhaseTimer pt(ctx->stream, "prepare");
-        rc = mr_graph_prepare(ctx, g);
-        pt.mark("done");
-    }
+    if (rc == MR_OK) rc = mr_graph_post_build(ctx, g);
     if (rc != MR_OK) {
         delete g;
         return rc;

@@ -316,4 +316,29 @@ struct PhaseTimer {
 inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 
 int mr_graph_prepare(mr_ctx* ctx, mr_graph* g);   // derived arrays + segments after structure upload
+int mr_graph_post_build(mr_ctx* ctx, mr_graph* g);   // trace-role fields + mr_graph_prepare after K1
+// An indexed K1 build between its launches and its size read-back (mr_graph_build.hip): several
+// builds (and the detector's counters) share one host round trip.  d_out receives 5 int64 words
+// (N, E, overflow, T, nnz); mr_ix_finish takes them (null when b.small is false) and prepares g.
+struct IxBuild {
+    DBuf<int32_t> tflag, ocnt, ofirst, ocov, node_of_code;
+    DBuf<int64_t> tpos, zoff;
+    DBuf<uint64_t> gk;
+    DBuf<uint32_t> gc;
+    uint64_t ecap = 0;
+    bool small = false;   // the one-block node order ran: its sizes are in d_out
+};
+int mr_ix_launch(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d_mask, mr_graph* g, IxBuild& b, int64_t* d_out);
+constexpr int MR_DETECT_SHARDS = 64;
+int mr_detect_indexed_launch(mr_ctx* ctx, const mr_spans* s, int64_t t0, int64_t t1, const double* d_a3,
+                             const uint8_t* d_a3v, uint8_t* d_state, unsigned long long* counts);
+void mr_detect_sum(const unsigned long long* sh, int32_t* n_abn, int32_t* n_nor, int64_t* n_in);
+// the window spectrum kernel alone, into a device slot of MR_WS_SLOT bytes (codes, scores, count);
+// MR_ERR_STATE when the window exceeds the one-block limits
+constexpr size_t MR_WS_SLOT = 12 * 256 + 16;
+int mr_win_spectrum_launch(mr_ctx* ctx, int32_t Na, const int32_t* a_podop, const double* a_w, const int32_t* a_cov,
+                           int32_t Nn, const int32_t* n_podop, const double* n_w, const int32_t* n_cov, int32_t NP,
+                           int64_t A, int64_t Nl, int method, int32_t k, unsigned char* d_slot);
+void mr_win_spectrum_unpack(const unsigned char* slot, int32_t* out_codes, double* out_score, int32_t* n_out);
+int mr_ix_finish(mr_ctx* ctx, const mr_spans* sp, mr_graph* g, IxBuild& b, const int64_t* h);
 int mr_pagerank_presetup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, int precision, uint32_t flags);

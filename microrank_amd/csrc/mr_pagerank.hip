@@ -66,9 +66,12 @@ __global__ void k_op_consts(const int32_t* len_o, const int32_t* nchild, float* 
 }
 // per-graph constants in one launch: w_t = fp32(1/len_t) (fp64 1/n -> fp32), u_o, pw, and the
 // u16 copy of the op ids (N <= 65536)
+// (and clears `nz` words of the layout's scratch: tr_layout's histogram and slot counters)
 __global__ void k_graph_consts(const int32_t* len_t, float* w_t, int32_t T, const int32_t* len_o, const int32_t* nchild,
-                               float* u_o, float* pw, int32_t N, const int32_t* ops, int64_t n, uint16_t* o16) {
+                               float* u_o, float* pw, int32_t N, const int32_t* ops, int64_t n, uint16_t* o16,
+                               int32_t* zero, int32_t nz) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < nz) zero[i] = 0;
     if (i < T) w_t[i] = len_t[i] > 0 ? (float)(1.0 / (double)len_t[i]) : 0.0f;
     if (i < N) {
         u_o[i] = len_o[i] > 0 ? (float)(1.0 / (double)len_o[i]) : 0.0f;
@@ -315,9 +318,13 @@ __global__ void __launch_bounds__(TRB) k_tr_hist(const int64_t* off, int32_t T, 
         if (lh[i]) atomicAdd(&hist[i], lh[i]);
 }
 // positions: bin start (cursor, claimed per block and bin) + the trace's rank in its block's bin
-// (a bin's remaining count hands out its slots from the end: hist is consumed, no cursor copy)
+// A bin's slots: boff given -- its start plus the bin's remaining count, handed out from the end
+// (hist is consumed, no cursor copy); boff null (nbin <= TP_LSCAN) -- each block scans the
+// histogram in LDS itself and claims slots through `taken` (no scan launch)
+constexpr int TP_LSCAN = 8192;
 __global__ void __launch_bounds__(TRB) k_tr_place(const int64_t* off, int32_t T, int32_t nbin, const int64_t* boff,
-                                                  int32_t* hist, const float* w_t, int32_t* tperm, float* w_tp) {
+                                                  int32_t* hist, int32_t* taken, const float* w_t, int32_t* tperm,
+                                                  float* w_tp) {
     extern __shared__ int32_t lh[];
     int32_t* lbase = lh + nbin;
     for (int32_t i = threadIdx.x; i < nbin; i += TRB) lh[i] = 0;
@@ -331,8 +338,29 @@ __global__ void __launch_bounds__(TRB) k_tr_place(const int64_t* off, int32_t T,
         rk[j] = ln[j] >= 0 ? atomicAdd(&lh[ln[j]], 1) : 0;
     }
     __syncthreads();
-    for (int32_t i = threadIdx.x; i < nbin; i += TRB)
-        if (lh[i]) lbase[i] = (int32_t)boff[i] + atomicSub(&hist[i], lh[i]) - lh[i];
+    if (boff) {
+        for (int32_t i = threadIdx.x; i < nbin; i += TRB)
+            if (lh[i]) lbase[i] = (int32_t)boff[i] + atomicSub(&hist[i], lh[i]) - lh[i];
+    } else {
+        __shared__ int32_t sbuf[TRB];
+        const int32_t per = (nbin + TRB - 1) / TRB, b0 = threadIdx.x * per, b1 = min(b0 + per, nbin);
+        int32_t run = 0;
+        for (int32_t i = b0; i < b1; ++i) run += hist[i];
+        sbuf[threadIdx.x] = run;
+        __syncthreads();
+        for (int o = 1; o < TRB; o <<= 1) {
+            const int32_t v = threadIdx.x >= o ? sbuf[threadIdx.x - o] : 0;
+            __syncthreads();
+            sbuf[threadIdx.x] += v;
+            __syncthreads();
+        }
+        run = sbuf[threadIdx.x] - run;   // exclusive start of this thread's bins
+        for (int32_t i = b0; i < b1; ++i) {
+            const int32_t c = hist[i];
+            lbase[i] = run + (lh[i] ? atomicAdd(&taken[i], lh[i]) : 0);
+            run += c;
+        }
+    }
     __syncthreads();
 #pragma unroll
     for (int32_t j = 0; j < TR_PER; ++j) {
@@ -343,12 +371,54 @@ __global__ void __launch_bounds__(TRB) k_tr_place(const int64_t* off, int32_t T,
         w_tp[p] = w_t[t];
     }
 }
-// chunks of 4 ids per tile: its last position holds its longest trace (ascending lengths)
-__global__ void k_tr_chunks(const int32_t* tperm, const int64_t* off, int32_t T, int32_t n_wt, int64_t* nch) {
-    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= n_wt) return;
-    const int32_t t = tperm[min(k * WAVE + WAVE - 1, (int64_t)T - 1)];
-    nch[k] = (off[t + 1] - off[t] + 3) >> 2;
+// chunks of 4 ids per wave tile (its last position holds its longest trace: lengths ascend), their
+// exclusive prefix and its int32 copy in one launch: runs of TS_TILE wave tiles per block, chained
+// by decoupled look-back
+constexpr int TS_T = 256, TS_I = 8, TS_TILE = TS_T * TS_I;
+__global__ void __launch_bounds__(TS_T) k_tr_chunk_scan(const int32_t* tperm, const int64_t* off, int32_t T, int32_t n_wt,
+                                                        int64_t* c64, int32_t* coff, unsigned long long* st,
+                                                        uint64_t epoch) {
+    __shared__ int64_t sa[TS_T];
+    __shared__ int64_t ex;
+    const int tid = threadIdx.x;
+    const int64_t tile = blockIdx.x, base = tile * TS_TILE + (int64_t)tid * TS_I;
+    int64_t v[TS_I], a = 0;
+#pragma unroll
+    for (int i = 0; i < TS_I; ++i) {
+        const int64_t k = base + i;
+        v[i] = 0;
+        if (k < n_wt) {
+            const int32_t t = tperm[min(k * WAVE + WAVE - 1, (int64_t)T - 1)];
+            v[i] = (off[t + 1] - off[t] + 3) >> 2;
+        }
+        a += v[i];
+    }
+    sa[tid] = a;
+    __syncthreads();
+    for (int o = 1; o < TS_T; o <<= 1) {
+        const int64_t x = tid >= o ? sa[tid - o] : 0;
+        __syncthreads();
+        sa[tid] += x;
+        __syncthreads();
+    }
+    if (tid == 0) {
+        ex = dl_lookback(st, tile, sa[TS_T - 1], epoch);
+        if (tile == (int64_t)gridDim.x - 1) {
+            c64[n_wt] = ex + sa[TS_T - 1];
+            coff[n_wt] = (int32_t)(ex + sa[TS_T - 1]);
+        }
+    }
+    __syncthreads();
+    int64_t r = ex + sa[tid] - a;
+#pragma unroll
+    for (int i = 0; i < TS_I; ++i) {
+        const int64_t k = base + i;
+        if (k < n_wt) {
+            c64[k] = r;
+            coff[k] = (int32_t)r;
+        }
+        r += v[i];
+    }
 }
 __global__ void k_tr_coff(const int64_t* c64, int32_t n, int32_t* coff) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2700,33 +2770,47 @@ static int fused_blocks(mr_ctx* ctx, mr_graph* g, const FxPlan& P, int TT_v1, in
 // chunk count sizes the id array; the chunk offsets stay on the host for the per-wave cut).
 // off / ids: the trace-major incidence the kernel walks (rs_off with rs16 / rsp, or a wide graph's
 // hot entries), N: the kernel's op count (pads N + lane)
-static int tr_layout(mr_ctx* ctx, mr_graph* g, const int64_t* off, const uint16_t* src, int32_t N, int64_t nent) {
+static int tr_layout(mr_ctx* ctx, mr_graph* g, const int64_t* off, const uint16_t* src, int32_t N, int64_t nent,
+                     int32_t* zeroed) {
     hipStream_t st = ctx->stream;
     const int32_t T = g->T;
     const int32_t W = cdiv(T, WAVE);
     g->n_wt = W;
     g->wtile_nw = 0;
     const int32_t nbin = N + 1;   // trace lengths 1..N (distinct ops)
-    DBuf<int32_t> hist;
+    // zeroed: 2 * nbin words the caller cleared (histogram, slot counters), else cleared here
+    const bool lscan = nbin <= TP_LSCAN;
+    DBuf<int32_t> hz;
     DBuf<int64_t> boff, c64, tmp;
-    MR_TRY(hist.zero(ctx, (size_t)nbin));
-    MR_TRY(boff.alloc(ctx, (size_t)nbin + 1));
+    if (!zeroed) {
+        MR_TRY(hz.zero(ctx, 2 * (size_t)nbin));
+        zeroed = hz.p;
+    }
+    int32_t* hist = zeroed;
+    int32_t* taken = zeroed + nbin;
     MR_TRY(c64.alloc(ctx, (size_t)W + 1));
-    MR_TRY(tmp.alloc(ctx, (size_t)std::max(scan_tmp_elems(std::max<int64_t>(W, 1)), scan_tmp_elems(nbin))));
     MR_TRY(g->tperm.alloc(ctx, (size_t)std::max(T, 1)));
     MR_TRY(g->w_tp.alloc(ctx, (size_t)std::max(T, 1)));
     MR_TRY(g->coff.alloc(ctx, (size_t)W + 1));
     if (T) {
         const int nb = cdiv(T, (int64_t)TRB * TR_PER);
-        hipLaunchKernelGGL(k_tr_hist, dim3(nb), dim3(TRB), (size_t)nbin * sizeof(int32_t), st, off, T, nbin,
-                           hist.p);
-        MR_TRY(mr_exclusive_scan_i32(ctx, hist.p, boff.p, nbin, tmp.p));
-        hipLaunchKernelGGL(k_tr_place, dim3(nb), dim3(TRB), 2 * (size_t)nbin * sizeof(int32_t), st, off, T,
-                           nbin, boff.p, hist.p, g->w_t.p, g->tperm.p, g->w_tp.p);
-        hipLaunchKernelGGL(k_tr_chunks, dim3(cdiv(W, 256)), dim3(256), 0, st, g->tperm.p, off, T, W, c64.p);
+        hipLaunchKernelGGL(k_tr_hist, dim3(nb), dim3(TRB), (size_t)nbin * sizeof(int32_t), st, off, T, nbin, hist);
+        if (!lscan) {
+            MR_TRY(boff.alloc(ctx, (size_t)nbin + 1));
+            MR_TRY(tmp.alloc(ctx, (size_t)scan_tmp_elems(nbin)));
+            MR_TRY(mr_exclusive_scan_i32(ctx, hist, boff.p, nbin, tmp.p));
+        }
+        hipLaunchKernelGGL(k_tr_place, dim3(nb), dim3(TRB), 2 * (size_t)nbin * sizeof(int32_t), st, off, T, nbin,
+                           lscan ? (const int64_t*)nullptr : boff.p, hist, taken, g->w_t.p, g->tperm.p, g->w_tp.p);
     }
-    MR_TRY(mr_exclusive_scan(ctx, c64.p, c64.p, W, tmp.p));
-    hipLaunchKernelGGL(k_tr_coff, dim3(cdiv((int64_t)W + 1, 256)), dim3(256), 0, st, c64.p, W, g->coff.p);
+    {   // chunk counts per wave tile, their prefix and its int32 copy: one launch
+        const int64_t nt = std::max<int64_t>(cdiv((int64_t)W, TS_TILE), 1);
+        unsigned long long* dst = nullptr;
+        uint64_t epoch = 0;
+        MR_TRY(mr_dl_status(ctx, nt, &dst, &epoch));
+        hipLaunchKernelGGL(k_tr_chunk_scan, dim3((unsigned)nt), dim3(TS_T), 0, st, g->tperm.p, off, T, W, c64.p,
+                           g->coff.p, dst, epoch);
+    }
     // the id array at an upper bound of the chunk count (no host round trip): tile k holds
     // ceil(maxlen_k / 4) chunks, and with lengths ascending maxlen_k <= every length of tile k + 1,
     // so sum_k maxlen_k <= nent / 64 + 2 N
@@ -2785,7 +2869,7 @@ static int wide_prepare(mr_ctx* ctx, mr_graph* g) {
     MR_TRY(g->hot16.alloc(ctx, (size_t)n_hot + 8));
     hipLaunchKernelGGL(k_wide_hot, dim3(cdiv(T, 256)), dim3(256), 0, st, g->rs_off.p, g->rs_ops.p, inv.p, T, NA,
                        g->hot_off.p, g->hot16.p);
-    MR_TRY(tr_layout(ctx, g, g->hot_off.p, g->hot16.p, NA, n_hot));   // tperm, w_tp, tids, coff (host copy)
+    MR_TRY(tr_layout(ctx, g, g->hot_off.p, g->hot16.p, NA, n_hot, nullptr));   // tperm, w_tp, tids, coff (host copy)
     // ---- cold entries in position order
     DBuf<int32_t> cnt;
     DBuf<int64_t> coff64;
@@ -2866,11 +2950,15 @@ int mr_graph_prepare(mr_ctx* ctx, mr_graph* g) {
     if (!g->cov_ready) MR_TRY(g->cov.alloc(ctx, (size_t)N));
     const bool u16 = N <= 65536 && g->nnz_rs;
     if (u16) MR_TRY(g->rs16.alloc(ctx, (size_t)g->nnz_rs + 8));
-    const int64_t nc = std::max<int64_t>({(int64_t)T, (int64_t)N, u16 ? g->nnz_rs : 0});
+    // the fused layout's histogram and slot counters, cleared by the same launch
+    DBuf<int32_t> trz;
+    const int32_t nz = N <= FX_NMAX ? 2 * (N + 1) : 0;
+    if (nz) MR_TRY(trz.alloc(ctx, (size_t)nz));
+    const int64_t nc = std::max<int64_t>({(int64_t)T, (int64_t)N, u16 ? g->nnz_rs : 0, (int64_t)nz});
     if (nc)
         hipLaunchKernelGGL(k_graph_consts, dim3(cdiv(nc, 256)), dim3(256), 0, st, g->len_t.p, g->w_t.p, T, g->len_o.p,
                            g->nchild.p, g->u_o.p, g->pw.p, N, g->rs_ops.p, u16 ? g->nnz_rs : 0,
-                           u16 ? g->rs16.p : (uint16_t*)nullptr);
+                           u16 ? g->rs16.p : (uint16_t*)nullptr, trz.p, nz);
     g->relabeled = false;   // (set below for fused graphs that need it)
     g->wide = false;
     g->NA = N;
@@ -2908,7 +2996,7 @@ int mr_graph_prepare(mr_ctx* ctx, mr_graph* g) {
             g->perm.reset();
             g->rsp.reset();
         }
-        MR_TRY(tr_layout(ctx, g, g->rs_off.p, g->relabeled ? g->rsp.p : g->rs16.p, N, nnz));
+        MR_TRY(tr_layout(ctx, g, g->rs_off.p, g->relabeled ? g->rsp.p : g->rs16.p, N, nnz, trz.p));
         g->n_tiles = 0;
         g->n_pairs = 0;
         MR_TRY_HIP(ctx, hipGetLastError());

@@ -51,6 +51,39 @@ __device__ __forceinline__ double block_max(double v, double* red) {
 // Exclusive scan of int64 counts: out[i] = sum(in[0..i)), out[n] = total (out has n+1 slots).
 // in == out is allowed.  Uses `tmp` device scratch of at least scan_tmp_elems(n) int64.
 int64_t scan_tmp_elems(int64_t n);
+// Decoupled look-back chains (single-pass scans, mr_prim.hip): status words
+// [epoch:20 | flag:2 | value:42] -- flag 1 = the tile's own sum, 2 = its inclusive prefix.
+// mr_dl_status hands out >= `words` per-context words with a fresh epoch (no clearing launch).
+constexpr int DL_EB = 20, DL_VB = 42;
+constexpr unsigned long long DL_VMASK = (1ull << DL_VB) - 1ull;
+int mr_dl_status(mr_ctx* ctx, int64_t words, unsigned long long** st, uint64_t* epoch);
+__device__ __forceinline__ unsigned long long dl_word(uint64_t epoch, unsigned flag, int64_t v) {
+    return (epoch << (DL_VB + 2)) | ((unsigned long long)flag << DL_VB) | ((unsigned long long)v & DL_VMASK);
+}
+// one thread of tile `tile`: publish the tile's sum, walk back to the tiles before it (lower
+// block indices: already dispatched) and publish the inclusive prefix; returns the exclusive one.
+// Relaxed agent-scope atomics (sc1): the word carries its value, nothing else is published.
+__device__ __forceinline__ int64_t dl_lookback(unsigned long long* st, int64_t tile, int64_t agg, uint64_t epoch) {
+    int64_t excl = 0;
+    if (tile == 0) {
+        __hip_atomic_store(&st[0], dl_word(epoch, 2, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return 0;
+    }
+    __hip_atomic_store(&st[tile], dl_word(epoch, 1, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int64_t j = tile - 1; j >= 0;) {
+        const unsigned long long w = __hip_atomic_load(&st[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned flag = (unsigned)(w >> DL_VB) & 3u;
+        if ((w >> (DL_VB + 2)) != epoch || flag == 0) {
+            __builtin_amdgcn_s_sleep(1);
+            continue;   // tile j has not published this call's value yet
+        }
+        excl += (int64_t)(w & DL_VMASK);
+        if (flag == 2) break;
+        --j;
+    }
+    __hip_atomic_store(&st[tile], dl_word(epoch, 2, excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return excl;
+}
 int mr_exclusive_scan(mr_ctx* ctx, const int64_t* in, int64_t* out, int64_t n, int64_t* tmp);
 // int32 counts -> int64 offsets
 int mr_exclusive_scan_i32(mr_ctx* ctx, const int32_t* in, int64_t* out, int64_t n, int64_t* tmp);

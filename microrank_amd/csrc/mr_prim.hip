@@ -128,11 +128,6 @@ __global__ void __launch_bounds__(SS_T) k_scan_single(const In* in, int64_t* out
 // per-context buffer; the epoch changes every call, so no clearing launch is needed (the buffer
 // is cleared once per 2^20 calls, when the epoch wraps).  Relaxed agent-scope atomics (sc1):
 // the word carries its value, no other data is published through it.
-constexpr int DL_EB = 20, DL_VB = 42;
-constexpr unsigned long long DL_VMASK = (1ull << DL_VB) - 1ull;
-__device__ __forceinline__ unsigned long long dl_word(uint64_t epoch, unsigned flag, int64_t v) {
-    return (epoch << (DL_VB + 2)) | ((unsigned long long)flag << DL_VB) | ((unsigned long long)v & DL_VMASK);
-}
 template <class In>
 __global__ void __launch_bounds__(SCAN_T) k_scan_dl(const In* in, int64_t* out, int64_t n, unsigned long long* st,
                                                     uint64_t epoch) {
@@ -158,24 +153,7 @@ __global__ void __launch_bounds__(SCAN_T) k_scan_dl(const In* in, int64_t* out, 
     }
     const int64_t agg = tsum[SCAN_T - 1];
     if (threadIdx.x == 0) {
-        int64_t excl = 0;
-        if (tile == 0) {
-            __hip_atomic_store(&st[0], dl_word(epoch, 2, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            __hip_atomic_store(&st[tile], dl_word(epoch, 1, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            for (int64_t j = tile - 1; j >= 0;) {
-                const unsigned long long w = __hip_atomic_load(&st[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const unsigned flag = (unsigned)(w >> DL_VB) & 3u;
-                if ((w >> (DL_VB + 2)) != epoch || flag == 0) {
-                    __builtin_amdgcn_s_sleep(1);
-                    continue;   // tile j has not published this call's value yet
-                }
-                excl += (int64_t)(w & DL_VMASK);
-                if (flag == 2) break;
-                --j;
-            }
-            __hip_atomic_store(&st[tile], dl_word(epoch, 2, excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        const int64_t excl = dl_lookback(st, tile, agg, epoch);
         s_excl = excl;
         if (tile == (int64_t)gridDim.x - 1) out[n] = excl + agg;
     }
@@ -203,23 +181,10 @@ int scan_impl(mr_ctx* ctx, const In* in, int64_t* out, int64_t n, int64_t* tmp) 
     }
     static const bool three_pass = getenv("MR_SCAN_3PASS") != nullptr;   // A/B knob
     if (!three_pass) {
-        if ((size_t)nb > ctx->scan_cap) {   // grow the status words (stream-ordered: sync first)
-            MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));
-            if (ctx->scan_st) MR_TRY_HIP(ctx, hipFree(ctx->scan_st));
-            ctx->scan_st = nullptr;
-            const size_t cap = std::max<size_t>((size_t)nb, 4096);
-            MR_TRY_HIP(ctx, hipMalloc((void**)&ctx->scan_st, cap * sizeof(unsigned long long)));
-            MR_TRY_HIP(ctx, hipMemsetAsync(ctx->scan_st, 0, cap * sizeof(unsigned long long), ctx->stream));
-            ctx->scan_cap = cap;
-            ctx->scan_epoch = 0;
-        }
-        ctx->scan_epoch = (ctx->scan_epoch + 1) & ((1u << DL_EB) - 1u);
-        if (ctx->scan_epoch == 0) {   // wrapped: clear every word (epoch 0 marks a cleared word)
-            MR_TRY_HIP(ctx, hipMemsetAsync(ctx->scan_st, 0, ctx->scan_cap * sizeof(unsigned long long), ctx->stream));
-            ctx->scan_epoch = 1;
-        }
-        hipLaunchKernelGGL(k_scan_dl<In>, dim3((unsigned)nb), dim3(SCAN_T), 0, ctx->stream, in, out, n, ctx->scan_st,
-                           (uint64_t)ctx->scan_epoch);
+        unsigned long long* st = nullptr;
+        uint64_t epoch = 0;
+        MR_TRY(mr_dl_status(ctx, nb, &st, &epoch));
+        hipLaunchKernelGGL(k_scan_dl<In>, dim3((unsigned)nb), dim3(SCAN_T), 0, ctx->stream, in, out, n, st, epoch);
         MR_TRY_HIP(ctx, hipGetLastError());
         return MR_OK;
     }
@@ -232,6 +197,27 @@ int scan_impl(mr_ctx* ctx, const In* in, int64_t* out, int64_t n, int64_t* tmp) 
 }  // namespace
 
 int64_t scan_tmp_elems(int64_t n) { return (n + SCAN_TILE - 1) / SCAN_TILE + 1; }
+
+int mr_dl_status(mr_ctx* ctx, int64_t words, unsigned long long** st, uint64_t* epoch) {
+    if ((size_t)words > ctx->scan_cap) {   // grow the status words (stream-ordered: sync first)
+        MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        if (ctx->scan_st) MR_TRY_HIP(ctx, hipFree(ctx->scan_st));
+        ctx->scan_st = nullptr;
+        const size_t cap = std::max<size_t>((size_t)words, 8192);
+        MR_TRY_HIP(ctx, hipMalloc((void**)&ctx->scan_st, cap * sizeof(unsigned long long)));
+        MR_TRY_HIP(ctx, hipMemsetAsync(ctx->scan_st, 0, cap * sizeof(unsigned long long), ctx->stream));
+        ctx->scan_cap = cap;
+        ctx->scan_epoch = 0;
+    }
+    ctx->scan_epoch = (ctx->scan_epoch + 1) & ((1u << DL_EB) - 1u);
+    if (ctx->scan_epoch == 0) {   // wrapped: clear every word (epoch 0 marks a cleared word)
+        MR_TRY_HIP(ctx, hipMemsetAsync(ctx->scan_st, 0, ctx->scan_cap * sizeof(unsigned long long), ctx->stream));
+        ctx->scan_epoch = 1;
+    }
+    *st = ctx->scan_st;
+    *epoch = ctx->scan_epoch;
+    return MR_OK;
+}
 
 int mr_exclusive_scan(mr_ctx* ctx, const int64_t* in, int64_t* out, int64_t n, int64_t* tmp) {
     return scan_impl<int64_t>(ctx, in, out, n, tmp);

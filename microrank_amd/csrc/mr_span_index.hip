@@ -404,23 +404,34 @@ int mr_spans_index(mr_ctx* ctx, mr_spans* s) {
     return MR_OK;
 }
 
-// Window detector on the index (uniform trace times): state[t] 0 out / 1 normal / 2 abnormal.
-int mr_detect_indexed(mr_ctx* ctx, const mr_spans* s, int64_t t0, int64_t t1, const double* d_a3, const uint8_t* d_a3v,
-                      uint8_t* d_state, int32_t* n_abn, int32_t* n_nor, int64_t* n_in) {
-    hipStream_t st = ctx->stream;
+static_assert(CSH == MR_DETECT_SHARDS, "detector counter shards");
+// Window detector on the index (uniform trace times): state[t] 0 out / 1 normal / 2 abnormal for
+// EVERY trace; counts (3 * MR_DETECT_SHARDS words, zeroed by the caller) receive the abnormal /
+// normal / in-window-row counter shards (mr_detect_sum adds them up on the host).
+int mr_detect_indexed_launch(mr_ctx* ctx, const mr_spans* s, int64_t t0, int64_t t1, const double* d_a3,
+                             const uint8_t* d_a3v, uint8_t* d_state, unsigned long long* counts) {
     const int32_t NT = s->n_traces;
-    DBuf<unsigned long long> counts;
-    MR_TRY(counts.zero(ctx, 3 * CSH));
-    hipLaunchKernelGGL(k_ix_detect, dim3(cdiv(NT, DB)), dim3(DB), 0, st, NT, s->tlen.p, s->tts.p, s->tte.p, s->tmaxd.p,
-                       s->sv_off.p, s->sv_op.p, s->sv_cnt.p, d_a3, d_a3v, t0, t1, d_state, counts.p);
+    if (NT)
+        hipLaunchKernelGGL(k_ix_detect, dim3(cdiv(NT, DB)), dim3(DB), 0, ctx->stream, NT, s->tlen.p, s->tts.p, s->tte.p,
+                           s->tmaxd.p, s->sv_off.p, s->sv_op.p, s->sv_cnt.p, d_a3, d_a3v, t0, t1, d_state, counts);
     MR_TRY_HIP(ctx, hipGetLastError());
-    unsigned long long sh[3 * CSH], hc[3] = {0, 0, 0};
-    MR_TRY(counts.download(ctx, sh, 3 * CSH));
-    MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+    return MR_OK;
+}
+void mr_detect_sum(const unsigned long long* sh, int32_t* n_abn, int32_t* n_nor, int64_t* n_in) {
+    unsigned long long hc[3] = {0, 0, 0};
     for (int k = 0; k < 3 * CSH; ++k) hc[k % 3] += sh[k];
-    *n_in = (int64_t)hc[2];
-    if (hc[2] == 0) return mr_fail(ctx, MR_ERR_VALUE, "Current span list is empty");
     *n_abn = (int32_t)hc[0];
     *n_nor = (int32_t)hc[1];
+    *n_in = (int64_t)hc[2];
+}
+int mr_detect_indexed(mr_ctx* ctx, const mr_spans* s, int64_t t0, int64_t t1, const double* d_a3, const uint8_t* d_a3v,
+                      uint8_t* d_state, int32_t* n_abn, int32_t* n_nor, int64_t* n_in) {
+    DBuf<unsigned long long> counts;
+    MR_TRY(counts.zero(ctx, 3 * CSH));
+    MR_TRY(mr_detect_indexed_launch(ctx, s, t0, t1, d_a3, d_a3v, d_state, counts.p));
+    unsigned char* h = nullptr;
+    MR_TRY(mr_read_bytes(ctx, counts.p, 3 * CSH * sizeof(unsigned long long), &h));
+    mr_detect_sum((const unsigned long long*)h, n_abn, n_nor, n_in);
+    if (*n_in == 0) return mr_fail(ctx, MR_ERR_VALUE, "Current span list is empty");
     return MR_OK;
 }

@@ -259,22 +259,34 @@ __global__ void __launch_bounds__(WS_T) k_win_spectrum(int32_t Na, const int32_t
 
 // The window spectrum in one launch and one read-back (k_win_spectrum), or MR_ERR_STATE when the
 // sizes exceed its one-block limits (the caller then takes the general path).
+static_assert(MR_WS_SLOT == 12 * WS_KMAX + 16, "window spectrum slot");
+int mr_win_spectrum_launch(mr_ctx* ctx, int32_t Na, const int32_t* a_podop, const double* a_w, const int32_t* a_cov,
+                           int32_t Nn, const int32_t* n_podop, const double* n_w, const int32_t* n_cov, int32_t NP,
+                           int64_t A, int64_t Nl, int method, int32_t k, unsigned char* d_slot) {
+    if (Na + Nn > WS_MAX || NP > WS_PMAX || k > WS_KMAX || k < 0) return MR_ERR_STATE;
+    hipLaunchKernelGGL(k_win_spectrum, dim3(1), dim3(WS_T), 0, ctx->stream, Na, a_podop, a_w, a_cov, Nn, n_podop, n_w,
+                       n_cov, NP, A, Nl, method, k, d_slot);
+    MR_TRY_HIP(ctx, hipGetLastError());
+    return MR_OK;
+}
+void mr_win_spectrum_unpack(const unsigned char* slot, int32_t* out_codes, double* out_score, int32_t* n_out) {
+    const int32_t kk = ((const int32_t*)(slot + 12 * WS_KMAX))[0];
+    if (out_codes) memcpy(out_codes, slot, (size_t)kk * sizeof(int32_t));
+    if (out_score) memcpy(out_score, slot + 4 * WS_KMAX, (size_t)kk * sizeof(double));
+    *n_out = kk;
+}
 int mr_win_spectrum_small(mr_ctx* ctx, int32_t Na, const int32_t* a_podop, const double* a_w, const int32_t* a_cov,
                           int32_t Nn, const int32_t* n_podop, const double* n_w, const int32_t* n_cov, int32_t NP,
                           int64_t A, int64_t Nl, int method, int32_t k, int32_t* out_codes, double* out_score,
                           int32_t* n_out) {
-    if (Na + Nn > WS_MAX || NP > WS_PMAX || k > WS_KMAX || k < 0) return MR_ERR_STATE;
     DBuf<unsigned char> out;
-    MR_TRY(out.alloc(ctx, 12 * WS_KMAX + 16));
-    hipLaunchKernelGGL(k_win_spectrum, dim3(1), dim3(WS_T), 0, ctx->stream, Na, a_podop, a_w, a_cov, Nn, n_podop, n_w,
-                       n_cov, NP, A, Nl, method, k, out.p);
-    MR_TRY_HIP(ctx, hipGetLastError());
+    MR_TRY(out.alloc(ctx, MR_WS_SLOT));
+    const int rc = mr_win_spectrum_launch(ctx, Na, a_podop, a_w, a_cov, Nn, n_podop, n_w, n_cov, NP, A, Nl, method, k,
+                                          out.p);
+    if (rc != MR_OK) return rc;
     unsigned char* h = nullptr;
-    MR_TRY(mr_read_bytes(ctx, out.p, 12 * WS_KMAX + 16, &h));
-    const int32_t kk = ((const int32_t*)(h + 12 * WS_KMAX))[0];
-    if (out_codes) memcpy(out_codes, h, (size_t)kk * sizeof(int32_t));
-    if (out_score) memcpy(out_score, h + 4 * WS_KMAX, (size_t)kk * sizeof(double));
-    *n_out = kk;
+    MR_TRY(mr_read_bytes(ctx, out.p, MR_WS_SLOT, &h));
+    mr_win_spectrum_unpack(h, out_codes, out_score, n_out);
     return MR_OK;
 }
 
