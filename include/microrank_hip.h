@@ -133,6 +133,36 @@ typedef struct mr_span_cols {
 int mr_spans_upload(mr_ctx* ctx, const mr_span_cols* cols, mr_spans** out);
 int mr_spans_free(mr_spans* s);
 
+/* SURVEY §8(f) f2 -- span ingest on the device from the string columns of the OTel export
+ * (collect_data.py:35-46, renamed at online_rca.py:221-244).  A string column is Arrow-style:
+ * value i = bytes[offsets[i] .. offsets[i+1]); valid is an Arrow validity bitmap (bit i of byte
+ * i/8, 1 = present) or NULL (no nulls) -- only ParentSpanId may have nulls (a root span).
+ * Produces the same table mr_spans_upload would get from SpanTable.from_dataframe: traceID,
+ * podName_op and serviceName_op codes in sorted (code-point) name order, op = operationName with
+ * ts-ui-dashboard's last '/segment' dropped (preprocess_data.py:26-33, 151-155), ParentSpanId
+ * resolved to the equal spanID's code or -1.  Replaces the per-function string work of
+ * preprocess_data.py (:26-33, 53-57, 100-104, 151-165). */
+typedef struct mr_str_col {
+    const int64_t* offsets;   /* [n_spans + 1] */
+    const uint8_t* bytes;
+    const uint8_t* valid;     /* Arrow bitmap or NULL */
+} mr_str_col;
+typedef struct mr_span_strings {
+    int64_t n_spans;
+    mr_str_col trace_id, span_id, parent_id, service, operation, pod;
+    const int64_t* duration;  /* [n_spans] */
+    const int64_t* tstart;    /* [n_spans] trace-level start, ns (NULL if absent) */
+    const int64_t* tend;
+} mr_span_strings;
+int mr_spans_ingest(mr_ctx* ctx, const mr_span_strings* cols, mr_spans** out);
+int mr_spans_info(const mr_spans* s, int64_t* n_spans, int32_t* n_traces, int32_t* n_podops, int32_t* n_svcops);
+/* first row of each code in code order, which 0 trace / 1 pod-op / 2 service-op (ingested tables):
+ * name of code k = that row's traceID / podName_op / serviceName_op */
+int mr_spans_dict_rows(const mr_spans* s, int which, int32_t* rows);
+/* the code columns of a table (any pointer may be NULL), [n_spans] each */
+int mr_spans_codes(const mr_spans* s, int32_t* trace, int32_t* podop, int32_t* svcop, int64_t* span,
+                   int64_t* parent);
+
 /* K1: preprocess_data.get_pagerank_graph (preprocess_data.py:146-171) on the device.
  * trace_mask[n_traces] (host, 0/1) selects the trace_list.  Node order = sorted parent ops,
  * then never-parent ops in first-appearance row order (T10).  The parent join ignores
@@ -186,6 +216,18 @@ int mr_slo(mr_ctx* ctx, const mr_spans* s, double* mean /*[n_svcops]*/, double* 
 int mr_detect(mr_ctx* ctx, const mr_spans* s, int64_t t0, int64_t t1, const double* a3,
               const uint8_t* a3_valid, uint8_t* state, int32_t* n_abnormal, int32_t* n_normal,
               int64_t* n_spans_in_window);
+
+/* SURVEY §8(f) f3 -- the driver's whole window sweep (online_rca.py:161-216) detected at once:
+ * for window m in [0, n_win) = [t_begin + m*grain, t_begin + m*grain + window] the counts of
+ * mr_detect (abnormal / normal traces, in-window rows; n_rows[m] = 0 is the reference's empty
+ * window, T2).  Needs trace-level times constant within each trace (the renamed TraceStart /
+ * TraceEnd columns, online_rca.py:229-230): then a trace's partition does not depend on the window
+ * and is computed once; state[n_traces] (host, optional) receives it (0 dropped, 1 normal,
+ * 2 abnormal), so window m's lists are the traces of that state inside the window.
+ * MR_ERR_STATE when times vary within a trace (run mr_detect per window instead). */
+int mr_detect_sweep(mr_ctx* ctx, const mr_spans* s, int64_t t_begin, int64_t grain, int64_t window,
+                    int32_t n_win, const double* a3, const uint8_t* a3_valid, uint8_t* state,
+                    int32_t* n_abnormal, int32_t* n_normal, int64_t* n_rows);
 
 /* ------------------------------------------------------------------ whole RCA window on device
  * online_rca.online_anomaly_detect_RCA body for one window (online_rca.py:164-215):

@@ -46,6 +46,16 @@ class SpanCols(C.Structure):
                 ("row", i32p)]
 
 
+class StrCol(C.Structure):
+    _fields_ = [("offsets", i64p), ("bytes", C.c_void_p), ("valid", C.c_void_p)]
+
+
+class SpanStrings(C.Structure):
+    _fields_ = [("n_spans", C.c_int64), ("trace_id", StrCol), ("span_id", StrCol), ("parent_id", StrCol),
+                ("service", StrCol), ("operation", StrCol), ("pod", StrCol), ("duration", i64p),
+                ("tstart", i64p), ("tend", i64p)]
+
+
 # name -> (restype, argtypes); every symbol here must be exported (tests check it)
 SIGNATURES = {
     "mr_version": (C.c_int, []),
@@ -67,6 +77,10 @@ SIGNATURES = {
     "mr_spans_upload": (C.c_int, [P, C.POINTER(SpanCols), C.POINTER(P)]),
     "mr_graph_build_sharded": (C.c_int, [P, P, C.POINTER(C.c_uint8), C.POINTER(P)]),
     "mr_spans_free": (C.c_int, [P]),
+    "mr_spans_ingest": (C.c_int, [P, C.POINTER(SpanStrings), C.POINTER(P)]),
+    "mr_spans_info": (C.c_int, [P, i64p, i32p, i32p, i32p]),
+    "mr_spans_dict_rows": (C.c_int, [P, C.c_int, i32p]),
+    "mr_spans_codes": (C.c_int, [P, i32p, i32p, i32p, i64p, i64p]),
     "mr_graph_build": (C.c_int, [P, P, u8p, C.POINTER(P)]),
     "mr_graph_nodes": (C.c_int, [P, i32p, i32p]),
     "mr_graph_export": (C.c_int, [P, i64p, i32p, i32p, i32p, i64p, i32p, i32p]),
@@ -74,6 +88,8 @@ SIGNATURES = {
                               C.c_int, C.c_int32, i32p, f64p, i32p, i32p]),
     "mr_slo": (C.c_int, [P, P, f64p, f64p, i64p]),
     "mr_detect": (C.c_int, [P, P, C.c_int64, C.c_int64, f64p, u8p, u8p, i32p, i32p, i64p]),
+    "mr_detect_sweep": (C.c_int, [P, P, C.c_int64, C.c_int64, C.c_int64, C.c_int32, f64p, u8p, u8p, i32p, i32p,
+                                  i64p]),
     "mr_windows_batch": (C.c_int, [P, C.c_int32, C.POINTER(P), i64p, i64p, C.POINTER(C.c_void_p),
                                    C.POINTER(C.c_void_p), C.c_int, C.c_int32, C.c_int, i32p, f64p, i32p, i64p, i32p,
                                    i32p, i32p]),

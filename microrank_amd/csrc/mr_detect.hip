@@ -238,6 +238,41 @@ extern "C" int mr_detect(mr_ctx* ctx, const mr_spans* s, int64_t t0, int64_t t1,
     return MR_OK;
 }
 
+// f3: every window start of the driver's sweep (online_rca.py:161-216) detected in
+// one pass -- each trace classified once, window counts from difference arrays (k_ix_sweep).
+extern "C" int mr_detect_sweep(mr_ctx* ctx, const mr_spans* s, int64_t t_begin, int64_t grain, int64_t window,
+                               int32_t n_win, const double* a3, const uint8_t* a3_valid, uint8_t* state,
+                               int32_t* n_abnormal, int32_t* n_normal, int64_t* n_rows) {
+    if (!ctx || !s || s->ctx != ctx || !a3 || !a3_valid || grain <= 0 || window < 0 || n_win < 0 ||
+        (n_win && (!n_abnormal || !n_normal || !n_rows)))
+        return mr_fail(ctx, MR_ERR_ARG, "mr_detect_sweep: bad arguments");
+    if (!s->has_times) return mr_fail(ctx, MR_ERR_ARG, "spans have no startTime/endTime columns");
+    if (!s->indexed || !s->uniform_times)
+        return mr_fail(ctx, MR_ERR_STATE, "mr_detect_sweep: trace-level times differ within a trace (use mr_detect per window)");
+    MR_TRY_HIP(ctx, hipSetDevice(ctx->device));
+    const int32_t NT = s->n_traces;
+    DBuf<double> da3;
+    DBuf<uint8_t> dv, dst;
+    DBuf<unsigned long long> diff;
+    MR_TRY(da3.upload(ctx, a3, (size_t)std::max(s->n_svcops, 1)));
+    MR_TRY(dv.upload(ctx, a3_valid, (size_t)std::max(s->n_svcops, 1)));
+    MR_TRY(dst.alloc(ctx, (size_t)std::max(NT, 1)));
+    MR_TRY(diff.zero(ctx, (size_t)3 * (n_win + 1)));
+    MR_TRY(mr_detect_sweep_launch(ctx, s, t_begin, grain, window, n_win, da3.p, dv.p, dst.p, diff.p));
+    std::vector<unsigned long long> h((size_t)3 * (n_win + 1));
+    MR_TRY(diff.download(ctx, h.data(), h.size()));
+    if (state && NT) MR_TRY(dst.download(ctx, state, (size_t)NT));
+    MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    unsigned long long run[3] = {0, 0, 0};   // prefix sums mod 2^64 of exact integer differences
+    for (int32_t m = 0; m < n_win; ++m) {
+        for (int k = 0; k < 3; ++k) run[k] += h[(size_t)k * (n_win + 1) + m];
+        n_abnormal[m] = (int32_t)run[0];
+        n_normal[m] = (int32_t)run[1];
+        n_rows[m] = (int64_t)run[2];
+    }
+    return MR_OK;
+}
+
 namespace {
 __global__ void k_masks(const uint8_t* state, int32_t n, uint8_t* m_abn, uint8_t* m_nor) {
     int32_t t = blockIdx.x * blockDim.x + threadIdx.x;

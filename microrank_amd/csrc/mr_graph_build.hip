@@ -684,6 +684,8 @@ __global__ void k_neg_i32(int32_t* a, int32_t n) {
 }  // namespace
 
 // ------------------------------------------------------------------------------ host
+int mr_spans_finish(mr_ctx* ctx, mr_spans* s);
+
 extern "C" int mr_spans_upload(mr_ctx* ctx, const mr_span_cols* c, mr_spans** out) {
     if (!ctx || !c || !out) return mr_fail(ctx, MR_ERR_ARG, "mr_spans_upload: null argument");
     *out = nullptr;
@@ -730,26 +732,32 @@ extern "C" int mr_spans_upload(mr_ctx* ctx, const mr_span_cols* c, mr_spans** ou
     if (s->has_times && ((rc = s->tstart.upload(ctx, c->tstart, S)) || (rc = s->tend.upload(ctx, c->tend, S))))
         return fail(rc);
     if (c->row && (rc = s->grow.upload(ctx, c->row, S))) return fail(rc);
-    // spanID -> rows multimap (counting sort by code)
-    const int64_t U = s->n_span_codes;
+    if ((rc = mr_spans_finish(ctx, s))) return fail(rc);
+    mr_handle_add(ctx, s, [](void* h) { delete (mr_spans*)h; });
+    *out = s;
+    return MR_OK;
+}
+
+// device columns in place -> the spanID -> rows multimap (counting sort by code) and the
+// per-trace index; shared by mr_spans_upload (int codes) and mr_spans_ingest (strings)
+int mr_spans_finish(mr_ctx* ctx, mr_spans* s) {
+    const int64_t S = s->S, U = s->n_span_codes;
     DBuf<int32_t> cnt;
     DBuf<int64_t> tmp;
-    if ((rc = cnt.zero(ctx, (size_t)U)) || (rc = s->id_off.alloc(ctx, (size_t)U + 1)) ||
-        (rc = s->id_rows.alloc(ctx, (size_t)S)) || (rc = tmp.alloc(ctx, (size_t)scan_tmp_elems(U))))
-        return fail(rc);
+    MR_TRY(cnt.zero(ctx, (size_t)U));
+    MR_TRY(s->id_off.alloc(ctx, (size_t)U + 1));
+    MR_TRY(s->id_rows.alloc(ctx, (size_t)S));
+    MR_TRY(tmp.alloc(ctx, (size_t)scan_tmp_elems(U)));
     if (S) hipLaunchKernelGGL(k_count_codes, dim3(cdiv(S, 256)), dim3(256), 0, ctx->stream, s->span.p, S, cnt.p);
-    if ((rc = mr_exclusive_scan_i32(ctx, cnt.p, s->id_off.p, U, tmp.p))) return fail(rc);
-    if (U && hipMemsetAsync(cnt.p, 0, U * sizeof(int32_t), ctx->stream) != hipSuccess) return fail(MR_ERR_HIP);
+    MR_TRY(mr_exclusive_scan_i32(ctx, cnt.p, s->id_off.p, U, tmp.p));
+    if (U) MR_TRY_HIP(ctx, hipMemsetAsync(cnt.p, 0, U * sizeof(int32_t), ctx->stream));
     if (S)
         hipLaunchKernelGGL(k_fill_ids, dim3(cdiv(S, 256)), dim3(256), 0, ctx->stream, s->span.p, S, s->id_off.p, cnt.p,
                            s->id_rows.p);
     if (U) hipLaunchKernelGGL(k_sort_buckets, dim3(cdiv(U, 256)), dim3(256), 0, ctx->stream, s->id_off.p, U, s->id_rows.p);
     if (hipGetLastError() != hipSuccess || hipStreamSynchronize(ctx->stream) != hipSuccess)
-        return fail(mr_fail(ctx, MR_ERR_HIP, "mr_spans_upload: kernel failure"));
-    if ((rc = mr_spans_index(ctx, s))) return fail(rc);
-    mr_handle_add(ctx, s, [](void* h) { delete (mr_spans*)h; });
-    *out = s;
-    return MR_OK;
+        return mr_fail(ctx, MR_ERR_HIP, "span table setup: kernel failure");
+    return mr_spans_index(ctx, s);
 }
 
 extern "C" int mr_spans_free(mr_spans* s) {

@@ -285,6 +285,9 @@ struct mr_spans {
     DBuf<int32_t> ed_cnt, ed_tr;         // ... with multiplicity and trace
     DBuf<int32_t> xj_tc, xj_tp;          // [n_xj] join pairs across traces (T11): child / parent trace
     DBuf<uint64_t> xj_key;               //        and key
+    // tables ingested from strings (mr_spans_ingest): the first row of each trace / pod-op /
+    // service-op code, in code order (the host builds the name lists from them)
+    DBuf<int32_t> dict_rows[3];
 };
 
 int mr_spans_index(mr_ctx* ctx, mr_spans* s);
@@ -333,6 +336,8 @@ constexpr int MR_DETECT_SHARDS = 64;
 int mr_detect_indexed_launch(mr_ctx* ctx, const mr_spans* s, int64_t t0, int64_t t1, const double* d_a3,
                              const uint8_t* d_a3v, uint8_t* d_state, unsigned long long* counts);
 void mr_detect_sum(const unsigned long long* sh, int32_t* n_abn, int32_t* n_nor, int64_t* n_in);
+int mr_detect_sweep_launch(mr_ctx* ctx, const mr_spans* s, int64_t t_begin, int64_t grain, int64_t window, int32_t M,
+                           const double* d_a3, const uint8_t* d_a3v, uint8_t* d_state, unsigned long long* diff);
 // the window spectrum kernel alone, into a device slot of MR_WS_SLOT bytes (codes, scores, count);
 // MR_ERR_STATE when the window exceeds the one-block limits
 constexpr size_t MR_WS_SLOT = 12 * 256 + 16;

@@ -245,6 +245,89 @@ __global__ void __launch_bounds__(DB) k_ix_detect(int32_t NT, const int32_t* tle
         if (v) atomicAdd(&counts[(size_t)(blockIdx.x % CSH) * 3 + threadIdx.x], v);
     }
 }
+
+// ---------------------------------------------------------------- the driver's window sweep (f3)
+// online_rca.py:161-216 visits windows [t_begin + m*grain, + window] (m a whole number of grains:
+// the steps of 5 and 5 + 4 minutes are multiples of one minute).  With trace-level times constant
+// inside each trace a window selects whole traces and a trace's partition (abnormal / normal /
+// dropped) does not depend on the window: its rows are all in or all out, and real and expect are
+// sums over its own rows.  So each trace is classified ONCE and adds itself to the contiguous
+// range of window starts that contain it:
+//   t_begin + m*grain <= ts  and  te <= t_begin + m*grain + window
+//   <=>  ceil((te - window - t_begin) / grain) <= m <= floor((ts - t_begin) / grain),
+// as +1 / -1 at the range ends of three difference arrays (abnormal, normal, in-window rows);
+// a prefix sum over m then gives every window's detector counts.
+__device__ __forceinline__ int64_t floor_div(int64_t a, int64_t b) {   // b > 0
+    const int64_t q = a / b;
+    return (a % b != 0 && a < 0) ? q - 1 : q;
+}
+constexpr int SWB = 256, SWT = 16;        // threads per block, traces per thread
+constexpr int SW_LDS = 4096;              // window starts histogrammed in LDS (else global atomics)
+__global__ void __launch_bounds__(SWB) k_ix_sweep(int32_t NT, const int32_t* tlen, const long long* tts,
+                                                  const long long* tte, const long long* tmaxd, const int64_t* sv_off,
+                                                  const int32_t* sv_op, const int32_t* sv_cnt, const double* a3,
+                                                  const uint8_t* a3v, int64_t t_begin, int64_t grain, int64_t window,
+                                                  int32_t M, uint8_t* state, unsigned long long* diff) {
+    __shared__ uint32_t h[3 * (SW_LDS + 1)];
+    const bool lds = M + 1 <= SW_LDS + 1;
+    if (lds)
+        for (int i = threadIdx.x; i < 3 * (M + 1); i += SWB) h[i] = 0;
+    __syncthreads();
+    const int32_t tb = blockIdx.x * SWB * SWT;
+    for (int j = 0; j < SWT; ++j) {
+        const int32_t t = tb + j * SWB + threadIdx.x;
+        if (t >= NT) break;
+        int st = 0;
+        const int32_t n = tlen[t];
+        if (n > 0) {
+            const long long mx = tmaxd[t];
+            if (mx > 0) {   // grouped[grouped['duration'] > 0] (preprocess_data.py:117)
+                double expect = 0.0;
+                for (int64_t r = sv_off[t]; r < sv_off[t + 1]; ++r) {   // name order, no FMA (T14)
+                    const int32_t op = sv_op[r];
+                    if (a3v[op]) expect += (double)sv_cnt[r] * a3[op];  // anormaly_detector.py:64-65
+                }
+                st = (double)mx / 1000.0 > expect ? 2 : 1;            // :58, :69
+            }
+            state[t] = (uint8_t)st;
+            const int64_t hi = floor_div((int64_t)tts[t] - t_begin, grain);
+            const int64_t lo = max((int64_t)0, -floor_div(window + t_begin - (int64_t)tte[t], grain));   // ceil
+            if (hi >= lo && lo < M && hi >= 0) {
+                const int32_t a = (int32_t)lo, b = (int32_t)min(hi + 1, (int64_t)M);
+                // counters: 0 abnormal, 1 normal (a dropped trace counts only its rows), 2 rows
+                if (lds && n <= 65536) {   // (a block's partial stays below 2^31 in magnitude)
+                    if (st) {
+                        atomicAdd(&h[(st == 2 ? 0 : 1) * (M + 1) + a], 1u);
+                        atomicSub(&h[(st == 2 ? 0 : 1) * (M + 1) + b], 1u);
+                    }
+                    atomicAdd(&h[2 * (M + 1) + a], (uint32_t)n);
+                    atomicSub(&h[2 * (M + 1) + b], (uint32_t)n);
+                } else if (lds) {
+                    if (st) {
+                        atomicAdd(&h[(st == 2 ? 0 : 1) * (M + 1) + a], 1u);
+                        atomicSub(&h[(st == 2 ? 0 : 1) * (M + 1) + b], 1u);
+                    }
+                    atomicAdd(&diff[(size_t)2 * (M + 1) + a], (unsigned long long)n);
+                    atomicAdd(&diff[(size_t)2 * (M + 1) + b], (unsigned long long)(-(int64_t)n));
+                } else {
+                    if (st) {
+                        atomicAdd(&diff[(size_t)(st == 2 ? 0 : 1) * (M + 1) + a], 1ull);
+                        atomicAdd(&diff[(size_t)(st == 2 ? 0 : 1) * (M + 1) + b], ~0ull);   // -1 mod 2^64
+                    }
+                    atomicAdd(&diff[(size_t)2 * (M + 1) + a], (unsigned long long)n);
+                    atomicAdd(&diff[(size_t)2 * (M + 1) + b], (unsigned long long)(-(int64_t)n));
+                }
+            }
+        } else {
+            state[t] = 0;
+        }
+    }
+    if (!lds) return;
+    __syncthreads();
+    // per-block counts are exact mod 2^32; the sign-extended flush keeps the global sums exact
+    for (int i = threadIdx.x; i < 3 * (M + 1); i += SWB)
+        if (h[i]) atomicAdd(&diff[i], (unsigned long long)(int64_t)(int32_t)h[i]);
+}
 }  // namespace
 
 // (trace, code) runs of the rows: offsets per trace, code, count and (optionally) first row
@@ -433,5 +516,20 @@ int mr_detect_indexed(mr_ctx* ctx, const mr_spans* s, int64_t t0, int64_t t1, co
     MR_TRY(mr_read_bytes(ctx, counts.p, 3 * CSH * sizeof(unsigned long long), &h));
     mr_detect_sum((const unsigned long long*)h, n_abn, n_nor, n_in);
     if (*n_in == 0) return mr_fail(ctx, MR_ERR_VALUE, "Current span list is empty");
+    return MR_OK;
+}
+
+// f3: the detector counts of every window start t_begin + m * grain (m < M) in one pass over the
+// traces (k_ix_sweep); state[t] receives each trace's window-independent partition.  diff:
+// 3 * (M + 1) words zeroed by the caller (abnormal, normal, rows difference arrays).
+int mr_detect_sweep_launch(mr_ctx* ctx, const mr_spans* s, int64_t t_begin, int64_t grain, int64_t window, int32_t M,
+                           const double* d_a3, const uint8_t* d_a3v, uint8_t* d_state, unsigned long long* diff) {
+    const int32_t NT = s->n_traces;
+    if (!s->indexed || !s->uniform_times) return mr_fail(ctx, MR_ERR_STATE, "sweep needs trace-level window times");
+    if (NT)
+        hipLaunchKernelGGL(k_ix_sweep, dim3(cdiv(NT, SWB * SWT)), dim3(SWB), 0, ctx->stream, NT, s->tlen.p, s->tts.p,
+                           s->tte.p, s->tmaxd.p, s->sv_off.p, s->sv_op.p, s->sv_cnt.p, d_a3, d_a3v, t_begin, grain,
+                           window, M, d_state, diff);
+    MR_TRY_HIP(ctx, hipGetLastError());
     return MR_OK;
 }

@@ -97,14 +97,107 @@ def calculate_spectrum_without_delay_list(anomaly_result, normal_result, anomaly
     return top_list, score_list
 
 
-def online_anomaly_detect_RCA(data, slo, operation_list):
+def _write_result(top_list, score_list):
+    ranked = sorted(zip(top_list, score_list), key=lambda x: x[1], reverse=True)
+    with open("result.csv", "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["level", "result", "rank", "confidence"])
+        for rank, (service, score) in enumerate(ranked, start=1):
+            w.writerow(["span", service, rank, float(score)])
+
+
+def _sweep_plan(data, slo, start, end, window_normal, window_abnormal, ctx):
+    """the whole sweep of online_rca.py:161-216 detected on the device at once
+    (mr_detect_sweep).  Returns None when it does not apply (no datetime window columns, times
+    that vary within a trace, an empty frame) -- the per-window loop then runs instead."""
+    if len(data) == 0 or not all(np.issubdtype(data[c].dtype, np.datetime64) for c in ("startTime", "endTime")):
+        return None
+    if pd.isna(start) or pd.isna(end) or not start < end:
+        return None
+    step_n, step_a = int(window_normal.value), int(window_abnormal.value)
+    grain = math.gcd(step_n, step_n + step_a)   # every visited start is start + m * grain
+    t_begin = int(pd.Timestamp(start).value)
+    n_win = -(-(int(pd.Timestamp(end).value) - t_begin) // grain)   # starts with start + m*grain < end
+    if n_win <= 0 or n_win > 1 << 24:
+        return None
+    ctx = ctx or _lib.default_context()
+    table, dev = span_table(data, ctx)
+    a3, ok = slo_arrays(table, slo)
+    na, nn, rows = np.zeros(n_win, np.int32), np.zeros(n_win, np.int32), np.zeros(n_win, np.int64)
+    rc = _lib.load().mr_detect_sweep(ctx.h, dev.h, t_begin, grain, step_n, n_win, ptr(a3, C.c_double),
+                                     ptr(ok, C.c_uint8), None, ptr(na, C.c_int32), ptr(nn, C.c_int32),
+                                     ptr(rows, C.c_int64))
+    if rc == _lib.MR_ERR_STATE:
+        return None
+    ctx.check(rc, "mr_detect_sweep")
+    return dict(ctx=ctx, table=table, dev=dev, a3=a3, ok=ok, t_begin=t_begin, grain=grain, step_n=step_n // grain,
+                step_a=step_a // grain, n_win=n_win, na=na, nn=nn, rows=rows)
+
+
+def _sweep_run(plan):
+    """Walk the driver's window chain over the sweep's counts (only the counts decide the next
+    start), rank every triggered window in ONE mr_windows_batch call, then replay the driver's
+    output in window order; an empty window raises the reference's TypeError (T2) after the
+    output of the windows before it."""
+    events, m = [], 0
+    while m < plan["n_win"]:
+        if plan["rows"][m] == 0:
+            events.append(("empty", m))
+            break
+        na, nn = int(plan["na"][m]), int(plan["nn"][m])
+        ranked = na > 0 and nn > 0
+        events.append(("window", m, na, nn, ranked))
+        m += plan["step_n"] + (plan["step_a"] if ranked else 0)
+    todo = [e[1] for e in events if e[0] == "window" and e[4]]
+    width = plan["step_n"] * plan["grain"]
+    results = {}
+    if todo:
+        wins = [(plan["dev"], plan["t_begin"] + mm * plan["grain"], plan["t_begin"] + mm * plan["grain"] + width,
+                 plan["a3"], plan["ok"]) for mm in todo]
+        for mm, r in zip(todo, rank_windows(plan["ctx"], wins)):
+            results[mm] = r
+    names = plan["table"].podop_names
+    for e in events:
+        if e[0] == "empty":
+            print("Error: Current span list is empty ")
+            anomaly_flag, normal_list, abnormal_list = False   # noqa: F841 -- TypeError, as the reference (T2)
+        _, mm, na, nn, ranked = e
+        print("anormaly_trace", na)                       # anormaly_detector.py:74-76
+        print("total_trace", na + nn)
+        print()
+        if not na:
+            continue
+        print("anomaly_list", nn)                         # T1: the driver's abnormal_list is the
+        print("normal_list", na)                          # detector's normal list
+        print("total", na + nn)
+        if not ranked:
+            continue
+        codes, scores, r_na, r_nn, _edges, status = results[mm]
+        if status != _lib.MR_OK or (r_na, r_nn) != (na, nn):
+            raise RuntimeError(f"window {mm}: batch ranking disagrees with the sweep (status {status})")
+        top_list = [names[c] for c in codes] if names is not None else codes.tolist()
+        score_list = [np.float64(x) for x in scores]    # dstar2 over np.float64 weights
+        for node, sc in zip(top_list, score_list):
+            print("%-50s: %.8f" % (node, sc))             # online_rca.py:151
+        print(top_list, score_list)
+        _write_result(top_list, score_list)
+
+
+def online_anomaly_detect_RCA(data, slo, operation_list, *, ctx=None):
     """online_rca.online_anomaly_detect_RCA (online_rca.py:155-216): 5-minute windows, a triggered
     window advances by 9 minutes; the detector's lists are unpacked swapped (T1), an empty
-    window makes the unpacking raise TypeError (T2); result.csv is rewritten per trigger."""
+    window makes the unpacking raise TypeError (T2); result.csv is rewritten per trigger.
+
+    With trace-level window times (the renamed TraceStart/TraceEnd, online_rca.py:229-230) the
+    whole sweep runs as one device detector pass, one batched ranking of the triggered windows
+    and a replay of the output (f3, :func:`_sweep_run`); otherwise window by window."""
     window_normal = pd.Timedelta(minutes=5)
     window_abnormal = pd.Timedelta(minutes=4)
     start = data["startTime"].min()
     end = data["endTime"].max()
+    plan = _sweep_plan(data, slo, start, end, window_normal, window_abnormal, ctx)
+    if plan is not None:
+        return _sweep_run(plan)
     current_time = start
     while current_time < end:
         start_time = current_time
@@ -127,12 +220,7 @@ def online_anomaly_detect_RCA(data, slo, operation_list):
                 anomaly_list_len=len(abnormal_list), normal_list_len=len(normal_list), top_max=5,
                 anomaly_num_list=anomaly_num_list, normal_num_list=normal_num_list, spectrum_method="dstar2")
             print(top_list, score_list)
-            ranked = sorted(zip(top_list, score_list), key=lambda x: x[1], reverse=True)
-            with open("result.csv", "w", newline="") as f:
-                w = csv.writer(f)
-                w.writerow(["level", "result", "rank", "confidence"])
-                for rank, (service, score) in enumerate(ranked, start=1):
-                    w.writerow(["span", service, rank, float(score)])
+            _write_result(top_list, score_list)
             current_time += window_abnormal
         current_time += window_normal
 

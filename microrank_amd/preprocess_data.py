@@ -16,6 +16,7 @@ cached per DataFrame object (see :func:`span_table`).
 from __future__ import annotations
 
 import ctypes as C
+import os
 import sys
 import weakref
 from collections.abc import Mapping
@@ -25,7 +26,7 @@ import pandas as pd
 
 from . import _lib
 from ._lib import SpanCols, ptr
-from .spans import UI_SERVICE, SpanTable, op_display
+from .spans import UI_SERVICE, IngestedTable, SpanTable, _as_ns, arrow_columns, op_display
 
 ROOT_INDEX = "root"   # preprocess_data.py:7
 
@@ -33,6 +34,49 @@ ROOT_INDEX = "root"   # preprocess_data.py:7
 # ------------------------------------------------------------------------ span table cache
 class DeviceSpans:
     """An mr_spans handle: the span columns resident in HBM."""
+
+    @classmethod
+    def ingest(cls, ctx, df: pd.DataFrame, arrays):
+        """The table built on the device from the DataFrame's strings (mr_spans_ingest, SURVEY 8(f)
+        f2): factorisation, name rules and dictionaries in HBM.  Returns (IngestedTable, DeviceSpans)."""
+        lib = _lib.load()
+        S = len(df)
+        ss = _lib.SpanStrings()
+        ss.n_spans = S
+        keep = {"arrays": arrays}
+        for field, col in (("trace_id", "traceID"), ("span_id", "spanID"), ("parent_id", "ParentSpanId"),
+                           ("service", "serviceName"), ("operation", "operationName"), ("pod", "podName")):
+            a = arrays[col]
+            validity, offsets, data = a.buffers()[:3]
+            sc = getattr(ss, field)
+            if offsets is None:   # an all-null column (no ParentSpanId): zero offsets, no bytes
+                z = np.zeros(S + 1, np.int64)
+                keep[col] = z
+                sc.offsets = ptr(z, C.c_int64)
+                sc.bytes = None
+            else:
+                sc.offsets = C.cast(C.c_void_p(offsets.address + 8 * a.offset), C.POINTER(C.c_int64))
+                sc.bytes = data.address if data is not None and data.size else None
+            if a.null_count:
+                vb = np.unpackbits(np.frombuffer(validity, np.uint8), bitorder="little")[a.offset:a.offset + S]
+                v = np.packbits(vb, bitorder="little")
+                keep[col + ".valid"] = v
+                sc.valid = v.ctypes.data
+            else:
+                sc.valid = None
+        dur = np.ascontiguousarray(df["duration"].to_numpy(dtype=np.int64))
+        ss.duration = ptr(dur, C.c_int64)
+        ts = te = None
+        if "startTime" in df and "endTime" in df:
+            ts, te = np.ascontiguousarray(_as_ns(df["startTime"])), np.ascontiguousarray(_as_ns(df["endTime"]))
+            ss.tstart, ss.tend = ptr(ts, C.c_int64), ptr(te, C.c_int64)
+        h = _lib.P()
+        ctx.check(lib.mr_spans_ingest(ctx.h, C.byref(ss), C.byref(h)), "mr_spans_ingest")
+        dev = cls.__new__(cls)
+        dev.ctx, dev.h = ctx, h
+        table = IngestedTable(dev, arrays, dur, ts, te)
+        dev.table = table
+        return table, dev
 
     def __init__(self, ctx, table: SpanTable):
         lib = _lib.load()
@@ -70,6 +114,9 @@ class DeviceSpans:
 
 
 _CACHE: dict = {}
+# MR_HOST_FACTORIZE=1: factorise the DataFrame's strings on the host (SpanTable.from_dataframe)
+# instead of on the device (A/B and parity tests)
+_HOST_FACTORIZE = os.environ.get("MR_HOST_FACTORIZE", "") not in ("", "0")
 # every column SpanTable.from_dataframe reads: an in-place edit of any of them (the reference's own
 # get_operation_duration_data rewrites operationName, preprocess_data.py:100) must rebuild the table
 _TABLE_COLUMNS = ("traceID", "spanID", "ParentSpanId", "serviceName", "operationName", "podName", "duration",
@@ -97,8 +144,12 @@ def span_table(df: pd.DataFrame, ctx=None):
     hit = _CACHE.get(key)
     if hit is not None and hit[0]() is df and hit[1]() is ctx and hit[2] == fp:
         return hit[3], hit[4]
-    table = SpanTable.from_dataframe(df)
-    dev = DeviceSpans(ctx, table)
+    arrays = None if _HOST_FACTORIZE else arrow_columns(df)
+    if arrays is not None:   # strings -> codes on the device
+        table, dev = DeviceSpans.ingest(ctx, df, arrays)
+    else:                    # non-string / null-bearing columns: the host factorisation
+        table = SpanTable.from_dataframe(df)
+        dev = DeviceSpans(ctx, table)
     try:
         ref = weakref.ref(df, lambda _r, k=key: _CACHE.pop(k, None))
         cref = weakref.ref(ctx, lambda _r, k=key: _CACHE.pop(k, None))

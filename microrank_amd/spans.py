@@ -130,6 +130,136 @@ class SpanTable:
                    df["duration"].to_numpy(dtype=np.int64), tstart, tend, tnames, pnames, snames)
 
 
+# ------------------------------------------------------------------ device ingest
+_STR_COLS = ("traceID", "spanID", "ParentSpanId", "serviceName", "operationName", "podName")
+
+
+def arrow_columns(df):
+    """The string columns as Arrow large_string arrays (C++ conversion, no per-row Python), or
+    None when a column is not all strings or a required one has nulls (the host factorisation of
+    :meth:`SpanTable.from_dataframe` then builds the table)."""
+    try:
+        import pyarrow as pa
+    except ImportError:  # pragma: no cover
+        return None
+    if any(c not in df.columns for c in _STR_COLS if c != "ParentSpanId") or len(df) == 0:
+        return None
+    out = {}
+    for c in _STR_COLS:
+        if c not in df.columns:   # no ParentSpanId column: every span a root
+            out[c] = pa.nulls(len(df), type=pa.large_string())
+            continue
+        try:
+            a = pa.array(df[c], type=pa.large_string(), from_pandas=True)
+        except (pa.ArrowInvalid, pa.ArrowTypeError, TypeError):
+            return None
+        if isinstance(a, pa.ChunkedArray):
+            a = a.combine_chunks()
+        if c != "ParentSpanId" and a.null_count:
+            return None
+        out[c] = a
+    return out
+
+
+class IngestedTable:
+    """SpanTable-compatible view of a table built on the device from strings (mr_spans_ingest):
+    sizes and name lists come from the device dictionaries (the first row of each code); the code
+    columns are copied back only if something asks for them (PagerankGraph list materialisation)."""
+
+    def __init__(self, dev, arrays, duration, tstart, tend):
+        from . import _lib
+
+        self._dev, self._arrays = dev, arrays
+        self.duration, self.tstart, self.tend = duration, tstart, tend
+        self.meta, self.row = {}, None
+        S, nt, npo, nsv = C_i64(), C_i32(), C_i32(), C_i32()
+        _lib.load().mr_spans_info(dev.h, S, nt, npo, nsv)
+        self.n_spans, self.n_traces, self.n_podops, self.n_svcops = S.value, nt.value, npo.value, nsv.value
+        self._names = {}
+        self._codes = None
+
+    def _rows(self, which):
+        import ctypes as C
+
+        from . import _lib
+
+        n = (self.n_traces, self.n_podops, self.n_svcops)[which]
+        rows = np.zeros(max(n, 1), np.int32)
+        self._dev.ctx.check(_lib.load().mr_spans_dict_rows(self._dev.h, which, rows.ctypes.data_as(C.POINTER(C.c_int32))),
+                            "mr_spans_dict_rows")
+        return rows[:n]
+
+    def _op_names(self, rows):
+        import pyarrow as pa
+
+        idx = pa.array(rows)
+        svc = np.array(self._arrays["serviceName"].take(idx).to_pylist(), dtype=object)
+        op = np.array(self._arrays["operationName"].take(idx).to_pylist(), dtype=object)
+        return svc, op_display(svc, op)
+
+    @property
+    def trace_names(self):
+        if "trace" not in self._names:
+            import pyarrow as pa
+
+            self._names["trace"] = self._arrays["traceID"].take(pa.array(self._rows(0))).to_pylist()
+        return self._names["trace"]
+
+    @property
+    def podop_names(self):
+        if "podop" not in self._names:
+            import pyarrow as pa
+
+            rows = self._rows(1)
+            _, op = self._op_names(rows)
+            pod = self._arrays["podName"].take(pa.array(rows)).to_pylist()
+            self._names["podop"] = [f"{a}_{b}" for a, b in zip(pod, op)]
+        return self._names["podop"]
+
+    @property
+    def svcop_names(self):
+        if "svcop" not in self._names:
+            rows = self._rows(2)
+            svc, op = self._op_names(rows)
+            self._names["svcop"] = [f"{a}_{b}" for a, b in zip(svc, op)]
+        return self._names["svcop"]
+
+    def _code_cols(self):
+        if self._codes is None:
+            import ctypes as C
+
+            from . import _lib
+
+            S = self.n_spans
+            cols = [np.empty(S, np.int32), np.empty(S, np.int32), np.empty(S, np.int32), np.empty(S, np.int64),
+                    np.empty(S, np.int64)]
+            ptrs = [a.ctypes.data_as(C.POINTER(C.c_int32 if a.dtype == np.int32 else C.c_int64)) for a in cols]
+            self._dev.ctx.check(_lib.load().mr_spans_codes(self._dev.h, *ptrs), "mr_spans_codes")
+            self._codes = cols
+        return self._codes
+
+    trace = property(lambda self: self._code_cols()[0])
+    podop = property(lambda self: self._code_cols()[1])
+    svcop = property(lambda self: self._code_cols()[2])
+    span = property(lambda self: self._code_cols()[3])
+    parent = property(lambda self: self._code_cols()[4])
+
+    def check(self) -> None:
+        pass
+
+
+def C_i64():
+    import ctypes as C
+
+    return C.c_int64()
+
+
+def C_i32():
+    import ctypes as C
+
+    return C.c_int32()
+
+
 def _as_ns(col) -> np.ndarray:
     import pandas as pd
 

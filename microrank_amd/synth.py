@@ -274,6 +274,28 @@ def window_dataframes(n_ops: int, n_traces: int, seed: int, **kw):
     return to_dataframe(normal, topo, seed + 1), to_dataframe(abnormal, topo, seed + 2)
 
 
+def stream_dataframes(n_ops: int, n_traces: int, seed: int, *, minutes: float = 60.0, fault_frac: float = 0.003,
+                      gap_after_min: Optional[float] = None, gap_min: float = 0.0, **kw):
+    """A long span stream for the driver's window sweep (online_rca.py:161-216): normal frame for
+    the SLO and an abnormal frame of ``minutes`` of traffic with a rare fault, so that some 5-minute
+    windows trigger and some do not.  ``gap_after_min``: traces starting that many minutes after
+    the first one are shifted ``gap_min`` minutes later (a silent gap: an empty window, T2)."""
+    ndf, adf = window_dataframes(n_ops, n_traces, seed, minutes=minutes, fault_frac=fault_frac, **kw)
+    if gap_after_min is not None:
+        cut = adf["startTime"].min() + pd_timedelta(minutes=gap_after_min)
+        late = adf["startTime"] >= cut
+        shift = pd_timedelta(minutes=gap_min)
+        adf.loc[late, "startTime"] = adf.loc[late, "startTime"] + shift
+        adf.loc[late, "endTime"] = adf.loc[late, "endTime"] + shift
+    return ndf, adf
+
+
+def pd_timedelta(**kw):
+    import pandas as pd
+
+    return pd.Timedelta(**kw)
+
+
 def frame_digest(df) -> str:
     """sha256 over the reference-schema columns, so a fixture can check that the
     generator re-created exactly the frame the reference was run on."""

@@ -486,6 +486,26 @@ def detect(trace: np.ndarray, svcop: np.ndarray, duration: np.ndarray, tstart, t
     return bool(ab), ab, no
 
 
+def driver_sweep(trace, svcop, duration, tstart, tend, slo_mean_plus3std: Dict[int, float], *,
+                 step_normal: int = 5 * 60 * 10**9, step_abnormal: int = 4 * 60 * 10**9):
+    """The window chain of online_rca.online_anomaly_detect_RCA (online_rca.py:161-216): windows
+    [t, t + 5 min] from min(startTime) while t < max(endTime); a window whose detector flags an
+    anomaly with both lists non-empty is ranked and the next starts 9 minutes later, otherwise 5
+    (:170-178, :215-216).  Returns [(t0, flag, abnormal codes, normal codes, ranked)] and True
+    when the chain ended in an empty window (the detector's False: the driver's TypeError, T2)."""
+    t, end = int(tstart.min()), int(tend.max())
+    out = []
+    while t < end:
+        r = detect(trace, svcop, duration, tstart, tend, t, t + step_normal, slo_mean_plus3std)
+        if r is None:
+            return out, True
+        flag, ab, no = r
+        ranked = bool(flag and ab and no)
+        out.append((t, flag, ab, no, ranked))
+        t += step_normal + (step_abnormal if ranked else 0)
+    return out, False
+
+
 # ----------------------------------------------------------------------------- trace sharding
 def sharded_pagerank(g: Graph, comm, anomaly: bool, d: float = D_DEFAULT, alpha: float = ALPHA_DEFAULT,
                      iters: int = ITERS_DEFAULT):

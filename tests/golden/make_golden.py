@@ -241,8 +241,53 @@ def span_times_case(outdir):
     span_case("span_times", dict(n_ops=40, n_traces=1500, seed=400, span_times=True, minutes=5.2), outdir)
 
 
+STREAM_CASES = {
+    # 60 minutes of traffic, a rare fault: a mix of quiet, triggered and one-list-empty windows
+    "stream": dict(n_ops=40, n_traces=6000, seed=500, minutes=60.0, fault_frac=0.006),
+    # the same with a silent 15-minute gap after minute 30: the sweep ends in the empty-window
+    # TypeError (T2) after the windows before it
+    "stream_gap": dict(n_ops=40, n_traces=6000, seed=510, minutes=60.0, fault_frac=0.003, gap_after_min=30.0,
+                       gap_min=15.0),
+}
+
+
+def stream_case(name, params, outdir):
+    """The reference driver over a multi-window stream (online_rca.py:161-216): stdout, error and
+    result.csv."""
+    ndf, adf = synth.stream_dataframes(**params)
+    span_df = ndf.copy()
+    op_list = ref_pp.get_service_operation_list(span_df)
+    slo = ref_pp.get_operation_slo(op_list, span_df)
+    res = {"name": name, "params": params, "operation_list": op_list,
+           "slo": {k: [fhex(v[0]), fhex(v[1])] for k, v in slo.items()}}
+    cwd = os.getcwd()
+    t0 = time.perf_counter()
+    with tempfile.TemporaryDirectory() as td:
+        os.chdir(td)
+        buf = io.StringIO()
+        try:
+            with contextlib.redirect_stdout(buf):
+                ref_rca.online_anomaly_detect_RCA(adf.copy(), slo, op_list)
+            res["driver_error"] = None
+        except Exception as e:
+            res["driver_error"] = type(e).__name__
+        res["driver_stdout"] = buf.getvalue()
+        res["result_csv"] = open("result.csv").read() if os.path.exists("result.csv") else None
+        os.chdir(cwd)
+    res["timing_s"] = time.perf_counter() - t0
+    res["input_digest"] = {"normal": synth.frame_digest(ndf), "abnormal": synth.frame_digest(adf)}
+    with open(os.path.join(outdir, f"{name}.json"), "w") as f:
+        json.dump(res, f, indent=0)
+    print(name, "traces", adf.traceID.nunique(), "error", res["driver_error"], "windows ranked",
+          res["driver_stdout"].count("anomaly_list"), "time %.1fs" % res["timing_s"])
+
+
 def main():
     outdir = HERE
+    if sys.argv[1:] == ["stream"]:
+        for name, params in STREAM_CASES.items():
+            stream_case(name, params, outdir)
+        return
     if sys.argv[1:] == ["slo_large"]:
         slo_large(outdir)
         return
@@ -312,6 +357,8 @@ def main():
     slo_large(outdir)
     span_case("ops200", dict(n_ops=200, n_traces=1500, seed=300, branch=1.9, p_max=0.8, fault_ms=6000.0), outdir, driver=False)
     span_times_case(outdir)
+    for name, params in STREAM_CASES.items():
+        stream_case(name, params, outdir)
     with open(os.path.join(outdir, "manifest.json"), "w") as f:
         json.dump(man, f, indent=1, sort_keys=True)
 

@@ -159,18 +159,41 @@ def test_empty_window_returns_false_and_driver_raises():
         online_anomaly_detect_RCA(long, {}, [])
 
 
-@pytest.mark.parametrize("name", ["c1", "pods_dup_broken", "span_times"])
+def _run_driver(adf, case, sweep=True, monkeypatch=None):
+    """stdout and error type of the drop-in driver (the window sweep on the device, or window by
+    window with ``sweep=False``)."""
+    from microrank_amd import online_rca
+
+    slo = {k: [np.float64(float.fromhex(a)), np.float64(float.fromhex(b))] for k, (a, b) in case["slo"].items()}
+    if not sweep:
+        monkeypatch.setattr(online_rca, "_sweep_plan", lambda *a, **k: None)
+    buf = io.StringIO()
+    err = None
+    try:
+        with contextlib.redirect_stdout(buf):
+            online_rca.online_anomaly_detect_RCA(adf.copy(), slo, case["operation_list"])
+    except TypeError as e:
+        err = type(e).__name__
+    return buf.getvalue(), err
+
+
+@pytest.mark.parametrize("name", ["c1", "pods_dup_broken", "span_times", "stream", "stream_gap"])
 def test_driver_matches_reference(name, tmp_path, monkeypatch):
-    from microrank_amd.online_rca import online_anomaly_detect_RCA
+    """The driver's stdout / result.csv / error against the reference's.  c1 and pods_dup_broken,
+    stream and stream_gap (multi-window, one ending in the empty-window TypeError) run as one
+    device sweep (mr_detect_sweep + mr_windows_batch); span_times (per-span times) window by window."""
+    from microrank_amd import synth
 
     case = load_golden(f"{name}.json")
-    _, adf = regen_window(case)
-    slo = {k: [np.float64(float.fromhex(a)), np.float64(float.fromhex(b))] for k, (a, b) in case["slo"].items()}
+    if name.startswith("stream"):
+        _, adf = synth.stream_dataframes(**case["params"])
+        assert synth.frame_digest(adf) == case["input_digest"]["abnormal"]
+    else:
+        _, adf = regen_window(case)
     monkeypatch.chdir(tmp_path)
-    buf = io.StringIO()
-    with contextlib.redirect_stdout(buf):
-        online_anomaly_detect_RCA(adf.copy(), slo, case["operation_list"])
-    got = buf.getvalue().splitlines()
+    out, err = _run_driver(adf, case)
+    assert err == case.get("driver_error")
+    got = out.splitlines()
     exp = case["driver_stdout"].splitlines()
     assert len(got) == len(exp)
     for g, x in zip(got, exp):
@@ -182,6 +205,9 @@ def test_driver_matches_reference(name, tmp_path, monkeypatch):
             np.testing.assert_allclose(gs, xs, rtol=1e-10)
         else:
             assert g == x
+    if case["result_csv"] is None:
+        assert not os.path.exists("result.csv")
+        return
     got_csv = open("result.csv").read().splitlines()
     exp_csv = case["result_csv"].splitlines()
     assert len(got_csv) == len(exp_csv)
@@ -190,6 +216,72 @@ def test_driver_matches_reference(name, tmp_path, monkeypatch):
         assert gp[:-1] == xp[:-1]
         if gp[-1] != "confidence":
             assert math.isclose(float(gp[-1]), float(xp[-1]), rel_tol=1e-10)
+
+
+@pytest.mark.parametrize("name", ["stream", "stream_gap"])
+def test_driver_sweep_equals_window_loop(name, tmp_path, monkeypatch):
+    """f3: the device sweep prints exactly what the window-by-window driver prints (same windows,
+    same counts, same rankings), and writes the same result.csv."""
+    from microrank_amd import synth
+
+    case = load_golden(f"{name}.json")
+    _, adf = synth.stream_dataframes(**case["params"])
+    (tmp_path / "a").mkdir()
+    (tmp_path / "b").mkdir()
+    monkeypatch.chdir(tmp_path / "a")
+    out_a, err_a = _run_driver(adf, case)
+    monkeypatch.chdir(tmp_path / "b")
+    out_b, err_b = _run_driver(adf, case, sweep=False, monkeypatch=monkeypatch)
+    assert out_a == out_b and err_a == err_b
+    csv_a, csv_b = tmp_path / "a" / "result.csv", tmp_path / "b" / "result.csv"
+    assert csv_a.exists() == csv_b.exists()
+    if csv_a.exists():
+        assert csv_a.read_text() == csv_b.read_text()
+
+
+def test_detect_sweep_counts_equal_per_window_detector():
+    """mr_detect_sweep: every 1-minute window start's counts and the per-trace partition equal the
+    per-window detector (mr_detect) and the numpy oracle, over a 60-minute stream with a gap."""
+    import ctypes as C
+
+    import oracle as orc
+    from microrank_amd import _lib, synth
+    from microrank_amd._lib import ptr
+    from microrank_amd.anormaly_detector import detect_states, slo_arrays
+    from microrank_amd.preprocess_data import span_table
+
+    case = load_golden("stream_gap.json")
+    _, adf = synth.stream_dataframes(**case["params"])
+    slo = {k: [np.float64(float.fromhex(a)), np.float64(float.fromhex(b))] for k, (a, b) in case["slo"].items()}
+    ctx = _lib.default_context()
+    table, dev = span_table(adf, ctx)
+    a3, ok = slo_arrays(table, slo)
+    grain, width = 60 * 10**9, 5 * 60 * 10**9
+    t_begin = int(table.tstart.min())
+    M = -(-(int(table.tend.max()) - t_begin) // grain)
+    na, nn, rows = np.zeros(M, np.int32), np.zeros(M, np.int32), np.zeros(M, np.int64)
+    state = np.zeros(table.n_traces, np.uint8)
+    ctx.check(_lib.load().mr_detect_sweep(ctx.h, dev.h, t_begin, grain, width, M, ptr(a3, C.c_double),
+                                          ptr(ok, C.c_uint8), ptr(state, C.c_uint8), ptr(na, C.c_int32),
+                                          ptr(nn, C.c_int32), ptr(rows, C.c_int64)), "mr_detect_sweep")
+    a3d = {c: float(a3[c]) for c in range(len(a3)) if ok[c]}
+    n_empty = 0
+    for m in range(M):
+        t0 = t_begin + m * grain
+        inwin = (table.tstart >= t0) & (table.tend <= t0 + width)
+        assert rows[m] == int(inwin.sum()), m
+        res = detect_states(adf, pd.Timestamp(t0), pd.Timestamp(t0 + width), slo, ctx=ctx)
+        ref = orc.detect(table.trace, table.svcop, table.duration, table.tstart, table.tend, t0, t0 + width, a3d)
+        if res is None:
+            assert rows[m] == 0 and ref is None
+            n_empty += 1
+            continue
+        st, a_, n_, _ = res
+        assert (na[m], nn[m]) == (a_, n_) == (len(ref[1]), len(ref[2])), m
+        tw = np.zeros(table.n_traces, bool)
+        tw[table.trace[inwin]] = True
+        assert np.array_equal(np.where(tw, state, 0), st), m   # the window's partition is the global one
+    assert n_empty > 0 and (na > 0).any()
 
 
 @pytest.mark.parametrize("name", ["c1", "pods_dup_broken", "ops200", "span_times"])

@@ -216,3 +216,30 @@ def test_slo_large_ops_numpy_buffering():
     slo = orc.operation_slo(st.svcop, st.duration, st.svcop_names, case["operation_list"])
     assert {k: [float(v[0]).hex(), float(v[1]).hex()] for k, v in slo.items()} == case["slo"]
     assert list(slo) == sorted(case["slo"])
+
+
+@pytest.mark.parametrize("name", ["stream", "stream_gap"])
+def test_driver_sweep_matches_reference(name):
+    """The oracle's window chain (online_rca.py:161-216) reproduces every detector line of the
+    reference driver over a multi-window stream, and where it ends (T2)."""
+    from microrank_amd import synth
+
+    case = load_golden(f"{name}.json")
+    ndf, adf = synth.stream_dataframes(**case["params"])
+    assert synth.frame_digest(ndf) == case["input_digest"]["normal"], "generator drifted (normal)"
+    assert synth.frame_digest(adf) == case["input_digest"]["abnormal"], "generator drifted (abnormal)"
+    ast = _spans(adf)
+    slo = {k: (float.fromhex(a), float.fromhex(b)) for k, (a, b) in case["slo"].items()}
+    a3 = {c: slo[n][0] + 3 * slo[n][1] for c, n in enumerate(ast.svcop_names) if n in slo}
+    events, empty = orc.driver_sweep(ast.trace, ast.svcop, ast.duration, ast.tstart, ast.tend, a3)
+    lines = []
+    for _t, flag, ab, no, _ranked in events:
+        lines += [f"anormaly_trace {len(ab)}", f"total_trace {len(ab) + len(no)}"]
+        if flag:
+            lines += [f"anomaly_list {len(no)}", f"normal_list {len(ab)}"]
+    if empty:
+        lines.append("Error: Current span list is empty")
+    exp = [ln.rstrip() for ln in case["driver_stdout"].splitlines()
+           if ln.startswith(("anormaly_trace", "total_trace", "anomaly_list", "normal_list", "Error"))]
+    assert lines == exp
+    assert empty == (case["driver_error"] == "TypeError")
