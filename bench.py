@@ -365,6 +365,155 @@ def run_c4(args, world, rank, dist):
     return out
 
 
+def run_sweep(args):
+    """SURVEY 8(f) f3 -- the driver's window sweep over a long resident span stream (C3-shaped
+    traffic: 500 ops, 20k traces per 5 minutes).  A step is the whole online_anomaly_detect_RCA
+    chain (online_rca.py:161-216) on the device: one mr_detect_sweep pass for every window start,
+    the chain walk, ONE mr_windows_batch over its triggered windows.  Beside it: every 1-minute
+    sliding window of the stream ranked over the same resident table (C3's "sliding windows"), and
+    the window-by-window loop of round 1 (mr_detect + mr_rca_window per visited window)."""
+    import ctypes as C
+
+    from microrank_amd import _lib, synth
+    from microrank_amd._lib import ptr
+    from microrank_amd.online_rca import rank_windows, sweep_chain, sweep_plan, sweep_rank
+    from microrank_amd.preprocess_data import DeviceSpans
+
+    minutes = args.sweep_minutes
+    n_tr = int(4000 * minutes)
+    topo = synth.make_topology(500, 1234)
+    normal = synth.gen_spans(topo, 20_000, 1235, branch=1.9, p_max=0.8, names=False)
+    stream = synth.gen_spans(topo, n_tr, 1236, minutes=minutes / 0.97, branch=1.9, p_max=0.8, names=False,
+                             fault_op=synth.fault_op_of(topo), fault_frac=args.sweep_fault, fault_ms=6000.0)
+    ctx = _lib.default_context()
+    a3, ok = slo_from_gpu(ctx, normal)
+    dev = DeviceSpans(ctx, stream)
+    t_begin, t_end = int(stream.tstart.min()), int(stream.tend.max())
+    step_n, step_a = 5 * 60 * 10**9, 4 * 60 * 10**9
+
+    def driver_step():
+        plan = sweep_plan(ctx, stream, dev, a3, ok, t_begin, t_end, step_n, step_a)
+        ev = sweep_chain(plan)
+        res = sweep_rank(plan, ev)
+        return ev, res
+
+    for _ in range(args.warmup):
+        driver_step()
+    ctx.sync()
+    ts = time.perf_counter()
+    for _ in range(args.steps):
+        ev, res = driver_step()
+    ctx.sync()
+    dt = (time.perf_counter() - ts) / args.steps
+    visited = sum(1 for e in ev if e[0] == "window")
+    ranked = len(res)
+    # the round-1 loop: the detector of each visited window, then mr_rca_window for the triggered ones
+    lib = _lib.load()
+    state = np.zeros(stream.n_traces, np.uint8)
+
+    def loop_step():
+        t, out = t_begin, 0
+        na, nn, nin = C.c_int32(), C.c_int32(), C.c_int64()
+        while t < t_end:
+            rc = lib.mr_detect(ctx.h, dev.h, t, t + step_n, ptr(a3, C.c_double), ptr(ok, C.c_uint8),
+                               ptr(state, C.c_uint8), C.byref(na), C.byref(nn), C.byref(nin))
+            if rc == _lib.MR_ERR_VALUE and nin.value == 0:
+                break
+            ctx.check(rc, "mr_detect")
+            trig = na.value > 0 and nn.value > 0
+            if trig:
+                run_window(ctx, dev, t, t + step_n, a3, ok, 0)
+                out += 1
+            t += step_n + (step_a if trig else 0)
+        return out
+
+    loop_step()
+    ts = time.perf_counter()
+    n_loop = loop_step()
+    ctx.sync()
+    dt_loop = time.perf_counter() - ts
+    assert n_loop == ranked
+    # every 1-minute sliding window of the stream, ranked in calls of 64 over the one resident table
+    grain = 60 * 10**9
+    starts = [t for t in range(t_begin, t_end - step_n + 1, grain)]
+    wins = [(dev, t, t + step_n, a3, ok) for t in starts]
+    rank_windows(ctx, wins[:64])
+    ctx.sync()
+    ts = time.perf_counter()
+    n_ok = 0
+    for i in range(0, len(wins), 64):
+        n_ok += sum(1 for r in rank_windows(ctx, wins[i:i + 64]) if r[5] == _lib.MR_OK and r[1].size)
+    ctx.sync()
+    dt_slide = time.perf_counter() - ts
+    return {"metric": "RCA driver sweep: windows ranked/sec (SURVEY 8(f) f3)", "value": round(ranked / dt, 2),
+            "unit": "windows/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(dt * 1e3, 3), "higher_is_better": True, "scaling": "none", "vs_baseline": None,
+            "dtype": "f64", "data": "synthetic (seeded C3-shaped span stream, int-coded, resident in HBM)",
+            "config": {"workload": f"online_anomaly_detect_RCA over {minutes:.0f} minutes of traffic: 500 ops, "
+                                   f"{n_tr} traces, {stream.n_spans} spans, fault in {args.sweep_fault:.1%} of traces",
+                       "windows_visited": visited, "windows_ranked": ranked, "window_starts_swept": int(plan_starts(t_begin, t_end))},
+            "visited_per_s": round(visited / dt, 2),
+            "window_loop": {"what": "round-1 loop: mr_detect per visited window + mr_rca_window per triggered one",
+                            "ms": round(dt_loop * 1e3, 3), "windows_ranked_per_s": round(n_loop / dt_loop, 2),
+                            "speedup_of_sweep": round(dt_loop / dt, 2)},
+            "sliding": {"what": "every 1-minute window start of the stream ranked (mr_windows_batch, 64 per call, "
+                                "one resident table)", "windows": len(wins), "ranked": n_ok,
+                        "windows_per_s": round(len(wins) / dt_slide, 2)}}
+
+
+def plan_starts(t_begin, t_end, grain=60 * 10**9):
+    return -(-(t_end - t_begin) // grain)
+
+
+def run_ingest(args):
+    """SURVEY 8(f) f2 -- span ingest: the C2 window's reference-schema DataFrame (strings) into
+    the device span table.  A step is mr_spans_ingest on the DataFrame's Arrow string buffers
+    (host memory: the copy over PCIe is inside the time) incl. the table's per-trace index; the
+    CPU baseline is the pandas factorisation it replaces (SpanTable.from_dataframe)."""
+    from microrank_amd import _lib, synth
+    from microrank_amd.preprocess_data import DeviceSpans
+    from microrank_amd.spans import SpanTable, arrow_columns
+
+    topo, normal, abnormal = synth.window_pair(args.ops, args.traces, 1234, branch=1.9, p_max=0.8, fault_ms=6000.0)
+    df = synth.to_dataframe(abnormal, topo, 1236)
+    S = len(df)
+    ts = time.perf_counter()
+    arrays = arrow_columns(df)
+    t_arrow = time.perf_counter() - ts
+    ctx = _lib.default_context()
+    for _ in range(args.warmup):
+        t, d = DeviceSpans.ingest(ctx, df, arrays)
+        d.close()
+    ctx.sync()
+    ts = time.perf_counter()
+    for _ in range(args.steps):
+        t, d = DeviceSpans.ingest(ctx, df, arrays)
+        if _ != args.steps - 1:
+            d.close()
+    ctx.sync()
+    dt = (time.perf_counter() - ts) / args.steps
+    ts = time.perf_counter()
+    host = SpanTable.from_dataframe(df)
+    dt_host = time.perf_counter() - ts
+    same = bool(np.array_equal(t.trace, host.trace) and np.array_equal(t.podop, host.podop) and
+                np.array_equal(t.svcop, host.svcop) and list(t.podop_names) == list(host.podop_names))
+    str_bytes = sum(int(a.buffers()[2].size) if a.buffers()[2] is not None else 0 for a in arrays.values())
+    in_bytes = str_bytes + 6 * 8 * (S + 1) + 3 * 8 * S
+    d.close()
+    return {"metric": "span ingest: spans/sec, strings -> device span table (SURVEY 8(f) f2)",
+            "value": round(S / dt / 1e6, 3), "unit": "Mspans/s", "n_gpus": 1, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(dt * 1e3, 3), "higher_is_better": True, "scaling": "none",
+            "vs_baseline": None, "dtype": "u8/int64", "data": "synthetic (C2 window as the reference's string schema)",
+            "config": {"workload": f"C2 window DataFrame: {S} spans, {abnormal.n_traces} traces, {len(host.podop_names)} "
+                                   f"pod-ops; input {in_bytes / 1e6:.1f} MB of Arrow buffers in host memory",
+                       "pcie_inclusive": True},
+            "arrow_ms": round(t_arrow * 1e3, 3), "codes_equal_host": same,
+            "input_GBps": round(in_bytes / dt / 1e9, 2),
+            "cpu_baseline": {"value": round(S / dt_host / 1e6, 3), "unit": "Mspans/s", "cores": 1, "kind": "port",
+                             "sample": "SpanTable.from_dataframe (pandas factorize of the same DataFrame), once",
+                             "ms": round(dt_host * 1e3, 1)}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -382,10 +531,13 @@ def main():
     ap.add_argument("--streams-mode", action="store_true",
                     help="c2/c3: W contexts + W host threads, one mr_rca_window per window (instead of mr_windows_batch)")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
-    ap.add_argument("--config", choices=["c2", "c3", "c4", "c5"], default="c2",
+    ap.add_argument("--config", choices=["c2", "c3", "c4", "c5", "sweep", "ingest"], default="c2",
                     help="c2: RCA windows (default, weak scaling); c3: a batch of --c3-windows 500-op / 20k-trace "
                          "windows split over the ranks (strong scaling); c4 / c5: one trace-sharded graph (strong "
-                         "scaling; c5 = 100k ops / 100M traces fp32, the wide fused iteration)")
+                         "scaling; c5 = 100k ops / 100M traces fp32, the wide fused iteration); sweep: the driver's "
+                         "window sweep over a long stream (f3); ingest: strings -> device span table (f2)")
+    ap.add_argument("--sweep-minutes", type=float, default=240.0, help="sweep: minutes of traffic in the stream")
+    ap.add_argument("--sweep-fault", type=float, default=0.00005, help="sweep: fraction of traces hit by the fault")
     ap.add_argument("--c3-windows", type=int, default=4096, help="c3: windows in the whole batch (all ranks)")
     ap.add_argument("--c3-distinct", type=int, default=4,
                     help="c3: distinct seeded windows resident per stream (the batch cycles through them)")
@@ -414,7 +566,7 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # PMC passes first, in child processes, before this process initialises the GPU
     traffic = None
-    if world == 1 and not args.pmc_child and not args.no_traffic:
+    if world == 1 and not args.pmc_child and not args.no_traffic and args.config not in ("sweep", "ingest"):
         traffic = pmc_traffic(args, timeout_s=240 if args.config in ("c2", "c3") else 400)
     dist = None
     if world > 1:
@@ -422,6 +574,14 @@ def main():
 
         dist.init_process_group("gloo")
     os.environ.setdefault("MICRORANK_DEVICE", str(local))
+    if args.config in ("sweep", "ingest"):   # single-GPU supplementary lines (f2 / f3)
+        if args.config == "ingest" and "--steps" not in sys.argv:
+            args.steps, args.warmup = 5, 1
+        if args.config == "sweep" and "--steps" not in sys.argv:
+            args.steps, args.warmup = 3, 1
+        out = (run_sweep if args.config == "sweep" else run_ingest)(args)
+        print(json.dumps(out), flush=True)
+        return
     if args.config in ("c4", "c5"):
         out = run_c4(args, world, rank, dist)
         if out is not None and traffic is not None:

@@ -106,39 +106,30 @@ def _write_result(top_list, score_list):
             w.writerow(["span", service, rank, float(score)])
 
 
-def _sweep_plan(data, slo, start, end, window_normal, window_abnormal, ctx):
-    """the whole sweep of online_rca.py:161-216 detected on the device at once
-    (mr_detect_sweep).  Returns None when it does not apply (no datetime window columns, times
-    that vary within a trace, an empty frame) -- the per-window loop then runs instead."""
-    if len(data) == 0 or not all(np.issubdtype(data[c].dtype, np.datetime64) for c in ("startTime", "endTime")):
-        return None
-    if pd.isna(start) or pd.isna(end) or not start < end:
-        return None
-    step_n, step_a = int(window_normal.value), int(window_abnormal.value)
-    grain = math.gcd(step_n, step_n + step_a)   # every visited start is start + m * grain
-    t_begin = int(pd.Timestamp(start).value)
-    n_win = -(-(int(pd.Timestamp(end).value) - t_begin) // grain)   # starts with start + m*grain < end
+def sweep_plan(ctx, table, dev, a3, ok, t_begin: int, t_end: int, step_normal: int, step_abnormal: int):
+    """SURVEY 8(f) f3 on a resident span table: the detector counts of every window start the
+    driver's chain can reach (online_rca.py:161-216: starts t_begin + m * grain while < t_end,
+    grain = gcd of the two steps) from ONE device pass (mr_detect_sweep).  None when the table's
+    window times vary within a trace (the per-window loop applies then)."""
+    grain = math.gcd(step_normal, step_normal + step_abnormal)
+    n_win = -(-(t_end - t_begin) // grain)
     if n_win <= 0 or n_win > 1 << 24:
         return None
-    ctx = ctx or _lib.default_context()
-    table, dev = span_table(data, ctx)
-    a3, ok = slo_arrays(table, slo)
     na, nn, rows = np.zeros(n_win, np.int32), np.zeros(n_win, np.int32), np.zeros(n_win, np.int64)
-    rc = _lib.load().mr_detect_sweep(ctx.h, dev.h, t_begin, grain, step_n, n_win, ptr(a3, C.c_double),
+    rc = _lib.load().mr_detect_sweep(ctx.h, dev.h, t_begin, grain, step_normal, n_win, ptr(a3, C.c_double),
                                      ptr(ok, C.c_uint8), None, ptr(na, C.c_int32), ptr(nn, C.c_int32),
                                      ptr(rows, C.c_int64))
     if rc == _lib.MR_ERR_STATE:
         return None
     ctx.check(rc, "mr_detect_sweep")
-    return dict(ctx=ctx, table=table, dev=dev, a3=a3, ok=ok, t_begin=t_begin, grain=grain, step_n=step_n // grain,
-                step_a=step_a // grain, n_win=n_win, na=na, nn=nn, rows=rows)
+    return dict(ctx=ctx, table=table, dev=dev, a3=a3, ok=ok, t_begin=t_begin, grain=grain,
+                step_n=step_normal // grain, step_a=step_abnormal // grain, n_win=n_win, na=na, nn=nn, rows=rows)
 
 
-def _sweep_run(plan):
-    """Walk the driver's window chain over the sweep's counts (only the counts decide the next
-    start), rank every triggered window in ONE mr_windows_batch call, then replay the driver's
-    output in window order; an empty window raises the reference's TypeError (T2) after the
-    output of the windows before it."""
+def sweep_chain(plan):
+    """Walk the driver's window chain over the sweep's counts -- only the counts decide the next
+    start: ("window", m, n_abnormal, n_normal, ranked) per visited window, ("empty", m) where the
+    reference's detector returns False (T2) and the chain stops."""
     events, m = [], 0
     while m < plan["n_win"]:
         if plan["rows"][m] == 0:
@@ -148,14 +139,40 @@ def _sweep_run(plan):
         ranked = na > 0 and nn > 0
         events.append(("window", m, na, nn, ranked))
         m += plan["step_n"] + (plan["step_a"] if ranked else 0)
+    return events
+
+
+def sweep_rank(plan, events, precision="fp64"):
+    """Every ranked window of the chain in ONE mr_windows_batch call: {m: (codes, scores, ...)}."""
     todo = [e[1] for e in events if e[0] == "window" and e[4]]
     width = plan["step_n"] * plan["grain"]
-    results = {}
-    if todo:
-        wins = [(plan["dev"], plan["t_begin"] + mm * plan["grain"], plan["t_begin"] + mm * plan["grain"] + width,
-                 plan["a3"], plan["ok"]) for mm in todo]
-        for mm, r in zip(todo, rank_windows(plan["ctx"], wins)):
-            results[mm] = r
+    if not todo:
+        return {}
+    wins = [(plan["dev"], plan["t_begin"] + mm * plan["grain"], plan["t_begin"] + mm * plan["grain"] + width,
+             plan["a3"], plan["ok"]) for mm in todo]
+    return dict(zip(todo, rank_windows(plan["ctx"], wins, precision=precision)))
+
+
+def _sweep_plan(data, slo, start, end, window_normal, window_abnormal, ctx):
+    """The driver's sweep plan for a DataFrame (None: not applicable -- no datetime window columns,
+    an empty frame, or times that vary within a trace)."""
+    if len(data) == 0 or not all(np.issubdtype(data[c].dtype, np.datetime64) for c in ("startTime", "endTime")):
+        return None
+    if pd.isna(start) or pd.isna(end) or not start < end:
+        return None
+    ctx = ctx or _lib.default_context()
+    table, dev = span_table(data, ctx)
+    a3, ok = slo_arrays(table, slo)
+    return sweep_plan(ctx, table, dev, a3, ok, int(pd.Timestamp(start).value), int(pd.Timestamp(end).value),
+                      int(window_normal.value), int(window_abnormal.value))
+
+
+def _sweep_run(plan):
+    """The chain, one batched ranking of its triggered windows, then the driver's output replayed
+    in window order; an empty window raises the reference's TypeError (T2) after the output of
+    the windows before it."""
+    events = sweep_chain(plan)
+    results = sweep_rank(plan, events)
     names = plan["table"].podop_names
     for e in events:
         if e[0] == "empty":
