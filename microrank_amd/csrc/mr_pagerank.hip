@@ -2694,10 +2694,26 @@ static int64_t wv_blocks(int32_t T, int32_t N, const FxPlan& P) {
 // k_tr_a: blocks of one graph and the cut of its tiles into contiguous per-wave runs of about
 // equal cost (chunks + 2 per tile: a tile's q/r words weigh about two chunks).  Cached per
 // graph for the wave count; at most 1023 tiles (65472 traces) per block.
-static int tr_split(mr_ctx* ctx, mr_graph* g, const FxPlan& P, int64_t* nfa) {
+// wsum: wave tiles of all fused graphs of the launch.  A graph of a batch gets its share of
+// MR_TR_BUDGET (default 1) x the resident blocks in proportion to its tiles: a small graph of a
+// batch then runs a few blocks with several tiles per wave instead of one block per tile set --
+// the per-block fixed cost (LDS image, the N-word partial row written here and re-read by
+// k_fx_b) falls with the block count while the batch still fills the chip.
+static double tr_budget() {
+    static const double v = [] {
+        const char* e = getenv("MR_TR_BUDGET");
+        return e ? std::max(0.0, atof(e)) : 1.0;
+    }();
+    return v;
+}
+static int tr_split(mr_ctx* ctx, mr_graph* g, const FxPlan& P, int64_t wsum, int64_t* nfa) {
     const int64_t W = g->n_wt, NW = P.NT / WAVE;
     const int64_t resident = plan_resident(kern_n(g), P);
     int64_t nb = std::max<int64_t>({std::min<int64_t>(resident, cdiv(W, NW)), cdiv(W, 1023), 1});
+    if (tr_budget() > 0.0 && wsum > W) {
+        const int64_t share = (int64_t)std::ceil((double)resident * tr_budget() * (double)W / (double)wsum);
+        nb = std::max<int64_t>({std::min(nb, share), cdiv(W, 1023), 1});
+    }
     // on the device (k_tr_cut: no host round trip) unless a block's traces must be weighed by
     // their kinds' multiplicities (kind-compressed graphs) or the cut table exceeds its LDS
     if (g->tile_mult_h.empty() && nb * NW <= TC_MAX) {
@@ -2759,8 +2775,8 @@ static int tr_split(mr_ctx* ctx, mr_graph* g, const FxPlan& P, int64_t* nfa) {
     return MR_OK;
 }
 
-static int fused_blocks(mr_ctx* ctx, mr_graph* g, const FxPlan& P, int TT_v1, int64_t* nfa) {
-    if (P.tr) return tr_split(ctx, g, P, nfa);
+static int fused_blocks(mr_ctx* ctx, mr_graph* g, const FxPlan& P, int TT_v1, int64_t wsum, int64_t* nfa) {
+    if (P.tr) return tr_split(ctx, g, P, wsum, nfa);
     *nfa = P.v2 ? wv_blocks(g->T, g->N, P) : fx_blocks(g->T, g->N, TT_v1);
     return MR_OK;
 }
@@ -3276,9 +3292,15 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
                          g->pre_flags == flags && g->pre_seed == seed && g->pre_hmask == hmask && !sharded;
         g->pre_ok = false;   // the iteration state is consumed by this call
         if (!pre) MR_TRY(pagerank_setup(ctx, g, anomaly[i], d, fp32, flags, plan.tr, sharded, seed, hmask));
+    }
+    int64_t wsum = 0;   // wave tiles of the launch's fused graphs (k_tr_a's block budget)
+    for (int i = 0; i < ng; ++i)
+        if (gs[i]->fused) wsum += gs[i]->n_wt;
+    for (int i = 0; i < ng; ++i) {
+        mr_graph* g = gs[i];
         if (g->fused) {   // the plan's blocks: partial rows and (k_tr_a) the per-wave cut
             int64_t nfa = 0;
-            MR_TRY(fused_blocks(ctx, g, plan, TT, &nfa));
+            MR_TRY(fused_blocks(ctx, g, plan, TT, wsum, &nfa));
             MR_TRY(g->fx_part.alloc(ctx, (size_t)std::max<int64_t>(nfa, 1) * (size_t)kern_n(g)));
         }
     }
@@ -3347,7 +3369,7 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         // a shard without traces still runs one (empty) block: it clears the maxima slot and
         // writes a zero partial row, and the collectives after the launch need every rank
         int64_t nfa = 0;
-        if (g->fused) MR_TRY(fused_blocks(ctx, g, plan, TT, &nfa));
+        if (g->fused) MR_TRY(fused_blocks(ctx, g, plan, TT, wsum, &nfa));
         nfa = g->fused ? std::max<int64_t>(nfa, sharded ? 1 : 0) : 0;
         // a row entry stays below 2^63; shards of one graph hold different trace counts, and their
         // limbs are summed, so they share the scale of the largest block (2^15 traces)
