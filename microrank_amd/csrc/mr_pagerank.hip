@@ -2199,10 +2199,15 @@ __global__ void __launch_bounds__(NT) k_tr_a(const GDev* __restrict__ gs, int32_
 // limb sums meet in LDS (integers: order-free).  mode 0: whole graph; sharded graphs split it
 // around the limb all-reduce: mode 1 writes this rank's limbs (lo, hi) per op to fx_limb, mode 2
 // finishes from the reduced limbs.
-constexpr int FB_W = 16;
+// FB_W waves per block: 16 for graphs with many partial rows (a large graph alone: ~1k rows per
+// op), 4 when every graph of the launch has few (batched window graphs: tens of rows) -- the block
+// is then latency-bound (ss term, rows, LDS meet: a chain of dependent loads), and 4-wave blocks
+// put the whole grid on the chip in one round instead of several.
+constexpr int FB_W = 16, FB_W_SMALL = 4, FB_SMALL_ROWS = 256;
 // ops per k_fx_b block: a lane reads op (lane % ops) of every (64/ops)-th row of its wave's share,
 // so a row read stays one 128-B line per op group while small graphs still spread over many CUs
 static int fb_ops(int32_t N) { return N <= 8192 ? 16 : 32; }
+template <int FB_W>
 __global__ void __launch_bounds__(WAVE * FB_W) k_fx_b(const GDev* __restrict__ gs, int32_t ng, int32_t split,
                                                      double d, int it, int mode) {
     __shared__ unsigned long long slo[FB_W * WAVE], shi[FB_W * WAVE];
@@ -3457,6 +3462,14 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
     // bound) and k_tr_a on the main stream; k_fx_b waits for both
     bool any_wide = false;
     for (int i = 0; i < ng; ++i) any_wide = any_wide || gs[i]->wide;
+    // k_fx_b's block size: 4 waves when no graph of the launch has many partial rows
+    static const int fb_force = [] {
+        const char* e = getenv("MR_FB_W");
+        return e ? atoi(e) : 0;
+    }();
+    bool fb_small = !any_wide;
+    for (int i = 0; i < ng; ++i) fb_small = fb_small && hv[(size_t)i].n_fa <= FB_SMALL_ROWS;
+    if (fb_force) fb_small = fb_force == FB_W_SMALL;
     static const bool no_side = getenv("MR_WIDE_SERIAL") != nullptr;   // A/B knob: one stream
     hipStream_t sst = st;
     if (any_wide && !no_side) {
@@ -3496,12 +3509,20 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
             else hipLaunchKernelGGL(fx_a, dim3(blocks_fa), dim3(fx_bs), lds_f, st, dv.p, ng, split_fa, d, alpha, it, TT);
             MR_DEBUG_CHECK(ctx, "k_fx_a");
             if (any_wide && sst != st) MR_TRY_HIP(ctx, hipStreamWaitEvent(st, ctx->side_ev[1], 0));   // k_cold_ops done
+            auto fx_b = [&](int mode) {
+                if (fb_small)
+                    hipLaunchKernelGGL(k_fx_b<FB_W_SMALL>, dim3(blocks_fb), dim3(WAVE * FB_W_SMALL), 0, st, dv.p, ng,
+                                       split_fb, d, it, mode);
+                else
+                    hipLaunchKernelGGL(k_fx_b<FB_W>, dim3(blocks_fb), dim3(WAVE * FB_W), 0, st, dv.p, ng, split_fb, d,
+                                       it, mode);
+            };
             if (!coll) {
-                hipLaunchKernelGGL(k_fx_b, dim3(blocks_fb), dim3(WAVE * FB_W), 0, st, dv.p, ng, split_fb, d, it, 0);
+                fx_b(0);
             } else {   // ONE all-reduce: the P_sr r limbs and every rank's r' max (exact: integers)
-                hipLaunchKernelGGL(k_fx_b, dim3(blocks_fb), dim3(WAVE * FB_W), 0, st, dv.p, ng, split_fb, d, it, 1);
+                fx_b(1);
                 MR_TRY(mr_coll_allreduce(ctx, gs[0]->fx_limb.p, 2 * (int64_t)gs[0]->N + ctx->nranks, MR_DT_U64, 0));
-                hipLaunchKernelGGL(k_fx_b, dim3(blocks_fb), dim3(WAVE * FB_W), 0, st, dv.p, ng, split_fb, d, it, 2);
+                fx_b(2);
             }
             MR_DEBUG_CHECK(ctx, "k_fx_b");
         }
