@@ -53,7 +53,7 @@ __global__ void k_pr_reset(int32_t T, int64_t cap, int32_t N, float* pref, float
         hk[i] = 0ull;
         cr[i] = KCnt{0u, -1};
     }
-    if (i < 4) flag[i] = 0;
+    if (i < 8) flag[i] = 0;
     if (i < 8) scal[i] = 0.0;
 }
 
@@ -862,9 +862,13 @@ __global__ void k_kc_tile_mult(const int32_t* tperm, const double* mult, int32_t
 // ---------------------------------------------------------------- preference (pagerank.py:68-85)
 // sums over pr_trace entries: [0] sum 1/k, [1] sum 1/len; block partials then one fixed-order pass
 // mult (kind-compressed graphs): trace i stands for mult[i] traces of its kind
+// The block partials' sum (formerly k_pref_total) is taken by the block that finishes last (a
+// counter in flag word 4, cleared by k_pr_reset): one launch instead of two.
 __global__ void k_pref_partial(const double* kind, const int32_t* pr_trace, const int32_t* pr_len,
-                               const int32_t* len_t, int32_t n_pr, const double* mult, double* part, int32_t* flag) {
+                               const int32_t* len_t, int32_t n_pr, const double* mult, double* part, int32_t* flag,
+                               double* scal) {
     __shared__ double red[TB / WAVE];
+    __shared__ bool last;
     double a = 0.0, b = 0.0;
     int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n_pr) {
@@ -883,6 +887,22 @@ __global__ void k_pref_partial(const double* kind, const int32_t* pr_trace, cons
     if (threadIdx.x == 0) {
         part[2 * blockIdx.x] = a;
         part[2 * blockIdx.x + 1] = b;
+        __threadfence();   // the partial is visible before the count says so
+        last = atomicAdd(flag + 4, 1) == (int32_t)gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+    __threadfence();
+    a = b = 0.0;
+    for (int32_t i = threadIdx.x; i < (int32_t)gridDim.x; i += blockDim.x) {   // fixed order
+        a += __hip_atomic_load(part + 2 * i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        b += __hip_atomic_load(part + 2 * i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    a = block_sum(a, red);
+    b = block_sum(b, red);
+    if (threadIdx.x == 0) {
+        scal[2] = a;
+        scal[3] = b;
     }
 }
 
@@ -916,12 +936,14 @@ __global__ void k_pref_total_exact(const double* kind, const int32_t* pr_trace, 
     scal[3] = b;
 }
 
+// tperm (k_tr_a graphs with pr_trace = operation_trace): thread i is position i, and c_t goes to
+// c_tp[i] too (formerly k_tr_gather)
 __global__ void k_pref_apply(const double* kind, const int32_t* pr_trace, const int32_t* pr_len,
                              const int32_t* len_t, int32_t n_pr, const double* scal, int anomaly,
-                             float cd, float* pref, float* c_t) {
+                             float cd, float* pref, float* c_t, const int32_t* tperm, float* c_tp) {
     int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n_pr) return;
-    int32_t t = pr_trace ? pr_trace[i] : i;
+    int32_t t = tperm ? tperm[i] : pr_trace ? pr_trace[i] : i;
     int32_t ln = pr_len ? pr_len[i] : len_t[t];
     double k = kind[t];
     double v;
@@ -933,6 +955,7 @@ __global__ void k_pref_apply(const double* kind, const int32_t* pr_trace, const 
     float vf = (float)v;
     pref[t] = vf;
     c_t[t] = cd * vf;   // (1.0 - d) * v: float32 array times a Python float stays float32 (T4)
+    if (tperm) c_tp[i] = cd * vf;
 }
 
 // ---------------------------------------------------------------- iteration
@@ -964,6 +987,35 @@ __global__ void k_iter_init(const float* w_t, const double* mw, const float* u_o
         if (fp32) q32[i] = (float)q; else q64[i] = q;
     }
     // M_s(0) = M_r(0) = 1: s_0, r_0 are used as they are; slots 1, 2 start cleared
+    if (i < 6 * MSH) mslot[i] = i < 2 * MSH ? d2bits(1.0) : 0ull;
+}
+// k_pr_reset and k_iter_init in one launch (the iteration state depends on nothing the kinds or
+// the preference compute)
+__global__ void k_pr_reset_init(int32_t T, int64_t cap, int32_t N, float* pref, float* c_t, unsigned long long* hk,
+                                KCnt* cr, int32_t* flag, double* scal, const float* w_t, const double* mw,
+                                const float* u_o, int64_t T_all, double* sp0, double* su0, double* su1, double* q64,
+                                float* q32, int fp32, unsigned long long* mslot, const int32_t* perm) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < T) {
+        pref[i] = 0.0f;
+        c_t[i] = 0.0f;
+    }
+    if (i < cap) {
+        hk[i] = 0ull;
+        cr[i] = KCnt{0u, -1};
+    }
+    if (i < 8) flag[i] = 0;
+    if (i < 8) scal[i] = 0.0;
+    const double v0 = 1.0 / (double)((int64_t)N + T_all);      // pagerank.py:118-119
+    if (i < N) {
+        sp0[i] = v0;
+        su0[i] = (double)u_o[perm ? perm[i] : i] * v0;
+    }
+    if (i >= N && i < N + TR_PAD) su0[i] = su1[i] = 0.0;
+    if (i < T) {
+        const double q = (mw ? mw[i] : (double)w_t[i]) * v0;
+        if (fp32) q32[i] = (float)q; else q64[i] = q;
+    }
     if (i < 6 * MSH) mslot[i] = i < 2 * MSH ? d2bits(1.0) : 0ull;
 }
 
@@ -3131,7 +3183,7 @@ static int pagerank_setup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool 
     MR_TRY(g->kind.alloc(ctx, (size_t)T));
     MR_TRY(g->pref.alloc(ctx, (size_t)T));
     MR_TRY(g->c_t.alloc(ctx, (size_t)T));
-    MR_TRY(g->flag.alloc(ctx, 4));
+    MR_TRY(g->flag.alloc(ctx, 8));
     MR_TRY(g->scal.alloc(ctx, 8));
     MR_TRY(g->ppart.alloc(ctx, 2 * (size_t)nbp));
     if (ktab) {
@@ -3154,11 +3206,15 @@ static int pagerank_setup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool 
         if (fp32) MR_TRY(g->q32[i].alloc(ctx, (size_t)T + 1));   // [T]: k_fx_a's pad slot
         else MR_TRY(g->q64[i].alloc(ctx, (size_t)T + 1));
     }
-    // one launch clears every per-call word (instead of a memset per buffer)
-    hipLaunchKernelGGL(k_pr_reset, dim3(cdiv(std::max<int64_t>({(int64_t)T, (int64_t)cap, (int64_t)N, 16}), 256)),
+    // one launch clears every per-call word (instead of a memset per buffer) and sets the iteration
+    // state up (k_iter_init's part: it depends on nothing the kinds / preference compute)
+    hipLaunchKernelGGL(k_pr_reset_init,
+                       dim3(cdiv(std::max<int64_t>({(int64_t)T, (int64_t)cap, (int64_t)N + TR_PAD, 6 * MSH, 16}), 256)),
                        dim3(256), 0, st, T, (int64_t)cap, N, g->pref.p, g->c_t.p, g->ht_key.p, g->ht_cr.p,
-                       g->flag.p, g->scal.p);
-    MR_DEBUG_CHECK(ctx, "k_pr_reset");
+                       g->flag.p, g->scal.p, tr ? g->w_tp.p : g->w_t.p, tr ? g->mw_tp.p : nullptr, g->u_o.p,
+                       g->T_all > 0 ? g->T_all : (int64_t)T, g->spb[0].p, g->sub[0].p, g->sub[1].p, g->q64[0].p,
+                       g->q32[0].p, (int)fp32, g->mslot.p, g->relabeled ? (const int32_t*)g->perm.p : nullptr);
+    MR_DEBUG_CHECK(ctx, "k_pr_reset_init");
     // ---- kinds (a kind-compressed graph carries its class sizes: kinds_given)
     if (!g->kinds_given) MR_TRY(graph_kinds(ctx, g, chk, ktab, cap, seed, hmask));
     if (chk) MR_TRY(shard_kinds(ctx, g, cap));   // class sizes over all ranks (one rank: already global)
@@ -3167,26 +3223,22 @@ static int pagerank_setup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool 
     const int32_t* prl = g->pr_identity ? nullptr : g->pr_len.p;
     // also with n_pr == 0 (an empty shard): the one block writes the zero partials the sums read
     hipLaunchKernelGGL(k_pref_partial, dim3(nbp), dim3(TB), 0, st, g->kind.p, prt, prl, g->len_t.p, n_pr,
-                       g->mult.p, g->ppart.p, g->flag.p);
+                       g->mult.p, g->ppart.p, g->flag.p, g->scal.p);   // (and the total: its last block)
     if ((flags & MR_PR_EXACT_SUMS) && !sharded && !g->mult.p)
         hipLaunchKernelGGL(k_pref_total_exact, dim3(1), dim3(64), 0, st, g->kind.p, prt, prl, g->len_t.p, n_pr,
                            g->scal.p);
-    else
-        hipLaunchKernelGGL(k_pref_total, dim3(1), dim3(1024), 0, st, g->ppart.p, nbp, g->scal.p);
     MR_DEBUG_CHECK(ctx, "k_pref");
     if (sharded) MR_TRY(mr_coll_allreduce(ctx, g->scal.p + 2, 2, MR_DT_F64, 0));   // sum(1/k), sum(1/len)
     const float cd = (float)(1.0 - d);
+    // k_tr_a graphs whose pr_trace is operation_trace: c_t in position order from the same launch
+    const bool fuse_gather = tr && !prt && !prl && n_pr == T;
     if (n_pr > 0)
         hipLaunchKernelGGL(k_pref_apply, dim3(nbp), dim3(TB), 0, st, g->kind.p, prt, prl, g->len_t.p, n_pr,
-                           g->scal.p, anomaly, cd, g->pref.p, g->c_t.p);
+                           g->scal.p, anomaly, cd, g->pref.p, g->c_t.p, fuse_gather ? (const int32_t*)g->tperm.p : nullptr,
+                           fuse_gather ? g->c_tp.p : nullptr);
     MR_DEBUG_CHECK(ctx, "k_pref_apply");
-    if (tr && T) hipLaunchKernelGGL(k_tr_gather, dim3(cdiv(T, 256)), dim3(256), 0, st, g->c_t.p, g->tperm.p, T, g->c_tp.p);
-    hipLaunchKernelGGL(k_iter_init, dim3(cdiv(std::max<int64_t>({(int64_t)N + TR_PAD, T, 6 * MSH}), 256)), dim3(256), 0, st,
-                       tr ? g->w_tp.p : g->w_t.p, tr ? g->mw_tp.p : nullptr, g->u_o.p, N, T,
-                       g->T_all > 0 ? g->T_all : (int64_t)T, g->spb[0].p, g->sub[0].p,
-                       g->sub[1].p, g->q64[0].p, g->q32[0].p, (int)fp32, g->mslot.p,
-                       g->relabeled ? (const int32_t*)g->perm.p : nullptr);
-    MR_DEBUG_CHECK(ctx, "k_iter_init");
+    if (tr && T && !fuse_gather)
+        hipLaunchKernelGGL(k_tr_gather, dim3(cdiv(T, 256)), dim3(256), 0, st, g->c_t.p, g->tperm.p, T, g->c_tp.p);
     return MR_OK;
 }
 
@@ -3661,7 +3713,7 @@ static int kind_compressed_pagerank(mr_ctx* ctx, mr_graph* g, int anomaly, doubl
     MR_TRY(g->krep.alloc(ctx, (size_t)T));
     MR_TRY(g->pref.alloc(ctx, (size_t)T));
     MR_TRY(g->c_t.alloc(ctx, (size_t)T));
-    MR_TRY(g->flag.alloc(ctx, 4));
+    MR_TRY(g->flag.alloc(ctx, 8));
     MR_TRY(g->scal.alloc(ctx, 8));
     if (ktab) {
         MR_TRY(g->ht_key.alloc(ctx, cap));
