@@ -149,9 +149,11 @@ __global__ void __launch_bounds__(BT) k_rows(const int32_t* rows, int64_t Ssel, 
 }
 
 // ---------------------------------------------------------------- node order
-__global__ void k_edge_flags(const uint64_t* gk, int64_t cap, int32_t* flag) {
+// a slot holds an edge when its key is set and counted (the dense form lists every key of the
+// table, counted or not)
+__global__ void k_edge_flags(const uint64_t* gk, const uint32_t* gc, int64_t cap, int32_t* flag) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < cap) flag[i] = gk[i] != EMPTY;
+    if (i < cap) flag[i] = gk[i] != EMPTY && gc[i] != 0u;
 }
 __global__ void k_edge_compact(const uint64_t* gk, const uint32_t* gc, const int32_t* flag, const int64_t* pos,
                                int64_t cap, uint64_t* ekey, uint32_t* ecnt, int32_t* is_par, int32_t* nchild_code) {
@@ -317,7 +319,7 @@ __global__ void __launch_bounds__(NS_T) k_nodes_small(const uint64_t* gk, const 
     // call edges out of the hash table (parent code << 32 | child code): parents and child counts
     for (int64_t i = tid; i < ecap; i += NS_T) {
         const uint64_t k = gk[i];
-        if (k == EMPTY) continue;
+        if (k == EMPTY || gc[i] == 0u) continue;   // (dense ids: a key of the table not in this graph)
         const int32_t par = (int32_t)(k >> 32);
         is_par[par] = 1;
         atomicAdd(&nch[par], (int32_t)gc[i]);
@@ -412,6 +414,7 @@ constexpr int IX_EPT = 16;  // index entries per thread in k_ix_stats (fewer blo
 constexpr int IX_BT = 1024;
 constexpr int IX_HIST = 12288;   // three per-code counters (span count, first row, traces)
 constexpr int IX_B = 8;     // entries per thread whose loads are batched
+constexpr int64_t IX_LDS_WORDS = 36864;   // k_ix_stats' dynamic LDS budget (144 KB) in 4-B words
 // The indexed build's first launch: the trace selection with BOTH exclusive scans -- tpos over
 // the selection flags, zoff over the selected traces' op-list lengths -- chained across tiles by
 // decoupled look-back (two status chains), plus the clearing of the per-code counters and the
@@ -433,7 +436,7 @@ __global__ void __launch_bounds__(SEL_T) k_ix_sel_scan(const uint8_t* mask, cons
             ocov[i] = 0;
         }
         if (i < ecap) {
-            gk[i] = ~0ull;
+            if (gk) gk[i] = ~0ull;
             gc[i] = 0u;
         }
     }
@@ -490,23 +493,28 @@ __global__ void __launch_bounds__(IX_BT) k_ix_stats(const int32_t* tflag, int64_
                                                  int64_t n_ed, const int32_t* ed_tr, const uint64_t* ed_key,
                                                  const int32_t* ed_cnt, int32_t n_podops, int use_lds_hist,
                                                  int32_t* ocnt, int32_t* ofirst, int32_t* ocov, uint64_t* gk,
-                                                 uint32_t* gc, uint64_t gmask) {
+                                                 uint32_t* gc, uint64_t gmask, const int32_t* ed_eid, int32_t n_ek,
+                                                 int lds_ek) {
     extern __shared__ int32_t lh[];
     __shared__ unsigned long long ek[ESET];
     __shared__ uint32_t ec[ESET];
     int32_t* lcnt = lh;
     int32_t* lfirst = lh + n_podops;
     int32_t* lcov = lh + 2 * n_podops;   // traces per pod-op (the graph's coverage)
+    uint32_t* lec = (uint32_t*)(lh + (use_lds_hist ? 3 * n_podops : 0));   // dense edge ids: counts per id
     if (use_lds_hist)
         for (int32_t i = threadIdx.x; i < n_podops; i += IX_BT) {
             lcnt[i] = 0;
             lfirst[i] = 0x7fffffff;
             lcov[i] = 0;
         }
-    for (int i = threadIdx.x; i < ESET; i += IX_BT) {
-        ek[i] = EMPTY;
-        ec[i] = 0;
-    }
+    if (ed_eid && lds_ek)
+        for (int32_t i = threadIdx.x; i < n_ek; i += IX_BT) lec[i] = 0u;
+    else if (!ed_eid)
+        for (int i = threadIdx.x; i < ESET; i += IX_BT) {
+            ek[i] = EMPTY;
+            ec[i] = 0;
+        }
     __syncthreads();
     const int64_t pper = (n_po + gridDim.x - 1) / gridDim.x, eper = (n_ed + gridDim.x - 1) / gridDim.x;
     // loads of a round of IX_B entries per thread go out together, then the trace flags
@@ -539,6 +547,36 @@ __global__ void __launch_bounds__(IX_BT) k_ix_stats(const int32_t* tflag, int64_
         }
     }
     const int64_t q0 = (int64_t)blockIdx.x * eper, q1 = min(q0 + eper, n_ed);
+    if (ed_eid) {   // dense edge ids: one counter add per selected entry
+        for (int64_t rb = q0; rb < q1; rb += (int64_t)IX_BT * IX_B) {
+            int32_t tr[IX_B], cn[IX_B], id[IX_B];
+#pragma unroll
+            for (int j = 0; j < IX_B; ++j) {
+                const int64_t r = min(rb + threadIdx.x + (int64_t)j * IX_BT, q1 - 1);
+                tr[j] = ed_tr[r];
+                id[j] = ed_eid[r];
+                cn[j] = ed_cnt[r];
+            }
+#pragma unroll
+            for (int j = 0; j < IX_B; ++j)
+                if (rb + threadIdx.x + (int64_t)j * IX_BT < q1 && tflag[tr[j]]) {
+                    if (lds_ek) atomicAdd(&lec[id[j]], (uint32_t)cn[j]);
+                    else atomicAdd(&gc[id[j]], (uint32_t)cn[j]);
+                }
+        }
+        __syncthreads();
+        if (lds_ek)
+            for (int32_t i = threadIdx.x; i < n_ek; i += IX_BT)
+                if (lec[i]) atomicAdd(&gc[i], lec[i]);
+        if (use_lds_hist)
+            for (int32_t i = threadIdx.x; i < n_podops; i += IX_BT)
+                if (lcnt[i]) {
+                    atomicAdd(&ocnt[i], lcnt[i]);
+                    atomicMin(&ofirst[i], lfirst[i]);
+                    atomicAdd(&ocov[i], lcov[i]);
+                }
+        return;
+    }
     for (int64_t rb = q0; rb < q1; rb += (int64_t)IX_BT * IX_B) {
         int32_t tr[IX_B], cn[IX_B];
         uint64_t ky[IX_B];
@@ -582,9 +620,12 @@ __global__ void __launch_bounds__(IX_BT) k_ix_stats(const int32_t* tflag, int64_
 }
 // join pairs whose rows lie in different traces count when both traces are selected (T11)
 __global__ void k_ix_cross(const uint8_t* mask, const int32_t* tc, const int32_t* tp, const uint64_t* key, int64_t n,
-                           uint64_t* gk, uint32_t* gc, uint64_t gmask) {
+                           uint64_t* gk, uint32_t* gc, uint64_t gmask, const int32_t* eid) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n && mask[tc[i]] && mask[tp[i]]) global_edge_add(key[i], 1u, gk, gc, gmask);
+    if (i < n && mask[tc[i]] && mask[tp[i]]) {
+        if (eid) atomicAdd(&gc[eid[i]], 1u);
+        else global_edge_add(key[i], 1u, gk, gc, gmask);
+    }
 }
 // the selected traces' rows (trace_code, len_t, CSR offsets) and, entry-parallel, their op lists
 // rs_ops[zoff[t] + k] = node of the k-th pod-op: one launch over max(NT, n_po)
@@ -798,7 +839,7 @@ static int build_nodes(mr_ctx* ctx, mr_graph* g, int32_t NP, const int32_t* ocnt
     MR_TRY(is_par.alloc(ctx, NP));
     MR_TRY(nchild_code.alloc(ctx, NP));
     if (NP) hipLaunchKernelGGL(k_zero2_i32, dim3(cdiv(NP, 256)), dim3(256), 0, st, is_par.p, nchild_code.p, NP);
-    hipLaunchKernelGGL(k_edge_flags, dim3(cdiv(ecap, 256)), dim3(256), 0, st, gk, (int64_t)ecap, eflag.p);
+    hipLaunchKernelGGL(k_edge_flags, dim3(cdiv(ecap, 256)), dim3(256), 0, st, gk, gc, (int64_t)ecap, eflag.p);
     MR_TRY(mr_exclusive_scan_i32(ctx, eflag.p, epos.p, ecap, etmp.p));
     int64_t E = 0;
     MR_TRY(read_i64(ctx, epos.p + ecap, &E));
@@ -1062,22 +1103,29 @@ static int ix_launch(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d_mask, mr_
     MR_TRY(b.ocnt.alloc(ctx, NP));
     MR_TRY(b.ofirst.alloc(ctx, NP));
     MR_TRY(b.ocov.alloc(ctx, NP));
-    b.ecap = edge_capacity(sp->n_edge_keys + X.matches, NP);
+    // dense edge ids (one table's keys, counted per id) unless joins across ranks bring keys the
+    // table does not hold
+    static const bool no_dense = getenv("MR_EDGE_HASH") != nullptr;   // A/B knob: the hash set
+    b.dense = !sharded && !no_dense && sp->ekey.p != nullptr;
+    b.ecap = b.dense ? (uint64_t)sp->n_edge_keys : edge_capacity(sp->n_edge_keys + X.matches, NP);
     const uint64_t ecap = b.ecap;
-    MR_TRY(b.gk.alloc(ctx, ecap));
-    MR_TRY(b.gc.alloc(ctx, ecap));
+    if (!b.dense) MR_TRY(b.gk.alloc(ctx, ecap));
+    MR_TRY(b.gc.alloc(ctx, std::max<uint64_t>(ecap, 1)));
+    b.gkp = b.dense ? sp->ekey.p : b.gk.p;
     {   // selection + both trace scans + clearing, one launch
         const int64_t nt = std::max<int64_t>(cdiv((int64_t)NT, SEL_TILE), 1);
         unsigned long long* dst = nullptr;
         uint64_t epoch = 0;
         MR_TRY(mr_dl_status(ctx, 2 * nt, &dst, &epoch));
         hipLaunchKernelGGL(k_ix_sel_scan, dim3((unsigned)nt), dim3(SEL_T), 0, st, d_mask, sp->tlen.p, sp->po_off.p, NT,
-                           b.tflag.p, b.tpos.p, b.zoff.p, dst, epoch, b.ocnt.p, b.ofirst.p, b.ocov.p, NP, b.gk.p,
-                           b.gc.p, (int64_t)ecap);
+                           b.tflag.p, b.tpos.p, b.zoff.p, dst, epoch, b.ocnt.p, b.ofirst.p, b.ocov.p, NP,
+                           b.dense ? (uint64_t*)nullptr : b.gk.p, b.gc.p, (int64_t)ecap);
     }
     if (NT) {
         const int use_lds = NP <= IX_HIST;
-        const size_t lds = use_lds ? 3 * (size_t)NP * sizeof(int32_t) : 0;
+        // dense edge counts in LDS beside the pod-op histogram while both fit (else global adds)
+        const int lds_ek = b.dense && (use_lds ? 3 * (int64_t)NP : 0) + (int64_t)ecap <= IX_LDS_WORDS;
+        const size_t lds = (use_lds ? 3 * (size_t)NP * sizeof(int32_t) : 0) + (lds_ek ? ecap * sizeof(uint32_t) : 0);
         // block cap 256 (one per CU); MR_IX_BLOCKS overrides it for measurements
         static const int ix_cap = [] {
             const char* e = getenv("MR_IX_BLOCKS");
@@ -1086,11 +1134,13 @@ static int ix_launch(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d_mask, mr_
         const int nblk = std::max(1, std::min(ix_cap, cdiv(std::max(sp->n_po, sp->n_ed), IX_BT * IX_EPT)));
         hipLaunchKernelGGL(k_ix_stats, dim3(nblk), dim3(IX_BT), lds, st, b.tflag.p, sp->n_po, sp->po_tr.p, sp->po_op.p,
                            sp->po_cnt.p, sp->po_first.p, sp->n_ed, sp->ed_tr.p, sp->ed_key.p, sp->ed_cnt.p, NP, use_lds,
-                           b.ocnt.p, b.ofirst.p, b.ocov.p, b.gk.p, b.gc.p, ecap - 1);
+                           b.ocnt.p, b.ofirst.p, b.ocov.p, b.gk.p, b.gc.p, ecap - 1,
+                           b.dense ? (const int32_t*)sp->ed_eid.p : nullptr, (int32_t)ecap, lds_ek);
     }
     if (sp->n_xj)
         hipLaunchKernelGGL(k_ix_cross, dim3(cdiv(sp->n_xj, 256)), dim3(256), 0, st, d_mask, sp->xj_tc.p, sp->xj_tp.p,
-                           sp->xj_key.p, sp->n_xj, b.gk.p, b.gc.p, ecap - 1);
+                           sp->xj_key.p, sp->n_xj, b.gk.p, b.gc.p, ecap - 1,
+                           b.dense ? (const int32_t*)sp->xj_eid.p : nullptr);
     if (X.matches && sp->S)   // cross-rank parent joins, counted at the child's rank
         hipLaunchKernelGGL(k_cross_join<true>, dim3(cdiv(sp->S, 256)), dim3(256), 0, st, sp->trace.p, sp->parent.p,
                            sp->podop.p, sp->S, d_mask, X.key.p, X.val.p, X.rec.p, X.n, ctx->rank,
@@ -1111,7 +1161,7 @@ static int ix_launch(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d_mask, mr_
         MR_TRY(g->len_t.alloc(ctx, std::max(NT, 1)));
         MR_TRY(g->rs_ops.alloc(ctx, (size_t)std::max<int64_t>(sp->n_po, 1)));
         MR_TRY(g->rs_off.alloc(ctx, (size_t)NT + 1));
-        hipLaunchKernelGGL(k_nodes_small, dim3(1), dim3(NS_T), 0, st, b.gk.p, b.gc.p, (int64_t)ecap, b.ocnt.p,
+        hipLaunchKernelGGL(k_nodes_small, dim3(1), dim3(NS_T), 0, st, b.gkp, b.gc.p, (int64_t)ecap, b.ocnt.p,
                            b.ofirst.p, NP, b.node_of_code.p, g->node_podop.p, g->len_o.p, g->nchild.p, b.ocov.p,
                            g->cov.p, g->ss_par.p, g->ss_off.p, b.tpos.p + NT, b.zoff.p + NT, g->rs_off.p, d_out);
         if (NT || sp->n_po)
@@ -1135,7 +1185,7 @@ static int ix_finish(mr_ctx* ctx, const mr_spans* sp, mr_graph* g, IxBuild& b, c
         return MR_OK;
     }
     // the general node order (sharded graphs; more call edges than the one-block path holds)
-    MR_TRY(build_nodes(ctx, g, NP, b.ocnt.p, b.ofirst.p, b.ocov.p, sp->row_bits, b.gk.p, b.gc.p, b.ecap, b.node_of_code,
+    MR_TRY(build_nodes(ctx, g, NP, b.ocnt.p, b.ofirst.p, b.ocov.p, sp->row_bits, b.gkp, b.gc.p, b.ecap, b.node_of_code,
                        nullptr, sharded));
     int64_t hh[2] = {0, 0};   // T, nnz (their scans ran before build_nodes' syncs)
     MR_TRY_HIP(ctx, hipMemcpyAsync(&hh[0], b.tpos.p + NT, sizeof(int64_t), hipMemcpyDeviceToHost, st));

@@ -276,6 +276,8 @@ struct mr_spans {
     DBuf<long long> tmaxd, tts, tte;     // [NT] max duration, trace-level start / end
     int64_t n_po = 0, n_sv = 0, n_ed = 0, n_xj = 0;
     int64_t n_edge_keys = 0;             // distinct (parent op, child op) over the table: edge-set bound
+    DBuf<uint64_t> ekey;                 // [n_edge_keys] those keys, ascending (parent << 32 | child)
+    DBuf<int32_t> ed_eid, xj_eid;        // [n_ed], [n_xj] the dense edge id (index into ekey) of a key
     DBuf<int64_t> po_off;                // [NT+1] distinct pod-ops of a trace (code order) ...
     DBuf<int32_t> po_op, po_cnt, po_first, po_tr;   // ... with span count, first row and trace
     DBuf<int64_t> sv_off;                // [NT+1] distinct service-ops of a trace (code order) ...
@@ -329,6 +331,8 @@ struct IxBuild {
     DBuf<uint64_t> gk;
     DBuf<uint32_t> gc;
     uint64_t ecap = 0;
+    const uint64_t* gkp = nullptr;   // the edge table's keys: gk (hash table) or the table's ekey (dense ids)
+    bool dense = false;              // edge counts per dense edge id (gc[ecap], ecap = n_edge_keys)
     bool small = false;   // the one-block node order ran: its sizes are in d_out
 };
 int mr_ix_launch(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d_mask, mr_graph* g, IxBuild& b, int64_t* d_out);

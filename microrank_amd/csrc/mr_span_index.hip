@@ -148,6 +148,27 @@ __global__ void k_ix_pack_keys(const uint64_t* ed_key, int64_t n_ed, const uint6
     const uint64_t k = i < n_ed ? ed_key[i] : xj_key[i - n_ed];
     out[i] = ((k >> 32) << nbp) | (k & 0xffffffffull);
 }
+// the distinct edge keys (heads of the sorted packed keys) as (parent << 32 | child), ascending
+__global__ void k_ix_ekeys(const uint64_t* key, const int32_t* head, const int64_t* hpos, int64_t n, int nbp,
+                           uint64_t* ekey) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || !head[i]) return;
+    const uint64_t k = key[i], m = (1ull << nbp) - 1ull;
+    ekey[hpos[i]] = ((k >> nbp) << 32) | (k & m);
+}
+// dense edge id of each key: its position among the distinct keys (binary search)
+__global__ void k_ix_eid(const uint64_t* key, int64_t n, const uint64_t* ekey, int64_t E, int32_t* eid) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t k = key[i];
+    int64_t lo = 0, hi = E;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (ekey[mid] < k) lo = mid + 1;
+        else hi = mid;
+    }
+    eid[i] = (int32_t)lo;
+}
 __global__ void k_ix_edge_runs(const uint64_t* key, const int32_t* head, const int64_t* hpos, int64_t n, int nbp,
                                uint64_t* ed_key, int32_t* ed_tr, int64_t* r_start, int32_t* truns) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -477,6 +498,21 @@ int mr_spans_index(mr_ctx* ctx, mr_spans* s) {
         if (K) hipLaunchKernelGGL(k_ix_heads, dim3(cdiv(K, XB)), dim3(XB), 0, st, k2.p, K, head.p);
         MR_TRY(mr_exclusive_scan_i32(ctx, head.p, hpos.p, K, tmp.p));
         MR_TRY_HIP(ctx, hipMemcpyAsync(&s->n_edge_keys, hpos.p + K, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+        MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+        // dense edge ids: a window's build counts its edges per id (an LDS histogram) instead of
+        // probing a hash set per entry
+        const int64_t E = s->n_edge_keys;
+        MR_TRY(s->ekey.alloc(ctx, (size_t)std::max<int64_t>(E, 1)));
+        MR_TRY(s->ed_eid.alloc(ctx, (size_t)std::max<int64_t>(s->n_ed, 1)));
+        MR_TRY(s->xj_eid.alloc(ctx, (size_t)std::max<int64_t>(s->n_xj, 1)));
+        if (K) hipLaunchKernelGGL(k_ix_ekeys, dim3(cdiv(K, XB)), dim3(XB), 0, st, k2.p, head.p, hpos.p, K, nbp, s->ekey.p);
+        if (s->n_ed)
+            hipLaunchKernelGGL(k_ix_eid, dim3(cdiv(s->n_ed, XB)), dim3(XB), 0, st, s->ed_key.p, s->n_ed, s->ekey.p, E,
+                               s->ed_eid.p);
+        if (s->n_xj)
+            hipLaunchKernelGGL(k_ix_eid, dim3(cdiv(s->n_xj, XB)), dim3(XB), 0, st, s->xj_key.p, s->n_xj, s->ekey.p, E,
+                               s->xj_eid.p);
+        MR_TRY_HIP(ctx, hipGetLastError());
         MR_TRY_HIP(ctx, hipStreamSynchronize(st));
     }
     int32_t hb = 0;
