@@ -370,16 +370,22 @@ static int win_detect_build_async(mr_ctx* ctx, const mr_spans* s, int64_t t0, in
     MR_TRY(m_abn.alloc(ctx, std::max(NT, 1)));
     MR_TRY(m_nor.alloc(ctx, std::max(NT, 1)));
     MR_TRY(mr_detect_indexed_launch(ctx, s, t0, t1, d_a3, d_a3v, dst.p, (unsigned long long*)wb.p));
-    if (NT) hipLaunchKernelGGL(k_masks, dim3(cdiv(NT, 256)), dim3(256), 0, st, dst.p, NT, m_abn.p, m_nor.p);
     w.gn = new mr_graph();
     w.gn->ctx = ctx;
     w.ga = new mr_graph();
     w.ga->ctx = ctx;
     IxBuild bn, ba;
     // (the graphs take EVERY row of the selected traces: get_pagerank_graph(list, data),
-    // online_rca.py:180,185 / preprocess_data.py:148)
-    MR_TRY(mr_ix_launch(ctx, s, m_abn.p, w.gn, bn, wb.p + CW));       // "normal" graph = detector's abnormal traces
-    MR_TRY(mr_ix_launch(ctx, s, m_nor.p, w.ga, ba, wb.p + CW + 8));
+    // online_rca.py:180,185 / preprocess_data.py:148).  Both from the states in one pass over the
+    // index when the table allows it, else one build per mask.
+    const int rc2 = mr_ix_launch2(ctx, s, dst.p, w.gn, w.ga, bn, ba, wb.p + CW);
+    if (rc2 == MR_ERR_STATE) {
+        if (NT) hipLaunchKernelGGL(k_masks, dim3(cdiv(NT, 256)), dim3(256), 0, st, dst.p, NT, m_abn.p, m_nor.p);
+        MR_TRY(mr_ix_launch(ctx, s, m_abn.p, w.gn, bn, wb.p + CW));       // "normal" graph = detector's abnormal traces
+        MR_TRY(mr_ix_launch(ctx, s, m_nor.p, w.ga, ba, wb.p + CW + 8));
+    } else {
+        MR_TRY(rc2);
+    }
     int64_t h[CW + 16];
     {
         unsigned char* hp = nullptr;

@@ -299,12 +299,11 @@ __device__ __forceinline__ int32_t ns_scan(int32_t v, int32_t* sbuf, int32_t* to
     __syncthreads();
     return incl - v;
 }
-__global__ void __launch_bounds__(NS_T) k_nodes_small(const uint64_t* gk, const uint32_t* gc, int64_t ecap,
-                                                     const int32_t* ocnt, const int32_t* ofirst, int32_t NP,
-                                                     int32_t* node_of_code, int32_t* node_podop, int32_t* len_o,
-                                                     int32_t* nchild, const int32_t* ocov, int32_t* cov,
-                                                     int32_t* ss_par, int64_t* ss_off, const int64_t* T_dev, const int64_t* nnz_dev, int64_t* rs_off,
-                                                     int64_t* out) {
+__device__ void nodes_small(const uint64_t* gk, const uint32_t* gc, int64_t ecap, const int32_t* ocnt,
+                            const int32_t* ofirst, int32_t NP, int32_t* node_of_code, int32_t* node_podop,
+                            int32_t* len_o, int32_t* nchild, const int32_t* ocov, int32_t* cov, int32_t* ss_par,
+                            int64_t* ss_off, const int64_t* T_dev, const int64_t* nnz_dev, int64_t* rs_off,
+                            int64_t* out) {
     __shared__ int32_t is_par[NS_PMAX], nch[NS_PMAX], noc[NS_PMAX];
     __shared__ uint64_t qb[NS_PMAX], eb[NS_EMAX];
     __shared__ int32_t sbuf[NS_T];
@@ -404,6 +403,32 @@ __global__ void __launch_bounds__(NS_T) k_nodes_small(const uint64_t* gk, const 
         out[1] = E;
         out[2] = 0;
     }
+}
+__global__ void __launch_bounds__(NS_T) k_nodes_small(const uint64_t* gk, const uint32_t* gc, int64_t ecap,
+                                                     const int32_t* ocnt, const int32_t* ofirst, int32_t NP,
+                                                     int32_t* node_of_code, int32_t* node_podop, int32_t* len_o,
+                                                     int32_t* nchild, const int32_t* ocov, int32_t* cov,
+                                                     int32_t* ss_par, int64_t* ss_off, const int64_t* T_dev,
+                                                     const int64_t* nnz_dev, int64_t* rs_off, int64_t* out) {
+    nodes_small(gk, gc, ecap, ocnt, ofirst, NP, node_of_code, node_podop, len_o, nchild, ocov, cov, ss_par, ss_off,
+                T_dev, nnz_dev, rs_off, out);
+}
+// the two graphs of a window (mr_ix_launch2): block g builds graph g
+struct NsArgs {
+    const uint32_t* gc;
+    const int32_t *ocnt, *ofirst, *ocov;
+    int32_t *node_of_code, *node_podop, *len_o, *nchild, *cov, *ss_par;
+    int64_t* ss_off;
+    const int64_t *T_dev, *nnz_dev;
+    int64_t *rs_off, *out;
+};
+struct NsArgs2 {
+    NsArgs g[2];
+};
+__global__ void __launch_bounds__(NS_T) k_nodes_small2(const uint64_t* gk, int64_t ecap, int32_t NP, NsArgs2 a) {
+    const NsArgs& x = a.g[blockIdx.x];
+    nodes_small(gk, x.gc, ecap, x.ocnt, x.ofirst, NP, x.node_of_code, x.node_podop, x.len_o, x.nchild, x.ocov, x.cov,
+                x.ss_par, x.ss_off, x.T_dev, x.nnz_dev, x.rs_off, x.out);
 }
 
 // ---------------------------------------------------------------- indexed build (whole traces)
@@ -645,6 +670,200 @@ __global__ void k_ix_traces(const int32_t* tflag, const int64_t* tpos, const int
         if (tflag[t]) rs_ops[zoff[t] + (i - po_off[t])] = node_of_code[po_op[i]];
     }
 }
+// ---------------------------------------------------------------- both graphs of a window in one pass
+// A window's two graphs (online_rca.py:180,185: the detector's abnormal traces, state 2 -> graph 0
+// "normal"; its normal traces, state 1 -> graph 1, T1) select disjoint traces of one table, so one
+// pass over the per-trace index serves both: each entry goes to the graph of its trace's state.
+struct IxSide {
+    int32_t *tflag, *ocnt, *ofirst, *ocov;
+    int64_t *tpos, *zoff;
+    uint32_t* gc;
+};
+struct IxSide2 {
+    IxSide g[2];
+};
+__device__ __forceinline__ int side_of(uint8_t st) { return st == 2 ? 0 : st == 1 ? 1 : -1; }
+// selection + the four exclusive scans (tpos and zoff of each graph) by decoupled look-back, and the
+// clearing of both graphs' counters
+__global__ void __launch_bounds__(SEL_T) k_ix_sel_scan2(const uint8_t* state, const int32_t* tlen, const int64_t* po_off,
+                                                       int32_t NT, IxSide2 x, unsigned long long* st, uint64_t epoch,
+                                                       int32_t NP, int64_t ecap) {
+    __shared__ int64_t sa[4][SEL_T];
+    __shared__ int64_t ex[4];
+    const int tid = threadIdx.x;
+    const int64_t gsz = (int64_t)gridDim.x * SEL_T, gi = (int64_t)blockIdx.x * SEL_T + tid;
+    for (int64_t i = gi; i < max((int64_t)NP, ecap); i += gsz)
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+            if (i < NP) {
+                x.g[g].ocnt[i] = 0;
+                x.g[g].ofirst[i] = 0x7f7f7f7f;
+                x.g[g].ocov[i] = 0;
+            }
+            if (i < ecap) x.g[g].gc[i] = 0u;
+        }
+    const int64_t tile = blockIdx.x, base = tile * SEL_TILE + (int64_t)tid * SEL_I;
+    int8_t sd[SEL_I];
+    int64_t z[SEL_I], acc[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < SEL_I; ++i) {
+        const int64_t t = base + i;
+        const int s_ = t < NT && tlen[t] > 0 ? side_of(state[t]) : -1;
+        sd[i] = (int8_t)s_;
+        z[i] = s_ >= 0 ? po_off[t + 1] - po_off[t] : 0;
+        if (t < NT) {
+            x.g[0].tflag[t] = s_ == 0;
+            x.g[1].tflag[t] = s_ == 1;
+        }
+        if (s_ >= 0) {
+            acc[2 * s_] += 1;
+            acc[2 * s_ + 1] += z[i];
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) sa[c][tid] = acc[c];
+    __syncthreads();
+    for (int o = 1; o < SEL_T; o <<= 1) {
+        int64_t v[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) v[c] = tid >= o ? sa[c][tid - o] : 0;
+        __syncthreads();
+#pragma unroll
+        for (int c = 0; c < 4; ++c) sa[c][tid] += v[c];
+        __syncthreads();
+    }
+    if (tid < 4) {   // chain c: (graph c / 2, tpos or zoff)
+        const int64_t agg = sa[tid][SEL_T - 1];
+        ex[tid] = dl_lookback(st + (size_t)tid * gridDim.x, tile, agg, epoch);
+        if (tile == (int64_t)gridDim.x - 1) {
+            int64_t* dst = (tid & 1) ? x.g[tid >> 1].zoff : x.g[tid >> 1].tpos;
+            dst[NT] = ex[tid] + agg;
+        }
+    }
+    __syncthreads();
+    int64_t r[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) r[c] = ex[c] + sa[c][tid] - acc[c];
+#pragma unroll
+    for (int i = 0; i < SEL_I; ++i) {
+        const int64_t t = base + i;
+        if (t < NT) {   // (values of the graph the trace is not in are never read)
+            x.g[0].tpos[t] = r[0];
+            x.g[0].zoff[t] = r[1];
+            x.g[1].tpos[t] = r[2];
+            x.g[1].zoff[t] = r[3];
+        }
+        if (sd[i] >= 0) {
+            r[2 * sd[i]] += 1;
+            r[2 * sd[i] + 1] += z[i];
+        }
+    }
+}
+// both graphs' per-pod-op counts / first rows / coverage and edge counts per dense id, one pass
+__global__ void __launch_bounds__(IX_BT) k_ix_stats2(const uint8_t* state, int64_t n_po, const int32_t* po_tr,
+                                                    const int32_t* po_op, const int32_t* po_cnt,
+                                                    const int32_t* po_first, int64_t n_ed, const int32_t* ed_tr,
+                                                    const int32_t* ed_eid, const int32_t* ed_cnt, int32_t NP,
+                                                    int32_t n_ek, IxSide2 x) {
+    extern __shared__ int32_t lh[];
+    const int32_t W = 3 * NP + n_ek;   // words per graph: cnt, first, cov, edge counts
+    for (int32_t i = threadIdx.x; i < 2 * W; i += IX_BT) {
+        const int32_t j = i % W;
+        lh[i] = (j >= NP && j < 2 * NP) ? 0x7fffffff : 0;
+    }
+    __syncthreads();
+    const int64_t pper = (n_po + gridDim.x - 1) / gridDim.x, eper = (n_ed + gridDim.x - 1) / gridDim.x;
+    const int64_t p0 = (int64_t)blockIdx.x * pper, p1 = min(p0 + pper, n_po);
+    for (int64_t rb = p0; rb < p1; rb += (int64_t)IX_BT * IX_B) {
+        int32_t tr[IX_B], op[IX_B], cn[IX_B], fr[IX_B];
+#pragma unroll
+        for (int j = 0; j < IX_B; ++j) {
+            const int64_t r = min(rb + threadIdx.x + (int64_t)j * IX_BT, p1 - 1);
+            tr[j] = po_tr[r];
+            op[j] = po_op[r];
+            cn[j] = po_cnt[r];
+            fr[j] = po_first[r];
+        }
+        int sd[IX_B];
+#pragma unroll
+        for (int j = 0; j < IX_B; ++j) sd[j] = rb + threadIdx.x + (int64_t)j * IX_BT < p1 ? side_of(state[tr[j]]) : -1;
+#pragma unroll
+        for (int j = 0; j < IX_B; ++j) {
+            if (sd[j] < 0) continue;
+            int32_t* L = lh + sd[j] * W;
+            atomicAdd(&L[op[j]], cn[j]);
+            atomicMin(&L[NP + op[j]], fr[j]);
+            atomicAdd(&L[2 * NP + op[j]], 1);
+        }
+    }
+    const int64_t q0 = (int64_t)blockIdx.x * eper, q1 = min(q0 + eper, n_ed);
+    for (int64_t rb = q0; rb < q1; rb += (int64_t)IX_BT * IX_B) {
+        int32_t tr[IX_B], cn[IX_B], id[IX_B];
+#pragma unroll
+        for (int j = 0; j < IX_B; ++j) {
+            const int64_t r = min(rb + threadIdx.x + (int64_t)j * IX_BT, q1 - 1);
+            tr[j] = ed_tr[r];
+            id[j] = ed_eid[r];
+            cn[j] = ed_cnt[r];
+        }
+#pragma unroll
+        for (int j = 0; j < IX_B; ++j) {
+            const int sd = rb + threadIdx.x + (int64_t)j * IX_BT < q1 ? side_of(state[tr[j]]) : -1;
+            if (sd >= 0) atomicAdd((uint32_t*)&lh[sd * W + 3 * NP + id[j]], (uint32_t)cn[j]);
+        }
+    }
+    __syncthreads();
+    for (int32_t i = threadIdx.x; i < 2 * W; i += IX_BT) {
+        const int32_t g = i / W, j = i % W;
+        const int32_t v = lh[i];
+        if (j < NP) {
+            if (v) {
+                atomicAdd(&x.g[g].ocnt[j], v);
+                atomicMin(&x.g[g].ofirst[j], lh[g * W + NP + j]);
+                atomicAdd(&x.g[g].ocov[j], lh[g * W + 2 * NP + j]);
+            }
+        } else if (j >= 3 * NP && v) {
+            atomicAdd(&x.g[g].gc[j - 3 * NP], (uint32_t)v);
+        }
+    }
+}
+// join pairs across traces (T11): counted in a graph when both traces are in it
+__global__ void k_ix_cross2(const uint8_t* state, const int32_t* tc, const int32_t* tp, const int32_t* eid, int64_t n,
+                            IxSide2 x) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int sd = side_of(state[tc[i]]);
+    if (sd >= 0 && side_of(state[tp[i]]) == sd) atomicAdd(&x.g[sd].gc[eid[i]], 1u);
+}
+// both graphs' trace rows and op lists (k_ix_traces per graph)
+struct TrOut {
+    int32_t *trace_code, *len_t, *rs_ops;
+    int64_t* rs_off;
+    const int32_t* node_of_code;
+};
+struct TrOut2 {
+    TrOut g[2];
+};
+__global__ void k_ix_traces2(const uint8_t* state, IxSide2 x, int32_t NT, const int32_t* tlen, int64_t n_po,
+                             const int32_t* po_tr, const int64_t* po_off, const int32_t* po_op, TrOut2 o) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < NT) {
+        const int sd = side_of(state[i]);
+        if (sd >= 0 && x.g[sd].tflag[i]) {
+            const int32_t p = (int32_t)x.g[sd].tpos[i];
+            o.g[sd].trace_code[p] = (int32_t)i;
+            o.g[sd].len_t[p] = tlen[i];
+            o.g[sd].rs_off[p] = x.g[sd].zoff[i];
+        }
+    }
+    if (i < n_po) {
+        const int32_t t = po_tr[i];
+        const int sd = side_of(state[t]);
+        if (sd >= 0 && x.g[sd].tflag[t])
+            o.g[sd].rs_ops[x.g[sd].zoff[t] + (i - po_off[t])] = o.g[sd].node_of_code[po_op[i]];
+    }
+}
+
 // ---------------------------------------------------------------- sharded build: the join across ranks
 // A child row's parent rows may lie in traces of another rank (T11).  Each rank publishes a
 // Bloom filter of the ParentSpanIds of its selected rows; a rank exports the selected rows whose
@@ -1217,6 +1436,83 @@ static int graph_build_indexed(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d
     int64_t h[5] = {0, 0, 0, 0, 0};   // N, E, overflow, T, nnz
     if (b.small) MR_TRY(mr_read_words(ctx, dout.p, 5, h));
     return ix_finish(ctx, sp, g, b, b.small ? h : nullptr, sharded);
+}
+
+// Both graphs of a window from the detector's states in one pass over the index (k_ix_sel_scan2,
+// k_ix_stats2, k_ix_cross2, k_nodes_small2, k_ix_traces2: five launches for two graphs); sizes of
+// graph g to d_out + 8 g.  MR_ERR_STATE when the table is past the one-pass limits (dense edge ids,
+// both graphs' LDS histograms, the one-block node order): the caller builds them one by one.
+int mr_ix_launch2(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d_state, mr_graph* g0, mr_graph* g1, IxBuild& b0,
+                  IxBuild& b1, int64_t* d_out) {
+    static const bool off = getenv("MR_NO_IX2") != nullptr;   // A/B knob
+    const int32_t NT = sp->n_traces, NP = sp->n_podops;
+    const int64_t nek = sp->n_edge_keys;
+    if (off || !sp->ekey.p || NP > NS_PMAX || 2 * (3 * (int64_t)NP + nek) > IX_LDS_WORDS) return MR_ERR_STATE;
+    hipStream_t st = ctx->stream;
+    IxBuild* b[2] = {&b0, &b1};
+    mr_graph* g[2] = {g0, g1};
+    IxSide2 xs;
+    NsArgs2 na;
+    TrOut2 to;
+    for (int k = 0; k < 2; ++k) {
+        IxBuild& B = *b[k];
+        mr_graph* G = g[k];
+        B.dense = true;
+        B.small = true;
+        B.ecap = (uint64_t)nek;
+        B.gkp = sp->ekey.p;
+        MR_TRY(B.tflag.alloc(ctx, std::max(NT, 1)));
+        MR_TRY(B.tpos.alloc(ctx, (size_t)NT + 1));
+        MR_TRY(B.zoff.alloc(ctx, (size_t)NT + 1));
+        MR_TRY(B.ocnt.alloc(ctx, std::max(NP, 1)));
+        MR_TRY(B.ofirst.alloc(ctx, std::max(NP, 1)));
+        MR_TRY(B.ocov.alloc(ctx, std::max(NP, 1)));
+        MR_TRY(B.gc.alloc(ctx, (size_t)std::max<int64_t>(nek, 1)));
+        MR_TRY(B.node_of_code.alloc(ctx, std::max(NP, 1)));
+        MR_TRY(G->node_podop.alloc(ctx, std::max(NP, 1)));
+        MR_TRY(G->len_o.alloc(ctx, std::max(NP, 1)));
+        MR_TRY(G->nchild.alloc(ctx, std::max(NP, 1)));
+        MR_TRY(G->cov.alloc(ctx, std::max(NP, 1)));
+        MR_TRY(G->ss_par.alloc(ctx, NS_EMAX));
+        MR_TRY(G->ss_off.alloc(ctx, (size_t)NP + 1));
+        MR_TRY(G->trace_code.alloc(ctx, std::max(NT, 1)));
+        MR_TRY(G->len_t.alloc(ctx, std::max(NT, 1)));
+        MR_TRY(G->rs_ops.alloc(ctx, (size_t)std::max<int64_t>(sp->n_po, 1)));
+        MR_TRY(G->rs_off.alloc(ctx, (size_t)NT + 1));
+        xs.g[k] = IxSide{B.tflag.p, B.ocnt.p, B.ofirst.p, B.ocov.p, B.tpos.p, B.zoff.p, B.gc.p};
+        na.g[k] = NsArgs{B.gc.p, B.ocnt.p, B.ofirst.p, B.ocov.p, B.node_of_code.p, G->node_podop.p, G->len_o.p,
+                         G->nchild.p, G->cov.p, G->ss_par.p, G->ss_off.p, B.tpos.p + NT, B.zoff.p + NT, G->rs_off.p,
+                         d_out + 8 * k};
+        to.g[k] = TrOut{G->trace_code.p, G->len_t.p, G->rs_ops.p, G->rs_off.p, B.node_of_code.p};
+    }
+    {
+        const int64_t nt = std::max<int64_t>(cdiv((int64_t)NT, SEL_TILE), 1);
+        unsigned long long* dst = nullptr;
+        uint64_t epoch = 0;
+        MR_TRY(mr_dl_status(ctx, 4 * nt, &dst, &epoch));
+        hipLaunchKernelGGL(k_ix_sel_scan2, dim3((unsigned)nt), dim3(SEL_T), 0, st, d_state, sp->tlen.p, sp->po_off.p,
+                           NT, xs, dst, epoch, NP, nek);
+    }
+    if (NT) {
+        static const int ix_cap = [] {
+            const char* e = getenv("MR_IX_BLOCKS");
+            return e ? std::max(1, atoi(e)) : 256;
+        }();
+        const int nblk = std::max(1, std::min(ix_cap, cdiv(std::max(sp->n_po, sp->n_ed), IX_BT * IX_EPT)));
+        const size_t lds = 2 * (3 * (size_t)NP + (size_t)nek) * sizeof(int32_t);
+        hipLaunchKernelGGL(k_ix_stats2, dim3(nblk), dim3(IX_BT), lds, st, d_state, sp->n_po, sp->po_tr.p, sp->po_op.p,
+                           sp->po_cnt.p, sp->po_first.p, sp->n_ed, sp->ed_tr.p, sp->ed_eid.p, sp->ed_cnt.p, NP,
+                           (int32_t)nek, xs);
+    }
+    if (sp->n_xj)
+        hipLaunchKernelGGL(k_ix_cross2, dim3(cdiv(sp->n_xj, 256)), dim3(256), 0, st, d_state, sp->xj_tc.p, sp->xj_tp.p,
+                           sp->xj_eid.p, sp->n_xj, xs);
+    hipLaunchKernelGGL(k_nodes_small2, dim3(2), dim3(NS_T), 0, st, sp->ekey.p, nek, NP, na);
+    if (NT || sp->n_po)
+        hipLaunchKernelGGL(k_ix_traces2, dim3(cdiv(std::max<int64_t>(NT, sp->n_po), 256)), dim3(256), 0, st, d_state, xs,
+                           NT, sp->tlen.p, sp->n_po, sp->po_tr.p, sp->po_off.p, sp->po_op.p, to);
+    MR_TRY_HIP(ctx, hipGetLastError());
+    return MR_OK;
 }
 
 int mr_ix_launch(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d_mask, mr_graph* g, IxBuild& b, int64_t* d_out) {
