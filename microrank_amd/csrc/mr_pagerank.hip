@@ -302,8 +302,10 @@ __global__ void k_wide_span(const int64_t* cb_beg, int32_t n_cb, const int32_t* 
 // ---------------------------------------------------------------- trace-parallel layout (k_tr_a)
 // Traces by op count: a counting sort (lengths <= N <= FX_NMAX), order within a length free --
 // nothing numeric depends on it (a trace's ids are rotated by trace mod len, not by position;
-// the accumulator is integer).  Blocks of TRB threads take TRB * TR_PER traces each.
-constexpr int TRB = 1024, TR_PER = 16;
+// the accumulator is integer).  Blocks of TRB threads take TRB * TR_PER traces each: 16 per
+// thread for large graphs, 2 for window-sized ones (187k traces in 12 blocks had left the chip idle)
+constexpr int TRB = 1024, TR_PER_BIG = 16, TR_PER_SMALL = 2;
+template <int TR_PER>
 __global__ void __launch_bounds__(TRB) k_tr_hist(const int64_t* off, int32_t T, int32_t nbin, int32_t* hist) {
     extern __shared__ int32_t lh[];
     for (int32_t i = threadIdx.x; i < nbin; i += TRB) lh[i] = 0;
@@ -322,6 +324,7 @@ __global__ void __launch_bounds__(TRB) k_tr_hist(const int64_t* off, int32_t T, 
 // (hist is consumed, no cursor copy); boff null (nbin <= TP_LSCAN) -- each block scans the
 // histogram in LDS itself and claims slots through `taken` (no scan launch)
 constexpr int TP_LSCAN = 8192;
+template <int TR_PER>
 __global__ void __launch_bounds__(TRB) k_tr_place(const int64_t* off, int32_t T, int32_t nbin, const int64_t* boff,
                                                   int32_t* hist, int32_t* taken, const float* w_t, int32_t* tperm,
                                                   float* w_tp) {
@@ -2848,14 +2851,18 @@ static int tr_layout(mr_ctx* ctx, mr_graph* g, const int64_t* off, const uint16_
     MR_TRY(g->w_tp.alloc(ctx, (size_t)std::max(T, 1)));
     MR_TRY(g->coff.alloc(ctx, (size_t)W + 1));
     if (T) {
-        const int nb = cdiv(T, (int64_t)TRB * TR_PER);
-        hipLaunchKernelGGL(k_tr_hist, dim3(nb), dim3(TRB), (size_t)nbin * sizeof(int32_t), st, off, T, nbin, hist);
+        const bool big = (int64_t)T >= (int64_t)num_cus() * TRB * TR_PER_SMALL * 4;
+        const int per = big ? TR_PER_BIG : TR_PER_SMALL;
+        const int nb = cdiv(T, (int64_t)TRB * per);
+        hipLaunchKernelGGL(big ? k_tr_hist<TR_PER_BIG> : k_tr_hist<TR_PER_SMALL>, dim3(nb), dim3(TRB),
+                           (size_t)nbin * sizeof(int32_t), st, off, T, nbin, hist);
         if (!lscan) {
             MR_TRY(boff.alloc(ctx, (size_t)nbin + 1));
             MR_TRY(tmp.alloc(ctx, (size_t)scan_tmp_elems(nbin)));
             MR_TRY(mr_exclusive_scan_i32(ctx, hist, boff.p, nbin, tmp.p));
         }
-        hipLaunchKernelGGL(k_tr_place, dim3(nb), dim3(TRB), 2 * (size_t)nbin * sizeof(int32_t), st, off, T, nbin,
+        hipLaunchKernelGGL(big ? k_tr_place<TR_PER_BIG> : k_tr_place<TR_PER_SMALL>, dim3(nb), dim3(TRB),
+                           2 * (size_t)nbin * sizeof(int32_t), st, off, T, nbin,
                            lscan ? (const int64_t*)nullptr : boff.p, hist, taken, g->w_t.p, g->tperm.p, g->w_tp.p);
     }
     {   // chunk counts per wave tile, their prefix and its int32 copy: one launch
