@@ -402,8 +402,19 @@ static int win_detect_build_async(mr_ctx* ctx, const mr_spans* s, int64_t t0, in
     }
     MR_TRY(mr_ix_finish(ctx, s, w.gn, bn, bn.small ? h + CW : nullptr));
     MR_TRY(mr_ix_finish(ctx, s, w.ga, ba, ba.small ? h + CW + 8 : nullptr));
-    MR_TRY(mr_pagerank_presetup(ctx, w.gn, 0, 0.85, precision, 0));
-    MR_TRY(mr_pagerank_presetup(ctx, w.ga, 1, 0.85, precision, 0));
+    // the graphs' kinds / preference / iteration state: small windows (C3: 20k traces) leave it to
+    // the PageRank stream, which sets up the whole group's graphs in six launches
+    // (pagerank_setup_batch) -- the host's launches, not the GPU, bound them; large windows (C2:
+    // 200k traces) set up here, where the work overlaps the previous group's iterations.
+    // MR_WIN_SETUP_SPLIT: traces of a window from which it sets up here (default 65536)
+    static const int64_t split = [] {
+        const char* e = getenv("MR_WIN_SETUP_SPLIT");
+        return e ? (int64_t)atoll(e) : (int64_t)65536;
+    }();
+    if ((int64_t)w.gn->T + w.ga->T >= split) {
+        MR_TRY(mr_pagerank_presetup(ctx, w.gn, 0, 0.85, precision, 0));
+        MR_TRY(mr_pagerank_presetup(ctx, w.ga, 1, 0.85, precision, 0));
+    }
     if (!w.ev) MR_TRY_HIP(ctx, hipEventCreateWithFlags(&w.ev, hipEventDisableTiming));
     MR_TRY_HIP(ctx, hipEventRecord(w.ev, st));
     return MR_OK;

@@ -616,9 +616,10 @@ __device__ __forceinline__ void kind_block_hash(const int64_t* off, const int32_
 }
 
 template <bool CHK, bool U16>
-__global__ void __launch_bounds__(KB) k_kind_insert(const int64_t* off, const int32_t* ops, const uint16_t* o16,
-                                                    const float* w_t, int32_t T, unsigned long long* hk, KCnt* cr, int32_t* slot_of,
-                                                    uint64_t mask, uint64_t seed, uint64_t* chk, uint64_t hmask) {
+__device__ __forceinline__ void kind_insert_body(int32_t blk, const int64_t* off, const int32_t* ops, const uint16_t* o16,
+                                                 const float* w_t, int32_t T, unsigned long long* hk, KCnt* cr,
+                                                 int32_t* slot_of, uint64_t mask, uint64_t seed, uint64_t* chk,
+                                                 uint64_t hmask) {
     __shared__ unsigned long long lkey[KLDS];
     __shared__ uint32_t lcnt[KLDS];
     __shared__ int32_t lrep[KLDS];
@@ -631,7 +632,7 @@ __global__ void __launch_bounds__(KB) k_kind_insert(const int64_t* off, const in
         lcnt[i] = 0u;
         lrep[i] = -1;
     }
-    const int32_t tb = blockIdx.x * KB;
+    const int32_t tb = blk * KB;
     const int32_t t = tb + threadIdx.x;
     uint64_t h = 0, h2 = 0;
     kind_block_hash<CHK, U16>(off, ops, o16, w_t, T, tb, seed, loff, lacc, lacc2, &h, &h2);
@@ -670,6 +671,12 @@ __global__ void __launch_bounds__(KB) k_kind_insert(const int64_t* off, const in
     }
     __syncthreads();
     if (t < T) slot_of[t] = lglob[myslot];
+}
+template <bool CHK, bool U16>
+__global__ void __launch_bounds__(KB) k_kind_insert(const int64_t* off, const int32_t* ops, const uint16_t* o16,
+                                                    const float* w_t, int32_t T, unsigned long long* hk, KCnt* cr, int32_t* slot_of,
+                                                    uint64_t mask, uint64_t seed, uint64_t* chk, uint64_t hmask) {
+    kind_insert_body<CHK, U16>((int32_t)blockIdx.x, off, ops, o16, w_t, T, hk, cr, slot_of, mask, seed, chk, hmask);
 }
 
 template <typename ID>   // int32 ids, or their u16 copy (rs16)
@@ -953,6 +960,137 @@ __device__ __forceinline__ unsigned long long d2bits(double v) {
 }
 
 constexpr int TR_PAD = WAVE;   // k_tr_a's pad ids N .. N + 63 (su = 0)
+__device__ __forceinline__ int32_t cdiv_d(int32_t a, int32_t b) { return (a + b - 1) / b; }
+// ---------------------------------------------------------------- batched set-up
+// The set-up of many window graphs (reset + iteration state, kinds, preference) as ONE launch per
+// step for all of them (a block range per graph, as the iteration's launches are), instead of six
+// launches per graph from the windows' host threads.  Same bodies, same results.
+struct SDev {
+    int32_t T, N, anomaly, fp32;
+    int64_t cap, T_all;
+    float cd;
+    int32_t b_reset, b_kins, b_kver, b_pref;   // the graph's first block in each launch
+    float *pref, *c_t, *c_tp;
+    const int32_t* tperm;
+    unsigned long long* hk;
+    KCnt* cr;
+    int32_t *slot_of, *flag;
+    double *kind, *scal, *ppart;
+    const float *w_t, *w_tq, *u_o;              // w_t by trace; in q's order (position order for k_tr_a graphs)
+    double *sp0, *su0, *su1, *q64;
+    float* q32;
+    unsigned long long* mslot;
+    const int32_t* perm;
+    const int64_t* off;
+    const uint16_t* o16;
+    const int32_t* len_t;
+};
+__device__ __forceinline__ int32_t sd_graph(const SDev* sd, int32_t ng, int32_t blk, int which) {
+    int32_t lo = 0, hi = ng - 1;
+    while (lo < hi) {
+        const int32_t mid = (lo + hi + 1) >> 1;
+        const SDev& g = sd[mid];
+        const int32_t s0 = which == 0 ? g.b_reset : which == 1 ? g.b_kins : which == 2 ? g.b_kver : g.b_pref;
+        if (s0 <= blk) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+__global__ void k_reset_init_b(const SDev* __restrict__ sd, int32_t ng) {
+    const SDev& G = sd[sd_graph(sd, ng, (int32_t)blockIdx.x, 0)];
+    const int64_t i = (int64_t)((int32_t)blockIdx.x - G.b_reset) * blockDim.x + threadIdx.x;
+    const int32_t T = G.T, N = G.N;
+    if (i < T) {
+        G.pref[i] = 0.0f;
+        G.c_t[i] = 0.0f;
+    }
+    if (i < G.cap) {
+        G.hk[i] = 0ull;
+        G.cr[i] = KCnt{0u, -1};
+    }
+    if (i < 8) G.flag[i] = 0;
+    if (i < 8) G.scal[i] = 0.0;
+    const double v0 = 1.0 / (double)((int64_t)N + G.T_all);      // pagerank.py:118-119
+    if (i < N) {
+        G.sp0[i] = v0;
+        G.su0[i] = (double)G.u_o[G.perm ? G.perm[i] : i] * v0;
+    }
+    if (i >= N && i < N + TR_PAD) G.su0[i] = G.su1[i] = 0.0;
+    if (i < T) {
+        const double q = (double)G.w_tq[i] * v0;
+        if (G.fp32) G.q32[i] = (float)q; else G.q64[i] = q;
+    }
+    if (i < 6 * MSH) G.mslot[i] = i < 2 * MSH ? d2bits(1.0) : 0ull;
+}
+__global__ void __launch_bounds__(KB) k_kind_insert_b(const SDev* __restrict__ sd, int32_t ng, uint64_t seed,
+                                                      uint64_t hmask) {
+    const SDev& G = sd[sd_graph(sd, ng, (int32_t)blockIdx.x, 1)];
+    kind_insert_body<false, true>((int32_t)blockIdx.x - G.b_kins, G.off, nullptr, G.o16, G.w_t, G.T, G.hk, G.cr,
+                                  G.slot_of, (uint64_t)(G.cap - 1), seed, nullptr, hmask);
+}
+__global__ void k_kind_verify_b(const SDev* __restrict__ sd, int32_t ng) {
+    const SDev& G = sd[sd_graph(sd, ng, (int32_t)blockIdx.x, 2)];
+    const int32_t t = ((int32_t)blockIdx.x - G.b_kver) * blockDim.x + threadIdx.x;
+    if (t >= G.T) return;
+    const KCnt ks = G.cr[G.slot_of[t]];
+    const int32_t r = ks.rep;
+    G.kind[t] = (double)ks.cnt;
+    if (r == t) return;
+    const int64_t a0 = G.off[t], a1 = G.off[t + 1], b0 = G.off[r], b1 = G.off[r + 1];
+    bool eq = (a1 - a0) == (b1 - b0);
+    if (eq && a1 > a0) eq = __float_as_uint(G.w_t[t]) == __float_as_uint(G.w_t[r]);
+    for (int64_t i = 0; eq && i < a1 - a0; ++i) eq = G.o16[a0 + i] == G.o16[b0 + i];
+    if (!eq) atomicOr(G.flag, 1);
+}
+__global__ void k_pref_partial_b(const SDev* __restrict__ sd, int32_t ng) {
+    __shared__ double red[TB / WAVE];
+    const SDev& G = sd[sd_graph(sd, ng, (int32_t)blockIdx.x, 3)];
+    const int32_t blk = (int32_t)blockIdx.x - G.b_pref;
+    double a = 0.0, b = 0.0;
+    const int32_t i = blk * blockDim.x + threadIdx.x;
+    if (i < G.T) {
+        const int32_t ln = G.len_t[i];
+        a = 1.0 / G.kind[i];
+        if (ln == 0) atomicOr(G.flag + 1, 1);
+        b = ln ? 1.0 / (double)ln : 0.0;
+    }
+    a = block_sum(a, red);
+    b = block_sum(b, red);
+    if (threadIdx.x == 0) {
+        G.ppart[2 * blk] = a;
+        G.ppart[2 * blk + 1] = b;
+    }
+}
+__global__ void k_pref_total_b(const SDev* __restrict__ sd) {   // block g: graph g
+    __shared__ double red[1024 / WAVE];
+    const SDev& G = sd[blockIdx.x];
+    const int32_t nb = cdiv_d(G.T, TB);
+    double a = 0.0, b = 0.0;
+    for (int32_t i = threadIdx.x; i < nb; i += blockDim.x) {
+        a += G.ppart[2 * i];
+        b += G.ppart[2 * i + 1];
+    }
+    a = block_sum(a, red);
+    b = block_sum(b, red);
+    if (threadIdx.x == 0) {
+        G.scal[2] = a;
+        G.scal[3] = b;
+    }
+}
+__global__ void k_pref_apply_b(const SDev* __restrict__ sd, int32_t ng) {
+    const SDev& G = sd[sd_graph(sd, ng, (int32_t)blockIdx.x, 3)];
+    const int32_t i = ((int32_t)blockIdx.x - G.b_pref) * blockDim.x + threadIdx.x;   // position
+    if (i >= G.T) return;
+    const int32_t t = G.tperm[i];
+    const double k = G.kind[t];
+    double v;
+    if (!G.anomaly) v = 1.0 / k / G.scal[2];                                               // :74
+    else v = 1.0 / (k / G.scal[2] * 0.5 + 1.0 / (double)G.len_t[t]) / G.scal[3] * 0.5;     // :80-85
+    const float vf = (float)v;
+    G.pref[t] = vf;
+    G.c_t[t] = G.cd * vf;   // (1.0 - d) * v in float32 (T4)
+    G.c_tp[i] = G.cd * vf;
+}
+
 
 // T_all: traces of the whole graph (all shards) for the initial value
 // perm (relabelled fused graphs): su is kept in the kernel's op labels, su[new] = u_o[perm[new]] s
@@ -1038,6 +1176,8 @@ struct GDev {
     double* spb[2];
     double* part;
     unsigned long long* mslot;
+    double *sn, *weight, *scal;    // k_weights_batch: normalised s, weights, scalars
+    const int32_t* flag;           // the graph's error words (gathered after the iterations)
     unsigned long long* fx_part;
     double* fx_ssv;
     unsigned long long* fx_limb;   // sharded: [2N] (lo, hi) limb sums per op, then [nranks] r' maxima
@@ -2459,6 +2599,50 @@ __global__ void __launch_bounds__(1024) k_weights(const double* sp, const unsign
     for (int32_t o = threadIdx.x; o < N; o += blockDim.x) weight[o] = sn[o] * total / (double)N;
     if (threadIdx.x == 0) scal[4] = total;
 }
+// k_weights for every graph of a batch (block g: graph g) plus a gather of each graph's four error
+// words into one buffer, so the call's single read-back is one pinned copy
+__global__ void __launch_bounds__(1024) k_weights_batch(const GDev* __restrict__ gs, int iters, int exact,
+                                                        int32_t* flags_out) {
+    const GDev& G = gs[blockIdx.x];
+    if (threadIdx.x < 4) flags_out[4 * blockIdx.x + threadIdx.x] = G.flag[threadIdx.x];
+    __shared__ double red[1024 / WAVE];
+    __shared__ double tot;
+    const double* sp = G.spb[iters & 1];
+    const int k3 = iters % 3;
+    const int32_t N = G.N;
+    double* sn = G.sn;
+    double ms = -__builtin_huge_val();
+    for (int i = threadIdx.x; i < MSH; i += blockDim.x) ms = nmax(ms, bits2d(G.mslot[(size_t)2 * MSH * k3 + i]));
+    const double Ms = block_max(ms, red);
+    double m = -__builtin_huge_val();
+    for (int32_t o = threadIdx.x; o < N; o += blockDim.x) {
+        double v = sp[o] / Ms;
+        sn[o] = v;
+        m = nmax(m, v);
+    }
+    m = block_max(m, red);
+    for (int32_t o = threadIdx.x; o < N; o += blockDim.x) sn[o] = sn[o] / m;
+    __syncthreads();
+    if (exact) {
+        if (threadIdx.x == 0) {
+            double s = 0.0;
+            for (int32_t o = 0; o < N; ++o) s += sn[o];
+            tot = s;
+        }
+        __syncthreads();
+    } else {
+        int32_t per = (N + blockDim.x - 1) / blockDim.x;
+        int32_t a = threadIdx.x * per, b = min(a + per, N);
+        double s = 0.0;
+        for (int32_t o = a; o < b; ++o) s += sn[o];
+        s = block_sum(s, red);
+        if (threadIdx.x == 0) tot = s;
+        __syncthreads();
+    }
+    const double total = tot;
+    for (int32_t o = threadIdx.x; o < N; o += blockDim.x) G.weight[o] = sn[o] * total / (double)N;
+    if (threadIdx.x == 0) G.scal[4] = total;
+}
 // ---------------------------------------------------------------- trace-sharded graphs
 // local call edges (child, parent) as sort keys c << nb | p
 __global__ void k_sh_edge_keys(const int64_t* ss_off, const int32_t* ss_par, int32_t N, int nb, uint64_t* key) {
@@ -3233,6 +3417,103 @@ static int pagerank_setup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool 
     return MR_OK;
 }
 
+// Can pagerank_setup of g run inside a batched set-up?  The window graphs' case: a whole graph on
+// one rank, kinds through the hash table with u16 ids, pr_trace = operation_trace, k_tr_a layout.
+static bool setup_batchable(const mr_graph* g, bool tr_plan, uint32_t flags) {
+    const char* kpe = getenv("MR_KIND_PART_MIN");
+    const int64_t kp_min = kpe ? (int64_t)atoll(kpe) : (int64_t)(1 << 21);
+    return g->T > 0 && (int64_t)g->T < kp_min && !g->kinds_given && !g->mult.p && g->rs_is_sr && g->rs16.p &&
+           g->pr_identity && g->n_pr == g->T && g->fused && tr_plan && g->tperm.p && g->w_tp.p && !g->mw_tp.p &&
+           !(flags & MR_PR_EXACT_SUMS) && g->T_all == 0;
+}
+
+// pagerank_setup of several graphs (all setup_batchable) in six launches
+// hs / dsd: the descriptors (host and device), owned by the caller until its stream work is done
+static int pagerank_setup_batch(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly, int ng, double d, bool fp32,
+                                uint64_t seed, uint64_t hmask, std::vector<SDev>& hs, DBuf<SDev>& dsd) {
+    hipStream_t st = ctx->stream;
+    hs.assign((size_t)ng, SDev{});
+    int32_t br = 0, bk = 0, bv = 0, bp = 0;
+    for (int i = 0; i < ng; ++i) {
+        mr_graph* g = gs[i];
+        const int32_t N = g->N, T = g->T;
+        uint64_t cap = 1;
+        while (cap < 2ull * (uint64_t)T) cap <<= 1;
+        const int nbp = cdiv(T, TB);
+        MR_TRY(g->kind.alloc(ctx, (size_t)T));
+        MR_TRY(g->pref.alloc(ctx, (size_t)T));
+        MR_TRY(g->c_t.alloc(ctx, (size_t)T));
+        MR_TRY(g->flag.alloc(ctx, 8));
+        MR_TRY(g->scal.alloc(ctx, 8));
+        MR_TRY(g->ppart.alloc(ctx, 2 * (size_t)nbp));
+        MR_TRY(g->ht_key.alloc(ctx, cap));
+        MR_TRY(g->ht_cr.alloc(ctx, cap));
+        MR_TRY(g->slot_of.alloc(ctx, (size_t)T));
+        MR_TRY(g->mslot.alloc(ctx, 6 * MSH));
+        MR_TRY(g->sn.alloc(ctx, (size_t)N));
+        MR_TRY(g->spb[0].alloc(ctx, (size_t)N));
+        MR_TRY(g->spb[1].alloc(ctx, (size_t)N));
+        MR_TRY(g->sub[0].alloc(ctx, (size_t)N + TR_PAD));
+        MR_TRY(g->sub[1].alloc(ctx, (size_t)N + TR_PAD));
+        MR_TRY(g->weight.alloc(ctx, (size_t)N));
+        MR_TRY(g->c_tp.alloc(ctx, (size_t)std::max(T, 1)));
+        MR_TRY(g->fx_ssv.alloc(ctx, (size_t)N));
+        for (int j = 0; j < 2; ++j) {
+            if (fp32) MR_TRY(g->q32[j].alloc(ctx, (size_t)T + 1));
+            else MR_TRY(g->q64[j].alloc(ctx, (size_t)T + 1));
+        }
+        SDev& v = hs[(size_t)i];
+        v.T = T;
+        v.N = N;
+        v.anomaly = anomaly[i];
+        v.fp32 = fp32 ? 1 : 0;
+        v.cap = (int64_t)cap;
+        v.T_all = T;
+        v.cd = (float)(1.0 - d);
+        v.pref = g->pref.p;
+        v.c_t = g->c_t.p;
+        v.c_tp = g->c_tp.p;
+        v.tperm = g->tperm.p;
+        v.hk = g->ht_key.p;
+        v.cr = g->ht_cr.p;
+        v.slot_of = g->slot_of.p;
+        v.flag = g->flag.p;
+        v.kind = g->kind.p;
+        v.scal = g->scal.p;
+        v.ppart = g->ppart.p;
+        v.w_t = g->w_t.p;
+        v.w_tq = g->w_tp.p;
+        v.u_o = g->u_o.p;
+        v.sp0 = g->spb[0].p;
+        v.su0 = g->sub[0].p;
+        v.su1 = g->sub[1].p;
+        v.q64 = g->q64[0].p;
+        v.q32 = g->q32[0].p;
+        v.mslot = g->mslot.p;
+        v.perm = g->relabeled ? g->perm.p : nullptr;
+        v.off = g->rs_off.p;
+        v.o16 = g->rs16.p;
+        v.len_t = g->len_t.p;
+        v.b_reset = br;
+        br += cdiv(std::max<int64_t>({(int64_t)T, (int64_t)cap, (int64_t)N + TR_PAD, 6 * MSH, 16}), 256);
+        v.b_kins = bk;
+        bk += cdiv(T, KB);
+        v.b_kver = bv;
+        bv += cdiv(T, 256);
+        v.b_pref = bp;
+        bp += nbp;
+    }
+    MR_TRY(dsd.upload(ctx, hs.data(), hs.size()));
+    hipLaunchKernelGGL(k_reset_init_b, dim3(br), dim3(256), 0, st, dsd.p, ng);
+    hipLaunchKernelGGL(k_kind_insert_b, dim3(bk), dim3(KB), 0, st, dsd.p, ng, seed, hmask);
+    hipLaunchKernelGGL(k_kind_verify_b, dim3(bv), dim3(256), 0, st, dsd.p, ng);
+    hipLaunchKernelGGL(k_pref_partial_b, dim3(bp), dim3(TB), 0, st, dsd.p, ng);
+    hipLaunchKernelGGL(k_pref_total_b, dim3(ng), dim3(1024), 0, st, dsd.p);
+    hipLaunchKernelGGL(k_pref_apply_b, dim3(bp), dim3(TB), 0, st, dsd.p, ng);
+    MR_TRY_HIP(ctx, hipGetLastError());
+    return MR_OK;
+}
+
 // Kinds of g (pagerank.py:54-66) into g->kind, the class representative of each trace into
 // g->krep when that is allocated; a 64-bit key collision sets flag word 0.
 static int graph_kinds(mr_ctx* ctx, mr_graph* g, bool chk, bool ktab, uint64_t cap, uint64_t seed, uint64_t hmask) {
@@ -3334,12 +3615,29 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         if (gs[i]->fused) TT = std::min(TT, fx_tt(gs[i]->N));
     const FxPlan plan = fx_plan(gs, ng);
     if (plan.v2) TT = WAVE;   // wave tiles
-    for (int i = 0; i < ng; ++i) {
-        mr_graph* g = gs[i];
-        const bool pre = g->pre_ok && g->pre_anomaly == anomaly[i] && g->pre_d == d && g->pre_fp32 == fp32 &&
-                         g->pre_flags == flags && g->pre_seed == seed && g->pre_hmask == hmask && !sharded;
-        g->pre_ok = false;   // the iteration state is consumed by this call
-        if (!pre) MR_TRY(pagerank_setup(ctx, g, anomaly[i], d, fp32, flags, plan.tr, sharded, seed, hmask));
+    std::vector<SDev> setup_h;   // (batched set-up descriptors: alive until the call's final sync)
+    DBuf<SDev> setup_d;
+    {   // set-up of every graph not set up ahead (mr_pagerank_presetup): batched when they allow it
+        std::vector<mr_graph*> need;
+        std::vector<int> need_a;
+        bool batch = !sharded && getenv("MR_NO_SETUP_BATCH") == nullptr;
+        for (int i = 0; i < ng; ++i) {
+            mr_graph* g = gs[i];
+            const bool pre = g->pre_ok && g->pre_anomaly == anomaly[i] && g->pre_d == d && g->pre_fp32 == fp32 &&
+                             g->pre_flags == flags && g->pre_seed == seed && g->pre_hmask == hmask && !sharded;
+            g->pre_ok = false;   // the iteration state is consumed by this call
+            if (pre) continue;
+            need.push_back(g);
+            need_a.push_back(anomaly[i]);
+            batch = batch && setup_batchable(g, plan.tr, flags);
+        }
+        if (batch && need.size() >= 2) {
+            MR_TRY(pagerank_setup_batch(ctx, need.data(), need_a.data(), (int)need.size(), d, fp32, seed, hmask,
+                                        setup_h, setup_d));
+        } else {
+            for (size_t j = 0; j < need.size(); ++j)
+                MR_TRY(pagerank_setup(ctx, need[j], need_a[j], d, fp32, flags, plan.tr, sharded, seed, hmask));
+        }
     }
     int64_t wsum = 0;   // wave tiles of the launch's fused graphs (k_tr_a's block budget)
     for (int i = 0; i < ng; ++i)
@@ -3407,6 +3705,10 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         }
         v.part = g->part.p;
         v.mslot = g->mslot.p;
+        v.sn = g->sn.p;
+        v.weight = g->weight.p;
+        v.scal = g->scal.p;
+        v.flag = g->flag.p;
         v.fx_part = (unsigned long long*)g->fx_part.p;
         v.fx_ssv = g->fx_ssv.p;
         v.fx_limb = (unsigned long long*)g->fx_limb.p;
@@ -3586,12 +3888,14 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         }
         mr_prof_end(ctx, bytes);
     }
-    for (int i = 0; i < ng; ++i) {
-        mr_graph* g = gs[i];
-        hipLaunchKernelGGL(k_weights, dim3(1), dim3(1024), 0, st, g->spb[iters & 1].p, g->mslot.p, iters % 3, g->N,
-                           (int)((flags & MR_PR_EXACT_SUMS) != 0), g->sn.p, g->weight.p, g->scal.p);
-        MR_DEBUG_CHECK(ctx, "k_weights");
-    }
+    // weights of every graph and the gathered error words in one launch (the flags are final:
+    // the kernels that raise them ran before the iterations; a sharded graph's words meet in a
+    // MAX first, below, so it reads them after that)
+    DBuf<int32_t> fl;
+    MR_TRY(fl.alloc(ctx, (size_t)4 * ng));
+    hipLaunchKernelGGL(k_weights_batch, dim3(ng), dim3(1024), 0, st, dv.p, iters, (int)((flags & MR_PR_EXACT_SUMS) != 0),
+                       fl.p);
+    MR_DEBUG_CHECK(ctx, "k_weights");
     MR_TRY_HIP(ctx, hipGetLastError());
     if (dstamp.p) {   // diagnostics: phase times of the last k_fx_a launch, in 10 ns ticks
         std::vector<unsigned long long> h((size_t)blocks_fa * 16);
@@ -3619,12 +3923,20 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         fprintf(stderr, "\n");
     }
     // a shard's local collision must make every rank retry: the error words meet in a MAX
-    if (coll) MR_TRY(mr_coll_allreduce(ctx, gs[0]->flag.p, 4, MR_DT_I32, 1));
-    // the only host round trip of the call: error words raised by the kernels
+    if (coll) {
+        MR_TRY(mr_coll_allreduce(ctx, gs[0]->flag.p, 4, MR_DT_I32, 1));
+        MR_TRY_HIP(ctx, hipMemcpyAsync(fl.p, gs[0]->flag.p, 4 * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
+    }
+    // the only host round trip of the call: error words raised by the kernels (one pinned read)
     std::vector<int32_t> hflag((size_t)4 * ng, 0);
-    for (int i = 0; i < ng; ++i)
-        MR_TRY_HIP(ctx, hipMemcpyAsync(&hflag[(size_t)4 * i], gs[i]->flag.p, 4 * sizeof(int32_t), hipMemcpyDeviceToHost, st));
-    MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+    if ((size_t)4 * ng * sizeof(int32_t) <= MR_PIN_BYTES) {
+        unsigned char* hp = nullptr;
+        MR_TRY(mr_read_bytes(ctx, fl.p, (size_t)4 * ng * sizeof(int32_t), &hp));
+        memcpy(hflag.data(), hp, hflag.size() * sizeof(int32_t));
+    } else {
+        MR_TRY(fl.download(ctx, hflag.data(), hflag.size()));
+        MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+    }
     for (int i = 0; i < ng; ++i) {
         if (hflag[(size_t)4 * i] & 1) {
             *collided = true;
