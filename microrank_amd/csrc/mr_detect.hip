@@ -295,6 +295,7 @@ struct WinRun {
     int64_t nin = 0;
     mr_graph *gn = nullptr, *ga = nullptr;   // "normal" graph (detector's abnormal traces), "anomaly" graph
     hipEvent_t ev = nullptr;                 // batch: the window's graphs are ready on its stream
+    std::vector<unsigned char> keep;         // batch: host descriptors of its graphs' batched prepare
     bool slot = false;                       // batch: its spectrum went to the device result slot
     ~WinRun() {
         delete gn;
@@ -400,8 +401,8 @@ static int win_detect_build_async(mr_ctx* ctx, const mr_spans* s, int64_t t0, in
         if (w.nin == 0) return mr_fail(ctx, MR_ERR_VALUE, "Current span list is empty");
         return MR_OK;
     }
-    MR_TRY(mr_ix_finish(ctx, s, w.gn, bn, bn.small ? h + CW : nullptr));
-    MR_TRY(mr_ix_finish(ctx, s, w.ga, ba, ba.small ? h + CW + 8 : nullptr));
+    MR_TRY(mr_ix_finish2(ctx, s, w.gn, bn, bn.small ? h + CW : nullptr, w.ga, ba, ba.small ? h + CW + 8 : nullptr,
+                         w.keep));
     // the graphs' kinds / preference / iteration state: small windows (C3: 20k traces) leave it to
     // the PageRank stream, which sets up the whole group's graphs in six launches
     // (pagerank_setup_batch) -- the host's launches, not the GPU, bound them; large windows (C2:

@@ -1522,6 +1522,18 @@ int mr_ix_finish(mr_ctx* ctx, const mr_spans* sp, mr_graph* g, IxBuild& b, const
     MR_TRY(ix_finish(ctx, sp, g, b, h, false));
     return mr_graph_post_build(ctx, g);
 }
+int mr_ix_finish2(mr_ctx* ctx, const mr_spans* sp, mr_graph* g0, IxBuild& b0, const int64_t* h0, mr_graph* g1,
+                  IxBuild& b1, const int64_t* h1, std::vector<unsigned char>& keep) {
+    MR_TRY(ix_finish(ctx, sp, g0, b0, h0, false));
+    MR_TRY(ix_finish(ctx, sp, g1, b1, h1, false));
+    mr_graph* gs[2] = {g0, g1};
+    for (mr_graph* g : gs) {   // (mr_graph_post_build's fields)
+        g->rs_is_sr = true;
+        g->pr_identity = true;
+        g->n_pr = g->T;
+    }
+    return mr_graph_prepare_batch(ctx, gs, 2, keep);
+}
 
 // a built graph's trace-role fields and derived arrays (the K1 result is P_rs = P_sr)
 int mr_graph_post_build(mr_ctx* ctx, mr_graph* g) {

@@ -321,6 +321,8 @@ struct PhaseTimer {
 inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 
 int mr_graph_prepare(mr_ctx* ctx, mr_graph* g);   // derived arrays + segments after structure upload
+// several graphs' prepare in one launch per step when they allow it (keep: host descriptors)
+int mr_graph_prepare_batch(mr_ctx* ctx, mr_graph* const* gs, int n, std::vector<unsigned char>& keep);
 int mr_graph_post_build(mr_ctx* ctx, mr_graph* g);   // trace-role fields + mr_graph_prepare after K1
 // An indexed K1 build between its launches and its size read-back (mr_graph_build.hip): several
 // builds (and the detector's counters) share one host round trip.  d_out receives 5 int64 words
@@ -352,4 +354,7 @@ int mr_win_spectrum_launch(mr_ctx* ctx, int32_t Na, const int32_t* a_podop, cons
                            int64_t A, int64_t Nl, int method, int32_t k, unsigned char* d_slot);
 void mr_win_spectrum_unpack(const unsigned char* slot, int32_t* out_codes, double* out_score, int32_t* n_out);
 int mr_ix_finish(mr_ctx* ctx, const mr_spans* sp, mr_graph* g, IxBuild& b, const int64_t* h);
+// both graphs of mr_ix_launch2 finished and prepared together (mr_graph_prepare_batch)
+int mr_ix_finish2(mr_ctx* ctx, const mr_spans* sp, mr_graph* g0, IxBuild& b0, const int64_t* h0, mr_graph* g1,
+                  IxBuild& b1, const int64_t* h1, std::vector<unsigned char>& keep);
 int mr_pagerank_presetup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, int precision, uint32_t flags);

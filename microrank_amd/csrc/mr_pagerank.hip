@@ -67,10 +67,11 @@ __global__ void k_op_consts(const int32_t* len_o, const int32_t* nchild, float* 
 // per-graph constants in one launch: w_t = fp32(1/len_t) (fp64 1/n -> fp32), u_o, pw, and the
 // u16 copy of the op ids (N <= 65536)
 // (and clears `nz` words of the layout's scratch: tr_layout's histogram and slot counters)
-__global__ void k_graph_consts(const int32_t* len_t, float* w_t, int32_t T, const int32_t* len_o, const int32_t* nchild,
-                               float* u_o, float* pw, int32_t N, const int32_t* ops, int64_t n, uint16_t* o16,
-                               int32_t* zero, int32_t nz) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void graph_consts_body(int32_t blk, const int32_t* len_t, float* w_t, int32_t T,
+                                                  const int32_t* len_o, const int32_t* nchild, float* u_o, float* pw,
+                                                  int32_t N, const int32_t* ops, int64_t n, uint16_t* o16,
+                                                  int32_t* zero, int32_t nz) {
+    const int64_t i = (int64_t)blk * blockDim.x + threadIdx.x;
     if (i < nz) zero[i] = 0;
     if (i < T) w_t[i] = len_t[i] > 0 ? (float)(1.0 / (double)len_t[i]) : 0.0f;
     if (i < N) {
@@ -78,6 +79,11 @@ __global__ void k_graph_consts(const int32_t* len_t, float* w_t, int32_t T, cons
         pw[i] = nchild[i] > 0 ? (float)(1.0 / (double)nchild[i]) : 0.0f;
     }
     if (o16 && i < n) o16[i] = (uint16_t)ops[i];
+}
+__global__ void k_graph_consts(const int32_t* len_t, float* w_t, int32_t T, const int32_t* len_o, const int32_t* nchild,
+                               float* u_o, float* pw, int32_t N, const int32_t* ops, int64_t n, uint16_t* o16,
+                               int32_t* zero, int32_t nz) {
+    graph_consts_body((int32_t)blockIdx.x, len_t, w_t, T, len_o, nchild, u_o, pw, N, ops, n, o16, zero, nz);
 }
 
 // ---------------------------------------------------------------- P_sr tiles (compressed sparse blocks)
@@ -306,11 +312,11 @@ __global__ void k_wide_span(const int64_t* cb_beg, int32_t n_cb, const int32_t* 
 // thread for large graphs, 2 for window-sized ones (187k traces in 12 blocks had left the chip idle)
 constexpr int TRB = 1024, TR_PER_BIG = 16, TR_PER_SMALL = 2;
 template <int TR_PER>
-__global__ void __launch_bounds__(TRB) k_tr_hist(const int64_t* off, int32_t T, int32_t nbin, int32_t* hist) {
+__device__ __forceinline__ void tr_hist_body(int32_t blk, const int64_t* off, int32_t T, int32_t nbin, int32_t* hist) {
     extern __shared__ int32_t lh[];
     for (int32_t i = threadIdx.x; i < nbin; i += TRB) lh[i] = 0;
     __syncthreads();
-    const int64_t t0 = (int64_t)blockIdx.x * TRB * TR_PER;
+    const int64_t t0 = (int64_t)blk * TRB * TR_PER;
     for (int32_t j = 0; j < TR_PER; ++j) {
         const int64_t t = t0 + (int64_t)j * TRB + threadIdx.x;
         if (t < T) atomicAdd(&lh[off[t + 1] - off[t]], 1);
@@ -319,20 +325,24 @@ __global__ void __launch_bounds__(TRB) k_tr_hist(const int64_t* off, int32_t T, 
     for (int32_t i = threadIdx.x; i < nbin; i += TRB)
         if (lh[i]) atomicAdd(&hist[i], lh[i]);
 }
+template <int TR_PER>
+__global__ void __launch_bounds__(TRB) k_tr_hist(const int64_t* off, int32_t T, int32_t nbin, int32_t* hist) {
+    tr_hist_body<TR_PER>((int32_t)blockIdx.x, off, T, nbin, hist);
+}
 // positions: bin start (cursor, claimed per block and bin) + the trace's rank in its block's bin
 // A bin's slots: boff given -- its start plus the bin's remaining count, handed out from the end
 // (hist is consumed, no cursor copy); boff null (nbin <= TP_LSCAN) -- each block scans the
 // histogram in LDS itself and claims slots through `taken` (no scan launch)
 constexpr int TP_LSCAN = 8192;
 template <int TR_PER>
-__global__ void __launch_bounds__(TRB) k_tr_place(const int64_t* off, int32_t T, int32_t nbin, const int64_t* boff,
-                                                  int32_t* hist, int32_t* taken, const float* w_t, int32_t* tperm,
-                                                  float* w_tp) {
+__device__ __forceinline__ void tr_place_body(int32_t blk, const int64_t* off, int32_t T, int32_t nbin,
+                                              const int64_t* boff, int32_t* hist, int32_t* taken, const float* w_t,
+                                              int32_t* tperm, float* w_tp) {
     extern __shared__ int32_t lh[];
     int32_t* lbase = lh + nbin;
     for (int32_t i = threadIdx.x; i < nbin; i += TRB) lh[i] = 0;
     __syncthreads();
-    const int64_t t0 = (int64_t)blockIdx.x * TRB * TR_PER;
+    const int64_t t0 = (int64_t)blk * TRB * TR_PER;
     int32_t rk[TR_PER], ln[TR_PER];
 #pragma unroll
     for (int32_t j = 0; j < TR_PER; ++j) {
@@ -374,17 +384,23 @@ __global__ void __launch_bounds__(TRB) k_tr_place(const int64_t* off, int32_t T,
         w_tp[p] = w_t[t];
     }
 }
+template <int TR_PER>
+__global__ void __launch_bounds__(TRB) k_tr_place(const int64_t* off, int32_t T, int32_t nbin, const int64_t* boff,
+                                                  int32_t* hist, int32_t* taken, const float* w_t, int32_t* tperm,
+                                                  float* w_tp) {
+    tr_place_body<TR_PER>((int32_t)blockIdx.x, off, T, nbin, boff, hist, taken, w_t, tperm, w_tp);
+}
 // chunks of 4 ids per wave tile (its last position holds its longest trace: lengths ascend), their
 // exclusive prefix and its int32 copy in one launch: runs of TS_TILE wave tiles per block, chained
 // by decoupled look-back
 constexpr int TS_T = 256, TS_I = 8, TS_TILE = TS_T * TS_I;
-__global__ void __launch_bounds__(TS_T) k_tr_chunk_scan(const int32_t* tperm, const int64_t* off, int32_t T, int32_t n_wt,
-                                                        int64_t* c64, int32_t* coff, unsigned long long* st,
-                                                        uint64_t epoch) {
+__device__ __forceinline__ void tr_chunk_scan_body(int32_t tile_, int32_t ntiles, const int32_t* tperm,
+                                                   const int64_t* off, int32_t T, int32_t n_wt, int64_t* c64,
+                                                   int32_t* coff, unsigned long long* st, uint64_t epoch) {
     __shared__ int64_t sa[TS_T];
     __shared__ int64_t ex;
     const int tid = threadIdx.x;
-    const int64_t tile = blockIdx.x, base = tile * TS_TILE + (int64_t)tid * TS_I;
+    const int64_t tile = tile_, base = tile * TS_TILE + (int64_t)tid * TS_I;
     int64_t v[TS_I], a = 0;
 #pragma unroll
     for (int i = 0; i < TS_I; ++i) {
@@ -406,7 +422,7 @@ __global__ void __launch_bounds__(TS_T) k_tr_chunk_scan(const int32_t* tperm, co
     }
     if (tid == 0) {
         ex = dl_lookback(st, tile, sa[TS_T - 1], epoch);
-        if (tile == (int64_t)gridDim.x - 1) {
+        if (tile == (int64_t)ntiles - 1) {
             c64[n_wt] = ex + sa[TS_T - 1];
             coff[n_wt] = (int32_t)(ex + sa[TS_T - 1]);
         }
@@ -423,6 +439,11 @@ __global__ void __launch_bounds__(TS_T) k_tr_chunk_scan(const int32_t* tperm, co
         r += v[i];
     }
 }
+__global__ void __launch_bounds__(TS_T) k_tr_chunk_scan(const int32_t* tperm, const int64_t* off, int32_t T, int32_t n_wt,
+                                                        int64_t* c64, int32_t* coff, unsigned long long* st,
+                                                        uint64_t epoch) {
+    tr_chunk_scan_body((int32_t)blockIdx.x, (int32_t)gridDim.x, tperm, off, T, n_wt, c64, coff, st, epoch);
+}
 __global__ void k_tr_coff(const int64_t* c64, int32_t n, int32_t* coff) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i <= n) coff[i] = (int32_t)c64[i];
@@ -433,8 +454,8 @@ __global__ void k_tr_coff(const int64_t* c64, int32_t n, int32_t* coff) {
 // traces: the fixed-point budget); a cost cut that breaks it falls back to equal tile counts (the
 // host sizes the grid so those fit).  scale = {2^SC, 2^-SC}, SC = 64 - bits(most traces of a block).
 constexpr int TC_T = 1024, TC_MAX = 16384;
-__global__ void __launch_bounds__(TC_T) k_tr_cut(const int32_t* coff, int32_t W, int32_t nw, int32_t NW, int32_t* cut,
-                                                 double* scale) {
+__device__ __forceinline__ void tr_cut_body(const int32_t* coff, int32_t W, int32_t nw, int32_t NW, int32_t* cut,
+                                            double* scale) {
     __shared__ int32_t lc[TC_MAX + 1];
     __shared__ int32_t mx;
     if (threadIdx.x == 0) mx = 0;
@@ -468,10 +489,29 @@ __global__ void __launch_bounds__(TC_T) k_tr_cut(const int32_t* coff, int32_t W,
         scale[1] = __longlong_as_double((long long)(1023 - sc) << 52);
     }
 }
+__global__ void __launch_bounds__(TC_T) k_tr_cut(const int32_t* coff, int32_t W, int32_t nw, int32_t NW, int32_t* cut,
+                                                 double* scale) {
+    tr_cut_body(coff, W, nw, NW, cut, scale);
+}
+// the cuts of a batch's graphs in one launch (block g: graph g)
+struct CutArg {
+    const int32_t* coff;
+    int32_t* cut;
+    double* scale;
+    int32_t W, nw, NW, pad_;
+};
+constexpr int TC_BATCH = 64;
+struct CutBatch {
+    CutArg a[TC_BATCH];
+};
+__global__ void __launch_bounds__(TC_T) k_tr_cut_b(CutBatch b) {
+    const CutArg& x = b.a[blockIdx.x];
+    tr_cut_body(x.coff, x.W, x.nw, x.NW, x.cut, x.scale);
+}
 // thread per (tile, lane): the lane's trace rotated by (trace mod len), then pads N + lane
-__global__ void k_tr_fill(const int32_t* tperm, const int64_t* off, const uint16_t* ids, const int64_t* c64, int32_t T,
-                          int32_t N, int32_t n_wt, uint16_t* tids) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void tr_fill_body(int32_t blk, const int32_t* tperm, const int64_t* off, const uint16_t* ids,
+                                             const int64_t* c64, int32_t T, int32_t N, int32_t n_wt, uint16_t* tids) {
+    const int64_t i = (int64_t)blk * blockDim.x + threadIdx.x;
     if (i >= (int64_t)n_wt * WAVE) return;
     const int32_t k = (int32_t)(i / WAVE), lane = (int32_t)(i % WAVE);
     const int64_t p = (int64_t)k * WAVE + lane;
@@ -496,6 +536,57 @@ __global__ void k_tr_fill(const int32_t* tperm, const int64_t* off, const uint16
         }
         dst[(size_t)c * WAVE] = v;
     }
+}
+__global__ void k_tr_fill(const int32_t* tperm, const int64_t* off, const uint16_t* ids, const int64_t* c64, int32_t T,
+                          int32_t N, int32_t n_wt, uint16_t* tids) {
+    tr_fill_body((int32_t)blockIdx.x, tperm, off, ids, c64, T, N, n_wt, tids);
+}
+// The prepare of several small fused graphs (a window's two) in one launch per step: block ranges
+// per graph, the same bodies (mr_graph_prepare_batch)
+struct PDev {
+    int32_t T, N, nbin, W, nz, n_cs;
+    int64_t nnz, st_off;
+    int32_t b_gc, b_th, b_cs, b_fill;
+    const int32_t *len_t, *len_o, *nchild, *rs_ops;
+    const int64_t* rs_off;
+    float *w_t, *u_o, *pw, *w_tp;
+    uint16_t *rs16, *tids;
+    int32_t *trz, *tperm, *coff;
+    int64_t* c64;
+};
+__device__ __forceinline__ int32_t pd_graph(const PDev* pd, int32_t n, int32_t blk, int which) {
+    int32_t lo = 0, hi = n - 1;
+    while (lo < hi) {
+        const int32_t mid = (lo + hi + 1) >> 1;
+        const PDev& g = pd[mid];
+        const int32_t s0 = which == 0 ? g.b_gc : which == 1 ? g.b_th : which == 2 ? g.b_cs : g.b_fill;
+        if (s0 <= blk) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+__global__ void k_graph_consts_b(const PDev* __restrict__ pd, int32_t n) {
+    const PDev& G = pd[pd_graph(pd, n, (int32_t)blockIdx.x, 0)];
+    graph_consts_body((int32_t)blockIdx.x - G.b_gc, G.len_t, G.w_t, G.T, G.len_o, G.nchild, G.u_o, G.pw, G.N, G.rs_ops,
+                      G.nnz, G.rs16, G.trz, G.nz);
+}
+__global__ void __launch_bounds__(TRB) k_tr_hist_b(const PDev* __restrict__ pd, int32_t n) {
+    const PDev& G = pd[pd_graph(pd, n, (int32_t)blockIdx.x, 1)];
+    tr_hist_body<TR_PER_SMALL>((int32_t)blockIdx.x - G.b_th, G.rs_off, G.T, G.nbin, G.trz);
+}
+__global__ void __launch_bounds__(TRB) k_tr_place_b(const PDev* __restrict__ pd, int32_t n) {
+    const PDev& G = pd[pd_graph(pd, n, (int32_t)blockIdx.x, 1)];
+    tr_place_body<TR_PER_SMALL>((int32_t)blockIdx.x - G.b_th, G.rs_off, G.T, G.nbin, nullptr, G.trz, G.trz + G.nbin,
+                                G.w_t, G.tperm, G.w_tp);
+}
+__global__ void __launch_bounds__(TS_T) k_tr_chunk_scan_b(const PDev* __restrict__ pd, int32_t n, unsigned long long* st,
+                                                         uint64_t epoch) {
+    const PDev& G = pd[pd_graph(pd, n, (int32_t)blockIdx.x, 2)];
+    tr_chunk_scan_body((int32_t)blockIdx.x - G.b_cs, G.n_cs, G.tperm, G.rs_off, G.T, G.W, G.c64, G.coff, st + G.st_off,
+                       epoch);
+}
+__global__ void k_tr_fill_b(const PDev* __restrict__ pd, int32_t n) {
+    const PDev& G = pd[pd_graph(pd, n, (int32_t)blockIdx.x, 3)];
+    tr_fill_body((int32_t)blockIdx.x - G.b_fill, G.tperm, G.rs_off, G.rs16, G.c64, G.T, G.N, G.W, G.tids);
 }
 __global__ void k_tr_gather(const float* src, const int32_t* tperm, int32_t T, float* dst) {
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2932,7 +3023,8 @@ static double tr_budget() {
     }();
     return v;
 }
-static int tr_split(mr_ctx* ctx, mr_graph* g, const FxPlan& P, int64_t wsum, int64_t* nfa) {
+static int tr_split(mr_ctx* ctx, mr_graph* g, const FxPlan& P, int64_t wsum, int64_t* nfa,
+                    std::vector<CutArg>* defer = nullptr) {
     const int64_t W = g->n_wt, NW = P.NT / WAVE;
     const int64_t resident = plan_resident(kern_n(g), P);
     int64_t nb = std::max<int64_t>({std::min<int64_t>(resident, cdiv(W, NW)), cdiv(W, 1023), 1});
@@ -2947,9 +3039,13 @@ static int tr_split(mr_ctx* ctx, mr_graph* g, const FxPlan& P, int64_t wsum, int
         if (!(g->wtile.p && g->wtile_nw == nw && g->wtile_msum < 0)) {
             MR_TRY(g->wtile.alloc(ctx, (size_t)nw + 1));
             MR_TRY(g->dscale.alloc(ctx, 2));
-            hipLaunchKernelGGL(k_tr_cut, dim3(1), dim3(TC_T), 0, ctx->stream, g->coff.p, (int32_t)W, (int32_t)nw,
-                               (int32_t)NW, g->wtile.p, g->dscale.p);
-            MR_TRY_HIP(ctx, hipGetLastError());
+            if (defer) {   // launched with the batch's other cuts (k_tr_cut_b)
+                defer->push_back(CutArg{g->coff.p, g->wtile.p, g->dscale.p, (int32_t)W, (int32_t)nw, (int32_t)NW, 0});
+            } else {
+                hipLaunchKernelGGL(k_tr_cut, dim3(1), dim3(TC_T), 0, ctx->stream, g->coff.p, (int32_t)W, (int32_t)nw,
+                                   (int32_t)NW, g->wtile.p, g->dscale.p);
+                MR_TRY_HIP(ctx, hipGetLastError());
+            }
             g->wtile_nw = (int32_t)nw;
             g->wtile_msum = -1;   // the scale is on the device
         }
@@ -3001,8 +3097,9 @@ static int tr_split(mr_ctx* ctx, mr_graph* g, const FxPlan& P, int64_t wsum, int
     return MR_OK;
 }
 
-static int fused_blocks(mr_ctx* ctx, mr_graph* g, const FxPlan& P, int TT_v1, int64_t wsum, int64_t* nfa) {
-    if (P.tr) return tr_split(ctx, g, P, wsum, nfa);
+static int fused_blocks(mr_ctx* ctx, mr_graph* g, const FxPlan& P, int TT_v1, int64_t wsum, int64_t* nfa,
+                        std::vector<CutArg>* defer = nullptr) {
+    if (P.tr) return tr_split(ctx, g, P, wsum, nfa, defer);
     *nfa = P.v2 ? wv_blocks(g->T, g->N, P) : fx_blocks(g->T, g->N, TT_v1);
     return MR_OK;
 }
@@ -3185,6 +3282,106 @@ static int wide_prepare(mr_ctx* ctx, mr_graph* g) {
 
 // Derived per-graph arrays: fp32 reciprocals, u16 ids, and the P_sr tiles.  One host round trip
 // (the number of (tile, op) pairs sizes the pair arrays).
+// mr_graph_prepare of several graphs built from spans (a window's two): one launch per step when
+// all are small fused graphs whose su stays in LDS (no relabelling, one-block histogram scan),
+// else one prepare each.  keep: the descriptors' host copy, alive until the stream has used it.
+int mr_graph_prepare_batch(mr_ctx* ctx, mr_graph* const* gs, int n, std::vector<unsigned char>& keep) {
+    static const bool off = getenv("MR_NO_PREP_BATCH") != nullptr;   // A/B knob
+    bool ok = !off && n >= 2 && plan_is_tr() && getenv("MR_NO_FUSED") == nullptr;
+    for (int i = 0; i < n && ok; ++i) {
+        const mr_graph* g = gs[i];
+        ok = g->rs_is_sr && g->traces_nonempty && !g->force_tile && g->cov_ready && g->N > 0 && g->T > 0 &&
+             g->N <= FX_NMAX && g->N + 1 <= TP_LSCAN && g->nnz_rs == g->nnz_sr && g->nnz_sr < (1ll << 31) &&
+             fx_tt(g->N) > 0 && TrLds(g->N, WV_SU_ALL).su_lds &&
+             (int64_t)g->T < (int64_t)num_cus() * TRB * TR_PER_SMALL * 4;
+    }
+    if (!ok) {
+        for (int i = 0; i < n; ++i) MR_TRY(mr_graph_prepare(ctx, gs[i]));
+        return MR_OK;
+    }
+    hipStream_t st = ctx->stream;
+    keep.assign((size_t)n * sizeof(PDev), 0);
+    PDev* hp = reinterpret_cast<PDev*>(keep.data());
+    std::vector<DBuf<int32_t>> trz((size_t)n);
+    std::vector<DBuf<int64_t>> c64((size_t)n);
+    int32_t bgc = 0, bth = 0, bcs = 0, bfl = 0, nbin_max = 0;
+    int64_t st_words = 0;
+    for (int i = 0; i < n; ++i) {
+        mr_graph* g = gs[i];
+        const int32_t N = g->N, T = g->T, W = cdiv(T, WAVE);
+        const int64_t nnz = g->nnz_sr;
+        MR_TRY(g->w_t.alloc(ctx, (size_t)T));
+        MR_TRY(g->u_o.alloc(ctx, (size_t)N));
+        MR_TRY(g->pw.alloc(ctx, (size_t)N));
+        MR_TRY(g->rs16.alloc(ctx, (size_t)nnz + 8));
+        const int32_t nz = 2 * (N + 1);
+        MR_TRY(trz[(size_t)i].alloc(ctx, (size_t)nz));
+        MR_TRY(c64[(size_t)i].alloc(ctx, (size_t)W + 1));
+        MR_TRY(g->tperm.alloc(ctx, (size_t)std::max(T, 1)));
+        MR_TRY(g->w_tp.alloc(ctx, (size_t)std::max(T, 1)));
+        MR_TRY(g->coff.alloc(ctx, (size_t)W + 1));
+        const int64_t nch = (int64_t)W + (nnz / WAVE + 2 * (int64_t)N) / 4 + 2;   // as tr_layout
+        MR_TRY(g->tids.alloc(ctx, (size_t)std::max<int64_t>(nch, 1) * WAVE * 4));
+        g->relabeled = false;
+        g->wide = false;
+        g->NA = N;
+        g->fused = true;
+        g->perm.reset();
+        g->rsp.reset();
+        g->n_wt = W;
+        g->wtile_nw = 0;
+        g->coff_h.clear();
+        g->n_tiles = 0;
+        g->n_pairs = 0;
+        PDev& v = hp[i];
+        v.T = T;
+        v.N = N;
+        v.nbin = N + 1;
+        v.W = W;
+        v.nz = nz;
+        v.nnz = nnz;
+        v.n_cs = (int32_t)std::max<int64_t>(cdiv((int64_t)W, TS_TILE), 1);
+        v.st_off = st_words;
+        st_words += v.n_cs;
+        v.len_t = g->len_t.p;
+        v.len_o = g->len_o.p;
+        v.nchild = g->nchild.p;
+        v.rs_ops = g->rs_ops.p;
+        v.rs_off = g->rs_off.p;
+        v.w_t = g->w_t.p;
+        v.u_o = g->u_o.p;
+        v.pw = g->pw.p;
+        v.w_tp = g->w_tp.p;
+        v.rs16 = g->rs16.p;
+        v.tids = g->tids.p;
+        v.trz = trz[(size_t)i].p;
+        v.tperm = g->tperm.p;
+        v.coff = g->coff.p;
+        v.c64 = c64[(size_t)i].p;
+        v.b_gc = bgc;
+        bgc += cdiv(std::max<int64_t>({(int64_t)T, (int64_t)N, nnz, (int64_t)nz}), 256);
+        v.b_th = bth;
+        bth += cdiv(T, (int64_t)TRB * TR_PER_SMALL);
+        v.b_cs = bcs;
+        bcs += v.n_cs;
+        v.b_fill = bfl;
+        bfl += cdiv((int64_t)W * WAVE, 256);
+        nbin_max = std::max(nbin_max, N + 1);
+    }
+    DBuf<PDev> dpd;
+    MR_TRY(dpd.upload(ctx, hp, (size_t)n));
+    unsigned long long* dst = nullptr;
+    uint64_t epoch = 0;
+    MR_TRY(mr_dl_status(ctx, st_words, &dst, &epoch));
+    hipLaunchKernelGGL(k_graph_consts_b, dim3(bgc), dim3(256), 0, st, dpd.p, n);
+    hipLaunchKernelGGL(k_tr_hist_b, dim3(bth), dim3(TRB), (size_t)nbin_max * sizeof(int32_t), st, dpd.p, n);
+    hipLaunchKernelGGL(k_tr_place_b, dim3(bth), dim3(TRB), 2 * (size_t)nbin_max * sizeof(int32_t), st, dpd.p, n);
+    hipLaunchKernelGGL(k_tr_chunk_scan_b, dim3(bcs), dim3(TS_T), 0, st, dpd.p, n, dst, epoch);
+    hipLaunchKernelGGL(k_tr_fill_b, dim3(bfl), dim3(256), 0, st, dpd.p, n);
+    MR_TRY_HIP(ctx, hipGetLastError());
+    return MR_OK;   // (scratch returns to the stream-ordered pool)
+}
+
 int mr_graph_prepare(mr_ctx* ctx, mr_graph* g) {
     hipStream_t st = ctx->stream;
     const int32_t N = g->N, T = g->T;
@@ -3642,13 +3839,21 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
     int64_t wsum = 0;   // wave tiles of the launch's fused graphs (k_tr_a's block budget)
     for (int i = 0; i < ng; ++i)
         if (gs[i]->fused) wsum += gs[i]->n_wt;
+    std::vector<CutArg> cuts;   // the graphs' per-wave cuts, launched together
     for (int i = 0; i < ng; ++i) {
         mr_graph* g = gs[i];
         if (g->fused) {   // the plan's blocks: partial rows and (k_tr_a) the per-wave cut
             int64_t nfa = 0;
-            MR_TRY(fused_blocks(ctx, g, plan, TT, wsum, &nfa));
+            MR_TRY(fused_blocks(ctx, g, plan, TT, wsum, &nfa, &cuts));
             MR_TRY(g->fx_part.alloc(ctx, (size_t)std::max<int64_t>(nfa, 1) * (size_t)kern_n(g)));
         }
+    }
+    for (size_t c0 = 0; c0 < cuts.size(); c0 += TC_BATCH) {
+        CutBatch cb;
+        const size_t n = std::min<size_t>(TC_BATCH, cuts.size() - c0);
+        for (size_t j = 0; j < n; ++j) cb.a[j] = cuts[c0 + j];
+        hipLaunchKernelGGL(k_tr_cut_b, dim3((unsigned)n), dim3(TC_T), 0, st, cb);
+        MR_TRY_HIP(ctx, hipGetLastError());
     }
     // a sharded wide graph: the widest cold slice span over the ranks (one scale for every rank)
     uint64_t cold_span_all = 1;
