@@ -296,6 +296,7 @@ struct WinRun {
     mr_graph *gn = nullptr, *ga = nullptr;   // "normal" graph (detector's abnormal traces), "anomaly" graph
     hipEvent_t ev = nullptr;                 // batch: the window's graphs are ready on its stream
     std::vector<unsigned char> keep;         // batch: host descriptors of its graphs' batched prepare
+    std::vector<unsigned char> keep2;        // ... and of their batched set-up
     bool slot = false;                       // batch: its spectrum went to the device result slot
     ~WinRun() {
         delete gn;
@@ -412,10 +413,7 @@ static int win_detect_build_async(mr_ctx* ctx, const mr_spans* s, int64_t t0, in
         const char* e = getenv("MR_WIN_SETUP_SPLIT");
         return e ? (int64_t)atoll(e) : (int64_t)65536;
     }();
-    if ((int64_t)w.gn->T + w.ga->T >= split) {
-        MR_TRY(mr_pagerank_presetup(ctx, w.gn, 0, 0.85, precision, 0));
-        MR_TRY(mr_pagerank_presetup(ctx, w.ga, 1, 0.85, precision, 0));
-    }
+    if ((int64_t)w.gn->T + w.ga->T >= split) MR_TRY(mr_pagerank_presetup2(ctx, w.gn, w.ga, 0.85, precision, w.keep2));
     if (!w.ev) MR_TRY_HIP(ctx, hipEventCreateWithFlags(&w.ev, hipEventDisableTiming));
     MR_TRY_HIP(ctx, hipEventRecord(w.ev, st));
     return MR_OK;

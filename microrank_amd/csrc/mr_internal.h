@@ -358,3 +358,5 @@ int mr_ix_finish(mr_ctx* ctx, const mr_spans* sp, mr_graph* g, IxBuild& b, const
 int mr_ix_finish2(mr_ctx* ctx, const mr_spans* sp, mr_graph* g0, IxBuild& b0, const int64_t* h0, mr_graph* g1,
                   IxBuild& b1, const int64_t* h1, std::vector<unsigned char>& keep);
 int mr_pagerank_presetup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, int precision, uint32_t flags);
+int mr_pagerank_presetup2(mr_ctx* ctx, mr_graph* g0, mr_graph* g1, double d, int precision,
+                          std::vector<unsigned char>& keep);

@@ -3627,9 +3627,10 @@ static bool setup_batchable(const mr_graph* g, bool tr_plan, uint32_t flags) {
 // pagerank_setup of several graphs (all setup_batchable) in six launches
 // hs / dsd: the descriptors (host and device), owned by the caller until its stream work is done
 static int pagerank_setup_batch(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly, int ng, double d, bool fp32,
-                                uint64_t seed, uint64_t hmask, std::vector<SDev>& hs, DBuf<SDev>& dsd) {
+                                uint64_t seed, uint64_t hmask, std::vector<unsigned char>& keep, DBuf<SDev>& dsd) {
     hipStream_t st = ctx->stream;
-    hs.assign((size_t)ng, SDev{});
+    keep.assign((size_t)ng * sizeof(SDev), 0);
+    SDev* hs = reinterpret_cast<SDev*>(keep.data());
     int32_t br = 0, bk = 0, bv = 0, bp = 0;
     for (int i = 0; i < ng; ++i) {
         mr_graph* g = gs[i];
@@ -3659,7 +3660,7 @@ static int pagerank_setup_batch(mr_ctx* ctx, mr_graph* const* gs, const int* ano
             if (fp32) MR_TRY(g->q32[j].alloc(ctx, (size_t)T + 1));
             else MR_TRY(g->q64[j].alloc(ctx, (size_t)T + 1));
         }
-        SDev& v = hs[(size_t)i];
+        SDev& v = hs[i];
         v.T = T;
         v.N = N;
         v.anomaly = anomaly[i];
@@ -3700,7 +3701,7 @@ static int pagerank_setup_batch(mr_ctx* ctx, mr_graph* const* gs, const int* ano
         v.b_pref = bp;
         bp += nbp;
     }
-    MR_TRY(dsd.upload(ctx, hs.data(), hs.size()));
+    MR_TRY(dsd.upload(ctx, hs, (size_t)ng));
     hipLaunchKernelGGL(k_reset_init_b, dim3(br), dim3(256), 0, st, dsd.p, ng);
     hipLaunchKernelGGL(k_kind_insert_b, dim3(bk), dim3(KB), 0, st, dsd.p, ng, seed, hmask);
     hipLaunchKernelGGL(k_kind_verify_b, dim3(bv), dim3(256), 0, st, dsd.p, ng);
@@ -3812,7 +3813,7 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         if (gs[i]->fused) TT = std::min(TT, fx_tt(gs[i]->N));
     const FxPlan plan = fx_plan(gs, ng);
     if (plan.v2) TT = WAVE;   // wave tiles
-    std::vector<SDev> setup_h;   // (batched set-up descriptors: alive until the call's final sync)
+    std::vector<unsigned char> setup_h;   // (batched set-up descriptors: alive until the call's final sync)
     DBuf<SDev> setup_d;
     {   // set-up of every graph not set up ahead (mr_pagerank_presetup): batched when they allow it
         std::vector<mr_graph*> need;
@@ -4172,6 +4173,34 @@ static uint64_t kind_hmask(int a) { return (a == 0 && getenv("MR_KIND_TEST_COLLI
 // these arguments, on THIS context's stream (the one that built it): mr_windows_batch sets up a
 // window's graphs while the previous group's iterations run.  The next call on the graph skips
 // its own setup when the arguments match (first kind-hash seed; a collision retries in full).
+// mr_pagerank_presetup of a window's two graphs in six launches when both allow the batched set-up
+// (keep: its host descriptors, alive until the stream has used them)
+int mr_pagerank_presetup2(mr_ctx* ctx, mr_graph* g0, mr_graph* g1, double d, int precision,
+                          std::vector<unsigned char>& keep) {
+    const bool fp32 = precision == MR_FP32;
+    const bool tr = fx_kind() == FXK_TR;
+    if (!(g0->N && g0->T && g1->N && g1->T && setup_batchable(g0, tr, 0) && setup_batchable(g1, tr, 0)) ||
+        getenv("MR_NO_SETUP_BATCH") != nullptr) {
+        MR_TRY(mr_pagerank_presetup(ctx, g0, 0, d, precision, 0));
+        return mr_pagerank_presetup(ctx, g1, 1, d, precision, 0);
+    }
+    mr_graph* gs[2] = {g0, g1};
+    const int an[2] = {0, 1};
+    DBuf<SDev> dsd;   // (returns to this context's pool: reused only by later work on this stream)
+    MR_TRY(pagerank_setup_batch(ctx, gs, an, 2, d, fp32, kind_seed(0), kind_hmask(0), keep, dsd));
+    for (int i = 0; i < 2; ++i) {
+        mr_graph* g = gs[i];
+        g->pre_ok = true;
+        g->pre_anomaly = an[i];
+        g->pre_d = d;
+        g->pre_fp32 = fp32;
+        g->pre_flags = 0;
+        g->pre_seed = kind_seed(0);
+        g->pre_hmask = kind_hmask(0);
+    }
+    return MR_OK;
+}
+
 int mr_pagerank_presetup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, int precision, uint32_t flags) {
     const bool fp32 = precision == MR_FP32;
     if (g->N == 0 || g->T == 0) return MR_OK;   // (the call itself raises)
