@@ -409,10 +409,8 @@ static int win_detect_build_async(mr_ctx* ctx, const mr_spans* s, int64_t t0, in
     // (pagerank_setup_batch) -- the host's launches, not the GPU, bound them; large windows (C2:
     // 200k traces) set up here, where the work overlaps the previous group's iterations.
     // MR_WIN_SETUP_SPLIT: traces of a window from which it sets up here (default 65536)
-    static const int64_t split = [] {
-        const char* e = getenv("MR_WIN_SETUP_SPLIT");
-        return e ? (int64_t)atoll(e) : (int64_t)65536;
-    }();
+    const char* se = getenv("MR_WIN_SETUP_SPLIT");   // (read per call: tests flip it)
+    const int64_t split = se ? (int64_t)atoll(se) : (int64_t)65536;
     if ((int64_t)w.gn->T + w.ga->T >= split) MR_TRY(mr_pagerank_presetup2(ctx, w.gn, w.ga, 0.85, precision, w.keep2));
     if (!w.ev) MR_TRY_HIP(ctx, hipEventCreateWithFlags(&w.ev, hipEventDisableTiming));
     MR_TRY_HIP(ctx, hipEventRecord(w.ev, st));

@@ -1324,7 +1324,7 @@ static int ix_launch(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d_mask, mr_
     MR_TRY(b.ocov.alloc(ctx, NP));
     // dense edge ids (one table's keys, counted per id) unless joins across ranks bring keys the
     // table does not hold
-    static const bool no_dense = getenv("MR_EDGE_HASH") != nullptr;   // A/B knob: the hash set
+    const bool no_dense = getenv("MR_EDGE_HASH") != nullptr;   // A/B knob (read per call: tests flip it)
     b.dense = !sharded && !no_dense && sp->ekey.p != nullptr;
     b.ecap = b.dense ? (uint64_t)sp->n_edge_keys : edge_capacity(sp->n_edge_keys + X.matches, NP);
     const uint64_t ecap = b.ecap;
@@ -1444,7 +1444,7 @@ static int graph_build_indexed(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d
 // both graphs' LDS histograms, the one-block node order): the caller builds them one by one.
 int mr_ix_launch2(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d_state, mr_graph* g0, mr_graph* g1, IxBuild& b0,
                   IxBuild& b1, int64_t* d_out) {
-    static const bool off = getenv("MR_NO_IX2") != nullptr;   // A/B knob
+    const bool off = getenv("MR_NO_IX2") != nullptr;   // A/B knob (read per call: tests flip it)
     const int32_t NT = sp->n_traces, NP = sp->n_podops;
     const int64_t nek = sp->n_edge_keys;
     if (off || !sp->ekey.p || NP > NS_PMAX || 2 * (3 * (int64_t)NP + nek) > IX_LDS_WORDS) return MR_ERR_STATE;

@@ -3286,7 +3286,7 @@ static int wide_prepare(mr_ctx* ctx, mr_graph* g) {
 // all are small fused graphs whose su stays in LDS (no relabelling, one-block histogram scan),
 // else one prepare each.  keep: the descriptors' host copy, alive until the stream has used it.
 int mr_graph_prepare_batch(mr_ctx* ctx, mr_graph* const* gs, int n, std::vector<unsigned char>& keep) {
-    static const bool off = getenv("MR_NO_PREP_BATCH") != nullptr;   // A/B knob
+    const bool off = getenv("MR_NO_PREP_BATCH") != nullptr;   // A/B knob (read per call: tests flip it)
     bool ok = !off && n >= 2 && plan_is_tr() && getenv("MR_NO_FUSED") == nullptr;
     for (int i = 0; i < n && ok; ++i) {
         const mr_graph* g = gs[i];

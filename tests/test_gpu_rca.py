@@ -459,3 +459,46 @@ def test_windows_batch_matches_standalone(c3_window):
     assert got[4][5] == _lib.MR_ERR_VALUE
     for d in devs:
         d.close()
+
+
+def test_windows_batch_fast_paths_equal_general_paths(c3_window, monkeypatch):
+    """The window batch's fast paths -- both graphs built in one index pass (mr_ix_launch2) with
+    dense edge ids, prepared together (mr_graph_prepare_batch), set up in batched launches over
+    the group (pagerank_setup_batch) or over the window (mr_pagerank_presetup2) -- give the same
+    rankings as the one-graph-at-a-time paths (MR_NO_IX2 / MR_EDGE_HASH / MR_NO_PREP_BATCH /
+    MR_NO_SETUP_BATCH): top lists identical, scores within 1e-12, counts and edges equal."""
+    import bench
+    from microrank_amd import _lib
+    from microrank_amd.online_rca import rank_windows
+    from microrank_amd.preprocess_data import DeviceSpans
+
+    ctx = _lib.default_context()
+    normal, abnormal, t0, t1 = c3_window
+    a3, ok = bench.slo_from_gpu(ctx, normal)
+    devs = [DeviceSpans(ctx, abnormal)]
+    wins = [(devs[0], t0, t1, a3, ok)]
+    for seed in (91, 92, 93):
+        _, nrm, ab = bench.make_window(seed, 500, 20_000)
+        s3, sok = bench.slo_from_gpu(ctx, nrm)
+        d = DeviceSpans(ctx, ab)
+        devs.append(d)
+        u0 = int(ab.tstart.min())
+        wins.append((d, u0, u0 + 5 * 60 * 10**9, s3, sok))
+    runs = {}
+    for mode in ("fast", "split0", "general"):
+        for k in ("MR_NO_IX2", "MR_EDGE_HASH", "MR_NO_PREP_BATCH", "MR_NO_SETUP_BATCH", "MR_WIN_SETUP_SPLIT"):
+            monkeypatch.delenv(k, raising=False)
+        if mode == "split0":   # every window sets its graphs up on its own stream (presetup2)
+            monkeypatch.setenv("MR_WIN_SETUP_SPLIT", "0")
+        if mode == "general":
+            for k in ("MR_NO_IX2", "MR_EDGE_HASH", "MR_NO_PREP_BATCH", "MR_NO_SETUP_BATCH"):
+                monkeypatch.setenv(k, "1")
+        runs[mode] = rank_windows(ctx, wins)
+    for mode in ("split0", "general"):
+        for a, b in zip(runs["fast"], runs[mode]):
+            assert a[5] == b[5] == 0
+            assert (a[2], a[3], a[4]) == (b[2], b[3], b[4]), mode
+            assert list(a[0]) == list(b[0]), mode
+            np.testing.assert_allclose(a[1], b[1], rtol=1e-12, atol=0)
+    for d in devs:
+        d.close()
