@@ -797,7 +797,7 @@ def main():
         out["kind_compressed"] = kind_compressed_probe(ctx, dev0, t0, t1, a3, ok)
     except Exception as e:  # a side metric never sinks the line
         out["kind_compressed"] = {"error": f"{type(e).__name__}: {e}"}
-    if not args.no_cpu:
+    if not args.no_cpu and world == 1:   # the CPU baseline: rank 0 at N = 1 only
         try:
             cb, cres = cpu_baseline(abnormal, t0, t1, a3, ok)
             out["cpu_baseline"] = cb
