@@ -511,10 +511,26 @@ extern "C" int mr_rca_window(mr_ctx* ctx, const mr_spans* s, int64_t t0, int64_t
 // time (all of the group's graphs share each iteration's k_tr_a + k_fx_b launches) while the
 // auxiliary streams already build the next group's graphs.
 static int win_aux(mr_ctx* ctx, int n) {
+    // MR_WIN_AUX_PRIO=low|high|same: the auxiliary streams' priority against the PageRank stream's
+    static const int prio = [] {
+        const char* e = getenv("MR_WIN_AUX_PRIO");
+        if (e && !strcmp(e, "low")) return 1;
+        if (e && !strcmp(e, "high")) return 2;
+        return 0;
+    }();
     while ((int)ctx->aux.size() < n) {
         mr_ctx* a = nullptr;
         const int rc = mr_ctx_create(ctx->device, ctx->flags, &a);
         if (rc != MR_OK) return mr_fail(ctx, rc, "mr_windows_batch: auxiliary context creation failed");
+        if (prio) {   // (lower number = higher priority)
+            int lo = 0, hi = 0;
+            hipStream_t s2 = nullptr;
+            if (hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess &&
+                hipStreamCreateWithPriority(&s2, hipStreamNonBlocking, prio == 1 ? lo : hi) == hipSuccess) {
+                (void)hipStreamDestroy(a->stream);
+                a->stream = s2;
+            }
+        }
         ctx->aux.push_back(a);
     }
     return MR_OK;
