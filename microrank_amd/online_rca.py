@@ -139,6 +139,7 @@ def sweep_chain(plan):
         ranked = na > 0 and nn > 0
         events.append(("window", m, na, nn, ranked))
         m += plan["step_n"] + (plan["step_a"] if ranked else 0)
+    plan["next_m"] = m   # where the chain goes on (RCAStream)
     return events
 
 
@@ -172,7 +173,10 @@ def _sweep_run(plan):
     in window order; an empty window raises the reference's TypeError (T2) after the output of
     the windows before it."""
     events = sweep_chain(plan)
-    results = sweep_rank(plan, events)
+    _sweep_emit(plan, events, sweep_rank(plan, events))
+
+
+def _sweep_emit(plan, events, results):
     names = plan["table"].podop_names
     for e in events:
         if e[0] == "empty":
@@ -215,7 +219,14 @@ def online_anomaly_detect_RCA(data, slo, operation_list, *, ctx=None):
     plan = _sweep_plan(data, slo, start, end, window_normal, window_abnormal, ctx)
     if plan is not None:
         return _sweep_run(plan)
-    current_time = start
+    _window_loop(data, slo, operation_list, start, end)
+
+
+def _window_loop(data, slo, operation_list, current_time, end):
+    """online_rca.py:164-216 window by window from current_time while it is before end; returns
+    where the chain goes on."""
+    window_normal = pd.Timedelta(minutes=5)
+    window_abnormal = pd.Timedelta(minutes=4)
     while current_time < end:
         start_time = current_time
         end_time = current_time + window_normal
@@ -240,6 +251,81 @@ def online_anomaly_detect_RCA(data, slo, operation_list, *, ctx=None):
             _write_result(top_list, score_list)
             current_time += window_abnormal
         current_time += window_normal
+    return current_time
+
+
+class RCAStream:
+    """SURVEY 8(f) f3, online: online_anomaly_detect_RCA (online_rca.py:161-216) over spans that
+    arrive in chunks.  Each chunk holds whole traces and chunks come in trace-start order (the
+    OTel export's TraceStart order); push() ranks every window of the driver's chain that the data
+    seen so far completes (a window [t, t + 5 min] is complete once a trace starting after t + 5 min
+    has arrived), close() the rest up to the last endTime, as the offline driver would.  The
+    output -- prints, result.csv, the T2 TypeError -- equals the offline driver's on the
+    concatenated chunks.  Spans of traces that start before the chain's next window are dropped,
+    so the resident table stays a few windows long; each push re-ingests that table on the device
+    (mr_spans_ingest) and runs the chain's new windows as one sweep + one batched ranking."""
+
+    WINDOW = pd.Timedelta(minutes=5)
+    STEP_ABNORMAL = pd.Timedelta(minutes=4)
+
+    def __init__(self, slo, operation_list, *, ctx=None):
+        self.slo, self.operation_list = slo, operation_list
+        self.ctx = ctx or _lib.default_context()
+        self.data = None          # retained spans (traces that can still be in a window)
+        self.cur = None           # the chain's next window start (pd.Timestamp)
+        self.watermark = None     # largest trace start seen
+        self.end = None           # largest trace end seen (the offline driver's loop bound)
+        self.dead = False         # an empty window ended the driver (T2)
+
+    def push(self, chunk: pd.DataFrame):
+        if self.dead:
+            raise RuntimeError("RCAStream: the driver ended at an empty window")
+        if len(chunk) == 0:
+            return
+        lo, hi, e = chunk["startTime"].min(), chunk["startTime"].max(), chunk["endTime"].max()
+        if self.cur is None:
+            self.cur = lo
+        elif self.watermark is not None and lo < self.watermark:
+            raise ValueError("RCAStream.push: chunks must arrive in trace-start order")
+        self.watermark = hi if self.watermark is None else max(self.watermark, hi)
+        self.end = e if self.end is None else max(self.end, e)
+        self.data = chunk if self.data is None else pd.concat([self.data, chunk], ignore_index=True)
+        # complete windows: start + 5 min < watermark
+        self._advance(self.watermark - self.WINDOW, final=False)
+
+    def close(self):
+        if self.dead or self.data is None:
+            return
+        self._advance(self.end, final=True)
+
+    def _advance(self, limit, final):
+        if not self.cur < limit:
+            return
+        try:
+            plan = _sweep_plan(self.data, self.slo, self.cur, limit, self.WINDOW, self.STEP_ABNORMAL, self.ctx)
+            if plan is None:   # window times vary within a trace: window by window
+                if final:
+                    self.cur = _window_loop(self.data, self.slo, self.operation_list, self.cur, limit)
+                else:
+                    self.cur = self._loop_complete(limit)
+            else:
+                events = sweep_chain(plan)
+                _sweep_emit(plan, events, sweep_rank(plan, events))
+                self.cur = self.cur + pd.Timedelta(plan["next_m"] * plan["grain"], unit="ns")
+        except TypeError:
+            self.dead = True
+            raise
+        keep = self.data["startTime"] >= self.cur   # traces before the next window leave the table
+        if not keep.all():
+            self.data = self.data[keep].reset_index(drop=True)
+
+    def _loop_complete(self, limit):
+        """The window loop for per-span times, one window at a time while its start is before limit."""
+        cur = self.cur
+        while cur < limit:
+            nxt = _window_loop(self.data, self.slo, self.operation_list, cur, cur + pd.Timedelta(1, unit="ns"))
+            cur = nxt
+        return cur
 
 
 def rca_window(data, start_time, end_time, slo, *, top_max=5, spectrum_method="dstar2", precision="fp64", ctx=None,

@@ -502,3 +502,45 @@ def test_windows_batch_fast_paths_equal_general_paths(c3_window, monkeypatch):
             np.testing.assert_allclose(a[1], b[1], rtol=1e-12, atol=0)
     for d in devs:
         d.close()
+
+
+@pytest.mark.parametrize("name,minutes", [("stream", 7), ("stream", 3), ("stream_gap", 7)])
+def test_rca_stream_matches_offline_driver(name, minutes, tmp_path, monkeypatch):
+    """f3 online (RCAStream): the reference-captured 60-minute streams pushed in trace-aligned
+    chunks of a few minutes print what the reference's offline driver printed over the whole frame
+    (and write its result.csv, and raise its empty-window TypeError)."""
+    from microrank_amd import synth
+    from microrank_amd.online_rca import RCAStream
+
+    case = load_golden(f"{name}.json")
+    _, adf = synth.stream_dataframes(**case["params"])
+    slo = {k: [np.float64(float.fromhex(a)), np.float64(float.fromhex(b))] for k, (a, b) in case["slo"].items()}
+    monkeypatch.chdir(tmp_path)
+    t0 = adf["startTime"].min()
+    bucket = ((adf["startTime"] - t0) // pd.Timedelta(minutes=minutes)).to_numpy()
+    assert (np.diff(bucket) >= 0).all()   # rows in trace-start order: chunks keep the frame's order
+    buf = io.StringIO()
+    err = None
+    try:
+        with contextlib.redirect_stdout(buf):
+            s = RCAStream(slo, case["operation_list"])
+            for b in np.unique(bucket):
+                s.push(adf[bucket == b].copy())
+            s.close()
+    except TypeError as e:
+        err = type(e).__name__
+    assert err == case["driver_error"]
+    got, exp = buf.getvalue().splitlines(), case["driver_stdout"].splitlines()
+    assert len(got) == len(exp)
+    for g, x in zip(got, exp):
+        if g.startswith("[") and x.startswith("["):
+            gl, xl = g.split("] [", 1), x.split("] [", 1)
+            assert gl[0] == xl[0]
+            gs = [float(v.split("(")[-1].rstrip(")]")) for v in gl[1].split(", ")]
+            xs = [float(v.split("(")[-1].rstrip(")]")) for v in xl[1].split(", ")]
+            np.testing.assert_allclose(gs, xs, rtol=1e-10)
+        else:
+            assert g == x
+    if case["result_csv"] is not None:
+        got_csv = open("result.csv").read().splitlines()
+        assert [r.split(",")[:-1] for r in got_csv] == [r.split(",")[:-1] for r in case["result_csv"].splitlines()]
