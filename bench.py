@@ -497,6 +497,40 @@ def run_ingest(args):
     dt_host = time.perf_counter() - ts
     same = bool(np.array_equal(t.trace, host.trace) and np.array_equal(t.podop, host.podop) and
                 np.array_equal(t.svcop, host.svcop) and list(t.podop_names) == list(host.podop_names))
+    # end to end from the OTel CSV export: pyarrow reader + device ingest vs pandas read_csv +
+    # rename + to_datetime + the factorisation (online_rca.py:221-248 and SpanTable.from_dataframe)
+    import tempfile
+
+    import pandas as pd
+
+    from microrank_amd.spans import OTEL_RENAME, read_traces_csv
+
+    csv_line = None
+    with tempfile.TemporaryDirectory(dir="/tmp") as td:
+        path = os.path.join(td, "traces.csv")
+        df.rename(columns={v: k for k, v in OTEL_RENAME.items()}).to_csv(path, index=False)
+        ts = time.perf_counter()
+        dfa = read_traces_csv(path)
+        t_read = time.perf_counter() - ts
+        ts = time.perf_counter()
+        ta, da = DeviceSpans.ingest(ctx, dfa, arrow_columns(dfa))
+        ctx.sync()
+        t_ing = time.perf_counter() - ts
+        da.close()
+        ts = time.perf_counter()
+        dfp = pd.read_csv(path).rename(columns=OTEL_RENAME)
+        dfp["startTime"] = pd.to_datetime(dfp["startTime"])
+        dfp["endTime"] = pd.to_datetime(dfp["endTime"])
+        t_pread = time.perf_counter() - ts
+        ts = time.perf_counter()
+        SpanTable.from_dataframe(dfp)
+        t_pfact = time.perf_counter() - ts
+        csv_line = {"what": "OTel CSV -> device span table: read_traces_csv (pyarrow) + mr_spans_ingest, "
+                            "vs pandas read_csv + rename + to_datetime + factorisation",
+                    "csv_MB": round(os.path.getsize(path) / 1e6, 1), "read_ms": round(t_read * 1e3, 1),
+                    "ingest_ms": round(t_ing * 1e3, 1), "total_ms": round((t_read + t_ing) * 1e3, 1),
+                    "pandas_read_ms": round(t_pread * 1e3, 1), "pandas_factorize_ms": round(t_pfact * 1e3, 1),
+                    "speedup": round((t_pread + t_pfact) / (t_read + t_ing), 1)}
     str_bytes = sum(int(a.buffers()[2].size) if a.buffers()[2] is not None else 0 for a in arrays.values())
     in_bytes = str_bytes + 6 * 8 * (S + 1) + 3 * 8 * S
     d.close()
@@ -507,7 +541,7 @@ def run_ingest(args):
             "config": {"workload": f"C2 window DataFrame: {S} spans, {abnormal.n_traces} traces, {len(host.podop_names)} "
                                    f"pod-ops; input {in_bytes / 1e6:.1f} MB of Arrow buffers in host memory",
                        "pcie_inclusive": True},
-            "arrow_ms": round(t_arrow * 1e3, 3), "codes_equal_host": same,
+            "arrow_ms": round(t_arrow * 1e3, 3), "codes_equal_host": same, "csv": csv_line,
             "input_GBps": round(in_bytes / dt / 1e9, 2),
             "cpu_baseline": {"value": round(S / dt_host / 1e6, 3), "unit": "Mspans/s", "cores": 1, "kind": "port",
                              "sample": "SpanTable.from_dataframe (pandas factorize of the same DataFrame), once",

@@ -130,6 +130,32 @@ class SpanTable:
                    df["duration"].to_numpy(dtype=np.int64), tstart, tend, tnames, pnames, snames)
 
 
+# ------------------------------------------------------------------ the OTel CSV export (f2)
+# collect_data.py:35-46 exports TraceId, SpanId, ParentSpanId, SpanName, ServiceName, PodName,
+# Duration, TraceStart, TraceEnd (plus Timestamp, SpanKind); online_rca.py:221-232 renames them
+OTEL_RENAME = {"TraceId": "traceID", "ServiceName": "serviceName", "SpanName": "operationName", "PodName": "podName",
+               "SpanId": "spanID", "Duration": "duration", "TraceStart": "startTime", "TraceEnd": "endTime"}
+
+
+def read_traces_csv(path):
+    """``pd.read_csv(path).rename(columns=...)`` + ``pd.to_datetime`` of online_rca.py:221-248
+    through pyarrow's multithreaded CSV reader: the string columns stay Arrow-backed
+    (``string[pyarrow]``), so the device ingest (mr_spans_ingest) takes their buffers without a
+    Python-object round trip.  Empty fields read as missing, as pandas reads them."""
+    import pandas as pd
+    import pyarrow as pa
+    import pyarrow.csv as pv
+
+    t = pv.read_csv(path, convert_options=pv.ConvertOptions(strings_can_be_null=True))
+    t = t.rename_columns([OTEL_RENAME.get(c, c) for c in t.column_names])
+    df = t.to_pandas(types_mapper=lambda ty: pd.ArrowDtype(ty) if pa.types.is_string(ty) or pa.types.is_large_string(ty)
+                     else None)
+    for c in ("startTime", "endTime"):
+        if c in df and not np.issubdtype(df[c].dtype, np.datetime64):
+            df[c] = pd.to_datetime(df[c])
+    return df
+
+
 # ------------------------------------------------------------------ device ingest (SURVEY 8(f) f2)
 _STR_COLS = ("traceID", "spanID", "ParentSpanId", "serviceName", "operationName", "podName")
 

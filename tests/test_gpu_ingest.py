@@ -146,3 +146,34 @@ def test_driver_same_on_host_factorisation(name, tmp_path, monkeypatch):
 def test_edges_parquet_ingest():
     df = pd.read_parquet(os.path.join(GOLDEN, "edges_spans.parquet"))
     _check(df)
+
+
+@pytest.mark.parametrize("name", ["c1", "pods_dup_broken"])
+def test_driver_from_otel_csv(name, tmp_path, monkeypatch):
+    """f2 end to end: the window written as the OTel export (collect_data.py:35-46), read back with
+    read_traces_csv (Arrow-backed strings), ingested on the device and run through the drop-in
+    driver: the reference's stdout, rank lines included."""
+    from microrank_amd import online_rca
+    from microrank_amd.spans import OTEL_RENAME, read_traces_csv
+
+    case = load_golden(f"{name}.json")
+    _, adf = regen_window(case)
+    inv = {v: k for k, v in OTEL_RENAME.items()}
+    p = tmp_path / "traces.csv"
+    adf.rename(columns=inv).to_csv(p, index=False)
+    df = read_traces_csv(p)
+    slo = {k: [np.float64(float.fromhex(a)), np.float64(float.fromhex(b))] for k, (a, b) in case["slo"].items()}
+    monkeypatch.chdir(tmp_path)
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        online_rca.online_anomaly_detect_RCA(df, slo, case["operation_list"])
+    got, exp = buf.getvalue().splitlines(), case["driver_stdout"].splitlines()
+    assert len(got) == len(exp)
+    for g, x in zip(got, exp):
+        if g.startswith("[") and x.startswith("["):
+            gs = [float(v.split("(")[-1].rstrip(")]")) for v in g.split("] [", 1)[1].split(", ")]
+            xs = [float(v.split("(")[-1].rstrip(")]")) for v in x.split("] [", 1)[1].split(", ")]
+            assert g.split("] [", 1)[0] == x.split("] [", 1)[0]
+            np.testing.assert_allclose(gs, xs, rtol=1e-10)
+        else:
+            assert g == x

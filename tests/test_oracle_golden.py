@@ -243,3 +243,32 @@ def test_driver_sweep_matches_reference(name):
            if ln.startswith(("anormaly_trace", "total_trace", "anomaly_list", "normal_list", "Error"))]
     assert lines == exp
     assert empty == (case["driver_error"] == "TypeError")
+
+
+def test_read_traces_csv_equals_pandas(tmp_path):
+    """f2: the OTel export (collect_data.py:35-46) read through pyarrow (Arrow-backed strings) holds
+    what pandas' read_csv + rename + to_datetime (online_rca.py:221-248) holds, and factorises
+    to the same codes."""
+    import pandas as pd
+
+    from microrank_amd import synth
+    from microrank_amd.spans import OTEL_RENAME, SpanTable, read_traces_csv
+
+    case = load_golden("pods_dup_broken.json")
+    _, adf = regen_window(case)
+    inv = {v: k for k, v in OTEL_RENAME.items()}
+    p = tmp_path / "traces.csv"
+    adf.rename(columns=inv).to_csv(p, index=False)
+    ref = pd.read_csv(p).rename(columns=OTEL_RENAME)
+    ref["startTime"] = pd.to_datetime(ref["startTime"])
+    ref["endTime"] = pd.to_datetime(ref["endTime"])
+    got = read_traces_csv(p)
+    assert list(got.columns) == list(ref.columns)
+    for c in ref.columns:
+        a, b = got[c].to_numpy(dtype=object), ref[c].to_numpy(dtype=object)
+        same = [(pd.isna(x) and pd.isna(y)) if (pd.isna(x) or pd.isna(y)) else x == y for x, y in zip(a, b)]
+        assert all(same), c
+    h1, h2 = SpanTable.from_dataframe(ref), SpanTable.from_dataframe(got)
+    for c in ("trace", "podop", "svcop", "span", "parent", "duration", "tstart", "tend"):
+        assert np.array_equal(getattr(h1, c), getattr(h2, c)), c
+    assert synth.frame_digest(adf) == case["input_digest"]["abnormal"]
