@@ -307,3 +307,63 @@ def test_kind_compressed_c2_matches_uncompressed(c2, anomaly, part_min, monkeypa
     np.testing.assert_allclose(w1, w0, rtol=1e-10, atol=0)
     assert (1.0 / k0).sum() < 0.6 * g.T   # the C2 window repeats call paths (113k kinds of 200k traces)
     dg.close()
+
+
+def test_c4_full_scale_properties():
+    """BASELINE configs[3] at full size (10k ops / 10M traces, fp64, one GPU): no oracle finishes
+    at this size, so size-independent properties -- bitwise reruns, coverage summing to the pairs,
+    the kind classes partitioning the traces, the weights' max-normalisation identity
+    (pagerank.py:107: N * sum(w) = (N * max(w))^2 when max(s) = 1), and the kind-compressed
+    ranking equal to the uncompressed one (1e-10, top-5 identical)."""
+    from microrank_amd import _lib, synth
+    from microrank_amd.graph import DeviceGraph
+
+    hg = synth.big_graph(10_000, 10_000_000, seed=11)
+    nnz = int(hg.sr_ops.size)
+    ctx = _lib.default_context()
+    dg = DeviceGraph.upload(ctx, hg)
+    del hg
+    dg.pagerank(True)
+    w1, cov, kind, _ = dg.fetch(kinds=True)
+    dg.pagerank(True)
+    w2, _ = dg.fetch()
+    assert w1.tobytes() == w2.tobytes()
+    assert int(cov.astype(np.int64).sum()) == nnz
+    n_kinds = float((1.0 / kind).sum())
+    assert abs(n_kinds - round(n_kinds)) < 1e-6 * n_kinds and 1 <= round(n_kinds) <= 10_000_000
+    N = w1.size
+    np.testing.assert_allclose(N * w1.sum(), (N * w1.max()) ** 2, rtol=1e-9)
+    dg.pagerank(True, compress_kinds=True)
+    w3, _ = dg.fetch()
+    np.testing.assert_allclose(w3, w1, rtol=1e-10, atol=0)
+    assert list(np.argsort(-w3, kind="stable")[:5]) == list(np.argsort(-w1, kind="stable")[:5])
+    dg.close()
+
+
+def test_c5_op_space_properties():
+    """BASELINE configs[4]'s op space (100k ops: the wide fused iteration, hot ops through k_tr_a,
+    the cold tail through k_cold_trace / k_cold_ops) over 10M traces: bitwise fp32 reruns,
+    coverage summing to the pairs, fp32 within 1e-4 of fp64 (the north star's fp32 tolerance) with
+    the same top-5, and fp64 satisfying the max-normalisation identity."""
+    from microrank_amd import _lib, synth
+    from microrank_amd.graph import DeviceGraph
+
+    hg = synth.big_graph(100_000, 10_000_000, seed=12)
+    nnz = int(hg.sr_ops.size)
+    ctx = _lib.default_context()
+    dg = DeviceGraph.upload(ctx, hg)
+    del hg
+    dg.pagerank(True, precision="fp32")
+    w32, cov = dg.fetch()
+    dg.pagerank(True, precision="fp32")
+    w32b, _ = dg.fetch()
+    assert w32.tobytes() == w32b.tobytes()
+    assert int(cov.astype(np.int64).sum()) == nnz
+    dg.pagerank(True, precision="fp64")
+    w64, _ = dg.fetch()
+    N = w64.size
+    np.testing.assert_allclose(N * w64.sum(), (N * w64.max()) ** 2, rtol=1e-9)
+    big = w64 > 1e-6 * w64.max()
+    np.testing.assert_allclose(w32[big], w64[big], rtol=1e-4)
+    assert list(np.argsort(-w32, kind="stable")[:5]) == list(np.argsort(-w64, kind="stable")[:5])
+    dg.close()
