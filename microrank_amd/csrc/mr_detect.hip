@@ -294,14 +294,10 @@ struct WinRun {
     int32_t na = 0, nn = 0;
     int64_t nin = 0;
     mr_graph *gn = nullptr, *ga = nullptr;   // "normal" graph (detector's abnormal traces), "anomaly" graph
-    hipEvent_t ev = nullptr;                 // batch: the window's graphs are ready on its stream
-    std::vector<unsigned char> keep;         // batch: host descriptors of its graphs' batched prepare
-    std::vector<unsigned char> keep2;        // ... and of their batched set-up
     bool slot = false;                       // batch: its spectrum went to the device result slot
     ~WinRun() {
         delete gn;
         delete ga;
-        if (ev) (void)hipEventDestroy(ev);
     }
 };
 
@@ -356,64 +352,104 @@ static int win_detect_build(mr_ctx* ctx, const mr_spans* s, int64_t t0, int64_t 
     return MR_OK;
 }
 
-// Batch form of win_detect_build for indexed spans with trace-level times: the detector, both
-// masks and both graph builds are enqueued first and their counters / sizes come back in ONE host
-// round trip; the graphs' prepare and PageRank set-up follow, and an event (w.ev) marks them
-// ready on this stream -- the caller's PageRank waits on it instead of on the host.
-static int win_detect_build_async(mr_ctx* ctx, const mr_spans* s, int64_t t0, int64_t t1, const double* d_a3,
-                                  const uint8_t* d_a3v, WinRun& w, int precision) {
-    hipStream_t st = ctx->stream;
-    const int32_t NT = s->n_traces;
-    constexpr size_t CW = 3 * MR_DETECT_SHARDS;   // detector counter shards, then 8 + 8 size words
-    DBuf<int64_t> wb;
-    DBuf<uint8_t> dst, m_abn, m_nor;
-    MR_TRY(wb.zero(ctx, CW + 16));
-    MR_TRY(dst.alloc(ctx, std::max(NT, 1)));
-    MR_TRY(m_abn.alloc(ctx, std::max(NT, 1)));
-    MR_TRY(m_nor.alloc(ctx, std::max(NT, 1)));
-    MR_TRY(mr_detect_indexed_launch(ctx, s, t0, t1, d_a3, d_a3v, dst.p, (unsigned long long*)wb.p));
-    w.gn = new mr_graph();
-    w.gn->ctx = ctx;
-    w.ga = new mr_graph();
-    w.ga->ctx = ctx;
-    IxBuild bn, ba;
-    // (the graphs take EVERY row of the selected traces: get_pagerank_graph(list, data),
-    // online_rca.py:180,185 / preprocess_data.py:148).  Both from the states in one pass over the
-    // index when the table allows it, else one build per mask.
-    const int rc2 = mr_ix_launch2(ctx, s, dst.p, w.gn, w.ga, bn, ba, wb.p + CW);
-    if (rc2 == MR_ERR_STATE) {
-        if (NT) hipLaunchKernelGGL(k_masks, dim3(cdiv(NT, 256)), dim3(256), 0, st, dst.p, NT, m_abn.p, m_nor.p);
-        MR_TRY(mr_ix_launch(ctx, s, m_abn.p, w.gn, bn, wb.p + CW));       // "normal" graph = detector's abnormal traces
-        MR_TRY(mr_ix_launch(ctx, s, m_nor.p, w.ga, ba, wb.p + CW + 8));
-    } else {
-        MR_TRY(rc2);
+// Batch form of win_detect_build for a CHUNK of windows over indexed spans with trace-level times,
+// all on this context's stream: every window's detector and both graph builds are enqueued first,
+// their counters / sizes come back in ONE host round trip, and the chunk's graphs are prepared
+// (and, when large, set up for PageRank) together -- five + six launches for all of them
+// (mr_graph_prepare_batch, mr_pagerank_presetup_n).  A window costs its own seven build
+// launches, the chunk one read-back; `ev` marks the chunk's graphs ready on this stream, and the
+// caller's PageRank waits on it instead of on the host.  Per-window outcome in w->rc (MR_ERR_VALUE:
+// empty window); a non-OK return fails the whole chunk.
+struct WinIn {
+    const mr_spans* s;
+    int64_t t0, t1;
+    const double* a3;      // (device)
+    const uint8_t* a3v;    // (device)
+    WinRun* w;
+};
+struct WinChunk {
+    hipEvent_t ev = nullptr;
+    std::vector<unsigned char> keep, keep2;   // host descriptors of the batched prepare / set-up
+    ~WinChunk() {
+        if (ev) (void)hipEventDestroy(ev);
     }
-    int64_t h[CW + 16];
+};
+static int win_chunk_build_async(mr_ctx* ctx, const WinIn* in, int n, int precision, WinChunk& c) {
+    hipStream_t st = ctx->stream;
+    constexpr size_t CW = 3 * MR_DETECT_SHARDS;   // per window: detector counter shards, then 8 + 8 size words
+    constexpr size_t WW = CW + 16;
+    DBuf<int64_t> wb;
+    MR_TRY(wb.zero(ctx, (size_t)n * WW));
+    std::vector<DBuf<uint8_t>> dst((size_t)n);   // (DBufs return to the pool stream-ordered: the
+    std::vector<IxBuild> bx(2 * (size_t)n);      //  kernels enqueued on them run first)
+    for (int k = 0; k < n; ++k) {
+        const mr_spans* s = in[k].s;
+        WinRun& w = *in[k].w;
+        const int32_t NT = s->n_traces;
+        int64_t* wk = wb.p + (size_t)k * WW;
+        MR_TRY(dst[(size_t)k].alloc(ctx, std::max(NT, 1)));
+        MR_TRY(mr_detect_indexed_launch(ctx, s, in[k].t0, in[k].t1, in[k].a3, in[k].a3v, dst[(size_t)k].p,
+                                        (unsigned long long*)wk));
+        w.gn = new mr_graph();
+        w.gn->ctx = ctx;
+        w.ga = new mr_graph();
+        w.ga->ctx = ctx;
+        IxBuild &bn = bx[2 * (size_t)k], &ba = bx[2 * (size_t)k + 1];
+        // (the graphs take EVERY row of the selected traces: get_pagerank_graph(list, data),
+        // online_rca.py:180,185 / preprocess_data.py:148).  Both from the states in one pass over
+        // the index when the table allows it, else one build per mask.
+        const int rc2 = mr_ix_launch2(ctx, s, dst[(size_t)k].p, w.gn, w.ga, bn, ba, wk + CW);
+        if (rc2 == MR_ERR_STATE) {
+            DBuf<uint8_t> m_abn, m_nor;
+            MR_TRY(m_abn.alloc(ctx, std::max(NT, 1)));
+            MR_TRY(m_nor.alloc(ctx, std::max(NT, 1)));
+            if (NT) hipLaunchKernelGGL(k_masks, dim3(cdiv(NT, 256)), dim3(256), 0, st, dst[(size_t)k].p, NT, m_abn.p, m_nor.p);
+            MR_TRY(mr_ix_launch(ctx, s, m_abn.p, w.gn, bn, wk + CW));   // "normal" graph = detector's abnormal traces
+            MR_TRY(mr_ix_launch(ctx, s, m_nor.p, w.ga, ba, wk + CW + 8));
+        } else {
+            MR_TRY(rc2);
+        }
+    }
+    std::vector<int64_t> h((size_t)n * WW);
     {
         unsigned char* hp = nullptr;
-        MR_TRY(mr_read_bytes(ctx, wb.p, (CW + 16) * sizeof(int64_t), &hp));
-        memcpy(h, hp, sizeof h);
+        MR_TRY(mr_read_bytes(ctx, wb.p, h.size() * sizeof(int64_t), &hp));
+        memcpy(h.data(), hp, h.size() * sizeof(int64_t));
     }
-    mr_detect_sum((const unsigned long long*)h, &w.na, &w.nn, &w.nin);
-    if (w.nin == 0 || w.na == 0 || w.nn == 0) {   // empty window, or a list empty: nothing is ranked (T1)
-        delete w.gn;
-        delete w.ga;
-        w.gn = w.ga = nullptr;
-        if (w.nin == 0) return mr_fail(ctx, MR_ERR_VALUE, "Current span list is empty");
-        return MR_OK;
-    }
-    MR_TRY(mr_ix_finish2(ctx, s, w.gn, bn, bn.small ? h + CW : nullptr, w.ga, ba, ba.small ? h + CW + 8 : nullptr,
-                         w.keep));
-    // the graphs' kinds / preference / iteration state: small windows (C3: 20k traces) leave it to
-    // the PageRank stream, which sets up the whole group's graphs in six launches
-    // (pagerank_setup_batch) -- the host's launches, not the GPU, bound them; large windows (C2:
-    // 200k traces) set up here, where the work overlaps the previous group's iterations.
-    // MR_WIN_SETUP_SPLIT: traces of a window from which it sets up here (default 65536)
+    // MR_WIN_SETUP_SPLIT: traces of a window from which it sets up here (default 65536): small
+    // windows (C3: 20k traces) leave it to the PageRank stream, which sets up the whole group's
+    // graphs at once; large ones (C2: 200k traces) set up here, overlapping other work
     const char* se = getenv("MR_WIN_SETUP_SPLIT");   // (read per call: tests flip it)
     const int64_t split = se ? (int64_t)atoll(se) : (int64_t)65536;
-    if ((int64_t)w.gn->T + w.ga->T >= split) MR_TRY(mr_pagerank_presetup2(ctx, w.gn, w.ga, 0.85, precision, w.keep2));
-    if (!w.ev) MR_TRY_HIP(ctx, hipEventCreateWithFlags(&w.ev, hipEventDisableTiming));
-    MR_TRY_HIP(ctx, hipEventRecord(w.ev, st));
+    std::vector<mr_graph*> gs, pre;
+    std::vector<int> pre_an;
+    for (int k = 0; k < n; ++k) {
+        WinRun& w = *in[k].w;
+        const int64_t* hk = h.data() + (size_t)k * WW;
+        mr_detect_sum((const unsigned long long*)hk, &w.na, &w.nn, &w.nin);
+        if (w.nin == 0 || w.na == 0 || w.nn == 0) {   // empty window, or a list empty: nothing is ranked (T1)
+            delete w.gn;
+            delete w.ga;
+            w.gn = w.ga = nullptr;
+            if (w.nin == 0) w.rc = MR_ERR_VALUE;   // "Current span list is empty"
+            continue;
+        }
+        IxBuild &bn = bx[2 * (size_t)k], &ba = bx[2 * (size_t)k + 1];
+        MR_TRY(mr_ix_finish_unprepared(ctx, in[k].s, w.gn, bn, bn.small ? hk + CW : nullptr));
+        MR_TRY(mr_ix_finish_unprepared(ctx, in[k].s, w.ga, ba, ba.small ? hk + CW + 8 : nullptr));
+        gs.push_back(w.gn);
+        gs.push_back(w.ga);
+        if ((int64_t)w.gn->T + w.ga->T >= split) {
+            pre.push_back(w.gn);
+            pre.push_back(w.ga);
+            pre_an.push_back(0);
+            pre_an.push_back(1);
+        }
+    }
+    if (!gs.empty()) MR_TRY(mr_graph_prepare_batch(ctx, gs.data(), (int)gs.size(), c.keep));
+    if (!pre.empty()) MR_TRY(mr_pagerank_presetup_n(ctx, pre.data(), pre_an.data(), (int)pre.size(), 0.85, precision, c.keep2));
+    if (!c.ev) MR_TRY_HIP(ctx, hipEventCreateWithFlags(&c.ev, hipEventDisableTiming));
+    MR_TRY_HIP(ctx, hipEventRecord(c.ev, st));
     return MR_OK;
 }
 
@@ -559,9 +595,16 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
         const char* e = getenv("MR_WIN_GROUP");
         return e ? std::max(1, atoi(e)) : 16;
     }();
-    const int nthr = std::min<int>(n_windows, max_streams);
+    const char* ce = getenv("MR_WIN_CHUNK");   // windows built together on one stream (read per call)
+    const int chunk_size = ce ? std::max(1, atoi(ce)) : 4;
     const int gsz = std::min<int>(n_windows, group_size);
     const int ngroups = (n_windows + gsz - 1) / gsz;
+    // build chunks: consecutive windows of one group
+    std::vector<std::pair<int32_t, int32_t>> chunks;
+    for (int g = 0; g < ngroups; ++g)
+        for (int32_t i = g * gsz, e = std::min<int32_t>(n_windows, (g + 1) * gsz); i < e; i += chunk_size)
+            chunks.emplace_back(i, std::min<int32_t>(e, i + chunk_size));
+    const int nthr = std::min<int>((int)chunks.size(), max_streams);
     MR_TRY(win_aux(ctx, nthr));
     // the SLO vectors once per distinct (a3, a3_valid, length) of the batch (windows usually share
     // one pair), resident before any window's detector runs
@@ -587,15 +630,16 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
     MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));   // uploads done before other streams read them
     static const bool no_index = getenv("MR_NO_INDEX") != nullptr;
     std::vector<WinRun> w((size_t)n_windows);
+    std::vector<WinChunk> cw(chunks.size());
     std::vector<hipEvent_t> gev((size_t)ngroups, nullptr);   // a group's PageRanks are done
     std::vector<std::string> err((size_t)nthr);
-    // task queue: phase-1 tasks (window i -> i) first, phase-3 tasks (~i) appended per group
+    // task queue: phase-1 tasks (chunk c -> c) first, phase-3 tasks (window i -> ~i) appended per group
     std::mutex mu;
     std::condition_variable cv_task, cv_done;
     std::deque<int32_t> q;
     bool closed = false;
     std::vector<int> built((size_t)ngroups, 0);
-    for (int32_t i = 0; i < n_windows; ++i) q.push_back(i);
+    for (int32_t c = 0; c < (int32_t)chunks.size(); ++c) q.push_back(c);
     std::vector<std::thread> th;
     for (int k = 0; k < nthr; ++k)
         th.emplace_back([&, k] {
@@ -610,18 +654,28 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
                     task = q.front();
                     q.pop_front();
                 }
-                if (task >= 0) {   // detect + both builds
-                    const int32_t i = task;
-                    WinRun& r = w[(size_t)i];
-                    const mr_spans* sp = spans[i];
-                    if (sp->indexed && sp->uniform_times && sp->has_times && !no_index)
-                        r.rc = win_detect_build_async(a, sp, t0[i], t1[i], d_a3[slo_of[(size_t)i]]->p,
-                                                      d_a3v[slo_of[(size_t)i]]->p, r, precision);
-                    else   // (synchronised at its end: no event needed)
-                        r.rc = win_detect_build(a, sp, t0[i], t1[i], a3[i], a3_valid[i], r, nullptr, precision);
-                    if (r.rc != MR_OK && r.rc != MR_ERR_VALUE) err[(size_t)k] = a->err;
+                if (task >= 0) {   // a chunk's detectors + graph builds
+                    const int32_t i0 = chunks[(size_t)task].first, i1 = chunks[(size_t)task].second;
+                    std::vector<WinIn> fast;
+                    for (int32_t i = i0; i < i1; ++i) {
+                        WinRun& r = w[(size_t)i];
+                        const mr_spans* sp = spans[i];
+                        if (sp->indexed && sp->uniform_times && sp->has_times && !no_index) {
+                            fast.push_back(WinIn{sp, t0[i], t1[i], d_a3[slo_of[(size_t)i]]->p, d_a3v[slo_of[(size_t)i]]->p, &r});
+                        } else {   // (synchronised at its end: no event needed)
+                            r.rc = win_detect_build(a, sp, t0[i], t1[i], a3[i], a3_valid[i], r, nullptr, precision);
+                            if (r.rc != MR_OK && r.rc != MR_ERR_VALUE) err[(size_t)k] = a->err;
+                        }
+                    }
+                    if (!fast.empty()) {
+                        const int rc = win_chunk_build_async(a, fast.data(), (int)fast.size(), precision, cw[(size_t)task]);
+                        if (rc != MR_OK) {
+                            err[(size_t)k] = a->err;
+                            for (WinIn& f : fast) f.w->rc = rc;
+                        }
+                    }
                     std::lock_guard<std::mutex> lk(mu);
-                    ++built[(size_t)(i / gsz)];
+                    built[(size_t)(i0 / gsz)] += i1 - i0;
                     cv_done.notify_all();
                 } else {           // spectrum, after the group's PageRanks (an event, not a host wait)
                     const int32_t i = ~task;
@@ -646,13 +700,15 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
             std::unique_lock<std::mutex> lk(mu);
             cv_done.wait(lk, [&] { return built[(size_t)g] == i1 - i0; });
         }
+        for (size_t c = 0; c < chunks.size(); ++c)   // the group's chunks' graphs are ready
+            if (chunks[c].first >= i0 && chunks[c].first < i1 && cw[c].ev)
+                MR_TRY_HIP(ctx, hipStreamWaitEvent(ctx->stream, cw[c].ev, 0));
         std::vector<mr_graph*> gs;
         std::vector<int> anom;
         for (int32_t i = i0; i < i1; ++i) {
             WinRun& r = w[(size_t)i];
             n_out[i] = 0;
             if (r.rc == MR_OK && r.gn) {
-                if (r.ev) MR_TRY_HIP(ctx, hipStreamWaitEvent(ctx->stream, r.ev, 0));   // its graphs are ready
                 r.gn->ctx = r.ga->ctx = ctx;   // (built on an auxiliary context)
                 gs.push_back(r.gn);
                 gs.push_back(r.ga);

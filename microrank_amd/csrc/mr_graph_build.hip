@@ -445,6 +445,7 @@ constexpr int64_t IX_LDS_WORDS = 36864;   // k_ix_stats' dynamic LDS budget (144
 // decoupled look-back (two status chains), plus the clearing of the per-code counters and the
 // edge hash (a grid-stride share per block): one launch where there were four.
 constexpr int SEL_T = 256, SEL_I = 8, SEL_TILE = SEL_T * SEL_I;
+static_assert(SEL_T == 4 * WAVE, "k_ix_sel_scan2: one wave per look-back chain");
 __global__ void __launch_bounds__(SEL_T) k_ix_sel_scan(const uint8_t* mask, const int32_t* tlen, const int64_t* po_off,
                                                       int32_t NT, int32_t* tflag, int64_t* tpos, int64_t* zoff,
                                                       unsigned long long* st, uint64_t epoch, int32_t* ocnt,
@@ -488,13 +489,13 @@ __global__ void __launch_bounds__(SEL_T) k_ix_sel_scan(const uint8_t* mask, cons
         sb[tid] += y;
         __syncthreads();
     }
-    if (tid == 0) {
-        const int64_t aggA = sa[SEL_T - 1], aggB = sb[SEL_T - 1];
-        ex[0] = dl_lookback(st, tile, aggA, epoch);
-        ex[1] = dl_lookback(st + gridDim.x, tile, aggB, epoch);
-        if (tile == (int64_t)gridDim.x - 1) {
-            tpos[NT] = ex[0] + aggA;
-            zoff[NT] = ex[1] + aggB;
+    if (tid < 2 * WAVE) {   // wave c: chain c
+        const int c = tid / WAVE;
+        const int64_t agg = c ? sb[SEL_T - 1] : sa[SEL_T - 1];
+        const int64_t e = dl_lookback_wave(st + (size_t)c * gridDim.x, tile, agg, epoch);
+        if ((tid & (WAVE - 1)) == 0) {
+            ex[c] = e;
+            if (tile == (int64_t)gridDim.x - 1) (c ? zoff : tpos)[NT] = e + agg;
         }
     }
     __syncthreads();
@@ -732,12 +733,16 @@ __global__ void __launch_bounds__(SEL_T) k_ix_sel_scan2(const uint8_t* state, co
         for (int c = 0; c < 4; ++c) sa[c][tid] += v[c];
         __syncthreads();
     }
-    if (tid < 4) {   // chain c: (graph c / 2, tpos or zoff)
-        const int64_t agg = sa[tid][SEL_T - 1];
-        ex[tid] = dl_lookback(st + (size_t)tid * gridDim.x, tile, agg, epoch);
-        if (tile == (int64_t)gridDim.x - 1) {
-            int64_t* dst = (tid & 1) ? x.g[tid >> 1].zoff : x.g[tid >> 1].tpos;
-            dst[NT] = ex[tid] + agg;
+    {   // wave c: chain c (graph c / 2, tpos or zoff)
+        const int c = tid / WAVE;
+        const int64_t agg = sa[c][SEL_T - 1];
+        const int64_t e = dl_lookback_wave(st + (size_t)c * gridDim.x, tile, agg, epoch);
+        if ((tid & (WAVE - 1)) == 0) {
+            ex[c] = e;
+            if (tile == (int64_t)gridDim.x - 1) {
+                int64_t* dst = (c & 1) ? x.g[c >> 1].zoff : x.g[c >> 1].tpos;
+                dst[NT] = e + agg;
+            }
         }
     }
     __syncthreads();
@@ -1522,17 +1527,12 @@ int mr_ix_finish(mr_ctx* ctx, const mr_spans* sp, mr_graph* g, IxBuild& b, const
     MR_TRY(ix_finish(ctx, sp, g, b, h, false));
     return mr_graph_post_build(ctx, g);
 }
-int mr_ix_finish2(mr_ctx* ctx, const mr_spans* sp, mr_graph* g0, IxBuild& b0, const int64_t* h0, mr_graph* g1,
-                  IxBuild& b1, const int64_t* h1, std::vector<unsigned char>& keep) {
-    MR_TRY(ix_finish(ctx, sp, g0, b0, h0, false));
-    MR_TRY(ix_finish(ctx, sp, g1, b1, h1, false));
-    mr_graph* gs[2] = {g0, g1};
-    for (mr_graph* g : gs) {   // (mr_graph_post_build's fields)
-        g->rs_is_sr = true;
-        g->pr_identity = true;
-        g->n_pr = g->T;
-    }
-    return mr_graph_prepare_batch(ctx, gs, 2, keep);
+int mr_ix_finish_unprepared(mr_ctx* ctx, const mr_spans* sp, mr_graph* g, IxBuild& b, const int64_t* h) {
+    MR_TRY(ix_finish(ctx, sp, g, b, h, false));
+    g->rs_is_sr = true;   // (mr_graph_post_build's fields)
+    g->pr_identity = true;
+    g->n_pr = g->T;
+    return MR_OK;
 }
 
 // a built graph's trace-role fields and derived arrays (the K1 result is P_rs = P_sr)

@@ -59,7 +59,7 @@ void mr_pool_release(mr_ctx* ctx);
 int mr_read_words(mr_ctx* ctx, const int64_t* dev, int n, int64_t* out);
 // up to MR_PIN_BYTES bytes from the device into the context's pinned buffer (*host points there,
 // valid until the next read-back on this context); syncs the stream
-constexpr size_t MR_PIN_BYTES = 8192;
+constexpr size_t MR_PIN_BYTES = 65536;
 int mr_read_bytes(mr_ctx* ctx, const void* dev, size_t bytes, unsigned char** host);
 int mr_win_spectrum_small(mr_ctx* ctx, int32_t Na, const int32_t* a_podop, const double* a_w, const int32_t* a_cov,
                           int32_t Nn, const int32_t* n_podop, const double* n_w, const int32_t* n_cov, int32_t NP,
@@ -354,9 +354,11 @@ int mr_win_spectrum_launch(mr_ctx* ctx, int32_t Na, const int32_t* a_podop, cons
                            int64_t A, int64_t Nl, int method, int32_t k, unsigned char* d_slot);
 void mr_win_spectrum_unpack(const unsigned char* slot, int32_t* out_codes, double* out_score, int32_t* n_out);
 int mr_ix_finish(mr_ctx* ctx, const mr_spans* sp, mr_graph* g, IxBuild& b, const int64_t* h);
-// both graphs of mr_ix_launch2 finished and prepared together (mr_graph_prepare_batch)
-int mr_ix_finish2(mr_ctx* ctx, const mr_spans* sp, mr_graph* g0, IxBuild& b0, const int64_t* h0, mr_graph* g1,
-                  IxBuild& b1, const int64_t* h1, std::vector<unsigned char>& keep);
+// a graph of mr_ix_launch / mr_ix_launch2 finished WITHOUT its prepare: the caller prepares many
+// such graphs together (mr_graph_prepare_batch)
+int mr_ix_finish_unprepared(mr_ctx* ctx, const mr_spans* sp, mr_graph* g, IxBuild& b, const int64_t* h);
 int mr_pagerank_presetup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, int precision, uint32_t flags);
-int mr_pagerank_presetup2(mr_ctx* ctx, mr_graph* g0, mr_graph* g1, double d, int precision,
-                          std::vector<unsigned char>& keep);
+// mr_pagerank_presetup of n graphs in six launches when all allow the batched set-up (keep: its
+// host descriptors, alive until the stream has used them)
+int mr_pagerank_presetup_n(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly, int n, double d, int precision,
+                           std::vector<unsigned char>& keep);

@@ -420,9 +420,10 @@ __device__ __forceinline__ void tr_chunk_scan_body(int32_t tile_, int32_t ntiles
         sa[tid] += x;
         __syncthreads();
     }
-    if (tid == 0) {
-        ex = dl_lookback(st, tile, sa[TS_T - 1], epoch);
-        if (tile == (int64_t)ntiles - 1) {
+    if (tid < WAVE) {
+        const int64_t e = dl_lookback_wave(st, tile, sa[TS_T - 1], epoch);
+        if (tid == 0) ex = e;
+        if (tid == 0 && tile == (int64_t)ntiles - 1) {
             c64[n_wt] = ex + sa[TS_T - 1];
             coff[n_wt] = (int32_t)(ex + sa[TS_T - 1]);
         }
@@ -4173,22 +4174,19 @@ static uint64_t kind_hmask(int a) { return (a == 0 && getenv("MR_KIND_TEST_COLLI
 // these arguments, on THIS context's stream (the one that built it): mr_windows_batch sets up a
 // window's graphs while the previous group's iterations run.  The next call on the graph skips
 // its own setup when the arguments match (first kind-hash seed; a collision retries in full).
-// mr_pagerank_presetup of a window's two graphs in six launches when both allow the batched set-up
-// (keep: its host descriptors, alive until the stream has used them)
-int mr_pagerank_presetup2(mr_ctx* ctx, mr_graph* g0, mr_graph* g1, double d, int precision,
-                          std::vector<unsigned char>& keep) {
+int mr_pagerank_presetup_n(mr_ctx* ctx, mr_graph* const* gs, const int* an, int n, double d, int precision,
+                           std::vector<unsigned char>& keep) {
     const bool fp32 = precision == MR_FP32;
     const bool tr = fx_kind() == FXK_TR;
-    if (!(g0->N && g0->T && g1->N && g1->T && setup_batchable(g0, tr, 0) && setup_batchable(g1, tr, 0)) ||
-        getenv("MR_NO_SETUP_BATCH") != nullptr) {
-        MR_TRY(mr_pagerank_presetup(ctx, g0, 0, d, precision, 0));
-        return mr_pagerank_presetup(ctx, g1, 1, d, precision, 0);
+    bool batch = n >= 2 && getenv("MR_NO_SETUP_BATCH") == nullptr;
+    for (int i = 0; i < n && batch; ++i) batch = gs[i]->N && gs[i]->T && setup_batchable(gs[i], tr, 0);
+    if (!batch) {
+        for (int i = 0; i < n; ++i) MR_TRY(mr_pagerank_presetup(ctx, gs[i], an[i], d, precision, 0));
+        return MR_OK;
     }
-    mr_graph* gs[2] = {g0, g1};
-    const int an[2] = {0, 1};
     DBuf<SDev> dsd;   // (returns to this context's pool: reused only by later work on this stream)
-    MR_TRY(pagerank_setup_batch(ctx, gs, an, 2, d, fp32, kind_seed(0), kind_hmask(0), keep, dsd));
-    for (int i = 0; i < 2; ++i) {
+    MR_TRY(pagerank_setup_batch(ctx, gs, an, n, d, fp32, kind_seed(0), kind_hmask(0), keep, dsd));
+    for (int i = 0; i < n; ++i) {
         mr_graph* g = gs[i];
         g->pre_ok = true;
         g->pre_anomaly = an[i];

@@ -60,28 +60,43 @@ int mr_dl_status(mr_ctx* ctx, int64_t words, unsigned long long** st, uint64_t* 
 __device__ __forceinline__ unsigned long long dl_word(uint64_t epoch, unsigned flag, int64_t v) {
     return (epoch << (DL_VB + 2)) | ((unsigned long long)flag << DL_VB) | ((unsigned long long)v & DL_VMASK);
 }
-// one thread of tile `tile`: publish the tile's sum, walk back to the tiles before it (lower
-// block indices: already dispatched) and publish the inclusive prefix; returns the exclusive one.
-// Relaxed agent-scope atomics (sc1): the word carries its value, nothing else is published.
-__device__ __forceinline__ int64_t dl_lookback(unsigned long long* st, int64_t tile, int64_t agg, uint64_t epoch) {
-    int64_t excl = 0;
+// Tile `tile` publishes its sum, walks back over the tiles before it (lower block indices: already
+// dispatched) and publishes its inclusive prefix.  ONE whole wave calls it (every lane, uniformly):
+// lane l polls tile (hi - l), so a poll covers 64 predecessors -- a one-thread walk pays one
+// cross-XCD round trip per predecessor that has only its own sum up (~1 us each: 100 tiles had
+// cost ~30 us), this one pays one per 64.  Lanes [0, L] count, L the nearest tile with its
+// inclusive prefix (flag 2), and only they must have published.  Relaxed agent-scope atomics: the
+// word carries its value, nothing else is published.  Returns the exclusive prefix to every lane.
+__device__ __forceinline__ int64_t dl_lookback_wave(unsigned long long* st, int64_t tile, int64_t agg, uint64_t epoch) {
+    const int lane = threadIdx.x & (WAVE - 1);
     if (tile == 0) {
-        __hip_atomic_store(&st[0], dl_word(epoch, 2, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0) __hip_atomic_store(&st[0], dl_word(epoch, 2, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return 0;
     }
-    __hip_atomic_store(&st[tile], dl_word(epoch, 1, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (int64_t j = tile - 1; j >= 0;) {
-        const unsigned long long w = __hip_atomic_load(&st[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0) __hip_atomic_store(&st[tile], dl_word(epoch, 1, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int64_t excl = 0;
+    for (int64_t hi = tile - 1;;) {
+        const int64_t j = hi - lane;
+        const unsigned long long w = j >= 0 ? __hip_atomic_load(&st[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                            : dl_word(epoch, 2, 0);
         const unsigned flag = (unsigned)(w >> DL_VB) & 3u;
-        if ((w >> (DL_VB + 2)) != epoch || flag == 0) {
+        const bool ok = (w >> (DL_VB + 2)) == epoch && flag != 0;
+        const unsigned long long inc = __ballot(ok && flag == 2), bad = __ballot(!ok);
+        const int L = inc ? __builtin_ctzll(inc) : WAVE;
+        const unsigned long long need = L == WAVE ? ~0ull : (2ull << L) - 1ull;
+        if (bad & need) {   // a tile this poll needs has not published this call's value yet
             __builtin_amdgcn_s_sleep(1);
-            continue;   // tile j has not published this call's value yet
+            continue;
         }
-        excl += (int64_t)(w & DL_VMASK);
-        if (flag == 2) break;
-        --j;
+        int64_t v = lane <= L ? (int64_t)(w & DL_VMASK) : 0;
+#pragma unroll
+        for (int m = WAVE / 2; m >= 1; m >>= 1) v += __shfl_xor(v, m, WAVE);
+        excl += v;
+        if (inc) break;
+        hi -= WAVE;
     }
-    __hip_atomic_store(&st[tile], dl_word(epoch, 2, excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0)
+        __hip_atomic_store(&st[tile], dl_word(epoch, 2, excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return excl;
 }
 int mr_exclusive_scan(mr_ctx* ctx, const int64_t* in, int64_t* out, int64_t n, int64_t* tmp);

@@ -152,10 +152,12 @@ __global__ void __launch_bounds__(SCAN_T) k_scan_dl(const In* in, int64_t* out, 
         __syncthreads();
     }
     const int64_t agg = tsum[SCAN_T - 1];
-    if (threadIdx.x == 0) {
-        const int64_t excl = dl_lookback(st, tile, agg, epoch);
-        s_excl = excl;
-        if (tile == (int64_t)gridDim.x - 1) out[n] = excl + agg;
+    if (threadIdx.x < WAVE) {
+        const int64_t excl = dl_lookback_wave(st, tile, agg, epoch);
+        if (threadIdx.x == 0) {
+            s_excl = excl;
+            if (tile == (int64_t)gridDim.x - 1) out[n] = excl + agg;
+        }
     }
     __syncthreads();
     int64_t run = s_excl + (threadIdx.x ? tsum[threadIdx.x - 1] : 0);
