@@ -23,6 +23,7 @@
 #include <string>
 #include <thread>
 
+#include "mr_detect_dev.h"
 #include "mr_prim.h"
 #include "mr_sort.h"
 
@@ -388,8 +389,7 @@ static int win_chunk_build_async(mr_ctx* ctx, const WinIn* in, int n, int precis
         const int32_t NT = s->n_traces;
         int64_t* wk = wb.p + (size_t)k * WW;
         MR_TRY(dst[(size_t)k].alloc(ctx, std::max(NT, 1)));
-        MR_TRY(mr_detect_indexed_launch(ctx, s, in[k].t0, in[k].t1, in[k].a3, in[k].a3v, dst[(size_t)k].p,
-                                        (unsigned long long*)wk));
+        const DetIn di = mr_detect_in(s, in[k].t0, in[k].t1, in[k].a3, in[k].a3v, dst[(size_t)k].p, (unsigned long long*)wk);
         w.gn = new mr_graph();
         w.gn->ctx = ctx;
         w.ga = new mr_graph();
@@ -398,8 +398,18 @@ static int win_chunk_build_async(mr_ctx* ctx, const WinIn* in, int n, int precis
         // (the graphs take EVERY row of the selected traces: get_pagerank_graph(list, data),
         // online_rca.py:180,185 / preprocess_data.py:148).  Both from the states in one pass over
         // the index when the table allows it, else one build per mask.
-        const int rc2 = mr_ix_launch2(ctx, s, dst[(size_t)k].p, w.gn, w.ga, bn, ba, wk + CW);
+        // the detector inside the index pass's first launch for tables up to MR_DET_FUSE_MAX traces
+        // (default 65536; measured: C3's 20k traces +2%, C2's 200k -3% -- the fused launch's tiles
+        // are the detector's 256 traces, 8x k_ix_sel_scan2's, and its look-back chains 8x longer).
+        // MR_NO_DET_FUSE: never.  (Both read per call.)
+        const char* fm = getenv("MR_DET_FUSE_MAX");
+        const bool fuse = getenv("MR_NO_DET_FUSE") == nullptr && (int64_t)NT <= (fm ? (int64_t)atoll(fm) : 65536);
+        if (!fuse) MR_TRY(mr_detect_indexed_launch(ctx, s, in[k].t0, in[k].t1, in[k].a3, in[k].a3v, dst[(size_t)k].p,
+                                                   (unsigned long long*)wk));
+        const int rc2 = mr_ix_launch2(ctx, s, dst[(size_t)k].p, w.gn, w.ga, bn, ba, wk + CW, fuse ? &di : nullptr);
         if (rc2 == MR_ERR_STATE) {
+            if (fuse) MR_TRY(mr_detect_indexed_launch(ctx, s, in[k].t0, in[k].t1, in[k].a3, in[k].a3v, dst[(size_t)k].p,
+                                                      (unsigned long long*)wk));
             DBuf<uint8_t> m_abn, m_nor;
             MR_TRY(m_abn.alloc(ctx, std::max(NT, 1)));
             MR_TRY(m_nor.alloc(ctx, std::max(NT, 1)));

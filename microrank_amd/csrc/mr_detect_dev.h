@@ -1,0 +1,108 @@
+// The window detector's per-block body (anormaly_detector.system_anomaly_detect on whole traces),
+// shared by k_ix_detect (mr_span_index.hip) and the fused detector + selection scan of a window's
+// two graph builds (k_ix_detect_scan2, mr_graph_build.hip).
+//
+// A trace is in the window iff its trace-level [start, end] lies in [t0, t1] (T15); expect = sum
+// over the trace's service-ops in name order of count * (mean + 3 std) (sequential, no FMA: T14);
+// abnormal iff max duration / 1000 > expect; traces with max <= 0 are dropped
+// (preprocess_data.py:117).
+#pragma once
+#include "mr_internal.h"
+
+constexpr int DB = 256, DCAP = 16;   // detector: traces per block, staged entries per thread
+constexpr int CSH = 64;              // counter shards
+static_assert(CSH == MR_DETECT_SHARDS, "detector counter shards");
+
+struct DetIn {
+    const int32_t* tlen;
+    const long long *tts, *tte, *tmaxd;
+    const int64_t* sv_off;
+    const int32_t *sv_op, *sv_cnt;
+    const double* a3;
+    const uint8_t* a3v;
+    int64_t t0, t1;
+    uint8_t* state;                 // out: 0 out / 1 normal / 2 abnormal, every trace
+    unsigned long long* counts;     // out: 3 * CSH counter shards (abnormal, normal, in-window rows)
+};
+
+// Block of DB threads, trace blockIdx.x * DB + threadIdx.x per thread: its state (also returned)
+// and the block's counts.  `term` is the caller's LDS of DB * DCAP doubles.
+__device__ __forceinline__ int detect_block(int32_t NT, const DetIn& d, double* term) {
+    const int32_t tb = blockIdx.x * DB, te_ = min(tb + DB, NT);
+    const int32_t t = tb + threadIdx.x;
+    const int64_t r0 = d.sv_off[tb], r1 = d.sv_off[te_];
+    const bool fits = r1 - r0 <= (int64_t)DB * DCAP;
+    // the block's (count * (mean + 3 std)) terms, entry-parallel: one product per entry as the
+    // reference rounds it; ops without an SLO contribute +0.0 (an exact no-op on the sum)
+    if (fits) {   // all loads of a thread in flight together: ids and counts, then the SLO gathers
+        int32_t op[DCAP], cn[DCAP];
+#pragma unroll
+        for (int j = 0; j < DCAP; ++j) {
+            const int64_t r = min(r0 + threadIdx.x + (int64_t)j * DB, max(r1 - 1, r0));
+            op[j] = d.sv_op[r];
+            cn[j] = d.sv_cnt[r];
+        }
+        double av[DCAP];
+        uint8_t vv[DCAP];
+#pragma unroll
+        for (int j = 0; j < DCAP; ++j) {
+            av[j] = d.a3[op[j]];
+            vv[j] = d.a3v[op[j]];
+        }
+#pragma unroll
+        for (int j = 0; j < DCAP; ++j) {
+            const int64_t r = r0 + threadIdx.x + (int64_t)j * DB;
+            if (r < r1) term[r - r0] = vv[j] ? (double)cn[j] * av[j] : 0.0;
+        }
+    }
+    __syncthreads();
+    int st = 0;
+    int64_t rows = 0;
+    if (t < NT) {
+        const bool in = d.tlen[t] > 0 && d.tts[t] >= d.t0 && d.tte[t] <= d.t1;
+        if (in) {
+            rows = d.tlen[t];
+            const long long mx = d.tmaxd[t];
+            if (mx > 0) {   // grouped[grouped['duration'] > 0] (preprocess_data.py:117)
+                double expect = 0.0;
+                const int64_t a = d.sv_off[t], b = d.sv_off[t + 1];
+                if (fits) {
+                    for (int64_t r = a; r < b; ++r) expect += term[r - r0];   // name order (T14)
+                } else {
+                    for (int64_t r = a; r < b; ++r) {
+                        const int32_t op = d.sv_op[r];
+                        if (d.a3v[op]) expect += (double)d.sv_cnt[r] * d.a3[op];   // anormaly_detector.py:64-65
+                    }
+                }
+                st = (double)mx / 1000.0 > expect ? 2 : 1;                   // :58, :69
+            }
+        }
+        d.state[t] = (uint8_t)st;
+    }
+    // counts: per wave, per block, then one add per block into one of CSH shards (~200k traces
+    // on three same-address counters had cost ~0.1 ms of serialised atomics)
+    __shared__ unsigned long long bc[3][DB / 64];
+    const uint64_t ab = __ballot(st == 2), nr = __ballot(st == 1);
+    int64_t rw = rows;
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) rw += __shfl_xor(rw, m, 64);
+    const int w = threadIdx.x / 64;
+    if ((threadIdx.x & 63) == 0) {
+        bc[0][w] = (unsigned long long)__popcll(ab);
+        bc[1][w] = (unsigned long long)__popcll(nr);
+        bc[2][w] = (unsigned long long)rw;
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        unsigned long long v = 0;
+        for (int k = 0; k < DB / 64; ++k) v += bc[threadIdx.x][k];
+        if (v) atomicAdd(&d.counts[(size_t)(blockIdx.x % CSH) * 3 + threadIdx.x], v);
+    }
+    return st;
+}
+
+inline DetIn mr_detect_in(const mr_spans* s, int64_t t0, int64_t t1, const double* a3, const uint8_t* a3v,
+                          uint8_t* state, unsigned long long* counts) {
+    return DetIn{s->tlen.p, s->tts.p, s->tte.p, s->tmaxd.p, s->sv_off.p, s->sv_op.p, s->sv_cnt.p, a3, a3v, t0, t1,
+                 state, counts};
+}

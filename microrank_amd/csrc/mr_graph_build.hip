@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <vector>
 
+#include "mr_detect_dev.h"
 #include "mr_prim.h"
 #include "mr_sort.h"
 
@@ -268,6 +269,7 @@ __global__ void k_edge_csr(const uint64_t* skey, int64_t E, int nb, int32_t* ss_
 // instead of ~15 launches and two host round trips.  Sizes go to `out` (N, E, overflow); a graph
 // with more than NS_EMAX edges sets overflow and the caller runs build_nodes instead.
 constexpr int NS_T = 1024, NS_PMAX = 4096, NS_EMAX = 8192;
+static_assert(NS_EMAX <= 2 * NS_PMAX, "nodes_small: the CSR parents reuse the 64-bit key buffer");
 __device__ __forceinline__ void ns_bitonic(uint64_t* a, int n) {   // n a power of two
     for (int k = 2; k <= n; k <<= 1)
         for (int j = k >> 1; j > 0; j >>= 1) {
@@ -359,15 +361,27 @@ __device__ void nodes_small(const uint64_t* gk, const uint32_t* gc, int64_t ecap
             qb[qp++] = ((uint64_t)(uint32_t)ofirst[c] << 32) | (uint32_t)c;
         }
     }
-    int qn = 1;
-    while (qn < nQ) qn <<= 1;
-    for (int i = nQ + tid; i < qn; i += NS_T) qb[i] = EMPTY;
     __syncthreads();
-    if (nQ > 1) ns_bitonic(qb, qn);
-    for (int i = tid; i < nQ; i += NS_T) {
-        const int32_t c = (int32_t)(qb[i] & 0xffffffffu);
-        noc[c] = nP + i;
-        node_podop[nP + i] = c;
+    if (nQ <= NS_T) {   // rank of each (distinct) key by counting: one pass, no sorting network
+        if (tid < nQ) {
+            const uint64_t key = qb[tid];
+            int32_t r = 0;
+            for (int j = 0; j < nQ; ++j) r += qb[j] < key;
+            const int32_t c = (int32_t)(key & 0xffffffffu);
+            noc[c] = nP + r;
+            node_podop[nP + r] = c;
+        }
+    } else {
+        int qn = 1;
+        while (qn < nQ) qn <<= 1;
+        for (int i = nQ + tid; i < qn; i += NS_T) qb[i] = EMPTY;
+        __syncthreads();
+        ns_bitonic(qb, qn);
+        for (int i = tid; i < nQ; i += NS_T) {
+            const int32_t c = (int32_t)(qb[i] & 0xffffffffu);
+            noc[c] = nP + i;
+            node_podop[nP + i] = c;
+        }
     }
     __syncthreads();
     const int32_t N = nP + nQ;
@@ -378,26 +392,53 @@ __device__ void nodes_small(const uint64_t* gk, const uint32_t* gc, int64_t ecap
             nchild[noc[c]] = nch[c];
             cov[noc[c]] = ocov[c];
         }
-    // P_ss by child: edges as (child node << 32 | parent node), sorted; offsets by binary search
+    // P_ss by child (edges sorted by (child node, parent node)): a counting sort by child into
+    // the CSR, then each child's few parents sorted in place.  (is_par / nch / qb are free now.)
+    __syncthreads();
+    int32_t* ccnt = nch;           // edges per child node
+    int32_t* cpos = is_par;        // running insert position per child node
+    int32_t* cpar = (int32_t*)qb;  // parents in CSR order (NS_EMAX <= 2 NS_PMAX slots)
+    for (int n = tid; n < N; n += NS_T) ccnt[n] = 0;
+    __syncthreads();
     for (int e = tid; e < E; e += NS_T) {
         const uint64_t k = eb[e];
-        eb[e] = ((uint64_t)(uint32_t)noc[(int32_t)(k & 0xffffffffu)] << 32) | (uint32_t)noc[(int32_t)(k >> 32)];
+        const int32_t ch = noc[(int32_t)(k & 0xffffffffu)];
+        eb[e] = ((uint64_t)(uint32_t)ch << 32) | (uint32_t)noc[(int32_t)(k >> 32)];
+        atomicAdd(&ccnt[ch], 1);
     }
-    int en = 1;
-    while (en < E) en <<= 1;
-    for (int i = E + tid; i < en; i += NS_T) eb[i] = EMPTY;
     __syncthreads();
-    if (E > 1) ns_bitonic(eb, en);
-    for (int e = tid; e < E; e += NS_T) ss_par[e] = (int32_t)(eb[e] & 0xffffffffu);
-    for (int n = tid; n <= N; n += NS_T) {
-        int32_t lo = 0, hi = E;   // first edge whose child >= n
-        while (lo < hi) {
-            const int32_t mid = (lo + hi) >> 1;
-            if ((int32_t)(eb[mid] >> 32) < n) lo = mid + 1;
-            else hi = mid;
+    {
+        const int perN = (N + NS_T - 1) / NS_T, n0 = tid * perN;
+        int32_t run = 0;
+        for (int n = n0; n < min(n0 + perN, N); ++n) run += ccnt[n];
+        int32_t off = ns_scan(run, sbuf, &tot);
+        for (int n = n0; n < min(n0 + perN, N); ++n) {
+            cpos[n] = off;
+            ss_off[n] = off;
+            off += ccnt[n];
         }
-        ss_off[n] = lo;
+        if (tid == 0) ss_off[N] = E;
     }
+    __syncthreads();
+    for (int e = tid; e < E; e += NS_T) {
+        const uint64_t k = eb[e];
+        cpar[atomicAdd(&cpos[(int32_t)(k >> 32)], 1)] = (int32_t)(k & 0xffffffffu);
+    }
+    __syncthreads();
+    for (int n = tid; n < N; n += NS_T) {   // cpos[n] is now the end of child n's run
+        const int32_t b = cpos[n], a = b - ccnt[n];
+        for (int32_t i = a + 1; i < b; ++i) {   // insertion sort: runs are a child's few parents
+            const int32_t v = cpar[i];
+            int32_t j = i - 1;
+            while (j >= a && cpar[j] > v) {
+                cpar[j + 1] = cpar[j];
+                --j;
+            }
+            cpar[j + 1] = v;
+        }
+    }
+    __syncthreads();
+    for (int e = tid; e < E; e += NS_T) ss_par[e] = cpar[e];
     if (tid == 0) {
         out[0] = N;
         out[1] = E;
@@ -764,6 +805,73 @@ __global__ void __launch_bounds__(SEL_T) k_ix_sel_scan2(const uint8_t* state, co
         }
     }
 }
+// The window's detector and k_ix_sel_scan2's selection scans in ONE launch: tiles of DB traces,
+// each thread its trace's state (detect_block, into d.state for the later passes) and then the
+// four look-back chains over one trace per thread.
+__global__ void __launch_bounds__(DB) k_ix_detect_scan2(DetIn d, const int64_t* po_off, int32_t NT, IxSide2 x,
+                                                        unsigned long long* st, uint64_t epoch, int32_t NP,
+                                                        int64_t ecap) {
+    __shared__ double term[DB * DCAP];
+    __shared__ int64_t sa[4][DB];
+    __shared__ int64_t ex[4];
+    const int tid = threadIdx.x;
+    const int64_t gsz = (int64_t)gridDim.x * DB, gi = (int64_t)blockIdx.x * DB + tid;
+    for (int64_t i = gi; i < max((int64_t)NP, ecap); i += gsz)
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+            if (i < NP) {
+                x.g[g].ocnt[i] = 0;
+                x.g[g].ofirst[i] = 0x7f7f7f7f;
+                x.g[g].ocov[i] = 0;
+            }
+            if (i < ecap) x.g[g].gc[i] = 0u;
+        }
+    const int stt = detect_block(NT, d, term);
+    const int64_t tile = blockIdx.x, t = tile * DB + tid;
+    const int s_ = t < NT && d.tlen[t] > 0 ? side_of((uint8_t)stt) : -1;
+    const int64_t z = s_ >= 0 ? po_off[t + 1] - po_off[t] : 0;
+    if (t < NT) {
+        x.g[0].tflag[t] = s_ == 0;
+        x.g[1].tflag[t] = s_ == 1;
+    }
+    int64_t acc[4] = {0, 0, 0, 0};
+    if (s_ >= 0) {
+        acc[2 * s_] = 1;
+        acc[2 * s_ + 1] = z;
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) sa[c][tid] = acc[c];
+    __syncthreads();
+    for (int o = 1; o < DB; o <<= 1) {
+        int64_t v[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) v[c] = tid >= o ? sa[c][tid - o] : 0;
+        __syncthreads();
+#pragma unroll
+        for (int c = 0; c < 4; ++c) sa[c][tid] += v[c];
+        __syncthreads();
+    }
+    {   // wave c: chain c (graph c / 2, tpos or zoff)
+        const int c = tid / WAVE;
+        const int64_t agg = sa[c][DB - 1];
+        const int64_t e = dl_lookback_wave(st + (size_t)c * gridDim.x, tile, agg, epoch);
+        if ((tid & (WAVE - 1)) == 0) {
+            ex[c] = e;
+            if (tile == (int64_t)gridDim.x - 1) {
+                int64_t* dst = (c & 1) ? x.g[c >> 1].zoff : x.g[c >> 1].tpos;
+                dst[NT] = e + agg;
+            }
+        }
+    }
+    __syncthreads();
+    if (t < NT) {   // (values of the graph the trace is not in are never read)
+        x.g[0].tpos[t] = ex[0] + sa[0][tid] - acc[0];
+        x.g[0].zoff[t] = ex[1] + sa[1][tid] - acc[1];
+        x.g[1].tpos[t] = ex[2] + sa[2][tid] - acc[2];
+        x.g[1].zoff[t] = ex[3] + sa[3][tid] - acc[3];
+    }
+}
+static_assert(DB == 4 * WAVE, "k_ix_detect_scan2: one wave per look-back chain");
 // both graphs' per-pod-op counts / first rows / coverage and edge counts per dense id, one pass
 __global__ void __launch_bounds__(IX_BT) k_ix_stats2(const uint8_t* state, int64_t n_po, const int32_t* po_tr,
                                                     const int32_t* po_op, const int32_t* po_cnt,
@@ -1445,10 +1553,11 @@ static int graph_build_indexed(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d
 
 // Both graphs of a window from the detector's states in one pass over the index (k_ix_sel_scan2,
 // k_ix_stats2, k_ix_cross2, k_nodes_small2, k_ix_traces2: five launches for two graphs); sizes of
-// graph g to d_out + 8 g.  MR_ERR_STATE when the table is past the one-pass limits (dense edge ids,
+// graph g to d_out + 8 g.  det (nullable): the detector runs in the first launch
+// (k_ix_detect_scan2) and writes the states to d_state.  MR_ERR_STATE when the table is past the one-pass limits (dense edge ids,
 // both graphs' LDS histograms, the one-block node order): the caller builds them one by one.
 int mr_ix_launch2(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d_state, mr_graph* g0, mr_graph* g1, IxBuild& b0,
-                  IxBuild& b1, int64_t* d_out) {
+                  IxBuild& b1, int64_t* d_out, const DetIn* det) {
     const bool off = getenv("MR_NO_IX2") != nullptr;   // A/B knob (read per call: tests flip it)
     const int32_t NT = sp->n_traces, NP = sp->n_podops;
     const int64_t nek = sp->n_edge_keys;
@@ -1490,7 +1599,14 @@ int mr_ix_launch2(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d_state, mr_gr
                          d_out + 8 * k};
         to.g[k] = TrOut{G->trace_code.p, G->len_t.p, G->rs_ops.p, G->rs_off.p, B.node_of_code.p};
     }
-    {
+    if (det) {   // the detector's states come out of the same launch (into det->state == d_state)
+        const int64_t nt = std::max<int64_t>(cdiv((int64_t)NT, DB), 1);
+        unsigned long long* dst = nullptr;
+        uint64_t epoch = 0;
+        MR_TRY(mr_dl_status(ctx, 4 * nt, &dst, &epoch));
+        hipLaunchKernelGGL(k_ix_detect_scan2, dim3((unsigned)nt), dim3(DB), 0, st, *det, sp->po_off.p, NT, xs, dst,
+                           epoch, NP, nek);
+    } else {
         const int64_t nt = std::max<int64_t>(cdiv((int64_t)NT, SEL_TILE), 1);
         unsigned long long* dst = nullptr;
         uint64_t epoch = 0;

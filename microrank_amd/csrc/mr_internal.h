@@ -338,8 +338,9 @@ struct IxBuild {
     bool small = false;   // the one-block node order ran: its sizes are in d_out
 };
 int mr_ix_launch(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d_mask, mr_graph* g, IxBuild& b, int64_t* d_out);
+struct DetIn;   // (mr_detect_dev.h)
 int mr_ix_launch2(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d_state, mr_graph* g0, mr_graph* g1, IxBuild& b0,
-                  IxBuild& b1, int64_t* d_out);
+                  IxBuild& b1, int64_t* d_out, const DetIn* det = nullptr);
 constexpr int MR_DETECT_SHARDS = 64;
 int mr_detect_indexed_launch(mr_ctx* ctx, const mr_spans* s, int64_t t0, int64_t t1, const double* d_a3,
                              const uint8_t* d_a3v, uint8_t* d_state, unsigned long long* counts);

@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <climits>
 
+#include "mr_detect_dev.h"
 #include "mr_prim.h"
 #include "mr_sort.h"
 
@@ -184,87 +185,10 @@ __global__ void k_ix_edge_runs(const uint64_t* key, const int32_t* head, const i
 }
 
 // ---------------------------------------------------------------- window detector (uniform times)
-// anormaly_detector.system_anomaly_detect on whole traces: in window iff the trace-level
-// [start, end] lies in [t0, t1] (T15); expect = sum over the trace's service-ops in name order of
-// count * (mean + 3 std) (sequential, no FMA: T14); abnormal iff max duration / 1000 > expect.
-constexpr int DB = 256, DCAP = 16;   // detector: traces per block, staged entries per thread
-constexpr int CSH = 64;              // counter shards
-__global__ void __launch_bounds__(DB) k_ix_detect(int32_t NT, const int32_t* tlen, const long long* tts,
-                                                  const long long* tte, const long long* tmaxd, const int64_t* sv_off,
-                                                  const int32_t* sv_op, const int32_t* sv_cnt, const double* a3,
-                                                  const uint8_t* a3v, int64_t t0, int64_t t1, uint8_t* state,
-                                                  unsigned long long* counts) {
+// (the per-block body: mr_detect_dev.h)
+__global__ void __launch_bounds__(DB) k_ix_detect(int32_t NT, DetIn d) {
     __shared__ double term[DB * DCAP];
-    const int32_t tb = blockIdx.x * DB, te_ = min(tb + DB, NT);
-    const int32_t t = tb + threadIdx.x;
-    const int64_t r0 = sv_off[tb], r1 = sv_off[te_];
-    const bool fits = r1 - r0 <= (int64_t)DB * DCAP;
-    // the block's (count * (mean + 3 std)) terms, entry-parallel: one product per entry as the
-    // reference rounds it; ops without an SLO contribute +0.0 (an exact no-op on the sum)
-    if (fits) {   // all loads of a thread in flight together: ids and counts, then the SLO gathers
-        int32_t op[DCAP], cn[DCAP];
-#pragma unroll
-        for (int j = 0; j < DCAP; ++j) {
-            const int64_t r = min(r0 + threadIdx.x + (int64_t)j * DB, max(r1 - 1, r0));
-            op[j] = sv_op[r];
-            cn[j] = sv_cnt[r];
-        }
-        double av[DCAP];
-        uint8_t vv[DCAP];
-#pragma unroll
-        for (int j = 0; j < DCAP; ++j) {
-            av[j] = a3[op[j]];
-            vv[j] = a3v[op[j]];
-        }
-#pragma unroll
-        for (int j = 0; j < DCAP; ++j) {
-            const int64_t r = r0 + threadIdx.x + (int64_t)j * DB;
-            if (r < r1) term[r - r0] = vv[j] ? (double)cn[j] * av[j] : 0.0;
-        }
-    }
-    __syncthreads();
-    int st = 0;
-    int64_t rows = 0;
-    if (t < NT) {
-        const bool in = tlen[t] > 0 && tts[t] >= t0 && tte[t] <= t1;
-        if (in) {
-            rows = tlen[t];
-            const long long mx = tmaxd[t];
-            if (mx > 0) {   // grouped[grouped['duration'] > 0] (preprocess_data.py:117)
-                double expect = 0.0;
-                const int64_t a = sv_off[t], b = sv_off[t + 1];
-                if (fits) {
-                    for (int64_t r = a; r < b; ++r) expect += term[r - r0];   // name order (T14)
-                } else {
-                    for (int64_t r = a; r < b; ++r) {
-                        const int32_t op = sv_op[r];
-                        if (a3v[op]) expect += (double)sv_cnt[r] * a3[op];   // anormaly_detector.py:64-65
-                    }
-                }
-                st = (double)mx / 1000.0 > expect ? 2 : 1;                   // :58, :69
-            }
-        }
-        state[t] = (uint8_t)st;
-    }
-    // counts: per wave, per block, then one add per block into one of CSH shards (~200k traces
-    // on three same-address counters had cost ~0.1 ms of serialised atomics)
-    __shared__ unsigned long long bc[3][DB / 64];
-    const uint64_t ab = __ballot(st == 2), nr = __ballot(st == 1);
-    int64_t rw = rows;
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) rw += __shfl_xor(rw, m, 64);
-    const int w = threadIdx.x / 64;
-    if ((threadIdx.x & 63) == 0) {
-        bc[0][w] = (unsigned long long)__popcll(ab);
-        bc[1][w] = (unsigned long long)__popcll(nr);
-        bc[2][w] = (unsigned long long)rw;
-    }
-    __syncthreads();
-    if (threadIdx.x < 3) {
-        unsigned long long v = 0;
-        for (int k = 0; k < DB / 64; ++k) v += bc[threadIdx.x][k];
-        if (v) atomicAdd(&counts[(size_t)(blockIdx.x % CSH) * 3 + threadIdx.x], v);
-    }
+    (void)detect_block(NT, d, term);
 }
 
 // ---------------------------------------------------------------- the driver's window sweep (f3)
@@ -523,7 +447,6 @@ int mr_spans_index(mr_ctx* ctx, mr_spans* s) {
     return MR_OK;
 }
 
-static_assert(CSH == MR_DETECT_SHARDS, "detector counter shards");
 // Window detector on the index (uniform trace times): state[t] 0 out / 1 normal / 2 abnormal for
 // EVERY trace; counts (3 * MR_DETECT_SHARDS words, zeroed by the caller) receive the abnormal /
 // normal / in-window-row counter shards (mr_detect_sum adds them up on the host).
@@ -531,8 +454,8 @@ int mr_detect_indexed_launch(mr_ctx* ctx, const mr_spans* s, int64_t t0, int64_t
                              const uint8_t* d_a3v, uint8_t* d_state, unsigned long long* counts) {
     const int32_t NT = s->n_traces;
     if (NT)
-        hipLaunchKernelGGL(k_ix_detect, dim3(cdiv(NT, DB)), dim3(DB), 0, ctx->stream, NT, s->tlen.p, s->tts.p, s->tte.p,
-                           s->tmaxd.p, s->sv_off.p, s->sv_op.p, s->sv_cnt.p, d_a3, d_a3v, t0, t1, d_state, counts);
+        hipLaunchKernelGGL(k_ix_detect, dim3(cdiv(NT, DB)), dim3(DB), 0, ctx->stream, NT,
+                           mr_detect_in(s, t0, t1, d_a3, d_a3v, d_state, counts));
     MR_TRY_HIP(ctx, hipGetLastError());
     return MR_OK;
 }

@@ -462,11 +462,14 @@ def test_windows_batch_matches_standalone(c3_window):
 
 
 def test_windows_batch_fast_paths_equal_general_paths(c3_window, monkeypatch):
-    """The window batch's fast paths -- both graphs built in one index pass (mr_ix_launch2) with
-    dense edge ids, prepared together (mr_graph_prepare_batch), set up in batched launches over
-    the group (pagerank_setup_batch) or over the window (mr_pagerank_presetup2) -- give the same
-    rankings as the one-graph-at-a-time paths (MR_NO_IX2 / MR_EDGE_HASH / MR_NO_PREP_BATCH /
-    MR_NO_SETUP_BATCH): top lists identical, scores within 1e-12, counts and edges equal."""
+    """The window batch's fast paths -- the detector fused into the index pass's first launch
+    (k_ix_detect_scan2), both graphs built in one index pass (mr_ix_launch2) with dense edge ids,
+    windows built in chunks and prepared together (mr_graph_prepare_batch), set up in batched
+    launches over the group (pagerank_setup_batch) or over the chunk (mr_pagerank_presetup_n) --
+    give the same rankings as the one-graph-at-a-time paths (MR_NO_IX2 / MR_EDGE_HASH /
+    MR_NO_PREP_BATCH / MR_NO_SETUP_BATCH): top lists identical, scores within 1e-12, counts and
+    edges equal; the separate detector launch (MR_NO_DET_FUSE) and one-window chunks
+    (MR_WIN_CHUNK=1) give bitwise the same results."""
     import bench
     from microrank_amd import _lib
     from microrank_amd.online_rca import rank_windows
@@ -485,11 +488,16 @@ def test_windows_batch_fast_paths_equal_general_paths(c3_window, monkeypatch):
         u0 = int(ab.tstart.min())
         wins.append((d, u0, u0 + 5 * 60 * 10**9, s3, sok))
     runs = {}
-    for mode in ("fast", "split0", "general"):
-        for k in ("MR_NO_IX2", "MR_EDGE_HASH", "MR_NO_PREP_BATCH", "MR_NO_SETUP_BATCH", "MR_WIN_SETUP_SPLIT"):
+    knobs = ("MR_NO_IX2", "MR_EDGE_HASH", "MR_NO_PREP_BATCH", "MR_NO_SETUP_BATCH", "MR_WIN_SETUP_SPLIT",
+             "MR_NO_DET_FUSE", "MR_WIN_CHUNK")
+    for mode in ("fast", "split0", "general", "nofuse_chunk1"):
+        for k in knobs:
             monkeypatch.delenv(k, raising=False)
-        if mode == "split0":   # every window sets its graphs up on its own stream (presetup2)
+        if mode == "split0":   # every chunk sets its graphs up on its own stream (presetup_n)
             monkeypatch.setenv("MR_WIN_SETUP_SPLIT", "0")
+        if mode == "nofuse_chunk1":
+            monkeypatch.setenv("MR_NO_DET_FUSE", "1")
+            monkeypatch.setenv("MR_WIN_CHUNK", "1")
         if mode == "general":
             for k in ("MR_NO_IX2", "MR_EDGE_HASH", "MR_NO_PREP_BATCH", "MR_NO_SETUP_BATCH"):
                 monkeypatch.setenv(k, "1")
@@ -500,6 +508,8 @@ def test_windows_batch_fast_paths_equal_general_paths(c3_window, monkeypatch):
             assert (a[2], a[3], a[4]) == (b[2], b[3], b[4]), mode
             assert list(a[0]) == list(b[0]), mode
             np.testing.assert_allclose(a[1], b[1], rtol=1e-12, atol=0)
+    for a, b in zip(runs["fast"], runs["nofuse_chunk1"]):
+        assert a[2:] == b[2:] and list(a[0]) == list(b[0]) and a[1].tobytes() == b[1].tobytes()
     for d in devs:
         d.close()
 
