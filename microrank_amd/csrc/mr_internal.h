@@ -8,6 +8,7 @@
 #include <map>
 #include <string>
 #include <utility>
+#include <memory>
 #include <vector>
 
 #include "../../include/microrank_hip.h"
@@ -187,6 +188,7 @@ struct mr_graph {
     std::vector<int64_t> tile_mult_h;   // per wave tile: the multiplicity its traces stand for
     DBuf<int32_t> krep;              // [T] class representative of each trace (when allocated)
     int64_t kc_kinds = 0;            // kinds of the last kind-compressed ranking (0: none)
+    std::unique_ptr<mr_graph> kc;    // the representatives' graph of a kind-compressed ranking, kept for the next call
     // mr_pagerank_presetup: kinds / preference / iteration state already set up for the next call
     bool pre_ok = false, pre_fp32 = false;
     int pre_anomaly = 0;

@@ -51,7 +51,7 @@ __global__ void k_pr_reset(int32_t T, int64_t cap, int32_t N, float* pref, float
     }
     if (i < cap) {
         hk[i] = 0ull;
-        cr[i] = KCnt{0u, -1};
+        cr[i] = KCnt{0u, 0x7fffffff};
     }
     if (i < 8) flag[i] = 0;
     if (i < 8) scal[i] = 0.0;
@@ -722,7 +722,7 @@ __device__ __forceinline__ void kind_insert_body(int32_t blk, const int64_t* off
     for (int i = threadIdx.x; i < KLDS; i += KB) {
         lkey[i] = 0ull;
         lcnt[i] = 0u;
-        lrep[i] = -1;
+        lrep[i] = 0x7fffffff;
     }
     const int32_t tb = blk * KB;
     const int32_t t = tb + threadIdx.x;
@@ -740,9 +740,11 @@ __device__ __forceinline__ void kind_insert_body(int32_t blk, const int64_t* off
             s = (s + 1) & (KLDS - 1);
         }
         atomicAdd(&lcnt[s], 1u);
-        if (atomicCAS(&lrep[s], -1, t) == -1 && CHK) lchk[s] = h2;
+        atomicMin(&lrep[s], t);   // the class's lowest trace of the block (deterministic)
         myslot = s;
     }
+    __syncthreads();
+    if (CHK && myslot >= 0 && lrep[myslot] == t) lchk[myslot] = h2;
     __syncthreads();
     for (int i = threadIdx.x; i < KLDS; i += KB) {
         const uint64_t h = lkey[i];
@@ -750,12 +752,11 @@ __device__ __forceinline__ void kind_insert_body(int32_t blk, const int64_t* off
         uint64_t slot = h & mask;
         for (;;) {
             const uint64_t k = atomicCAS(&hk[slot], 0ull, (unsigned long long)h);
-            if (k == 0) {   // the class's first block names its representative (read after this kernel)
-                cr[slot].rep = lrep[i];
-                if (CHK) chk[slot] = lchk[i];
+            if (k == 0 || k == h) {   // the representative: the class's lowest trace over the blocks
+                atomicMin(&cr[slot].rep, lrep[i]);   // (read after this kernel; deterministic)
+                if (k == 0 && CHK) chk[slot] = lchk[i];
                 break;
             }
-            if (k == h) break;
             slot = (slot + 1) & mask;
         }
         atomicAdd(&cr[slot].cnt, lcnt[i]);
@@ -1097,7 +1098,7 @@ __global__ void k_reset_init_b(const SDev* __restrict__ sd, int32_t ng) {
     }
     if (i < G.cap) {
         G.hk[i] = 0ull;
-        G.cr[i] = KCnt{0u, -1};
+        G.cr[i] = KCnt{0u, 0x7fffffff};
     }
     if (i < 8) G.flag[i] = 0;
     if (i < 8) G.scal[i] = 0.0;
@@ -1217,7 +1218,7 @@ __global__ void k_pr_reset_init(int32_t T, int64_t cap, int32_t N, float* pref, 
     }
     if (i < cap) {
         hk[i] = 0ull;
-        cr[i] = KCnt{0u, -1};
+        cr[i] = KCnt{0u, 0x7fffffff};
     }
     if (i < 8) flag[i] = 0;
     if (i < 8) scal[i] = 0.0;
@@ -4238,6 +4239,19 @@ static int kind_compressed_pagerank(mr_ctx* ctx, mr_graph* g, int anomaly, doubl
         return mr_pagerank_batch_impl(ctx, &g, &anomaly, 1, d, alpha, iters, precision, plain);
     MR_TRY_HIP(ctx, hipSetDevice(ctx->device));
     hipStream_t st = ctx->stream;
+    // the representatives' graph depends on g's structure only (built, never changed): a later call
+    // ranks the kept one (its preference and iteration state are set up per call as usual).
+    // MR_KC_NOCACHE: rebuild every call (read per call)
+    auto rank_kc = [&](mr_graph* gcp) -> int {
+        MR_TRY(mr_pagerank_batch_impl(ctx, &gcp, &anomaly, 1, d, alpha, iters, precision, plain));
+        MR_TRY(g->weight.alloc(ctx, (size_t)N));
+        MR_TRY(g->sn.alloc(ctx, (size_t)N));
+        MR_TRY_HIP(ctx, hipMemcpyAsync(g->weight.p, gcp->weight.p, (size_t)N * 8, hipMemcpyDeviceToDevice, st));
+        MR_TRY_HIP(ctx, hipMemcpyAsync(g->sn.p, gcp->sn.p, (size_t)N * 8, hipMemcpyDeviceToDevice, st));
+        return MR_OK;
+    };
+    if (g->kc && getenv("MR_KC_NOCACHE") == nullptr) return rank_kc(g->kc.get());
+    g->kc.reset();
     // ---- kinds with representatives (the seed sequence of mr_pagerank_batch_impl)
     uint64_t cap = 1;
     while (cap < 2ull * (uint64_t)T) cap <<= 1;
@@ -4327,14 +4341,9 @@ static int kind_compressed_pagerank(mr_ctx* ctx, mr_graph* g, int anomaly, doubl
     MR_TRY_HIP(ctx, hipMemcpyAsync(gc->kind.p, gc->mult.p, (size_t)K * 8, hipMemcpyDeviceToDevice, st));
     MR_TRY_HIP(ctx, hipStreamSynchronize(st));
     gc->kinds_given = true;
-    mr_graph* gcp = gc.get();
-    MR_TRY(mr_pagerank_batch_impl(ctx, &gcp, &anomaly, 1, d, alpha, iters, precision, plain));
-    MR_TRY(g->weight.alloc(ctx, (size_t)N));
-    MR_TRY(g->sn.alloc(ctx, (size_t)N));
-    MR_TRY_HIP(ctx, hipMemcpyAsync(g->weight.p, gc->weight.p, (size_t)N * 8, hipMemcpyDeviceToDevice, st));
-    MR_TRY_HIP(ctx, hipMemcpyAsync(g->sn.p, gc->sn.p, (size_t)N * 8, hipMemcpyDeviceToDevice, st));
-    MR_TRY_HIP(ctx, hipStreamSynchronize(st));   // gc's buffers return to the pool
+    MR_TRY(rank_kc(gc.get()));
     g->kc_kinds = K;
+    g->kc = std::move(gc);
     return MR_OK;
 }
 

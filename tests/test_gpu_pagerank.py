@@ -306,6 +306,18 @@ def test_kind_compressed_c2_matches_uncompressed(c2, anomaly, part_min, monkeypa
     np.testing.assert_array_equal(k1, k0)
     np.testing.assert_allclose(w1, w0, rtol=1e-10, atol=0)
     assert (1.0 / k0).sum() < 0.6 * g.T   # the C2 window repeats call paths (113k kinds of 200k traces)
+    # a later call ranks the kept representatives' graph: with the other preference as well, bitwise
+    # the same as a call that rebuilds it (MR_KC_NOCACHE), and within 1e-10 of the uncompressed one
+    dg.pagerank(not anomaly, compress_kinds=True)
+    w2, _ = dg.fetch()
+    monkeypatch.setenv("MR_KC_NOCACHE", "1")
+    dg.pagerank(not anomaly, compress_kinds=True)
+    w3, _ = dg.fetch()
+    monkeypatch.delenv("MR_KC_NOCACHE")
+    assert w2.tobytes() == w3.tobytes()
+    dg.pagerank(not anomaly)
+    w4, _ = dg.fetch()
+    np.testing.assert_allclose(w2, w4, rtol=1e-10, atol=0)
     dg.close()
 
 
