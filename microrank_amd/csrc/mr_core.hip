@@ -74,6 +74,7 @@ static size_t pool_round(size_t b) {
 
 void* mr_pool_alloc(mr_ctx* ctx, size_t bytes) {
     const size_t want = pool_round(bytes);
+    std::lock_guard<std::mutex> lk(ctx->pool_mu);
     auto it = ctx->pool_free.lower_bound(want);
     if (it != ctx->pool_free.end() && it->first <= 2 * want) {   // reuse a block at most 2x too big
         void* p = it->second;
@@ -99,6 +100,7 @@ void* mr_pool_alloc(mr_ctx* ctx, size_t bytes) {
 
 void mr_pool_free(mr_ctx* ctx, void* p) {
     if (!ctx || !p) return;
+    std::lock_guard<std::mutex> lk(ctx->pool_mu);
     auto it = ctx->pool_live.find(p);
     if (it == ctx->pool_live.end()) return;
     ctx->pool_free.emplace(it->second, p);   // stream-ordered reuse: no sync needed
@@ -124,6 +126,7 @@ int mr_read_words(mr_ctx* ctx, const int64_t* dev, int n, int64_t* out) {
 
 void mr_pool_release(mr_ctx* ctx) {
     (void)hipStreamSynchronize(ctx->stream);
+    std::lock_guard<std::mutex> lk(ctx->pool_mu);
     for (auto& kv : ctx->pool_free) (void)hipFree(kv.second);
     ctx->pool_free.clear();
 }
@@ -192,6 +195,8 @@ extern "C" void mr_ctx_destroy(mr_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
     if (ctx->side) (void)hipStreamSynchronize(ctx->side);
+    for (mr_graph* g : ctx->graveyard) delete g;   // (their blocks belong to the auxiliary contexts too)
+    ctx->graveyard.clear();
     for (mr_ctx* a : ctx->aux) mr_ctx_destroy(a);
     ctx->aux.clear();
     {   // the context's live handles go first (their buffers return to its pool)

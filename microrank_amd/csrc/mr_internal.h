@@ -9,6 +9,7 @@
 #include <string>
 #include <utility>
 #include <memory>
+#include <mutex>
 #include <vector>
 
 #include "../../include/microrank_hip.h"
@@ -34,12 +35,16 @@ struct mr_ctx {
     // stream-ordered caching allocator: every buffer of this context is used on `stream` only,
     // so a block released by one call can be handed to the next without a hipFree/hipMalloc
     // (each of which synchronises the device and costs tens of microseconds)
+    std::mutex pool_mu;   // (mr_windows_batch releases a call's graphs while its threads allocate)
     std::multimap<size_t, void*> pool_free;
     std::map<void*, size_t> pool_live;
     size_t pool_bytes = 0;
     // mr_windows_batch: auxiliary contexts (own stream + pool) for the windows' concurrent
     // detector / graph-build / spectrum phases; created on first use, destroyed with this one
     std::vector<mr_ctx*> aux;
+    // mr_windows_batch: the previous call's window graphs, released by the next call while its
+    // PageRank stream waits for the first group's builds (or by mr_ctx_destroy)
+    std::vector<struct mr_graph*> graveyard;
     // a second stream for work that overlaps the main stream inside one call (wide graphs:
     // k_cold_ops beside k_cold_trace / k_tr_a), joined back by events; created on first use
     hipStream_t side = nullptr;

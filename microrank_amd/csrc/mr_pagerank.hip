@@ -18,6 +18,7 @@
 // sum_t w_t (r'_t / M_r) is evaluated as (sum_t w_t r'_t) / M_r.  Every float reduction has a
 // fixed order (no float atomics), so results are bitwise reproducible run to run.
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -3793,10 +3794,28 @@ static double iter_bytes(const mr_graph* g, bool fp32) {
 
 // one attempt with kind-hash seed `seed`; *collided reports a 64-bit key collision found by the
 // exact verification (k_kind_verify / k_sh_kind_check), after which the caller retries
+// MR_PR_HOST_TIMING: host wall time of pagerank_attempt's phases (no syncs added; diagnostics only)
+struct HostMarks {
+    bool on = getenv("MR_PR_HOST_TIMING") != nullptr;
+    int ng;
+    std::vector<std::pair<const char*, std::chrono::steady_clock::time_point>> m;
+    explicit HostMarks(int n) : ng(n) { mark("start"); }
+    void mark(const char* name) {
+        if (on) m.emplace_back(name, std::chrono::steady_clock::now());
+    }
+    ~HostMarks() {
+        if (m.size() < 2) return;
+        fprintf(stderr, "[pagerank host ng=%d]", ng);
+        for (size_t i = 1; i < m.size(); ++i)
+            fprintf(stderr, " %s %.1f", m[i].first, std::chrono::duration<double, std::micro>(m[i].second - m[i - 1].second).count());
+        fprintf(stderr, " us\n");
+    }
+};
 static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly, int ng, double d, double alpha,
                             int iters, int precision, uint32_t flags, bool sharded, uint64_t seed, uint64_t hmask,
                             bool* collided) {
     *collided = false;
+    HostMarks hm(ng);
     if (!ctx || ng <= 0 || !gs || !anomaly) return mr_fail(ctx, MR_ERR_ARG, "mr_pagerank: bad arguments");
     if (iters < 0) return mr_fail(ctx, MR_ERR_ARG, "iters < 0");
     for (int i = 0; i < ng; ++i) {
@@ -3839,6 +3858,7 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
                 MR_TRY(pagerank_setup(ctx, need[j], need_a[j], d, fp32, flags, plan.tr, sharded, seed, hmask));
         }
     }
+    hm.mark("setup");
     int64_t wsum = 0;   // wave tiles of the launch's fused graphs (k_tr_a's block budget)
     for (int i = 0; i < ng; ++i)
         if (gs[i]->fused) wsum += gs[i]->n_wt;
@@ -3851,6 +3871,7 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
             MR_TRY(g->fx_part.alloc(ctx, (size_t)std::max<int64_t>(nfa, 1) * (size_t)kern_n(g)));
         }
     }
+    hm.mark("blocks");
     for (size_t c0 = 0; c0 < cuts.size(); c0 += TC_BATCH) {
         CutBatch cb;
         const size_t n = std::min<size_t>(TC_BATCH, cuts.size() - c0);
@@ -3999,6 +4020,7 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         for (auto& v : hv) v.stamp = dstamp.p;
     }
     DBuf<GDev> dv;
+    hm.mark("descr");
     MR_TRY(dv.upload(ctx, hv.data(), hv.size()));
     const int32_t split_fa = ng == 2 ? hv[1].blk0f : 0, split_fb = ng == 2 ? hv[1].blk0fb : 0;
     const int fx_S = fx_s(multi);
@@ -4032,6 +4054,7 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         }
         sst = ctx->side;
     }
+    hm.mark("pre-loop");
     for (int it = 0; it < iters; ++it) {
         mr_prof_begin(ctx);
         if (any_wide && sst != st) {
@@ -4101,6 +4124,7 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
     // MAX first, below, so it reads them after that)
     DBuf<int32_t> fl;
     MR_TRY(fl.alloc(ctx, (size_t)4 * ng));
+    hm.mark("loop");
     hipLaunchKernelGGL(k_weights_batch, dim3(ng), dim3(1024), 0, st, dv.p, iters, (int)((flags & MR_PR_EXACT_SUMS) != 0),
                        fl.p);
     MR_DEBUG_CHECK(ctx, "k_weights");
