@@ -246,7 +246,9 @@ int mr_rca_window(mr_ctx* ctx, const mr_spans* s, int64_t t0, int64_t t1, const 
  * out_podop / out_score[i * (top_max + 6) ..], n_out[i], edges_traversed[i], n_abnormal[i],
  * n_normal[i], status[i] (MR_OK, or MR_ERR_VALUE for an empty window -- the reference's
  * unpack of False, T2).  Replaces a loop of online_anomaly_detect_RCA windows
- * (online_rca.py:161-216) over independent windows. */
+ * (online_rca.py:161-216) over independent windows.  Device memory: the graphs of large windows
+ * (>= 64k traces on average) stay in the context's pools until the next call on it (released
+ * there beside the new builds) or mr_ctx_destroy. */
 int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* const* spans, const int64_t* t0,
                      const int64_t* t1, const double* const* a3, const uint8_t* const* a3_valid, int method,
                      int32_t top_max, int precision, int32_t* out_podop, double* out_score, int32_t* n_out,

@@ -77,19 +77,21 @@ void* mr_pool_alloc(mr_ctx* ctx, size_t bytes) {
     std::lock_guard<std::mutex> lk(ctx->pool_mu);
     auto it = ctx->pool_free.lower_bound(want);
     if (it != ctx->pool_free.end() && it->first <= 2 * want) {   // reuse a block at most 2x too big
-        void* p = it->second;
+        void* p = it->second.back();   // (a class is erased when it empties: never empty here)
         ctx->pool_live[p] = it->first;
-        ctx->pool_free.erase(it);
+        it->second.pop_back();
+        if (it->second.empty()) ctx->pool_free.erase(it);
         return p;
     }
     void* p = nullptr;
     if (hipMalloc(&p, want) != hipSuccess) {
         // give the cached blocks back and retry once
         (void)hipStreamSynchronize(ctx->stream);
-        for (auto& kv : ctx->pool_free) {
-            (void)hipFree(kv.second);
-            ctx->pool_bytes -= kv.first;
-        }
+        for (auto& kv : ctx->pool_free)
+            for (void* q : kv.second) {
+                (void)hipFree(q);
+                ctx->pool_bytes -= kv.first;
+            }
         ctx->pool_free.clear();
         if (hipMalloc(&p, want) != hipSuccess) return nullptr;
     }
@@ -103,7 +105,7 @@ void mr_pool_free(mr_ctx* ctx, void* p) {
     std::lock_guard<std::mutex> lk(ctx->pool_mu);
     auto it = ctx->pool_live.find(p);
     if (it == ctx->pool_live.end()) return;
-    ctx->pool_free.emplace(it->second, p);   // stream-ordered reuse: no sync needed
+    ctx->pool_free[it->second].push_back(p);   // stream-ordered reuse: no sync needed
     ctx->pool_live.erase(it);
 }
 
@@ -127,7 +129,8 @@ int mr_read_words(mr_ctx* ctx, const int64_t* dev, int n, int64_t* out) {
 void mr_pool_release(mr_ctx* ctx) {
     (void)hipStreamSynchronize(ctx->stream);
     std::lock_guard<std::mutex> lk(ctx->pool_mu);
-    for (auto& kv : ctx->pool_free) (void)hipFree(kv.second);
+    for (auto& kv : ctx->pool_free)
+        for (void* q : kv.second) (void)hipFree(q);
     ctx->pool_free.clear();
 }
 

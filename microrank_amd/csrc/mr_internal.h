@@ -7,6 +7,7 @@
 #include <cstdio>
 #include <map>
 #include <string>
+#include <unordered_map>
 #include <utility>
 #include <memory>
 #include <mutex>
@@ -36,8 +37,10 @@ struct mr_ctx {
     // so a block released by one call can be handed to the next without a hipFree/hipMalloc
     // (each of which synchronises the device and costs tens of microseconds)
     std::mutex pool_mu;   // (mr_windows_batch releases a call's graphs while its threads allocate)
-    std::multimap<size_t, void*> pool_free;
-    std::map<void*, size_t> pool_live;
+    // (free blocks as one stack per size class -- a free is a push, no node allocation; live
+    // blocks hashed: a window batch releases thousands of blocks on the host's critical path)
+    std::map<size_t, std::vector<void*>> pool_free;
+    std::unordered_map<void*, size_t> pool_live;
     size_t pool_bytes = 0;
     // mr_windows_batch: auxiliary contexts (own stream + pool) for the windows' concurrent
     // detector / graph-build / spectrum phases; created on first use, destroyed with this one
