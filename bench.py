@@ -20,7 +20,7 @@ no collective on the data path -> "scaling": "weak".
 value = edges traversed by all PageRank iterations of all ranks (25 * (2 nnz + E_c) per graph)
 / max-over-ranks wall time of the K steps  [GTEPS].  Every other part of the window (detector,
 graph builds, spectrum) is inside that time.  windows_per_s is reported beside it.
-roofline: one power iteration (the k_fx_a + k_fx_b launch pair), algorithmic bytes (SURVEY §8(d)
+roofline: one power iteration (the k_tr_a + k_fx_b launch pair), algorithmic bytes (SURVEY §8(d)
 B_iter, both graphs of the window) over its live HIP-event duration on the library's stream;
 traffic = FETCH_SIZE (x2, gfx950) + WRITE_SIZE of the same launches per iteration from two
 rocprofv3 --pmc child runs made before this process touches the GPU (--no-traffic skips them).
@@ -51,6 +51,36 @@ def make_window(seed: int, n_ops: int, n_traces: int):
     for st in (normal, abnormal):
         st.trace_names = None
     return topo, normal, abnormal
+
+
+def _c2_abnormal(job):
+    """One distinct C2 window's spans (process-pool worker): the shared topology, its own seed."""
+    from microrank_amd import synth
+
+    topo, n_traces, seed = job
+    st = synth.gen_spans(topo, n_traces, seed, branch=1.9, p_max=0.8, fault_op=synth.fault_op_of(topo),
+                         fault_frac=0.4, fault_ms=6000.0, names=False)
+    st.trace_names = None
+    st.meta = {}
+    return st
+
+
+def c2_windows(n: int, n_ops: int, n_traces: int, rank: int):
+    """n DISTINCT C2 windows of one system (BASELINE configs[1]: 1k ops / 200k traces each): one
+    topology and normal SLO period, each window's traffic from its own seed (a 5-minute window of a
+    different time).  Generated in a process pool before this process touches the GPU.  Returns
+    (normal SpanTable, [abnormal SpanTable] * n)."""
+    from concurrent.futures import ProcessPoolExecutor
+
+    seed = 1234 + 7919 * rank
+    topo, normal, first = make_window(seed, n_ops, n_traces)
+    jobs = [(topo, n_traces, seed + 2 + 104729 * i) for i in range(1, n)]
+    threads, _ = host_cores()
+    if not jobs:
+        return normal, [first]
+    with ProcessPoolExecutor(max_workers=max(1, min(16, threads, len(jobs)))) as ex:
+        rest = list(ex.map(_c2_abnormal, jobs))
+    return normal, [first] + rest
 
 
 def slo_from_gpu(ctx, normal):
@@ -86,7 +116,7 @@ def run_window(ctx, dev, t0, t1, a3, ok, prec):
     return edges.value, codes[:n_out.value].copy(), scores[:n_out.value].copy(), na.value, nn.value
 
 
-ITER_KERNELS = ("k_tr_a", "k_wv_a", "k_fx_a", "k_fx_b", "k_iter_a", "k_iter_b", "k_cold_trace", "k_cold_ops")
+ITER_KERNELS = ("k_tr_a", "k_fx_b", "k_iter_a", "k_iter_b", "k_cold_trace", "k_cold_ops")
 
 
 def kind_compressed_probe(ctx, dev, t0, t1, a3, ok, reps=5):
@@ -137,7 +167,7 @@ def kind_compressed_probe(ctx, dev, t0, t1, a3, ok, reps=5):
 
 
 def pmc_traffic(args, timeout_s=240):
-    """HBM bytes per power iteration (all kernels of one iteration: k_fx_a + k_fx_b, or the tile
+    """HBM bytes per power iteration (all kernels of one iteration: k_tr_a + k_fx_b, or the tile
     path's k_iter_a + k_iter_b) from two rocprofv3 --pmc child runs of this bench (FETCH_SIZE and
     WRITE_SIZE in separate passes, MI355X_MICROARCH.md 'HBM': FETCH_SIZE reads half the bytes of
     wide streaming loads on gfx950 -> x2).  Child processes only: this process has not touched
@@ -173,7 +203,7 @@ def pmc_traffic(args, timeout_s=240):
                     name = r["Kernel_Name"]
                     if r["Counter_Name"] == ctr and any(k in name for k in ITER_KERNELS):
                         per_iter += float(r["Counter_Value"])
-                        n_a += any(k in name for k in ("k_tr_a", "k_wv_a", "k_fx_a", "k_iter_a"))
+                        n_a += any(k in name for k in ("k_tr_a", "k_iter_a"))
             if n_a == 0:
                 return None
             vals[ctr] = per_iter / n_a * 1024.0   # KB -> bytes, per iteration
@@ -219,34 +249,30 @@ def cpu_baseline(abnormal, t0, t1, a3, ok, target_s=10.0, one_core_s=8.0):
             "one_core": {"value": round(edges1 / el1 / 1e9, 4), "windows_per_s": round(n1 / el1, 4), "cores": 1}}, res
 
 
-def c4_cpu_baseline(n_ops, n_traces, target_s=15.0):
-    """25 power iterations of a C4-shaped graph of n_traces traces on the host: the oracle's numpy
-    restatement (bincount SpMV per product), one core.  Preference = uniform (the iteration cost
-    does not depend on it); kinds are not part of this timing."""
+def c4_cpu_baseline(hg, anomaly=True, one_core_iters=2):
+    """SURVEY 8(d) CPU baseline of a C4 / C5 step on the same graph the GPU ranks: the C restatement
+    (oracle/mr_oracle.c oracle_incidence_pagerank: kinds by column hash + exact check, preference,
+    25 OpenMP power iterations, weights) on every core this process may use, one whole
+    trace_pagerank; on one core, kinds + preference and `one_core_iters` iterations, the 25-iteration
+    time extrapolated from them (a bounded sample).  GTEPS = 25 (2 nnz + E) / time, as the GPU line."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
-    import oracle as orc
+    import c_oracle
 
-    from microrank_amd import synth
-
-    hg = synth.big_graph(n_ops, n_traces, seed=5)
-    T, N = hg.T, hg.N
-    sr_t = np.repeat(np.arange(T, dtype=np.int64), np.diff(hg.sr_off))
-    sr_o = hg.sr_ops.astype(np.int64)
-    ss_c = np.repeat(np.arange(N, dtype=np.int64), np.diff(hg.ss_off))
-    g = orc.Graph(list(range(N)), list(range(T)), sr_t, sr_o, sr_t, sr_o, hg.len_t, hg.len_o, ss_c,
-                  hg.ss_par.astype(np.int64), hg.nchild, np.arange(T), hg.len_t.copy())
-    v = np.full(T, 1.0 / T, np.float32)
-    n, edges, t_start = 0, 0, time.perf_counter()
-    while True:
-        orc.power_iteration(g, v)
-        n += 1
-        edges += 25 * (2 * sr_o.size + ss_c.size)
-        el = time.perf_counter() - t_start
-        if el >= target_s or n >= 5:
-            break
-    return {"value": round(edges / el / 1e9, 4), "unit": "GTEPS", "cores": 1, "kind": "port",
-            "sample": f"{n} x 25 power iterations of a {T}-trace / {N}-op graph (same generator), "
-                      f"oracle numpy restatement, {el:.1f} s"}
+    threads, machine = host_cores()
+    edges = 25.0 * (2.0 * float(hg.sr_ops.size) + float(hg.ss_par.size))
+    ts = time.perf_counter()
+    _, _, tp = c_oracle.incidence_pagerank(hg, anomaly, 25, nthreads=threads)
+    t_all = tp[0] + tp[1]
+    el = time.perf_counter() - ts
+    _, _, tp1 = c_oracle.incidence_pagerank(hg, anomaly, one_core_iters, nthreads=1)
+    t_one = tp1[0] + tp1[1] * 25.0 / one_core_iters
+    return {"value": round(edges / t_all / 1e9, 4), "unit": "GTEPS", "cores": threads, "kind": "port",
+            "sample": f"one whole trace_pagerank of this graph ({hg.T} traces / {hg.N} ops: kinds + preference "
+                      f"{tp[0]:.2f} s, 25 iterations + weights {tp[1]:.2f} s) by oracle/mr_oracle.c on {threads} "
+                      f"OpenMP threads ({el:.1f} s wall incl. the op-major copy); one core: kinds + preference "
+                      f"{tp1[0]:.2f} s + {one_core_iters} iterations {tp1[1]:.2f} s, extrapolated to 25",
+            "ms_per_step": round(t_all * 1e3, 1), "nproc": machine,
+            "one_core": {"value": round(edges / t_one / 1e9, 4), "cores": 1, "ms_per_step_est": round(t_one * 1e3, 1)}}
 
 
 def run_c4(args, world, rank, dist):
@@ -258,7 +284,9 @@ def run_c4(args, world, rank, dist):
     from microrank_amd import _lib, shard, synth
     from microrank_amd.graph import DeviceGraph
 
-    t_local = args.c4_traces // world + (1 if rank < args.c4_traces % world else 0)
+    # --shard-of K at N = 1: this GPU holds rank 0's share of a K-rank deployment
+    sw, sr = (world, rank) if world > 1 else (max(1, args.shard_of), 0)
+    t_local = args.c4_traces // sw + (1 if sr < args.c4_traces % sw else 0)
     t_gen = time.perf_counter()
     ctx = _lib.default_context()
     if world > 1:
@@ -275,7 +303,7 @@ def run_c4(args, world, rank, dist):
         # cross-rank parent joins over the collectives) and ranks it
         from microrank_amd.preprocess_data import DeviceSpans
 
-        st = synth.big_spans(args.c4_ops, args.c4_traces, seed=11, shard=(rank, world))
+        st = synth.big_spans(args.c4_ops, args.c4_traces, seed=11, shard=(sr, sw))
         print(f"[bench] rank {rank}: generated {t_local} traces / {st.n_spans} spans in "
               f"{time.perf_counter() - t_gen:.1f} s", file=sys.stderr, flush=True)
         dev = DeviceSpans(ctx, st)
@@ -288,7 +316,8 @@ def run_c4(args, world, rank, dist):
         print(f"[bench] rank {rank}: generated {t_local} traces / {hg.sr_ops.size} pairs in "
               f"{time.perf_counter() - t_gen:.1f} s", file=sys.stderr, flush=True)
         dg = DeviceGraph.upload(ctx, hg)
-        del hg
+        if world > 1 or args.no_cpu:
+            del hg   # (kept on rank 0 at N = 1: the CPU baseline ranks the same graph)
     build_s = [0.0]
 
     def step():
@@ -345,7 +374,9 @@ def run_c4(args, world, rank, dist):
         "config": {"workload": f"{args.config.upper()} sharded "
                                + ("K1 graph build from span shards + " if dev is not None else "")
                                + f"trace_pagerank: {args.c4_ops} ops / {args.c4_traces} "
-                               f"traces over {world} GPU(s), anomaly preference, 25 iterations", "nnz": int(nnz_all),
+                               f"traces over {world} GPU(s), anomaly preference, 25 iterations"
+                               + (f"; this GPU: rank 0's share of {sw} ({t_local} traces)" if sw != world else ""),
+                   "nnz": int(nnz_all),
                    "call_edges": E,
                    "parallelism": f"trace shards x{world}, RCCL " + ("limb" if fused else "fp64 op-sum")
                                   + " all-reduce per iteration"},
@@ -363,9 +394,9 @@ def run_c4(args, world, rank, dist):
                        "5% broken traces, 1% duplicated root spanIDs across ranks), int-coded, resident in HBM")
         out["config"]["n_spans_rank0"] = int(n_spans_local)
         out["build_ms"] = round(build_s[0] / args.steps * 1e3, 3)   # rank 0's K1 share of a step
-    if not args.no_cpu and world == 1:
+    if not args.no_cpu and world == 1 and dev is None:
         try:
-            out["cpu_baseline"] = c4_cpu_baseline(args.c4_ops, 1_000_000)
+            out["cpu_baseline"] = c4_cpu_baseline(hg)
         except Exception as e:
             out["cpu_baseline"] = {"value": None, "error": f"{type(e).__name__}: {e}"}
     return out
@@ -465,6 +496,70 @@ def run_sweep(args):
             "sliding": {"what": "every 1-minute window start of the stream ranked (mr_windows_batch, 64 per call, "
                                 "one resident table)", "windows": len(wins), "ranked": n_ok,
                         "windows_per_s": round(len(wins) / dt_slide, 2)}}
+
+
+def run_dropin(args):
+    """The north star's drop-in path, measured: the reference driver's window body
+    (online_rca.py:167-201 -- system_anomaly_detect, get_pagerank_graph + trace_pagerank twice,
+    calculate_spectrum_without_delay_list, the prints and result.csv) through the swapped imports
+    (microrank_amd's drop-in modules, called on the reference's DataFrame exactly as the unchanged
+    driver calls them: microrank_amd.online_rca._window_loop is that loop), at C1 and C2.  A step is
+    one window on a resident DataFrame (its device span table cached after the first call); the
+    reference's own C1 number is 0.43 windows/s (measured in the dev container)."""
+    import contextlib
+    import io
+    import tempfile
+
+    import pandas as pd
+
+    from microrank_amd import synth
+    from microrank_amd.online_rca import _window_loop
+    from microrank_amd.preprocess_data import get_operation_slo, get_service_operation_list
+
+    sizes = {"C1": (40, 2000, 100), "C2": (args.ops, args.traces, 1234)}
+    lines = {}
+    cwd = os.getcwd()
+    with tempfile.TemporaryDirectory(dir="/tmp") as td:
+        os.chdir(td)
+        try:
+            for name, (n_ops, n_tr, seed) in sizes.items():
+                t_gen = time.perf_counter()
+                ndf, adf = synth.window_dataframes(n_ops, n_tr, seed, branch=1.9, p_max=0.8, fault_ms=6000.0)
+                print(f"[bench] dropin {name}: {len(adf)} spans generated in {time.perf_counter() - t_gen:.1f} s",
+                      file=sys.stderr, flush=True)
+                op_list = get_service_operation_list(ndf)
+                slo = get_operation_slo(op_list, ndf)
+                start = adf["startTime"].min()
+                one = start + pd.Timedelta(1, unit="ns")   # the loop runs exactly the window at `start`
+                sink = io.StringIO()
+                ts = time.perf_counter()
+                with contextlib.redirect_stdout(sink):
+                    _window_loop(adf, slo, op_list, start, one)   # first call: ingests the DataFrame
+                first_ms = (time.perf_counter() - ts) * 1e3
+                ranked = "normal_list" in sink.getvalue()
+                n = max(1, args.steps)
+                ts = time.perf_counter()
+                for _ in range(n):
+                    with contextlib.redirect_stdout(io.StringIO()):
+                        _window_loop(adf, slo, op_list, start, one)
+                dt = (time.perf_counter() - ts) / n
+                lines[name] = {"windows_per_s": round(1.0 / dt, 3), "ms_per_window": round(dt * 1e3, 3),
+                               "first_window_ms": round(first_ms, 1), "ranked": ranked,
+                               "spans": int(len(adf)), "traces": int(adf["traceID"].nunique()), "ops": n_ops}
+                del ndf, adf
+        finally:
+            os.chdir(cwd)
+    c1 = lines["C1"]["windows_per_s"]
+    return {"metric": "drop-in RCA windows/sec through the reference driver's call sequence (north star)",
+            "value": lines["C2"]["windows_per_s"], "unit": "windows/s", "n_gpus": 1, "steps": args.steps,
+            "warmup": 1, "ms_per_step": lines["C2"]["ms_per_window"], "higher_is_better": True, "scaling": "none",
+            "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic reference-schema DataFrames (strings), resident in host memory; device span table "
+                    "cached per DataFrame after the first call",
+            "config": {"workload": "online_rca.py:167-201 window body via the swapped imports, C2 (C1 beside)",
+                       "C1": lines["C1"], "C2": lines["C2"]},
+            "reference_cpu": {"C1_windows_per_s": 0.43, "source": "BASELINE.md / SURVEY 6 (reference Python, 1 core)",
+                              "speedup_C1": round(c1 / 0.43, 1)}}
 
 
 def plan_starts(t_begin, t_end, grain=60 * 10**9):
@@ -571,11 +666,12 @@ def main():
     ap.add_argument("--streams-mode", action="store_true",
                     help="c2/c3: W contexts + W host threads, one mr_rca_window per window (instead of mr_windows_batch)")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
-    ap.add_argument("--config", choices=["c2", "c3", "c4", "c5", "sweep", "ingest"], default="c2",
+    ap.add_argument("--config", choices=["c2", "c3", "c4", "c5", "sweep", "ingest", "dropin"], default="c2",
                     help="c2: RCA windows (default, weak scaling); c3: a batch of --c3-windows 500-op / 20k-trace "
                          "windows split over the ranks (strong scaling); c4 / c5: one trace-sharded graph (strong "
                          "scaling; c5 = 100k ops / 100M traces fp32, the wide fused iteration); sweep: the driver's "
-                         "window sweep over a long stream (f3); ingest: strings -> device span table (f2)")
+                         "window sweep over a long stream (f3); ingest: strings -> device span table (f2); "
+                         "dropin: the reference driver's window body through the drop-in modules (C1, C2)")
     ap.add_argument("--sweep-minutes", type=float, default=240.0, help="sweep: minutes of traffic in the stream")
     ap.add_argument("--sweep-fault", type=float, default=0.00005, help="sweep: fraction of traces hit by the fault")
     ap.add_argument("--c3-windows", type=int, default=4096, help="c3: windows in the whole batch (all ranks)")
@@ -584,7 +680,12 @@ def main():
     ap.add_argument("--c4-ops", type=int, default=None, help="c4/c5 op count (default 10k / 100k)")
     ap.add_argument("--c4-traces", type=int, default=None, help="c4/c5 trace count over all ranks (10M / 100M)")
     ap.add_argument("--from-spans", action="store_true",
-                    help="c4: each rank holds a span shard and a step includes the K1 graph build (mr_graph_build_sharded)")
+                    help="c4/c5: each rank holds a span shard and a step includes the K1 graph build (mr_graph_build_sharded)")
+    ap.add_argument("--shard-of", type=int, default=1,
+                    help="c4/c5 --from-spans at N=1: rank 0's share of a K-GPU deployment (c5: 12.5M of the 100M traces "
+                         "at K=8), built and ranked on this GPU")
+    ap.add_argument("--c2-distinct", type=int, default=None,
+                    help="c2: distinct seeded windows per step (default: every window of the step distinct)")
     args = ap.parse_args()
     if args.streams is None:
         # c3: a 4096-window batch in calls of 256 (measured: 64 -> 7.7k, 256 -> 9.0k windows/s; a
@@ -608,7 +709,7 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # PMC passes first, in child processes, before this process initialises the GPU
     traffic = None
-    if world == 1 and not args.pmc_child and not args.no_traffic and args.config not in ("sweep", "ingest"):
+    if world == 1 and not args.pmc_child and not args.no_traffic and args.config not in ("sweep", "ingest", "dropin"):
         traffic = pmc_traffic(args, timeout_s=240 if args.config in ("c2", "c3") else 400)
     dist = None
     if world > 1:
@@ -616,12 +717,12 @@ def main():
 
         dist.init_process_group("gloo")
     os.environ.setdefault("MICRORANK_DEVICE", str(local))
-    if args.config in ("sweep", "ingest"):   # single-GPU supplementary lines (f2 / f3)
-        if args.config == "ingest" and "--steps" not in sys.argv:
+    if args.config in ("sweep", "ingest", "dropin"):   # single-GPU supplementary lines (f2 / f3 / drop-in)
+        if args.config in ("ingest", "dropin") and "--steps" not in sys.argv:
             args.steps, args.warmup = 5, 1
         if args.config == "sweep" and "--steps" not in sys.argv:
             args.steps, args.warmup = 3, 1
-        out = (run_sweep if args.config == "sweep" else run_ingest)(args)
+        out = {"sweep": run_sweep, "ingest": run_ingest, "dropin": run_dropin}[args.config](args)
         print(json.dumps(out), flush=True)
         return
     if args.config in ("c4", "c5"):
@@ -647,16 +748,34 @@ def main():
     W = max(1, args.streams)
     dev_id = int(os.environ["MICRORANK_DEVICE"])
     batch = not args.streams_mode
+    c2_tabs = None
+    if batch and args.config == "c2":   # distinct windows, generated before the GPU is touched
+        nd = W if args.c2_distinct is None else max(1, min(W, args.c2_distinct))
+        t_gen = time.perf_counter()
+        c2_tabs = c2_windows(nd, args.ops, args.traces, rank)
+        print(f"[bench] rank {rank}: {nd} distinct C2 windows generated in {time.perf_counter() - t_gen:.1f} s",
+              file=sys.stderr, flush=True)
     # batch (default): one context; a step is ONE mr_windows_batch call over W windows (their
     # detectors / builds / spectra on the library's auxiliary streams, their PageRanks sharing
     # each iteration's launches).  --streams-mode: W contexts driven by W host threads, one
     # mr_rca_window call per window (round-1 design, kept for A/B).
     ctxs = [_lib.default_context()] + ([] if batch else [_lib.Context(dev_id) for _ in range(W - 1)])
-    # c2: the same window's spans on every context (separate HBM copies): every window of a step is
-    # the configured C2 window, so GTEPS and windows/s stay comparable across W.
+    # c2 (batch): W distinct seeded windows of one system, each its own span table resident in HBM
+    # (one 5-minute window of 200k traces each), ranked by one mr_windows_batch call per step.
+    # c2 --streams-mode: the same window's spans on every context (separate HBM copies).
     # c3: D distinct seeded windows per context; the rank's share of the batch cycles through them.
     D = max(1, args.c3_distinct) if args.config == "c3" else 1
     wins = [[] for _ in range(1 if batch else W)]   # per context: [(dev, t0, t1, a3, ok, abnormal)]
+    if c2_tabs is not None:
+        normal, tabs = c2_tabs
+        a3, ok = slo_from_gpu(ctxs[0], normal)   # one SLO period; every table has the topology's codes
+        for i, abnormal_i in enumerate(tabs):
+            t0 = int(abnormal_i.tstart.min())
+            wins[0].append((DeviceSpans(ctxs[0], abnormal_i), t0, t0 + 5 * 60 * 10**9, a3, ok, abnormal_i))
+            if i:
+                tabs[i] = None   # host copy no longer needed (window 0's feeds the CPU baseline)
+        abnormal, topo = tabs[0], None
+        D = 0
     for d in range(D):
         seed = 1234 + 7919 * rank + 104729 * d
         if d == 0 or args.config == "c3":
@@ -676,6 +795,7 @@ def main():
             dev = DeviceSpans(cx, abnormal)          # window spans resident in HBM from here on
             wins[0 if batch else ci].append((dev, t0, t0 + 5 * 60 * 10**9, a3, ok, abnormal))
     del topo, normal
+    c2_tabs = None
     ctx = ctxs[0]
     dev0, t0, t1, a3, ok, abnormal = wins[0][0]
     prec = _lib.MR_FP32 if args.precision == "fp32" else _lib.MR_FP64
@@ -699,7 +819,7 @@ def main():
             from microrank_amd.online_rca import rank_windows
 
             pool = wins[0]
-            per_step = share if share is not None else W
+            per_step = share if share is not None else W   # c2: W windows, cycling the distinct ones
             res, first = [], None
             for _ in range(n):
                 for c0 in range(0, per_step, W):   # c3: calls of <= W windows
@@ -778,7 +898,8 @@ def main():
         "vs_baseline": None,
         "dtype": "f64" if args.precision == "fp64" else "f32",
         "data": "synthetic (seeded Train-Ticket-like spans, int-coded, resident in HBM)"
-                + (f"; {D * W} distinct windows per rank, the batch cycles through them" if c3 else ""),
+                + (f"; {D * W} distinct windows per rank, the batch cycles through them" if c3 else
+                   f"; {len(wins[0])} distinct windows per step (own seed and span table each)" if batch else ""),
         "config": {"workload": (f"C3 batch of {args.c3_windows} RCA windows ({args.ops} ops / {args.traces} traces "
                                 f"each) over {world} GPU(s)" if c3 else
                                 f"C2 RCA window: {args.ops} ops / {args.traces} traces per rank")
@@ -787,11 +908,11 @@ def main():
                    "edges_per_window": int(edges // max(n_win, 1)),
                    "windows_per_step": (win_all // args.steps) if c3 else W,
                    "parallelism": (f"windows x{world} ranks, mr_windows_batch of {W} windows per call "
-                                   f"(PageRanks of all {2 * W} graphs share each iteration's launches)") if batch
+                                   f"(the PageRanks of a group of 16 windows share each iteration's launches)") if batch
                                   else f"windows x{world} ranks x{W} streams"},
         "windows_per_s": round(win_all / elapsed, 3),
-        "roofline": {"bound": "hbm", "kernel": ("one Jacobi iteration of the batch's graphs: k_tr_a + k_fx_b "
-                                                f"launches over {2 * W} graphs") if batch else
+        "roofline": {"bound": "hbm", "kernel": ("one Jacobi iteration of a window group's graphs: the "
+                                                "k_tr_a + k_fx_b launch pair over the 32 graphs of 16 windows") if batch else
                                                ("one Jacobi iteration: k_tr_a + k_fx_b (fused path)"
                                                 + (f", stream 0 of {W} concurrent windows" if W > 1 else "")),
                      "achieved": round(achieved, 1),

@@ -104,6 +104,11 @@ int mr_graph_info(const mr_graph* g, int32_t* n_nodes, int32_t* n_traces, int64_
  */
 int mr_pagerank(mr_ctx* ctx, mr_graph* g, int anomaly, double d, double alpha, int iters,
                 int precision, uint32_t flags);
+/* mr_pagerank with the anomaly preference's weight phi exposed (the 0.5 at both places of
+ * pagerank.py:82-84; SURVEY §5 config defaults: d = 0.85, alpha = 0.01 at :116, iters = 25 at
+ * :117, phi = 0.5).  mr_pagerank is mr_pagerank_ex with phi = 0.5. */
+int mr_pagerank_ex(mr_ctx* ctx, mr_graph* g, int anomaly, double d, double alpha, int iters, double phi,
+                   int precision, uint32_t flags);
 /* several independent graphs (e.g. the normal and anomaly graphs of a window, or many windows)
  * ranked together: one launch per Jacobi iteration covers every graph */
 int mr_pagerank_batch(mr_ctx* ctx, mr_graph* const* graphs, const int* anomaly, int n_graphs, double d,

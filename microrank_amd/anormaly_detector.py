@@ -62,6 +62,32 @@ def detect_states(data, start_time, end_time, slo, *, ctx=None):
     return state, na.value, nn.value, table
 
 
+class TraceList(list):
+    """The detector's trace lists: plain lists of traceIDs (sorted, as the reference returns them)
+    that also remember their trace codes in the span table they came from, so the driver's next
+    call, get_pagerank_graph(list, data), selects them without a Python lookup per trace."""
+
+    __slots__ = ("_mr_codes", "_mr_table")
+
+    @classmethod
+    def of(cls, table, codes):
+        names = table.meta.get("trace_names_arr")
+        if names is None:
+            names = table.meta["trace_names_arr"] = np.asarray(table.trace_names, dtype=object)
+        out = cls(names[codes].tolist())
+        out._mr_codes, out._mr_table = codes, table
+        return out
+
+    def codes_for(self, table):
+        """The trace codes when this list is unchanged and from ``table``, else None."""
+        c = getattr(self, "_mr_codes", None)
+        if c is None or getattr(self, "_mr_table", None) is not table or len(self) != c.size:
+            return None
+        if c.size and (self[0] != table.trace_names[c[0]] or self[-1] != table.trace_names[c[-1]]):
+            return None
+        return c
+
+
 def system_anomaly_detect(data, start_time, end_time, slo, operation_list, *, ctx=None):
     """anormaly_detector.system_anomaly_detect on the GPU (anormaly_detector.py:44-84)."""
     res = detect_states(data, start_time, end_time, slo, ctx=ctx)
@@ -69,9 +95,8 @@ def system_anomaly_detect(data, start_time, end_time, slo, operation_list, *, ct
         print("Error: Current span list is empty ")
         return False
     state, na, nn, table = res
-    names = table.trace_names
-    abnormal_list = [names[i] for i in np.flatnonzero(state == 2)]
-    normal_list = [names[i] for i in np.flatnonzero(state == 1)]
+    abnormal_list = TraceList.of(table, np.flatnonzero(state == 2))
+    normal_list = TraceList.of(table, np.flatnonzero(state == 1))
     print("anormaly_trace", na)
     print("total_trace", na + nn)
     print()

@@ -200,7 +200,9 @@ struct mr_graph {
     // mr_pagerank_presetup: kinds / preference / iteration state already set up for the next call
     bool pre_ok = false, pre_fp32 = false;
     int pre_anomaly = 0;
-    double pre_d = 0.0;
+    double pre_d = 0.0, pre_phi = 0.5;
+    // the anomaly preference's weight phi (pagerank.py:82-84: 0.5 at both places), set per call
+    double phi = 0.5;
     uint32_t pre_flags = 0;
     uint64_t pre_seed = 0, pre_hmask = 0;
     DBuf<int32_t> wtile;             // [waves+1] first tile of each wave of the last launch plan

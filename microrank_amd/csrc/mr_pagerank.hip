@@ -1026,7 +1026,7 @@ __global__ void k_pref_total_exact(const double* kind, const int32_t* pr_trace, 
 // c_tp[i] too (formerly k_tr_gather)
 __global__ void k_pref_apply(const double* kind, const int32_t* pr_trace, const int32_t* pr_len,
                              const int32_t* len_t, int32_t n_pr, const double* scal, int anomaly,
-                             float cd, float* pref, float* c_t, const int32_t* tperm, float* c_tp) {
+                             float cd, double phi, float* pref, float* c_t, const int32_t* tperm, float* c_tp) {
     int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n_pr) return;
     int32_t t = tperm ? tperm[i] : pr_trace ? pr_trace[i] : i;
@@ -1036,7 +1036,7 @@ __global__ void k_pref_apply(const double* kind, const int32_t* pr_trace, const 
     if (!anomaly) {
         v = 1.0 / k / scal[2];                                               // :74
     } else {
-        v = 1.0 / (k / scal[2] * 0.5 + 1.0 / (double)ln) / scal[3] * 0.5;   // :80-85
+        v = 1.0 / (k / scal[2] * phi + 1.0 / (double)ln) / scal[3] * phi;   // :80-85 (phi = 0.5)
     }
     float vf = (float)v;
     pref[t] = vf;
@@ -1063,6 +1063,7 @@ struct SDev {
     int32_t T, N, anomaly, fp32;
     int64_t cap, T_all;
     float cd;
+    double phi;                                 // the anomaly preference's 0.5 (pagerank.py:82-84)
     int32_t b_reset, b_kins, b_kver, b_pref;   // the graph's first block in each launch
     float *pref, *c_t, *c_tp;
     const int32_t* tperm;
@@ -1178,7 +1179,7 @@ __global__ void k_pref_apply_b(const SDev* __restrict__ sd, int32_t ng) {
     const double k = G.kind[t];
     double v;
     if (!G.anomaly) v = 1.0 / k / G.scal[2];                                               // :74
-    else v = 1.0 / (k / G.scal[2] * 0.5 + 1.0 / (double)G.len_t[t]) / G.scal[3] * 0.5;     // :80-85
+    else v = 1.0 / (k / G.scal[2] * G.phi + 1.0 / (double)G.len_t[t]) / G.scal[3] * G.phi;   // :80-85
     const float vf = (float)v;
     G.pref[t] = vf;
     G.c_t[t] = G.cd * vf;   // (1.0 - d) * v in float32 (T4)
@@ -1277,7 +1278,6 @@ struct GDev {
     unsigned long long* fx_limb;   // sharded: [2N] (lo, hi) limb sums per op, then [nranks] r' maxima
     int32_t rank, nranks;          // sharded: this rank's slot of the r' maxima appended to the sum
     double* op_sum;                // sharded tile path: [N] pair-partial sums per op
-    unsigned long long* stamp;   // diagnostics (MR_FX_STAMP): per-block phase clocks, else null
     double fx_scale, fx_iscale;
     const double* dscale;          // k_tr_a graphs cut on the device: {2^SC, 2^-SC} (k_tr_cut), else null
     // wide fused graphs: k_tr_a's ops [0, NA) (NA = N otherwise); ops [NA, N) in ranges of
@@ -1289,11 +1289,11 @@ struct GDev {
     double cx_scale, cx_iscale;
     double alpha;                  // P_ss weight (k_fx_b's call-graph term)
     int32_t T, N, n_tb, n_tiles, tshift, lds_su, blk0, n_ob, blk0b;
-    int32_t blk0f, n_fa, blk0fb, n_fb;   // fused path: k_fx_a / k_fx_b block ranges
+    int32_t blk0f, n_fa, blk0fb, n_fb;   // fused path: k_tr_a / k_fx_b block ranges
     int32_t fb_ops;                      // k_fx_b ops per block
 };
 
-// graph owning block `blk` of launch kind `which` (0 k_iter_a, 1 k_iter_b, 2 k_fx_a, 3 k_fx_b);
+// graph owning block `blk` of launch kind `which` (0 k_iter_a, 1 k_iter_b, 2 k_tr_a, 3 k_fx_b);
 // the start offsets are non-decreasing over graphs (graphs without blocks in a launch repeat it)
 __device__ __forceinline__ int32_t graph_of(const GDev* gs, int32_t ng, int32_t blk, int which) {
     int32_t lo = 0, hi = ng - 1;
@@ -1494,18 +1494,17 @@ __global__ void __launch_bounds__(TB) k_iter_b(const GDev* __restrict__ gs, int3
 // ---------------------------------------------------------------- fused single-pass iteration
 // For graphs with N <= FX_NMAX and P_rs == P_sr (every graph built from spans): ONE read of the
 // trace-major u16 ids per iteration serves both products of pagerank.py:122-125.
-//   k_fx_a  block = TT consecutive traces (a thread each):
-//     r'[t]   = d * sum_{o in ops(t)} su_k[o] / M_s(k) + fp32((1-d) v_t)        (node order)
+//   k_tr_a  lane = trace (wave tiles of 64 traces, below):
+//     r'[t]   = d * sum_{o in ops(t)} su_k[o] / M_s(k) + fp32((1-d) v_t)        (layout order)
 //     lacc[o] += X_t for o in ops(t),   X_t = rint(w_t r'_k[t] / M_r(k) * 2^SC)   (LDS, u64)
 //   The block's N accumulators go out as one dense row part[block][0..N).  Because X_t <= 2^SC
-//   (w_t <= 1, r'_k <= M_r(k)) and SC = 63 - log2(TT), a row entry never exceeds 2^63.
+//   (w_t <= 1, r'_k <= M_r(k)) and SC = 64 - bits(traces of the block), a row entry stays < 2^64.
 //   k_fx_b  wave per op: S_o = sum over blocks of part[.][o] as two exact 32-bit-limb sums, one
 //   rounding to double, then s'[o] = d * (S_o 2^-SC + alpha * sum_p pw_p s_k[p] / M_s(k)).
 // Integer sums are exact, so the result does not depend on atomic or reduction order: runs are
 // bitwise reproducible, and the quantisation (2^-SC absolute per term, SC >= 53) sits below
 // fp64's own rounding of the reference's dot products.
 constexpr int FX_NMAX = 16384;
-constexpr size_t FX_LDS_BUDGET = 150 * 1024;   // su joins lacc in LDS while both fit this budget
 // global-memory views of pointers read from GDev: loads through them compile to global_load
 // (vmcnt only) instead of flat_load, whose lgkmcnt share would make every LDS wait also wait
 // for outstanding HBM loads
@@ -1522,11 +1521,6 @@ __device__ __forceinline__ const GLB T* gp(const T* p) { return (const GLB T*)p;
 template <class T>
 __device__ __forceinline__ GLB T* gpw(T* p) { return (GLB T*)p; }
 
-// k_fx_a block size cap: 512 threads leave each wave 256 VGPRs for the pipelined walk (1024 would
-// cap it at 128 and spill); small graphs still fill the chip with two resident blocks per CU
-constexpr int FX_TMAX = 512;
-constexpr int FX_CAP = 24;   // staged ids per thread: blocks with more entries take the long path
-
 // graph of a fused-launch block: ng <= 2 resolves from the scalar split (no memory hop)
 __device__ __forceinline__ int32_t fx_graph(const GDev* gs, int32_t ng, int32_t split, int which) {
     if (ng == 1) return 0;
@@ -1534,747 +1528,11 @@ __device__ __forceinline__ int32_t fx_graph(const GDev* gs, int32_t ng, int32_t 
     return graph_of(gs, ng, (int32_t)blockIdx.x, which);
 }
 
-// LDS layout of k_fx_a (byte offsets), shared by kernel and host
-struct FxLds {
-    size_t su, lacc, head, tail, tsum, xl, owner, hbits, ids, total;
-    bool su_lds;   // su staged in LDS; otherwise gathered from its global copy (L2-resident)
-    // TT traces per tile, NS walk segments (the block size, a multiple of TT)
-    __host__ __device__ FxLds(int32_t N, int32_t TT, int32_t NS, bool allow_su = true) {
-        size_t rest = ((size_t)N + 1) * 8 + 2 * (size_t)NS * 8 + (size_t)TT * 8 + (size_t)TT * 8 + 8 +
-                      (size_t)NS * 4 + ((size_t)FX_CAP * TT / 32 + 2) * 8 + 16 + ((size_t)FX_CAP * TT + 16) * 2;
-        su_lds = allow_su && ((size_t)N + 1) * 8 + rest <= FX_LDS_BUDGET;
-        // with su in LDS, su and the accumulator interleave (16 B per op: one address for the
-        // gather and the atomic of an entry)
-        su = 0;
-        lacc = su_lds ? 8 : 0;
-        head = ((size_t)N + 1) * (su_lds ? 16 : 8);
-        tail = head + (size_t)NS * 8;
-        tsum = tail + (size_t)NS * 8;
-        xl = tsum + (size_t)TT * 8;
-        owner = xl + ((size_t)TT + 1) * 8;
-        hbits = owner + (size_t)NS * 4;
-        ids = (hbits + ((size_t)FX_CAP * TT / 32 + 2) * 8 + 15) / 16 * 16;   // hbits: two buffers
-        total = ids + ((size_t)FX_CAP * TT + 16) * 2;
-    }
-};
-
-// Balanced walk (blocks whose id range fits FX_CAP*TT - 8 entries): the block's ids are staged
-// in LDS from a 16-B aligned base (positions q = entry - base; the entry range starts at `shift`)
-// and cut into TT equal segments of L positions (L a multiple of 8); lane s walks segment s in
-// order.  Trace starts are bits of an LDS bitmap.  Per trace the walk yields pieces: a whole
-// trace inside one segment -> tsum[t]; a trace crossing segments -> tail[first segment] +
-// head[each later segment], combined in segment order by the trace's own thread.  Sums stay
-// sequential within a piece: fixed order, deterministic.  Requires non-empty traces (every
-// graph built from spans; uploaded graphs are checked on the host).
-// staged id chunk `cidx` (positions 8*cidx .. 8*cidx+7): positions outside the tile's entries
-// [shift, np) become N, the zero slot, so the walk needs no per-entry bounds tests
-__device__ __forceinline__ u32x4 fx_pad(u32x4 v, int32_t cidx, int32_t shift, int64_t np, int32_t N) {
-    // keep positions k (0..7) of the chunk with kb <= k < ke; 32-bit, only k is a constant
-    const int32_t q0 = cidx * 8;
-    const int32_t kb = shift - q0, ke = (int32_t)min(np - (int64_t)q0, (int64_t)8);
-    if (kb <= 0 && ke >= 8) return v;
-    const uint32_t n = (uint32_t)N;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        uint32_t x = v[k];
-        if (2 * k < kb || 2 * k >= ke) x = (x & 0xffff0000u) | n;
-        if (2 * k + 1 < kb || 2 * k + 1 >= ke) x = (x & 0x0000ffffu) | (n << 16);
-        v[k] = x;
-    }
-    return v;
-}
-
-// PF: blocks walk several tiles with the next tile's loads in flight; without PF every block
-// has one tile.  S: walk segments (threads) per trace of a tile -- S = 2 doubles the waves that
-// hide the gathers' latency at the same LDS image.  All variants fit 128 VGPRs.
-template <class Q, bool SUL, bool PF, int S>
-__global__ void __launch_bounds__(S * FX_TMAX, 4) k_fx_a(const GDev* __restrict__ gs, int32_t ng, int32_t split,
-                                                         double d, double alpha, int it, int32_t TT) {
-    static_assert(FX_CAP == 24, "at most three 16-B id chunks per thread");
-    extern __shared__ __attribute__((aligned(16))) unsigned char lraw[];
-    __shared__ double red[S * FX_TMAX / WAVE];
-    __shared__ double msh[2];
-    __shared__ int64_t nxe[2];   // the next tile's id range
-    const unsigned long long ts0 = __builtin_amdgcn_s_memrealtime();
-    const GDev& G = gs[fx_graph(gs, ng, split, 2)];
-    const int32_t NS = S * TT;   // == blockDim.x
-    const int32_t lb = (int32_t)blockIdx.x - G.blk0f;
-    const int cur = it & 1, nxt = cur ^ 1, k3 = it % 3;
-    const int32_t T = G.T, N = G.N;
-    const int32_t i = (int32_t)threadIdx.x;
-    const FxLds L_(N, TT, NS, SUL);
-    // global operands through addrspace(1) pointers: global_load (vmcnt only), never flat
-    const GLB int64_t* rs_off = gp(G.rs_off);
-    const GLB u32x4* rs16 = gp((const u32x4*)G.rs16);   // 8 ids per 16 B; padded past nnz
-    const GLB uint16_t* rs16s = gp(G.rs16);
-    const GLB Q* qc = gp((const Q*)G.q[cur]);
-    GLB Q* qn = gpw((Q*)G.q[nxt]);
-    const GLB float* c_t = gp(G.c_t);
-    const GLB float* w_t = gp(G.w_t);
-    const GLB double* sug = gp(G.sub[cur]);   // N + 1 entries, sub[N] = 0 (the pad slot)
-    constexpr int AS = SUL ? 2 : 1;   // word stride of su / lacc in LDS (interleaved when SUL)
-    double* su_l = (double*)(lraw + L_.su);
-    unsigned long long* lacc = (unsigned long long*)(lraw + L_.lacc);
-    double* head = (double*)(lraw + L_.head);
-    double* tail = (double*)(lraw + L_.tail);
-    double* tsum = (double*)(lraw + L_.tsum);
-    unsigned long long* xl = (unsigned long long*)(lraw + L_.xl);   // xl[c + 1] = X of trace c; xl[0] = 0
-    int32_t* owner = (int32_t*)(lraw + L_.owner);
-    uint32_t* hbits = (uint32_t*)(lraw + L_.hbits);
-    uint16_t* ids = (uint16_t*)(lraw + L_.ids);
-    GLB unsigned long long* mslot = gpw(G.mslot);
-    const GLB unsigned long long* Mcur = mslot + (size_t)2 * MSH * k3;
-    GLB unsigned long long* Mnext = mslot + (size_t)2 * MSH * ((k3 + 1) % 3);
-    if (lb == 0 && i < 2 * MSH) mslot[(size_t)2 * MSH * ((k3 + 2) % 3) + i] = 0ull;
-    for (int32_t o = i; o <= N; o += NS) {   // once per block: the accumulator spans all its tiles
-        if (SUL) su_l[AS * o] = sug[o];
-        lacc[AS * o] = 0ull;
-    }
-    const int32_t HW = FX_CAP * TT / 32 + 2;   // words of one trace-start bitmap (tile parity)
-    for (int32_t w = i; w < 2 * HW; w += NS) hbits[w] = 0u;
-    if (i == 0) xl[0] = 0ull;
-    if (i < WAVE) {
-        const double ms = wave_max(bits2d(Mcur[i]));
-        const double mr = wave_max(bits2d(Mcur[MSH + i]));
-        if (i == 0) {
-            msh[0] = ms;
-            msh[1] = mr;
-        }
-    }
-    const int32_t n_tiles = (T + TT - 1) / TT;   // this block's tiles: an even share of the graph's
-    const int32_t tb = (int32_t)((int64_t)lb * n_tiles / G.n_fa), te = (int32_t)((int64_t)(lb + 1) * n_tiles / G.n_fa);
-    // Software pipeline over the block's tiles: trace offsets run two tiles ahead, ids and
-    // per-trace words one tile ahead, so their HBM latency hides behind the current tile's walk.
-    // gfx9 counts loads and stores in one in-order vmcnt, so every global access in the loop is
-    // unconditional (clamped indices, a pad slot for the store) -- the compiler can then wait for
-    // exactly the load it needs -- and loaded values are consumed at the end of an iteration.
-    // A tile's id range [e0, e1) comes from its first and last traces' offsets through LDS.
-    int64_t e0 = 0, e1 = 0, p_a = 0, p_b = 0, o_a = 0, o_b = 0;
-    double p_qk = 0.0;
-    float p_ct = 0.0f, p_wt = 0.0f;
-    u32x4 pv0 = {0u, 0u, 0u, 0u}, pv1 = pv0, pv2 = pv0;
-#define FX_OFFS(tile_, a_, b_)                                          \
-    do {                                                                \
-        const int32_t t0_ = (tile_) * TT, tc_ = t0_ + min(min(i, TT - 1), T - t0_ - 1); \
-        a_ = rs_off[tc_];                                               \
-        b_ = rs_off[tc_ + 1];                                           \
-    } while (0)
-    // ids chunks clamped in-bounds (the buffer is padded past nnz; a long tile ignores them)
-#define FX_BODY(tile_, e0s_, e1s_, qk_, ct_, wt_, v0_, v1_, v2_)                                   \
-    do {                                                                                           \
-        const int32_t tc_ = (tile_) * TT + min(min(i, TT - 1), T - (tile_) * TT - 1);              \
-        qk_ = (double)qc[tc_];                                                                     \
-        ct_ = c_t[tc_];                                                                            \
-        wt_ = w_t[tc_];                                                                            \
-        const int64_t base_ = (e0s_) & ~(int64_t)7;                                                \
-        const GLB u32x4* src_ = rs16 + (base_ >> 3);                                               \
-        const int32_t nch_ = (int32_t)min((((e1s_) - base_) + 7) >> 3, (int64_t)FX_CAP / 8 * TT);  \
-        v0_ = src_[min(i, nch_ - 1)];                                                              \
-        if (S < 3) v1_ = src_[min(i + NS, nch_ - 1)];                                              \
-        if (S < 2) v2_ = src_[min(i + 2 * NS, nch_ - 1)];                                          \
-    } while (0)
-#define FX_BOUNDS(tile_, e0_, e1_)                                            \
-    do {                                                                      \
-        e0_ = rs_off[(tile_) * TT];                                           \
-        e1_ = rs_off[min((tile_) * TT + TT, T)];                              \
-    } while (0)
-    if (tb < te) {
-        FX_BOUNDS(tb, e0, e1);
-        FX_OFFS(tb, p_a, p_b);
-        FX_BODY(tb, e0, e1, p_qk, p_ct, p_wt, pv0, pv1, pv2);
-        if (PF) {
-            const int32_t t1 = min(tb + 1, te - 1), nt1 = min(TT, T - t1 * TT);
-            FX_OFFS(t1, o_a, o_b);
-            if (i == 0) nxe[0] = o_a;   // tile tb + 1's id range, from its first and last traces
-            if (i == nt1 - 1) nxe[1] = o_b;
-        }
-    }
-    double rmax = -__builtin_huge_val();
-    // diagnostics (MR_FX_STAMP): thread 0 sums its clock per tile phase
-    // (sums in LDS: no registers held across the walk)
-    __shared__ unsigned long long ph[7];   // [6]: the last clock
-    const bool stamp = G.stamp != nullptr;
-    const unsigned long long t_init = stamp ? __builtin_amdgcn_s_memrealtime() : 0ull;
-    if (stamp && i == 0) {
-        for (int k = 0; k < 6; ++k) ph[k] = 0ull;
-        ph[6] = t_init;
-    }
-#define FX_MARK(slot)                                                        \
-    do {                                                                     \
-        if (stamp && i == 0) {                                               \
-            const unsigned long long nw_ = __builtin_amdgcn_s_memrealtime(); \
-            ph[slot] += nw_ - ph[6];                                         \
-            ph[6] = nw_;                                                     \
-        }                                                                    \
-    } while (0)
-    __syncthreads();   // accumulator, bitmaps and maxima ready
-    const double xsc = G.fx_scale / msh[1];   // X = rint(q / M_r * 2^SC), as one multiply
-    for (int32_t tile = tb; tile < te; ++tile) {
-        const bool first = tile == tb;
-        if (!PF && !first) {
-            FX_BOUNDS(tile, e0, e1);
-            FX_OFFS(tile, p_a, p_b);
-            FX_BODY(tile, e0, e1, p_qk, p_ct, p_wt, pv0, pv1, pv2);
-        }
-        const int32_t t0 = tile * TT;
-        const int32_t nt = min(TT, T - t0);
-        const int32_t t = t0 + i;
-        const bool own = i < nt;
-        const int64_t a = p_a, b = p_b;
-        const double qk = p_qk;
-        const float ct = p_ct, wt = p_wt;
-        const int64_t base = e0 & ~(int64_t)7;
-        const int32_t shift = (int32_t)(e0 - base);
-        const int64_t np_ = e1 - base;                 // positions [shift, np_) hold the tile's entries
-        const bool bal = np_ <= (int64_t)FX_CAP * TT;
-        // No barrier opens the tile: the previous tile's walk barrier already orders its readers
-        // of ids/owner/xl before this staging, its combine reads of tsum/head/tail come before
-        // this tile's stage barrier in every thread, and the trace-start bitmaps alternate by
-        // tile parity (the other one is cleared here, for the next tile).
-        uint32_t* hb = hbits + (tile & 1) * HW;
-        // segment length L = 8, 16 or 32 positions (a power of two: divisions become shifts;
-        // 32 still fits the 64-bit start window read at a segment's first position)
-        const int32_t lgL = np_ <= 8 * (int64_t)NS ? 3 : np_ <= 16 * (int64_t)NS ? 4 : 5;
-        const int32_t L = 1 << lgL;
-        const int32_t ra = (int32_t)(a - base), rb = (int32_t)(b - base);
-        const unsigned long long X = own ? (unsigned long long)__double2ull_rn(qk * xsc) : 0ull;
-        {
-            uint32_t* hb_next = hbits + ((tile + 1) & 1) * HW;
-            for (int32_t w = i; w < HW; w += NS) hb_next[w] = 0u;
-        }
-        if (bal) {   // stage the id range and mark the trace starts / segment owners
-            const int32_t nch = (int32_t)((np_ + 7) >> 3);
-            if (i < nch) *(u32x4*)(ids + (size_t)i * 8) = fx_pad(pv0, i, shift, np_, N);
-            if (S < 3 && i + NS < nch) *(u32x4*)(ids + (size_t)(i + NS) * 8) = fx_pad(pv1, i + NS, shift, np_, N);
-            if (S < 2 && i + 2 * NS < nch)
-                *(u32x4*)(ids + (size_t)(i + 2 * NS) * 8) = fx_pad(pv2, i + 2 * NS, shift, np_, N);
-            if (i == 0) owner[0] = -1;   // positions before `shift` belong to the previous tile
-            if (own) {
-                xl[i + 1] = X;
-                atomicOr(&hb[ra >> 5], 1u << (ra & 31));
-                for (int32_t sg = (ra + L - 1) >> lgL; (sg << lgL) < rb; ++sg) owner[sg] = i;   // segments starting in t
-            }
-        }
-        FX_MARK(4);
-        __syncthreads();
-        FX_MARK(5);
-        // prefetch: tile + 1's ids and words, tile + 2's offsets (the last tiles reload themselves)
-        int64_t m_a = 0, m_b = 0, e0n = e0, e1n = e1;
-        double n_qk = 0.0;
-        float n_ct = 0.0f, n_wt = 0.0f;
-        u32x4 nv0 = pv0, nv1 = pv1, nv2 = pv2;
-        if (PF) {
-            if (tile + 1 < te) {
-                e0n = nxe[0];
-                e1n = nxe[1];
-            }
-            FX_BODY(min(tile + 1, te - 1), e0n, e1n, n_qk, n_ct, n_wt, nv0, nv1, nv2);
-            FX_OFFS(min(tile + 2, te - 1), m_a, m_b);
-        }
-        FX_MARK(0);
-        double acc = 0.0;
-        if (bal) {
-            const int32_t p = i * L;
-            if (p < np_) {
-                const int32_t qe = (int32_t)min((int64_t)p + L, np_);
-                // trace starts of the segment (L <= 32 positions fit the 33+ bits left after the
-                // shift); position p's own start is `st`, the rest are tested per 8-entry chunk
-                const unsigned long long bits =
-                    (((unsigned long long)hb[(p >> 5) + 1] << 32) | hb[p >> 5]) >> (p & 31);
-                int32_t c = owner[i];
-                bool st = bits & 1ull;                   // the segment's first piece starts a trace
-                const unsigned long long sb = bits & ~1ull;
-                for (int32_t ch = p; ch < qe; ch += 8) {
-                    // 8 ids, 16-B aligned (ch % 8 == 0); positions outside the tile hold N (zero slot)
-                    const uint4 w = *(const uint4*)(ids + ch);
-                    const uint32_t m8 = (uint32_t)(sb >> (ch - p)) & 0xffu;
-                    int32_t o[8];
-                    o[0] = (int32_t)(w.x & 0xffffu); o[1] = (int32_t)(w.x >> 16);
-                    o[2] = (int32_t)(w.y & 0xffffu); o[3] = (int32_t)(w.y >> 16);
-                    o[4] = (int32_t)(w.z & 0xffffu); o[5] = (int32_t)(w.z >> 16);
-                    o[6] = (int32_t)(w.w & 0xffffu); o[7] = (int32_t)(w.w >> 16);
-                    // all LDS reads of the chunk go out together (su and each entry's trace X),
-                    // then the 8 atomics issue back to back: an LDS wait inside the entry loop
-                    // would also wait for every atomic before it
-                    double g[8];
-                    unsigned long long xj[8];
-#ifndef MR_EXP
-#define MR_EXP 0   // timing experiments only: 1 drops the atomics, 2 the gathers, 3 both
-#endif
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) g[j] = (MR_EXP & 2) ? (double)o[j] : SUL ? su_l[AS * o[j]] : sug[o[j]];
-                    if (!(MR_EXP & 1)) {
-#pragma unroll
-                        for (int j = 0; j < 8; ++j)
-                            xj[j] = xl[c + 1 + (int32_t)__builtin_popcount(m8 & ((2u << j) - 1u))];
-#pragma unroll
-                        for (int j = 0; j < 8; ++j) atomicAdd(&lacc[AS * o[j]], xj[j]);
-                    }
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) {
-                        if (m8 & (1u << j)) {   // a new trace starts at ch + j
-                            if (st) tsum[c] = acc; else head[i] = acc;
-                            acc = 0.0;
-                            st = true;
-                            ++c;
-                        }
-                        acc += g[j];
-                    }
-                }
-                const bool ends = qe == np_ || ((bits >> (qe - p)) & 1ull);
-                if (st) {
-                    if (ends) tsum[c] = acc; else tail[i] = acc;
-                } else {
-                    head[i] = acc;
-                }
-            }
-            __syncthreads();
-            FX_MARK(2);
-            if (own && rb > ra) {
-                const int32_t sa = ra >> lgL, sb = (rb - 1) >> lgL;
-                if (sa == sb) {
-                    acc = tsum[i];
-                } else {
-                    acc = tail[sa];
-                    for (int32_t sg = sa + 1; sg <= sb; ++sg) acc += head[sg];
-                }
-            } else {
-                acc = 0.0;
-            }
-        } else {
-            // long tile (rare): thread per trace in rounds of FX_CAP*TT staged ids, 8-entry chunks
-            const int32_t cap = FX_CAP * TT;
-            const int lane = i & (WAVE - 1);
-            for (int64_t lo = e0; lo < e1; lo += cap) {
-                const int64_t hi = min(lo + (int64_t)cap, e1);
-                __syncthreads();
-                for (int64_t e = lo + i; e < hi; e += NS) ids[e - lo] = rs16s[e];
-                __syncthreads();
-                const int32_t x0 = (int32_t)(max(a, lo) - lo), x1 = (int32_t)(min(b, hi) - lo);
-                for (int32_t c = x0; c < x1; c += 8) {
-                    int32_t o[8];
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) o[j] = c + j < x1 ? (int32_t)ids[c + j] : N;
-                    double g[8];
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) g[j] = SUL ? su_l[AS * o[j]] : sug[o[j]];
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) acc += g[j];
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) atomicAdd(&lacc[AS * o[(j + lane) & 7]], X);
-                }
-            }
-            __syncthreads();   // the next tile's staging overwrites ids
-        }
-        const double rp = d * (acc / msh[0]) + (double)ct;   // pagerank.py:125
-        if (own) rmax = nmax(rmax, rp);
-        FX_MARK(3);
-        if (PF) {
-            // tile + 2's id range for the next iteration's prefetch (read after its first barrier)
-            const int32_t t2 = min(tile + 2, te - 1), nt2 = min(TT, T - t2 * TT);
-            if (i == 0) nxe[0] = m_a;
-            if (i == nt2 - 1) nxe[1] = m_b;
-            e0 = e0n;
-            e1 = e1n;
-            p_a = o_a;
-            p_b = o_b;
-            p_qk = n_qk;
-            p_ct = n_ct;
-            p_wt = n_wt;
-            pv0 = nv0;
-            pv1 = nv1;
-            pv2 = nv2;
-            o_a = m_a;
-            o_b = m_b;
-        }
-        qn[own ? t : T] = (Q)((double)wt * rp);   // last: no wait above queues behind it (q[T]: pad slot)
-    }
-#undef FX_MARK
-#undef FX_BODY
-#undef FX_OFFS
-#undef FX_BOUNDS
-    // call-graph term for the next s' (pagerank.py:122-124, alpha P_ss s_k), a thread per op
-    {
-        const GLB double* sp_cur = gp(G.spb[cur]);
-        const GLB int64_t* ss_off = gp(G.ss_off);
-        const GLB int32_t* ss_par = gp(G.ss_par);
-        const GLB float* pw = gp(G.pw);
-        GLB double* ssv = gpw(G.fx_ssv);
-        for (int32_t oss = lb * NS + i; oss < N; oss += G.n_fa * NS) {
-            double bb = 0.0;
-            for (int64_t e = ss_off[oss]; e < ss_off[oss + 1]; ++e) {
-                const int32_t pp = ss_par[e];
-                bb += (double)pw[pp] * sp_cur[pp];
-            }
-            ssv[oss] = alpha * (bb / msh[0]);
-        }
-    }
-    const unsigned long long t_loop = stamp ? __builtin_amdgcn_s_memrealtime() : 0ull;
-    __syncthreads();
-    GLB unsigned long long* prow = gpw(G.fx_part) + (size_t)lb * N;
-    for (int32_t o = i; o < N; o += NS) prow[o] = lacc[AS * o];
-    rmax = block_max(rmax, red);
-    if (i == 0) {
-        if (rmax >= 0.0)   // -inf: a block without traces (an empty shard's placeholder)
-            atomicMax((unsigned long long*)&Mnext[MSH + blockIdx.x % MSH], d2bits(rmax));
-        if (G.stamp) {
-            unsigned long long* sp = G.stamp + (size_t)blockIdx.x * 16;
-            sp[0] = ts0;
-            sp[1] = t_init - ts0;
-            for (int k = 0; k < 6; ++k) sp[2 + k] = ph[k];
-            sp[8] = t_loop;
-            sp[9] = __builtin_amdgcn_s_memrealtime();
-        }
-    }
-}
-
-// ---------------------------------------------------------------- fused iteration, wave-autonomous (k_wv_a)
-// The single-pass iteration of k_fx_a (same sums in the same order: bitwise the same results)
-// with no block barrier inside the trace loop.  Every wave streams its own WAVE TILES of 64
-// consecutive traces:
-//   * lane i owns trace i of the wave tile (X_t, the combine, the q store) AND the contiguous
-//     position segment [i*L, i*L + L) of the tile's 16-B aligned id range (L = 8 or 16: wave
-//     tiles of up to 1024 positions; larger ones take the thread-per-trace path);
-//   * the segment's ids come straight into registers (two 16-B chunks), the tile's offsets two
-//     tiles ahead and its ids / per-trace words one tile ahead, so 16 independent waves per CU
-//     keep their loads in flight while others walk;
-//   * trace starts, segment owners, X values and the walk's pieces live in a per-wave LDS
-//     scratch: written and read by the same wave, so in order with no barrier;
-//   * the block's waves share the per-op accumulator (LDS u64 atomics: integers, order-free)
-//     and su (LDS when it fits beside the accumulator; otherwise gathered from its global copy
-//     right after the tile's ids arrive, before the bitmap staging).
-// The block synchronises only to clear the accumulator and to write its partial row.
-constexpr int WV_POS = 1024;                 // positions of a wave tile's pipelined path (64 x 16)
-constexpr int WV_POS_MAX = 4096;             // segment path up to 64 positions per lane
-struct WvScratch {                           // per-wave LDS scratch (byte offsets)
-    static constexpr size_t hb = 0;          // 130 words: trace starts of 4096 positions (+2 read-ahead)
-    static constexpr size_t owner = 528;     // int32[64]: trace (in the tile) of a segment's first position
-    static constexpr size_t xl = 784;        // u64[66]: xl[c + 1] = X of trace c, xl[0] = 0
-    static constexpr size_t tsum = 1312;     // double[64]
-    static constexpr size_t head = 1824;     // double[64]
-    static constexpr size_t tail = 2336;     // double[64]
-    static constexpr size_t bytes = 2848;    // (the long path's staged ids, u16[1024], alias it)
-};
+// ---------------------------------------------------------------- fused iteration: LDS budget and su modes
 constexpr size_t WV_LDS_MAX = 160 * 1024 - 512;
-// su modes of k_wv_a: global gathers only / every op's su in LDS (interleaved with the
-// accumulator: one address for the gather and the atomic) / the n_hot most covered ops' su in
+// su modes of k_tr_a: global gathers only / every op's su in LDS / the n_hot most covered ops' su in
 // LDS (relabelled graphs, ops [0, n_hot)), the rest gathered
 enum { WV_SU_GLOBAL = 0, WV_SU_ALL = 1, WV_SU_HOT = 2 };
-struct WvLds {
-    size_t su, lacc, wave, total;
-    bool su_lds;       // every op's su fits beside the accumulator
-    int32_t n_hot;     // WV_SU_HOT: ops whose su fits
-    __host__ __device__ WvLds(int32_t N, int32_t NT, int mode = WV_SU_ALL) {
-        const size_t scratch = (size_t)(NT / WAVE) * WvScratch::bytes;
-        su_lds = ((size_t)N + 1) * 16 + scratch <= WV_LDS_MAX;
-        const bool all = mode == WV_SU_ALL && su_lds;
-        const size_t accb = ((size_t)N + 1) * (all ? 16 : 8);
-        n_hot = 0;
-        if (mode == WV_SU_HOT) {
-            const size_t room = WV_LDS_MAX - scratch - (accb + 15) / 16 * 16;
-            n_hot = (int32_t)std::min<size_t>((size_t)N, room / 8 / 64 * 64);
-        }
-        lacc = all ? 8 : 0;
-        su = all ? 0 : (accb + 15) / 16 * 16;   // WV_SU_HOT: su_hot[n_hot] after the accumulator
-        wave = su + (mode == WV_SU_HOT ? ((size_t)n_hot * 8 + 15) / 16 * 16 : all ? 0 : 0);
-        if (all) wave = (accb + 15) / 16 * 16;
-        total = wave + scratch;
-    }
-};
-
-template <class Q, int SUM, int NT>
-__global__ void __launch_bounds__(NT) k_wv_a(const GDev* __restrict__ gs, int32_t ng, int32_t split, double d,
-                                             double alpha, int it, int32_t unused) {
-    constexpr bool SUL = SUM == WV_SU_ALL, HOT = SUM == WV_SU_HOT;
-    constexpr int NW = NT / WAVE;
-    extern __shared__ __attribute__((aligned(16))) unsigned char lraw[];
-    __shared__ double red[NW];
-    __shared__ double msh[2];
-    const GDev& G = gs[fx_graph(gs, ng, split, 2)];
-    const int32_t lb = (int32_t)blockIdx.x - G.blk0f;
-    const int cur = it & 1, nxt = cur ^ 1, k3 = it % 3;
-    const int32_t T = G.T, N = G.N;
-    const int32_t tid = (int32_t)threadIdx.x, lane = tid & (WAVE - 1), wv = tid / WAVE;
-    const WvLds L_(N, NT, SUM);
-    const int32_t NH = HOT ? G.n_hot : 0;   // <= L_.n_hot (the host sizes both alike)
-    const GLB int32_t* rs_off = gp((const int32_t*)G.rs_off);   // low words (offsets < 2^31)
-    const GLB u32x4* rs16 = gp((const u32x4*)G.rsw);           // 8 ids per 16 B; padded past nnz
-    const GLB uint16_t* rs16s = gp(G.rsw);
-    const GLB Q* qc = gp((const Q*)G.q[cur]);
-    GLB Q* qn = gpw((Q*)G.q[nxt]);
-    const GLB float* c_t = gp(G.c_t);
-    const GLB float* w_t = gp(G.w_t);
-    const GLB double* sug = gp(G.sub[cur]);   // N + 1 entries, sub[N] = 0 (the pad slot)
-    constexpr int AS = SUL ? 2 : 1;
-    double* su_l = (double*)(lraw + L_.su);
-    unsigned long long* lacc = (unsigned long long*)(lraw + L_.lacc);
-    unsigned char* ws = lraw + L_.wave + (size_t)wv * WvScratch::bytes;
-    uint32_t* hb = (uint32_t*)(ws + WvScratch::hb);
-    int32_t* owner = (int32_t*)(ws + WvScratch::owner);
-    unsigned long long* xl = (unsigned long long*)(ws + WvScratch::xl);
-    double* tsum = (double*)(ws + WvScratch::tsum);
-    double* head = (double*)(ws + WvScratch::head);
-    double* tail = (double*)(ws + WvScratch::tail);
-    uint16_t* lids = (uint16_t*)ws;
-    GLB unsigned long long* mslot = gpw(G.mslot);
-    const GLB unsigned long long* Mcur = mslot + (size_t)2 * MSH * k3;
-    GLB unsigned long long* Mnext = mslot + (size_t)2 * MSH * ((k3 + 1) % 3);
-    if (lb == 0 && tid < 2 * MSH) mslot[(size_t)2 * MSH * ((k3 + 2) % 3) + tid] = 0ull;
-    for (int32_t o = tid; o <= N; o += NT) {
-        if (SUL) su_l[AS * o] = sug[o];
-        lacc[AS * o] = 0ull;
-    }
-    if (HOT)
-        for (int32_t o = tid; o < NH; o += NT) su_l[o] = sug[o];
-    if (tid < WAVE) {
-        const double ms = wave_max(bits2d(Mcur[tid]));
-        const double mr = wave_max(bits2d(Mcur[MSH + tid]));
-        if (tid == 0) {
-            msh[0] = ms;
-            msh[1] = mr;
-        }
-    }
-    __syncthreads();   // accumulator and maxima ready
-    const double xsc = G.fx_scale / msh[1], Ms = msh[0];
-    // this block's wave tiles [kb, ke); wave wv takes kb + wv, kb + wv + NW, ...
-    const int32_t W = (T + WAVE - 1) / WAVE;
-    const int32_t kb = (int32_t)((int64_t)lb * W / G.n_fa), ke = (int32_t)((int64_t)(lb + 1) * W / G.n_fa);
-    // per-lane trace of wave tile k (clamped into the graph: lanes past T repeat the last trace)
-    auto tr_of = [&](int32_t k) { return min(k * WAVE + lane, T - 1); };
-    // pipeline: offsets two tiles ahead, ids + per-trace words one tile ahead; every global load
-    // in the loop is unconditional (clamped), so each use waits for exactly its own load
-    int32_t k = kb + wv;
-    const int32_t kl = max(ke - 1, kb);   // clamp target of the look-ahead
-    int32_t a0 = 0, b0 = 0, a1 = 0, b1 = 0;   // offsets of tiles k and k + NW
-    double qk = 0.0;
-    u32x4 v0 = {0u, 0u, 0u, 0u}, v1 = v0;
-    if (k < ke) {   // (a wave without tiles -- e.g. an empty shard -- loads nothing)
-        const int32_t t = tr_of(min(k, kl));
-        a0 = rs_off[2 * t];
-        b0 = rs_off[2 * t + 2];
-        const int32_t t1 = tr_of(min(k + NW, kl));
-        a1 = rs_off[2 * t1];
-        b1 = rs_off[2 * t1 + 2];
-    // words + ids of the tile whose offsets are (a_, b_)
-#define WV_LOAD(kk_, a_, b_, qk_, v0_, v1_)                                                         \
-    do {                                                                                            \
-        const int32_t t_ = tr_of(min((kk_), kl));                                                   \
-        qk_ = (double)qc[t_];                                                                       \
-        const int32_t e0_ = __builtin_amdgcn_readfirstlane(a_);                                     \
-        const int32_t e1_ = __builtin_amdgcn_readlane(b_, WAVE - 1);                                \
-        const int32_t base_ = e0_ & ~7, np_ = e1_ - base_;                                          \
-        const int32_t nch_ = (np_ + 7) >> 3;                                                        \
-        const int32_t cpl_ = np_ <= 8 * WAVE ? 1 : np_ <= WV_POS ? 2 : np_ <= 2 * WV_POS ? 4 : 8;   \
-        const GLB u32x4* src_ = rs16 + (base_ >> 3);                                                \
-        v0_ = src_[min(lane * cpl_, nch_ - 1)];                                                     \
-        v1_ = src_[min(lane * cpl_ + 1, nch_ - 1)];                                                 \
-    } while (0)
-        WV_LOAD(k, a0, b0, qk, v0, v1);
-    }
-    double rmax = -__builtin_huge_val();
-    for (; k < ke; k += NW) {
-        // ---- this tile's state (loaded one tile ago)
-        const int32_t t = k * WAVE + lane;
-        const bool own = t < T;
-        const int32_t a = a0, b = b0;
-        const int32_t e0 = __builtin_amdgcn_readfirstlane(a), e1 = __builtin_amdgcn_readlane(b, WAVE - 1);
-        const double q_k = qk;
-        u32x4 c0 = v0, c1 = v1;
-        const int32_t base = e0 & ~7, shift = e0 - base, np_ = e1 - base;
-        // segment length 8 / 16 (ids prefetched) or 32 / 64 positions; 0: long tile
-        const int lgL = np_ <= 8 * WAVE ? 3 : np_ <= WV_POS ? 4 : np_ <= 2 * WV_POS ? 5 : np_ <= WV_POS_MAX ? 6 : 0;
-        const int32_t L = 1 << lgL, p = lane * L, cpl = L >> 3;
-        const int32_t qe = lgL ? min(p + L, np_) : 0;
-        const int32_t ra = a - base, rb = b - base;
-        const unsigned long long X = own ? (unsigned long long)__double2ull_rn(q_k * xsc) : 0ull;
-        c0 = fx_pad(c0, lane * cpl, shift, np_, N);
-        c1 = fx_pad(c1, lane * cpl + 1, shift, np_, N);
-        // !SUL: the segment's su values from the global copy, in flight during the staging; HOT:
-        // only the cold ops' -- a hot entry loads the pad slot sug[N] instead (every hot lane the
-        // same line: no L2 traffic, and the load stays unconditional for exact vmcnt waits)
-        double gv0[8], gv1[8];
-        if (!SUL && !(MR_EXP & 2)) {
-            const uint32_t w0[4] = {c0.x, c0.y, c0.z, c0.w}, w1[4] = {c1.x, c1.y, c1.z, c1.w};
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int32_t o = (int32_t)((w0[j >> 1] >> ((j & 1) * 16)) & 0xffffu);
-                gv0[j] = sug[HOT && o < NH ? N : o];
-            }
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int32_t o = (int32_t)((w1[j >> 1] >> ((j & 1) * 16)) & 0xffffu);
-                gv1[j] = sug[HOT && o < NH ? N : o];
-            }
-        }
-        // ---- look-ahead: tile k + NW's words and ids, tile k + 2NW's offsets -- issued AFTER
-        // the gathers (compiler barrier): loads complete in issue order (one vmcnt), so the walk
-        // then waits for its L2 gathers only, not for these HBM loads
-        asm volatile("" ::: "memory");
-        WV_LOAD(k + NW, a1, b1, qk, v0, v1);
-        a0 = a1;
-        b0 = b1;
-        {
-            const int32_t t2 = tr_of(min(k + 2 * NW, kl));
-            a1 = rs_off[2 * t2];
-            b1 = rs_off[2 * t2 + 2];
-        }
-        // this tile's (1-d) v_t and w_t, needed only after the walk (their latency hides behind it)
-        const float c_k = c_t[tr_of(k)], w_k = w_t[tr_of(k)];
-        double acc = 0.0;
-        if (lgL) {
-            // ---- staging (per-wave scratch): trace starts, segment owners, X
-            for (int32_t w = lane; w < 130; w += WAVE) hb[w] = 0u;
-            owner[lane] = -1;
-            __builtin_amdgcn_wave_barrier();
-            if (own) {
-                xl[lane + 1] = X;
-                atomicOr(&hb[ra >> 5], 1u << (ra & 31));
-                for (int32_t sg = (ra + L - 1) >> lgL; (sg << lgL) < rb; ++sg) owner[sg] = lane;
-            }
-            if (lane == 0) xl[0] = 0ull;
-            __builtin_amdgcn_wave_barrier();
-            // ---- walk
-            if (p < qe) {
-                // trace starts of the segment: L <= 64 bits from position p, and whether a trace
-                // starts right after it (the segment's last piece is then complete)
-                const int32_t w0 = p >> 5;
-                const unsigned long long bits =
-                    (((unsigned long long)hb[w0 + 1] << 32) | hb[w0]) >> (p & 31);
-                int32_t c = owner[lane];
-                bool st = bits & 1ull;
-                // one chunk of 8 positions: op-side atomics (X of each entry's trace) and the
-                // trace side's sequential sums restarted at each trace start; a finished piece
-                // goes to tsum[c] (a trace inside the segment) or head[lane] (the segment's first
-                // piece, continuing a trace from an earlier segment).  Only the store is
-                // predicated (one address select, one masked ds_write).
-                auto chunk = [&](const u32x4 w, const double* gsrc, int kc) {
-                    // starts after the segment's first position (that one is `st`)
-                    const uint32_t m8 = (uint32_t)(bits >> (8 * kc)) & (kc ? 0xffu : 0xfeu);
-                    int32_t o[8];
-                    o[0] = (int32_t)(w.x & 0xffffu); o[1] = (int32_t)(w.x >> 16);
-                    o[2] = (int32_t)(w.y & 0xffffu); o[3] = (int32_t)(w.y >> 16);
-                    o[4] = (int32_t)(w.z & 0xffffu); o[5] = (int32_t)(w.z >> 16);
-                    o[6] = (int32_t)(w.w & 0xffffu); o[7] = (int32_t)(w.w >> 16);
-                    double g[8];
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) {
-                        const double gg = gsrc[j];
-                        g[j] = (MR_EXP & 2) ? (double)o[j]
-                               : SUL      ? su_l[AS * o[j]]
-                               : HOT      ? (o[j] < NH ? su_l[min(o[j], NH - 1)] : gg)
-                                          : gg;
-                    }
-                    unsigned long long xj[8];
-#pragma unroll
-                    for (int j = 0; j < 8; ++j)
-                        xj[j] = (MR_EXP & 4) ? X : xl[c + 1 + (int32_t)__builtin_popcount(m8 & ((2u << j) - 1u))];
-                    if (!(MR_EXP & 1)) {
-#pragma unroll
-                        for (int j = 0; j < 8; ++j) atomicAdd(&lacc[AS * o[j]], xj[j]);
-                    }
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) {
-                        const bool sj = (m8 >> j) & 1u;   // a new trace starts at p + 8 kc + j
-                        double* dst = st ? tsum + c : head + lane;
-                        if (sj) *dst = acc;
-                        c += sj ? 1 : 0;
-                        st = st || sj;
-                        acc = (sj ? 0.0 : acc) + g[j];
-                    }
-                };
-                chunk(c0, gv0, 0);
-                if (cpl > 1 && p + 8 < qe) chunk(c1, gv1, 1);
-                if (cpl > 2) {
-                    // segments of 32 / 64 positions (wave tiles of heavy traces): chunks 2.. are
-                    // loaded here, latency exposed; the wait below leaves nothing of this rare
-                    // path pending where it rejoins the pipelined one
-                    const GLB u32x4* src = rs16 + (base >> 3);
-                    for (int kc = 2; kc < cpl; ++kc) {
-                        if (p + 8 * kc >= qe) break;
-                        const u32x4 w = fx_pad(src[lane * cpl + kc], lane * cpl + kc, shift, np_, N);
-                        if (!SUL) {   // the su gathers land in gv0's registers (chunk 0 is done)
-                            const uint32_t wd[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-                            for (int j = 0; j < 8; ++j) {
-                                const int32_t o = (int32_t)((wd[j >> 1] >> ((j & 1) * 16)) & 0xffffu);
-                                gv0[j] = sug[HOT && o < NH ? N : o];
-                            }
-                        }
-                        chunk(w, gv0, kc);
-                    }
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                }
-                const bool ends = qe == np_ || (qe - p < L ? ((bits >> (qe - p)) & 1ull)
-                                                           : lgL == 6 ? (hb[w0 + 2] & 1u) : ((bits >> L) & 1ull));
-                *(st ? (ends ? tsum + c : tail + lane) : head + lane) = acc;
-            }
-            __builtin_amdgcn_wave_barrier();
-            // ---- combine: trace = its pieces in segment order
-            if (own && rb > ra) {
-                const int32_t sa = ra >> lgL, sbg = (rb - 1) >> lgL;
-                if (sa == sbg) {
-                    acc = tsum[lane];
-                } else {
-                    acc = tail[sa];
-                    for (int32_t sg = sa + 1; sg <= sbg; ++sg) acc += head[sg];
-                }
-            } else {
-                acc = 0.0;
-            }
-            __builtin_amdgcn_wave_barrier();   // the scratch is rewritten by the next tile
-        } else {
-            // ---- long wave tile (rare): thread per trace in rounds of 1024 staged ids
-            for (int32_t lo = e0; lo < e1; lo += WV_POS) {
-                const int32_t hi = min(lo + WV_POS, e1);
-                __builtin_amdgcn_wave_barrier();
-                for (int32_t e = lo + lane; e < hi; e += WAVE) lids[e - lo] = rs16s[e];
-                __builtin_amdgcn_wave_barrier();
-                const int32_t x0 = max(a, lo) - lo, x1 = min(b, hi) - lo;
-                for (int32_t cc = x0; cc < x1; cc += 8) {
-                    int32_t o[8];
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) o[j] = cc + j < x1 ? (int32_t)lids[cc + j] : N;
-                    double g[8];
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) g[j] = SUL ? su_l[AS * o[j]] : (HOT && o[j] < NH) ? su_l[o[j]] : sug[o[j]];
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) acc += g[j];
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) atomicAdd(&lacc[AS * o[(j + lane) & 7]], X);
-                }
-            }
-            if (!own) acc = 0.0;
-            __builtin_amdgcn_wave_barrier();
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this rare path's loads: none pending at the merge
-        }
-        const double rp = d * (acc / Ms) + (double)c_k;   // pagerank.py:125
-        if (own) rmax = nmax(rmax, rp);
-        qn[own ? t : T] = (Q)((double)w_k * rp);          // q[T]: pad slot
-    }
-#undef WV_LOAD
-    // call-graph term for the next s' (pagerank.py:122-124, alpha P_ss s_k), a thread per op
-    {
-        const GLB double* sp_cur = gp(G.spb[cur]);
-        const GLB int64_t* ss_off = gp(G.ss_off);
-        const GLB int32_t* ss_par = gp(G.ss_par);
-        const GLB float* pw = gp(G.pw);
-        GLB double* ssv = gpw(G.fx_ssv);
-        for (int32_t oss = lb * NT + tid; oss < N; oss += G.n_fa * NT) {
-            double bb = 0.0;
-            for (int64_t e = ss_off[oss]; e < ss_off[oss + 1]; ++e) {
-                const int32_t pp = ss_par[e];
-                bb += (double)pw[pp] * sp_cur[pp];
-            }
-            ssv[oss] = alpha * (bb / Ms);
-        }
-    }
-    __syncthreads();
-    GLB unsigned long long* prow = gpw(G.fx_part) + (size_t)lb * N;
-    for (int32_t o = tid; o < N; o += NT) prow[o] = lacc[AS * o];
-    rmax = block_max(rmax, red);
-    if (tid == 0 && rmax >= 0.0)   // -inf: a block without traces (an empty shard's placeholder)
-        atomicMax((unsigned long long*)&Mnext[MSH + blockIdx.x % MSH], d2bits(rmax));
-}
 
 // ---------------------------------------------------------------- fused iteration, trace-parallel (k_tr_a)
 #ifndef MR_TREXP
@@ -2830,101 +2088,9 @@ static const bool g_debug = getenv("MR_DEBUG") != nullptr;
 void mr_prof_begin(mr_ctx* ctx);
 void mr_prof_end(mr_ctx* ctx, double bytes);
 
-// traces per k_fx_a block (= its block size): the larger of 512/256 whose LDS image fits
-// (MR_TT caps it for measurements); 0 when none fits
-constexpr size_t FX_LDS_MAX = 160 * 1024 - 512;   // minus the kernel's static LDS
-// walk segments per trace of a tile (k_fx_a's S): one-tile blocks take S = 1 (two 512-thread
-// blocks per CU), pipelined multi-tile blocks S = 2 (16 waves per CU on one LDS image);
-// MR_FX_S = 1 or 2 forces it for measurements
-static int fx_s(bool multi) {
-    static const int v = [] {
-        const char* e = getenv("MR_FX_S");
-        return e ? (atoi(e) == 1 ? 1 : 2) : 0;
-    }();
-    return v ? v : (multi ? 2 : 1);
-}
-
-using FxA = void (*)(const GDev*, int32_t, int32_t, double, double, int, int32_t);
-static FxA fx_kernel(bool fp32, bool sul, bool pf, int S) {
-    static const FxA tab[2][2][2][2] = {
-        {{{k_fx_a<double, false, false, 1>, k_fx_a<double, false, false, 2>},
-          {k_fx_a<double, false, true, 1>, k_fx_a<double, false, true, 2>}},
-         {{k_fx_a<double, true, false, 1>, k_fx_a<double, true, false, 2>},
-          {k_fx_a<double, true, true, 1>, k_fx_a<double, true, true, 2>}}},
-        {{{k_fx_a<float, false, false, 1>, k_fx_a<float, false, false, 2>},
-          {k_fx_a<float, false, true, 1>, k_fx_a<float, false, true, 2>}},
-         {{k_fx_a<float, true, false, 1>, k_fx_a<float, true, false, 2>},
-          {k_fx_a<float, true, true, 1>, k_fx_a<float, true, true, 2>}}}};
-    return tab[fp32 ? 1 : 0][sul ? 1 : 0][pf ? 1 : 0][S == 2 ? 1 : 0];
-}
-
-static int fx_tt(int32_t N) {
-    static const int cap = [] {
-        const char* e = getenv("MR_TT");
-        const int v = e ? atoi(e) : FX_TMAX;
-        return (v == 256 || v == FX_TMAX) ? v : FX_TMAX;
-    }();
-    for (int tt = cap; tt >= 256; tt >>= 1)
-        if (FxLds(N, tt, 2 * tt).total <= FX_LDS_MAX) return tt;   // fits either S
-    return 0;
-}
-
-// k_fx_a blocks of a graph: one tile each while the tiles fit the resident blocks, else the
-// resident block count (times r) with an even share of the tiles each, so no tail round is
-// left; the dense partial rows (N words per block) stay a small part of an iteration's bytes.
-// At most 2^15 traces per block keeps the fixed-point scale >= 2^48.
-static int64_t fx_blocks(int32_t T, int32_t N, int TT) {
-    static const int ncu = [] {
-        int dev = 0, v = 0;
-        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            v = 256;
-        return std::max(v, 1);
-    }();
-    const int64_t tiles = cdiv((int64_t)T, TT);
-    // resident blocks per CU: LDS image and VGPRs (the runtime's occupancy for the variant)
-    auto per_cu = [&](bool pf) {
-        const int S = fx_s(pf);
-        const FxLds L(N, TT, S * TT);
-        int n = 0;
-        const void* kfn = (const void*)fx_kernel(false, L.su_lds, pf, S);
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kfn, S * TT, L.total) != hipSuccess || n < 1)
-            n = std::max<int>(1, (int)(FX_LDS_MAX / L.total));
-        return (int64_t)n;
-    };
-    if (tiles <= ncu * per_cu(false)) return tiles;   // one tile per block, no pipeline
-    const int64_t resident = ncu * per_cu(true);
-    int64_t nb = resident;
-    while (cdiv(tiles, nb) * TT > 32768) nb += resident;
-    return std::min(nb, tiles);
-}
-
-// ---- fused iteration kernel: k_tr_a (default); MR_FX_KERNEL=wv / v1 selects k_wv_a / k_fx_a
-// for A/B measurements
-enum { FXK_V1 = 1, FXK_WV = 2, FXK_TR = 3 };
-static int fx_kind() {
-    static const int v = [] {
-        const char* e = getenv("MR_FX_KERNEL");
-        if (e && !strcmp(e, "v1")) return (int)FXK_V1;
-        if (e && !strcmp(e, "wv")) return (int)FXK_WV;
-        return (int)FXK_TR;
-    }();
-    return v;
-}
-static bool fx_v1() { return fx_kind() == FXK_V1; }
-static bool plan_is_tr() { return fx_kind() == FXK_TR; }
-using WvA = void (*)(const GDev*, int32_t, int32_t, double, double, int, int32_t);
-static WvA wv_kernel(bool fp32, int mode, int NT) {
-    static const WvA tab[2][3][2] = {
-        {{k_wv_a<double, 0, 512>, k_wv_a<double, 0, 1024>},
-         {k_wv_a<double, 1, 512>, k_wv_a<double, 1, 1024>},
-         {k_wv_a<double, 2, 512>, k_wv_a<double, 2, 1024>}},
-        {{k_wv_a<float, 0, 512>, k_wv_a<float, 0, 1024>},
-         {k_wv_a<float, 1, 512>, k_wv_a<float, 1, 1024>},
-         {k_wv_a<float, 2, 512>, k_wv_a<float, 2, 1024>}}};
-    return tab[fp32 ? 1 : 0][mode][NT == 1024 ? 1 : 0];
-}
-static WvA tr_kernel(bool fp32, int mode, int NT) {
-    static const WvA tab[2][3][2] = {
+using TrA = void (*)(const GDev*, int32_t, int32_t, double, double, int, int32_t);
+static TrA tr_kernel(bool fp32, int mode, int NT) {
+    static const TrA tab[2][3][2] = {
         {{k_tr_a<double, 0, 512>, k_tr_a<double, 0, 1024>},
          {k_tr_a<double, 1, 512>, k_tr_a<double, 1, 1024>},
          {k_tr_a<double, 2, 512>, k_tr_a<double, 2, 1024>}},
@@ -2946,19 +2112,14 @@ static int num_cus() {
 // ops of the fused kernel's walk: a wide graph's hot ops, else all
 static int32_t kern_n(const mr_graph* g) { return g->wide ? g->NA : g->N; }
 
-// Launch plan of the fused iteration for a batch of graphs (one kernel variant per launch).
+// Launch plan of the fused iteration (k_tr_a) for a batch of graphs (one kernel variant per launch).
 struct FxPlan {
-    bool v2 = true;     // wave tiles (k_tr_a / k_wv_a), else k_fx_a
-    bool tr = true;     // k_tr_a
     int NT = 1024;      // block size (16 waves; 512 when the graphs are small)
     int mode = WV_SU_ALL;   // su in LDS for every fused graph of the batch / hot ops / none
     bool sul = true;    // mode == WV_SU_ALL
 };
 static FxPlan fx_plan(mr_graph* const* gs, int ng) {
     FxPlan P;
-    P.v2 = !fx_v1();
-    P.tr = fx_kind() == FXK_TR;
-    if (!P.v2) return P;
     int32_t nmax = 0;
     int64_t tmax = 0;
     for (int i = 0; i < ng; ++i)
@@ -2966,49 +2127,31 @@ static FxPlan fx_plan(mr_graph* const* gs, int ng) {
             nmax = std::max(nmax, kern_n(gs[i]));
             tmax = std::max<int64_t>(tmax, gs[i]->T);
         }
-    static const int force_nt = [] {
-        const char* e = getenv("MR_WV_NT");
-        return e ? atoi(e) : 0;
-    }();
     // 1024-thread blocks when the largest graph has a wave tile for every wave of the chip
-    P.NT = force_nt == 512 || force_nt == 1024 ? force_nt : (cdiv(tmax, WAVE) >= (int64_t)num_cus() * 16 ? 1024 : 512);
+    P.NT = cdiv(tmax, WAVE) >= (int64_t)num_cus() * 16 ? 1024 : 512;
     bool relabeled = false;
     for (int i = 0; i < ng; ++i) relabeled = relabeled || (gs[i]->fused && gs[i]->relabeled);
-    P.sul = P.tr ? TrLds(nmax, WV_SU_ALL).su_lds : WvLds(nmax, P.NT, WV_SU_ALL).su_lds;
+    P.sul = TrLds(nmax, WV_SU_ALL).su_lds;
     P.mode = P.sul ? WV_SU_ALL : relabeled ? WV_SU_HOT : WV_SU_GLOBAL;
     if (P.mode == WV_SU_HOT)   // every graph of the launch must be relabelled (hot ops = low labels)
         for (int i = 0; i < ng; ++i)
             if (gs[i]->fused && !gs[i]->relabeled) P.mode = WV_SU_GLOBAL;
-    if (P.tr && P.mode == WV_SU_HOT && TrLds(nmax, WV_SU_HOT).n_hot < 64) P.mode = WV_SU_GLOBAL;
+    if (P.mode == WV_SU_HOT && TrLds(nmax, WV_SU_HOT).n_hot < 64) P.mode = WV_SU_GLOBAL;
     return P;
 }
 static int32_t plan_n_hot(int32_t N, const FxPlan& P) {
-    if (!P.v2 || P.mode != WV_SU_HOT) return 0;
-    return P.tr ? TrLds(N, WV_SU_HOT).n_hot : WvLds(N, P.NT, WV_SU_HOT).n_hot;
+    return P.mode == WV_SU_HOT ? TrLds(N, WV_SU_HOT).n_hot : 0;
 }
-static size_t plan_lds(int32_t N, const FxPlan& P) {
-    return P.tr ? TrLds(N, P.mode).total : WvLds(N, P.NT, P.mode).total;
-}
+static size_t plan_lds(int32_t N, const FxPlan& P) { return TrLds(N, P.mode).total; }
 
 // resident blocks of the plan's kernel on the chip (occupancy by LDS image and VGPRs)
 static int64_t plan_resident(int32_t N, const FxPlan& P) {
     const size_t lds = plan_lds(N, P);
-    const WvA kfn = P.tr ? tr_kernel(false, P.mode, P.NT) : wv_kernel(false, P.mode, P.NT);
+    const TrA kfn = tr_kernel(false, P.mode, P.NT);
     int n = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, (const void*)kfn, P.NT, lds) != hipSuccess || n < 1)
         n = std::max<int>(1, (int)(WV_LDS_MAX / std::max<size_t>(lds, 1)));
     return (int64_t)num_cus() * n;
-}
-
-// blocks of one graph: a resident block per CU (its waves stream the wave tiles), fewer when the
-// graph has fewer wave tiles than waves, more when a block would exceed 65535 traces (the
-// fixed-point scale 2^48 keeps a block's per-op sums below 2^64)
-static int64_t wv_blocks(int32_t T, int32_t N, const FxPlan& P) {
-    const int64_t W = cdiv((int64_t)T, WAVE), NW = P.NT / WAVE;
-    const int64_t resident = plan_resident(N, P);
-    int64_t nb = std::min<int64_t>(resident, cdiv(W, NW));
-    nb = std::max<int64_t>(nb, (int64_t)cdiv(W, 1023));   // <= 1023 wave tiles (65472 traces) per block
-    return std::max<int64_t>(std::min(nb, W), W ? 1 : 0);
 }
 
 // k_tr_a: blocks of one graph and the cut of its tiles into contiguous per-wave runs of about
@@ -3100,11 +2243,9 @@ static int tr_split(mr_ctx* ctx, mr_graph* g, const FxPlan& P, int64_t wsum, int
     return MR_OK;
 }
 
-static int fused_blocks(mr_ctx* ctx, mr_graph* g, const FxPlan& P, int TT_v1, int64_t wsum, int64_t* nfa,
+static int fused_blocks(mr_ctx* ctx, mr_graph* g, const FxPlan& P, int64_t wsum, int64_t* nfa,
                         std::vector<CutArg>* defer = nullptr) {
-    if (P.tr) return tr_split(ctx, g, P, wsum, nfa, defer);
-    *nfa = P.v2 ? wv_blocks(g->T, g->N, P) : fx_blocks(g->T, g->N, TT_v1);
-    return MR_OK;
+    return tr_split(ctx, g, P, wsum, nfa, defer);
 }
 
 // k_tr_a's layout of a fused graph (after w_t and the kernel's ids rs16 / rsp): traces sorted by
@@ -3290,12 +2431,12 @@ static int wide_prepare(mr_ctx* ctx, mr_graph* g) {
 // else one prepare each.  keep: the descriptors' host copy, alive until the stream has used it.
 int mr_graph_prepare_batch(mr_ctx* ctx, mr_graph* const* gs, int n, std::vector<unsigned char>& keep) {
     const bool off = getenv("MR_NO_PREP_BATCH") != nullptr;   // A/B knob (read per call: tests flip it)
-    bool ok = !off && n >= 2 && plan_is_tr() && getenv("MR_NO_FUSED") == nullptr;
+    bool ok = !off && n >= 2 && getenv("MR_NO_FUSED") == nullptr;
     for (int i = 0; i < n && ok; ++i) {
         const mr_graph* g = gs[i];
         ok = g->rs_is_sr && g->traces_nonempty && !g->force_tile && g->cov_ready && g->N > 0 && g->T > 0 &&
              g->N <= FX_NMAX && g->N + 1 <= TP_LSCAN && g->nnz_rs == g->nnz_sr && g->nnz_sr < (1ll << 31) &&
-             fx_tt(g->N) > 0 && TrLds(g->N, WV_SU_ALL).su_lds &&
+             TrLds(g->N, WV_SU_ALL).su_lds &&
              (int64_t)g->T < (int64_t)num_cus() * TRB * TR_PER_SMALL * 4;
     }
     if (!ok) {
@@ -3411,11 +2552,11 @@ int mr_graph_prepare(mr_ctx* ctx, mr_graph* g) {
     static const bool no_fused = getenv("MR_NO_FUSED") != nullptr;   // A/B knob: force the tile path
     static const bool no_wide = getenv("MR_NO_WIDE") != nullptr;     // A/B knob: N > FX_NMAX on the tile path
     const bool fusable = !no_fused && !g->force_tile && g->rs_is_sr && g->traces_nonempty;
-    if (fusable && !no_wide && N > FX_NMAX && plan_is_tr() && (int64_t)N <= (int64_t)WIDE_NA + (int64_t)WIDE_RMAX * WIDE_RW_MAX) {
+    if (fusable && !no_wide && N > FX_NMAX && (int64_t)N <= (int64_t)WIDE_NA + (int64_t)WIDE_RMAX * WIDE_RW_MAX) {
         g->fused = true;
         return wide_prepare(ctx, g);
     }
-    g->fused = fusable && N <= FX_NMAX && fx_tt(N) > 0;
+    g->fused = fusable && N <= FX_NMAX;
     if (g->fused) {   // no P_sr tiles: the fused iteration reads the trace-major ids only
         if (!g->cov_ready) MR_TRY_HIP(ctx, hipMemsetAsync(g->cov.p, 0, (size_t)std::max(N, 1) * sizeof(int32_t), st));
         if (nnz && N && !g->cov_ready)
@@ -3425,7 +2566,7 @@ int mr_graph_prepare(mr_ctx* ctx, mr_graph* g) {
         // k_wv_a stages the su of the most covered ops (ops [0, n_hot)) and gathers the rest.
         // The kinds keep rs16 (original labels, the same hash on every rank); only the
         // iteration's id stream (rsp), su and the partial rows use the new labels.
-        g->relabeled = fx_kind() == FXK_TR ? !TrLds(N, WV_SU_ALL).su_lds : fx_kind() == FXK_WV && !WvLds(N, 1024, WV_SU_ALL).su_lds;
+        g->relabeled = !TrLds(N, WV_SU_ALL).su_lds;
         if (g->relabeled) {
             DBuf<uint64_t> key;
             DBuf<int32_t> inv;
@@ -3537,8 +2678,8 @@ static int graph_kinds(mr_ctx* ctx, mr_graph* g, bool chk, bool ktab, uint64_t c
 
 // (plan-independent: a window's graphs are set up on the stream that built them, before the
 // batch's plan exists -- mr_pagerank_presetup)
-static int pagerank_setup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool fp32, uint32_t flags, bool tr_plan,
-                          bool sharded, uint64_t seed, uint64_t hmask) {
+static int pagerank_setup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool fp32, uint32_t flags, bool sharded,
+                          uint64_t seed, uint64_t hmask) {
     hipStream_t st = ctx->stream;
     const int32_t N = g->N, T = g->T;
     // Kinds through a global hash table (k_kind_insert) while it stays cache-resident, and for one
@@ -3571,12 +2712,12 @@ static int pagerank_setup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool 
     MR_TRY(g->sub[0].alloc(ctx, (size_t)N + TR_PAD));   // [N, N + TR_PAD) = 0: the fused walks' pad slots
     MR_TRY(g->sub[1].alloc(ctx, (size_t)N + TR_PAD));
     MR_TRY(g->weight.alloc(ctx, (size_t)N));
-    const bool tr = g->fused && tr_plan;
+    const bool tr = g->fused;
     if (tr) MR_TRY(g->c_tp.alloc(ctx, (size_t)std::max(T, 1)));
     if (g->fused) MR_TRY(g->fx_ssv.alloc(ctx, (size_t)N));
     else MR_TRY(g->part.alloc(ctx, (size_t)std::max<int64_t>(g->n_pairs, 1)));
     for (int i = 0; i < 2; ++i) {
-        if (fp32) MR_TRY(g->q32[i].alloc(ctx, (size_t)T + 1));   // [T]: k_fx_a's pad slot
+        if (fp32) MR_TRY(g->q32[i].alloc(ctx, (size_t)T + 1));   // [T]: k_tr_a's pad slot
         else MR_TRY(g->q64[i].alloc(ctx, (size_t)T + 1));
     }
     // one launch clears every per-call word (instead of a memset per buffer) and sets the iteration
@@ -3609,7 +2750,7 @@ static int pagerank_setup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool 
     const bool fuse_gather = tr && !prt && !prl && n_pr == T;
     if (n_pr > 0)
         hipLaunchKernelGGL(k_pref_apply, dim3(nbp), dim3(TB), 0, st, g->kind.p, prt, prl, g->len_t.p, n_pr,
-                           g->scal.p, anomaly, cd, g->pref.p, g->c_t.p, fuse_gather ? (const int32_t*)g->tperm.p : nullptr,
+                           g->scal.p, anomaly, cd, g->phi, g->pref.p, g->c_t.p, fuse_gather ? (const int32_t*)g->tperm.p : nullptr,
                            fuse_gather ? g->c_tp.p : nullptr);
     MR_DEBUG_CHECK(ctx, "k_pref_apply");
     if (tr && T && !fuse_gather)
@@ -3619,11 +2760,11 @@ static int pagerank_setup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool 
 
 // Can pagerank_setup of g run inside a batched set-up?  The window graphs' case: a whole graph on
 // one rank, kinds through the hash table with u16 ids, pr_trace = operation_trace, k_tr_a layout.
-static bool setup_batchable(const mr_graph* g, bool tr_plan, uint32_t flags) {
+static bool setup_batchable(const mr_graph* g, uint32_t flags) {
     const char* kpe = getenv("MR_KIND_PART_MIN");
     const int64_t kp_min = kpe ? (int64_t)atoll(kpe) : (int64_t)(1 << 21);
     return g->T > 0 && (int64_t)g->T < kp_min && !g->kinds_given && !g->mult.p && g->rs_is_sr && g->rs16.p &&
-           g->pr_identity && g->n_pr == g->T && g->fused && tr_plan && g->tperm.p && g->w_tp.p && !g->mw_tp.p &&
+           g->pr_identity && g->n_pr == g->T && g->fused && g->tperm.p && g->w_tp.p && !g->mw_tp.p &&
            !(flags & MR_PR_EXACT_SUMS) && g->T_all == 0;
 }
 
@@ -3671,6 +2812,7 @@ static int pagerank_setup_batch(mr_ctx* ctx, mr_graph* const* gs, const int* ano
         v.cap = (int64_t)cap;
         v.T_all = T;
         v.cd = (float)(1.0 - d);
+        v.phi = g->phi;
         v.pref = g->pref.p;
         v.c_t = g->c_t.p;
         v.c_tp = g->c_tp.p;
@@ -3829,11 +2971,7 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
     MR_TRY_HIP(ctx, hipSetDevice(ctx->device));
     hipStream_t st = ctx->stream;
     const bool fp32 = precision == MR_FP32;
-    int TT = FX_TMAX;   // one block size for the batch: the largest that fits every fused graph
-    for (int i = 0; i < ng; ++i)
-        if (gs[i]->fused) TT = std::min(TT, fx_tt(gs[i]->N));
     const FxPlan plan = fx_plan(gs, ng);
-    if (plan.v2) TT = WAVE;   // wave tiles
     std::vector<unsigned char> setup_h;   // (batched set-up descriptors: alive until the call's final sync)
     DBuf<SDev> setup_d;
     {   // set-up of every graph not set up ahead (mr_pagerank_presetup): batched when they allow it
@@ -3842,20 +2980,20 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         bool batch = !sharded && getenv("MR_NO_SETUP_BATCH") == nullptr;
         for (int i = 0; i < ng; ++i) {
             mr_graph* g = gs[i];
-            const bool pre = g->pre_ok && g->pre_anomaly == anomaly[i] && g->pre_d == d && g->pre_fp32 == fp32 &&
+            const bool pre = g->pre_ok && g->pre_anomaly == anomaly[i] && g->pre_d == d && g->pre_phi == g->phi && g->pre_fp32 == fp32 &&
                              g->pre_flags == flags && g->pre_seed == seed && g->pre_hmask == hmask && !sharded;
             g->pre_ok = false;   // the iteration state is consumed by this call
             if (pre) continue;
             need.push_back(g);
             need_a.push_back(anomaly[i]);
-            batch = batch && setup_batchable(g, plan.tr, flags);
+            batch = batch && setup_batchable(g, flags);
         }
         if (batch && need.size() >= 2) {
             MR_TRY(pagerank_setup_batch(ctx, need.data(), need_a.data(), (int)need.size(), d, fp32, seed, hmask,
                                         setup_h, setup_d));
         } else {
             for (size_t j = 0; j < need.size(); ++j)
-                MR_TRY(pagerank_setup(ctx, need[j], need_a[j], d, fp32, flags, plan.tr, sharded, seed, hmask));
+                MR_TRY(pagerank_setup(ctx, need[j], need_a[j], d, fp32, flags, sharded, seed, hmask));
         }
     }
     hm.mark("setup");
@@ -3867,7 +3005,7 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         mr_graph* g = gs[i];
         if (g->fused) {   // the plan's blocks: partial rows and (k_tr_a) the per-wave cut
             int64_t nfa = 0;
-            MR_TRY(fused_blocks(ctx, g, plan, TT, wsum, &nfa, &cuts));
+            MR_TRY(fused_blocks(ctx, g, plan, wsum, &nfa, &cuts));
             MR_TRY(g->fx_part.alloc(ctx, (size_t)std::max<int64_t>(nfa, 1) * (size_t)kern_n(g)));
         }
     }
@@ -3896,8 +3034,6 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
     std::vector<GDev> hv((size_t)ng);
     int32_t blocks_a = 0, blocks_b = 0, blocks_fa = 0, blocks_fb = 0;
     size_t lds = VCAP * sizeof(double), lds_f = 0;
-    bool sul = true;   // every fused graph stages su in LDS
-    bool multi = false;   // some fused block walks several tiles (the pipelined variant)
     double bytes = 0.0;
     for (int i = 0; i < ng; ++i) {
         mr_graph* g = gs[i];
@@ -3944,22 +3080,18 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         v.op_sum = g->op_sum.p;
         v.rank = ctx->rank;
         v.nranks = ctx->nranks;
-        v.stamp = nullptr;
         // a shard without traces still runs one (empty) block: it clears the maxima slot and
         // writes a zero partial row, and the collectives after the launch need every rank
         int64_t nfa = 0;
-        if (g->fused) MR_TRY(fused_blocks(ctx, g, plan, TT, wsum, &nfa));
+        if (g->fused) MR_TRY(fused_blocks(ctx, g, plan, wsum, &nfa));
         nfa = g->fused ? std::max<int64_t>(nfa, sharded ? 1 : 0) : 0;
         // a row entry stays below 2^63; shards of one graph hold different trace counts, and their
         // limbs are summed, so they share the scale of the largest block (2^15 traces)
         // v1: a row entry stays below 2^63; v2: below 2^64 (traces per block < 2^(64-sc)).
         // Shards of one graph hold different trace counts and their limbs are summed, so they
         // share one scale, 2^48 (<= 65535 traces per block: wv_blocks / fx_blocks)
-        const int64_t tpb = plan.tr && g->fused ? g->wtile_msum
-                                                : cdiv(cdiv((int64_t)g->T, TT), std::max<int64_t>(nfa, 1)) * TT;
-        const int sc = sharded ? 48
-                               : plan.v2 ? 64 - bits_for((uint64_t)std::max<int64_t>(tpb, 1))
-                                         : 63 - bits_for((uint64_t)std::max<int64_t>(tpb - 1, 1));
+        const int64_t tpb = g->fused ? g->wtile_msum : 0;
+        const int sc = sharded ? 48 : 64 - bits_for((uint64_t)std::max<int64_t>(tpb, 1));
         v.alpha = alpha;
         v.fx_scale = std::ldexp(1.0, sc);
         v.fx_iscale = std::ldexp(1.0, -sc);
@@ -3973,7 +3105,7 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         v.cx_scale = v.fx_scale;
         v.cx_iscale = v.fx_iscale;
         // the graph's scale on the device (k_tr_cut) unless the ranks share the fixed one
-        v.dscale = (!sharded && plan.tr && g->fused && g->wtile_msum < 0) ? g->dscale.p : nullptr;
+        v.dscale = (!sharded && g->fused && g->wtile_msum < 0) ? g->dscale.p : nullptr;
         if (g->wide) {
             // cold rows: at most cold_span adds per op and row; a sharded graph's ranks sum their
             // limbs per op, and an op hot on one rank may be cold on another: one scale for both
@@ -3999,8 +3131,6 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         v.blk0b = blocks_b;
         bytes += iter_bytes(g, fp32);
         if (g->fused) {
-            sul = sul && (plan.v2 ? plan.sul : FxLds(g->N, TT, 2 * TT).su_lds);   // (v1: fits either S)
-            multi = multi || v.n_fa < cdiv(g->T, TT);
             continue;   // no tile-path blocks (n_tb = n_tiles = n_ob = 0)
         }
         v.n_tb = (mask & 1) ? std::max(cdiv(g->T, TB), sharded ? 1 : 0) : 0;   // (empty shard: see nfa)
@@ -4013,23 +3143,13 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         if (v.lds_su) lds = std::max(lds, ((size_t)g->N + VCAP) * sizeof(double));
         lds = std::max(lds, ((size_t)1 << g->tshift) * (fp32 ? sizeof(float) : sizeof(double)));
     }
-    static const bool stamps = getenv("MR_FX_STAMP") != nullptr;
-    DBuf<unsigned long long> dstamp;
-    if (stamps && blocks_fa) {
-        MR_TRY(dstamp.zero(ctx, (size_t)blocks_fa * 16));
-        for (auto& v : hv) v.stamp = dstamp.p;
-    }
     DBuf<GDev> dv;
     hm.mark("descr");
     MR_TRY(dv.upload(ctx, hv.data(), hv.size()));
     const int32_t split_fa = ng == 2 ? hv[1].blk0f : 0, split_fb = ng == 2 ? hv[1].blk0fb : 0;
-    const int fx_S = fx_s(multi);
-    const FxA fx_a = fx_kernel(fp32, sul, multi, fx_S);
     for (int i = 0; i < ng; ++i)
-        if (gs[i]->fused)
-            lds_f = std::max(lds_f, plan.v2 ? plan_lds(kern_n(gs[i]), plan) : FxLds(gs[i]->N, TT, fx_S * TT, sul).total);
-    const WvA sg_a = plan.tr ? tr_kernel(fp32, plan.mode, plan.NT) : plan.v2 ? wv_kernel(fp32, plan.mode, plan.NT) : nullptr;
-    const int fx_bs = plan.v2 ? plan.NT : fx_S * TT;
+        if (gs[i]->fused) lds_f = std::max(lds_f, plan_lds(kern_n(gs[i]), plan));
+    const TrA tr_a = tr_kernel(fp32, plan.mode, plan.NT);
     // a sharded graph with no collective backend is one whole shard: the split launches around the
     // (no-op) all-reduces would compute the same integers / sums in two halves
     const bool coll = sharded && mr_coll_ready(ctx);
@@ -4081,9 +3201,8 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         }
         if (any_wide && sst != st) MR_TRY_HIP(ctx, hipEventRecord(ctx->side_ev[1], sst));
         if (blocks_fa) {
-            if (sg_a) hipLaunchKernelGGL(sg_a, dim3(blocks_fa), dim3(fx_bs), lds_f, st, dv.p, ng, split_fa, d, alpha, it, TT);
-            else hipLaunchKernelGGL(fx_a, dim3(blocks_fa), dim3(fx_bs), lds_f, st, dv.p, ng, split_fa, d, alpha, it, TT);
-            MR_DEBUG_CHECK(ctx, "k_fx_a");
+            hipLaunchKernelGGL(tr_a, dim3(blocks_fa), dim3(plan.NT), lds_f, st, dv.p, ng, split_fa, d, alpha, it, 0);
+            MR_DEBUG_CHECK(ctx, "k_tr_a");
             if (any_wide && sst != st) MR_TRY_HIP(ctx, hipStreamWaitEvent(st, ctx->side_ev[1], 0));   // k_cold_ops done
             auto fx_b = [&](int mode) {
                 if (fb_small)
@@ -4129,31 +3248,6 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
                        fl.p);
     MR_DEBUG_CHECK(ctx, "k_weights");
     MR_TRY_HIP(ctx, hipGetLastError());
-    if (dstamp.p) {   // diagnostics: phase times of the last k_fx_a launch, in 10 ns ticks
-        std::vector<unsigned long long> h((size_t)blocks_fa * 16);
-        MR_TRY(dstamp.download(ctx, h.data(), h.size()));
-        MR_TRY_HIP(ctx, hipStreamSynchronize(st));
-        unsigned long long t0 = ~0ull, t9 = 0;
-        const char* nm[8] = {"init", "stage", "bar", "pf", "-", "walk", "rest", "ss+rows"};
-        const int slot[8] = {1, 6, 7, 2, 3, 4, 5, -1};
-        double sum[8] = {0}, mx[8] = {0};
-        int nb = 0;
-        for (int32_t b = 0; b < blocks_fa; ++b) {
-            const unsigned long long* x = &h[(size_t)b * 16];
-            if (!x[9]) continue;
-            ++nb;
-            t0 = std::min(t0, x[0]);
-            t9 = std::max(t9, x[9]);
-            for (int k = 0; k < 8; ++k) {
-                const double dt = (slot[k] < 0 ? (double)(x[9] - x[8]) : (double)x[slot[k]]) * 0.01;
-                sum[k] += dt;
-                mx[k] = std::max(mx[k], dt);
-            }
-        }
-        fprintf(stderr, "[stamp] k_fx_a %d blocks span %.2f us; per block avg/max us:", nb, (t9 - t0) * 0.01);
-        for (int k = 0; k < 8; ++k) fprintf(stderr, " %s %.2f/%.2f", nm[k], sum[k] / std::max(nb, 1), mx[k]);
-        fprintf(stderr, "\n");
-    }
     // a shard's local collision must make every rank retry: the error words meet in a MAX
     if (coll) {
         MR_TRY(mr_coll_allreduce(ctx, gs[0]->flag.p, 4, MR_DT_I32, 1));
@@ -4202,9 +3296,8 @@ static uint64_t kind_hmask(int a) { return (a == 0 && getenv("MR_KIND_TEST_COLLI
 int mr_pagerank_presetup_n(mr_ctx* ctx, mr_graph* const* gs, const int* an, int n, double d, int precision,
                            std::vector<unsigned char>& keep) {
     const bool fp32 = precision == MR_FP32;
-    const bool tr = fx_kind() == FXK_TR;
     bool batch = n >= 2 && getenv("MR_NO_SETUP_BATCH") == nullptr;
-    for (int i = 0; i < n && batch; ++i) batch = gs[i]->N && gs[i]->T && setup_batchable(gs[i], tr, 0);
+    for (int i = 0; i < n && batch; ++i) batch = gs[i]->N && gs[i]->T && setup_batchable(gs[i], 0);
     if (!batch) {
         for (int i = 0; i < n; ++i) MR_TRY(mr_pagerank_presetup(ctx, gs[i], an[i], d, precision, 0));
         return MR_OK;
@@ -4216,6 +3309,7 @@ int mr_pagerank_presetup_n(mr_ctx* ctx, mr_graph* const* gs, const int* an, int 
         g->pre_ok = true;
         g->pre_anomaly = an[i];
         g->pre_d = d;
+        g->pre_phi = g->phi;
         g->pre_fp32 = fp32;
         g->pre_flags = 0;
         g->pre_seed = kind_seed(0);
@@ -4227,10 +3321,11 @@ int mr_pagerank_presetup_n(mr_ctx* ctx, mr_graph* const* gs, const int* an, int 
 int mr_pagerank_presetup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, int precision, uint32_t flags) {
     const bool fp32 = precision == MR_FP32;
     if (g->N == 0 || g->T == 0) return MR_OK;   // (the call itself raises)
-    MR_TRY(pagerank_setup(ctx, g, anomaly, d, fp32, flags, fx_kind() == FXK_TR, false, kind_seed(0), kind_hmask(0)));
+    MR_TRY(pagerank_setup(ctx, g, anomaly, d, fp32, flags, false, kind_seed(0), kind_hmask(0)));
     g->pre_ok = true;
     g->pre_anomaly = anomaly;
     g->pre_d = d;
+    g->pre_phi = g->phi;
     g->pre_fp32 = fp32;
     g->pre_flags = flags;
     g->pre_seed = kind_seed(0);
@@ -4267,6 +3362,7 @@ static int kind_compressed_pagerank(mr_ctx* ctx, mr_graph* g, int anomaly, doubl
     // ranks the kept one (its preference and iteration state are set up per call as usual).
     // MR_KC_NOCACHE: rebuild every call (read per call)
     auto rank_kc = [&](mr_graph* gcp) -> int {
+        gcp->phi = g->phi;
         MR_TRY(mr_pagerank_batch_impl(ctx, &gcp, &anomaly, 1, d, alpha, iters, precision, plain));
         MR_TRY(g->weight.alloc(ctx, (size_t)N));
         MR_TRY(g->sn.alloc(ctx, (size_t)N));
@@ -4350,7 +3446,7 @@ static int kind_compressed_pagerank(mr_ctx* ctx, mr_graph* g, int anomaly, doubl
     gc->n_pr = (int32_t)K;
     gc->nnz_sr = gc->nnz_rs = nnz;
     MR_TRY(mr_graph_prepare(ctx, gc.get()));
-    if (!gc->fused || !plan_is_tr())
+    if (!gc->fused)
         return mr_pagerank_batch_impl(ctx, &g, &anomaly, 1, d, alpha, iters, precision, plain);
     MR_TRY(gc->mw_tp.alloc(ctx, (size_t)K));
     hipLaunchKernelGGL(k_kc_mw, dim3(cdiv(K, 256)), dim3(256), 0, st, gc->tperm.p, gc->w_tp.p, gc->mult.p, (int32_t)K,
@@ -4373,8 +3469,19 @@ static int kind_compressed_pagerank(mr_ctx* ctx, mr_graph* g, int anomaly, doubl
 
 extern "C" int mr_pagerank(mr_ctx* ctx, mr_graph* g, int anomaly, double d, double alpha, int iters,
                            int precision, uint32_t flags) {
+    if (g) g->phi = 0.5;
     if (flags & MR_PR_KIND_COMPRESS) return kind_compressed_pagerank(ctx, g, anomaly, d, alpha, iters, precision, flags);
     return mr_pagerank_batch_impl(ctx, &g, &anomaly, 1, d, alpha, iters, precision, flags);
+}
+
+extern "C" int mr_pagerank_ex(mr_ctx* ctx, mr_graph* g, int anomaly, double d, double alpha, int iters, double phi,
+                              int precision, uint32_t flags) {
+    if (!g || !(phi > 0.0)) return mr_fail(ctx, MR_ERR_ARG, "mr_pagerank_ex: bad graph or phi");
+    g->phi = phi;
+    const int rc = (flags & MR_PR_KIND_COMPRESS) ? kind_compressed_pagerank(ctx, g, anomaly, d, alpha, iters, precision, flags)
+                                                 : mr_pagerank_batch_impl(ctx, &g, &anomaly, 1, d, alpha, iters, precision, flags);
+    g->phi = 0.5;
+    return rc;
 }
 
 extern "C" int mr_pagerank_batch(mr_ctx* ctx, mr_graph* const* graphs, const int* anomaly, int n_graphs, double d,

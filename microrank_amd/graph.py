@@ -158,14 +158,18 @@ class DeviceGraph:
         return cls(ctx, h, hg.nodes, hg.traces, hg.N, hg.T)
 
     def pagerank(self, anomaly: bool, d: float = 0.85, alpha: float = 0.01, iters: int = 25,
-                 precision: str = "fp64", exact_sums: bool = False, compress_kinds: bool = False):
+                 precision: str = "fp64", exact_sums: bool = False, compress_kinds: bool = False,
+                 phi: float = 0.5):
         """compress_kinds: iterate over one representative trace per kind (pagerank.py:54-66 --
-        traces of a kind have identical r), the multiplicities carried; same weights."""
+        traces of a kind have identical r), the multiplicities carried; same weights.  phi: the
+        anomaly preference's weight (pagerank.py:82-84)."""
         lib = _lib.load()
         prec = _lib.MR_FP32 if precision == "fp32" else _lib.MR_FP64
         flags = (_lib.MR_PR_EXACT_SUMS if exact_sums else 0) | (_lib.MR_PR_KIND_COMPRESS if compress_kinds else 0)
-        self.ctx.check(lib.mr_pagerank(self.ctx.h, self.h, int(bool(anomaly)), d, alpha, iters, prec, flags),
-                       "mr_pagerank")
+        if iters < 0:
+            raise ValueError("iters must be >= 0")
+        self.ctx.check(lib.mr_pagerank_ex(self.ctx.h, self.h, int(bool(anomaly)), float(d), float(alpha), int(iters),
+                                          float(phi), prec, flags), "mr_pagerank_ex")
 
     def fetch(self, kinds: bool = False):
         lib = _lib.load()

@@ -15,6 +15,7 @@ from . import _lib
 from .graph import DeviceGraph, host_graph_from_dicts
 
 D, ALPHA, ITERATIONS = 0.85, 0.01, 25   # pagerank.py:116-117
+PHI = 0.5                               # pagerank.py:82-84 (the anomaly preference's two 0.5s)
 
 
 def _device_graph(operation_operation, operation_trace, trace_operation, pr_trace, ctx):
@@ -32,14 +33,16 @@ def _device_graph(operation_operation, operation_trace, trace_operation, pr_trac
 
 
 def trace_pagerank(operation_operation, operation_trace, trace_operation, pr_trace, anomaly, *,
+                   d: float = D, alpha: float = ALPHA, iters: int = ITERATIONS, phi: float = PHI,
                    precision: str = "fp64", ctx=None, compress_kinds: bool = False):
-    """pagerank.trace_pagerank on MI355X (pagerank.py:15-112).  compress_kinds: rank one
-    representative per trace kind with its multiplicity (same weights within
-    fp64 rounding)."""
+    """pagerank.trace_pagerank on MI355X (pagerank.py:15-112).  The reference hard-codes d, alpha
+    (pageRank's defaults, :116), the 25 iterations (:117) and phi (:82-84); they are keywords here
+    with the reference's values as defaults.  compress_kinds: rank one representative per trace
+    kind with its multiplicity (same weights within fp64 rounding)."""
     ctx = ctx or _lib.default_context()
     g, owned = _device_graph(operation_operation, operation_trace, trace_operation, pr_trace, ctx)
     try:
-        g.pagerank(bool(anomaly), D, ALPHA, ITERATIONS, precision, compress_kinds=compress_kinds)
+        g.pagerank(bool(anomaly), d, alpha, iters, precision, compress_kinds=compress_kinds, phi=phi)
         w, cov = g.fetch()
     finally:
         if owned:

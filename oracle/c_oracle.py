@@ -67,3 +67,24 @@ def graph_pagerank(st, mask, anomaly):
         raise ValueError("zero-size array to reduction operation maximum which has no identity")
     n = nn.value
     return node[:n], w[:n], cov[:n], nnz.value
+
+
+def incidence_pagerank(hg, anomaly, iters=25, nthreads=0):
+    """trace_pagerank of a graph given as incidence lists (graph.HostGraph), on the CPU
+    (oracle_incidence_pagerank).  Returns (weights, coverage, [s kinds + preference, s iterations])."""
+    N, T = int(hg.N), int(hg.T)
+    arrs = [np.ascontiguousarray(hg.sr_off, np.int64), np.ascontiguousarray(hg.sr_ops, np.int32),
+            np.ascontiguousarray(hg.len_t, np.int32), np.ascontiguousarray(hg.len_o, np.int32),
+            np.ascontiguousarray(hg.ss_off, np.int64), np.ascontiguousarray(hg.ss_par, np.int32),
+            np.ascontiguousarray(hg.nchild, np.int32)]
+    w = np.zeros(N, np.float64)
+    cov = np.zeros(N, np.int32)
+    tp = np.zeros(2, np.float64)
+    rc = lib().oracle_incidence_pagerank(
+        C.c_int32(N), C.c_int32(T), _p(arrs[0], C.c_int64), _p(arrs[1], C.c_int32), _p(arrs[2], C.c_int32),
+        _p(arrs[3], C.c_int32), _p(arrs[4], C.c_int64), _p(arrs[5], C.c_int32), _p(arrs[6], C.c_int32),
+        C.c_int(int(anomaly)), C.c_int(iters), C.c_int(nthreads), _p(w, C.c_double), _p(cov, C.c_int32),
+        _p(tp, C.c_double))
+    if rc != 0:
+        raise ValueError("zero-size array to reduction operation maximum which has no identity")
+    return w, cov, tp

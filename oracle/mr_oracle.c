@@ -193,31 +193,89 @@ static double vmax(const double* v, int64_t n) {
     return m;
 }
 
-/* weight[N], cov[N]; returns 0 or -1 (empty graph: ValueError) */
-int oracle_pagerank(const ograph* g, int anomaly, int iters, double* weight, int32_t* cov, double* kind_out) {
-    const int32_t N = g->N, T = g->T;
-    if (N == 0 || T == 0) return -1;
-    const double d = 0.85, alpha = 0.01;
-    double* kind = (double*)malloc(sizeof(double) * T);
+/* two traces have equal P_sr columns (pagerank.py:62): same op set and fp32(1/len_t) */
+static int same_column(const ograph* g, int32_t a, int32_t b) {
+    int64_t na = g->sr_off[a + 1] - g->sr_off[a], nb_ = g->sr_off[b + 1] - g->sr_off[b];
+    float wa = (float)(1.0 / g->len_t[a]), wb = (float)(1.0 / g->len_t[b]);
+    int eq = na == nb_ && (na == 0 || wa == wb);
+    for (int64_t k = 0; eq && k < na; ++k) eq = g->sr_ops[g->sr_off[a] + k] == g->sr_ops[g->sr_off[b] + k];
+    return eq;
+}
+
+/* kind[t] = size of t's class of equal P_sr columns (T6), by a sort of the traces by column */
+static void kinds_sorted(const ograph* g, double* kind) {
+    const int32_t T = g->T;
     int32_t* ord = (int32_t*)malloc(sizeof(int32_t) * T);
     for (int32_t t = 0; t < T; ++t) ord[t] = t;
     g_cmp = g;
     qsort(ord, T, sizeof(int32_t), cmp_trace);
-    for (int32_t i = 0; i < T;) {   /* equivalence classes of P_sr columns (T6) */
+    for (int32_t i = 0; i < T;) {
         int32_t j = i + 1;
-        while (j < T) {
-            int32_t a = ord[i], b = ord[j];
-            int64_t na = g->sr_off[a + 1] - g->sr_off[a], nb_ = g->sr_off[b + 1] - g->sr_off[b];
-            float wa = (float)(1.0 / g->len_t[a]), wb = (float)(1.0 / g->len_t[b]);
-            int eq = na == nb_ && (na == 0 || wa == wb);
-            for (int64_t k = 0; eq && k < na; ++k) eq = g->sr_ops[g->sr_off[a] + k] == g->sr_ops[g->sr_off[b] + k];
-            if (!eq) break;
-            ++j;
-        }
+        while (j < T && same_column(g, ord[i], ord[j])) ++j;
         for (int32_t k = i; k < j; ++k) kind[ord[k]] = (double)(j - i);
         i = j;
     }
     free(ord);
+}
+
+static uint64_t mix64c(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+/* the same classes for large graphs: a 64-bit hash of each column (in parallel), a radix sort of
+ * (hash, trace), and an exact check of every trace against its run's first; any collision falls
+ * back to kinds_sorted */
+static void kinds_hashed(const ograph* g, double* kind) {
+    const int32_t T = g->T;
+    uint64_t* h = (uint64_t*)malloc(sizeof(uint64_t) * T);
+    uint32_t* ord = (uint32_t*)malloc(sizeof(uint32_t) * T);
+#pragma omp parallel for schedule(static, 4096)
+    for (int32_t t = 0; t < T; ++t) {
+        float w = (float)(1.0 / g->len_t[t]);
+        uint32_t wb;
+        memcpy(&wb, &w, 4);
+        uint64_t x = mix64c(((uint64_t)wb << 32) ^ (uint64_t)(g->sr_off[t + 1] - g->sr_off[t]));
+        for (int64_t e = g->sr_off[t]; e < g->sr_off[t + 1]; ++e) x = mix64c(x ^ (uint64_t)(uint32_t)g->sr_ops[e]);
+        h[t] = x;
+        ord[t] = (uint32_t)t;
+    }
+    rsort(h, ord, T, 64);
+    int collided = 0;
+#pragma omp parallel for schedule(dynamic, 4096) reduction(| : collided)
+    for (int32_t i = 0; i < T; ++i) {
+        if (i > 0 && h[i] == h[i - 1]) continue;   /* one thread per run */
+        int32_t j = i + 1;
+        while (j < T && h[j] == h[i]) ++j;
+        for (int32_t k = i + 1; k < j; ++k) collided |= !same_column(g, (int32_t)ord[i], (int32_t)ord[k]);
+        for (int32_t k = i; k < j; ++k) kind[ord[k]] = (double)(j - i);
+    }
+    free(h);
+    free(ord);
+    if (collided) kinds_sorted(g, kind);
+}
+
+static double wtime(void) {
+#ifdef _OPENMP
+    return omp_get_wtime();
+#else
+    return 0.0;
+#endif
+}
+
+/* weight[N], cov[N]; returns 0 or -1 (empty graph: ValueError).  t_phase (optional): seconds of
+ * [kinds + preference, iterations + weights] */
+static int pagerank_core(const ograph* g, int anomaly, int iters, double* weight, int32_t* cov, double* kind_out,
+                         int hashed_kinds, double* t_phase) {
+    const int32_t N = g->N, T = g->T;
+    if (N == 0 || T == 0) return -1;
+    const double d = 0.85, alpha = 0.01;
+    const double t0 = wtime();
+    double* kind = (double*)malloc(sizeof(double) * T);
+    if (hashed_kinds) kinds_hashed(g, kind);
+    else kinds_sorted(g, kind);
     if (kind_out) memcpy(kind_out, kind, sizeof(double) * T);
     /* preference (:68-85), sequential sums in trace order (T7), stored fp32 */
     float* v = (float*)malloc(sizeof(float) * T);
@@ -231,6 +289,7 @@ int oracle_pagerank(const ograph* g, int anomaly, int iters, double* weight, int
         for (int32_t t = 0; t < T; ++t) v[t] = (float)(1.0 / (kind[t] / ks * 0.5 + 1.0 / (double)g->len_t[t]) / ns * 0.5);
     }
     const float cd = (float)(1.0 - d);
+    const double t1 = wtime();
     double *s = (double*)malloc(sizeof(double) * N), *r = (double*)malloc(sizeof(double) * T);
     double *s2 = (double*)malloc(sizeof(double) * N), *r2 = (double*)malloc(sizeof(double) * T);
     double *wt = (double*)malloc(sizeof(double) * T), *uo = (double*)malloc(sizeof(double) * N);
@@ -241,13 +300,44 @@ int oracle_pagerank(const ograph* g, int anomaly, int iters, double* weight, int
         uo[o] = g->len_o[o] ? (double)(float)(1.0 / g->len_o[o]) : 0.0;
         pw[o] = g->nchild[o] ? (double)(float)(1.0 / g->nchild[o]) : 0.0;
     }
+    /* hashed_kinds (large graphs): P_sr r as per-thread trace-range partials summed in thread order
+     * (the root op is in every trace: an op-parallel loop would leave it to one thread) */
+    int nthr = 1;
+#ifdef _OPENMP
+    if (hashed_kinds) nthr = omp_get_max_threads();
+#endif
+    double* part = hashed_kinds ? (double*)malloc(sizeof(double) * (size_t)N * nthr) : NULL;
     for (int it = 0; it < iters; ++it) {   /* Jacobi update (T8), max normalisation (T3) */
+        if (part) {
+#pragma omp parallel num_threads(nthr)
+            {
+                int tid = 0;
+#ifdef _OPENMP
+                tid = omp_get_thread_num();
+#endif
+                double* pp = part + (size_t)N * tid;
+                memset(pp, 0, sizeof(double) * N);
+                const int32_t t0_ = (int32_t)((int64_t)T * tid / nthr), t1_ = (int32_t)((int64_t)T * (tid + 1) / nthr);
+                for (int32_t t = t0_; t < t1_; ++t) {
+                    const double x = wt[t] * r[t];
+                    for (int64_t e = g->sr_off[t]; e < g->sr_off[t + 1]; ++e) pp[g->sr_ops[e]] += x;
+                }
+            }
+#pragma omp parallel for schedule(static, 256)
+            for (int32_t o = 0; o < N; ++o) {
+                double a = 0.0, b = 0.0;
+                for (int k = 0; k < nthr; ++k) a += part[(size_t)N * k + o];
+                for (int64_t e = g->ss_off[o]; e < g->ss_off[o + 1]; ++e) b += pw[g->ss_par[e]] * s[g->ss_par[e]];
+                s2[o] = d * (a + alpha * b);
+            }
+        } else {
 #pragma omp parallel for schedule(dynamic, 64)
-        for (int32_t o = 0; o < N; ++o) {
-            double a = 0.0, b = 0.0;
-            for (int64_t e = g->op_off[o]; e < g->op_off[o + 1]; ++e) a += wt[g->op_trs[e]] * r[g->op_trs[e]];
-            for (int64_t e = g->ss_off[o]; e < g->ss_off[o + 1]; ++e) b += pw[g->ss_par[e]] * s[g->ss_par[e]];
-            s2[o] = d * (a + alpha * b);
+            for (int32_t o = 0; o < N; ++o) {
+                double a = 0.0, b = 0.0;
+                for (int64_t e = g->op_off[o]; e < g->op_off[o + 1]; ++e) a += wt[g->op_trs[e]] * r[g->op_trs[e]];
+                for (int64_t e = g->ss_off[o]; e < g->ss_off[o + 1]; ++e) b += pw[g->ss_par[e]] * s[g->ss_par[e]];
+                s2[o] = d * (a + alpha * b);
+            }
         }
 #pragma omp parallel for schedule(static, 1024)
         for (int32_t t = 0; t < T; ++t) {
@@ -267,8 +357,16 @@ int oracle_pagerank(const ograph* g, int anomaly, int iters, double* weight, int
         weight[o] = s[o] * total / (double)N;
         cov[o] = (int32_t)(g->op_off[o + 1] - g->op_off[o]);
     }
-    free(kind); free(v); free(s); free(r); free(s2); free(r2); free(wt); free(uo); free(pw);
+    free(kind); free(v); free(s); free(r); free(s2); free(r2); free(wt); free(uo); free(pw); free(part);
+    if (t_phase) {
+        t_phase[0] = t1 - t0;
+        t_phase[1] = wtime() - t1;
+    }
     return 0;
+}
+
+int oracle_pagerank(const ograph* g, int anomaly, int iters, double* weight, int32_t* cov, double* kind_out) {
+    return pagerank_core(g, anomaly, iters, weight, cov, kind_out, 0, NULL);
 }
 
 /* ---------------------------------------------------------------- spectrum (online_rca.py:33-152) */
@@ -427,5 +525,47 @@ int oracle_graph_pagerank(int64_t S, const int32_t* trace, const int32_t* podop,
     if (rc == 0) memcpy(node_podop, g.node_podop, sizeof(int32_t) * g.N);
     free(id_off); free(id_rows);
     ograph_free(&g);
+    return rc;
+}
+
+/* ---------------------------------------------------------------- a graph given as incidence lists
+ * trace_pagerank (pagerank.py:15-130) of a graph built elsewhere (bench.py's C4 CPU baseline: the
+ * same synthetic graph the GPU ranks).  sr_off/sr_ops: trace-major distinct ops (ascending);
+ * ss_off/ss_par: parents by child.  The op-major copy is built before the clock starts.
+ * nthreads 0: OpenMP default.  t_phase[2]: seconds of kinds + preference, iterations + weights. */
+int oracle_incidence_pagerank(int32_t N, int32_t T, const int64_t* sr_off, const int32_t* sr_ops, const int32_t* len_t,
+                              const int32_t* len_o, const int64_t* ss_off, const int32_t* ss_par,
+                              const int32_t* nchild, int anomaly, int iters, int nthreads, double* weight,
+                              int32_t* cov, double* t_phase) {
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#else
+    (void)nthreads;
+#endif
+    ograph g;
+    memset(&g, 0, sizeof g);
+    g.N = N;
+    g.T = T;
+    g.nnz = sr_off[T];
+    g.E = ss_off[N];
+    g.sr_off = (int64_t*)sr_off;
+    g.sr_ops = (int32_t*)sr_ops;
+    g.len_t = (int32_t*)len_t;
+    g.len_o = (int32_t*)len_o;
+    g.nchild = (int32_t*)nchild;
+    g.ss_off = (int64_t*)ss_off;
+    g.ss_par = (int32_t*)ss_par;
+    g.op_off = (int64_t*)calloc((size_t)N + 1, sizeof(int64_t));
+    g.op_trs = (int32_t*)malloc(sizeof(int32_t) * (g.nnz ? g.nnz : 1));
+    for (int64_t e = 0; e < g.nnz; ++e) g.op_off[sr_ops[e] + 1]++;
+    for (int32_t o = 0; o < N; ++o) g.op_off[o + 1] += g.op_off[o];
+    int64_t* pos = (int64_t*)malloc(sizeof(int64_t) * (N ? N : 1));
+    memcpy(pos, g.op_off, sizeof(int64_t) * N);
+    for (int32_t t = 0; t < T; ++t)
+        for (int64_t e = sr_off[t]; e < sr_off[t + 1]; ++e) g.op_trs[pos[sr_ops[e]]++] = t;
+    free(pos);
+    int rc = pagerank_core(&g, anomaly, iters, weight, cov, NULL, 1, t_phase);
+    free(g.op_off);
+    free(g.op_trs);
     return rc;
 }

@@ -135,8 +135,9 @@ def trace_kinds(g: Graph) -> np.ndarray:
     return counts[kid].astype(np.float64)
 
 
-def preference(g: Graph, kind: np.ndarray, anomaly: bool) -> np.ndarray:
-    """pagerank.py:68-85 -- sequential fp64 sums in pr_trace order (T7), stored as fp32."""
+def preference(g: Graph, kind: np.ndarray, anomaly: bool, phi: float = 0.5) -> np.ndarray:
+    """pagerank.py:68-85 -- sequential fp64 sums in pr_trace order (T7), stored as fp32.  phi: the
+    two 0.5 weights of the anomaly form (:82-84), a keyword of the build's surface."""
     pr = np.zeros(g.T, dtype=np.float32)
     if not anomaly:
         s = 0.0
@@ -151,7 +152,7 @@ def preference(g: Graph, kind: np.ndarray, anomaly: bool) -> np.ndarray:
             ks += 1.0 / kind[t]
             ns += 1.0 / ln  # ZeroDivisionError for an empty list, as in the reference
         for t, ln in zip(g.pr_idx, g.pr_len):
-            pr[t] = 1.0 / (kind[t] / ks * 0.5 + 1.0 / ln) / ns * 0.5
+            pr[t] = 1.0 / (kind[t] / ks * phi + 1.0 / ln) / ns * phi
     return pr
 
 
@@ -203,12 +204,14 @@ def weights(g: Graph, s: np.ndarray):
 
 
 def trace_pagerank(operation_operation, operation_trace, trace_operation, pr_trace, anomaly,
-                   precision: str = "fp64"):
-    """pagerank.trace_pagerank (pagerank.py:15-112)."""
+                   precision: str = "fp64", d: float = D_DEFAULT, alpha: float = ALPHA_DEFAULT,
+                   iters: int = ITERS_DEFAULT, phi: float = 0.5):
+    """pagerank.trace_pagerank (pagerank.py:15-112); d / alpha / iters / phi default to the
+    reference's hard-coded values (:116-117, :82-84)."""
     g = graph_from_dicts(operation_operation, operation_trace, trace_operation, pr_trace)
     kind = trace_kinds(g)
-    v = preference(g, kind, anomaly)
-    s = power_iteration(g, v, precision=precision)
+    v = preference(g, kind, anomaly, phi)
+    s = power_iteration(g, v, d, alpha, iters, precision=precision)
     return weights(g, s)
 
 

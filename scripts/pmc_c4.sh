@@ -1,7 +1,7 @@
 #!/bin/bash
 # PMC passes over the C4 iteration kernel (one rocprofv3 run per counter group, <= 8 SQ each).
 #   scripts/pmc_c4.sh TAG [kernel-pattern] [config]   (GPU box; summaries to gpurun_out/pmc_TAG_*.txt)
-TAG=${1:-c4}; PAT=${2:-k_wv_a}; CFG=${3:-c4}; OPS=${OPS:-10000}; TRACES=${TRACES:-10000000}
+TAG=${1:-c4}; PAT=${2:-k_tr_a}; CFG=${3:-c4}; OPS=${OPS:-10000}; TRACES=${TRACES:-10000000}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 i=0

@@ -282,8 +282,62 @@ def stream_case(name, params, outdir):
           res["driver_stdout"].count("anomaly_list"), "time %.1fs" % res["timing_s"])
 
 
+C3_WINDOW = dict(n_ops=500, n_traces=20_000, seed=4242, branch=1.9, p_max=0.8, fault_ms=6000.0)
+
+
+def c3_window_case(outdir):
+    """One C3-sized window (BASELINE configs[2]: 500 ops / 20k traces) through the reference's
+    per-window body (online_rca.py:167-201): detector, the two swapped graphs (T1), both
+    trace_pagerank calls and the DStar2 spectrum.  Lean on purpose (no extra flavours, no driver
+    re-run): the two trace_pagerank calls alone take minutes (O(T^2) kinds, pagerank.py:54-66).
+    Only outputs are stored; the inputs are re-created by synth from the recorded params."""
+    ndf, adf = make_windows(**C3_WINDOW)
+    res = {"name": "c3_window", "params": C3_WINDOW}
+    span_df = ndf.copy()
+    op_list = ref_pp.get_service_operation_list(span_df)
+    slo = ref_pp.get_operation_slo(op_list, span_df)
+    res["operation_list"] = op_list
+    res["slo"] = {k: [fhex(v[0]), fhex(v[1])] for k, v in slo.items()}
+    start = adf["startTime"].min()
+    end = start + pd.Timedelta(minutes=5)
+    buf = io.StringIO()
+    t0 = time.perf_counter()
+    with contextlib.redirect_stdout(buf):
+        flag, abn, nor = ref_det.system_anomaly_detect(adf, start_time=start, end_time=end, slo=slo,
+                                                       operation_list=op_list)
+    tn = sorted(adf["traceID"].unique())
+    ti = {n: i for i, n in enumerate(tn)}
+    res["detect"] = {"flag": bool(flag), "abnormal": [ti[x] for x in abn], "normal": [ti[x] for x in nor],
+                     "stdout": buf.getvalue(), "start_ns": int(start.value), "end_ns": int(end.value)}
+    g_n = ref_pp.get_pagerank_graph(abn, adf)
+    g_a = ref_pp.get_pagerank_graph(nor, adf)
+    res["nodes_normal"] = list(g_n[0].keys())
+    res["nodes_anomaly"] = list(g_a[0].keys())
+    t1 = time.perf_counter()
+    w_n, c_n = ref_pr.trace_pagerank(*g_n, False)
+    w_a, c_a = ref_pr.trace_pagerank(*g_a, True)
+    t2 = time.perf_counter()
+    res["pr_normal"] = dump_pr(w_n, c_n)
+    res["pr_anomaly"] = dump_pr(w_a, c_a)
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        top, score = ref_rca.calculate_spectrum_without_delay_list(
+            anomaly_result=w_a, normal_result=w_n, anomaly_list_len=len(nor), normal_list_len=len(abn), top_max=5,
+            normal_num_list=c_n, anomaly_num_list=c_a, spectrum_method="dstar2")
+    res["spectrum_dstar2"] = {"top": list(top), "score": [fhex(s) for s in score], "stdout": buf.getvalue()}
+    res["timing_s"] = {"detect+graphs": t1 - t0, "trace_pagerank_x2": t2 - t1}
+    res["input_digest"] = {"normal": synth.frame_digest(ndf), "abnormal": synth.frame_digest(adf)}
+    with open(os.path.join(outdir, "c3_window.json"), "w") as f:
+        json.dump(res, f, indent=0)
+    print("c3_window traces", adf.traceID.nunique(), "spans", len(adf), "abn", len(abn), "nor", len(nor),
+          "pr time %.1fs" % (t2 - t1))
+
+
 def main():
     outdir = HERE
+    if sys.argv[1:] == ["c3_window"]:
+        c3_window_case(outdir)
+        return
     if sys.argv[1:] == ["stream"]:
         for name, params in STREAM_CASES.items():
             stream_case(name, params, outdir)

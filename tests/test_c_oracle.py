@@ -85,3 +85,26 @@ def test_c_restatement_under_asan_ubsan(name, tmp_path):
     assert [c for c, _ in got] == list(codes)
     assert [s for _, s in got] == list(scores)
     assert [st.podop_names[c] for c, _ in got] == case["spectrum"]["dstar2"]["top"]
+
+
+@pytest.mark.parametrize("anomaly", [False, True])
+def test_c_incidence_pagerank_matches_numpy_oracle(anomaly):
+    """oracle_incidence_pagerank (bench.py's C4 CPU baseline: hashed kinds, OpenMP iterations) on
+    a power-law incidence graph equals the numpy oracle (1e-12) with the same coverage, on one
+    thread and on four."""
+    from microrank_amd import synth
+
+    hg = synth.big_graph(300, 30_000, seed=3)
+    T, N = hg.T, hg.N
+    sr_t = np.repeat(np.arange(T, dtype=np.int64), np.diff(hg.sr_off))
+    ss_c = np.repeat(np.arange(N, dtype=np.int64), np.diff(hg.ss_off))
+    g = orc.Graph(list(range(N)), list(range(T)), sr_t, hg.sr_ops.astype(np.int64), sr_t,
+                  hg.sr_ops.astype(np.int64), hg.len_t, hg.len_o, ss_c, hg.ss_par.astype(np.int64), hg.nchild,
+                  np.arange(T), hg.len_t.copy())
+    s = orc.power_iteration(g, orc.preference(g, orc.trace_kinds(g), anomaly))
+    w_ref, cov_ref = orc.weights(g, s)
+    for nt in (1, 4):
+        w, cov, tp = c_oracle.incidence_pagerank(hg, anomaly, nthreads=nt)
+        np.testing.assert_array_equal(cov, np.array(list(cov_ref.values())))
+        np.testing.assert_allclose(w, np.array(list(w_ref.values())), rtol=1e-12, atol=0)
+        assert tp[0] > 0 and tp[1] > 0

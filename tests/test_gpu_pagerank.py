@@ -352,30 +352,104 @@ def test_c4_full_scale_properties():
     dg.close()
 
 
-def test_c5_op_space_properties():
-    """BASELINE configs[4]'s op space (100k ops: the wide fused iteration, hot ops through k_tr_a,
-    the cold tail through k_cold_trace / k_cold_ops) over 10M traces: bitwise fp32 reruns,
-    coverage summing to the pairs, fp32 within 1e-4 of fp64 (the north star's fp32 tolerance) with
-    the same top-5, and fp64 satisfying the max-normalisation identity."""
+def test_c5_full_scale_properties():
+    """BASELINE configs[4] at its stated size: 100k ops / 100M traces (1.5G distinct pairs, power-law
+    op popularity, the root op in every trace) -- the wide fused iteration (hot ops through k_tr_a,
+    the cold tail through k_cold_trace / k_cold_ops).  No oracle finishes at this size, so
+    size-independent properties: bitwise reruns in fp32 and fp64, coverage summing to the pairs,
+    the max-normalisation identity (pagerank.py:107: N sum(w) = (N max(w))^2) in both precisions,
+    fp32 within 1e-4 of fp64 (the north star's fp32 tolerance) with the same top-5."""
     from microrank_amd import _lib, synth
     from microrank_amd.graph import DeviceGraph
 
-    hg = synth.big_graph(100_000, 10_000_000, seed=12)
+    hg = synth.big_graph(100_000, 100_000_000, seed=12)
     nnz = int(hg.sr_ops.size)
+    assert nnz > 2**30
     ctx = _lib.default_context()
     dg = DeviceGraph.upload(ctx, hg)
     del hg
-    dg.pagerank(True, precision="fp32")
-    w32, cov = dg.fetch()
-    dg.pagerank(True, precision="fp32")
-    w32b, _ = dg.fetch()
-    assert w32.tobytes() == w32b.tobytes()
-    assert int(cov.astype(np.int64).sum()) == nnz
-    dg.pagerank(True, precision="fp64")
-    w64, _ = dg.fetch()
-    N = w64.size
-    np.testing.assert_allclose(N * w64.sum(), (N * w64.max()) ** 2, rtol=1e-9)
-    big = w64 > 1e-6 * w64.max()
-    np.testing.assert_allclose(w32[big], w64[big], rtol=1e-4)
-    assert list(np.argsort(-w32, kind="stable")[:5]) == list(np.argsort(-w64, kind="stable")[:5])
+    res = {}
+    for prec in ("fp32", "fp64"):
+        dg.pagerank(True, precision=prec)
+        w, cov = dg.fetch()
+        dg.pagerank(True, precision=prec)
+        w2, _ = dg.fetch()
+        assert w.tobytes() == w2.tobytes(), prec
+        assert int(cov.astype(np.int64).sum()) == nnz
+        N = w.size
+        np.testing.assert_allclose(N * w.sum(), (N * w.max()) ** 2, rtol=1e-9 if prec == "fp64" else 1e-5)
+        res[prec] = w
+    big = res["fp64"] > 1e-6 * res["fp64"].max()
+    np.testing.assert_allclose(res["fp32"][big], res["fp64"][big], rtol=1e-4)
+    assert list(np.argsort(-res["fp32"], kind="stable")[:5]) == list(np.argsort(-res["fp64"], kind="stable")[:5])
     dg.close()
+
+
+@pytest.mark.parametrize("precision", ["fp64", "fp32"])
+def test_wide_span_graph_with_broken_traces_against_oracle(precision):
+    """C5's span form at oracle size: 60k ops / 40k traces of spans with 5 % broken traces (a
+    dropped parent span: orphans, T11) and 1 % duplicated root spanIDs, built on the device (K1,
+    mr_graph_build) into a graph wide enough for the wide fused iteration (N > 16384), then ranked:
+    node order, coverage and weights against the oracle's span_graph + trace_pagerank (fp64 1e-10,
+    fp32 1e-4)."""
+    from microrank_amd import _lib, synth
+    from microrank_amd.graph import DeviceGraph
+    from microrank_amd.preprocess_data import DeviceSpans
+    import ctypes as C
+    from microrank_amd._lib import ptr
+
+    st = synth.big_spans(60_000, 40_000, seed=21, dup_frac=0.01, broken_frac=0.05)
+    # spread the non-root spans' ops over the op space (per-trace offsets), so ~59k ops appear
+    op = st.podop.astype(np.int64)
+    st.podop = st.svcop = np.where(st.parent < 0, op, (op + (st.trace.astype(np.int64) % 997) * 61) % 60_000
+                                   ).astype(np.int32)
+    sel = np.ones(st.n_traces, bool)
+    sel[::7] = False                                    # a trace_list that is not every trace
+    sg = orc.span_graph(st.trace, st.podop, st.span, st.parent, sel)
+    g = sg.as_graph()
+    assert g.N > 16384 and g.ss_c.size > 0
+    s = orc.power_iteration(g, orc.preference(g, orc.trace_kinds(g), True))
+    w_ref, cov_ref = orc.weights(g, s)
+    ctx = _lib.default_context()
+    dev = DeviceSpans(ctx, st)
+    lib = _lib.load()
+    mask = sel.astype(np.uint8)
+    h = _lib.P()
+    ctx.check(lib.mr_graph_build(ctx.h, dev.h, ptr(mask, C.c_uint8), C.byref(h)), "mr_graph_build")
+    n, t, nnz, e = C.c_int32(), C.c_int32(), C.c_int64(), C.c_int64()
+    lib.mr_graph_info(h, C.byref(n), C.byref(t), C.byref(nnz), C.byref(e))
+    node = np.empty(n.value, np.int32)
+    tcode = np.empty(t.value, np.int32)
+    ctx.check(lib.mr_graph_nodes(h, ptr(node, C.c_int32), ptr(tcode, C.c_int32)), "mr_graph_nodes")
+    assert node.tolist() == list(sg.node_podop) and tcode.tolist() == list(sg.trace_codes)
+    assert (nnz.value, e.value) == (g.sr_o.size, g.ss_c.size)
+    dg = DeviceGraph(ctx, h, None, None, n.value, t.value)
+    dg.pagerank(True, precision=precision)
+    w, cov = dg.fetch()
+    np.testing.assert_array_equal(cov, np.array(list(cov_ref.values())))
+    np.testing.assert_allclose(w, np.array(list(w_ref.values())), rtol=RTOL64 if precision == "fp64" else RTOL32,
+                               atol=0)
+    dg.close()
+    dev.close()
+
+
+@pytest.mark.parametrize("anomaly", [False, True])
+def test_config_keywords_against_oracle(anomaly):
+    """d / alpha / iters / phi as keywords (pagerank.py:116-117, :82-84): non-default
+    values on the c1 window's graph equal the oracle run with the same values (1e-10)."""
+    from microrank_amd.pagerank import trace_pagerank
+    from conftest import regen_window
+
+    case = load_golden("c1.json")
+    _, adf = regen_window(case)
+    tnames = sorted(adf["traceID"].unique())
+    dicts = golden_graph_dicts(case["graph_swapped_anomaly"], tnames)
+    kw = dict(d=0.7, alpha=0.05, iters=10, phi=0.3)
+    w, num = trace_pagerank(*dicts, anomaly, **kw)
+    w_ref, num_ref = orc.trace_pagerank(*dicts, anomaly, **kw)
+    assert list(w) == list(w_ref) and num == num_ref
+    np.testing.assert_allclose(np.array(list(w.values())), np.array(list(w_ref.values())), rtol=1e-10, atol=0)
+    w0, _ = trace_pagerank(*dicts, anomaly)
+    assert [float(x) for x in w0.values()] != [float(x) for x in w.values()]
+    with pytest.raises(ValueError):
+        trace_pagerank(*dicts, anomaly, iters=-1)

@@ -554,3 +554,57 @@ def test_rca_stream_matches_offline_driver(name, minutes, tmp_path, monkeypatch)
     if case["result_csv"] is not None:
         got_csv = open("result.csv").read().splitlines()
         assert [r.split(",")[:-1] for r in got_csv] == [r.split(",")[:-1] for r in case["result_csv"].splitlines()]
+
+
+def test_c3_window_matches_reference_golden():
+    """One C3-sized window (BASELINE configs[2]: 500 ops / 20k traces, 471k spans) against the
+    REFERENCE's own outputs (tests/golden/c3_window.json, make_golden.py c3_window: 835 s of
+    reference trace_pagerank): SLO bit-exact, the detector's lists identical, both swapped graphs'
+    node order and weights (1e-10) and coverage, the DStar2 top-11 identical with scores at 1e-10 --
+    through the drop-in functions the unchanged driver calls (online_rca.py:167-201), and the
+    device window pipeline (mr_rca_window) giving the same top list."""
+    from microrank_amd import synth
+    from microrank_amd.anormaly_detector import system_anomaly_detect
+    from microrank_amd.online_rca import calculate_spectrum_without_delay_list, rca_window
+    from microrank_amd.pagerank import trace_pagerank
+    from microrank_amd.preprocess_data import (get_operation_slo, get_pagerank_graph,
+                                               get_service_operation_list)
+
+    case = load_golden("c3_window.json")
+    p = dict(case["params"])
+    ndf, adf = synth.window_dataframes(p.pop("n_ops"), p.pop("n_traces"), p.pop("seed"), **p)
+    assert synth.frame_digest(ndf) == case["input_digest"]["normal"]
+    assert synth.frame_digest(adf) == case["input_digest"]["abnormal"]
+    span_df = ndf.copy()
+    op_list = get_service_operation_list(span_df)
+    assert op_list == case["operation_list"]
+    slo = get_operation_slo(op_list, span_df)
+    assert {k: [v[0].hex(), v[1].hex()] for k, v in slo.items()} == case["slo"]
+    det = case["detect"]
+    start, end = pd.Timestamp(det["start_ns"]), pd.Timestamp(det["end_ns"])
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        flag, abn, nor = system_anomaly_detect(adf, start_time=start, end_time=end, slo=slo, operation_list=op_list)
+    assert buf.getvalue() == det["stdout"] and flag == det["flag"]
+    tn = sorted(adf["traceID"].unique())
+    assert abn == [tn[i] for i in det["abnormal"]] and nor == [tn[i] for i in det["normal"]]
+    w_n, c_n = trace_pagerank(*get_pagerank_graph(abn, adf), False)   # T1: the driver's swap
+    w_a, c_a = trace_pagerank(*get_pagerank_graph(nor, adf), True)
+    for got_w, got_c, key, nodes in ((w_n, c_n, "pr_normal", "nodes_normal"), (w_a, c_a, "pr_anomaly", "nodes_anomaly")):
+        exp = case[key]
+        assert list(got_w) == exp["keys"] == case[nodes] and list(got_c) == exp["num_keys"]
+        assert [int(v) for v in got_c.values()] == exp["num"]
+        np.testing.assert_allclose(np.array(list(got_w.values())), unhex(exp["weight"]), rtol=1e-10, atol=0)
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        top, score = calculate_spectrum_without_delay_list(
+            anomaly_result=w_a, normal_result=w_n, anomaly_list_len=len(nor), normal_list_len=len(abn), top_max=5,
+            normal_num_list=c_n, anomaly_num_list=c_a, spectrum_method="dstar2")
+    sp = case["spectrum_dstar2"]
+    assert list(top) == sp["top"]
+    np.testing.assert_allclose(np.array(score, dtype=np.float64), unhex(sp["score"]), rtol=1e-10, atol=0)
+    got_lines, exp_lines = buf.getvalue().splitlines(), sp["stdout"].splitlines()
+    assert [ln.split(":")[0] for ln in got_lines] == [ln.split(":")[0] for ln in exp_lines]
+    res = rca_window(adf, start, end, slo)
+    assert res["top"] == sp["top"] and (res["n_abnormal"], res["n_normal"]) == (len(abn), len(nor))
+    np.testing.assert_allclose(np.array(res["score"], dtype=np.float64), unhex(sp["score"]), rtol=1e-10, atol=0)
