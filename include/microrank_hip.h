@@ -274,6 +274,14 @@ int mr_comm_allreduce_f64(mr_ctx* ctx, double* dev_buf, int64_t n, int op /*0 su
 typedef int (*mr_host_coll_fn)(void* user, int coll, void* buf, int64_t n, int dtype, int op);
 int mr_comm_set_host(mr_ctx* ctx, mr_host_coll_fn fn, void* user, int nranks, int rank);
 
+/* One-shot peer all-reduce for the per-iteration exchange of mr_pagerank_sharded (collective:
+ * every rank of the context's backend calls it).  enable != 0: each rank exports a receive region
+ * (uncached device memory) by IPC and maps every other rank's; an iteration's P_sr r limbs are then
+ * written straight into every rank's region (xGMI stores between GPUs, one hop) and summed locally
+ * in rank order, instead of an RCCL ring all-reduce (2 (R - 1) dependent steps).  The handles are
+ * exchanged over the context's collectives on first use; enable = 0 unmaps them. */
+int mr_comm_peer_enable(mr_ctx* ctx, int enable);
+
 /* Trace-sharded PageRank: g holds THIS rank's traces (every span of
  * a trace on one rank) over the GLOBAL node index space, with this rank's partial len_o and
  * nchild and its local call edges.  Once per graph the library sums len_o / nchild / coverage,

@@ -140,3 +140,168 @@ int mr_coll_allgather(mr_ctx* ctx, const void* dsend, void* drecv, int64_t n, in
     MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));
     return MR_OK;
 }
+
+// ------------------------------------------------------------------------------ one-shot peer all-reduce
+// The per-iteration all-reduce of the trace-sharded PageRank (2N limb words + the r' maxima,
+// 160 KB at C4) is latency-bound: RCCL's ring takes 2 (R - 1) dependent steps.  Here every rank
+// writes its words straight into every rank's receive region (peer memory mapped by IPC: xGMI
+// stores on a node, the same HBM for ranks sharing one GPU), then signals with one system-scope
+// atomic add per block on each destination's flag word for it, and each rank sums the R slots of
+// its own region in rank order once all R flags have counted this round's blocks: one hop, exact
+// (integer sums), identical on every rank.  Regions are uncached device memory (no stale L2 lines
+// across devices); slots alternate by round parity, so a rank one round ahead never overwrites a
+// slot still being summed (its next push of that parity needs every rank's flag of the round
+// between).  Every spin is bounded (PEER_TIMEOUT): a missing peer becomes an error, not a hang.
+constexpr int PEER_FLAGS = 64;                         // flag words (<= 63 ranks) + the error word
+constexpr int PEER_T = 256;
+constexpr unsigned long long PEER_TIMEOUT = 200000000ull;   // 2 s of the 100 MHz s_memrealtime clock
+#define GLBP __attribute__((address_space(1)))
+
+__global__ void __launch_bounds__(PEER_T) k_peer_push(const unsigned long long* __restrict__ src, int64_t n,
+                                                      unsigned long long* const* __restrict__ peers, int nranks, int rank,
+                                                      int64_t W, uint64_t seq) {
+    const int64_t j = (int64_t)blockIdx.x * PEER_T + threadIdx.x;
+    const unsigned long long v = j < n ? src[j] : 0ull;
+    const size_t slot = (size_t)PEER_FLAGS + ((size_t)(seq & 1) * nranks + rank) * (size_t)W;
+    for (int r = 0; r < nranks; ++r)
+        if (j < n)
+            __hip_atomic_store((GLBP unsigned long long*)peers[r] + slot + j, v, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x < nranks) {   // this block's words are out: count it in every destination's flag
+        __atomic_thread_fence(__ATOMIC_RELEASE);
+        __hip_atomic_fetch_add((GLBP unsigned long long*)peers[threadIdx.x] + rank, 1ull, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+template <class T>
+__global__ void __launch_bounds__(PEER_T) k_peer_reduce(T* __restrict__ dst, int64_t n,
+                                                        unsigned long long* __restrict__ region, int nranks, int64_t W,
+                                                        uint64_t seq, unsigned long long need) {
+    __shared__ int s_ok;
+    GLBP unsigned long long* reg = (GLBP unsigned long long*)region;
+    if (threadIdx.x == 0) {
+        s_ok = 1;
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        for (int r = 0; r < nranks && s_ok; ++r)
+            while (__hip_atomic_load(reg + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < need) {
+                __builtin_amdgcn_s_sleep(2);
+                if (__builtin_amdgcn_s_memrealtime() - t0 > PEER_TIMEOUT) {
+                    s_ok = 0;
+                    __hip_atomic_store(reg + (PEER_FLAGS - 1), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    break;
+                }
+            }
+        __atomic_thread_fence(__ATOMIC_ACQUIRE);
+    }
+    __syncthreads();
+    if (!s_ok) return;
+    const int64_t j = (int64_t)blockIdx.x * PEER_T + threadIdx.x;
+    if (j >= n) return;
+    const size_t base = (size_t)PEER_FLAGS + (size_t)(seq & 1) * nranks * (size_t)W + (size_t)j;
+    T s = (T)0;
+    for (int r = 0; r < nranks; ++r) {   // rank order: the same sum, bit for bit, on every rank
+        const unsigned long long w = __hip_atomic_load(reg + base + (size_t)r * W, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_SYSTEM);
+        if constexpr (sizeof(T) == 8 && (T)0.5 != (T)0) s += __longlong_as_double((long long)w);
+        else s += (T)w;
+    }
+    dst[j] = s;
+}
+
+void mr_comm_peer_destroy(mr_ctx* ctx) {
+    if (!ctx) return;
+    if (ctx->peer_region) (void)hipStreamSynchronize(ctx->stream);
+    for (size_t r = 0; r < ctx->peer_map.size(); ++r)
+        if (ctx->peer_map[r] && (int)r != ctx->rank) (void)hipIpcCloseMemHandle(ctx->peer_map[r]);
+    ctx->peer_map.clear();
+    if (ctx->peer_region) (void)hipFree(ctx->peer_region);
+    if (ctx->peer_dev) (void)hipFree(ctx->peer_dev);
+    ctx->peer_region = nullptr;
+    ctx->peer_dev = nullptr;
+    ctx->peer_words = 0;
+    ctx->peer_seq = 0;
+}
+
+// (collective) a receive region of at least `words` words per slot on every rank, mapped everywhere
+static int peer_ensure(mr_ctx* ctx, int64_t words) {
+    if (ctx->peer_region && ctx->peer_words >= words) return MR_OK;
+    const int R = ctx->nranks;
+    if (R > PEER_FLAGS - 1) return mr_fail(ctx, MR_ERR_ARG, "peer all-reduce: at most %d ranks", PEER_FLAGS - 1);
+    mr_comm_peer_destroy(ctx);
+    const size_t bytes = ((size_t)PEER_FLAGS + 2 * (size_t)R * (size_t)words) * sizeof(unsigned long long);
+    MR_TRY_HIP(ctx, hipExtMallocWithFlags(&ctx->peer_region, bytes, hipDeviceMallocUncached));
+    MR_TRY_HIP(ctx, hipMemsetAsync(ctx->peer_region, 0, bytes, ctx->stream));
+    MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    ctx->peer_words = words;
+    ctx->peer_seq = 0;
+    hipIpcMemHandle_t mine;
+    MR_TRY_HIP(ctx, hipIpcGetMemHandle(&mine, ctx->peer_region));
+    static_assert(sizeof(hipIpcMemHandle_t) % 8 == 0, "IPC handle size");
+    const int64_t hw = (int64_t)(sizeof(hipIpcMemHandle_t) / 8);
+    DBuf<uint64_t> hs, all;
+    MR_TRY(hs.upload(ctx, (const uint64_t*)&mine, (size_t)hw));
+    MR_TRY(all.alloc(ctx, (size_t)hw * R));
+    MR_TRY(mr_coll_allgather(ctx, hs.p, all.p, hw, MR_DT_U64));
+    std::vector<hipIpcMemHandle_t> hh((size_t)R);
+    MR_TRY_HIP(ctx, hipMemcpyAsync(hh.data(), all.p, sizeof(hipIpcMemHandle_t) * R, hipMemcpyDeviceToHost, ctx->stream));
+    MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    ctx->peer_map.assign((size_t)R, nullptr);
+    for (int r = 0; r < R; ++r) {
+        if (r == ctx->rank) {
+            ctx->peer_map[(size_t)r] = ctx->peer_region;
+            continue;
+        }
+        hipError_t e = hipIpcOpenMemHandle(&ctx->peer_map[(size_t)r], hh[(size_t)r], hipIpcMemLazyEnablePeerAccess);
+        if (e != hipSuccess) {
+            ctx->peer_map[(size_t)r] = nullptr;
+            return mr_fail(ctx, MR_ERR_COMM, "hipIpcOpenMemHandle(rank %d): %s", r, hipGetErrorString(e));
+        }
+    }
+    MR_TRY_HIP(ctx, hipMalloc((void**)&ctx->peer_dev, sizeof(void*) * R));
+    MR_TRY_HIP(ctx, hipMemcpy(ctx->peer_dev, ctx->peer_map.data(), sizeof(void*) * R, hipMemcpyHostToDevice));
+    // every rank's region is mapped before anyone pushes into it
+    DBuf<int32_t> one;
+    MR_TRY(one.zero(ctx, 1));
+    MR_TRY(mr_coll_allreduce(ctx, one.p, 1, MR_DT_I32, 0));
+    MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return MR_OK;
+}
+
+template <class T>
+static int peer_allreduce(mr_ctx* ctx, T* dbuf, int64_t n) {
+    if (!ctx->peer_on || ctx->nranks < 2 || !mr_coll_ready(ctx)) return MR_ERR_STATE;
+    MR_TRY(peer_ensure(ctx, n));
+    const int nb = cdiv(n, PEER_T);
+    const uint64_t seq = ctx->peer_seq++;
+    hipLaunchKernelGGL(k_peer_push, dim3(nb), dim3(PEER_T), 0, ctx->stream, (const unsigned long long*)dbuf, n,
+                       ctx->peer_dev, ctx->nranks, ctx->rank, ctx->peer_words, seq);
+    hipLaunchKernelGGL(k_peer_reduce<T>, dim3(nb), dim3(PEER_T), 0, ctx->stream, dbuf, n,
+                       (unsigned long long*)ctx->peer_region, ctx->nranks, ctx->peer_words, seq,
+                       (unsigned long long)nb * (seq + 1));
+    MR_TRY_HIP(ctx, hipGetLastError());
+    return MR_OK;
+}
+int mr_peer_allreduce_u64(mr_ctx* ctx, unsigned long long* dbuf, int64_t n) { return peer_allreduce(ctx, dbuf, n); }
+int mr_peer_allreduce_f64(mr_ctx* ctx, double* dbuf, int64_t n) { return peer_allreduce(ctx, dbuf, n); }
+
+// a peer that never arrived (k_peer_reduce's timeout) is reported by the caller's read-back
+int mr_peer_error(mr_ctx* ctx, bool* failed) {
+    *failed = false;
+    if (!ctx->peer_region) return MR_OK;
+    unsigned long long w = 0;
+    MR_TRY_HIP(ctx, hipMemcpyAsync(&w, (unsigned long long*)ctx->peer_region + (PEER_FLAGS - 1), 8,
+                                   hipMemcpyDeviceToHost, ctx->stream));
+    MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    *failed = w != 0;
+    return MR_OK;
+}
+
+extern "C" int mr_comm_peer_enable(mr_ctx* ctx, int enable) {
+    if (!ctx) return MR_ERR_ARG;
+    if (!enable) mr_comm_peer_destroy(ctx);
+    ctx->peer_on = enable != 0;
+    return MR_OK;
+}

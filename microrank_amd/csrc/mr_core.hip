@@ -63,7 +63,9 @@ extern "C" int mr_ctx_create(int device, uint32_t flags, mr_ctx** out) {
     return MR_OK;
 }
 
-void mr_comm_destroy(mr_ctx* ctx);  // mr_comm.cpp
+void mr_comm_destroy(mr_ctx* ctx);  // mr_comm.hip
+
+void mr_graph_delete(mr_graph* g) { delete g; }
 
 // ------------------------------------------------------------------------------ pool
 static size_t pool_round(size_t b) {
@@ -72,9 +74,33 @@ static size_t pool_round(size_t b) {
     return (b + (1u << 20) - 1) & ~(size_t)((1u << 20) - 1);
 }
 
+// Give cached device memory back to the driver after an allocation failed: this context's free
+// blocks, the window graphs it holds for release by its next mr_windows_batch call, and its
+// auxiliary contexts' free blocks (each stream synchronised first: a free block may still be read
+// by work queued before it was freed).  Called without the context's pool lock held.
+static void pool_trim(mr_ctx* ctx) {
+    (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->side) (void)hipStreamSynchronize(ctx->side);
+    for (mr_ctx* a : ctx->aux) (void)hipStreamSynchronize(a->stream);
+    std::vector<struct mr_graph*> dead;
+    dead.swap(ctx->graveyard);
+    for (struct mr_graph* g : dead) mr_graph_delete(g);   // (their blocks return to the aux pools)
+    auto drain = [](mr_ctx* c) {
+        std::lock_guard<std::mutex> lk(c->pool_mu);
+        for (auto& kv : c->pool_free)
+            for (void* q : kv.second) {
+                (void)hipFree(q);
+                c->pool_bytes -= kv.first;
+            }
+        c->pool_free.clear();
+    };
+    for (mr_ctx* a : ctx->aux) drain(a);
+    drain(ctx);
+}
+
 void* mr_pool_alloc(mr_ctx* ctx, size_t bytes) {
     const size_t want = pool_round(bytes);
-    std::lock_guard<std::mutex> lk(ctx->pool_mu);
+    std::unique_lock<std::mutex> lk(ctx->pool_mu);
     auto it = ctx->pool_free.lower_bound(want);
     if (it != ctx->pool_free.end() && it->first <= 2 * want) {   // reuse a block at most 2x too big
         void* p = it->second.back();   // (a class is erased when it empties: never empty here)
@@ -85,15 +111,14 @@ void* mr_pool_alloc(mr_ctx* ctx, size_t bytes) {
     }
     void* p = nullptr;
     if (hipMalloc(&p, want) != hipSuccess) {
-        // give the cached blocks back and retry once
-        (void)hipStreamSynchronize(ctx->stream);
-        for (auto& kv : ctx->pool_free)
-            for (void* q : kv.second) {
-                (void)hipFree(q);
-                ctx->pool_bytes -= kv.first;
-            }
-        ctx->pool_free.clear();
-        if (hipMalloc(&p, want) != hipSuccess) return nullptr;
+        (void)hipGetLastError();
+        lk.unlock();   // give the cached blocks back and retry once
+        pool_trim(ctx);
+        lk.lock();
+        if (hipMalloc(&p, want) != hipSuccess) {
+            (void)hipGetLastError();
+            return nullptr;
+        }
     }
     ctx->pool_bytes += want;
     ctx->pool_live[p] = want;
@@ -198,7 +223,7 @@ extern "C" void mr_ctx_destroy(mr_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
     if (ctx->side) (void)hipStreamSynchronize(ctx->side);
-    for (mr_graph* g : ctx->graveyard) delete g;   // (their blocks belong to the auxiliary contexts too)
+    for (mr_graph* g : ctx->graveyard) mr_graph_delete(g);   // (their blocks belong to the auxiliary contexts too)
     ctx->graveyard.clear();
     for (mr_ctx* a : ctx->aux) mr_ctx_destroy(a);
     ctx->aux.clear();
@@ -217,6 +242,7 @@ extern "C" void mr_ctx_destroy(mr_ctx* ctx) {
         }
         for (auto& m : mine) m.second(m.first);
     }
+    mr_comm_peer_destroy(ctx);
     mr_comm_destroy(ctx);
     prof_clear(ctx);
     mr_pool_release(ctx);

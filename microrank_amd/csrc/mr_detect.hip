@@ -754,6 +754,9 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
     for (auto& t : th) t.join();
     reaper.join();
     for (int k = 0; k < nthr; ++k) (void)hipStreamSynchronize(ctx->aux[(size_t)k]->stream);
+    // (an error may leave PageRank work queued on the main stream that still reads window graphs
+    // whose blocks return to the worker pools below: drain it first)
+    (void)hipStreamSynchronize(ctx->stream);
     for (hipEvent_t e : gev)
         if (e) (void)hipEventDestroy(e);
     MR_TRY(rc);

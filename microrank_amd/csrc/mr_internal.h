@@ -55,6 +55,18 @@ struct mr_ctx {
     // pinned host words for the small size read-backs of a call (a DMA straight into host memory
     // instead of the runtime's pageable staging path); created on first use
     int64_t* pin = nullptr;
+    // one-shot peer all-reduce (mr_comm_peer_enable; mr_comm.hip): a receive region in uncached
+    // device memory exported by IPC -- [flags: PEER_FLAGS u64][data: 2 parities x nranks x
+    // peer_words u64] -- and every rank's region mapped into this process (peer_map[rank] = ours)
+    bool peer_on = false;
+    void* peer_region = nullptr;
+    int64_t peer_words = 0;
+    std::vector<void*> peer_map;
+    unsigned long long** peer_dev = nullptr;   // device copy of peer_map
+    uint64_t peer_seq = 0;                      // all-reduces completed (the flags count them)
+    // k_pr_cluster timed out on this context (its clusters were not co-resident): launch per
+    // iteration from then on
+    bool no_persist = false;
     // status words of the single-pass scans (mr_prim.hip k_scan_dl): per-call epochs, no clearing
     unsigned long long* scan_st = nullptr;
     size_t scan_cap = 0;
@@ -62,6 +74,7 @@ struct mr_ctx {
 };
 
 void* mr_pool_alloc(mr_ctx* ctx, size_t bytes);
+void mr_graph_delete(struct mr_graph* g);   // delete a graph (defined where mr_graph is complete)
 void mr_pool_free(mr_ctx* ctx, void* p);
 void mr_pool_release(mr_ctx* ctx);
 // n (<= 64) int64 words from the device into out, through the context's pinned words; syncs the stream
@@ -171,6 +184,7 @@ struct mr_graph {
     DBuf<int32_t> coff;              // [n_wt+1] first chunk of a tile
     std::vector<int32_t> coff_h;     // host copy (the per-wave tile split of a launch)
     DBuf<float> w_tp, c_tp;          // [T] w_t, c_t in position order
+    DBuf<int32_t> hot;               // [HOT_N + 1] the layout's hot ops (tile chunk 0) and their count
     // kind compression (MR_PR_KIND_COMPRESS): a graph of one representative trace per kind whose
     // q carries the kind's multiplicity (mw_tp = w_t * mult in position order); kind = mult
     bool kinds_given = false;
@@ -317,6 +331,13 @@ enum { MR_DT_F64 = 0, MR_DT_I32 = 1, MR_DT_U64 = 2, MR_DT_I64 = 3 };
 int mr_coll_allreduce(mr_ctx* ctx, void* dbuf, int64_t n, int dtype, int op /*0 sum, 1 max*/);
 int mr_coll_allgather(mr_ctx* ctx, const void* dsend, void* drecv, int64_t n, int dtype);
 inline bool mr_coll_ready(const mr_ctx* ctx) { return ctx->comm || ctx->host_coll; }
+// SUM all-reduce of n uint64 words through the peer receive regions (one push to every rank, one
+// local sum in rank order); MR_ERR_STATE when the peer path is off (callers then use
+// mr_coll_allreduce).  Collective: every rank calls it with the same n.
+int mr_peer_allreduce_u64(mr_ctx* ctx, unsigned long long* dbuf, int64_t n);
+int mr_peer_allreduce_f64(mr_ctx* ctx, double* dbuf, int64_t n);   // (fp64 sums in rank order)
+int mr_peer_error(mr_ctx* ctx, bool* failed);   // a round timed out (a peer never pushed)
+void mr_comm_peer_destroy(mr_ctx* ctx);
 
 // MR_WIN_TIMING diagnostics: wall-clock phase marks (each mark synchronises the stream)
 struct PhaseTimer {

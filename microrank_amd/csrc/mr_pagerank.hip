@@ -392,12 +392,96 @@ __global__ void __launch_bounds__(TRB) k_tr_place(const int64_t* off, int32_t T,
     tr_place_body<TR_PER>((int32_t)blockIdx.x, off, T, nbin, boff, hist, taken, w_t, tperm, w_tp);
 }
 // chunks of 4 ids per wave tile (its last position holds its longest trace: lengths ascend), their
+// ---- hot chunk (k_tr_a's LDS traffic): an op in most traces (the root op in
+// every one) hits the same LDS accumulator word from every lane of a 16-lane atomic group -- a
+// 16-way serialised atomic no order of the ids avoids.  The HOT_N most covered ops (each in at
+// least 1/8 of the traces) get a fixed place instead: chunk 0 of every tile holds hot op q at
+// position q for the traces that have it (else the lane's pad).  k_tr_a adds X_t for them into
+// per-lane registers and folds those into the accumulator once per wave run; their su reads are
+// broadcasts.  hot[HOT_N] = how many hot ops the layout has (0: no hot chunk).
+// (2: the two per-lane u64 registers keep k_tr_a at 8 waves per SIMD; with 4 it drops to 7)
+constexpr int HOT_N = 2;
+static_assert(HOT_N >= 1 && HOT_N <= 4, "the hot chunk holds at most 4 positions");
+// the layout's hot ops (labels: perm maps a label to its op for relabelled graphs); one block
+__device__ __forceinline__ void hot_ops_body(const int32_t* __restrict__ cov, int32_t N, int32_t T,
+                                             const int32_t* __restrict__ perm, int32_t* __restrict__ hot) {
+    __shared__ unsigned long long red[256 / WAVE];
+    __shared__ int32_t chosen[HOT_N];
+    int n_hot = 0;
+    for (int h = 0; h < HOT_N; ++h) {
+        unsigned long long best = 0ull;   // (coverage << 32) | ~label: most covered, then lowest label
+        for (int32_t l = threadIdx.x; l < N; l += 256) {
+            bool taken = false;
+            for (int j = 0; j < h; ++j) taken = taken || chosen[j] == l;
+            if (taken) continue;
+            const uint32_t c = (uint32_t)cov[perm ? perm[l] : l];
+            best = max(best, ((unsigned long long)c << 32) | (unsigned long long)(0xffffffffu - (uint32_t)l));
+        }
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) best = max(best, (unsigned long long)__shfl_xor((long long)best, m, WAVE));
+        if ((threadIdx.x & (WAVE - 1)) == 0) red[threadIdx.x / WAVE] = best;
+        __syncthreads();
+        best = red[0];
+        for (int w = 1; w < 256 / WAVE; ++w) best = max(best, red[w]);
+        __syncthreads();
+        const int64_t c = (int64_t)(best >> 32);
+        if (best == 0ull || c * 8 < (int64_t)T) break;   // in fewer than 1/8 of the traces
+        if (threadIdx.x == 0) chosen[h] = (int32_t)(0xffffffffu - (uint32_t)(best & 0xffffffffull));
+        n_hot = h + 1;
+        __syncthreads();
+    }
+    if (threadIdx.x < HOT_N) hot[threadIdx.x] = (int32_t)threadIdx.x < n_hot ? chosen[threadIdx.x] : -1;
+    if (threadIdx.x == 0) hot[HOT_N] = n_hot;
+}
+__global__ void __launch_bounds__(256) k_hot_ops(const int32_t* __restrict__ cov, int32_t N, int32_t T,
+                                                 const int32_t* __restrict__ perm, int32_t* __restrict__ hot) {
+    hot_ops_body(cov, N, T, perm, hot);
+}
+__device__ __forceinline__ bool is_hot(uint32_t x, int32_t h0, int32_t h1, int32_t h2, int32_t h3) {
+    return (int32_t)x == h0 || (int32_t)x == h1 || (int32_t)x == h2 || (int32_t)x == h3;
+}
+// chunks of each wave tile with a hot chunk: 1 + ceil(max over its traces of the non-hot ids / 4);
+// a wave per tile
+__device__ __forceinline__ void tr_tnc_body(int32_t blk, const int32_t* tperm, const int64_t* off, const uint16_t* ids,
+                                            int32_t T, int32_t n_wt, const int32_t* hot, int32_t* tnc) {
+    const int64_t i = (int64_t)blk * blockDim.x + threadIdx.x;
+    const int32_t k = (int32_t)(i / WAVE), lane = (int32_t)(i % WAVE);
+    if (k >= n_wt) return;   // (whole waves: blockDim is a multiple of WAVE)
+    const int32_t hn = hot[HOT_N], h0 = hot[0], h1 = HOT_N > 1 ? hot[1] : -1, h2 = HOT_N > 2 ? hot[2] : -1,
+                  h3 = HOT_N > 3 ? hot[3] : -1;
+    const int64_t p = (int64_t)k * WAVE + lane;
+    int64_t m = 0;
+    if (p < T) {
+        const int32_t t = tperm[p];
+        const int64_t a = off[t], b = off[t + 1];
+        m = b - a;
+        if (hn > 0)
+            for (int64_t e = a; e < b; ++e) m -= is_hot(ids[e], h0, h1, h2, h3) ? 1 : 0;
+    }
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1) m = max(m, (int64_t)__shfl_xor((long long)m, s, WAVE));
+    if (lane == 0) tnc[k] = (int32_t)((hn > 0 ? 1 : 0) + ((m + 3) >> 2));
+}
+__global__ void k_tr_tnc(const int32_t* tperm, const int64_t* off, const uint16_t* ids, int32_t T, int32_t n_wt,
+                         const int32_t* hot, int32_t* tnc) {
+    tr_tnc_body((int32_t)blockIdx.x, tperm, off, ids, T, n_wt, hot, tnc);
+}
+// MR_TR_HOT=0: no hot chunk (A/B)
+static bool tr_hot_on() {
+    static const bool on = [] {
+        const char* e = getenv("MR_TR_HOT");
+        return !(e && !strcmp(e, "0"));
+    }();
+    return on;
+}
+
 // exclusive prefix and its int32 copy in one launch: runs of TS_TILE wave tiles per block, chained
 // by decoupled look-back
 constexpr int TS_T = 256, TS_I = 8, TS_TILE = TS_T * TS_I;
 __device__ __forceinline__ void tr_chunk_scan_body(int32_t tile_, int32_t ntiles, const int32_t* tperm,
                                                    const int64_t* off, int32_t T, int32_t n_wt, int64_t* c64,
-                                                   int32_t* coff, unsigned long long* st, uint64_t epoch) {
+                                                   int32_t* coff, unsigned long long* st, uint64_t epoch,
+                                                   const int32_t* tnc) {
     __shared__ int64_t sa[TS_T];
     __shared__ int64_t ex;
     const int tid = threadIdx.x;
@@ -408,8 +492,12 @@ __device__ __forceinline__ void tr_chunk_scan_body(int32_t tile_, int32_t ntiles
         const int64_t k = base + i;
         v[i] = 0;
         if (k < n_wt) {
-            const int32_t t = tperm[min(k * WAVE + WAVE - 1, (int64_t)T - 1)];
-            v[i] = (off[t + 1] - off[t] + 3) >> 2;
+            if (tnc) {   // (hot chunk layouts: counted by k_tr_tnc)
+                v[i] = tnc[k];
+            } else {
+                const int32_t t = tperm[min(k * WAVE + WAVE - 1, (int64_t)T - 1)];
+                v[i] = (off[t + 1] - off[t] + 3) >> 2;
+            }
         }
         a += v[i];
     }
@@ -443,8 +531,8 @@ __device__ __forceinline__ void tr_chunk_scan_body(int32_t tile_, int32_t ntiles
 }
 __global__ void __launch_bounds__(TS_T) k_tr_chunk_scan(const int32_t* tperm, const int64_t* off, int32_t T, int32_t n_wt,
                                                         int64_t* c64, int32_t* coff, unsigned long long* st,
-                                                        uint64_t epoch) {
-    tr_chunk_scan_body((int32_t)blockIdx.x, (int32_t)gridDim.x, tperm, off, T, n_wt, c64, coff, st, epoch);
+                                                        uint64_t epoch, const int32_t* tnc) {
+    tr_chunk_scan_body((int32_t)blockIdx.x, (int32_t)gridDim.x, tperm, off, T, n_wt, c64, coff, st, epoch, tnc);
 }
 __global__ void k_tr_coff(const int64_t* c64, int32_t n, int32_t* coff) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -512,7 +600,8 @@ __global__ void __launch_bounds__(TC_T) k_tr_cut_b(CutBatch b) {
 }
 // thread per (tile, lane): the lane's trace rotated by (trace mod len), then pads N + lane
 __device__ __forceinline__ void tr_fill_body(int32_t blk, const int32_t* tperm, const int64_t* off, const uint16_t* ids,
-                                             const int64_t* c64, int32_t T, int32_t N, int32_t n_wt, uint16_t* tids) {
+                                             const int64_t* c64, int32_t T, int32_t N, int32_t n_wt, uint16_t* tids,
+                                             const int32_t* hot) {
     const int64_t i = (int64_t)blk * blockDim.x + threadIdx.x;
     if (i >= (int64_t)n_wt * WAVE) return;
     const int32_t k = (int32_t)(i / WAVE), lane = (int32_t)(i % WAVE);
@@ -526,42 +615,157 @@ __device__ __forceinline__ void tr_fill_body(int32_t blk, const int32_t* tperm, 
     }
     const int64_t nc = c64[k + 1] - c64[k];
     unsigned long long* dst = (unsigned long long*)tids + (size_t)c64[k] * WAVE + lane;   // 4 ids per 8-B store
-    int64_t jj = rot;
-    for (int64_t c = 0; c < nc; ++c) {
+    const int32_t hn = hot ? hot[HOT_N] : 0;
+    const int32_t h0 = hn > 0 ? hot[0] : -1, h1 = hn > 0 && HOT_N > 1 ? hot[1] : -1,
+                  h2 = hn > 0 && HOT_N > 2 ? hot[2] : -1, h3 = hn > 0 && HOT_N > 3 ? hot[3] : -1;
+    int64_t c = 0;
+    if (hn > 0) {   // the hot chunk: hot op q at position q where the trace has it, else the pad
+        const int32_t hq[4] = {h0, h1, h2, h3};
         unsigned long long v = 0ull;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const int64_t j = 4 * c + q;
-            const uint16_t id = j < len ? ids[a + jj] : (uint16_t)(N + lane);
-            if (j < len && ++jj == len) jj = 0;
+            uint32_t id = (uint32_t)(N + lane);
+            if (q < hn)
+                for (int64_t e = a; e < a + len; ++e)
+                    if ((int32_t)ids[e] == hq[q]) {
+                        id = (uint32_t)hq[q];
+                        break;
+                    }
+            v |= (unsigned long long)(id & 0xffffu) << (16 * q);
+        }
+        dst[0] = v;
+        c = 1;
+    }
+    // the other ids from the rotation start (the hot ones skipped), padded with N + lane
+    int64_t jj = rot, used = 0;
+    for (; c < nc; ++c) {
+        unsigned long long v = 0ull;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            uint16_t id = (uint16_t)(N + lane);
+            while (used < len) {
+                const uint16_t x = ids[a + jj];
+                ++used;
+                if (++jj == len) jj = 0;
+                if (!is_hot(x, h0, h1, h2, h3)) {
+                    id = x;
+                    break;
+                }
+            }
             v |= (unsigned long long)id << (16 * q);
         }
         dst[(size_t)c * WAVE] = v;
     }
 }
 __global__ void k_tr_fill(const int32_t* tperm, const int64_t* off, const uint16_t* ids, const int64_t* c64, int32_t T,
-                          int32_t N, int32_t n_wt, uint16_t* tids) {
-    tr_fill_body((int32_t)blockIdx.x, tperm, off, ids, c64, T, N, n_wt, tids);
+                          int32_t N, int32_t n_wt, uint16_t* tids, const int32_t* hot) {
+    tr_fill_body((int32_t)blockIdx.x, tperm, off, ids, c64, T, N, n_wt, tids, hot);
+}
+// Bank-conflict-aware order of a tile's ids (k_tr_a's LDS traffic).  Per step
+// every lane reads su[o] (ds_read_b64: lanes in groups of 32, 8-B slot o mod 32) and adds into
+// lacc[o] (u64 LDS atomic: groups of 16, slot o mod 16; equal addresses serialise).  A trace's ops
+// can be walked in any order, so per 32-lane half of a tile one thread assigns each lane's items
+// (ops and pads) to steps greedily: lane by lane, the first remaining item whose atomic slot is
+// free in its 16-lane group and whose read slot is free (or holds the same op) in the half; else
+// one clear for the atomic; else any.  Pads (N + lane) are items too.  Tiles longer than
+// SCHED_L steps keep the rotated order.  Deterministic: a graph's layout (hence its fp64 sums) is
+// the same every time it is prepared.
+constexpr int SCHED_T = 16, SCHED_L = 64;
+__device__ __forceinline__ void tr_sched_body(int64_t u, const int32_t* coff, int32_t n_wt, uint16_t* tids,
+                                              uint16_t* items, unsigned long long* rem, uint16_t* cbuf,
+                                              const int32_t* hot) {
+    if (u >= 2 * (int64_t)n_wt) return;
+    const int32_t tile = (int32_t)(u >> 1), half = (int32_t)(u & 1);
+    const int32_t hc = hot && hot[HOT_N] > 0 ? 1 : 0;   // (the hot chunk keeps its fixed places)
+    const int32_t c0 = coff[tile] + hc, nc = coff[tile + 1] - c0, L = 4 * nc;
+    if (L > SCHED_L || nc <= 0) return;
+    unsigned long long* w = (unsigned long long*)tids + (size_t)c0 * WAVE + 32 * half;   // chunk c, lane li: w[c * WAVE + li]
+    for (int32_t c = 0; c < nc; ++c)
+        for (int li = 0; li < 32; ++li) {
+            const unsigned long long v = w[(size_t)c * WAVE + li];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) items[li * SCHED_L + 4 * c + q] = (uint16_t)(v >> (16 * q));
+        }
+    const unsigned long long full = L == 64 ? ~0ull : ((1ull << L) - 1ull);
+    for (int li = 0; li < 32; ++li) rem[li] = full;
+    for (int32_t s = 0; s < L; ++s) {
+        uint32_t used16[2] = {0u, 0u};
+        uint32_t occ32 = 0u;             // read slots taken this step ...
+        uint16_t op32[32];               // ... and by which op (a broadcast when equal)
+        for (int li = 0; li < 32; ++li) {
+            const int g = li >> 4;
+            const uint16_t* it = items + li * SCHED_L;
+            unsigned long long m = rem[li];
+            int best = -1, best_sc = 4;
+            while (m) {
+                const int j = __builtin_ctzll(m);
+                m &= m - 1ull;
+                const uint32_t o = it[j];
+                const uint32_t b16 = o & 15u, b32 = o & 31u;
+                const int sc = (int)((used16[g] >> b16) & 1u) * 2 + (int)(((occ32 >> b32) & 1u) && op32[b32] != o);
+                if (sc < best_sc) {
+                    best_sc = sc;
+                    best = j;
+                    if (sc == 0) break;
+                }
+            }
+            const uint32_t o = it[best];
+            rem[li] &= ~(1ull << best);
+            used16[g] |= 1u << (o & 15u);
+            if (!((occ32 >> (o & 31u)) & 1u)) {
+                occ32 |= 1u << (o & 31u);
+                op32[o & 31u] = (uint16_t)o;
+            }
+            cbuf[li * 4 + (s & 3)] = (uint16_t)o;
+        }
+        if ((s & 3) == 3)
+            for (int li = 0; li < 32; ++li) {
+                unsigned long long v = 0ull;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) v |= (unsigned long long)cbuf[li * 4 + q] << (16 * q);
+                w[(size_t)(s >> 2) * WAVE + li] = v;
+            }
+    }
+}
+__global__ void __launch_bounds__(SCHED_T) k_tr_sched(const int32_t* coff, int32_t n_wt, uint16_t* tids,
+                                                      const int32_t* hot) {
+    __shared__ uint16_t items[SCHED_T][32 * SCHED_L];
+    __shared__ unsigned long long rem[SCHED_T][32];
+    __shared__ uint16_t cbuf[SCHED_T][32 * 4];
+    tr_sched_body((int64_t)blockIdx.x * SCHED_T + threadIdx.x, coff, n_wt, tids, items[threadIdx.x], rem[threadIdx.x],
+                  cbuf[threadIdx.x], hot);
+}
+// MR_TR_SCHED=0: keep the rotated order (A/B)
+static bool tr_sched_on() {
+    static const bool on = [] {
+        const char* e = getenv("MR_TR_SCHED");
+        return !(e && !strcmp(e, "0"));
+    }();
+    return on;
 }
 // The prepare of several small fused graphs (a window's two) in one launch per step: block ranges
 // per graph, the same bodies (mr_graph_prepare_batch)
 struct PDev {
     int32_t T, N, nbin, W, nz, n_cs;
     int64_t nnz, st_off;
-    int32_t b_gc, b_th, b_cs, b_fill;
+    int32_t b_gc, b_th, b_cs, b_fill, b_sch;
     const int32_t *len_t, *len_o, *nchild, *rs_ops;
     const int64_t* rs_off;
     float *w_t, *u_o, *pw, *w_tp;
     uint16_t *rs16, *tids;
     int32_t *trz, *tperm, *coff;
     int64_t* c64;
+    const int32_t* cov;
+    int32_t *hot, *tnc;   // hot ops (HOT_N + 1 words), chunks per wave tile (null: no hot chunk)
+    int32_t b_tnc;
 };
 __device__ __forceinline__ int32_t pd_graph(const PDev* pd, int32_t n, int32_t blk, int which) {
     int32_t lo = 0, hi = n - 1;
     while (lo < hi) {
         const int32_t mid = (lo + hi + 1) >> 1;
         const PDev& g = pd[mid];
-        const int32_t s0 = which == 0 ? g.b_gc : which == 1 ? g.b_th : which == 2 ? g.b_cs : g.b_fill;
+        const int32_t s0 = which == 0 ? g.b_gc : which == 1 ? g.b_th : which == 2 ? g.b_cs : which == 3 ? g.b_fill :
+                           which == 4 ? g.b_sch : g.b_tnc;
         if (s0 <= blk) lo = mid; else hi = mid - 1;
     }
     return lo;
@@ -584,11 +788,27 @@ __global__ void __launch_bounds__(TS_T) k_tr_chunk_scan_b(const PDev* __restrict
                                                          uint64_t epoch) {
     const PDev& G = pd[pd_graph(pd, n, (int32_t)blockIdx.x, 2)];
     tr_chunk_scan_body((int32_t)blockIdx.x - G.b_cs, G.n_cs, G.tperm, G.rs_off, G.T, G.W, G.c64, G.coff, st + G.st_off,
-                       epoch);
+                       epoch, G.tnc);
+}
+__global__ void __launch_bounds__(256) k_hot_ops_b(const PDev* __restrict__ pd) {   // block g: graph g
+    const PDev& G = pd[blockIdx.x];
+    hot_ops_body(G.cov, G.N, G.T, nullptr, G.hot);
+}
+__global__ void k_tr_tnc_b(const PDev* __restrict__ pd, int32_t n) {
+    const PDev& G = pd[pd_graph(pd, n, (int32_t)blockIdx.x, 5)];
+    tr_tnc_body((int32_t)blockIdx.x - G.b_tnc, G.tperm, G.rs_off, G.rs16, G.T, G.W, G.hot, G.tnc);
 }
 __global__ void k_tr_fill_b(const PDev* __restrict__ pd, int32_t n) {
     const PDev& G = pd[pd_graph(pd, n, (int32_t)blockIdx.x, 3)];
-    tr_fill_body((int32_t)blockIdx.x - G.b_fill, G.tperm, G.rs_off, G.rs16, G.c64, G.T, G.N, G.W, G.tids);
+    tr_fill_body((int32_t)blockIdx.x - G.b_fill, G.tperm, G.rs_off, G.rs16, G.c64, G.T, G.N, G.W, G.tids, G.hot);
+}
+__global__ void __launch_bounds__(SCHED_T) k_tr_sched_b(const PDev* __restrict__ pd, int32_t n) {
+    __shared__ uint16_t items[SCHED_T][32 * SCHED_L];
+    __shared__ unsigned long long rem[SCHED_T][32];
+    __shared__ uint16_t cbuf[SCHED_T][32 * 4];
+    const PDev& G = pd[pd_graph(pd, n, (int32_t)blockIdx.x, 4)];
+    tr_sched_body((int64_t)((int32_t)blockIdx.x - G.b_sch) * SCHED_T + threadIdx.x, G.coff, G.W, G.tids,
+                  items[threadIdx.x], rem[threadIdx.x], cbuf[threadIdx.x], G.hot);
 }
 __global__ void k_tr_gather(const float* src, const int32_t* tperm, int32_t T, float* dst) {
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1048,6 +1268,8 @@ __global__ void k_pref_apply(const double* kind, const int32_t* pr_trace, const 
 // M_s / M_r per iteration live in MSH shards (an atomicMax per block or op on ONE word would
 // serialise ~2k same-address atomics per iteration); readers reduce the shards.
 constexpr int MSH = 64;
+// mslot: [3 iterations][s | r][MSH] maxima, then k_pr_cluster's arrival counter (word 6 MSH)
+constexpr int MSLOT_WORDS = 6 * MSH + 8;
 __device__ __forceinline__ double bits2d(unsigned long long b) { return __longlong_as_double((long long)b); }
 __device__ __forceinline__ unsigned long long d2bits(double v) {
     return (unsigned long long)__double_as_longlong(v);
@@ -1114,7 +1336,7 @@ __global__ void k_reset_init_b(const SDev* __restrict__ sd, int32_t ng) {
         const double q = (double)G.w_tq[i] * v0;
         if (G.fp32) G.q32[i] = (float)q; else G.q64[i] = q;
     }
-    if (i < 6 * MSH) G.mslot[i] = i < 2 * MSH ? d2bits(1.0) : 0ull;
+    if (i < MSLOT_WORDS) G.mslot[i] = i < 2 * MSH ? d2bits(1.0) : 0ull;
 }
 __global__ void __launch_bounds__(KB) k_kind_insert_b(const SDev* __restrict__ sd, int32_t ng, uint64_t seed,
                                                       uint64_t hmask) {
@@ -1205,7 +1427,7 @@ __global__ void k_iter_init(const float* w_t, const double* mw, const float* u_o
         if (fp32) q32[i] = (float)q; else q64[i] = q;
     }
     // M_s(0) = M_r(0) = 1: s_0, r_0 are used as they are; slots 1, 2 start cleared
-    if (i < 6 * MSH) mslot[i] = i < 2 * MSH ? d2bits(1.0) : 0ull;
+    if (i < MSLOT_WORDS) mslot[i] = i < 2 * MSH ? d2bits(1.0) : 0ull;
 }
 // k_pr_reset and k_iter_init in one launch (the iteration state depends on nothing the kinds or
 // the preference compute)
@@ -1234,7 +1456,7 @@ __global__ void k_pr_reset_init(int32_t T, int64_t cap, int32_t N, float* pref, 
         const double q = (mw ? mw[i] : (double)w_t[i]) * v0;
         if (fp32) q32[i] = (float)q; else q64[i] = q;
     }
-    if (i < 6 * MSH) mslot[i] = i < 2 * MSH ? d2bits(1.0) : 0ull;
+    if (i < MSLOT_WORDS) mslot[i] = i < 2 * MSH ? d2bits(1.0) : 0ull;
 }
 
 // Per-graph view for the batched iteration: one k_iter_a / k_iter_b pair per Jacobi iteration
@@ -1253,6 +1475,7 @@ struct GDev {
     const float* c_tp;          // c_t, w_t in position order (tperm)
     const float* w_tp;
     const double* mw_tp;        // kind-compressed graphs: w_t * multiplicity (position order), else null
+    const int32_t* hot;         // [HOT_N + 1] hot ops of the layout's chunk 0 of every tile, or null
     const float* c_t;
     const float* w_t;
     const float* u_o;
@@ -1571,21 +1794,16 @@ struct TrLds {
     }
 };
 
+// The wave's walk of k_tr_a over its run of wave tiles (shared with k_pr_cluster): per entry one
+// su read, one add into the lane's trace sum, one LDS u64 atomic of X_t; per tile r' of its traces
+// and their next q.  Returns the wave's largest r' (-inf when it owns no trace).
 template <class Q, int SUM, int NT>
-__global__ void __launch_bounds__(NT) k_tr_a(const GDev* __restrict__ gs, int32_t ng, int32_t split, double d,
-                                             double alpha, int it, int32_t unused) {
+__device__ __forceinline__ double tr_walk(const GDev& G, int32_t lb, int cur, int nxt, int32_t N, int32_t NH, double d,
+                                          double Ms, double xsc, const double* su_l, unsigned long long* lacc) {
     constexpr bool SUL = SUM == WV_SU_ALL, HOT = SUM == WV_SU_HOT;
     constexpr int NW = NT / WAVE;
-    extern __shared__ __attribute__((aligned(16))) unsigned char lraw[];
-    __shared__ double red[NW];
-    __shared__ double msh[2];
-    const GDev& G = gs[fx_graph(gs, ng, split, 2)];
-    const int32_t lb = (int32_t)blockIdx.x - G.blk0f;
-    const int cur = it & 1, nxt = cur ^ 1, k3 = it % 3;
-    const int32_t T = G.T, N = G.NA;   // (wide graphs: the hot ops)
+    const int32_t T = G.T;
     const int32_t tid = (int32_t)threadIdx.x, lane = tid & (WAVE - 1), wv = tid / WAVE;
-    const TrLds L_(N, SUM);
-    const int32_t NH = HOT ? G.n_hot : 0;   // <= L_.n_hot (the host sizes both alike), >= 64
     const GLB u32x2* ids = gp((const u32x2*)G.tids) + lane;   // chunk c of this lane: ids[c * WAVE]
     const GLB int32_t* coff = gp(G.coff);
     const GLB Q* qc = gp((const Q*)G.q[cur]);
@@ -1593,33 +1811,17 @@ __global__ void __launch_bounds__(NT) k_tr_a(const GDev* __restrict__ gs, int32_
     const GLB float* c_tp = gp(G.c_tp);
     const GLB float* w_tp = gp(G.w_tp);
     const GLB double* sug = gp(G.sub[cur]);   // ids >= N are pads (su 0)
-    double* su_l = (double*)(lraw + L_.su);
-    unsigned long long* lacc = (unsigned long long*)(lraw + L_.lacc);
-    GLB unsigned long long* mslot = gpw(G.mslot);
-    const GLB unsigned long long* Mcur = mslot + (size_t)2 * MSH * k3;
-    GLB unsigned long long* Mnext = mslot + (size_t)2 * MSH * ((k3 + 1) % 3);
-    if (lb == 0 && tid < 2 * MSH) mslot[(size_t)2 * MSH * ((k3 + 2) % 3) + tid] = 0ull;
     // this wave's tiles [k, ke) (a contiguous run: the host cuts them by chunk count)
     const GLB int32_t* wt = gp(G.wtile) + ((size_t)lb * NW + wv);
     int32_t k = __builtin_amdgcn_readfirstlane(wt[0]);
     const int32_t ke = __builtin_amdgcn_readfirstlane(wt[1]);
-    for (int32_t o = tid; o < N + TR_PAD; o += NT) {
-        if (SUL) su_l[o] = o < N ? sug[o] : 0.0;
-        lacc[o] = 0ull;
-    }
-    if (HOT)
-        for (int32_t o = tid; o < NH; o += NT) su_l[o] = sug[o];
-    if (tid < WAVE) {
-        const double ms = wave_max(bits2d(Mcur[tid]));
-        const double mr = wave_max(bits2d(Mcur[MSH + tid]));
-        if (tid == 0) {
-            msh[0] = ms;
-            msh[1] = mr;
-        }
-    }
-    __syncthreads();   // accumulator and maxima ready
-    const double xsc = (G.dscale ? G.dscale[0] : G.fx_scale) / msh[1], Ms = msh[0];
     double rmax = -__builtin_huge_val();
+    // hot chunk: chunk 0 of every tile holds hot op q at position q (or the lane's pad); its X go
+    // to registers, folded into the accumulator once at the end of the run
+    const GLB int32_t* hotp = gp(G.hot);
+    const int32_t hn = hotp ? __builtin_amdgcn_readfirstlane(hotp[HOT_N]) : 0;
+    static_assert(HOT_N == 2, "k_tr_a keeps two hot-op registers");
+    unsigned long long xh0 = 0ull, xh1 = 0ull;
     if (k < ke) {
         auto pos = [&](int32_t kk) { return min(kk * WAVE + lane, T - 1); };
         // cold-op su of a chunk (hot ops load sug[0]: one line, no traffic; pads read as 0)
@@ -1633,6 +1835,7 @@ __global__ void __launch_bounds__(NT) k_tr_a(const GDev* __restrict__ gs, int32_
             }
         };
         int32_t c = __builtin_amdgcn_readfirstlane(coff[k]);
+        int32_t ch = hn > 0 ? c : -1;                               // the current tile's hot chunk
         int32_t ce = __builtin_amdgcn_readfirstlane(coff[k + 1]);   // end of tile k
         const int32_t cl = __builtin_amdgcn_readfirstlane(coff[ke]) - 1;   // the run's last chunk
         // tile k's words; tile k + 1's q and end chunk (one tile ahead, clamped into the run).  The
@@ -1682,7 +1885,12 @@ __global__ void __launch_bounds__(NT) k_tr_a(const GDev* __restrict__ gs, int32_
             if (SUL || HOT) lds_su(NXT, SN);                                                               \
             const int32_t o_[4] = {(int32_t)(CUR.x & 0xffffu), (int32_t)(CUR.x >> 16),                     \
                                    (int32_t)(CUR.y & 0xffffu), (int32_t)(CUR.y >> 16)};                    \
-            _Pragma("unroll") for (int j = 0; j < 4; ++j) atomicAdd(&lacc[(MR_TREXP & 1) ? N + lane : o_[j]], X); \
+            if (c == ch) {   /* the tile's hot chunk: positions q hold hot op q or the pad */                \
+                xh0 += o_[0] < N ? X : 0ull;                                                               \
+                xh1 += o_[1] < N ? X : 0ull;                                                               \
+            } else {                                                                                       \
+                _Pragma("unroll") for (int j = 0; j < 4; ++j) atomicAdd(&lacc[(MR_TREXP & 1) ? N + lane : o_[j]], X); \
+            }                                                                                              \
             _Pragma("unroll") for (int j = 0; j < 4; ++j)                                                  \
                 acc += SUL ? SC[j] : HOT ? (o_[j] < NH ? SC[j] : GC[j]) : GC[j];                          \
             if (++c == ce) {                                                                               \
@@ -1694,6 +1902,7 @@ __global__ void __launch_bounds__(NT) k_tr_a(const GDev* __restrict__ gs, int32_
                 qn[own_ ? p_ : T] = (Q)(w_cur * rp_);   /* q[T]: pad slot */                              \
                 if (++k == ke) goto tr_done;                                                               \
                 ce = __builtin_amdgcn_readfirstlane(ce_nx);                                                \
+                ch = hn > 0 ? c : -1;                                                                      \
                 q_cur = q_nx;                                                                              \
                 const int32_t kk_ = min(k + 1, ke - 1);                                                    \
                 c_cur = c_tp[pos(k)];                                                                      \
@@ -1713,12 +1922,65 @@ __global__ void __launch_bounds__(NT) k_tr_a(const GDev* __restrict__ gs, int32_
         }
 #undef TR_STEP
     tr_done:;
+        if (hn > 0) {   // the run's hot-op sums: one LDS atomic per hot op per wave
+#pragma unroll
+            for (int m = 32; m >= 1; m >>= 1) {
+                xh0 += (unsigned long long)__shfl_xor((long long)xh0, m, WAVE);
+                xh1 += (unsigned long long)__shfl_xor((long long)xh1, m, WAVE);
+            }
+            if (lane == 0) {
+                const unsigned long long xs[2] = {xh0, xh1};
+                for (int q = 0; q < hn; ++q) atomicAdd(&lacc[hotp[q]], xs[q]);
+            }
+        }
     }
+    return rmax;
+}
+
+template <class Q, int SUM, int NT>
+__global__ void __launch_bounds__(NT) k_tr_a(const GDev* __restrict__ gs, int32_t ng, int32_t split, double d,
+                                             double alpha, int it, int32_t unused) {
+    constexpr bool SUL = SUM == WV_SU_ALL, HOT = SUM == WV_SU_HOT;
+    constexpr int NW = NT / WAVE;
+    extern __shared__ __attribute__((aligned(16))) unsigned char lraw[];
+    __shared__ double red[NW];
+    __shared__ double msh[2];
+    const GDev& G = gs[fx_graph(gs, ng, split, 2)];
+    const int32_t lb = (int32_t)blockIdx.x - G.blk0f;
+    const int cur = it & 1, nxt = cur ^ 1, k3 = it % 3;
+    const int32_t N = G.NA;   // (wide graphs: the hot ops)
+    const int32_t tid = (int32_t)threadIdx.x;
+    const TrLds L_(N, SUM);
+    const int32_t NH = HOT ? G.n_hot : 0;   // <= L_.n_hot (the host sizes both alike), >= 64
+    const GLB double* sug = gp(G.sub[cur]);   // ids >= N are pads (su 0)
+    double* su_l = (double*)(lraw + L_.su);
+    unsigned long long* lacc = (unsigned long long*)(lraw + L_.lacc);
+    GLB unsigned long long* mslot = gpw(G.mslot);
+    const GLB unsigned long long* Mcur = mslot + (size_t)2 * MSH * k3;
+    GLB unsigned long long* Mnext = mslot + (size_t)2 * MSH * ((k3 + 1) % 3);
+    if (lb == 0 && tid < 2 * MSH) mslot[(size_t)2 * MSH * ((k3 + 2) % 3) + tid] = 0ull;
+    for (int32_t o = tid; o < N + TR_PAD; o += NT) {
+        if (SUL) su_l[o] = o < N ? sug[o] : 0.0;
+        lacc[o] = 0ull;
+    }
+    if (HOT)
+        for (int32_t o = tid; o < NH; o += NT) su_l[o] = sug[o];
+    if (tid < WAVE) {
+        const double ms = wave_max(bits2d(Mcur[tid]));
+        const double mr = wave_max(bits2d(Mcur[MSH + tid]));
+        if (tid == 0) {
+            msh[0] = ms;
+            msh[1] = mr;
+        }
+    }
+    __syncthreads();   // accumulator and maxima ready
+    const double xsc = (G.dscale ? G.dscale[0] : G.fx_scale) / msh[1], Ms = msh[0];
+    const double rmax_w = tr_walk<Q, SUM, NT>(G, lb, cur, nxt, N, NH, d, Ms, xsc, su_l, lacc);
     // (the call-graph term alpha P_ss s_k is k_fx_b's: a wave per op)
     __syncthreads();
     GLB unsigned long long* prow = gpw(G.fx_part) + (size_t)lb * N;
     for (int32_t o = tid; o < N; o += NT) prow[o] = lacc[o];
-    rmax = block_max(rmax, red);
+    const double rmax = block_max(rmax_w, red);
     if (tid == 0 && rmax >= 0.0)   // -inf: a block without traces (an empty shard's placeholder)
         atomicMax((unsigned long long*)&Mnext[MSH + blockIdx.x % MSH], d2bits(rmax));
 }
@@ -1849,6 +2111,163 @@ __global__ void __launch_bounds__(WAVE * FB_W) k_fx_b(const GDev* __restrict__ g
     G.spb[nxt][op] = v;
     G.sub[nxt][o] = (double)uo * v;   // su in the kernel's labels
     atomicMax(&Mnext[op % MSH], d2bits(v));
+}
+
+// ---------------------------------------------------------------- persistent iteration (k_pr_cluster)
+// All `iters` Jacobi iterations of a batch of fused graphs in ONE launch (one
+// persistent launch for many small windows).  Graph g owns a CLUSTER of n_fa blocks; its blocks sync
+// only with each other, so the graphs of a batch advance independently (no kernel boundary per
+// iteration, no batch-wide tail).  Per iteration a block
+//   (A) walks its wave tiles exactly as k_tr_a (tr_walk: same sums, same order);
+//   (B) with n_fa > 1 publishes its accumulator row write-through (sc1 stores, vmcnt(0), barrier),
+//       adds its r' maximum and arrives at the cluster's counter (agent atomics), polls it (sc1),
+//       then reads every block's row with sc1 loads (MI355X_MICROARCH.md inter-workgroup hand-off,
+//       table row 1); with n_fa == 1 the row stays in LDS;
+//   (C) computes s' for EVERY op itself (k_fx_b's arithmetic: exact limb sums, the call-graph term
+//       a wave per op), its maximum M_s, su = u_o s' -- all in LDS, identical in every block.
+// With the per-wave cut of the launch-per-iteration path the results are bitwise those of
+// k_tr_a + k_fx_b.  Every spin is bounded (PC_TIMEOUT): a cluster whose blocks are not co-resident
+// raises flag[3], every block leaves, and the host reruns the call launch by launch.
+constexpr unsigned long long PC_TIMEOUT = 5000000ull;   // 50 ms of the 100 MHz s_memrealtime clock
+constexpr int PC_MAXB = 64;                               // blocks of one cluster
+struct PcLds {
+    size_t lacc, su, s0, s1, total;
+    __host__ __device__ explicit PcLds(int32_t N) {
+        const TrLds t(N, WV_SU_ALL);   // the accumulator and su as k_tr_a's
+        lacc = t.lacc;
+        su = t.su;
+        s0 = t.total;
+        s1 = s0 + ((size_t)N * 8 + 15) / 16 * 16;
+        total = s1 + ((size_t)N * 8 + 15) / 16 * 16;
+    }
+};
+template <class Q, int NT>
+__global__ void __launch_bounds__(NT) k_pr_cluster(const GDev* __restrict__ gs, int32_t ng, double d, int iters) {
+    constexpr int NW = NT / WAVE;
+    extern __shared__ __attribute__((aligned(16))) unsigned char lraw[];
+    __shared__ double red[NW];
+    __shared__ double mb[2];
+    __shared__ int s_abort;
+    const GDev& G = gs[graph_of(gs, ng, (int32_t)blockIdx.x, 2)];
+    const int32_t lb = (int32_t)blockIdx.x - G.blk0f, B = G.n_fa, N = G.N;
+    const int32_t tid = (int32_t)threadIdx.x, lane = tid & (WAVE - 1), wv = tid / WAVE;
+    const PcLds L(N);
+    unsigned long long* lacc = (unsigned long long*)(lraw + L.lacc);
+    double* su_l = (double*)(lraw + L.su);
+    double* s_cur = (double*)(lraw + L.s0);
+    double* s_nxt = (double*)(lraw + L.s1);
+    // (global-address views: the hand-off's sc1 loads / stores and atomics must be global_, not flat_)
+    GLB unsigned long long* mslot = gpw(G.mslot);
+    GLB unsigned long long* cnt = mslot + 6 * MSH;
+    GLB unsigned long long* rows = gpw(G.fx_part);   // [2][B][N] (B > 1)
+    const double scale = G.dscale ? G.dscale[0] : G.fx_scale, iscale = G.dscale ? G.dscale[1] : G.fx_iscale;
+    const GLB int64_t* ss_off = gp(G.ss_off);
+    const GLB int32_t* ss_par = gp(G.ss_par);
+    const GLB float* pw = gp(G.pw);
+    const GLB float* u_o = gp(G.u_o);
+    // the set-up's state: s_0, su_0, M_s(0), M_r(0) (earlier launches on this stream)
+    for (int32_t o = tid; o < N + TR_PAD; o += NT) {
+        lacc[o] = 0ull;
+        su_l[o] = o < N ? G.sub[0][o] : 0.0;
+        if (o < N) s_cur[o] = G.spb[0][o];
+    }
+    if (tid < WAVE) {
+        const double ms = wave_max(bits2d(mslot[tid]));
+        const double mr = wave_max(bits2d(mslot[MSH + tid]));
+        if (tid == 0) {
+            mb[0] = ms;
+            mb[1] = mr;
+            s_abort = 0;
+        }
+    }
+    __syncthreads();
+    double Ms = mb[0], Mr = mb[1];
+    for (int it = 0; it < iters; ++it) {
+        const int cur = it & 1, nxt = cur ^ 1;
+        GLB unsigned long long* Mr_next = mslot + (size_t)2 * MSH * ((it + 1) % 3) + MSH;
+        if (B > 1 && lb == 0 && tid < MSH)   // slot it + 2 (last read in iteration it - 1)
+            __hip_atomic_store(mslot + (size_t)2 * MSH * ((it + 2) % 3) + MSH + tid, 0ull, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        const double rw = tr_walk<Q, WV_SU_ALL, NT>(G, lb, cur, nxt, N, 0, d, Ms, scale / Mr, su_l, lacc);
+        const double rmax = block_max(rw, red);   // (its barriers: every wave's LDS atomics are done)
+        double Mr_n = rmax;
+        if (B > 1) {
+            GLB unsigned long long* mine = rows + ((size_t)cur * B + lb) * N;
+            for (int32_t o = tid; o < N; o += NT) {
+                __hip_atomic_store(mine + o, lacc[o], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                lacc[o] = 0ull;
+            }
+            if (tid == 0 && rmax >= 0.0)
+                __hip_atomic_fetch_max(Mr_next + lb % MSH, d2bits(rmax), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (tid == 0) {
+                __hip_atomic_fetch_add(cnt, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const unsigned long long target = (unsigned long long)B * (unsigned long long)(it + 1);
+                const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+                while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+                    __builtin_amdgcn_s_sleep(1);
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > PC_TIMEOUT) {
+                        s_abort = 1;
+                        __hip_atomic_fetch_or(gpw((int32_t*)G.flag) + 3, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        break;
+                    }
+                }
+            }
+            __syncthreads();
+            if (s_abort) return;   // (every block of the cluster times out the same way)
+            if (tid < WAVE) {
+                const double mr = wave_max(bits2d(__hip_atomic_load(Mr_next + tid, __ATOMIC_RELAXED,
+                                                                    __HIP_MEMORY_SCOPE_AGENT)));
+                if (tid == 0) mb[1] = mr;
+            }
+        }
+        // the call-graph term alpha (P_ss s_k)[o] / M_s(k): a wave per op (k_fx_b's order)
+        for (int32_t o = wv; o < N; o += NW) {
+            double bb = 0.0;
+            for (int64_t e = ss_off[o] + lane; e < ss_off[o + 1]; e += WAVE) {
+                const int32_t p = ss_par[e];
+                bb += (double)pw[p] * s_cur[p];
+            }
+            bb = wave_sum(bb);
+            if (lane == 0) s_nxt[o] = G.alpha * (bb / Ms);
+        }
+        __syncthreads();
+        if (B > 1) Mr_n = mb[1];
+        double vmax = -__builtin_huge_val();
+        const GLB unsigned long long* rcur = rows + (size_t)cur * B * N;
+        for (int32_t o = tid; o < N; o += NT) {
+            unsigned long long lo = 0ull, hi = 0ull;
+            if (B > 1) {
+                for (int32_t b = 0; b < B; ++b) {
+                    const unsigned long long v = __hip_atomic_load(rcur + (size_t)b * N + o, __ATOMIC_RELAXED,
+                                                                   __HIP_MEMORY_SCOPE_AGENT);
+                    lo += v & 0xffffffffull;
+                    hi += v >> 32;
+                }
+            } else {
+                const unsigned long long v = lacc[o];
+                lacc[o] = 0ull;
+                lo = v & 0xffffffffull;
+                hi = v >> 32;
+            }
+            const double sum = ((double)hi * 4294967296.0 + (double)lo) * iscale;
+            const double v = d * (sum + s_nxt[o]);      // pagerank.py:122-124
+            s_nxt[o] = v;
+            su_l[o] = (double)u_o[o] * v;
+            vmax = nmax(vmax, v);
+        }
+        Ms = block_max(vmax, red);   // (its barriers publish s_nxt / su_l to the block)
+        Mr = Mr_n;
+        double* t = s_cur;
+        s_cur = s_nxt;
+        s_nxt = t;
+    }
+    if (lb == 0) {   // k_weights_batch's inputs: s'(iters) and M_s(iters)
+        GLB double* sp = gpw(G.spb[iters & 1]);
+        for (int32_t o = tid; o < N; o += NT) sp[o] = s_cur[o];
+        if (tid < MSH) mslot[(size_t)2 * MSH * (iters % 3) + tid] = tid == 0 ? d2bits(Ms) : 0ull;
+    }
 }
 
 // ---- wide fused graphs, per iteration, before k_tr_a
@@ -2170,11 +2589,13 @@ static double tr_budget() {
     return v;
 }
 static int tr_split(mr_ctx* ctx, mr_graph* g, const FxPlan& P, int64_t wsum, int64_t* nfa,
-                    std::vector<CutArg>* defer = nullptr) {
+                    std::vector<CutArg>* defer = nullptr, int64_t force_nb = 0) {
     const int64_t W = g->n_wt, NW = P.NT / WAVE;
     const int64_t resident = plan_resident(kern_n(g), P);
     int64_t nb = std::max<int64_t>({std::min<int64_t>(resident, cdiv(W, NW)), cdiv(W, 1023), 1});
-    if (tr_budget() > 0.0 && wsum > W) {
+    if (force_nb > 0) {   // k_pr_cluster's cluster size (at most 1023 wave tiles per block still)
+        nb = std::max<int64_t>(force_nb, cdiv(W, 1023));
+    } else if (tr_budget() > 0.0 && wsum > W) {
         const int64_t share = (int64_t)std::ceil((double)resident * tr_budget() * (double)W / (double)wsum);
         nb = std::max<int64_t>({std::min(nb, share), cdiv(W, 1023), 1});
     }
@@ -2244,8 +2665,72 @@ static int tr_split(mr_ctx* ctx, mr_graph* g, const FxPlan& P, int64_t wsum, int
 }
 
 static int fused_blocks(mr_ctx* ctx, mr_graph* g, const FxPlan& P, int64_t wsum, int64_t* nfa,
-                        std::vector<CutArg>* defer = nullptr) {
-    return tr_split(ctx, g, P, wsum, nfa, defer);
+                        std::vector<CutArg>* defer = nullptr, int64_t force_nb = 0) {
+    return tr_split(ctx, g, P, wsum, nfa, defer, force_nb);
+}
+
+// ---- k_pr_cluster: eligibility and cluster sizes
+// MR_PR_PERSIST (read per call): unset / 1 = persistent launch where eligible, 0 = launch per
+// iteration, "split" = the persistent plan's block counts launched per iteration (k_tr_a +
+// k_fx_b: bitwise the persistent results -- parity tests).  MR_PC_TPW: wave tiles per wave a
+// cluster is sized for (default 4).
+constexpr size_t PC_LDS_MAX = 76 * 1024;   // two 1024-thread blocks per CU
+enum { PC_OFF = 0, PC_ON = 1, PC_SPLIT = 2 };
+static int pc_mode() {
+    const char* e = getenv("MR_PR_PERSIST");
+    if (!e) return PC_ON;
+    if (!strcmp(e, "split")) return PC_SPLIT;
+    return strcmp(e, "0") ? PC_ON : PC_OFF;
+}
+static int64_t pc_tpw() {
+    const char* e = getenv("MR_PC_TPW");
+    return e ? std::max<int64_t>(1, atoll(e)) : 4;
+}
+using PcA = void (*)(const GDev*, int32_t, double, int);
+static PcA pc_kernel(bool fp32, int NT) {
+    static const PcA tab[2][2] = {{k_pr_cluster<double, 512>, k_pr_cluster<double, 1024>},
+                                  {k_pr_cluster<float, 512>, k_pr_cluster<float, 1024>}};
+    return tab[fp32 ? 1 : 0][NT == 1024 ? 1 : 0];
+}
+// per graph the cluster's block count, or an empty vector when the batch is not eligible
+static std::vector<int64_t> pc_plan(mr_ctx* ctx, mr_graph* const* gs, int ng, const FxPlan& P, bool sharded, int iters,
+                                    bool fp32) {
+    std::vector<int64_t> nb;
+    if (sharded || iters <= 0 || ctx->no_persist || pc_mode() == PC_OFF || P.mode != WV_SU_ALL) return nb;
+    int32_t nmax = 0;
+    for (int i = 0; i < ng; ++i) {
+        const mr_graph* g = gs[i];
+        if (!g->fused || g->wide || g->relabeled || !g->tile_mult_h.empty() || g->n_wt == 0) return nb;
+        nmax = std::max(nmax, g->N);
+    }
+    const size_t lds = PcLds(nmax).total;
+    if (lds > PC_LDS_MAX) return nb;
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)pc_kernel(fp32, P.NT), P.NT, lds) != hipSuccess ||
+        per_cu < 1)
+        return nb;
+    // one block per CU fewer than the API's answer allows (MI355X_MICROARCH.md: the API can be one
+    // block high), at least one: the grid must be co-resident for the clusters' spins
+    const int64_t cap = (int64_t)num_cus() * std::max(1, per_cu - 1);
+    const int64_t NW = P.NT / WAVE, tpw = pc_tpw();
+    int64_t tot = 0;
+    nb.resize((size_t)ng);
+    for (int i = 0; i < ng; ++i) {
+        const int64_t W = gs[i]->n_wt;
+        nb[(size_t)i] = std::min<int64_t>(std::max<int64_t>({cdiv(W, NW * tpw), cdiv(W, 1023), 1}), PC_MAXB);
+        tot += nb[(size_t)i];
+    }
+    if (tot > cap) {   // shrink every cluster in proportion
+        const int64_t tot0 = tot;
+        tot = 0;
+        for (int i = 0; i < ng; ++i) {
+            int64_t& n = nb[(size_t)i];
+            n = std::max<int64_t>({n * cap / tot0, cdiv(gs[i]->n_wt, 1023), 1});
+            tot += n;
+        }
+        if (tot > cap) nb.clear();   // (more graphs than resident blocks)
+    }
+    return nb;
 }
 
 // k_tr_a's layout of a fused graph (after w_t and the kernel's ids rs16 / rsp): traces sorted by
@@ -2254,7 +2739,7 @@ static int fused_blocks(mr_ctx* ctx, mr_graph* g, const FxPlan& P, int64_t wsum,
 // off / ids: the trace-major incidence the kernel walks (rs_off with rs16 / rsp, or a wide graph's
 // hot entries), N: the kernel's op count (pads N + lane)
 static int tr_layout(mr_ctx* ctx, mr_graph* g, const int64_t* off, const uint16_t* src, int32_t N, int64_t nent,
-                     int32_t* zeroed) {
+                     int32_t* zeroed, const int32_t* cov = nullptr, const int32_t* perm = nullptr) {
     hipStream_t st = ctx->stream;
     const int32_t T = g->T;
     const int32_t W = cdiv(T, WAVE);
@@ -2290,23 +2775,39 @@ static int tr_layout(mr_ctx* ctx, mr_graph* g, const int64_t* off, const uint16_
                            2 * (size_t)nbin * sizeof(int32_t), st, off, T, nbin,
                            lscan ? (const int64_t*)nullptr : boff.p, hist, taken, g->w_t.p, g->tperm.p, g->w_tp.p);
     }
+    // the hot chunk (cov given: the layout's coverage by op, perm: label -> op when relabelled)
+    DBuf<int32_t> tnc;
+    const bool hot = cov && tr_hot_on() && W > 0;
+    if (hot) {
+        MR_TRY(g->hot.alloc(ctx, HOT_N + 1));
+        MR_TRY(tnc.alloc(ctx, (size_t)W));
+        hipLaunchKernelGGL(k_hot_ops, dim3(1), dim3(256), 0, st, cov, N, T, perm, g->hot.p);
+        hipLaunchKernelGGL(k_tr_tnc, dim3(cdiv((int64_t)W * WAVE, 256)), dim3(256), 0, st, g->tperm.p, off, src, T, W,
+                           g->hot.p, tnc.p);
+    } else {
+        g->hot.reset();
+    }
     {   // chunk counts per wave tile, their prefix and its int32 copy: one launch
         const int64_t nt = std::max<int64_t>(cdiv((int64_t)W, TS_TILE), 1);
         unsigned long long* dst = nullptr;
         uint64_t epoch = 0;
         MR_TRY(mr_dl_status(ctx, nt, &dst, &epoch));
         hipLaunchKernelGGL(k_tr_chunk_scan, dim3((unsigned)nt), dim3(TS_T), 0, st, g->tperm.p, off, T, W, c64.p,
-                           g->coff.p, dst, epoch);
+                           g->coff.p, dst, epoch, hot ? (const int32_t*)tnc.p : nullptr);
     }
     // the id array at an upper bound of the chunk count (no host round trip): tile k holds
-    // ceil(maxlen_k / 4) chunks, and with lengths ascending maxlen_k <= every length of tile k + 1,
-    // so sum_k maxlen_k <= nent / 64 + 2 N
+    // ceil(maxlen_k / 4) chunks (+ 1: the hot chunk), and with lengths ascending maxlen_k <= every
+    // length of tile k + 1, so sum_k maxlen_k <= nent / 64 + 2 N
     g->coff_h.clear();
-    const int64_t nch = (int64_t)W + (nent / WAVE + 2 * (int64_t)N) / 4 + 2;
+    const int64_t nch = 2 * (int64_t)W + (nent / WAVE + 2 * (int64_t)N) / 4 + 2;
     MR_TRY(g->tids.alloc(ctx, (size_t)std::max<int64_t>(nch, 1) * WAVE * 4));
+    const int32_t* hp = hot ? (const int32_t*)g->hot.p : nullptr;
     if (W)
         hipLaunchKernelGGL(k_tr_fill, dim3(cdiv((int64_t)W * WAVE, 256)), dim3(256), 0, st, g->tperm.p, off, src,
-                           c64.p, T, N, W, g->tids.p);
+                           c64.p, T, N, W, g->tids.p, hp);
+    if (W && tr_sched_on())
+        hipLaunchKernelGGL(k_tr_sched, dim3(cdiv(2 * (int64_t)W, SCHED_T)), dim3(SCHED_T), 0, st, g->coff.p, W,
+                           g->tids.p, hp);
     MR_TRY_HIP(ctx, hipGetLastError());
     return MR_OK;   // (scratch returns to the stream-ordered pool)
 }
@@ -2356,7 +2857,7 @@ static int wide_prepare(mr_ctx* ctx, mr_graph* g) {
     MR_TRY(g->hot16.alloc(ctx, (size_t)n_hot + 8));
     hipLaunchKernelGGL(k_wide_hot, dim3(cdiv(T, 256)), dim3(256), 0, st, g->rs_off.p, g->rs_ops.p, inv.p, T, NA,
                        g->hot_off.p, g->hot16.p);
-    MR_TRY(tr_layout(ctx, g, g->hot_off.p, g->hot16.p, NA, n_hot, nullptr));   // tperm, w_tp, tids, coff (host copy)
+    MR_TRY(tr_layout(ctx, g, g->hot_off.p, g->hot16.p, NA, n_hot, nullptr, g->cov.p, g->perm.p));   // tperm, w_tp, tids, coff
     // ---- cold entries in position order
     DBuf<int32_t> cnt;
     DBuf<int64_t> coff64;
@@ -2448,7 +2949,8 @@ int mr_graph_prepare_batch(mr_ctx* ctx, mr_graph* const* gs, int n, std::vector<
     PDev* hp = reinterpret_cast<PDev*>(keep.data());
     std::vector<DBuf<int32_t>> trz((size_t)n);
     std::vector<DBuf<int64_t>> c64((size_t)n);
-    int32_t bgc = 0, bth = 0, bcs = 0, bfl = 0, nbin_max = 0;
+    std::vector<DBuf<int32_t>> tnc((size_t)n);
+    int32_t bgc = 0, bth = 0, bcs = 0, bfl = 0, bsch = 0, btnc = 0, nbin_max = 0;
     int64_t st_words = 0;
     for (int i = 0; i < n; ++i) {
         mr_graph* g = gs[i];
@@ -2464,8 +2966,14 @@ int mr_graph_prepare_batch(mr_ctx* ctx, mr_graph* const* gs, int n, std::vector<
         MR_TRY(g->tperm.alloc(ctx, (size_t)std::max(T, 1)));
         MR_TRY(g->w_tp.alloc(ctx, (size_t)std::max(T, 1)));
         MR_TRY(g->coff.alloc(ctx, (size_t)W + 1));
-        const int64_t nch = (int64_t)W + (nnz / WAVE + 2 * (int64_t)N) / 4 + 2;   // as tr_layout
+        const int64_t nch = 2 * (int64_t)W + (nnz / WAVE + 2 * (int64_t)N) / 4 + 2;   // as tr_layout
         MR_TRY(g->tids.alloc(ctx, (size_t)std::max<int64_t>(nch, 1) * WAVE * 4));
+        if (tr_hot_on()) {
+            MR_TRY(g->hot.alloc(ctx, HOT_N + 1));
+            MR_TRY(tnc[(size_t)i].alloc(ctx, (size_t)std::max(W, 1)));
+        } else {
+            g->hot.reset();
+        }
         g->relabeled = false;
         g->wide = false;
         g->NA = N;
@@ -2510,6 +3018,13 @@ int mr_graph_prepare_batch(mr_ctx* ctx, mr_graph* const* gs, int n, std::vector<
         bcs += v.n_cs;
         v.b_fill = bfl;
         bfl += cdiv((int64_t)W * WAVE, 256);
+        v.b_sch = bsch;
+        bsch += cdiv(2 * (int64_t)W, SCHED_T);
+        v.cov = g->cov.p;
+        v.hot = g->hot.p;
+        v.tnc = g->hot.p ? tnc[(size_t)i].p : nullptr;
+        v.b_tnc = btnc;
+        btnc += cdiv((int64_t)W * WAVE, 256);
         nbin_max = std::max(nbin_max, N + 1);
     }
     DBuf<PDev> dpd;
@@ -2520,8 +3035,13 @@ int mr_graph_prepare_batch(mr_ctx* ctx, mr_graph* const* gs, int n, std::vector<
     hipLaunchKernelGGL(k_graph_consts_b, dim3(bgc), dim3(256), 0, st, dpd.p, n);
     hipLaunchKernelGGL(k_tr_hist_b, dim3(bth), dim3(TRB), (size_t)nbin_max * sizeof(int32_t), st, dpd.p, n);
     hipLaunchKernelGGL(k_tr_place_b, dim3(bth), dim3(TRB), 2 * (size_t)nbin_max * sizeof(int32_t), st, dpd.p, n);
+    if (tr_hot_on()) {   // hot ops (a block per graph) and the chunks per wave tile
+        hipLaunchKernelGGL(k_hot_ops_b, dim3(n), dim3(256), 0, st, dpd.p);
+        hipLaunchKernelGGL(k_tr_tnc_b, dim3(btnc), dim3(256), 0, st, dpd.p, n);
+    }
     hipLaunchKernelGGL(k_tr_chunk_scan_b, dim3(bcs), dim3(TS_T), 0, st, dpd.p, n, dst, epoch);
     hipLaunchKernelGGL(k_tr_fill_b, dim3(bfl), dim3(256), 0, st, dpd.p, n);
+    if (bsch && tr_sched_on()) hipLaunchKernelGGL(k_tr_sched_b, dim3(bsch), dim3(SCHED_T), 0, st, dpd.p, n);
     MR_TRY_HIP(ctx, hipGetLastError());
     return MR_OK;   // (scratch returns to the stream-ordered pool)
 }
@@ -2583,7 +3103,8 @@ int mr_graph_prepare(mr_ctx* ctx, mr_graph* g) {
             g->perm.reset();
             g->rsp.reset();
         }
-        MR_TRY(tr_layout(ctx, g, g->rs_off.p, g->relabeled ? g->rsp.p : g->rs16.p, N, nnz, trz.p));
+        MR_TRY(tr_layout(ctx, g, g->rs_off.p, g->relabeled ? g->rsp.p : g->rs16.p, N, nnz, trz.p, g->cov.p,
+                         g->relabeled ? (const int32_t*)g->perm.p : nullptr));
         g->n_tiles = 0;
         g->n_pairs = 0;
         MR_TRY_HIP(ctx, hipGetLastError());
@@ -2705,7 +3226,7 @@ static int pagerank_setup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool 
         MR_TRY(g->ht_cr.alloc(ctx, cap));
         MR_TRY(g->slot_of.alloc(ctx, (size_t)T));
     }
-    MR_TRY(g->mslot.alloc(ctx, 6 * MSH));
+    MR_TRY(g->mslot.alloc(ctx, MSLOT_WORDS));
     MR_TRY(g->sn.alloc(ctx, (size_t)N));
     MR_TRY(g->spb[0].alloc(ctx, (size_t)N));
     MR_TRY(g->spb[1].alloc(ctx, (size_t)N));
@@ -2723,7 +3244,7 @@ static int pagerank_setup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool 
     // one launch clears every per-call word (instead of a memset per buffer) and sets the iteration
     // state up (k_iter_init's part: it depends on nothing the kinds / preference compute)
     hipLaunchKernelGGL(k_pr_reset_init,
-                       dim3(cdiv(std::max<int64_t>({(int64_t)T, (int64_t)cap, (int64_t)N + TR_PAD, 6 * MSH, 16}), 256)),
+                       dim3(cdiv(std::max<int64_t>({(int64_t)T, (int64_t)cap, (int64_t)N + TR_PAD, MSLOT_WORDS, 16}), 256)),
                        dim3(256), 0, st, T, (int64_t)cap, N, g->pref.p, g->c_t.p, g->ht_key.p, g->ht_cr.p,
                        g->flag.p, g->scal.p, tr ? g->w_tp.p : g->w_t.p, tr ? g->mw_tp.p : nullptr, g->u_o.p,
                        g->T_all > 0 ? g->T_all : (int64_t)T, g->spb[0].p, g->sub[0].p, g->sub[1].p, g->q64[0].p,
@@ -2791,7 +3312,7 @@ static int pagerank_setup_batch(mr_ctx* ctx, mr_graph* const* gs, const int* ano
         MR_TRY(g->ht_key.alloc(ctx, cap));
         MR_TRY(g->ht_cr.alloc(ctx, cap));
         MR_TRY(g->slot_of.alloc(ctx, (size_t)T));
-        MR_TRY(g->mslot.alloc(ctx, 6 * MSH));
+        MR_TRY(g->mslot.alloc(ctx, MSLOT_WORDS));
         MR_TRY(g->sn.alloc(ctx, (size_t)N));
         MR_TRY(g->spb[0].alloc(ctx, (size_t)N));
         MR_TRY(g->spb[1].alloc(ctx, (size_t)N));
@@ -2838,7 +3359,7 @@ static int pagerank_setup_batch(mr_ctx* ctx, mr_graph* const* gs, const int* ano
         v.o16 = g->rs16.p;
         v.len_t = g->len_t.p;
         v.b_reset = br;
-        br += cdiv(std::max<int64_t>({(int64_t)T, (int64_t)cap, (int64_t)N + TR_PAD, 6 * MSH, 16}), 256);
+        br += cdiv(std::max<int64_t>({(int64_t)T, (int64_t)cap, (int64_t)N + TR_PAD, MSLOT_WORDS, 16}), 256);
         v.b_kins = bk;
         bk += cdiv(T, KB);
         v.b_kver = bv;
@@ -2955,8 +3476,9 @@ struct HostMarks {
 };
 static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly, int ng, double d, double alpha,
                             int iters, int precision, uint32_t flags, bool sharded, uint64_t seed, uint64_t hmask,
-                            bool* collided) {
+                            bool* collided, bool* timed_out) {
     *collided = false;
+    *timed_out = false;
     HostMarks hm(ng);
     if (!ctx || ng <= 0 || !gs || !anomaly) return mr_fail(ctx, MR_ERR_ARG, "mr_pagerank: bad arguments");
     if (iters < 0) return mr_fail(ctx, MR_ERR_ARG, "iters < 0");
@@ -2997,6 +3519,9 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         }
     }
     hm.mark("setup");
+    // k_pr_cluster: every iteration in one launch, a cluster of blocks per graph (pc: cluster sizes)
+    const std::vector<int64_t> pc = pc_plan(ctx, gs, ng, plan, sharded, iters, fp32);
+    const bool persist = !pc.empty() && pc_mode() == PC_ON;
     int64_t wsum = 0;   // wave tiles of the launch's fused graphs (k_tr_a's block budget)
     for (int i = 0; i < ng; ++i)
         if (gs[i]->fused) wsum += gs[i]->n_wt;
@@ -3005,8 +3530,10 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         mr_graph* g = gs[i];
         if (g->fused) {   // the plan's blocks: partial rows and (k_tr_a) the per-wave cut
             int64_t nfa = 0;
-            MR_TRY(fused_blocks(ctx, g, plan, wsum, &nfa, &cuts));
-            MR_TRY(g->fx_part.alloc(ctx, (size_t)std::max<int64_t>(nfa, 1) * (size_t)kern_n(g)));
+            MR_TRY(fused_blocks(ctx, g, plan, wsum, &nfa, &cuts, pc.empty() ? 0 : pc[(size_t)i]));
+            // (k_pr_cluster: two rows per block, one per iteration parity)
+            MR_TRY(g->fx_part.alloc(ctx, (size_t)(persist ? 2 : 1) * (size_t)std::max<int64_t>(nfa, 1) *
+                                             (size_t)kern_n(g)));
         }
     }
     hm.mark("blocks");
@@ -3050,6 +3577,7 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         v.c_tp = g->c_tp.p;
         v.w_tp = g->w_tp.p;
         v.mw_tp = g->mw_tp.p;
+        v.hot = g->hot.p;
         v.c_t = g->c_t.p;
         v.w_t = g->w_t.p;
         v.u_o = g->u_o.p;
@@ -3083,7 +3611,7 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         // a shard without traces still runs one (empty) block: it clears the maxima slot and
         // writes a zero partial row, and the collectives after the launch need every rank
         int64_t nfa = 0;
-        if (g->fused) MR_TRY(fused_blocks(ctx, g, plan, wsum, &nfa));
+        if (g->fused) MR_TRY(fused_blocks(ctx, g, plan, wsum, &nfa, nullptr, pc.empty() ? 0 : pc[(size_t)i]));
         nfa = g->fused ? std::max<int64_t>(nfa, sharded ? 1 : 0) : 0;
         // a row entry stays below 2^63; shards of one graph hold different trace counts, and their
         // limbs are summed, so they share the scale of the largest block (2^15 traces)
@@ -3175,7 +3703,17 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         sst = ctx->side;
     }
     hm.mark("pre-loop");
-    for (int it = 0; it < iters; ++it) {
+    if (persist) {   // all iterations in one launch (k_pr_cluster)
+        int32_t nmax = 0;
+        for (int i = 0; i < ng; ++i) nmax = std::max(nmax, gs[i]->N);
+        mr_prof_begin(ctx);
+        hipLaunchKernelGGL(pc_kernel(fp32, plan.NT), dim3(blocks_fa), dim3(plan.NT), PcLds(nmax).total, st, dv.p, ng, d,
+                           iters);
+        MR_TRY_HIP(ctx, hipGetLastError());
+        MR_DEBUG_CHECK(ctx, "k_pr_cluster");
+        mr_prof_end(ctx, bytes * iters);
+    }
+    for (int it = 0; it < iters && !persist; ++it) {
         mr_prof_begin(ctx);
         if (any_wide && sst != st) {
             MR_TRY_HIP(ctx, hipEventRecord(ctx->side_ev[0], st));   // this iteration's su and q are ready
@@ -3216,7 +3754,10 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
                 fx_b(0);
             } else {   // ONE all-reduce: the P_sr r limbs and every rank's r' max (exact: integers)
                 fx_b(1);
-                MR_TRY(mr_coll_allreduce(ctx, gs[0]->fx_limb.p, 2 * (int64_t)gs[0]->N + ctx->nranks, MR_DT_U64, 0));
+                const int64_t nw = 2 * (int64_t)gs[0]->N + ctx->nranks;
+                const int prc = mr_peer_allreduce_u64(ctx, (unsigned long long*)gs[0]->fx_limb.p, nw);
+                if (prc == MR_ERR_STATE) MR_TRY(mr_coll_allreduce(ctx, gs[0]->fx_limb.p, nw, MR_DT_U64, 0));
+                else MR_TRY(prc);
                 fx_b(2);
             }
             MR_DEBUG_CHECK(ctx, "k_fx_b");
@@ -3231,7 +3772,10 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
                 hipLaunchKernelGGL(k_iter_b, dim3(blocks_b), dim3(TB), 0, st, dv.p, ng, d, alpha, it, 0);
             } else {   // ONE all-reduce: the per-op P_sr r sums (fp64 SUM) and every rank's r' max
                 hipLaunchKernelGGL(k_iter_b, dim3(blocks_b), dim3(TB), 0, st, dv.p, ng, d, alpha, it, 1);
-                MR_TRY(mr_coll_allreduce(ctx, gs[0]->op_sum.p, (int64_t)gs[0]->N + ctx->nranks, MR_DT_F64, 0));
+                const int64_t nw = (int64_t)gs[0]->N + ctx->nranks;
+                const int prc = mr_peer_allreduce_f64(ctx, gs[0]->op_sum.p, nw);
+                if (prc == MR_ERR_STATE) MR_TRY(mr_coll_allreduce(ctx, gs[0]->op_sum.p, nw, MR_DT_F64, 0));
+                else MR_TRY(prc);
                 hipLaunchKernelGGL(k_iter_b, dim3(blocks_b), dim3(TB), 0, st, dv.p, ng, d, alpha, it, 2);
             }
             MR_DEBUG_CHECK(ctx, "k_iter_b");
@@ -3248,6 +3792,11 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
                        fl.p);
     MR_DEBUG_CHECK(ctx, "k_weights");
     MR_TRY_HIP(ctx, hipGetLastError());
+    if (coll && ctx->peer_on) {   // a peer that never pushed its round: an error, not wrong sums
+        bool failed = false;
+        MR_TRY(mr_peer_error(ctx, &failed));
+        if (failed) return mr_fail(ctx, MR_ERR_COMM, "peer all-reduce: a rank did not arrive (timeout)");
+    }
     // a shard's local collision must make every rank retry: the error words meet in a MAX
     if (coll) {
         MR_TRY(mr_coll_allreduce(ctx, gs[0]->flag.p, 4, MR_DT_I32, 1));
@@ -3264,6 +3813,10 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         MR_TRY_HIP(ctx, hipStreamSynchronize(st));
     }
     for (int i = 0; i < ng; ++i) {
+        if (hflag[(size_t)4 * i + 3] & 1) {   // k_pr_cluster: a cluster's blocks were not co-resident
+            *timed_out = true;
+            return MR_OK;
+        }
         if (hflag[(size_t)4 * i] & 1) {
             *collided = true;
             return MR_OK;
@@ -3337,9 +3890,15 @@ int mr_pagerank_batch_impl(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly,
                            int iters, int precision, uint32_t flags, bool sharded = false) {
     constexpr int ATTEMPTS = 4;
     for (int a = 0; a < ATTEMPTS; ++a) {
-        bool collided = false;
+        bool collided = false, timed_out = false;
         MR_TRY(pagerank_attempt(ctx, gs, anomaly, ng, d, alpha, iters, precision, flags, sharded, kind_seed(a),
-                                kind_hmask(a), &collided));
+                                kind_hmask(a), &collided, &timed_out));
+        if (timed_out) {   // k_pr_cluster's clusters were not co-resident: per-iteration launches from now on
+            if (!ctx->no_persist) fprintf(stderr, "[microrank] k_pr_cluster timed out; launching per iteration\n");
+            ctx->no_persist = true;
+            --a;
+            continue;
+        }
         if (!collided) return MR_OK;
     }
     return mr_fail(ctx, MR_ERR_STATE, "trace-kind hash collision under %d seeds", ATTEMPTS);

@@ -99,6 +99,9 @@ __device__ __forceinline__ int64_t dl_lookback_wave(unsigned long long* st, int6
         __hip_atomic_store(&st[tile], dl_word(epoch, 2, excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return excl;
 }
+// LIMIT: the default single-pass path carries tile prefixes in the status words' 42-bit value
+// field, so the total must stay below 2^42 (4.4e12); every caller scans counts of rows, pairs,
+// traces or tiles (C5's 2e9 spans: < 2^31).  MR_SCAN_3PASS selects the 3-pass path (full int64).
 int mr_exclusive_scan(mr_ctx* ctx, const int64_t* in, int64_t* out, int64_t n, int64_t* tmp);
 // int32 counts -> int64 offsets
 int mr_exclusive_scan_i32(mr_ctx* ctx, const int32_t* in, int64_t* out, int64_t n, int64_t* tmp);

@@ -85,6 +85,14 @@ def use_rccl(ctx: "_lib.Context", group=None):
     ctx.check(lib.mr_comm_init(ctx.h, world, rank, ptr(uid, C.c_uint8)), "mr_comm_init")
 
 
+def use_peer(ctx: "_lib.Context", enable: bool = True):
+    """The per-iteration all-reduce through IPC-mapped peer memory (mr_comm_peer_enable): one
+    push of this rank's limbs into every rank's receive region, one local sum -- instead of the
+    RCCL / host-staged all-reduce.  Needs a collective backend first (use_rccl / use_host) for the
+    one-time exchange of the IPC handles."""
+    ctx.check(_lib.load().mr_comm_peer_enable(ctx.h, int(bool(enable))), "mr_comm_peer_enable")
+
+
 def sharded_pagerank(dg, anomaly: bool, d: float = 0.85, alpha: float = 0.01, iters: int = 25,
                      precision: str = "fp64"):
     """PageRank of the whole graph from this rank's shard ``dg`` (a DeviceGraph whose len_o /

@@ -81,15 +81,17 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("anomaly,empty_last", [(False, False), (True, False), (True, True)])
-def test_two_rank_sharded_pagerank_matches_single(anomaly, empty_last):
-    """empty_last: rank 1 holds no trace at all -- it still takes part in every reduction."""
+@pytest.mark.parametrize("anomaly,empty_last,world", [(False, False, 2), (True, False, 2), (True, True, 2),
+                                                      (True, False, 4)])
+def test_two_rank_sharded_pagerank_matches_single(anomaly, empty_last, world):
+    """empty_last: ranks >= 1 hold no trace at all -- they still take part in every reduction.
+    world 4: the decomposition over four ranks."""
     g = _window_graph()
     s_ref = orc.power_iteration(g, orc.preference(g, orc.trace_kinds(g), anomaly))
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, anomaly, q, empty_last)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, anomaly, q, empty_last)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in procs]
@@ -99,4 +101,5 @@ def test_two_rank_sharded_pagerank_matches_single(anomaly, empty_last):
     for rank, s, cov in res:
         np.testing.assert_allclose(s, s_ref, rtol=1e-12)
         np.testing.assert_array_equal(cov, np.bincount(g.sr_o, minlength=g.N))
-    assert res[0][1].tobytes() == res[1][1].tobytes(), "ranks disagree"
+    for r in res[1:]:
+        assert r[1].tobytes() == res[0][1].tobytes(), "ranks disagree"

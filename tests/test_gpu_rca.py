@@ -608,3 +608,66 @@ def test_c3_window_matches_reference_golden():
     res = rca_window(adf, start, end, slo)
     assert res["top"] == sp["top"] and (res["n_abnormal"], res["n_normal"]) == (len(abn), len(nor))
     np.testing.assert_allclose(np.array(res["score"], dtype=np.float64), unhex(sp["score"]), rtol=1e-10, atol=0)
+
+
+def test_windows_batch_reaper_and_context_destroy(c3_window, monkeypatch):
+    """large windows' graphs are held by the context and released by its NEXT
+    mr_windows_batch call (MR_WIN_REAP): two calls on one context with the reaper forced on give
+    bitwise the results of calls with it off; a context destroyed while it still holds such graphs
+    frees them, and a stale handle freed afterwards is a no-op."""
+    import bench
+    from microrank_amd import _lib
+    from microrank_amd.online_rca import rank_windows
+    from microrank_amd.preprocess_data import DeviceSpans
+
+    normal, abnormal, t0, t1 = c3_window
+    runs = {}
+    for reap in ("0", "1"):
+        monkeypatch.setenv("MR_WIN_REAP", reap)
+        cx = _lib.Context(0)
+        a3, ok = bench.slo_from_gpu(cx, normal)
+        dev = DeviceSpans(cx, abnormal)
+        wins = [(dev, t0, t1, a3, ok)] * 3
+        first = rank_windows(cx, wins)
+        second = rank_windows(cx, wins)    # reap=1: releases the first call's graphs meanwhile
+        runs[reap] = (first, second)
+        h = dev.h
+        cx.close()                         # reap=1: the second call's graphs are still held
+        assert _lib.load().mr_spans_free(h) == 0
+        dev.close()
+    for a, b in zip(runs["0"][0] + runs["0"][1], runs["1"][0] + runs["1"][1]):
+        assert a[2:] == b[2:] and list(a[0]) == list(b[0]) and a[1].tobytes() == b[1].tobytes()
+
+
+def test_windows_batch_persistent_equals_split(c3_window, monkeypatch):
+    """The window batch's PageRanks in one persistent launch per group (k_pr_cluster) equal,
+    bitwise, the same cut launched per iteration (MR_PR_PERSIST=split), and the launch-per-iteration
+    plan of round 2 (MR_PR_PERSIST=0) within 1e-12 with identical top lists."""
+    import bench
+    from microrank_amd import _lib
+    from microrank_amd.online_rca import rank_windows
+    from microrank_amd.preprocess_data import DeviceSpans
+
+    ctx = _lib.default_context()
+    normal, abnormal, t0, t1 = c3_window
+    a3, ok = bench.slo_from_gpu(ctx, normal)
+    devs = [DeviceSpans(ctx, abnormal)]
+    wins = [(devs[0], t0, t1, a3, ok)]
+    for seed in (61, 62, 63):
+        _, nrm, ab = bench.make_window(seed, 500, 20_000)
+        s3, sok = bench.slo_from_gpu(ctx, nrm)
+        d = DeviceSpans(ctx, ab)
+        devs.append(d)
+        u0 = int(ab.tstart.min())
+        wins.append((d, u0, u0 + 5 * 60 * 10**9, s3, sok))
+    runs = {}
+    for mode in ("1", "split", "0"):
+        monkeypatch.setenv("MR_PR_PERSIST", mode)
+        runs[mode] = rank_windows(ctx, wins)
+    for a, b in zip(runs["1"], runs["split"]):
+        assert a[2:] == b[2:] and list(a[0]) == list(b[0]) and a[1].tobytes() == b[1].tobytes()
+    for a, b in zip(runs["1"], runs["0"]):
+        assert a[2:] == b[2:] and list(a[0]) == list(b[0])
+        np.testing.assert_allclose(a[1], b[1], rtol=1e-12, atol=0)
+    for d in devs:
+        d.close()

@@ -38,7 +38,7 @@ def _whole(anomaly):
     return w, cov
 
 
-def _worker(rank, world, port, anomaly, backend, q, big=None, tile=False, walk_ranks=(), empty_last=False):
+def _worker(rank, world, port, anomaly, backend, q, big=None, tile=False, walk_ranks=(), empty_last=False, peer=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     if tile is True or (tile and rank in tile):   # True: every rank; a tuple: those ranks
         os.environ["MR_NO_FUSED"] = "1"   # read once, at this process's first graph prepare
@@ -55,6 +55,8 @@ def _worker(rank, world, port, anomaly, backend, q, big=None, tile=False, walk_r
             shard.use_host(ctx)
         else:
             shard.use_rccl(ctx)
+        if peer:
+            shard.use_peer(ctx)
         if big is None:
             g = _window_graph()
             bounds = [0] + [g.T] * world if empty_last else None   # rank 0 all traces, the rest none
@@ -74,12 +76,12 @@ def _worker(rank, world, port, anomaly, backend, q, big=None, tile=False, walk_r
         dist.destroy_process_group()
 
 
-def _run(world, anomaly, backend, big=None, tile=False, walk_ranks=(), empty_last=False):
+def _run(world, anomaly, backend, big=None, tile=False, walk_ranks=(), empty_last=False, peer=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_worker, args=(r, world, port, anomaly, backend, q, big, tile, walk_ranks,
-                                               empty_last))
+                                               empty_last, peer))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -101,6 +103,34 @@ def test_two_shards_one_gpu_match_whole_graph(anomaly):
         np.testing.assert_array_equal(cov, cov_ref)
     assert res[0][1].tobytes() == res[1][1].tobytes(), "ranks disagree"
     assert res[0][3]["T"] + res[1][3]["T"] == _window_graph().T
+
+
+@pytest.mark.parametrize("peer", [False, True])
+@pytest.mark.parametrize("tile", [False, True])
+def test_four_shards_one_gpu_match_whole_graph(tile, peer):
+    """FOUR processes share the GPU, a quarter of the window's traces each: the r' maxima ride the
+    all-reduce in four one-hot slots, the kind classes merge over four ranks.  peer: the
+    per-iteration all-reduce goes through IPC-mapped receive regions (mr_comm_peer_enable: every
+    rank writes its limbs into every rank's region and sums its own in rank order) instead of the
+    host-staged collective.  Fused path: the whole graph's weights within 1e-12 (exact integer
+    limbs); tile path (fp64 per-op sums): 1e-10; all ranks bitwise."""
+    w_ref, cov_ref = _whole(True)
+    res = _run(4, True, "host", tile=tile, peer=peer)
+    for rank, w, cov, info in res:
+        np.testing.assert_allclose(w, w_ref, rtol=1e-10 if tile else 1e-12, atol=0)
+        np.testing.assert_array_equal(cov, cov_ref)
+    for r in res[1:]:
+        assert r[1].tobytes() == res[0][1].tobytes(), "ranks disagree"
+    assert sum(r[3]["T"] for r in res) == _window_graph().T
+
+
+def test_four_shards_peer_matches_host_collective_bitwise():
+    """The peer all-reduce and the host-staged all-reduce give bitwise the same weights on the
+    fused path (both sum the same exact integer limbs)."""
+    a = _run(4, False, "host", peer=False)
+    b = _run(4, False, "host", peer=True)
+    for x, y in zip(a, b):
+        assert x[1].tobytes() == y[1].tobytes()
 
 
 def test_one_rank_rccl_matches_whole_graph():
@@ -250,12 +280,20 @@ def _span_table():
     return synth.gen_spans(topo, 6000, 9, branch=1.9, p_max=0.8, dup_span_frac=0.03, broken_frac=0.05, names=False)
 
 
+def _shard_owner(st, world):
+    """Rank of each trace code under SpanTable.shard(rank, world)."""
+    owner = np.full(st.n_traces, -1, np.int64)
+    for r in range(world):
+        owner[np.unique(st.shard(r, world).trace)] = r
+    return owner
+
+
 def _span_mask(st):
     rng = np.random.default_rng(4)
     return (rng.random(st.n_traces) < 0.7).astype(np.uint8)
 
 
-def _span_worker(rank, world, port, anomaly, q):
+def _span_worker(rank, world, port, anomaly, q, peer=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -265,6 +303,8 @@ def _span_worker(rank, world, port, anomaly, q):
         st = _span_table()
         ctx = _lib.Context(0)
         shard.use_host(ctx)
+        if peer:
+            shard.use_peer(ctx)
         dev = DeviceSpans(ctx, st.shard(rank, world))
         dg = shard.build_graph(dev, _span_mask(st))
         nodes = np.array(dg.nodes)
@@ -280,8 +320,9 @@ def _span_worker(rank, world, port, anomaly, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("anomaly", [False, True])
-def test_sharded_build_from_spans_matches_single_gpu(anomaly):
+@pytest.mark.parametrize("anomaly,world,peer", [(False, 2, False), (True, 2, False), (True, 4, False),
+                                                (False, 4, True)])
+def test_sharded_build_from_spans_matches_single_gpu(anomaly, world, peer):
     """Two ranks each build their graph from their own span shard (mr_graph_build_sharded: global
     node order over the ranks, T10; parent joins across the shards, T11) and rank it with
     mr_pagerank_sharded: node order equal to the single-GPU K1 graph of the whole table,
@@ -297,10 +338,12 @@ def test_sharded_build_from_spans_matches_single_gpu(anomaly):
     st = _span_table()
     mask = _span_mask(st)
     sel = mask[st.trace].astype(bool)
-    child_rank = st.trace[sel] % 2
+    owner = _shard_owner(st, world)
+    child_rank = owner[st.trace[sel]]
     par = st.parent[sel]
-    spans_by_rank = [set(st.span[sel & (st.trace % 2 == r)].tolist()) for r in range(2)]
-    cross = sum(1 for p, r in zip(par.tolist(), child_rank.tolist()) if p >= 0 and p in spans_by_rank[1 - r])
+    spans_by_rank = [set(st.span[sel & (owner[st.trace] == r)].tolist()) for r in range(world)]
+    cross = sum(1 for p, r in zip(par.tolist(), child_rank.tolist())
+                if p >= 0 and any(p in spans_by_rank[o] for o in range(world) if o != r))
     assert cross > 0, "no cross-rank parent joins in the test table"
     ctx = _lib.Context(0)
     dev = DeviceSpans(ctx, st)
@@ -323,7 +366,7 @@ def test_sharded_build_from_spans_matches_single_gpu(anomaly):
     mpc = mp.get_context("spawn")
     q = mpc.Queue()
     port = _free_port()
-    procs = [mpc.Process(target=_span_worker, args=(r, 2, port, anomaly, q)) for r in range(2)]
+    procs = [mpc.Process(target=_span_worker, args=(r, world, port, anomaly, q, peer)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=180) for _ in procs], key=lambda r: r[0])
@@ -335,6 +378,7 @@ def test_sharded_build_from_spans_matches_single_gpu(anomaly):
         np.testing.assert_array_equal(extra[0], nodes)
         np.testing.assert_allclose(w, w_ref, rtol=1e-10, atol=0)
         np.testing.assert_array_equal(cov, cov_ref)
-    assert res[0][1].tobytes() == res[1][1].tobytes(), "ranks disagree"
-    assert res[0][3][1]["T"] + res[1][3][1]["T"] == t.value
+    for r in res[1:]:
+        assert r[1].tobytes() == res[0][1].tobytes(), "ranks disagree"
+    assert sum(r[3][1]["T"] for r in res) == t.value
     assert res[0][3][1]["E"] == E_whole   # after the exchange: the whole graph's call edges
