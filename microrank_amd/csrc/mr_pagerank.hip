@@ -735,11 +735,14 @@ __global__ void __launch_bounds__(SCHED_T) k_tr_sched(const int32_t* coff, int32
     tr_sched_body((int64_t)blockIdx.x * SCHED_T + threadIdx.x, coff, n_wt, tids, items[threadIdx.x], rem[threadIdx.x],
                   cbuf[threadIdx.x], hot);
 }
-// MR_TR_SCHED=0: keep the rotated order (A/B)
+// MR_TR_SCHED=1: schedule the tiles (off by default: the greedy order of a trace depends on its
+// tile neighbours, and the counting sort that forms the tiles (k_tr_place) places traces of equal
+// length in a run-dependent order -- two preparations of one graph would then sum a trace's
+// entries in different orders, and runs would no longer be bitwise reproducible)
 static bool tr_sched_on() {
     static const bool on = [] {
         const char* e = getenv("MR_TR_SCHED");
-        return !(e && !strcmp(e, "0"));
+        return e && !strcmp(e, "1");
     }();
     return on;
 }
