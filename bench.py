@@ -116,7 +116,7 @@ def run_window(ctx, dev, t0, t1, a3, ok, prec):
     return edges.value, codes[:n_out.value].copy(), scores[:n_out.value].copy(), na.value, nn.value
 
 
-ITER_KERNELS = ("k_tr_a", "k_fx_b", "k_iter_a", "k_iter_b", "k_cold_trace", "k_cold_ops")
+ITER_KERNELS = ("k_tr_a", "k_fx_b", "k_iter_a", "k_iter_b", "k_cold_trace", "k_cold_ops", "k_pr_cluster")
 
 
 def kind_compressed_probe(ctx, dev, t0, t1, a3, ok, reps=5):
@@ -203,7 +203,8 @@ def pmc_traffic(args, timeout_s=240):
                     name = r["Kernel_Name"]
                     if r["Counter_Name"] == ctr and any(k in name for k in ITER_KERNELS):
                         per_iter += float(r["Counter_Value"])
-                        n_a += any(k in name for k in ("k_tr_a", "k_iter_a"))
+                        # iterations the dispatch covers: a persistent k_pr_cluster launch runs all 25
+                        n_a += 25 if "k_pr_cluster" in name else any(k in name for k in ("k_tr_a", "k_iter_a"))
             if n_a == 0:
                 return None
             vals[ctr] = per_iter / n_a * 1024.0   # KB -> bytes, per iteration
@@ -498,6 +499,102 @@ def run_sweep(args):
                         "windows_per_s": round(len(wins) / dt_slide, 2)}}
 
 
+def run_stream(args):
+    """SURVEY 8(f) f3 online -- RCAStream over a C3-shaped string stream (500 ops, 4000 traces per
+    minute, the reference's DataFrame schema) pushed in trace-aligned chunks of several sizes.  Per
+    chunk size: the table update of one push on its own (device mode: mr_spans_append -- the chunk
+    crosses PCIe, the resident rows are gathered and re-coded in HBM; host mode: pd.concat of the
+    resident frame + a full re-ingest, the round-2 RCAStream) once the resident table has reached
+    its steady size, and the whole stream's wall time through RCAStream in both modes (ranking
+    included).  The device update should scale with the chunk, the host one with the table."""
+    import contextlib
+    import io
+    import tempfile
+
+    import pandas as pd
+
+    from microrank_amd import _lib, synth
+    from microrank_amd.online_rca import RCAStream
+    from microrank_amd.preprocess_data import SpanStream, get_operation_slo, get_service_operation_list, span_table
+
+    minutes = args.stream_minutes
+    t_gen = time.perf_counter()
+    ndf, adf = synth.stream_dataframes(500, int(4000 * minutes), 1301, minutes=minutes, branch=1.9, p_max=0.8,
+                                       fault_ms=6000.0, fault_frac=0.0003)
+    print(f"[bench] stream: {len(adf)} spans generated in {time.perf_counter() - t_gen:.1f} s", file=sys.stderr,
+          flush=True)
+    ctx = _lib.default_context()
+    slo = get_operation_slo(get_service_operation_list(ndf), ndf)
+    op_list = list(slo)
+    t0 = adf["startTime"].min()
+    window = pd.Timedelta(minutes=5)
+    per_chunk = {}
+    for cm in args.stream_chunks:
+        bucket = ((adf["startTime"] - t0) // pd.Timedelta(minutes=cm)).to_numpy()
+        cuts = np.flatnonzero(np.diff(bucket)) + 1
+        bounds = np.concatenate([[0], cuts, [len(adf)]])
+        chunks = [adf.iloc[bounds[i]:bounds[i + 1]] for i in range(len(bounds) - 1)]
+        # steady state: the resident table holds the last 5 minutes + the chunk
+        dev_ms, host_ms, res_spans = [], [], []
+        st = SpanStream(ctx)
+        resident = None
+        for i, ch in enumerate(chunks):
+            keep_from = ch["startTime"].min() - window
+            ts = time.perf_counter()
+            st.append(ch, int(keep_from.value))
+            ctx.sync()
+            t_dev = time.perf_counter() - ts
+            ts = time.perf_counter()
+            resident = ch if resident is None else pd.concat([resident[resident["startTime"] >= keep_from], ch],
+                                                             ignore_index=True)
+            span_table(resident, ctx)
+            ctx.sync()
+            t_host = time.perf_counter() - ts
+            if ch["startTime"].min() - t0 >= window + pd.Timedelta(minutes=cm):
+                dev_ms.append(t_dev * 1e3)
+                host_ms.append(t_host * 1e3)
+                res_spans.append(st.table.n_spans)
+        st.close()
+        # the whole stream through RCAStream, both modes (same printed output)
+        walls, outs = {}, {}
+        cwd = os.getcwd()
+        with tempfile.TemporaryDirectory(dir="/tmp") as td:
+            os.chdir(td)
+            try:
+                for mode in (True, False):
+                    sink = io.StringIO()
+                    ts = time.perf_counter()
+                    with contextlib.redirect_stdout(sink):
+                        s = RCAStream(slo, op_list, ctx=ctx, device_append=mode)
+                        for ch in chunks:
+                            s.push(ch)
+                        s.close()
+                    ctx.sync()
+                    walls[mode] = time.perf_counter() - ts
+                    outs[mode] = sink.getvalue()
+            finally:
+                os.chdir(cwd)
+        n_chunk = [len(c) for c in chunks]
+        per_chunk[f"{cm:g}min"] = {
+            "chunks": len(chunks), "spans_per_chunk": int(np.mean(n_chunk)),
+            "resident_spans": int(np.mean(res_spans)) if res_spans else None,
+            "device_append_ms": round(float(np.median(dev_ms)), 2) if dev_ms else None,
+            "host_concat_reingest_ms": round(float(np.median(host_ms)), 2) if host_ms else None,
+            "stream_wall_s": {"device_append": round(walls[True], 3), "host_mode": round(walls[False], 3)},
+            "windows_printed": outs[True].count("total_trace"),
+            "same_output": outs[True] == outs[False]}
+        print(f"[bench] stream {cm:g} min chunks: {per_chunk[f'{cm:g}min']}", file=sys.stderr, flush=True)
+    best = per_chunk[f"{args.stream_chunks[0]:g}min"]
+    return {"metric": "RCAStream push: table update ms per chunk (SURVEY 8(f) f3 online)",
+            "value": best["device_append_ms"], "unit": "ms", "n_gpus": 1, "steps": len(args.stream_chunks),
+            "warmup": 0, "ms_per_step": best["device_append_ms"], "higher_is_better": False, "scaling": "none",
+            "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic reference-schema span DataFrames (strings), pushed in trace-start order",
+            "config": {"workload": f"{minutes:g} minutes of C3-shaped traffic (500 ops, 4000 traces/min, "
+                                   f"{len(adf)} spans), chunk sizes {args.stream_chunks} min",
+                       "per_chunk": per_chunk}}
+
+
 def run_dropin(args):
     """The north star's drop-in path, measured: the reference driver's window body
     (online_rca.py:167-201 -- system_anomaly_detect, get_pagerank_graph + trace_pagerank twice,
@@ -666,13 +763,16 @@ def main():
     ap.add_argument("--streams-mode", action="store_true",
                     help="c2/c3: W contexts + W host threads, one mr_rca_window per window (instead of mr_windows_batch)")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
-    ap.add_argument("--config", choices=["c2", "c3", "c4", "c5", "sweep", "ingest", "dropin"], default="c2",
+    ap.add_argument("--config", choices=["c2", "c3", "c4", "c5", "sweep", "stream", "ingest", "dropin"], default="c2",
                     help="c2: RCA windows (default, weak scaling); c3: a batch of --c3-windows 500-op / 20k-trace "
                          "windows split over the ranks (strong scaling); c4 / c5: one trace-sharded graph (strong "
                          "scaling; c5 = 100k ops / 100M traces fp32, the wide fused iteration); sweep: the driver's "
                          "window sweep over a long stream (f3); ingest: strings -> device span table (f2); "
                          "dropin: the reference driver's window body through the drop-in modules (C1, C2)")
     ap.add_argument("--sweep-minutes", type=float, default=240.0, help="sweep: minutes of traffic in the stream")
+    ap.add_argument("--stream-minutes", type=float, default=30.0, help="stream: minutes of traffic pushed")
+    ap.add_argument("--stream-chunks", type=float, nargs="+", default=[0.5, 1.0, 2.0, 5.0],
+                    help="stream: chunk sizes in minutes (the first one is the headline)")
     ap.add_argument("--sweep-fault", type=float, default=0.00005, help="sweep: fraction of traces hit by the fault")
     ap.add_argument("--c3-windows", type=int, default=4096, help="c3: windows in the whole batch (all ranks)")
     ap.add_argument("--c3-distinct", type=int, default=4,
@@ -709,7 +809,7 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # PMC passes first, in child processes, before this process initialises the GPU
     traffic = None
-    if world == 1 and not args.pmc_child and not args.no_traffic and args.config not in ("sweep", "ingest", "dropin"):
+    if world == 1 and not args.pmc_child and not args.no_traffic and args.config not in ("sweep", "stream", "ingest", "dropin"):
         traffic = pmc_traffic(args, timeout_s=240 if args.config in ("c2", "c3") else 400)
     dist = None
     if world > 1:
@@ -717,12 +817,12 @@ def main():
 
         dist.init_process_group("gloo")
     os.environ.setdefault("MICRORANK_DEVICE", str(local))
-    if args.config in ("sweep", "ingest", "dropin"):   # single-GPU supplementary lines (f2 / f3 / drop-in)
+    if args.config in ("sweep", "stream", "ingest", "dropin"):   # single-GPU supplementary lines (f2 / f3 / drop-in)
         if args.config in ("ingest", "dropin") and "--steps" not in sys.argv:
             args.steps, args.warmup = 5, 1
         if args.config == "sweep" and "--steps" not in sys.argv:
             args.steps, args.warmup = 3, 1
-        out = {"sweep": run_sweep, "ingest": run_ingest, "dropin": run_dropin}[args.config](args)
+        out = {"sweep": run_sweep, "stream": run_stream, "ingest": run_ingest, "dropin": run_dropin}[args.config](args)
         print(json.dumps(out), flush=True)
         return
     if args.config in ("c4", "c5"):

@@ -61,8 +61,10 @@ int         mr_ctx_sync(mr_ctx* ctx);
 /* stream the context launches on (a hipStream_t), for callers that time with HIP events */
 void*       mr_ctx_stream(mr_ctx* ctx);
 /* live timing of the power-iteration kernel: while enabled every launch is bracketed by HIP
- * events on the context stream; mr_ctx_prof_read syncs, returns the launch count, the summed
- * kernel time and the summed algorithmic bytes (SURVEY §8(d) B_iter), and clears the record */
+ * events on the context stream; mr_ctx_prof_read syncs, returns the number of ITERATIONS the
+ * recorded launches covered (one per launch pair; all of a call's for a persistent k_pr_cluster
+ * launch), the summed kernel time and the summed algorithmic bytes (SURVEY §8(d) B_iter), and
+ * clears the record */
 int         mr_ctx_profile(mr_ctx* ctx, int enable);
 int         mr_ctx_prof_read(mr_ctx* ctx, int64_t* launches, double* total_ms, double* total_bytes);
 
@@ -164,6 +166,19 @@ int mr_spans_info(const mr_spans* s, int64_t* n_spans, int32_t* n_traces, int32_
 /* first row of each code in code order, which 0 trace / 1 pod-op / 2 service-op (ingested tables):
  * name of code k = that row's traceID / podName_op / serviceName_op */
 int mr_spans_dict_rows(const mr_spans* s, int which, int32_t* rows);
+/* SURVEY 8(f) f3, streaming: a new table = the rows of `prev` whose trace-level start is >=
+ * keep_from (ns), in their order, then the chunk's rows -- the same table mr_spans_ingest builds
+ * from those rows' strings.  The string columns stay on the device, so only the chunk crosses
+ * PCIe (the resident rows are gathered device to device and re-coded there).  prev: NULL (the
+ * first chunk) or a table this function returned on the same context; it stays valid (free it
+ * with mr_spans_free).  The chunk needs tstart / tend.  Replaces the reference's per-window
+ * re-read of the whole span frame (online_rca.py:161-216 over preprocess_data.get_span, :10-14). */
+int mr_spans_append(mr_ctx* ctx, const mr_spans* prev, int64_t keep_from, const mr_span_strings* chunk,
+                    mr_spans** out);
+/* tables from mr_spans_append: the stream row number (position in the concatenation of every
+ * chunk appended so far) of each code's first row, in code order -- mr_spans_dict_rows in stream
+ * terms, so the host can read names from the chunk that holds the row */
+int mr_spans_dict_sources(const mr_spans* s, int which, int64_t* src);
 /* the code columns of a table (any pointer may be NULL), [n_spans] each */
 int mr_spans_codes(const mr_spans* s, int32_t* trace, int32_t* podop, int32_t* svcop, int64_t* span,
                    int64_t* parent);

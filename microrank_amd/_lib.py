@@ -82,6 +82,8 @@ SIGNATURES = {
     "mr_spans_ingest": (C.c_int, [P, C.POINTER(SpanStrings), C.POINTER(P)]),
     "mr_spans_info": (C.c_int, [P, i64p, i32p, i32p, i32p]),
     "mr_spans_dict_rows": (C.c_int, [P, C.c_int, i32p]),
+    "mr_spans_append": (C.c_int, [P, P, C.c_int64, C.POINTER(SpanStrings), C.POINTER(P)]),
+    "mr_spans_dict_sources": (C.c_int, [P, C.c_int, i64p]),
     "mr_spans_codes": (C.c_int, [P, i32p, i32p, i32p, i64p, i64p]),
     "mr_graph_build": (C.c_int, [P, P, u8p, C.POINTER(P)]),
     "mr_graph_nodes": (C.c_int, [P, i32p, i32p]),

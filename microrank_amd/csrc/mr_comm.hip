@@ -152,7 +152,10 @@ int mr_coll_allgather(mr_ctx* ctx, const void* dsend, void* drecv, int64_t n, in
 // across devices); slots alternate by round parity, so a rank one round ahead never overwrites a
 // slot still being summed (its next push of that parity needs every rank's flag of the round
 // between).  Every spin is bounded (PEER_TIMEOUT): a missing peer becomes an error, not a hang.
-constexpr int PEER_FLAGS = 64;                         // flag words (<= 63 ranks) + the error word
+// region: [flag words][all-reduce slots: 2 parities x R x W][exchange area A][exchange area B]
+// flag words: [0, 64) all-reduce arrivals by source rank, [64, 127) exchange arrivals by source,
+// 127 the error word
+constexpr int PEER_FLAGS = 128, PEER_XF = 64, PEER_ERR = 127, PEER_MAXR = 63;
 constexpr int PEER_T = 256;
 constexpr unsigned long long PEER_TIMEOUT = 200000000ull;   // 2 s of the 100 MHz s_memrealtime clock
 #define GLBP __attribute__((address_space(1)))
@@ -190,7 +193,7 @@ __global__ void __launch_bounds__(PEER_T) k_peer_reduce(T* __restrict__ dst, int
                 __builtin_amdgcn_s_sleep(2);
                 if (__builtin_amdgcn_s_memrealtime() - t0 > PEER_TIMEOUT) {
                     s_ok = 0;
-                    __hip_atomic_store(reg + (PEER_FLAGS - 1), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    __hip_atomic_store(reg + PEER_ERR, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     break;
                 }
             }
@@ -221,22 +224,30 @@ void mr_comm_peer_destroy(mr_ctx* ctx) {
     if (ctx->peer_dev) (void)hipFree(ctx->peer_dev);
     ctx->peer_region = nullptr;
     ctx->peer_dev = nullptr;
-    ctx->peer_words = 0;
-    ctx->peer_seq = 0;
+    ctx->peer_words = ctx->peer_xa = ctx->peer_xb = 0;
+    ctx->peer_seq = ctx->peer_xseq = 0;
 }
 
 // (collective) a receive region of at least `words` words per slot on every rank, mapped everywhere
-static int peer_ensure(mr_ctx* ctx, int64_t words) {
-    if (ctx->peer_region && ctx->peer_words >= words) return MR_OK;
+// (collective: every rank asks for the same sizes) words per all-reduce slot, words of exchange
+// areas A and B; a region too small is replaced (and re-exported) on every rank
+static int peer_ensure(mr_ctx* ctx, int64_t words, int64_t xa = 0, int64_t xb = 0) {
+    if (ctx->peer_region && ctx->peer_words >= words && ctx->peer_xa >= xa && ctx->peer_xb >= xb) return MR_OK;
     const int R = ctx->nranks;
-    if (R > PEER_FLAGS - 1) return mr_fail(ctx, MR_ERR_ARG, "peer all-reduce: at most %d ranks", PEER_FLAGS - 1);
+    if (R > PEER_MAXR) return mr_fail(ctx, MR_ERR_ARG, "peer collectives: at most %d ranks", PEER_MAXR);
+    words = std::max(words, ctx->peer_words);
+    xa = std::max(xa, ctx->peer_xa);
+    xb = std::max(xb, ctx->peer_xb);
     mr_comm_peer_destroy(ctx);
-    const size_t bytes = ((size_t)PEER_FLAGS + 2 * (size_t)R * (size_t)words) * sizeof(unsigned long long);
+    const size_t bytes = ((size_t)PEER_FLAGS + 2 * (size_t)R * (size_t)words + (size_t)xa + (size_t)xb) *
+                         sizeof(unsigned long long);
     MR_TRY_HIP(ctx, hipExtMallocWithFlags(&ctx->peer_region, bytes, hipDeviceMallocUncached));
     MR_TRY_HIP(ctx, hipMemsetAsync(ctx->peer_region, 0, bytes, ctx->stream));
     MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));
     ctx->peer_words = words;
-    ctx->peer_seq = 0;
+    ctx->peer_xa = xa;
+    ctx->peer_xb = xb;
+    ctx->peer_seq = ctx->peer_xseq = 0;
     hipIpcMemHandle_t mine;
     MR_TRY_HIP(ctx, hipIpcGetMemHandle(&mine, ctx->peer_region));
     static_assert(sizeof(hipIpcMemHandle_t) % 8 == 0, "IPC handle size");
@@ -292,12 +303,71 @@ int mr_peer_error(mr_ctx* ctx, bool* failed) {
     *failed = false;
     if (!ctx->peer_region) return MR_OK;
     unsigned long long w = 0;
-    MR_TRY_HIP(ctx, hipMemcpyAsync(&w, (unsigned long long*)ctx->peer_region + (PEER_FLAGS - 1), 8,
+    MR_TRY_HIP(ctx, hipMemcpyAsync(&w, (unsigned long long*)ctx->peer_region + PEER_ERR, 8,
                                    hipMemcpyDeviceToHost, ctx->stream));
     MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));
     *failed = w != 0;
     return MR_OK;
 }
+
+// ---- exchanges (all-to-all) through the regions' areas A and B: a round is a set of puts into
+// other ranks' areas, then one signal per destination; a rank waits for every source's signal
+constexpr int PUT_B = 64;   // blocks of a put kernel (grid-stride): each counts once at its destination
+__global__ void __launch_bounds__(PEER_T) k_peer_put(const unsigned long long* __restrict__ src, int64_t n,
+                                                     unsigned long long* dst) {
+    for (int64_t j = (int64_t)blockIdx.x * PEER_T + threadIdx.x; j < n; j += (int64_t)PUT_B * PEER_T)
+        __hip_atomic_store((GLBP unsigned long long*)dst + j, src[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// after the round's puts (earlier launches on this stream, complete): one signal per destination
+__global__ void k_peer_signal(unsigned long long* const* __restrict__ peers, int nranks, int rank) {
+    if ((int)threadIdx.x < nranks) {
+        __atomic_thread_fence(__ATOMIC_RELEASE);
+        __hip_atomic_fetch_add((GLBP unsigned long long*)peers[threadIdx.x] + PEER_XF + rank, 1ull, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+__global__ void k_peer_wait(unsigned long long* region, int nranks, unsigned long long need) {
+    GLBP unsigned long long* reg = (GLBP unsigned long long*)region;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (int r = 0; r < nranks; ++r)
+        while (__hip_atomic_load(reg + PEER_XF + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < need) {
+            __builtin_amdgcn_s_sleep(2);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > PEER_TIMEOUT) {
+                __hip_atomic_store(reg + PEER_ERR, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                return;
+            }
+        }
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);
+}
+
+bool mr_peer_ready(const mr_ctx* ctx) { return ctx->peer_on && ctx->nranks >= 2 && mr_coll_ready(ctx); }
+
+int mr_peer_xensure(mr_ctx* ctx, int64_t xa, int64_t xb) { return peer_ensure(ctx, 1, xa, xb); }
+
+unsigned long long* mr_peer_area(mr_ctx* ctx, int rank, int area) {
+    unsigned long long* base = (unsigned long long*)ctx->peer_map[(size_t)rank];
+    return base + PEER_FLAGS + 2 * (size_t)ctx->nranks * (size_t)ctx->peer_words + (area ? (size_t)ctx->peer_xa : 0);
+}
+
+int mr_peer_put(mr_ctx* ctx, const unsigned long long* d_src, int64_t n, int rank, int area, int64_t offset) {
+    if (n <= 0) return MR_OK;
+    hipLaunchKernelGGL(k_peer_put, dim3(PUT_B), dim3(PEER_T), 0, ctx->stream, d_src, n,
+                       mr_peer_area(ctx, rank, area) + offset);
+    MR_TRY_HIP(ctx, hipGetLastError());
+    return MR_OK;
+}
+
+// the round's signals, then the wait for every rank's
+int mr_peer_round(mr_ctx* ctx) {
+    const uint64_t x = ctx->peer_xseq++;
+    hipLaunchKernelGGL(k_peer_signal, dim3(1), dim3(64), 0, ctx->stream, ctx->peer_dev, ctx->nranks, ctx->rank);
+    hipLaunchKernelGGL(k_peer_wait, dim3(1), dim3(1), 0, ctx->stream, (unsigned long long*)ctx->peer_region,
+                       ctx->nranks, (unsigned long long)(x + 1));
+    MR_TRY_HIP(ctx, hipGetLastError());
+    return MR_OK;
+}
+
+unsigned long long* const* mr_peer_map_dev(mr_ctx* ctx) { return ctx->peer_dev; }
 
 extern "C" int mr_comm_peer_enable(mr_ctx* ctx, int enable) {
     if (!ctx) return MR_ERR_ARG;

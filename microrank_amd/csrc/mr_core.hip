@@ -163,6 +163,7 @@ static void prof_clear(mr_ctx* ctx) {
     for (hipEvent_t e : ctx->prof_ev) (void)hipEventDestroy(e);
     ctx->prof_ev.clear();
     ctx->prof_bytes.clear();
+    ctx->prof_iters.clear();
 }
 
 extern "C" int mr_ctx_profile(mr_ctx* ctx, int enable) {
@@ -183,7 +184,9 @@ extern "C" int mr_ctx_prof_read(mr_ctx* ctx, int64_t* launches, double* total_ms
         ms += t;
         by += ctx->prof_bytes[i / 2];
     }
-    if (launches) *launches = (int64_t)(ctx->prof_ev.size() / 2);
+    int64_t its = 0;   // iterations covered (a persistent launch covers all of a call's)
+    for (size_t i = 0; i < ctx->prof_bytes.size(); ++i) its += i < ctx->prof_iters.size() ? ctx->prof_iters[i] : 1;
+    if (launches) *launches = its;
     if (total_ms) *total_ms = ms;
     if (total_bytes) *total_bytes = by;
     prof_clear(ctx);
@@ -198,13 +201,14 @@ void mr_prof_begin(mr_ctx* ctx) {
     (void)hipEventRecord(e, ctx->stream);
     ctx->prof_ev.push_back(e);
 }
-void mr_prof_end(mr_ctx* ctx, double bytes) {
+void mr_prof_end(mr_ctx* ctx, double bytes, int64_t iters) {
     if (!ctx->prof) return;
     hipEvent_t e;
     if (hipEventCreate(&e) != hipSuccess) return;
     (void)hipEventRecord(e, ctx->stream);
     ctx->prof_ev.push_back(e);
     ctx->prof_bytes.push_back(bytes);
+    ctx->prof_iters.push_back(iters);
 }
 
 static std::mutex g_handles_mu;

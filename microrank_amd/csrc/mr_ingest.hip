@@ -294,6 +294,8 @@ static int build_dict(mr_ctx* ctx, const Cols& c, int d, int64_t S, bool sorted,
     return MR_OK;
 }
 
+static const char* const COL_NAME[6] = {"traceID", "spanID", "ParentSpanId", "serviceName", "operationName", "podName"};
+
 static int upload_str(mr_ctx* ctx, const mr_str_col& col, int64_t S, const char* name, DBuf<int64_t>& off,
                       DBuf<uint8_t>& bytes) {
     if (!col.offsets) return mr_fail(ctx, MR_ERR_ARG, "mr_spans_ingest: column %s missing", name);
@@ -314,81 +316,270 @@ static int upload_str(mr_ctx* ctx, const mr_str_col& col, int64_t S, const char*
     return MR_OK;
 }
 
-extern "C" int mr_spans_ingest(mr_ctx* ctx, const mr_span_strings* in, mr_spans** out) {
-    if (!ctx || !in || !out) return mr_fail(ctx, MR_ERR_ARG, "mr_spans_ingest: null argument");
-    *out = nullptr;
+static int check_strings(mr_ctx* ctx, const mr_span_strings* in, const char* fn) {
     const int64_t S = in->n_spans;
-    if (S <= 0 || S >= (1ll << 31)) return mr_fail(ctx, MR_ERR_ARG, "n_spans out of range (1 .. 2^31-1)");
-    if (!in->duration) return mr_fail(ctx, MR_ERR_ARG, "mr_spans_ingest: duration missing");
+    if (S <= 0 || S >= (1ll << 31)) return mr_fail(ctx, MR_ERR_ARG, "%s: n_spans out of range (1 .. 2^31-1)", fn);
+    if (!in->duration) return mr_fail(ctx, MR_ERR_ARG, "%s: duration missing", fn);
     const mr_str_col* sc[6] = {&in->trace_id, &in->span_id, &in->parent_id, &in->service, &in->operation, &in->pod};
-    static const char* nm[6] = {"traceID", "spanID", "ParentSpanId", "serviceName", "operationName", "podName"};
     for (int k = 0; k < 6; ++k)
         if (k != C_PARENT && sc[k]->valid)
-            return mr_fail(ctx, MR_ERR_ARG, "mr_spans_ingest: column %s must have no nulls", nm[k]);
+            return mr_fail(ctx, MR_ERR_ARG, "%s: column %s must have no nulls", fn, COL_NAME[k]);
     for (int k = 0; k < 6; ++k)
         for (int64_t i = 0; i < S; ++i)
             if (sc[k]->offsets && sc[k]->offsets[i + 1] < sc[k]->offsets[i])
-                return mr_fail(ctx, MR_ERR_ARG, "mr_spans_ingest: column %s: offsets not ascending", nm[k]);
-    MR_TRY_HIP(ctx, hipSetDevice(ctx->device));
+                return mr_fail(ctx, MR_ERR_ARG, "%s: column %s: offsets not ascending", fn, COL_NAME[k]);
+    return MR_OK;
+}
+
+// The dictionaries, code columns and index of a table whose string columns are on the device
+// (c: offsets / bytes / validity; op_len is filled here).  s->S, the value columns and the
+// times flag are set by the caller.
+static int ingest_core(mr_ctx* ctx, Cols c, mr_spans* s) {
     hipStream_t st = ctx->stream;
-    DBuf<int64_t> off[6];
-    DBuf<uint8_t> bytes[6], valid2;
-    for (int k = 0; k < 6; ++k) MR_TRY(upload_str(ctx, *sc[k], S, nm[k], off[k], bytes[k]));
-    if (in->parent_id.valid) MR_TRY(valid2.upload(ctx, in->parent_id.valid, (size_t)(S + 7) / 8));
+    const int64_t S = s->S;
     DBuf<int32_t> op_len;
     MR_TRY(op_len.alloc(ctx, (size_t)S));
-    Cols c;
-    for (int k = 0; k < 6; ++k) {
-        c.off[k] = off[k].p;
-        c.bytes[k] = bytes[k].p;
-    }
-    c.valid2 = in->parent_id.valid ? valid2.p : nullptr;
     c.op_len = op_len.p;
     hipLaunchKernelGGL(k_op_len, dim3(cdiv(S, IB)), dim3(IB), 0, st, c, S, op_len.p);
-    auto* s = new mr_spans();
-    s->ctx = ctx;
-    s->S = S;
-    s->has_times = in->tstart && in->tend;
     s->row_bits = bits_for((uint64_t)std::max<int64_t>(S, 1));
-    int rc = MR_OK;
-    auto fail = [&](int code) {
-        delete s;
-        return code;
-    };
     IngestDict dt, dp, dv, ds;
     uint64_t x = 0, xs = 0;
-    if ((rc = build_dict(ctx, c, 0, S, true, dt, &x)) || (rc = build_dict(ctx, c, 1, S, true, dp, &x)) ||
-        (rc = build_dict(ctx, c, 2, S, true, dv, &x)) || (rc = build_dict(ctx, c, 3, S, false, ds, &xs)))
-        return fail(rc);
+    MR_TRY(build_dict(ctx, c, 0, S, true, dt, &x));
+    MR_TRY(build_dict(ctx, c, 1, S, true, dp, &x));
+    MR_TRY(build_dict(ctx, c, 2, S, true, dv, &x));
+    MR_TRY(build_dict(ctx, c, 3, S, false, ds, &xs));
     s->n_traces = (int32_t)dt.U;
     s->n_podops = (int32_t)dp.U;
     s->n_svcops = (int32_t)dv.U;
     s->n_span_codes = ds.U;
-    if ((rc = s->trace.alloc(ctx, (size_t)S)) || (rc = s->podop.alloc(ctx, (size_t)S)) ||
-        (rc = s->svcop.alloc(ctx, (size_t)S)) || (rc = s->span.alloc(ctx, (size_t)S)) ||
-        (rc = s->parent.alloc(ctx, (size_t)S)) || (rc = s->duration.upload(ctx, in->duration, (size_t)S)))
-        return fail(rc);
-    if (s->has_times && ((rc = s->tstart.upload(ctx, in->tstart, (size_t)S)) || (rc = s->tend.upload(ctx, in->tend, (size_t)S))))
-        return fail(rc);
+    MR_TRY(s->trace.alloc(ctx, (size_t)S));
+    MR_TRY(s->podop.alloc(ctx, (size_t)S));
+    MR_TRY(s->svcop.alloc(ctx, (size_t)S));
+    MR_TRY(s->span.alloc(ctx, (size_t)S));
+    MR_TRY(s->parent.alloc(ctx, (size_t)S));
     hipLaunchKernelGGL(k_codes<int32_t>, dim3(cdiv(S, IB)), dim3(IB), 0, st, dt.cls.p, dt.code_of_run.p, S, s->trace.p);
     hipLaunchKernelGGL(k_codes<int32_t>, dim3(cdiv(S, IB)), dim3(IB), 0, st, dp.cls.p, dp.code_of_run.p, S, s->podop.p);
     hipLaunchKernelGGL(k_codes<int32_t>, dim3(cdiv(S, IB)), dim3(IB), 0, st, dv.cls.p, dv.code_of_run.p, S, s->svcop.p);
     hipLaunchKernelGGL(k_codes<int64_t>, dim3(cdiv(S, IB)), dim3(IB), 0, st, ds.cls.p, (const int32_t*)nullptr, S,
                        s->span.p);
     hipLaunchKernelGGL(k_parent, dim3(cdiv(S, IB)), dim3(IB), 0, st, c, S, xs, ds.rkey.p, ds.rep.p, ds.U, s->parent.p);
-    if (hipGetLastError() != hipSuccess) return fail(mr_fail(ctx, MR_ERR_HIP, "mr_spans_ingest: kernel launch failed"));
+    if (hipGetLastError() != hipSuccess) return mr_fail(ctx, MR_ERR_HIP, "mr_spans_ingest: kernel launch failed");
     // the representative row of every code, for the host's name lists (mr_spans_dict_rows)
-    if ((rc = s->dict_rows[0].alloc(ctx, (size_t)std::max(s->n_traces, 1))) ||
-        (rc = s->dict_rows[1].alloc(ctx, (size_t)std::max(s->n_podops, 1))) ||
-        (rc = s->dict_rows[2].alloc(ctx, (size_t)std::max(s->n_svcops, 1))))
-        return fail(rc);
-    if (hipMemcpyAsync(s->dict_rows[0].p, dt.rep_sorted.p, dt.U * sizeof(int32_t), hipMemcpyDeviceToDevice, st) ||
-        hipMemcpyAsync(s->dict_rows[1].p, dp.rep_sorted.p, dp.U * sizeof(int32_t), hipMemcpyDeviceToDevice, st) ||
-        hipMemcpyAsync(s->dict_rows[2].p, dv.rep_sorted.p, dv.U * sizeof(int32_t), hipMemcpyDeviceToDevice, st))
-        return fail(mr_fail(ctx, MR_ERR_HIP, "mr_spans_ingest: copy failed"));
-    if ((rc = mr_spans_finish(ctx, s))) return fail(rc);
-    mr_handle_add(ctx, s, [](void* h) { delete (mr_spans*)h; });
-    *out = s;
+    MR_TRY(s->dict_rows[0].alloc(ctx, (size_t)std::max(s->n_traces, 1)));
+    MR_TRY(s->dict_rows[1].alloc(ctx, (size_t)std::max(s->n_podops, 1)));
+    MR_TRY(s->dict_rows[2].alloc(ctx, (size_t)std::max(s->n_svcops, 1)));
+    MR_TRY_HIP(ctx, hipMemcpyAsync(s->dict_rows[0].p, dt.rep_sorted.p, dt.U * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
+    MR_TRY_HIP(ctx, hipMemcpyAsync(s->dict_rows[1].p, dp.rep_sorted.p, dp.U * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
+    MR_TRY_HIP(ctx, hipMemcpyAsync(s->dict_rows[2].p, dv.rep_sorted.p, dv.U * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
+    return mr_spans_finish(ctx, s);
+}
+
+extern "C" int mr_spans_ingest(mr_ctx* ctx, const mr_span_strings* in, mr_spans** out) {
+    if (!ctx || !in || !out) return mr_fail(ctx, MR_ERR_ARG, "mr_spans_ingest: null argument");
+    *out = nullptr;
+    MR_TRY(check_strings(ctx, in, "mr_spans_ingest"));
+    const int64_t S = in->n_spans;
+    const mr_str_col* sc[6] = {&in->trace_id, &in->span_id, &in->parent_id, &in->service, &in->operation, &in->pod};
+    MR_TRY_HIP(ctx, hipSetDevice(ctx->device));
+    DBuf<int64_t> off[6];
+    DBuf<uint8_t> bytes[6], valid2;
+    for (int k = 0; k < 6; ++k) MR_TRY(upload_str(ctx, *sc[k], S, COL_NAME[k], off[k], bytes[k]));
+    if (in->parent_id.valid) MR_TRY(valid2.upload(ctx, in->parent_id.valid, (size_t)(S + 7) / 8));
+    Cols c;
+    for (int k = 0; k < 6; ++k) {
+        c.off[k] = off[k].p;
+        c.bytes[k] = bytes[k].p;
+    }
+    c.valid2 = in->parent_id.valid ? valid2.p : nullptr;
+    std::unique_ptr<mr_spans> s(new mr_spans());
+    s->ctx = ctx;
+    s->S = S;
+    s->has_times = in->tstart && in->tend;
+    MR_TRY(s->duration.upload(ctx, in->duration, (size_t)S));
+    if (s->has_times) {
+        MR_TRY(s->tstart.upload(ctx, in->tstart, (size_t)S));
+        MR_TRY(s->tend.upload(ctx, in->tend, (size_t)S));
+    }
+    MR_TRY(ingest_core(ctx, c, s.get()));
+    mr_handle_add(ctx, s.get(), [](void* h) { delete (mr_spans*)h; });
+    *out = s.release();
+    return MR_OK;
+}
+
+// ---------------------------------------------------------------------------------- streaming
+// mr_spans_append: the previous table's rows whose trace-level start is >= keep_from, then the
+// chunk's rows, as one new table -- the same table mr_spans_ingest builds from those rows' strings
+// in that order.  The kept rows are gathered device to device; only the chunk crosses PCIe.
+namespace {
+__global__ void k_keep_flag(const int64_t* tstart, int64_t n, int64_t keep_from, int32_t* flag) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) flag[i] = tstart[i] >= keep_from ? 1 : 0;
+}
+// from[j] = the source of output row j: a kept row i of the previous table (< Sp) or Sp + b for
+// chunk row b
+__global__ void k_keep_from(const int32_t* flag, const int64_t* pos, int64_t Sp, int64_t K, int64_t Sc, int64_t* from) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < Sp && flag[i]) from[pos[i]] = i;
+    if (i < Sc) from[K + i] = Sp + i;
+}
+struct StrSrc {
+    const int64_t* off[2];    // previous table / chunk
+    const uint8_t* bytes[2];
+};
+__global__ void k_str_len(const int64_t* from, int64_t S, int64_t Sp, StrSrc src, int64_t* len) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= S) return;
+    const int64_t f = from[j];
+    const int w = f >= Sp;
+    const int64_t r = w ? f - Sp : f;
+    len[j] = src.off[w][r + 1] - src.off[w][r];
+}
+// one wave per row, a byte per lane: rows are tens of bytes, so the copy stays coalesced
+__global__ void k_str_copy(const int64_t* from, int64_t S, int64_t Sp, StrSrc src, const int64_t* off, uint8_t* out) {
+    const int64_t j = (int64_t)blockIdx.x * (blockDim.x / WAVE) + threadIdx.x / WAVE;
+    const int lane = threadIdx.x & (WAVE - 1);
+    if (j >= S) return;
+    const int64_t f = from[j];
+    const int w = f >= Sp;
+    const int64_t r = w ? f - Sp : f;
+    const int64_t b0 = src.off[w][r], n = src.off[w][r + 1] - b0, o = off[j];
+    for (int64_t k = lane; k < n; k += WAVE) out[o + k] = src.bytes[w][b0 + k];
+}
+// ParentSpanId validity, 8 rows per output byte (a source without a bitmap: all valid)
+__global__ void k_valid_pack(const int64_t* from, int64_t S, int64_t Sp, const uint8_t* vp, const uint8_t* vc,
+                             uint8_t* out) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q * 8 >= S) return;
+    unsigned v = 0;
+    for (int b = 0; b < 8 && q * 8 + b < S; ++b) {
+        const int64_t f = from[q * 8 + b];
+        const uint8_t* m = f >= Sp ? vc : vp;
+        const int64_t r = f >= Sp ? f - Sp : f;
+        if (!m || ((m[r >> 3] >> (r & 7)) & 1u)) v |= 1u << b;
+    }
+    out[q] = (uint8_t)v;
+}
+// value columns: previous table's value, or the chunk's (chunk == null: src_base + chunk row)
+__global__ void k_gather_i64(const int64_t* from, int64_t S, int64_t Sp, const int64_t* prev, const int64_t* chunk,
+                             int64_t src_base, int64_t* out) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= S) return;
+    const int64_t f = from[j];
+    out[j] = f < Sp ? prev[f] : chunk ? chunk[f - Sp] : src_base + (f - Sp);
+}
+__global__ void k_dict_src(const int32_t* rows, int64_t n, const int64_t* src, int64_t* out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = src[rows[i]];
+}
+}  // namespace
+
+extern "C" int mr_spans_append(mr_ctx* ctx, const mr_spans* prev, int64_t keep_from, const mr_span_strings* in,
+                               mr_spans** out) {
+    if (!ctx || !in || !out) return mr_fail(ctx, MR_ERR_ARG, "mr_spans_append: null argument");
+    *out = nullptr;
+    if (prev && (prev->ctx != ctx || !prev->raw))
+        return mr_fail(ctx, MR_ERR_STATE, "mr_spans_append: the previous table was not built by mr_spans_append on this context");
+    MR_TRY(check_strings(ctx, in, "mr_spans_append"));
+    if (!in->tstart || !in->tend) return mr_fail(ctx, MR_ERR_ARG, "mr_spans_append: trace start / end times missing");
+    const int64_t Sc = in->n_spans, Sp = prev ? prev->S : 0;
+    const mr_str_col* sc[6] = {&in->trace_id, &in->span_id, &in->parent_id, &in->service, &in->operation, &in->pod};
+    MR_TRY_HIP(ctx, hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    // the chunk: one upload
+    DBuf<int64_t> off[6], cdur, cts, cte;
+    DBuf<uint8_t> bytes[6], cvalid;
+    for (int k = 0; k < 6; ++k) MR_TRY(upload_str(ctx, *sc[k], Sc, COL_NAME[k], off[k], bytes[k]));
+    if (in->parent_id.valid) MR_TRY(cvalid.upload(ctx, in->parent_id.valid, (size_t)(Sc + 7) / 8));
+    MR_TRY(cdur.upload(ctx, in->duration, (size_t)Sc));
+    MR_TRY(cts.upload(ctx, in->tstart, (size_t)Sc));
+    MR_TRY(cte.upload(ctx, in->tend, (size_t)Sc));
+    // the kept rows of the previous table
+    int64_t K = 0;
+    DBuf<int32_t> flag;
+    DBuf<int64_t> pos, tmp;
+    MR_TRY(tmp.alloc(ctx, (size_t)std::max<int64_t>(scan_tmp_elems(Sp + Sc), 1)));   // covers both scans
+    if (Sp) {
+        MR_TRY(flag.alloc(ctx, (size_t)Sp));
+        MR_TRY(pos.alloc(ctx, (size_t)Sp + 1));
+        hipLaunchKernelGGL(k_keep_flag, dim3(cdiv(Sp, IB)), dim3(IB), 0, st, prev->tstart.p, Sp, keep_from, flag.p);
+        MR_TRY(mr_exclusive_scan_i32(ctx, flag.p, pos.p, Sp, tmp.p));
+        MR_TRY(mr_read_words(ctx, pos.p + Sp, 1, &K));
+    }
+    const int64_t S = K + Sc;
+    if (S >= (1ll << 31)) return mr_fail(ctx, MR_ERR_ARG, "mr_spans_append: table would exceed 2^31-1 spans");
+    DBuf<int64_t> from;
+    MR_TRY(from.alloc(ctx, (size_t)S));
+    hipLaunchKernelGGL(k_keep_from, dim3(cdiv(std::max(Sp, Sc), IB)), dim3(IB), 0, st, flag.p, pos.p, Sp, K, Sc, from.p);
+    std::unique_ptr<mr_spans> s(new mr_spans());
+    s->ctx = ctx;
+    s->S = S;
+    s->has_times = true;
+    s->raw = true;
+    // string columns: lengths -> offsets -> bytes
+    DBuf<int64_t> len;
+    MR_TRY(len.alloc(ctx, (size_t)S));
+    Cols c;
+    for (int k = 0; k < 6; ++k) {
+        StrSrc src;
+        src.off[0] = prev ? prev->raw_off[k].p : nullptr;
+        src.bytes[0] = prev ? prev->raw_bytes[k].p : nullptr;
+        src.off[1] = off[k].p;
+        src.bytes[1] = bytes[k].p;
+        MR_TRY(s->raw_off[k].alloc(ctx, (size_t)S + 1));
+        hipLaunchKernelGGL(k_str_len, dim3(cdiv(S, IB)), dim3(IB), 0, st, from.p, S, Sp, src, len.p);
+        MR_TRY(mr_exclusive_scan(ctx, len.p, s->raw_off[k].p, S, tmp.p));
+        int64_t nb = 0;
+        MR_TRY(mr_read_words(ctx, s->raw_off[k].p + S, 1, &nb));
+        MR_TRY(s->raw_bytes[k].alloc(ctx, (size_t)nb + 16));
+        MR_TRY_HIP(ctx, hipMemsetAsync(s->raw_bytes[k].p + nb, 0, 16, st));
+        hipLaunchKernelGGL(k_str_copy, dim3(cdiv(S, IB / WAVE)), dim3(IB), 0, st, from.p, S, Sp, src,
+                           s->raw_off[k].p, s->raw_bytes[k].p);
+        c.off[k] = s->raw_off[k].p;
+        c.bytes[k] = s->raw_bytes[k].p;
+    }
+    const uint8_t* pv = prev && prev->raw_valid.p ? prev->raw_valid.p : nullptr;
+    c.valid2 = nullptr;
+    if (pv || cvalid.p) {
+        MR_TRY(s->raw_valid.alloc(ctx, (size_t)(S + 7) / 8));
+        hipLaunchKernelGGL(k_valid_pack, dim3(cdiv((S + 7) / 8, IB)), dim3(IB), 0, st, from.p, S, Sp, pv, cvalid.p,
+                           s->raw_valid.p);
+        c.valid2 = s->raw_valid.p;
+    }
+    // value columns and the stream row numbers
+    const int64_t src_base = prev ? prev->src_next : 0;
+    MR_TRY(s->duration.alloc(ctx, (size_t)S));
+    MR_TRY(s->tstart.alloc(ctx, (size_t)S));
+    MR_TRY(s->tend.alloc(ctx, (size_t)S));
+    MR_TRY(s->src.alloc(ctx, (size_t)S));
+    hipLaunchKernelGGL(k_gather_i64, dim3(cdiv(S, IB)), dim3(IB), 0, st, from.p, S, Sp, prev ? prev->duration.p : nullptr,
+                       cdur.p, 0, s->duration.p);
+    hipLaunchKernelGGL(k_gather_i64, dim3(cdiv(S, IB)), dim3(IB), 0, st, from.p, S, Sp, prev ? prev->tstart.p : nullptr,
+                       cts.p, 0, s->tstart.p);
+    hipLaunchKernelGGL(k_gather_i64, dim3(cdiv(S, IB)), dim3(IB), 0, st, from.p, S, Sp, prev ? prev->tend.p : nullptr,
+                       cte.p, 0, s->tend.p);
+    hipLaunchKernelGGL(k_gather_i64, dim3(cdiv(S, IB)), dim3(IB), 0, st, from.p, S, Sp, prev ? prev->src.p : nullptr,
+                       (const int64_t*)nullptr, src_base, s->src.p);
+    MR_TRY_HIP(ctx, hipGetLastError());
+    s->src_next = src_base + Sc;
+    MR_TRY(ingest_core(ctx, c, s.get()));
+    MR_TRY_HIP(ctx, hipStreamSynchronize(st));   // the chunk's staging buffers are released on return
+    mr_handle_add(ctx, s.get(), [](void* h) { delete (mr_spans*)h; });
+    *out = s.release();
+    return MR_OK;
+}
+
+extern "C" int mr_spans_dict_sources(const mr_spans* s, int which, int64_t* src) {
+    if (!s || which < 0 || which > 2 || !src) return MR_ERR_ARG;
+    mr_ctx* ctx = s->ctx;
+    if (!s->raw) return mr_fail(ctx, MR_ERR_STATE, "mr_spans_dict_sources: table was not built by mr_spans_append");
+    const int64_t n = which == 0 ? s->n_traces : which == 1 ? s->n_podops : s->n_svcops;
+    MR_TRY_HIP(ctx, hipSetDevice(ctx->device));
+    DBuf<int64_t> out;
+    MR_TRY(out.alloc(ctx, (size_t)std::max<int64_t>(n, 1)));
+    if (n) hipLaunchKernelGGL(k_dict_src, dim3(cdiv(n, IB)), dim3(IB), 0, ctx->stream, s->dict_rows[which].p, n, s->src.p, out.p);
+    MR_TRY_HIP(ctx, hipGetLastError());
+    MR_TRY(out.download(ctx, src, (size_t)n));
+    MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));
     return MR_OK;
 }
 

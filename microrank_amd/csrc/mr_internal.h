@@ -33,6 +33,7 @@ struct mr_ctx {
     bool prof = false;
     std::vector<hipEvent_t> prof_ev;
     std::vector<double> prof_bytes;
+    std::vector<int64_t> prof_iters;   // iterations each record covers (k_pr_cluster: all of a call's)
     // stream-ordered caching allocator: every buffer of this context is used on `stream` only,
     // so a block released by one call can be handed to the next without a hipFree/hipMalloc
     // (each of which synchronises the device and costs tens of microseconds)
@@ -60,10 +61,11 @@ struct mr_ctx {
     // peer_words u64] -- and every rank's region mapped into this process (peer_map[rank] = ours)
     bool peer_on = false;
     void* peer_region = nullptr;
-    int64_t peer_words = 0;
+    int64_t peer_words = 0, peer_xa = 0, peer_xb = 0;   // all-reduce slot words, exchange areas
     std::vector<void*> peer_map;
     unsigned long long** peer_dev = nullptr;   // device copy of peer_map
     uint64_t peer_seq = 0;                      // all-reduces completed (the flags count them)
+    uint64_t peer_xseq = 0;                     // exchange rounds completed
     // k_pr_cluster timed out on this context (its clusters were not co-resident): launch per
     // iteration from then on
     bool no_persist = false;
@@ -114,6 +116,11 @@ struct DBuf {
     DBuf(const DBuf&) = delete;
     DBuf& operator=(const DBuf&) = delete;
     ~DBuf() { reset(); }
+    void swap(DBuf& o) {
+        std::swap(p, o.p);
+        std::swap(n, o.n);
+        std::swap(owner, o.owner);
+    }
     void reset() {
         if (p) mr_pool_free(owner, p);
         p = nullptr;
@@ -184,7 +191,6 @@ struct mr_graph {
     DBuf<int32_t> coff;              // [n_wt+1] first chunk of a tile
     std::vector<int32_t> coff_h;     // host copy (the per-wave tile split of a launch)
     DBuf<float> w_tp, c_tp;          // [T] w_t, c_t in position order
-    DBuf<int32_t> hot;               // [HOT_N + 1] the layout's hot ops (tile chunk 0) and their count
     // kind compression (MR_PR_KIND_COMPRESS): a graph of one representative trace per kind whose
     // q carries the kind's multiplicity (mw_tp = w_t * mult in position order); kind = mult
     bool kinds_given = false;
@@ -316,6 +322,15 @@ struct mr_spans {
     // tables ingested from strings (mr_spans_ingest): the first row of each trace / pod-op /
     // service-op code, in code order (the host builds the name lists from them)
     DBuf<int32_t> dict_rows[3];
+    // streaming tables (mr_spans_append): the six string columns stay on the device (offsets +
+    // bytes with 16 zero bytes of tail padding, ParentSpanId validity bitmap or empty) so the next
+    // append uploads only its chunk, and src[row] numbers every row by its position in the stream
+    // of appended chunks (the host looks names up in the chunk that holds that row)
+    bool raw = false;
+    DBuf<int64_t> raw_off[6];
+    DBuf<uint8_t> raw_bytes[6], raw_valid;
+    DBuf<int64_t> src;
+    int64_t src_next = 0;
 };
 
 int mr_spans_index(mr_ctx* ctx, mr_spans* s);
@@ -337,6 +352,13 @@ inline bool mr_coll_ready(const mr_ctx* ctx) { return ctx->comm || ctx->host_col
 int mr_peer_allreduce_u64(mr_ctx* ctx, unsigned long long* dbuf, int64_t n);
 int mr_peer_allreduce_f64(mr_ctx* ctx, double* dbuf, int64_t n);   // (fp64 sums in rank order)
 int mr_peer_error(mr_ctx* ctx, bool* failed);   // a round timed out (a peer never pushed)
+// exchanges through the peer regions: areas A (0) and B (1) of every rank's region
+bool mr_peer_ready(const mr_ctx* ctx);
+int mr_peer_xensure(mr_ctx* ctx, int64_t xa, int64_t xb);    // (collective) area sizes in words
+unsigned long long* mr_peer_area(mr_ctx* ctx, int rank, int area);   // rank's area as mapped here
+int mr_peer_put(mr_ctx* ctx, const unsigned long long* d_src, int64_t n, int rank, int area, int64_t offset);
+int mr_peer_round(mr_ctx* ctx);   // signal every rank, wait until every rank signalled this round
+unsigned long long* const* mr_peer_map_dev(mr_ctx* ctx);   // [nranks] device table of the regions
 void mr_comm_peer_destroy(mr_ctx* ctx);
 
 // MR_WIN_TIMING diagnostics: wall-clock phase marks (each mark synchronises the stream)

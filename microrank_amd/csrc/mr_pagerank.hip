@@ -392,96 +392,12 @@ __global__ void __launch_bounds__(TRB) k_tr_place(const int64_t* off, int32_t T,
     tr_place_body<TR_PER>((int32_t)blockIdx.x, off, T, nbin, boff, hist, taken, w_t, tperm, w_tp);
 }
 // chunks of 4 ids per wave tile (its last position holds its longest trace: lengths ascend), their
-// ---- hot chunk (k_tr_a's LDS traffic): an op in most traces (the root op in
-// every one) hits the same LDS accumulator word from every lane of a 16-lane atomic group -- a
-// 16-way serialised atomic no order of the ids avoids.  The HOT_N most covered ops (each in at
-// least 1/8 of the traces) get a fixed place instead: chunk 0 of every tile holds hot op q at
-// position q for the traces that have it (else the lane's pad).  k_tr_a adds X_t for them into
-// per-lane registers and folds those into the accumulator once per wave run; their su reads are
-// broadcasts.  hot[HOT_N] = how many hot ops the layout has (0: no hot chunk).
-// (2: the two per-lane u64 registers keep k_tr_a at 8 waves per SIMD; with 4 it drops to 7)
-constexpr int HOT_N = 2;
-static_assert(HOT_N >= 1 && HOT_N <= 4, "the hot chunk holds at most 4 positions");
-// the layout's hot ops (labels: perm maps a label to its op for relabelled graphs); one block
-__device__ __forceinline__ void hot_ops_body(const int32_t* __restrict__ cov, int32_t N, int32_t T,
-                                             const int32_t* __restrict__ perm, int32_t* __restrict__ hot) {
-    __shared__ unsigned long long red[256 / WAVE];
-    __shared__ int32_t chosen[HOT_N];
-    int n_hot = 0;
-    for (int h = 0; h < HOT_N; ++h) {
-        unsigned long long best = 0ull;   // (coverage << 32) | ~label: most covered, then lowest label
-        for (int32_t l = threadIdx.x; l < N; l += 256) {
-            bool taken = false;
-            for (int j = 0; j < h; ++j) taken = taken || chosen[j] == l;
-            if (taken) continue;
-            const uint32_t c = (uint32_t)cov[perm ? perm[l] : l];
-            best = max(best, ((unsigned long long)c << 32) | (unsigned long long)(0xffffffffu - (uint32_t)l));
-        }
-#pragma unroll
-        for (int m = 32; m >= 1; m >>= 1) best = max(best, (unsigned long long)__shfl_xor((long long)best, m, WAVE));
-        if ((threadIdx.x & (WAVE - 1)) == 0) red[threadIdx.x / WAVE] = best;
-        __syncthreads();
-        best = red[0];
-        for (int w = 1; w < 256 / WAVE; ++w) best = max(best, red[w]);
-        __syncthreads();
-        const int64_t c = (int64_t)(best >> 32);
-        if (best == 0ull || c * 8 < (int64_t)T) break;   // in fewer than 1/8 of the traces
-        if (threadIdx.x == 0) chosen[h] = (int32_t)(0xffffffffu - (uint32_t)(best & 0xffffffffull));
-        n_hot = h + 1;
-        __syncthreads();
-    }
-    if (threadIdx.x < HOT_N) hot[threadIdx.x] = (int32_t)threadIdx.x < n_hot ? chosen[threadIdx.x] : -1;
-    if (threadIdx.x == 0) hot[HOT_N] = n_hot;
-}
-__global__ void __launch_bounds__(256) k_hot_ops(const int32_t* __restrict__ cov, int32_t N, int32_t T,
-                                                 const int32_t* __restrict__ perm, int32_t* __restrict__ hot) {
-    hot_ops_body(cov, N, T, perm, hot);
-}
-__device__ __forceinline__ bool is_hot(uint32_t x, int32_t h0, int32_t h1, int32_t h2, int32_t h3) {
-    return (int32_t)x == h0 || (int32_t)x == h1 || (int32_t)x == h2 || (int32_t)x == h3;
-}
-// chunks of each wave tile with a hot chunk: 1 + ceil(max over its traces of the non-hot ids / 4);
-// a wave per tile
-__device__ __forceinline__ void tr_tnc_body(int32_t blk, const int32_t* tperm, const int64_t* off, const uint16_t* ids,
-                                            int32_t T, int32_t n_wt, const int32_t* hot, int32_t* tnc) {
-    const int64_t i = (int64_t)blk * blockDim.x + threadIdx.x;
-    const int32_t k = (int32_t)(i / WAVE), lane = (int32_t)(i % WAVE);
-    if (k >= n_wt) return;   // (whole waves: blockDim is a multiple of WAVE)
-    const int32_t hn = hot[HOT_N], h0 = hot[0], h1 = HOT_N > 1 ? hot[1] : -1, h2 = HOT_N > 2 ? hot[2] : -1,
-                  h3 = HOT_N > 3 ? hot[3] : -1;
-    const int64_t p = (int64_t)k * WAVE + lane;
-    int64_t m = 0;
-    if (p < T) {
-        const int32_t t = tperm[p];
-        const int64_t a = off[t], b = off[t + 1];
-        m = b - a;
-        if (hn > 0)
-            for (int64_t e = a; e < b; ++e) m -= is_hot(ids[e], h0, h1, h2, h3) ? 1 : 0;
-    }
-#pragma unroll
-    for (int s = 32; s >= 1; s >>= 1) m = max(m, (int64_t)__shfl_xor((long long)m, s, WAVE));
-    if (lane == 0) tnc[k] = (int32_t)((hn > 0 ? 1 : 0) + ((m + 3) >> 2));
-}
-__global__ void k_tr_tnc(const int32_t* tperm, const int64_t* off, const uint16_t* ids, int32_t T, int32_t n_wt,
-                         const int32_t* hot, int32_t* tnc) {
-    tr_tnc_body((int32_t)blockIdx.x, tperm, off, ids, T, n_wt, hot, tnc);
-}
-// MR_TR_HOT=0: no hot chunk (A/B)
-static bool tr_hot_on() {
-    static const bool on = [] {
-        const char* e = getenv("MR_TR_HOT");
-        return !(e && !strcmp(e, "0"));
-    }();
-    return on;
-}
-
 // exclusive prefix and its int32 copy in one launch: runs of TS_TILE wave tiles per block, chained
 // by decoupled look-back
 constexpr int TS_T = 256, TS_I = 8, TS_TILE = TS_T * TS_I;
 __device__ __forceinline__ void tr_chunk_scan_body(int32_t tile_, int32_t ntiles, const int32_t* tperm,
                                                    const int64_t* off, int32_t T, int32_t n_wt, int64_t* c64,
-                                                   int32_t* coff, unsigned long long* st, uint64_t epoch,
-                                                   const int32_t* tnc) {
+                                                   int32_t* coff, unsigned long long* st, uint64_t epoch) {
     __shared__ int64_t sa[TS_T];
     __shared__ int64_t ex;
     const int tid = threadIdx.x;
@@ -492,12 +408,8 @@ __device__ __forceinline__ void tr_chunk_scan_body(int32_t tile_, int32_t ntiles
         const int64_t k = base + i;
         v[i] = 0;
         if (k < n_wt) {
-            if (tnc) {   // (hot chunk layouts: counted by k_tr_tnc)
-                v[i] = tnc[k];
-            } else {
-                const int32_t t = tperm[min(k * WAVE + WAVE - 1, (int64_t)T - 1)];
-                v[i] = (off[t + 1] - off[t] + 3) >> 2;
-            }
+            const int32_t t = tperm[min(k * WAVE + WAVE - 1, (int64_t)T - 1)];
+            v[i] = (off[t + 1] - off[t] + 3) >> 2;
         }
         a += v[i];
     }
@@ -531,8 +443,8 @@ __device__ __forceinline__ void tr_chunk_scan_body(int32_t tile_, int32_t ntiles
 }
 __global__ void __launch_bounds__(TS_T) k_tr_chunk_scan(const int32_t* tperm, const int64_t* off, int32_t T, int32_t n_wt,
                                                         int64_t* c64, int32_t* coff, unsigned long long* st,
-                                                        uint64_t epoch, const int32_t* tnc) {
-    tr_chunk_scan_body((int32_t)blockIdx.x, (int32_t)gridDim.x, tperm, off, T, n_wt, c64, coff, st, epoch, tnc);
+                                                        uint64_t epoch) {
+    tr_chunk_scan_body((int32_t)blockIdx.x, (int32_t)gridDim.x, tperm, off, T, n_wt, c64, coff, st, epoch);
 }
 __global__ void k_tr_coff(const int64_t* c64, int32_t n, int32_t* coff) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -600,8 +512,7 @@ __global__ void __launch_bounds__(TC_T) k_tr_cut_b(CutBatch b) {
 }
 // thread per (tile, lane): the lane's trace rotated by (trace mod len), then pads N + lane
 __device__ __forceinline__ void tr_fill_body(int32_t blk, const int32_t* tperm, const int64_t* off, const uint16_t* ids,
-                                             const int64_t* c64, int32_t T, int32_t N, int32_t n_wt, uint16_t* tids,
-                                             const int32_t* hot) {
+                                             const int64_t* c64, int32_t T, int32_t N, int32_t n_wt, uint16_t* tids) {
     const int64_t i = (int64_t)blk * blockDim.x + threadIdx.x;
     if (i >= (int64_t)n_wt * WAVE) return;
     const int32_t k = (int32_t)(i / WAVE), lane = (int32_t)(i % WAVE);
@@ -615,42 +526,17 @@ __device__ __forceinline__ void tr_fill_body(int32_t blk, const int32_t* tperm, 
     }
     const int64_t nc = c64[k + 1] - c64[k];
     unsigned long long* dst = (unsigned long long*)tids + (size_t)c64[k] * WAVE + lane;   // 4 ids per 8-B store
-    const int32_t hn = hot ? hot[HOT_N] : 0;
-    const int32_t h0 = hn > 0 ? hot[0] : -1, h1 = hn > 0 && HOT_N > 1 ? hot[1] : -1,
-                  h2 = hn > 0 && HOT_N > 2 ? hot[2] : -1, h3 = hn > 0 && HOT_N > 3 ? hot[3] : -1;
-    int64_t c = 0;
-    if (hn > 0) {   // the hot chunk: hot op q at position q where the trace has it, else the pad
-        const int32_t hq[4] = {h0, h1, h2, h3};
+    // the ids from the rotation start, padded with N + lane
+    int64_t jj = rot;
+    for (int64_t c = 0; c < nc; ++c) {
         unsigned long long v = 0ull;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            uint32_t id = (uint32_t)(N + lane);
-            if (q < hn)
-                for (int64_t e = a; e < a + len; ++e)
-                    if ((int32_t)ids[e] == hq[q]) {
-                        id = (uint32_t)hq[q];
-                        break;
-                    }
-            v |= (unsigned long long)(id & 0xffffu) << (16 * q);
-        }
-        dst[0] = v;
-        c = 1;
-    }
-    // the other ids from the rotation start (the hot ones skipped), padded with N + lane
-    int64_t jj = rot, used = 0;
-    for (; c < nc; ++c) {
-        unsigned long long v = 0ull;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
+            const int64_t e = 4 * c + q;
             uint16_t id = (uint16_t)(N + lane);
-            while (used < len) {
-                const uint16_t x = ids[a + jj];
-                ++used;
+            if (e < len) {
+                id = ids[a + jj];
                 if (++jj == len) jj = 0;
-                if (!is_hot(x, h0, h1, h2, h3)) {
-                    id = x;
-                    break;
-                }
             }
             v |= (unsigned long long)id << (16 * q);
         }
@@ -658,117 +544,28 @@ __device__ __forceinline__ void tr_fill_body(int32_t blk, const int32_t* tperm, 
     }
 }
 __global__ void k_tr_fill(const int32_t* tperm, const int64_t* off, const uint16_t* ids, const int64_t* c64, int32_t T,
-                          int32_t N, int32_t n_wt, uint16_t* tids, const int32_t* hot) {
-    tr_fill_body((int32_t)blockIdx.x, tperm, off, ids, c64, T, N, n_wt, tids, hot);
-}
-// Bank-conflict-aware order of a tile's ids (k_tr_a's LDS traffic).  Per step
-// every lane reads su[o] (ds_read_b64: lanes in groups of 32, 8-B slot o mod 32) and adds into
-// lacc[o] (u64 LDS atomic: groups of 16, slot o mod 16; equal addresses serialise).  A trace's ops
-// can be walked in any order, so per 32-lane half of a tile one thread assigns each lane's items
-// (ops and pads) to steps greedily: lane by lane, the first remaining item whose atomic slot is
-// free in its 16-lane group and whose read slot is free (or holds the same op) in the half; else
-// one clear for the atomic; else any.  Pads (N + lane) are items too.  Tiles longer than
-// SCHED_L steps keep the rotated order.  Deterministic: a graph's layout (hence its fp64 sums) is
-// the same every time it is prepared.
-constexpr int SCHED_T = 16, SCHED_L = 64;
-__device__ __forceinline__ void tr_sched_body(int64_t u, const int32_t* coff, int32_t n_wt, uint16_t* tids,
-                                              uint16_t* items, unsigned long long* rem, uint16_t* cbuf,
-                                              const int32_t* hot) {
-    if (u >= 2 * (int64_t)n_wt) return;
-    const int32_t tile = (int32_t)(u >> 1), half = (int32_t)(u & 1);
-    const int32_t hc = hot && hot[HOT_N] > 0 ? 1 : 0;   // (the hot chunk keeps its fixed places)
-    const int32_t c0 = coff[tile] + hc, nc = coff[tile + 1] - c0, L = 4 * nc;
-    if (L > SCHED_L || nc <= 0) return;
-    unsigned long long* w = (unsigned long long*)tids + (size_t)c0 * WAVE + 32 * half;   // chunk c, lane li: w[c * WAVE + li]
-    for (int32_t c = 0; c < nc; ++c)
-        for (int li = 0; li < 32; ++li) {
-            const unsigned long long v = w[(size_t)c * WAVE + li];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) items[li * SCHED_L + 4 * c + q] = (uint16_t)(v >> (16 * q));
-        }
-    const unsigned long long full = L == 64 ? ~0ull : ((1ull << L) - 1ull);
-    for (int li = 0; li < 32; ++li) rem[li] = full;
-    for (int32_t s = 0; s < L; ++s) {
-        uint32_t used16[2] = {0u, 0u};
-        uint32_t occ32 = 0u;             // read slots taken this step ...
-        uint16_t op32[32];               // ... and by which op (a broadcast when equal)
-        for (int li = 0; li < 32; ++li) {
-            const int g = li >> 4;
-            const uint16_t* it = items + li * SCHED_L;
-            unsigned long long m = rem[li];
-            int best = -1, best_sc = 4;
-            while (m) {
-                const int j = __builtin_ctzll(m);
-                m &= m - 1ull;
-                const uint32_t o = it[j];
-                const uint32_t b16 = o & 15u, b32 = o & 31u;
-                const int sc = (int)((used16[g] >> b16) & 1u) * 2 + (int)(((occ32 >> b32) & 1u) && op32[b32] != o);
-                if (sc < best_sc) {
-                    best_sc = sc;
-                    best = j;
-                    if (sc == 0) break;
-                }
-            }
-            const uint32_t o = it[best];
-            rem[li] &= ~(1ull << best);
-            used16[g] |= 1u << (o & 15u);
-            if (!((occ32 >> (o & 31u)) & 1u)) {
-                occ32 |= 1u << (o & 31u);
-                op32[o & 31u] = (uint16_t)o;
-            }
-            cbuf[li * 4 + (s & 3)] = (uint16_t)o;
-        }
-        if ((s & 3) == 3)
-            for (int li = 0; li < 32; ++li) {
-                unsigned long long v = 0ull;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) v |= (unsigned long long)cbuf[li * 4 + q] << (16 * q);
-                w[(size_t)(s >> 2) * WAVE + li] = v;
-            }
-    }
-}
-__global__ void __launch_bounds__(SCHED_T) k_tr_sched(const int32_t* coff, int32_t n_wt, uint16_t* tids,
-                                                      const int32_t* hot) {
-    __shared__ uint16_t items[SCHED_T][32 * SCHED_L];
-    __shared__ unsigned long long rem[SCHED_T][32];
-    __shared__ uint16_t cbuf[SCHED_T][32 * 4];
-    tr_sched_body((int64_t)blockIdx.x * SCHED_T + threadIdx.x, coff, n_wt, tids, items[threadIdx.x], rem[threadIdx.x],
-                  cbuf[threadIdx.x], hot);
-}
-// MR_TR_SCHED=1: schedule the tiles (off by default: the greedy order of a trace depends on its
-// tile neighbours, and the counting sort that forms the tiles (k_tr_place) places traces of equal
-// length in a run-dependent order -- two preparations of one graph would then sum a trace's
-// entries in different orders, and runs would no longer be bitwise reproducible)
-static bool tr_sched_on() {
-    static const bool on = [] {
-        const char* e = getenv("MR_TR_SCHED");
-        return e && !strcmp(e, "1");
-    }();
-    return on;
+                          int32_t N, int32_t n_wt, uint16_t* tids) {
+    tr_fill_body((int32_t)blockIdx.x, tperm, off, ids, c64, T, N, n_wt, tids);
 }
 // The prepare of several small fused graphs (a window's two) in one launch per step: block ranges
 // per graph, the same bodies (mr_graph_prepare_batch)
 struct PDev {
     int32_t T, N, nbin, W, nz, n_cs;
     int64_t nnz, st_off;
-    int32_t b_gc, b_th, b_cs, b_fill, b_sch;
+    int32_t b_gc, b_th, b_cs, b_fill;
     const int32_t *len_t, *len_o, *nchild, *rs_ops;
     const int64_t* rs_off;
     float *w_t, *u_o, *pw, *w_tp;
     uint16_t *rs16, *tids;
     int32_t *trz, *tperm, *coff;
     int64_t* c64;
-    const int32_t* cov;
-    int32_t *hot, *tnc;   // hot ops (HOT_N + 1 words), chunks per wave tile (null: no hot chunk)
-    int32_t b_tnc;
 };
 __device__ __forceinline__ int32_t pd_graph(const PDev* pd, int32_t n, int32_t blk, int which) {
     int32_t lo = 0, hi = n - 1;
     while (lo < hi) {
         const int32_t mid = (lo + hi + 1) >> 1;
         const PDev& g = pd[mid];
-        const int32_t s0 = which == 0 ? g.b_gc : which == 1 ? g.b_th : which == 2 ? g.b_cs : which == 3 ? g.b_fill :
-                           which == 4 ? g.b_sch : g.b_tnc;
+        const int32_t s0 = which == 0 ? g.b_gc : which == 1 ? g.b_th : which == 2 ? g.b_cs : g.b_fill;
         if (s0 <= blk) lo = mid; else hi = mid - 1;
     }
     return lo;
@@ -791,27 +588,11 @@ __global__ void __launch_bounds__(TS_T) k_tr_chunk_scan_b(const PDev* __restrict
                                                          uint64_t epoch) {
     const PDev& G = pd[pd_graph(pd, n, (int32_t)blockIdx.x, 2)];
     tr_chunk_scan_body((int32_t)blockIdx.x - G.b_cs, G.n_cs, G.tperm, G.rs_off, G.T, G.W, G.c64, G.coff, st + G.st_off,
-                       epoch, G.tnc);
-}
-__global__ void __launch_bounds__(256) k_hot_ops_b(const PDev* __restrict__ pd) {   // block g: graph g
-    const PDev& G = pd[blockIdx.x];
-    hot_ops_body(G.cov, G.N, G.T, nullptr, G.hot);
-}
-__global__ void k_tr_tnc_b(const PDev* __restrict__ pd, int32_t n) {
-    const PDev& G = pd[pd_graph(pd, n, (int32_t)blockIdx.x, 5)];
-    tr_tnc_body((int32_t)blockIdx.x - G.b_tnc, G.tperm, G.rs_off, G.rs16, G.T, G.W, G.hot, G.tnc);
+                       epoch);
 }
 __global__ void k_tr_fill_b(const PDev* __restrict__ pd, int32_t n) {
     const PDev& G = pd[pd_graph(pd, n, (int32_t)blockIdx.x, 3)];
-    tr_fill_body((int32_t)blockIdx.x - G.b_fill, G.tperm, G.rs_off, G.rs16, G.c64, G.T, G.N, G.W, G.tids, G.hot);
-}
-__global__ void __launch_bounds__(SCHED_T) k_tr_sched_b(const PDev* __restrict__ pd, int32_t n) {
-    __shared__ uint16_t items[SCHED_T][32 * SCHED_L];
-    __shared__ unsigned long long rem[SCHED_T][32];
-    __shared__ uint16_t cbuf[SCHED_T][32 * 4];
-    const PDev& G = pd[pd_graph(pd, n, (int32_t)blockIdx.x, 4)];
-    tr_sched_body((int64_t)((int32_t)blockIdx.x - G.b_sch) * SCHED_T + threadIdx.x, G.coff, G.W, G.tids,
-                  items[threadIdx.x], rem[threadIdx.x], cbuf[threadIdx.x], G.hot);
+    tr_fill_body((int32_t)blockIdx.x - G.b_fill, G.tperm, G.rs_off, G.rs16, G.c64, G.T, G.N, G.W, G.tids);
 }
 __global__ void k_tr_gather(const float* src, const int32_t* tperm, int32_t T, float* dst) {
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1478,7 +1259,6 @@ struct GDev {
     const float* c_tp;          // c_t, w_t in position order (tperm)
     const float* w_tp;
     const double* mw_tp;        // kind-compressed graphs: w_t * multiplicity (position order), else null
-    const int32_t* hot;         // [HOT_N + 1] hot ops of the layout's chunk 0 of every tile, or null
     const float* c_t;
     const float* w_t;
     const float* u_o;
@@ -1819,15 +1599,9 @@ __device__ __forceinline__ double tr_walk(const GDev& G, int32_t lb, int cur, in
     int32_t k = __builtin_amdgcn_readfirstlane(wt[0]);
     const int32_t ke = __builtin_amdgcn_readfirstlane(wt[1]);
     double rmax = -__builtin_huge_val();
-    // hot chunk: chunk 0 of every tile holds hot op q at position q (or the lane's pad); its X go
-    // to registers, folded into the accumulator once at the end of the run
-    const GLB int32_t* hotp = gp(G.hot);
-    const int32_t hn = hotp ? __builtin_amdgcn_readfirstlane(hotp[HOT_N]) : 0;
-    static_assert(HOT_N == 2, "k_tr_a keeps two hot-op registers");
-    unsigned long long xh0 = 0ull, xh1 = 0ull;
     if (k < ke) {
         auto pos = [&](int32_t kk) { return min(kk * WAVE + lane, T - 1); };
-        // cold-op su of a chunk (hot ops load sug[0]: one line, no traffic; pads read as 0)
+        // cold-op su of a chunk (LDS-resident ops load sug[0]: one line, no traffic; pads read as 0)
         auto gather = [&](const u32x2 w, double* g) {
             const int32_t o[4] = {(int32_t)(w.x & 0xffffu), (int32_t)(w.x >> 16), (int32_t)(w.y & 0xffffu),
                                   (int32_t)(w.y >> 16)};
@@ -1838,7 +1612,6 @@ __device__ __forceinline__ double tr_walk(const GDev& G, int32_t lb, int cur, in
             }
         };
         int32_t c = __builtin_amdgcn_readfirstlane(coff[k]);
-        int32_t ch = hn > 0 ? c : -1;                               // the current tile's hot chunk
         int32_t ce = __builtin_amdgcn_readfirstlane(coff[k + 1]);   // end of tile k
         const int32_t cl = __builtin_amdgcn_readfirstlane(coff[ke]) - 1;   // the run's last chunk
         // tile k's words; tile k + 1's q and end chunk (one tile ahead, clamped into the run).  The
@@ -1888,12 +1661,7 @@ __device__ __forceinline__ double tr_walk(const GDev& G, int32_t lb, int cur, in
             if (SUL || HOT) lds_su(NXT, SN);                                                               \
             const int32_t o_[4] = {(int32_t)(CUR.x & 0xffffu), (int32_t)(CUR.x >> 16),                     \
                                    (int32_t)(CUR.y & 0xffffu), (int32_t)(CUR.y >> 16)};                    \
-            if (c == ch) {   /* the tile's hot chunk: positions q hold hot op q or the pad */                \
-                xh0 += o_[0] < N ? X : 0ull;                                                               \
-                xh1 += o_[1] < N ? X : 0ull;                                                               \
-            } else {                                                                                       \
-                _Pragma("unroll") for (int j = 0; j < 4; ++j) atomicAdd(&lacc[(MR_TREXP & 1) ? N + lane : o_[j]], X); \
-            }                                                                                              \
+            _Pragma("unroll") for (int j = 0; j < 4; ++j) atomicAdd(&lacc[(MR_TREXP & 1) ? N + lane : o_[j]], X); \
             _Pragma("unroll") for (int j = 0; j < 4; ++j)                                                  \
                 acc += SUL ? SC[j] : HOT ? (o_[j] < NH ? SC[j] : GC[j]) : GC[j];                          \
             if (++c == ce) {                                                                               \
@@ -1905,7 +1673,6 @@ __device__ __forceinline__ double tr_walk(const GDev& G, int32_t lb, int cur, in
                 qn[own_ ? p_ : T] = (Q)(w_cur * rp_);   /* q[T]: pad slot */                              \
                 if (++k == ke) goto tr_done;                                                               \
                 ce = __builtin_amdgcn_readfirstlane(ce_nx);                                                \
-                ch = hn > 0 ? c : -1;                                                                      \
                 q_cur = q_nx;                                                                              \
                 const int32_t kk_ = min(k + 1, ke - 1);                                                    \
                 c_cur = c_tp[pos(k)];                                                                      \
@@ -1925,17 +1692,6 @@ __device__ __forceinline__ double tr_walk(const GDev& G, int32_t lb, int cur, in
         }
 #undef TR_STEP
     tr_done:;
-        if (hn > 0) {   // the run's hot-op sums: one LDS atomic per hot op per wave
-#pragma unroll
-            for (int m = 32; m >= 1; m >>= 1) {
-                xh0 += (unsigned long long)__shfl_xor((long long)xh0, m, WAVE);
-                xh1 += (unsigned long long)__shfl_xor((long long)xh1, m, WAVE);
-            }
-            if (lane == 0) {
-                const unsigned long long xs[2] = {xh0, xh1};
-                for (int q = 0; q < hn; ++q) atomicAdd(&lacc[hotp[q]], xs[q]);
-            }
-        }
     }
     return rmax;
 }
@@ -2133,17 +1889,29 @@ __global__ void __launch_bounds__(WAVE * FB_W) k_fx_b(const GDev* __restrict__ g
 // raises flag[3], every block leaves, and the host reruns the call launch by launch.
 constexpr unsigned long long PC_TIMEOUT = 5000000ull;   // 50 ms of the 100 MHz s_memrealtime clock
 constexpr int PC_MAXB = 64;                               // blocks of one cluster
+// LDS of a cluster block: k_tr_a's accumulator and su, s_k and s_k+1, and the call graph P_ss
+// (offsets, parents, fp32(1/nchild)): graph constants staged once, so the per-iteration call-graph
+// term is LDS reads, not chains of dependent global loads
 struct PcLds {
-    size_t lacc, su, s0, s1, total;
-    __host__ __device__ explicit PcLds(int32_t N) {
+    size_t lacc, su, s0, s1, soff, spar, spw, total;
+    __host__ __device__ PcLds(int32_t N, int64_t E) {
         const TrLds t(N, WV_SU_ALL);   // the accumulator and su as k_tr_a's
+        auto up = [](size_t b) { return (b + 15) / 16 * 16; };
         lacc = t.lacc;
         su = t.su;
         s0 = t.total;
-        s1 = s0 + ((size_t)N * 8 + 15) / 16 * 16;
-        total = s1 + ((size_t)N * 8 + 15) / 16 * 16;
+        s1 = s0 + up((size_t)N * 8);
+        soff = s1 + up((size_t)N * 8);
+        spar = soff + up(((size_t)N + 1) * 4);
+        spw = spar + up((size_t)E * 4);
+        total = spw + up((size_t)N * 4);
     }
 };
+__device__ __forceinline__ double uni_d(double v) {   // a block-uniform double into SGPRs
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readfirstlane((int)(unsigned)b), hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
 template <class Q, int NT>
 __global__ void __launch_bounds__(NT) k_pr_cluster(const GDev* __restrict__ gs, int32_t ng, double d, int iters) {
     constexpr int NW = NT / WAVE;
@@ -2151,29 +1919,36 @@ __global__ void __launch_bounds__(NT) k_pr_cluster(const GDev* __restrict__ gs, 
     __shared__ double red[NW];
     __shared__ double mb[2];
     __shared__ int s_abort;
-    const GDev& G = gs[graph_of(gs, ng, (int32_t)blockIdx.x, 2)];
-    const int32_t lb = (int32_t)blockIdx.x - G.blk0f, B = G.n_fa, N = G.N;
+    const GDev& G = gs[__builtin_amdgcn_readfirstlane(graph_of(gs, ng, (int32_t)blockIdx.x, 2))];
+    const int32_t lb = __builtin_amdgcn_readfirstlane((int32_t)blockIdx.x - G.blk0f);
+    const int32_t B = __builtin_amdgcn_readfirstlane(G.n_fa), N = __builtin_amdgcn_readfirstlane(G.N);
     const int32_t tid = (int32_t)threadIdx.x, lane = tid & (WAVE - 1), wv = tid / WAVE;
-    const PcLds L(N);
+    const int64_t E = rfl64(G.ss_off[N]);
+    const PcLds L(N, E);
     unsigned long long* lacc = (unsigned long long*)(lraw + L.lacc);
     double* su_l = (double*)(lraw + L.su);
     double* s_cur = (double*)(lraw + L.s0);
     double* s_nxt = (double*)(lraw + L.s1);
+    int32_t* l_soff = (int32_t*)(lraw + L.soff);
+    int32_t* l_spar = (int32_t*)(lraw + L.spar);
+    float* l_spw = (float*)(lraw + L.spw);
     // (global-address views: the hand-off's sc1 loads / stores and atomics must be global_, not flat_)
     GLB unsigned long long* mslot = gpw(G.mslot);
     GLB unsigned long long* cnt = mslot + 6 * MSH;
     GLB unsigned long long* rows = gpw(G.fx_part);   // [2][B][N] (B > 1)
     const double scale = G.dscale ? G.dscale[0] : G.fx_scale, iscale = G.dscale ? G.dscale[1] : G.fx_iscale;
-    const GLB int64_t* ss_off = gp(G.ss_off);
-    const GLB int32_t* ss_par = gp(G.ss_par);
-    const GLB float* pw = gp(G.pw);
     const GLB float* u_o = gp(G.u_o);
-    // the set-up's state: s_0, su_0, M_s(0), M_r(0) (earlier launches on this stream)
+    // the set-up's state: s_0, su_0, M_s(0), M_r(0) (earlier launches on this stream); P_ss
     for (int32_t o = tid; o < N + TR_PAD; o += NT) {
         lacc[o] = 0ull;
         su_l[o] = o < N ? G.sub[0][o] : 0.0;
-        if (o < N) s_cur[o] = G.spb[0][o];
+        if (o < N) {
+            s_cur[o] = G.spb[0][o];
+            l_spw[o] = G.pw[o];
+        }
+        if (o <= N) l_soff[o] = (int32_t)G.ss_off[o];
     }
+    for (int64_t e = tid; e < E; e += NT) l_spar[e] = G.ss_par[e];
     if (tid < WAVE) {
         const double ms = wave_max(bits2d(mslot[tid]));
         const double mr = wave_max(bits2d(mslot[MSH + tid]));
@@ -2184,7 +1959,7 @@ __global__ void __launch_bounds__(NT) k_pr_cluster(const GDev* __restrict__ gs, 
         }
     }
     __syncthreads();
-    double Ms = mb[0], Mr = mb[1];
+    double Ms = uni_d(mb[0]), Mr = uni_d(mb[1]);
     for (int it = 0; it < iters; ++it) {
         const int cur = it & 1, nxt = cur ^ 1;
         GLB unsigned long long* Mr_next = mslot + (size_t)2 * MSH * ((it + 1) % 3) + MSH;
@@ -2228,9 +2003,9 @@ __global__ void __launch_bounds__(NT) k_pr_cluster(const GDev* __restrict__ gs, 
         // the call-graph term alpha (P_ss s_k)[o] / M_s(k): a wave per op (k_fx_b's order)
         for (int32_t o = wv; o < N; o += NW) {
             double bb = 0.0;
-            for (int64_t e = ss_off[o] + lane; e < ss_off[o + 1]; e += WAVE) {
-                const int32_t p = ss_par[e];
-                bb += (double)pw[p] * s_cur[p];
+            for (int32_t e = l_soff[o] + lane; e < l_soff[o + 1]; e += WAVE) {
+                const int32_t p = l_spar[e];
+                bb += (double)l_spw[p] * s_cur[p];
             }
             bb = wave_sum(bb);
             if (lane == 0) s_nxt[o] = G.alpha * (bb / Ms);
@@ -2260,8 +2035,8 @@ __global__ void __launch_bounds__(NT) k_pr_cluster(const GDev* __restrict__ gs, 
             su_l[o] = (double)u_o[o] * v;
             vmax = nmax(vmax, v);
         }
-        Ms = block_max(vmax, red);   // (its barriers publish s_nxt / su_l to the block)
-        Mr = Mr_n;
+        Ms = uni_d(block_max(vmax, red));   // (its barriers publish s_nxt / su_l to the block)
+        Mr = uni_d(Mr_n);
         double* t = s_cur;
         s_cur = s_nxt;
         s_nxt = t;
@@ -2483,6 +2258,50 @@ __global__ void k_sh_kind_check(const uint64_t* in, int64_t n, const uint64_t* g
     while (gk[s] != k) s = (s + 1) & mask;
     if (gh[s] != in[3 * i + 1]) atomicOr(flag, 1);
 }
+// ---- the kind-class exchange partitioned by key (peer regions): a class key is OWNED by rank
+// owner(key); every rank sends its (key, check hash, count) records to their owners, each owner
+// sums the counts of the keys it owns and returns every record's total to its sender
+__device__ __forceinline__ int kind_owner(uint64_t key, int R) { return (int)((mix64(key ^ 0x5bd1e995ull) >> 33) % (uint64_t)R); }
+__global__ void k_kx_count(const uint64_t* rec, int64_t n, int R, unsigned long long* cnt) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) atomicAdd(&cnt[kind_owner(rec[3 * i], R)], 1ull);
+}
+// records by owner: record i -> send slot spos[i] (order inside an owner's run arbitrary: the
+// owner's sums and the returned totals do not depend on it)
+__global__ void k_kx_place(const uint64_t* rec, int64_t n, int R, unsigned long long* cursor, uint64_t* send,
+                           int64_t* spos) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t p = (int64_t)atomicAdd(&cursor[kind_owner(rec[3 * i], R)], 1ull);
+    send[3 * p] = rec[3 * i];
+    send[3 * p + 1] = rec[3 * i + 1];
+    send[3 * p + 2] = rec[3 * i + 2];
+    spos[i] = p;
+}
+// the owner's totals back to the senders: received record j came from rank s (roff: first record of
+// each source) and goes to slot soff_at_s + (j - roff[s]) of s's area B
+__global__ void k_kx_return(const uint64_t* in, int64_t n, const uint64_t* gk, const unsigned long long* gc, uint64_t mask,
+                            const int64_t* roff, const int64_t* dbase, int R, unsigned long long* const* areas) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    const uint64_t k = in[3 * j];
+    uint64_t s = mix64(k) & mask;
+    while (gk[s] != k) s = (s + 1) & mask;
+    int src = 0;
+    while (src + 1 < R && roff[src + 1] <= j) ++src;
+    __hip_atomic_store((__attribute__((address_space(1))) unsigned long long*)areas[src] + dbase[src] + (j - roff[src]),
+                       gc[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// kind[t] = the returned total of its class's record
+__global__ void k_kx_apply(const unsigned long long* hk, const int32_t* slot_of, const int32_t* flag, const int64_t* pos,
+                           const int64_t* spos, const unsigned long long* ret, int32_t T, double* kind) {
+    const int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= T) return;
+    const int32_t sl = slot_of[t];
+    (void)hk;
+    (void)flag;
+    kind[t] = (double)ret[spos[pos[sl]]];
+}
 // kind[t] = the class size over all ranks
 __global__ void k_sh_kind_apply(const unsigned long long* hk, const int32_t* slot_of, int32_t T, const uint64_t* gk,
                                 const unsigned long long* gc, uint64_t mask, double* kind) {
@@ -2508,7 +2327,7 @@ static const bool g_debug = getenv("MR_DEBUG") != nullptr;
     } while (0)
 
 void mr_prof_begin(mr_ctx* ctx);
-void mr_prof_end(mr_ctx* ctx, double bytes);
+void mr_prof_end(mr_ctx* ctx, double bytes, int64_t iters = 1);
 
 using TrA = void (*)(const GDev*, int32_t, int32_t, double, double, int, int32_t);
 static TrA tr_kernel(bool fp32, int mode, int NT) {
@@ -2673,15 +2492,17 @@ static int fused_blocks(mr_ctx* ctx, mr_graph* g, const FxPlan& P, int64_t wsum,
 }
 
 // ---- k_pr_cluster: eligibility and cluster sizes
-// MR_PR_PERSIST (read per call): unset / 1 = persistent launch where eligible, 0 = launch per
-// iteration, "split" = the persistent plan's block counts launched per iteration (k_tr_a +
-// k_fx_b: bitwise the persistent results -- parity tests).  MR_PC_TPW: wave tiles per wave a
-// cluster is sized for (default 4).
+// MR_PR_PERSIST (read per call): 1 = persistent launch where eligible; unset / 0 = launch per
+// iteration (the default: measured faster, DESIGN.md §4 -- the persistent kernel runs one 16-wave
+// block per CU at 84 VGPRs where k_tr_a runs two, and its per-iteration row hand-off and s' pass
+// cost more than the two kernel boundaries they replace); "split" = the persistent plan's block
+// counts launched per iteration (k_tr_a + k_fx_b: bitwise the persistent results -- parity
+// tests).  MR_PC_TPW: wave tiles per wave a cluster is sized for (default 4).
 constexpr size_t PC_LDS_MAX = 76 * 1024;   // two 1024-thread blocks per CU
 enum { PC_OFF = 0, PC_ON = 1, PC_SPLIT = 2 };
 static int pc_mode() {
     const char* e = getenv("MR_PR_PERSIST");
-    if (!e) return PC_ON;
+    if (!e) return PC_OFF;
     if (!strcmp(e, "split")) return PC_SPLIT;
     return strcmp(e, "0") ? PC_ON : PC_OFF;
 }
@@ -2700,13 +2521,12 @@ static std::vector<int64_t> pc_plan(mr_ctx* ctx, mr_graph* const* gs, int ng, co
                                     bool fp32) {
     std::vector<int64_t> nb;
     if (sharded || iters <= 0 || ctx->no_persist || pc_mode() == PC_OFF || P.mode != WV_SU_ALL) return nb;
-    int32_t nmax = 0;
+    size_t lds = 0;
     for (int i = 0; i < ng; ++i) {
         const mr_graph* g = gs[i];
         if (!g->fused || g->wide || g->relabeled || !g->tile_mult_h.empty() || g->n_wt == 0) return nb;
-        nmax = std::max(nmax, g->N);
+        lds = std::max(lds, PcLds(g->N, g->E).total);
     }
-    const size_t lds = PcLds(nmax).total;
     if (lds > PC_LDS_MAX) return nb;
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)pc_kernel(fp32, P.NT), P.NT, lds) != hipSuccess ||
@@ -2742,7 +2562,7 @@ static std::vector<int64_t> pc_plan(mr_ctx* ctx, mr_graph* const* gs, int ng, co
 // off / ids: the trace-major incidence the kernel walks (rs_off with rs16 / rsp, or a wide graph's
 // hot entries), N: the kernel's op count (pads N + lane)
 static int tr_layout(mr_ctx* ctx, mr_graph* g, const int64_t* off, const uint16_t* src, int32_t N, int64_t nent,
-                     int32_t* zeroed, const int32_t* cov = nullptr, const int32_t* perm = nullptr) {
+                     int32_t* zeroed) {
     hipStream_t st = ctx->stream;
     const int32_t T = g->T;
     const int32_t W = cdiv(T, WAVE);
@@ -2778,39 +2598,23 @@ static int tr_layout(mr_ctx* ctx, mr_graph* g, const int64_t* off, const uint16_
                            2 * (size_t)nbin * sizeof(int32_t), st, off, T, nbin,
                            lscan ? (const int64_t*)nullptr : boff.p, hist, taken, g->w_t.p, g->tperm.p, g->w_tp.p);
     }
-    // the hot chunk (cov given: the layout's coverage by op, perm: label -> op when relabelled)
-    DBuf<int32_t> tnc;
-    const bool hot = cov && tr_hot_on() && W > 0;
-    if (hot) {
-        MR_TRY(g->hot.alloc(ctx, HOT_N + 1));
-        MR_TRY(tnc.alloc(ctx, (size_t)W));
-        hipLaunchKernelGGL(k_hot_ops, dim3(1), dim3(256), 0, st, cov, N, T, perm, g->hot.p);
-        hipLaunchKernelGGL(k_tr_tnc, dim3(cdiv((int64_t)W * WAVE, 256)), dim3(256), 0, st, g->tperm.p, off, src, T, W,
-                           g->hot.p, tnc.p);
-    } else {
-        g->hot.reset();
-    }
     {   // chunk counts per wave tile, their prefix and its int32 copy: one launch
         const int64_t nt = std::max<int64_t>(cdiv((int64_t)W, TS_TILE), 1);
         unsigned long long* dst = nullptr;
         uint64_t epoch = 0;
         MR_TRY(mr_dl_status(ctx, nt, &dst, &epoch));
         hipLaunchKernelGGL(k_tr_chunk_scan, dim3((unsigned)nt), dim3(TS_T), 0, st, g->tperm.p, off, T, W, c64.p,
-                           g->coff.p, dst, epoch, hot ? (const int32_t*)tnc.p : nullptr);
+                           g->coff.p, dst, epoch);
     }
     // the id array at an upper bound of the chunk count (no host round trip): tile k holds
-    // ceil(maxlen_k / 4) chunks (+ 1: the hot chunk), and with lengths ascending maxlen_k <= every
+    // ceil(maxlen_k / 4) chunks, and with lengths ascending maxlen_k <= every
     // length of tile k + 1, so sum_k maxlen_k <= nent / 64 + 2 N
     g->coff_h.clear();
     const int64_t nch = 2 * (int64_t)W + (nent / WAVE + 2 * (int64_t)N) / 4 + 2;
     MR_TRY(g->tids.alloc(ctx, (size_t)std::max<int64_t>(nch, 1) * WAVE * 4));
-    const int32_t* hp = hot ? (const int32_t*)g->hot.p : nullptr;
     if (W)
         hipLaunchKernelGGL(k_tr_fill, dim3(cdiv((int64_t)W * WAVE, 256)), dim3(256), 0, st, g->tperm.p, off, src,
-                           c64.p, T, N, W, g->tids.p, hp);
-    if (W && tr_sched_on())
-        hipLaunchKernelGGL(k_tr_sched, dim3(cdiv(2 * (int64_t)W, SCHED_T)), dim3(SCHED_T), 0, st, g->coff.p, W,
-                           g->tids.p, hp);
+                           c64.p, T, N, W, g->tids.p);
     MR_TRY_HIP(ctx, hipGetLastError());
     return MR_OK;   // (scratch returns to the stream-ordered pool)
 }
@@ -2860,7 +2664,7 @@ static int wide_prepare(mr_ctx* ctx, mr_graph* g) {
     MR_TRY(g->hot16.alloc(ctx, (size_t)n_hot + 8));
     hipLaunchKernelGGL(k_wide_hot, dim3(cdiv(T, 256)), dim3(256), 0, st, g->rs_off.p, g->rs_ops.p, inv.p, T, NA,
                        g->hot_off.p, g->hot16.p);
-    MR_TRY(tr_layout(ctx, g, g->hot_off.p, g->hot16.p, NA, n_hot, nullptr, g->cov.p, g->perm.p));   // tperm, w_tp, tids, coff
+    MR_TRY(tr_layout(ctx, g, g->hot_off.p, g->hot16.p, NA, n_hot, nullptr));   // tperm, w_tp, tids, coff
     // ---- cold entries in position order
     DBuf<int32_t> cnt;
     DBuf<int64_t> coff64;
@@ -2952,8 +2756,7 @@ int mr_graph_prepare_batch(mr_ctx* ctx, mr_graph* const* gs, int n, std::vector<
     PDev* hp = reinterpret_cast<PDev*>(keep.data());
     std::vector<DBuf<int32_t>> trz((size_t)n);
     std::vector<DBuf<int64_t>> c64((size_t)n);
-    std::vector<DBuf<int32_t>> tnc((size_t)n);
-    int32_t bgc = 0, bth = 0, bcs = 0, bfl = 0, bsch = 0, btnc = 0, nbin_max = 0;
+    int32_t bgc = 0, bth = 0, bcs = 0, bfl = 0, nbin_max = 0;
     int64_t st_words = 0;
     for (int i = 0; i < n; ++i) {
         mr_graph* g = gs[i];
@@ -2971,12 +2774,6 @@ int mr_graph_prepare_batch(mr_ctx* ctx, mr_graph* const* gs, int n, std::vector<
         MR_TRY(g->coff.alloc(ctx, (size_t)W + 1));
         const int64_t nch = 2 * (int64_t)W + (nnz / WAVE + 2 * (int64_t)N) / 4 + 2;   // as tr_layout
         MR_TRY(g->tids.alloc(ctx, (size_t)std::max<int64_t>(nch, 1) * WAVE * 4));
-        if (tr_hot_on()) {
-            MR_TRY(g->hot.alloc(ctx, HOT_N + 1));
-            MR_TRY(tnc[(size_t)i].alloc(ctx, (size_t)std::max(W, 1)));
-        } else {
-            g->hot.reset();
-        }
         g->relabeled = false;
         g->wide = false;
         g->NA = N;
@@ -3021,13 +2818,6 @@ int mr_graph_prepare_batch(mr_ctx* ctx, mr_graph* const* gs, int n, std::vector<
         bcs += v.n_cs;
         v.b_fill = bfl;
         bfl += cdiv((int64_t)W * WAVE, 256);
-        v.b_sch = bsch;
-        bsch += cdiv(2 * (int64_t)W, SCHED_T);
-        v.cov = g->cov.p;
-        v.hot = g->hot.p;
-        v.tnc = g->hot.p ? tnc[(size_t)i].p : nullptr;
-        v.b_tnc = btnc;
-        btnc += cdiv((int64_t)W * WAVE, 256);
         nbin_max = std::max(nbin_max, N + 1);
     }
     DBuf<PDev> dpd;
@@ -3038,13 +2828,8 @@ int mr_graph_prepare_batch(mr_ctx* ctx, mr_graph* const* gs, int n, std::vector<
     hipLaunchKernelGGL(k_graph_consts_b, dim3(bgc), dim3(256), 0, st, dpd.p, n);
     hipLaunchKernelGGL(k_tr_hist_b, dim3(bth), dim3(TRB), (size_t)nbin_max * sizeof(int32_t), st, dpd.p, n);
     hipLaunchKernelGGL(k_tr_place_b, dim3(bth), dim3(TRB), 2 * (size_t)nbin_max * sizeof(int32_t), st, dpd.p, n);
-    if (tr_hot_on()) {   // hot ops (a block per graph) and the chunks per wave tile
-        hipLaunchKernelGGL(k_hot_ops_b, dim3(n), dim3(256), 0, st, dpd.p);
-        hipLaunchKernelGGL(k_tr_tnc_b, dim3(btnc), dim3(256), 0, st, dpd.p, n);
-    }
     hipLaunchKernelGGL(k_tr_chunk_scan_b, dim3(bcs), dim3(TS_T), 0, st, dpd.p, n, dst, epoch);
     hipLaunchKernelGGL(k_tr_fill_b, dim3(bfl), dim3(256), 0, st, dpd.p, n);
-    if (bsch && tr_sched_on()) hipLaunchKernelGGL(k_tr_sched_b, dim3(bsch), dim3(SCHED_T), 0, st, dpd.p, n);
     MR_TRY_HIP(ctx, hipGetLastError());
     return MR_OK;   // (scratch returns to the stream-ordered pool)
 }
@@ -3106,8 +2891,7 @@ int mr_graph_prepare(mr_ctx* ctx, mr_graph* g) {
             g->perm.reset();
             g->rsp.reset();
         }
-        MR_TRY(tr_layout(ctx, g, g->rs_off.p, g->relabeled ? g->rsp.p : g->rs16.p, N, nnz, trz.p, g->cov.p,
-                         g->relabeled ? (const int32_t*)g->perm.p : nullptr));
+        MR_TRY(tr_layout(ctx, g, g->rs_off.p, g->relabeled ? g->rsp.p : g->rs16.p, N, nnz, trz.p));
         g->n_tiles = 0;
         g->n_pairs = 0;
         MR_TRY_HIP(ctx, hipGetLastError());
@@ -3580,7 +3364,6 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         v.c_tp = g->c_tp.p;
         v.w_tp = g->w_tp.p;
         v.mw_tp = g->mw_tp.p;
-        v.hot = g->hot.p;
         v.c_t = g->c_t.p;
         v.w_t = g->w_t.p;
         v.u_o = g->u_o.p;
@@ -3707,14 +3490,13 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
     }
     hm.mark("pre-loop");
     if (persist) {   // all iterations in one launch (k_pr_cluster)
-        int32_t nmax = 0;
-        for (int i = 0; i < ng; ++i) nmax = std::max(nmax, gs[i]->N);
+        size_t lds = 0;
+        for (int i = 0; i < ng; ++i) lds = std::max(lds, PcLds(gs[i]->N, gs[i]->E).total);
         mr_prof_begin(ctx);
-        hipLaunchKernelGGL(pc_kernel(fp32, plan.NT), dim3(blocks_fa), dim3(plan.NT), PcLds(nmax).total, st, dv.p, ng, d,
-                           iters);
+        hipLaunchKernelGGL(pc_kernel(fp32, plan.NT), dim3(blocks_fa), dim3(plan.NT), lds, st, dv.p, ng, d, iters);
         MR_TRY_HIP(ctx, hipGetLastError());
         MR_DEBUG_CHECK(ctx, "k_pr_cluster");
-        mr_prof_end(ctx, bytes * iters);
+        mr_prof_end(ctx, bytes * iters, iters);
     }
     for (int it = 0; it < iters && !persist; ++it) {
         mr_prof_begin(ctx);
@@ -4052,6 +3834,100 @@ extern "C" int mr_pagerank_batch(mr_ctx* ctx, mr_graph* const* graphs, const int
 }
 
 // ------------------------------------------------------------------------------ sharded graphs
+// the kind classes over the ranks through the peer regions: records partitioned by owner (one
+// exchange round), merged by their owners, totals returned (a second round).  Each rank sends and
+// receives ~ its own class count, instead of receiving every rank's list (the all-gather below).
+static int shard_kinds_peer(mr_ctx* ctx, mr_graph* g, uint64_t cap, const DBuf<int32_t>& fl, const DBuf<int64_t>& pos,
+                            int64_t Kl) {
+    hipStream_t st = ctx->stream;
+    const int32_t T = g->T;
+    const int R = ctx->nranks, me = ctx->rank;
+    DBuf<uint64_t> rec, send;
+    DBuf<int64_t> spos;
+    DBuf<unsigned long long> cnt;
+    MR_TRY(rec.alloc(ctx, (size_t)3 * std::max<int64_t>(Kl, 1)));
+    MR_TRY(send.alloc(ctx, (size_t)3 * std::max<int64_t>(Kl, 1)));
+    MR_TRY(spos.alloc(ctx, (size_t)std::max<int64_t>(Kl, 1)));
+    MR_TRY(cnt.zero(ctx, (size_t)R));
+    hipLaunchKernelGGL(k_sh_kind_list, dim3(cdiv(cap, 256)), dim3(256), 0, st, g->ht_key.p, g->ht_cr.p, g->ht_chk.p,
+                       (int64_t)cap, fl.p, pos.p, rec.p);
+    if (Kl) hipLaunchKernelGGL(k_kx_count, dim3(cdiv(Kl, 256)), dim3(256), 0, st, rec.p, Kl, R, cnt.p);
+    std::vector<int64_t> scnt((size_t)R), M((size_t)R * R);
+    MR_TRY_HIP(ctx, hipMemcpyAsync(scnt.data(), cnt.p, sizeof(int64_t) * R, hipMemcpyDeviceToHost, st));
+    MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+    std::vector<int64_t> soff((size_t)R + 1, 0);
+    for (int o = 0; o < R; ++o) soff[(size_t)o + 1] = soff[(size_t)o] + scnt[(size_t)o];
+    MR_TRY(cnt.upload(ctx, (const unsigned long long*)soff.data(), (size_t)R));   // cursors
+    if (Kl) hipLaunchKernelGGL(k_kx_place, dim3(cdiv(Kl, 256)), dim3(256), 0, st, rec.p, Kl, R, cnt.p, send.p, spos.p);
+    {   // every rank's counts per owner: M[s * R + o]
+        DBuf<int64_t> mine, all;
+        MR_TRY(mine.upload(ctx, scnt.data(), (size_t)R));
+        MR_TRY(all.alloc(ctx, (size_t)R * R));
+        MR_TRY(mr_coll_allgather(ctx, mine.p, all.p, R, MR_DT_I64));
+        MR_TRY(all.download(ctx, M.data(), (size_t)R * R));
+        MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+    }
+    int64_t xa = 1, xb = 1;   // words: area A receives 3 per record owned, area B one total per record sent
+    for (int o = 0; o < R; ++o) {
+        int64_t in = 0, out = 0;
+        for (int s = 0; s < R; ++s) {
+            in += M[(size_t)s * R + o];
+            out += M[(size_t)o * R + s];
+        }
+        xa = std::max(xa, 3 * in);
+        xb = std::max(xb, out);
+    }
+    MR_TRY(mr_peer_xensure(ctx, xa, xb));
+    // round 1: my records to their owners' areas A (after the records of lower ranks)
+    for (int o = 0; o < R; ++o) {
+        int64_t at = 0;
+        for (int s = 0; s < me; ++s) at += M[(size_t)s * R + o];
+        MR_TRY(mr_peer_put(ctx, (const unsigned long long*)send.p + 3 * soff[(size_t)o], 3 * scnt[(size_t)o], o, 0, 3 * at));
+    }
+    MR_TRY(mr_peer_round(ctx));
+    // merge the records I own
+    std::vector<int64_t> roff((size_t)R + 1, 0), dbase((size_t)R);
+    for (int s = 0; s < R; ++s) {
+        roff[(size_t)s + 1] = roff[(size_t)s] + M[(size_t)s * R + me];
+        int64_t b = 0;   // where s keeps the totals of its records for me: its send offset of owner me
+        for (int o = 0; o < me; ++o) b += M[(size_t)s * R + o];
+        dbase[(size_t)s] = b;
+    }
+    const int64_t n = roff[(size_t)R];
+    const uint64_t* in = (const uint64_t*)mr_peer_area(ctx, me, 0);
+    uint64_t gcap = 1;
+    while (gcap < 2 * (uint64_t)std::max<int64_t>(n, 1)) gcap <<= 1;
+    DBuf<uint64_t> gk, gh;
+    DBuf<unsigned long long> gc;
+    DBuf<int64_t> droff, ddbase;
+    MR_TRY(gk.zero(ctx, gcap));
+    MR_TRY(gh.zero(ctx, gcap));
+    MR_TRY(gc.zero(ctx, gcap));
+    MR_TRY(droff.upload(ctx, roff.data(), roff.size()));
+    MR_TRY(ddbase.upload(ctx, dbase.data(), dbase.size()));
+    std::vector<unsigned long long*> areas((size_t)R);
+    for (int s = 0; s < R; ++s) areas[(size_t)s] = mr_peer_area(ctx, s, 1);
+    DBuf<unsigned long long*> dareas;
+    MR_TRY(dareas.upload(ctx, areas.data(), areas.size()));
+    if (n) {
+        hipLaunchKernelGGL(k_sh_kind_merge, dim3(cdiv(n, 256)), dim3(256), 0, st, in, n, gk.p, gh.p, gc.p, gcap - 1,
+                           g->flag.p);
+        hipLaunchKernelGGL(k_sh_kind_check, dim3(cdiv(n, 256)), dim3(256), 0, st, in, n, gk.p, gh.p, gcap - 1, g->flag.p);
+        // round 2: every record's total back to its sender's area B
+        hipLaunchKernelGGL(k_kx_return, dim3(cdiv(n, 256)), dim3(256), 0, st, in, n, gk.p, gc.p, gcap - 1, droff.p,
+                           ddbase.p, R, dareas.p);
+    }
+    MR_TRY(mr_peer_round(ctx));
+    if (T)
+        hipLaunchKernelGGL(k_kx_apply, dim3(cdiv(T, 256)), dim3(256), 0, st, g->ht_key.p, g->slot_of.p, fl.p, pos.p,
+                           spos.p, (const unsigned long long*)mr_peer_area(ctx, me, 1), T, g->kind.p);
+    MR_TRY_HIP(ctx, hipGetLastError());
+    bool failed = false;
+    MR_TRY(mr_peer_error(ctx, &failed));   // (syncs: the scratch leaves scope)
+    if (failed) return mr_fail(ctx, MR_ERR_COMM, "kind exchange: a rank did not arrive (timeout)");
+    return MR_OK;
+}
+
 static int shard_kinds(mr_ctx* ctx, mr_graph* g, uint64_t cap) {
     hipStream_t st = ctx->stream;
     const int32_t T = g->T;
@@ -4068,6 +3944,7 @@ static int shard_kinds(mr_ctx* ctx, mr_graph* g, uint64_t cap) {
     int64_t Kl = 0;
     MR_TRY(kn.download(ctx, &Kl, 1));
     MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+    if (mr_peer_ready(ctx)) return shard_kinds_peer(ctx, g, cap, fl, pos, Kl);
     MR_TRY(mr_coll_allreduce(ctx, kn.p, 1, MR_DT_I64, 1));
     int64_t Kmax = 0;
     MR_TRY(kn.download(ctx, &Kmax, 1));

@@ -22,7 +22,7 @@ from . import _lib
 from ._lib import SPECTRUM_METHODS, ptr
 from .anormaly_detector import slo_arrays, system_anomaly_detect, trace_list_partition  # noqa: F401
 from .pagerank import trace_pagerank
-from .preprocess_data import (get_operation_duration_data, get_operation_slo, get_pagerank_graph,  # noqa: F401
+from .preprocess_data import (SpanStream, get_operation_duration_data, get_operation_slo, get_pagerank_graph,  # noqa: F401
                               get_service_operation_list, get_span, span_table)
 from .spans import to_ns
 
@@ -163,6 +163,13 @@ def _sweep_plan(data, slo, start, end, window_normal, window_abnormal, ctx):
         return None
     ctx = ctx or _lib.default_context()
     table, dev = span_table(data, ctx)
+    return _sweep_plan_dev(table, dev, slo, start, end, window_normal, window_abnormal, ctx)
+
+
+def _sweep_plan_dev(table, dev, slo, start, end, window_normal, window_abnormal, ctx):
+    """_sweep_plan over a resident device table (RCAStream's appended one)."""
+    if pd.isna(start) or pd.isna(end) or not start < end:
+        return None
     a3, ok = slo_arrays(table, slo)
     return sweep_plan(ctx, table, dev, a3, ok, int(pd.Timestamp(start).value), int(pd.Timestamp(end).value),
                       int(window_normal.value), int(window_abnormal.value))
@@ -268,14 +275,20 @@ class RCAStream:
     WINDOW = pd.Timedelta(minutes=5)
     STEP_ABNORMAL = pd.Timedelta(minutes=4)
 
-    def __init__(self, slo, operation_list, *, ctx=None):
+    def __init__(self, slo, operation_list, *, ctx=None, device_append=True):
         self.slo, self.operation_list = slo, operation_list
         self.ctx = ctx or _lib.default_context()
-        self.data = None          # retained spans (traces that can still be in a window)
+        self.data = None          # retained spans as a DataFrame (host mode only)
         self.cur = None           # the chain's next window start (pd.Timestamp)
         self.watermark = None     # largest trace start seen
         self.end = None           # largest trace end seen (the offline driver's loop bound)
         self.dead = False         # an empty window ended the driver (T2)
+        # device mode (default): the resident table lives in HBM and grows by mr_spans_append, so
+        # a push costs O(chunk) on the host and across PCIe; the chunk frames are kept (by
+        # reference) only for the per-window fallback.  Host mode: pd.concat + a full re-ingest.
+        self._stream = SpanStream(self.ctx) if device_append else None
+        self._frames = []         # (chunk, its largest trace start) of the device mode
+        self._empty = None        # a zero-row frame with the chunks' columns
 
     def push(self, chunk: pd.DataFrame):
         if self.dead:
@@ -289,25 +302,50 @@ class RCAStream:
             raise ValueError("RCAStream.push: chunks must arrive in trace-start order")
         self.watermark = hi if self.watermark is None else max(self.watermark, hi)
         self.end = e if self.end is None else max(self.end, e)
-        self.data = chunk if self.data is None else pd.concat([self.data, chunk], ignore_index=True)
+        arrays = SpanStream.accepts(chunk) if self._stream is not None else None
+        if arrays is not None:
+            self._stream.append(chunk, int(pd.Timestamp(self.cur).value), arrays)
+            self._frames.append((chunk, hi))
+            self._empty = chunk.iloc[:0]
+        else:
+            if self._stream is not None:   # a chunk the device append cannot take: host mode from here
+                self.data = self._frame()
+                self._stream.close()
+                self._stream, self._frames = None, []
+            self.data = chunk if self.data is None else pd.concat([self.data, chunk], ignore_index=True)
         # complete windows: start + 5 min < watermark
         self._advance(self.watermark - self.WINDOW, final=False)
 
     def close(self):
-        if self.dead or self.data is None:
+        if self.dead or (self.data is None if self._stream is None else self._stream.dev is None):
             return
         self._advance(self.end, final=True)
+
+    def _frame(self):
+        """The resident spans as a DataFrame (device mode: from the kept chunk frames)."""
+        if self._stream is None:
+            return self.data
+        if not self._frames:
+            return self._empty
+        df = pd.concat([f for f, _ in self._frames], ignore_index=True) if len(self._frames) > 1 else self._frames[0][0]
+        keep = df["startTime"] >= self.cur
+        return df if keep.all() else df[keep].reset_index(drop=True)
 
     def _advance(self, limit, final):
         if not self.cur < limit:
             return
         try:
-            plan = _sweep_plan(self.data, self.slo, self.cur, limit, self.WINDOW, self.STEP_ABNORMAL, self.ctx)
+            if self._stream is not None:
+                plan = _sweep_plan_dev(self._stream.table, self._stream.dev, self.slo, self.cur, limit, self.WINDOW,
+                                       self.STEP_ABNORMAL, self.ctx)
+            else:
+                plan = _sweep_plan(self.data, self.slo, self.cur, limit, self.WINDOW, self.STEP_ABNORMAL, self.ctx)
             if plan is None:   # window times vary within a trace: window by window
+                data = self._frame()
                 if final:
-                    self.cur = _window_loop(self.data, self.slo, self.operation_list, self.cur, limit)
+                    self.cur = _window_loop(data, self.slo, self.operation_list, self.cur, limit)
                 else:
-                    self.cur = self._loop_complete(limit)
+                    self.cur = self._loop_complete(data, limit)
             else:
                 events = sweep_chain(plan)
                 _sweep_emit(plan, events, sweep_rank(plan, events))
@@ -315,15 +353,18 @@ class RCAStream:
         except TypeError:
             self.dead = True
             raise
+        if self._stream is not None:   # frames whose every trace started before the next window go
+            self._frames = [(f, h) for f, h in self._frames if h >= self.cur]
+            return
         keep = self.data["startTime"] >= self.cur   # traces before the next window leave the table
         if not keep.all():
             self.data = self.data[keep].reset_index(drop=True)
 
-    def _loop_complete(self, limit):
+    def _loop_complete(self, data, limit):
         """The window loop for per-span times, one window at a time while its start is before limit."""
         cur = self.cur
         while cur < limit:
-            nxt = _window_loop(self.data, self.slo, self.operation_list, cur, cur + pd.Timedelta(1, unit="ns"))
+            nxt = _window_loop(data, self.slo, self.operation_list, cur, cur + pd.Timedelta(1, unit="ns"))
             cur = nxt
         return cur
 

@@ -32,6 +32,42 @@ ROOT_INDEX = "root"   # preprocess_data.py:7
 
 
 # ------------------------------------------------------------------------ span table cache
+def span_strings(df: pd.DataFrame, arrays):
+    """The mr_span_strings view of a DataFrame's Arrow string columns (no copies of the string
+    bytes) plus the host arrays it points into: (struct, keep-alive, duration, tstart, tend)."""
+    S = len(df)
+    ss = _lib.SpanStrings()
+    ss.n_spans = S
+    keep = {"arrays": arrays}
+    for field, col in (("trace_id", "traceID"), ("span_id", "spanID"), ("parent_id", "ParentSpanId"),
+                       ("service", "serviceName"), ("operation", "operationName"), ("pod", "podName")):
+        a = arrays[col]
+        validity, offsets, data = a.buffers()[:3]
+        sc = getattr(ss, field)
+        if offsets is None:   # an all-null column (no ParentSpanId): zero offsets, no bytes
+            z = np.zeros(S + 1, np.int64)
+            keep[col] = z
+            sc.offsets = ptr(z, C.c_int64)
+            sc.bytes = None
+        else:
+            sc.offsets = C.cast(C.c_void_p(offsets.address + 8 * a.offset), C.POINTER(C.c_int64))
+            sc.bytes = data.address if data is not None and data.size else None
+        if a.null_count:
+            vb = np.unpackbits(np.frombuffer(validity, np.uint8), bitorder="little")[a.offset:a.offset + S]
+            v = np.packbits(vb, bitorder="little")
+            keep[col + ".valid"] = v
+            sc.valid = v.ctypes.data
+        else:
+            sc.valid = None
+    dur = np.ascontiguousarray(df["duration"].to_numpy(dtype=np.int64))
+    ss.duration = ptr(dur, C.c_int64)
+    ts = te = None
+    if "startTime" in df and "endTime" in df:
+        ts, te = np.ascontiguousarray(_as_ns(df["startTime"])), np.ascontiguousarray(_as_ns(df["endTime"]))
+        ss.tstart, ss.tend = ptr(ts, C.c_int64), ptr(te, C.c_int64)
+    return ss, keep, dur, ts, te
+
+
 class DeviceSpans:
     """An mr_spans handle: the span columns resident in HBM."""
 
@@ -39,39 +75,9 @@ class DeviceSpans:
     def ingest(cls, ctx, df: pd.DataFrame, arrays):
         """The table built on the device from the DataFrame's strings (mr_spans_ingest, SURVEY 8(f)
         f2): factorisation, name rules and dictionaries in HBM.  Returns (IngestedTable, DeviceSpans)."""
-        lib = _lib.load()
-        S = len(df)
-        ss = _lib.SpanStrings()
-        ss.n_spans = S
-        keep = {"arrays": arrays}
-        for field, col in (("trace_id", "traceID"), ("span_id", "spanID"), ("parent_id", "ParentSpanId"),
-                           ("service", "serviceName"), ("operation", "operationName"), ("pod", "podName")):
-            a = arrays[col]
-            validity, offsets, data = a.buffers()[:3]
-            sc = getattr(ss, field)
-            if offsets is None:   # an all-null column (no ParentSpanId): zero offsets, no bytes
-                z = np.zeros(S + 1, np.int64)
-                keep[col] = z
-                sc.offsets = ptr(z, C.c_int64)
-                sc.bytes = None
-            else:
-                sc.offsets = C.cast(C.c_void_p(offsets.address + 8 * a.offset), C.POINTER(C.c_int64))
-                sc.bytes = data.address if data is not None and data.size else None
-            if a.null_count:
-                vb = np.unpackbits(np.frombuffer(validity, np.uint8), bitorder="little")[a.offset:a.offset + S]
-                v = np.packbits(vb, bitorder="little")
-                keep[col + ".valid"] = v
-                sc.valid = v.ctypes.data
-            else:
-                sc.valid = None
-        dur = np.ascontiguousarray(df["duration"].to_numpy(dtype=np.int64))
-        ss.duration = ptr(dur, C.c_int64)
-        ts = te = None
-        if "startTime" in df and "endTime" in df:
-            ts, te = np.ascontiguousarray(_as_ns(df["startTime"])), np.ascontiguousarray(_as_ns(df["endTime"]))
-            ss.tstart, ss.tend = ptr(ts, C.c_int64), ptr(te, C.c_int64)
+        ss, _keep, dur, ts, te = span_strings(df, arrays)
         h = _lib.P()
-        ctx.check(lib.mr_spans_ingest(ctx.h, C.byref(ss), C.byref(h)), "mr_spans_ingest")
+        ctx.check(_lib.load().mr_spans_ingest(ctx.h, C.byref(ss), C.byref(h)), "mr_spans_ingest")
         dev = cls.__new__(cls)
         dev.ctx, dev.h = ctx, h
         table = IngestedTable(dev, arrays, dur, ts, te)
@@ -190,6 +196,93 @@ def span_table(df: pd.DataFrame, ctx=None):
         ref, cref = (lambda: df), (lambda: ctx)
     _CACHE[key] = (ref, cref, fp, table, dev)
     return table, dev
+
+
+class StreamedTable(IngestedTable):
+    """IngestedTable of a table built by mr_spans_append: names are read from the chunk that holds
+    each code's first row (mr_spans_dict_sources gives its stream row number)."""
+
+    def __init__(self, dev, chunks):
+        super().__init__(dev, None, None, None, None)
+        self._chunks = chunks   # [(first stream row, rows, Arrow columns)], ascending
+
+    def _rows(self, which):
+        n = (self.n_traces, self.n_podops, self.n_svcops)[which]
+        src = np.zeros(max(n, 1), np.int64)
+        self._dev.ctx.check(_lib.load().mr_spans_dict_sources(self._dev.h, which, ptr(src, C.c_int64)),
+                            "mr_spans_dict_sources")
+        return src[:n]
+
+    def _take(self, col, rows):
+        import pyarrow as pa
+
+        rows = np.asarray(rows, np.int64)
+        bases = np.array([c[0] for c in self._chunks], np.int64)
+        which = np.searchsorted(bases, rows, side="right") - 1
+        out = [None] * rows.size
+        for ci in np.unique(which):
+            sel = np.flatnonzero(which == ci)
+            base, _n, arrays = self._chunks[ci]
+            vals = arrays[col].take(pa.array(rows[sel] - base)).to_pylist()
+            for k, v in zip(sel, vals):
+                out[k] = v
+        return out
+
+
+class SpanStream:
+    """an append-only device span table (mr_spans_append).  Each append keeps the
+    resident rows whose trace starts at or after ``keep_from`` and adds the chunk's rows; only the
+    chunk's strings cross PCIe and only its Arrow columns are built on the host, so the host cost of
+    an append scales with the chunk, not with the resident table.  The resulting table equals
+    :func:`span_table` of the concatenated, filtered DataFrame row for row."""
+
+    def __init__(self, ctx=None):
+        self.ctx = ctx or _lib.default_context()
+        self.dev = None
+        self.table = None
+        self.chunks = []        # (first stream row, rows, Arrow columns, largest trace start)
+        self.next = 0
+
+    @staticmethod
+    def accepts(chunk: pd.DataFrame):
+        """Arrow string columns for a chunk the device append can take (string columns, datetime
+        trace times), else None."""
+        if len(chunk) == 0 or not all(c in chunk.columns and np.issubdtype(chunk[c].dtype, np.datetime64)
+                                      for c in ("startTime", "endTime")):
+            return None
+        return arrow_columns(chunk)
+
+    def append(self, chunk: pd.DataFrame, keep_from_ns: int, arrays=None):
+        arrays = arrays if arrays is not None else self.accepts(chunk)
+        if arrays is None:
+            raise ValueError("SpanStream.append: the chunk needs string columns and datetime startTime/endTime")
+        ss, _keep, _dur, ts, _te = span_strings(chunk, arrays)
+        h = _lib.P()
+        self.ctx.check(_lib.load().mr_spans_append(self.ctx.h, self.dev.h if self.dev is not None else None,
+                                                   int(keep_from_ns), C.byref(ss), C.byref(h)), "mr_spans_append")
+        if self.dev is not None:
+            self.dev.close()
+        dev = DeviceSpans.__new__(DeviceSpans)
+        dev.ctx, dev.h = self.ctx, h
+        self.chunks.append((self.next, len(chunk), arrays, int(ts.max())))
+        self.next += len(chunk)
+        # chunks whose every trace started before keep_from hold no resident row any more
+        self.chunks = [c for c in self.chunks if c[3] >= keep_from_ns]
+        self.dev = dev
+        self.table = StreamedTable(dev, [c[:3] for c in self.chunks])
+        dev.table = self.table
+        return self.table, dev
+
+    def frame(self, keep_from_ns: int, frames):
+        """The resident rows as a DataFrame (the per-window fallback's input), from the chunk frames."""
+        df = pd.concat(frames, ignore_index=True) if len(frames) > 1 else frames[0]
+        keep = _as_ns(df["startTime"]) >= keep_from_ns
+        return df[keep].reset_index(drop=True) if not keep.all() else df
+
+    def close(self):
+        if self.dev is not None:
+            self.dev.close()
+        self.dev = self.table = None
 
 
 # ------------------------------------------------------------------------ reference utilities

@@ -215,30 +215,29 @@ class IngestedTable:
                             "mr_spans_dict_rows")
         return rows[:n]
 
-    def _op_names(self, rows):
+    def _take(self, col, rows):
+        """Values of string column ``col`` at ``rows`` (as returned by :meth:`_rows`), a list."""
         import pyarrow as pa
 
-        idx = pa.array(rows)
-        svc = np.array(self._arrays["serviceName"].take(idx).to_pylist(), dtype=object)
-        op = np.array(self._arrays["operationName"].take(idx).to_pylist(), dtype=object)
+        return self._arrays[col].take(pa.array(rows)).to_pylist()
+
+    def _op_names(self, rows):
+        svc = np.array(self._take("serviceName", rows), dtype=object)
+        op = np.array(self._take("operationName", rows), dtype=object)
         return svc, op_display(svc, op)
 
     @property
     def trace_names(self):
         if "trace" not in self._names:
-            import pyarrow as pa
-
-            self._names["trace"] = self._arrays["traceID"].take(pa.array(self._rows(0))).to_pylist()
+            self._names["trace"] = self._take("traceID", self._rows(0))
         return self._names["trace"]
 
     @property
     def podop_names(self):
         if "podop" not in self._names:
-            import pyarrow as pa
-
             rows = self._rows(1)
             _, op = self._op_names(rows)
-            pod = self._arrays["podName"].take(pa.array(rows)).to_pylist()
+            pod = self._take("podName", rows)
             self._names["podop"] = [f"{a}_{b}" for a, b in zip(pod, op)]
         return self._names["podop"]
 

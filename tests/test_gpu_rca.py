@@ -514,11 +514,14 @@ def test_windows_batch_fast_paths_equal_general_paths(c3_window, monkeypatch):
         d.close()
 
 
-@pytest.mark.parametrize("name,minutes", [("stream", 7), ("stream", 3), ("stream_gap", 7)])
-def test_rca_stream_matches_offline_driver(name, minutes, tmp_path, monkeypatch):
+@pytest.mark.parametrize("name,minutes,device_append", [("stream", 7, True), ("stream", 3, True),
+                                                         ("stream_gap", 7, True), ("stream", 7, False),
+                                                         ("stream_gap", 3, False)])
+def test_rca_stream_matches_offline_driver(name, minutes, device_append, tmp_path, monkeypatch):
     """f3 online (RCAStream): the reference-captured 60-minute streams pushed in trace-aligned
     chunks of a few minutes print what the reference's offline driver printed over the whole frame
-    (and write its result.csv, and raise its empty-window TypeError)."""
+    (and write its result.csv, and raise its empty-window TypeError) -- with the resident table grown
+    on the device (mr_spans_append) and with the host concat + re-ingest."""
     from microrank_amd import synth
     from microrank_amd.online_rca import RCAStream
 
@@ -533,7 +536,7 @@ def test_rca_stream_matches_offline_driver(name, minutes, tmp_path, monkeypatch)
     err = None
     try:
         with contextlib.redirect_stdout(buf):
-            s = RCAStream(slo, case["operation_list"])
+            s = RCAStream(slo, case["operation_list"], device_append=device_append)
             for b in np.unique(bucket):
                 s.push(adf[bucket == b].copy())
             s.close()
@@ -554,6 +557,51 @@ def test_rca_stream_matches_offline_driver(name, minutes, tmp_path, monkeypatch)
     if case["result_csv"] is not None:
         got_csv = open("result.csv").read().splitlines()
         assert [r.split(",")[:-1] for r in got_csv] == [r.split(",")[:-1] for r in case["result_csv"].splitlines()]
+
+
+def test_span_append_equals_ingest_of_concatenation():
+    """mr_spans_append: the table grown chunk by chunk (with resident rows retired by trace start)
+    is the table mr_spans_ingest builds from the concatenated, filtered frame -- same size,
+    dictionaries (names in code order), code columns bit for bit, and the same detector / graph
+    results; prev stays usable; a foreign prev is refused."""
+    from microrank_amd import _lib, synth
+    from microrank_amd.preprocess_data import SpanStream, span_table
+
+    _, adf = synth.stream_dataframes(24, 1200, 5, minutes=30.0)
+    ctx = _lib.default_context()
+    t0 = adf["startTime"].min()
+    bucket = ((adf["startTime"] - t0) // pd.Timedelta(minutes=4)).to_numpy()
+    st = SpanStream(ctx)
+    resident = None
+    cuts = [t0 + pd.Timedelta(minutes=m) for m in (0, 0, 3, 9, 9, 15, 22, 22)]
+    for i, b in enumerate(np.unique(bucket)):
+        chunk = adf[bucket == b].copy()
+        cut = cuts[min(i, len(cuts) - 1)]
+        prev_dev = st.dev
+        table, dev = st.append(chunk, int(cut.value))
+        if resident is not None:
+            resident = resident[resident["startTime"] >= cut]
+        resident = chunk if resident is None else pd.concat([resident, chunk], ignore_index=True)
+        resident = resident.reset_index(drop=True)
+        ref_table, _ = span_table(resident.copy(), ctx)
+        assert (table.n_spans, table.n_traces, table.n_podops, table.n_svcops) == \
+            (ref_table.n_spans, ref_table.n_traces, ref_table.n_podops, ref_table.n_svcops)
+        assert table.trace_names == ref_table.trace_names
+        assert table.podop_names == ref_table.podop_names
+        assert table.svcop_names == ref_table.svcop_names
+        for a, b_ in zip(table._code_cols(), ref_table._code_cols()):
+            assert np.array_equal(a, b_)
+        assert prev_dev is None or prev_dev.h is None   # the previous handle was released
+    # a table that was not appended cannot be the previous one
+    ref_table, ref_dev = span_table(adf.copy(), ctx)
+    from microrank_amd.preprocess_data import span_strings
+    from microrank_amd.spans import arrow_columns
+    import ctypes as C
+    ss, _keep, *_ = span_strings(adf, arrow_columns(adf))
+    h = _lib.P()
+    rc = _lib.load().mr_spans_append(ctx.h, ref_dev.h, 0, C.byref(ss), C.byref(h))
+    assert rc == _lib.MR_ERR_STATE
+    st.close()
 
 
 def test_c3_window_matches_reference_golden():
