@@ -1544,6 +1544,9 @@ enum { WV_SU_GLOBAL = 0, WV_SU_ALL = 1, WV_SU_HOT = 2 };
 #ifndef MR_TREXP
 #define MR_TREXP 0   // timing experiments only: 1 atomics / 2 su reads at conflict-free addresses
 #endif
+#ifndef MR_TRSHORT
+#define MR_TRSHORT 0   // timing experiments only: bit i set = no short-tile walk of 2^i chunks
+#endif
 // The single-pass iteration with lane = trace.  At prepare a graph's traces are sorted by op
 // count (tperm: position -> trace) and cut into wave tiles of 64 positions; a tile stores its
 // traces' ids lane-interleaved in chunks of 4 (chunk c = 64 lanes x 4 u16: one coalesced 512-B
@@ -1577,10 +1580,119 @@ struct TrLds {
     }
 };
 
+// Short tiles (every trace of the tile has at most 4 NC ops), su in LDS: a tile is ONE register
+// set -- its NC id chunks, q, c = (1-d) v, w (EXT & 1: the kind multiplicity's mw instead),
+// the cold half of the sums (EXT & 2), and the chunk offsets of the next two tiles -- loaded
+// unconditionally (addresses clamped) one whole tile ahead.  The tile loop is unrolled by two so
+// the two register sets alternate by renaming: no register with a load in flight is ever copied,
+// so the only memory waits are for loads issued a tile earlier (the ring of tr_walk's general
+// loop below rotates per chunk and at tile ends has to copy the next tile's q, which made every
+// tile end wait for all loads in flight, the ids three chunks ahead included).  Tiles are sorted
+// by length, so a wave's run is a prefix of short tiles (NC = 4, then 8) and a suffix the general
+// loop takes.  Same per-lane sums in the same order as the general loop: bitwise equal results.
+template <class Q, int NC, int EXT>
+struct TrTile {
+    u32x2 id[NC];
+    Q q;
+    float c;
+    float w;
+    double mw;     // EXT & 1: w times the kind multiplicity (kind-compressed graphs)
+    double x;      // EXT & 2: the cold half of the trace's su sum (wide graphs)
+    int32_t cw;    // lane j: coff[k + 1 + j] (readlane 0 / 1: the next tile's chunk range)
+};
+template <class Q, int NC, int EXT>
+__device__ __forceinline__ int32_t tr_walk_short(const GDev& G, int32_t k, const int32_t ke, int32_t T, int32_t lane,
+                                                 int cur, int nxt, double d, double Ms, double xsc, const double* su_l,
+                                                 unsigned long long* lacc, double& rmax) {
+    const GLB u32x2* ids = gp((const u32x2*)G.tids) + lane;
+    const GLB int32_t* coff = gp(G.coff);
+    const GLB Q* qc = gp((const Q*)G.q[cur]);
+    GLB Q* qn = gpw((Q*)G.q[nxt]);
+    const GLB float* c_tp = gp(G.c_tp);
+    const GLB float* w_tp = gp(G.w_tp);
+    // EXT: a graph of the launch may carry mw / cold sums; graphs without them load a valid dummy
+    // (su[0]) and select the plain value -- unconditional loads, no branches around them
+    const GLB double* sug = gp(G.sub[cur]);
+    const bool kc = (EXT & 1) && G.mw_tp, cx = (EXT & 2) && G.cold_acc;
+    const GLB double* mw_tp = kc ? gp(G.mw_tp) : sug;
+    const GLB double* cacc = cx ? gp(G.cold_acc) : sug;
+    const int32_t cl = __builtin_amdgcn_readfirstlane(coff[ke]) - 1;   // the run's last chunk
+    // the first tile's chunk range
+    int32_t c0, n;
+    {
+        const int32_t v = coff[min(k + lane, ke)];
+        c0 = __builtin_amdgcn_readfirstlane(v);
+        n = __builtin_amdgcn_readlane(v, 1) - c0;
+    }
+    if (n > NC) return k;
+    using R = TrTile<Q, NC, EXT>;
+    auto load = [&](R& r, int32_t kk, int32_t cc0) {
+        const int32_t kq = min(kk, ke - 1);
+        const int32_t p = min(kq * WAVE + lane, T - 1);
+#pragma unroll
+        for (int j = 0; j < NC; ++j) r.id[j] = ids[(size_t)min(cc0 + j, cl) * WAVE];
+        r.q = qc[p];
+        r.c = c_tp[p];
+        r.w = w_tp[p];
+        if constexpr ((EXT & 1) != 0) r.mw = mw_tp[kc ? p : 0];
+        if constexpr ((EXT & 2) != 0) r.x = cacc[cx ? p : 0];
+        r.cw = coff[min(kq + 1 + lane, ke)];
+    };
+    // tile kk from r: lane = position kk * 64 + lane
+    auto run = [&](const R& r, int32_t kk, int32_t nn) {
+        const int32_t p = kk * WAVE + lane;
+        const bool own = p < T;
+        const unsigned long long X = own ? (unsigned long long)__double2ull_rn((double)r.q * xsc) : 0ull;
+        double acc = 0.0;
+        double sv[2][4];
+        auto rd = [&](const u32x2 w, double* s) {
+            s[0] = su_l[w.x & 0xffffu];
+            s[1] = su_l[w.x >> 16];
+            s[2] = su_l[w.y & 0xffffu];
+            s[3] = su_l[w.y >> 16];
+        };
+        rd(r.id[0], sv[0]);
+#pragma unroll
+        for (int j = 0; j < NC; ++j) {
+            if (j >= nn) break;
+            if (j + 1 < NC && j + 1 < nn) rd(r.id[j + 1], sv[(j + 1) & 1]);
+            const u32x2 w = r.id[j];
+            atomicAdd(&lacc[w.x & 0xffffu], X);
+            atomicAdd(&lacc[w.x >> 16], X);
+            atomicAdd(&lacc[w.y & 0xffffu], X);
+            atomicAdd(&lacc[w.y >> 16], X);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) acc += sv[j & 1][i];
+        }
+        const double x = cx ? r.x : 0.0;
+        const double rp = d * ((acc + x) / Ms) + (double)r.c;   // pagerank.py:125
+        if (own) rmax = nmax(rmax, rp);
+        const double wq = kc ? r.mw : (double)r.w;
+        qn[own ? p : T] = (Q)(wq * rp);   // q[T]: pad slot
+    };
+    R A, B;
+    load(A, k, c0);
+    int32_t nA = n;
+    for (;;) {
+        // B = tile k + 1 (its range from A's offsets), then A's tile
+        int32_t c0B = __builtin_amdgcn_readfirstlane(A.cw);
+        int32_t nB = __builtin_amdgcn_readlane(A.cw, 1) - c0B;
+        load(B, k + 1, c0B);
+        run(A, k, nA);
+        if (++k == ke || nB > NC) break;
+        int32_t c0A = __builtin_amdgcn_readfirstlane(B.cw);
+        nA = __builtin_amdgcn_readlane(B.cw, 1) - c0A;
+        load(A, k + 1, c0A);
+        run(B, k, nB);
+        if (++k == ke || nA > NC) break;
+    }
+    return k;
+}
+
 // The wave's walk of k_tr_a over its run of wave tiles (shared with k_pr_cluster): per entry one
 // su read, one add into the lane's trace sum, one LDS u64 atomic of X_t; per tile r' of its traces
 // and their next q.  Returns the wave's largest r' (-inf when it owns no trace).
-template <class Q, int SUM, int NT>
+template <class Q, int SUM, int NT, int EXT = 0>
 __device__ __forceinline__ double tr_walk(const GDev& G, int32_t lb, int cur, int nxt, int32_t N, int32_t NH, double d,
                                           double Ms, double xsc, const double* su_l, unsigned long long* lacc) {
     constexpr bool SUL = SUM == WV_SU_ALL, HOT = SUM == WV_SU_HOT;
@@ -1599,6 +1711,12 @@ __device__ __forceinline__ double tr_walk(const GDev& G, int32_t lb, int cur, in
     int32_t k = __builtin_amdgcn_readfirstlane(wt[0]);
     const int32_t ke = __builtin_amdgcn_readfirstlane(wt[1]);
     double rmax = -__builtin_huge_val();
+    if constexpr (SUL && !(MR_TREXP & 3)) {
+        if (k < ke && !(MR_TRSHORT & 1)) k = tr_walk_short<Q, 1, EXT>(G, k, ke, T, lane, cur, nxt, d, Ms, xsc, su_l, lacc, rmax);
+        if (k < ke && !(MR_TRSHORT & 2)) k = tr_walk_short<Q, 2, EXT>(G, k, ke, T, lane, cur, nxt, d, Ms, xsc, su_l, lacc, rmax);
+        if (k < ke && !(MR_TRSHORT & 4)) k = tr_walk_short<Q, 4, EXT>(G, k, ke, T, lane, cur, nxt, d, Ms, xsc, su_l, lacc, rmax);
+        if (k < ke && !(MR_TRSHORT & 8)) k = tr_walk_short<Q, 8, EXT>(G, k, ke, T, lane, cur, nxt, d, Ms, xsc, su_l, lacc, rmax);
+    }
     if (k < ke) {
         auto pos = [&](int32_t kk) { return min(kk * WAVE + lane, T - 1); };
         // cold-op su of a chunk (LDS-resident ops load sug[0]: one line, no traffic; pads read as 0)
@@ -1696,7 +1814,7 @@ __device__ __forceinline__ double tr_walk(const GDev& G, int32_t lb, int cur, in
     return rmax;
 }
 
-template <class Q, int SUM, int NT>
+template <class Q, int SUM, int NT, int EXT>
 __global__ void __launch_bounds__(NT) k_tr_a(const GDev* __restrict__ gs, int32_t ng, int32_t split, double d,
                                              double alpha, int it, int32_t unused) {
     constexpr bool SUL = SUM == WV_SU_ALL, HOT = SUM == WV_SU_HOT;
@@ -1734,7 +1852,7 @@ __global__ void __launch_bounds__(NT) k_tr_a(const GDev* __restrict__ gs, int32_
     }
     __syncthreads();   // accumulator and maxima ready
     const double xsc = (G.dscale ? G.dscale[0] : G.fx_scale) / msh[1], Ms = msh[0];
-    const double rmax_w = tr_walk<Q, SUM, NT>(G, lb, cur, nxt, N, NH, d, Ms, xsc, su_l, lacc);
+    const double rmax_w = tr_walk<Q, SUM, NT, EXT>(G, lb, cur, nxt, N, NH, d, Ms, xsc, su_l, lacc);
     // (the call-graph term alpha P_ss s_k is k_fx_b's: a wave per op)
     __syncthreads();
     GLB unsigned long long* prow = gpw(G.fx_part) + (size_t)lb * N;
@@ -2330,14 +2448,19 @@ void mr_prof_begin(mr_ctx* ctx);
 void mr_prof_end(mr_ctx* ctx, double bytes, int64_t iters = 1);
 
 using TrA = void (*)(const GDev*, int32_t, int32_t, double, double, int, int32_t);
-static TrA tr_kernel(bool fp32, int mode, int NT) {
+// ext: some graph of the launch carries kind multiplicities (mw_tp) or cold sums (cold_acc) --
+// only the short-tile walk of the su-in-LDS mode distinguishes it
+static TrA tr_kernel(bool fp32, int mode, int NT, bool ext = false) {
     static const TrA tab[2][3][2] = {
-        {{k_tr_a<double, 0, 512>, k_tr_a<double, 0, 1024>},
-         {k_tr_a<double, 1, 512>, k_tr_a<double, 1, 1024>},
-         {k_tr_a<double, 2, 512>, k_tr_a<double, 2, 1024>}},
-        {{k_tr_a<float, 0, 512>, k_tr_a<float, 0, 1024>},
-         {k_tr_a<float, 1, 512>, k_tr_a<float, 1, 1024>},
-         {k_tr_a<float, 2, 512>, k_tr_a<float, 2, 1024>}}};
+        {{k_tr_a<double, 0, 512, 0>, k_tr_a<double, 0, 1024, 0>},
+         {k_tr_a<double, 1, 512, 0>, k_tr_a<double, 1, 1024, 0>},
+         {k_tr_a<double, 2, 512, 0>, k_tr_a<double, 2, 1024, 0>}},
+        {{k_tr_a<float, 0, 512, 0>, k_tr_a<float, 0, 1024, 0>},
+         {k_tr_a<float, 1, 512, 0>, k_tr_a<float, 1, 1024, 0>},
+         {k_tr_a<float, 2, 512, 0>, k_tr_a<float, 2, 1024, 0>}}};
+    static const TrA tab_ext[2][2] = {{k_tr_a<double, 1, 512, 3>, k_tr_a<double, 1, 1024, 3>},
+                                      {k_tr_a<float, 1, 512, 3>, k_tr_a<float, 1, 1024, 3>}};
+    if (ext && mode == WV_SU_ALL) return tab_ext[fp32 ? 1 : 0][NT == 1024 ? 1 : 0];
     return tab[fp32 ? 1 : 0][mode][NT == 1024 ? 1 : 0];
 }
 static int num_cus() {
@@ -3463,7 +3586,9 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
     const int32_t split_fa = ng == 2 ? hv[1].blk0f : 0, split_fb = ng == 2 ? hv[1].blk0fb : 0;
     for (int i = 0; i < ng; ++i)
         if (gs[i]->fused) lds_f = std::max(lds_f, plan_lds(kern_n(gs[i]), plan));
-    const TrA tr_a = tr_kernel(fp32, plan.mode, plan.NT);
+    bool any_ext = false;   // kind multiplicities or cold sums in some fused graph of the launch
+    for (int i = 0; i < ng; ++i) any_ext = any_ext || (gs[i]->fused && (hv[(size_t)i].mw_tp || hv[(size_t)i].cold_acc));
+    const TrA tr_a = tr_kernel(fp32, plan.mode, plan.NT, any_ext);
     // a sharded graph with no collective backend is one whole shard: the split launches around the
     // (no-op) all-reduces would compute the same integers / sums in two halves
     const bool coll = sharded && mr_coll_ready(ctx);
