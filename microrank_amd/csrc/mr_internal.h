@@ -191,6 +191,11 @@ struct mr_graph {
     DBuf<int32_t> coff;              // [n_wt+1] first chunk of a tile
     std::vector<int32_t> coff_h;     // host copy (the per-wave tile split of a launch)
     DBuf<float> w_tp, c_tp;          // [T] w_t, c_t in position order
+    // register-accumulated hot ops (large graphs, su in LDS): the nhr <= 8 ops present in most
+    // traces leave the id chunks; hmask[p] (position order) says which of them trace p holds
+    int32_t nhr = 0;
+    int32_t hop[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    DBuf<uint8_t> hmask;
     // kind compression (MR_PR_KIND_COMPRESS): a graph of one representative trace per kind whose
     // q carries the kind's multiplicity (mw_tp = w_t * mult in position order); kind = mult
     bool kinds_given = false;

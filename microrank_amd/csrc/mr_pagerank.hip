@@ -200,7 +200,7 @@ __global__ void k_relabel_ids(const uint16_t* ids, int64_t n, const int32_t* inv
 // ids, su and accumulator in LDS); the other ("cold") entries of each trace are summed per
 // position by k_cold_trace and accumulated per op range by k_cold_ops (LDS accumulator of one
 // range, (position, op) pairs grouped by range, position order within a range).
-constexpr int32_t WIDE_NA = 10112;      // (WIDE_NA + TR_PAD) * 16 B <= k_tr_a's LDS (su + accumulator)
+constexpr int32_t WIDE_NA = 10000;      // (WIDE_NA + TR_PAD) * 16 B + the hot-op sums <= k_tr_a's LDS
 constexpr int32_t WIDE_RW_MAX = 19456;  // ops per cold range: k_cold_ops' accumulator <= 152 KB
 constexpr int WIDE_CB = 256;            // k_cold_ops blocks over all ranges (one per CU: LDS-bound)
 constexpr int WIDE_CT = 1024;           // k_cold_ops block size
@@ -457,17 +457,17 @@ __global__ void k_tr_coff(const int64_t* c64, int32_t n, int32_t* coff) {
 // host sizes the grid so those fit).  scale = {2^SC, 2^-SC}, SC = 64 - bits(most traces of a block).
 constexpr int TC_T = 1024, TC_MAX = 16384;
 __device__ __forceinline__ void tr_cut_body(const int32_t* coff, int32_t W, int32_t nw, int32_t NW, int32_t* cut,
-                                            double* scale) {
+                                            double* scale, double tw) {
     __shared__ int32_t lc[TC_MAX + 1];
     __shared__ int32_t mx;
     if (threadIdx.x == 0) mx = 0;
-    const double total = W ? (double)coff[W] + 2.0 * (double)W : 0.0;
+    const double total = W ? (double)coff[W] + tw * (double)W : 0.0;
     for (int32_t i = threadIdx.x; i <= nw; i += TC_T) {
         const double target = total * (double)i / (double)nw;
         int32_t lo = 0, hi = W;
         while (lo < hi) {
             const int32_t mid = (lo + hi) >> 1;
-            if ((double)coff[mid] + 2.0 * (double)mid < target) lo = mid + 1;
+            if ((double)coff[mid] + tw * (double)mid < target) lo = mid + 1;
             else hi = mid;
         }
         lc[i] = i == nw ? W : lo;
@@ -492,15 +492,16 @@ __device__ __forceinline__ void tr_cut_body(const int32_t* coff, int32_t W, int3
     }
 }
 __global__ void __launch_bounds__(TC_T) k_tr_cut(const int32_t* coff, int32_t W, int32_t nw, int32_t NW, int32_t* cut,
-                                                 double* scale) {
-    tr_cut_body(coff, W, nw, NW, cut, scale);
+                                                 double* scale, double tw) {
+    tr_cut_body(coff, W, nw, NW, cut, scale, tw);
 }
 // the cuts of a batch's graphs in one launch (block g: graph g)
 struct CutArg {
     const int32_t* coff;
     int32_t* cut;
     double* scale;
-    int32_t W, nw, NW, pad_;
+    int32_t W, nw, NW;
+    float tw;   // a tile's fixed cost in chunks
 };
 constexpr int TC_BATCH = 64;
 struct CutBatch {
@@ -508,7 +509,7 @@ struct CutBatch {
 };
 __global__ void __launch_bounds__(TC_T) k_tr_cut_b(CutBatch b) {
     const CutArg& x = b.a[blockIdx.x];
-    tr_cut_body(x.coff, x.W, x.nw, x.NW, x.cut, x.scale);
+    tr_cut_body(x.coff, x.W, x.nw, x.NW, x.cut, x.scale, (double)x.tw);
 }
 // thread per (tile, lane): the lane's trace rotated by (trace mod len), then pads N + lane
 __device__ __forceinline__ void tr_fill_body(int32_t blk, const int32_t* tperm, const int64_t* off, const uint16_t* ids,
@@ -547,6 +548,140 @@ __global__ void k_tr_fill(const int32_t* tperm, const int64_t* off, const uint16
                           int32_t N, int32_t n_wt, uint16_t* tids) {
     tr_fill_body((int32_t)blockIdx.x, tperm, off, ids, c64, T, N, n_wt, tids);
 }
+// Register-accumulated hot ops (large graphs): the HOT_MAX ops present in the most traces leave the
+// id chunks -- op 0 of the C4 graph is in every trace, so each 16-lane atomic group of every step
+// that holds it adds to ONE LDS address 16 times -- and trace t keeps the bit set of the hot ops it
+// holds instead (hmask).  A trace whose ops are all hot keeps its first one in the list (no empty
+// traces: every tile has a chunk).  hidx[o] = h or -1.
+#ifndef MR_TR_TIERS512
+#define MR_TR_TIERS512 4   // short-tile tiers of the 512-thread k_tr_a (window graphs: occupancy)
+#endif
+#ifndef MR_HOT_MAX
+#define MR_HOT_MAX 8
+#endif
+constexpr int HOT_MAX = MR_HOT_MAX;
+__global__ void __launch_bounds__(256) k_hot_count(const int64_t* off, const uint16_t* ids, int32_t T, const int8_t* hidx,
+                                                   int32_t N, int32_t* rlen, uint8_t* mask) {
+    extern __shared__ int8_t lh8[];
+    for (int32_t o = threadIdx.x; o < N; o += 256) lh8[o] = hidx[o];
+    __syncthreads();
+    const int32_t t = blockIdx.x * 256 + threadIdx.x;
+    if (t >= T) return;
+    uint32_t m = 0, first = 0xffu;
+    int32_t n = 0;
+    for (int64_t e = off[t]; e < off[t + 1]; ++e) {
+        const int h = lh8[ids[e]];
+        if (h >= 0) {
+            if (first == 0xffu) first = (uint32_t)h;
+            m |= 1u << h;
+        } else {
+            ++n;
+        }
+    }
+    if (n == 0 && m) {   // all hot: the first stays in the list
+        m &= ~(1u << first);
+        n = 1;
+    }
+    rlen[t] = n;
+    mask[t] = (uint8_t)m;
+}
+__global__ void __launch_bounds__(256) k_hot_fill(const int64_t* off, const uint16_t* ids, int32_t T, const int8_t* hidx,
+                                                  int32_t N, const uint8_t* mask, const int64_t* roff, uint16_t* rids) {
+    extern __shared__ int8_t lh8[];
+    for (int32_t o = threadIdx.x; o < N; o += 256) lh8[o] = hidx[o];
+    __syncthreads();
+    const int32_t t = blockIdx.x * 256 + threadIdx.x;
+    if (t >= T) return;
+    const uint32_t m = mask[t];
+    int64_t w = roff[t];
+    for (int64_t e = off[t]; e < off[t + 1]; ++e) {
+        const uint16_t o = ids[e];
+        const int h = lh8[o];
+        if (h < 0 || !((m >> h) & 1u)) rids[w++] = o;
+    }
+}
+__global__ void k_hot_perm(const int32_t* tperm, const uint8_t* mask, int32_t T, uint8_t* hmask) {
+    const int32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < T) hmask[p] = mask[tperm[p]];
+}
+
+// Bank-conflict-aware order of a tile's ids (k_tr_a's LDS traffic).  Per step every lane reads
+// su[o] (ds_read_b64: lanes in groups of 32, 8-B slot o mod 32; equal addresses broadcast) and
+// adds into lacc[o] (u64 LDS atomic: groups of 16, slot o mod 16; equal addresses serialise).  A
+// trace's ops can be walked in any order, so per 32-lane half of a tile one thread assigns each
+// lane's items (ops and pads) to steps greedily: lane by lane, the first remaining item whose
+// atomic slot is free in its 16-lane group and whose read slot is free (or holds the same op) in
+// the half; else one clear for the atomic; else any.  Tiles longer than SCHED_L steps keep the
+// rotated order.
+constexpr int SCHED_T = 16, SCHED_L = 64;
+__global__ void __launch_bounds__(SCHED_T) k_tr_sched(const int32_t* coff, int32_t n_wt, uint16_t* tids) {
+    __shared__ uint16_t items_s[SCHED_T][32 * SCHED_L];
+    __shared__ unsigned long long rem_s[SCHED_T][32];
+    __shared__ uint16_t cbuf_s[SCHED_T][32 * 4];
+    const int64_t u = (int64_t)blockIdx.x * SCHED_T + threadIdx.x;
+    if (u >= 2 * (int64_t)n_wt) return;
+    uint16_t* items = items_s[threadIdx.x];
+    unsigned long long* rem = rem_s[threadIdx.x];
+    uint16_t* cbuf = cbuf_s[threadIdx.x];
+    const int32_t tile = (int32_t)(u >> 1), half = (int32_t)(u & 1);
+    const int32_t c0 = coff[tile], nc = coff[tile + 1] - c0, L = 4 * nc;
+    if (L > SCHED_L || nc <= 0) return;
+    unsigned long long* w = (unsigned long long*)tids + (size_t)c0 * WAVE + 32 * half;   // chunk c, lane li: w[c * WAVE + li]
+    for (int32_t c = 0; c < nc; ++c)
+        for (int li = 0; li < 32; ++li) {
+            const unsigned long long v = w[(size_t)c * WAVE + li];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) items[li * SCHED_L + 4 * c + q] = (uint16_t)(v >> (16 * q));
+        }
+    const unsigned long long full = L == 64 ? ~0ull : ((1ull << L) - 1ull);
+    for (int li = 0; li < 32; ++li) rem[li] = full;
+    for (int32_t s = 0; s < L; ++s) {
+        uint32_t used16[2] = {0u, 0u};
+        uint32_t occ32 = 0u;             // read slots taken this step ...
+        uint16_t op32[32];               // ... and by which op (a broadcast when equal)
+        for (int li = 0; li < 32; ++li) {
+            const int g = li >> 4;
+            const uint16_t* it = items + li * SCHED_L;
+            unsigned long long m = rem[li];
+            int best = -1, best_sc = 4;
+            while (m) {
+                const int j = __builtin_ctzll(m);
+                m &= m - 1ull;
+                const uint32_t o = it[j];
+                const uint32_t b16 = o & 15u, b32 = o & 31u;
+                const int sc = (int)((used16[g] >> b16) & 1u) * 2 + (int)(((occ32 >> b32) & 1u) && op32[b32] != o);
+                if (sc < best_sc) {
+                    best_sc = sc;
+                    best = j;
+                    if (sc == 0) break;
+                }
+            }
+            const uint32_t o = it[best];
+            rem[li] &= ~(1ull << best);
+            used16[g] |= 1u << (o & 15u);
+            if (!((occ32 >> (o & 31u)) & 1u)) {
+                occ32 |= 1u << (o & 31u);
+                op32[o & 31u] = (uint16_t)o;
+            }
+            cbuf[li * 4 + (s & 3)] = (uint16_t)o;
+        }
+        if ((s & 3) == 3)
+            for (int li = 0; li < 32; ++li) {
+                unsigned long long v = 0ull;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) v |= (unsigned long long)cbuf[li * 4 + q] << (16 * q);
+                w[(size_t)(s >> 2) * WAVE + li] = v;
+            }
+    }
+}
+static bool tr_sched_on() {
+    static const bool on = [] {
+        const char* e = getenv("MR_TR_SCHED");
+        return e && !strcmp(e, "1");
+    }();
+    return on;
+}
+
 // The prepare of several small fused graphs (a window's two) in one launch per step: block ranges
 // per graph, the same bodies (mr_graph_prepare_batch)
 struct PDev {
@@ -1259,6 +1394,9 @@ struct GDev {
     const float* c_tp;          // c_t, w_t in position order (tperm)
     const float* w_tp;
     const double* mw_tp;        // kind-compressed graphs: w_t * multiplicity (position order), else null
+    const uint8_t* hmask;       // register-accumulated hot ops: trace bits in position order (nhr > 0)
+    int32_t nhr;
+    int32_t hop[8];
     const float* c_t;
     const float* w_t;
     const float* u_o;
@@ -1544,9 +1682,6 @@ enum { WV_SU_GLOBAL = 0, WV_SU_ALL = 1, WV_SU_HOT = 2 };
 #ifndef MR_TREXP
 #define MR_TREXP 0   // timing experiments only: 1 atomics / 2 su reads at conflict-free addresses
 #endif
-#ifndef MR_TRSHORT
-#define MR_TRSHORT 0   // timing experiments only: bit i set = no short-tile walk of 2^i chunks
-#endif
 // The single-pass iteration with lane = trace.  At prepare a graph's traces are sorted by op
 // count (tperm: position -> trace) and cut into wave tiles of 64 positions; a tile stores its
 // traces' ids lane-interleaved in chunks of 4 (chunk c = 64 lanes x 4 u16: one coalesced 512-B
@@ -1561,8 +1696,9 @@ enum { WV_SU_GLOBAL = 0, WV_SU_ALL = 1, WV_SU_HOT = 2 };
 // (sequential: deterministic), one LDS u64 atomic of the lane's X_t (integers: order-free).  The
 // block synchronises only to clear the accumulator and to write its partial row.
 struct TrLds {
-    size_t su, lacc, total;
+    size_t su, lacc, hs, total;
     bool su_lds;      // every op's su fits beside the accumulator (interleaved: 16 B per op)
+    bool hot_ok;      // WV_SU_ALL: the hot-op mask sums (256 doubles) fit too
     int32_t n_hot;    // WV_SU_HOT: su of ops [0, n_hot) in LDS
     // the accumulator first, then su (8-B strides: a 32-lane read group spreads over 32 bank
     // pairs, a 16-lane atomic group over 16)
@@ -1577,10 +1713,18 @@ struct TrLds {
         lacc = 0;
         su = accb;
         total = all ? 2 * accb : accb + (size_t)n_hot * 8;
+        hs = total;
+        hot_ok = all && total + 256 * 8 <= WV_LDS_MAX;
+        if (hot_ok) total += 256 * 8;
     }
 };
 
-// Short tiles (every trace of the tile has at most 4 NC ops), su in LDS: a tile is ONE register
+__device__ __forceinline__ double uni_d(double v) {   // a block-uniform double into SGPRs
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readfirstlane((int)(unsigned)b), hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+// Short tiles (tiles of exactly NC chunks, NC <= 8: traces of <= 32 ops), su in LDS: a tile is ONE register
 // set -- its NC id chunks, q, c = (1-d) v, w (EXT & 1: the kind multiplicity's mw instead),
 // the cold half of the sums (EXT & 2), and the chunk offsets of the next two tiles -- loaded
 // unconditionally (addresses clamped) one whole tile ahead.  The tile loop is unrolled by two so
@@ -1588,8 +1732,9 @@ struct TrLds {
 // so the only memory waits are for loads issued a tile earlier (the ring of tr_walk's general
 // loop below rotates per chunk and at tile ends has to copy the next tile's q, which made every
 // tile end wait for all loads in flight, the ids three chunks ahead included).  Tiles are sorted
-// by length, so a wave's run is a prefix of short tiles (NC = 4, then 8) and a suffix the general
-// loop takes.  Same per-lane sums in the same order as the general loop: bitwise equal results.
+// by length, so a wave's run is a sequence of short-tile tiers (NC = 1, 2, .., 8, each a code copy
+// with every count static) and a suffix of longer tiles the general loop takes.  Same per-lane sums
+// in the same order as the general loop: bitwise equal results.
 template <class Q, int NC, int EXT>
 struct TrTile {
     u32x2 id[NC];
@@ -1599,11 +1744,41 @@ struct TrTile {
     double mw;     // EXT & 1: w times the kind multiplicity (kind-compressed graphs)
     double x;      // EXT & 2: the cold half of the trace's su sum (wide graphs)
     int32_t cw;    // lane j: coff[k + 1 + j] (readlane 0 / 1: the next tile's chunk range)
+    uint32_t hm;   // the trace's hot-op bits (nhr > 0)
 };
+// the hot ops of a trace: their su first in the lane's sum (the same order in both walks), X into
+// the lane's register accumulators (integers: order-free; flushed once per walk)
+// The su part is one LDS read of hs[hm] = the sum of the trace's hot su in h order (k_tr_a builds
+// the 256 sums per iteration: adding the absent ops' +0.0 would not change a sum, so hs[hm] is the
+// lane's own sequential sum over its hot ops).
+struct TrHot {
+    int32_t n;
+    const double* hs;   // LDS [256]
+    unsigned long long acc[HOT_MAX];
+};
+// (every one of the HOT_MAX accumulators is updated: ops past nhr are never in a mask, so they
+// add 0 -- no per-op condition, no duplicated registers)
+__device__ __forceinline__ double tr_hot_init(TrHot& H, uint32_t hm, unsigned long long X) {
+#pragma unroll
+    for (int h = 0; h < HOT_MAX; ++h) {
+        const unsigned long long sel = (unsigned long long)(long long)(((int32_t)(hm << (31 - h))) >> 31);
+        H.acc[h] += X & sel;
+    }
+    return H.hs[hm];
+}
+// hs[m] for m = tid < 256 (su of every op in LDS; the caller synchronises before and after)
+__device__ __forceinline__ void tr_hot_sums(const GDev& G, const double* su_l, double* hs, int32_t tid) {
+    if (tid < 256) {
+        double a = 0.0;
+        for (int h = 0; h < G.nhr; ++h)
+            if ((tid >> h) & 1) a += su_l[G.hop[h]];
+        hs[tid] = a;
+    }
+}
 template <class Q, int NC, int EXT>
 __device__ __forceinline__ int32_t tr_walk_short(const GDev& G, int32_t k, const int32_t ke, int32_t T, int32_t lane,
                                                  int cur, int nxt, double d, double Ms, double xsc, const double* su_l,
-                                                 unsigned long long* lacc, double& rmax) {
+                                                 unsigned long long* lacc, double& rmax, TrHot& H) {
     const GLB u32x2* ids = gp((const u32x2*)G.tids) + lane;
     const GLB int32_t* coff = gp(G.coff);
     const GLB Q* qc = gp((const Q*)G.q[cur]);
@@ -1616,6 +1791,8 @@ __device__ __forceinline__ int32_t tr_walk_short(const GDev& G, int32_t k, const
     const bool kc = (EXT & 1) && G.mw_tp, cx = (EXT & 2) && G.cold_acc;
     const GLB double* mw_tp = kc ? gp(G.mw_tp) : sug;
     const GLB double* cacc = cx ? gp(G.cold_acc) : sug;
+    const bool hot = H.n > 0;
+    const GLB uint8_t* hmk = hot ? gp(G.hmask) : (const GLB uint8_t*)coff;
     const int32_t cl = __builtin_amdgcn_readfirstlane(coff[ke]) - 1;   // the run's last chunk
     // the first tile's chunk range
     int32_t c0, n;
@@ -1624,7 +1801,7 @@ __device__ __forceinline__ int32_t tr_walk_short(const GDev& G, int32_t k, const
         c0 = __builtin_amdgcn_readfirstlane(v);
         n = __builtin_amdgcn_readlane(v, 1) - c0;
     }
-    if (n > NC) return k;
+    if (n != NC) return k;
     using R = TrTile<Q, NC, EXT>;
     auto load = [&](R& r, int32_t kk, int32_t cc0) {
         const int32_t kq = min(kk, ke - 1);
@@ -1637,30 +1814,33 @@ __device__ __forceinline__ int32_t tr_walk_short(const GDev& G, int32_t k, const
         if constexpr ((EXT & 1) != 0) r.mw = mw_tp[kc ? p : 0];
         if constexpr ((EXT & 2) != 0) r.x = cacc[cx ? p : 0];
         r.cw = coff[min(kq + 1 + lane, ke)];
+        r.hm = hmk[hot ? p : 0];
     };
     // tile kk from r: lane = position kk * 64 + lane
-    auto run = [&](const R& r, int32_t kk, int32_t nn) {
+    auto run = [&](const R& r, int32_t kk) {
         const int32_t p = kk * WAVE + lane;
         const bool own = p < T;
         const unsigned long long X = own ? (unsigned long long)__double2ull_rn((double)r.q * xsc) : 0ull;
-        double acc = 0.0;
+        double acc = H.n ? tr_hot_init(H, r.hm, X) : 0.0;
         double sv[2][4];
+        // (MR_TREXP: timing experiments only -- reads / atomics at conflict-free addresses)
+        auto ra = [&](uint32_t o) { return (MR_TREXP & 2) ? (uint32_t)(G.NA + lane) : o; };
+        auto aa = [&](uint32_t o) { return (MR_TREXP & 1) ? (uint32_t)(G.NA + lane) : o; };
         auto rd = [&](const u32x2 w, double* s) {
-            s[0] = su_l[w.x & 0xffffu];
-            s[1] = su_l[w.x >> 16];
-            s[2] = su_l[w.y & 0xffffu];
-            s[3] = su_l[w.y >> 16];
+            s[0] = su_l[ra(w.x & 0xffffu)];
+            s[1] = su_l[ra(w.x >> 16)];
+            s[2] = su_l[ra(w.y & 0xffffu)];
+            s[3] = su_l[ra(w.y >> 16)];
         };
         rd(r.id[0], sv[0]);
 #pragma unroll
         for (int j = 0; j < NC; ++j) {
-            if (j >= nn) break;
-            if (j + 1 < NC && j + 1 < nn) rd(r.id[j + 1], sv[(j + 1) & 1]);
+            if (j + 1 < NC) rd(r.id[j + 1], sv[(j + 1) & 1]);
             const u32x2 w = r.id[j];
-            atomicAdd(&lacc[w.x & 0xffffu], X);
-            atomicAdd(&lacc[w.x >> 16], X);
-            atomicAdd(&lacc[w.y & 0xffffu], X);
-            atomicAdd(&lacc[w.y >> 16], X);
+            atomicAdd(&lacc[aa(w.x & 0xffffu)], X);
+            atomicAdd(&lacc[aa(w.x >> 16)], X);
+            atomicAdd(&lacc[aa(w.y & 0xffffu)], X);
+            atomicAdd(&lacc[aa(w.y >> 16)], X);
 #pragma unroll
             for (int i = 0; i < 4; ++i) acc += sv[j & 1][i];
         }
@@ -1678,13 +1858,13 @@ __device__ __forceinline__ int32_t tr_walk_short(const GDev& G, int32_t k, const
         int32_t c0B = __builtin_amdgcn_readfirstlane(A.cw);
         int32_t nB = __builtin_amdgcn_readlane(A.cw, 1) - c0B;
         load(B, k + 1, c0B);
-        run(A, k, nA);
-        if (++k == ke || nB > NC) break;
+        run(A, k);
+        if (++k == ke || nB != NC) break;
         int32_t c0A = __builtin_amdgcn_readfirstlane(B.cw);
         nA = __builtin_amdgcn_readlane(B.cw, 1) - c0A;
         load(A, k + 1, c0A);
-        run(B, k, nB);
-        if (++k == ke || nA > NC) break;
+        run(B, k);
+        if (++k == ke || nA != NC) break;
     }
     return k;
 }
@@ -1692,9 +1872,10 @@ __device__ __forceinline__ int32_t tr_walk_short(const GDev& G, int32_t k, const
 // The wave's walk of k_tr_a over its run of wave tiles (shared with k_pr_cluster): per entry one
 // su read, one add into the lane's trace sum, one LDS u64 atomic of X_t; per tile r' of its traces
 // and their next q.  Returns the wave's largest r' (-inf when it owns no trace).
-template <class Q, int SUM, int NT, int EXT = 0>
+template <class Q, int SUM, int NT, int EXT = 0, bool HOTT = false>
 __device__ __forceinline__ double tr_walk(const GDev& G, int32_t lb, int cur, int nxt, int32_t N, int32_t NH, double d,
-                                          double Ms, double xsc, const double* su_l, unsigned long long* lacc) {
+                                          double Ms, double xsc, const double* su_l, unsigned long long* lacc,
+                                          const double* hs = nullptr) {
     constexpr bool SUL = SUM == WV_SU_ALL, HOT = SUM == WV_SU_HOT;
     constexpr int NW = NT / WAVE;
     const int32_t T = G.T;
@@ -1711,12 +1892,20 @@ __device__ __forceinline__ double tr_walk(const GDev& G, int32_t lb, int cur, in
     int32_t k = __builtin_amdgcn_readfirstlane(wt[0]);
     const int32_t ke = __builtin_amdgcn_readfirstlane(wt[1]);
     double rmax = -__builtin_huge_val();
-    if constexpr (SUL && !(MR_TREXP & 3)) {
-        if (k < ke && !(MR_TRSHORT & 1)) k = tr_walk_short<Q, 1, EXT>(G, k, ke, T, lane, cur, nxt, d, Ms, xsc, su_l, lacc, rmax);
-        if (k < ke && !(MR_TRSHORT & 2)) k = tr_walk_short<Q, 2, EXT>(G, k, ke, T, lane, cur, nxt, d, Ms, xsc, su_l, lacc, rmax);
-        if (k < ke && !(MR_TRSHORT & 4)) k = tr_walk_short<Q, 4, EXT>(G, k, ke, T, lane, cur, nxt, d, Ms, xsc, su_l, lacc, rmax);
-        if (k < ke && !(MR_TRSHORT & 8)) k = tr_walk_short<Q, 8, EXT>(G, k, ke, T, lane, cur, nxt, d, Ms, xsc, su_l, lacc, rmax);
+    TrHot H;
+    H.n = SUL && HOTT ? __builtin_amdgcn_readfirstlane(G.nhr) : 0;   // (the host strips only such graphs)
+    H.hs = hs;
+#pragma unroll
+    for (int h = 0; h < HOT_MAX; ++h) H.acc[h] = 0ull;
+    const int32_t k_first = k;
+    if constexpr (SUL) {
+        // one tier per chunk count (the run's tiles ascend in it): every count static, no branch
+        // inside a tile, so each wait is for exactly the LDS reads and loads it consumes
+#define TR_TIER(NC_) if (NC_ <= (NT == 1024 ? 8 : MR_TR_TIERS512) && k < ke) k = tr_walk_short<Q, NC_, EXT>(G, k, ke, T, lane, cur, nxt, d, Ms, xsc, su_l, lacc, rmax, H);
+        TR_TIER(1) TR_TIER(2) TR_TIER(3) TR_TIER(4) TR_TIER(5) TR_TIER(6) TR_TIER(7) TR_TIER(8)
+#undef TR_TIER
     }
+    const GLB uint8_t* hmk = gp(G.hmask);
     if (k < ke) {
         auto pos = [&](int32_t kk) { return min(kk * WAVE + lane, T - 1); };
         // cold-op su of a chunk (LDS-resident ops load sug[0]: one line, no traffic; pads read as 0)
@@ -1766,7 +1955,7 @@ __device__ __forceinline__ double tr_walk(const GDev& G, int32_t lb, int cur, in
         if (!SUL) gather(wa, gA);
         if (SUL || HOT) lds_su(wa, sA);
         unsigned long long X = k * WAVE + lane < T ? (unsigned long long)__double2ull_rn(q_cur * xsc) : 0ull;
-        double acc = 0.0;
+        double acc = H.n ? tr_hot_init(H, hmk[pos(k)], X) : 0.0;
         // One chunk: ids CUR (here), su SC / GC (LDS here, cold gathers in flight); NXT's cold
         // gathers and LDS reads go out before CUR's atomics (their latency, bank conflicts
         // included, overlaps a whole chunk), and the ids three chunks ahead land in LD.  The loop
@@ -1799,7 +1988,7 @@ __device__ __forceinline__ double tr_walk(const GDev& G, int32_t lb, int cur, in
                 q_nx = (double)qc[pos(kk_)];                                                               \
                 ce_nx = coff[min(kk_ + 1 + lane, ke)];                                                     \
                 X = p_ + WAVE < T ? (unsigned long long)__double2ull_rn(q_cur * xsc) : 0ull;               \
-                acc = 0.0;                                                                                 \
+                acc = H.n ? tr_hot_init(H, hmk[pos(k)], X) : 0.0;                                          \
             }                                                                                              \
         }
         for (;;) {
@@ -1811,6 +2000,16 @@ __device__ __forceinline__ double tr_walk(const GDev& G, int32_t lb, int cur, in
 #undef TR_STEP
     tr_done:;
     }
+    // the hot ops' accumulators: a wave sum each (integers), one LDS add
+    if (k_first < ke)
+#pragma unroll
+        for (int h = 0; h < HOT_MAX; ++h)
+            if (h < H.n) {
+                unsigned long long a = H.acc[h];
+#pragma unroll
+                for (int m = WAVE / 2; m >= 1; m >>= 1) a += (unsigned long long)__shfl_xor((long long)a, m, WAVE);
+                if (lane == 0) atomicAdd(&lacc[G.hop[h]], a);
+            }
     return rmax;
 }
 
@@ -1851,8 +2050,15 @@ __global__ void __launch_bounds__(NT) k_tr_a(const GDev* __restrict__ gs, int32_
         }
     }
     __syncthreads();   // accumulator and maxima ready
+    // hot ops (large graphs: the 1024-thread variant only) -- the mask sums of this iteration's su
+    constexpr bool HOTT = SUL && NT == 1024;
+    double* hs = (double*)(lraw + L_.hs);
+    if (HOTT && L_.hot_ok && G.nhr) {
+        tr_hot_sums(G, su_l, hs, tid);
+        __syncthreads();
+    }
     const double xsc = (G.dscale ? G.dscale[0] : G.fx_scale) / msh[1], Ms = msh[0];
-    const double rmax_w = tr_walk<Q, SUM, NT, EXT>(G, lb, cur, nxt, N, NH, d, Ms, xsc, su_l, lacc);
+    const double rmax_w = tr_walk<Q, SUM, NT, EXT, HOTT>(G, lb, cur, nxt, N, NH, d, Ms, xsc, su_l, lacc, hs);
     // (the call-graph term alpha P_ss s_k is k_fx_b's: a wave per op)
     __syncthreads();
     GLB unsigned long long* prow = gpw(G.fx_part) + (size_t)lb * N;
@@ -2025,11 +2231,6 @@ struct PcLds {
         total = spw + up((size_t)N * 4);
     }
 };
-__device__ __forceinline__ double uni_d(double v) {   // a block-uniform double into SGPRs
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_readfirstlane((int)(unsigned)b), hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
-    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-}
 template <class Q, int NT>
 __global__ void __launch_bounds__(NT) k_pr_cluster(const GDev* __restrict__ gs, int32_t ng, double d, int iters) {
     constexpr int NW = NT / WAVE;
@@ -2491,8 +2692,11 @@ static FxPlan fx_plan(mr_graph* const* gs, int ng) {
             nmax = std::max(nmax, kern_n(gs[i]));
             tmax = std::max<int64_t>(tmax, gs[i]->T);
         }
-    // 1024-thread blocks when the largest graph has a wave tile for every wave of the chip
+    // 1024-thread blocks when the largest graph has a wave tile for every wave of the chip (and
+    // always for graphs with register-accumulated hot ops: only that variant carries them)
     P.NT = cdiv(tmax, WAVE) >= (int64_t)num_cus() * 16 ? 1024 : 512;
+    for (int i = 0; i < ng; ++i)
+        if (gs[i]->fused && gs[i]->nhr) P.NT = 1024;
     bool relabeled = false;
     for (int i = 0; i < ng; ++i) relabeled = relabeled || (gs[i]->fused && gs[i]->relabeled);
     P.sul = TrLds(nmax, WV_SU_ALL).su_lds;
@@ -2533,6 +2737,19 @@ static double tr_budget() {
     }();
     return v;
 }
+// a tile's fixed cost in chunks for the per-wave cut: its q / r words and r' (about two chunks),
+// plus the hot-op accumulators and mask sum on hot-op layouts (MR_TR_TILEW / MR_TR_TILEW_HOT)
+static double tr_tile_weight(const mr_graph* g) {
+    static const double w0 = [] {
+        const char* e = getenv("MR_TR_TILEW");
+        return e ? atof(e) : 2.0;
+    }();
+    static const double wh = [] {
+        const char* e = getenv("MR_TR_TILEW_HOT");
+        return e ? atof(e) : 3.0;
+    }();
+    return g->nhr ? wh : w0;
+}
 static int tr_split(mr_ctx* ctx, mr_graph* g, const FxPlan& P, int64_t wsum, int64_t* nfa,
                     std::vector<CutArg>* defer = nullptr, int64_t force_nb = 0) {
     const int64_t W = g->n_wt, NW = P.NT / WAVE;
@@ -2552,10 +2769,11 @@ static int tr_split(mr_ctx* ctx, mr_graph* g, const FxPlan& P, int64_t wsum, int
             MR_TRY(g->wtile.alloc(ctx, (size_t)nw + 1));
             MR_TRY(g->dscale.alloc(ctx, 2));
             if (defer) {   // launched with the batch's other cuts (k_tr_cut_b)
-                defer->push_back(CutArg{g->coff.p, g->wtile.p, g->dscale.p, (int32_t)W, (int32_t)nw, (int32_t)NW, 0});
+                defer->push_back(CutArg{g->coff.p, g->wtile.p, g->dscale.p, (int32_t)W, (int32_t)nw, (int32_t)NW,
+                                        (float)tr_tile_weight(g)});
             } else {
                 hipLaunchKernelGGL(k_tr_cut, dim3(1), dim3(TC_T), 0, ctx->stream, g->coff.p, (int32_t)W, (int32_t)nw,
-                                   (int32_t)NW, g->wtile.p, g->dscale.p);
+                                   (int32_t)NW, g->wtile.p, g->dscale.p, tr_tile_weight(g));
                 MR_TRY_HIP(ctx, hipGetLastError());
             }
             g->wtile_nw = (int32_t)nw;
@@ -2574,11 +2792,12 @@ static int tr_split(mr_ctx* ctx, mr_graph* g, const FxPlan& P, int64_t wsum, int
         const int64_t nw = nb * NW;
         if (g->wtile.p && g->wtile_nw == nw && g->wtile_msum >= 0) break;
         std::vector<int32_t> cut((size_t)nw + 1);
-        const double total = W ? (double)co[(size_t)W] + 2.0 * (double)W : 0.0;
+        const double tw = tr_tile_weight(g);
+        const double total = W ? (double)co[(size_t)W] + tw * (double)W : 0.0;
         int64_t k = 0;
         for (int64_t i = 0; i <= nw; ++i) {   // first tile whose cost prefix reaches the target
             const double target = total * (double)i / (double)nw;
-            while (k < W && (double)co[(size_t)k] + 2.0 * (double)k < target) ++k;
+            while (k < W && (double)co[(size_t)k] + tw * (double)k < target) ++k;
             cut[(size_t)i] = (int32_t)k;
         }
         cut[(size_t)nw] = (int32_t)W;
@@ -2647,7 +2866,7 @@ static std::vector<int64_t> pc_plan(mr_ctx* ctx, mr_graph* const* gs, int ng, co
     size_t lds = 0;
     for (int i = 0; i < ng; ++i) {
         const mr_graph* g = gs[i];
-        if (!g->fused || g->wide || g->relabeled || !g->tile_mult_h.empty() || g->n_wt == 0) return nb;
+        if (!g->fused || g->wide || g->relabeled || !g->tile_mult_h.empty() || g->n_wt == 0 || g->nhr) return nb;
         lds = std::max(lds, PcLds(g->N, g->E).total);
     }
     if (lds > PC_LDS_MAX) return nb;
@@ -2684,10 +2903,73 @@ static std::vector<int64_t> pc_plan(mr_ctx* ctx, mr_graph* const* gs, int ng, co
 // chunk count sizes the id array; the chunk offsets stay on the host for the per-wave cut).
 // off / ids: the trace-major incidence the kernel walks (rs_off with rs16 / rsp, or a wide graph's
 // hot entries), N: the kernel's op count (pads N + lane)
+// hot ops stripped from the id chunks (register-accumulated in k_tr_a): MR_TR_HOT ops (default
+// HOT_MAX, 0 = none) covering at least 1/8 of the traces, on graphs of >= MR_TR_HOT_MIN traces
+// (default 2^20: window graphs keep their layout) whose su fits in LDS
+static int hot_strip(mr_ctx* ctx, mr_graph* g, const int64_t*& off, const uint16_t*& src, int32_t N, int64_t& nent,
+                     DBuf<int64_t>& roff, DBuf<uint16_t>& rids, DBuf<uint8_t>& mask) {
+    // (read per preparation: tests flip them)
+    const char* eh = getenv("MR_TR_HOT");
+    const char* em = getenv("MR_TR_HOT_MIN");
+    const int hmax = eh ? std::min(std::max(atoi(eh), 0), HOT_MAX) : HOT_MAX;
+    const int64_t tmin = em ? (int64_t)atoll(em) : (int64_t)1 << 20;
+    g->nhr = 0;
+    g->hmask.reset();
+    const int32_t T = g->T;
+    if (hmax == 0 || (int64_t)T < tmin || N < 1 || N > 16384 || !TrLds(N, WV_SU_ALL).hot_ok) return MR_OK;
+    hipStream_t st = ctx->stream;
+    std::vector<int32_t> cov((size_t)N);
+    {
+        DBuf<int32_t> dc;
+        MR_TRY(dc.zero(ctx, (size_t)N));
+        if (nent)
+            hipLaunchKernelGGL(k_cov_hist, dim3(cdiv(nent, 256 * 64)), dim3(256), (size_t)N * sizeof(int32_t), st, src,
+                               nent, N, dc.p);
+        MR_TRY(dc.download(ctx, cov.data(), (size_t)N));
+        MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+    }
+    std::vector<int32_t> ord((size_t)N);
+    for (int32_t o = 0; o < N; ++o) ord[(size_t)o] = o;
+    std::stable_sort(ord.begin(), ord.end(), [&](int32_t a, int32_t b) { return cov[(size_t)a] > cov[(size_t)b]; });
+    std::vector<int8_t> hidx((size_t)N, (int8_t)-1);
+    int nh = 0;
+    for (; nh < hmax && nh < N && (int64_t)cov[(size_t)ord[(size_t)nh]] * 8 >= (int64_t)T; ++nh) {
+        hidx[(size_t)ord[(size_t)nh]] = (int8_t)nh;
+        g->hop[nh] = ord[(size_t)nh];
+    }
+    if (nh == 0) return MR_OK;
+    DBuf<int8_t> dh;
+    DBuf<int32_t> rlen;
+    DBuf<int64_t> tmp;
+    MR_TRY(dh.upload(ctx, hidx.data(), hidx.size()));
+    MR_TRY(rlen.alloc(ctx, (size_t)T));
+    MR_TRY(mask.alloc(ctx, (size_t)T));
+    MR_TRY(roff.alloc(ctx, (size_t)T + 1));
+    MR_TRY(tmp.alloc(ctx, (size_t)scan_tmp_elems(T)));
+    hipLaunchKernelGGL(k_hot_count, dim3(cdiv(T, 256)), dim3(256), (size_t)N, st, off, src, T, dh.p, N, rlen.p, mask.p);
+    MR_TRY(mr_exclusive_scan_i32(ctx, rlen.p, roff.p, T, tmp.p));
+    int64_t n2 = 0;
+    MR_TRY_HIP(ctx, hipMemcpyAsync(&n2, roff.p + T, sizeof n2, hipMemcpyDeviceToHost, st));
+    MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+    MR_TRY(rids.alloc(ctx, (size_t)std::max<int64_t>(n2, 1) + 8));
+    hipLaunchKernelGGL(k_hot_fill, dim3(cdiv(T, 256)), dim3(256), (size_t)N, st, off, src, T, dh.p, N, mask.p, roff.p, rids.p);
+    MR_TRY_HIP(ctx, hipGetLastError());
+    MR_TRY_HIP(ctx, hipStreamSynchronize(st));   // (dh, rlen, tmp leave scope)
+    g->nhr = nh;
+    off = roff.p;
+    src = rids.p;
+    nent = n2;
+    return MR_OK;
+}
+
 static int tr_layout(mr_ctx* ctx, mr_graph* g, const int64_t* off, const uint16_t* src, int32_t N, int64_t nent,
                      int32_t* zeroed) {
     hipStream_t st = ctx->stream;
     const int32_t T = g->T;
+    DBuf<int64_t> roff;
+    DBuf<uint16_t> rids;
+    DBuf<uint8_t> hm;
+    MR_TRY(hot_strip(ctx, g, off, src, N, nent, roff, rids, hm));
     const int32_t W = cdiv(T, WAVE);
     g->n_wt = W;
     g->wtile_nw = 0;
@@ -2738,6 +3020,13 @@ static int tr_layout(mr_ctx* ctx, mr_graph* g, const int64_t* off, const uint16_
     if (W)
         hipLaunchKernelGGL(k_tr_fill, dim3(cdiv((int64_t)W * WAVE, 256)), dim3(256), 0, st, g->tperm.p, off, src,
                            c64.p, T, N, W, g->tids.p);
+    if (W && tr_sched_on())
+        hipLaunchKernelGGL(k_tr_sched, dim3(cdiv(2 * (int64_t)W, SCHED_T)), dim3(SCHED_T), 0, st, g->coff.p, W, g->tids.p);
+    if (g->nhr) {   // the hot-op bits in position order
+        MR_TRY(g->hmask.alloc(ctx, (size_t)T));
+        hipLaunchKernelGGL(k_hot_perm, dim3(cdiv(T, 256)), dim3(256), 0, st, g->tperm.p, hm.p, T, g->hmask.p);
+        MR_TRY_HIP(ctx, hipStreamSynchronize(st));   // (the stripped lists leave scope)
+    }
     MR_TRY_HIP(ctx, hipGetLastError());
     return MR_OK;   // (scratch returns to the stream-ordered pool)
 }
@@ -2873,6 +3162,10 @@ int mr_graph_prepare_batch(mr_ctx* ctx, mr_graph* const* gs, int n, std::vector<
     if (!ok) {
         for (int i = 0; i < n; ++i) MR_TRY(mr_graph_prepare(ctx, gs[i]));
         return MR_OK;
+    }
+    for (int i = 0; i < n; ++i) {   // (the batched layout keeps every op in the id chunks)
+        gs[i]->nhr = 0;
+        gs[i]->hmask.reset();
     }
     hipStream_t st = ctx->stream;
     keep.assign((size_t)n * sizeof(PDev), 0);
@@ -3487,6 +3780,9 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         v.c_tp = g->c_tp.p;
         v.w_tp = g->w_tp.p;
         v.mw_tp = g->mw_tp.p;
+        v.hmask = g->nhr ? g->hmask.p : nullptr;
+        v.nhr = g->fused ? g->nhr : 0;
+        for (int h = 0; h < 8; ++h) v.hop[h] = g->hop[h];
         v.c_t = g->c_t.p;
         v.w_t = g->w_t.p;
         v.u_o = g->u_o.p;
@@ -3586,6 +3882,10 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
     const int32_t split_fa = ng == 2 ? hv[1].blk0f : 0, split_fb = ng == 2 ? hv[1].blk0fb : 0;
     for (int i = 0; i < ng; ++i)
         if (gs[i]->fused) lds_f = std::max(lds_f, plan_lds(kern_n(gs[i]), plan));
+    for (int i = 0; i < ng; ++i)   // hot-op layouts need every op's su in LDS (a batch with a much wider graph)
+        if (gs[i]->fused && gs[i]->nhr && plan.mode != WV_SU_ALL)
+            return mr_fail(ctx, MR_ERR_ARG, "pagerank batch: a hot-op layout (T >= MR_TR_HOT_MIN) with a graph of > %d ops",
+                           (int)WIDE_NA);
     bool any_ext = false;   // kind multiplicities or cold sums in some fused graph of the launch
     for (int i = 0; i < ng; ++i) any_ext = any_ext || (gs[i]->fused && (hv[(size_t)i].mw_tp || hv[(size_t)i].cold_acc));
     const TrA tr_a = tr_kernel(fp32, plan.mode, plan.NT, any_ext);

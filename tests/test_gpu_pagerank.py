@@ -481,3 +481,82 @@ def test_persistent_iteration_equals_split_launches(c2, tpw, monkeypatch):
         w_ref, _ = orc.weights(g, s)
         np.testing.assert_allclose(out[("1", anomaly)], np.array(list(w_ref.values())), rtol=RTOL64, atol=0)
     dg.close()
+
+
+def _with_hot_only_traces(hg, hot, seed):
+    """Append traces made of hot ops only (1..len(hot) of them): with the hot ops stripped from the
+    id chunks such a trace keeps its first hot op in the list (no empty traces)."""
+    from microrank_amd.graph import HostGraph
+
+    rng = np.random.default_rng(seed)
+    ops = [np.sort(rng.choice(hot, k, replace=False)) for k in range(1, len(hot) + 1) for _ in range(40)]
+    width = np.array([len(o) for o in ops])
+    flat = np.concatenate(ops).astype(np.int32)
+    sr_ops = np.concatenate([hg.sr_ops, flat])
+    sr_off = np.concatenate([hg.sr_off, hg.sr_off[-1] + np.cumsum(width).astype(np.int64)])
+    len_t = np.concatenate([hg.len_t, width.astype(np.int32)])
+    len_o = hg.len_o + np.bincount(flat, minlength=hg.N).astype(np.int32)
+    return HostGraph(range(hg.N), range(hg.T + len(ops)), sr_off, sr_ops, None, None, len_t, len_o, hg.ss_off,
+                     hg.ss_par, hg.nchild, None, None)
+
+
+@pytest.mark.parametrize("anomaly", [False, True])
+def test_hot_op_layout_against_oracle(anomaly, monkeypatch):
+    """Register-accumulated hot ops (the 8 most covered ops leave k_tr_a's id chunks; forced here
+    on a 300k-trace graph with MR_TR_HOT_MIN=0): short tiles, long tiles (60-op traces: the general
+    walk) and hot-only traces.  GPU vs oracle at 1e-10 (fp64) / 1e-4 (fp32), coverage exact, bitwise
+    reruns, and within 1e-12 of the layout without hot ops (only the summation order differs)."""
+    from microrank_amd import _lib, synth
+    from microrank_amd.graph import DeviceGraph
+
+    hg = _with_hot_only_traces(_with_long_traces(synth.big_graph(1000, 300_000, seed=21), 2000, 60, seed=22),
+                               np.arange(8), seed=23)
+    g = _oracle_graph_from_host(hg)
+    kind = orc.trace_kinds(g)
+    s = orc.power_iteration(g, orc.preference(g, kind, anomaly))
+    w_ref, cov_ref = orc.weights(g, s)
+    ctx = _lib.default_context()
+    res = {}
+    for hot in ("0", "8"):
+        monkeypatch.setenv("MR_TR_HOT", hot)
+        monkeypatch.setenv("MR_TR_HOT_MIN", "0")
+        dg = DeviceGraph.upload(ctx, hg)
+        dg.pagerank(anomaly)
+        w, cov = dg.fetch()
+        np.testing.assert_array_equal(cov, np.array(list(cov_ref.values())))
+        np.testing.assert_allclose(w, np.array(list(w_ref.values())), rtol=RTOL64, atol=0)
+        dg.pagerank(anomaly)
+        w2, _ = dg.fetch()
+        assert w2.tobytes() == w.tobytes(), "rerun not bitwise identical"
+        dg.pagerank(anomaly, precision="fp32")
+        w3, _ = dg.fetch()
+        np.testing.assert_allclose(w3, np.array(list(w_ref.values())), rtol=RTOL32, atol=0)
+        res[hot] = w
+        dg.close()
+    np.testing.assert_allclose(res["8"], res["0"], rtol=1e-12, atol=0)
+
+
+@pytest.mark.parametrize("precision", ["fp64", "fp32"])
+def test_wide_hot_op_layout_against_oracle(precision, monkeypatch):
+    """The wide path (N = 50000) with the hot ops of its LDS walk register-accumulated (forced with
+    MR_TR_HOT_MIN=0): GPU vs oracle, bitwise reruns."""
+    from microrank_amd import _lib, synth
+    from microrank_amd.graph import DeviceGraph
+
+    monkeypatch.setenv("MR_TR_HOT_MIN", "0")
+    hg = _with_cold_traces(synth.big_graph(50_000, 40_000, seed=9), 3000, 30_000, seed=10)
+    g = _oracle_graph_from_host(hg)
+    kind = orc.trace_kinds(g)
+    s = orc.power_iteration(g, orc.preference(g, kind, False))
+    w_ref, cov_ref = orc.weights(g, s)
+    ctx = _lib.default_context()
+    dg = DeviceGraph.upload(ctx, hg)
+    dg.pagerank(False, precision=precision)
+    w, cov = dg.fetch()
+    tol = RTOL64 if precision == "fp64" else 1e-4
+    np.testing.assert_array_equal(cov, np.array(list(cov_ref.values())))
+    np.testing.assert_allclose(w, np.array(list(w_ref.values())), rtol=tol, atol=0)
+    dg.pagerank(False, precision=precision)
+    w2, _ = dg.fetch()
+    assert w2.tobytes() == w.tobytes(), "rerun not bitwise identical"
+    dg.close()
