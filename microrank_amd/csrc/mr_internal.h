@@ -217,6 +217,13 @@ struct mr_graph {
     DBuf<int64_t> cb_beg;            // [n_cb+1] pair slice of each block
     DBuf<uint64_t> cold_part;        // [n_cb * cold_rw] partial rows of the cold ranges
     DBuf<double> cold_acc;           // [T] per position: sum of su over the trace's cold entries
+    // the short-tile walk takes each tile's cold entries itself (su gathered from L2): per wave
+    // tile ceil(max cold / 2) chunks of 64 lanes x 2 u32 op labels (pads N + lane), cold_acc only
+    // for the long tiles of the general walk and the tiles with more than two cold chunks (ctl)
+    DBuf<uint32_t> ctids;
+    DBuf<int32_t> ccoff;             // [n_wt+1] first cold chunk of a tile
+    DBuf<int32_t> ctl;               // [n_ctl] tiles whose cold sums k_cold_trace computes
+    int32_t n_ctl = 0;
     DBuf<double> mult, mw_tp;
     std::vector<int64_t> tile_mult_h;   // per wave tile: the multiplicity its traces stand for
     DBuf<int32_t> krep;              // [T] class representative of each trace (when allocated)

@@ -306,6 +306,46 @@ __global__ void k_wide_span(const int64_t* cb_beg, int32_t n_cb, const int32_t* 
     if (b1 > b0) atomicMax(span, (unsigned long long)(cp_pos[b1 - 1] - cp_pos[b0] + 1));
 }
 
+// Cold entries of the short-tile walk: per wave tile ceil(max cold of its traces / 2) chunks of
+// 64 lanes x 2 u32 labels, a lane's entries in cold_ops_p order (k_cold_trace's), pads N + lane
+// (a zero su slot).  Secondary sort key of the wide layout (cold count) keeps tiles homogeneous.
+__global__ void k_ctile_cnt(const int32_t* coff_p, int32_t T, int32_t W, int32_t* cnt) {
+    const int32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= W) return;
+    int32_t m = 0;
+    for (int32_t p = k * WAVE; p < min(k * WAVE + WAVE, T); ++p) m = max(m, coff_p[p + 1] - coff_p[p]);
+    cnt[k] = (m + 1) >> 1;
+}
+__global__ void k_ctile_fill(const int32_t* coff_p, const int32_t* cops, const int64_t* cc64, int32_t T, int32_t N,
+                             int32_t W, uint32_t* ctids) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)W * WAVE) return;
+    const int32_t k = (int32_t)(i / WAVE), lane = (int32_t)(i % WAVE);
+    const int32_t p = k * WAVE + lane;
+    const int32_t a = p < T ? coff_p[p] : 0, n = p < T ? coff_p[p + 1] - a : 0;
+    const int64_t c0 = cc64[k], nc = cc64[k + 1] - c0;
+    for (int64_t c = 0; c < nc; ++c)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int64_t e = 2 * c + q;
+            ctids[((size_t)(c0 + c) * WAVE + lane) * 2 + q] = e < n ? (uint32_t)cops[a + e] : (uint32_t)(N + lane);
+        }
+}
+// sort keys of a layout with a secondary key: (length << 4 | min(skey, 15)), the trace as value
+__global__ void k_tr_skey(const int64_t* off, const int32_t* skey, int32_t T, uint64_t* key, uint32_t* val) {
+    const int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= T) return;
+    key[t] = ((uint64_t)(off[t + 1] - off[t]) << 4) | (uint64_t)(skey ? min(skey[t], 15) : 0);
+    val[t] = (uint32_t)t;
+}
+__global__ void k_tr_perm_w(const uint32_t* val, const float* w_t, int32_t T, int32_t* tperm, float* w_tp) {
+    const int32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= T) return;
+    const int32_t t = (int32_t)val[p];
+    tperm[p] = t;
+    w_tp[p] = w_t[t];
+}
+
 // ---------------------------------------------------------------- trace-parallel layout (k_tr_a)
 // Traces by op count: a counting sort (lengths <= N <= FX_NMAX), order within a length free --
 // nothing numeric depends on it (a trace's ids are rotated by trace mod len, not by position;
@@ -556,6 +596,7 @@ __global__ void k_tr_fill(const int32_t* tperm, const int64_t* off, const uint16
 #ifndef MR_TR_TIERS512
 #define MR_TR_TIERS512 4   // short-tile tiers of the 512-thread k_tr_a (window graphs: occupancy)
 #endif
+constexpr int TR_TIERS_EXT = 8;   // short-tile tiers of the EXT (kind-compressed / wide) variants
 #ifndef MR_HOT_MAX
 #define MR_HOT_MAX 8
 #endif
@@ -1395,6 +1436,8 @@ struct GDev {
     const float* w_tp;
     const double* mw_tp;        // kind-compressed graphs: w_t * multiplicity (position order), else null
     const uint8_t* hmask;       // register-accumulated hot ops: trace bits in position order (nhr > 0)
+    const uint32_t* ctids;      // wide graphs: cold chunks of the short-tile walk ([chunk][lane] x 2 labels)
+    const int32_t* ccoff;       // [n_wt+1] first cold chunk of a tile
     int32_t nhr;
     int32_t hop[8];
     const float* c_t;
@@ -1742,7 +1785,9 @@ struct TrTile {
     float c;
     float w;
     double mw;     // EXT & 1: w times the kind multiplicity (kind-compressed graphs)
-    double x;      // EXT & 2: the cold half of the trace's su sum (wide graphs)
+    u32x2 cid[2];  // EXT & 2: the tile's first two cold chunks (wide graphs: 2 cold labels per lane each)
+    double xo;     // EXT & 2: k_cold_trace's sum when the tile has more cold chunks (else a dummy)
+    int32_t ccw;   // EXT & 2: lane j: ccoff[k + 1 + j] (the next tile's cold chunk range)
     int32_t cw;    // lane j: coff[k + 1 + j] (readlane 0 / 1: the next tile's chunk range)
     uint32_t hm;   // the trace's hot-op bits (nhr > 0)
 };
@@ -1751,16 +1796,19 @@ struct TrTile {
 // The su part is one LDS read of hs[hm] = the sum of the trace's hot su in h order (k_tr_a builds
 // the 256 sums per iteration: adding the absent ops' +0.0 would not change a sum, so hs[hm] is the
 // lane's own sequential sum over its hot ops).
+constexpr int HOT_MAX_WIDE = 4;   // wide graphs' k_tr_a variant (its cold registers): 4 accumulators
+template <int HN>
 struct TrHot {
     int32_t n;
     const double* hs;   // LDS [256]
-    unsigned long long acc[HOT_MAX];
+    unsigned long long acc[HN];
 };
 // (every one of the HOT_MAX accumulators is updated: ops past nhr are never in a mask, so they
 // add 0 -- no per-op condition, no duplicated registers)
-__device__ __forceinline__ double tr_hot_init(TrHot& H, uint32_t hm, unsigned long long X) {
+template <int HN>
+__device__ __forceinline__ double tr_hot_init(TrHot<HN>& H, uint32_t hm, unsigned long long X) {
 #pragma unroll
-    for (int h = 0; h < HOT_MAX; ++h) {
+    for (int h = 0; h < HN; ++h) {
         const unsigned long long sel = (unsigned long long)(long long)(((int32_t)(hm << (31 - h))) >> 31);
         H.acc[h] += X & sel;
     }
@@ -1775,10 +1823,10 @@ __device__ __forceinline__ void tr_hot_sums(const GDev& G, const double* su_l, d
         hs[tid] = a;
     }
 }
-template <class Q, int NC, int EXT>
+template <class Q, int NC, int EXT, int HN>
 __device__ __forceinline__ int32_t tr_walk_short(const GDev& G, int32_t k, const int32_t ke, int32_t T, int32_t lane,
                                                  int cur, int nxt, double d, double Ms, double xsc, const double* su_l,
-                                                 unsigned long long* lacc, double& rmax, TrHot& H) {
+                                                 unsigned long long* lacc, double& rmax, TrHot<HN>& H) {
     const GLB u32x2* ids = gp((const u32x2*)G.tids) + lane;
     const GLB int32_t* coff = gp(G.coff);
     const GLB Q* qc = gp((const Q*)G.q[cur]);
@@ -1790,7 +1838,12 @@ __device__ __forceinline__ int32_t tr_walk_short(const GDev& G, int32_t k, const
     const GLB double* sug = gp(G.sub[cur]);
     const bool kc = (EXT & 1) && G.mw_tp, cx = (EXT & 2) && G.cold_acc;
     const GLB double* mw_tp = kc ? gp(G.mw_tp) : sug;
-    const GLB double* cacc = cx ? gp(G.cold_acc) : sug;
+    // wide graphs: the cold entries' su gathered here (issued when a tile starts, summed when it
+    // ends: a tile of LDS work hides the L2 latency), no cold_acc pass for these tiles
+    const GLB u32x2* cids = gp((const u32x2*)G.ctids) + lane;
+    const GLB int32_t* ccoff = cx ? gp(G.ccoff) : coff;
+    const int32_t ccl = max(__builtin_amdgcn_readfirstlane(ccoff[ke]) - 1, 0);
+    const uint32_t cpad = (uint32_t)(G.N + lane);
     const bool hot = H.n > 0;
     const GLB uint8_t* hmk = hot ? gp(G.hmask) : (const GLB uint8_t*)coff;
     const int32_t cl = __builtin_amdgcn_readfirstlane(coff[ke]) - 1;   // the run's last chunk
@@ -1802,8 +1855,15 @@ __device__ __forceinline__ int32_t tr_walk_short(const GDev& G, int32_t k, const
         n = __builtin_amdgcn_readlane(v, 1) - c0;
     }
     if (n != NC) return k;
+    int32_t q0 = 0, nq = 0;   // the first tile's cold chunk range
+    if constexpr ((EXT & 2) != 0) {
+        const int32_t v = ccoff[min(k + lane, ke)];
+        q0 = __builtin_amdgcn_readfirstlane(v);
+        nq = __builtin_amdgcn_readlane(v, 1) - q0;
+    }
     using R = TrTile<Q, NC, EXT>;
-    auto load = [&](R& r, int32_t kk, int32_t cc0) {
+    const GLB double* cacc = cx ? gp(G.cold_acc) : sug;
+    auto load = [&](R& r, int32_t kk, int32_t cc0, int32_t qq0, int32_t nqq) {
         const int32_t kq = min(kk, ke - 1);
         const int32_t p = min(kq * WAVE + lane, T - 1);
 #pragma unroll
@@ -1812,14 +1872,29 @@ __device__ __forceinline__ int32_t tr_walk_short(const GDev& G, int32_t k, const
         r.c = c_tp[p];
         r.w = w_tp[p];
         if constexpr ((EXT & 1) != 0) r.mw = mw_tp[kc ? p : 0];
-        if constexpr ((EXT & 2) != 0) r.x = cacc[cx ? p : 0];
+        if constexpr ((EXT & 2) != 0) {
+            if (cx) {   // (uniform; ctids exists only on wide graphs)
+                r.cid[0] = cids[(size_t)min(qq0, ccl) * WAVE];
+                r.cid[1] = cids[(size_t)min(qq0 + 1, ccl) * WAVE];
+            }
+            r.xo = cacc[nqq > 2 ? p : 0];   // (unconditional: a branch here costs ~50 VGPRs)
+            r.ccw = ccoff[min(kq + 1 + lane, ke)];
+        }
         r.cw = coff[min(kq + 1 + lane, ke)];
         r.hm = hmk[hot ? p : 0];
     };
     // tile kk from r: lane = position kk * 64 + lane
-    auto run = [&](const R& r, int32_t kk) {
+    auto run = [&](const R& r, int32_t kk, int32_t qq0, int32_t nqq) {
         const int32_t p = kk * WAVE + lane;
         const bool own = p < T;
+        double cg[4] = {0.0, 0.0, 0.0, 0.0};
+        if constexpr ((EXT & 2) != 0)
+            if (cx) {   // the first two cold chunks' su (pads past the tile's chunk count: N + lane, 0)
+                cg[0] = sug[nqq > 0 ? r.cid[0].x : cpad];
+                cg[1] = sug[nqq > 0 ? r.cid[0].y : cpad];
+                cg[2] = sug[nqq > 1 ? r.cid[1].x : cpad];
+                cg[3] = sug[nqq > 1 ? r.cid[1].y : cpad];
+            }
         const unsigned long long X = own ? (unsigned long long)__double2ull_rn((double)r.q * xsc) : 0ull;
         double acc = H.n ? tr_hot_init(H, r.hm, X) : 0.0;
         double sv[2][4];
@@ -1844,26 +1919,41 @@ __device__ __forceinline__ int32_t tr_walk_short(const GDev& G, int32_t k, const
 #pragma unroll
             for (int i = 0; i < 4; ++i) acc += sv[j & 1][i];
         }
-        const double x = cx ? r.x : 0.0;
+        double x = 0.0;   // the cold half, sequential in the trace's cold order (k_cold_trace's)
+        if constexpr ((EXT & 2) != 0)
+            if (cx) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) x += cg[i];
+                if (nqq > 2) x = r.xo;   // (rare: > 4 cold entries in a trace of the tile: k_cold_trace's sum)
+            }
         const double rp = d * ((acc + x) / Ms) + (double)r.c;   // pagerank.py:125
         if (own) rmax = nmax(rmax, rp);
         const double wq = kc ? r.mw : (double)r.w;
         qn[own ? p : T] = (Q)(wq * rp);   // q[T]: pad slot
     };
     R A, B;
-    load(A, k, c0);
-    int32_t nA = n;
+    load(A, k, c0, q0, nq);
+    int32_t nA = n, qA = q0, nqA = nq;
     for (;;) {
-        // B = tile k + 1 (its range from A's offsets), then A's tile
-        int32_t c0B = __builtin_amdgcn_readfirstlane(A.cw);
-        int32_t nB = __builtin_amdgcn_readlane(A.cw, 1) - c0B;
-        load(B, k + 1, c0B);
-        run(A, k);
+        // B = tile k + 1 (its ranges from A's offsets), then A's tile
+        const int32_t c0B = __builtin_amdgcn_readfirstlane(A.cw);
+        const int32_t nB = __builtin_amdgcn_readlane(A.cw, 1) - c0B;
+        int32_t qB = 0, nqB = 0;
+        if constexpr ((EXT & 2) != 0) {
+            qB = __builtin_amdgcn_readfirstlane(A.ccw);
+            nqB = __builtin_amdgcn_readlane(A.ccw, 1) - qB;
+        }
+        load(B, k + 1, c0B, qB, nqB);
+        run(A, k, qA, nqA);
         if (++k == ke || nB != NC) break;
-        int32_t c0A = __builtin_amdgcn_readfirstlane(B.cw);
+        const int32_t c0A = __builtin_amdgcn_readfirstlane(B.cw);
         nA = __builtin_amdgcn_readlane(B.cw, 1) - c0A;
-        load(A, k + 1, c0A);
-        run(B, k);
+        if constexpr ((EXT & 2) != 0) {
+            qA = __builtin_amdgcn_readfirstlane(B.ccw);
+            nqA = __builtin_amdgcn_readlane(B.ccw, 1) - qA;
+        }
+        load(A, k + 1, c0A, qA, nqA);
+        run(B, k, qB, nqB);
         if (++k == ke || nA != NC) break;
     }
     return k;
@@ -1892,16 +1982,17 @@ __device__ __forceinline__ double tr_walk(const GDev& G, int32_t lb, int cur, in
     int32_t k = __builtin_amdgcn_readfirstlane(wt[0]);
     const int32_t ke = __builtin_amdgcn_readfirstlane(wt[1]);
     double rmax = -__builtin_huge_val();
-    TrHot H;
+    constexpr int HN = (EXT & 2) ? HOT_MAX_WIDE : HOT_MAX;
+    TrHot<HN> H;
     H.n = SUL && HOTT ? __builtin_amdgcn_readfirstlane(G.nhr) : 0;   // (the host strips only such graphs)
     H.hs = hs;
 #pragma unroll
-    for (int h = 0; h < HOT_MAX; ++h) H.acc[h] = 0ull;
+    for (int h = 0; h < HN; ++h) H.acc[h] = 0ull;
     const int32_t k_first = k;
     if constexpr (SUL) {
         // one tier per chunk count (the run's tiles ascend in it): every count static, no branch
         // inside a tile, so each wait is for exactly the LDS reads and loads it consumes
-#define TR_TIER(NC_) if (NC_ <= (NT == 1024 ? 8 : MR_TR_TIERS512) && k < ke) k = tr_walk_short<Q, NC_, EXT>(G, k, ke, T, lane, cur, nxt, d, Ms, xsc, su_l, lacc, rmax, H);
+#define TR_TIER(NC_) if (NC_ <= (NT == 1024 || EXT ? TR_TIERS_EXT : MR_TR_TIERS512) && k < ke) k = tr_walk_short<Q, NC_, EXT, HN>(G, k, ke, T, lane, cur, nxt, d, Ms, xsc, su_l, lacc, rmax, H);
         TR_TIER(1) TR_TIER(2) TR_TIER(3) TR_TIER(4) TR_TIER(5) TR_TIER(6) TR_TIER(7) TR_TIER(8)
 #undef TR_TIER
     }
@@ -2003,7 +2094,7 @@ __device__ __forceinline__ double tr_walk(const GDev& G, int32_t lb, int cur, in
     // the hot ops' accumulators: a wave sum each (integers), one LDS add
     if (k_first < ke)
 #pragma unroll
-        for (int h = 0; h < HOT_MAX; ++h)
+        for (int h = 0; h < HN; ++h)
             if (h < H.n) {
                 unsigned long long a = H.acc[h];
 #pragma unroll
@@ -2370,9 +2461,14 @@ __global__ void __launch_bounds__(NT) k_pr_cluster(const GDev* __restrict__ gs, 
 // ---- wide fused graphs, per iteration, before k_tr_a
 // cold half of each trace's su sum (pagerank.py:125), in position order: k_tr_a adds it to the
 // lane's hot sum before the division by M_s(k)
+// (over the listed wave tiles only: the long tiles of the general walk and the short tiles with
+// more than two cold chunks -- the short-tile walk gathers the rest itself)
 __global__ void k_cold_trace(const int32_t* __restrict__ coff, const int32_t* __restrict__ cops,
-                             const double* __restrict__ su, int32_t T, double* __restrict__ cacc) {
-    const int32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+                             const double* __restrict__ su, const int32_t* __restrict__ tiles, int32_t ntl, int32_t T,
+                             double* __restrict__ cacc) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)ntl * WAVE) return;
+    const int32_t p = tiles[i / WAVE] * WAVE + (int32_t)(i % WAVE);
     if (p >= T) return;
     const int32_t a = coff[p], b = coff[p + 1];
     double acc = 0.0;
@@ -2649,9 +2745,9 @@ void mr_prof_begin(mr_ctx* ctx);
 void mr_prof_end(mr_ctx* ctx, double bytes, int64_t iters = 1);
 
 using TrA = void (*)(const GDev*, int32_t, int32_t, double, double, int, int32_t);
-// ext: some graph of the launch carries kind multiplicities (mw_tp) or cold sums (cold_acc) --
-// only the short-tile walk of the su-in-LDS mode distinguishes it
-static TrA tr_kernel(bool fp32, int mode, int NT, bool ext = false) {
+// ext: some graph of the launch carries kind multiplicities (bit 0: mw_tp) or a cold side (bit 1:
+// wide graphs) -- only the short-tile walk of the su-in-LDS mode distinguishes them
+static TrA tr_kernel(bool fp32, int mode, int NT, int ext = 0) {
     static const TrA tab[2][3][2] = {
         {{k_tr_a<double, 0, 512, 0>, k_tr_a<double, 0, 1024, 0>},
          {k_tr_a<double, 1, 512, 0>, k_tr_a<double, 1, 1024, 0>},
@@ -2659,9 +2755,11 @@ static TrA tr_kernel(bool fp32, int mode, int NT, bool ext = false) {
         {{k_tr_a<float, 0, 512, 0>, k_tr_a<float, 0, 1024, 0>},
          {k_tr_a<float, 1, 512, 0>, k_tr_a<float, 1, 1024, 0>},
          {k_tr_a<float, 2, 512, 0>, k_tr_a<float, 2, 1024, 0>}}};
-    static const TrA tab_ext[2][2] = {{k_tr_a<double, 1, 512, 3>, k_tr_a<double, 1, 1024, 3>},
-                                      {k_tr_a<float, 1, 512, 3>, k_tr_a<float, 1, 1024, 3>}};
-    if (ext && mode == WV_SU_ALL) return tab_ext[fp32 ? 1 : 0][NT == 1024 ? 1 : 0];
+    static const TrA tab_ext[3][2][2] = {
+        {{k_tr_a<double, 1, 512, 1>, k_tr_a<double, 1, 1024, 1>}, {k_tr_a<float, 1, 512, 1>, k_tr_a<float, 1, 1024, 1>}},
+        {{k_tr_a<double, 1, 512, 2>, k_tr_a<double, 1, 1024, 2>}, {k_tr_a<float, 1, 512, 2>, k_tr_a<float, 1, 1024, 2>}},
+        {{k_tr_a<double, 1, 512, 3>, k_tr_a<double, 1, 1024, 3>}, {k_tr_a<float, 1, 512, 3>, k_tr_a<float, 1, 1024, 3>}}};
+    if (ext && mode == WV_SU_ALL) return tab_ext[ext - 1][fp32 ? 1 : 0][NT == 1024 ? 1 : 0];
     return tab[fp32 ? 1 : 0][mode][NT == 1024 ? 1 : 0];
 }
 static int num_cus() {
@@ -2911,7 +3009,8 @@ static int hot_strip(mr_ctx* ctx, mr_graph* g, const int64_t*& off, const uint16
     // (read per preparation: tests flip them)
     const char* eh = getenv("MR_TR_HOT");
     const char* em = getenv("MR_TR_HOT_MIN");
-    const int hmax = eh ? std::min(std::max(atoi(eh), 0), HOT_MAX) : HOT_MAX;
+    const int hcap = g->wide ? HOT_MAX_WIDE : HOT_MAX;   // (the wide variant carries fewer accumulators)
+    const int hmax = eh ? std::min(std::max(atoi(eh), 0), hcap) : hcap;
     const int64_t tmin = em ? (int64_t)atoll(em) : (int64_t)1 << 20;
     g->nhr = 0;
     g->hmask.reset();
@@ -2963,7 +3062,7 @@ static int hot_strip(mr_ctx* ctx, mr_graph* g, const int64_t*& off, const uint16
 }
 
 static int tr_layout(mr_ctx* ctx, mr_graph* g, const int64_t* off, const uint16_t* src, int32_t N, int64_t nent,
-                     int32_t* zeroed) {
+                     int32_t* zeroed, const int32_t* skey = nullptr) {
     hipStream_t st = ctx->stream;
     const int32_t T = g->T;
     DBuf<int64_t> roff;
@@ -2988,7 +3087,22 @@ static int tr_layout(mr_ctx* ctx, mr_graph* g, const int64_t* off, const uint16_
     MR_TRY(g->tperm.alloc(ctx, (size_t)std::max(T, 1)));
     MR_TRY(g->w_tp.alloc(ctx, (size_t)std::max(T, 1)));
     MR_TRY(g->coff.alloc(ctx, (size_t)W + 1));
-    if (T) {
+    // (length, secondary key): a stable radix sort, equal keys in trace order -- for wide graphs (the
+    // cold count as secondary key) and kind-compressed ones, whose fixed-point scale depends on
+    // the tiles' multiplicity sums (the counting sort below orders equal lengths run-dependently)
+    if (T && (skey || g->kinds_given)) {
+        DBuf<uint64_t> key;
+        DBuf<uint32_t> val;
+        MR_TRY(key.alloc(ctx, (size_t)T));
+        MR_TRY(val.alloc(ctx, (size_t)T));
+        hipLaunchKernelGGL(k_tr_skey, dim3(cdiv(T, 256)), dim3(256), 0, st, off, skey, T, key.p, val.p);
+        {
+            SortScratch ws;
+            MR_TRY(mr_radix_sort(ctx, key.p, val.p, T, bits_for((uint64_t)N) + 4, ws));
+        }
+        hipLaunchKernelGGL(k_tr_perm_w, dim3(cdiv(T, 256)), dim3(256), 0, st, val.p, g->w_t.p, T, g->tperm.p, g->w_tp.p);
+        MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+    } else if (T) {
         const bool big = (int64_t)T >= (int64_t)num_cus() * TRB * TR_PER_SMALL * 4;
         const int per = big ? TR_PER_BIG : TR_PER_SMALL;
         const int nb = cdiv(T, (int64_t)TRB * per);
@@ -3076,7 +3190,7 @@ static int wide_prepare(mr_ctx* ctx, mr_graph* g) {
     MR_TRY(g->hot16.alloc(ctx, (size_t)n_hot + 8));
     hipLaunchKernelGGL(k_wide_hot, dim3(cdiv(T, 256)), dim3(256), 0, st, g->rs_off.p, g->rs_ops.p, inv.p, T, NA,
                        g->hot_off.p, g->hot16.p);
-    MR_TRY(tr_layout(ctx, g, g->hot_off.p, g->hot16.p, NA, n_hot, nullptr));   // tperm, w_tp, tids, coff
+    MR_TRY(tr_layout(ctx, g, g->hot_off.p, g->hot16.p, NA, n_hot, nullptr, nc.p));   // tperm, w_tp, tids, coff
     // ---- cold entries in position order
     DBuf<int32_t> cnt;
     DBuf<int64_t> coff64;
@@ -3090,6 +3204,13 @@ static int wide_prepare(mr_ctx* ctx, mr_graph* g) {
     g->n_cold = n_cold;
     MR_TRY(g->cold_off_p.alloc(ctx, (size_t)T + 1));
     hipLaunchKernelGGL(k_tr_coff, dim3(cdiv((int64_t)T + 1, 256)), dim3(256), 0, st, coff64.p, T, g->cold_off_p.p);
+    const int32_t W = g->n_wt;
+    // ---- cold tiles of the short-tile walk (after cold_ops_p, below) and the long-tile start
+    DBuf<int32_t> ccnt;
+    DBuf<int64_t> cc64;
+    MR_TRY(ccnt.alloc(ctx, (size_t)std::max(W, 1)));
+    MR_TRY(cc64.alloc(ctx, (size_t)W + 1));
+    MR_TRY(g->ccoff.alloc(ctx, (size_t)W + 1));
     const int32_t R = (int32_t)cdiv((int64_t)N - NA, WIDE_RW_MAX);
     const int32_t RW = (int32_t)(cdiv(cdiv((int64_t)N - NA, R), WAVE) * WAVE);
     g->n_ranges = R;
@@ -3111,6 +3232,34 @@ static int wide_prepare(mr_ctx* ctx, mr_graph* g) {
             hipLaunchKernelGGL(k_wide_unpack, dim3(cdiv(n_cold, 256)), dim3(256), 0, st, ck.p, n_cold, g->cp_pos.p,
                                g->cp_op.p);
         }
+    }
+    if (W) {
+        hipLaunchKernelGGL(k_ctile_cnt, dim3(cdiv(W, 256)), dim3(256), 0, st, g->cold_off_p.p, T, W, ccnt.p);
+        DBuf<int64_t> tmp2;
+        MR_TRY(tmp2.alloc(ctx, (size_t)scan_tmp_elems(W)));
+        MR_TRY(mr_exclusive_scan_i32(ctx, ccnt.p, cc64.p, W, tmp2.p));
+        hipLaunchKernelGGL(k_tr_coff, dim3(cdiv((int64_t)W + 1, 256)), dim3(256), 0, st, cc64.p, W, g->ccoff.p);
+        int64_t nch = 0;
+        MR_TRY_HIP(ctx, hipMemcpyAsync(&nch, cc64.p + W, sizeof nch, hipMemcpyDeviceToHost, st));
+        MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+        MR_TRY(g->ctids.alloc(ctx, (size_t)std::max<int64_t>(nch, 1) * WAVE * 2));
+        hipLaunchKernelGGL(k_ctile_fill, dim3(cdiv((int64_t)W * WAVE, 256)), dim3(256), 0, st, g->cold_off_p.p,
+                           g->cold_ops_p.p, cc64.p, T, N, W, g->ctids.p);
+        // long tiles (more hot chunks than the short walk's last tier) and short tiles with more
+        // than two cold chunks keep k_cold_trace's sums: the list of those tiles
+        std::vector<int32_t> co((size_t)W + 1), cn((size_t)W), tl;
+        MR_TRY(g->coff.download(ctx, co.data(), co.size()));
+        MR_TRY(ccnt.download(ctx, cn.data(), cn.size()));
+        MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+        for (int32_t k = 0; k < W; ++k)
+            if (co[(size_t)k + 1] - co[(size_t)k] > TR_TIERS_EXT || cn[(size_t)k] > 2) tl.push_back(k);
+        g->n_ctl = (int32_t)tl.size();
+        MR_TRY(g->ctl.alloc(ctx, std::max<size_t>(tl.size(), 1)));
+        if (!tl.empty()) MR_TRY(g->ctl.upload(ctx, tl.data(), tl.size()));
+        MR_TRY_HIP(ctx, hipStreamSynchronize(st));   // (the host list leaves scope)
+    } else {
+        MR_TRY_HIP(ctx, hipMemsetAsync(g->ccoff.p, 0, sizeof(int32_t), st));
+        g->n_ctl = 0;
     }
     std::vector<int64_t> rbh((size_t)R + 1);
     MR_TRY(rb.download(ctx, rbh.data(), rbh.size()));
@@ -3781,6 +3930,8 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         v.w_tp = g->w_tp.p;
         v.mw_tp = g->mw_tp.p;
         v.hmask = g->nhr ? g->hmask.p : nullptr;
+        v.ctids = g->wide ? g->ctids.p : nullptr;
+        v.ccoff = g->wide ? g->ccoff.p : nullptr;
         v.nhr = g->fused ? g->nhr : 0;
         for (int h = 0; h < 8; ++h) v.hop[h] = g->hop[h];
         v.c_t = g->c_t.p;
@@ -3886,8 +4037,12 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         if (gs[i]->fused && gs[i]->nhr && plan.mode != WV_SU_ALL)
             return mr_fail(ctx, MR_ERR_ARG, "pagerank batch: a hot-op layout (T >= MR_TR_HOT_MIN) with a graph of > %d ops",
                            (int)WIDE_NA);
-    bool any_ext = false;   // kind multiplicities or cold sums in some fused graph of the launch
-    for (int i = 0; i < ng; ++i) any_ext = any_ext || (gs[i]->fused && (hv[(size_t)i].mw_tp || hv[(size_t)i].cold_acc));
+    int any_ext = 0;   // kind multiplicities (1) or cold sums (2) in some fused graph of the launch
+    for (int i = 0; i < ng; ++i)
+        if (gs[i]->fused) any_ext |= (hv[(size_t)i].mw_tp ? 1 : 0) | (hv[(size_t)i].cold_acc ? 2 : 0);
+    for (int i = 0; i < ng; ++i)   // the wide variant carries HOT_MAX_WIDE hot accumulators
+        if ((any_ext & 2) && gs[i]->fused && gs[i]->nhr > HOT_MAX_WIDE)
+            return mr_fail(ctx, MR_ERR_ARG, "pagerank batch: a hot-op layout of %d ops beside a wide graph", gs[i]->nhr);
     const TrA tr_a = tr_kernel(fp32, plan.mode, plan.NT, any_ext);
     // a sharded graph with no collective backend is one whole shard: the split launches around the
     // (no-op) all-reduces would compute the same integers / sums in two halves
@@ -3942,9 +4097,10 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
                 hipLaunchKernelGGL(k_cold_ops<double>, dim3(g->n_cb), dim3(WIDE_CT), lds_c, sst, g->cb_beg.p, g->cp_pos.p,
                                    g->cp_op.p, qc, g->mslot.p, it, hv[(size_t)i].cx_scale, g->cold_rw,
                                    (unsigned long long*)g->cold_part.p);
-            if (g->T)
-                hipLaunchKernelGGL(k_cold_trace, dim3(cdiv(g->T, 256)), dim3(256), 0, st, g->cold_off_p.p, g->cold_ops_p.p,
-                                   g->sub[it & 1].p, g->T, g->cold_acc.p);
+            if (g->n_ctl)   // (the listed tiles only: the short-tile walk gathers the rest itself)
+                hipLaunchKernelGGL(k_cold_trace, dim3(cdiv((int64_t)g->n_ctl * WAVE, 256)), dim3(256), 0, st,
+                                   g->cold_off_p.p, g->cold_ops_p.p, g->sub[it & 1].p, g->ctl.p, g->n_ctl, g->T,
+                                   g->cold_acc.p);
             MR_DEBUG_CHECK(ctx, "k_cold");
         }
         if (any_wide && sst != st) MR_TRY_HIP(ctx, hipEventRecord(ctx->side_ev[1], sst));
@@ -4214,6 +4370,7 @@ static int kind_compressed_pagerank(mr_ctx* ctx, mr_graph* g, int anomaly, doubl
     gc->pr_identity = true;
     gc->n_pr = (int32_t)K;
     gc->nnz_sr = gc->nnz_rs = nnz;
+    gc->kinds_given = true;   // (before the prepare: its layout is then the stable sort)
     MR_TRY(mr_graph_prepare(ctx, gc.get()));
     if (!gc->fused)
         return mr_pagerank_batch_impl(ctx, &g, &anomaly, 1, d, alpha, iters, precision, plain);
@@ -4229,7 +4386,6 @@ static int kind_compressed_pagerank(mr_ctx* ctx, mr_graph* g, int anomaly, doubl
     MR_TRY(gc->kind.alloc(ctx, (size_t)K));   // the class sizes, as the preference reads them
     MR_TRY_HIP(ctx, hipMemcpyAsync(gc->kind.p, gc->mult.p, (size_t)K * 8, hipMemcpyDeviceToDevice, st));
     MR_TRY_HIP(ctx, hipStreamSynchronize(st));
-    gc->kinds_given = true;
     MR_TRY(rank_kc(gc.get()));
     g->kc_kinds = K;
     g->kc = std::move(gc);
