@@ -1826,7 +1826,8 @@ __device__ __forceinline__ void tr_hot_sums(const GDev& G, const double* su_l, d
 template <class Q, int NC, int EXT, int HN>
 __device__ __forceinline__ int32_t tr_walk_short(const GDev& G, int32_t k, const int32_t ke, int32_t T, int32_t lane,
                                                  int cur, int nxt, double d, double Ms, double xsc, const double* su_l,
-                                                 unsigned long long* lacc, double& rmax, TrHot<HN>& H) {
+                                                 unsigned long long* lacc, double& rmax, TrHot<HN>& H, int32_t& c0,
+                                                 int32_t& n, int32_t& q0, int32_t& nq) {
     const GLB u32x2* ids = gp((const u32x2*)G.tids) + lane;
     const GLB int32_t* coff = gp(G.coff);
     const GLB Q* qc = gp((const Q*)G.q[cur]);
@@ -1847,20 +1848,18 @@ __device__ __forceinline__ int32_t tr_walk_short(const GDev& G, int32_t k, const
     const bool hot = H.n > 0;
     const GLB uint8_t* hmk = hot ? gp(G.hmask) : (const GLB uint8_t*)coff;
     const int32_t cl = __builtin_amdgcn_readfirstlane(coff[ke]) - 1;   // the run's last chunk
-    // the first tile's chunk range
-    int32_t c0, n;
-    {
+    // the first tile's chunk ranges: handed over by the previous tier (n >= 0), else loaded
+    if (n < 0) {
         const int32_t v = coff[min(k + lane, ke)];
         c0 = __builtin_amdgcn_readfirstlane(v);
         n = __builtin_amdgcn_readlane(v, 1) - c0;
+        if constexpr ((EXT & 2) != 0) {
+            const int32_t u = ccoff[min(k + lane, ke)];
+            q0 = __builtin_amdgcn_readfirstlane(u);
+            nq = __builtin_amdgcn_readlane(u, 1) - q0;
+        }
     }
     if (n != NC) return k;
-    int32_t q0 = 0, nq = 0;   // the first tile's cold chunk range
-    if constexpr ((EXT & 2) != 0) {
-        const int32_t v = ccoff[min(k + lane, ke)];
-        q0 = __builtin_amdgcn_readfirstlane(v);
-        nq = __builtin_amdgcn_readlane(v, 1) - q0;
-    }
     using R = TrTile<Q, NC, EXT>;
     const GLB double* cacc = cx ? gp(G.cold_acc) : sug;
     auto load = [&](R& r, int32_t kk, int32_t cc0, int32_t qq0, int32_t nqq) {
@@ -1945,7 +1944,10 @@ __device__ __forceinline__ int32_t tr_walk_short(const GDev& G, int32_t k, const
         }
         load(B, k + 1, c0B, qB, nqB);
         run(A, k, qA, nqA);
-        if (++k == ke || nB != NC) break;
+        if (++k == ke || nB != NC) {
+            c0 = c0B, n = nB, q0 = qB, nq = nqB;
+            break;
+        }
         const int32_t c0A = __builtin_amdgcn_readfirstlane(B.cw);
         nA = __builtin_amdgcn_readlane(B.cw, 1) - c0A;
         if constexpr ((EXT & 2) != 0) {
@@ -1954,7 +1956,10 @@ __device__ __forceinline__ int32_t tr_walk_short(const GDev& G, int32_t k, const
         }
         load(A, k + 1, c0A, qA, nqA);
         run(B, k, qB, nqB);
-        if (++k == ke || nA != NC) break;
+        if (++k == ke || nA != NC) {
+            c0 = c0A, n = nA, q0 = qA, nq = nqA;
+            break;
+        }
     }
     return k;
 }
@@ -1992,7 +1997,8 @@ __device__ __forceinline__ double tr_walk(const GDev& G, int32_t lb, int cur, in
     if constexpr (SUL) {
         // one tier per chunk count (the run's tiles ascend in it): every count static, no branch
         // inside a tile, so each wait is for exactly the LDS reads and loads it consumes
-#define TR_TIER(NC_) if (NC_ <= (NT == 1024 || EXT ? TR_TIERS_EXT : MR_TR_TIERS512) && k < ke) k = tr_walk_short<Q, NC_, EXT, HN>(G, k, ke, T, lane, cur, nxt, d, Ms, xsc, su_l, lacc, rmax, H);
+        int32_t tc0 = 0, tn = -1, tq0 = 0, tnq = 0;   // the next tile's ranges, handed from tier to tier
+#define TR_TIER(NC_) if (NC_ <= (NT == 1024 || EXT ? TR_TIERS_EXT : MR_TR_TIERS512) && k < ke) k = tr_walk_short<Q, NC_, EXT, HN>(G, k, ke, T, lane, cur, nxt, d, Ms, xsc, su_l, lacc, rmax, H, tc0, tn, tq0, tnq);
         TR_TIER(1) TR_TIER(2) TR_TIER(3) TR_TIER(4) TR_TIER(5) TR_TIER(6) TR_TIER(7) TR_TIER(8)
 #undef TR_TIER
     }
