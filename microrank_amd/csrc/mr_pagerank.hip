@@ -4063,7 +4063,8 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         return e ? atoi(e) : 0;
     }();
     bool fb_small = !any_wide;
-    for (int i = 0; i < ng; ++i) fb_small = fb_small && hv[(size_t)i].n_fa <= FB_SMALL_ROWS;
+    // (a large graph alone -- C4: 256 rows of 10k ops -- sums faster with 16-wave blocks: 137 -> 134 us)
+    for (int i = 0; i < ng; ++i) fb_small = fb_small && hv[(size_t)i].n_fa <= FB_SMALL_ROWS && hv[(size_t)i].N <= 4096;
     if (fb_force) fb_small = fb_force == FB_W_SMALL;
     static const bool no_side = getenv("MR_WIDE_SERIAL") != nullptr;   // A/B knob: one stream
     hipStream_t sst = st;
