@@ -715,12 +715,15 @@ __global__ void __launch_bounds__(SCHED_T) k_tr_sched(const int32_t* coff, int32
             }
     }
 }
-static bool tr_sched_on() {
-    static const bool on = [] {
-        const char* e = getenv("MR_TR_SCHED");
-        return e && !strcmp(e, "1");
-    }();
-    return on;
+// MR_TR_SCHED=1: the greedy order (on the stable radix layout, so a graph's tiles -- hence each
+// trace's summation order -- are the same every time it is prepared).  Off by default: on C4 it
+// gains 2 % per iteration (142.5 -> 139.8 us) but costs 41 ms per preparation (one thread per
+// half tile), and most graphs are ranked once (the driver builds two per window).
+constexpr int64_t TR_LARGE = (int64_t)1 << 20;   // "large graph": the hot-op threshold
+static bool tr_sched_on(int64_t T) {
+    (void)T;
+    const char* e = getenv("MR_TR_SCHED");   // (read per preparation: tests flip it)
+    return e && !strcmp(e, "1");
 }
 
 // The prepare of several small fused graphs (a window's two) in one launch per step: block ranges
@@ -3017,14 +3020,17 @@ static int hot_strip(mr_ctx* ctx, mr_graph* g, const int64_t*& off, const uint16
     const char* em = getenv("MR_TR_HOT_MIN");
     const int hcap = g->wide ? HOT_MAX_WIDE : HOT_MAX;   // (the wide variant carries fewer accumulators)
     const int hmax = eh ? std::min(std::max(atoi(eh), 0), hcap) : hcap;
-    const int64_t tmin = em ? (int64_t)atoll(em) : (int64_t)1 << 20;
+    const int64_t tmin = em ? (int64_t)atoll(em) : TR_LARGE;
     g->nhr = 0;
     g->hmask.reset();
     const int32_t T = g->T;
     if (hmax == 0 || (int64_t)T < tmin || N < 1 || N > 16384 || !TrLds(N, WV_SU_ALL).hot_ok) return MR_OK;
     hipStream_t st = ctx->stream;
     std::vector<int32_t> cov((size_t)N);
-    {
+    if (!g->wide && g->cov.p) {   // the kernel's ids are the graph's: its coverage (prepare / build) serves
+        MR_TRY(g->cov.download(ctx, cov.data(), (size_t)N));
+        MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+    } else {   // (wide graphs: the hot half's relabelled ids)
         DBuf<int32_t> dc;
         MR_TRY(dc.zero(ctx, (size_t)N));
         if (nent)
@@ -3042,7 +3048,16 @@ static int hot_strip(mr_ctx* ctx, mr_graph* g, const int64_t*& off, const uint16
         hidx[(size_t)ord[(size_t)nh]] = (int8_t)nh;
         g->hop[nh] = ord[(size_t)nh];
     }
-    if (nh == 0) return MR_OK;
+    // worth its pass only when the hot ops carry a quarter of the entries: the C4 graph's top 8
+    // carry 26 % (iteration 154 -> 145 us); the span-built C4 graph's 23 % (op 0 in every trace, then
+    // seven at 30 %) gained nothing measurable per iteration while the strip added ~1 ms to its
+    // build (c4 --from-spans, A/B in the commit log)
+    // (MR_TR_HOT_FRAC: that share, default 0.25; tests force the layout with 0)
+    const char* ef = getenv("MR_TR_HOT_FRAC");
+    const double fmin = ef ? atof(ef) : 0.25;
+    int64_t hsum = 0;
+    for (int h = 0; h < nh; ++h) hsum += cov[(size_t)g->hop[h]];
+    if (nh == 0 || (double)hsum < fmin * (double)nent) return MR_OK;
     DBuf<int8_t> dh;
     DBuf<int32_t> rlen;
     DBuf<int64_t> tmp;
@@ -3053,17 +3068,14 @@ static int hot_strip(mr_ctx* ctx, mr_graph* g, const int64_t*& off, const uint16
     MR_TRY(tmp.alloc(ctx, (size_t)scan_tmp_elems(T)));
     hipLaunchKernelGGL(k_hot_count, dim3(cdiv(T, 256)), dim3(256), (size_t)N, st, off, src, T, dh.p, N, rlen.p, mask.p);
     MR_TRY(mr_exclusive_scan_i32(ctx, rlen.p, roff.p, T, tmp.p));
-    int64_t n2 = 0;
-    MR_TRY_HIP(ctx, hipMemcpyAsync(&n2, roff.p + T, sizeof n2, hipMemcpyDeviceToHost, st));
-    MR_TRY_HIP(ctx, hipStreamSynchronize(st));
-    MR_TRY(rids.alloc(ctx, (size_t)std::max<int64_t>(n2, 1) + 8));
+    // (sized by the full entry count: no read-back; nent stays an upper bound for the layout)
+    MR_TRY(rids.alloc(ctx, (size_t)std::max<int64_t>(nent, 1) + 8));
     hipLaunchKernelGGL(k_hot_fill, dim3(cdiv(T, 256)), dim3(256), (size_t)N, st, off, src, T, dh.p, N, mask.p, roff.p, rids.p);
     MR_TRY_HIP(ctx, hipGetLastError());
-    MR_TRY_HIP(ctx, hipStreamSynchronize(st));   // (dh, rlen, tmp leave scope)
+    MR_TRY_HIP(ctx, hipStreamSynchronize(st));   // (the host hidx leaves scope)
     g->nhr = nh;
     off = roff.p;
     src = rids.p;
-    nent = n2;
     return MR_OK;
 }
 
@@ -3096,7 +3108,8 @@ static int tr_layout(mr_ctx* ctx, mr_graph* g, const int64_t* off, const uint16_
     // (length, secondary key): a stable radix sort, equal keys in trace order -- for wide graphs (the
     // cold count as secondary key) and kind-compressed ones, whose fixed-point scale depends on
     // the tiles' multiplicity sums (the counting sort below orders equal lengths run-dependently)
-    if (T && (skey || g->kinds_given)) {
+    const bool sched = tr_sched_on(T);
+    if (T && (skey || g->kinds_given || sched)) {
         DBuf<uint64_t> key;
         DBuf<uint32_t> val;
         MR_TRY(key.alloc(ctx, (size_t)T));
@@ -3140,7 +3153,7 @@ static int tr_layout(mr_ctx* ctx, mr_graph* g, const int64_t* off, const uint16_
     if (W)
         hipLaunchKernelGGL(k_tr_fill, dim3(cdiv((int64_t)W * WAVE, 256)), dim3(256), 0, st, g->tperm.p, off, src,
                            c64.p, T, N, W, g->tids.p);
-    if (W && tr_sched_on())
+    if (W && sched)
         hipLaunchKernelGGL(k_tr_sched, dim3(cdiv(2 * (int64_t)W, SCHED_T)), dim3(SCHED_T), 0, st, g->coff.p, W, g->tids.p);
     if (g->nhr) {   // the hot-op bits in position order
         MR_TRY(g->hmask.alloc(ctx, (size_t)T));

@@ -520,6 +520,7 @@ def test_hot_op_layout_against_oracle(anomaly, monkeypatch):
     for hot in ("0", "8"):
         monkeypatch.setenv("MR_TR_HOT", hot)
         monkeypatch.setenv("MR_TR_HOT_MIN", "0")
+        monkeypatch.setenv("MR_TR_HOT_FRAC", "0")
         dg = DeviceGraph.upload(ctx, hg)
         dg.pagerank(anomaly)
         w, cov = dg.fetch()
@@ -544,6 +545,7 @@ def test_wide_hot_op_layout_against_oracle(precision, monkeypatch):
     from microrank_amd.graph import DeviceGraph
 
     monkeypatch.setenv("MR_TR_HOT_MIN", "0")
+    monkeypatch.setenv("MR_TR_HOT_FRAC", "0")
     hg = _with_cold_traces(synth.big_graph(50_000, 40_000, seed=9), 3000, 30_000, seed=10)
     g = _oracle_graph_from_host(hg)
     kind = orc.trace_kinds(g)
