@@ -2196,6 +2196,31 @@ __global__ void __launch_bounds__(WAVE * FB_W) k_fx_b(const GDev* __restrict__ g
     const int32_t N = G.N, nb = G.n_fa;
     const bool on = o < N;
     const int k3c = it % 3;
+    // the op's rows: k_tr_a's (stride NA), or on a wide graph its cold range's (stride cold_rw).
+    // The first batch of 16 rows per lane is issued before the call-graph term below, so the two
+    // chains of dependent loads overlap (window graphs: tens of rows, one batch covers them)
+    const int32_t stride = FB_W * GR;
+    const GLB unsigned long long* col = gp((const unsigned long long*)G.fx_part);
+    int32_t nbl = 0;
+    size_t rs = 1;
+    if (on && mode != 2) {
+        if (o < G.NA) {
+            col = gp((const unsigned long long*)G.fx_part) + o;
+            nbl = nb;
+            rs = (size_t)G.NA;
+        } else {
+            const int32_t oc = o - G.NA, r = oc / G.cold_rw, rb0 = G.cold_rowbase[r];
+            nbl = G.cold_rowbase[r + 1] - rb0;
+            col = gp(G.cold_part) + (size_t)rb0 * G.cold_rw + (oc - r * G.cold_rw);
+            rs = (size_t)G.cold_rw;
+        }
+    }
+    const int32_t rfirst = w * GR + grp;
+    unsigned long long v0[16];
+    if (nbl > 0) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) v0[k] = col[(size_t)min(rfirst + k * stride, nbl - 1) * rs];
+    }
     // the call-graph term alpha (P_ss s_k)[op] / M_s(k) (pagerank.py:122-124) of the block's ops: a
     // wave per op, its lanes striding the op's parents, one fixed-order wave sum (a hub op with
     // thousands of parents costs one wave, not one thread)
@@ -2229,25 +2254,16 @@ __global__ void __launch_bounds__(WAVE * FB_W) k_fx_b(const GDev* __restrict__ g
         else rmax_take_bits(G.fx_limb + 2 * (size_t)N, G.nranks, Mn, lane);
     }
     unsigned long long lo = 0ull, hi = 0ull;
-    if (on && mode != 2) {
-        // batches of 16 rows per lane, every load in flight before the sums (indices clamped:
-        // the repeats are cache hits and are not added)
-        const int32_t stride = FB_W * GR;
-        // the op's rows: k_tr_a's (stride NA), or on a wide graph its cold range's (stride cold_rw)
-        const GLB unsigned long long* col;
-        int32_t nbl;
-        size_t rs;
-        if (o < G.NA) {
-            col = gp((const unsigned long long*)G.fx_part) + o;
-            nbl = nb;
-            rs = (size_t)G.NA;
-        } else {
-            const int32_t oc = o - G.NA, r = oc / G.cold_rw, rb0 = G.cold_rowbase[r];
-            nbl = G.cold_rowbase[r + 1] - rb0;
-            col = gp(G.cold_part) + (size_t)rb0 * G.cold_rw + (oc - r * G.cold_rw);
-            rs = (size_t)G.cold_rw;
-        }
-        for (int32_t r0 = w * GR + grp; r0 < nbl; r0 += 16 * stride) {
+    if (nbl > 0) {
+        // the first batch (loaded above), then batches of 16 rows per lane, every load in flight
+        // before the sums (indices clamped: the repeats are cache hits and are not added)
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            if (rfirst + k * stride < nbl) {
+                lo += v0[k] & 0xffffffffull;
+                hi += v0[k] >> 32;
+            }
+        for (int32_t r0 = rfirst + 16 * stride; r0 < nbl; r0 += 16 * stride) {
             unsigned long long v[16];
 #pragma unroll
             for (int k = 0; k < 16; ++k) v[k] = col[(size_t)min(r0 + k * stride, nbl - 1) * rs];
