@@ -9,6 +9,7 @@
 // dropped (preprocess_data.py:117).  The sum is sequential per trace with separate multiply and add (T14), so
 // the partition is bit-exact.
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <utility>
 #include <vector>
@@ -361,6 +362,30 @@ static int win_detect_build(mr_ctx* ctx, const mr_spans* s, int64_t t0, int64_t 
 // launches, the chunk one read-back; `ev` marks the chunk's graphs ready on this stream, and the
 // caller's PageRank waits on it instead of on the host.  Per-window outcome in w->rc (MR_ERR_VALUE:
 // empty window); a non-OK return fails the whole chunk.
+// MR_WIN_PHASES=1 (read per call): host time per phase of mr_windows_batch, summed over the
+// threads, printed to stderr at the end of a call (diagnostic)
+struct WinPhases {
+    std::atomic<long long> ns[10];
+    WinPhases() {
+        for (auto& x : ns) x = 0;
+    }
+};
+static WinPhases* g_phases = nullptr;
+static inline long long win_now() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+struct WinPhase {   // adds the scope's duration to phase i when timing is on
+    int i;
+    long long t;
+    explicit WinPhase(int i_) : i(i_), t(g_phases ? win_now() : 0) {}
+    ~WinPhase() {
+        if (g_phases) g_phases->ns[i] += win_now() - t;
+    }
+};
+static const char* const WIN_PHASE_NAME[10] = {"chunk launch", "chunk read-back wait", "chunk finish+prepare",
+                                               "spectrum task", "worker idle", "main: wait builds",
+                                               "main: pagerank batch", "main: tail", "", ""};
+
 struct WinIn {
     const mr_spans* s;
     int64_t t0, t1;
@@ -380,30 +405,70 @@ static int win_chunk_build_async(mr_ctx* ctx, const WinIn* in, int n, int precis
     constexpr size_t CW = 3 * MR_DETECT_SHARDS;   // per window: detector counter shards, then 8 + 8 size words
     constexpr size_t WW = CW + 16;
     DBuf<int64_t> wb;
+    auto ph0 = std::make_unique<WinPhase>(0);
     MR_TRY(wb.zero(ctx, (size_t)n * WW));
     std::vector<DBuf<uint8_t>> dst((size_t)n);   // (DBufs return to the pool stream-ordered: the
     std::vector<IxBuild> bx(2 * (size_t)n);      //  kernels enqueued on them run first)
+    // the detector inside the index pass's first launch for tables up to MR_DET_FUSE_MAX traces
+    // (default 65536; measured: C3's 20k traces +2%, C2's 200k -3% -- the fused launch's tiles
+    // are the detector's 256 traces, 8x k_ix_sel_scan2's, and its look-back chains 8x longer).
+    // MR_NO_DET_FUSE: never.  (Both read per call.)
+    const char* fm = getenv("MR_DET_FUSE_MAX");
+    const bool no_fuse = getenv("MR_NO_DET_FUSE") != nullptr;
+    const int64_t fuse_max = fm ? (int64_t)atoll(fm) : 65536;
+    std::vector<DetIn> dis((size_t)n);
+    std::vector<char> fz((size_t)n);
     for (int k = 0; k < n; ++k) {
         const mr_spans* s = in[k].s;
         WinRun& w = *in[k].w;
         const int32_t NT = s->n_traces;
         int64_t* wk = wb.p + (size_t)k * WW;
         MR_TRY(dst[(size_t)k].alloc(ctx, std::max(NT, 1)));
-        const DetIn di = mr_detect_in(s, in[k].t0, in[k].t1, in[k].a3, in[k].a3v, dst[(size_t)k].p, (unsigned long long*)wk);
+        dis[(size_t)k] = mr_detect_in(s, in[k].t0, in[k].t1, in[k].a3, in[k].a3v, dst[(size_t)k].p, (unsigned long long*)wk);
+        fz[(size_t)k] = !no_fuse && (int64_t)NT <= fuse_max;
         w.gn = new mr_graph();
         w.gn->ctx = ctx;
         w.ga = new mr_graph();
         w.ga->ctx = ctx;
+    }
+    // the whole chunk's index pass in one launch per stage when every window allows it (and the
+    // windows agree on the detector fusion), else window by window
+    bool batched = false;
+    if (n >= 2) {
+        bool same = true;
+        for (int k = 1; k < n; ++k) same = same && fz[(size_t)k] == fz[0];
+        if (same) {
+            std::vector<const mr_spans*> sps((size_t)n);
+            std::vector<uint8_t*> sts((size_t)n);
+            std::vector<mr_graph*> g0((size_t)n), g1((size_t)n);
+            std::vector<IxBuild*> b0((size_t)n), b1((size_t)n);
+            std::vector<int64_t*> outs((size_t)n);
+            for (int k = 0; k < n; ++k) {
+                sps[(size_t)k] = in[k].s;
+                sts[(size_t)k] = dst[(size_t)k].p;
+                g0[(size_t)k] = in[k].w->gn;
+                g1[(size_t)k] = in[k].w->ga;
+                b0[(size_t)k] = &bx[2 * (size_t)k];
+                b1[(size_t)k] = &bx[2 * (size_t)k + 1];
+                outs[(size_t)k] = wb.p + (size_t)k * WW + CW;
+            }
+            const int rcb = mr_ix_launch2_batch(ctx, n, sps.data(), sts.data(), g0.data(), g1.data(), b0.data(), b1.data(),
+                                                outs.data(), dis.data(), fz[0] != 0);
+            if (rcb != MR_ERR_STATE) MR_TRY(rcb);
+            batched = rcb == MR_OK;
+        }
+    }
+    for (int k = 0; k < n && !batched; ++k) {
+        const mr_spans* s = in[k].s;
+        WinRun& w = *in[k].w;
+        const int32_t NT = s->n_traces;
+        int64_t* wk = wb.p + (size_t)k * WW;
+        const DetIn& di = dis[(size_t)k];
         IxBuild &bn = bx[2 * (size_t)k], &ba = bx[2 * (size_t)k + 1];
         // (the graphs take EVERY row of the selected traces: get_pagerank_graph(list, data),
         // online_rca.py:180,185 / preprocess_data.py:148).  Both from the states in one pass over
         // the index when the table allows it, else one build per mask.
-        // the detector inside the index pass's first launch for tables up to MR_DET_FUSE_MAX traces
-        // (default 65536; measured: C3's 20k traces +2%, C2's 200k -3% -- the fused launch's tiles
-        // are the detector's 256 traces, 8x k_ix_sel_scan2's, and its look-back chains 8x longer).
-        // MR_NO_DET_FUSE: never.  (Both read per call.)
-        const char* fm = getenv("MR_DET_FUSE_MAX");
-        const bool fuse = getenv("MR_NO_DET_FUSE") == nullptr && (int64_t)NT <= (fm ? (int64_t)atoll(fm) : 65536);
+        const bool fuse = fz[(size_t)k] != 0;
         if (!fuse) MR_TRY(mr_detect_indexed_launch(ctx, s, in[k].t0, in[k].t1, in[k].a3, in[k].a3v, dst[(size_t)k].p,
                                                    (unsigned long long*)wk));
         const int rc2 = mr_ix_launch2(ctx, s, dst[(size_t)k].p, w.gn, w.ga, bn, ba, wk + CW, fuse ? &di : nullptr);
@@ -420,12 +485,15 @@ static int win_chunk_build_async(mr_ctx* ctx, const WinIn* in, int n, int precis
             MR_TRY(rc2);
         }
     }
+    ph0.reset();
     std::vector<int64_t> h((size_t)n * WW);
     {
+        WinPhase ph(1);
         unsigned char* hp = nullptr;
         MR_TRY(mr_read_bytes(ctx, wb.p, h.size() * sizeof(int64_t), &hp));
         memcpy(h.data(), hp, h.size() * sizeof(int64_t));
     }
+    WinPhase ph2(2);
     // MR_WIN_SETUP_SPLIT: traces of a window from which it sets up here (default 65536): small
     // windows (C3: 20k traces) leave it to the PageRank stream, which sets up the whole group's
     // graphs at once; large ones (C2: 200k traces) set up here, overlapping other work
@@ -593,6 +661,14 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
             return mr_fail(ctx, MR_ERR_ARG, "mr_windows_batch: bad window %d", i);
     MR_TRY_HIP(ctx, hipSetDevice(ctx->device));
     if (n_windows == 0) return MR_OK;
+    // (diagnostic phase timers: one call at a time sets them)
+    static WinPhases phases_store;
+    const bool timing = getenv("MR_WIN_PHASES") != nullptr;
+    if (timing) {
+        for (auto& x : phases_store.ns) x = 0;
+        g_phases = &phases_store;
+    }
+    const long long t_call = timing ? win_now() : 0;
     const int32_t K = std::max(0, top_max + 6);
     // MR_WIN_STREAMS: auxiliary streams (and host threads) of a batch.  4 measured best (C2 2908 /
     // C3 4850 windows/s vs 2705 / 4247 at 16): the windows' launches come from the host threads
@@ -659,6 +735,7 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
                 int32_t task;
                 {
                     std::unique_lock<std::mutex> lk(mu);
+                    WinPhase ph(4);
                     cv_task.wait(lk, [&] { return closed || !q.empty(); });
                     if (q.empty()) return;
                     task = q.front();
@@ -688,6 +765,7 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
                     built[(size_t)(i0 / gsz)] += i1 - i0;
                     cv_done.notify_all();
                 } else {           // spectrum, after the group's PageRanks (an event, not a host wait)
+                    WinPhase ph(3);
                     const int32_t i = ~task;
                     WinRun& r = w[(size_t)i];
                     (void)hipStreamWaitEvent(a->stream, gev[(size_t)(i / gsz)], 0);
@@ -716,6 +794,7 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
         const int32_t i0 = g * gsz, i1 = std::min<int32_t>(n_windows, i0 + gsz);
         {
             std::unique_lock<std::mutex> lk(mu);
+            WinPhase ph(5);
             cv_done.wait(lk, [&] { return built[(size_t)g] == i1 - i0; });
         }
         for (size_t c = 0; c < chunks.size(); ++c)   // the group's chunks' graphs are ready
@@ -736,7 +815,10 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
                 anom.push_back(1);
             }
         }
-        if (!gs.empty()) rc = mr_pagerank_batch(ctx, gs.data(), anom.data(), (int)gs.size(), 0.85, 0.01, 25, precision, 0);
+        if (!gs.empty()) {
+            WinPhase ph(6);
+            rc = mr_pagerank_batch(ctx, gs.data(), anom.data(), (int)gs.size(), 0.85, 0.01, 25, precision, 0);
+        }
         if (rc == MR_OK) {
             if (!gev[(size_t)g]) rc = hipEventCreateWithFlags(&gev[(size_t)g], hipEventDisableTiming) == hipSuccess ? MR_OK : MR_ERR_HIP;
             if (rc == MR_OK) rc = hipEventRecord(gev[(size_t)g], ctx->stream) == hipSuccess ? MR_OK : MR_ERR_HIP;
@@ -751,6 +833,7 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
         closed = true;
         cv_task.notify_all();
     }
+    std::unique_ptr<WinPhase> ph_tail(new WinPhase(7));
     for (auto& t : th) t.join();
     reaper.join();
     for (int k = 0; k < nthr; ++k) (void)hipStreamSynchronize(ctx->aux[(size_t)k]->stream);
@@ -795,5 +878,12 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
             if (r.ga) ctx->graveyard.push_back(r.ga);
             r.gn = r.ga = nullptr;
         }
+    ph_tail.reset();
+    if (timing) {
+        fprintf(stderr, "[mr_windows_batch] %d windows, %.3f ms:", n_windows, (win_now() - t_call) * 1e-6);
+        for (int i = 0; i < 8; ++i) fprintf(stderr, " %s %.3f ms;", WIN_PHASE_NAME[i], g_phases->ns[i] * 1e-6);
+        fprintf(stderr, "\n");
+        g_phases = nullptr;
+    }
     return MR_OK;
 }

@@ -25,10 +25,12 @@ struct DetIn {
     unsigned long long* counts;     // out: 3 * CSH counter shards (abnormal, normal, in-window rows)
 };
 
-// Block of DB threads, trace blockIdx.x * DB + threadIdx.x per thread: its state (also returned)
-// and the block's counts.  `term` is the caller's LDS of DB * DCAP doubles.
-__device__ __forceinline__ int detect_block(int32_t NT, const DetIn& d, double* term) {
-    const int32_t tb = blockIdx.x * DB, te_ = min(tb + DB, NT);
+// Block of DB threads, trace blk * DB + threadIdx.x per thread: its state (also returned) and the
+// block's counts.  `term` is the caller's LDS of DB * DCAP doubles.  blk: the block's index among
+// the window's (blockIdx.x, or its offset in a launch over several windows)
+__device__ __forceinline__ int detect_block(int32_t NT, const DetIn& d, double* term, int32_t blk = -1) {
+    if (blk < 0) blk = (int32_t)blockIdx.x;
+    const int32_t tb = blk * DB, te_ = min(tb + DB, NT);
     const int32_t t = tb + threadIdx.x;
     const int64_t r0 = d.sv_off[tb], r1 = d.sv_off[te_];
     const bool fits = r1 - r0 <= (int64_t)DB * DCAP;
@@ -96,7 +98,7 @@ __device__ __forceinline__ int detect_block(int32_t NT, const DetIn& d, double* 
     if (threadIdx.x < 3) {
         unsigned long long v = 0;
         for (int k = 0; k < DB / 64; ++k) v += bc[threadIdx.x][k];
-        if (v) atomicAdd(&d.counts[(size_t)(blockIdx.x % CSH) * 3 + threadIdx.x], v);
+        if (v) atomicAdd(&d.counts[(size_t)(blk % CSH) * 3 + threadIdx.x], v);
     }
     return st;
 }

@@ -727,13 +727,13 @@ struct IxSide2 {
 __device__ __forceinline__ int side_of(uint8_t st) { return st == 2 ? 0 : st == 1 ? 1 : -1; }
 // selection + the four exclusive scans (tpos and zoff of each graph) by decoupled look-back, and the
 // clearing of both graphs' counters
-__global__ void __launch_bounds__(SEL_T) k_ix_sel_scan2(const uint8_t* state, const int32_t* tlen, const int64_t* po_off,
+__device__ __forceinline__ void ix_sel_scan2_body(const uint8_t* state, const int32_t* tlen, const int64_t* po_off,
                                                        int32_t NT, IxSide2 x, unsigned long long* st, uint64_t epoch,
-                                                       int32_t NP, int64_t ecap) {
+                                                       int32_t NP, int64_t ecap, int32_t blk_, int32_t nblk_) {
     __shared__ int64_t sa[4][SEL_T];
     __shared__ int64_t ex[4];
     const int tid = threadIdx.x;
-    const int64_t gsz = (int64_t)gridDim.x * SEL_T, gi = (int64_t)blockIdx.x * SEL_T + tid;
+    const int64_t gsz = (int64_t)nblk_ * SEL_T, gi = (int64_t)blk_ * SEL_T + tid;
     for (int64_t i = gi; i < max((int64_t)NP, ecap); i += gsz)
 #pragma unroll
         for (int g = 0; g < 2; ++g) {
@@ -744,7 +744,7 @@ __global__ void __launch_bounds__(SEL_T) k_ix_sel_scan2(const uint8_t* state, co
             }
             if (i < ecap) x.g[g].gc[i] = 0u;
         }
-    const int64_t tile = blockIdx.x, base = tile * SEL_TILE + (int64_t)tid * SEL_I;
+    const int64_t tile = blk_, base = tile * SEL_TILE + (int64_t)tid * SEL_I;
     int8_t sd[SEL_I];
     int64_t z[SEL_I], acc[4] = {0, 0, 0, 0};
 #pragma unroll
@@ -777,10 +777,10 @@ __global__ void __launch_bounds__(SEL_T) k_ix_sel_scan2(const uint8_t* state, co
     {   // wave c: chain c (graph c / 2, tpos or zoff)
         const int c = tid / WAVE;
         const int64_t agg = sa[c][SEL_T - 1];
-        const int64_t e = dl_lookback_wave(st + (size_t)c * gridDim.x, tile, agg, epoch);
+        const int64_t e = dl_lookback_wave(st + (size_t)c * nblk_, tile, agg, epoch);
         if ((tid & (WAVE - 1)) == 0) {
             ex[c] = e;
-            if (tile == (int64_t)gridDim.x - 1) {
+            if (tile == (int64_t)nblk_ - 1) {
                 int64_t* dst = (c & 1) ? x.g[c >> 1].zoff : x.g[c >> 1].tpos;
                 dst[NT] = e + agg;
             }
@@ -805,17 +805,22 @@ __global__ void __launch_bounds__(SEL_T) k_ix_sel_scan2(const uint8_t* state, co
         }
     }
 }
+__global__ void __launch_bounds__(SEL_T) k_ix_sel_scan2(const uint8_t* state, const int32_t* tlen, const int64_t* po_off,
+                                                       int32_t NT, IxSide2 x, unsigned long long* st, uint64_t epoch,
+                                                       int32_t NP, int64_t ecap) {
+    ix_sel_scan2_body(state, tlen, po_off, NT, x, st, epoch, NP, ecap, (int32_t)blockIdx.x, (int32_t)gridDim.x);
+}
 // The window's detector and k_ix_sel_scan2's selection scans in ONE launch: tiles of DB traces,
 // each thread its trace's state (detect_block, into d.state for the later passes) and then the
 // four look-back chains over one trace per thread.
-__global__ void __launch_bounds__(DB) k_ix_detect_scan2(DetIn d, const int64_t* po_off, int32_t NT, IxSide2 x,
+__device__ __forceinline__ void ix_detect_scan2_body(DetIn d, const int64_t* po_off, int32_t NT, IxSide2 x,
                                                         unsigned long long* st, uint64_t epoch, int32_t NP,
-                                                        int64_t ecap) {
+                                                        int64_t ecap, int32_t blk_, int32_t nblk_) {
     __shared__ double term[DB * DCAP];
     __shared__ int64_t sa[4][DB];
     __shared__ int64_t ex[4];
     const int tid = threadIdx.x;
-    const int64_t gsz = (int64_t)gridDim.x * DB, gi = (int64_t)blockIdx.x * DB + tid;
+    const int64_t gsz = (int64_t)nblk_ * DB, gi = (int64_t)blk_ * DB + tid;
     for (int64_t i = gi; i < max((int64_t)NP, ecap); i += gsz)
 #pragma unroll
         for (int g = 0; g < 2; ++g) {
@@ -826,8 +831,8 @@ __global__ void __launch_bounds__(DB) k_ix_detect_scan2(DetIn d, const int64_t* 
             }
             if (i < ecap) x.g[g].gc[i] = 0u;
         }
-    const int stt = detect_block(NT, d, term);
-    const int64_t tile = blockIdx.x, t = tile * DB + tid;
+    const int stt = detect_block(NT, d, term, blk_);
+    const int64_t tile = blk_, t = tile * DB + tid;
     const int s_ = t < NT && d.tlen[t] > 0 ? side_of((uint8_t)stt) : -1;
     const int64_t z = s_ >= 0 ? po_off[t + 1] - po_off[t] : 0;
     if (t < NT) {
@@ -854,10 +859,10 @@ __global__ void __launch_bounds__(DB) k_ix_detect_scan2(DetIn d, const int64_t* 
     {   // wave c: chain c (graph c / 2, tpos or zoff)
         const int c = tid / WAVE;
         const int64_t agg = sa[c][DB - 1];
-        const int64_t e = dl_lookback_wave(st + (size_t)c * gridDim.x, tile, agg, epoch);
+        const int64_t e = dl_lookback_wave(st + (size_t)c * nblk_, tile, agg, epoch);
         if ((tid & (WAVE - 1)) == 0) {
             ex[c] = e;
-            if (tile == (int64_t)gridDim.x - 1) {
+            if (tile == (int64_t)nblk_ - 1) {
                 int64_t* dst = (c & 1) ? x.g[c >> 1].zoff : x.g[c >> 1].tpos;
                 dst[NT] = e + agg;
             }
@@ -871,13 +876,18 @@ __global__ void __launch_bounds__(DB) k_ix_detect_scan2(DetIn d, const int64_t* 
         x.g[1].zoff[t] = ex[3] + sa[3][tid] - acc[3];
     }
 }
+__global__ void __launch_bounds__(DB) k_ix_detect_scan2(DetIn d, const int64_t* po_off, int32_t NT, IxSide2 x,
+                                                        unsigned long long* st, uint64_t epoch, int32_t NP,
+                                                        int64_t ecap) {
+    ix_detect_scan2_body(d, po_off, NT, x, st, epoch, NP, ecap, (int32_t)blockIdx.x, (int32_t)gridDim.x);
+}
 static_assert(DB == 4 * WAVE, "k_ix_detect_scan2: one wave per look-back chain");
 // both graphs' per-pod-op counts / first rows / coverage and edge counts per dense id, one pass
-__global__ void __launch_bounds__(IX_BT) k_ix_stats2(const uint8_t* state, int64_t n_po, const int32_t* po_tr,
+__device__ __forceinline__ void ix_stats2_body(const uint8_t* state, int64_t n_po, const int32_t* po_tr,
                                                     const int32_t* po_op, const int32_t* po_cnt,
                                                     const int32_t* po_first, int64_t n_ed, const int32_t* ed_tr,
                                                     const int32_t* ed_eid, const int32_t* ed_cnt, int32_t NP,
-                                                    int32_t n_ek, IxSide2 x) {
+                                                    int32_t n_ek, IxSide2 x, int32_t blk_, int32_t nblk_) {
     extern __shared__ int32_t lh[];
     const int32_t W = 3 * NP + n_ek;   // words per graph: cnt, first, cov, edge counts
     for (int32_t i = threadIdx.x; i < 2 * W; i += IX_BT) {
@@ -885,8 +895,8 @@ __global__ void __launch_bounds__(IX_BT) k_ix_stats2(const uint8_t* state, int64
         lh[i] = (j >= NP && j < 2 * NP) ? 0x7fffffff : 0;
     }
     __syncthreads();
-    const int64_t pper = (n_po + gridDim.x - 1) / gridDim.x, eper = (n_ed + gridDim.x - 1) / gridDim.x;
-    const int64_t p0 = (int64_t)blockIdx.x * pper, p1 = min(p0 + pper, n_po);
+    const int64_t pper = (n_po + nblk_ - 1) / nblk_, eper = (n_ed + nblk_ - 1) / nblk_;
+    const int64_t p0 = (int64_t)blk_ * pper, p1 = min(p0 + pper, n_po);
     for (int64_t rb = p0; rb < p1; rb += (int64_t)IX_BT * IX_B) {
         int32_t tr[IX_B], op[IX_B], cn[IX_B], fr[IX_B];
 #pragma unroll
@@ -909,7 +919,7 @@ __global__ void __launch_bounds__(IX_BT) k_ix_stats2(const uint8_t* state, int64
             atomicAdd(&L[2 * NP + op[j]], 1);
         }
     }
-    const int64_t q0 = (int64_t)blockIdx.x * eper, q1 = min(q0 + eper, n_ed);
+    const int64_t q0 = (int64_t)blk_ * eper, q1 = min(q0 + eper, n_ed);
     for (int64_t rb = q0; rb < q1; rb += (int64_t)IX_BT * IX_B) {
         int32_t tr[IX_B], cn[IX_B], id[IX_B];
 #pragma unroll
@@ -939,6 +949,13 @@ __global__ void __launch_bounds__(IX_BT) k_ix_stats2(const uint8_t* state, int64
             atomicAdd(&x.g[g].gc[j - 3 * NP], (uint32_t)v);
         }
     }
+}
+__global__ void __launch_bounds__(IX_BT) k_ix_stats2(const uint8_t* state, int64_t n_po, const int32_t* po_tr,
+                                                    const int32_t* po_op, const int32_t* po_cnt,
+                                                    const int32_t* po_first, int64_t n_ed, const int32_t* ed_tr,
+                                                    const int32_t* ed_eid, const int32_t* ed_cnt, int32_t NP,
+                                                    int32_t n_ek, IxSide2 x) {
+    ix_stats2_body(state, n_po, po_tr, po_op, po_cnt, po_first, n_ed, ed_tr, ed_eid, ed_cnt, NP, n_ek, x, (int32_t)blockIdx.x, (int32_t)gridDim.x);
 }
 // join pairs across traces (T11): counted in a graph when both traces are in it
 __global__ void k_ix_cross2(const uint8_t* state, const int32_t* tc, const int32_t* tp, const int32_t* eid, int64_t n,
@@ -1632,6 +1649,244 @@ int mr_ix_launch2(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d_state, mr_gr
     if (NT || sp->n_po)
         hipLaunchKernelGGL(k_ix_traces2, dim3(cdiv(std::max<int64_t>(NT, sp->n_po), 256)), dim3(256), 0, st, d_state, xs,
                            NT, sp->tlen.p, sp->n_po, sp->po_tr.p, sp->po_off.p, sp->po_op.p, to);
+    MR_TRY_HIP(ctx, hipGetLastError());
+    return MR_OK;
+}
+
+// ---------------------------------------------------------------- the index pass of several windows
+// A chunk of windows (mr_windows_batch builds 4 per auxiliary stream) in ONE launch per stage
+// instead of one per window: the per-window chains of ~6 small, latency-bound launches ran back
+// to back on the stream (a C2 chunk: 24 launches before its read-back), now 6.  Per stage the
+// windows' arguments travel by value; a block finds its window by the launch's block offsets
+// (windows without blocks in a stage repeat the next offset) and runs the single-window body with
+// its index inside the window.
+constexpr int IXW = 8;   // windows per batched launch
+template <class A>
+struct IxBatch {
+    int32_t n;
+    int32_t b0[IXW + 1];
+    A w[IXW];
+};
+__device__ __forceinline__ int ixb_pick(const int32_t* b0, int32_t n) {
+    const int32_t b = (int32_t)blockIdx.x;
+    int k = 0;
+    while (k + 1 < n && b0[k + 1] <= b) ++k;
+    return k;
+}
+struct IxWinSel {
+    DetIn d;   // (the detector-fused variant)
+    const uint8_t* state;
+    const int32_t* tlen;
+    const int64_t* po_off;
+    unsigned long long* st;   // this window's look-back status words (4 chains x its tiles)
+    int64_t ecap;
+    int32_t NT, NP;
+    IxSide2 x;
+};
+struct IxWinStats {
+    const uint8_t* state;
+    const int32_t *po_tr, *po_op, *po_cnt, *po_first, *ed_tr, *ed_eid, *ed_cnt;
+    int64_t n_po, n_ed;
+    int32_t NP, n_ek;
+    IxSide2 x;
+};
+struct IxWinCross {
+    const uint8_t* state;
+    const int32_t *tc, *tp, *eid;
+    int64_t n;
+    IxSide2 x;
+};
+struct IxWinNodes {
+    const uint64_t* gk;
+    int64_t ecap;
+    int32_t NP, pad_;
+    NsArgs2 a;
+};
+struct IxWinTraces {
+    const uint8_t* state;
+    const int32_t *tlen, *po_tr, *po_op;
+    const int64_t* po_off;
+    int64_t n_po;
+    int32_t NT, pad_;
+    IxSide2 x;
+    TrOut2 o;
+};
+__global__ void __launch_bounds__(DB) k_ix_detect_b(IxBatch<IxWinSel> a) {
+    __shared__ double term[DB * DCAP];
+    const int k = ixb_pick(a.b0, a.n);
+    (void)detect_block(a.w[k].NT, a.w[k].d, term, (int32_t)blockIdx.x - a.b0[k]);
+}
+__global__ void __launch_bounds__(SEL_T) k_ix_sel_scan2_b(IxBatch<IxWinSel> a, uint64_t epoch) {
+    const int k = ixb_pick(a.b0, a.n);
+    const IxWinSel& w = a.w[k];
+    ix_sel_scan2_body(w.state, w.tlen, w.po_off, w.NT, w.x, w.st, epoch, w.NP, w.ecap, (int32_t)blockIdx.x - a.b0[k],
+                      a.b0[k + 1] - a.b0[k]);
+}
+__global__ void __launch_bounds__(DB) k_ix_detect_scan2_b(IxBatch<IxWinSel> a, uint64_t epoch) {
+    const int k = ixb_pick(a.b0, a.n);
+    const IxWinSel& w = a.w[k];
+    ix_detect_scan2_body(w.d, w.po_off, w.NT, w.x, w.st, epoch, w.NP, w.ecap, (int32_t)blockIdx.x - a.b0[k],
+                         a.b0[k + 1] - a.b0[k]);
+}
+__global__ void __launch_bounds__(IX_BT) k_ix_stats2_b(IxBatch<IxWinStats> a) {
+    const int k = ixb_pick(a.b0, a.n);
+    const IxWinStats& w = a.w[k];
+    ix_stats2_body(w.state, w.n_po, w.po_tr, w.po_op, w.po_cnt, w.po_first, w.n_ed, w.ed_tr, w.ed_eid, w.ed_cnt, w.NP,
+                   w.n_ek, w.x, (int32_t)blockIdx.x - a.b0[k], a.b0[k + 1] - a.b0[k]);
+}
+__global__ void k_ix_cross2_b(IxBatch<IxWinCross> a) {
+    const int k = ixb_pick(a.b0, a.n);
+    const IxWinCross& w = a.w[k];
+    const int64_t i = (int64_t)((int32_t)blockIdx.x - a.b0[k]) * blockDim.x + threadIdx.x;
+    if (i >= w.n) return;
+    const int sd = side_of(w.state[w.tc[i]]);
+    if (sd >= 0 && side_of(w.state[w.tp[i]]) == sd) atomicAdd(&w.x.g[sd].gc[w.eid[i]], 1u);
+}
+__global__ void __launch_bounds__(NS_T) k_nodes_small2_b(IxBatch<IxWinNodes> a) {   // block 2k + g: window k, graph g
+    const int k = (int)blockIdx.x >> 1;
+    const IxWinNodes& w = a.w[k];
+    const NsArgs& x = w.a.g[blockIdx.x & 1];
+    nodes_small(w.gk, x.gc, w.ecap, x.ocnt, x.ofirst, w.NP, x.node_of_code, x.node_podop, x.len_o, x.nchild, x.ocov, x.cov,
+                x.ss_par, x.ss_off, x.T_dev, x.nnz_dev, x.rs_off, x.out);
+}
+__global__ void k_ix_traces2_b(IxBatch<IxWinTraces> a) {
+    const int k = ixb_pick(a.b0, a.n);
+    const IxWinTraces& w = a.w[k];
+    const int64_t i = (int64_t)((int32_t)blockIdx.x - a.b0[k]) * blockDim.x + threadIdx.x;
+    if (i < w.NT) {
+        const int sd = side_of(w.state[i]);
+        if (sd >= 0 && w.x.g[sd].tflag[i]) {
+            const int32_t p = (int32_t)w.x.g[sd].tpos[i];
+            w.o.g[sd].trace_code[p] = (int32_t)i;
+            w.o.g[sd].len_t[p] = w.tlen[i];
+            w.o.g[sd].rs_off[p] = w.x.g[sd].zoff[i];
+        }
+    }
+    if (i < w.n_po) {
+        const int32_t t = w.po_tr[i];
+        const int sd = side_of(w.state[t]);
+        if (sd >= 0 && w.x.g[sd].tflag[t])
+            w.o.g[sd].rs_ops[w.x.g[sd].zoff[t] + (i - w.po_off[t])] = w.o.g[sd].node_of_code[w.po_op[i]];
+    }
+}
+
+// mr_ix_launch2 for n <= IXW windows at once (each: its table, state, graph pair, builds, size
+// words); det: the windows' detector inputs -- fused into the selection launch (fuse) or a
+// launch of their own before it.  MR_ERR_STATE: a window outside the one-pass limits (the caller
+// then builds window by window).
+int mr_ix_launch2_batch(mr_ctx* ctx, int n, const mr_spans* const* sps, uint8_t* const* d_states, mr_graph* const* g0s,
+                        mr_graph* const* g1s, IxBuild* const* b0s, IxBuild* const* b1s, int64_t* const* d_outs,
+                        const DetIn* dets, bool fuse) {
+    if (n < 1 || n > IXW || getenv("MR_NO_IX2") != nullptr || getenv("MR_NO_IXB") != nullptr) return MR_ERR_STATE;
+    for (int k = 0; k < n; ++k) {
+        const mr_spans* sp = sps[k];
+        if (!sp->ekey.p || sp->n_podops > NS_PMAX || 2 * (3 * (int64_t)sp->n_podops + sp->n_edge_keys) > IX_LDS_WORDS)
+            return MR_ERR_STATE;
+    }
+    hipStream_t st = ctx->stream;
+    IxBatch<IxWinSel> as{};
+    IxBatch<IxWinStats> at{};
+    IxBatch<IxWinCross> ac{};
+    IxBatch<IxWinNodes> an{};
+    IxBatch<IxWinTraces> ar{};
+    as.n = at.n = ac.n = an.n = ar.n = n;
+    int32_t bs = 0, bt = 0, bc = 0, br = 0;
+    size_t lds = 4;
+    int64_t words = 0;
+    std::vector<int64_t> woff((size_t)n);
+    const int TP = fuse ? DB : SEL_TILE;   // traces per selection tile
+    for (int k = 0; k < n; ++k) {
+        const mr_spans* sp = sps[k];
+        const int32_t NT = sp->n_traces, NP = sp->n_podops;
+        const int64_t nek = sp->n_edge_keys;
+        IxSide2 xs;
+        NsArgs2 na;
+        TrOut2 to;
+        IxBuild* b[2] = {b0s[k], b1s[k]};
+        mr_graph* g[2] = {g0s[k], g1s[k]};
+        for (int j = 0; j < 2; ++j) {   // (mr_ix_launch2's buffers)
+            IxBuild& B = *b[j];
+            mr_graph* G = g[j];
+            B.dense = true;
+            B.small = true;
+            B.ecap = (uint64_t)nek;
+            B.gkp = sp->ekey.p;
+            MR_TRY(B.tflag.alloc(ctx, std::max(NT, 1)));
+            MR_TRY(B.tpos.alloc(ctx, (size_t)NT + 1));
+            MR_TRY(B.zoff.alloc(ctx, (size_t)NT + 1));
+            MR_TRY(B.ocnt.alloc(ctx, std::max(NP, 1)));
+            MR_TRY(B.ofirst.alloc(ctx, std::max(NP, 1)));
+            MR_TRY(B.ocov.alloc(ctx, std::max(NP, 1)));
+            MR_TRY(B.gc.alloc(ctx, (size_t)std::max<int64_t>(nek, 1)));
+            MR_TRY(B.node_of_code.alloc(ctx, std::max(NP, 1)));
+            MR_TRY(G->node_podop.alloc(ctx, std::max(NP, 1)));
+            MR_TRY(G->len_o.alloc(ctx, std::max(NP, 1)));
+            MR_TRY(G->nchild.alloc(ctx, std::max(NP, 1)));
+            MR_TRY(G->cov.alloc(ctx, std::max(NP, 1)));
+            MR_TRY(G->ss_par.alloc(ctx, NS_EMAX));
+            MR_TRY(G->ss_off.alloc(ctx, (size_t)NP + 1));
+            MR_TRY(G->trace_code.alloc(ctx, std::max(NT, 1)));
+            MR_TRY(G->len_t.alloc(ctx, std::max(NT, 1)));
+            MR_TRY(G->rs_ops.alloc(ctx, (size_t)std::max<int64_t>(sp->n_po, 1)));
+            MR_TRY(G->rs_off.alloc(ctx, (size_t)NT + 1));
+            xs.g[j] = IxSide{B.tflag.p, B.ocnt.p, B.ofirst.p, B.ocov.p, B.tpos.p, B.zoff.p, B.gc.p};
+            na.g[j] = NsArgs{B.gc.p, B.ocnt.p, B.ofirst.p, B.ocov.p, B.node_of_code.p, G->node_podop.p, G->len_o.p,
+                             G->nchild.p, G->cov.p, G->ss_par.p, G->ss_off.p, B.tpos.p + NT, B.zoff.p + NT, G->rs_off.p,
+                             d_outs[k] + 8 * j};
+            to.g[j] = TrOut{G->trace_code.p, G->len_t.p, G->rs_ops.p, G->rs_off.p, B.node_of_code.p};
+        }
+        const int32_t nt = (int32_t)std::max<int64_t>(cdiv((int64_t)NT, TP), 1);
+        woff[(size_t)k] = words;
+        words += 4 * (int64_t)nt;
+        as.b0[k] = bs;
+        bs += nt;
+        as.w[k] = IxWinSel{dets ? dets[k] : DetIn{}, d_states[k], sp->tlen.p, sp->po_off.p, nullptr, nek, NT, NP, xs};
+        at.b0[k] = bt;
+        if (NT) bt += std::max(1, std::min(256, cdiv(std::max(sp->n_po, sp->n_ed), IX_BT * IX_EPT)));
+        lds = std::max(lds, 2 * (3 * (size_t)NP + (size_t)nek) * sizeof(int32_t));
+        at.w[k] = IxWinStats{d_states[k], sp->po_tr.p, sp->po_op.p, sp->po_cnt.p, sp->po_first.p, sp->ed_tr.p, sp->ed_eid.p,
+                             sp->ed_cnt.p, sp->n_po, sp->n_ed, NP, (int32_t)nek, xs};
+        ac.b0[k] = bc;
+        bc += (int32_t)cdiv(sp->n_xj, 256);
+        ac.w[k] = IxWinCross{d_states[k], sp->xj_tc.p, sp->xj_tp.p, sp->xj_eid.p, sp->n_xj, xs};
+        an.b0[k] = 2 * k;
+        an.w[k] = IxWinNodes{sp->ekey.p, nek, NP, 0, na};
+        ar.b0[k] = br;
+        if (NT || sp->n_po) br += (int32_t)cdiv(std::max<int64_t>(NT, sp->n_po), 256);
+        ar.w[k] = IxWinTraces{d_states[k], sp->tlen.p, sp->po_tr.p, sp->po_op.p, sp->po_off.p, sp->n_po, NT, 0, xs, to};
+    }
+    for (int k = n; k <= IXW; ++k) {   // (offsets past the last window: its end)
+        if (k <= IXW) {
+            as.b0[k] = bs;
+            at.b0[k] = bt;
+            ac.b0[k] = bc;
+            an.b0[k] = 2 * n;
+            ar.b0[k] = br;
+        }
+    }
+    unsigned long long* dst = nullptr;
+    uint64_t epoch = 0;
+    MR_TRY(mr_dl_status(ctx, words, &dst, &epoch));
+    for (int k = 0; k < n; ++k) as.w[k].st = dst + woff[(size_t)k];
+    if (fuse) {
+        hipLaunchKernelGGL(k_ix_detect_scan2_b, dim3(bs), dim3(DB), 0, st, as, epoch);
+    } else {
+        if (dets) {
+            int32_t bd = 0;   // the detector's own launch: DB traces per block
+            IxBatch<IxWinSel> ad = as;
+            for (int k = 0; k < n; ++k) {
+                ad.b0[k] = bd;
+                bd += (int32_t)cdiv((int64_t)sps[k]->n_traces, DB);
+            }
+            for (int k = n; k <= IXW; ++k) ad.b0[k] = bd;
+            if (bd) hipLaunchKernelGGL(k_ix_detect_b, dim3(bd), dim3(DB), 0, st, ad);
+        }
+        hipLaunchKernelGGL(k_ix_sel_scan2_b, dim3(bs), dim3(SEL_T), 0, st, as, epoch);
+    }
+    if (bt) hipLaunchKernelGGL(k_ix_stats2_b, dim3(bt), dim3(IX_BT), lds, st, at);
+    if (bc) hipLaunchKernelGGL(k_ix_cross2_b, dim3(bc), dim3(256), 0, st, ac);
+    hipLaunchKernelGGL(k_nodes_small2_b, dim3(2 * n), dim3(NS_T), 0, st, an);
+    if (br) hipLaunchKernelGGL(k_ix_traces2_b, dim3(br), dim3(256), 0, st, ar);
     MR_TRY_HIP(ctx, hipGetLastError());
     return MR_OK;
 }

@@ -408,6 +408,11 @@ int mr_ix_launch(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d_mask, mr_grap
 struct DetIn;   // (mr_detect_dev.h)
 int mr_ix_launch2(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d_state, mr_graph* g0, mr_graph* g1, IxBuild& b0,
                   IxBuild& b1, int64_t* d_out, const DetIn* det = nullptr);
+// the same for n <= 8 windows, one launch per stage (det: each window's detector inputs, fused
+// into the selection launch when fuse, else launched before it; null: states given)
+int mr_ix_launch2_batch(mr_ctx* ctx, int n, const mr_spans* const* sps, uint8_t* const* d_states, mr_graph* const* g0s,
+                        mr_graph* const* g1s, IxBuild* const* b0s, IxBuild* const* b1s, int64_t* const* d_outs,
+                        const DetIn* dets, bool fuse);
 constexpr int MR_DETECT_SHARDS = 64;
 int mr_detect_indexed_launch(mr_ctx* ctx, const mr_spans* s, int64_t t0, int64_t t1, const double* d_a3,
                              const uint8_t* d_a3v, uint8_t* d_state, unsigned long long* counts);
