@@ -256,6 +256,7 @@ extern "C" void mr_ctx_destroy(mr_ctx* ctx) {
         if (e) (void)hipEventDestroy(e);
     if (ctx->side) (void)hipStreamDestroy(ctx->side);
     if (ctx->pin) (void)hipHostFree(ctx->pin);
+    if (ctx->pin_flags) (void)hipHostFree(ctx->pin_flags);
     if (ctx->scan_st) (void)hipFree(ctx->scan_st);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;

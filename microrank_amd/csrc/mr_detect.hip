@@ -790,6 +790,54 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
     std::thread reaper([&dead] {
         for (mr_graph* g : dead) delete g;
     });
+    // Each group's PageRanks are enqueued without their closing read-back (mr_pagerank_batch_async),
+    // so the next group's go in behind them while they run: the PageRank stream no longer idles
+    // while this thread waits for a group and then enqueues the next (measured: this thread had
+    // spent 12 of a C2 call's 14.5 ms inside the synchronous batch).  A group's error words are
+    // read one group later; only then are its spectra queued (a kind-hash collision reruns the
+    // group synchronously first).  MR_WIN_PR_SYNC=1: the synchronous batch per group.
+    const bool pr_sync = getenv("MR_WIN_PR_SYNC") != nullptr;   // (read per call)
+    {
+        const size_t need = (size_t)8 * n_windows;   // 4 words per graph, 2 graphs per window
+        if (ctx->pin_flags_n < need) {
+            if (ctx->pin_flags) (void)hipHostFree(ctx->pin_flags);
+            ctx->pin_flags = nullptr;
+            ctx->pin_flags_n = 0;
+            if (hipHostMalloc((void**)&ctx->pin_flags, need * sizeof(int32_t), hipHostMallocDefault) != hipSuccess)
+                rc = mr_fail(ctx, MR_ERR_OOM, "mr_windows_batch: pinned error words");
+            else
+                ctx->pin_flags_n = need;
+        }
+    }
+    std::vector<PrAsync*> pend((size_t)ngroups, nullptr);
+    std::vector<std::vector<mr_graph*>> ggs((size_t)ngroups);
+    std::vector<std::vector<int>> gan((size_t)ngroups);
+    auto record = [&](int g) -> int {
+        if (!gev[(size_t)g] && hipEventCreateWithFlags(&gev[(size_t)g], hipEventDisableTiming) != hipSuccess) return MR_ERR_HIP;
+        return hipEventRecord(gev[(size_t)g], ctx->stream) == hipSuccess ? MR_OK : MR_ERR_HIP;
+    };
+    // group g's results are final: check its words (rerun on a collision) and queue its spectra
+    auto settle = [&](int g) -> int {
+        int r = MR_OK;
+        if (pend[(size_t)g]) {
+            bool rerun = false;
+            r = mr_pagerank_async_finish(ctx, pend[(size_t)g], &rerun);
+            mr_pagerank_async_free(pend[(size_t)g]);
+            pend[(size_t)g] = nullptr;
+            if (r == MR_OK && rerun) {
+                r = mr_pagerank_batch(ctx, ggs[(size_t)g].data(), gan[(size_t)g].data(), (int)ggs[(size_t)g].size(), 0.85,
+                                      0.01, 25, precision, 0);
+                if (r == MR_OK) r = record(g);
+            }
+        }
+        const int32_t i0 = g * gsz, i1 = std::min<int32_t>(n_windows, i0 + gsz);
+        std::lock_guard<std::mutex> lk(mu);
+        for (int32_t i = i0; i < i1; ++i)
+            if (r == MR_OK && w[(size_t)i].rc == MR_OK && w[(size_t)i].gn) q.push_back(~i);
+        cv_task.notify_all();
+        return r;
+    };
+    int settled = 0;   // groups whose spectra are queued
     for (int g = 0; g < ngroups && rc == MR_OK; ++g) {
         const int32_t i0 = g * gsz, i1 = std::min<int32_t>(n_windows, i0 + gsz);
         {
@@ -802,8 +850,8 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
                 hipStreamWaitEvent(ctx->stream, cw[c].ev, 0) != hipSuccess)
                 rc = mr_fail(ctx, MR_ERR_HIP, "mr_windows_batch: hipStreamWaitEvent failed");   // (threads joined below)
         if (rc != MR_OK) break;
-        std::vector<mr_graph*> gs;
-        std::vector<int> anom;
+        std::vector<mr_graph*>& gs = ggs[(size_t)g];
+        std::vector<int>& anom = gan[(size_t)g];
         for (int32_t i = i0; i < i1; ++i) {
             WinRun& r = w[(size_t)i];
             n_out[i] = 0;
@@ -817,17 +865,20 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
         }
         if (!gs.empty()) {
             WinPhase ph(6);
-            rc = mr_pagerank_batch(ctx, gs.data(), anom.data(), (int)gs.size(), 0.85, 0.01, 25, precision, 0);
+            if (pr_sync)
+                rc = mr_pagerank_batch(ctx, gs.data(), anom.data(), (int)gs.size(), 0.85, 0.01, 25, precision, 0);
+            else
+                rc = mr_pagerank_batch_async(ctx, gs.data(), anom.data(), (int)gs.size(), 0.85, 0.01, 25, precision,
+                                             ctx->pin_flags + (size_t)8 * i0, &pend[(size_t)g]);
         }
-        if (rc == MR_OK) {
-            if (!gev[(size_t)g]) rc = hipEventCreateWithFlags(&gev[(size_t)g], hipEventDisableTiming) == hipSuccess ? MR_OK : MR_ERR_HIP;
-            if (rc == MR_OK) rc = hipEventRecord(gev[(size_t)g], ctx->stream) == hipSuccess ? MR_OK : MR_ERR_HIP;
-        }
-        std::lock_guard<std::mutex> lk(mu);
-        for (int32_t i = i0; i < i1; ++i)
-            if (rc == MR_OK && w[(size_t)i].rc == MR_OK && w[(size_t)i].gn) q.push_back(~i);
-        cv_task.notify_all();
+        if (rc == MR_OK) rc = record(g);
+        // the previous group's words are in by now, or nearly: settle it (this one stays in flight)
+        for (; rc == MR_OK && settled < (pr_sync ? g + 1 : g); ++settled) rc = settle(settled);
     }
+    for (; rc == MR_OK && settled < ngroups; ++settled) rc = settle(settled);
+    if (rc != MR_OK) (void)hipStreamSynchronize(ctx->stream);   // (an error left groups in flight)
+    for (PrAsync* a : pend)
+        if (a) mr_pagerank_async_free(a);
     {
         std::lock_guard<std::mutex> lk(mu);
         closed = true;

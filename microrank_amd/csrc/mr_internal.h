@@ -56,6 +56,9 @@ struct mr_ctx {
     // pinned host words for the small size read-backs of a call (a DMA straight into host memory
     // instead of the runtime's pageable staging path); created on first use
     int64_t* pin = nullptr;
+    // pinned error words of the PageRank groups a window batch has in flight (grown per call)
+    int32_t* pin_flags = nullptr;
+    size_t pin_flags_n = 0;
     // one-shot peer all-reduce (mr_comm_peer_enable; mr_comm.hip): a receive region in uncached
     // device memory exported by IPC -- [flags: PEER_FLAGS u64][data: 2 parities x nranks x
     // peer_words u64] -- and every rank's region mapped into this process (peer_map[rank] = ours)
@@ -410,6 +413,15 @@ int mr_ix_launch2(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d_state, mr_gr
                   IxBuild& b1, int64_t* d_out, const DetIn* det = nullptr);
 // the same for n <= 8 windows, one launch per stage (det: each window's detector inputs, fused
 // into the selection launch when fuse, else launched before it; null: states given)
+// A PageRank batch enqueued without its closing read-back (mr_windows_batch keeps one group of
+// windows in flight while it enqueues the next): its kernels' descriptors and error words stay
+// alive in the handle; finish waits for it and reports a kind-hash collision (rerun with the
+// synchronous batch) or an error.  hflag: 4 * ng pinned words.
+struct PrAsync;
+int mr_pagerank_batch_async(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly, int ng, double d, double alpha,
+                            int iters, int precision, int32_t* hflag, PrAsync** out);
+int mr_pagerank_async_finish(mr_ctx* ctx, PrAsync* a, bool* rerun);
+void mr_pagerank_async_free(PrAsync* a);
 int mr_ix_launch2_batch(mr_ctx* ctx, int n, const mr_spans* const* sps, uint8_t* const* d_states, mr_graph* const* g0s,
                         mr_graph* const* g1s, IxBuild* const* b0s, IxBuild* const* b1s, int64_t* const* d_outs,
                         const DetIn* dets, bool fuse);

@@ -3861,9 +3861,23 @@ struct HostMarks {
         fprintf(stderr, " us\n");
     }
 };
+struct PrAsync {   // (mr_internal.h) what an enqueued batch's kernels still read, and its error words
+    std::vector<unsigned char> setup_h;
+    DBuf<SDev> setup_d;
+    std::vector<GDev> hv;
+    DBuf<GDev> dv;
+    DBuf<int32_t> fl;
+    hipEvent_t ev = nullptr;
+    int32_t* hflag = nullptr;   // pinned, 4 per graph
+    std::vector<int> anomaly;
+    int ng = 0;
+    ~PrAsync() {
+        if (ev) (void)hipEventDestroy(ev);
+    }
+};
 static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly, int ng, double d, double alpha,
                             int iters, int precision, uint32_t flags, bool sharded, uint64_t seed, uint64_t hmask,
-                            bool* collided, bool* timed_out) {
+                            bool* collided, bool* timed_out, PrAsync* as = nullptr) {
     *collided = false;
     *timed_out = false;
     HostMarks hm(ng);
@@ -4204,6 +4218,19 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         MR_TRY(mr_coll_allreduce(ctx, gs[0]->flag.p, 4, MR_DT_I32, 1));
         MR_TRY_HIP(ctx, hipMemcpyAsync(fl.p, gs[0]->flag.p, 4 * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
     }
+    if (as) {   // enqueued only: the words go to the caller's pinned slot, the finish reads them
+        MR_TRY_HIP(ctx, hipMemcpyAsync(as->hflag, fl.p, (size_t)4 * ng * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+        if (!as->ev) MR_TRY_HIP(ctx, hipEventCreateWithFlags(&as->ev, hipEventDisableTiming));
+        MR_TRY_HIP(ctx, hipEventRecord(as->ev, st));
+        as->setup_h = std::move(setup_h);
+        as->setup_d.swap(setup_d);
+        as->hv = std::move(hv);
+        as->dv.swap(dv);
+        as->fl.swap(fl);
+        as->anomaly.assign(anomaly, anomaly + ng);
+        as->ng = ng;
+        return MR_OK;
+    }
     // the only host round trip of the call: error words raised by the kernels (one pinned read)
     std::vector<int32_t> hflag((size_t)4 * ng, 0);
     if ((size_t)4 * ng * sizeof(int32_t) <= MR_PIN_BYTES) {
@@ -4444,6 +4471,33 @@ extern "C" int mr_pagerank_ex(mr_ctx* ctx, mr_graph* g, int anomaly, double d, d
     g->phi = 0.5;
     return rc;
 }
+
+int mr_pagerank_batch_async(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly, int ng, double d, double alpha,
+                            int iters, int precision, int32_t* hflag, PrAsync** out) {
+    std::unique_ptr<PrAsync> a(new PrAsync());
+    a->hflag = hflag;
+    bool collided = false, timed_out = false;
+    MR_TRY(pagerank_attempt(ctx, gs, anomaly, ng, d, alpha, iters, precision, 0, false, kind_seed(0), kind_hmask(0),
+                            &collided, &timed_out, a.get()));
+    *out = a.release();
+    return MR_OK;
+}
+int mr_pagerank_async_finish(mr_ctx* ctx, PrAsync* a, bool* rerun) {
+    *rerun = false;
+    MR_TRY_HIP(ctx, hipEventSynchronize(a->ev));
+    for (int i = 0; i < a->ng; ++i) {
+        const int32_t* w = a->hflag + 4 * i;
+        if ((w[3] & 1) || (w[0] & 1)) {   // a cluster time-out or a kind-hash collision: the caller reruns
+            if (w[3] & 1) ctx->no_persist = true;   // (as mr_pagerank_batch_impl: per-iteration launches)
+            *rerun = true;
+            return MR_OK;
+        }
+        if (w[2] & 1) return mr_fail(ctx, MR_ERR_STATE, "trace kinds: a partition exceeded its table");
+        if (a->anomaly[(size_t)i] && (w[1] & 1)) return mr_fail(ctx, MR_ERR_ZERODIV, "float division by zero");
+    }
+    return MR_OK;
+}
+void mr_pagerank_async_free(PrAsync* a) { delete a; }
 
 extern "C" int mr_pagerank_batch(mr_ctx* ctx, mr_graph* const* graphs, const int* anomaly, int n_graphs, double d,
                                  double alpha, int iters, int precision, uint32_t flags) {
