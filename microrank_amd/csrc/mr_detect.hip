@@ -677,12 +677,22 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
         const char* e = getenv("MR_WIN_STREAMS");
         return e ? std::max(1, atoi(e)) : 4;
     }();
-    static const int group_size = [] {    // MR_WIN_GROUP: windows whose PageRanks share launches
-        const char* e = getenv("MR_WIN_GROUP");
-        return e ? std::max(1, atoi(e)) : 16;
-    }();
-    const char* ce = getenv("MR_WIN_CHUNK");   // windows built together on one stream (read per call)
-    const int chunk_size = ce ? std::max(1, atoi(ce)) : 4;
+    // Windows whose PageRanks share launches (a group): about WIN_GROUP_TRACES traces per group,
+    // 16..128 windows.  The iteration pair of a small-window group is latency-bound, so its cost per
+    // window falls with the group (C3, 20k-trace windows, on one box: group 16 / 32 / 64 / 128 ->
+    // 9.4k / 12.1k / 14.8k / 15.4k windows/s with chunks of 8 at 128; C2's 200k-trace windows stay
+    // at 16: 32 and 64 within noise there).  A window's trace count is bounded by its table's (a
+    // window of a long shared table gets the small group: the round-2 behaviour).
+    // MR_WIN_GROUP / MR_WIN_CHUNK: fixed group / chunk sizes (read per call)
+    constexpr int64_t WIN_GROUP_TRACES = (int64_t)4 << 20;
+    int64_t tsum_tab = 0;
+    for (int32_t i = 0; i < n_windows; ++i) tsum_tab += std::max<int32_t>(spans[i]->n_traces, 1);
+    const int64_t tper = std::max<int64_t>(1, tsum_tab / n_windows);
+    int group_size = 16;
+    while (group_size < 128 && (int64_t)group_size * 2 * tper <= WIN_GROUP_TRACES) group_size *= 2;
+    if (const char* e = getenv("MR_WIN_GROUP")) group_size = std::max(1, atoi(e));
+    const char* ce = getenv("MR_WIN_CHUNK");   // windows built together on one stream
+    const int chunk_size = ce ? std::max(1, atoi(ce)) : group_size >= 64 ? 8 : 4;
     const int gsz = std::min<int>(n_windows, group_size);
     const int ngroups = (n_windows + gsz - 1) / gsz;
     // build chunks: consecutive windows of one group
