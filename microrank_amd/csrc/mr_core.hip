@@ -90,6 +90,7 @@ static void pool_trim(mr_ctx* ctx) {
         for (auto& kv : c->pool_free)
             for (void* q : kv.second) {
                 (void)hipFree(q);
+                c->pool_all.erase(q);
                 c->pool_bytes -= kv.first;
             }
         c->pool_free.clear();
@@ -98,13 +99,13 @@ static void pool_trim(mr_ctx* ctx) {
     drain(ctx);
 }
 
-void* mr_pool_alloc(mr_ctx* ctx, size_t bytes) {
+void* mr_pool_alloc(mr_ctx* ctx, size_t bytes, size_t* cls) {
     const size_t want = pool_round(bytes);
     std::unique_lock<std::mutex> lk(ctx->pool_mu);
     auto it = ctx->pool_free.lower_bound(want);
     if (it != ctx->pool_free.end() && it->first <= 2 * want) {   // reuse a block at most 2x too big
         void* p = it->second.back();   // (a class is erased when it empties: never empty here)
-        ctx->pool_live[p] = it->first;
+        *cls = it->first;
         it->second.pop_back();
         if (it->second.empty()) ctx->pool_free.erase(it);
         return p;
@@ -121,17 +122,15 @@ void* mr_pool_alloc(mr_ctx* ctx, size_t bytes) {
         }
     }
     ctx->pool_bytes += want;
-    ctx->pool_live[p] = want;
+    ctx->pool_all[p] = want;
+    *cls = want;
     return p;
 }
 
-void mr_pool_free(mr_ctx* ctx, void* p) {
+void mr_pool_free(mr_ctx* ctx, void* p, size_t cls) {
     if (!ctx || !p) return;
     std::lock_guard<std::mutex> lk(ctx->pool_mu);
-    auto it = ctx->pool_live.find(p);
-    if (it == ctx->pool_live.end()) return;
-    ctx->pool_free[it->second].push_back(p);   // stream-ordered reuse: no sync needed
-    ctx->pool_live.erase(it);
+    ctx->pool_free[cls].push_back(p);   // stream-ordered reuse: no sync needed
 }
 
 int mr_read_bytes(mr_ctx* ctx, const void* dev, size_t bytes, unsigned char** host) {
@@ -155,7 +154,11 @@ void mr_pool_release(mr_ctx* ctx) {
     (void)hipStreamSynchronize(ctx->stream);
     std::lock_guard<std::mutex> lk(ctx->pool_mu);
     for (auto& kv : ctx->pool_free)
-        for (void* q : kv.second) (void)hipFree(q);
+        for (void* q : kv.second) {
+            (void)hipFree(q);
+            ctx->pool_all.erase(q);
+            ctx->pool_bytes -= kv.first;
+        }
     ctx->pool_free.clear();
 }
 
@@ -250,8 +253,8 @@ extern "C" void mr_ctx_destroy(mr_ctx* ctx) {
     mr_comm_destroy(ctx);
     prof_clear(ctx);
     mr_pool_release(ctx);
-    for (auto& kv : ctx->pool_live) (void)hipFree(kv.first);   // handles the caller leaked
-    ctx->pool_live.clear();
+    for (auto& kv : ctx->pool_all) (void)hipFree(kv.first);   // blocks of handles the caller leaked
+    ctx->pool_all.clear();
     for (hipEvent_t& e : ctx->side_ev)
         if (e) (void)hipEventDestroy(e);
     if (ctx->side) (void)hipStreamDestroy(ctx->side);

@@ -384,7 +384,8 @@ struct WinPhase {   // adds the scope's duration to phase i when timing is on
 };
 static const char* const WIN_PHASE_NAME[10] = {"chunk launch", "chunk read-back wait", "chunk finish+prepare",
                                                "spectrum task", "worker idle", "main: wait builds",
-                                               "main: pagerank batch", "main: tail", "", ""};
+                                               "main: pagerank batch", "main: tail", "main: call setup",
+                                               "main: release graphs"};
 
 struct WinIn {
     const mr_spans* s;
@@ -538,7 +539,7 @@ static int win_spectrum(mr_ctx* ctx, const mr_spans* s, const WinRun& w, int met
     const int32_t NP = s->n_podops;
     const mr_graph *gn = w.gn, *ga = w.ga;
     const int32_t Na = ga->N, Nn = gn->N;
-    static const bool no_small = getenv("MR_NO_WIN_SPECTRUM_SMALL") != nullptr;   // A/B knob
+    const bool no_small = getenv("MR_NO_WIN_SPECTRUM_SMALL") != nullptr;   // general path (read per call: tests)
     if (!no_small) {   // one block, one read-back (k_win_spectrum) when the window fits it
         const int rc = mr_win_spectrum_small(ctx, Na, ga->node_podop.p, ga->weight.p, ga->cov.p, Nn, gn->node_podop.p,
                                              gn->weight.p, gn->cov.p, NP, w.nn, w.na, method,
@@ -704,6 +705,7 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
     MR_TRY(win_aux(ctx, nthr));
     // the SLO vectors once per distinct (a3, a3_valid, length) of the batch (windows usually share
     // one pair), resident before any window's detector runs
+    std::unique_ptr<WinPhase> ph_setup(new WinPhase(8));
     std::map<std::tuple<const double*, const uint8_t*, int32_t>, size_t> slo_ix;
     std::vector<std::unique_ptr<DBuf<double>>> d_a3;
     std::vector<std::unique_ptr<DBuf<uint8_t>>> d_a3v;
@@ -725,6 +727,8 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
     MR_TRY(slots.alloc(ctx, (size_t)n_windows * MR_WS_SLOT));
     MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));   // uploads done before other streams read them
     static const bool no_index = getenv("MR_NO_INDEX") != nullptr;
+    const bool spec_general = getenv("MR_NO_WIN_SPECTRUM_SMALL") != nullptr;   // (read per call: tests)
+    ph_setup.reset();
     std::vector<WinRun> w((size_t)n_windows);
     std::vector<WinChunk> cw(chunks.size());
     std::vector<hipEvent_t> gev((size_t)ngroups, nullptr);   // a group's PageRanks are done
@@ -779,7 +783,7 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
                     const int32_t i = ~task;
                     WinRun& r = w[(size_t)i];
                     (void)hipStreamWaitEvent(a->stream, gev[(size_t)(i / gsz)], 0);
-                    r.rc = mr_win_spectrum_launch(a, r.ga->N, r.ga->node_podop.p, r.ga->weight.p, r.ga->cov.p, r.gn->N,
+                    r.rc = spec_general ? MR_ERR_STATE : mr_win_spectrum_launch(a, r.ga->N, r.ga->node_podop.p, r.ga->weight.p, r.ga->cov.p, r.gn->N,
                                                   r.gn->node_podop.p, r.gn->weight.p, r.gn->cov.p, spans[i]->n_podops,
                                                   r.nn, r.na, method, K, slots.p + (size_t)i * MR_WS_SLOT);
                     r.slot = r.rc == MR_OK;
@@ -941,8 +945,16 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
         }
     ph_tail.reset();
     if (timing) {
+        {
+            WinPhase ph(9);
+            for (WinRun& r : w) {
+                delete r.gn;
+                delete r.ga;
+                r.gn = r.ga = nullptr;
+            }
+        }
         fprintf(stderr, "[mr_windows_batch] %d windows, %.3f ms:", n_windows, (win_now() - t_call) * 1e-6);
-        for (int i = 0; i < 8; ++i) fprintf(stderr, " %s %.3f ms;", WIN_PHASE_NAME[i], g_phases->ns[i] * 1e-6);
+        for (int i = 0; i < 10; ++i) fprintf(stderr, " %s %.3f ms;", WIN_PHASE_NAME[i], g_phases->ns[i] * 1e-6);
         fprintf(stderr, "\n");
         g_phases = nullptr;
     }

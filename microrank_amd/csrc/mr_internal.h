@@ -38,10 +38,12 @@ struct mr_ctx {
     // so a block released by one call can be handed to the next without a hipFree/hipMalloc
     // (each of which synchronises the device and costs tens of microseconds)
     std::mutex pool_mu;   // (mr_windows_batch releases a call's graphs while its threads allocate)
-    // (free blocks as one stack per size class -- a free is a push, no node allocation; live
-    // blocks hashed: a window batch releases thousands of blocks on the host's critical path)
+    // (free blocks as one stack per size class -- a free is a push, no node allocation; a block's
+    // class travels with its DBuf, so a free needs no lookup of the block: a window batch releases
+    // thousands of blocks on the host's critical path.  pool_all: every block hipMalloc'ed here,
+    // touched only by hipMalloc / hipFree, for the context's destruction)
     std::map<size_t, std::vector<void*>> pool_free;
-    std::unordered_map<void*, size_t> pool_live;
+    std::unordered_map<void*, size_t> pool_all;
     size_t pool_bytes = 0;
     // mr_windows_batch: auxiliary contexts (own stream + pool) for the windows' concurrent
     // detector / graph-build / spectrum phases; created on first use, destroyed with this one
@@ -78,9 +80,9 @@ struct mr_ctx {
     uint32_t scan_epoch = 0;
 };
 
-void* mr_pool_alloc(mr_ctx* ctx, size_t bytes);
+void* mr_pool_alloc(mr_ctx* ctx, size_t bytes, size_t* cls);   // *cls: the block's size class
 void mr_graph_delete(struct mr_graph* g);   // delete a graph (defined where mr_graph is complete)
-void mr_pool_free(mr_ctx* ctx, void* p);
+void mr_pool_free(mr_ctx* ctx, void* p, size_t cls);
 void mr_pool_release(mr_ctx* ctx);
 // n (<= 64) int64 words from the device into out, through the context's pinned words; syncs the stream
 int mr_read_words(mr_ctx* ctx, const int64_t* dev, int n, int64_t* out);
@@ -115,6 +117,7 @@ struct DBuf {
     T* p = nullptr;
     size_t n = 0;
     mr_ctx* owner = nullptr;
+    size_t cls = 0;   // the pool block's size class
     DBuf() = default;
     DBuf(const DBuf&) = delete;
     DBuf& operator=(const DBuf&) = delete;
@@ -123,9 +126,10 @@ struct DBuf {
         std::swap(p, o.p);
         std::swap(n, o.n);
         std::swap(owner, o.owner);
+        std::swap(cls, o.cls);
     }
     void reset() {
-        if (p) mr_pool_free(owner, p);
+        if (p) mr_pool_free(owner, p, cls);
         p = nullptr;
         n = 0;
     }
@@ -133,7 +137,7 @@ struct DBuf {
         if (count <= n && p) return MR_OK;
         reset();
         size_t bytes = (count ? count : 1) * sizeof(T);
-        p = (T*)mr_pool_alloc(ctx, bytes);
+        p = (T*)mr_pool_alloc(ctx, bytes, &cls);
         if (!p) return mr_fail(ctx, MR_ERR_OOM, "device allocation of %zu bytes failed", bytes);
         owner = ctx;
         n = count;

@@ -156,6 +156,22 @@ __global__ void k_gather_top(const uint32_t* idx, const double* score, const uin
 // formula and typing), the stable descending sort and the top k -- instead of ~10 launches and
 // three host round trips.  out: [k] codes (int32, at 0), [k] scores (double, at 8 * WS_KMAX / 2)
 constexpr int WS_T = 1024, WS_MAX = 4096, WS_PMAX = 4096, WS_KMAX = 256;
+// the bitonic network's stages of stride < 64 inside a wave: lane i's element meets lane i ^ stride
+// by a lane exchange (no LDS round trip, no barrier).  size: the merge's block size (direction),
+// strides s_hi, s_hi / 2, .., 1.  (key, index) pairs are unique except the padding's, which are
+// equal to each other (either order of two equal pairs is the same sequence)
+__device__ __forceinline__ void ws_bitonic_lanes(uint64_t& k, uint32_t& v, int32_t i, int32_t size, int32_t s_hi) {
+    for (int32_t stride = s_hi; stride > 0; stride >>= 1) {
+        const uint64_t pk = (uint64_t)__shfl_xor((long long)k, stride, WAVE);
+        const uint32_t pv = (uint32_t)__shfl_xor((int)v, stride, WAVE);
+        const bool lower = (i & stride) == 0, up = (i & size) == 0;
+        const bool gt = k > pk || (k == pk && v > pv);
+        if (lower == up ? gt : !gt) {   // lower half of an ascending pair keeps the min, ...
+            k = pk;
+            v = pv;
+        }
+    }
+}
 __global__ void __launch_bounds__(WS_T) k_win_spectrum(int32_t Na, const int32_t* a_podop, const double* a_w,
                                                       const int32_t* a_cov, int32_t Nn, const int32_t* n_podop,
                                                       const double* n_w, const int32_t* n_cov, int32_t NP, int64_t A,
@@ -177,19 +193,26 @@ __global__ void __launch_bounds__(WS_T) k_win_spectrum(int32_t Na, const int32_t
     for (int i = tid; i < Na; i += WS_T) apos[a_podop[i]] = i;
     __syncthreads();
     // normal-only nodes in normal order: each thread a run of j, a block scan of the run counts
+    // (inclusive scan per wave by lane exchanges, the waves' totals through LDS: two barriers)
     const int per = (Nn + WS_T - 1) / WS_T, j0 = tid * per, j1 = min(j0 + per, Nn);
+    const int lane = tid & (WAVE - 1), wv = tid / WAVE;
     int32_t cnt = 0;
     for (int j = j0; j < j1; ++j) cnt += apos[n_podop[j]] < 0 ? 1 : 0;
-    sbuf[tid] = cnt;
-    __syncthreads();
-    for (int o = 1; o < WS_T; o <<= 1) {
-        const int32_t v = tid >= o ? sbuf[tid - o] : 0;
-        __syncthreads();
-        sbuf[tid] += v;
-        __syncthreads();
+    int32_t inc = cnt;
+#pragma unroll
+    for (int o = 1; o < WAVE; o <<= 1) {
+        const int32_t u = __shfl_up(inc, o, WAVE);
+        if (lane >= o) inc += u;
     }
-    if (tid == WS_T - 1) nonly = sbuf[tid];
-    int32_t pos = Na + sbuf[tid] - cnt;
+    if (lane == WAVE - 1) sbuf[wv] = inc;
+    __syncthreads();
+    int32_t before = 0, total = 0;
+    for (int q = 0; q < WS_T / WAVE; ++q) {
+        before += q < wv ? sbuf[q] : 0;
+        total += sbuf[q];
+    }
+    if (tid == 0) nonly = total;
+    int32_t pos = Na + before + inc - cnt;
     const TV eps{0.0000001, false};
     for (int j = j0; j < j1; ++j) {   // normal-only entries (:60-69)
         const int32_t c = n_podop[j];
@@ -227,8 +250,25 @@ __global__ void __launch_bounds__(WS_T) k_win_spectrum(int32_t Na, const int32_t
         vix[i] = 0xffffffffu;
     }
     __syncthreads();
-    for (int32_t size = 2; size <= m; size <<= 1)
-        for (int32_t stride = size >> 1; stride > 0; stride >>= 1) {
+    // bitonic network: strides >= 64 through LDS (a barrier each), the rest of every merge inside
+    // the waves (ws_bitonic_lanes) -- 10 barriers for m = 512 instead of 45
+    auto lanes = [&](int32_t size_lo, int32_t size_hi) {   // merges size_lo..size_hi, strides < 64
+        for (int32_t i0 = tid - lane; i0 < m; i0 += WS_T) {   // (whole waves: every lane exchanges)
+            const int32_t i = i0 + lane;
+            uint64_t kr = i < m ? key[i] : ~0ull;
+            uint32_t vr = i < m ? vix[i] : 0xffffffffu;
+            for (int32_t size = size_lo; size <= size_hi; size <<= 1)
+                ws_bitonic_lanes(kr, vr, i, size, min(size >> 1, WAVE / 2));
+            if (i < m) {
+                key[i] = kr;
+                vix[i] = vr;
+            }
+        }
+        __syncthreads();
+    };
+    lanes(2, min(m, WAVE));
+    for (int32_t size = 2 * WAVE; size <= m; size <<= 1) {
+        for (int32_t stride = size >> 1; stride >= WAVE; stride >>= 1) {
             for (int32_t i = tid; i < m; i += WS_T) {
                 const int32_t jj = i ^ stride;
                 if (jj > i) {
@@ -246,6 +286,8 @@ __global__ void __launch_bounds__(WS_T) k_win_spectrum(int32_t Na, const int32_t
             }
             __syncthreads();
         }
+        lanes(size, size);
+    }
     const int32_t kk = min(k, n);
     int32_t* oc = (int32_t*)out;
     double* os = (double*)(out + 4 * WS_KMAX);

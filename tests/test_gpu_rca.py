@@ -461,6 +461,41 @@ def test_windows_batch_matches_standalone(c3_window):
         d.close()
 
 
+def test_window_spectrum_one_block_equals_general_path(monkeypatch):
+    """k_win_spectrum (the window's union, scores, bitonic sort -- lane-exchange stages below
+    stride 64 -- and top k in one block) against the general multi-launch spectrum path
+    (MR_NO_WIN_SPECTRUM_SMALL), on windows of 40 to 2500 ops (unions from a few nodes to > 2048:
+    one to four elements per thread) with top lists of 256: codes and scores bitwise equal."""
+    import bench
+    from microrank_amd import _lib
+    from microrank_amd.online_rca import rank_windows
+    from microrank_amd.preprocess_data import DeviceSpans
+
+    ctx = _lib.default_context()
+    wins, devs = [], []
+    for seed, ops in ((501, 40), (502, 300), (503, 700), (504, 1500), (505, 2500)):
+        _, nrm, ab = bench.make_window(seed, ops, 12_000)
+        s3, sok = bench.slo_from_gpu(ctx, nrm)
+        d = DeviceSpans(ctx, ab)
+        devs.append(d)
+        u0 = int(ab.tstart.min())
+        wins.append((d, u0, u0 + 5 * 60 * 10**9, s3, sok))
+    runs = {}
+    for mode in ("one_block", "general"):
+        monkeypatch.delenv("MR_NO_WIN_SPECTRUM_SMALL", raising=False)
+        if mode == "general":
+            monkeypatch.setenv("MR_NO_WIN_SPECTRUM_SMALL", "1")
+        runs[mode] = rank_windows(ctx, wins, top_max=250)
+    lens = []
+    for a, b in zip(runs["one_block"], runs["general"]):
+        assert a[5] == b[5] == 0
+        assert list(a[0]) == list(b[0]) and a[1].tobytes() == b[1].tobytes()
+        lens.append(len(a[0]))
+    assert max(lens) == 256 and min(lens) < 256   # (a window with fewer nodes than k)
+    for d in devs:
+        d.close()
+
+
 def test_windows_batch_fast_paths_equal_general_paths(c3_window, monkeypatch):
     """The window batch's fast paths -- the detector fused into the index pass's first launch
     (k_ix_detect_scan2), both graphs built in one index pass (mr_ix_launch2) with dense edge ids,
