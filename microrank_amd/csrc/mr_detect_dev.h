@@ -32,15 +32,33 @@ __device__ __forceinline__ int detect_block(int32_t NT, const DetIn& d, double* 
     if (blk < 0) blk = (int32_t)blockIdx.x;
     const int32_t tb = blk * DB, te_ = min(tb + DB, NT);
     const int32_t t = tb + threadIdx.x;
+    // the thread's trace, loaded before the block's entries so both latencies overlap
+    bool in = false;
+    int64_t rows = 0, a = 0, b = 0;
+    long long mx = 0;
+    if (t < NT) {
+        const int32_t len = d.tlen[t];
+        const long long ts = d.tts[t], te = d.tte[t];
+        mx = d.tmaxd[t];
+        a = d.sv_off[t];
+        b = d.sv_off[t + 1];
+        in = len > 0 && ts >= d.t0 && te <= d.t1;
+        rows = in ? len : 0;
+    }
+    const bool need = in && mx > 0;   // grouped[grouped['duration'] > 0] (preprocess_data.py:117)
+    // the block's (count * (mean + 3 std)) terms, entry-parallel in stages of DB * DCAP entries
+    // (one product per entry as the reference rounds it; ops without an SLO contribute +0.0, an
+    // exact no-op on the sum); after each stage every thread adds the staged terms of its trace
+    // in name order (T14: a trace's entries are contiguous, the stages ascend -- the sequential
+    // sum of anormaly_detector.py:64-65).  C3 windows carry ~5k entries per block: two stages.
     const int64_t r0 = d.sv_off[tb], r1 = d.sv_off[te_];
-    const bool fits = r1 - r0 <= (int64_t)DB * DCAP;
-    // the block's (count * (mean + 3 std)) terms, entry-parallel: one product per entry as the
-    // reference rounds it; ops without an SLO contribute +0.0 (an exact no-op on the sum)
-    if (fits) {   // all loads of a thread in flight together: ids and counts, then the SLO gathers
-        int32_t op[DCAP], cn[DCAP];
+    double expect = 0.0;
+    for (int64_t c0 = r0; c0 < r1; c0 += (int64_t)DB * DCAP) {   // (block-uniform bounds)
+        const int64_t c1 = min(c0 + (int64_t)DB * DCAP, r1);
+        int32_t op[DCAP], cn[DCAP];   // all loads of a thread in flight together
 #pragma unroll
         for (int j = 0; j < DCAP; ++j) {
-            const int64_t r = min(r0 + threadIdx.x + (int64_t)j * DB, max(r1 - 1, r0));
+            const int64_t r = min(c0 + threadIdx.x + (int64_t)j * DB, c1 - 1);
             op[j] = d.sv_op[r];
             cn[j] = d.sv_cnt[r];
         }
@@ -53,32 +71,17 @@ __device__ __forceinline__ int detect_block(int32_t NT, const DetIn& d, double* 
         }
 #pragma unroll
         for (int j = 0; j < DCAP; ++j) {
-            const int64_t r = r0 + threadIdx.x + (int64_t)j * DB;
-            if (r < r1) term[r - r0] = vv[j] ? (double)cn[j] * av[j] : 0.0;
+            const int64_t r = c0 + threadIdx.x + (int64_t)j * DB;
+            if (r < c1) term[r - c0] = vv[j] ? (double)cn[j] * av[j] : 0.0;
         }
+        __syncthreads();
+        if (need)
+            for (int64_t r = max(a, c0), re = min(b, c1); r < re; ++r) expect += term[r - c0];
+        __syncthreads();
     }
-    __syncthreads();
     int st = 0;
-    int64_t rows = 0;
     if (t < NT) {
-        const bool in = d.tlen[t] > 0 && d.tts[t] >= d.t0 && d.tte[t] <= d.t1;
-        if (in) {
-            rows = d.tlen[t];
-            const long long mx = d.tmaxd[t];
-            if (mx > 0) {   // grouped[grouped['duration'] > 0] (preprocess_data.py:117)
-                double expect = 0.0;
-                const int64_t a = d.sv_off[t], b = d.sv_off[t + 1];
-                if (fits) {
-                    for (int64_t r = a; r < b; ++r) expect += term[r - r0];   // name order (T14)
-                } else {
-                    for (int64_t r = a; r < b; ++r) {
-                        const int32_t op = d.sv_op[r];
-                        if (d.a3v[op]) expect += (double)d.sv_cnt[r] * d.a3[op];   // anormaly_detector.py:64-65
-                    }
-                }
-                st = (double)mx / 1000.0 > expect ? 2 : 1;                   // :58, :69
-            }
-        }
+        if (need) st = (double)mx / 1000.0 > expect ? 2 : 1;   // :58, :69
         d.state[t] = (uint8_t)st;
     }
     // counts: per wave, per block, then one add per block into one of CSH shards (~200k traces
