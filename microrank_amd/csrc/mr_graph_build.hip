@@ -1786,6 +1786,8 @@ int mr_ix_launch2_batch(mr_ctx* ctx, int n, const mr_spans* const* sps, uint8_t*
     hipStream_t st = ctx->stream;
     IxBatch<IxWinSel> as{};
     IxBatch<IxWinStats> at{};
+    const char* ee = getenv("MR_IX_EPT");   // (A/B knob, read per call)
+    const int ept = ee ? std::max(1, atoi(ee)) : IX_EPT;
     IxBatch<IxWinCross> ac{};
     IxBatch<IxWinNodes> an{};
     IxBatch<IxWinTraces> ar{};
@@ -1842,7 +1844,7 @@ int mr_ix_launch2_batch(mr_ctx* ctx, int n, const mr_spans* const* sps, uint8_t*
         bs += nt;
         as.w[k] = IxWinSel{dets ? dets[k] : DetIn{}, d_states[k], sp->tlen.p, sp->po_off.p, nullptr, nek, NT, NP, xs};
         at.b0[k] = bt;
-        if (NT) bt += std::max(1, std::min(256, cdiv(std::max(sp->n_po, sp->n_ed), IX_BT * IX_EPT)));
+        if (NT) bt += std::max(1, std::min(256, cdiv(std::max(sp->n_po, sp->n_ed), (int64_t)IX_BT * ept)));
         lds = std::max(lds, 2 * (3 * (size_t)NP + (size_t)nek) * sizeof(int32_t));
         at.w[k] = IxWinStats{d_states[k], sp->po_tr.p, sp->po_op.p, sp->po_cnt.p, sp->po_first.p, sp->ed_tr.p, sp->ed_eid.p,
                              sp->ed_cnt.p, sp->n_po, sp->n_ed, NP, (int32_t)nek, xs};

@@ -2230,9 +2230,34 @@ __global__ void __launch_bounds__(WAVE * FB_W) k_fx_b(const GDev* __restrict__ g
         const GLB int64_t* ss_off = gp(G.ss_off);
         const GLB int32_t* ss_par = gp(G.ss_par);
         const GLB float* pw = gp(G.pw);
-        for (int32_t j = w; j < OPB; j += FB_W) {
-            const int32_t oj = o0 + j;
-            if (oj >= N) break;
+        // the wave's ops j = w, w + FB_W, ..: one lane each for ops of <= 8 parents -- the lane
+        // forms the wave sum's value itself (the butterfly of wave_sum over 64 slots with the
+        // terms in slots 0..7 and zeros elsewhere: adding +0.0 is exact, so only the pairs
+        // (l, l+4), (l, l+2), (0, 1) round) -- all the wave's ops in one chain of loads instead
+        // of one chain per op; ops with more parents take the wave path after them
+        const int32_t nj = (OPB - w + FB_W - 1) / FB_W;
+        bool big = false;
+        if (lane < nj) {
+            const int32_t j = w + lane * FB_W, oj = o0 + j;
+            if (oj < N) {
+                const int32_t opj = G.perm ? G.perm[oj] : oj;
+                const int64_t e0 = ss_off[opj], e1 = ss_off[opj + 1];
+                if (e1 - e0 <= 8) {
+                    int32_t pp[8];
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) pp[k] = e0 + k < e1 ? ss_par[e0 + k] : -1;
+                    double t[8];
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) t[k] = pp[k] >= 0 ? (double)pw[pp[k]] * sp_cur[pp[k]] : 0.0;
+                    const double bb = ((t[0] + t[4]) + (t[2] + t[6])) + ((t[1] + t[5]) + (t[3] + t[7]));
+                    lssv[j] = G.alpha * (bb / Ms);
+                } else {
+                    big = true;
+                }
+            }
+        }
+        for (uint64_t bm = __ballot(big); bm; bm &= bm - 1) {   // (wave-uniform)
+            const int32_t j = w + (int32_t)(__ffsll((unsigned long long)bm) - 1) * FB_W, oj = o0 + j;
             const int32_t opj = G.perm ? G.perm[oj] : oj;
             const int64_t e0 = ss_off[opj], e1 = ss_off[opj + 1];
             double bb = 0.0;
