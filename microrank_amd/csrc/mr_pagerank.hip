@@ -2358,7 +2358,7 @@ constexpr int PC_MAXB = 64;                               // blocks of one clust
 // (offsets, parents, fp32(1/nchild)): graph constants staged once, so the per-iteration call-graph
 // term is LDS reads, not chains of dependent global loads
 struct PcLds {
-    size_t lacc, su, s0, s1, soff, spar, spw, total;
+    size_t lacc, su, s0, s1, soff, spar, spw, big, total;
     __host__ __device__ PcLds(int32_t N, int64_t E) {
         const TrLds t(N, WV_SU_ALL);   // the accumulator and su as k_tr_a's
         auto up = [](size_t b) { return (b + 15) / 16 * 16; };
@@ -2369,7 +2369,8 @@ struct PcLds {
         soff = s1 + up((size_t)N * 8);
         spar = soff + up(((size_t)N + 1) * 4);
         spw = spar + up((size_t)E * 4);
-        total = spw + up((size_t)N * 4);
+        big = spw + up((size_t)N * 4);   // [0] count, then the ops of > 8 parents
+        total = big + up(((size_t)N + 1) * 4);
     }
 };
 template <class Q, int NT>
@@ -2392,6 +2393,7 @@ __global__ void __launch_bounds__(NT) k_pr_cluster(const GDev* __restrict__ gs, 
     int32_t* l_soff = (int32_t*)(lraw + L.soff);
     int32_t* l_spar = (int32_t*)(lraw + L.spar);
     float* l_spw = (float*)(lraw + L.spw);
+    int32_t* l_big = (int32_t*)(lraw + L.big);
     // (global-address views: the hand-off's sc1 loads / stores and atomics must be global_, not flat_)
     GLB unsigned long long* mslot = gpw(G.mslot);
     GLB unsigned long long* cnt = mslot + 6 * MSH;
@@ -2409,6 +2411,10 @@ __global__ void __launch_bounds__(NT) k_pr_cluster(const GDev* __restrict__ gs, 
         if (o <= N) l_soff[o] = (int32_t)G.ss_off[o];
     }
     for (int64_t e = tid; e < E; e += NT) l_spar[e] = G.ss_par[e];
+    if (tid == 0) l_big[0] = 0;
+    __syncthreads();
+    for (int32_t o = tid; o < N; o += NT)   // the ops the (C) pass sums a wave each (any order)
+        if (l_soff[o + 1] - l_soff[o] > 8) l_big[1 + atomicAdd(&l_big[0], 1)] = o;
     if (tid < WAVE) {
         const double ms = wave_max(bits2d(mslot[tid]));
         const double mr = wave_max(bits2d(mslot[MSH + tid]));
@@ -2460,8 +2466,23 @@ __global__ void __launch_bounds__(NT) k_pr_cluster(const GDev* __restrict__ gs, 
                 if (tid == 0) mb[1] = mr;
             }
         }
-        // the call-graph term alpha (P_ss s_k)[o] / M_s(k): a wave per op (k_fx_b's order)
-        for (int32_t o = wv; o < N; o += NW) {
+        // the call-graph term alpha (P_ss s_k)[o] / M_s(k) in k_fx_b's order: a thread per op of
+        // <= 8 parents (wave_sum's butterfly value formed by the thread, as k_fx_b's lanes), a
+        // wave per op of more
+        for (int32_t o = tid; o < N; o += NT) {
+            const int32_t e0 = l_soff[o], e1 = l_soff[o + 1];
+            if (e1 - e0 > 8) continue;
+            double t[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int32_t p = e0 + k < e1 ? l_spar[e0 + k] : -1;
+                t[k] = p >= 0 ? (double)l_spw[p] * s_cur[p] : 0.0;
+            }
+            const double bb = ((t[0] + t[4]) + (t[2] + t[6])) + ((t[1] + t[5]) + (t[3] + t[7]));
+            s_nxt[o] = G.alpha * (bb / Ms);
+        }
+        for (int32_t i = wv; i < l_big[0]; i += NW) {
+            const int32_t o = l_big[1 + i];
             double bb = 0.0;
             for (int32_t e = l_soff[o] + lane; e < l_soff[o + 1]; e += WAVE) {
                 const int32_t p = l_spar[e];
