@@ -678,14 +678,15 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
         const char* e = getenv("MR_WIN_STREAMS");
         return e ? std::max(1, atoi(e)) : 4;
     }();
-    // Windows whose PageRanks share launches (a group): about WIN_GROUP_TRACES traces per group,
+    // Windows whose PageRanks share launches (a group): at most WIN_GROUP_TRACES traces per group,
     // 16..128 windows.  The iteration pair of a small-window group is latency-bound, so its cost per
     // window falls with the group (C3, 20k-trace windows, on one box: group 16 / 32 / 64 / 128 ->
-    // 9.4k / 12.1k / 14.8k / 15.4k windows/s with chunks of 8 at 128; C2's 200k-trace windows stay
-    // at 16: 32 and 64 within noise there).  A window's trace count is bounded by its table's (a
-    // window of a long shared table gets the small group: the round-2 behaviour).
+    // 9.4k / 12.1k / 14.8k / 15.4k windows/s with chunks of 8 at 128; C2, 200k-trace windows in
+    // calls of 64: group 16 / 32 -> 4578 / 4773 windows/s, iteration frac 0.355 / 0.51, two
+    // repeats each on one box).  A window's trace count is bounded by its table's (a window of a
+    // long shared table gets the small group: the round-2 behaviour).
     // MR_WIN_GROUP / MR_WIN_CHUNK: fixed group / chunk sizes (read per call)
-    constexpr int64_t WIN_GROUP_TRACES = (int64_t)4 << 20;
+    constexpr int64_t WIN_GROUP_TRACES = (int64_t)8 << 20;
     int64_t tsum_tab = 0;
     for (int32_t i = 0; i < n_windows; ++i) tsum_tab += std::max<int32_t>(spans[i]->n_traces, 1);
     const int64_t tper = std::max<int64_t>(1, tsum_tab / n_windows);
@@ -695,11 +696,23 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
     const char* ce = getenv("MR_WIN_CHUNK");   // windows built together on one stream
     const int chunk_size = ce ? std::max(1, atoi(ce)) : group_size >= 64 ? 8 : 4;
     const int gsz = std::min<int>(n_windows, group_size);
-    const int ngroups = (n_windows + gsz - 1) / gsz;
+    // group g: windows [gbeg[g], gbeg[g + 1]).  MR_WIN_RAMP=k (read per call): a first group of k
+    // windows, so the PageRank stream starts after k builds instead of a whole group's (C2: 4 / 8 /
+    // 16 with groups of 20-30 within noise of plain groups of 32 -- not default)
+    std::vector<int32_t> gbeg(1, 0);
+    if (const char* re = getenv("MR_WIN_RAMP")) {
+        const int32_t k = std::max(0, atoi(re));
+        if (k > 0 && k < n_windows) gbeg.push_back(k);
+    }
+    while (gbeg.back() < n_windows) gbeg.push_back(std::min<int32_t>(n_windows, gbeg.back() + gsz));
+    const int ngroups = (int)gbeg.size() - 1;
+    std::vector<int32_t> group_of((size_t)n_windows);
+    for (int g = 0; g < ngroups; ++g)
+        for (int32_t i = gbeg[(size_t)g]; i < gbeg[(size_t)g + 1]; ++i) group_of[(size_t)i] = g;
     // build chunks: consecutive windows of one group
     std::vector<std::pair<int32_t, int32_t>> chunks;
     for (int g = 0; g < ngroups; ++g)
-        for (int32_t i = g * gsz, e = std::min<int32_t>(n_windows, (g + 1) * gsz); i < e; i += chunk_size)
+        for (int32_t i = gbeg[(size_t)g], e = gbeg[(size_t)g + 1]; i < e; i += chunk_size)
             chunks.emplace_back(i, std::min<int32_t>(e, i + chunk_size));
     const int nthr = std::min<int>((int)chunks.size(), max_streams);
     MR_TRY(win_aux(ctx, nthr));
@@ -776,13 +789,13 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
                         }
                     }
                     std::lock_guard<std::mutex> lk(mu);
-                    built[(size_t)(i0 / gsz)] += i1 - i0;
+                    built[(size_t)group_of[(size_t)i0]] += i1 - i0;
                     cv_done.notify_all();
                 } else {           // spectrum, after the group's PageRanks (an event, not a host wait)
                     WinPhase ph(3);
                     const int32_t i = ~task;
                     WinRun& r = w[(size_t)i];
-                    (void)hipStreamWaitEvent(a->stream, gev[(size_t)(i / gsz)], 0);
+                    (void)hipStreamWaitEvent(a->stream, gev[(size_t)group_of[(size_t)i]], 0);
                     r.rc = spec_general ? MR_ERR_STATE : mr_win_spectrum_launch(a, r.ga->N, r.ga->node_podop.p, r.ga->weight.p, r.ga->cov.p, r.gn->N,
                                                   r.gn->node_podop.p, r.gn->weight.p, r.gn->cov.p, spans[i]->n_podops,
                                                   r.nn, r.na, method, K, slots.p + (size_t)i * MR_WS_SLOT);
@@ -844,7 +857,7 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
                 if (r == MR_OK) r = record(g);
             }
         }
-        const int32_t i0 = g * gsz, i1 = std::min<int32_t>(n_windows, i0 + gsz);
+        const int32_t i0 = gbeg[(size_t)g], i1 = gbeg[(size_t)g + 1];
         std::lock_guard<std::mutex> lk(mu);
         for (int32_t i = i0; i < i1; ++i)
             if (r == MR_OK && w[(size_t)i].rc == MR_OK && w[(size_t)i].gn) q.push_back(~i);
@@ -853,7 +866,7 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
     };
     int settled = 0;   // groups whose spectra are queued
     for (int g = 0; g < ngroups && rc == MR_OK; ++g) {
-        const int32_t i0 = g * gsz, i1 = std::min<int32_t>(n_windows, i0 + gsz);
+        const int32_t i0 = gbeg[(size_t)g], i1 = gbeg[(size_t)g + 1];
         {
             std::unique_lock<std::mutex> lk(mu);
             WinPhase ph(5);
