@@ -1008,11 +1008,13 @@ def main():
                    "edges_per_window": int(edges // max(n_win, 1)),
                    "windows_per_step": (win_all // args.steps) if c3 else W,
                    "parallelism": (f"windows x{world} ranks, mr_windows_batch of {W} windows per call "
-                                   f"(the PageRanks of a group of 16 windows share each iteration's launches)") if batch
+                                   f"(the PageRanks of a group of windows -- up to 8M traces, 16..128 windows -- share each "
+                                   f"iteration's launches)") if batch
                                   else f"windows x{world} ranks x{W} streams"},
         "windows_per_s": round(win_all / elapsed, 3),
         "roofline": {"bound": "hbm", "kernel": ("one Jacobi iteration of a window group's graphs: the "
-                                                "k_tr_a + k_fx_b launch pair over the 32 graphs of 16 windows") if batch else
+                                                "k_tr_a + k_fx_b launch pair over the graphs of one group (c2: 64 graphs of 32 "
+                                                "windows; c3: 256 graphs of 128)") if batch else
                                                ("one Jacobi iteration: k_tr_a + k_fx_b (fused path)"
                                                 + (f", stream 0 of {W} concurrent windows" if W > 1 else "")),
                      "achieved": round(achieved, 1),
