@@ -1,6 +1,6 @@
 """GPU busy time from a rocprofv3 kernel_trace.csv: union of kernel intervals over the last
-SPAN ms of the trace (SPAN 0: the run of kernels with no gap > 20 ms that lasts longest
-(wall) -- the timed steps), the sum of kernel durations (concurrency = sum / union), and the
+SPAN ms of the trace (SPAN 0: the run of kernels with no gap > 20 ms that holds the most
+k_tr_a launches -- the timed steps), the sum of kernel durations (concurrency = sum / union), and the
 kernels' share of the sum.   python3 scripts/ktrace_busy.py TRACE.csv SPAN_MS [TOP]"""
 import csv
 import sys
@@ -22,7 +22,7 @@ else:
         cur.append(x)
         hi = x[1] if hi is None or not cur[:-1] else max(hi, x[1])
     segs.append(cur)
-    iv = max(segs, key=lambda sg: max(e for _, e, *_ in sg) - sg[0][0])   # the longest in wall time
+    iv = max(segs, key=lambda sg: (sum('k_tr_a' in x[2] for x in sg), len(sg)))   # the most iterations
 t_end = max(e for _, e, _ in iv)
 busy, cur_s, cur_e, tot = 0, None, None, 0
 per = defaultdict(lambda: [0, 0])

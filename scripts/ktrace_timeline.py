@@ -19,7 +19,7 @@ for x in iv:
     cur.append(x)
     hi = x[1] if hi is None else max(hi, x[1])
 segs.append(cur)
-iv = max(segs, key=lambda sg: max(e for _, e, *_ in sg) - sg[0][0])   # the longest in wall time
+iv = max(segs, key=lambda sg: (sum('k_tr_a' in x[2] for x in sg), len(sg)))   # the most iterations
 t0 = (iv[0][0] + max(e for _, e, _, _ in iv)) / 2
 t1 = t0 + span
 
