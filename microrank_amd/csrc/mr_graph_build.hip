@@ -1753,20 +1753,22 @@ __global__ void k_ix_traces2_b(IxBatch<IxWinTraces> a) {
     const int k = ixb_pick(a.b0, a.n);
     const IxWinTraces& w = a.w[k];
     const int64_t i = (int64_t)((int32_t)blockIdx.x - a.b0[k]) * blockDim.x + threadIdx.x;
+    // (a trace is in graph sd iff its state's side is sd and it has rows -- the selection scan's
+    // tflag, read from the state here: one gather less per entry; a trace with entries has rows)
     if (i < w.NT) {
         const int sd = side_of(w.state[i]);
-        if (sd >= 0 && w.x.g[sd].tflag[i]) {
+        const int32_t len = w.tlen[i];
+        if (sd >= 0 && len > 0) {
             const int32_t p = (int32_t)w.x.g[sd].tpos[i];
             w.o.g[sd].trace_code[p] = (int32_t)i;
-            w.o.g[sd].len_t[p] = w.tlen[i];
+            w.o.g[sd].len_t[p] = len;
             w.o.g[sd].rs_off[p] = w.x.g[sd].zoff[i];
         }
     }
     if (i < w.n_po) {
-        const int32_t t = w.po_tr[i];
+        const int32_t t = w.po_tr[i], op = w.po_op[i];
         const int sd = side_of(w.state[t]);
-        if (sd >= 0 && w.x.g[sd].tflag[t])
-            w.o.g[sd].rs_ops[w.x.g[sd].zoff[t] + (i - w.po_off[t])] = w.o.g[sd].node_of_code[w.po_op[i]];
+        if (sd >= 0) w.o.g[sd].rs_ops[w.x.g[sd].zoff[t] + (i - w.po_off[t])] = w.o.g[sd].node_of_code[op];
     }
 }
 

@@ -2180,7 +2180,17 @@ __global__ void __launch_bounds__(NT) k_tr_a(const GDev* __restrict__ gs, int32_
 constexpr int FB_W = 16, FB_W_SMALL = 4, FB_SMALL_ROWS = 256;
 // ops per k_fx_b block: a lane reads op (lane % ops) of every (64/ops)-th row of its wave's share,
 // so a row read stays one 128-B line per op group while small graphs still spread over many CUs
-static int fb_ops(int32_t N) { return N <= 8192 ? 16 : 32; }
+// A batch of many small graphs (C2 / C3 window groups: thousands of 16-op blocks, several rounds
+// of the chip) takes 64 ops per block instead: lane = op, one row group per wave -- the same
+// integer limb sums and call-graph terms, so bitwise the same results.  MR_FB_OPS: force 16 / 32 /
+// 64 (read per call: tests)
+static int fb_ops(int32_t N, bool many) {
+    const char* e = getenv("MR_FB_OPS");
+    const int force = e ? atoi(e) : 0;
+    if (force == 16 || force == 32 || force == 64) return force;
+    return N <= 8192 ? (many ? 64 : 16) : 32;
+}
+constexpr int64_t FB_MANY_BLOCKS = 1024;   // 16-op blocks of a launch from which "many" holds
 template <int FB_W>
 __global__ void __launch_bounds__(WAVE * FB_W) k_fx_b(const GDev* __restrict__ gs, int32_t ng, int32_t split,
                                                      double d, int it, int mode) {
@@ -4006,6 +4016,10 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
     int mask = 3;
     if (const char* rm = getenv("MR_ROLE_MASK")) mask = atoi(rm);   // profiling knob: 1 trace / 2 op side
     std::vector<GDev> hv((size_t)ng);
+    int64_t fb16 = 0;   // k_fx_b blocks of the launch at 16 ops per block
+    for (int i = 0; i < ng; ++i)
+        if (gs[i]->fused) fb16 += cdiv(gs[i]->N, 16);
+    const bool fb_many = fb16 > FB_MANY_BLOCKS;
     int32_t blocks_a = 0, blocks_b = 0, blocks_fa = 0, blocks_fb = 0;
     size_t lds = VCAP * sizeof(double), lds_f = 0;
     double bytes = 0.0;
@@ -4103,7 +4117,7 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         v.n_fa = (int32_t)nfa;
         blocks_fa += v.n_fa;
         v.blk0fb = blocks_fb;
-        v.fb_ops = fb_ops(g->N);
+        v.fb_ops = fb_ops(g->N, fb_many);
         v.n_fb = g->fused ? cdiv(g->N, v.fb_ops) : 0;
         blocks_fb += v.n_fb;
         v.blk0 = blocks_a;

@@ -496,6 +496,39 @@ def test_window_spectrum_one_block_equals_general_path(monkeypatch):
         d.close()
 
 
+def test_windows_batch_fx_ops_per_block_bitwise(c3_window, monkeypatch):
+    """k_fx_b's ops per block (16 for few graphs, 64 for batches of many: MR_FB_OPS forces either)
+    only regroups the integer limb sums and the per-op call-graph terms: a 4-window batch ranks
+    bitwise the same with 16, 32 and 64."""
+    import bench
+    from microrank_amd import _lib
+    from microrank_amd.online_rca import rank_windows
+    from microrank_amd.preprocess_data import DeviceSpans
+
+    ctx = _lib.default_context()
+    normal, abnormal, t0, t1 = c3_window
+    a3, ok = bench.slo_from_gpu(ctx, normal)
+    devs = [DeviceSpans(ctx, abnormal)]
+    wins = [(devs[0], t0, t1, a3, ok)]
+    for seed in (71, 72, 73):
+        _, nrm, ab = bench.make_window(seed, 500, 20_000)
+        s3, sok = bench.slo_from_gpu(ctx, nrm)
+        d = DeviceSpans(ctx, ab)
+        devs.append(d)
+        u0 = int(ab.tstart.min())
+        wins.append((d, u0, u0 + 5 * 60 * 10**9, s3, sok))
+    runs = {}
+    for v in ("16", "32", "64"):
+        monkeypatch.setenv("MR_FB_OPS", v)
+        runs[v] = rank_windows(ctx, wins, top_max=60)
+    for v in ("32", "64"):
+        for a, b in zip(runs["16"], runs[v]):
+            assert a[5] == b[5] == 0
+            assert a[2:] == b[2:] and list(a[0]) == list(b[0]) and a[1].tobytes() == b[1].tobytes(), v
+    for d in devs:
+        d.close()
+
+
 def test_windows_batch_fast_paths_equal_general_paths(c3_window, monkeypatch):
     """The window batch's fast paths -- the detector fused into the index pass's first launch
     (k_ix_detect_scan2), both graphs built in one index pass (mr_ix_launch2) with dense edge ids,
