@@ -1431,7 +1431,7 @@ struct GDev {
     const uint16_t* rs16;       // u16 copy of rs_ops (N <= 65536) or null
     const uint16_t* rsw;        // the fused kernel's ids: rs16, or rsp in relabelled ops
     const int32_t* perm;        // relabelled ops: perm[new] = old (null: identity)
-    int32_t n_hot;              // k_wv_a / k_tr_a: su of ops [0, n_hot) in LDS (relabelled graphs)
+    int32_t n_hot;              // k_tr_a: su of ops [0, n_hot) in LDS (relabelled graphs)
     const uint16_t* tids;       // k_tr_a: lane-interleaved id chunks of the wave tiles
     const int32_t* coff;        // [n_wt+1] first chunk of a tile
     const int32_t* wtile;       // [waves+1] first tile of each wave of the launch
@@ -3527,7 +3527,7 @@ int mr_graph_prepare(mr_ctx* ctx, mr_graph* g) {
             hipLaunchKernelGGL(k_cov_hist, dim3(cdiv(nnz, 256 * 64)), dim3(256), (size_t)N * sizeof(int32_t), st,
                                g->rs16.p, nnz, N, g->cov.p);
         // su does not fit in LDS beside the accumulators: relabel ops by descending coverage so
-        // k_wv_a stages the su of the most covered ops (ops [0, n_hot)) and gathers the rest.
+        // k_tr_a stages the su of the most covered ops (ops [0, n_hot)) and gathers the rest.
         // The kinds keep rs16 (original labels, the same hash on every rank); only the
         // iteration's id stream (rsp), su and the partial rows use the new labels.
         g->relabeled = !TrLds(N, WV_SU_ALL).su_lds;
