@@ -741,15 +741,19 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
     MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));   // uploads done before other streams read them
     static const bool no_index = getenv("MR_NO_INDEX") != nullptr;
     const bool spec_general = getenv("MR_NO_WIN_SPECTRUM_SMALL") != nullptr;   // (read per call: tests)
+    const char* sbe = getenv("MR_WIN_SPEC_BATCH");   // windows per spectrum launch, 1..MR_WS_BATCH (A/B)
+    const int spec_batch = sbe ? std::min(MR_WS_BATCH, std::max(1, atoi(sbe))) : MR_WS_BATCH;
     ph_setup.reset();
     std::vector<WinRun> w((size_t)n_windows);
     std::vector<WinChunk> cw(chunks.size());
     std::vector<hipEvent_t> gev((size_t)ngroups, nullptr);   // a group's PageRanks are done
     std::vector<std::string> err((size_t)nthr);
-    // task queue: phase-1 tasks (chunk c -> c) first, phase-3 tasks (window i -> ~i) appended per group
+    // task queue: phase-1 tasks (chunk c -> c) first, phase-3 tasks (the spectra of spec[i] -> ~i)
+    // appended per group
     std::mutex mu;
     std::condition_variable cv_task, cv_done;
     std::deque<int32_t> q;
+    std::vector<std::vector<int32_t>> spec((size_t)n_windows);   // a spectrum task's windows (by its first)
     bool closed = false;
     std::vector<int> built((size_t)ngroups, 0);
     for (int32_t c = 0; c < (int32_t)chunks.size(); ++c) q.push_back(c);
@@ -791,20 +795,39 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
                     std::lock_guard<std::mutex> lk(mu);
                     built[(size_t)group_of[(size_t)i0]] += i1 - i0;
                     cv_done.notify_all();
-                } else {           // spectrum, after the group's PageRanks (an event, not a host wait)
-                    WinPhase ph(3);
-                    const int32_t i = ~task;
-                    WinRun& r = w[(size_t)i];
-                    (void)hipStreamWaitEvent(a->stream, gev[(size_t)group_of[(size_t)i]], 0);
-                    r.rc = spec_general ? MR_ERR_STATE : mr_win_spectrum_launch(a, r.ga->N, r.ga->node_podop.p, r.ga->weight.p, r.ga->cov.p, r.gn->N,
-                                                  r.gn->node_podop.p, r.gn->weight.p, r.gn->cov.p, spans[i]->n_podops,
-                                                  r.nn, r.na, method, K, slots.p + (size_t)i * MR_WS_SLOT);
-                    r.slot = r.rc == MR_OK;
-                    if (r.rc == MR_ERR_STATE)   // past the one-block limits: the general path (synchronous)
+                } else {           // spectra of up to MR_WS_BATCH windows, after their group's PageRanks
+                    WinPhase ph(3);   // (an event, not a host wait; one launch, a block per window)
+                    const std::vector<int32_t>& ids = spec[(size_t)~task];
+                    (void)hipStreamWaitEvent(a->stream, gev[(size_t)group_of[(size_t)ids[0]]], 0);
+                    MrWsWin ws[MR_WS_BATCH];
+                    int nb = 0;
+                    std::vector<int32_t> general;
+                    for (int32_t i : ids) {
+                        const WinRun& r = w[(size_t)i];
+                        if (spec_general || !mr_win_spectrum_fits(r.ga->N, r.gn->N, spans[i]->n_podops, K)) {
+                            general.push_back(i);
+                            continue;
+                        }
+                        ws[nb++] = MrWsWin{r.ga->node_podop.p, r.ga->cov.p, r.gn->node_podop.p, r.gn->cov.p, r.ga->weight.p,
+                                           r.gn->weight.p, slots.p + (size_t)i * MR_WS_SLOT, r.nn, r.na, r.ga->N,
+                                           r.gn->N, spans[i]->n_podops};
+                    }
+                    if (nb) {
+                        const int rc = mr_win_spectrum_launch_n(a, ws, nb, method, K);
+                        for (int32_t i : ids)
+                            if (std::find(general.begin(), general.end(), i) == general.end()) {
+                                w[(size_t)i].rc = rc;
+                                w[(size_t)i].slot = rc == MR_OK;
+                            }
+                        if (rc != MR_OK) err[(size_t)k] = a->err;
+                    }
+                    for (int32_t i : general) {   // past the one-block limits: the general path (synchronous)
+                        WinRun& r = w[(size_t)i];
                         r.rc = win_spectrum(a, spans[i], r, method, top_max,
                                             out_podop ? out_podop + (size_t)i * K : nullptr,
                                             out_score ? out_score + (size_t)i * K : nullptr, &n_out[i]);
-                    if (r.rc != MR_OK) err[(size_t)k] = a->err;
+                        if (r.rc != MR_OK) err[(size_t)k] = a->err;
+                    }
                 }
             }
         });
@@ -859,8 +882,18 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
         }
         const int32_t i0 = gbeg[(size_t)g], i1 = gbeg[(size_t)g + 1];
         std::lock_guard<std::mutex> lk(mu);
-        for (int32_t i = i0; i < i1; ++i)
-            if (r == MR_OK && w[(size_t)i].rc == MR_OK && w[(size_t)i].gn) q.push_back(~i);
+        if (r == MR_OK) {   // spectrum tasks of up to MR_WS_BATCH ranked windows: task ~i = list spec[i]
+            int32_t head = -1;
+            for (int32_t i = i0; i < i1; ++i) {
+                if (w[(size_t)i].rc != MR_OK || !w[(size_t)i].gn) continue;
+                if (head < 0 || (int)spec[(size_t)head].size() == spec_batch) {
+                    if (head >= 0) q.push_back(~head);
+                    head = i;
+                }
+                spec[(size_t)head].push_back(i);
+            }
+            if (head >= 0) q.push_back(~head);
+        }
         cv_task.notify_all();
         return r;
     };

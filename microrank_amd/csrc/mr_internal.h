@@ -442,6 +442,18 @@ int mr_win_spectrum_launch(mr_ctx* ctx, int32_t Na, const int32_t* a_podop, cons
                            int32_t Nn, const int32_t* n_podop, const double* n_w, const int32_t* n_cov, int32_t NP,
                            int64_t A, int64_t Nl, int method, int32_t k, unsigned char* d_slot);
 void mr_win_spectrum_unpack(const unsigned char* slot, int32_t* out_codes, double* out_score, int32_t* n_out);
+// several windows' spectra in one launch (a block each; every window within the one-block limits:
+// mr_win_spectrum_fits), at most MR_WS_BATCH per launch
+constexpr int MR_WS_BATCH = 8;
+struct MrWsWin {
+    const int32_t *a_podop, *a_cov, *n_podop, *n_cov;
+    const double *a_w, *n_w;
+    unsigned char* out;
+    int64_t A, Nl;
+    int32_t Na, Nn, NP;
+};
+bool mr_win_spectrum_fits(int32_t Na, int32_t Nn, int32_t NP, int32_t k);
+int mr_win_spectrum_launch_n(mr_ctx* ctx, const MrWsWin* ws, int n, int method, int32_t k);
 int mr_ix_finish(mr_ctx* ctx, const mr_spans* sp, mr_graph* g, IxBuild& b, const int64_t* h);
 // a graph of mr_ix_launch / mr_ix_launch2 finished WITHOUT its prepare: the caller prepares many
 // such graphs together (mr_graph_prepare_batch)

@@ -172,10 +172,10 @@ __device__ __forceinline__ void ws_bitonic_lanes(uint64_t& k, uint32_t& v, int32
         }
     }
 }
-__global__ void __launch_bounds__(WS_T) k_win_spectrum(int32_t Na, const int32_t* a_podop, const double* a_w,
-                                                      const int32_t* a_cov, int32_t Nn, const int32_t* n_podop,
-                                                      const double* n_w, const int32_t* n_cov, int32_t NP, int64_t A,
-                                                      int64_t Nl, int method, int32_t k, unsigned char* out) {
+__device__ __forceinline__ void win_spectrum_block(int32_t Na, const int32_t* a_podop, const double* a_w,
+                                                   const int32_t* a_cov, int32_t Nn, const int32_t* n_podop,
+                                                   const double* n_w, const int32_t* n_cov, int32_t NP, int64_t A,
+                                                   int64_t Nl, int method, int32_t k, unsigned char* out) {
     __shared__ int32_t nidx[WS_PMAX], apos[WS_PMAX];
     __shared__ uint64_t key[WS_MAX];
     __shared__ uint32_t vix[WS_MAX];
@@ -297,6 +297,23 @@ __global__ void __launch_bounds__(WS_T) k_win_spectrum(int32_t Na, const int32_t
     }
     if (tid == 0) ((int32_t*)(out + 12 * WS_KMAX))[0] = kk;
 }
+__global__ void __launch_bounds__(WS_T) k_win_spectrum(int32_t Na, const int32_t* a_podop, const double* a_w,
+                                                      const int32_t* a_cov, int32_t Nn, const int32_t* n_podop,
+                                                      const double* n_w, const int32_t* n_cov, int32_t NP, int64_t A,
+                                                      int64_t Nl, int method, int32_t k, unsigned char* out) {
+    win_spectrum_block(Na, a_podop, a_w, a_cov, Nn, n_podop, n_w, n_cov, NP, A, Nl, method, k, out);
+}
+// a block per window (the window batch's spectra of a group, MR_WS_BATCH per launch)
+struct WsBatchArg {
+    MrWsWin w[MR_WS_BATCH];
+    int method;
+    int32_t k;
+};
+__global__ void __launch_bounds__(WS_T) k_win_spectrum_b(WsBatchArg b) {
+    const MrWsWin& x = b.w[blockIdx.x];
+    win_spectrum_block(x.Na, x.a_podop, x.a_w, x.a_cov, x.Nn, x.n_podop, x.n_w, x.n_cov, x.NP, x.A, x.Nl, b.method, b.k,
+                       x.out);
+}
 }  // namespace
 
 // The window spectrum in one launch and one read-back (k_win_spectrum), or MR_ERR_STATE when the
@@ -305,9 +322,25 @@ static_assert(MR_WS_SLOT == 12 * WS_KMAX + 16, "window spectrum slot");
 int mr_win_spectrum_launch(mr_ctx* ctx, int32_t Na, const int32_t* a_podop, const double* a_w, const int32_t* a_cov,
                            int32_t Nn, const int32_t* n_podop, const double* n_w, const int32_t* n_cov, int32_t NP,
                            int64_t A, int64_t Nl, int method, int32_t k, unsigned char* d_slot) {
-    if (Na + Nn > WS_MAX || NP > WS_PMAX || k > WS_KMAX || k < 0) return MR_ERR_STATE;
+    if (!mr_win_spectrum_fits(Na, Nn, NP, k)) return MR_ERR_STATE;
     hipLaunchKernelGGL(k_win_spectrum, dim3(1), dim3(WS_T), 0, ctx->stream, Na, a_podop, a_w, a_cov, Nn, n_podop, n_w,
                        n_cov, NP, A, Nl, method, k, d_slot);
+    MR_TRY_HIP(ctx, hipGetLastError());
+    return MR_OK;
+}
+bool mr_win_spectrum_fits(int32_t Na, int32_t Nn, int32_t NP, int32_t k) {
+    return Na + Nn <= WS_MAX && NP <= WS_PMAX && k <= WS_KMAX && k >= 0;
+}
+int mr_win_spectrum_launch_n(mr_ctx* ctx, const MrWsWin* ws, int n, int method, int32_t k) {
+    if (n < 1 || n > MR_WS_BATCH) return mr_fail(ctx, MR_ERR_ARG, "mr_win_spectrum_launch_n: %d windows", n);
+    WsBatchArg b{};
+    for (int i = 0; i < n; ++i) {
+        if (!mr_win_spectrum_fits(ws[i].Na, ws[i].Nn, ws[i].NP, k)) return MR_ERR_STATE;
+        b.w[i] = ws[i];
+    }
+    b.method = method;
+    b.k = k;
+    hipLaunchKernelGGL(k_win_spectrum_b, dim3((unsigned)n), dim3(WS_T), 0, ctx->stream, b);
     MR_TRY_HIP(ctx, hipGetLastError());
     return MR_OK;
 }
