@@ -3,27 +3,32 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--precision fp64|fp32] [--no-cpu]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (driver, N > 1)
 
-Workload (BASELINE.json configs[1], "C2"): one RCA window of 1k operations / 200k traces
-(~22 spans/trace, Train-Ticket-like synthetic call tree with one faulty operation), fp64.
-The span columns are generated, factorised and uploaded BEFORE the timed region; a window is
-ranked on the device: detector -> two graph builds (T1 swap) -> two 25-iteration PageRanks ->
-DStar2 spectrum + top list (mr_rca_window).  A "step" ranks --streams W (default 8) copies of
-that window concurrently, each on its own library context (HIP stream) driven by its own host
-thread: one window alone leaves the GPU idle between its small dependent launches and host
-round trips, W windows fill those gaps (independent windows are data-parallel,
-no collective).  W = 8 (measured r01: W=4 172, 6 166, 8 195, 12 200 GTEPS; the 8 streams share
-the box's 4 hardware queues).
+Workload (BASELINE.json configs[1], "C2"): RCA windows of 1k operations / 200k traces each
+(~13.7 spans per trace, ~2.74M spans per window; Train-Ticket-like synthetic call tree with one
+faulty operation), fp64.  The span columns are generated, factorised and uploaded BEFORE the
+timed region; a window is ranked on the device: detector -> two graph builds (T1 swap) -> two
+25-iteration PageRanks -> DStar2 spectrum + top list.  A "step" ranks 64 DISTINCT windows (own
+seed and span table each) with ONE mr_windows_batch call (their detectors / builds / spectra on
+the library's auxiliary streams, the PageRanks of a group of windows sharing each iteration's
+launches).
 
 N > 1: every rank ranks its own independent windows (different seed): data-parallel windows,
-no collective on the data path -> "scaling": "weak".
+no collective on the data path -> "scaling": "weak".  Beside the headline
+the line carries "c4_sharded": ONE C4 graph (10k ops / 10M traces, BASELINE configs[3]) split by
+trace over the N ranks (strong scaling: 10M/N traces per rank), a whole trace_pagerank per step
+with the per-iteration exact-limb all-reduce (IPC peer push over xGMI, RCCL fallback) -- the
+north star's >= 6x-at-8-GPUs workload, so the driver's 1/2/4/8 run yields its curve.
 
 value = edges traversed by all PageRank iterations of all ranks (25 * (2 nnz + E_c) per graph)
 / max-over-ranks wall time of the K steps  [GTEPS].  Every other part of the window (detector,
 graph builds, spectrum) is inside that time.  windows_per_s is reported beside it.
-roofline: one power iteration (the k_tr_a + k_fx_b launch pair), algorithmic bytes (SURVEY §8(d)
-B_iter, both graphs of the window) over its live HIP-event duration on the library's stream;
-traffic = FETCH_SIZE (x2, gfx950) + WRITE_SIZE of the same launches per iteration from two
-rocprofv3 --pmc child runs made before this process touches the GPU (--no-traffic skips them).
+roofline: one power iteration (the k_tr_a + k_fx_b launch pair over a window group's graphs),
+algorithmic bytes (SURVEY §8(d) B_iter of every graph of the launch) over its live HIP-event
+duration on the library's stream; traffic = FETCH_SIZE (x2, gfx950) + WRITE_SIZE of the same
+launches per iteration from two rocprofv3 --pmc child runs made before this process touches the
+GPU (--no-traffic skips them).  --no-side: the timed steps only (no single-window latency, kind-
+compressed probe or c4_sharded leg), so a rocprofv3 kernel table of the command holds only the
+timed shape's launches (profiles/README.md).
 cpu_baseline: the C restatement (oracle/, OpenMP) of the same window on this host's cores.
 """
 from __future__ import annotations
@@ -291,7 +296,9 @@ def run_c4(args, world, rank, dist):
     t_gen = time.perf_counter()
     ctx = _lib.default_context()
     if world > 1:
-        shard.use_rccl(ctx)
+        shard.use_rccl(ctx)   # the once-per-graph collectives (and the fallback per iteration)
+        if not os.environ.get("MR_BENCH_NO_PEER"):
+            shard.use_peer(ctx)   # per iteration: IPC peer push over xGMI (falls back to RCCL collectively)
     prec = args.precision
     # N <= FX_NMAX: k_tr_a + k_fx_b; above it the wide fused path (hot ops through k_tr_a, cold
     # entries through k_cold_trace / k_cold_ops); MR_NO_WIDE=1 keeps the tile path for A/B runs
@@ -379,8 +386,9 @@ def run_c4(args, world, rank, dist):
                                + (f"; this GPU: rank 0's share of {sw} ({t_local} traces)" if sw != world else ""),
                    "nnz": int(nnz_all),
                    "call_edges": E,
-                   "parallelism": f"trace shards x{world}, RCCL " + ("limb" if fused else "fp64 op-sum")
-                                  + " all-reduce per iteration"},
+                   "parallelism": f"trace shards x{world}, "
+                                  + (("IPC peer push" if shard.peer_active(ctx) else "RCCL") if world > 1 else "no")
+                                  + (" limb" if fused else " fp64 op-sum") + " all-reduce per iteration"},
         "roofline": {"bound": "hbm", "kernel": "one Jacobi iteration on this rank ("
                                                + (("k_cold_trace + k_cold_ops + k_tr_a + k_fx_b" if wide else
                                                    "k_tr_a + k_fx_b") if fused else "k_iter_a + k_iter_b")
@@ -401,6 +409,111 @@ def run_c4(args, world, rank, dist):
         except Exception as e:
             out["cpu_baseline"] = {"value": None, "error": f"{type(e).__name__}: {e}"}
     return out
+
+
+C4_OPS, C4_TRACES = 10_000, 10_000_000   # BASELINE configs[3]
+
+
+def c4_leg_generate(world, rank):
+    """This rank's share of the C4 graph for the default line's c4_sharded leg (generated before
+    the process touches the GPU: the generator forks a process pool)."""
+    from microrank_amd import synth
+
+    t_local = C4_TRACES // world + (1 if rank < C4_TRACES % world else 0)
+    ts = time.perf_counter()
+    hg = synth.big_graph(C4_OPS, t_local, seed=11, shard=(rank, world))
+    print(f"[bench] rank {rank}: c4_sharded shard {t_local} traces / {hg.sr_ops.size} pairs in "
+          f"{time.perf_counter() - ts:.1f} s", file=sys.stderr, flush=True)
+    return hg
+
+
+def c4_leg_run(hg, world, rank, dist, steps=10, warmup=2):
+    """The c4_sharded leg: ONE 10k-op / 10M-trace graph split by trace over the ranks (strong
+    scaling), a step = one whole trace_pagerank (kinds, preference, 25 iterations with one exact
+    limb all-reduce each: IPC peer push over xGMI, RCCL fallback).  Max-over-ranks wall time.
+    The driver's N = 1/2/4/8 runs of the default command give the north star's C4 curve."""
+    import ctypes as C
+
+    import torch
+
+    from microrank_amd import _lib, shard
+    from microrank_amd.graph import DeviceGraph
+
+    ctx = _lib.Context(int(os.environ.get("MICRORANK_DEVICE", "0")))
+    if world > 1:
+        shard.use_rccl(ctx)
+        if not os.environ.get("MR_BENCH_NO_PEER"):
+            shard.use_peer(ctx)
+    dg = DeviceGraph.upload(ctx, hg)
+    nnz = float(dg.info()["nnz"])
+    for _ in range(warmup):
+        shard.sharded_pagerank(dg, True)
+    E = dg.info()["E"]
+    lib = _lib.load()
+    lib.mr_ctx_profile(ctx.h, 1)
+    ctx.sync()
+    if dist is not None:
+        dist.barrier()
+    ts = time.perf_counter()
+    for _ in range(steps):
+        w, _cov = shard.sharded_pagerank(dg, True)
+    ctx.sync()
+    if dist is not None:
+        dist.barrier()
+    el = time.perf_counter() - ts
+    launches, kms, kbytes = C.c_int64(), C.c_double(), C.c_double()
+    lib.mr_ctx_prof_read(ctx.h, C.byref(launches), C.byref(kms), C.byref(kbytes))
+    lib.mr_ctx_profile(ctx.h, 0)
+    it_us = kms.value / max(launches.value, 1) * 1e3
+    it_bytes = kbytes.value / max(launches.value, 1)
+    coll = ("IPC peer push" if shard.peer_active(ctx) else "RCCL") if world > 1 else "none (one rank)"
+    t = torch.tensor([el, nnz, it_us, it_bytes], dtype=torch.float64)
+    if dist is not None:
+        mx, sm = t.clone(), t.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        el, nnz, it_us, it_bytes = float(mx[0]), float(sm[1]), float(mx[2]), float(sm[3])
+    dg.close()
+    ctx.close()
+    edges = 25.0 * (2.0 * nnz + E) * steps
+    return {"workload": f"C4: one {C4_OPS}-op / {C4_TRACES}-trace graph (fp64, anomaly preference) sharded by "
+                        f"trace over {world} GPU(s); a step = one whole trace_pagerank",
+            "value": round(edges / el / 1e9, 3), "unit": "GTEPS", "ms_per_step": round(el / steps * 1e3, 4),
+            "steps": steps, "warmup": warmup, "n_gpus": world, "scaling": "strong", "nnz": int(nnz),
+            "call_edges": int(E), "traces_per_rank": C4_TRACES // world,
+            "iteration_us_max_rank": round(it_us, 3),
+            "iteration_frac": round(it_bytes / (it_us * 1e-6) / 1e9 / HBM_PEAK_GBS / world, 4) if it_us > 0 else None,
+            "all_reduce": coll,
+            "what": "iteration_us_max_rank: the slowest rank's HIP-event time of one iteration's launches (walk, "
+                    "column sums, all-reduce, finish); iteration_frac: SURVEY B_iter of the whole graph / that "
+                    "time / (N x 8 TB/s)"}
+
+
+def c4_leg_guarded(hg, world, rank, dist, line, limit_s=240.0):
+    """c4_leg_run behind a watchdog: a leg that raises becomes {"error": ...} (ranks stay in step:
+    every rank raises on a library error the ranks agreed on); a leg still running after limit_s
+    (a rank lost inside a collective) ends the process with the headline line printed on rank 0,
+    so the driver keeps its C2 number."""
+    import threading
+
+    if isinstance(hg, Exception):
+        return {"error": f"generation: {type(hg).__name__}: {hg}"}
+
+    def expire():
+        if line is not None:
+            line["c4_sharded"] = {"error": f"timed out after {limit_s:.0f} s"}
+            print(json.dumps(line), flush=True)
+        os._exit(0)
+
+    wd = threading.Timer(limit_s, expire)
+    wd.daemon = True
+    wd.start()
+    try:
+        return c4_leg_run(hg, world, rank, dist)
+    except Exception as e:
+        return {"error": f"{type(e).__name__}: {e}"}
+    finally:
+        wd.cancel()
 
 
 def run_sweep(args):
@@ -784,6 +897,12 @@ def main():
     ap.add_argument("--shard-of", type=int, default=1,
                     help="c4/c5 --from-spans at N=1: rank 0's share of a K-GPU deployment (c5: 12.5M of the 100M traces "
                          "at K=8), built and ranked on this GPU")
+    ap.add_argument("--no-side", action="store_true",
+                    help="c2/c3: the timed steps only -- no single-window latency, kind-compressed probe or "
+                         "c4_sharded leg (rocprofv3 kernel tables of the timed shape alone)")
+    ap.add_argument("--no-c4-leg", action="store_true", help="c2: skip the c4_sharded leg of the default line")
+    ap.add_argument("--dump-maps", default=None,
+                    help="write /proc/self/maps here after the warm-up (resolving native stack frames of a crash)")
     ap.add_argument("--c2-distinct", type=int, default=None,
                     help="c2: distinct seeded windows per step (default: every window of the step distinct)")
     args = ap.parse_args()
@@ -849,6 +968,13 @@ def main():
     dev_id = int(os.environ["MICRORANK_DEVICE"])
     batch = not args.streams_mode
     c2_tabs = None
+    c4_hg = None   # the c4_sharded leg's shard (default line only), generated before the GPU is touched
+    if (args.config == "c2" and batch and not args.pmc_child and not args.no_side and not args.no_c4_leg
+            and not os.environ.get("MR_BENCH_NO_C4_LEG")):
+        try:
+            c4_hg = c4_leg_generate(world, rank)
+        except Exception as e:   # (a side leg never sinks the line)
+            c4_hg = e
     if batch and args.config == "c2":   # distinct windows, generated before the GPU is touched
         nd = W if args.c2_distinct is None else max(1, min(W, args.c2_distinct))
         t_gen = time.perf_counter()
@@ -953,6 +1079,9 @@ def main():
         return sum(r[0] for o in outs for r in o), sum(len(o) for o in outs), last0
 
     run_all(args.warmup)
+    if args.dump_maps:   # the libraries are all mapped by now (rocprofv3's tool included)
+        with open("/proc/self/maps") as f, open(args.dump_maps, "w") as g:
+            g.write(f.read())
     load = _lib.load()
     load.mr_ctx_profile(ctx.h, 1)
     barrier()
@@ -978,6 +1107,8 @@ def main():
     else:
         edges_all, win_all = float(edges), n_win
     if rank != 0:
+        if c4_hg is not None:   # (collective: every rank runs the leg)
+            c4_leg_guarded(c4_hg, world, rank, dist, None)
         if dist is not None:
             dist.barrier()
             dist.destroy_process_group()
@@ -1038,6 +1169,12 @@ def main():
                               "peak": HBM_PEAK_GBS, "unit": "GB/s",
                               "frac": round(bytes_w * n_win / elapsed / 1e9 / HBM_PEAK_GBS, 4),
                               "formula": "52 S + 2 (24 S + 4 nnz + 4 T) + 25 B_iter per graph (SURVEY 8(d))"}
+    if args.no_side:
+        print(json.dumps(out), flush=True)
+        if dist is not None:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
     try:   # single-window latency: one window per mr_windows_batch call, nothing to overlap with
         from microrank_amd.online_rca import rank_windows
 
@@ -1062,6 +1199,9 @@ def main():
         out["kind_compressed"] = kind_compressed_probe(ctx, dev0, t0, t1, a3, ok)
     except Exception as e:  # a side metric never sinks the line
         out["kind_compressed"] = {"error": f"{type(e).__name__}: {e}"}
+    if c4_hg is not None:
+        out["c4_sharded"] = c4_leg_guarded(c4_hg, world, rank, dist, out)
+        c4_hg = None
     if not args.no_cpu and world == 1:   # the CPU baseline: rank 0 at N = 1 only
         try:
             cb, cres = cpu_baseline(abnormal, t0, t1, a3, ok)

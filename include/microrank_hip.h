@@ -296,6 +296,10 @@ int mr_comm_set_host(mr_ctx* ctx, mr_host_coll_fn fn, void* user, int nranks, in
  * in rank order, instead of an RCCL ring all-reduce (2 (R - 1) dependent steps).  The handles are
  * exchanged over the context's collectives on first use; enable = 0 unmaps them. */
 int mr_comm_peer_enable(mr_ctx* ctx, int enable);
+/* *active: 1 while the peer path carries this context's all-reduces (enabled and its regions
+ * mapped on every rank), 0 otherwise -- e.g. after the ranks agreed that a mapping failed and fell
+ * back to the RCCL / host collective, or after a peer timeout reset the regions.  Not collective. */
+int mr_comm_peer_active(mr_ctx* ctx, int* active);
 
 /* Trace-sharded PageRank: g holds THIS rank's traces (every span of
  * a trace on one rank) over the GLOBAL node index space, with this rank's partial len_o and

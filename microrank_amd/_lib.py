@@ -72,6 +72,7 @@ SIGNATURES = {
     "mr_graph_info": (C.c_int, [P, i32p, i32p, i64p, i64p]),
     "mr_pagerank": (C.c_int, [P, P, C.c_int, C.c_double, C.c_double, C.c_int, C.c_int, C.c_uint32]),
     "mr_comm_peer_enable": (C.c_int, [P, C.c_int]),
+    "mr_comm_peer_active": (C.c_int, [P, i32p]),
     "mr_pagerank_ex": (C.c_int, [P, P, C.c_int, C.c_double, C.c_double, C.c_int, C.c_double, C.c_int, C.c_uint32]),
     "mr_pagerank_batch": (C.c_int, [P, C.POINTER(P), C.POINTER(C.c_int), C.c_int, C.c_double, C.c_double, C.c_int,
                                     C.c_int, C.c_uint32]),

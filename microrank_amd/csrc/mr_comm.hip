@@ -182,7 +182,8 @@ __global__ void __launch_bounds__(PEER_T) k_peer_push(const unsigned long long* 
 template <class T>
 __global__ void __launch_bounds__(PEER_T) k_peer_reduce(T* __restrict__ dst, int64_t n,
                                                         unsigned long long* __restrict__ region, int nranks, int64_t W,
-                                                        uint64_t seq, unsigned long long need) {
+                                                        uint64_t seq, unsigned long long need,
+                                                        unsigned long long timeout) {
     __shared__ int s_ok;
     GLBP unsigned long long* reg = (GLBP unsigned long long*)region;
     if (threadIdx.x == 0) {
@@ -191,7 +192,7 @@ __global__ void __launch_bounds__(PEER_T) k_peer_reduce(T* __restrict__ dst, int
         for (int r = 0; r < nranks && s_ok; ++r)
             while (__hip_atomic_load(reg + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < need) {
                 __builtin_amdgcn_s_sleep(2);
-                if (__builtin_amdgcn_s_memrealtime() - t0 > PEER_TIMEOUT) {
+                if (__builtin_amdgcn_s_memrealtime() - t0 > timeout) {
                     s_ok = 0;
                     __hip_atomic_store(reg + PEER_ERR, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     break;
@@ -225,7 +226,7 @@ void mr_comm_peer_destroy(mr_ctx* ctx) {
     ctx->peer_region = nullptr;
     ctx->peer_dev = nullptr;
     ctx->peer_words = ctx->peer_xa = ctx->peer_xb = 0;
-    ctx->peer_seq = ctx->peer_xseq = 0;
+    ctx->peer_seq = ctx->peer_xseq = ctx->peer_arrived = 0;
 }
 
 // (collective) a receive region of at least `words` words per slot on every rank, mapped everywhere
@@ -241,15 +242,23 @@ static int peer_ensure(mr_ctx* ctx, int64_t words, int64_t xa = 0, int64_t xb = 
     mr_comm_peer_destroy(ctx);
     const size_t bytes = ((size_t)PEER_FLAGS + 2 * (size_t)R * (size_t)words + (size_t)xa + (size_t)xb) *
                          sizeof(unsigned long long);
-    MR_TRY_HIP(ctx, hipExtMallocWithFlags(&ctx->peer_region, bytes, hipDeviceMallocUncached));
-    MR_TRY_HIP(ctx, hipMemsetAsync(ctx->peer_region, 0, bytes, ctx->stream));
-    MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    // (local failures from here on are agreed over the ranks below, never returned alone: every
+    // rank must reach the same collectives)
+    int32_t bad = 0;
+    char why[160] = "";
+    hipIpcMemHandle_t mine;
+    memset(&mine, 0, sizeof mine);
+    if (hipExtMallocWithFlags(&ctx->peer_region, bytes, hipDeviceMallocUncached) != hipSuccess ||
+        hipMemsetAsync(ctx->peer_region, 0, bytes, ctx->stream) != hipSuccess ||
+        hipStreamSynchronize(ctx->stream) != hipSuccess || hipIpcGetMemHandle(&mine, ctx->peer_region) != hipSuccess) {
+        (void)hipGetLastError();
+        snprintf(why, sizeof why, "receive region of %zu bytes (uncached, IPC-exported)", bytes);
+        bad = 1;
+    }
     ctx->peer_words = words;
     ctx->peer_xa = xa;
     ctx->peer_xb = xb;
-    ctx->peer_seq = ctx->peer_xseq = 0;
-    hipIpcMemHandle_t mine;
-    MR_TRY_HIP(ctx, hipIpcGetMemHandle(&mine, ctx->peer_region));
+    ctx->peer_seq = ctx->peer_xseq = ctx->peer_arrived = 0;
     static_assert(sizeof(hipIpcMemHandle_t) % 8 == 0, "IPC handle size");
     const int64_t hw = (int64_t)(sizeof(hipIpcMemHandle_t) / 8);
     DBuf<uint64_t> hs, all;
@@ -260,7 +269,7 @@ static int peer_ensure(mr_ctx* ctx, int64_t words, int64_t xa = 0, int64_t xb = 
     MR_TRY_HIP(ctx, hipMemcpyAsync(hh.data(), all.p, sizeof(hipIpcMemHandle_t) * R, hipMemcpyDeviceToHost, ctx->stream));
     MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));
     ctx->peer_map.assign((size_t)R, nullptr);
-    for (int r = 0; r < R; ++r) {
+    for (int r = 0; r < R && !bad; ++r) {   // (a mapping may fail: no peer access between these devices)
         if (r == ctx->rank) {
             ctx->peer_map[(size_t)r] = ctx->peer_region;
             continue;
@@ -268,17 +277,41 @@ static int peer_ensure(mr_ctx* ctx, int64_t words, int64_t xa = 0, int64_t xb = 
         hipError_t e = hipIpcOpenMemHandle(&ctx->peer_map[(size_t)r], hh[(size_t)r], hipIpcMemLazyEnablePeerAccess);
         if (e != hipSuccess) {
             ctx->peer_map[(size_t)r] = nullptr;
-            return mr_fail(ctx, MR_ERR_COMM, "hipIpcOpenMemHandle(rank %d): %s", r, hipGetErrorString(e));
+            snprintf(why, sizeof why, "hipIpcOpenMemHandle(rank %d): %s", r, hipGetErrorString(e));
+            bad = 1;
         }
     }
-    MR_TRY_HIP(ctx, hipMalloc((void**)&ctx->peer_dev, sizeof(void*) * R));
-    MR_TRY_HIP(ctx, hipMemcpy(ctx->peer_dev, ctx->peer_map.data(), sizeof(void*) * R, hipMemcpyHostToDevice));
-    // every rank's region is mapped before anyone pushes into it
+    if (!bad && (hipMalloc((void**)&ctx->peer_dev, sizeof(void*) * R) != hipSuccess ||
+                 hipMemcpy(ctx->peer_dev, ctx->peer_map.data(), sizeof(void*) * R, hipMemcpyHostToDevice) != hipSuccess)) {
+        snprintf(why, sizeof why, "peer pointer table");
+        bad = 1;
+    }
+    // every rank's region is mapped before anyone pushes into it, and the ranks agree on whether
+    // every mapping succeeded: a rank that failed alone would otherwise leave the others waiting in
+    // their next all-reduce for pushes that never come.  On failure every rank drops the peer path
+    // (MR_ERR_STATE: the callers take the RCCL / host collective instead).
     DBuf<int32_t> one;
-    MR_TRY(one.zero(ctx, 1));
-    MR_TRY(mr_coll_allreduce(ctx, one.p, 1, MR_DT_I32, 0));
+    MR_TRY(one.upload(ctx, &bad, 1));
+    MR_TRY(mr_coll_allreduce(ctx, one.p, 1, MR_DT_I32, 1));
+    MR_TRY(one.download(ctx, &bad, 1));
     MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (bad) {
+        mr_comm_peer_destroy(ctx);
+        ctx->peer_on = false;
+        if (why[0]) fprintf(stderr, "[microrank] peer collectives off on rank %d: %s\n", ctx->rank, why);
+        return MR_ERR_STATE;
+    }
     return MR_OK;
+}
+
+// MR_PEER_TIMEOUT_MS: the bounded spins' limit (default 2000 ms)
+unsigned long long mr_peer_timeout_ticks() {
+    static const unsigned long long t = [] {
+        const char* e = getenv("MR_PEER_TIMEOUT_MS");
+        const long long ms = e ? atoll(e) : 0;
+        return ms > 0 ? (unsigned long long)ms * 100000ull : PEER_TIMEOUT;
+    }();
+    return t;
 }
 
 template <class T>
@@ -287,27 +320,43 @@ static int peer_allreduce(mr_ctx* ctx, T* dbuf, int64_t n) {
     MR_TRY(peer_ensure(ctx, n));
     const int nb = cdiv(n, PEER_T);
     const uint64_t seq = ctx->peer_seq++;
+    // a source's flag counts every block it has pushed into this region since the region was made;
+    // n (hence nb) changes between calls (2N + R on the fused path, N + R on the tile path, N per
+    // graph), so the round's target is the running total, not nb * rounds.  Every rank runs the
+    // same sequence of all-reduces with the same n (a collective), so every source's flag reaches
+    // exactly this total when it has pushed this round.
+    ctx->peer_arrived += (uint64_t)nb;
     hipLaunchKernelGGL(k_peer_push, dim3(nb), dim3(PEER_T), 0, ctx->stream, (const unsigned long long*)dbuf, n,
                        ctx->peer_dev, ctx->nranks, ctx->rank, ctx->peer_words, seq);
     hipLaunchKernelGGL(k_peer_reduce<T>, dim3(nb), dim3(PEER_T), 0, ctx->stream, dbuf, n,
                        (unsigned long long*)ctx->peer_region, ctx->nranks, ctx->peer_words, seq,
-                       (unsigned long long)nb * (seq + 1));
+                       (unsigned long long)ctx->peer_arrived, mr_peer_timeout_ticks());
     MR_TRY_HIP(ctx, hipGetLastError());
     return MR_OK;
 }
 int mr_peer_allreduce_u64(mr_ctx* ctx, unsigned long long* dbuf, int64_t n) { return peer_allreduce(ctx, dbuf, n); }
 int mr_peer_allreduce_f64(mr_ctx* ctx, double* dbuf, int64_t n) { return peer_allreduce(ctx, dbuf, n); }
 
-// a peer that never arrived (k_peer_reduce's timeout) is reported by the caller's read-back
-int mr_peer_error(mr_ctx* ctx, bool* failed) {
-    *failed = false;
-    if (!ctx->peer_region) return MR_OK;
+// (collective) a peer that never arrived (a k_peer_reduce / k_peer_wait timeout) on ANY rank:
+// the ranks agree on it through the fallback collective (RCCL or the host callback, never the
+// regions themselves), and then every rank drops its region -- the error word and the arrival
+// counts of an aborted round are stale -- so the next peer operation maps fresh, zeroed regions
+// everywhere.  A rank whose own rounds completed still reports the failure: its peers' did not.
+int mr_peer_check(mr_ctx* ctx, const char* what) {
+    if (!ctx->peer_region) return MR_OK;   // (created and dropped collectively: the same on every rank)
     unsigned long long w = 0;
     MR_TRY_HIP(ctx, hipMemcpyAsync(&w, (unsigned long long*)ctx->peer_region + PEER_ERR, 8,
                                    hipMemcpyDeviceToHost, ctx->stream));
     MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    *failed = w != 0;
-    return MR_OK;
+    int32_t any = w != 0 ? 1 : 0;
+    DBuf<int32_t> f;
+    MR_TRY(f.upload(ctx, &any, 1));
+    MR_TRY(mr_coll_allreduce(ctx, f.p, 1, MR_DT_I32, 1));
+    MR_TRY(f.download(ctx, &any, 1));
+    MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (!any) return MR_OK;
+    mr_comm_peer_destroy(ctx);
+    return mr_fail(ctx, MR_ERR_COMM, "%s: a rank did not arrive within the peer timeout (regions reset)", what);
 }
 
 // ---- exchanges (all-to-all) through the regions' areas A and B: a round is a set of puts into
@@ -326,13 +375,14 @@ __global__ void k_peer_signal(unsigned long long* const* __restrict__ peers, int
                                __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
-__global__ void k_peer_wait(unsigned long long* region, int nranks, unsigned long long need) {
+__global__ void k_peer_wait(unsigned long long* region, int nranks, unsigned long long need,
+                            unsigned long long timeout) {
     GLBP unsigned long long* reg = (GLBP unsigned long long*)region;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     for (int r = 0; r < nranks; ++r)
         while (__hip_atomic_load(reg + PEER_XF + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < need) {
             __builtin_amdgcn_s_sleep(2);
-            if (__builtin_amdgcn_s_memrealtime() - t0 > PEER_TIMEOUT) {
+            if (__builtin_amdgcn_s_memrealtime() - t0 > timeout) {
                 __hip_atomic_store(reg + PEER_ERR, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 return;
             }
@@ -362,7 +412,7 @@ int mr_peer_round(mr_ctx* ctx) {
     const uint64_t x = ctx->peer_xseq++;
     hipLaunchKernelGGL(k_peer_signal, dim3(1), dim3(64), 0, ctx->stream, ctx->peer_dev, ctx->nranks, ctx->rank);
     hipLaunchKernelGGL(k_peer_wait, dim3(1), dim3(1), 0, ctx->stream, (unsigned long long*)ctx->peer_region,
-                       ctx->nranks, (unsigned long long)(x + 1));
+                       ctx->nranks, (unsigned long long)(x + 1), mr_peer_timeout_ticks());
     MR_TRY_HIP(ctx, hipGetLastError());
     return MR_OK;
 }
@@ -373,5 +423,11 @@ extern "C" int mr_comm_peer_enable(mr_ctx* ctx, int enable) {
     if (!ctx) return MR_ERR_ARG;
     if (!enable) mr_comm_peer_destroy(ctx);
     ctx->peer_on = enable != 0;
+    return MR_OK;
+}
+
+extern "C" int mr_comm_peer_active(mr_ctx* ctx, int* active) {
+    if (!ctx || !active) return MR_ERR_ARG;
+    *active = ctx->peer_on && ctx->peer_region ? 1 : 0;
     return MR_OK;
 }

@@ -69,7 +69,8 @@ struct mr_ctx {
     int64_t peer_words = 0, peer_xa = 0, peer_xb = 0;   // all-reduce slot words, exchange areas
     std::vector<void*> peer_map;
     unsigned long long** peer_dev = nullptr;   // device copy of peer_map
-    uint64_t peer_seq = 0;                      // all-reduces completed (the flags count them)
+    uint64_t peer_seq = 0;                      // all-reduces completed (slot parity)
+    uint64_t peer_arrived = 0;                  // blocks every source has pushed so far (the flags' target)
     uint64_t peer_xseq = 0;                     // exchange rounds completed
     // k_pr_cluster timed out on this context (its clusters were not co-resident): launch per
     // iteration from then on
@@ -370,7 +371,9 @@ inline bool mr_coll_ready(const mr_ctx* ctx) { return ctx->comm || ctx->host_col
 // mr_coll_allreduce).  Collective: every rank calls it with the same n.
 int mr_peer_allreduce_u64(mr_ctx* ctx, unsigned long long* dbuf, int64_t n);
 int mr_peer_allreduce_f64(mr_ctx* ctx, double* dbuf, int64_t n);   // (fp64 sums in rank order)
-int mr_peer_error(mr_ctx* ctx, bool* failed);   // a round timed out (a peer never pushed)
+// (collective) MR_ERR_COMM when a round timed out on any rank (a peer never pushed); the regions
+// are then reset on every rank
+int mr_peer_check(mr_ctx* ctx, const char* what);
 // exchanges through the peer regions: areas A (0) and B (1) of every rank's region
 bool mr_peer_ready(const mr_ctx* ctx);
 int mr_peer_xensure(mr_ctx* ctx, int64_t xa, int64_t xb);    // (collective) area sizes in words

@@ -4268,11 +4268,7 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
                        fl.p);
     MR_DEBUG_CHECK(ctx, "k_weights");
     MR_TRY_HIP(ctx, hipGetLastError());
-    if (coll && ctx->peer_on) {   // a peer that never pushed its round: an error, not wrong sums
-        bool failed = false;
-        MR_TRY(mr_peer_error(ctx, &failed));
-        if (failed) return mr_fail(ctx, MR_ERR_COMM, "peer all-reduce: a rank did not arrive (timeout)");
-    }
+    if (coll && ctx->peer_on) MR_TRY(mr_peer_check(ctx, "peer all-reduce"));   // an error, not wrong sums
     // a shard's local collision must make every rank retry: the error words meet in a MAX
     if (coll) {
         MR_TRY(mr_coll_allreduce(ctx, gs[0]->flag.p, 4, MR_DT_I32, 1));
@@ -4653,10 +4649,7 @@ static int shard_kinds_peer(mr_ctx* ctx, mr_graph* g, uint64_t cap, const DBuf<i
         hipLaunchKernelGGL(k_kx_apply, dim3(cdiv(T, 256)), dim3(256), 0, st, g->ht_key.p, g->slot_of.p, fl.p, pos.p,
                            spos.p, (const unsigned long long*)mr_peer_area(ctx, me, 1), T, g->kind.p);
     MR_TRY_HIP(ctx, hipGetLastError());
-    bool failed = false;
-    MR_TRY(mr_peer_error(ctx, &failed));   // (syncs: the scratch leaves scope)
-    if (failed) return mr_fail(ctx, MR_ERR_COMM, "kind exchange: a rank did not arrive (timeout)");
-    return MR_OK;
+    return mr_peer_check(ctx, "kind exchange");   // (syncs: the scratch leaves scope)
 }
 
 static int shard_kinds(mr_ctx* ctx, mr_graph* g, uint64_t cap) {
@@ -4675,7 +4668,10 @@ static int shard_kinds(mr_ctx* ctx, mr_graph* g, uint64_t cap) {
     int64_t Kl = 0;
     MR_TRY(kn.download(ctx, &Kl, 1));
     MR_TRY_HIP(ctx, hipStreamSynchronize(st));
-    if (mr_peer_ready(ctx)) return shard_kinds_peer(ctx, g, cap, fl, pos, Kl);
+    if (mr_peer_ready(ctx)) {   // MR_ERR_STATE: the ranks could not map each other's regions (collective)
+        const int rc = shard_kinds_peer(ctx, g, cap, fl, pos, Kl);
+        if (rc != MR_ERR_STATE) return rc;
+    }
     MR_TRY(mr_coll_allreduce(ctx, kn.p, 1, MR_DT_I64, 1));
     int64_t Kmax = 0;
     MR_TRY(kn.download(ctx, &Kmax, 1));

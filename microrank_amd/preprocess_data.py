@@ -129,40 +129,86 @@ _TABLE_COLUMNS = ("traceID", "spanID", "ParentSpanId", "serviceName", "operation
                   "startTime", "endTime")
 
 
-_SAMPLE_ROWS = 64
+_memcmp = C.CDLL(None).memcmp
+_memcmp.restype = C.c_int
+_memcmp.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
 
 
-def _column_identity(s: pd.Series):
-    """Where a column's values live: (dtype, buffer addresses / sizes).  A replaced column (the
-    reference's own mutations assign whole columns: preprocess_data.py:27, 53, 100) always gets a
-    new buffer; Arrow buffers are immutable."""
-    arr = s.array
-    pa_arr = getattr(arr, "_pa_array", None)
-    if pa_arr is not None:
-        return ("arrow", tuple((b.address, b.size) for ch in pa_arr.chunks for b in ch.buffers() if b is not None))
-    a = getattr(arr, "_ndarray", None)
-    if a is None:
-        a = np.asarray(arr)
-    return (str(a.dtype), a.__array_interface__["data"][0], a.strides, a.shape)
+class _ColumnSnapshot:
+    """What a column held when the device table was built, held so that "unchanged" is decided
+    exactly, never by sampling (an in-place cell edit outside a sample must
+    rebuild the table, as the reference -- which has no cache -- would see the edit):
+      * Arrow-backed columns: the ChunkedArray itself (immutable: an in-place edit replaces it, and
+        holding the old one keeps its buffers from being reused at the same addresses);
+      * NumPy columns: a copy of the values -- for object columns a copy of the pointer array, which
+        also holds a reference to every string, so equal pointers mean the same (immutable) string
+        objects: a word-by-word compare of 8 B per row decides it."""
+
+    def __init__(self, s: pd.Series):
+        arr = s.array
+        self.pa = getattr(arr, "_pa_array", None)
+        self.np = None
+        if self.pa is None:
+            a = getattr(arr, "_ndarray", None)
+            self.np = np.array(np.asarray(arr) if a is None else a, copy=True)
+
+    def matches(self, s: pd.Series) -> bool:
+        arr = s.array
+        pa_arr = getattr(arr, "_pa_array", None)
+        if self.pa is not None or pa_arr is not None:
+            return pa_arr is self.pa
+        a = getattr(arr, "_ndarray", None)
+        a = np.asarray(arr) if a is None else a
+        if a.dtype != self.np.dtype or a.shape != self.np.shape:
+            return False
+        if a.flags.c_contiguous and self.np.flags.c_contiguous:
+            # values, or an object column's pointers: memcmp (ctypes releases the GIL)
+            return a.nbytes == 0 or _memcmp(C.c_void_p(a.ctypes.data), C.c_void_p(self.np.ctypes.data),
+                                            C.c_size_t(a.nbytes)) == 0
+        return bool(np.array_equal(a, self.np)) if a.dtype != object else all(
+            u is v for u, v in zip(a.tolist(), self.np.tolist()))
 
 
-def _fingerprint(df: pd.DataFrame):
-    """Cheap cache key of the columns the span table is built from: every column's buffer
-    identity, the frame's mutation version (bumped by this module's mutating drop-ins) and a
-    content hash of 64 rows spread over the frame (first and last included) -- O(columns), not
-    O(rows), so the unchanged reference driver's three lookups per window cost microseconds
-    (VERDICT r2 'drop-in path host-bound by the cache fingerprint').  An in-place cell edit
-    (``df.loc[i, c] = x``) of a row outside the sample keeps the key: call :func:`invalidate`
-    after such edits."""
-    cols = [c for c in _TABLE_COLUMNS if c in df.columns]
-    n = len(df)
-    if n == 0:
-        return (0, tuple(cols))
-    ident = tuple(_column_identity(df[c]) for c in cols)
-    idx = np.unique(np.linspace(0, n - 1, min(n, _SAMPLE_ROWS)).astype(np.int64))
-    samp = tuple(int(pd.util.hash_pandas_object(df[c].iloc[idx], index=False).to_numpy().sum(dtype=np.uint64))
-                 for c in cols)
-    return (n, tuple(cols), ident, samp, df.attrs.get("_mr_version", 0))
+class _FrameSnapshot:
+    """Exact cache key of the columns a span table is built from: row count, column set, this
+    module's mutation version and a _ColumnSnapshot per column.  A lookup compares 8 B per row and
+    column (the columns in parallel: the compares release the GIL) -- O(rows) like the reference's
+    own per-window DataFrame filtering (preprocess_data.py:13), and exact."""
+
+    def __init__(self, df: pd.DataFrame):
+        self.cols = tuple(c for c in _TABLE_COLUMNS if c in df.columns)
+        self.n = len(df)
+        self.version = df.attrs.get("_mr_version", 0)
+        self.parts = [_ColumnSnapshot(df[c]) for c in self.cols]
+
+    def matches(self, df: pd.DataFrame) -> bool:
+        cols = tuple(c for c in _TABLE_COLUMNS if c in df.columns)
+        if cols != self.cols or len(df) != self.n or df.attrs.get("_mr_version", 0) != self.version:
+            return False
+        if self.n == 0:
+            return True
+        series = [df[c] for c in cols]
+        if self.n < 65536:
+            return all(p.matches(x) for p, x in zip(self.parts, series))
+        return all(_pool().map(lambda px: px[0].matches(px[1]), zip(self.parts, series)))
+
+
+_POOL = None
+
+
+def _pool():
+    global _POOL
+    if _POOL is None:
+        from concurrent.futures import ThreadPoolExecutor
+
+        _POOL = ThreadPoolExecutor(max_workers=len(_TABLE_COLUMNS), thread_name_prefix="mr-fp")
+    return _POOL
+
+
+def _fingerprint(df: pd.DataFrame) -> _FrameSnapshot:
+    """The exact snapshot of df's span-table columns (``_fingerprint(df).matches(df)`` until any of
+    them changes, in place or by replacement)."""
+    return _FrameSnapshot(df)
 
 
 def invalidate(df: pd.DataFrame) -> None:
@@ -179,10 +225,10 @@ def span_table(df: pd.DataFrame, ctx=None):
     (mr_spans handles are per mr_ctx), so two contexts sharing a DataFrame get a handle each."""
     ctx = ctx or _lib.default_context()
     key = (id(df), id(ctx))
-    fp = _fingerprint(df)
     hit = _CACHE.get(key)
-    if hit is not None and hit[0]() is df and hit[1]() is ctx and hit[2] == fp:
+    if hit is not None and hit[0]() is df and hit[1]() is ctx and hit[2].matches(df):
         return hit[3], hit[4]
+    fp = _fingerprint(df)   # (taken before the build: the table is built from these values)
     arrays = None if _HOST_FACTORIZE else arrow_columns(df)
     if arrays is not None:   # strings -> codes on the device (SURVEY 8(f) f2)
         table, dev = DeviceSpans.ingest(ctx, df, arrays)

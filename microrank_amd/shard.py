@@ -93,6 +93,15 @@ def use_peer(ctx: "_lib.Context", enable: bool = True):
     ctx.check(_lib.load().mr_comm_peer_enable(ctx.h, int(bool(enable))), "mr_comm_peer_enable")
 
 
+def peer_active(ctx: "_lib.Context") -> bool:
+    """True while the peer path carries this context's all-reduces (its regions mapped on every
+    rank); False before the first sharded call, or after the ranks fell back to RCCL / the host
+    collective (a failed mapping, a peer timeout)."""
+    a = C.c_int32()
+    ctx.check(_lib.load().mr_comm_peer_active(ctx.h, C.byref(a)), "mr_comm_peer_active")
+    return bool(a.value)
+
+
 def sharded_pagerank(dg, anomaly: bool, d: float = 0.85, alpha: float = 0.01, iters: int = 25,
                      precision: str = "fp64"):
     """PageRank of the whole graph from this rank's shard ``dg`` (a DeviceGraph whose len_o /

@@ -1,0 +1,70 @@
+#!/bin/bash
+# GPU box, round 4 evidence: scripts/r04.sh TAG "stages"
+#   t       full -m gpu suite          s      smoke
+#   c2      default bench line (c2 windows + c4_sharded leg, PMC traffic, CPU baseline)
+#   pc2     rocprofv3 kernel table of the timed c2 groups only (--no-side: no latency / kind / c4 legs)
+#   c4      c4 line (traffic, CPU baseline)       pc4   rocprofv3 kernel table of the c4 command
+#   c4s8    c4 at N=1 holding rank 0's share of an 8-GPU deployment (per-rank compute at N=8)
+#   pmc4    k_tr_a LDS / wait PMC passes at C4 (scripts/pmc_c4.sh)
+#   segv    the rocprofv3 --kernel-trace --stats c3 command that crashed in round 3, once, with maps
+#   c3 c5   c3 / c5 lines
+#   shard   the shard tests only
+TAG=${1:-x}
+STAGES=${2:-"t s c2"}
+has() { [[ " $STAGES " == *" $1 "* ]]; }
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out profiles
+line() { python3 -c "import json,sys;d=json.load(open(sys.argv[1]));r=d.get('roofline',{});print(sys.argv[2], d['value'], d.get('windows_per_s'), r.get('avg_launch_us'), r.get('frac'), r.get('traffic'), (d.get('cpu_baseline') or {}).get('value'), d.get('window_ms'), json.dumps(d.get('c4_sharded')))" "$1" "$2"; }
+if has shard; then
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_shard.py -x -v --timeout 240 --timeout-method thread > gpurun_out/shard_$TAG.log 2>&1
+  rc=$?; echo "shard rc=$rc"; tail -3 gpurun_out/shard_$TAG.log; [ $rc -eq 0 ] || exit $rc
+fi
+if has t; then
+  timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/t_$TAG.log 2>&1
+  rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/t_$TAG.log; [ $rc -eq 0 ] || exit $rc
+fi
+if has s; then
+  timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 || { echo smoke failed; tail -5 gpurun_out/smoke_$TAG.log; exit 1; }
+  echo "smoke: $(tail -1 gpurun_out/smoke_$TAG.log)"
+fi
+if has c2; then
+  timeout -k 10 900 python3 bench.py > gpurun_out/c2_$TAG.json 2> gpurun_out/c2_$TAG.err || { tail -5 gpurun_out/c2_$TAG.err; exit 1; }
+  line gpurun_out/c2_$TAG.json c2
+fi
+if has pc2; then
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/pc2_$TAG -o run --output-format csv \
+      -- python3 bench.py --no-traffic --no-cpu --no-side --steps 10 --warmup 2 > gpurun_out/pc2_$TAG.json 2> gpurun_out/pc2_$TAG.err || { echo "rocprof pc2 failed"; tail -5 gpurun_out/pc2_$TAG.err; exit 1; }
+  line gpurun_out/pc2_$TAG.json pc2
+fi
+if has c4; then
+  timeout -k 10 600 python3 bench.py --config c4 --steps 5 --warmup 1 > gpurun_out/c4_$TAG.json 2> gpurun_out/c4_$TAG.err || { tail -5 gpurun_out/c4_$TAG.err; exit 1; }
+  line gpurun_out/c4_$TAG.json c4
+fi
+if has pc4; then
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/pc4_$TAG -o run --output-format csv \
+      -- python3 bench.py --config c4 --no-traffic --no-cpu --steps 5 --warmup 1 > gpurun_out/pc4_$TAG.json 2> gpurun_out/pc4_$TAG.err || { echo "rocprof pc4 failed"; tail -5 gpurun_out/pc4_$TAG.err; exit 1; }
+  line gpurun_out/pc4_$TAG.json pc4
+fi
+if has c4s8; then
+  timeout -k 10 600 python3 bench.py --config c4 --shard-of 8 --steps 10 --warmup 2 --no-cpu > gpurun_out/c4s8_$TAG.json 2> gpurun_out/c4s8_$TAG.err || { tail -5 gpurun_out/c4s8_$TAG.err; exit 1; }
+  line gpurun_out/c4s8_$TAG.json c4s8
+fi
+if has pmc4; then
+  bash scripts/pmc_c4.sh $TAG k_tr_a c4 || exit 1
+fi
+if has segv; then
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/segv_$TAG -o run --output-format csv \
+      -- python3 bench.py --no-traffic --config c3 --steps 3 --warmup 1 --no-cpu --dump-maps gpurun_out/maps_$TAG.txt \
+      > gpurun_out/segv_$TAG.json 2> gpurun_out/segv_$TAG.err
+  rc=$?; echo "segv-command rc=$rc"; [ $rc -eq 0 ] || { tail -40 gpurun_out/segv_$TAG.err; exit $rc; }
+  line gpurun_out/segv_$TAG.json segv
+fi
+if has c3; then
+  timeout -k 10 400 python3 bench.py --config c3 > gpurun_out/c3_$TAG.json 2> gpurun_out/c3_$TAG.err || { tail -5 gpurun_out/c3_$TAG.err; exit 1; }
+  line gpurun_out/c3_$TAG.json c3
+fi
+if has c5; then
+  timeout -k 10 600 python3 bench.py --config c5 --steps 3 --warmup 1 > gpurun_out/c5_$TAG.json 2> gpurun_out/c5_$TAG.err || { tail -5 gpurun_out/c5_$TAG.err; exit 1; }
+  line gpurun_out/c5_$TAG.json c5
+fi
+exit 0

@@ -177,7 +177,33 @@ def test_graph_sees_in_place_column_edits():
 
     fp = _fingerprint(df)
     df.loc[df.index[0], "duration"] += 1   # any used column, in place
-    assert _fingerprint(df) != fp
+    assert not fp.matches(df)
+
+
+def test_in_place_cell_edit_anywhere_reranks():
+    """one in-place cell edit at an interior row (no sample would see it) --
+    a span's operationName and another span's duration -- must reach the next drop-in call: the
+    ranking equals the one computed on a fresh copy of the edited frame (a cache miss by
+    construction), not the stale device table's."""
+    from microrank_amd.pagerank import trace_pagerank
+    from microrank_amd.preprocess_data import get_pagerank_graph
+
+    case = load_golden("c1.json")
+    _, adf = regen_window(case)
+    df = adf.copy()
+    tnames = sorted(df["traceID"].unique())
+    lst = [tnames[i] for i in case["detect"]["normal"]]
+    w0, c0 = trace_pagerank(*get_pagerank_graph(lst, df), False)
+    rows = np.flatnonzero(df["traceID"].isin(lst).to_numpy())
+    r = df.index[rows[len(rows) // 2 + 3]]   # an interior span of a listed trace
+    df.loc[r, "operationName"] = "edited_operation"
+    w1, c1 = trace_pagerank(*get_pagerank_graph(lst, df), False)
+    fresh = df.copy()
+    w2, c2 = trace_pagerank(*get_pagerank_graph(lst, fresh), False)
+    assert list(w1) == list(w2) and c1 == c2
+    assert [float(x) for x in w1.values()] == [float(x) for x in w2.values()]
+    assert list(w1) != list(w0)   # the edited span's node appears
+    assert any(k.endswith("_edited_operation") for k in w1)
 
 
 def test_two_contexts_share_one_dataframe():

@@ -382,3 +382,74 @@ def test_sharded_build_from_spans_matches_single_gpu(anomaly, world, peer):
         assert r[1].tobytes() == res[0][1].tobytes(), "ranks disagree"
     assert sum(r[3][1]["T"] for r in res) == t.value
     assert res[0][3][1]["E"] == E_whole   # after the exchange: the whole graph's call edges
+
+
+# ------------------------------------------------------------ peer regions over several graphs
+def _seq_worker(rank, world, port, peer, q):
+    """One context ranks a sequence of graphs of different op counts: the window graph (fused,
+    2N + R words), a 20k-op graph (tile path, N + R words), the window graph again (smaller than
+    the one before) and a 10k-op fused graph.  Every all-reduce of the sequence goes through the
+    same peer region, whose arrival counts carry over from one graph to the next."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from gpu_util import host_graph_from_oracle
+        from microrank_amd import _lib, shard, synth
+        from microrank_amd.graph import DeviceGraph
+
+        ctx = _lib.Context(0)
+        shard.use_host(ctx)
+        if peer:
+            shard.use_peer(ctx)
+        win = host_graph_from_oracle(_shard(_window_graph(), rank, world))
+        seq = [win, synth.big_graph(20_000, 6_000, seed=3, shard=(rank, world)), win,
+               synth.big_graph(10_000, 6_000, seed=5, shard=(rank, world))]
+        out = []
+        for hg in seq:
+            dg = DeviceGraph.upload(ctx, hg)
+            w, cov = shard.sharded_pagerank(dg, True)
+            out.append((w, cov))
+            dg.close()
+        ctx.close()
+        q.put((rank, out, True, None))
+    except Exception as e:
+        q.put((rank, repr(e), None, None))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run_seq(world, peer):
+    mpc = mp.get_context("spawn")
+    q = mpc.Queue()
+    port = _free_port()
+    procs = [mpc.Process(target=_seq_worker, args=(r, world, port, peer, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in procs], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in res:
+        assert r[2] is not None, f"rank {r[0]} failed: {r[1]}"
+    return res
+
+
+def test_peer_regions_carry_over_graphs_of_different_sizes():
+    """the peer all-reduce's arrival target must be the running count of pushed
+    blocks, not blocks x rounds -- a smaller graph after a larger one (the window graph after the
+    20k-op graph) would otherwise find its target already met and sum slots the peers had not
+    written yet.  Four processes on one GPU, one context each, four graphs in sequence on the
+    fused and the tile path: peer == the host-staged collective (bitwise on the fused graphs'
+    exact limbs, 1e-12 on the tile path's fp64 sums) and every rank bitwise equal."""
+    a = _run_seq(4, peer=False)
+    b = _run_seq(4, peer=True)
+    for k in range(4):
+        for r in range(4):
+            wa, ca = a[r][1][k]
+            wb, cb = b[r][1][k]
+            np.testing.assert_array_equal(ca, cb)
+            if k == 1:
+                np.testing.assert_allclose(wb, wa, rtol=1e-12, atol=0)
+            else:
+                assert wa.tobytes() == wb.tobytes(), f"graph {k} rank {r}: peer != host collective"
+            assert b[r][1][k][0].tobytes() == b[0][1][k][0].tobytes(), "ranks disagree"

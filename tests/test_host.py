@@ -9,33 +9,75 @@ import pytest
 from conftest import load_golden, regen_window
 
 
-def test_fingerprint_sees_column_replacement_sampled_edits_and_invalidate():
-    """The cache key is O(columns): buffer identity (the reference's own mutations replace whole
-    columns, preprocess_data.py:27,53,100), a 64-row content sample (first and last rows included)
-    and a version bumped by this package's mutating drop-ins / invalidate()."""
+def test_fingerprint_is_exact_for_any_in_place_edit_and_invalidate():
+    """The cache key decides "unchanged" exactly: any in-place cell edit of a
+    column the span table reads -- at any row, not a sample -- and any column replacement (the
+    reference's own mutations, preprocess_data.py:27,53,100) no longer match; columns the table
+    does not read do not matter; invalidate() and this package's mutating drop-ins bump the
+    version."""
     from microrank_amd.preprocess_data import _fingerprint, get_operation_duration_data, invalidate
 
     case = load_golden("c1.json")
     _, adf = regen_window(case)
     df = adf.copy()
+    n = len(df)
     fp = _fingerprint(df)
-    assert _fingerprint(df) == fp                        # stable while nothing changes
+    assert fp.matches(df) and fp.matches(df)             # stable while nothing changes
     df["operation"] = "x"                               # a column the table does not read
-    assert _fingerprint(df) == fp
-    df.loc[df.index[0], "duration"] += 1                 # in place, a sampled row
-    fp2 = _fingerprint(df)
-    assert fp2 != fp
-    df.loc[df.index[-1], "spanID"] = "changed"           # in place, last row (sampled)
-    fp3 = _fingerprint(df)
-    assert fp3 != fp2
+    assert fp.matches(df)
+    mid = df.index[n // 2 + 7]                          # an arbitrary interior row
+    for col, val in (("duration", int(df["duration"].iloc[n // 2 + 7]) + 1), ("operationName", "changed-op"),
+                     ("spanID", "changed-span"), ("startTime", df["startTime"].iloc[0])):
+        fp = _fingerprint(df)
+        assert fp.matches(df)
+        df.loc[mid, col] = val                          # in place, one cell
+        assert not fp.matches(df), col
+    # the same value written back: the content is what it was, the key matches again
+    fp = _fingerprint(df)
+    old = df.loc[mid, "operationName"]
+    df.loc[mid, "operationName"] = "tmp"
+    df.loc[mid, "operationName"] = old
+    assert fp.matches(df)
+    fp = _fingerprint(df)
     get_operation_duration_data(case["operation_list"], df)   # replaces operationName (+ version)
-    fp4 = _fingerprint(df)
-    assert fp4 != fp3
+    assert not fp.matches(df)
+    fp = _fingerprint(df)
     invalidate(df)
-    assert _fingerprint(df) != fp4
-    assert _fingerprint(df.iloc[:0]) == (0, tuple(c for c in df.columns if c in (
-        "traceID", "spanID", "ParentSpanId", "serviceName", "operationName", "podName", "duration", "startTime",
-        "endTime")))
+    assert not fp.matches(df)
+    fp = _fingerprint(df.iloc[:0])
+    assert fp.matches(df.iloc[:0]) and not fp.matches(df)
+
+
+def test_fingerprint_arrow_columns_and_cost():
+    """Arrow-backed columns (read_traces_csv) match by identity of their immutable arrays (an
+    in-place edit replaces the array); a C2-sized frame (2.7M spans) is checked in a few tens
+    of ms -- O(rows) like the reference's own per-window filtering."""
+    import time
+
+    import pyarrow as pa
+
+    from microrank_amd.preprocess_data import _fingerprint
+
+    n = 50_000
+    df = pd.DataFrame({"traceID": pd.array([f"t{i // 20}" for i in range(n)], dtype=pd.ArrowDtype(pa.string())),
+                       "duration": np.arange(n, dtype=np.int64)})
+    fp = _fingerprint(df)
+    assert fp.matches(df)
+    df.loc[df.index[n // 3], "traceID"] = "edited"
+    assert not fp.matches(df)
+    n = 2_740_000
+    big = pd.DataFrame({c: np.array([f"s{i % 9973}" for i in range(n)], dtype=object) for c in
+                        ("traceID", "spanID", "ParentSpanId", "serviceName", "operationName", "podName")})
+    for c in ("duration", "startTime", "endTime"):
+        big[c] = np.arange(n, dtype=np.int64)
+    fp = _fingerprint(big)
+    ts = time.perf_counter()
+    for _ in range(5):
+        assert fp.matches(big)
+    per = (time.perf_counter() - ts) / 5
+    assert per < 0.25, per
+    big.loc[big.index[n - 12345], "podName"] = "edited"
+    assert not fp.matches(big)
 
 
 def test_trace_list_is_a_plain_list_with_codes():
