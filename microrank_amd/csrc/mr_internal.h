@@ -199,6 +199,8 @@ struct mr_graph {
     DBuf<int32_t> coff;              // [n_wt+1] first chunk of a tile
     std::vector<int32_t> coff_h;     // host copy (the per-wave tile split of a launch)
     DBuf<float> w_tp, c_tp;          // [T] w_t, c_t in position order
+    DBuf<int32_t> tpos;              // [T] position of each trace (inverse of tperm; large graphs, built on first use)
+    bool tpos_ok = false;
     // register-accumulated hot ops (large graphs, su in LDS): the nhr <= 8 ops present in most
     // traces leave the id chunks; hmask[p] (position order) says which of them trace p holds
     int32_t nhr = 0;

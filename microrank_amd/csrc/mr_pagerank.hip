@@ -1227,6 +1227,28 @@ __global__ void k_pref_apply(const double* kind, const int32_t* pr_trace, const 
     if (tperm) c_tp[i] = cd * vf;
 }
 
+// Large k_tr_a graphs (pr_trace = operation_trace): the same values in TRACE order -- kind[t],
+// len_t[t] read and pref[t] written coalesced, only c_tp scattered (through tpos, the inverse of
+// tperm).  The position-order form above gathers kind / len_t and scatters pref / c_t at random
+// t: four random streams per trace, 11 ms at C5's 100M traces.  c_t itself
+// is not written: the fused iteration reads only c_tp.
+__global__ void k_pref_apply_t(const double* __restrict__ kind, const int32_t* __restrict__ len_t, int32_t T,
+                               const double* __restrict__ scal, int anomaly, float cd, double phi, float* __restrict__ pref,
+                               const int32_t* __restrict__ tpos, float* __restrict__ c_tp) {
+    const int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= T) return;
+    const double k = kind[t];
+    const double v = !anomaly ? 1.0 / k / scal[2]                                               // :74
+                              : 1.0 / (k / scal[2] * phi + 1.0 / (double)len_t[t]) / scal[3] * phi;   // :80-85
+    const float vf = (float)v;
+    pref[t] = vf;
+    c_tp[tpos[t]] = cd * vf;   // (1.0 - d) * v in float32 (T4)
+}
+__global__ void k_inv_perm(const int32_t* __restrict__ perm, int32_t n, int32_t* __restrict__ inv) {
+    const int32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < n) inv[perm[p]] = p;
+}
+
 // ---------------------------------------------------------------- iteration
 // M_s / M_r per iteration live in MSH shards (an atomicMax per block or op on ONE word would
 // serialise ~2k same-address atomics per iteration); readers reduce the shards.
@@ -3176,6 +3198,7 @@ static int tr_layout(mr_ctx* ctx, mr_graph* g, const int64_t* off, const uint16_
     MR_TRY(c64.alloc(ctx, (size_t)W + 1));
     MR_TRY(g->tperm.alloc(ctx, (size_t)std::max(T, 1)));
     MR_TRY(g->w_tp.alloc(ctx, (size_t)std::max(T, 1)));
+    g->tpos_ok = false;
     MR_TRY(g->coff.alloc(ctx, (size_t)W + 1));
     // (length, secondary key): a stable radix sort, equal keys in trace order -- for wide graphs (the
     // cold count as secondary key) and kind-compressed ones, whose fixed-point scale depends on
@@ -3426,6 +3449,7 @@ int mr_graph_prepare_batch(mr_ctx* ctx, mr_graph* const* gs, int n, std::vector<
         MR_TRY(trz[(size_t)i].alloc(ctx, (size_t)nz));
         MR_TRY(c64[(size_t)i].alloc(ctx, (size_t)W + 1));
         MR_TRY(g->tperm.alloc(ctx, (size_t)std::max(T, 1)));
+        g->tpos_ok = false;
         MR_TRY(g->w_tp.alloc(ctx, (size_t)std::max(T, 1)));
         MR_TRY(g->coff.alloc(ctx, (size_t)W + 1));
         const int64_t nch = 2 * (int64_t)W + (nnz / WAVE + 2 * (int64_t)N) / 4 + 2;   // as tr_layout
@@ -3712,6 +3736,20 @@ static int pagerank_setup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool 
     const float cd = (float)(1.0 - d);
     // k_tr_a graphs whose pr_trace is operation_trace: c_t in position order from the same launch
     const bool fuse_gather = tr && !prt && !prl && n_pr == T;
+    // large graphs: trace order, c_tp scattered through the inverse permutation (built once per layout)
+    const char* pte = getenv("MR_PREF_T_MIN");   // (tests, A/B; read per call) traces from which the trace-order form runs
+    const int64_t pref_t_min = pte ? (int64_t)atoll(pte) : (int64_t)1 << 20;
+    if (fuse_gather && T > 0 && (int64_t)T >= pref_t_min) {
+        if (!g->tpos_ok) {
+            MR_TRY(g->tpos.alloc(ctx, (size_t)T));
+            hipLaunchKernelGGL(k_inv_perm, dim3(cdiv(T, 256)), dim3(256), 0, st, g->tperm.p, T, g->tpos.p);
+            g->tpos_ok = true;
+        }
+        hipLaunchKernelGGL(k_pref_apply_t, dim3(cdiv(T, 256)), dim3(256), 0, st, g->kind.p, g->len_t.p, T, g->scal.p,
+                           anomaly, cd, g->phi, g->pref.p, g->tpos.p, g->c_tp.p);
+        MR_DEBUG_CHECK(ctx, "k_pref_apply_t");
+        return MR_OK;
+    }
     if (n_pr > 0)
         hipLaunchKernelGGL(k_pref_apply, dim3(nbp), dim3(TB), 0, st, g->kind.p, prt, prl, g->len_t.p, n_pr,
                            g->scal.p, anomaly, cd, g->phi, g->pref.p, g->c_t.p, fuse_gather ? (const int32_t*)g->tperm.p : nullptr,

@@ -126,6 +126,31 @@ def test_kinds_partition_and_table_paths(c2, part_min, monkeypatch):
     dg.close()
 
 
+@pytest.mark.parametrize("anomaly", [False, True])
+def test_trace_order_preference_equals_position_order(c2, anomaly, monkeypatch):
+    """The trace-order preference form (k_pref_apply_t: large graphs, c_tp scattered through the
+    inverse of tperm) against the position-order form on the C2 graph: the same pref vector and
+    the same weights, bitwise; and the oracle's preference within 1 fp32 ulp."""
+    from microrank_amd import _lib
+    from microrank_amd.graph import DeviceGraph
+
+    st, sg = c2
+    g = sg.as_graph()
+    v = orc.preference(g, orc.trace_kinds(g), anomaly)
+    ctx = _lib.default_context()
+    dg = DeviceGraph.upload(ctx, host_graph_from_oracle(g))
+    monkeypatch.setenv("MR_PREF_T_MIN", "1000000000")   # position order
+    dg.pagerank(anomaly)
+    w0, _c0, _k0, p0 = dg.fetch(kinds=True)
+    monkeypatch.setenv("MR_PREF_T_MIN", "0")            # trace order
+    dg.pagerank(anomaly)
+    w1, _c1, _k1, p1 = dg.fetch(kinds=True)
+    assert p1.tobytes() == p0.tobytes()
+    assert w1.tobytes() == w0.tobytes()
+    np.testing.assert_allclose(p1, v, rtol=1.2e-7, atol=0)
+    dg.close()
+
+
 def _oracle_graph_from_host(hg) -> "orc.Graph":
     T, N = hg.T, hg.N
     sr_t = np.repeat(np.arange(T, dtype=np.int64), np.diff(hg.sr_off))
