@@ -153,6 +153,7 @@ int mr_coll_allgather(mr_ctx* ctx, const void* dsend, void* drecv, int64_t n, in
 // slot still being summed (its next push of that parity needs every rank's flag of the round
 // between).  Every spin is bounded (PEER_TIMEOUT): a missing peer becomes an error, not a hang.
 // region: [flag words][all-reduce slots: 2 parities x R x W][exchange area A][exchange area B]
+//         [block flags: R x nbf] (the k_fx_b-fused exchange, mr_peer_fx_prepare)
 // flag words: [0, 64) all-reduce arrivals by source rank, [64, 127) exchange arrivals by source,
 // 127 the error word
 constexpr int PEER_FLAGS = 128, PEER_XF = 64, PEER_ERR = 127, PEER_MAXR = 63;
@@ -225,23 +226,25 @@ void mr_comm_peer_destroy(mr_ctx* ctx) {
     if (ctx->peer_dev) (void)hipFree(ctx->peer_dev);
     ctx->peer_region = nullptr;
     ctx->peer_dev = nullptr;
-    ctx->peer_words = ctx->peer_xa = ctx->peer_xb = 0;
+    ctx->peer_words = ctx->peer_xa = ctx->peer_xb = ctx->peer_nbf = 0;
     ctx->peer_seq = ctx->peer_xseq = ctx->peer_arrived = 0;
 }
 
 // (collective) a receive region of at least `words` words per slot on every rank, mapped everywhere
 // (collective: every rank asks for the same sizes) words per all-reduce slot, words of exchange
 // areas A and B; a region too small is replaced (and re-exported) on every rank
-static int peer_ensure(mr_ctx* ctx, int64_t words, int64_t xa = 0, int64_t xb = 0) {
-    if (ctx->peer_region && ctx->peer_words >= words && ctx->peer_xa >= xa && ctx->peer_xb >= xb) return MR_OK;
+static int peer_ensure(mr_ctx* ctx, int64_t words, int64_t xa = 0, int64_t xb = 0, int64_t nbf = 0) {
+    if (ctx->peer_region && ctx->peer_words >= words && ctx->peer_xa >= xa && ctx->peer_xb >= xb && ctx->peer_nbf >= nbf)
+        return MR_OK;
     const int R = ctx->nranks;
     if (R > PEER_MAXR) return mr_fail(ctx, MR_ERR_ARG, "peer collectives: at most %d ranks", PEER_MAXR);
     words = std::max(words, ctx->peer_words);
     xa = std::max(xa, ctx->peer_xa);
     xb = std::max(xb, ctx->peer_xb);
+    nbf = std::max(nbf, ctx->peer_nbf);
     mr_comm_peer_destroy(ctx);
-    const size_t bytes = ((size_t)PEER_FLAGS + 2 * (size_t)R * (size_t)words + (size_t)xa + (size_t)xb) *
-                         sizeof(unsigned long long);
+    const size_t bytes = ((size_t)PEER_FLAGS + 2 * (size_t)R * (size_t)words + (size_t)xa + (size_t)xb +
+                          (size_t)R * (size_t)nbf) * sizeof(unsigned long long);
     // (local failures from here on are agreed over the ranks below, never returned alone: every
     // rank must reach the same collectives)
     int32_t bad = 0;
@@ -258,16 +261,33 @@ static int peer_ensure(mr_ctx* ctx, int64_t words, int64_t xa = 0, int64_t xb = 
     ctx->peer_words = words;
     ctx->peer_xa = xa;
     ctx->peer_xb = xb;
+    ctx->peer_nbf = nbf;
     ctx->peer_seq = ctx->peer_xseq = ctx->peer_arrived = 0;
     static_assert(sizeof(hipIpcMemHandle_t) % 8 == 0, "IPC handle size");
     const int64_t hw = (int64_t)(sizeof(hipIpcMemHandle_t) / 8);
+    // the handle and this rank's device (PCI domain / bus / device) in one gather: ranks that share
+    // a device must not spin inside large launches (mr_peer_fx_prepare)
+    std::vector<uint64_t> mine_w((size_t)hw + 1);
+    memcpy(mine_w.data(), &mine, sizeof mine);
+    {
+        hipDeviceProp_t pr;
+        mine_w[(size_t)hw] = hipGetDeviceProperties(&pr, ctx->device) == hipSuccess
+                                 ? ((uint64_t)(uint32_t)pr.pciDomainID << 32 | (uint64_t)pr.pciBusID << 8 | (uint64_t)pr.pciDeviceID)
+                                 : (uint64_t)ctx->rank + 1;   // (unknown: assume distinct)
+    }
     DBuf<uint64_t> hs, all;
-    MR_TRY(hs.upload(ctx, (const uint64_t*)&mine, (size_t)hw));
-    MR_TRY(all.alloc(ctx, (size_t)hw * R));
-    MR_TRY(mr_coll_allgather(ctx, hs.p, all.p, hw, MR_DT_U64));
-    std::vector<hipIpcMemHandle_t> hh((size_t)R);
-    MR_TRY_HIP(ctx, hipMemcpyAsync(hh.data(), all.p, sizeof(hipIpcMemHandle_t) * R, hipMemcpyDeviceToHost, ctx->stream));
+    MR_TRY(hs.upload(ctx, mine_w.data(), (size_t)hw + 1));
+    MR_TRY(all.alloc(ctx, (size_t)(hw + 1) * R));
+    MR_TRY(mr_coll_allgather(ctx, hs.p, all.p, hw + 1, MR_DT_U64));
+    std::vector<uint64_t> allw((size_t)(hw + 1) * R);
+    MR_TRY_HIP(ctx, hipMemcpyAsync(allw.data(), all.p, allw.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, ctx->stream));
     MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    std::vector<hipIpcMemHandle_t> hh((size_t)R);
+    ctx->peer_same_dev = false;
+    for (int r = 0; r < R; ++r) {
+        memcpy(&hh[(size_t)r], allw.data() + (size_t)(hw + 1) * r, sizeof(hipIpcMemHandle_t));
+        if (r != ctx->rank && allw[(size_t)(hw + 1) * r + hw] == mine_w[(size_t)hw]) ctx->peer_same_dev = true;
+    }
     ctx->peer_map.assign((size_t)R, nullptr);
     for (int r = 0; r < R && !bad; ++r) {   // (a mapping may fail: no peer access between these devices)
         if (r == ctx->rank) {
@@ -388,6 +408,61 @@ __global__ void k_peer_wait(unsigned long long* region, int nranks, unsigned lon
             }
         }
     __atomic_thread_fence(__ATOMIC_ACQUIRE);
+}
+
+// ---- the exchange fused into k_fx_b (mr_pagerank.hip): mode 1 blocks push their ops' limbs into
+// every rank's slot for this rank and then store the round number (seq + 1) in a per-(source,
+// block) flag; mode 2 block b waits for flag (src, b) of every source -- only the words it sums --
+// and sums the R slots in rank order.  A flag holds the number of the last round its block pushed
+// (a store, not a count), so graphs of different sizes on one context need no bookkeeping.
+// (collective) px for words per slot (2N + R) and nbf k_fx_b blocks; MR_ERR_STATE when the peer path
+// is off or the ranks could not map each other's regions.
+int mr_peer_fx_prepare(mr_ctx* ctx, int64_t words, int32_t nbf, MrPeerX* px) {
+    if (!ctx->peer_on || ctx->nranks < 2 || !mr_coll_ready(ctx)) return MR_ERR_STATE;
+    const int rc = peer_ensure(ctx, words, 0, 0, nbf);
+    if (rc != MR_OK) return rc;
+    const int R = ctx->nranks;
+    px->peers = ctx->peer_dev;
+    px->region = (unsigned long long*)ctx->peer_region;
+    px->R = R;
+    px->rank = ctx->rank;
+    px->nbf = (int32_t)ctx->peer_nbf;
+    px->W = ctx->peer_words;
+    px->slots = PEER_FLAGS;
+    px->bflags = (int64_t)PEER_FLAGS + 2 * (int64_t)R * ctx->peer_words + ctx->peer_xa + ctx->peer_xb;
+    px->err = PEER_ERR;
+    px->seq = ctx->peer_seq;
+    px->timeout = mr_peer_timeout_ticks();
+    px->spin = 1;
+    return MR_OK;
+}
+void mr_peer_fx_round_done(mr_ctx* ctx, MrPeerX* px) {
+    ++ctx->peer_seq;
+    px->seq = ctx->peer_seq;
+}
+bool mr_peer_same_device(const mr_ctx* ctx) { return ctx->peer_same_dev; }
+
+// one block waits for every (source, block) flag of round seq (ranks sharing a device: mode-2
+// blocks spinning beside a peer's k_tr_a would hold the CUs its 160-KB blocks need)
+__global__ void __launch_bounds__(PEER_T) k_peer_bwait(const MrPeerX px, int32_t nb) {
+    GLBP unsigned long long* reg = (GLBP unsigned long long*)px.region;
+    const unsigned long long need = px.seq + 1, t0 = __builtin_amdgcn_s_memrealtime();
+    for (int64_t i = threadIdx.x; i < (int64_t)px.R * nb; i += PEER_T) {
+        const int64_t w = px.bflags + (i / nb) * px.nbf + i % nb;
+        while (__hip_atomic_load(reg + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < need) {
+            __builtin_amdgcn_s_sleep(2);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > px.timeout) {
+                __hip_atomic_store(reg + px.err, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                return;
+            }
+        }
+    }
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);
+}
+int mr_peer_fx_wait(mr_ctx* ctx, const MrPeerX& px, int32_t nb) {
+    hipLaunchKernelGGL(k_peer_bwait, dim3(1), dim3(PEER_T), 0, ctx->stream, px, nb);
+    MR_TRY_HIP(ctx, hipGetLastError());
+    return MR_OK;
 }
 
 bool mr_peer_ready(const mr_ctx* ctx) { return ctx->peer_on && ctx->nranks >= 2 && mr_coll_ready(ctx); }

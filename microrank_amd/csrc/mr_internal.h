@@ -72,6 +72,8 @@ struct mr_ctx {
     uint64_t peer_seq = 0;                      // all-reduces completed (slot parity)
     uint64_t peer_arrived = 0;                  // blocks every source has pushed so far (the flags' target)
     uint64_t peer_xseq = 0;                     // exchange rounds completed
+    int64_t peer_nbf = 0;                       // k_fx_b blocks the block-flag area holds per source
+    bool peer_same_dev = false;                 // some other rank runs on this rank's device
     // k_pr_cluster timed out on this context (its clusters were not co-resident): launch per
     // iteration from then on
     bool no_persist = false;
@@ -376,6 +378,20 @@ int mr_peer_allreduce_f64(mr_ctx* ctx, double* dbuf, int64_t n);   // (fp64 sums
 // (collective) MR_ERR_COMM when a round timed out on any rank (a peer never pushed); the regions
 // are then reset on every rank
 int mr_peer_check(mr_ctx* ctx, const char* what);
+// the exchange fused into k_fx_b (mr_comm.hip): region addresses and the round
+struct MrPeerX {
+    unsigned long long* const* peers;   // device table of every rank's region (null: off)
+    unsigned long long* region;         // this rank's region
+    int32_t R, rank, nbf, spin;         // spin: mode-2 blocks wait themselves (0: k_peer_bwait did)
+    int64_t slots, W, bflags, err;      // word offsets in a region: slot area, words per slot, block flags, error word
+    uint64_t seq;                       // the round (slot parity seq & 1, flags store seq + 1)
+    unsigned long long timeout;         // s_memrealtime ticks
+};
+int mr_peer_fx_prepare(mr_ctx* ctx, int64_t words, int32_t nbf, MrPeerX* px);   // (collective)
+int mr_peer_fx_wait(mr_ctx* ctx, const MrPeerX& px, int32_t nb);   // one block waits for every flag of the round
+void mr_peer_fx_round_done(mr_ctx* ctx, MrPeerX* px);
+bool mr_peer_same_device(const mr_ctx* ctx);
+unsigned long long mr_peer_timeout_ticks();
 // exchanges through the peer regions: areas A (0) and B (1) of every rank's region
 bool mr_peer_ready(const mr_ctx* ctx);
 int mr_peer_xensure(mr_ctx* ctx, int64_t xa, int64_t xb);    // (collective) area sizes in words

@@ -2213,12 +2213,20 @@ static int fb_ops(int32_t N, bool many) {
     return N <= 8192 ? (many ? 64 : 16) : 32;
 }
 constexpr int64_t FB_MANY_BLOCKS = 1024;   // 16-op blocks of a launch from which "many" holds
+// px.peers (sharded graphs on the peer path, one graph per launch): the exchange is fused in --
+// mode 1 pushes the block's limbs (and block 0 this rank's r' maximum) into every rank's slot for
+// this rank and stores the round number in the block's flag there; mode 2 block b waits for flag
+// (src, b) of every source (px.spin; else k_peer_bwait waited before the launch) and sums the R
+// slots in rank order.  Bitwise the all-reduce path: the same integers summed.
 template <int FB_W>
 __global__ void __launch_bounds__(WAVE * FB_W) k_fx_b(const GDev* __restrict__ gs, int32_t ng, int32_t split,
-                                                     double d, int it, int mode) {
+                                                     double d, int it, int mode, const MrPeerX px) {
     __shared__ unsigned long long slo[FB_W * WAVE], shi[FB_W * WAVE];
     __shared__ double lssv[WAVE];
+    __shared__ int s_ok;
     const GDev& G = gs[fx_graph(gs, ng, split, 3)];
+    const bool pxo = px.peers != nullptr;   // (uniform)
+    const GLB unsigned long long* preg = (const GLB unsigned long long*)px.region;
     const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
     const int32_t OPB = G.fb_ops, GR = WAVE / OPB;
     const int32_t ol = lane % OPB, grp = lane / OPB;
@@ -2255,8 +2263,8 @@ __global__ void __launch_bounds__(WAVE * FB_W) k_fx_b(const GDev* __restrict__ g
     }
     // the call-graph term alpha (P_ss s_k)[op] / M_s(k) (pagerank.py:122-124) of the block's ops: a
     // wave per op, its lanes striding the op's parents, one fixed-order wave sum (a hub op with
-    // thousands of parents costs one wave, not one thread)
-    {
+    // thousands of parents costs one wave, not one thread).  (Not in mode 1: its sums only.)
+    if (mode != 1) {
         const double Ms = wave_max(bits2d(G.mslot[(size_t)2 * MSH * k3c + lane]));
         const GLB double* sp_cur = gp(G.spb[it & 1]);
         const GLB int64_t* ss_off = gp(G.ss_off);
@@ -2305,10 +2313,50 @@ __global__ void __launch_bounds__(WAVE * FB_W) k_fx_b(const GDev* __restrict__ g
     const bool fin = w == 0 && lane < OPB && on;
     const int32_t op = fin && G.perm ? G.perm[o] : o;
     const float uo = fin ? G.u_o[op] : 0.0f;
-    if ((int32_t)blockIdx.x == G.blk0fb && w == 1 && mode) {   // r' maxima riding on the limb sum
+    const int32_t bidx = (int32_t)blockIdx.x - G.blk0fb;
+    const size_t par = (size_t)(px.seq & 1) * (size_t)px.R;   // this round's slots: [par + src] x W words
+    if (bidx == 0 && w == 1 && mode) {   // r' maxima riding on the limb sum
         unsigned long long* Mn = G.mslot + (size_t)2 * MSH * ((it % 3 + 1) % 3);
-        if (mode == 1) rmax_put(G, Mn, G.fx_limb + 2 * (size_t)N, lane);
-        else rmax_take_bits(G.fx_limb + 2 * (size_t)N, G.nranks, Mn, lane);
+        if (!pxo) {
+            if (mode == 1) rmax_put(G, Mn, G.fx_limb + 2 * (size_t)N, lane);
+            else rmax_take_bits(G.fx_limb + 2 * (size_t)N, G.nranks, Mn, lane);
+        } else if (mode == 1) {   // this rank's maximum into word 2N + rank of its slot on every rank
+            const double m = wave_max(bits2d(Mn[MSH + lane]));
+            if (lane < px.R)
+                __hip_atomic_store((GLB unsigned long long*)px.peers[lane] + px.slots + (par + px.rank) * px.W +
+                                       2 * (size_t)N + px.rank,
+                                   d2bits(m), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+    if (pxo && mode == 2) {
+        if (px.spin && threadIdx.x == 0) {   // flag (src, bidx) of every source: this round's words are in
+            s_ok = 1;
+            const unsigned long long need = px.seq + 1, t0 = __builtin_amdgcn_s_memrealtime();
+            for (int r = 0; r < px.R && s_ok; ++r)
+                while (__hip_atomic_load(preg + px.bflags + (int64_t)r * px.nbf + bidx, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_SYSTEM) < need) {
+                    __builtin_amdgcn_s_sleep(2);
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > px.timeout) {
+                        s_ok = 0;
+                        __hip_atomic_store((GLB unsigned long long*)px.region + px.err, 1ull, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_SYSTEM);
+                        break;
+                    }
+                }
+            __atomic_thread_fence(__ATOMIC_ACQUIRE);
+        } else if (!px.spin && threadIdx.x == 0) {
+            s_ok = 1;
+        }
+        __syncthreads();
+        if (!s_ok) return;   // (the error word reports it; the host raises MR_ERR_COMM)
+        if (bidx == 0 && w == 1) {   // every rank's r' maximum: word 2N + src of slot src
+            unsigned long long b = 0ull;
+            for (int j = lane; j < px.R; j += WAVE)
+                b = max(b, __hip_atomic_load(preg + px.slots + (par + j) * px.W + 2 * (size_t)N + j, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_SYSTEM));
+            const double m = wave_max(bits2d(b));
+            if (lane == 0) atomicMax(&G.mslot[(size_t)2 * MSH * ((it % 3 + 1) % 3) + MSH], d2bits(m));
+        }
     }
     unsigned long long lo = 0ull, hi = 0ull;
     if (nbl > 0) {
@@ -2343,6 +2391,29 @@ __global__ void __launch_bounds__(WAVE * FB_W) k_fx_b(const GDev* __restrict__ g
         shi[w * WAVE + lane] = hi;
     }
     __syncthreads();
+    if (pxo && mode == 1) {   // push the block's limbs to every rank, then the block's flag there
+        if (fin) {
+            lo = hi = 0ull;
+            for (int k = 0; k < FB_W; ++k) {
+                lo += slo[k * WAVE + lane];
+                hi += shi[k * WAVE + lane];
+            }
+            for (int r = 0; r < px.R; ++r) {
+                GLB unsigned long long* dst = (GLB unsigned long long*)px.peers[r] + px.slots + (par + px.rank) * px.W;
+                __hip_atomic_store(dst + 2 * op, lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(dst + 2 * op + 1, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (every wave: the r' word of wave 1 too)
+        __syncthreads();
+        if ((int32_t)threadIdx.x < px.R) {
+            __atomic_thread_fence(__ATOMIC_RELEASE);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store((GLB unsigned long long*)px.peers[threadIdx.x] + px.bflags + (int64_t)px.rank * px.nbf + bidx,
+                               (unsigned long long)(px.seq + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        return;
+    }
     if (!fin) return;
     lo = hi = 0ull;
     for (int k = 0; k < FB_W; ++k) {
@@ -2354,7 +2425,14 @@ __global__ void __launch_bounds__(WAVE * FB_W) k_fx_b(const GDev* __restrict__ g
         G.fx_limb[2 * op + 1] = hi;
         return;
     }
-    if (mode == 2) {
+    if (mode == 2 && pxo) {   // the R slots in rank order (integers: the all-reduce's sum)
+        lo = hi = 0ull;
+        for (int r = 0; r < px.R; ++r) {
+            const GLB unsigned long long* sl = preg + px.slots + (par + r) * px.W;
+            lo += __hip_atomic_load(sl + 2 * op, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            hi += __hip_atomic_load(sl + 2 * op + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    } else if (mode == 2) {
         lo = G.fx_limb[2 * op];
         hi = G.fx_limb[2 * op + 1];
     }
@@ -4216,6 +4294,24 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         }
         sst = ctx->side;
     }
+    // sharded fused graph on the peer path: the exchange inside k_fx_b (MR_PEER_SPLIT=1: the separate
+    // push / reduce launches; relabelled graphs always -- the ranks' op labels differ, so a block's
+    // columns on one rank are not the same ops on another)
+    MrPeerX px{}, px_off{};
+    bool px_on = false;
+    if (coll && ng == 1 && gs[0]->fused && !gs[0]->wide && !gs[0]->relabeled && mr_peer_ready(ctx) &&
+        !getenv("MR_PEER_SPLIT")) {
+        const int prc = mr_peer_fx_prepare(ctx, 2 * (int64_t)gs[0]->N + ctx->nranks, (int32_t)blocks_fb, &px);
+        if (prc == MR_OK) {
+            px_on = true;
+            // ranks sharing a device: mode-2 blocks spinning there would hold CUs a peer's 160-KB
+            // k_tr_a blocks need -- one waiting block instead (MR_PEER_SPIN=0/1 forces it)
+            const char* se = getenv("MR_PEER_SPIN");
+            px.spin = se ? atoi(se) != 0 : !mr_peer_same_device(ctx);
+        } else if (prc != MR_ERR_STATE) {
+            return prc;
+        }
+    }
     hm.mark("pre-loop");
     if (persist) {   // all iterations in one launch (k_pr_cluster)
         size_t lds = 0;
@@ -4256,23 +4352,28 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
             hipLaunchKernelGGL(tr_a, dim3(blocks_fa), dim3(plan.NT), lds_f, st, dv.p, ng, split_fa, d, alpha, it, 0);
             MR_DEBUG_CHECK(ctx, "k_tr_a");
             if (any_wide && sst != st) MR_TRY_HIP(ctx, hipStreamWaitEvent(st, ctx->side_ev[1], 0));   // k_cold_ops done
-            auto fx_b = [&](int mode) {
+            auto fx_b = [&](int mode, const MrPeerX& p) {
                 if (fb_small)
                     hipLaunchKernelGGL(k_fx_b<FB_W_SMALL>, dim3(blocks_fb), dim3(WAVE * FB_W_SMALL), 0, st, dv.p, ng,
-                                       split_fb, d, it, mode);
+                                       split_fb, d, it, mode, p);
                 else
                     hipLaunchKernelGGL(k_fx_b<FB_W>, dim3(blocks_fb), dim3(WAVE * FB_W), 0, st, dv.p, ng, split_fb, d,
-                                       it, mode);
+                                       it, mode, p);
             };
             if (!coll) {
-                fx_b(0);
+                fx_b(0, px_off);
+            } else if (px_on) {   // the exchange fused into k_fx_b: push in mode 1, per-block waits in mode 2
+                fx_b(1, px);
+                if (!px.spin) MR_TRY(mr_peer_fx_wait(ctx, px, blocks_fb));
+                fx_b(2, px);
+                mr_peer_fx_round_done(ctx, &px);
             } else {   // ONE all-reduce: the P_sr r limbs and every rank's r' max (exact: integers)
-                fx_b(1);
+                fx_b(1, px_off);
                 const int64_t nw = 2 * (int64_t)gs[0]->N + ctx->nranks;
                 const int prc = mr_peer_allreduce_u64(ctx, (unsigned long long*)gs[0]->fx_limb.p, nw);
                 if (prc == MR_ERR_STATE) MR_TRY(mr_coll_allreduce(ctx, gs[0]->fx_limb.p, nw, MR_DT_U64, 0));
                 else MR_TRY(prc);
-                fx_b(2);
+                fx_b(2, px_off);
             }
             MR_DEBUG_CHECK(ctx, "k_fx_b");
         }

@@ -38,8 +38,10 @@ def _whole(anomaly):
     return w, cov
 
 
-def _worker(rank, world, port, anomaly, backend, q, big=None, tile=False, walk_ranks=(), empty_last=False, peer=False):
+def _worker(rank, world, port, anomaly, backend, q, big=None, tile=False, walk_ranks=(), empty_last=False, peer=False,
+            env=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.update(env or {})
     if tile is True or (tile and rank in tile):   # True: every rank; a tuple: those ranks
         os.environ["MR_NO_FUSED"] = "1"   # read once, at this process's first graph prepare
     if rank in walk_ranks:
@@ -76,12 +78,12 @@ def _worker(rank, world, port, anomaly, backend, q, big=None, tile=False, walk_r
         dist.destroy_process_group()
 
 
-def _run(world, anomaly, backend, big=None, tile=False, walk_ranks=(), empty_last=False, peer=False):
+def _run(world, anomaly, backend, big=None, tile=False, walk_ranks=(), empty_last=False, peer=False, env=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_worker, args=(r, world, port, anomaly, backend, q, big, tile, walk_ranks,
-                                               empty_last, peer))
+                                               empty_last, peer, env))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -124,13 +126,20 @@ def test_four_shards_one_gpu_match_whole_graph(tile, peer):
     assert sum(r[3]["T"] for r in res) == _window_graph().T
 
 
-def test_four_shards_peer_matches_host_collective_bitwise():
-    """The peer all-reduce and the host-staged all-reduce give bitwise the same weights on the
-    fused path (both sum the same exact integer limbs)."""
+@pytest.mark.parametrize("mode", ["fused-wait", "fused-spin", "split"])
+def test_four_shards_peer_matches_host_collective_bitwise(mode):
+    """The peer exchange and the host-staged all-reduce give bitwise the same weights on the fused
+    path (both sum the same exact integer limbs).  fused-*: the exchange inside k_fx_b (mode-1
+    blocks push their limbs and store their round flag, mode-2 blocks sum the R slots) -- with
+    one waiting block before mode 2 (ranks sharing a device, the default here) or with every
+    mode-2 block spinning on its own flags (the distinct-GPU form; safe here: the window graph's
+    k_tr_a blocks are small); split: the separate push / reduce launches (MR_PEER_SPLIT)."""
+    env = {"fused-wait": {}, "fused-spin": {"MR_PEER_SPIN": "1"}, "split": {"MR_PEER_SPLIT": "1"}}[mode]
     a = _run(4, False, "host", peer=False)
-    b = _run(4, False, "host", peer=True)
+    b = _run(4, False, "host", peer=True, env=env)
     for x, y in zip(a, b):
         assert x[1].tobytes() == y[1].tobytes()
+        np.testing.assert_array_equal(x[2], y[2])
 
 
 def test_one_rank_rccl_matches_whole_graph():
