@@ -626,27 +626,11 @@ extern "C" int mr_rca_window(mr_ctx* ctx, const mr_spans* s, int64_t t0, int64_t
 // time (all of the group's graphs share each iteration's k_tr_a + k_fx_b launches) while the
 // auxiliary streams already build the next group's graphs.
 static int win_aux(mr_ctx* ctx, int n) {
-    // MR_WIN_AUX_PRIO=low|high|same: the auxiliary streams' priority against the PageRank stream's
-    static const int prio = [] {
-        const char* e = getenv("MR_WIN_AUX_PRIO");
-        if (e && !strcmp(e, "low")) return 1;
-        if (e && !strcmp(e, "high")) return 2;
-        return 0;
-    }();
     while ((int)ctx->aux.size() < n) {
         mr_ctx* a = nullptr;
         const int rc = mr_ctx_create(ctx->device, ctx->flags, &a);
         if (rc != MR_OK) return mr_fail(ctx, rc, "mr_windows_batch: auxiliary context creation failed");
-        if (prio) {   // (lower number = higher priority)
-            int lo = 0, hi = 0;
-            hipStream_t s2 = nullptr;
-            if (hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess &&
-                hipStreamCreateWithPriority(&s2, hipStreamNonBlocking, prio == 1 ? lo : hi) == hipSuccess) {
-                (void)hipStreamDestroy(a->stream);
-                a->stream = s2;
-            }
-        }
-        ctx->aux.push_back(a);
+        ctx->aux.push_back(a);   // (same stream priority as the PageRank stream: high priority measured C2 -4 %)
     }
     return MR_OK;
 }
@@ -696,14 +680,8 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
     const char* ce = getenv("MR_WIN_CHUNK");   // windows built together on one stream
     const int chunk_size = ce ? std::max(1, atoi(ce)) : group_size >= 64 ? 8 : 4;
     const int gsz = std::min<int>(n_windows, group_size);
-    // group g: windows [gbeg[g], gbeg[g + 1]).  MR_WIN_RAMP=k (read per call): a first group of k
-    // windows, so the PageRank stream starts after k builds instead of a whole group's (C2: 4 / 8 /
-    // 16 with groups of 20-30 within noise of plain groups of 32 -- not default)
+    // group g: windows [gbeg[g], gbeg[g + 1])
     std::vector<int32_t> gbeg(1, 0);
-    if (const char* re = getenv("MR_WIN_RAMP")) {
-        const int32_t k = std::max(0, atoi(re));
-        if (k > 0 && k < n_windows) gbeg.push_back(k);
-    }
     while (gbeg.back() < n_windows) gbeg.push_back(std::min<int32_t>(n_windows, gbeg.back() + gsz));
     const int ngroups = (int)gbeg.size() - 1;
     std::vector<int32_t> group_of((size_t)n_windows);

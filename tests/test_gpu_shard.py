@@ -394,13 +394,15 @@ def test_sharded_build_from_spans_matches_single_gpu(anomaly, world, peer):
 
 
 # ------------------------------------------------------------ peer regions over several graphs
-def _seq_worker(rank, world, port, peer, q):
+def _seq_worker(rank, world, port, peer, q, env=None):
     """One context ranks a sequence of graphs of different op counts: the window graph (fused,
     2N + R words), a 20k-op graph (tile path, N + R words), the window graph again (smaller than
     the one before) and a 10k-op fused graph.  Every all-reduce of the sequence goes through the
     same peer region, whose arrival counts carry over from one graph to the next."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.update(env or {})
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    k = -1
     try:
         from gpu_util import host_graph_from_oracle
         from microrank_amd import _lib, shard, synth
@@ -414,7 +416,7 @@ def _seq_worker(rank, world, port, peer, q):
         seq = [win, synth.big_graph(20_000, 6_000, seed=3, shard=(rank, world)), win,
                synth.big_graph(10_000, 6_000, seed=5, shard=(rank, world))]
         out = []
-        for hg in seq:
+        for k, hg in enumerate(seq):
             dg = DeviceGraph.upload(ctx, hg)
             w, cov = shard.sharded_pagerank(dg, True)
             out.append((w, cov))
@@ -422,28 +424,29 @@ def _seq_worker(rank, world, port, peer, q):
         ctx.close()
         q.put((rank, out, True, None))
     except Exception as e:
-        q.put((rank, repr(e), None, None))
+        q.put((rank, f"graph {k}: {e!r}", None, None))
     finally:
         dist.destroy_process_group()
 
 
-def _run_seq(world, peer):
+def _run_seq(world, peer, env=None):
     mpc = mp.get_context("spawn")
     q = mpc.Queue()
     port = _free_port()
-    procs = [mpc.Process(target=_seq_worker, args=(r, world, port, peer, q)) for r in range(world)]
+    procs = [mpc.Process(target=_seq_worker, args=(r, world, port, peer, q, env)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=240) for _ in procs], key=lambda r: r[0])
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for r in res:
-        assert r[2] is not None, f"rank {r[0]} failed: {r[1]}"
+    bad = [f"rank {r[0]} failed: {r[1]}" for r in res if r[2] is None]
+    assert not bad, "; ".join(bad)
     return res
 
 
-def test_peer_regions_carry_over_graphs_of_different_sizes():
+@pytest.mark.parametrize("mode", ["fused", "split"])
+def test_peer_regions_carry_over_graphs_of_different_sizes(mode):
     """the peer all-reduce's arrival target must be the running count of pushed
     blocks, not blocks x rounds -- a smaller graph after a larger one (the window graph after the
     20k-op graph) would otherwise find its target already met and sum slots the peers had not
@@ -451,7 +454,7 @@ def test_peer_regions_carry_over_graphs_of_different_sizes():
     fused and the tile path: peer == the host-staged collective (bitwise on the fused graphs'
     exact limbs, 1e-12 on the tile path's fp64 sums) and every rank bitwise equal."""
     a = _run_seq(4, peer=False)
-    b = _run_seq(4, peer=True)
+    b = _run_seq(4, peer=True, env={"MR_PEER_SPLIT": "1"} if mode == "split" else None)
     for k in range(4):
         for r in range(4):
             wa, ca = a[r][1][k]
