@@ -216,18 +216,34 @@ __global__ void __launch_bounds__(PEER_T) k_peer_reduce(T* __restrict__ dst, int
     dst[j] = s;
 }
 
-void mr_comm_peer_destroy(mr_ctx* ctx) {
-    if (!ctx) return;
-    if (ctx->peer_region) (void)hipStreamSynchronize(ctx->stream);
-    for (size_t r = 0; r < ctx->peer_map.size(); ++r)
-        if (ctx->peer_map[r] && (int)r != ctx->rank) (void)hipIpcCloseMemHandle(ctx->peer_map[r]);
+// A replaced region is RETIRED, not freed: its memory and this process's mappings of the other
+// ranks' old regions stay until the context goes.  Freeing it would let the next allocation reuse
+// its address, and a peer re-opening the new handle could be handed its cached mapping of the old
+// one -- its pushes and signals would land in freed memory (seen: a kind exchange after two region
+// replacements timed out on every rank).  Regions are a few MB; a context replaces one a handful
+// of times (sizes only grow).
+static void peer_retire(mr_ctx* ctx) {
+    if (ctx->peer_region || ctx->peer_dev || !ctx->peer_map.empty()) {
+        if (ctx->peer_region) (void)hipStreamSynchronize(ctx->stream);
+        ctx->peer_old.push_back(mr_ctx::PeerOld{ctx->peer_region, ctx->peer_dev, ctx->peer_map, ctx->rank});
+    }
     ctx->peer_map.clear();
-    if (ctx->peer_region) (void)hipFree(ctx->peer_region);
-    if (ctx->peer_dev) (void)hipFree(ctx->peer_dev);
     ctx->peer_region = nullptr;
     ctx->peer_dev = nullptr;
     ctx->peer_words = ctx->peer_xa = ctx->peer_xb = ctx->peer_nbf = 0;
     ctx->peer_seq = ctx->peer_xseq = ctx->peer_arrived = 0;
+}
+
+void mr_comm_peer_destroy(mr_ctx* ctx) {
+    if (!ctx) return;
+    peer_retire(ctx);
+    for (const mr_ctx::PeerOld& o : ctx->peer_old) {
+        for (size_t r = 0; r < o.map.size(); ++r)
+            if (o.map[r] && (int)r != o.rank) (void)hipIpcCloseMemHandle(o.map[r]);
+        if (o.region) (void)hipFree(o.region);
+        if (o.dev) (void)hipFree(o.dev);
+    }
+    ctx->peer_old.clear();
 }
 
 // (collective) a receive region of at least `words` words per slot on every rank, mapped everywhere
@@ -242,7 +258,9 @@ static int peer_ensure(mr_ctx* ctx, int64_t words, int64_t xa = 0, int64_t xb = 
     xa = std::max(xa, ctx->peer_xa);
     xb = std::max(xb, ctx->peer_xb);
     nbf = std::max(nbf, ctx->peer_nbf);
-    mr_comm_peer_destroy(ctx);
+    // (a first region already holds any fused graph's all-reduce: 2 x 16384 limbs + the r' slots)
+    words = std::max<int64_t>(words, 2 * 16384 + PEER_MAXR + 1);
+    peer_retire(ctx);
     const size_t bytes = ((size_t)PEER_FLAGS + 2 * (size_t)R * (size_t)words + (size_t)xa + (size_t)xb +
                           (size_t)R * (size_t)nbf) * sizeof(unsigned long long);
     // (local failures from here on are agreed over the ranks below, never returned alone: every
@@ -316,7 +334,7 @@ static int peer_ensure(mr_ctx* ctx, int64_t words, int64_t xa = 0, int64_t xb = 
     MR_TRY(one.download(ctx, &bad, 1));
     MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));
     if (bad) {
-        mr_comm_peer_destroy(ctx);
+        peer_retire(ctx);
         ctx->peer_on = false;
         if (why[0]) fprintf(stderr, "[microrank] peer collectives off on rank %d: %s\n", ctx->rank, why);
         return MR_ERR_STATE;
@@ -375,7 +393,7 @@ int mr_peer_check(mr_ctx* ctx, const char* what) {
     MR_TRY(f.download(ctx, &any, 1));
     MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));
     if (!any) return MR_OK;
-    mr_comm_peer_destroy(ctx);
+    peer_retire(ctx);
     return mr_fail(ctx, MR_ERR_COMM, "%s: a rank did not arrive within the peer timeout (regions reset)", what);
 }
 

@@ -74,6 +74,13 @@ struct mr_ctx {
     uint64_t peer_xseq = 0;                     // exchange rounds completed
     int64_t peer_nbf = 0;                       // k_fx_b blocks the block-flag area holds per source
     bool peer_same_dev = false;                 // some other rank runs on this rank's device
+    struct PeerOld {   // a replaced region and its mappings, kept until the context goes (mr_comm.hip)
+        void* region;
+        unsigned long long** dev;
+        std::vector<void*> map;
+        int rank;
+    };
+    std::vector<PeerOld> peer_old;
     // k_pr_cluster timed out on this context (its clusters were not co-resident): launch per
     // iteration from then on
     bool no_persist = false;

@@ -401,7 +401,10 @@ def _seq_worker(rank, world, port, peer, q, env=None):
     same peer region, whose arrival counts carry over from one graph to the next."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     os.environ.update(env or {})
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import datetime
+    import sys
+
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=90))
     k = -1
     try:
         from gpu_util import host_graph_from_oracle
@@ -417,6 +420,7 @@ def _seq_worker(rank, world, port, peer, q, env=None):
                synth.big_graph(10_000, 6_000, seed=5, shard=(rank, world))]
         out = []
         for k, hg in enumerate(seq):
+            print(f"[seq] rank {rank} graph {k} (N {hg.N}, T {hg.T}) peer={peer} env={env}", file=sys.stderr, flush=True)
             dg = DeviceGraph.upload(ctx, hg)
             w, cov = shard.sharded_pagerank(dg, True)
             out.append((w, cov))
@@ -424,6 +428,7 @@ def _seq_worker(rank, world, port, peer, q, env=None):
         ctx.close()
         q.put((rank, out, True, None))
     except Exception as e:
+        print(f"[seq] rank {rank} graph {k} FAILED: {e!r}", file=sys.stderr, flush=True)
         q.put((rank, f"graph {k}: {e!r}", None, None))
     finally:
         dist.destroy_process_group()
@@ -445,7 +450,7 @@ def _run_seq(world, peer, env=None):
     return res
 
 
-@pytest.mark.parametrize("mode", ["fused", "split"])
+@pytest.mark.parametrize("mode", ["split", "fused"])
 def test_peer_regions_carry_over_graphs_of_different_sizes(mode):
     """the peer all-reduce's arrival target must be the running count of pushed
     blocks, not blocks x rounds -- a smaller graph after a larger one (the window graph after the
