@@ -1503,6 +1503,7 @@ struct GDev {
     int32_t T, N, n_tb, n_tiles, tshift, lds_su, blk0, n_ob, blk0b;
     int32_t blk0f, n_fa, blk0fb, n_fb;   // fused path: k_tr_a / k_fx_b block ranges
     int32_t fb_ops;                      // k_fx_b ops per block
+    int32_t lastfin;                     // k_tr_a's last block of the graph finishes the iteration (no k_fx_b)
 };
 
 // graph owning block `blk` of launch kind `which` (0 k_iter_a, 1 k_iter_b, 2 k_tr_a, 3 k_fx_b);
@@ -2135,6 +2136,87 @@ __device__ __forceinline__ double tr_walk(const GDev& G, int32_t lb, int cur, in
     return rmax;
 }
 
+// The last k_tr_a block of a graph finishes the iteration itself (small graphs: window batches),
+// so an iteration is ONE launch instead of k_tr_a + k_fx_b.  Every block writes its partial row
+// write-through (sc1), waits for its stores, and takes a ticket from the graph's counter (an
+// agent-scope add, returned); the block whose ticket completes the iteration's count reads every
+// row with sc1 loads (MI355X_MICROARCH.md hand-off table, row 1: the last adder, told by the value
+// its add returned) and does k_fx_b's work for every op -- the same exact limb sums, the same
+// call-graph term (a lane per op of <= 8 parents, a wave per op of more: wave_sum's butterfly) and
+// the same finish: bitwise k_fx_b's results.
+template <int NT>
+__device__ __noinline__ void tr_last_finish(const GDev& G, int it, double d, double Ms,
+                                            GLB unsigned long long* Mnext) {
+    constexpr int NW = NT / WAVE;
+    __shared__ int s_last;
+    const int32_t tid = (int32_t)threadIdx.x, lane = tid & (WAVE - 1), wv = tid / WAVE;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave's row stores are out
+    __syncthreads();
+    if (tid == 0) {
+        const unsigned long long t = __hip_atomic_fetch_add(gpw(G.mslot) + 6 * MSH + 1, 1ull, __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_AGENT);
+        s_last = t + 1 == (unsigned long long)G.n_fa * (unsigned long long)(it + 1);
+    }
+    __syncthreads();
+    if (!s_last) return;
+    const int32_t N = G.N, nb = G.n_fa, nxt = (it & 1) ^ 1;
+    const GLB unsigned long long* rows = gp((const unsigned long long*)G.fx_part);
+    const GLB double* sp_cur = gp(G.spb[it & 1]);
+    const GLB int64_t* ss_off = gp(G.ss_off);
+    const GLB int32_t* ss_par = gp(G.ss_par);
+    const GLB float* pw = gp(G.pw);
+    const GLB float* u_o = gp(G.u_o);
+    const double iscale = G.dscale ? G.dscale[1] : G.fx_iscale;
+    for (int32_t ob = wv * WAVE; ob < N; ob += NW * WAVE) {   // lane = op
+        const int32_t o = ob + lane;
+        const bool on = o < N;
+        unsigned long long lo = 0ull, hi = 0ull;
+        if (on)
+            for (int32_t b = 0; b < nb; ++b) {
+                const unsigned long long v = __hip_atomic_load(rows + (size_t)b * N + o, __ATOMIC_RELAXED,
+                                                               __HIP_MEMORY_SCOPE_AGENT);
+                lo += v & 0xffffffffull;
+                hi += v >> 32;
+            }
+        double ssv = 0.0;
+        bool big = false;
+        if (on) {
+            const int64_t e0 = ss_off[o], e1 = ss_off[o + 1];
+            if (e1 - e0 <= 8) {
+                int32_t pp[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) pp[k] = e0 + k < e1 ? ss_par[e0 + k] : -1;
+                double t[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) t[k] = pp[k] >= 0 ? (double)pw[pp[k]] * sp_cur[pp[k]] : 0.0;
+                const double bb = ((t[0] + t[4]) + (t[2] + t[6])) + ((t[1] + t[5]) + (t[3] + t[7]));
+                ssv = G.alpha * (bb / Ms);
+            } else {
+                big = true;
+            }
+        }
+        for (uint64_t bm = __ballot(big); bm; bm &= bm - 1) {   // (wave-uniform)
+            const int j = __ffsll((unsigned long long)bm) - 1;
+            const int32_t oj = ob + j;
+            const int64_t e0 = ss_off[oj], e1 = ss_off[oj + 1];
+            double bb = 0.0;
+            for (int64_t e = e0 + lane; e < e1; e += WAVE) {
+                const int32_t pp = ss_par[e];
+                bb += (double)pw[pp] * sp_cur[pp];
+            }
+            bb = wave_sum(bb);
+            if (lane == j) ssv = G.alpha * (bb / Ms);
+        }
+        if (on) {
+            const double sum = ((double)hi * 4294967296.0 + (double)lo) * iscale;
+            const double v = d * (sum + ssv);   // pagerank.py:122-124
+            G.spb[nxt][o] = v;
+            G.sub[nxt][o] = (double)u_o[o] * v;
+            atomicMax((unsigned long long*)&Mnext[o % MSH], d2bits(v));
+        }
+    }
+}
+
 template <class Q, int SUM, int NT, int EXT>
 __global__ void __launch_bounds__(NT) k_tr_a(const GDev* __restrict__ gs, int32_t ng, int32_t split, double d,
                                              double alpha, int it, int32_t unused) {
@@ -2184,6 +2266,16 @@ __global__ void __launch_bounds__(NT) k_tr_a(const GDev* __restrict__ gs, int32_
     // (the call-graph term alpha P_ss s_k is k_fx_b's: a wave per op)
     __syncthreads();
     GLB unsigned long long* prow = gpw(G.fx_part) + (size_t)lb * N;
+    if constexpr (NT == 512) {   // (window-graph variant only: the large graphs' kernel stays as it is)
+        if (G.lastfin) {
+            for (int32_t o = tid; o < N; o += NT)   // write-through: the last block reads them with sc1 loads
+                __hip_atomic_store(prow + o, lacc[o], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const double rmax = block_max(rmax_w, red);
+            if (tid == 0 && rmax >= 0.0) atomicMax((unsigned long long*)&Mnext[MSH + blockIdx.x % MSH], d2bits(rmax));
+            tr_last_finish<NT>(G, it, d, Ms, Mnext);
+            return;
+        }
+    }
     for (int32_t o = tid; o < N; o += NT) prow[o] = lacc[o];
     const double rmax = block_max(rmax_w, red);
     if (tid == 0 && rmax >= 0.0)   // -inf: a block without traces (an empty shard's placeholder)
@@ -2213,6 +2305,7 @@ static int fb_ops(int32_t N, bool many) {
     return N <= 8192 ? (many ? 64 : 16) : 32;
 }
 constexpr int64_t FB_MANY_BLOCKS = 1024;   // 16-op blocks of a launch from which "many" holds
+constexpr int64_t LASTFIN_WORDS = 32768;   // k_tr_a's last-block finish: partial-row words it reads (256 KB)
 // px.peers (sharded graphs on the peer path, one graph per launch): the exchange is fused in --
 // mode 1 pushes the block's limbs (and block 0 this rank's r' maximum) into every rank's slot for
 // this rank and stores the round number in the block's flag there; mode 2 block b waits for flag
@@ -4138,6 +4231,8 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
     const bool fb_many = fb16 > FB_MANY_BLOCKS;
     int32_t blocks_a = 0, blocks_b = 0, blocks_fa = 0, blocks_fb = 0;
     size_t lds = VCAP * sizeof(double), lds_f = 0;
+    const char* lfe = getenv("MR_TR_LASTFIN");   // (A/B and tests, read per call) 0: k_fx_b for every graph
+    const bool lastfin_on = !(lfe && atoi(lfe) == 0);
     double bytes = 0.0;
     for (int i = 0; i < ng; ++i) {
         mr_graph* g = gs[i];
@@ -4234,7 +4329,11 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         blocks_fa += v.n_fa;
         v.blk0fb = blocks_fb;
         v.fb_ops = fb_ops(g->N, fb_many);
-        v.n_fb = g->fused ? cdiv(g->N, v.fb_ops) : 0;
+        // the last k_tr_a block finishes small graphs itself (window batches: one launch per
+        // iteration); its sc1 row reads stay short: at most LASTFIN_WORDS row words
+        v.lastfin = lastfin_on && plan.NT == 512 && !sharded && g->fused && !g->wide && !g->relabeled && !persist &&
+                    plan.mode == WV_SU_ALL && nfa >= 1 && nfa * (int64_t)g->N <= LASTFIN_WORDS;
+        v.n_fb = g->fused && !v.lastfin ? cdiv(g->N, v.fb_ops) : 0;
         blocks_fb += v.n_fb;
         v.blk0 = blocks_a;
         v.blk0b = blocks_b;
@@ -4361,7 +4460,7 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
                                        it, mode, p);
             };
             if (!coll) {
-                fx_b(0, px_off);
+                if (blocks_fb) fx_b(0, px_off);   // (none: every graph finished by its last k_tr_a block)
             } else if (px_on) {   // the exchange fused into k_fx_b: push in mode 1, per-block waits in mode 2
                 fx_b(1, px);
                 if (!px.spin) MR_TRY(mr_peer_fx_wait(ctx, px, blocks_fb));

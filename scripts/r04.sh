@@ -7,7 +7,9 @@
 #   c4s8    c4 at N=1 holding rank 0's share of an 8-GPU deployment (per-rank compute at N=8)
 #   pmc4    k_tr_a LDS / wait PMC passes at C4 (scripts/pmc_c4.sh)
 #   segv    the rocprofv3 --kernel-trace --stats c3 command that crashed in round 3, once, with maps
-#   c3 c5   c3 / c5 lines
+#   c3 c5   c3 / c5 lines          c5s / pc5s   c5 from span shards (rank 0 of 8) / its kernel table
+#   pc5     c5 kernel table          pc4s8  kernel table of c4 rank 0's share of 8
+#   c3ab c2ab  AB_VAR over AB_VALS on the c3 / c2 lines (interleaved, two repeats)
 #   shard   the shard tests only
 TAG=${1:-x}
 STAGES=${2:-"t s c2"}
@@ -58,6 +60,37 @@ if has segv; then
       > gpurun_out/segv_$TAG.json 2> gpurun_out/segv_$TAG.err
   rc=$?; echo "segv-command rc=$rc"; [ $rc -eq 0 ] || { tail -40 gpurun_out/segv_$TAG.err; exit $rc; }
   line gpurun_out/segv_$TAG.json segv
+fi
+if has c5s; then
+  timeout -k 10 600 python3 bench.py --config c5 --from-spans --shard-of 8 --steps 3 --warmup 1 --no-traffic --no-cpu > gpurun_out/c5s_$TAG.json 2> gpurun_out/c5s_$TAG.err || { tail -5 gpurun_out/c5s_$TAG.err; exit 1; }
+  line gpurun_out/c5s_$TAG.json c5s
+fi
+if has pc5s; then
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/pc5s_$TAG -o run --output-format csv \
+      -- python3 bench.py --config c5 --from-spans --shard-of 8 --steps 2 --warmup 1 --no-traffic --no-cpu > gpurun_out/pc5s_$TAG.json 2> gpurun_out/pc5s_$TAG.err || { echo "rocprof pc5s failed"; tail -5 gpurun_out/pc5s_$TAG.err; exit 1; }
+  line gpurun_out/pc5s_$TAG.json pc5s
+fi
+if has pc5; then
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/pc5_$TAG -o run --output-format csv \
+      -- python3 bench.py --config c5 --steps 2 --warmup 1 --no-traffic --no-cpu > gpurun_out/pc5_$TAG.json 2> gpurun_out/pc5_$TAG.err || { echo "rocprof pc5 failed"; tail -5 gpurun_out/pc5_$TAG.err; exit 1; }
+  line gpurun_out/pc5_$TAG.json pc5
+fi
+if has pc4s8; then
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/pc4s8_$TAG -o run --output-format csv \
+      -- python3 bench.py --config c4 --shard-of 8 --no-traffic --no-cpu --steps 5 --warmup 1 > gpurun_out/pc4s8_$TAG.json 2> gpurun_out/pc4s8_$TAG.err || { echo "rocprof pc4s8 failed"; tail -5 gpurun_out/pc4s8_$TAG.err; exit 1; }
+  line gpurun_out/pc4s8_$TAG.json pc4s8
+fi
+# A/B of one environment knob on the c3 / c2 lines: AB_VAR, AB_VALS (space-separated), interleaved twice
+if has c3ab || has c2ab; then
+  for cfg in c3 c2; do
+    has ${cfg}ab || continue
+    for rep in 1 2; do
+      for v in $AB_VALS; do
+        env $AB_VAR=$v timeout -k 10 400 python3 bench.py --config $cfg --no-traffic --no-cpu --no-c4-leg > gpurun_out/ab_${cfg}_${TAG}_${v}_$rep.json 2> gpurun_out/ab_${cfg}_${TAG}_${v}_$rep.err || { tail -5 gpurun_out/ab_${cfg}_${TAG}_${v}_$rep.err; exit 1; }
+        line gpurun_out/ab_${cfg}_${TAG}_${v}_$rep.json "$cfg $AB_VAR=$v rep $rep"
+      done
+    done
+  done
 fi
 if has c3; then
   timeout -k 10 400 python3 bench.py --config c3 > gpurun_out/c3_$TAG.json 2> gpurun_out/c3_$TAG.err || { tail -5 gpurun_out/c3_$TAG.err; exit 1; }

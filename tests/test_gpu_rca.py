@@ -518,6 +518,7 @@ def test_windows_batch_fx_ops_per_block_bitwise(c3_window, monkeypatch):
         u0 = int(ab.tstart.min())
         wins.append((d, u0, u0 + 5 * 60 * 10**9, s3, sok))
     runs = {}
+    monkeypatch.setenv("MR_TR_LASTFIN", "0")   # (k_fx_b for every graph: the path under test)
     for v in ("16", "32", "64"):
         monkeypatch.setenv("MR_FB_OPS", v)
         runs[v] = rank_windows(ctx, wins, top_max=60)
@@ -525,6 +526,39 @@ def test_windows_batch_fx_ops_per_block_bitwise(c3_window, monkeypatch):
         for a, b in zip(runs["16"], runs[v]):
             assert a[5] == b[5] == 0
             assert a[2:] == b[2:] and list(a[0]) == list(b[0]) and a[1].tobytes() == b[1].tobytes(), v
+    for d in devs:
+        d.close()
+
+
+def test_windows_batch_last_block_finish_bitwise(c3_window, monkeypatch):
+    """k_tr_a's last block of a graph finishing the iteration itself (window graphs: one launch per
+    iteration, MR_TR_LASTFIN) against the k_tr_a + k_fx_b pair: the same integer limb sums and
+    call-graph terms, so a 4-window batch ranks bitwise the same; one window alone too."""
+    import bench
+    from microrank_amd import _lib
+    from microrank_amd.online_rca import rank_windows
+    from microrank_amd.preprocess_data import DeviceSpans
+
+    ctx = _lib.default_context()
+    normal, abnormal, t0, t1 = c3_window
+    a3, ok = bench.slo_from_gpu(ctx, normal)
+    devs = [DeviceSpans(ctx, abnormal)]
+    wins = [(devs[0], t0, t1, a3, ok)]
+    for seed in (81, 82, 83):
+        _, nrm, ab = bench.make_window(seed, 500, 20_000)
+        s3, sok = bench.slo_from_gpu(ctx, nrm)
+        d = DeviceSpans(ctx, ab)
+        devs.append(d)
+        u0 = int(ab.tstart.min())
+        wins.append((d, u0, u0 + 5 * 60 * 10**9, s3, sok))
+    runs = {}
+    for v in ("0", "1"):
+        monkeypatch.setenv("MR_TR_LASTFIN", v)
+        runs[v] = (rank_windows(ctx, wins, top_max=60), rank_windows(ctx, wins[:1], top_max=60))
+    for many_a, many_b in zip(runs["0"], runs["1"]):
+        for a, b in zip(many_a, many_b):
+            assert a[5] == b[5] == 0
+            assert a[2:] == b[2:] and list(a[0]) == list(b[0]) and a[1].tobytes() == b[1].tobytes()
     for d in devs:
         d.close()
 
