@@ -2145,7 +2145,7 @@ __device__ __forceinline__ double tr_walk(const GDev& G, int32_t lb, int cur, in
 // call-graph term (a lane per op of <= 8 parents, a wave per op of more: wave_sum's butterfly) and
 // the same finish: bitwise k_fx_b's results.
 template <int NT>
-__device__ __noinline__ void tr_last_finish(const GDev& G, int it, double d, double Ms,
+__device__ __forceinline__ void tr_last_finish(const GDev& G, int it, double d, double Ms,
                                             GLB unsigned long long* Mnext) {
     constexpr int NW = NT / WAVE;
     __shared__ int s_last;
@@ -2171,13 +2171,21 @@ __device__ __noinline__ void tr_last_finish(const GDev& G, int it, double d, dou
         const int32_t o = ob + lane;
         const bool on = o < N;
         unsigned long long lo = 0ull, hi = 0ull;
-        if (on)
-            for (int32_t b = 0; b < nb; ++b) {
-                const unsigned long long v = __hip_atomic_load(rows + (size_t)b * N + o, __ATOMIC_RELAXED,
-                                                               __HIP_MEMORY_SCOPE_AGENT);
-                lo += v & 0xffffffffull;
-                hi += v >> 32;
-            }
+        // 16 rows per batch, every load in flight before the sums (indices clamped; repeats not added)
+        const int32_t oc = on ? o : N - 1;
+        for (int32_t b0 = 0; b0 < nb; b0 += 16) {
+            unsigned long long v[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                v[k] = __hip_atomic_load(rows + (size_t)min(b0 + k, nb - 1) * N + oc, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                if (b0 + k < nb) {
+                    lo += v[k] & 0xffffffffull;
+                    hi += v[k] >> 32;
+                }
+        }
         double ssv = 0.0;
         bool big = false;
         if (on) {
@@ -3127,6 +3135,8 @@ static int tr_split(mr_ctx* ctx, mr_graph* g, const FxPlan& P, int64_t wsum, int
     const int64_t W = g->n_wt, NW = P.NT / WAVE;
     const int64_t resident = plan_resident(kern_n(g), P);
     int64_t nb = std::max<int64_t>({std::min<int64_t>(resident, cdiv(W, NW)), cdiv(W, 1023), 1});
+    if (const char* fe = getenv("MR_TR_BLOCKS"))   // (A/B knob, read per call) blocks of a lone graph
+        if (force_nb <= 0 && wsum <= W && atoi(fe) > 0) force_nb = atoi(fe);
     if (force_nb > 0) {   // k_pr_cluster's cluster size (at most 1023 wave tiles per block still)
         nb = std::max<int64_t>(force_nb, cdiv(W, 1023));
     } else if (tr_budget() > 0.0 && wsum > W) {
