@@ -7,8 +7,8 @@ Workload (BASELINE.json configs[1], "C2"): RCA windows of 1k operations / 200k t
 (~13.7 spans per trace, ~2.74M spans per window; Train-Ticket-like synthetic call tree with one
 faulty operation), fp64.  The span columns are generated, factorised and uploaded BEFORE the
 timed region; a window is ranked on the device: detector -> two graph builds (T1 swap) -> two
-25-iteration PageRanks -> DStar2 spectrum + top list.  A "step" ranks 64 DISTINCT windows (own
-seed and span table each) with ONE mr_windows_batch call (their detectors / builds / spectra on
+25-iteration PageRanks -> DStar2 spectrum + top list.  A "step" ranks DISTINCT windows (own
+seed and span table each; 128 per step) with ONE mr_windows_batch call (their detectors / builds / spectra on
 the library's auxiliary streams, the PageRanks of a group of windows sharing each iteration's
 launches).
 
@@ -908,8 +908,9 @@ def main():
     args = ap.parse_args()
     if args.streams is None:
         # c3: a 4096-window batch in calls of 256 (measured: 64 -> 7.7k, 256 -> 9.0k windows/s; a
-        # call's pipeline fill / drain amortised); c2: calls of 64
-        args.streams = 8 if args.streams_mode else (256 if args.config == "c3" else 64)
+        # call's pipeline fill / drain amortised); c2: calls of 128 (r04: 128 vs 64 windows per call
+        # 5269 vs 4785 windows/s -- four 32-window PageRank groups per call instead of two)
+        args.streams = 8 if args.streams_mode else (256 if args.config == "c3" else 128)
     if args.precision is None:
         args.precision = "fp32" if args.config == "c5" else "fp64"
     if args.c4_ops is None:
@@ -1144,8 +1145,9 @@ def main():
                                   else f"windows x{world} ranks x{W} streams"},
         "windows_per_s": round(win_all / elapsed, 3),
         "roofline": {"bound": "hbm", "kernel": ("one Jacobi iteration of a window group's graphs: the "
-                                                "k_tr_a + k_fx_b launch pair over the graphs of one group (c2: 64 graphs of 32 "
-                                                "windows; c3: 256 graphs of 128)") if batch else
+                                                "k_tr_a (+ k_fx_b) launch(es) over the graphs of one group (c2: 64 graphs of 32 "
+                                                "windows; c3: 256 graphs of 128, one launch per iteration: the last "
+                                                "block of each graph finishes it)") if batch else
                                                ("one Jacobi iteration: k_tr_a + k_fx_b (fused path)"
                                                 + (f", stream 0 of {W} concurrent windows" if W > 1 else "")),
                      "achieved": round(achieved, 1),

@@ -1504,6 +1504,8 @@ struct GDev {
     int32_t blk0f, n_fa, blk0fb, n_fb;   // fused path: k_tr_a / k_fx_b block ranges
     int32_t fb_ops;                      // k_fx_b ops per block
     int32_t lastfin;                     // k_tr_a's last block of the graph finishes the iteration (no k_fx_b)
+    int32_t ssv_pre;                     // k_tr_a's blocks compute the call-graph terms (fx_ssv) for k_fx_b
+    int32_t row_wt;                      // k_tr_a's partial rows stored write-through (sc1)
 };
 
 // graph owning block `blk` of launch kind `which` (0 k_iter_a, 1 k_iter_b, 2 k_tr_a, 3 k_fx_b);
@@ -2136,6 +2138,60 @@ __device__ __forceinline__ double tr_walk(const GDev& G, int32_t lb, int cur, in
     return rmax;
 }
 
+// The call-graph term alpha (P_ss s_k)[o] / M_s(k) of k_fx_b (pagerank.py:122-124), computed in
+// k_tr_a instead: block lb owns the columns [lb N / n_fa, (lb + 1) N / n_fa), and every wave that
+// has finished its walk takes chunks of 64 of them (an LDS counter) -- the chains of dependent
+// loads (ss_off -> ss_par -> pw, s_k) then run in the slack of the block's slowest wave, not in
+// k_fx_b's critical path.  The same arithmetic as k_fx_b (a lane per column of <= 8 parents with
+// wave_sum's butterfly value, a wave per column of more): fx_ssv[o], read there bitwise.
+__device__ __forceinline__ void tr_ssv_share(const GDev& G, int32_t lb, int cur, double Ms, int* ctr, int lane) {
+    const int32_t N = G.N;
+    const int32_t oa = (int32_t)((int64_t)lb * N / G.n_fa), ob = (int32_t)((int64_t)(lb + 1) * N / G.n_fa);
+    for (;;) {
+        int c = 0;
+        if (lane == 0) c = atomicAdd(ctr, WAVE);
+        c = __builtin_amdgcn_readfirstlane(c);
+        if (oa + c >= ob) return;
+        const int32_t o = oa + c + lane;
+        const bool on = o < ob;
+        const int32_t op = on && G.perm ? G.perm[o] : o;
+        const GLB int64_t* ss_off = gp(G.ss_off);
+        const GLB int32_t* ss_par = gp(G.ss_par);
+        const GLB float* pw = gp(G.pw);
+        const GLB double* sp = gp(G.spb[cur]);
+        double ssv = 0.0;
+        bool big = false;
+        if (on) {
+            const int64_t e0 = ss_off[op], e1 = ss_off[op + 1];
+            if (e1 - e0 <= 8) {
+                int32_t pp[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) pp[k] = e0 + k < e1 ? ss_par[e0 + k] : -1;
+                double t[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) t[k] = pp[k] >= 0 ? (double)pw[pp[k]] * sp[pp[k]] : 0.0;
+                const double bb = ((t[0] + t[4]) + (t[2] + t[6])) + ((t[1] + t[5]) + (t[3] + t[7]));
+                ssv = G.alpha * (bb / Ms);
+            } else {
+                big = true;
+            }
+        }
+        for (uint64_t bm = __ballot(big); bm; bm &= bm - 1) {   // (wave-uniform)
+            const int j = __ffsll((unsigned long long)bm) - 1;
+            const int32_t opj = G.perm ? G.perm[oa + c + j] : oa + c + j;
+            const int64_t e0 = ss_off[opj], e1 = ss_off[opj + 1];
+            double bb = 0.0;
+            for (int64_t e = e0 + lane; e < e1; e += WAVE) {
+                const int32_t pp = ss_par[e];
+                bb += (double)pw[pp] * sp[pp];
+            }
+            bb = wave_sum(bb);
+            if (lane == j) ssv = G.alpha * (bb / Ms);
+        }
+        if (on) G.fx_ssv[o] = ssv;
+    }
+}
+
 // The last k_tr_a block of a graph finishes the iteration itself (small graphs: window batches),
 // so an iteration is ONE launch instead of k_tr_a + k_fx_b.  Every block writes its partial row
 // write-through (sc1), waits for its stores, and takes a ticket from the graph's counter (an
@@ -2253,12 +2309,14 @@ __global__ void __launch_bounds__(NT) k_tr_a(const GDev* __restrict__ gs, int32_
     }
     if (HOT)
         for (int32_t o = tid; o < NH; o += NT) su_l[o] = sug[o];
+    __shared__ int s_ssv;   // the call-graph term chunks taken (G.ssv_pre)
     if (tid < WAVE) {
         const double ms = wave_max(bits2d(Mcur[tid]));
         const double mr = wave_max(bits2d(Mcur[MSH + tid]));
         if (tid == 0) {
             msh[0] = ms;
             msh[1] = mr;
+            s_ssv = 0;
         }
     }
     __syncthreads();   // accumulator and maxima ready
@@ -2271,7 +2329,8 @@ __global__ void __launch_bounds__(NT) k_tr_a(const GDev* __restrict__ gs, int32_
     }
     const double xsc = (G.dscale ? G.dscale[0] : G.fx_scale) / msh[1], Ms = msh[0];
     const double rmax_w = tr_walk<Q, SUM, NT, EXT, HOTT>(G, lb, cur, nxt, N, NH, d, Ms, xsc, su_l, lacc, hs);
-    // (the call-graph term alpha P_ss s_k is k_fx_b's: a wave per op)
+    // the call-graph terms of this block's share of the columns, by the waves done walking
+    if (G.ssv_pre) tr_ssv_share(G, lb, cur, Ms, &s_ssv, tid & (WAVE - 1));
     __syncthreads();
     GLB unsigned long long* prow = gpw(G.fx_part) + (size_t)lb * N;
     if constexpr (NT == 512) {   // (window-graph variant only: the large graphs' kernel stays as it is)
@@ -2284,7 +2343,10 @@ __global__ void __launch_bounds__(NT) k_tr_a(const GDev* __restrict__ gs, int32_
             return;
         }
     }
-    for (int32_t o = tid; o < N; o += NT) prow[o] = lacc[o];
+    if (G.row_wt)   // write-through (sc1): the boundary to k_fx_b has no dirty lines to write back
+        for (int32_t o = tid; o < N; o += NT) __hip_atomic_store(prow + o, lacc[o], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+        for (int32_t o = tid; o < N; o += NT) prow[o] = lacc[o];
     const double rmax = block_max(rmax_w, red);
     if (tid == 0 && rmax >= 0.0)   // -inf: a block without traces (an empty shard's placeholder)
         atomicMax((unsigned long long*)&Mnext[MSH + blockIdx.x % MSH], d2bits(rmax));
@@ -2365,7 +2427,10 @@ __global__ void __launch_bounds__(WAVE * FB_W) k_fx_b(const GDev* __restrict__ g
     // the call-graph term alpha (P_ss s_k)[op] / M_s(k) (pagerank.py:122-124) of the block's ops: a
     // wave per op, its lanes striding the op's parents, one fixed-order wave sum (a hub op with
     // thousands of parents costs one wave, not one thread).  (Not in mode 1: its sums only.)
-    if (mode != 1) {
+    // ssv_pre: k_tr_a computed them (tr_ssv_share) -- one coalesced load
+    if (mode != 1 && G.ssv_pre) {
+        if (threadIdx.x < (unsigned)OPB) lssv[threadIdx.x] = o0 + (int32_t)threadIdx.x < N ? G.fx_ssv[o0 + threadIdx.x] : 0.0;
+    } else if (mode != 1) {
         const double Ms = wave_max(bits2d(G.mslot[(size_t)2 * MSH * k3c + lane]));
         const GLB double* sp_cur = gp(G.spb[it & 1]);
         const GLB int64_t* ss_off = gp(G.ss_off);
@@ -4243,6 +4308,10 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
     size_t lds = VCAP * sizeof(double), lds_f = 0;
     const char* lfe = getenv("MR_TR_LASTFIN");   // (A/B and tests, read per call) 0: k_fx_b for every graph
     const bool lastfin_on = !(lfe && atoi(lfe) == 0);
+    const char* sve = getenv("MR_TR_SSV");   // (A/B and tests, read per call) 0: k_fx_b computes the call-graph terms
+    const bool ssv_on = !(sve && atoi(sve) == 0);
+    const char* rwe = getenv("MR_TR_ROW_WT");   // (A/B, read per call) 1: partial rows stored write-through
+    const bool row_wt_on = rwe && atoi(rwe) != 0;
     double bytes = 0.0;
     for (int i = 0; i < ng; ++i) {
         mr_graph* g = gs[i];
@@ -4341,9 +4410,15 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         v.fb_ops = fb_ops(g->N, fb_many);
         // the last k_tr_a block finishes small graphs itself (window batches: one launch per
         // iteration); its sc1 row reads stay short: at most LASTFIN_WORDS row words
+        // (ops <= threads: the finishing block takes every op in one round -- C3's 500-op windows;
+        // C2's 1000-op windows measured -1.5 % with it, C3 +6.5 % windows/s, -7 % single window)
         v.lastfin = lastfin_on && plan.NT == 512 && !sharded && g->fused && !g->wide && !g->relabeled && !persist &&
-                    plan.mode == WV_SU_ALL && nfa >= 1 && nfa * (int64_t)g->N <= LASTFIN_WORDS;
+                    plan.mode == WV_SU_ALL && nfa >= 1 && g->N <= plan.NT && nfa * (int64_t)g->N <= LASTFIN_WORDS;
         v.n_fb = g->fused && !v.lastfin ? cdiv(g->N, v.fb_ops) : 0;
+        // the call-graph terms in k_tr_a (large graphs: k_fx_b's chains of dependent loads leave its
+        // critical path); not for wide graphs (k_fx_b's columns past NA) nor the persistent kernel
+        v.ssv_pre = ssv_on && v.n_fb > 0 && nfa >= 1 && !g->wide && !persist && g->N >= 2048;
+        v.row_wt = row_wt_on && g->N >= 2048;
         blocks_fb += v.n_fb;
         v.blk0 = blocks_a;
         v.blk0b = blocks_b;

@@ -92,6 +92,17 @@ if has c3ab || has c2ab; then
     done
   done
 fi
+# A/B of AB_VAR over AB_VALS on c4 (full) and c4 rank 0's share of 8, interleaved twice
+if has c4ab; then
+  for rep in 1 2; do
+    for v in $AB_VALS; do
+      for sh in 8 1; do
+        env $AB_VAR=$v timeout -k 10 300 python3 bench.py --config c4 --shard-of $sh --steps 10 --warmup 2 --no-cpu --no-traffic > gpurun_out/ab_c4s${sh}_${TAG}_${v}_$rep.json 2> gpurun_out/ab_c4s${sh}_${TAG}_${v}_$rep.err || { tail -5 gpurun_out/ab_c4s${sh}_${TAG}_${v}_$rep.err; exit 1; }
+        line gpurun_out/ab_c4s${sh}_${TAG}_${v}_$rep.json "c4 shard-of $sh $AB_VAR=$v rep $rep"
+      done
+    done
+  done
+fi
 if has c3; then
   timeout -k 10 400 python3 bench.py --config c3 > gpurun_out/c3_$TAG.json 2> gpurun_out/c3_$TAG.err || { tail -5 gpurun_out/c3_$TAG.err; exit 1; }
   line gpurun_out/c3_$TAG.json c3

@@ -151,6 +151,29 @@ def test_trace_order_preference_equals_position_order(c2, anomaly, monkeypatch):
     dg.close()
 
 
+@pytest.mark.parametrize("n_ops", [9000, 12000])
+def test_call_graph_terms_in_walk_kernel_bitwise(n_ops, monkeypatch):
+    """The call-graph terms computed by k_tr_a's waves that finished their walk (MR_TR_SSV=1, large
+    graphs) instead of k_fx_b: bitwise the same weights; N = 12000 is relabelled (su of the hot
+    ops in LDS), so the terms are in column order there.  Write-through rows (MR_TR_ROW_WT) too."""
+    from microrank_amd import _lib, synth
+    from microrank_amd.graph import DeviceGraph
+
+    hg = synth.big_graph(n_ops, 200_000, seed=8)
+    ctx = _lib.default_context()
+    dg = DeviceGraph.upload(ctx, hg)
+    out = {}
+    for ssv, wt in (("0", "0"), ("1", "0"), ("1", "1")):
+        monkeypatch.setenv("MR_TR_SSV", ssv)
+        monkeypatch.setenv("MR_TR_ROW_WT", wt)
+        dg.pagerank(True)
+        out[(ssv, wt)] = dg.fetch()
+    for k in (("1", "0"), ("1", "1")):
+        assert out[k][0].tobytes() == out[("0", "0")][0].tobytes(), k
+        np.testing.assert_array_equal(out[k][1], out[("0", "0")][1])
+    dg.close()
+
+
 def _oracle_graph_from_host(hg) -> "orc.Graph":
     T, N = hg.T, hg.N
     sr_t = np.repeat(np.arange(T, dtype=np.int64), np.diff(hg.sr_off))
