@@ -565,6 +565,14 @@ __global__ void __launch_bounds__(IX_BT) k_ix_stats(const int32_t* tflag, int64_
     extern __shared__ int32_t lh[];
     __shared__ unsigned long long ek[ESET];
     __shared__ uint32_t ec[ESET];
+    // more pod-op codes than one LDS histogram holds (wide op spaces, C5's 100k ops): blockIdx.y is an
+    // op range of IX_HIST codes whose entries this block counts in LDS (the range's blocks share the
+    // index: each reads its share of every entry and keeps those of its range); range 0 also takes
+    // the join keys.  Was: three global atomics per entry at up to 10^5 codes.
+    const int32_t op_lo = (int32_t)blockIdx.y * IX_HIST;
+    const bool ranged = gridDim.y > 1;
+    const int32_t NPL = ranged ? min(IX_HIST, n_podops - op_lo) : n_podops;   // this block's codes
+    n_podops = NPL;
     int32_t* lcnt = lh;
     int32_t* lfirst = lh + n_podops;
     int32_t* lcov = lh + 2 * n_podops;   // traces per pod-op (the graph's coverage)
@@ -598,7 +606,11 @@ __global__ void __launch_bounds__(IX_BT) k_ix_stats(const int32_t* tflag, int64_
             fr[j] = po_first[r];
         }
 #pragma unroll
-        for (int j = 0; j < IX_B; ++j) on[j] = rb + threadIdx.x + (int64_t)j * IX_BT < p1 && tflag[tr[j]];
+        for (int j = 0; j < IX_B; ++j) {
+            op[j] -= op_lo;   // (0 unless ranged)
+            on[j] = rb + threadIdx.x + (int64_t)j * IX_BT < p1 && (!ranged || (uint32_t)op[j] < (uint32_t)NPL) &&
+                    tflag[tr[j]];
+        }
 #pragma unroll
         for (int j = 0; j < IX_B; ++j) {
             if (!on[j]) continue;
@@ -613,7 +625,7 @@ __global__ void __launch_bounds__(IX_BT) k_ix_stats(const int32_t* tflag, int64_
             }
         }
     }
-    const int64_t q0 = (int64_t)blockIdx.x * eper, q1 = min(q0 + eper, n_ed);
+    const int64_t q0 = (int64_t)blockIdx.x * eper, q1 = blockIdx.y ? q0 : min(q0 + eper, n_ed);   // (range 0: the keys)
     if (ed_eid) {   // dense edge ids: one counter add per selected entry
         for (int64_t rb = q0; rb < q1; rb += (int64_t)IX_BT * IX_B) {
             int32_t tr[IX_B], cn[IX_B], id[IX_B];
@@ -638,9 +650,9 @@ __global__ void __launch_bounds__(IX_BT) k_ix_stats(const int32_t* tflag, int64_
         if (use_lds_hist)
             for (int32_t i = threadIdx.x; i < n_podops; i += IX_BT)
                 if (lcnt[i]) {
-                    atomicAdd(&ocnt[i], lcnt[i]);
-                    atomicMin(&ofirst[i], lfirst[i]);
-                    atomicAdd(&ocov[i], lcov[i]);
+                    atomicAdd(&ocnt[op_lo + i], lcnt[i]);
+                    atomicMin(&ofirst[op_lo + i], lfirst[i]);
+                    atomicAdd(&ocov[op_lo + i], lcov[i]);
                 }
         return;
     }
@@ -680,9 +692,9 @@ __global__ void __launch_bounds__(IX_BT) k_ix_stats(const int32_t* tflag, int64_
     if (use_lds_hist)
         for (int32_t i = threadIdx.x; i < n_podops; i += IX_BT)
             if (lcnt[i]) {
-                atomicAdd(&ocnt[i], lcnt[i]);
-                atomicMin(&ofirst[i], lfirst[i]);
-                atomicAdd(&ocov[i], lcov[i]);
+                atomicAdd(&ocnt[op_lo + i], lcnt[i]);
+                atomicMin(&ofirst[op_lo + i], lfirst[i]);
+                atomicAdd(&ocov[op_lo + i], lcov[i]);
             }
 }
 // join pairs whose rows lie in different traces count when both traces are selected (T11)
@@ -1471,17 +1483,23 @@ static int ix_launch(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d_mask, mr_
                            b.dense ? (uint64_t*)nullptr : b.gk.p, b.gc.p, (int64_t)ecap);
     }
     if (NT) {
-        const int use_lds = NP <= IX_HIST;
+        // more codes than one LDS histogram: op ranges of IX_HIST codes in blockIdx.y (MR_IX_RANGED=0:
+        // the global-atomic form, A/B)
+        static const bool no_ranged = getenv("MR_IX_RANGED") && atoi(getenv("MR_IX_RANGED")) == 0;
+        const int nrange = NP > IX_HIST && !no_ranged ? cdiv(NP, IX_HIST) : 1;
+        const int use_lds = NP <= IX_HIST || nrange > 1;
+        const int64_t NPL = std::min<int64_t>(NP, IX_HIST);
         // dense edge counts in LDS beside the pod-op histogram while both fit (else global adds)
-        const int lds_ek = b.dense && (use_lds ? 3 * (int64_t)NP : 0) + (int64_t)ecap <= IX_LDS_WORDS;
-        const size_t lds = (use_lds ? 3 * (size_t)NP * sizeof(int32_t) : 0) + (lds_ek ? ecap * sizeof(uint32_t) : 0);
+        const int lds_ek = b.dense && (use_lds ? 3 * NPL : 0) + (int64_t)ecap <= IX_LDS_WORDS;
+        const size_t lds = (use_lds ? 3 * (size_t)NPL * sizeof(int32_t) : 0) + (lds_ek ? ecap * sizeof(uint32_t) : 0);
         // block cap 256 (one per CU); MR_IX_BLOCKS overrides it for measurements
         static const int ix_cap = [] {
             const char* e = getenv("MR_IX_BLOCKS");
             return e ? std::max(1, atoi(e)) : 256;
         }();
-        const int nblk = std::max(1, std::min(ix_cap, cdiv(std::max(sp->n_po, sp->n_ed), IX_BT * IX_EPT)));
-        hipLaunchKernelGGL(k_ix_stats, dim3(nblk), dim3(IX_BT), lds, st, b.tflag.p, sp->n_po, sp->po_tr.p, sp->po_op.p,
+        int nblk = std::max(1, std::min(ix_cap, cdiv(std::max(sp->n_po, sp->n_ed), IX_BT * IX_EPT)));
+        if (nrange > 1) nblk = std::max(1, std::min(nblk, cdiv(2 * ix_cap, nrange)));   // ~2 blocks per CU over the ranges
+        hipLaunchKernelGGL(k_ix_stats, dim3(nblk, nrange), dim3(IX_BT), lds, st, b.tflag.p, sp->n_po, sp->po_tr.p, sp->po_op.p,
                            sp->po_cnt.p, sp->po_first.p, sp->n_ed, sp->ed_tr.p, sp->ed_key.p, sp->ed_cnt.p, NP, use_lds,
                            b.ocnt.p, b.ofirst.p, b.ocov.p, b.gk.p, b.gc.p, ecap - 1,
                            b.dense ? (const int32_t*)sp->ed_eid.p : nullptr, (int32_t)ecap, lds_ek);
