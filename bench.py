@@ -489,6 +489,37 @@ def c4_leg_run(hg, world, rank, dist, steps=10, warmup=2):
                     "time / (N x 8 TB/s)"}
 
 
+def isolated_group_roofline(ctx, group, prec, reps=3):
+    """roofline.isolated: the timed line's iteration pair measured while builds of other windows run
+    beside it on the auxiliary streams (the pipeline's contention included); here one call of ONE
+    32-window group, whose builds finish before its PageRanks start, so the 64-graph iterations run
+    alone -- the kernel's own share of the HBM roofline."""
+    import ctypes as C
+
+    from microrank_amd import _lib
+    from microrank_amd.online_rca import rank_windows
+
+    lib = _lib.load()
+    pr = "fp32" if prec == _lib.MR_FP32 else "fp64"
+    rank_windows(ctx, [w[:5] for w in group], precision=pr)
+    ctx.sync()
+    lib.mr_ctx_profile(ctx.h, 1)
+    for _ in range(reps):
+        rank_windows(ctx, [w[:5] for w in group], precision=pr)
+    ctx.sync()
+    launches, kms, kbytes = C.c_int64(), C.c_double(), C.c_double()
+    lib.mr_ctx_prof_read(ctx.h, C.byref(launches), C.byref(kms), C.byref(kbytes))
+    lib.mr_ctx_profile(ctx.h, 0)
+    avg_ms = kms.value / max(launches.value, 1)
+    achieved = (kbytes.value / max(launches.value, 1)) / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+    return {"achieved": round(achieved, 1), "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "avg_launch_us": round(avg_ms * 1e3, 3), "launches": launches.value,
+            "bytes_per_launch": round(kbytes.value / max(launches.value, 1)),
+            "what": "one 32-window group per mr_windows_batch call (its builds done before its 25 iterations): "
+                    "the iteration launches without concurrent builds; the line's frac is the same launches "
+                    "inside the timed 128-window calls, beside the next group's builds"}
+
+
 def c4_leg_guarded(hg, world, rank, dist, line, limit_s=240.0):
     """c4_leg_run behind a watchdog: a leg that raises becomes {"error": ...} (ranks stay in step:
     every rank raises on a library error the ranks agreed on); a leg still running after limit_s
@@ -1177,6 +1208,11 @@ def main():
             dist.barrier()
             dist.destroy_process_group()
         return
+    if batch and args.config == "c2" and len(wins[0]) >= 32:
+        try:   # the same iteration kernel with nothing beside it: ONE 32-window group per call
+            out["roofline"]["isolated"] = isolated_group_roofline(ctx, wins[0][:32], prec)
+        except Exception as e:  # a side metric never sinks the line
+            out["roofline"]["isolated"] = {"error": f"{type(e).__name__}: {e}"}
     try:   # single-window latency: one window per mr_windows_batch call, nothing to overlap with
         from microrank_amd.online_rca import rank_windows
 
