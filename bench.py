@@ -398,6 +398,10 @@ def run_c4(args, world, rank, dist):
                      "avg_launch_us": round(avg_ms * 1e3, 3), "launches": launches.value,
                      "bytes_per_launch": round(kbytes.value / max(launches.value, 1))},
     }
+    if fused and not wide and avg_ms > 0:   # the same iteration on the bytes it moves: u16 op ids, not SURVEY's 4-B ids
+        b16 = kbytes.value / max(launches.value, 1) - 2.0 * float(nnz_local)
+        out["roofline"]["u16_ids"] = {"bytes_per_launch": round(b16), "achieved": round(b16 / (avg_ms * 1e-3) / 1e9, 1),
+                                      "frac": round(b16 / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
     if dev is not None:
         out["data"] = ("synthetic span shards (power-law ops, root op in every trace, random parent per span, "
                        "5% broken traces, 1% duplicated root spanIDs across ranks), int-coded, resident in HBM")
