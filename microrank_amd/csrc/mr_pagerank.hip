@@ -79,7 +79,18 @@ __device__ __forceinline__ void graph_consts_body(int32_t blk, const int32_t* le
         u_o[i] = len_o[i] > 0 ? (float)(1.0 / (double)len_o[i]) : 0.0f;
         pw[i] = nchild[i] > 0 ? (float)(1.0 / (double)nchild[i]) : 0.0f;
     }
-    if (o16 && i < n) o16[i] = (uint16_t)ops[i];
+    // the u16 copy, four ids per thread (one 16-B load, one 8-B store instead of 2-B stores)
+    if (o16 && 4 * i < n) {
+        if (4 * i + 3 < n) {
+            const int4 v = *(const int4*)(ops + 4 * i);
+            uint2 w;
+            w.x = (uint32_t)(uint16_t)v.x | ((uint32_t)(uint16_t)v.y << 16);
+            w.y = (uint32_t)(uint16_t)v.z | ((uint32_t)(uint16_t)v.w << 16);
+            *(uint2*)(o16 + 4 * i) = w;
+        } else {
+            for (int64_t k = 4 * i; k < n; ++k) o16[k] = (uint16_t)ops[k];
+        }
+    }
 }
 __global__ void k_graph_consts(const int32_t* len_t, float* w_t, int32_t T, const int32_t* len_o, const int32_t* nchild,
                                float* u_o, float* pw, int32_t N, const int32_t* ops, int64_t n, uint16_t* o16,
@@ -3770,7 +3781,7 @@ int mr_graph_prepare_batch(mr_ctx* ctx, mr_graph* const* gs, int n, std::vector<
         v.coff = g->coff.p;
         v.c64 = c64[(size_t)i].p;
         v.b_gc = bgc;
-        bgc += cdiv(std::max<int64_t>({(int64_t)T, (int64_t)N, nnz, (int64_t)nz}), 256);
+        bgc += cdiv(std::max<int64_t>({(int64_t)T, (int64_t)N, cdiv(nnz, 4), (int64_t)nz}), 256);
         v.b_th = bth;
         bth += cdiv(T, (int64_t)TRB * TR_PER_SMALL);
         v.b_cs = bcs;
@@ -3808,7 +3819,7 @@ int mr_graph_prepare(mr_ctx* ctx, mr_graph* g) {
     DBuf<int32_t> trz;
     const int32_t nz = N <= FX_NMAX ? 2 * (N + 1) : 0;
     if (nz) MR_TRY(trz.alloc(ctx, (size_t)nz));
-    const int64_t nc = std::max<int64_t>({(int64_t)T, (int64_t)N, u16 ? g->nnz_rs : 0, (int64_t)nz});
+    const int64_t nc = std::max<int64_t>({(int64_t)T, (int64_t)N, u16 ? cdiv(g->nnz_rs, 4) : 0, (int64_t)nz});
     if (nc)
         hipLaunchKernelGGL(k_graph_consts, dim3(cdiv(nc, 256)), dim3(256), 0, st, g->len_t.p, g->w_t.p, T, g->len_o.p,
                            g->nchild.p, g->u_o.p, g->pw.p, N, g->rs_ops.p, u16 ? g->nnz_rs : 0,
