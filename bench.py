@@ -121,7 +121,7 @@ def run_window(ctx, dev, t0, t1, a3, ok, prec):
     return edges.value, codes[:n_out.value].copy(), scores[:n_out.value].copy(), na.value, nn.value
 
 
-ITER_KERNELS = ("k_tr_a", "k_fx_b", "k_iter_a", "k_iter_b", "k_cold_trace", "k_cold_ops", "k_pr_cluster")
+ITER_KERNELS = ("k_tr_a", "k_fx_b", "k_iter_a", "k_iter_b", "k_cold_trace", "k_cold_ops")
 
 
 def kind_compressed_probe(ctx, dev, t0, t1, a3, ok, reps=5):
@@ -208,8 +208,7 @@ def pmc_traffic(args, timeout_s=240):
                     name = r["Kernel_Name"]
                     if r["Counter_Name"] == ctr and any(k in name for k in ITER_KERNELS):
                         per_iter += float(r["Counter_Value"])
-                        # iterations the dispatch covers: a persistent k_pr_cluster launch runs all 25
-                        n_a += 25 if "k_pr_cluster" in name else any(k in name for k in ("k_tr_a", "k_iter_a"))
+                        n_a += any(k in name for k in ("k_tr_a", "k_iter_a"))   # one walk launch per iteration
             if n_a == 0:
                 return None
             vals[ctr] = per_iter / n_a * 1024.0   # KB -> bytes, per iteration

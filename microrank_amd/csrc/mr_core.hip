@@ -187,7 +187,7 @@ extern "C" int mr_ctx_prof_read(mr_ctx* ctx, int64_t* launches, double* total_ms
         ms += t;
         by += ctx->prof_bytes[i / 2];
     }
-    int64_t its = 0;   // iterations covered (a persistent launch covers all of a call's)
+    int64_t its = 0;   // iterations covered
     for (size_t i = 0; i < ctx->prof_bytes.size(); ++i) its += i < ctx->prof_iters.size() ? ctx->prof_iters[i] : 1;
     if (launches) *launches = its;
     if (total_ms) *total_ms = ms;

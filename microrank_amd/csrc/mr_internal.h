@@ -33,7 +33,7 @@ struct mr_ctx {
     bool prof = false;
     std::vector<hipEvent_t> prof_ev;
     std::vector<double> prof_bytes;
-    std::vector<int64_t> prof_iters;   // iterations each record covers (k_pr_cluster: all of a call's)
+    std::vector<int64_t> prof_iters;   // iterations each record covers
     // stream-ordered caching allocator: every buffer of this context is used on `stream` only,
     // so a block released by one call can be handed to the next without a hipFree/hipMalloc
     // (each of which synchronises the device and costs tens of microseconds)
@@ -81,9 +81,6 @@ struct mr_ctx {
         int rank;
     };
     std::vector<PeerOld> peer_old;
-    // k_pr_cluster timed out on this context (its clusters were not co-resident): launch per
-    // iteration from then on
-    bool no_persist = false;
     // status words of the single-pass scans (mr_prim.hip k_scan_dl): per-call epochs, no clearing
     unsigned long long* scan_st = nullptr;
     size_t scan_cap = 0;

@@ -1297,7 +1297,7 @@ __global__ void k_inv_perm(const int32_t* __restrict__ perm, int32_t n, int32_t*
 // M_s / M_r per iteration live in MSH shards (an atomicMax per block or op on ONE word would
 // serialise ~2k same-address atomics per iteration); readers reduce the shards.
 constexpr int MSH = 64;
-// mslot: [3 iterations][s | r][MSH] maxima, then k_pr_cluster's arrival counter (word 6 MSH)
+// mslot: [3 iterations][s | r][MSH] maxima, then words of the hand-offs (6 MSH + 1: the last-block ticket)
 constexpr int MSLOT_WORDS = 6 * MSH + 8;
 __device__ __forceinline__ double bits2d(unsigned long long b) { return __longlong_as_double((long long)b); }
 __device__ __forceinline__ unsigned long long d2bits(double v) {
@@ -2036,7 +2036,7 @@ __device__ __forceinline__ int32_t tr_walk_short(const GDev& G, int32_t k, const
     return k;
 }
 
-// The wave's walk of k_tr_a over its run of wave tiles (shared with k_pr_cluster): per entry one
+// The wave's walk of k_tr_a over its run of wave tiles: per entry one
 // su read, one add into the lane's trace sum, one LDS u64 atomic of X_t; per tile r' of its traces
 // and their next q.  Returns the wave's largest r' (-inf when it owns no trace).
 template <class Q, int SUM, int NT, int EXT = 0, bool HOTT = false>
@@ -2657,198 +2657,6 @@ __global__ void __launch_bounds__(WAVE * FB_W) k_fx_b(const GDev* __restrict__ g
     atomicMax(&Mnext[op % MSH], d2bits(v));
 }
 
-// ---------------------------------------------------------------- persistent iteration (k_pr_cluster)
-// All `iters` Jacobi iterations of a batch of fused graphs in ONE launch (one
-// persistent launch for many small windows).  Graph g owns a CLUSTER of n_fa blocks; its blocks sync
-// only with each other, so the graphs of a batch advance independently (no kernel boundary per
-// iteration, no batch-wide tail).  Per iteration a block
-//   (A) walks its wave tiles exactly as k_tr_a (tr_walk: same sums, same order);
-//   (B) with n_fa > 1 publishes its accumulator row write-through (sc1 stores, vmcnt(0), barrier),
-//       adds its r' maximum and arrives at the cluster's counter (agent atomics), polls it (sc1),
-//       then reads every block's row with sc1 loads (MI355X_MICROARCH.md inter-workgroup hand-off,
-//       table row 1); with n_fa == 1 the row stays in LDS;
-//   (C) computes s' for EVERY op itself (k_fx_b's arithmetic: exact limb sums, the call-graph term
-//       a wave per op), its maximum M_s, su = u_o s' -- all in LDS, identical in every block.
-// With the per-wave cut of the launch-per-iteration path the results are bitwise those of
-// k_tr_a + k_fx_b.  Every spin is bounded (PC_TIMEOUT): a cluster whose blocks are not co-resident
-// raises flag[3], every block leaves, and the host reruns the call launch by launch.
-constexpr unsigned long long PC_TIMEOUT = 5000000ull;   // 50 ms of the 100 MHz s_memrealtime clock
-constexpr int PC_MAXB = 64;                               // blocks of one cluster
-// LDS of a cluster block: k_tr_a's accumulator and su, s_k and s_k+1, and the call graph P_ss
-// (offsets, parents, fp32(1/nchild)): graph constants staged once, so the per-iteration call-graph
-// term is LDS reads, not chains of dependent global loads
-struct PcLds {
-    size_t lacc, su, s0, s1, soff, spar, spw, big, total;
-    __host__ __device__ PcLds(int32_t N, int64_t E) {
-        const TrLds t(N, WV_SU_ALL);   // the accumulator and su as k_tr_a's
-        auto up = [](size_t b) { return (b + 15) / 16 * 16; };
-        lacc = t.lacc;
-        su = t.su;
-        s0 = t.total;
-        s1 = s0 + up((size_t)N * 8);
-        soff = s1 + up((size_t)N * 8);
-        spar = soff + up(((size_t)N + 1) * 4);
-        spw = spar + up((size_t)E * 4);
-        big = spw + up((size_t)N * 4);   // [0] count, then the ops of > 8 parents
-        total = big + up(((size_t)N + 1) * 4);
-    }
-};
-template <class Q, int NT>
-__global__ void __launch_bounds__(NT) k_pr_cluster(const GDev* __restrict__ gs, int32_t ng, double d, int iters) {
-    constexpr int NW = NT / WAVE;
-    extern __shared__ __attribute__((aligned(16))) unsigned char lraw[];
-    __shared__ double red[NW];
-    __shared__ double mb[2];
-    __shared__ int s_abort;
-    const GDev& G = gs[__builtin_amdgcn_readfirstlane(graph_of(gs, ng, (int32_t)blockIdx.x, 2))];
-    const int32_t lb = __builtin_amdgcn_readfirstlane((int32_t)blockIdx.x - G.blk0f);
-    const int32_t B = __builtin_amdgcn_readfirstlane(G.n_fa), N = __builtin_amdgcn_readfirstlane(G.N);
-    const int32_t tid = (int32_t)threadIdx.x, lane = tid & (WAVE - 1), wv = tid / WAVE;
-    const int64_t E = rfl64(G.ss_off[N]);
-    const PcLds L(N, E);
-    unsigned long long* lacc = (unsigned long long*)(lraw + L.lacc);
-    double* su_l = (double*)(lraw + L.su);
-    double* s_cur = (double*)(lraw + L.s0);
-    double* s_nxt = (double*)(lraw + L.s1);
-    int32_t* l_soff = (int32_t*)(lraw + L.soff);
-    int32_t* l_spar = (int32_t*)(lraw + L.spar);
-    float* l_spw = (float*)(lraw + L.spw);
-    int32_t* l_big = (int32_t*)(lraw + L.big);
-    // (global-address views: the hand-off's sc1 loads / stores and atomics must be global_, not flat_)
-    GLB unsigned long long* mslot = gpw(G.mslot);
-    GLB unsigned long long* cnt = mslot + 6 * MSH;
-    GLB unsigned long long* rows = gpw(G.fx_part);   // [2][B][N] (B > 1)
-    const double scale = G.dscale ? G.dscale[0] : G.fx_scale, iscale = G.dscale ? G.dscale[1] : G.fx_iscale;
-    const GLB float* u_o = gp(G.u_o);
-    // the set-up's state: s_0, su_0, M_s(0), M_r(0) (earlier launches on this stream); P_ss
-    for (int32_t o = tid; o < N + TR_PAD; o += NT) {
-        lacc[o] = 0ull;
-        su_l[o] = o < N ? G.sub[0][o] : 0.0;
-        if (o < N) {
-            s_cur[o] = G.spb[0][o];
-            l_spw[o] = G.pw[o];
-        }
-        if (o <= N) l_soff[o] = (int32_t)G.ss_off[o];
-    }
-    for (int64_t e = tid; e < E; e += NT) l_spar[e] = G.ss_par[e];
-    if (tid == 0) l_big[0] = 0;
-    __syncthreads();
-    for (int32_t o = tid; o < N; o += NT)   // the ops the (C) pass sums a wave each (any order)
-        if (l_soff[o + 1] - l_soff[o] > 8) l_big[1 + atomicAdd(&l_big[0], 1)] = o;
-    if (tid < WAVE) {
-        const double ms = wave_max(bits2d(mslot[tid]));
-        const double mr = wave_max(bits2d(mslot[MSH + tid]));
-        if (tid == 0) {
-            mb[0] = ms;
-            mb[1] = mr;
-            s_abort = 0;
-        }
-    }
-    __syncthreads();
-    double Ms = uni_d(mb[0]), Mr = uni_d(mb[1]);
-    for (int it = 0; it < iters; ++it) {
-        const int cur = it & 1, nxt = cur ^ 1;
-        GLB unsigned long long* Mr_next = mslot + (size_t)2 * MSH * ((it + 1) % 3) + MSH;
-        if (B > 1 && lb == 0 && tid < MSH)   // slot it + 2 (last read in iteration it - 1)
-            __hip_atomic_store(mslot + (size_t)2 * MSH * ((it + 2) % 3) + MSH + tid, 0ull, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        const double rw = tr_walk<Q, WV_SU_ALL, NT>(G, lb, cur, nxt, N, 0, d, Ms, scale / Mr, su_l, lacc);
-        const double rmax = block_max(rw, red);   // (its barriers: every wave's LDS atomics are done)
-        double Mr_n = rmax;
-        if (B > 1) {
-            GLB unsigned long long* mine = rows + ((size_t)cur * B + lb) * N;
-            for (int32_t o = tid; o < N; o += NT) {
-                __hip_atomic_store(mine + o, lacc[o], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                lacc[o] = 0ull;
-            }
-            if (tid == 0 && rmax >= 0.0)
-                __hip_atomic_fetch_max(Mr_next + lb % MSH, d2bits(rmax), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            if (tid == 0) {
-                __hip_atomic_fetch_add(cnt, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const unsigned long long target = (unsigned long long)B * (unsigned long long)(it + 1);
-                const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-                while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-                    __builtin_amdgcn_s_sleep(1);
-                    if (__builtin_amdgcn_s_memrealtime() - t0 > PC_TIMEOUT) {
-                        s_abort = 1;
-                        __hip_atomic_fetch_or(gpw((int32_t*)G.flag) + 3, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        break;
-                    }
-                }
-            }
-            __syncthreads();
-            if (s_abort) return;   // (every block of the cluster times out the same way)
-            if (tid < WAVE) {
-                const double mr = wave_max(bits2d(__hip_atomic_load(Mr_next + tid, __ATOMIC_RELAXED,
-                                                                    __HIP_MEMORY_SCOPE_AGENT)));
-                if (tid == 0) mb[1] = mr;
-            }
-        }
-        // the call-graph term alpha (P_ss s_k)[o] / M_s(k) in k_fx_b's order: a thread per op of
-        // <= 8 parents (wave_sum's butterfly value formed by the thread, as k_fx_b's lanes), a
-        // wave per op of more
-        for (int32_t o = tid; o < N; o += NT) {
-            const int32_t e0 = l_soff[o], e1 = l_soff[o + 1];
-            if (e1 - e0 > 8) continue;
-            double t[8];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const int32_t p = e0 + k < e1 ? l_spar[e0 + k] : -1;
-                t[k] = p >= 0 ? (double)l_spw[p] * s_cur[p] : 0.0;
-            }
-            const double bb = ((t[0] + t[4]) + (t[2] + t[6])) + ((t[1] + t[5]) + (t[3] + t[7]));
-            s_nxt[o] = G.alpha * (bb / Ms);
-        }
-        for (int32_t i = wv; i < l_big[0]; i += NW) {
-            const int32_t o = l_big[1 + i];
-            double bb = 0.0;
-            for (int32_t e = l_soff[o] + lane; e < l_soff[o + 1]; e += WAVE) {
-                const int32_t p = l_spar[e];
-                bb += (double)l_spw[p] * s_cur[p];
-            }
-            bb = wave_sum(bb);
-            if (lane == 0) s_nxt[o] = G.alpha * (bb / Ms);
-        }
-        __syncthreads();
-        if (B > 1) Mr_n = mb[1];
-        double vmax = -__builtin_huge_val();
-        const GLB unsigned long long* rcur = rows + (size_t)cur * B * N;
-        for (int32_t o = tid; o < N; o += NT) {
-            unsigned long long lo = 0ull, hi = 0ull;
-            if (B > 1) {
-                for (int32_t b = 0; b < B; ++b) {
-                    const unsigned long long v = __hip_atomic_load(rcur + (size_t)b * N + o, __ATOMIC_RELAXED,
-                                                                   __HIP_MEMORY_SCOPE_AGENT);
-                    lo += v & 0xffffffffull;
-                    hi += v >> 32;
-                }
-            } else {
-                const unsigned long long v = lacc[o];
-                lacc[o] = 0ull;
-                lo = v & 0xffffffffull;
-                hi = v >> 32;
-            }
-            const double sum = ((double)hi * 4294967296.0 + (double)lo) * iscale;
-            const double v = d * (sum + s_nxt[o]);      // pagerank.py:122-124
-            s_nxt[o] = v;
-            su_l[o] = (double)u_o[o] * v;
-            vmax = nmax(vmax, v);
-        }
-        Ms = uni_d(block_max(vmax, red));   // (its barriers publish s_nxt / su_l to the block)
-        Mr = uni_d(Mr_n);
-        double* t = s_cur;
-        s_cur = s_nxt;
-        s_nxt = t;
-    }
-    if (lb == 0) {   // k_weights_batch's inputs: s'(iters) and M_s(iters)
-        GLB double* sp = gpw(G.spb[iters & 1]);
-        for (int32_t o = tid; o < N; o += NT) sp[o] = s_cur[o];
-        if (tid < MSH) mslot[(size_t)2 * MSH * (iters % 3) + tid] = tid == 0 ? d2bits(Ms) : 0ull;
-    }
-}
-
 // ---- wide fused graphs, per iteration, before k_tr_a
 // cold half of each trace's su sum (pagerank.py:125), in position order: k_tr_a adds it to the
 // lane's hot sum before the division by M_s(k)
@@ -3246,7 +3054,7 @@ static int tr_split(mr_ctx* ctx, mr_graph* g, const FxPlan& P, int64_t wsum, int
     int64_t nb = std::max<int64_t>({std::min<int64_t>(resident, cdiv(W, NW)), cdiv(W, 1023), 1});
     if (const char* fe = getenv("MR_TR_BLOCKS"))   // (A/B knob, read per call) blocks of a lone graph
         if (force_nb <= 0 && wsum <= W && atoi(fe) > 0) force_nb = atoi(fe);
-    if (force_nb > 0) {   // k_pr_cluster's cluster size (at most 1023 wave tiles per block still)
+    if (force_nb > 0) {   // (at most 1023 wave tiles per block still)
         nb = std::max<int64_t>(force_nb, cdiv(W, 1023));
     } else if (tr_budget() > 0.0 && wsum > W) {
         const int64_t share = (int64_t)std::ceil((double)resident * tr_budget() * (double)W / (double)wsum);
@@ -3322,71 +3130,6 @@ static int tr_split(mr_ctx* ctx, mr_graph* g, const FxPlan& P, int64_t wsum, int
 static int fused_blocks(mr_ctx* ctx, mr_graph* g, const FxPlan& P, int64_t wsum, int64_t* nfa,
                         std::vector<CutArg>* defer = nullptr, int64_t force_nb = 0) {
     return tr_split(ctx, g, P, wsum, nfa, defer, force_nb);
-}
-
-// ---- k_pr_cluster: eligibility and cluster sizes
-// MR_PR_PERSIST (read per call): 1 = persistent launch where eligible; unset / 0 = launch per
-// iteration (the default: measured faster, DESIGN.md §4 -- the persistent kernel runs one 16-wave
-// block per CU at 84 VGPRs where k_tr_a runs two, and its per-iteration row hand-off and s' pass
-// cost more than the two kernel boundaries they replace); "split" = the persistent plan's block
-// counts launched per iteration (k_tr_a + k_fx_b: bitwise the persistent results -- parity
-// tests).  MR_PC_TPW: wave tiles per wave a cluster is sized for (default 4).
-constexpr size_t PC_LDS_MAX = 76 * 1024;   // two 1024-thread blocks per CU
-enum { PC_OFF = 0, PC_ON = 1, PC_SPLIT = 2 };
-static int pc_mode() {
-    const char* e = getenv("MR_PR_PERSIST");
-    if (!e) return PC_OFF;
-    if (!strcmp(e, "split")) return PC_SPLIT;
-    return strcmp(e, "0") ? PC_ON : PC_OFF;
-}
-static int64_t pc_tpw() {
-    const char* e = getenv("MR_PC_TPW");
-    return e ? std::max<int64_t>(1, atoll(e)) : 4;
-}
-using PcA = void (*)(const GDev*, int32_t, double, int);
-static PcA pc_kernel(bool fp32, int NT) {
-    static const PcA tab[2][2] = {{k_pr_cluster<double, 512>, k_pr_cluster<double, 1024>},
-                                  {k_pr_cluster<float, 512>, k_pr_cluster<float, 1024>}};
-    return tab[fp32 ? 1 : 0][NT == 1024 ? 1 : 0];
-}
-// per graph the cluster's block count, or an empty vector when the batch is not eligible
-static std::vector<int64_t> pc_plan(mr_ctx* ctx, mr_graph* const* gs, int ng, const FxPlan& P, bool sharded, int iters,
-                                    bool fp32) {
-    std::vector<int64_t> nb;
-    if (sharded || iters <= 0 || ctx->no_persist || pc_mode() == PC_OFF || P.mode != WV_SU_ALL) return nb;
-    size_t lds = 0;
-    for (int i = 0; i < ng; ++i) {
-        const mr_graph* g = gs[i];
-        if (!g->fused || g->wide || g->relabeled || !g->tile_mult_h.empty() || g->n_wt == 0 || g->nhr) return nb;
-        lds = std::max(lds, PcLds(g->N, g->E).total);
-    }
-    if (lds > PC_LDS_MAX) return nb;
-    int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)pc_kernel(fp32, P.NT), P.NT, lds) != hipSuccess ||
-        per_cu < 1)
-        return nb;
-    // one block per CU fewer than the API's answer allows (MI355X_MICROARCH.md: the API can be one
-    // block high), at least one: the grid must be co-resident for the clusters' spins
-    const int64_t cap = (int64_t)num_cus() * std::max(1, per_cu - 1);
-    const int64_t NW = P.NT / WAVE, tpw = pc_tpw();
-    int64_t tot = 0;
-    nb.resize((size_t)ng);
-    for (int i = 0; i < ng; ++i) {
-        const int64_t W = gs[i]->n_wt;
-        nb[(size_t)i] = std::min<int64_t>(std::max<int64_t>({cdiv(W, NW * tpw), cdiv(W, 1023), 1}), PC_MAXB);
-        tot += nb[(size_t)i];
-    }
-    if (tot > cap) {   // shrink every cluster in proportion
-        const int64_t tot0 = tot;
-        tot = 0;
-        for (int i = 0; i < ng; ++i) {
-            int64_t& n = nb[(size_t)i];
-            n = std::max<int64_t>({n * cap / tot0, cdiv(gs[i]->n_wt, 1023), 1});
-            tot += n;
-        }
-        if (tot > cap) nb.clear();   // (more graphs than resident blocks)
-    }
-    return nb;
 }
 
 // k_tr_a's layout of a fused graph (after w_t and the kernel's ids rs16 / rsp): traces sorted by
@@ -4282,9 +4025,8 @@ struct PrAsync {   // (mr_internal.h) what an enqueued batch's kernels still rea
 };
 static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly, int ng, double d, double alpha,
                             int iters, int precision, uint32_t flags, bool sharded, uint64_t seed, uint64_t hmask,
-                            bool* collided, bool* timed_out, PrAsync* as = nullptr) {
+                            bool* collided, PrAsync* as = nullptr) {
     *collided = false;
-    *timed_out = false;
     HostMarks hm(ng);
     if (!ctx || ng <= 0 || !gs || !anomaly) return mr_fail(ctx, MR_ERR_ARG, "mr_pagerank: bad arguments");
     if (iters < 0) return mr_fail(ctx, MR_ERR_ARG, "iters < 0");
@@ -4325,9 +4067,6 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         }
     }
     hm.mark("setup");
-    // k_pr_cluster: every iteration in one launch, a cluster of blocks per graph (pc: cluster sizes)
-    const std::vector<int64_t> pc = pc_plan(ctx, gs, ng, plan, sharded, iters, fp32);
-    const bool persist = !pc.empty() && pc_mode() == PC_ON;
     int64_t wsum = 0;   // wave tiles of the launch's fused graphs (k_tr_a's block budget)
     for (int i = 0; i < ng; ++i)
         if (gs[i]->fused) wsum += gs[i]->n_wt;
@@ -4336,10 +4075,8 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         mr_graph* g = gs[i];
         if (g->fused) {   // the plan's blocks: partial rows and (k_tr_a) the per-wave cut
             int64_t nfa = 0;
-            MR_TRY(fused_blocks(ctx, g, plan, wsum, &nfa, &cuts, pc.empty() ? 0 : pc[(size_t)i]));
-            // (k_pr_cluster: two rows per block, one per iteration parity)
-            MR_TRY(g->fx_part.alloc(ctx, (size_t)(persist ? 2 : 1) * (size_t)std::max<int64_t>(nfa, 1) *
-                                             (size_t)kern_n(g)));
+            MR_TRY(fused_blocks(ctx, g, plan, wsum, &nfa, &cuts));
+            MR_TRY(g->fx_part.alloc(ctx, (size_t)std::max<int64_t>(nfa, 1) * (size_t)kern_n(g)));
         }
     }
     hm.mark("blocks");
@@ -4433,7 +4170,7 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         // a shard without traces still runs one (empty) block: it clears the maxima slot and
         // writes a zero partial row, and the collectives after the launch need every rank
         int64_t nfa = 0;
-        if (g->fused) MR_TRY(fused_blocks(ctx, g, plan, wsum, &nfa, nullptr, pc.empty() ? 0 : pc[(size_t)i]));
+        if (g->fused) MR_TRY(fused_blocks(ctx, g, plan, wsum, &nfa));
         nfa = g->fused ? std::max<int64_t>(nfa, sharded ? 1 : 0) : 0;
         // a row entry stays below 2^63; shards of one graph hold different trace counts, and their
         // limbs are summed, so they share the scale of the largest block (2^15 traces)
@@ -4479,12 +4216,12 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         // iteration); its sc1 row reads stay short: at most LASTFIN_WORDS row words
         // (ops <= threads: the finishing block takes every op in one round -- C3's 500-op windows;
         // C2's 1000-op windows measured -1.5 % with it, C3 +6.5 % windows/s, -7 % single window)
-        v.lastfin = lastfin_on && plan.NT == 512 && !sharded && g->fused && !g->wide && !g->relabeled && !persist &&
+        v.lastfin = lastfin_on && plan.NT == 512 && !sharded && g->fused && !g->wide && !g->relabeled &&
                     plan.mode == WV_SU_ALL && nfa >= 1 && g->N <= plan.NT && nfa * (int64_t)g->N <= LASTFIN_WORDS;
         v.n_fb = g->fused && !v.lastfin ? cdiv(g->N, v.fb_ops) : 0;
         // the call-graph terms in k_tr_a (large graphs: k_fx_b's chains of dependent loads leave its
-        // critical path); not for wide graphs (k_fx_b's columns past NA) nor the persistent kernel
-        v.ssv_pre = ssv_on && v.n_fb > 0 && nfa >= 1 && !g->wide && !persist && g->N >= 2048;
+        // critical path); not for wide graphs (k_fx_b's columns past NA)
+        v.ssv_pre = ssv_on && v.n_fb > 0 && nfa >= 1 && !g->wide && g->N >= 2048;
         v.row_wt = row_wt_on && g->N >= 2048;
         blocks_fb += v.n_fb;
         v.blk0 = blocks_a;
@@ -4564,16 +4301,7 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         }
     }
     hm.mark("pre-loop");
-    if (persist) {   // all iterations in one launch (k_pr_cluster)
-        size_t lds = 0;
-        for (int i = 0; i < ng; ++i) lds = std::max(lds, PcLds(gs[i]->N, gs[i]->E).total);
-        mr_prof_begin(ctx);
-        hipLaunchKernelGGL(pc_kernel(fp32, plan.NT), dim3(blocks_fa), dim3(plan.NT), lds, st, dv.p, ng, d, iters);
-        MR_TRY_HIP(ctx, hipGetLastError());
-        MR_DEBUG_CHECK(ctx, "k_pr_cluster");
-        mr_prof_end(ctx, bytes * iters, iters);
-    }
-    for (int it = 0; it < iters && !persist; ++it) {
+    for (int it = 0; it < iters; ++it) {
         mr_prof_begin(ctx);
         if (any_wide && sst != st) {
             MR_TRY_HIP(ctx, hipEventRecord(ctx->side_ev[0], st));   // this iteration's su and q are ready
@@ -4688,10 +4416,6 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         MR_TRY_HIP(ctx, hipStreamSynchronize(st));
     }
     for (int i = 0; i < ng; ++i) {
-        if (hflag[(size_t)4 * i + 3] & 1) {   // k_pr_cluster: a cluster's blocks were not co-resident
-            *timed_out = true;
-            return MR_OK;
-        }
         if (hflag[(size_t)4 * i] & 1) {
             *collided = true;
             return MR_OK;
@@ -4765,15 +4489,9 @@ int mr_pagerank_batch_impl(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly,
                            int iters, int precision, uint32_t flags, bool sharded = false) {
     constexpr int ATTEMPTS = 4;
     for (int a = 0; a < ATTEMPTS; ++a) {
-        bool collided = false, timed_out = false;
+        bool collided = false;
         MR_TRY(pagerank_attempt(ctx, gs, anomaly, ng, d, alpha, iters, precision, flags, sharded, kind_seed(a),
-                                kind_hmask(a), &collided, &timed_out));
-        if (timed_out) {   // k_pr_cluster's clusters were not co-resident: per-iteration launches from now on
-            if (!ctx->no_persist) fprintf(stderr, "[microrank] k_pr_cluster timed out; launching per iteration\n");
-            ctx->no_persist = true;
-            --a;
-            continue;
-        }
+                                kind_hmask(a), &collided));
         if (!collided) return MR_OK;
     }
     return mr_fail(ctx, MR_ERR_STATE, "trace-kind hash collision under %d seeds", ATTEMPTS);
@@ -4922,9 +4640,9 @@ int mr_pagerank_batch_async(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
                             int iters, int precision, int32_t* hflag, PrAsync** out) {
     std::unique_ptr<PrAsync> a(new PrAsync());
     a->hflag = hflag;
-    bool collided = false, timed_out = false;
+    bool collided = false;
     MR_TRY(pagerank_attempt(ctx, gs, anomaly, ng, d, alpha, iters, precision, 0, false, kind_seed(0), kind_hmask(0),
-                            &collided, &timed_out, a.get()));
+                            &collided, a.get()));
     *out = a.release();
     return MR_OK;
 }
@@ -4933,8 +4651,7 @@ int mr_pagerank_async_finish(mr_ctx* ctx, PrAsync* a, bool* rerun) {
     MR_TRY_HIP(ctx, hipEventSynchronize(a->ev));
     for (int i = 0; i < a->ng; ++i) {
         const int32_t* w = a->hflag + 4 * i;
-        if ((w[3] & 1) || (w[0] & 1)) {   // a cluster time-out or a kind-hash collision: the caller reruns
-            if (w[3] & 1) ctx->no_persist = true;   // (as mr_pagerank_batch_impl: per-iteration launches)
+        if (w[0] & 1) {   // a kind-hash collision: the caller reruns
             *rerun = true;
             return MR_OK;
         }

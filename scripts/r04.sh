@@ -3,6 +3,7 @@
 #   t       full -m gpu suite          s      smoke
 #   c2      default bench line (c2 windows + c4_sharded leg, PMC traffic, CPU baseline)
 #   pc2     rocprofv3 kernel table of the timed c2 groups only (--no-side: no latency / kind / c4 legs)
+#   pc2ser  the same with one auxiliary stream and synchronous PageRank groups (kernels alone on the chip)
 #   c4      c4 line (traffic, CPU baseline)       pc4   rocprofv3 kernel table of the c4 command
 #   c4s8    c4 at N=1 holding rank 0's share of an 8-GPU deployment (per-rank compute at N=8)
 #   pmc4    k_tr_a LDS / wait PMC passes at C4 (scripts/pmc_c4.sh)
@@ -37,6 +38,11 @@ if has pc2; then
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/pc2_$TAG -o run --output-format csv \
       -- python3 bench.py --no-traffic --no-cpu --no-side --steps 10 --warmup 2 > gpurun_out/pc2_$TAG.json 2> gpurun_out/pc2_$TAG.err || { echo "rocprof pc2 failed"; tail -5 gpurun_out/pc2_$TAG.err; exit 1; }
   line gpurun_out/pc2_$TAG.json pc2
+fi
+if has pc2ser; then   # the same, one auxiliary stream and synchronous PageRank groups: kernels alone on the chip
+  MR_WIN_STREAMS=1 MR_WIN_PR_SYNC=1 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/pc2ser_$TAG -o run --output-format csv \
+      -- python3 bench.py --no-traffic --no-cpu --no-side --steps 3 --warmup 1 > gpurun_out/pc2ser_$TAG.json 2> gpurun_out/pc2ser_$TAG.err || { echo "rocprof pc2ser failed"; tail -5 gpurun_out/pc2ser_$TAG.err; exit 1; }
+  line gpurun_out/pc2ser_$TAG.json pc2ser
 fi
 if has c4; then
   timeout -k 10 600 python3 bench.py --config c4 --steps 5 --warmup 1 > gpurun_out/c4_$TAG.json 2> gpurun_out/c4_$TAG.err || { tail -5 gpurun_out/c4_$TAG.err; exit 1; }

@@ -511,34 +511,6 @@ def test_config_keywords_against_oracle(anomaly):
         trace_pagerank(*dicts, anomaly, iters=-1)
 
 
-@pytest.mark.parametrize("tpw", ["1", "4", "100000"])
-def test_persistent_iteration_equals_split_launches(c2, tpw, monkeypatch):
-    """k_pr_cluster (all 25 iterations in one launch, a cluster of blocks per graph) gives BITWISE
-    the results of the launch-per-iteration path (k_tr_a + k_fx_b) cut into the same blocks
-    (MR_PR_PERSIST=split), for clusters of one block (MR_PC_TPW large: the row stays in LDS) and
-    of several (write-through row hand-off between blocks); and the oracle's weights at 1e-10."""
-    from microrank_amd import _lib
-    from microrank_amd.graph import DeviceGraph
-
-    st, sg = c2
-    g = sg.as_graph()
-    ctx = _lib.default_context()
-    dg = DeviceGraph.upload(ctx, host_graph_from_oracle(g))
-    monkeypatch.setenv("MR_PC_TPW", tpw)
-    out = {}
-    for mode in ("1", "split"):
-        monkeypatch.setenv("MR_PR_PERSIST", mode)
-        for anomaly in (False, True):
-            dg.pagerank(anomaly)
-            out[(mode, anomaly)] = dg.fetch()[0]
-    for anomaly in (False, True):
-        assert out[("1", anomaly)].tobytes() == out[("split", anomaly)].tobytes()
-        s = orc.power_iteration(g, orc.preference(g, orc.trace_kinds(g), anomaly))
-        w_ref, _ = orc.weights(g, s)
-        np.testing.assert_allclose(out[("1", anomaly)], np.array(list(w_ref.values())), rtol=RTOL64, atol=0)
-    dg.close()
-
-
 def _with_hot_only_traces(hg, hot, seed):
     """Append traces made of hot ops only (1..len(hot) of them): with the hot ops stripped from the
     id chunks such a trace keeps its first hot op in the list (no empty traces)."""

@@ -787,37 +787,3 @@ def test_windows_batch_reaper_and_context_destroy(c3_window, monkeypatch):
         dev.close()
     for a, b in zip(runs["0"][0] + runs["0"][1], runs["1"][0] + runs["1"][1]):
         assert a[2:] == b[2:] and list(a[0]) == list(b[0]) and a[1].tobytes() == b[1].tobytes()
-
-
-def test_windows_batch_persistent_equals_split(c3_window, monkeypatch):
-    """The window batch's PageRanks in one persistent launch per group (k_pr_cluster) equal,
-    bitwise, the same cut launched per iteration (MR_PR_PERSIST=split), and the launch-per-iteration
-    plan of round 2 (MR_PR_PERSIST=0) within 1e-12 with identical top lists."""
-    import bench
-    from microrank_amd import _lib
-    from microrank_amd.online_rca import rank_windows
-    from microrank_amd.preprocess_data import DeviceSpans
-
-    ctx = _lib.default_context()
-    normal, abnormal, t0, t1 = c3_window
-    a3, ok = bench.slo_from_gpu(ctx, normal)
-    devs = [DeviceSpans(ctx, abnormal)]
-    wins = [(devs[0], t0, t1, a3, ok)]
-    for seed in (61, 62, 63):
-        _, nrm, ab = bench.make_window(seed, 500, 20_000)
-        s3, sok = bench.slo_from_gpu(ctx, nrm)
-        d = DeviceSpans(ctx, ab)
-        devs.append(d)
-        u0 = int(ab.tstart.min())
-        wins.append((d, u0, u0 + 5 * 60 * 10**9, s3, sok))
-    runs = {}
-    for mode in ("1", "split", "0"):
-        monkeypatch.setenv("MR_PR_PERSIST", mode)
-        runs[mode] = rank_windows(ctx, wins)
-    for a, b in zip(runs["1"], runs["split"]):
-        assert a[2:] == b[2:] and list(a[0]) == list(b[0]) and a[1].tobytes() == b[1].tobytes()
-    for a, b in zip(runs["1"], runs["0"]):
-        assert a[2:] == b[2:] and list(a[0]) == list(b[0])
-        np.testing.assert_allclose(a[1], b[1], rtol=1e-12, atol=0)
-    for d in devs:
-        d.close()
