@@ -565,12 +565,15 @@ __global__ void __launch_bounds__(IX_BT) k_ix_stats(const int32_t* tflag, int64_
     extern __shared__ int32_t lh[];
     __shared__ unsigned long long ek[ESET];
     __shared__ uint32_t ec[ESET];
-    // more pod-op codes than one LDS histogram holds (wide op spaces, C5's 100k ops): blockIdx.y is an
+    // more pod-op codes than one LDS histogram holds (wide op spaces, C5's 100k ops): blockIdx.x is an
     // op range of IX_HIST codes whose entries this block counts in LDS (the range's blocks share the
     // index: each reads its share of every entry and keeps those of its range); range 0 also takes
-    // the join keys.  Was: three global atomics per entry at up to 10^5 codes.
-    const int32_t op_lo = (int32_t)blockIdx.y * IX_HIST;
-    const bool ranged = gridDim.y > 1;
+    // the join keys.  Was: three global atomics per entry at up to 10^5 codes.  blockIdx.y is the
+    // share of the index: the ranges of one share are dispatched together, so they read the same
+    // entries at about the same time (one HBM read, the other ranges' from the MALL / L2).
+    const int32_t rng = (int32_t)blockIdx.x, chunk = (int32_t)blockIdx.y, nchunk = (int32_t)gridDim.y;
+    const int32_t op_lo = rng * IX_HIST;
+    const bool ranged = gridDim.x > 1;
     const int32_t NPL = ranged ? min(IX_HIST, n_podops - op_lo) : n_podops;   // this block's codes
     n_podops = NPL;
     int32_t* lcnt = lh;
@@ -591,12 +594,12 @@ __global__ void __launch_bounds__(IX_BT) k_ix_stats(const int32_t* tflag, int64_
             ec[i] = 0;
         }
     __syncthreads();
-    const int64_t pper = (n_po + gridDim.x - 1) / gridDim.x, eper = (n_ed + gridDim.x - 1) / gridDim.x;
-    // loads of a round of IX_B entries per thread go out together, then the trace flags
-    const int64_t p0 = (int64_t)blockIdx.x * pper, p1 = min(p0 + pper, n_po);
-    for (int64_t rb = p0; rb < p1; rb += (int64_t)IX_BT * IX_B) {
-        int32_t tr[IX_B], op[IX_B], cn[IX_B], fr[IX_B];
-        bool on[IX_B];
+    const int64_t pper = (n_po + nchunk - 1) / nchunk, eper = (n_ed + nchunk - 1) / nchunk;
+    // a round of IX_B entries per thread: its trace-flag gathers go out, then the NEXT round's loads,
+    // then this round's atomics (the flags' wait leaves the younger loads in flight)
+    const int64_t p0 = (int64_t)chunk * pper, p1 = min(p0 + pper, n_po);
+    int32_t tr[IX_B], op[IX_B], cn[IX_B], fr[IX_B];
+    auto po_load = [&](int64_t rb) {
 #pragma unroll
         for (int j = 0; j < IX_B; ++j) {
             const int64_t r = min(rb + threadIdx.x + (int64_t)j * IX_BT, p1 - 1);
@@ -605,27 +608,34 @@ __global__ void __launch_bounds__(IX_BT) k_ix_stats(const int32_t* tflag, int64_
             cn[j] = po_cnt[r];
             fr[j] = po_first[r];
         }
+    };
+    if (p0 < p1) po_load(p0);
+    for (int64_t rb = p0; rb < p1; rb += (int64_t)IX_BT * IX_B) {
+        int32_t fl[IX_B], cop[IX_B], ccn[IX_B], cfr[IX_B];
 #pragma unroll
         for (int j = 0; j < IX_B; ++j) {
-            op[j] -= op_lo;   // (0 unless ranged)
-            on[j] = rb + threadIdx.x + (int64_t)j * IX_BT < p1 && (!ranged || (uint32_t)op[j] < (uint32_t)NPL) &&
-                    tflag[tr[j]];
+            fl[j] = tflag[tr[j]];
+            cop[j] = op[j] - op_lo;   // (0 unless ranged)
+            ccn[j] = cn[j];
+            cfr[j] = fr[j];
         }
+        if (rb + (int64_t)IX_BT * IX_B < p1) po_load(rb + (int64_t)IX_BT * IX_B);
 #pragma unroll
         for (int j = 0; j < IX_B; ++j) {
-            if (!on[j]) continue;
+            if (!(rb + threadIdx.x + (int64_t)j * IX_BT < p1 && (!ranged || (uint32_t)cop[j] < (uint32_t)NPL) && fl[j]))
+                continue;
             if (use_lds_hist) {
-                atomicAdd(&lcnt[op[j]], cn[j]);
-                atomicMin(&lfirst[op[j]], fr[j]);
-                atomicAdd(&lcov[op[j]], 1);
+                atomicAdd(&lcnt[cop[j]], ccn[j]);
+                atomicMin(&lfirst[cop[j]], cfr[j]);
+                atomicAdd(&lcov[cop[j]], 1);
             } else {
-                atomicAdd(&ocnt[op[j]], cn[j]);
-                atomicMin(&ofirst[op[j]], fr[j]);
-                atomicAdd(&ocov[op[j]], 1);
+                atomicAdd(&ocnt[cop[j]], ccn[j]);
+                atomicMin(&ofirst[cop[j]], cfr[j]);
+                atomicAdd(&ocov[cop[j]], 1);
             }
         }
     }
-    const int64_t q0 = (int64_t)blockIdx.x * eper, q1 = blockIdx.y ? q0 : min(q0 + eper, n_ed);   // (range 0: the keys)
+    const int64_t q0 = (int64_t)chunk * eper, q1 = rng ? q0 : min(q0 + eper, n_ed);   // (range 0: the keys)
     if (ed_eid) {   // dense edge ids: one counter add per selected entry
         for (int64_t rb = q0; rb < q1; rb += (int64_t)IX_BT * IX_B) {
             int32_t tr[IX_B], cn[IX_B], id[IX_B];
@@ -909,8 +919,9 @@ __device__ __forceinline__ void ix_stats2_body(const uint8_t* state, int64_t n_p
     __syncthreads();
     const int64_t pper = (n_po + nblk_ - 1) / nblk_, eper = (n_ed + nblk_ - 1) / nblk_;
     const int64_t p0 = (int64_t)blk_ * pper, p1 = min(p0 + pper, n_po);
-    for (int64_t rb = p0; rb < p1; rb += (int64_t)IX_BT * IX_B) {
-        int32_t tr[IX_B], op[IX_B], cn[IX_B], fr[IX_B];
+    // (as k_ix_stats: a round's state gathers, then the next round's loads, then its atomics)
+    int32_t tr[IX_B], op[IX_B], cn[IX_B], fr[IX_B];
+    auto po_load = [&](int64_t rb) {
 #pragma unroll
         for (int j = 0; j < IX_B; ++j) {
             const int64_t r = min(rb + threadIdx.x + (int64_t)j * IX_BT, p1 - 1);
@@ -919,32 +930,55 @@ __device__ __forceinline__ void ix_stats2_body(const uint8_t* state, int64_t n_p
             cn[j] = po_cnt[r];
             fr[j] = po_first[r];
         }
-        int sd[IX_B];
-#pragma unroll
-        for (int j = 0; j < IX_B; ++j) sd[j] = rb + threadIdx.x + (int64_t)j * IX_BT < p1 ? side_of(state[tr[j]]) : -1;
+    };
+    if (p0 < p1) po_load(p0);
+    for (int64_t rb = p0; rb < p1; rb += (int64_t)IX_BT * IX_B) {
+        uint8_t sv[IX_B];
+        int32_t cop[IX_B], ccn[IX_B], cfr[IX_B];
 #pragma unroll
         for (int j = 0; j < IX_B; ++j) {
-            if (sd[j] < 0) continue;
-            int32_t* L = lh + sd[j] * W;
-            atomicAdd(&L[op[j]], cn[j]);
-            atomicMin(&L[NP + op[j]], fr[j]);
-            atomicAdd(&L[2 * NP + op[j]], 1);
+            sv[j] = state[tr[j]];
+            cop[j] = op[j];
+            ccn[j] = cn[j];
+            cfr[j] = fr[j];
+        }
+        if (rb + (int64_t)IX_BT * IX_B < p1) po_load(rb + (int64_t)IX_BT * IX_B);
+#pragma unroll
+        for (int j = 0; j < IX_B; ++j) {
+            const int sd = rb + threadIdx.x + (int64_t)j * IX_BT < p1 ? side_of(sv[j]) : -1;
+            if (sd < 0) continue;
+            int32_t* L = lh + sd * W;
+            atomicAdd(&L[cop[j]], ccn[j]);
+            atomicMin(&L[NP + cop[j]], cfr[j]);
+            atomicAdd(&L[2 * NP + cop[j]], 1);
         }
     }
     const int64_t q0 = (int64_t)blk_ * eper, q1 = min(q0 + eper, n_ed);
-    for (int64_t rb = q0; rb < q1; rb += (int64_t)IX_BT * IX_B) {
-        int32_t tr[IX_B], cn[IX_B], id[IX_B];
+    int32_t et[IX_B], ei[IX_B], en[IX_B];
+    auto ed_load = [&](int64_t rb) {
 #pragma unroll
         for (int j = 0; j < IX_B; ++j) {
             const int64_t r = min(rb + threadIdx.x + (int64_t)j * IX_BT, q1 - 1);
-            tr[j] = ed_tr[r];
-            id[j] = ed_eid[r];
-            cn[j] = ed_cnt[r];
+            et[j] = ed_tr[r];
+            ei[j] = ed_eid[r];
+            en[j] = ed_cnt[r];
         }
+    };
+    if (q0 < q1) ed_load(q0);
+    for (int64_t rb = q0; rb < q1; rb += (int64_t)IX_BT * IX_B) {
+        uint8_t sv[IX_B];
+        int32_t cid[IX_B], ccn[IX_B];
 #pragma unroll
         for (int j = 0; j < IX_B; ++j) {
-            const int sd = rb + threadIdx.x + (int64_t)j * IX_BT < q1 ? side_of(state[tr[j]]) : -1;
-            if (sd >= 0) atomicAdd((uint32_t*)&lh[sd * W + 3 * NP + id[j]], (uint32_t)cn[j]);
+            sv[j] = state[et[j]];
+            cid[j] = ei[j];
+            ccn[j] = en[j];
+        }
+        if (rb + (int64_t)IX_BT * IX_B < q1) ed_load(rb + (int64_t)IX_BT * IX_B);
+#pragma unroll
+        for (int j = 0; j < IX_B; ++j) {
+            const int sd = rb + threadIdx.x + (int64_t)j * IX_BT < q1 ? side_of(sv[j]) : -1;
+            if (sd >= 0) atomicAdd((uint32_t*)&lh[sd * W + 3 * NP + cid[j]], (uint32_t)ccn[j]);
         }
     }
     __syncthreads();
@@ -1498,8 +1532,8 @@ static int ix_launch(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d_mask, mr_
             return e ? std::max(1, atoi(e)) : 256;
         }();
         int nblk = std::max(1, std::min(ix_cap, cdiv(std::max(sp->n_po, sp->n_ed), IX_BT * IX_EPT)));
-        if (nrange > 1) nblk = std::max(1, std::min(nblk, cdiv(2 * ix_cap, nrange)));   // ~2 blocks per CU over the ranges
-        hipLaunchKernelGGL(k_ix_stats, dim3(nblk, nrange), dim3(IX_BT), lds, st, b.tflag.p, sp->n_po, sp->po_tr.p, sp->po_op.p,
+        if (nrange > 1) nblk = std::max(1, std::min(nblk, 2 * ix_cap / nrange));   // ~2 rounds of one block per CU
+        hipLaunchKernelGGL(k_ix_stats, dim3(nrange, nblk), dim3(IX_BT), lds, st, b.tflag.p, sp->n_po, sp->po_tr.p, sp->po_op.p,
                            sp->po_cnt.p, sp->po_first.p, sp->n_ed, sp->ed_tr.p, sp->ed_key.p, sp->ed_cnt.p, NP, use_lds,
                            b.ocnt.p, b.ofirst.p, b.ocov.p, b.gk.p, b.gc.p, ecap - 1,
                            b.dense ? (const int32_t*)sp->ed_eid.p : nullptr, (int32_t)ecap, lds_ek);

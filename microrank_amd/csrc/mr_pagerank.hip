@@ -1044,7 +1044,7 @@ __global__ void __launch_bounds__(KB) k_kind_rec(const int64_t* off, const int32
         rh[rec] = k;
         rc[rec] = lcnt[i];
         rr[rec] = lrep[i];
-        if (hist) atomicAdd(&hist[kind_part(k, pb)], 1);   // (null: the records are sorted by partition instead)
+        atomicAdd(&hist[kind_part(k, pb)], 1);
     }
     __syncthreads();
     if (t < T) rec_of[t] = tb + lidx[s];
@@ -1061,39 +1061,6 @@ __global__ void k_kind_rscatter(const uint64_t* rh, const uint32_t* rc, const in
     ec[pos] = rc[rec];
     er[pos] = rr[rec];
     rpos[rec] = pos;
-}
-// the records grouped by partition with the library's radix sort instead of a global cursor per
-// partition (one device-scope atomic per record, plus one per record for the histogram: 635 us of
-// k_kind_rscatter at C4's 10M traces): sort keys = the partition (holes of the per-block record
-// ranges: P, sorted last), values = the record; then the records gathered in partition order and
-// each partition's first position by binary search
-__global__ void k_kind_pkeys(const uint64_t* rh, const int32_t* nrec, int64_t R, int pb, int64_t P, uint64_t* key,
-                             uint32_t* val) {
-    const int64_t rec = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (rec >= R) return;
-    key[rec] = (rec % KB) < nrec[rec / KB] ? (uint64_t)kind_part(rh[rec], pb) : (uint64_t)P;
-    val[rec] = (uint32_t)rec;
-}
-__global__ void k_kind_pgather(const uint64_t* key, const uint32_t* val, int64_t R, int64_t P, const uint64_t* rh,
-                               const uint32_t* rc, const int32_t* rr, uint64_t* eh, uint32_t* ec, int32_t* er,
-                               int32_t* rpos) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= R || key[i] >= (uint64_t)P) return;
-    const uint32_t r = val[i];
-    eh[i] = rh[r];
-    ec[i] = rc[r];
-    er[i] = rr[r];
-    rpos[r] = (int32_t)i;
-}
-__global__ void k_kind_pstart(const uint64_t* key, int64_t R, int64_t P, int64_t* pstart) {
-    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (q > P) return;
-    int64_t lo = 0, hi = R;
-    while (lo < hi) {
-        const int64_t mid = (lo + hi) >> 1;
-        if (key[mid] < (uint64_t)q) lo = mid + 1; else hi = mid;
-    }
-    pstart[q] = lo;
 }
 __global__ void __launch_bounds__(KP_B) k_kind_part(const int64_t* pstart, const uint64_t* eh, uint32_t* ec, int32_t* er,
                                                     int32_t* flag) {
@@ -3929,47 +3896,26 @@ static int graph_kinds(mr_ctx* ctx, mr_graph* g, bool chk, bool ktab, uint64_t c
         DBuf<int32_t> rr, er, nrec, rec_of, rpos, hist;
         DBuf<int64_t> pstart, tmp;
         DBuf<unsigned long long> cur;
-        const char* kse = getenv("MR_KIND_SORT");   // (A/B, read per call) 0: the per-record cursor scatter
-        const bool ksort = !(kse && atoi(kse) == 0);
         MR_TRY(rh.alloc(ctx, R));
         MR_TRY(rc.alloc(ctx, R));
         MR_TRY(rr.alloc(ctx, R));
         MR_TRY(rpos.alloc(ctx, R));
-        MR_TRY(eh.alloc(ctx, ksort ? R : (size_t)T));
-        MR_TRY(ec.alloc(ctx, ksort ? R : (size_t)T));
-        MR_TRY(er.alloc(ctx, ksort ? R : (size_t)T));
+        MR_TRY(eh.alloc(ctx, (size_t)T));
+        MR_TRY(ec.alloc(ctx, (size_t)T));
+        MR_TRY(er.alloc(ctx, (size_t)T));
         MR_TRY(nrec.alloc(ctx, (size_t)nb));
         MR_TRY(rec_of.alloc(ctx, (size_t)T));
         MR_TRY(pstart.alloc(ctx, (size_t)P + 1));
-        if (!ksort) {
-            MR_TRY(hist.zero(ctx, (size_t)P));
-            MR_TRY(cur.alloc(ctx, (size_t)P));
-            MR_TRY(tmp.alloc(ctx, (size_t)scan_tmp_elems(P)));
-        }
+        MR_TRY(hist.zero(ctx, (size_t)P));
+        MR_TRY(cur.alloc(ctx, (size_t)P));
+        MR_TRY(tmp.alloc(ctx, (size_t)scan_tmp_elems(P)));
         auto krec = u16 ? k_kind_rec<true> : k_kind_rec<false>;
         hipLaunchKernelGGL(krec, dim3(nb), dim3(KB), 0, st, koff, kops, (const uint16_t*)g->rs16.p, g->w_t.p, T, seed,
-                           hmask, pb, rh.p, rc.p, rr.p, nrec.p, rec_of.p, ksort ? (int32_t*)nullptr : hist.p);
-        if (ksort) {
-            DBuf<uint64_t> key;
-            DBuf<uint32_t> val;
-            MR_TRY(key.alloc(ctx, R));
-            MR_TRY(val.alloc(ctx, R));
-            hipLaunchKernelGGL(k_kind_pkeys, dim3(cdiv((int64_t)R, 256)), dim3(256), 0, st, rh.p, nrec.p, (int64_t)R, pb,
-                               P, key.p, val.p);
-            {
-                SortScratch ws;
-                MR_TRY(mr_radix_sort(ctx, key.p, val.p, (int64_t)R, bits_for((uint64_t)P), ws));
-            }
-            hipLaunchKernelGGL(k_kind_pgather, dim3(cdiv((int64_t)R, 256)), dim3(256), 0, st, key.p, val.p, (int64_t)R,
-                               P, rh.p, rc.p, rr.p, eh.p, ec.p, er.p, rpos.p);
-            hipLaunchKernelGGL(k_kind_pstart, dim3(cdiv(P + 1, 256)), dim3(256), 0, st, key.p, (int64_t)R, P, pstart.p);
-            MR_TRY_HIP(ctx, hipStreamSynchronize(st));   // (the sort's scratch and the keys leave scope)
-        } else {
-            MR_TRY(mr_exclusive_scan_i32(ctx, hist.p, pstart.p, P, tmp.p));
-            MR_TRY_HIP(ctx, hipMemcpyAsync(cur.p, pstart.p, (size_t)P * sizeof(int64_t), hipMemcpyDeviceToDevice, st));
-            hipLaunchKernelGGL(k_kind_rscatter, dim3(cdiv((int64_t)R, 256)), dim3(256), 0, st, rh.p, rc.p, rr.p, nrec.p,
-                               (int32_t)std::min<size_t>(R, 0x7fffffff), pb, cur.p, eh.p, ec.p, er.p, rpos.p);
-        }
+                           hmask, pb, rh.p, rc.p, rr.p, nrec.p, rec_of.p, hist.p);
+        MR_TRY(mr_exclusive_scan_i32(ctx, hist.p, pstart.p, P, tmp.p));
+        MR_TRY_HIP(ctx, hipMemcpyAsync(cur.p, pstart.p, (size_t)P * sizeof(int64_t), hipMemcpyDeviceToDevice, st));
+        hipLaunchKernelGGL(k_kind_rscatter, dim3(cdiv((int64_t)R, 256)), dim3(256), 0, st, rh.p, rc.p, rr.p, nrec.p,
+                           (int32_t)std::min<size_t>(R, 0x7fffffff), pb, cur.p, eh.p, ec.p, er.p, rpos.p);
         hipLaunchKernelGGL(k_kind_part, dim3((uint32_t)P), dim3(KP_B), 0, st, pstart.p, eh.p, ec.p, er.p, g->flag.p);
         if (u16)
             hipLaunchKernelGGL(k_kind_final<uint16_t>, dim3(cdiv(T, 256)), dim3(256), 0, st, rec_of.p, rpos.p, ec.p, er.p,

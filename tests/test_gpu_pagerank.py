@@ -123,14 +123,6 @@ def test_kinds_partition_and_table_paths(c2, part_min, monkeypatch):
     dg.pagerank(True)
     w2, _ = dg.fetch()
     assert w2.tobytes() == w.tobytes()
-    # the partition path's two ways of grouping records (radix sort by partition, the default; a
-    # cursor per partition, MR_KIND_SORT=0): the same classes and representatives
-    monkeypatch.setenv("MR_KIND_PART_MIN", "0")
-    monkeypatch.setenv("MR_KIND_SORT", "0")
-    dg.pagerank(True)
-    w3, _, k3, _ = dg.fetch(kinds=True)
-    np.testing.assert_array_equal(k3, kind)
-    assert w3.tobytes() == w.tobytes()
     dg.close()
 
 
