@@ -999,11 +999,17 @@ constexpr int KP_MEAN = 1024;   // mean records per partition (at most)
 constexpr int KP_LDS = 4096;    // LDS table slots of a partition block
 constexpr int KP_B = 256;
 __device__ __forceinline__ int32_t kind_part(uint64_t h, int pb) { return pb ? (int32_t)(h >> (64 - pb)) : 0; }
+// a record: key, count, first trace -- one 16-B store / load where three arrays cost three
+// scattered partial-line writes per record in k_kind_rscatter
+struct __attribute__((aligned(16))) KRec {
+    unsigned long long h;
+    uint32_t c;
+    int32_t r;
+};
 template <bool U16>
 __global__ void __launch_bounds__(KB) k_kind_rec(const int64_t* off, const int32_t* ops, const uint16_t* o16,
                                                  const float* w_t, int32_t T, uint64_t seed, uint64_t hmask, int pb,
-                                                 uint64_t* rh, uint32_t* rc, int32_t* rr, int32_t* nrec, int32_t* rec_of,
-                                                 int32_t* hist) {
+                                                 KRec* rec_out, int32_t* nrec, int32_t* rec_of, int32_t* hist) {
     __shared__ unsigned long long lkey[KLDS];
     __shared__ uint32_t lcnt[KLDS];
     __shared__ int32_t lrep[KLDS];
@@ -1040,42 +1046,40 @@ __global__ void __launch_bounds__(KB) k_kind_rec(const int64_t* off, const int32
         if (!k) continue;
         const int32_t r = atomicAdd(&ln, 1);   // record order within the block: free (sums / mins)
         lidx[i] = r;
-        const int64_t rec = (int64_t)tb + r;
-        rh[rec] = k;
-        rc[rec] = lcnt[i];
-        rr[rec] = lrep[i];
+        KRec v;
+        v.h = k;
+        v.c = lcnt[i];
+        v.r = lrep[i];
+        rec_out[(int64_t)tb + r] = v;
         atomicAdd(&hist[kind_part(k, pb)], 1);
     }
     __syncthreads();
     if (t < T) rec_of[t] = tb + lidx[s];
     if (threadIdx.x == 0) nrec[blockIdx.x] = ln;
 }
-__global__ void k_kind_rscatter(const uint64_t* rh, const uint32_t* rc, const int32_t* rr, const int32_t* nrec,
-                                int32_t T, int pb, unsigned long long* cur, uint64_t* eh, uint32_t* ec, int32_t* er,
-                                int32_t* rpos) {
+__global__ void k_kind_rscatter(const KRec* rin, const int32_t* nrec, int32_t T, int pb, unsigned long long* cur,
+                                KRec* e, int32_t* rpos) {
     const int32_t rec = blockIdx.x * blockDim.x + threadIdx.x;
     if (rec >= T || (rec % KB) >= nrec[rec / KB]) return;
-    const uint64_t k = rh[rec];
-    const int32_t pos = (int32_t)atomicAdd(&cur[kind_part(k, pb)], 1ull);
-    eh[pos] = k;
-    ec[pos] = rc[rec];
-    er[pos] = rr[rec];
+    const KRec v = rin[rec];
+    const int32_t pos = (int32_t)atomicAdd(&cur[kind_part(v.h, pb)], 1ull);
+    e[pos] = v;
     rpos[rec] = pos;
 }
-__global__ void __launch_bounds__(KP_B) k_kind_part(const int64_t* pstart, const uint64_t* eh, uint32_t* ec, int32_t* er,
-                                                    int32_t* flag) {
+__global__ void __launch_bounds__(KP_B) k_kind_part(const int64_t* pstart, KRec* e, int32_t* flag) {
     __shared__ unsigned long long tkey[KP_LDS];
     __shared__ uint32_t tcnt[KP_LDS];
     __shared__ int32_t trep[KP_LDS];
-    const int64_t b = pstart[blockIdx.x], e = pstart[blockIdx.x + 1];
+    const int64_t b = pstart[blockIdx.x], en = pstart[blockIdx.x + 1];
     for (int i = threadIdx.x; i < KP_LDS; i += KP_B) {
         tkey[i] = 0ull;
         tcnt[i] = 0u;
         trep[i] = 0x7fffffff;
     }
     __syncthreads();
-    for (int64_t i = b + threadIdx.x; i < e; i += KP_B) {
-        const uint64_t h = eh[i];
+    for (int64_t i = b + threadIdx.x; i < en; i += KP_B) {
+        const KRec v = e[i];
+        const uint64_t h = v.h;
         int s = (int)(h & (KP_LDS - 1));
         for (int probe = 0;; ++probe) {
             if (probe == KP_LDS) {   // more distinct keys than slots: not with hashed partitions
@@ -1084,32 +1088,31 @@ __global__ void __launch_bounds__(KP_B) k_kind_part(const int64_t* pstart, const
             }
             const unsigned long long k = atomicCAS(&tkey[s], 0ull, (unsigned long long)h);
             if (k == 0ull || k == h) {
-                atomicAdd(&tcnt[s], ec[i]);
-                atomicMin(&trep[s], er[i]);   // the class's first trace (deterministic)
+                atomicAdd(&tcnt[s], v.c);
+                atomicMin(&trep[s], v.r);   // the class's first trace (deterministic)
                 break;
             }
             s = (s + 1) & (KP_LDS - 1);
         }
     }
     __syncthreads();
-    for (int64_t i = b + threadIdx.x; i < e; i += KP_B) {
-        const uint64_t h = eh[i];
+    for (int64_t i = b + threadIdx.x; i < en; i += KP_B) {
+        const uint64_t h = e[i].h;
         int s = (int)(h & (KP_LDS - 1));
         for (int probe = 0; probe < KP_LDS && tkey[s] != h; ++probe) s = (s + 1) & (KP_LDS - 1);
         if (tkey[s] != h) continue;   // (overflowed: flagged above)
-        ec[i] = tcnt[s];
-        er[i] = trep[s];
+        *(uint2*)&e[i].c = make_uint2(tcnt[s], (uint32_t)trep[s]);   // (c, r): one 8-B store
     }
 }
 template <typename ID>
-__global__ void k_kind_final(const int32_t* rec_of, const int32_t* rpos, const uint32_t* ec, const int32_t* er,
-                             const int64_t* off, const ID* ops, const float* w_t, int32_t T, double* kind,
-                             int32_t* flag, int32_t* krep) {
+__global__ void k_kind_final(const int32_t* rec_of, const int32_t* rpos, const KRec* e, const int64_t* off,
+                             const ID* ops, const float* w_t, int32_t T, double* kind, int32_t* flag, int32_t* krep) {
     const int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= T) return;
     const int32_t pos = rpos[rec_of[t]];
-    kind[t] = (double)ec[pos];
-    const int32_t r = er[pos];
+    const uint2 cr = *(const uint2*)&e[pos].c;
+    kind[t] = (double)cr.x;
+    const int32_t r = (int32_t)cr.y;
     if (krep) krep[t] = r;   // (kind compression: the class representative)
     if (r == t) return;
     // exact membership: same ids and the same fp32(1/len_t) as the representative
@@ -3891,18 +3894,13 @@ static int graph_kinds(mr_ctx* ctx, mr_graph* g, bool chk, bool ktab, uint64_t c
         const int64_t P = (int64_t)1 << pb;
         const int32_t nb = cdiv(T, KB);
         const size_t R = (size_t)nb * KB;
-        DBuf<uint64_t> rh, eh;
-        DBuf<uint32_t> rc, ec;
-        DBuf<int32_t> rr, er, nrec, rec_of, rpos, hist;
+        DBuf<KRec> rec, e;
+        DBuf<int32_t> nrec, rec_of, rpos, hist;
         DBuf<int64_t> pstart, tmp;
         DBuf<unsigned long long> cur;
-        MR_TRY(rh.alloc(ctx, R));
-        MR_TRY(rc.alloc(ctx, R));
-        MR_TRY(rr.alloc(ctx, R));
+        MR_TRY(rec.alloc(ctx, R));
         MR_TRY(rpos.alloc(ctx, R));
-        MR_TRY(eh.alloc(ctx, (size_t)T));
-        MR_TRY(ec.alloc(ctx, (size_t)T));
-        MR_TRY(er.alloc(ctx, (size_t)T));
+        MR_TRY(e.alloc(ctx, (size_t)T));
         MR_TRY(nrec.alloc(ctx, (size_t)nb));
         MR_TRY(rec_of.alloc(ctx, (size_t)T));
         MR_TRY(pstart.alloc(ctx, (size_t)P + 1));
@@ -3911,18 +3909,18 @@ static int graph_kinds(mr_ctx* ctx, mr_graph* g, bool chk, bool ktab, uint64_t c
         MR_TRY(tmp.alloc(ctx, (size_t)scan_tmp_elems(P)));
         auto krec = u16 ? k_kind_rec<true> : k_kind_rec<false>;
         hipLaunchKernelGGL(krec, dim3(nb), dim3(KB), 0, st, koff, kops, (const uint16_t*)g->rs16.p, g->w_t.p, T, seed,
-                           hmask, pb, rh.p, rc.p, rr.p, nrec.p, rec_of.p, hist.p);
+                           hmask, pb, rec.p, nrec.p, rec_of.p, hist.p);
         MR_TRY(mr_exclusive_scan_i32(ctx, hist.p, pstart.p, P, tmp.p));
         MR_TRY_HIP(ctx, hipMemcpyAsync(cur.p, pstart.p, (size_t)P * sizeof(int64_t), hipMemcpyDeviceToDevice, st));
-        hipLaunchKernelGGL(k_kind_rscatter, dim3(cdiv((int64_t)R, 256)), dim3(256), 0, st, rh.p, rc.p, rr.p, nrec.p,
-                           (int32_t)std::min<size_t>(R, 0x7fffffff), pb, cur.p, eh.p, ec.p, er.p, rpos.p);
-        hipLaunchKernelGGL(k_kind_part, dim3((uint32_t)P), dim3(KP_B), 0, st, pstart.p, eh.p, ec.p, er.p, g->flag.p);
+        hipLaunchKernelGGL(k_kind_rscatter, dim3(cdiv((int64_t)R, 256)), dim3(256), 0, st, rec.p, nrec.p,
+                           (int32_t)std::min<size_t>(R, 0x7fffffff), pb, cur.p, e.p, rpos.p);
+        hipLaunchKernelGGL(k_kind_part, dim3((uint32_t)P), dim3(KP_B), 0, st, pstart.p, e.p, g->flag.p);
         if (u16)
-            hipLaunchKernelGGL(k_kind_final<uint16_t>, dim3(cdiv(T, 256)), dim3(256), 0, st, rec_of.p, rpos.p, ec.p, er.p,
-                               koff, (const uint16_t*)g->rs16.p, g->w_t.p, T, g->kind.p, g->flag.p, g->krep.p);
+            hipLaunchKernelGGL(k_kind_final<uint16_t>, dim3(cdiv(T, 256)), dim3(256), 0, st, rec_of.p, rpos.p, e.p, koff,
+                               (const uint16_t*)g->rs16.p, g->w_t.p, T, g->kind.p, g->flag.p, g->krep.p);
         else
-            hipLaunchKernelGGL(k_kind_final<int32_t>, dim3(cdiv(T, 256)), dim3(256), 0, st, rec_of.p, rpos.p, ec.p, er.p,
-                               koff, kops, g->w_t.p, T, g->kind.p, g->flag.p, g->krep.p);
+            hipLaunchKernelGGL(k_kind_final<int32_t>, dim3(cdiv(T, 256)), dim3(256), 0, st, rec_of.p, rpos.p, e.p, koff,
+                               kops, g->w_t.p, T, g->kind.p, g->flag.p, g->krep.p);
         MR_DEBUG_CHECK(ctx, "k_kind_part");
     }
     return MR_OK;

@@ -4,6 +4,7 @@
 #   c2      default bench line (c2 windows + c4_sharded leg, PMC traffic, CPU baseline)
 #   pc2     rocprofv3 kernel table of the timed c2 groups only (--no-side: no latency / kind / c4 legs)
 #   pc2ser  the same with one auxiliary stream and synchronous PageRank groups (kernels alone on the chip)
+#   w1      one C3 window per call under rocprofv3 --kernel-trace (scripts/win1_trace.py)
 #   c4      c4 line (traffic, CPU baseline)       pc4   rocprofv3 kernel table of the c4 command
 #   c4s8    c4 at N=1 holding rank 0's share of an 8-GPU deployment (per-rank compute at N=8)
 #   pmc4    k_tr_a LDS / wait PMC passes at C4 (scripts/pmc_c4.sh)
@@ -43,6 +44,11 @@ if has pc2ser; then   # the same, one auxiliary stream and synchronous PageRank 
   MR_WIN_STREAMS=1 MR_WIN_PR_SYNC=1 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/pc2ser_$TAG -o run --output-format csv \
       -- python3 bench.py --no-traffic --no-cpu --no-side --steps 3 --warmup 1 > gpurun_out/pc2ser_$TAG.json 2> gpurun_out/pc2ser_$TAG.err || { echo "rocprof pc2ser failed"; tail -5 gpurun_out/pc2ser_$TAG.err; exit 1; }
   line gpurun_out/pc2ser_$TAG.json pc2ser
+fi
+if has w1; then   # one C3 window per call: host time, and the kernel trace split per call
+  timeout -k 10 300 rocprofv3 --kernel-trace -d gpurun_out/w1_$TAG -o run --output-format csv \
+      -- python3 scripts/win1_trace.py 20 > gpurun_out/w1_$TAG.log 2>&1 || { echo "w1 failed"; tail -5 gpurun_out/w1_$TAG.log; exit 1; }
+  grep "W=1" gpurun_out/w1_$TAG.log; python3 scripts/win1_trace.py --analyze gpurun_out/w1_$TAG/run_kernel_trace.csv | tail -4
 fi
 if has c4; then
   timeout -k 10 600 python3 bench.py --config c4 --steps 5 --warmup 1 > gpurun_out/c4_$TAG.json 2> gpurun_out/c4_$TAG.err || { tail -5 gpurun_out/c4_$TAG.err; exit 1; }
