@@ -552,6 +552,67 @@ __global__ void __launch_bounds__(SEL_T) k_ix_sel_scan(const uint8_t* mask, cons
         rb += z[i];
     }
 }
+// Wide op spaces (more pod-op codes than one LDS histogram): the selected index entries of share b
+// (the same 1/nblk shares k_ix_stats takes) grouped by op range of IX_HIST codes into out[p0, p1):
+// a counting pass, then a scatter through wave-aggregated LDS cursors; tab[b (R + 1) + r] = the
+// offset of range r in the share.  Each range's k_ix_stats blocks then read only their entries,
+// once, instead of every range reading (and flag-checking) the whole index.
+constexpr int IX_RMAX = 64;   // op ranges the grouping takes (786k codes)
+__global__ void __launch_bounds__(IX_BT) k_ix_rpart(const int32_t* tflag, int64_t n_po, const int32_t* po_tr,
+                                                 const int32_t* po_op, const int32_t* po_cnt, const int32_t* po_first,
+                                                 int32_t nrange, int4* out, int32_t* tab) {
+    __shared__ int32_t cnt[IX_RMAX], cur[IX_RMAX];
+    const int32_t tid = (int32_t)threadIdx.x, lane = tid & (WAVE - 1);
+    const int64_t pper = (n_po + gridDim.x - 1) / gridDim.x, p0 = (int64_t)blockIdx.x * pper, p1 = min(p0 + pper, n_po);
+    if (tid < IX_RMAX) cnt[tid] = 0;
+    __syncthreads();
+    for (int64_t rb = p0; rb < p1; rb += IX_BT) {   // counts per range (a ballot per range present)
+        const int64_t r = rb + tid;
+        int32_t g = -1;
+        if (r < p1 && tflag[po_tr[r]]) g = po_op[r] / IX_HIST;
+        for (uint64_t todo = __ballot(g >= 0); todo;) {
+            const int32_t q = __builtin_amdgcn_readlane(g, __ffsll((unsigned long long)todo) - 1);
+            const uint64_t m = __ballot(g == q);
+            if (lane == 0) atomicAdd(&cnt[q], __popcll(m));
+            todo &= ~m;
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        int32_t a = 0;
+        int32_t* tb = tab + (size_t)blockIdx.x * (nrange + 1);
+        for (int q = 0; q < nrange; ++q) {
+            cur[q] = a;
+            tb[q] = a;
+            a += cnt[q];
+        }
+        tb[nrange] = a;
+    }
+    __syncthreads();
+    for (int64_t rb = p0; rb < p1; rb += IX_BT) {   // the scatter: one cursor add per range present
+        const int64_t r = rb + tid;
+        int32_t g = -1, op = 0, c = 0, f = 0;
+        if (r < p1 && tflag[po_tr[r]]) {
+            op = po_op[r];
+            c = po_cnt[r];
+            f = po_first[r];
+            g = op / IX_HIST;
+        }
+        for (uint64_t todo = __ballot(g >= 0); todo;) {
+            const int ld = __ffsll((unsigned long long)todo) - 1;
+            const int32_t q = __builtin_amdgcn_readlane(g, ld);
+            const uint64_t m = __ballot(g == q);
+            int32_t base = 0;
+            if (lane == ld) base = atomicAdd(&cur[q], __popcll(m));
+            base = __builtin_amdgcn_readlane(base, ld);
+            if (g == q) {
+                const int32_t k = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                out[p0 + base + k] = make_int4(op - q * IX_HIST, c, f, 0);
+            }
+            todo &= ~m;
+        }
+    }
+}
 // entry-parallel over the index: span counts and first rows per pod-op of the selected traces
 // (LDS-aggregated per block), and their join keys with multiplicity into the block's LDS edge
 // set (hot keys aggregated before global atomics).  Block b takes a 1/gridDim share of each list.
@@ -561,7 +622,7 @@ __global__ void __launch_bounds__(IX_BT) k_ix_stats(const int32_t* tflag, int64_
                                                  const int32_t* ed_cnt, int32_t n_podops, int use_lds_hist,
                                                  int32_t* ocnt, int32_t* ofirst, int32_t* ocov, uint64_t* gk,
                                                  uint32_t* gc, uint64_t gmask, const int32_t* ed_eid, int32_t n_ek,
-                                                 int lds_ek) {
+                                                 int lds_ek, const int4* rent, const int32_t* rtab, int32_t nshare) {
     extern __shared__ int32_t lh[];
     __shared__ unsigned long long ek[ESET];
     __shared__ uint32_t ec[ESET];
@@ -569,8 +630,8 @@ __global__ void __launch_bounds__(IX_BT) k_ix_stats(const int32_t* tflag, int64_
     // op range of IX_HIST codes whose entries this block counts in LDS (the range's blocks share the
     // index: each reads its share of every entry and keeps those of its range); range 0 also takes
     // the join keys.  Was: three global atomics per entry at up to 10^5 codes.  blockIdx.y is the
-    // share of the index: the ranges of one share are dispatched together, so they read the same
-    // entries at about the same time (one HBM read, the other ranges' from the MALL / L2).
+    // share of the index.  rent: the share's selected entries grouped by range (k_ix_rpart) -- the
+    // block reads only its range's.
     const int32_t rng = (int32_t)blockIdx.x, chunk = (int32_t)blockIdx.y, nchunk = (int32_t)gridDim.y;
     const int32_t op_lo = rng * IX_HIST;
     const bool ranged = gridDim.x > 1;
@@ -609,8 +670,28 @@ __global__ void __launch_bounds__(IX_BT) k_ix_stats(const int32_t* tflag, int64_
             fr[j] = po_first[r];
         }
     };
-    if (p0 < p1) po_load(p0);
-    for (int64_t rb = p0; rb < p1; rb += (int64_t)IX_BT * IX_B) {
+    // (ranged: LDS histograms; this block's chunk = rpart's shares [s0, s1))
+    const int32_t s0 = rent ? (int32_t)((int64_t)chunk * nshare / nchunk) : 0;
+    const int32_t s1 = rent ? (int32_t)((int64_t)(chunk + 1) * nshare / nchunk) : 0;
+    const int64_t sper = rent ? (n_po + nshare - 1) / nshare : 0;
+    for (int32_t sh = s0; sh < s1; ++sh) {
+        const int32_t* tb = rtab + (size_t)sh * (gridDim.x + 1);
+        const int64_t e0 = sh * sper + tb[rng], e1 = sh * sper + tb[rng + 1];
+        for (int64_t rb = e0; rb < e1; rb += (int64_t)IX_BT * IX_B) {
+            int4 v[IX_B];
+#pragma unroll
+            for (int j = 0; j < IX_B; ++j) v[j] = rent[min(rb + threadIdx.x + (int64_t)j * IX_BT, e1 - 1)];
+#pragma unroll
+            for (int j = 0; j < IX_B; ++j) {
+                if (rb + threadIdx.x + (int64_t)j * IX_BT >= e1) continue;
+                atomicAdd(&lcnt[v[j].x], v[j].y);
+                atomicMin(&lfirst[v[j].x], v[j].z);
+                atomicAdd(&lcov[v[j].x], 1);
+            }
+        }
+    }
+    if (!rent && p0 < p1) po_load(p0);
+    for (int64_t rb = p0; !rent && rb < p1; rb += (int64_t)IX_BT * IX_B) {
         int32_t fl[IX_B], cop[IX_B], ccn[IX_B], cfr[IX_B];
 #pragma unroll
         for (int j = 0; j < IX_B; ++j) {
@@ -1533,10 +1614,22 @@ static int ix_launch(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d_mask, mr_
         }();
         int nblk = std::max(1, std::min(ix_cap, cdiv(std::max(sp->n_po, sp->n_ed), IX_BT * IX_EPT)));
         if (nrange > 1) nblk = std::max(1, std::min(nblk, 2 * ix_cap / nrange));   // ~2 rounds of one block per CU
+        // ranged: the entries grouped by range first (k_ix_rpart over nshare shares, 4 blocks per CU)
+        DBuf<int4> rent;
+        DBuf<int32_t> rtab;
+        int32_t nshare = 0;
+        if (nrange > 1 && nrange <= IX_RMAX && sp->n_po > 0) {
+            nshare = (int32_t)std::max<int64_t>(nblk, std::min<int64_t>(4 * (int64_t)ix_cap, cdiv(sp->n_po, IX_BT * 16)));
+            MR_TRY(rent.alloc(ctx, (size_t)sp->n_po));
+            MR_TRY(rtab.alloc(ctx, (size_t)nshare * (nrange + 1)));
+            hipLaunchKernelGGL(k_ix_rpart, dim3(nshare), dim3(IX_BT), 0, st, b.tflag.p, sp->n_po, sp->po_tr.p, sp->po_op.p,
+                               sp->po_cnt.p, sp->po_first.p, (int32_t)nrange, rent.p, rtab.p);
+        }
         hipLaunchKernelGGL(k_ix_stats, dim3(nrange, nblk), dim3(IX_BT), lds, st, b.tflag.p, sp->n_po, sp->po_tr.p, sp->po_op.p,
                            sp->po_cnt.p, sp->po_first.p, sp->n_ed, sp->ed_tr.p, sp->ed_key.p, sp->ed_cnt.p, NP, use_lds,
                            b.ocnt.p, b.ofirst.p, b.ocov.p, b.gk.p, b.gc.p, ecap - 1,
-                           b.dense ? (const int32_t*)sp->ed_eid.p : nullptr, (int32_t)ecap, lds_ek);
+                           b.dense ? (const int32_t*)sp->ed_eid.p : nullptr, (int32_t)ecap, lds_ek,
+                           (const int4*)rent.p, (const int32_t*)rtab.p, nshare);
     }
     if (sp->n_xj)
         hipLaunchKernelGGL(k_ix_cross, dim3(cdiv(sp->n_xj, 256)), dim3(256), 0, st, d_mask, sp->xj_tc.p, sp->xj_tp.p,
