@@ -13,6 +13,7 @@
 //      op-major side is derived by mr_graph_prepare as tiles); call edges sorted by
 //      (child, parent) give P_ss by child.
 #include <algorithm>
+#include <cstring>
 #include <vector>
 
 #include "mr_detect_dev.h"
@@ -787,6 +788,38 @@ __global__ void __launch_bounds__(IX_BT) k_ix_stats(const int32_t* tflag, int64_
                 atomicMin(&ofirst[op_lo + i], lfirst[i]);
                 atomicAdd(&ocov[op_lo + i], lcov[i]);
             }
+}
+// Edges counted in edge-id order (mr_spans.eb_*, large tables): a lane per entry, the wave's runs
+// of one id summed by a segmented scan (ids ascend along the wave), one add per run and wave into
+// cnt[id] -- in place of an atomic (or a hash probe) per entry.  The selection is read from a
+// bitmap of the traces (NT / 8 bytes: the gathers stay in L2).
+__global__ void k_tbits(const int32_t* tflag, int32_t NT, uint64_t* bits) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t m = __ballot(t < NT && tflag[t] != 0);
+    if ((threadIdx.x & (WAVE - 1)) == 0 && t < NT) bits[t >> 6] = m;
+}
+__global__ void k_ix_ecount(const int32_t* eb_tr, const int32_t* eb_cnt, const int32_t* eb_eid, int64_t n,
+                            const uint64_t* tb, uint32_t* cnt) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int lane = (int)(threadIdx.x & (WAVE - 1));
+    const bool in = i < n;
+    const int32_t e = in ? eb_eid[i] : -1;
+    const int32_t t = in ? eb_tr[i] : 0;
+    uint32_t v = (in && ((tb[t >> 6] >> (t & 63)) & 1ull)) ? (uint32_t)eb_cnt[i] : 0u;
+#pragma unroll
+    for (int o = 1; o < WAVE; o <<= 1) {   // inclusive segmented scan
+        const uint32_t u = __shfl_up(v, o, WAVE);
+        const int32_t eu = __shfl_up(e, o, WAVE);
+        if (lane >= o && eu == e) v += u;
+    }
+    const int32_t en = __shfl_down(e, 1, WAVE);
+    if (in && v && (lane == WAVE - 1 || en != e)) atomicAdd(&cnt[e], v);
+}
+// a sharded build's hash set from the per-id counts (one insert per id present, not per entry)
+__global__ void k_ix_edense_hash(const uint64_t* ekey, const uint32_t* cnt, int64_t E, uint64_t* gk, uint32_t* gc,
+                                 uint64_t gmask) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < E && cnt[i]) global_edge_add(ekey[i], cnt[i], gk, gc, gmask);
 }
 // join pairs whose rows lie in different traces count when both traces are selected (T11)
 __global__ void k_ix_cross(const uint8_t* mask, const int32_t* tc, const int32_t* tp, const uint64_t* key, int64_t n,
@@ -1625,11 +1658,30 @@ static int ix_launch(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d_mask, mr_
             hipLaunchKernelGGL(k_ix_rpart, dim3(nshare), dim3(IX_BT), 0, st, b.tflag.p, sp->n_po, sp->po_tr.p, sp->po_op.p,
                                sp->po_cnt.p, sp->po_first.p, (int32_t)nrange, rent.p, rtab.p);
         }
+        // edges in edge-id order when the table keeps them (large tables) and the counts do not sit
+        // in LDS beside the histogram: a segmented sum per id (k_ix_ecount) instead of k_ix_stats'
+        // atomic or hash probe per entry; sharded builds then insert each id's count into the hash set
+        const char* ebe = getenv("MR_IX_EB");   // (read per call) "0": never
+        const bool eb = sp->eb_eid.p && sp->n_ed > 0 && !(ebe && !strcmp(ebe, "0")) &&
+                        (!lds_ek || (ebe && !strcmp(ebe, "force")));
         hipLaunchKernelGGL(k_ix_stats, dim3(nrange, nblk), dim3(IX_BT), lds, st, b.tflag.p, sp->n_po, sp->po_tr.p, sp->po_op.p,
-                           sp->po_cnt.p, sp->po_first.p, sp->n_ed, sp->ed_tr.p, sp->ed_key.p, sp->ed_cnt.p, NP, use_lds,
-                           b.ocnt.p, b.ofirst.p, b.ocov.p, b.gk.p, b.gc.p, ecap - 1,
+                           sp->po_cnt.p, sp->po_first.p, eb ? (int64_t)0 : sp->n_ed, sp->ed_tr.p, sp->ed_key.p, sp->ed_cnt.p,
+                           NP, use_lds, b.ocnt.p, b.ofirst.p, b.ocov.p, b.gk.p, b.gc.p, ecap - 1,
                            b.dense ? (const int32_t*)sp->ed_eid.p : nullptr, (int32_t)ecap, lds_ek,
                            (const int4*)rent.p, (const int32_t*)rtab.p, nshare);
+        if (eb) {
+            const int64_t E = sp->n_edge_keys;
+            DBuf<uint64_t> tb;
+            DBuf<uint32_t> idc;   // (sharded: the per-id counts before the hash set)
+            MR_TRY(tb.alloc(ctx, (size_t)cdiv((int64_t)NT, 64)));
+            if (!b.dense) MR_TRY(idc.zero(ctx, (size_t)E));
+            hipLaunchKernelGGL(k_tbits, dim3(cdiv((int64_t)NT, 256)), dim3(256), 0, st, b.tflag.p, NT, tb.p);
+            hipLaunchKernelGGL(k_ix_ecount, dim3(cdiv(sp->n_ed, 256)), dim3(256), 0, st, sp->eb_tr.p, sp->eb_cnt.p,
+                               sp->eb_eid.p, sp->n_ed, tb.p, b.dense ? b.gc.p : idc.p);
+            if (!b.dense)
+                hipLaunchKernelGGL(k_ix_edense_hash, dim3(cdiv(E, 256)), dim3(256), 0, st, sp->ekey.p, idc.p, E, b.gk.p,
+                                   b.gc.p, ecap - 1);
+        }
     }
     if (sp->n_xj)
         hipLaunchKernelGGL(k_ix_cross, dim3(cdiv(sp->n_xj, 256)), dim3(256), 0, st, d_mask, sp->xj_tc.p, sp->xj_tp.p,

@@ -315,6 +315,9 @@ struct mr_graph {
     DBuf<int32_t> flag;          // [4] error flags written by kernels
 };
 
+// edge entries from which the index also keeps them in edge-id order (mr_spans.eb_*);
+// MR_IX_EB (read per ingest / build): "0" never, "force" at any size (tests)
+constexpr int64_t ED_BYID_MIN = (int64_t)1 << 22;
 struct mr_spans {
     mr_ctx* ctx = nullptr;
     int64_t S = 0;
@@ -345,6 +348,9 @@ struct mr_spans {
     DBuf<int64_t> ed_off;                // [NT+1] distinct (parent pod-op, child pod-op) join keys
     DBuf<uint64_t> ed_key;               //        inside the trace, (parent << 32 | child) ...
     DBuf<int32_t> ed_cnt, ed_tr;         // ... with multiplicity and trace
+    // large tables (n_ed >= ED_BYID_MIN): the edge entries again, in edge-id order (trace, count,
+    // id), so a build counts its edges by a segmented sum per id instead of an atomic per entry
+    DBuf<int32_t> eb_tr, eb_cnt, eb_eid;
     DBuf<int32_t> xj_tc, xj_tp;          // [n_xj] join pairs across traces (T11): child / parent trace
     DBuf<uint64_t> xj_key;               //        and key
     // tables ingested from strings (mr_spans_ingest): the first row of each trace / pod-op /

@@ -15,6 +15,7 @@
 // The index is a derived view of the uploaded columns: no result depends on it being present.
 #include <algorithm>
 #include <climits>
+#include <cstring>
 
 #include "mr_detect_dev.h"
 #include "mr_prim.h"
@@ -158,6 +159,22 @@ __global__ void k_ix_ekeys(const uint64_t* key, const int32_t* head, const int64
     ekey[hpos[i]] = ((k >> nbp) << 32) | (k & m);
 }
 // dense edge id of each key: its position among the distinct keys (binary search)
+// the edge entries in edge-id order (mr_spans.eb_*): sort keys = the ids, values = the entry
+__global__ void k_ix_eb_keys(const int32_t* eid, int64_t n, uint64_t* key, uint32_t* val) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    key[i] = (uint64_t)(uint32_t)eid[i];
+    val[i] = (uint32_t)i;
+}
+__global__ void k_ix_eb_gather(const uint64_t* key, const uint32_t* val, int64_t n, const int32_t* ed_tr,
+                               const int32_t* ed_cnt, int32_t* eb_tr, int32_t* eb_cnt, int32_t* eb_eid) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t r = val[i];
+    eb_tr[i] = ed_tr[r];
+    eb_cnt[i] = ed_cnt[r];
+    eb_eid[i] = (int32_t)key[i];
+}
 __global__ void k_ix_eid(const uint64_t* key, int64_t n, const uint64_t* ekey, int64_t E, int32_t* eid) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -438,6 +455,33 @@ int mr_spans_index(mr_ctx* ctx, mr_spans* s) {
                                s->xj_eid.p);
         MR_TRY_HIP(ctx, hipGetLastError());
         MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+        // large tables: the entries in edge-id order as well (a radix sort of the ids carrying the
+        // entry index, then a gather), so a build's edge count is a segmented sum per id
+        const char* ebe = getenv("MR_IX_EB");
+        const bool eb = ebe ? strcmp(ebe, "0") != 0 && (!strcmp(ebe, "force") || s->n_ed >= ED_BYID_MIN)
+                            : s->n_ed >= ED_BYID_MIN;
+        s->eb_tr.reset();
+        s->eb_cnt.reset();
+        s->eb_eid.reset();
+        if (eb && s->n_ed > 0 && E > 0 && s->n_ed < ((int64_t)1 << 32)) {
+            const int64_t n = s->n_ed;
+            DBuf<uint64_t> key;
+            DBuf<uint32_t> val;
+            MR_TRY(key.alloc(ctx, (size_t)n));
+            MR_TRY(val.alloc(ctx, (size_t)n));
+            hipLaunchKernelGGL(k_ix_eb_keys, dim3(cdiv(n, XB)), dim3(XB), 0, st, s->ed_eid.p, n, key.p, val.p);
+            SortScratch ws;
+            int bits = 1;
+            while (bits < 63 && ((int64_t)1 << bits) < E) ++bits;
+            MR_TRY(mr_radix_sort(ctx, key.p, val.p, n, bits, ws));
+            MR_TRY(s->eb_tr.alloc(ctx, (size_t)n));
+            MR_TRY(s->eb_cnt.alloc(ctx, (size_t)n));
+            MR_TRY(s->eb_eid.alloc(ctx, (size_t)n));
+            hipLaunchKernelGGL(k_ix_eb_gather, dim3(cdiv(n, XB)), dim3(XB), 0, st, key.p, val.p, n, s->ed_tr.p, s->ed_cnt.p,
+                               s->eb_tr.p, s->eb_cnt.p, s->eb_eid.p);
+            MR_TRY_HIP(ctx, hipGetLastError());
+            MR_TRY_HIP(ctx, hipStreamSynchronize(st));   // (the sort's scratch leaves scope)
+        }
     }
     int32_t hb = 0;
     MR_TRY(bad.download(ctx, &hb, 1));

@@ -4,6 +4,7 @@
 #   c2      default bench line (c2 windows + c4_sharded leg, PMC traffic, CPU baseline)
 #   pc2     rocprofv3 kernel table of the timed c2 groups only (--no-side: no latency / kind / c4 legs)
 #   pc2ser  the same with one auxiliary stream and synchronous PageRank groups (kernels alone on the chip)
+#   c4sp    c4 from span shards at N=1 (build inside the step)
 #   w1      one C3 window per call under rocprofv3 --kernel-trace (scripts/win1_trace.py)
 #   c4      c4 line (traffic, CPU baseline)       pc4   rocprofv3 kernel table of the c4 command
 #   c4s8    c4 at N=1 holding rank 0's share of an 8-GPU deployment (per-rank compute at N=8)
@@ -73,9 +74,13 @@ if has segv; then
   rc=$?; echo "segv-command rc=$rc"; [ $rc -eq 0 ] || { tail -40 gpurun_out/segv_$TAG.err; exit $rc; }
   line gpurun_out/segv_$TAG.json segv
 fi
+if has c4sp; then   # c4 from span shards at N=1 (K1 build inside the step)
+  timeout -k 10 600 python3 bench.py --config c4 --from-spans --steps 3 --warmup 1 --no-traffic --no-cpu > gpurun_out/c4sp_$TAG.json 2> gpurun_out/c4sp_$TAG.err || { tail -5 gpurun_out/c4sp_$TAG.err; exit 1; }
+  line gpurun_out/c4sp_$TAG.json c4sp; python3 -c "import json;d=json.load(open('gpurun_out/c4sp_$TAG.json'));print('c4sp build_ms', d.get('build_ms'), 'ms_per_step', d['ms_per_step'])"
+fi
 if has c5s; then
   timeout -k 10 600 python3 bench.py --config c5 --from-spans --shard-of 8 --steps 3 --warmup 1 --no-traffic --no-cpu > gpurun_out/c5s_$TAG.json 2> gpurun_out/c5s_$TAG.err || { tail -5 gpurun_out/c5s_$TAG.err; exit 1; }
-  line gpurun_out/c5s_$TAG.json c5s
+  line gpurun_out/c5s_$TAG.json c5s; python3 -c "import json;d=json.load(open('gpurun_out/c5s_$TAG.json'));print('c5s build_ms', d.get('build_ms'), 'ms_per_step', d['ms_per_step'])"
 fi
 if has pc5s; then
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/pc5s_$TAG -o run --output-format csv \

@@ -225,3 +225,48 @@ def test_two_contexts_share_one_dataframe():
     w2, _ = trace_pagerank(*get_pagerank_graph(lst, adf, ctx=c2), False, ctx=c2)
     assert list(w1) == list(w2) and [float(x) for x in w1.values()] == [float(x) for x in w2.values()]
     np.testing.assert_allclose(list(w1.values()), unhex(case["pr_normal"]["weight"]), rtol=1e-10)
+
+
+def test_edge_count_in_edge_id_order_equals_per_entry_count(monkeypatch):
+    """Large tables keep their edge entries in edge-id order too (mr_spans.eb_*) and a build counts
+    edges by a segmented sum per id (k_ix_ecount) instead of an atomic / hash probe per entry:
+    forced on a small table (MR_IX_EB=force) the dense build (mr_graph_build) and the sharded one
+    (mr_graph_build_sharded, one rank: the per-id counts inserted into its hash set) give the same
+    graphs and bitwise the same weights as the per-entry count (MR_IX_EB=0), with a trace_list
+    that is not every trace and broken / duplicated traces."""
+    from microrank_amd import _lib, shard, synth
+    from microrank_amd._lib import ptr
+    from microrank_amd.graph import DeviceGraph
+    from microrank_amd.preprocess_data import DeviceSpans
+
+    st = synth.big_spans(3000, 20_000, seed=5, dup_frac=0.01, broken_frac=0.05)
+    sel = np.ones(st.n_traces, np.uint8)
+    sel[::5] = 0
+    ctx = _lib.default_context()
+    lib = _lib.load()
+    out = {}
+    for mode in ("0", "force"):
+        monkeypatch.setenv("MR_IX_EB", mode)
+        dev = DeviceSpans(ctx, st)
+        h = _lib.P()
+        ctx.check(lib.mr_graph_build(ctx.h, dev.h, ptr(sel, C.c_uint8), C.byref(h)), "mr_graph_build")
+        n, t, nnz, e = C.c_int32(), C.c_int32(), C.c_int64(), C.c_int64()
+        lib.mr_graph_info(h, C.byref(n), C.byref(t), C.byref(nnz), C.byref(e))
+        node = np.empty(n.value, np.int32)
+        tcode = np.empty(t.value, np.int32)
+        ctx.check(lib.mr_graph_nodes(h, ptr(node, C.c_int32), ptr(tcode, C.c_int32)), "mr_graph_nodes")
+        dg = DeviceGraph(ctx, h, node, tcode, n.value, t.value)
+        dg.pagerank(True)
+        w, cov = dg.fetch()
+        sg = shard.build_graph(dev, sel)
+        ws, covs = shard.sharded_pagerank(sg, True)
+        out[mode] = ((n.value, t.value, nnz.value, e.value), node.copy(), tcode.copy(), w.copy(), cov.copy(),
+                     sg.info(), np.asarray(ws).copy(), np.asarray(covs).copy())
+        assert e.value > 0
+        dg.close()
+        sg.close()
+        dev.close()
+    a, b = out["0"], out["force"]
+    assert a[0] == b[0] and a[5] == b[5]
+    for x, y in zip(a[1:5] + a[6:], b[1:5] + b[6:]):
+        assert x.tobytes() == y.tobytes()
