@@ -790,30 +790,43 @@ __global__ void __launch_bounds__(IX_BT) k_ix_stats(const int32_t* tflag, int64_
             }
 }
 // Edges counted in edge-id order (mr_spans.eb_*, large tables): a lane per entry, the wave's runs
-// of one id summed by a segmented scan (ids ascend along the wave), one add per run and wave into
-// cnt[id] -- in place of an atomic (or a hash probe) per entry.  The selection is read from a
+// of one id summed by a segmented scan (ids ascend along the wave), a wave walking EC_CH chunks
+// with the last run's sum carried from chunk to chunk, one add per run into cnt[id] -- in place of
+// an atomic (or a hash probe) per entry, and a hot id (millions of entries) takes one add per
+// 2048 entries, not per 64.  The selection is read from a
 // bitmap of the traces (NT / 8 bytes: the gathers stay in L2).
 __global__ void k_tbits(const int32_t* tflag, int32_t NT, uint64_t* bits) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t m = __ballot(t < NT && tflag[t] != 0);
     if ((threadIdx.x & (WAVE - 1)) == 0 && t < NT) bits[t >> 6] = m;
 }
+constexpr int EC_CH = 32;   // k_ix_ecount: chunks of 64 entries per wave (a run's sum carried across them)
 __global__ void k_ix_ecount(const int32_t* eb_tr, const int32_t* eb_cnt, const int32_t* eb_eid, int64_t n,
                             const uint64_t* tb, uint32_t* cnt) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int lane = (int)(threadIdx.x & (WAVE - 1));
-    const bool in = i < n;
-    const int32_t e = in ? eb_eid[i] : -1;
-    const int32_t t = in ? eb_tr[i] : 0;
-    uint32_t v = (in && ((tb[t >> 6] >> (t & 63)) & 1ull)) ? (uint32_t)eb_cnt[i] : 0u;
+    const int64_t w = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
+    int32_t ce = -1;   // the run that continues into the next chunk (wave-uniform) and its sum so far
+    uint32_t cv = 0u;
+    for (int c = 0; c < EC_CH; ++c) {
+        const int64_t i = (w * EC_CH + c) * WAVE + lane;
+        if (w * EC_CH * WAVE + (int64_t)c * WAVE >= n) break;   // (wave-uniform)
+        const bool in = i < n;
+        const int32_t e = in ? eb_eid[i] : -1;
+        const int32_t t = in ? eb_tr[i] : 0;
+        uint32_t v = (in && ((tb[t >> 6] >> (t & 63)) & 1ull)) ? (uint32_t)eb_cnt[i] : 0u;
 #pragma unroll
-    for (int o = 1; o < WAVE; o <<= 1) {   // inclusive segmented scan
-        const uint32_t u = __shfl_up(v, o, WAVE);
-        const int32_t eu = __shfl_up(e, o, WAVE);
-        if (lane >= o && eu == e) v += u;
+        for (int o = 1; o < WAVE; o <<= 1) {   // inclusive segmented scan (ids ascend along the wave)
+            const uint32_t u = __shfl_up(v, o, WAVE);
+            const int32_t eu = __shfl_up(e, o, WAVE);
+            if (lane >= o && eu == e) v += u;
+        }
+        if (e == ce) v += cv;   // (the chunk's first run continues the carried one)
+        const int32_t en = __shfl_down(e, 1, WAVE);
+        if (in && v && lane != WAVE - 1 && en != e) atomicAdd(&cnt[e], v);
+        ce = __builtin_amdgcn_readlane(e, WAVE - 1);
+        cv = (uint32_t)__builtin_amdgcn_readlane((int)v, WAVE - 1);
     }
-    const int32_t en = __shfl_down(e, 1, WAVE);
-    if (in && v && (lane == WAVE - 1 || en != e)) atomicAdd(&cnt[e], v);
+    if (lane == 0 && ce >= 0 && cv) atomicAdd(&cnt[ce], cv);
 }
 // a sharded build's hash set from the per-id counts (one insert per id present, not per entry)
 __global__ void k_ix_edense_hash(const uint64_t* ekey, const uint32_t* cnt, int64_t E, uint64_t* gk, uint32_t* gc,
@@ -1676,7 +1689,7 @@ static int ix_launch(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d_mask, mr_
             MR_TRY(tb.alloc(ctx, (size_t)cdiv((int64_t)NT, 64)));
             if (!b.dense) MR_TRY(idc.zero(ctx, (size_t)E));
             hipLaunchKernelGGL(k_tbits, dim3(cdiv((int64_t)NT, 256)), dim3(256), 0, st, b.tflag.p, NT, tb.p);
-            hipLaunchKernelGGL(k_ix_ecount, dim3(cdiv(sp->n_ed, 256)), dim3(256), 0, st, sp->eb_tr.p, sp->eb_cnt.p,
+            hipLaunchKernelGGL(k_ix_ecount, dim3(cdiv(sp->n_ed, 256 * EC_CH)), dim3(256), 0, st, sp->eb_tr.p, sp->eb_cnt.p,
                                sp->eb_eid.p, sp->n_ed, tb.p, b.dense ? b.gc.p : idc.p);
             if (!b.dense)
                 hipLaunchKernelGGL(k_ix_edense_hash, dim3(cdiv(E, 256)), dim3(256), 0, st, sp->ekey.p, idc.p, E, b.gk.p,

@@ -13,6 +13,7 @@
 #   c3 c5   c3 / c5 lines          c5s / pc5s   c5 from span shards (rank 0 of 8) / its kernel table
 #   pc5     c5 kernel table          pc4s8  kernel table of c4 rank 0's share of 8
 #   c3ab c2ab  AB_VAR over AB_VALS on the c3 / c2 lines (interleaved, two repeats)
+#   spab    AB_VAR over AB_VALS on the span-built c4 / c5-share steps (build_ms)
 #   shard   the shard tests only
 TAG=${1:-x}
 STAGES=${2:-"t s c2"}
@@ -117,6 +118,16 @@ if has c4ab; then
         env $AB_VAR=$v timeout -k 10 300 python3 bench.py --config c4 --shard-of $sh --steps 10 --warmup 2 --no-cpu --no-traffic > gpurun_out/ab_c4s${sh}_${TAG}_${v}_$rep.json 2> gpurun_out/ab_c4s${sh}_${TAG}_${v}_$rep.err || { tail -5 gpurun_out/ab_c4s${sh}_${TAG}_${v}_$rep.err; exit 1; }
         line gpurun_out/ab_c4s${sh}_${TAG}_${v}_$rep.json "c4 shard-of $sh $AB_VAR=$v rep $rep"
       done
+    done
+  done
+fi
+# A/B of AB_VAR over AB_VALS on the span-built c4 (N=1) and c5 (rank 0 of 8) steps, interleaved twice
+if has spab; then
+  for rep in 1 2; do
+    for v in $AB_VALS; do
+      env $AB_VAR=$v timeout -k 10 300 python3 bench.py --config c4 --from-spans --steps 3 --warmup 1 --no-traffic --no-cpu > gpurun_out/ab_c4sp_${TAG}_${v}_$rep.json 2> gpurun_out/ab_c4sp_${TAG}_${v}_$rep.err || { tail -5 gpurun_out/ab_c4sp_${TAG}_${v}_$rep.err; exit 1; }
+      env $AB_VAR=$v timeout -k 10 300 python3 bench.py --config c5 --from-spans --shard-of 8 --steps 3 --warmup 1 --no-traffic --no-cpu > gpurun_out/ab_c5s_${TAG}_${v}_$rep.json 2> gpurun_out/ab_c5s_${TAG}_${v}_$rep.err || { tail -5 gpurun_out/ab_c5s_${TAG}_${v}_$rep.err; exit 1; }
+      for c in c4sp c5s; do python3 -c "import json,sys;d=json.load(open(sys.argv[1]));print(sys.argv[2], 'build_ms', d.get('build_ms'), 'ms_per_step', d['ms_per_step'])" gpurun_out/ab_${c}_${TAG}_${v}_$rep.json "$c $AB_VAR=$v rep $rep"; done
     done
   done
 fi
