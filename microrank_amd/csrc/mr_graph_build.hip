@@ -821,6 +821,7 @@ __global__ void k_ix_ecount(const int32_t* eb_tr, const int32_t* eb_cnt, const i
             if (lane >= o && eu == e) v += u;
         }
         if (e == ce) v += cv;   // (the chunk's first run continues the carried one)
+        else if (lane == 0 && ce >= 0 && cv) atomicAdd(&cnt[ce], cv);   // (or the carried run ended with the chunk)
         const int32_t en = __shfl_down(e, 1, WAVE);
         if (in && v && lane != WAVE - 1 && en != e) atomicAdd(&cnt[e], v);
         ce = __builtin_amdgcn_readlane(e, WAVE - 1);
