@@ -825,34 +825,48 @@ constexpr uint64_t KCHK_SEED = 0x0ddba11cafeull;
 // counter), then each distinct key of the block does ONE global insert + add.
 // CHK (sharded graphs on >1 rank): the representative's check hash is stored per global slot
 // (chk) for the cross-rank merge, computed in the same walk instead of a later re-read.
-// U16 (u16 trace-major ids, N <= 65536): the block's 256 traces are hashed cooperatively -- the
-// threads stream the block's contiguous id range in aligned 8-id (16 B) chunks, coalesced across
-// the wave, and add mix64(op) into per-trace LDS sums (an order-free SET hash: the ids of a
-// trace are distinct and ascending, so the set is the list).  The walk-per-thread form (int32
-// ids) reads one trace per lane, ~60 B apart.  Either hash only buckets traces; membership is
-// decided by k_kind_verify's exact comparison.
-// Set hashes of the block's KB traces (tb = first trace): U16 -- the cooperative walk below,
-// through per-trace LDS sums (loff, lacc, lacc2: KB + 1 / KB / KB entries); else a walk per
-// thread.  Every thread of the block must call it; *h (and *h2 with CHK) is set for t < T.
-template <bool CHK, bool U16>
+// IDW 2 / 4 (u16 ids, N <= 65536 / int32 ids): the block's 256 traces are hashed cooperatively --
+// the threads stream the block's contiguous id range in aligned 16-B chunks (8 / 4 ids), coalesced
+// across the wave, and add mix64(op) into per-trace LDS sums (an order-free SET hash: the ids of a
+// trace are distinct and ascending, so the set is the list).  The walk-per-thread form (IDW 0,
+// MR_KIND_WALK) reads one trace per lane, ~60 B apart (C5's kinds: 4.6 ms of dependent loads).
+// Either hash only buckets traces; membership is decided by an exact comparison.
+// Set hashes of the block's KB traces (tb = first trace), through per-trace LDS sums (loff, lacc,
+// lacc2: KB + 1 / KB / KB entries) or a walk per thread.  Every thread of the block must call it;
+// *h (and *h2 with CHK) is set for t < T.
+// IDW (id width of the cooperative walk): 2 -- u16 ids (rs16, N <= 65536), 4 -- int32 ids (wide
+// graphs: C5's 100k ops; the same 16-B chunks, 4 ids each), 0 -- a walk per thread (MR_KIND_WALK).
+template <bool CHK, int IDW>
 __device__ __forceinline__ void kind_block_hash(const int64_t* off, const int32_t* ops, const uint16_t* o16,
                                                 const float* w_t, int32_t T, int32_t tb, uint64_t seed, int64_t* loff,
                                                 unsigned long long* lacc, unsigned long long* lacc2, uint64_t* h,
                                                 uint64_t* h2) {
     const int32_t t = tb + threadIdx.x;
-    if (U16) {
+    if constexpr (IDW != 0) {
+        constexpr int IPC = IDW == 2 ? 8 : 4;   // ids per 16-B chunk
+        __shared__ int64_t s_end;               // the id array's end (the last chunk's loads stop there)
         const int nt = min(KB, T - tb);
         if ((int)threadIdx.x < nt) {
             loff[threadIdx.x] = off[t];
             lacc[threadIdx.x] = 0ull;
             if (CHK) lacc2[threadIdx.x] = 0ull;
         }
-        if (threadIdx.x == 0) loff[nt] = off[tb + nt];
+        if (threadIdx.x == 0) {
+            loff[nt] = off[tb + nt];
+            s_end = off[T];
+        }
         __syncthreads();
-        const int64_t b = loff[0], e = loff[nt];
-        for (int64_t c = (b & ~7ll) + 8ll * threadIdx.x; c < e; c += 8ll * KB) {
-            const uint4 v = *reinterpret_cast<const uint4*>(o16 + c);   // rs16 holds nnz + 8 ids
-            const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+        const int64_t b = loff[0], e = loff[nt], eall = s_end;
+        for (int64_t c = (b & ~(int64_t)(IPC - 1)) + (int64_t)IPC * threadIdx.x; c < e; c += (int64_t)IPC * KB) {
+            uint32_t wd[4];
+            if (IDW == 2 || c + IPC <= eall) {   // (rs16 holds nnz + 8 ids)
+                const uint4 v = IDW == 2 ? *reinterpret_cast<const uint4*>(o16 + c)
+                                         : *reinterpret_cast<const uint4*>(ops + c);
+                wd[0] = v.x, wd[1] = v.y, wd[2] = v.z, wd[3] = v.w;
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) wd[k] = c + k < eall ? (uint32_t)ops[c + k] : 0u;
+            }
             const int64_t p0 = c > b ? c : b;
             int lo = 0, hi = nt - 1;   // the trace holding p0: last lt with loff[lt] <= p0
             while (lo < hi) {
@@ -865,7 +879,7 @@ __device__ __forceinline__ void kind_block_hash(const int64_t* off, const int32_
             unsigned long long a = 0ull, a2 = 0ull;
             bool any = false;
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {
+            for (int k = 0; k < IPC; ++k) {
                 const int64_t idx = c + k;
                 if (idx < b || idx >= e) continue;
                 while (idx >= nb) {
@@ -878,7 +892,7 @@ __device__ __forceinline__ void kind_block_hash(const int64_t* off, const int32_
                     ++lt;
                     nb = loff[lt + 1];
                 }
-                const uint64_t op = (wd[k >> 1] >> ((k & 1) * 16)) & 0xffffu;
+                const uint64_t op = IDW == 2 ? (wd[k >> 1] >> ((k & 1) * 16)) & 0xffffu : (uint64_t)wd[k];
                 a += mix64(op ^ seed);
                 if (CHK) a2 += mix64(op ^ KCHK_SEED);
                 any = true;
@@ -891,7 +905,7 @@ __device__ __forceinline__ void kind_block_hash(const int64_t* off, const int32_
         __syncthreads();
     }
     if (t < T) {
-        if (U16) {
+        if constexpr (IDW != 0) {
             const int64_t n = loff[threadIdx.x + 1] - loff[threadIdx.x];
             const uint64_t wb = n > 0 ? (uint64_t)__float_as_uint(w_t[t]) : 0ull;
             *h = kind_fold(seed, wb, n, lacc[threadIdx.x]);
@@ -902,7 +916,7 @@ __device__ __forceinline__ void kind_block_hash(const int64_t* off, const int32_
     }
 }
 
-template <bool CHK, bool U16>
+template <bool CHK, int IDW>
 __device__ __forceinline__ void kind_insert_body(int32_t blk, const int64_t* off, const int32_t* ops, const uint16_t* o16,
                                                  const float* w_t, int32_t T, unsigned long long* hk, KCnt* cr,
                                                  int32_t* slot_of, uint64_t mask, uint64_t seed, uint64_t* chk,
@@ -912,8 +926,8 @@ __device__ __forceinline__ void kind_insert_body(int32_t blk, const int64_t* off
     __shared__ int32_t lrep[KLDS];
     __shared__ int32_t lglob[KLDS];
     __shared__ uint64_t lchk[CHK ? KLDS : 1];
-    __shared__ int64_t loff[U16 ? KB + 1 : 1];
-    __shared__ unsigned long long lacc[U16 ? KB : 1], lacc2[U16 && CHK ? KB : 1];
+    __shared__ int64_t loff[IDW ? KB + 1 : 1];
+    __shared__ unsigned long long lacc[IDW ? KB : 1], lacc2[IDW && CHK ? KB : 1];
     for (int i = threadIdx.x; i < KLDS; i += KB) {
         lkey[i] = 0ull;
         lcnt[i] = 0u;
@@ -922,7 +936,7 @@ __device__ __forceinline__ void kind_insert_body(int32_t blk, const int64_t* off
     const int32_t tb = blk * KB;
     const int32_t t = tb + threadIdx.x;
     uint64_t h = 0, h2 = 0;
-    kind_block_hash<CHK, U16>(off, ops, o16, w_t, T, tb, seed, loff, lacc, lacc2, &h, &h2);
+    kind_block_hash<CHK, IDW>(off, ops, o16, w_t, T, tb, seed, loff, lacc, lacc2, &h, &h2);
     __syncthreads();
     int myslot = -1;
     if (t < T) {
@@ -960,11 +974,11 @@ __device__ __forceinline__ void kind_insert_body(int32_t blk, const int64_t* off
     __syncthreads();
     if (t < T) slot_of[t] = lglob[myslot];
 }
-template <bool CHK, bool U16>
+template <bool CHK, int IDW>
 __global__ void __launch_bounds__(KB) k_kind_insert(const int64_t* off, const int32_t* ops, const uint16_t* o16,
                                                     const float* w_t, int32_t T, unsigned long long* hk, KCnt* cr, int32_t* slot_of,
                                                     uint64_t mask, uint64_t seed, uint64_t* chk, uint64_t hmask) {
-    kind_insert_body<CHK, U16>((int32_t)blockIdx.x, off, ops, o16, w_t, T, hk, cr, slot_of, mask, seed, chk, hmask);
+    kind_insert_body<CHK, IDW>((int32_t)blockIdx.x, off, ops, o16, w_t, T, hk, cr, slot_of, mask, seed, chk, hmask);
 }
 
 template <typename ID>   // int32 ids, or their u16 copy (rs16)
@@ -1006,7 +1020,7 @@ struct __attribute__((aligned(16))) KRec {
     uint32_t c;
     int32_t r;
 };
-template <bool U16>
+template <int IDW>
 __global__ void __launch_bounds__(KB) k_kind_rec(const int64_t* off, const int32_t* ops, const uint16_t* o16,
                                                  const float* w_t, int32_t T, uint64_t seed, uint64_t hmask, int pb,
                                                  KRec* rec_out, int32_t* nrec, int32_t* rec_of, int32_t* hist) {
@@ -1015,8 +1029,8 @@ __global__ void __launch_bounds__(KB) k_kind_rec(const int64_t* off, const int32
     __shared__ int32_t lrep[KLDS];
     __shared__ int32_t lidx[KLDS];
     __shared__ int32_t ln;
-    __shared__ int64_t loff[U16 ? KB + 1 : 1];
-    __shared__ unsigned long long lacc[U16 ? KB : 1], lacc2[1];
+    __shared__ int64_t loff[IDW ? KB + 1 : 1];
+    __shared__ unsigned long long lacc[IDW ? KB : 1], lacc2[1];
     for (int i = threadIdx.x; i < KLDS; i += KB) {
         lkey[i] = 0ull;
         lcnt[i] = 0u;
@@ -1025,7 +1039,7 @@ __global__ void __launch_bounds__(KB) k_kind_rec(const int64_t* off, const int32
     if (threadIdx.x == 0) ln = 0;
     const int32_t tb = blockIdx.x * KB, t = tb + threadIdx.x;
     uint64_t h = 0, h2 = 0;
-    kind_block_hash<false, U16>(off, ops, o16, w_t, T, tb, seed, loff, lacc, lacc2, &h, &h2);
+    kind_block_hash<false, IDW>(off, ops, o16, w_t, T, tb, seed, loff, lacc, lacc2, &h, &h2);
     __syncthreads();
     int s = -1;
     if (t < T) {
@@ -1340,7 +1354,7 @@ __global__ void k_reset_init_b(const SDev* __restrict__ sd, int32_t ng) {
 __global__ void __launch_bounds__(KB) k_kind_insert_b(const SDev* __restrict__ sd, int32_t ng, uint64_t seed,
                                                       uint64_t hmask) {
     const SDev& G = sd[sd_graph(sd, ng, (int32_t)blockIdx.x, 1)];
-    kind_insert_body<false, true>((int32_t)blockIdx.x - G.b_kins, G.off, nullptr, G.o16, G.w_t, G.T, G.hk, G.cr,
+    kind_insert_body<false, 2>((int32_t)blockIdx.x - G.b_kins, G.off, nullptr, G.o16, G.w_t, G.T, G.hk, G.cr,
                                   G.slot_of, (uint64_t)(G.cap - 1), seed, nullptr, hmask);
 }
 __global__ void k_kind_verify_b(const SDev* __restrict__ sd, int32_t ng) {
@@ -3847,12 +3861,12 @@ static int graph_kinds(mr_ctx* ctx, mr_graph* g, bool chk, bool ktab, uint64_t c
     const int32_t T = g->T;
     const int64_t* koff = g->rs_is_sr ? g->rs_off.p : g->srt_off.p;
     const int32_t* kops = g->rs_is_sr ? g->rs_ops.p : g->srt_ops.p;
-    static const bool no_u16 = getenv("MR_KIND_WALK") != nullptr;   // A/B knob: per-thread int32 walk
-    const bool u16 = !no_u16 && g->rs_is_sr && g->rs16.p != nullptr;   // rs16 = u16 copy of rs_ops
+    static const bool walk = getenv("MR_KIND_WALK") != nullptr;   // A/B knob: per-thread int32 walk
+    const bool u16 = !walk && g->rs_is_sr && g->rs16.p != nullptr;   // rs16 = u16 copy of rs_ops
     if (ktab) {
         if (chk) MR_TRY(g->ht_chk.alloc(ctx, cap));
-        auto kins = chk ? (u16 ? k_kind_insert<true, true> : k_kind_insert<true, false>)
-                        : (u16 ? k_kind_insert<false, true> : k_kind_insert<false, false>);
+        auto kins = chk ? (u16 ? k_kind_insert<true, 2> : walk ? k_kind_insert<true, 0> : k_kind_insert<true, 4>)
+                        : (u16 ? k_kind_insert<false, 2> : walk ? k_kind_insert<false, 0> : k_kind_insert<false, 4>);
         if (T)
             hipLaunchKernelGGL(kins, dim3(cdiv(T, KB)), dim3(KB), 0, st, koff, kops, (const uint16_t*)g->rs16.p, g->w_t.p,
                                T, g->ht_key.p, g->ht_cr.p, g->slot_of.p, (uint64_t)(cap - 1), seed,
@@ -3885,7 +3899,7 @@ static int graph_kinds(mr_ctx* ctx, mr_graph* g, bool chk, bool ktab, uint64_t c
         MR_TRY(hist.zero(ctx, (size_t)P));
         MR_TRY(cur.alloc(ctx, (size_t)P));
         MR_TRY(tmp.alloc(ctx, (size_t)scan_tmp_elems(P)));
-        auto krec = u16 ? k_kind_rec<true> : k_kind_rec<false>;
+        auto krec = u16 ? k_kind_rec<2> : walk ? k_kind_rec<0> : k_kind_rec<4>;
         hipLaunchKernelGGL(krec, dim3(nb), dim3(KB), 0, st, koff, kops, (const uint16_t*)g->rs16.p, g->w_t.p, T, seed,
                            hmask, pb, rec.p, nrec.p, rec_of.p, hist.p);
         MR_TRY(mr_exclusive_scan_i32(ctx, hist.p, pstart.p, P, tmp.p));
