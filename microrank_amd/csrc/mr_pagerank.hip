@@ -1065,7 +1065,7 @@ __global__ void __launch_bounds__(KB) k_kind_rec(const int64_t* off, const int32
         v.c = lcnt[i];
         v.r = lrep[i];
         rec_out[(int64_t)tb + r] = v;
-        atomicAdd(&hist[kind_part(k, pb)], 1);
+        if (hist) atomicAdd(&hist[kind_part(k, pb)], 1);   // (the cursor scatter's counts)
     }
     __syncthreads();
     if (t < T) rec_of[t] = tb + lidx[s];
@@ -1079,6 +1079,95 @@ __global__ void k_kind_rscatter(const KRec* rin, const int32_t* nrec, int32_t T,
     const int32_t pos = (int32_t)atomicAdd(&cur[kind_part(v.h, pb)], 1ull);
     e[pos] = v;
     rpos[rec] = pos;
+}
+// The records grouped by partition in two passes over the partition's bits, with no device atomic
+// per record (the cursor scatter above takes two: its counts and its cursor, 7.4 ms of C5's
+// 100M records):
+//   k_kp1_count   tiles of KT slots: per tile a histogram of the partition's top b1 bits (the
+//                 coarse bucket), written bucket-major (cnt[b * ntile + tile]), so ONE exclusive
+//                 scan of it gives every (bucket, tile)'s first position;
+//   k_kp1_scatter the tile's records to their buckets through LDS cursors, each with its slot;
+//   k_kp2         a block per bucket: counts its fine partitions (the next pb - b1 bits) in LDS,
+//                 writes their starts, and scatters the bucket's records into partition order
+//                 inside the bucket's range, recording every slot's final position (rpos).
+// The order inside a partition depends on LDS atomics; k_kind_part's merge (sums, minimum) does
+// not: the same classes and representatives.
+constexpr int KP1_B = 8;    // coarse bits
+constexpr int KT = 4096;    // slots per level-1 tile
+constexpr int KT_T = 256;   // threads of a level-1 block
+constexpr int KP2_T = 1024;
+__device__ __forceinline__ int32_t kbits(uint64_t h, int n) { return n ? (int32_t)(h >> (64 - n)) : 0; }
+__global__ void __launch_bounds__(KT_T) k_kp1_count(const KRec* rec, const int32_t* nrec, int64_t R, int b1,
+                                                    int32_t ntile, int32_t* cnt) {
+    __shared__ int32_t hb[1 << KP1_B];
+    const int nbk = 1 << b1;
+    for (int i = threadIdx.x; i < nbk; i += KT_T) hb[i] = 0;
+    __syncthreads();
+    const int64_t s0 = (int64_t)blockIdx.x * KT;
+    for (int k = 0; k < KT / KT_T; ++k) {
+        const int64_t sl = s0 + k * KT_T + threadIdx.x;
+        if (sl < R && (int32_t)(sl % KB) < nrec[sl / KB]) atomicAdd(&hb[kbits(rec[sl].h, b1)], 1);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < nbk; i += KT_T) cnt[(int64_t)i * ntile + blockIdx.x] = hb[i];
+}
+__global__ void __launch_bounds__(KT_T) k_kp1_scatter(const KRec* rec, const int32_t* nrec, int64_t R, int b1,
+                                                      int32_t ntile, const int64_t* off, KRec* out, uint32_t* oslot) {
+    __shared__ unsigned long long cur[1 << KP1_B];
+    const int nbk = 1 << b1;
+    for (int i = threadIdx.x; i < nbk; i += KT_T) cur[i] = (unsigned long long)off[(int64_t)i * ntile + blockIdx.x];
+    __syncthreads();
+    const int64_t s0 = (int64_t)blockIdx.x * KT;
+    for (int k = 0; k < KT / KT_T; ++k) {
+        const int64_t sl = s0 + k * KT_T + threadIdx.x;
+        if (sl < R && (int32_t)(sl % KB) < nrec[sl / KB]) {
+            const KRec v = rec[sl];
+            const int64_t pos = (int64_t)atomicAdd(&cur[kbits(v.h, b1)], 1ull);
+            out[pos] = v;
+            oslot[pos] = (uint32_t)sl;
+        }
+    }
+}
+__global__ void __launch_bounds__(KP2_T) k_kp2(const KRec* in, const uint32_t* islot, const int64_t* off, int pb,
+                                               int b1, int32_t ntile, KRec* out, int32_t* rpos, int64_t* pstart) {
+    extern __shared__ int64_t kp2[];   // [nf] cursors, then [KP2_T] scan partials
+    const int nf = 1 << (pb - b1), b = (int)blockIdx.x, tid = (int)threadIdx.x;
+    const int64_t B0 = off[(int64_t)b * ntile], B1 = off[(int64_t)(b + 1) * ntile];
+    int64_t* cur = kp2;
+    int64_t* part = kp2 + nf;
+    for (int f = tid; f < nf; f += KP2_T) cur[f] = 0;
+    __syncthreads();
+    const uint64_t fm = (uint64_t)nf - 1;
+    for (int64_t i = B0 + tid; i < B1; i += KP2_T)
+        atomicAdd((unsigned long long*)&cur[(uint64_t)kbits(in[i].h, pb) & fm], 1ull);
+    __syncthreads();
+    // exclusive scan of the nf counts: a run of consecutive counts per thread, then its partials
+    const int per = (nf + KP2_T - 1) / KP2_T, f0 = tid * per, f1 = min(f0 + per, nf);
+    int64_t a = 0;
+    for (int f = f0; f < f1; ++f) a += cur[f];
+    part[tid] = a;
+    __syncthreads();
+    for (int o = 1; o < KP2_T; o <<= 1) {
+        const int64_t x = tid >= o ? part[tid - o] : 0;
+        __syncthreads();
+        part[tid] += x;
+        __syncthreads();
+    }
+    int64_t run = B0 + part[tid] - a;
+    for (int f = f0; f < f1; ++f) {
+        const int64_t c = cur[f];
+        cur[f] = run;
+        pstart[(int64_t)b * nf + f] = run;
+        run += c;
+    }
+    if (b == (int)gridDim.x - 1 && tid == 0) pstart[(int64_t)gridDim.x * nf] = B1;
+    __syncthreads();
+    for (int64_t i = B0 + tid; i < B1; i += KP2_T) {
+        const KRec v = in[i];
+        const int64_t pos = (int64_t)atomicAdd((unsigned long long*)&cur[(uint64_t)kbits(v.h, pb) & fm], 1ull);
+        out[pos] = v;
+        rpos[islot[i]] = (int32_t)pos;
+    }
 }
 __global__ void __launch_bounds__(KP_B) k_kind_part(const int64_t* pstart, KRec* e, int32_t* flag) {
     __shared__ unsigned long long tkey[KP_LDS];
@@ -3896,16 +3985,45 @@ static int graph_kinds(mr_ctx* ctx, mr_graph* g, bool chk, bool ktab, uint64_t c
         MR_TRY(nrec.alloc(ctx, (size_t)nb));
         MR_TRY(rec_of.alloc(ctx, (size_t)T));
         MR_TRY(pstart.alloc(ctx, (size_t)P + 1));
-        MR_TRY(hist.zero(ctx, (size_t)P));
-        MR_TRY(cur.alloc(ctx, (size_t)P));
-        MR_TRY(tmp.alloc(ctx, (size_t)scan_tmp_elems(P)));
+        // MR_KIND_GROUP (A/B, read per call): "cursor" -- the per-record cursor scatter; else the
+        // two-pass grouping (k_kp1_*, k_kp2)
+        const char* kge = getenv("MR_KIND_GROUP");
+        const bool cursor = kge && !strcmp(kge, "cursor");
         auto krec = u16 ? k_kind_rec<2> : walk ? k_kind_rec<0> : k_kind_rec<4>;
-        hipLaunchKernelGGL(krec, dim3(nb), dim3(KB), 0, st, koff, kops, (const uint16_t*)g->rs16.p, g->w_t.p, T, seed,
-                           hmask, pb, rec.p, nrec.p, rec_of.p, hist.p);
-        MR_TRY(mr_exclusive_scan_i32(ctx, hist.p, pstart.p, P, tmp.p));
-        MR_TRY_HIP(ctx, hipMemcpyAsync(cur.p, pstart.p, (size_t)P * sizeof(int64_t), hipMemcpyDeviceToDevice, st));
-        hipLaunchKernelGGL(k_kind_rscatter, dim3(cdiv((int64_t)R, 256)), dim3(256), 0, st, rec.p, nrec.p,
-                           (int32_t)std::min<size_t>(R, 0x7fffffff), pb, cur.p, e.p, rpos.p);
+        if (cursor) {
+            MR_TRY(hist.zero(ctx, (size_t)P));
+            MR_TRY(cur.alloc(ctx, (size_t)P));
+            MR_TRY(tmp.alloc(ctx, (size_t)scan_tmp_elems(P)));
+            hipLaunchKernelGGL(krec, dim3(nb), dim3(KB), 0, st, koff, kops, (const uint16_t*)g->rs16.p, g->w_t.p, T,
+                               seed, hmask, pb, rec.p, nrec.p, rec_of.p, hist.p);
+            MR_TRY(mr_exclusive_scan_i32(ctx, hist.p, pstart.p, P, tmp.p));
+            MR_TRY_HIP(ctx, hipMemcpyAsync(cur.p, pstart.p, (size_t)P * sizeof(int64_t), hipMemcpyDeviceToDevice, st));
+            hipLaunchKernelGGL(k_kind_rscatter, dim3(cdiv((int64_t)R, 256)), dim3(256), 0, st, rec.p, nrec.p,
+                               (int32_t)std::min<size_t>(R, 0x7fffffff), pb, cur.p, e.p, rpos.p);
+        } else {
+            const int b1 = std::min(pb, KP1_B), nbk = 1 << b1, nf = 1 << (pb - b1);
+            const int32_t ntile = (int32_t)cdiv((int64_t)R, KT);
+            const int64_t nc = (int64_t)nbk * ntile;
+            DBuf<int32_t> tcnt;
+            DBuf<int64_t> toff;
+            DBuf<KRec> r1;
+            DBuf<uint32_t> s1;
+            MR_TRY(tcnt.alloc(ctx, (size_t)nc));
+            MR_TRY(toff.alloc(ctx, (size_t)nc + 1));
+            MR_TRY(tmp.alloc(ctx, (size_t)scan_tmp_elems(nc)));
+            MR_TRY(r1.alloc(ctx, (size_t)T));
+            MR_TRY(s1.alloc(ctx, (size_t)T));
+            hipLaunchKernelGGL(krec, dim3(nb), dim3(KB), 0, st, koff, kops, (const uint16_t*)g->rs16.p, g->w_t.p, T,
+                               seed, hmask, pb, rec.p, nrec.p, rec_of.p, (int32_t*)nullptr);
+            hipLaunchKernelGGL(k_kp1_count, dim3(ntile), dim3(KT_T), 0, st, rec.p, nrec.p, (int64_t)R, b1, ntile, tcnt.p);
+            MR_TRY(mr_exclusive_scan_i32(ctx, tcnt.p, toff.p, nc, tmp.p));
+            hipLaunchKernelGGL(k_kp1_scatter, dim3(ntile), dim3(KT_T), 0, st, rec.p, nrec.p, (int64_t)R, b1, ntile,
+                               toff.p, r1.p, s1.p);
+            const size_t lds2 = ((size_t)nf + KP2_T) * sizeof(int64_t);
+            hipLaunchKernelGGL(k_kp2, dim3(nbk), dim3(KP2_T), lds2, st, r1.p, s1.p, toff.p, pb, b1, ntile, e.p, rpos.p,
+                               pstart.p);
+            MR_TRY_HIP(ctx, hipStreamSynchronize(st));   // (the level-1 buffers leave scope)
+        }
         hipLaunchKernelGGL(k_kind_part, dim3((uint32_t)P), dim3(KP_B), 0, st, pstart.p, e.p, g->flag.p);
         if (u16)
             hipLaunchKernelGGL(k_kind_final<uint16_t>, dim3(cdiv(T, 256)), dim3(256), 0, st, rec_of.p, rpos.p, e.p, koff,
