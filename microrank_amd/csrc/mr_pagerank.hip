@@ -1096,6 +1096,7 @@ constexpr int KP1_B = 8;    // coarse bits
 constexpr int KT = 4096;    // slots per level-1 tile
 constexpr int KT_T = 256;   // threads of a level-1 block
 constexpr int KP2_T = 1024;
+constexpr size_t KG_TWO_MAX = (size_t)1 << 25;   // record slots up to which the two-pass grouping runs
 __device__ __forceinline__ int32_t kbits(uint64_t h, int n) { return n ? (int32_t)(h >> (64 - n)) : 0; }
 __global__ void __launch_bounds__(KT_T) k_kp1_count(const KRec* rec, const int32_t* nrec, int64_t R, int b1,
                                                     int32_t ntile, int32_t* cnt) {
@@ -3985,10 +3986,12 @@ static int graph_kinds(mr_ctx* ctx, mr_graph* g, bool chk, bool ktab, uint64_t c
         MR_TRY(nrec.alloc(ctx, (size_t)nb));
         MR_TRY(rec_of.alloc(ctx, (size_t)T));
         MR_TRY(pstart.alloc(ctx, (size_t)P + 1));
-        // MR_KIND_GROUP (A/B, read per call): "cursor" -- the per-record cursor scatter; else the
-        // two-pass grouping (k_kp1_*, k_kp2)
+        // The two-pass grouping (k_kp1_*, k_kp2) up to KG_TWO_MAX record slots, the per-record cursor
+        // scatter above it: the two-pass form ends in one random 4-B write per record (rpos), which
+        // the MALL absorbs at C4's 10M records (+4.3 % C4 GTEPS, profiles/r04q) but not at C5's 100M
+        // (93.6 vs 92.0 ms per step).  MR_KIND_GROUP (A/B, read per call): "two" / "cursor" forces one.
         const char* kge = getenv("MR_KIND_GROUP");
-        const bool cursor = kge && !strcmp(kge, "cursor");
+        const bool cursor = kge ? !strcmp(kge, "cursor") : R > KG_TWO_MAX;
         auto krec = u16 ? k_kind_rec<2> : walk ? k_kind_rec<0> : k_kind_rec<4>;
         if (cursor) {
             MR_TRY(hist.zero(ctx, (size_t)P));
