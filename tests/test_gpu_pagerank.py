@@ -123,6 +123,16 @@ def test_kinds_partition_and_table_paths(c2, part_min, monkeypatch):
     dg.pagerank(True)
     w2, _ = dg.fetch()
     assert w2.tobytes() == w.tobytes()
+    # the partition path's two ways of grouping records by partition (two passes of its bits, the
+    # default at this size; a device cursor per partition, the default past 32M records): the same
+    # classes and representatives
+    monkeypatch.setenv("MR_KIND_PART_MIN", "0")
+    for grouping in ("two", "cursor"):
+        monkeypatch.setenv("MR_KIND_GROUP", grouping)
+        dg.pagerank(True)
+        w3, _, k3, _ = dg.fetch(kinds=True)
+        np.testing.assert_array_equal(k3, kind)
+        assert w3.tobytes() == w.tobytes()
     dg.close()
 
 
