@@ -2262,9 +2262,7 @@ __device__ __forceinline__ double tr_walk(const GDev& G, int32_t lb, int cur, in
 // loads (ss_off -> ss_par -> pw, s_k) then run in the slack of the block's slowest wave, not in
 // k_fx_b's critical path.  The same arithmetic as k_fx_b (a lane per column of <= 8 parents with
 // wave_sum's butterfly value, a wave per column of more): fx_ssv[o], read there bitwise.
-// (wt: stored write-through -- the last-block finish reads them with sc1 loads in the same launch)
-__device__ __forceinline__ void tr_ssv_share(const GDev& G, int32_t lb, int cur, double Ms, int* ctr, int lane,
-                                             bool wt) {
+__device__ __forceinline__ void tr_ssv_share(const GDev& G, int32_t lb, int cur, double Ms, int* ctr, int lane) {
     const int32_t N = G.N;
     const int32_t oa = (int32_t)((int64_t)lb * N / G.n_fa), ob = (int32_t)((int64_t)(lb + 1) * N / G.n_fa);
     for (;;) {
@@ -2308,13 +2306,7 @@ __device__ __forceinline__ void tr_ssv_share(const GDev& G, int32_t lb, int cur,
             bb = wave_sum(bb);
             if (lane == j) ssv = G.alpha * (bb / Ms);
         }
-        if (on) {
-            if (wt)
-                __hip_atomic_store(gpw((unsigned long long*)G.fx_ssv) + o, d2bits(ssv), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-            else
-                G.fx_ssv[o] = ssv;
-        }
+        if (on) G.fx_ssv[o] = ssv;
     }
 }
 
@@ -2324,9 +2316,8 @@ __device__ __forceinline__ void tr_ssv_share(const GDev& G, int32_t lb, int cur,
 // agent-scope add, returned); the block whose ticket completes the iteration's count reads every
 // row with sc1 loads (MI355X_MICROARCH.md hand-off table, row 1: the last adder, told by the value
 // its add returned) and does k_fx_b's work for every op -- the same exact limb sums, the same
-// call-graph term (computed before the ticket by every block for its share of the ops,
-// tr_ssv_share, stored write-through and read here with the rows) and the same finish: bitwise
-// k_fx_b's results.
+// call-graph term (a lane per op of <= 8 parents, a wave per op of more: wave_sum's butterfly) and
+// the same finish: bitwise k_fx_b's results.
 template <int NT>
 __device__ __forceinline__ void tr_last_finish(const GDev& G, int it, double d, double Ms,
                                             GLB unsigned long long* Mnext) {
@@ -2344,7 +2335,10 @@ __device__ __forceinline__ void tr_last_finish(const GDev& G, int it, double d, 
     if (!s_last) return;
     const int32_t N = G.N, nb = G.n_fa, nxt = (it & 1) ^ 1;
     const GLB unsigned long long* rows = gp((const unsigned long long*)G.fx_part);
-    const GLB unsigned long long* ssvw = gp((const unsigned long long*)G.fx_ssv);
+    const GLB double* sp_cur = gp(G.spb[it & 1]);
+    const GLB int64_t* ss_off = gp(G.ss_off);
+    const GLB int32_t* ss_par = gp(G.ss_par);
+    const GLB float* pw = gp(G.pw);
     const GLB float* u_o = gp(G.u_o);
     const double iscale = G.dscale ? G.dscale[1] : G.fx_iscale;
     for (int32_t ob = wv * WAVE; ob < N; ob += NW * WAVE) {   // lane = op
@@ -2353,7 +2347,6 @@ __device__ __forceinline__ void tr_last_finish(const GDev& G, int it, double d, 
         unsigned long long lo = 0ull, hi = 0ull;
         // 16 rows per batch, every load in flight before the sums (indices clamped; repeats not added)
         const int32_t oc = on ? o : N - 1;
-        const double ssv = bits2d(__hip_atomic_load(ssvw + oc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
         for (int32_t b0 = 0; b0 < nb; b0 += 16) {
             unsigned long long v[16];
 #pragma unroll
@@ -2366,6 +2359,35 @@ __device__ __forceinline__ void tr_last_finish(const GDev& G, int it, double d, 
                     lo += v[k] & 0xffffffffull;
                     hi += v[k] >> 32;
                 }
+        }
+        double ssv = 0.0;
+        bool big = false;
+        if (on) {
+            const int64_t e0 = ss_off[o], e1 = ss_off[o + 1];
+            if (e1 - e0 <= 8) {
+                int32_t pp[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) pp[k] = e0 + k < e1 ? ss_par[e0 + k] : -1;
+                double t[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) t[k] = pp[k] >= 0 ? (double)pw[pp[k]] * sp_cur[pp[k]] : 0.0;
+                const double bb = ((t[0] + t[4]) + (t[2] + t[6])) + ((t[1] + t[5]) + (t[3] + t[7]));
+                ssv = G.alpha * (bb / Ms);
+            } else {
+                big = true;
+            }
+        }
+        for (uint64_t bm = __ballot(big); bm; bm &= bm - 1) {   // (wave-uniform)
+            const int j = __ffsll((unsigned long long)bm) - 1;
+            const int32_t oj = ob + j;
+            const int64_t e0 = ss_off[oj], e1 = ss_off[oj + 1];
+            double bb = 0.0;
+            for (int64_t e = e0 + lane; e < e1; e += WAVE) {
+                const int32_t pp = ss_par[e];
+                bb += (double)pw[pp] * sp_cur[pp];
+            }
+            bb = wave_sum(bb);
+            if (lane == j) ssv = G.alpha * (bb / Ms);
         }
         if (on) {
             const double sum = ((double)hi * 4294967296.0 + (double)lo) * iscale;
@@ -2426,7 +2448,7 @@ __global__ void __launch_bounds__(NT) k_tr_a(const GDev* __restrict__ gs, int32_
     const double xsc = (G.dscale ? G.dscale[0] : G.fx_scale) / msh[1], Ms = msh[0];
     const double rmax_w = tr_walk<Q, SUM, NT, EXT, HOTT>(G, lb, cur, nxt, N, NH, d, Ms, xsc, su_l, lacc, hs);
     // the call-graph terms of this block's share of the columns, by the waves done walking
-    if (G.ssv_pre || G.lastfin) tr_ssv_share(G, lb, cur, Ms, &s_ssv, tid & (WAVE - 1), G.lastfin != 0);
+    if (G.ssv_pre) tr_ssv_share(G, lb, cur, Ms, &s_ssv, tid & (WAVE - 1));
     __syncthreads();
     GLB unsigned long long* prow = gpw(G.fx_part) + (size_t)lb * N;
     if constexpr (NT == 512) {   // (window-graph variant only: the large graphs' kernel stays as it is)
