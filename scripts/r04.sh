@@ -5,6 +5,7 @@
 #   pc2     rocprofv3 kernel table of the timed c2 groups only (--no-side: no latency / kind / c4 legs)
 #   pc2ser  the same with one auxiliary stream and synchronous PageRank groups (kernels alone on the chip)
 #   c4sp    c4 from span shards at N=1 (build inside the step)
+#   pc3     rocprofv3 kernel table / trace of the timed c3 steps only
 #   w1      one C3 window per call under rocprofv3 --kernel-trace (scripts/win1_trace.py)
 #   c4      c4 line (traffic, CPU baseline)       pc4   rocprofv3 kernel table of the c4 command
 #   c4s8    c4 at N=1 holding rank 0's share of an 8-GPU deployment (per-rank compute at N=8)
@@ -51,6 +52,11 @@ if has w1; then   # one C3 window per call: host time, and the kernel trace spli
   timeout -k 10 300 rocprofv3 --kernel-trace -d gpurun_out/w1_$TAG -o run --output-format csv \
       -- python3 scripts/win1_trace.py 20 > gpurun_out/w1_$TAG.log 2>&1 || { echo "w1 failed"; tail -5 gpurun_out/w1_$TAG.log; exit 1; }
   grep "W=1" gpurun_out/w1_$TAG.log; python3 scripts/win1_trace.py --analyze gpurun_out/w1_$TAG/run_kernel_trace.csv | tail -4
+fi
+if has pc3; then   # kernel table + trace of the timed c3 steps only
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/pc3_$TAG -o run --output-format csv \
+      -- python3 bench.py --config c3 --no-traffic --no-cpu --no-side --steps 5 --warmup 1 > gpurun_out/pc3_$TAG.json 2> gpurun_out/pc3_$TAG.err || { echo "rocprof pc3 failed"; tail -5 gpurun_out/pc3_$TAG.err; exit 1; }
+  line gpurun_out/pc3_$TAG.json pc3
 fi
 if has c4; then
   timeout -k 10 600 python3 bench.py --config c4 --steps 5 --warmup 1 > gpurun_out/c4_$TAG.json 2> gpurun_out/c4_$TAG.err || { tail -5 gpurun_out/c4_$TAG.err; exit 1; }
