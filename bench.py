@@ -8,7 +8,7 @@ Workload (BASELINE.json configs[1], "C2"): RCA windows of 1k operations / 200k t
 faulty operation), fp64.  The span columns are generated, factorised and uploaded BEFORE the
 timed region; a window is ranked on the device: detector -> two graph builds (T1 swap) -> two
 25-iteration PageRanks -> DStar2 spectrum + top list.  A "step" ranks DISTINCT windows (own
-seed and span table each; 128 per step) with ONE mr_windows_batch call (their detectors / builds / spectra on
+seed and span table each; 256 per step) with ONE mr_windows_batch call (their detectors / builds / spectra on
 the library's auxiliary streams, the PageRanks of a group of windows sharing each iteration's
 launches).
 
@@ -520,7 +520,7 @@ def isolated_group_roofline(ctx, group, prec, reps=3):
             "bytes_per_launch": round(kbytes.value / max(launches.value, 1)),
             "what": f"one {len(group)}-window group per mr_windows_batch call (its builds done before its 25 iterations): "
                     "the iteration launches without concurrent builds; the line's frac is the same launches "
-                    "inside the timed 128-window calls, beside the next group's builds"}
+                    "inside the timed 256-window calls, beside the next group's builds"}
 
 
 def c4_leg_guarded(hg, world, rank, dist, line, limit_s=240.0):
@@ -942,9 +942,10 @@ def main():
     args = ap.parse_args()
     if args.streams is None:
         # c3: a 4096-window batch in calls of 256 (measured: 64 -> 7.7k, 256 -> 9.0k windows/s; a
-        # call's pipeline fill / drain amortised); c2: calls of 128 (r04: 128 vs 64 windows per call
-        # 5269 vs 4785 windows/s -- four 32-window PageRank groups per call instead of two)
-        args.streams = 8 if args.streams_mode else (256 if args.config == "c3" else 128)
+        # call's pipeline fill / drain amortised); c2: calls of 256 (r04: 64 / 128 / 256 windows per
+        # call 4785 / 5269 / 6005-6091 windows/s -- the first group's build and the last group's
+        # iterations, which nothing overlaps, spread over more windows; profiles/r04y)
+        args.streams = 8 if args.streams_mode else 256
     if args.precision is None:
         args.precision = "fp32" if args.config == "c5" else "fp64"
     if args.c4_ops is None:
