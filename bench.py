@@ -1033,9 +1033,12 @@ def main():
         a3, ok = slo_from_gpu(ctxs[0], normal)   # one SLO period; every table has the topology's codes
         for i, abnormal_i in enumerate(tabs):
             t0 = int(abnormal_i.tstart.min())
-            wins[0].append((DeviceSpans(ctxs[0], abnormal_i), t0, t0 + 5 * 60 * 10**9, a3, ok, abnormal_i))
-            if i:
-                tabs[i] = None   # host copy no longer needed (window 0's feeds the CPU baseline)
+            dev_i = DeviceSpans(ctxs[0], abnormal_i)
+            if i:   # host copy no longer needed (window 0's feeds the CPU baseline): ~140 MB a window
+                dev_i.table = None
+                tabs[i] = None
+            wins[0].append((dev_i, t0, t0 + 5 * 60 * 10**9, a3, ok, abnormal_i if i == 0 else None))
+            del abnormal_i
         abnormal, topo = tabs[0], None
         D = 0
     for d in range(D):
