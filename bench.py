@@ -941,11 +941,12 @@ def main():
                     help="c2: distinct seeded windows per step (default: every window of the step distinct)")
     args = ap.parse_args()
     if args.streams is None:
-        # c3: a 4096-window batch in calls of 256 (measured: 64 -> 7.7k, 256 -> 9.0k windows/s; a
-        # call's pipeline fill / drain amortised); c2: calls of 256 (r04: 64 / 128 / 256 windows per
-        # call 4785 / 5269 / 6005-6091 windows/s -- the first group's build and the last group's
-        # iterations, which nothing overlaps, spread over more windows; profiles/r04y)
-        args.streams = 8 if args.streams_mode else 256
+        # c3: a 4096-window batch in calls of 2048 (r04: 256 / 512 / 1024 / 2048 / 4096 windows per
+        # call 26.0-26.6k / 28.4-28.6k / 29.2-30.1k / 30.1k / 29.2-30.3k windows/s, profiles/r04aa);
+        # c2: calls of 256 (r04: 64 / 128 / 256 -> 4785 / 5269 / 6005-6091 windows/s, profiles/r04y)
+        # -- the first group's build and the last group's iterations, which nothing overlaps,
+        # spread over more windows
+        args.streams = 8 if args.streams_mode else (2048 if args.config == "c3" else 256)
     if args.precision is None:
         args.precision = "fp32" if args.config == "c5" else "fp64"
     if args.c4_ops is None:
