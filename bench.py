@@ -197,6 +197,8 @@ def pmc_traffic(args, timeout_s=240):
                 cmd += ["--config", args.config, "--c4-ops", str(args.c4_ops), "--c4-traces", str(args.c4_traces)]
             else:
                 cmd += ["--streams", str(args.streams), "--ops", str(args.ops), "--traces", str(args.traces)]
+                if args.config == "c2":   # (the same launches; 64 distinct windows cycled: less generation)
+                    cmd += ["--c2-distinct", "64"]
             try:
                 subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
                                timeout=timeout_s, check=True)
