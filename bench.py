@@ -497,7 +497,7 @@ def c4_leg_run(hg, world, rank, dist, steps=10, warmup=2):
 def isolated_group_roofline(ctx, group, prec, reps=3):
     """roofline.isolated: the timed line's iteration pair measured while builds of other windows run
     beside it on the auxiliary streams (the pipeline's contention included); here one call of ONE
-    group (c2: 64 windows), whose builds finish before its PageRanks start, so the group's
+    group (c2: 128 windows), whose builds finish before its PageRanks start, so the group's
     iterations run alone -- the kernel's own share of the HBM roofline."""
     import ctypes as C
 
@@ -1181,12 +1181,12 @@ def main():
                    "edges_per_window": int(edges // max(n_win, 1)),
                    "windows_per_step": (win_all // args.steps) if c3 else W,
                    "parallelism": (f"windows x{world} ranks, mr_windows_batch of {W} windows per call "
-                                   f"(the PageRanks of a group of windows -- up to 16M traces, 16..128 windows -- share each "
+                                   f"(the PageRanks of a group of windows -- up to 32M traces, 16..128 windows -- share each "
                                    f"iteration's launches)") if batch
                                   else f"windows x{world} ranks x{W} streams"},
         "windows_per_s": round(win_all / elapsed, 3),
         "roofline": {"bound": "hbm", "kernel": ("one Jacobi iteration of a window group's graphs: the "
-                                                "k_tr_a (+ k_fx_b) launch(es) over the graphs of one group (c2: 128 graphs of 64 "
+                                                "k_tr_a (+ k_fx_b) launch(es) over the graphs of one group (c2: 256 graphs of 128 "
                                                 "windows; c3: 256 graphs of 128, one launch per iteration: the last "
                                                 "block of each graph finishes it)") if batch else
                                                ("one Jacobi iteration: k_tr_a + k_fx_b (fused path)"
@@ -1218,9 +1218,9 @@ def main():
             dist.barrier()
             dist.destroy_process_group()
         return
-    if batch and args.config == "c2" and len(wins[0]) >= 64:
-        try:   # the same iteration kernel with nothing beside it: ONE 64-window group per call
-            out["roofline"]["isolated"] = isolated_group_roofline(ctx, wins[0][:64], prec)
+    if batch and args.config == "c2" and len(wins[0]) >= 128:
+        try:   # the same iteration kernel with nothing beside it: ONE 128-window group per call
+            out["roofline"]["isolated"] = isolated_group_roofline(ctx, wins[0][:128], prec)
         except Exception as e:  # a side metric never sinks the line
             out["roofline"]["isolated"] = {"error": f"{type(e).__name__}: {e}"}
     try:   # single-window latency: one window per mr_windows_batch call, nothing to overlap with

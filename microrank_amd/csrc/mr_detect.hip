@@ -668,11 +668,12 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
     // 9.4k / 12.1k / 14.8k / 15.4k windows/s with chunks of 8 at 128; C2, 200k-trace windows in
     // calls of 64: group 16 / 32 -> 4578 / 4773 windows/s, iteration frac 0.355 / 0.51, two
     // repeats each on one box; round 4, calls of 128: group 32 / 64 -> 5351-5363 / 5402-5433
-    // windows/s, in-pipeline iteration frac 0.39 / 0.46, `profiles/r04s/`).  A window's trace count
+    // windows/s, in-pipeline iteration frac 0.39 / 0.46, `profiles/r04s/`; calls of 256: group
+    // 64 / 128 -> 5780-5868 / 5795-5838 windows/s, frac 0.47 / 0.54, `profiles/r04ac/`).  A window's trace count
     // is bounded by its table's (a window of a long shared table gets the small group: the round-2
     // behaviour).  Chunks of 8 windows for small windows (C3), 4 for large (C2: 4 measured better).
     // MR_WIN_GROUP / MR_WIN_CHUNK: fixed group / chunk sizes (read per call)
-    constexpr int64_t WIN_GROUP_TRACES = (int64_t)16 << 20;
+    constexpr int64_t WIN_GROUP_TRACES = (int64_t)32 << 20;
     int64_t tsum_tab = 0;
     for (int32_t i = 0; i < n_windows; ++i) tsum_tab += std::max<int32_t>(spans[i]->n_traces, 1);
     const int64_t tper = std::max<int64_t>(1, tsum_tab / n_windows);
