@@ -6,6 +6,7 @@
 #   pc2ser  the same with one auxiliary stream and synchronous PageRank groups (kernels alone on the chip)
 #   c4sp    c4 from span shards at N=1 (build inside the step)
 #   pc3     rocprofv3 kernel table / trace of the timed c3 steps only
+#   dropin  the drop-in line (reference driver's window body through the swapped imports)
 #   w1      one C3 window per call under rocprofv3 --kernel-trace (scripts/win1_trace.py)
 #   c4      c4 line (traffic, CPU baseline)       pc4   rocprofv3 kernel table of the c4 command
 #   c4s8    c4 at N=1 holding rank 0's share of an 8-GPU deployment (per-rank compute at N=8)
@@ -57,6 +58,10 @@ if has pc3; then   # kernel table + trace of the timed c3 steps only
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/pc3_$TAG -o run --output-format csv \
       -- python3 bench.py --config c3 --no-traffic --no-cpu --no-side --steps 5 --warmup 1 > gpurun_out/pc3_$TAG.json 2> gpurun_out/pc3_$TAG.err || { echo "rocprof pc3 failed"; tail -5 gpurun_out/pc3_$TAG.err; exit 1; }
   line gpurun_out/pc3_$TAG.json pc3
+fi
+if has dropin; then   # the reference driver's window body through the drop-in modules (C1, C2)
+  timeout -k 10 600 python3 bench.py --config dropin > gpurun_out/dropin_$TAG.json 2> gpurun_out/dropin_$TAG.err || { tail -5 gpurun_out/dropin_$TAG.err; exit 1; }
+  python3 -c "import json;d=json.load(open('gpurun_out/dropin_$TAG.json'));c=d['config'];print('dropin C1', c['C1']['windows_per_s'], c['C1']['ms_per_window'], 'C2', c['C2']['windows_per_s'], c['C2']['ms_per_window'])"
 fi
 if has c4; then
   timeout -k 10 600 python3 bench.py --config c4 --steps 5 --warmup 1 > gpurun_out/c4_$TAG.json 2> gpurun_out/c4_$TAG.err || { tail -5 gpurun_out/c4_$TAG.err; exit 1; }
