@@ -277,11 +277,16 @@ __global__ void k_wide_cold_cnt(const int32_t* tperm, const int32_t* nc, int32_t
 }
 // cold entries in position order: op ids for k_cold_trace, and sort keys p << 24 | (op - range
 // base) << 8 | range whose one stable 8-bit pass groups them by range (positions stay ascending)
-__global__ void k_wide_cold_fill(const int32_t* tperm, const int64_t* off, const int32_t* ops, const int32_t* inv,
-                                 int32_t T, int32_t NA, int32_t RW, const int64_t* coff, int32_t* cops, uint64_t* key) {
-    const int32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= T) return;
-    const int32_t t = tperm[p];
+// walked in trace order: thread t reads its own op list (a wave's traces are contiguous in the
+// CSR) and writes its cold entries at its position's slots (tpos = inverse of tperm) -- walking
+// in position order read a random trace per lane, ~16 lines fetched per trace's 60 B (C5's rank
+// share: 21 GB of FETCH_SIZE in one 2.8 ms launch)
+__global__ void k_wide_cold_fill_t(const int32_t* tpos, const int64_t* off, const int32_t* ops, const int32_t* inv,
+                                   int32_t T, int32_t NA, int32_t RW, const int64_t* coff, int32_t* cops,
+                                   uint64_t* key) {
+    const int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= T) return;
+    const int32_t p = tpos[t];
     int64_t k = coff[p];
     for (int64_t e = off[t]; e < off[t + 1]; ++e) {
         const int32_t o = inv[ops[e]];
@@ -3444,8 +3449,14 @@ static int wide_prepare(mr_ctx* ctx, mr_graph* g) {
     {
         DBuf<uint64_t> ck;
         MR_TRY(ck.alloc(ctx, (size_t)n_cold + 1));
-        hipLaunchKernelGGL(k_wide_cold_fill, dim3(cdiv(T, 256)), dim3(256), 0, st, g->tperm.p, g->rs_off.p, g->rs_ops.p,
-                           inv.p, T, NA, RW, coff64.p, g->cold_ops_p.p, ck.p);
+        if (T && !g->tpos_ok) {   // (the inverse of this layout's tperm; the preference reuses it)
+            MR_TRY(g->tpos.alloc(ctx, (size_t)T));
+            hipLaunchKernelGGL(k_inv_perm, dim3(cdiv(T, 256)), dim3(256), 0, st, g->tperm.p, T, g->tpos.p);
+            g->tpos_ok = true;
+        }
+        if (T)
+            hipLaunchKernelGGL(k_wide_cold_fill_t, dim3(cdiv(T, 256)), dim3(256), 0, st, g->tpos.p, g->rs_off.p,
+                               g->rs_ops.p, inv.p, T, NA, RW, coff64.p, g->cold_ops_p.p, ck.p);
         SortScratch ws;
         MR_TRY(mr_radix_sort(ctx, ck.p, nullptr, n_cold, 8, ws));   // stable: positions stay ascending
         if (n_cold) {
