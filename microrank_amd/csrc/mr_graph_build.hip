@@ -475,6 +475,9 @@ __global__ void __launch_bounds__(NS_T) k_nodes_small2(const uint64_t* gk, int64
 
 // ---------------------------------------------------------------- indexed build (whole traces)
 constexpr int IX_EPT = 16;  // index entries per thread in k_ix_stats (fewer blocks: fewer global flushes)
+// ... and in the window batches' k_ix_stats2_b (C2, 256 windows per call: 16 / 64 -> 5752-5799 /
+// 5926-5996 windows/s, profiles/r04ag; within noise at 64 windows per call in round 3)
+constexpr int IX_EPT_BATCH = 64;
 // k_ix_stats: 16-wave blocks (one per CU) whose LDS holds the per-pod-op counts and first rows
 // of up to IX_HIST codes (128 KB) beside the edge set: the C4 graph's 10k ops aggregate in LDS
 // instead of a global atomic pair per index entry
@@ -2000,7 +2003,7 @@ int mr_ix_launch2_batch(mr_ctx* ctx, int n, const mr_spans* const* sps, uint8_t*
     IxBatch<IxWinSel> as{};
     IxBatch<IxWinStats> at{};
     const char* ee = getenv("MR_IX_EPT");   // (A/B knob, read per call)
-    const int ept = ee ? std::max(1, atoi(ee)) : IX_EPT;
+    const int ept = ee ? std::max(1, atoi(ee)) : IX_EPT_BATCH;
     IxBatch<IxWinCross> ac{};
     IxBatch<IxWinNodes> an{};
     IxBatch<IxWinTraces> ar{};
