@@ -1119,16 +1119,21 @@ __global__ void __launch_bounds__(KT_T) k_kp1_count(const KRec* rec, const int32
 }
 __global__ void __launch_bounds__(KT_T) k_kp1_scatter(const KRec* rec, const int32_t* nrec, int64_t R, int b1,
                                                       int32_t ntile, const int64_t* off, KRec* out, uint32_t* oslot) {
-    __shared__ unsigned long long cur[1 << KP1_B];
+    __shared__ int64_t base[1 << KP1_B];   // the (bucket, tile)'s first position, and 32-bit cursors after it
+    __shared__ uint32_t cur[1 << KP1_B];
     const int nbk = 1 << b1;
-    for (int i = threadIdx.x; i < nbk; i += KT_T) cur[i] = (unsigned long long)off[(int64_t)i * ntile + blockIdx.x];
+    for (int i = threadIdx.x; i < nbk; i += KT_T) {
+        base[i] = off[(int64_t)i * ntile + blockIdx.x];
+        cur[i] = 0u;
+    }
     __syncthreads();
     const int64_t s0 = (int64_t)blockIdx.x * KT;
     for (int k = 0; k < KT / KT_T; ++k) {
         const int64_t sl = s0 + k * KT_T + threadIdx.x;
         if (sl < R && (int32_t)(sl % KB) < nrec[sl / KB]) {
             const KRec v = rec[sl];
-            const int64_t pos = (int64_t)atomicAdd(&cur[kbits(v.h, b1)], 1ull);
+            const int b = kbits(v.h, b1);
+            const int64_t pos = base[b] + (int64_t)atomicAdd(&cur[b], 1u);
             out[pos] = v;
             oslot[pos] = (uint32_t)sl;
         }
@@ -1136,16 +1141,15 @@ __global__ void __launch_bounds__(KT_T) k_kp1_scatter(const KRec* rec, const int
 }
 __global__ void __launch_bounds__(KP2_T) k_kp2(const KRec* in, const uint32_t* islot, const int64_t* off, int pb,
                                                int b1, int32_t ntile, KRec* out, int32_t* rpos, int64_t* pstart) {
-    extern __shared__ int64_t kp2[];   // [nf] cursors, then [KP2_T] scan partials
+    extern __shared__ int64_t kp2[];   // [KP2_T] scan partials, then [nf] 32-bit counts / cursors (from B0)
     const int nf = 1 << (pb - b1), b = (int)blockIdx.x, tid = (int)threadIdx.x;
     const int64_t B0 = off[(int64_t)b * ntile], B1 = off[(int64_t)(b + 1) * ntile];
-    int64_t* cur = kp2;
-    int64_t* part = kp2 + nf;
-    for (int f = tid; f < nf; f += KP2_T) cur[f] = 0;
+    int64_t* part = kp2;
+    uint32_t* cur = (uint32_t*)(kp2 + KP2_T);
+    for (int f = tid; f < nf; f += KP2_T) cur[f] = 0u;
     __syncthreads();
     const uint64_t fm = (uint64_t)nf - 1;
-    for (int64_t i = B0 + tid; i < B1; i += KP2_T)
-        atomicAdd((unsigned long long*)&cur[(uint64_t)kbits(in[i].h, pb) & fm], 1ull);
+    for (int64_t i = B0 + tid; i < B1; i += KP2_T) atomicAdd(&cur[(uint64_t)kbits(in[i].h, pb) & fm], 1u);
     __syncthreads();
     // exclusive scan of the nf counts: a run of consecutive counts per thread, then its partials
     const int per = (nf + KP2_T - 1) / KP2_T, f0 = tid * per, f1 = min(f0 + per, nf);
@@ -1159,18 +1163,18 @@ __global__ void __launch_bounds__(KP2_T) k_kp2(const KRec* in, const uint32_t* i
         part[tid] += x;
         __syncthreads();
     }
-    int64_t run = B0 + part[tid] - a;
+    int64_t run = part[tid] - a;   // (relative to B0)
     for (int f = f0; f < f1; ++f) {
-        const int64_t c = cur[f];
-        cur[f] = run;
-        pstart[(int64_t)b * nf + f] = run;
+        const uint32_t c = cur[f];
+        cur[f] = (uint32_t)run;
+        pstart[(int64_t)b * nf + f] = B0 + run;
         run += c;
     }
     if (b == (int)gridDim.x - 1 && tid == 0) pstart[(int64_t)gridDim.x * nf] = B1;
     __syncthreads();
     for (int64_t i = B0 + tid; i < B1; i += KP2_T) {
         const KRec v = in[i];
-        const int64_t pos = (int64_t)atomicAdd((unsigned long long*)&cur[(uint64_t)kbits(v.h, pb) & fm], 1ull);
+        const int64_t pos = B0 + (int64_t)atomicAdd(&cur[(uint64_t)kbits(v.h, pb) & fm], 1u);
         out[pos] = v;
         rpos[islot[i]] = (int32_t)pos;
     }
@@ -4055,7 +4059,7 @@ static int graph_kinds(mr_ctx* ctx, mr_graph* g, bool chk, bool ktab, uint64_t c
             MR_TRY(mr_exclusive_scan_i32(ctx, tcnt.p, toff.p, nc, tmp.p));
             hipLaunchKernelGGL(k_kp1_scatter, dim3(ntile), dim3(KT_T), 0, st, rec.p, nrec.p, (int64_t)R, b1, ntile,
                                toff.p, r1.p, s1.p);
-            const size_t lds2 = ((size_t)nf + KP2_T) * sizeof(int64_t);
+            const size_t lds2 = (size_t)KP2_T * sizeof(int64_t) + (size_t)nf * sizeof(uint32_t);
             hipLaunchKernelGGL(k_kp2, dim3(nbk), dim3(KP2_T), lds2, st, r1.p, s1.p, toff.p, pb, b1, ntile, e.p, rpos.p,
                                pstart.p);
             MR_TRY_HIP(ctx, hipStreamSynchronize(st));   // (the level-1 buffers leave scope)
