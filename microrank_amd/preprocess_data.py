@@ -212,8 +212,8 @@ def _fingerprint(df: pd.DataFrame) -> _FrameSnapshot:
 
 
 def invalidate(df: pd.DataFrame) -> None:
-    """Drop the cached device span table of ``df`` (after in-place cell edits the cheap
-    fingerprint may not see); the next drop-in call rebuilds it."""
+    """Drop the cached device span table of ``df``; the next drop-in call rebuilds it.  Not needed
+    for correctness (every lookup compares the columns exactly); frees the device table early."""
     df.attrs["_mr_version"] = df.attrs.get("_mr_version", 0) + 1
     for k in [k for k in _CACHE if k[0] == id(df)]:
         _CACHE.pop(k, None)
