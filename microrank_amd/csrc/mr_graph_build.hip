@@ -475,9 +475,11 @@ __global__ void __launch_bounds__(NS_T) k_nodes_small2(const uint64_t* gk, int64
 
 // ---------------------------------------------------------------- indexed build (whole traces)
 constexpr int IX_EPT = 16;  // index entries per thread in k_ix_stats (fewer blocks: fewer global flushes)
-// ... and in the window batches' k_ix_stats2_b (C2, 256 windows per call: 16 / 64 -> 5752-5799 /
-// 5926-5996 windows/s, profiles/r04ag; within noise at 64 windows per call in round 3)
+// ... and in the window batches' k_ix_stats2_b for windows of >= IX_EPT_BIG index entries (C2's
+// 2.3M, 256 windows per call: 16 / 64 -> 5752-5799 / 5926-5996 windows/s, profiles/r04ag); small
+// windows (C3's 400k) keep 16: their blocks are few already
 constexpr int IX_EPT_BATCH = 64;
+constexpr int64_t IX_EPT_BIG = (int64_t)1 << 20;
 // k_ix_stats: 16-wave blocks (one per CU) whose LDS holds the per-pod-op counts and first rows
 // of up to IX_HIST codes (128 KB) beside the edge set: the C4 graph's 10k ops aggregate in LDS
 // instead of a global atomic pair per index entry
@@ -2003,7 +2005,7 @@ int mr_ix_launch2_batch(mr_ctx* ctx, int n, const mr_spans* const* sps, uint8_t*
     IxBatch<IxWinSel> as{};
     IxBatch<IxWinStats> at{};
     const char* ee = getenv("MR_IX_EPT");   // (A/B knob, read per call)
-    const int ept = ee ? std::max(1, atoi(ee)) : IX_EPT_BATCH;
+    const int ept = ee ? std::max(1, atoi(ee)) : IX_EPT;   // (MR_IX_EPT forces it for every window)
     IxBatch<IxWinCross> ac{};
     IxBatch<IxWinNodes> an{};
     IxBatch<IxWinTraces> ar{};
@@ -2060,7 +2062,9 @@ int mr_ix_launch2_batch(mr_ctx* ctx, int n, const mr_spans* const* sps, uint8_t*
         bs += nt;
         as.w[k] = IxWinSel{dets ? dets[k] : DetIn{}, d_states[k], sp->tlen.p, sp->po_off.p, nullptr, nek, NT, NP, xs};
         at.b0[k] = bt;
-        if (NT) bt += std::max(1, std::min(256, cdiv(std::max(sp->n_po, sp->n_ed), (int64_t)IX_BT * ept)));
+        const int64_t ne = std::max(sp->n_po, sp->n_ed);
+        const int ek = ee ? ept : ne >= IX_EPT_BIG ? IX_EPT_BATCH : IX_EPT;
+        if (NT) bt += std::max(1, std::min(256, cdiv(ne, (int64_t)IX_BT * ek)));
         lds = std::max(lds, 2 * (3 * (size_t)NP + (size_t)nek) * sizeof(int32_t));
         at.w[k] = IxWinStats{d_states[k], sp->po_tr.p, sp->po_op.p, sp->po_cnt.p, sp->po_first.p, sp->ed_tr.p, sp->ed_eid.p,
                              sp->ed_cnt.p, sp->n_po, sp->n_ed, NP, (int32_t)nek, xs};
