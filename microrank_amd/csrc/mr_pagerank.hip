@@ -1103,22 +1103,33 @@ constexpr int KT_T = 256;   // threads of a level-1 block
 constexpr int KP2_T = 1024;
 constexpr size_t KG_TWO_MAX = (size_t)1 << 25;   // record slots up to which the two-pass grouping runs
 __device__ __forceinline__ int32_t kbits(uint64_t h, int n) { return n ? (int32_t)(h >> (64 - n)) : 0; }
-__global__ void __launch_bounds__(KT_T) k_kp1_count(const KRec* rec, const int32_t* nrec, int64_t R, int b1,
-                                                    int32_t ntile, int32_t* cnt) {
+// (the three loops take KP_BATCH records per thread per round: loads first, then the LDS atomics
+// and stores -- one round's loads in flight together instead of one dependent chain per record)
+constexpr int KP_BATCH = 4;
+__global__ void __launch_bounds__(KT_T) k_kp1_count(const KRec* __restrict__ rec, const int32_t* __restrict__ nrec,
+                                                    int64_t R, int b1, int32_t ntile, int32_t* __restrict__ cnt) {
     __shared__ int32_t hb[1 << KP1_B];
     const int nbk = 1 << b1;
     for (int i = threadIdx.x; i < nbk; i += KT_T) hb[i] = 0;
     __syncthreads();
     const int64_t s0 = (int64_t)blockIdx.x * KT;
-    for (int k = 0; k < KT / KT_T; ++k) {
-        const int64_t sl = s0 + k * KT_T + threadIdx.x;
-        if (sl < R && (int32_t)(sl % KB) < nrec[sl / KB]) atomicAdd(&hb[kbits(rec[sl].h, b1)], 1);
+    for (int k0 = 0; k0 < KT / KT_T; k0 += KP_BATCH) {
+        int bk[KP_BATCH];
+#pragma unroll
+        for (int j = 0; j < KP_BATCH; ++j) {
+            const int64_t sl = s0 + (k0 + j) * KT_T + threadIdx.x;
+            bk[j] = sl < R && (int32_t)(sl % KB) < nrec[sl / KB] ? kbits(rec[sl].h, b1) : -1;
+        }
+#pragma unroll
+        for (int j = 0; j < KP_BATCH; ++j)
+            if (bk[j] >= 0) atomicAdd(&hb[bk[j]], 1);
     }
     __syncthreads();
     for (int i = threadIdx.x; i < nbk; i += KT_T) cnt[(int64_t)i * ntile + blockIdx.x] = hb[i];
 }
-__global__ void __launch_bounds__(KT_T) k_kp1_scatter(const KRec* rec, const int32_t* nrec, int64_t R, int b1,
-                                                      int32_t ntile, const int64_t* off, KRec* out, uint32_t* oslot) {
+__global__ void __launch_bounds__(KT_T) k_kp1_scatter(const KRec* __restrict__ rec, const int32_t* __restrict__ nrec,
+                                                      int64_t R, int b1, int32_t ntile, const int64_t* __restrict__ off,
+                                                      KRec* __restrict__ out, uint32_t* __restrict__ oslot) {
     __shared__ int64_t base[1 << KP1_B];   // the (bucket, tile)'s first position, and 32-bit cursors after it
     __shared__ uint32_t cur[1 << KP1_B];
     const int nbk = 1 << b1;
@@ -1128,19 +1139,29 @@ __global__ void __launch_bounds__(KT_T) k_kp1_scatter(const KRec* rec, const int
     }
     __syncthreads();
     const int64_t s0 = (int64_t)blockIdx.x * KT;
-    for (int k = 0; k < KT / KT_T; ++k) {
-        const int64_t sl = s0 + k * KT_T + threadIdx.x;
-        if (sl < R && (int32_t)(sl % KB) < nrec[sl / KB]) {
-            const KRec v = rec[sl];
-            const int b = kbits(v.h, b1);
+    for (int k0 = 0; k0 < KT / KT_T; k0 += KP_BATCH) {
+        KRec v[KP_BATCH];
+        bool ok[KP_BATCH];
+#pragma unroll
+        for (int j = 0; j < KP_BATCH; ++j) {
+            const int64_t sl = s0 + (k0 + j) * KT_T + threadIdx.x;
+            ok[j] = sl < R && (int32_t)(sl % KB) < nrec[sl / KB];
+            if (ok[j]) v[j] = rec[sl];
+        }
+#pragma unroll
+        for (int j = 0; j < KP_BATCH; ++j) {
+            if (!ok[j]) continue;
+            const int b = kbits(v[j].h, b1);
             const int64_t pos = base[b] + (int64_t)atomicAdd(&cur[b], 1u);
-            out[pos] = v;
-            oslot[pos] = (uint32_t)sl;
+            out[pos] = v[j];
+            oslot[pos] = (uint32_t)(s0 + (k0 + j) * KT_T + threadIdx.x);
         }
     }
 }
-__global__ void __launch_bounds__(KP2_T) k_kp2(const KRec* in, const uint32_t* islot, const int64_t* off, int pb,
-                                               int b1, int32_t ntile, KRec* out, int32_t* rpos, int64_t* pstart) {
+__global__ void __launch_bounds__(KP2_T) k_kp2(const KRec* __restrict__ in, const uint32_t* __restrict__ islot,
+                                               const int64_t* __restrict__ off, int pb, int b1, int32_t ntile,
+                                               KRec* __restrict__ out, int32_t* __restrict__ rpos,
+                                               int64_t* __restrict__ pstart) {
     extern __shared__ int64_t kp2[];   // [KP2_T] scan partials, then [nf] 32-bit counts / cursors (from B0)
     const int nf = 1 << (pb - b1), b = (int)blockIdx.x, tid = (int)threadIdx.x;
     const int64_t B0 = off[(int64_t)b * ntile], B1 = off[(int64_t)(b + 1) * ntile];
@@ -1149,7 +1170,17 @@ __global__ void __launch_bounds__(KP2_T) k_kp2(const KRec* in, const uint32_t* i
     for (int f = tid; f < nf; f += KP2_T) cur[f] = 0u;
     __syncthreads();
     const uint64_t fm = (uint64_t)nf - 1;
-    for (int64_t i = B0 + tid; i < B1; i += KP2_T) atomicAdd(&cur[(uint64_t)kbits(in[i].h, pb) & fm], 1u);
+    for (int64_t i0 = B0 + tid; i0 < B1; i0 += (int64_t)KP2_T * KP_BATCH) {
+        int fk[KP_BATCH];
+#pragma unroll
+        for (int j = 0; j < KP_BATCH; ++j) {
+            const int64_t i = i0 + (int64_t)j * KP2_T;
+            fk[j] = i < B1 ? (int)((uint64_t)kbits(in[i].h, pb) & fm) : -1;
+        }
+#pragma unroll
+        for (int j = 0; j < KP_BATCH; ++j)
+            if (fk[j] >= 0) atomicAdd(&cur[fk[j]], 1u);
+    }
     __syncthreads();
     // exclusive scan of the nf counts: a run of consecutive counts per thread, then its partials
     const int per = (nf + KP2_T - 1) / KP2_T, f0 = tid * per, f1 = min(f0 + per, nf);
@@ -1172,11 +1203,24 @@ __global__ void __launch_bounds__(KP2_T) k_kp2(const KRec* in, const uint32_t* i
     }
     if (b == (int)gridDim.x - 1 && tid == 0) pstart[(int64_t)gridDim.x * nf] = B1;
     __syncthreads();
-    for (int64_t i = B0 + tid; i < B1; i += KP2_T) {
-        const KRec v = in[i];
-        const int64_t pos = B0 + (int64_t)atomicAdd(&cur[(uint64_t)kbits(v.h, pb) & fm], 1u);
-        out[pos] = v;
-        rpos[islot[i]] = (int32_t)pos;
+    for (int64_t i0 = B0 + tid; i0 < B1; i0 += (int64_t)KP2_T * KP_BATCH) {
+        KRec v[KP_BATCH];
+        uint32_t sl[KP_BATCH];
+#pragma unroll
+        for (int j = 0; j < KP_BATCH; ++j) {
+            const int64_t i = i0 + (int64_t)j * KP2_T;
+            if (i < B1) {
+                v[j] = in[i];
+                sl[j] = islot[i];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < KP_BATCH; ++j) {
+            if (i0 + (int64_t)j * KP2_T >= B1) continue;
+            const int64_t pos = B0 + (int64_t)atomicAdd(&cur[(uint64_t)kbits(v[j].h, pb) & fm], 1u);
+            out[pos] = v[j];
+            rpos[sl[j]] = (int32_t)pos;
+        }
     }
 }
 __global__ void __launch_bounds__(KP_B) k_kind_part(const int64_t* pstart, KRec* e, int32_t* flag) {
