@@ -1234,31 +1234,48 @@ __global__ void __launch_bounds__(KP_B) k_kind_part(const int64_t* pstart, KRec*
         trep[i] = 0x7fffffff;
     }
     __syncthreads();
-    for (int64_t i = b + threadIdx.x; i < en; i += KP_B) {
-        const KRec v = e[i];
-        const uint64_t h = v.h;
-        int s = (int)(h & (KP_LDS - 1));
-        for (int probe = 0;; ++probe) {
-            if (probe == KP_LDS) {   // more distinct keys than slots: not with hashed partitions
-                atomicOr(flag + 2, 1);
-                break;
+    // (KP_BATCH records per thread per round: their loads go out together)
+    for (int64_t i0 = b + threadIdx.x; i0 < en; i0 += (int64_t)KP_B * KP_BATCH) {
+        KRec vv[KP_BATCH];
+#pragma unroll
+        for (int j = 0; j < KP_BATCH; ++j)
+            if (i0 + (int64_t)j * KP_B < en) vv[j] = e[i0 + (int64_t)j * KP_B];
+#pragma unroll
+        for (int j = 0; j < KP_BATCH; ++j) {
+            if (i0 + (int64_t)j * KP_B >= en) continue;
+            const KRec& v = vv[j];
+            const uint64_t h = v.h;
+            int s = (int)(h & (KP_LDS - 1));
+            for (int probe = 0;; ++probe) {
+                if (probe == KP_LDS) {   // more distinct keys than slots: not with hashed partitions
+                    atomicOr(flag + 2, 1);
+                    break;
+                }
+                const unsigned long long k = atomicCAS(&tkey[s], 0ull, (unsigned long long)h);
+                if (k == 0ull || k == h) {
+                    atomicAdd(&tcnt[s], v.c);
+                    atomicMin(&trep[s], v.r);   // the class's first trace (deterministic)
+                    break;
+                }
+                s = (s + 1) & (KP_LDS - 1);
             }
-            const unsigned long long k = atomicCAS(&tkey[s], 0ull, (unsigned long long)h);
-            if (k == 0ull || k == h) {
-                atomicAdd(&tcnt[s], v.c);
-                atomicMin(&trep[s], v.r);   // the class's first trace (deterministic)
-                break;
-            }
-            s = (s + 1) & (KP_LDS - 1);
         }
     }
     __syncthreads();
-    for (int64_t i = b + threadIdx.x; i < en; i += KP_B) {
-        const uint64_t h = e[i].h;
-        int s = (int)(h & (KP_LDS - 1));
-        for (int probe = 0; probe < KP_LDS && tkey[s] != h; ++probe) s = (s + 1) & (KP_LDS - 1);
-        if (tkey[s] != h) continue;   // (overflowed: flagged above)
-        *(uint2*)&e[i].c = make_uint2(tcnt[s], (uint32_t)trep[s]);   // (c, r): one 8-B store
+    for (int64_t i0 = b + threadIdx.x; i0 < en; i0 += (int64_t)KP_B * KP_BATCH) {
+        uint64_t hh[KP_BATCH];
+#pragma unroll
+        for (int j = 0; j < KP_BATCH; ++j) hh[j] = i0 + (int64_t)j * KP_B < en ? e[i0 + (int64_t)j * KP_B].h : 0ull;
+#pragma unroll
+        for (int j = 0; j < KP_BATCH; ++j) {
+            const int64_t i = i0 + (int64_t)j * KP_B;
+            if (i >= en) continue;
+            const uint64_t h = hh[j];
+            int s = (int)(h & (KP_LDS - 1));
+            for (int probe = 0; probe < KP_LDS && tkey[s] != h; ++probe) s = (s + 1) & (KP_LDS - 1);
+            if (tkey[s] != h) continue;   // (overflowed: flagged above)
+            *(uint2*)&e[i].c = make_uint2(tcnt[s], (uint32_t)trep[s]);   // (c, r): one 8-B store
+        }
     }
 }
 template <typename ID>
