@@ -662,85 +662,7 @@ __global__ void k_hot_perm(const int32_t* tperm, const uint8_t* mask, int32_t T,
     if (p < T) hmask[p] = mask[tperm[p]];
 }
 
-// Bank-conflict-aware order of a tile's ids (k_tr_a's LDS traffic).  Per step every lane reads
-// su[o] (ds_read_b64: lanes in groups of 32, 8-B slot o mod 32; equal addresses broadcast) and
-// adds into lacc[o] (u64 LDS atomic: groups of 16, slot o mod 16; equal addresses serialise).  A
-// trace's ops can be walked in any order, so per 32-lane half of a tile one thread assigns each
-// lane's items (ops and pads) to steps greedily: lane by lane, the first remaining item whose
-// atomic slot is free in its 16-lane group and whose read slot is free (or holds the same op) in
-// the half; else one clear for the atomic; else any.  Tiles longer than SCHED_L steps keep the
-// rotated order.
-constexpr int SCHED_T = 16, SCHED_L = 64;
-__global__ void __launch_bounds__(SCHED_T) k_tr_sched(const int32_t* coff, int32_t n_wt, uint16_t* tids) {
-    __shared__ uint16_t items_s[SCHED_T][32 * SCHED_L];
-    __shared__ unsigned long long rem_s[SCHED_T][32];
-    __shared__ uint16_t cbuf_s[SCHED_T][32 * 4];
-    const int64_t u = (int64_t)blockIdx.x * SCHED_T + threadIdx.x;
-    if (u >= 2 * (int64_t)n_wt) return;
-    uint16_t* items = items_s[threadIdx.x];
-    unsigned long long* rem = rem_s[threadIdx.x];
-    uint16_t* cbuf = cbuf_s[threadIdx.x];
-    const int32_t tile = (int32_t)(u >> 1), half = (int32_t)(u & 1);
-    const int32_t c0 = coff[tile], nc = coff[tile + 1] - c0, L = 4 * nc;
-    if (L > SCHED_L || nc <= 0) return;
-    unsigned long long* w = (unsigned long long*)tids + (size_t)c0 * WAVE + 32 * half;   // chunk c, lane li: w[c * WAVE + li]
-    for (int32_t c = 0; c < nc; ++c)
-        for (int li = 0; li < 32; ++li) {
-            const unsigned long long v = w[(size_t)c * WAVE + li];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) items[li * SCHED_L + 4 * c + q] = (uint16_t)(v >> (16 * q));
-        }
-    const unsigned long long full = L == 64 ? ~0ull : ((1ull << L) - 1ull);
-    for (int li = 0; li < 32; ++li) rem[li] = full;
-    for (int32_t s = 0; s < L; ++s) {
-        uint32_t used16[2] = {0u, 0u};
-        uint32_t occ32 = 0u;             // read slots taken this step ...
-        uint16_t op32[32];               // ... and by which op (a broadcast when equal)
-        for (int li = 0; li < 32; ++li) {
-            const int g = li >> 4;
-            const uint16_t* it = items + li * SCHED_L;
-            unsigned long long m = rem[li];
-            int best = -1, best_sc = 4;
-            while (m) {
-                const int j = __builtin_ctzll(m);
-                m &= m - 1ull;
-                const uint32_t o = it[j];
-                const uint32_t b16 = o & 15u, b32 = o & 31u;
-                const int sc = (int)((used16[g] >> b16) & 1u) * 2 + (int)(((occ32 >> b32) & 1u) && op32[b32] != o);
-                if (sc < best_sc) {
-                    best_sc = sc;
-                    best = j;
-                    if (sc == 0) break;
-                }
-            }
-            const uint32_t o = it[best];
-            rem[li] &= ~(1ull << best);
-            used16[g] |= 1u << (o & 15u);
-            if (!((occ32 >> (o & 31u)) & 1u)) {
-                occ32 |= 1u << (o & 31u);
-                op32[o & 31u] = (uint16_t)o;
-            }
-            cbuf[li * 4 + (s & 3)] = (uint16_t)o;
-        }
-        if ((s & 3) == 3)
-            for (int li = 0; li < 32; ++li) {
-                unsigned long long v = 0ull;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) v |= (unsigned long long)cbuf[li * 4 + q] << (16 * q);
-                w[(size_t)(s >> 2) * WAVE + li] = v;
-            }
-    }
-}
-// MR_TR_SCHED=1: the greedy order (on the stable radix layout, so a graph's tiles -- hence each
-// trace's summation order -- are the same every time it is prepared).  Off by default: on C4 it
-// gains 2 % per iteration (142.5 -> 139.8 us) but costs 41 ms per preparation (one thread per
-// half tile), and most graphs are ranked once (the driver builds two per window).
 constexpr int64_t TR_LARGE = (int64_t)1 << 20;   // "large graph": the hot-op threshold
-static bool tr_sched_on(int64_t T) {
-    (void)T;
-    const char* e = getenv("MR_TR_SCHED");   // (read per preparation: tests flip it)
-    return e && !strcmp(e, "1");
-}
 
 // The prepare of several small fused graphs (a window's two) in one launch per step: block ranges
 // per graph, the same bodies (mr_graph_prepare_batch)
@@ -3380,8 +3302,7 @@ static int tr_layout(mr_ctx* ctx, mr_graph* g, const int64_t* off, const uint16_
     // (length, secondary key): a stable radix sort, equal keys in trace order -- for wide graphs (the
     // cold count as secondary key) and kind-compressed ones, whose fixed-point scale depends on
     // the tiles' multiplicity sums (the counting sort below orders equal lengths run-dependently)
-    const bool sched = tr_sched_on(T);
-    if (T && (skey || g->kinds_given || sched)) {
+    if (T && (skey || g->kinds_given)) {
         DBuf<uint64_t> key;
         DBuf<uint32_t> val;
         MR_TRY(key.alloc(ctx, (size_t)T));
@@ -3425,8 +3346,6 @@ static int tr_layout(mr_ctx* ctx, mr_graph* g, const int64_t* off, const uint16_
     if (W)
         hipLaunchKernelGGL(k_tr_fill, dim3(cdiv((int64_t)W * WAVE, 256)), dim3(256), 0, st, g->tperm.p, off, src,
                            c64.p, T, N, W, g->tids.p);
-    if (W && sched)
-        hipLaunchKernelGGL(k_tr_sched, dim3(cdiv(2 * (int64_t)W, SCHED_T)), dim3(SCHED_T), 0, st, g->coff.p, W, g->tids.p);
     if (g->nhr) {   // the hot-op bits in position order
         MR_TRY(g->hmask.alloc(ctx, (size_t)T));
         hipLaunchKernelGGL(k_hot_perm, dim3(cdiv(T, 256)), dim3(256), 0, st, g->tperm.p, hm.p, T, g->hmask.p);
