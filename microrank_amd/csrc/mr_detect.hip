@@ -696,7 +696,12 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
         for (int32_t i = gbeg[(size_t)g], e = gbeg[(size_t)g + 1]; i < e; i += chunk_size)
             chunks.emplace_back(i, std::min<int32_t>(e, i + chunk_size));
     const int nthr = std::min<int>((int)chunks.size(), max_streams);
-    MR_TRY(win_aux(ctx, nthr));
+    // MR_WIN_PR_STREAMS=2: odd groups' PageRanks on a second context (its own stream, pool and
+    // scratch: aux[nthr]), so one group's latency-bound iterations overlap the next group's
+    const char* pse = getenv("MR_WIN_PR_STREAMS");   // (A/B, read per call)
+    const int npr = pse && atoi(pse) >= 2 && ngroups >= 2 ? 2 : 1;
+    MR_TRY(win_aux(ctx, nthr + (npr > 1)));
+    auto pr_ctx = [&](int g) -> mr_ctx* { return npr > 1 && (g & 1) ? ctx->aux[(size_t)nthr] : ctx; };
     // the SLO vectors once per distinct (a3, a3_valid, length) of the batch (windows usually share
     // one pair), resident before any window's detector runs
     std::unique_ptr<WinPhase> ph_setup(new WinPhase(8));
@@ -845,21 +850,23 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
     std::vector<std::vector<int>> gan((size_t)ngroups);
     auto record = [&](int g) -> int {
         if (!gev[(size_t)g] && hipEventCreateWithFlags(&gev[(size_t)g], hipEventDisableTiming) != hipSuccess) return MR_ERR_HIP;
-        return hipEventRecord(gev[(size_t)g], ctx->stream) == hipSuccess ? MR_OK : MR_ERR_HIP;
+        return hipEventRecord(gev[(size_t)g], pr_ctx(g)->stream) == hipSuccess ? MR_OK : MR_ERR_HIP;
     };
     // group g's results are final: check its words (rerun on a collision) and queue its spectra
     auto settle = [&](int g) -> int {
         int r = MR_OK;
         if (pend[(size_t)g]) {
+            mr_ctx* pc = pr_ctx(g);
             bool rerun = false;
-            r = mr_pagerank_async_finish(ctx, pend[(size_t)g], &rerun);
+            r = mr_pagerank_async_finish(pc, pend[(size_t)g], &rerun);
             mr_pagerank_async_free(pend[(size_t)g]);
             pend[(size_t)g] = nullptr;
             if (r == MR_OK && rerun) {
-                r = mr_pagerank_batch(ctx, ggs[(size_t)g].data(), gan[(size_t)g].data(), (int)ggs[(size_t)g].size(), 0.85,
+                r = mr_pagerank_batch(pc, ggs[(size_t)g].data(), gan[(size_t)g].data(), (int)ggs[(size_t)g].size(), 0.85,
                                       0.01, 25, precision, 0);
                 if (r == MR_OK) r = record(g);
             }
+            if (r != MR_OK && pc != ctx) ctx->err = pc->err;
         }
         const int32_t i0 = gbeg[(size_t)g], i1 = gbeg[(size_t)g + 1];
         std::lock_guard<std::mutex> lk(mu);
@@ -886,9 +893,10 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
             WinPhase ph(5);
             cv_done.wait(lk, [&] { return built[(size_t)g] == i1 - i0; });
         }
+        mr_ctx* pc = pr_ctx(g);
         for (size_t c = 0; c < chunks.size(); ++c)   // the group's chunks' graphs are ready
             if (chunks[c].first >= i0 && chunks[c].first < i1 && cw[c].ev &&
-                hipStreamWaitEvent(ctx->stream, cw[c].ev, 0) != hipSuccess)
+                hipStreamWaitEvent(pc->stream, cw[c].ev, 0) != hipSuccess)
                 rc = mr_fail(ctx, MR_ERR_HIP, "mr_windows_batch: hipStreamWaitEvent failed");   // (threads joined below)
         if (rc != MR_OK) break;
         std::vector<mr_graph*>& gs = ggs[(size_t)g];
@@ -897,7 +905,7 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
             WinRun& r = w[(size_t)i];
             n_out[i] = 0;
             if (r.rc == MR_OK && r.gn) {
-                r.gn->ctx = r.ga->ctx = ctx;   // (built on an auxiliary context)
+                r.gn->ctx = r.ga->ctx = pc;   // (built on an auxiliary context)
                 gs.push_back(r.gn);
                 gs.push_back(r.ga);
                 anom.push_back(0);
@@ -907,17 +915,21 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
         if (!gs.empty()) {
             WinPhase ph(6);
             if (pr_sync)
-                rc = mr_pagerank_batch(ctx, gs.data(), anom.data(), (int)gs.size(), 0.85, 0.01, 25, precision, 0);
+                rc = mr_pagerank_batch(pc, gs.data(), anom.data(), (int)gs.size(), 0.85, 0.01, 25, precision, 0);
             else
-                rc = mr_pagerank_batch_async(ctx, gs.data(), anom.data(), (int)gs.size(), 0.85, 0.01, 25, precision,
+                rc = mr_pagerank_batch_async(pc, gs.data(), anom.data(), (int)gs.size(), 0.85, 0.01, 25, precision,
                                              ctx->pin_flags + (size_t)8 * i0, &pend[(size_t)g]);
+            if (rc != MR_OK && pc != ctx) ctx->err = pc->err;
         }
         if (rc == MR_OK) rc = record(g);
         // the previous group's words are in by now, or nearly: settle it (this one stays in flight)
         for (; rc == MR_OK && settled < (pr_sync ? g + 1 : g); ++settled) rc = settle(settled);
     }
     for (; rc == MR_OK && settled < ngroups; ++settled) rc = settle(settled);
-    if (rc != MR_OK) (void)hipStreamSynchronize(ctx->stream);   // (an error left groups in flight)
+    if (rc != MR_OK) {   // (an error left groups in flight)
+        (void)hipStreamSynchronize(ctx->stream);
+        if (npr > 1) (void)hipStreamSynchronize(ctx->aux[(size_t)nthr]->stream);
+    }
     for (PrAsync* a : pend)
         if (a) mr_pagerank_async_free(a);
     {
@@ -932,6 +944,7 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
     // (an error may leave PageRank work queued on the main stream that still reads window graphs
     // whose blocks return to the worker pools below: drain it first)
     (void)hipStreamSynchronize(ctx->stream);
+    if (npr > 1) (void)hipStreamSynchronize(ctx->aux[(size_t)nthr]->stream);
     for (hipEvent_t e : gev)
         if (e) (void)hipEventDestroy(e);
     MR_TRY(rc);

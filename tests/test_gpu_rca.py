@@ -616,6 +616,42 @@ def test_windows_batch_fast_paths_equal_general_paths(c3_window, monkeypatch):
         d.close()
 
 
+def test_windows_batch_second_pagerank_stream(c3_window, monkeypatch):
+    """MR_WIN_PR_STREAMS=2: odd window groups ranked on a second context (its own stream, pool and
+    scratch) give bitwise the results of one PageRank stream -- groups of one and two windows, two
+    calls on one context (the second reuses the first call's contexts)."""
+    import bench
+    from microrank_amd import _lib
+    from microrank_amd.online_rca import rank_windows
+    from microrank_amd.preprocess_data import DeviceSpans
+
+    ctx = _lib.default_context()
+    normal, abnormal, t0, t1 = c3_window
+    a3, ok = bench.slo_from_gpu(ctx, normal)
+    devs = [DeviceSpans(ctx, abnormal)]
+    wins = [(devs[0], t0, t1, a3, ok)]
+    for seed in (94, 95, 96, 97, 98):
+        _, nrm, ab = bench.make_window(seed, 500, 20_000)
+        s3, sok = bench.slo_from_gpu(ctx, nrm)
+        d = DeviceSpans(ctx, ab)
+        devs.append(d)
+        u0 = int(ab.tstart.min())
+        wins.append((d, u0, u0 + 5 * 60 * 10**9, s3, sok))
+    runs = {}
+    for group in ("1", "2"):
+        monkeypatch.setenv("MR_WIN_GROUP", group)
+        for ns in ("1", "2"):
+            monkeypatch.setenv("MR_WIN_PR_STREAMS", ns)
+            runs[(group, ns)] = rank_windows(ctx, wins) + rank_windows(ctx, wins[::-1])
+    base = runs[("1", "1")]
+    for key, got in runs.items():
+        for a, b in zip(base, got):
+            assert a[5] == b[5] == 0, key
+            assert a[2:] == b[2:] and list(a[0]) == list(b[0]) and a[1].tobytes() == b[1].tobytes(), key
+    for d in devs:
+        d.close()
+
+
 @pytest.mark.parametrize("name,minutes,device_append", [("stream", 7, True), ("stream", 3, True),
                                                          ("stream_gap", 7, True), ("stream", 7, False),
                                                          ("stream_gap", 3, False)])
