@@ -4173,8 +4173,6 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         MR_TRY_HIP(ctx, hipStreamSynchronize(st));
     }
     // ---- batched power iteration: one k_iter_a + k_iter_b pair per iteration for every graph
-    int mask = 3;
-    if (const char* rm = getenv("MR_ROLE_MASK")) mask = atoi(rm);   // profiling knob: 1 trace / 2 op side
     std::vector<GDev> hv((size_t)ng);
     int64_t fb16 = 0;   // k_fx_b blocks of the launch at 16 ops per block
     for (int i = 0; i < ng; ++i)
@@ -4304,12 +4302,12 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         if (g->fused) {
             continue;   // no tile-path blocks (n_tb = n_tiles = n_ob = 0)
         }
-        v.n_tb = (mask & 1) ? std::max(cdiv(g->T, TB), sharded ? 1 : 0) : 0;   // (empty shard: see nfa)
-        v.n_tiles = (mask & 2) ? g->n_tiles : 0;
+        v.n_tb = std::max(cdiv(g->T, TB), sharded ? 1 : 0);   // (empty shard: see nfa)
+        v.n_tiles = g->n_tiles;
         v.tshift = g->tshift;
         v.lds_su = g->N <= LDS_NODES;
         blocks_a += v.n_tb + v.n_tiles;
-        v.n_ob = (mask & 2) ? cdiv(g->N, TB / WAVE) : 0;
+        v.n_ob = cdiv(g->N, TB / WAVE);
         blocks_b += v.n_ob;
         if (v.lds_su) lds = std::max(lds, ((size_t)g->N + VCAP) * sizeof(double));
         lds = std::max(lds, ((size_t)1 << g->tshift) * (fp32 ? sizeof(float) : sizeof(double)));
