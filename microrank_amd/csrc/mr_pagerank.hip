@@ -583,21 +583,23 @@ __device__ __forceinline__ void tr_fill_body(int32_t blk, const int32_t* tperm, 
     }
     const int64_t nc = c64[k + 1] - c64[k];
     unsigned long long* dst = (unsigned long long*)tids + (size_t)c64[k] * WAVE + lane;   // 4 ids per 8-B store
-    // the ids from the rotation start, padded with N + lane
-    int64_t jj = rot;
-    for (int64_t c = 0; c < nc; ++c) {
-        unsigned long long v = 0ull;
+    // the ids from the rotation start, padded with N + lane; TF_CH chunks per round, their loads
+    // issued together (id e of the rotation sits at (rot + e) mod len: no carried index), so a
+    // window trace of <= 16 ids costs one load latency instead of one per chunk
+    constexpr int TF_CH = 4;
+    for (int64_t c0 = 0; c0 < nc; c0 += TF_CH) {
+        uint16_t idv[4 * TF_CH];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int64_t e = 4 * c + q;
-            uint16_t id = (uint16_t)(N + lane);
-            if (e < len) {
-                id = ids[a + jj];
-                if (++jj == len) jj = 0;
-            }
-            v |= (unsigned long long)id << (16 * q);
+        for (int q = 0; q < 4 * TF_CH; ++q) {
+            const int64_t e = 4 * c0 + q, jx = rot + e;
+            idv[q] = e < len ? ids[a + (jx >= len ? jx - len : jx)] : (uint16_t)(N + lane);
         }
-        dst[(size_t)c * WAVE] = v;
+#pragma unroll
+        for (int u = 0; u < TF_CH; ++u)
+            if (c0 + u < nc)
+                dst[(size_t)(c0 + u) * WAVE] = (unsigned long long)idv[4 * u] | (unsigned long long)idv[4 * u + 1] << 16 |
+                                               (unsigned long long)idv[4 * u + 2] << 32 |
+                                               (unsigned long long)idv[4 * u + 3] << 48;
     }
 }
 __global__ void k_tr_fill(const int32_t* tperm, const int64_t* off, const uint16_t* ids, const int64_t* c64, int32_t T,

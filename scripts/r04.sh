@@ -115,8 +115,9 @@ if has c3ab || has c2ab; then
     has ${cfg}ab || continue
     for rep in 1 2; do
       for v in $AB_VALS; do
-        env $AB_VAR=$v timeout -k 10 400 python3 bench.py --config $cfg --no-traffic --no-cpu --no-c4-leg > gpurun_out/ab_${cfg}_${TAG}_${v}_$rep.json 2> gpurun_out/ab_${cfg}_${TAG}_${v}_$rep.err || { tail -5 gpurun_out/ab_${cfg}_${TAG}_${v}_$rep.err; exit 1; }
-        line gpurun_out/ab_${cfg}_${TAG}_${v}_$rep.json "$cfg $AB_VAR=$v rep $rep"
+        vn=$(basename "$v")   # (a library path as the value: MR_LIB_PATH)
+        env $AB_VAR=$v timeout -k 10 400 python3 bench.py --config $cfg --no-traffic --no-cpu --no-c4-leg > gpurun_out/ab_${cfg}_${TAG}_${vn}_$rep.json 2> gpurun_out/ab_${cfg}_${TAG}_${vn}_$rep.err || { tail -5 gpurun_out/ab_${cfg}_${TAG}_${vn}_$rep.err; exit 1; }
+        line gpurun_out/ab_${cfg}_${TAG}_${vn}_$rep.json "$cfg $AB_VAR=$vn rep $rep"
       done
     done
   done
