@@ -887,6 +887,7 @@ __device__ __forceinline__ void ix_sel_scan2_body(const uint8_t* state, const in
                                                        int32_t NP, int64_t ecap, int32_t blk_, int32_t nblk_) {
     __shared__ int64_t sa[4][SEL_T];
     __shared__ int64_t ex[4];
+    __shared__ int64_t so[SEL_TILE];   // the tile's outputs, staged for coalesced stores
     const int tid = threadIdx.x;
     const int64_t gsz = (int64_t)nblk_ * SEL_T, gi = (int64_t)blk_ * SEL_T + tid;
     for (int64_t i = gi; i < max((int64_t)NP, ecap); i += gsz)
@@ -899,7 +900,7 @@ __device__ __forceinline__ void ix_sel_scan2_body(const uint8_t* state, const in
             }
             if (i < ecap) x.g[g].gc[i] = 0u;
         }
-    const int64_t tile = blk_, base = tile * SEL_TILE + (int64_t)tid * SEL_I;
+    const int64_t tile = blk_, t0 = tile * SEL_TILE, base = t0 + (int64_t)tid * SEL_I;
     int8_t sd[SEL_I];
     int64_t z[SEL_I], acc[4] = {0, 0, 0, 0};
 #pragma unroll
@@ -908,10 +909,6 @@ __device__ __forceinline__ void ix_sel_scan2_body(const uint8_t* state, const in
         const int s_ = t < NT && tlen[t] > 0 ? side_of(state[t]) : -1;
         sd[i] = (int8_t)s_;
         z[i] = s_ >= 0 ? po_off[t + 1] - po_off[t] : 0;
-        if (t < NT) {
-            x.g[0].tflag[t] = s_ == 0;
-            x.g[1].tflag[t] = s_ == 1;
-        }
         if (s_ >= 0) {
             acc[2 * s_] += 1;
             acc[2 * s_ + 1] += z[i];
@@ -942,21 +939,40 @@ __device__ __forceinline__ void ix_sel_scan2_body(const uint8_t* state, const in
         }
     }
     __syncthreads();
-    int64_t r[4];
+    // A thread's SEL_I values are consecutive traces: stored directly, each store instruction would
+    // write 8 B into each of 64 lines (measured: 117 MB of WRITE_SIZE per 4-window chunk for 32 MB of
+    // values); staged through LDS, every store is a coalesced run.  (Values of the graph a trace is
+    // not in are never read.)
+    int32_t* so32 = reinterpret_cast<int32_t*>(so);
 #pragma unroll
-    for (int c = 0; c < 4; ++c) r[c] = ex[c] + sa[c][tid] - acc[c];
+    for (int i = 0; i < SEL_I; ++i) {   // both graphs' trace flags: halves of the stage
+        so32[tid * SEL_I + i] = sd[i] == 0;
+        so32[SEL_TILE + tid * SEL_I + i] = sd[i] == 1;
+    }
+    __syncthreads();
 #pragma unroll
-    for (int i = 0; i < SEL_I; ++i) {
-        const int64_t t = base + i;
-        if (t < NT) {   // (values of the graph the trace is not in are never read)
-            x.g[0].tpos[t] = r[0];
-            x.g[0].zoff[t] = r[1];
-            x.g[1].tpos[t] = r[2];
-            x.g[1].zoff[t] = r[3];
+    for (int k = 0; k < SEL_I; ++k) {
+        const int j = k * SEL_T + tid;
+        if (t0 + j < NT) {
+            x.g[0].tflag[t0 + j] = so32[j];
+            x.g[1].tflag[t0 + j] = so32[SEL_TILE + j];
         }
-        if (sd[i] >= 0) {
-            r[2 * sd[i]] += 1;
-            r[2 * sd[i] + 1] += z[i];
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {   // c: graph c / 2, tpos (even) or zoff (odd)
+        int64_t run = ex[c] + sa[c][tid] - acc[c];
+        __syncthreads();   // (the previous round's stage has been read)
+#pragma unroll
+        for (int i = 0; i < SEL_I; ++i) {
+            so[tid * SEL_I + i] = run;
+            if (sd[i] == (c >> 1)) run += (c & 1) ? z[i] : 1;
+        }
+        __syncthreads();
+        int64_t* dst = (c & 1) ? x.g[c >> 1].zoff : x.g[c >> 1].tpos;
+#pragma unroll
+        for (int k = 0; k < SEL_I; ++k) {
+            const int j = k * SEL_T + tid;
+            if (t0 + j < NT) dst[t0 + j] = so[j];
         }
     }
 }
