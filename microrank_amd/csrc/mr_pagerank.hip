@@ -394,7 +394,7 @@ constexpr int TP_LSCAN = 8192;
 template <int TR_PER>
 __device__ __forceinline__ void tr_place_body(int32_t blk, const int64_t* off, int32_t T, int32_t nbin,
                                               const int64_t* boff, int32_t* hist, int32_t* taken, const float* w_t,
-                                              int32_t* tperm, float* w_tp) {
+                                              int32_t* tperm, float* w_tp, int32_t* tpos) {
     extern __shared__ int32_t lh[];
     int32_t* lbase = lh + nbin;
     for (int32_t i = threadIdx.x; i < nbin; i += TRB) lh[i] = 0;
@@ -439,13 +439,14 @@ __device__ __forceinline__ void tr_place_body(int32_t blk, const int64_t* off, i
         const int32_t p = lbase[ln[j]] + rk[j];
         tperm[p] = t;
         w_tp[p] = w_t[t];
+        if (tpos) tpos[t] = p;   // (the inverse, stored in trace order)
     }
 }
 template <int TR_PER>
 __global__ void __launch_bounds__(TRB) k_tr_place(const int64_t* off, int32_t T, int32_t nbin, const int64_t* boff,
                                                   int32_t* hist, int32_t* taken, const float* w_t, int32_t* tperm,
                                                   float* w_tp) {
-    tr_place_body<TR_PER>((int32_t)blockIdx.x, off, T, nbin, boff, hist, taken, w_t, tperm, w_tp);
+    tr_place_body<TR_PER>((int32_t)blockIdx.x, off, T, nbin, boff, hist, taken, w_t, tperm, w_tp, nullptr);
 }
 // chunks of 4 ids per wave tile (its last position holds its longest trace: lengths ascend), their
 // exclusive prefix and its int32 copy in one launch: runs of TS_TILE wave tiles per block, chained
@@ -676,7 +677,7 @@ struct PDev {
     const int64_t* rs_off;
     float *w_t, *u_o, *pw, *w_tp;
     uint16_t *rs16, *tids;
-    int32_t *trz, *tperm, *coff;
+    int32_t *trz, *tperm, *coff, *tpos;
     int64_t* c64;
 };
 __device__ __forceinline__ int32_t pd_graph(const PDev* pd, int32_t n, int32_t blk, int which) {
@@ -701,7 +702,7 @@ __global__ void __launch_bounds__(TRB) k_tr_hist_b(const PDev* __restrict__ pd, 
 __global__ void __launch_bounds__(TRB) k_tr_place_b(const PDev* __restrict__ pd, int32_t n) {
     const PDev& G = pd[pd_graph(pd, n, (int32_t)blockIdx.x, 1)];
     tr_place_body<TR_PER_SMALL>((int32_t)blockIdx.x - G.b_th, G.rs_off, G.T, G.nbin, nullptr, G.trz, G.trz + G.nbin,
-                                G.w_t, G.tperm, G.w_tp);
+                                G.w_t, G.tperm, G.w_tp, G.tpos);
 }
 __global__ void __launch_bounds__(TS_T) k_tr_chunk_scan_b(const PDev* __restrict__ pd, int32_t n, unsigned long long* st,
                                                          uint64_t epoch) {
@@ -1385,7 +1386,7 @@ struct SDev {
     double phi;                                 // the anomaly preference's 0.5 (pagerank.py:82-84)
     int32_t b_reset, b_kins, b_kver, b_pref;   // the graph's first block in each launch
     float *pref, *c_t, *c_tp;
-    const int32_t* tperm;
+    const int32_t *tperm, *tpos;
     unsigned long long* hk;
     KCnt* cr;
     int32_t *slot_of, *flag;
@@ -1490,11 +1491,13 @@ __global__ void k_pref_total_b(const SDev* __restrict__ sd) {   // block g: grap
         G.scal[3] = b;
     }
 }
+// in trace order (as k_pref_apply_t): the per-trace reads and writes are coalesced, the one
+// scattered store is c_tp at the trace's position (tpos, the inverse of tperm)
 __global__ void k_pref_apply_b(const SDev* __restrict__ sd, int32_t ng) {
     const SDev& G = sd[sd_graph(sd, ng, (int32_t)blockIdx.x, 3)];
-    const int32_t i = ((int32_t)blockIdx.x - G.b_pref) * blockDim.x + threadIdx.x;   // position
-    if (i >= G.T) return;
-    const int32_t t = G.tperm[i];
+    const int32_t t = ((int32_t)blockIdx.x - G.b_pref) * blockDim.x + threadIdx.x;
+    if (t >= G.T) return;
+    const int32_t i = G.tpos[t];
     const double k = G.kind[t];
     double v;
     if (!G.anomaly) v = 1.0 / k / G.scal[2];                                               // :74
@@ -3553,7 +3556,8 @@ int mr_graph_prepare_batch(mr_ctx* ctx, mr_graph* const* gs, int n, std::vector<
         MR_TRY(trz[(size_t)i].alloc(ctx, (size_t)nz));
         MR_TRY(c64[(size_t)i].alloc(ctx, (size_t)W + 1));
         MR_TRY(g->tperm.alloc(ctx, (size_t)std::max(T, 1)));
-        g->tpos_ok = false;
+        MR_TRY(g->tpos.alloc(ctx, (size_t)std::max(T, 1)));
+        g->tpos_ok = true;   // (k_tr_place_b writes the inverse beside tperm)
         MR_TRY(g->w_tp.alloc(ctx, (size_t)std::max(T, 1)));
         MR_TRY(g->coff.alloc(ctx, (size_t)W + 1));
         const int64_t nch = 2 * (int64_t)W + (nnz / WAVE + 2 * (int64_t)N) / 4 + 2;   // as tr_layout
@@ -3592,6 +3596,7 @@ int mr_graph_prepare_batch(mr_ctx* ctx, mr_graph* const* gs, int n, std::vector<
         v.tids = g->tids.p;
         v.trz = trz[(size_t)i].p;
         v.tperm = g->tperm.p;
+        v.tpos = g->tpos.p;
         v.coff = g->coff.p;
         v.c64 = c64[(size_t)i].p;
         v.b_gc = bgc;
@@ -3923,6 +3928,12 @@ static int pagerank_setup_batch(mr_ctx* ctx, mr_graph* const* gs, const int* ano
         v.c_t = g->c_t.p;
         v.c_tp = g->c_tp.p;
         v.tperm = g->tperm.p;
+        if (!g->tpos_ok) {   // (graphs prepared one at a time: the inverse of tperm, once per layout)
+            MR_TRY(g->tpos.alloc(ctx, (size_t)std::max(T, 1)));
+            if (T) hipLaunchKernelGGL(k_inv_perm, dim3(cdiv(T, 256)), dim3(256), 0, st, g->tperm.p, T, g->tpos.p);
+            g->tpos_ok = true;
+        }
+        v.tpos = g->tpos.p;
         v.hk = g->ht_key.p;
         v.cr = g->ht_cr.p;
         v.slot_of = g->slot_of.p;
