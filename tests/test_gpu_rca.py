@@ -823,3 +823,99 @@ def test_windows_batch_reaper_and_context_destroy(c3_window, monkeypatch):
         dev.close()
     for a, b in zip(runs["0"][0] + runs["0"][1], runs["1"][0] + runs["1"][1]):
         assert a[2:] == b[2:] and list(a[0]) == list(b[0]) and a[1].tobytes() == b[1].tobytes()
+
+
+# ---------------------------------------------------------------- the headline's own shape (C2 windows)
+C2_WINDOWS = 8
+
+
+@pytest.fixture(scope="module")
+def c2_batch():
+    """BASELINE configs[1] windows exactly as bench.py's default line builds them: 8 distinct
+    1k-op / 200k-trace windows of one system (own seed and span table each) and the SLO of its
+    normal period, resident on the device."""
+    import bench
+    from microrank_amd import _lib
+    from microrank_amd.preprocess_data import DeviceSpans
+
+    normal, tabs = bench.c2_windows(C2_WINDOWS, 1000, 200_000, rank=3)
+    ctx = _lib.default_context()
+    a3, ok = bench.slo_from_gpu(ctx, normal)
+    wins, devs = [], []
+    for st in tabs:
+        d = DeviceSpans(ctx, st)
+        devs.append(d)
+        t0 = int(st.tstart.min())
+        wins.append((d, t0, t0 + 5 * 60 * 10**9, a3, ok))
+    yield ctx, tabs, wins
+    for d in devs:
+        d.close()
+
+
+def test_c2_windows_batch_against_oracle(c2_batch, monkeypatch):
+    """bench.py's default line (online_rca.py:164-201 per window) at its own size: 8 distinct C2
+    windows (1k ops / 200k traces, ~2.3M index entries each) through ONE mr_windows_batch call with
+    the default grouping -- one PageRank group of all 8 windows (256 graphs per launch in the bench:
+    the same grouped k_tr_a / k_fx_b launches), chunks of 4 windows (> 65536 traces per window), the
+    batched stats pass at 64 entries per thread (>= 1M index entries) and the separate detector
+    launch (tables above the 65536-trace fuse limit).  Every window's top-11, DStar2 scores and
+    (abnormal, normal, edges) against the C restatement (oracle/mr_oracle.c, pinned to the
+    reference's goldens) at 1e-10 in fp64; top-5 at 1e-4 in fp32."""
+    import c_oracle
+    from microrank_amd.online_rca import rank_windows
+
+    for k in ("MR_WIN_GROUP", "MR_WIN_CHUNK", "MR_IX_EPT", "MR_DET_FUSE_MAX", "MR_NO_DET_FUSE"):
+        monkeypatch.delenv(k, raising=False)
+    ctx, tabs, wins = c2_batch
+    for st in tabs:   # the branches under test are the ones this shape selects
+        assert st.n_traces > 65536
+        pairs = np.unique(st.trace.astype(np.int64) * st.n_podops + st.podop).size
+        assert pairs >= 1 << 20
+    got = rank_windows(ctx, wins)
+    got32 = rank_windows(ctx, wins, precision="fp32")
+    for i, (st, w) in enumerate(zip(tabs, wins)):
+        codes, scores, na, nn, edges, status = got[i]
+        assert status == 0, i
+        ref = c_oracle.rca_window(st, w[1], w[2], w[3], w[4], nthreads=0)
+        rc, rs, rna, rnn, redges = ref
+        assert (na, nn) == (rna, rnn), i
+        assert na > 0 and nn > 0 and len(rc) == 11
+        assert edges == redges, i
+        assert list(codes) == list(rc), i
+        np.testing.assert_allclose(scores, rs, rtol=1e-10, atol=0, err_msg=f"window {i}")
+        c32, s32, _, _, e32, st32 = got32[i]
+        assert st32 == 0 and e32 == edges
+        assert list(c32[:5]) == list(rc[:5]), i
+        np.testing.assert_allclose(s32, rs, rtol=1e-4, atol=0, err_msg=f"window {i} fp32")
+
+
+def test_c2_windows_batch_groupings_agree(c2_batch, monkeypatch):
+    """The same 8 C2 windows under other batch shapes: chunks of 1 and 2 windows, the stats pass
+    at 16 entries per thread and the detector fused into the index pass (MR_DET_FUSE_MAX above the
+    table) rank bitwise as the default -- build-side choices, the PageRank launches untouched; and
+    PageRank groups of 4 and 2 windows (MR_WIN_GROUP) give the same top lists, counts and edges,
+    scores within 1e-12 (a group's block budget sets each graph's fixed-point scale, so only the
+    rounding of the exact limb sums may move)."""
+    from microrank_amd.online_rca import rank_windows
+
+    knobs = ("MR_WIN_GROUP", "MR_WIN_CHUNK", "MR_IX_EPT", "MR_DET_FUSE_MAX", "MR_NO_DET_FUSE")
+    ctx, _, wins = c2_batch
+    variants = {"default": {}, "chunk1_ept16": {"MR_WIN_CHUNK": "1", "MR_IX_EPT": "16"},
+                "chunk2_fused": {"MR_WIN_CHUNK": "2", "MR_DET_FUSE_MAX": "100000000"},
+                "group4_chunk4": {"MR_WIN_GROUP": "4", "MR_WIN_CHUNK": "4"}, "group2": {"MR_WIN_GROUP": "2"}}
+    runs = {}
+    for name, env in variants.items():
+        for k in knobs:
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        runs[name] = rank_windows(ctx, wins)
+    base = runs["default"]
+    for name, got in runs.items():
+        for i, (a, b) in enumerate(zip(base, got)):
+            assert a[5] == b[5] == 0, (name, i)
+            assert a[2:] == b[2:] and list(a[0]) == list(b[0]), (name, i)
+            if name.startswith("group"):
+                np.testing.assert_allclose(b[1], a[1], rtol=1e-12, atol=0, err_msg=f"{name} window {i}")
+            else:
+                assert a[1].tobytes() == b[1].tobytes(), (name, i)
