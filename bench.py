@@ -124,6 +124,33 @@ def run_window(ctx, dev, t0, t1, a3, ok, prec):
 ITER_KERNELS = ("k_tr_a", "k_fx_b", "k_iter_a", "k_iter_b", "k_cold_trace", "k_cold_ops")
 
 
+def copy_peak(ctx, nbytes=1 << 30, reps=5):
+    """This GPU's measured STREAM-copy rate (the roofline against a measured copy
+    peak beside the 8 TB/s spec): mr_copy_peak, a 16-B-per-lane copy of 1 GiB, best of 5."""
+    import ctypes as C
+
+    from microrank_amd import _lib
+
+    g = C.c_double()
+    ctx.check(_lib.load().mr_copy_peak(ctx.h, int(nbytes), int(reps), C.byref(g)), "mr_copy_peak")
+    return g.value
+
+
+def add_copy_frac(out, ctx):
+    """roofline.copy_peak and every roofline fraction also against it (frac_vs_copy)."""
+    try:
+        cp = copy_peak(ctx)
+    except Exception as e:  # a side metric never sinks the line
+        out["roofline"]["copy_peak"] = {"error": f"{type(e).__name__}: {e}"}
+        return
+    r = out["roofline"]
+    r["copy_peak"] = round(cp, 1)
+    for d in [r] + [r[k] for k in ("u16_ids", "isolated") if isinstance(r.get(k), dict)] + \
+             ([out["window_roofline"]] if isinstance(out.get("window_roofline"), dict) else []):
+        if isinstance(d.get("achieved"), (int, float)) and cp > 0:
+            d["frac_vs_copy"] = round(d["achieved"] / cp, 4)
+
+
 def kind_compressed_probe(ctx, dev, t0, t1, a3, ok, reps=5):
     """§8(f) f4, reported beside (not in) GTEPS: the window's larger graph (the detector's normal
     traces) ranked uncompressed and kind-compressed (MR_PR_KIND_COMPRESS: one representative per
@@ -408,6 +435,7 @@ def run_c4(args, world, rank, dist):
                        "5% broken traces, 1% duplicated root spanIDs across ranks), int-coded, resident in HBM")
         out["config"]["n_spans_rank0"] = int(n_spans_local)
         out["build_ms"] = round(build_s[0] / args.steps * 1e3, 3)   # rank 0's K1 share of a step
+    add_copy_frac(out, ctx)
     if not args.no_cpu and world == 1 and dev is None:
         try:
             out["cpu_baseline"] = c4_cpu_baseline(hg)
@@ -528,8 +556,9 @@ def isolated_group_roofline(ctx, group, prec, reps=3):
 def c4_leg_guarded(hg, world, rank, dist, line, limit_s=240.0):
     """c4_leg_run behind a watchdog: a leg that raises becomes {"error": ...} (ranks stay in step:
     every rank raises on a library error the ranks agreed on); a leg still running after limit_s
-    (a rank lost inside a collective) ends the process with the headline line printed on rank 0,
-    so the driver keeps its C2 number."""
+    (a rank lost inside a collective) prints the headline line on rank 0 (with the leg's error in
+    it) and ends the process with exit status 3, so the hang is visible to the driver as a failure
+    while the line stays on stdout."""
     import threading
 
     if isinstance(hg, Exception):
@@ -539,7 +568,8 @@ def c4_leg_guarded(hg, world, rank, dist, line, limit_s=240.0):
         if line is not None:
             line["c4_sharded"] = {"error": f"timed out after {limit_s:.0f} s"}
             print(json.dumps(line), flush=True)
-        os._exit(0)
+        print(f"[bench] c4_sharded leg hung for {limit_s:.0f} s: exiting with status 3", file=sys.stderr, flush=True)
+        os._exit(3)
 
     wd = threading.Timer(limit_s, expire)
     wd.daemon = True
@@ -1213,6 +1243,7 @@ def main():
                               "frac": round(bytes_w * n_win / elapsed / 1e9 / HBM_PEAK_GBS, 4),
                               "formula": "52 S + 2 (24 S + 4 nnz + 4 T) + 25 B_iter per graph (SURVEY 8(d))"}
     if args.no_side:
+        add_copy_frac(out, ctx)
         print(json.dumps(out), flush=True)
         if dist is not None:
             dist.barrier()
@@ -1250,6 +1281,7 @@ def main():
     if c4_hg is not None:
         out["c4_sharded"] = c4_leg_guarded(c4_hg, world, rank, dist, out)
         c4_hg = None
+    add_copy_frac(out, ctx)
     if not args.no_cpu and world == 1:   # the CPU baseline: rank 0 at N = 1 only
         try:
             cb, cres = cpu_baseline(abnormal, t0, t1, a3, ok)

@@ -67,6 +67,11 @@ void*       mr_ctx_stream(mr_ctx* ctx);
  * clears the record */
 int         mr_ctx_profile(mr_ctx* ctx, int enable);
 int         mr_ctx_prof_read(mr_ctx* ctx, int64_t* launches, double* total_ms, double* total_bytes);
+/* the device's measured copy peak (the HBM roofline is also reported against a
+ * measured STREAM-copy rate beside the 8 TB/s spec): a 16-B-per-lane copy kernel over two
+ * buffers of `bytes` each on the context stream, one warm-up and `reps` timed launches; *gbs =
+ * the best launch's (read + written) bytes / time in GB/s.  No reference counterpart (measurement) */
+int         mr_copy_peak(mr_ctx* ctx, int64_t bytes, int reps, double* gbs);
 
 /* ------------------------------------------------------------------ graph from index arrays
  * Replaces the dense matrix fill of pagerank.trace_pagerank (pagerank.py:16-52): the four

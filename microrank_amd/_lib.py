@@ -67,6 +67,7 @@ SIGNATURES = {
     "mr_ctx_stream": (P, [P]),
     "mr_ctx_profile": (C.c_int, [P, C.c_int]),
     "mr_ctx_prof_read": (C.c_int, [P, i64p, f64p, f64p]),
+    "mr_copy_peak": (C.c_int, [P, C.c_int64, C.c_int, f64p]),
     "mr_graph_upload": (C.c_int, [P, C.POINTER(GraphDesc), C.POINTER(P)]),
     "mr_graph_free": (C.c_int, [P]),
     "mr_graph_info": (C.c_int, [P, i32p, i32p, i64p, i64p]),

@@ -267,6 +267,55 @@ extern "C" void mr_ctx_destroy(mr_ctx* ctx) {
 
 extern "C" const char* mr_last_error(const mr_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
 
+// ---------------------------------------------------------------- measured copy peak
+// STREAM copy: every lane moves 4 x 16 B per round (all loads in flight before the stores),
+// grid-stride over the buffer
+__global__ void __launch_bounds__(256) k_copy16(const uint4* __restrict__ src, uint4* __restrict__ dst, int64_t n) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + 3 * stride < n; i += 4 * stride) {
+        const uint4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+        dst[i] = a;
+        dst[i + stride] = b;
+        dst[i + 2 * stride] = c;
+        dst[i + 3 * stride] = d;
+    }
+    for (; i < n; i += stride) dst[i] = src[i];
+}
+extern "C" int mr_copy_peak(mr_ctx* ctx, int64_t bytes, int reps, double* gbs) {
+    if (!ctx || bytes < 16 || reps < 1 || !gbs) return mr_fail(ctx, MR_ERR_ARG, "mr_copy_peak: bad arguments");
+    MR_TRY_HIP(ctx, hipSetDevice(ctx->device));
+    const int64_t n = bytes / 16;
+    DBuf<uint4> a, b;
+    MR_TRY(a.alloc(ctx, (size_t)n));
+    MR_TRY(b.alloc(ctx, (size_t)n));
+    MR_TRY_HIP(ctx, hipMemsetAsync(a.p, 1, (size_t)n * 16, ctx->stream));
+    int dev = 0, cus = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const int blocks = (int)std::min<int64_t>((int64_t)cus * 16, (n + 255) / 256);
+    hipEvent_t e0, e1;
+    MR_TRY_HIP(ctx, hipEventCreate(&e0));
+    MR_TRY_HIP(ctx, hipEventCreate(&e1));
+    double best = 0.0;
+    int rc = MR_OK;
+    for (int r = -1; r < reps && rc == MR_OK; ++r) {
+        (void)hipEventRecord(e0, ctx->stream);
+        hipLaunchKernelGGL(k_copy16, dim3(blocks), dim3(256), 0, ctx->stream, a.p, b.p, n);
+        (void)hipEventRecord(e1, ctx->stream);
+        if (hipEventSynchronize(e1) != hipSuccess) rc = mr_fail(ctx, MR_ERR_HIP, "mr_copy_peak: launch failed");
+        float ms = 0.0f;
+        if (rc == MR_OK && r >= 0 && hipEventElapsedTime(&ms, e0, e1) == hipSuccess && ms > 0.0f)
+            best = std::max(best, 2.0 * (double)n * 16.0 / (ms * 1e-3) / 1e9);
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    MR_TRY(rc);
+    MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    *gbs = best;
+    return MR_OK;
+}
+
 extern "C" int mr_ctx_sync(mr_ctx* ctx) {
     if (!ctx) return MR_ERR_ARG;
     MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));

@@ -433,9 +433,43 @@ static int win_chunk_build_async(mr_ctx* ctx, const WinIn* in, int n, int precis
         w.ga->ctx = ctx;
     }
     // the whole chunk's index pass in one launch per stage when every window allows it (and the
-    // windows agree on the detector fusion), else window by window
-    bool batched = false;
-    if (n >= 2) {
+    // windows agree on the detector fusion), else window by window.  Tables with a layout order
+    // (mr_spans.lo_ok): the layout-order build (mr_lo_launch_batch), its kind histograms in one
+    // zeroed buffer
+    bool batched = false, lo = false;
+    DBuf<uint32_t> zw;
+    {
+        bool ok = getenv("MR_NO_LO_WIN") == nullptr;   // (A/B and tests, read per call)
+        int64_t nzw = 0;
+        for (int k = 0; k < n && ok; ++k) {
+            ok = in[k].s->lo_ok && mr_lo_fits(in[k].s);
+            if (ok) nzw += mr_lo_zero_words(in[k].s);
+        }
+        if (ok) {
+            MR_TRY(zw.zero(ctx, (size_t)nzw));
+            std::vector<const mr_spans*> sps((size_t)n);
+            std::vector<mr_graph*> g0((size_t)n), g1((size_t)n);
+            std::vector<IxBuild*> b0((size_t)n), b1((size_t)n);
+            std::vector<int64_t*> outs((size_t)n);
+            std::vector<uint32_t*> zs((size_t)n);
+            int64_t zo = 0;
+            for (int k = 0; k < n; ++k) {
+                sps[(size_t)k] = in[k].s;
+                g0[(size_t)k] = in[k].w->gn;
+                g1[(size_t)k] = in[k].w->ga;
+                b0[(size_t)k] = &bx[2 * (size_t)k];
+                b1[(size_t)k] = &bx[2 * (size_t)k + 1];
+                outs[(size_t)k] = wb.p + (size_t)k * WW + CW;
+                zs[(size_t)k] = zw.p + zo;
+                zo += mr_lo_zero_words(in[k].s);
+            }
+            const int rcl = mr_lo_launch_batch(ctx, n, sps.data(), g0.data(), g1.data(), b0.data(), b1.data(), outs.data(),
+                                               dis.data(), zs.data());
+            if (rcl != MR_ERR_STATE) MR_TRY(rcl);
+            batched = lo = rcl == MR_OK;
+        }
+    }
+    if (n >= 2 && !batched) {
         bool same = true;
         for (int k = 1; k < n; ++k) same = same && fz[(size_t)k] == fz[0];
         if (same) {
@@ -502,6 +536,8 @@ static int win_chunk_build_async(mr_ctx* ctx, const WinIn* in, int n, int precis
     const int64_t split = se ? (int64_t)atoll(se) : (int64_t)65536;
     std::vector<mr_graph*> gs, pre;
     std::vector<int> pre_an;
+    std::vector<const mr_spans*> gsp;   // (layout-order builds: each graph's table and build)
+    std::vector<IxBuild*> gbx;
     for (int k = 0; k < n; ++k) {
         WinRun& w = *in[k].w;
         const int64_t* hk = h.data() + (size_t)k * WW;
@@ -514,10 +550,17 @@ static int win_chunk_build_async(mr_ctx* ctx, const WinIn* in, int n, int precis
             continue;
         }
         IxBuild &bn = bx[2 * (size_t)k], &ba = bx[2 * (size_t)k + 1];
+        if (lo && (hk[CW + 2] || hk[CW + 8 + 2]))   // (mr_lo_fits bounds the edges: cannot happen)
+            return mr_fail(ctx, MR_ERR_STATE, "mr_windows_batch: layout-order build past the node pass's edge limit");
         MR_TRY(mr_ix_finish_unprepared(ctx, in[k].s, w.gn, bn, bn.small ? hk + CW : nullptr));
         MR_TRY(mr_ix_finish_unprepared(ctx, in[k].s, w.ga, ba, ba.small ? hk + CW + 8 : nullptr));
         gs.push_back(w.gn);
         gs.push_back(w.ga);
+        gsp.push_back(in[k].s);
+        gsp.push_back(in[k].s);
+        gbx.push_back(&bn);
+        gbx.push_back(&ba);
+        if (lo) continue;
         if ((int64_t)w.gn->T + w.ga->T >= split) {
             pre.push_back(w.gn);
             pre.push_back(w.ga);
@@ -525,7 +568,14 @@ static int win_chunk_build_async(mr_ctx* ctx, const WinIn* in, int n, int precis
             pre_an.push_back(1);
         }
     }
-    if (!gs.empty()) MR_TRY(mr_graph_prepare_batch(ctx, gs.data(), (int)gs.size(), c.keep));
+    if (lo) {   // layout-order graphs: tiles, ids, kinds, preference and iteration state (pre_ok)
+        std::vector<int> an(gs.size());
+        for (size_t j = 0; j < gs.size(); ++j) an[j] = (int)(j & 1);   // (gn "normal", ga "anomaly": T1)
+        if (!gs.empty()) MR_TRY(mr_lo_prepare_batch(ctx, gs.data(), gsp.data(), gbx.data(), an.data(), (int)gs.size(), 0.85,
+                                                    precision, c.keep));
+    } else if (!gs.empty()) {
+        MR_TRY(mr_graph_prepare_batch(ctx, gs.data(), (int)gs.size(), c.keep));
+    }
     if (!pre.empty()) MR_TRY(mr_pagerank_presetup_n(ctx, pre.data(), pre_an.data(), (int)pre.size(), 0.85, precision, c.keep2));
     if (!c.ev) MR_TRY_HIP(ctx, hipEventCreateWithFlags(&c.ev, hipEventDisableTiming));
     MR_TRY_HIP(ctx, hipEventRecord(c.ev, st));
@@ -696,12 +746,10 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
         for (int32_t i = gbeg[(size_t)g], e = gbeg[(size_t)g + 1]; i < e; i += chunk_size)
             chunks.emplace_back(i, std::min<int32_t>(e, i + chunk_size));
     const int nthr = std::min<int>((int)chunks.size(), max_streams);
-    // MR_WIN_PR_STREAMS=2: odd groups' PageRanks on a second context (its own stream, pool and
-    // scratch: aux[nthr]), so one group's latency-bound iterations overlap the next group's
-    const char* pse = getenv("MR_WIN_PR_STREAMS");   // (A/B, read per call)
-    const int npr = pse && atoi(pse) >= 2 && ngroups >= 2 ? 2 : 1;
-    MR_TRY(win_aux(ctx, nthr + (npr > 1)));
-    auto pr_ctx = [&](int g) -> mr_ctx* { return npr > 1 && (g & 1) ? ctx->aux[(size_t)nthr] : ctx; };
+    // (every group's PageRanks on this context's stream: a second PageRank stream for odd groups
+    // measured within the spread, profiles/r04al/, and was removed)
+    MR_TRY(win_aux(ctx, nthr));
+    auto pr_ctx = [&](int) -> mr_ctx* { return ctx; };
     // the SLO vectors once per distinct (a3, a3_valid, length) of the batch (windows usually share
     // one pair), resident before any window's detector runs
     std::unique_ptr<WinPhase> ph_setup(new WinPhase(8));
@@ -928,7 +976,6 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
     for (; rc == MR_OK && settled < ngroups; ++settled) rc = settle(settled);
     if (rc != MR_OK) {   // (an error left groups in flight)
         (void)hipStreamSynchronize(ctx->stream);
-        if (npr > 1) (void)hipStreamSynchronize(ctx->aux[(size_t)nthr]->stream);
     }
     for (PrAsync* a : pend)
         if (a) mr_pagerank_async_free(a);
@@ -944,7 +991,6 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
     // (an error may leave PageRank work queued on the main stream that still reads window graphs
     // whose blocks return to the worker pools below: drain it first)
     (void)hipStreamSynchronize(ctx->stream);
-    if (npr > 1) (void)hipStreamSynchronize(ctx->aux[(size_t)nthr]->stream);
     for (hipEvent_t e : gev)
         if (e) (void)hipEventDestroy(e);
     MR_TRY(rc);

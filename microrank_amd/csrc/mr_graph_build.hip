@@ -306,7 +306,7 @@ __device__ void nodes_small(const uint64_t* gk, const uint32_t* gc, int64_t ecap
                             const int32_t* ofirst, int32_t NP, int32_t* node_of_code, int32_t* node_podop,
                             int32_t* len_o, int32_t* nchild, const int32_t* ocov, int32_t* cov, int32_t* ss_par,
                             int64_t* ss_off, const int64_t* T_dev, const int64_t* nnz_dev, int64_t* rs_off,
-                            int64_t* out) {
+                            int64_t* out, float* u_o = nullptr, float* pw = nullptr, bool first_inv = false) {
     __shared__ int32_t is_par[NS_PMAX], nch[NS_PMAX], noc[NS_PMAX];
     __shared__ uint64_t qb[NS_PMAX], eb[NS_EMAX];
     __shared__ int32_t sbuf[NS_T];
@@ -333,7 +333,7 @@ __device__ void nodes_small(const uint64_t* gk, const uint32_t* gc, int64_t ecap
     if (tid == 0) {   // the trace side's sizes (its scans ran before this launch)
         out[3] = *T_dev;
         out[4] = *nnz_dev;
-        rs_off[*T_dev] = *nnz_dev;
+        if (rs_off) rs_off[*T_dev] = *nnz_dev;
     }
     if (E > NS_EMAX) {
         if (tid == 0) out[2] = 1;
@@ -359,7 +359,9 @@ __device__ void nodes_small(const uint64_t* gk, const uint32_t* gc, int64_t ecap
             node_podop[pp] = c;
             ++pp;
         } else if (ocnt[c] > 0) {
-            qb[qp++] = ((uint64_t)(uint32_t)ofirst[c] << 32) | (uint32_t)c;
+            // (first_inv: the layout-order build keeps INT_MAX - first row, max-reduced)
+            const int32_t fr = first_inv ? 0x7fffffff - ofirst[c] : ofirst[c];
+            qb[qp++] = ((uint64_t)(uint32_t)fr << 32) | (uint32_t)c;
         }
     }
     __syncthreads();
@@ -392,6 +394,10 @@ __device__ void nodes_small(const uint64_t* gk, const uint32_t* gc, int64_t ecap
             len_o[noc[c]] = ocnt[c];
             nchild[noc[c]] = nch[c];
             cov[noc[c]] = ocov[c];
+            if (u_o) {   // (layout-order builds: graph_consts' fp32 reciprocals, pagerank.py:39-52)
+                u_o[noc[c]] = ocnt[c] > 0 ? (float)(1.0 / (double)ocnt[c]) : 0.0f;
+                pw[noc[c]] = nch[c] > 0 ? (float)(1.0 / (double)nch[c]) : 0.0f;
+            }
         }
     // P_ss by child (edges sorted by (child node, parent node)): a counting sort by child into
     // the CSR, then each child's few parents sorted in place.  (is_par / nch / qb are free now.)
@@ -463,6 +469,8 @@ struct NsArgs {
     int64_t* ss_off;
     const int64_t *T_dev, *nnz_dev;
     int64_t *rs_off, *out;
+    float *u_o, *pw;   // (layout-order builds; else null)
+    int32_t first_inv;  // (layout-order builds: ofirst holds INT_MAX - first row)
 };
 struct NsArgs2 {
     NsArgs g[2];
@@ -1845,7 +1853,7 @@ int mr_ix_launch2(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d_state, mr_gr
         xs.g[k] = IxSide{B.tflag.p, B.ocnt.p, B.ofirst.p, B.ocov.p, B.tpos.p, B.zoff.p, B.gc.p};
         na.g[k] = NsArgs{B.gc.p, B.ocnt.p, B.ofirst.p, B.ocov.p, B.node_of_code.p, G->node_podop.p, G->len_o.p,
                          G->nchild.p, G->cov.p, G->ss_par.p, G->ss_off.p, B.tpos.p + NT, B.zoff.p + NT, G->rs_off.p,
-                         d_out + 8 * k};
+                         d_out + 8 * k, nullptr, nullptr};
         to.g[k] = TrOut{G->trace_code.p, G->len_t.p, G->rs_ops.p, G->rs_off.p, B.node_of_code.p};
     }
     if (det) {   // the detector's states come out of the same launch (into det->state == d_state)
@@ -1979,7 +1987,7 @@ __global__ void __launch_bounds__(NS_T) k_nodes_small2_b(IxBatch<IxWinNodes> a) 
     const IxWinNodes& w = a.w[k];
     const NsArgs& x = w.a.g[blockIdx.x & 1];
     nodes_small(w.gk, x.gc, w.ecap, x.ocnt, x.ofirst, w.NP, x.node_of_code, x.node_podop, x.len_o, x.nchild, x.ocov, x.cov,
-                x.ss_par, x.ss_off, x.T_dev, x.nnz_dev, x.rs_off, x.out);
+                x.ss_par, x.ss_off, x.T_dev, x.nnz_dev, x.rs_off, x.out, x.u_o, x.pw, x.first_inv != 0);
 }
 __global__ void k_ix_traces2_b(IxBatch<IxWinTraces> a) {
     const int k = ixb_pick(a.b0, a.n);
@@ -2068,7 +2076,7 @@ int mr_ix_launch2_batch(mr_ctx* ctx, int n, const mr_spans* const* sps, uint8_t*
             xs.g[j] = IxSide{B.tflag.p, B.ocnt.p, B.ofirst.p, B.ocov.p, B.tpos.p, B.zoff.p, B.gc.p};
             na.g[j] = NsArgs{B.gc.p, B.ocnt.p, B.ofirst.p, B.ocov.p, B.node_of_code.p, G->node_podop.p, G->len_o.p,
                              G->nchild.p, G->cov.p, G->ss_par.p, G->ss_off.p, B.tpos.p + NT, B.zoff.p + NT, G->rs_off.p,
-                             d_outs[k] + 8 * j};
+                             d_outs[k] + 8 * j, nullptr, nullptr};
             to.g[j] = TrOut{G->trace_code.p, G->len_t.p, G->rs_ops.p, G->rs_off.p, B.node_of_code.p};
         }
         const int32_t nt = (int32_t)std::max<int64_t>(cdiv((int64_t)NT, TP), 1);
@@ -2125,6 +2133,299 @@ int mr_ix_launch2_batch(mr_ctx* ctx, int n, const mr_spans* const* sps, uint8_t*
     if (bc) hipLaunchKernelGGL(k_ix_cross2_b, dim3(bc), dim3(256), 0, st, ac);
     hipLaunchKernelGGL(k_nodes_small2_b, dim3(2 * n), dim3(NS_T), 0, st, an);
     if (br) hipLaunchKernelGGL(k_ix_traces2_b, dim3(br), dim3(256), 0, st, ar);
+    MR_TRY_HIP(ctx, hipGetLastError());
+    return MR_OK;
+}
+
+// ---------------------------------------------------------------- window graphs in layout order
+// A window's graphs tile their traces in the table's layout order (mr_spans.lo_*: by distinct
+// pod-op count, then code -- window-independent, built with the index).  The selection runs over
+// that order: each selected trace's position in its graph is its rank among the graph's traces
+// there (look-back scan), pinv[position] = its layout index, and its kind class is counted
+// (pagerank.py:54-66's class size = the histogram of the graph's class ids).  No trace-major
+// incidence, no per-graph sort by length, no kind hashing: the prepare reads each position's
+// codes from the layout-ordered u16 lists (near-contiguous for a tile) and relabels them.
+constexpr int LB_T = 1024, LB_I = 8, LB_TILE = LB_T * LB_I;   // k_lo_build_b: threads, traces per thread / block
+constexpr int64_t LB_LDS_WORDS = 34816;   // its two graphs' histograms (136 KB beside its static LDS)
+bool mr_lo_fits(const mr_spans* sp) {
+    return sp->indexed && sp->ekey.p && sp->n_podops <= NS_PMAX && sp->n_edge_keys <= NS_EMAX &&
+           2 * (3 * (int64_t)sp->n_podops + sp->n_edge_keys) <= LB_LDS_WORDS && sp->n_traces <= (1 << 24);
+}
+// Per window, in its table's layout order: the detector (anormaly_detector.py:44-84 as
+// detect_block: a trace's expect summed sequentially over its service-ops in name order, T14),
+// the selection of both graphs (T1 swap: state 2 -> graph 0, 1 -> graph 1) with each selected
+// trace's position (its rank among the graph's traces in layout order: look-back scan) and kind
+// class count, and both graphs' per-pod-op span counts / first rows / coverage and per-edge-id
+// multiplicities (get_pagerank_graph's len_o, node order and children multisets,
+// preprocess_data.py:146-171) in LDS, flushed once per block into zeroed words (the first row as
+// INT_MAX - row under atomicMax).  One pass over everything a trace holds.
+struct IxWinLoB {
+    const int32_t *lo_tr, *lo_len, *lo_kid, *lo_first;
+    const int64_t *lo_off, *lsv_off, *le_off;
+    const uint16_t *lo16, *lo_cnt;
+    const uint32_t *lsv, *le;
+    const long long *lo_ts, *lo_te, *lo_mx;
+    const double* a3;
+    const uint8_t* a3v;
+    int64_t t0, t1;
+    uint8_t* state;                  // by trace code (k_ix_cross2_b reads it)
+    unsigned long long* counts;      // detector counter shards (3 * CSH, zeroed)
+    unsigned long long* st;          // look-back words: 2 chains x the window's tiles
+    int32_t NT, NP, nek, pad_;
+    int32_t* pinv[2];                // position -> layout index
+    uint32_t* kcnt[2];               // kind class histograms (zeroed)
+    int64_t* tot[2];                 // [T, nnz] (zeroed)
+    int32_t *ocnt[2], *ofinv[2], *ocov[2];   // (zeroed)
+    uint32_t* gc[2];                 // (zeroed)
+};
+__global__ void __launch_bounds__(LB_T) k_lo_build_b(IxBatch<IxWinLoB> a, uint64_t epoch) {
+    extern __shared__ int32_t lh[];   // graph g: [g W, (g + 1) W): cnt | INT_MAX - first | cov | edges
+    __shared__ int8_t side[LB_TILE];
+    __shared__ int32_t sa[2][LB_T];
+    __shared__ int32_t ex[2];
+    __shared__ unsigned long long bc[3][LB_T / WAVE], bz[2][LB_T / WAVE];
+    const int k = ixb_pick(a.b0, a.n);
+    const IxWinLoB& w = a.w[k];
+    const int32_t blk = (int32_t)blockIdx.x - a.b0[k], nblk = a.b0[k + 1] - a.b0[k];
+    const int tid = threadIdx.x, lane = tid & (WAVE - 1), wv = tid / WAVE;
+    const int32_t NP = w.NP, W = 3 * NP + w.nek;
+    for (int32_t x = tid; x < 2 * W; x += LB_T) lh[x] = 0;
+    __syncthreads();
+    const int64_t base = (int64_t)blk * LB_TILE;
+    int64_t nz0 = 0, nz1 = 0, rows = 0;
+    int nab = 0, nno = 0;
+    for (int j = 0; j < LB_I; ++j) {   // consecutive lanes, consecutive traces: contiguous entries
+        const int64_t i = base + (int64_t)j * LB_T + tid;
+        int s_ = -1;
+        if (i < w.NT) {
+            const int32_t len = w.lo_len[i];
+            const long long ts = w.lo_ts[i], te = w.lo_te[i], mx = w.lo_mx[i];
+            const bool in = len > 0 && ts >= w.t0 && te <= w.t1;
+            rows += in ? len : 0;
+            int stt = 0;
+            if (in && mx > 0) {   // grouped[grouped['duration'] > 0] (preprocess_data.py:117)
+                double expect = 0.0;
+                for (int64_t e = w.lsv_off[i], e1 = w.lsv_off[i + 1]; e < e1; ++e) {
+                    const uint32_t v = w.lsv[e];
+                    const uint32_t op = v & 0xffffu;
+                    expect += w.a3v[op] ? (double)(v >> 16) * w.a3[op] : 0.0;   // :63-67 (T14)
+                }
+                stt = (double)mx / 1000.0 > expect ? 2 : 1;   // :58, :69
+            }
+            w.state[w.lo_tr[i]] = (uint8_t)stt;
+            nab += stt == 2;
+            nno += stt == 1;
+            s_ = stt == 2 ? 0 : stt == 1 ? 1 : -1;
+            if (s_ >= 0) {
+                atomicAdd(&w.kcnt[s_][w.lo_kid[i]], 1u);
+                int32_t* L = lh + s_ * W;
+                const int64_t e0 = w.lo_off[i], e1 = w.lo_off[i + 1];
+                if (s_ == 0) nz0 += e1 - e0; else nz1 += e1 - e0;
+                for (int64_t e = e0; e < e1; ++e) {
+                    const int32_t c = w.lo16[e];
+                    atomicAdd(&L[c], (int32_t)w.lo_cnt[e]);
+                    atomicMax(&L[NP + c], 0x7fffffff - w.lo_first[e]);
+                    atomicAdd(&L[2 * NP + c], 1);
+                }
+                for (int64_t e = w.le_off[i], e1e = w.le_off[i + 1]; e < e1e; ++e) {
+                    const uint32_t v = w.le[e];
+                    atomicAdd((uint32_t*)&L[3 * NP + (int32_t)(v & 0xffffu)], v >> 16);
+                }
+            }
+        }
+        side[j * LB_T + tid] = (int8_t)s_;
+    }
+    {   // the detector's counts and both graphs' entry totals: per wave, per block, one add each
+        unsigned long long ab = (unsigned long long)nab, no = (unsigned long long)nno, rw = (unsigned long long)rows;
+        unsigned long long z0 = (unsigned long long)nz0, z1 = (unsigned long long)nz1;
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) {
+            ab += __shfl_xor(ab, m, WAVE);
+            no += __shfl_xor(no, m, WAVE);
+            rw += __shfl_xor(rw, m, WAVE);
+            z0 += __shfl_xor(z0, m, WAVE);
+            z1 += __shfl_xor(z1, m, WAVE);
+        }
+        if (lane == 0) {
+            bc[0][wv] = ab;
+            bc[1][wv] = no;
+            bc[2][wv] = rw;
+            bz[0][wv] = z0;
+            bz[1][wv] = z1;
+        }
+    }
+    __syncthreads();
+    if (tid < 5) {
+        unsigned long long v = 0;
+        for (int q = 0; q < LB_T / WAVE; ++q) v += tid < 3 ? bc[tid][q] : bz[tid - 3][q];
+        if (v) {
+            if (tid < 3) atomicAdd(&w.counts[(size_t)(blk % CSH) * 3 + tid], v);
+            else atomicAdd((unsigned long long*)&w.tot[tid - 3][1], v);
+        }
+    }
+    // positions: thread tid owns the tile's traces [tid LB_I, (tid + 1) LB_I) for the scan
+    int32_t c0 = 0, c1 = 0;
+#pragma unroll
+    for (int q = 0; q < LB_I; ++q) {
+        const int sd = side[tid * LB_I + q];
+        c0 += sd == 0;
+        c1 += sd == 1;
+    }
+    sa[0][tid] = c0;
+    sa[1][tid] = c1;
+    __syncthreads();
+    for (int o = 1; o < LB_T; o <<= 1) {
+        const int32_t v0 = tid >= o ? sa[0][tid - o] : 0, v1 = tid >= o ? sa[1][tid - o] : 0;
+        __syncthreads();
+        sa[0][tid] += v0;
+        sa[1][tid] += v1;
+        __syncthreads();
+    }
+    if (tid < 2 * WAVE) {   // wave g: graph g's positions
+        const int g = tid / WAVE;
+        const int32_t agg = sa[g][LB_T - 1];
+        const int64_t e = dl_lookback_wave(w.st + (size_t)g * nblk, blk, agg, epoch);
+        if (lane == 0) {
+            ex[g] = (int32_t)e;
+            if (blk == nblk - 1) w.tot[g][0] = e + agg;
+        }
+    }
+    __syncthreads();
+    int32_t r0 = ex[0] + sa[0][tid] - c0, r1 = ex[1] + sa[1][tid] - c1;
+#pragma unroll
+    for (int q = 0; q < LB_I; ++q) {
+        const int sd = side[tid * LB_I + q];
+        const int32_t ix = (int32_t)(base + tid * LB_I + q);
+        if (sd == 0) w.pinv[0][r0++] = ix;
+        else if (sd == 1) w.pinv[1][r1++] = ix;
+    }
+    // the block's histograms into the window's zeroed words
+    for (int32_t x = tid; x < 2 * W; x += LB_T) {
+        const int32_t v = lh[x];
+        if (!v) continue;
+        const int g = x >= W, jx = x - g * W;
+        if (jx < NP) atomicAdd(&w.ocnt[g][jx], v);
+        else if (jx < 2 * NP) atomicMax(&w.ofinv[g][jx - NP], v);
+        else if (jx < 3 * NP) atomicAdd(&w.ocov[g][jx - 2 * NP], v);
+        else atomicAdd(&w.gc[g][jx - 3 * NP], (uint32_t)v);
+    }
+}
+
+// Per window (n <= IXW): k_lo_build_b, the rare joins across traces, the node order / P_ss / op
+// constants (k_nodes_small2_b): sizes of graph j of window k to d_outs[k] + 8 j (N, E, overflow,
+// T, nnz; words 5 / 6: the build's totals).  zw[k]: the window's zeroed words, lo_zero_words(sp)
+// of them.  MR_ERR_STATE: a window outside the limits (the caller takes mr_ix_launch2_batch).
+int64_t mr_lo_zero_words(const mr_spans* sp) {
+    return 2 * ((int64_t)std::max(sp->lo_nk, 1) + 3 * (int64_t)sp->n_podops + std::max<int64_t>(sp->n_edge_keys, 1));
+}
+int mr_lo_launch_batch(mr_ctx* ctx, int n, const mr_spans* const* sps, mr_graph* const* g0s, mr_graph* const* g1s,
+                       IxBuild* const* b0s, IxBuild* const* b1s, int64_t* const* d_outs, const DetIn* dets,
+                       uint32_t* const* zw) {
+    if (n < 1 || n > IXW || getenv("MR_NO_IX2") != nullptr || getenv("MR_NO_IXB") != nullptr) return MR_ERR_STATE;
+    for (int k = 0; k < n; ++k)
+        if (!sps[k]->lo_ok || !mr_lo_fits(sps[k])) return MR_ERR_STATE;
+    hipStream_t st = ctx->stream;
+    IxBatch<IxWinLoB> ab{};
+    IxBatch<IxWinCross> ac{};
+    IxBatch<IxWinNodes> an{};
+    ab.n = ac.n = an.n = n;
+    int32_t bb = 0, bc = 0;
+    size_t lds = 4;
+    int64_t words = 0;
+    std::vector<int64_t> woff((size_t)n);
+    for (int k = 0; k < n; ++k) {
+        const mr_spans* sp = sps[k];
+        const int32_t NT = sp->n_traces, NP = sp->n_podops;
+        const int64_t nek = sp->n_edge_keys, nk = std::max(sp->lo_nk, 1);
+        IxSide2 xs;
+        NsArgs2 na;
+        IxBuild* b[2] = {b0s[k], b1s[k]};
+        mr_graph* g[2] = {g0s[k], g1s[k]};
+        IxWinLoB& L = ab.w[k];
+        const int64_t per = nk + 3 * (int64_t)NP + std::max<int64_t>(nek, 1);   // zeroed words per graph
+        for (int j = 0; j < 2; ++j) {
+            IxBuild& B = *b[j];
+            mr_graph* G = g[j];
+            B.dense = true;
+            B.small = true;
+            B.ecap = (uint64_t)nek;
+            B.gkp = sp->ekey.p;
+            uint32_t* z = zw[k] + j * per;
+            B.kcnt = z;
+            int32_t* ocnt = (int32_t*)(z + nk);
+            int32_t* ofinv = ocnt + NP;
+            int32_t* ocov = ofinv + NP;
+            uint32_t* gc = (uint32_t*)(ocov + NP);
+            MR_TRY(B.pinv.alloc(ctx, std::max(NT, 1)));
+            MR_TRY(B.node_of_code.alloc(ctx, std::max(NP, 1)));
+            MR_TRY(G->node_podop.alloc(ctx, std::max(NP, 1)));
+            MR_TRY(G->len_o.alloc(ctx, std::max(NP, 1)));
+            MR_TRY(G->nchild.alloc(ctx, std::max(NP, 1)));
+            MR_TRY(G->cov.alloc(ctx, std::max(NP, 1)));
+            MR_TRY(G->u_o.alloc(ctx, std::max(NP, 1)));
+            MR_TRY(G->pw.alloc(ctx, std::max(NP, 1)));
+            MR_TRY(G->ss_par.alloc(ctx, NS_EMAX));
+            MR_TRY(G->ss_off.alloc(ctx, (size_t)NP + 1));
+            xs.g[j] = IxSide{nullptr, ocnt, ofinv, ocov, nullptr, nullptr, gc};
+            int64_t* out = d_outs[k] + 8 * j;
+            na.g[j] = NsArgs{gc, ocnt, ofinv, ocov, B.node_of_code.p, G->node_podop.p, G->len_o.p, G->nchild.p, G->cov.p,
+                             G->ss_par.p, G->ss_off.p, out + 5, out + 6, nullptr, out, G->u_o.p, G->pw.p, 1};
+            L.pinv[j] = B.pinv.p;
+            L.kcnt[j] = B.kcnt;
+            L.tot[j] = out + 5;
+            L.ocnt[j] = ocnt;
+            L.ofinv[j] = ofinv;
+            L.ocov[j] = ocov;
+            L.gc[j] = gc;
+        }
+        const int32_t nt = (int32_t)std::max<int64_t>(cdiv((int64_t)NT, LB_TILE), 1);
+        woff[(size_t)k] = words;
+        words += 2 * (int64_t)nt;
+        ab.b0[k] = bb;
+        bb += nt;
+        const DetIn& d = dets[k];
+        L.lo_tr = sp->lo_tr.p;
+        L.lo_len = sp->lo_len.p;
+        L.lo_kid = sp->lo_kid.p;
+        L.lo_first = sp->lo_first.p;
+        L.lo_off = sp->lo_off.p;
+        L.lsv_off = sp->lsv_off.p;
+        L.le_off = sp->le_off.p;
+        L.lo16 = sp->lo16.p;
+        L.lo_cnt = sp->lo_cnt.p;
+        L.lsv = sp->lsv.p;
+        L.le = sp->le.p;
+        L.lo_ts = sp->lo_ts.p;
+        L.lo_te = sp->lo_te.p;
+        L.lo_mx = sp->lo_mx.p;
+        L.a3 = d.a3;
+        L.a3v = d.a3v;
+        L.t0 = d.t0;
+        L.t1 = d.t1;
+        L.state = d.state;
+        L.counts = d.counts;
+        L.NT = NT;
+        L.NP = NP;
+        L.nek = (int32_t)nek;
+        lds = std::max(lds, 2 * (3 * (size_t)NP + (size_t)nek) * sizeof(int32_t));
+        ac.b0[k] = bc;
+        bc += (int32_t)cdiv(sp->n_xj, 256);
+        ac.w[k] = IxWinCross{d.state, sp->xj_tc.p, sp->xj_tp.p, sp->xj_eid.p, sp->n_xj, xs};
+        an.b0[k] = 2 * k;
+        an.w[k] = IxWinNodes{sp->ekey.p, nek, NP, 0, na};
+    }
+    for (int k = n; k <= IXW; ++k) {   // (offsets past the last window: its end)
+        ab.b0[k] = bb;
+        ac.b0[k] = bc;
+        an.b0[k] = 2 * n;
+    }
+    unsigned long long* dst = nullptr;
+    uint64_t epoch = 0;
+    MR_TRY(mr_dl_status(ctx, words, &dst, &epoch));
+    for (int k = 0; k < n; ++k) ab.w[k].st = dst + woff[(size_t)k];
+    hipLaunchKernelGGL(k_lo_build_b, dim3(bb), dim3(LB_T), lds, st, ab, epoch);
+    if (bc) hipLaunchKernelGGL(k_ix_cross2_b, dim3(bc), dim3(256), 0, st, ac);
+    hipLaunchKernelGGL(k_nodes_small2_b, dim3(2 * n), dim3(NS_T), 0, st, an);
     MR_TRY_HIP(ctx, hipGetLastError());
     return MR_OK;
 }

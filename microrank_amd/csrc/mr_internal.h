@@ -313,6 +313,12 @@ struct mr_graph {
     DBuf<int32_t> slot_of;
     DBuf<uint64_t> ht_chk;   // sharded on >1 rank: check hash of each class's representative
     DBuf<int32_t> flag;          // [4] error flags written by kernels
+    // a window graph tiled from its table's layout order (mr_lo_prepare_batch): no trace-major
+    // incidence (rs_off / rs_ops / rs16 / tperm are empty); kind counts and span counts by
+    // position (kind, lo_lenp) and the preference partials (ppart) stay for a re-set-up
+    bool lo = false;
+    DBuf<int32_t> lo_lenp;       // [T] span count by position
+    int32_t lo_nbp = 0;          // preference partial blocks
 };
 
 // edge entries from which the index also keeps them in edge-id order (mr_spans.eb_*);
@@ -353,6 +359,26 @@ struct mr_spans {
     DBuf<int32_t> eb_tr, eb_cnt, eb_eid;
     DBuf<int32_t> xj_tc, xj_tp;          // [n_xj] join pairs across traces (T11): child / parent trace
     DBuf<uint64_t> xj_key;               //        and key
+    // Window-independent layout of the traces (mr_span_index.hip lo_index; tables of <= NS_PMAX
+    // pod-ops): the trace ORDER k_tr_a tiles a graph in (by distinct pod-op count, then code), each
+    // trace's pod-op codes as u16 in that order, its span count, and its exact kind class among the
+    // table's traces (pagerank.py:54-66's key -- distinct op set, fp32(1/len_t) -- is a property of
+    // the trace alone, so a graph's class size is a histogram of the class ids of its traces).  A
+    // window's graphs then tile, fill and set up from these by position, without re-sorting,
+    // re-hashing or gathering per-trace lists in tile order (mr_lo_launch_batch / _prepare_batch).
+    // The window build (k_lo_build_b) reads everything of a trace from these copies in layout
+    // order: its detector inputs (times, max duration, service-op entries), its pod-op entries (code,
+    // span count, first row) and its join entries (dense edge id, multiplicity) -- consecutive lanes,
+    // consecutive traces, contiguous entries.
+    bool lo_ok = false;
+    int32_t lo_nk = 0;                   // kind classes of the table
+    DBuf<int32_t> lo_tr, lo_len, lo_kid; // [NT] by layout index: trace code, span count, kind class
+    DBuf<int64_t> lo_off;                // [NT+1] first entry of each trace in lo16
+    DBuf<uint16_t> lo16, lo_cnt;         // [n_po] pod-op codes (ascending) and span counts, layout order
+    DBuf<int32_t> lo_first;              // [n_po] first row of each pod-op entry
+    DBuf<long long> lo_ts, lo_te, lo_mx; // [NT] trace-level start / end, max duration
+    DBuf<int64_t> lsv_off, le_off;       // [NT+1] service-op entries / join entries of each trace
+    DBuf<uint32_t> lsv, le;              // svcop | count << 16 (code order); dense edge id | count << 16
     // tables ingested from strings (mr_spans_ingest): the first row of each trace / pod-op /
     // service-op code, in code order (the host builds the name lists from them)
     DBuf<int32_t> dict_rows[3];
@@ -441,6 +467,8 @@ struct IxBuild {
     const uint64_t* gkp = nullptr;   // the edge table's keys: gk (hash table) or the table's ekey (dense ids)
     bool dense = false;              // edge counts per dense edge id (gc[ecap], ecap = n_edge_keys)
     bool small = false;   // the one-block node order ran: its sizes are in d_out
+    DBuf<int32_t> pinv;   // layout-order builds (mr_lo_launch_batch): position -> layout index
+    uint32_t* kcnt = nullptr;   // ... and the graph's kind-class histogram (caller's zeroed buffer)
 };
 int mr_ix_launch(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d_mask, mr_graph* g, IxBuild& b, int64_t* d_out);
 struct DetIn;   // (mr_detect_dev.h)
@@ -486,6 +514,21 @@ struct MrWsWin {
 bool mr_win_spectrum_fits(int32_t Na, int32_t Nn, int32_t NP, int32_t k);
 int mr_win_spectrum_launch_n(mr_ctx* ctx, const MrWsWin* ws, int n, int method, int32_t k);
 int mr_ix_finish(mr_ctx* ctx, const mr_spans* sp, mr_graph* g, IxBuild& b, const int64_t* h);
+// Window graph pairs from the tables' layout order (sp->lo_ok; mr_graph_build.hip k_lo_build_b):
+// detector, selection by layout position with the kind histograms, the graphs' per-op and per-edge
+// counts, the node pass; d_outs as mr_ix_launch2_batch's (N, E, overflow, T, nnz per graph; words 5
+// / 6 of each graph's 8 must be zero: the build's totals), dets[k] the window's detector inputs,
+// zw[k] mr_lo_zero_words(sps[k]) zeroed words.  MR_ERR_STATE: a window outside the limits (the
+// caller takes mr_ix_launch2_batch)
+bool mr_lo_fits(const mr_spans* sp);
+int64_t mr_lo_zero_words(const mr_spans* sp);
+int mr_lo_launch_batch(mr_ctx* ctx, int n, const mr_spans* const* sps, mr_graph* const* g0s, mr_graph* const* g1s,
+                       IxBuild* const* b0s, IxBuild* const* b1s, int64_t* const* d_outs, const DetIn* dets,
+                       uint32_t* const* zw);
+// their prepare and PageRank set-up (tiles, ids, kinds, preference, iteration state: pre_ok) in
+// four launches; gs[i] built from sps[i / 2] with builds bs[i]
+int mr_lo_prepare_batch(mr_ctx* ctx, mr_graph* const* gs, const mr_spans* const* sps, IxBuild* const* bs,
+                        const int* anomaly, int n, double d, int precision, std::vector<unsigned char>& keep);
 // a graph of mr_ix_launch / mr_ix_launch2 finished WITHOUT its prepare: the caller prepares many
 // such graphs together (mr_graph_prepare_batch)
 int mr_ix_finish_unprepared(mr_ctx* ctx, const mr_spans* sp, mr_graph* g, IxBuild& b, const int64_t* h);

@@ -1508,6 +1508,143 @@ __global__ void k_pref_apply_b(const SDev* __restrict__ sd, int32_t ng) {
     G.c_tp[i] = G.cd * vf;
 }
 
+// ---------------------------------------------------------------- window graphs in layout order
+// (mr_lo_prepare_batch) A graph whose positions come from its table's layout order (pinv[p] =
+// the layout index of position p): chunk offsets, the lane-interleaved ids (the table's u16 codes
+// relabelled to node ids: node_of_code), w_t / span count / kind class size by position and the
+// preference partials, then the totals, then the preference and iteration state -- the work of
+// k_graph_consts .. k_tr_fill and k_reset_init .. k_pref_apply for these graphs, in four launches.
+struct LDev {
+    int32_t T, N, W, anomaly, fp32;
+    int32_t b_cs, n_cs, b_fill, nbp, b_app;   // first block in each launch; partial blocks
+    int64_t st_off;
+    float cd;
+    double phi, v0;
+    const int32_t* pinv;
+    const int64_t* lo_off;
+    const uint16_t* lo16;
+    const int32_t *lo_len, *lo_kid, *noc;
+    const uint32_t* kcnt;
+    int64_t* c64;
+    int32_t* coff;
+    uint16_t* tids;
+    float *w_tp, *c_tp;
+    double* kind;
+    int32_t* lenp;
+    double *ppart, *scal;
+    int32_t* flag;
+    unsigned long long* mslot;
+    double *sp0, *su0, *su1, *q64;
+    float* q32;
+    const float* u_o;
+};
+__device__ __forceinline__ int32_t ld_graph(const LDev* ld, int32_t n, int32_t blk, int which) {
+    int32_t lo = 0, hi = n - 1;
+    while (lo < hi) {
+        const int32_t mid = (lo + hi + 1) >> 1;
+        const LDev& g = ld[mid];
+        const int32_t s0 = which == 0 ? g.b_cs : which == 1 ? g.b_fill : g.b_app;
+        if (s0 <= blk) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+__global__ void __launch_bounds__(TS_T) k_lo_cs_b(const LDev* __restrict__ ld, int32_t n, unsigned long long* st,
+                                                 uint64_t epoch) {
+    const LDev& G = ld[ld_graph(ld, n, (int32_t)blockIdx.x, 0)];
+    tr_chunk_scan_body((int32_t)blockIdx.x - G.b_cs, G.n_cs, G.pinv, G.lo_off, G.T, G.W, G.c64, G.coff, st + G.st_off,
+                       epoch);
+}
+// thread per (tile, lane) = position: as tr_fill_body (the trace rotated by its index mod len, pads
+// N + lane), ids relabelled; w_t = fp32(1/len_t), the span count and the class size by position;
+// the block's 1/k and 1/len_t sums (pagerank.py:71-78) into ppart
+__global__ void __launch_bounds__(256) k_lo_fill_b(const LDev* __restrict__ ld, int32_t n) {
+    __shared__ double red[256 / WAVE];
+    const LDev& G = ld[ld_graph(ld, n, (int32_t)blockIdx.x, 1)];
+    const int32_t blk = (int32_t)blockIdx.x - G.b_fill;
+    const int64_t i = (int64_t)blk * 256 + threadIdx.x;
+    const int32_t T = G.T, N = G.N;
+    double a = 0.0, b = 0.0;
+    if (i < (int64_t)G.W * WAVE) {
+        const int32_t k = (int32_t)(i / WAVE), lane = (int32_t)(i % WAVE);
+        int64_t e0 = 0, len = 0, rot = 0;
+        if (i < T) {
+            const int32_t ix = G.pinv[i];
+            e0 = G.lo_off[ix];
+            len = G.lo_off[ix + 1] - e0;
+            rot = len ? ix % len : 0;
+            const int32_t L = G.lo_len[ix];
+            const uint32_t kc = G.kcnt[G.lo_kid[ix]];
+            G.w_tp[i] = L > 0 ? (float)(1.0 / (double)L) : 0.0f;
+            G.lenp[i] = L;
+            G.kind[i] = (double)kc;
+            a = 1.0 / (double)kc;
+            b = L ? 1.0 / (double)L : 0.0;
+        }
+        const int64_t nc = G.c64[k + 1] - G.c64[k];
+        unsigned long long* dst = (unsigned long long*)G.tids + (size_t)G.c64[k] * WAVE + lane;
+        constexpr int TF_CH = 4;
+        for (int64_t c0 = 0; c0 < nc; c0 += TF_CH) {
+            uint16_t idv[4 * TF_CH];
+#pragma unroll
+            for (int q = 0; q < 4 * TF_CH; ++q) {
+                const int64_t e = 4 * c0 + q, jx = rot + e;
+                idv[q] = e < len ? (uint16_t)G.noc[G.lo16[e0 + (jx >= len ? jx - len : jx)]] : (uint16_t)(N + lane);
+            }
+#pragma unroll
+            for (int u = 0; u < TF_CH; ++u)
+                if (c0 + u < nc)
+                    dst[(size_t)(c0 + u) * WAVE] = (unsigned long long)idv[4 * u] | (unsigned long long)idv[4 * u + 1] << 16 |
+                                                   (unsigned long long)idv[4 * u + 2] << 32 |
+                                                   (unsigned long long)idv[4 * u + 3] << 48;
+        }
+    }
+    a = block_sum(a, red);
+    b = block_sum(b, red);
+    if (threadIdx.x == 0) {
+        G.ppart[2 * blk] = a;
+        G.ppart[2 * blk + 1] = b;
+    }
+}
+__global__ void __launch_bounds__(1024) k_lo_total_b(const LDev* __restrict__ ld) {   // block g: graph g
+    __shared__ double red[1024 / WAVE];
+    const LDev& G = ld[blockIdx.x];
+    double a = 0.0, b = 0.0;
+    for (int32_t i = threadIdx.x; i < G.nbp; i += blockDim.x) {
+        a += G.ppart[2 * i];
+        b += G.ppart[2 * i + 1];
+    }
+    a = block_sum(a, red);
+    b = block_sum(b, red);
+    if (threadIdx.x == 0) {
+        G.scal[2] = a;
+        G.scal[3] = b;
+    }
+}
+// the preference (pagerank.py:68-85, T4) and the iteration state (k_reset_init_b's) by position
+__global__ void k_lo_apply_b(const LDev* __restrict__ ld, int32_t n) {
+    const LDev& G = ld[ld_graph(ld, n, (int32_t)blockIdx.x, 2)];
+    const int64_t i = (int64_t)((int32_t)blockIdx.x - G.b_app) * blockDim.x + threadIdx.x;
+    const int32_t T = G.T, N = G.N;
+    const double v0 = G.v0;
+    if (i < T) {
+        const double k = G.kind[i];
+        double v;
+        if (!G.anomaly) v = 1.0 / k / G.scal[2];                                                    // :74
+        else v = 1.0 / (k / G.scal[2] * G.phi + 1.0 / (double)G.lenp[i]) / G.scal[3] * G.phi;   // :80-85
+        const float vf = (float)v;
+        G.c_tp[i] = G.cd * vf;   // (1.0 - d) * v in float32 (T4)
+        const double q = (double)G.w_tp[i] * v0;
+        if (G.fp32) G.q32[i] = (float)q; else G.q64[i] = q;
+    }
+    if (i < N) {
+        G.sp0[i] = v0;
+        G.su0[i] = (double)G.u_o[i] * v0;
+    }
+    if (i >= N && i < N + TR_PAD) G.su0[i] = G.su1[i] = 0.0;
+    if (i < MSLOT_WORDS) G.mslot[i] = i < 2 * MSH ? d2bits(1.0) : 0ull;
+    if (i < 4) G.flag[i] = 0;
+    if (i < 8 && i != 2 && i != 3) G.scal[i] = 0.0;
+}
 
 // T_all: traces of the whole graph (all shards) for the initial value
 // perm (relabelled fused graphs): su is kept in the kernel's op labels, su[new] = u_o[perm[new]] s
@@ -1860,14 +1997,12 @@ __device__ __forceinline__ int32_t fx_graph(const GDev* gs, int32_t ng, int32_t 
 
 // ---------------------------------------------------------------- fused iteration: LDS budget and su modes
 constexpr size_t WV_LDS_MAX = 160 * 1024 - 512;
+constexpr int TR_AR_DEFAULT = 1;   // (tr_ar_want)
 // su modes of k_tr_a: global gathers only / every op's su in LDS / the n_hot most covered ops' su in
 // LDS (relabelled graphs, ops [0, n_hot)), the rest gathered
 enum { WV_SU_GLOBAL = 0, WV_SU_ALL = 1, WV_SU_HOT = 2 };
 
 // ---------------------------------------------------------------- fused iteration, trace-parallel (k_tr_a)
-#ifndef MR_TREXP
-#define MR_TREXP 0   // timing experiments only: 1 atomics / 2 su reads at conflict-free addresses
-#endif
 // The single-pass iteration with lane = trace.  At prepare a graph's traces are sorted by op
 // count (tperm: position -> trace) and cut into wave tiles of 64 positions; a tile stores its
 // traces' ids lane-interleaved in chunks of 4 (chunk c = 64 lanes x 4 u16: one coalesced 512-B
@@ -1888,11 +2023,13 @@ struct TrLds {
     int32_t n_hot;    // WV_SU_HOT: su of ops [0, n_hot) in LDS
     // the accumulator first, then su (8-B strides: a 32-lane read group spreads over 32 bank
     // pairs, a 16-lane atomic group over 16)
-    __host__ __device__ TrLds(int32_t N, int mode) {
+    // ar: accumulator replicas (k_tr_a's 512-thread window variant, TR_AR): op o of replica r at
+    // word o * ar + r, lane l adding into replica l mod ar
+    __host__ __device__ TrLds(int32_t N, int mode, int ar = 1) {
         const size_t ns = (size_t)N + TR_PAD;
         su_lds = ns * 16 <= WV_LDS_MAX;
         const bool all = mode == WV_SU_ALL && su_lds;
-        const size_t accb = (ns * 8 + 15) / 16 * 16;
+        const size_t accb = (ns * 8 * (size_t)ar + 15) / 16 * 16;
         n_hot = 0;
         if (mode == WV_SU_HOT && accb < WV_LDS_MAX)
             n_hot = (int32_t)std::min<size_t>((size_t)N, (WV_LDS_MAX - accb) / 8 / 64 * 64);
@@ -1966,7 +2103,7 @@ __device__ __forceinline__ void tr_hot_sums(const GDev& G, const double* su_l, d
         hs[tid] = a;
     }
 }
-template <class Q, int NC, int EXT, int HN>
+template <class Q, int NC, int EXT, int HN, int AR>
 __device__ __forceinline__ int32_t tr_walk_short(const GDev& G, int32_t k, const int32_t ke, int32_t T, int32_t lane,
                                                  int cur, int nxt, double d, double Ms, double xsc, const double* su_l,
                                                  unsigned long long* lacc, double& rmax, TrHot<HN>& H, int32_t& c0,
@@ -2040,24 +2177,21 @@ __device__ __forceinline__ int32_t tr_walk_short(const GDev& G, int32_t k, const
         const unsigned long long X = own ? (unsigned long long)__double2ull_rn((double)r.q * xsc) : 0ull;
         double acc = H.n ? tr_hot_init(H, r.hm, X) : 0.0;
         double sv[2][4];
-        // (MR_TREXP: timing experiments only -- reads / atomics at conflict-free addresses)
-        auto ra = [&](uint32_t o) { return (MR_TREXP & 2) ? (uint32_t)(G.NA + lane) : o; };
-        auto aa = [&](uint32_t o) { return (MR_TREXP & 1) ? (uint32_t)(G.NA + lane) : o; };
         auto rd = [&](const u32x2 w, double* s) {
-            s[0] = su_l[ra(w.x & 0xffffu)];
-            s[1] = su_l[ra(w.x >> 16)];
-            s[2] = su_l[ra(w.y & 0xffffu)];
-            s[3] = su_l[ra(w.y >> 16)];
+            s[0] = su_l[w.x & 0xffffu];
+            s[1] = su_l[w.x >> 16];
+            s[2] = su_l[w.y & 0xffffu];
+            s[3] = su_l[w.y >> 16];
         };
         rd(r.id[0], sv[0]);
 #pragma unroll
         for (int j = 0; j < NC; ++j) {
             if (j + 1 < NC) rd(r.id[j + 1], sv[(j + 1) & 1]);
             const u32x2 w = r.id[j];
-            atomicAdd(&lacc[aa(w.x & 0xffffu)], X);
-            atomicAdd(&lacc[aa(w.x >> 16)], X);
-            atomicAdd(&lacc[aa(w.y & 0xffffu)], X);
-            atomicAdd(&lacc[aa(w.y >> 16)], X);
+            atomicAdd(&lacc[(w.x & 0xffffu) * AR], X);   // (lacc: this lane's replica)
+            atomicAdd(&lacc[(w.x >> 16) * AR], X);
+            atomicAdd(&lacc[(w.y & 0xffffu) * AR], X);
+            atomicAdd(&lacc[(w.y >> 16) * AR], X);
 #pragma unroll
             for (int i = 0; i < 4; ++i) acc += sv[j & 1][i];
         }
@@ -2110,7 +2244,7 @@ __device__ __forceinline__ int32_t tr_walk_short(const GDev& G, int32_t k, const
 // The wave's walk of k_tr_a over its run of wave tiles: per entry one
 // su read, one add into the lane's trace sum, one LDS u64 atomic of X_t; per tile r' of its traces
 // and their next q.  Returns the wave's largest r' (-inf when it owns no trace).
-template <class Q, int SUM, int NT, int EXT = 0, bool HOTT = false>
+template <class Q, int SUM, int NT, int EXT = 0, bool HOTT = false, int AR = 1>
 __device__ __forceinline__ double tr_walk(const GDev& G, int32_t lb, int cur, int nxt, int32_t N, int32_t NH, double d,
                                           double Ms, double xsc, const double* su_l, unsigned long long* lacc,
                                           const double* hs = nullptr) {
@@ -2137,11 +2271,12 @@ __device__ __forceinline__ double tr_walk(const GDev& G, int32_t lb, int cur, in
 #pragma unroll
     for (int h = 0; h < HN; ++h) H.acc[h] = 0ull;
     const int32_t k_first = k;
+    unsigned long long* const lacc_l = lacc + (lane & (AR - 1));   // this lane's accumulator replica
     if constexpr (SUL) {
         // one tier per chunk count (the run's tiles ascend in it): every count static, no branch
         // inside a tile, so each wait is for exactly the LDS reads and loads it consumes
         int32_t tc0 = 0, tn = -1, tq0 = 0, tnq = 0;   // the next tile's ranges, handed from tier to tier
-#define TR_TIER(NC_) if (NC_ <= (NT == 1024 || EXT ? TR_TIERS_EXT : MR_TR_TIERS512) && k < ke) k = tr_walk_short<Q, NC_, EXT, HN>(G, k, ke, T, lane, cur, nxt, d, Ms, xsc, su_l, lacc, rmax, H, tc0, tn, tq0, tnq);
+#define TR_TIER(NC_) if (NC_ <= (NT == 1024 || EXT ? TR_TIERS_EXT : MR_TR_TIERS512) && k < ke) k = tr_walk_short<Q, NC_, EXT, HN, AR>(G, k, ke, T, lane, cur, nxt, d, Ms, xsc, su_l, lacc_l, rmax, H, tc0, tn, tq0, tnq);
         TR_TIER(1) TR_TIER(2) TR_TIER(3) TR_TIER(4) TR_TIER(5) TR_TIER(6) TR_TIER(7) TR_TIER(8)
 #undef TR_TIER
     }
@@ -2182,8 +2317,7 @@ __device__ __forceinline__ double tr_walk(const GDev& G, int32_t lb, int cur, in
                                   (int32_t)(w.y >> 16)};
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const int32_t orr = (MR_TREXP & 2) ? N + lane : o[j];   // (timing experiment: no conflicts)
-                sv[j] = SUL ? su_l[orr] : HOT ? su_l[min(orr, NH - 1)] : 0.0;
+                sv[j] = SUL ? su_l[o[j]] : HOT ? su_l[min(o[j], NH - 1)] : 0.0;
             }
         };
         // ids ring (4 chunks: the current one and three ahead), su ping-pong (current, next)
@@ -2208,7 +2342,7 @@ __device__ __forceinline__ double tr_walk(const GDev& G, int32_t lb, int cur, in
             if (SUL || HOT) lds_su(NXT, SN);                                                               \
             const int32_t o_[4] = {(int32_t)(CUR.x & 0xffffu), (int32_t)(CUR.x >> 16),                     \
                                    (int32_t)(CUR.y & 0xffffu), (int32_t)(CUR.y >> 16)};                    \
-            _Pragma("unroll") for (int j = 0; j < 4; ++j) atomicAdd(&lacc[(MR_TREXP & 1) ? N + lane : o_[j]], X); \
+            _Pragma("unroll") for (int j = 0; j < 4; ++j) atomicAdd(&lacc_l[o_[j] * AR], X);                 \
             _Pragma("unroll") for (int j = 0; j < 4; ++j)                                                  \
                 acc += SUL ? SC[j] : HOT ? (o_[j] < NH ? SC[j] : GC[j]) : GC[j];                          \
             if (++c == ce) {                                                                               \
@@ -2248,7 +2382,7 @@ __device__ __forceinline__ double tr_walk(const GDev& G, int32_t lb, int cur, in
                 unsigned long long a = H.acc[h];
 #pragma unroll
                 for (int m = WAVE / 2; m >= 1; m >>= 1) a += (unsigned long long)__shfl_xor((long long)a, m, WAVE);
-                if (lane == 0) atomicAdd(&lacc[G.hop[h]], a);
+                if (lane == 0) atomicAdd(&lacc[G.hop[h] * AR], a);
             }
     return rmax;
 }
@@ -2396,7 +2530,15 @@ __device__ __forceinline__ void tr_last_finish(const GDev& G, int it, double d, 
     }
 }
 
-template <class Q, int SUM, int NT, int EXT>
+// op o's column of the block's partial row: its AR replicas (integers: the sum is order-free)
+template <int AR>
+__device__ __forceinline__ unsigned long long tr_acc_sum(const unsigned long long* lacc, int32_t o) {
+    unsigned long long v = 0ull;
+#pragma unroll
+    for (int r = 0; r < AR; ++r) v += lacc[(size_t)o * AR + r];
+    return v;
+}
+template <class Q, int SUM, int NT, int EXT, int AR = 1>
 __global__ void __launch_bounds__(NT) k_tr_a(const GDev* __restrict__ gs, int32_t ng, int32_t split, double d,
                                              double alpha, int it, int32_t unused) {
     constexpr bool SUL = SUM == WV_SU_ALL, HOT = SUM == WV_SU_HOT;
@@ -2409,7 +2551,7 @@ __global__ void __launch_bounds__(NT) k_tr_a(const GDev* __restrict__ gs, int32_
     const int cur = it & 1, nxt = cur ^ 1, k3 = it % 3;
     const int32_t N = G.NA;   // (wide graphs: the hot ops)
     const int32_t tid = (int32_t)threadIdx.x;
-    const TrLds L_(N, SUM);
+    const TrLds L_(N, SUM, AR);
     const int32_t NH = HOT ? G.n_hot : 0;   // <= L_.n_hot (the host sizes both alike), >= 64
     const GLB double* sug = gp(G.sub[cur]);   // ids >= N are pads (su 0)
     double* su_l = (double*)(lraw + L_.su);
@@ -2418,10 +2560,9 @@ __global__ void __launch_bounds__(NT) k_tr_a(const GDev* __restrict__ gs, int32_
     const GLB unsigned long long* Mcur = mslot + (size_t)2 * MSH * k3;
     GLB unsigned long long* Mnext = mslot + (size_t)2 * MSH * ((k3 + 1) % 3);
     if (lb == 0 && tid < 2 * MSH) mslot[(size_t)2 * MSH * ((k3 + 2) % 3) + tid] = 0ull;
-    for (int32_t o = tid; o < N + TR_PAD; o += NT) {
-        if (SUL) su_l[o] = o < N ? sug[o] : 0.0;
-        lacc[o] = 0ull;
-    }
+    if (SUL)
+        for (int32_t o = tid; o < N + TR_PAD; o += NT) su_l[o] = o < N ? sug[o] : 0.0;
+    for (int32_t o = tid; o < (N + TR_PAD) * AR; o += NT) lacc[o] = 0ull;
     if (HOT)
         for (int32_t o = tid; o < NH; o += NT) su_l[o] = sug[o];
     __shared__ int s_ssv;   // the call-graph term chunks taken (G.ssv_pre)
@@ -2443,7 +2584,7 @@ __global__ void __launch_bounds__(NT) k_tr_a(const GDev* __restrict__ gs, int32_
         __syncthreads();
     }
     const double xsc = (G.dscale ? G.dscale[0] : G.fx_scale) / msh[1], Ms = msh[0];
-    const double rmax_w = tr_walk<Q, SUM, NT, EXT, HOTT>(G, lb, cur, nxt, N, NH, d, Ms, xsc, su_l, lacc, hs);
+    const double rmax_w = tr_walk<Q, SUM, NT, EXT, HOTT, AR>(G, lb, cur, nxt, N, NH, d, Ms, xsc, su_l, lacc, hs);
     // the call-graph terms of this block's share of the columns, by the waves done walking
     if (G.ssv_pre) tr_ssv_share(G, lb, cur, Ms, &s_ssv, tid & (WAVE - 1));
     __syncthreads();
@@ -2451,7 +2592,7 @@ __global__ void __launch_bounds__(NT) k_tr_a(const GDev* __restrict__ gs, int32_
     if constexpr (NT == 512) {   // (window-graph variant only: the large graphs' kernel stays as it is)
         if (G.lastfin) {
             for (int32_t o = tid; o < N; o += NT)   // write-through: the last block reads them with sc1 loads
-                __hip_atomic_store(prow + o, lacc[o], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(prow + o, tr_acc_sum<AR>(lacc, o), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const double rmax = block_max(rmax_w, red);
             if (tid == 0 && rmax >= 0.0) atomicMax((unsigned long long*)&Mnext[MSH + blockIdx.x % MSH], d2bits(rmax));
             tr_last_finish<NT>(G, it, d, Ms, Mnext);
@@ -2459,9 +2600,10 @@ __global__ void __launch_bounds__(NT) k_tr_a(const GDev* __restrict__ gs, int32_
         }
     }
     if (G.row_wt)   // write-through (sc1): the boundary to k_fx_b has no dirty lines to write back
-        for (int32_t o = tid; o < N; o += NT) __hip_atomic_store(prow + o, lacc[o], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int32_t o = tid; o < N; o += NT)
+            __hip_atomic_store(prow + o, tr_acc_sum<AR>(lacc, o), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     else
-        for (int32_t o = tid; o < N; o += NT) prow[o] = lacc[o];
+        for (int32_t o = tid; o < N; o += NT) prow[o] = tr_acc_sum<AR>(lacc, o);
     const double rmax = block_max(rmax_w, red);
     if (tid == 0 && rmax >= 0.0)   // -inf: a block without traces (an empty shard's placeholder)
         atomicMax((unsigned long long*)&Mnext[MSH + blockIdx.x % MSH], d2bits(rmax));
@@ -3017,7 +3159,13 @@ void mr_prof_end(mr_ctx* ctx, double bytes, int64_t iters = 1);
 using TrA = void (*)(const GDev*, int32_t, int32_t, double, double, int, int32_t);
 // ext: some graph of the launch carries kind multiplicities (bit 0: mw_tp) or a cold side (bit 1:
 // wide graphs) -- only the short-tile walk of the su-in-LDS mode distinguishes them
-static TrA tr_kernel(bool fp32, int mode, int NT, int ext = 0) {
+// ar > 1: the 512-thread su-in-LDS variant with accumulator replicas (TR_AR; no ext)
+static TrA tr_kernel(bool fp32, int mode, int NT, int ext = 0, int ar = 1) {
+    static const TrA tab_ar[2][4] = {
+        {k_tr_a<double, 1, 512, 0, 2>, k_tr_a<double, 1, 512, 0, 4>, k_tr_a<double, 1, 512, 0, 8>, k_tr_a<double, 1, 512, 0, 16>},
+        {k_tr_a<float, 1, 512, 0, 2>, k_tr_a<float, 1, 512, 0, 4>, k_tr_a<float, 1, 512, 0, 8>, k_tr_a<float, 1, 512, 0, 16>}};
+    if (ar > 1 && !ext && mode == WV_SU_ALL && NT == 512)
+        return tab_ar[fp32 ? 1 : 0][ar == 2 ? 0 : ar == 4 ? 1 : ar == 8 ? 2 : 3];
     static const TrA tab[2][3][2] = {
         {{k_tr_a<double, 0, 512, 0>, k_tr_a<double, 0, 1024, 0>},
          {k_tr_a<double, 1, 512, 0>, k_tr_a<double, 1, 1024, 0>},
@@ -3050,7 +3198,17 @@ struct FxPlan {
     int NT = 1024;      // block size (16 waves; 512 when the graphs are small)
     int mode = WV_SU_ALL;   // su in LDS for every fused graph of the batch / hot ops / none
     bool sul = true;    // mode == WV_SU_ALL
+    int ar = 1;         // accumulator replicas (tr_kernel)
 };
+// k_tr_a's accumulator replicas for the 512-thread window variant: the LDS u64 adds of a 16-lane
+// group go to bank pairs (op * AR + lane mod AR) mod 16, so lanes of different replicas never
+// share a bank pair and the random-op bank conflicts (and the same-address adds of popular ops)
+// fall with AR.  MR_TR_AR (read per call): 1 / 2 / 4 / 8 / 16
+static int tr_ar_want() {
+    const char* e = getenv("MR_TR_AR");
+    const int v = e ? atoi(e) : TR_AR_DEFAULT;
+    return v >= 16 ? 16 : v >= 8 ? 8 : v >= 4 ? 4 : v >= 2 ? 2 : 1;
+}
 static FxPlan fx_plan(mr_graph* const* gs, int ng) {
     FxPlan P;
     int32_t nmax = 0;
@@ -3073,17 +3231,22 @@ static FxPlan fx_plan(mr_graph* const* gs, int ng) {
         for (int i = 0; i < ng; ++i)
             if (gs[i]->fused && !gs[i]->relabeled) P.mode = WV_SU_GLOBAL;
     if (P.mode == WV_SU_HOT && TrLds(nmax, WV_SU_HOT).n_hot < 64) P.mode = WV_SU_GLOBAL;
+    bool plain = P.NT == 512 && P.mode == WV_SU_ALL;   // (kind-compressed / wide graphs: no replicas)
+    for (int i = 0; i < ng; ++i)
+        if (gs[i]->fused) plain = plain && !gs[i]->mw_tp.p && !gs[i]->wide && !gs[i]->nhr;
+    if (plain)
+        for (P.ar = tr_ar_want(); P.ar > 1 && TrLds(nmax, WV_SU_ALL, P.ar).total > WV_LDS_MAX; P.ar >>= 1) {}
     return P;
 }
 static int32_t plan_n_hot(int32_t N, const FxPlan& P) {
     return P.mode == WV_SU_HOT ? TrLds(N, WV_SU_HOT).n_hot : 0;
 }
-static size_t plan_lds(int32_t N, const FxPlan& P) { return TrLds(N, P.mode).total; }
+static size_t plan_lds(int32_t N, const FxPlan& P) { return TrLds(N, P.mode, P.ar).total; }
 
 // resident blocks of the plan's kernel on the chip (occupancy by LDS image and VGPRs)
 static int64_t plan_resident(int32_t N, const FxPlan& P) {
     const size_t lds = plan_lds(N, P);
-    const TrA kfn = tr_kernel(false, P.mode, P.NT);
+    const TrA kfn = tr_kernel(false, P.mode, P.NT, 0, P.ar);
     int n = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, (const void*)kfn, P.NT, lds) != hipSuccess || n < 1)
         n = std::max<int>(1, (int)(WV_LDS_MAX / std::max<size_t>(lds, 1)));
@@ -3106,18 +3269,9 @@ static double tr_budget() {
     return v;
 }
 // a tile's fixed cost in chunks for the per-wave cut: its q / r words and r' (about two chunks),
-// plus the hot-op accumulators and mask sum on hot-op layouts (MR_TR_TILEW / MR_TR_TILEW_HOT)
-static double tr_tile_weight(const mr_graph* g) {
-    static const double w0 = [] {
-        const char* e = getenv("MR_TR_TILEW");
-        return e ? atof(e) : 2.0;
-    }();
-    static const double wh = [] {
-        const char* e = getenv("MR_TR_TILEW_HOT");
-        return e ? atof(e) : 3.0;
-    }();
-    return g->nhr ? wh : w0;
-}
+// plus the hot-op accumulators and mask sum on hot-op layouts (3: with 2 the waves of short hot
+// tiles became a tail, C4 188 us per iteration)
+static double tr_tile_weight(const mr_graph* g) { return g->nhr ? 3.0 : 2.0; }
 static int tr_split(mr_ctx* ctx, mr_graph* g, const FxPlan& P, int64_t wsum, int64_t* nfa,
                     std::vector<CutArg>* defer = nullptr, int64_t force_nb = 0) {
     const int64_t W = g->n_wt, NW = P.NT / WAVE;
@@ -3775,8 +3929,10 @@ static int graph_kinds(mr_ctx* ctx, mr_graph* g, bool chk, bool ktab, uint64_t c
 
 // (plan-independent: a window's graphs are set up on the stream that built them, before the
 // batch's plan exists -- mr_pagerank_presetup)
+static int lo_setup_one(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool fp32);
 static int pagerank_setup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool fp32, uint32_t flags, bool sharded,
                           uint64_t seed, uint64_t hmask) {
+    if (g->lo) return lo_setup_one(ctx, g, anomaly, d, fp32);   // (exact kind classes: no seed to vary)
     hipStream_t st = ctx->stream;
     const int32_t N = g->N, T = g->T;
     // Kinds through a global hash table (k_kind_insert) while it stays cache-resident, and for one
@@ -4341,7 +4497,7 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
     for (int i = 0; i < ng; ++i)   // the wide variant carries HOT_MAX_WIDE hot accumulators
         if ((any_ext & 2) && gs[i]->fused && gs[i]->nhr > HOT_MAX_WIDE)
             return mr_fail(ctx, MR_ERR_ARG, "pagerank batch: a hot-op layout of %d ops beside a wide graph", gs[i]->nhr);
-    const TrA tr_a = tr_kernel(fp32, plan.mode, plan.NT, any_ext);
+    const TrA tr_a = tr_kernel(fp32, plan.mode, plan.NT, any_ext, any_ext ? 1 : plan.ar);
     // a sharded graph with no collective backend is one whole shard: the split launches around the
     // (no-op) all-reduces would compute the same integers / sums in two halves
     const bool coll = sharded && mr_coll_ready(ctx);
@@ -4350,14 +4506,9 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
     bool any_wide = false;
     for (int i = 0; i < ng; ++i) any_wide = any_wide || gs[i]->wide;
     // k_fx_b's block size: 4 waves when no graph of the launch has many partial rows
-    static const int fb_force = [] {
-        const char* e = getenv("MR_FB_W");
-        return e ? atoi(e) : 0;
-    }();
     bool fb_small = !any_wide;
     // (a large graph alone -- C4: 256 rows of 10k ops -- sums faster with 16-wave blocks: 137 -> 134 us)
     for (int i = 0; i < ng; ++i) fb_small = fb_small && hv[(size_t)i].n_fa <= FB_SMALL_ROWS && hv[(size_t)i].N <= 4096;
-    if (fb_force) fb_small = fb_force == FB_W_SMALL;
     static const bool no_side = getenv("MR_WIDE_SERIAL") != nullptr;   // A/B knob: one stream
     hipStream_t sst = st;
     if (any_wide && !no_side) {
@@ -4568,6 +4719,161 @@ int mr_pagerank_presetup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, int pr
     g->pre_seed = kind_seed(0);
     g->pre_hmask = kind_hmask(0);
     return MR_OK;
+}
+
+// ---------------------------------------------------------------- window graphs in layout order
+// the iteration state's buffers of a layout-order graph and its LDev set-up fields
+static int lo_state(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool fp32, LDev& v) {
+    const int32_t N = g->N, T = g->T;
+    MR_TRY(g->flag.alloc(ctx, 8));
+    MR_TRY(g->scal.alloc(ctx, 8));
+    MR_TRY(g->mslot.alloc(ctx, MSLOT_WORDS));
+    MR_TRY(g->sn.alloc(ctx, (size_t)N));
+    MR_TRY(g->spb[0].alloc(ctx, (size_t)N));
+    MR_TRY(g->spb[1].alloc(ctx, (size_t)N));
+    MR_TRY(g->sub[0].alloc(ctx, (size_t)N + TR_PAD));
+    MR_TRY(g->sub[1].alloc(ctx, (size_t)N + TR_PAD));
+    MR_TRY(g->weight.alloc(ctx, (size_t)N));
+    MR_TRY(g->fx_ssv.alloc(ctx, (size_t)N));
+    MR_TRY(g->c_tp.alloc(ctx, (size_t)std::max(T, 1)));
+    for (int j = 0; j < 2; ++j) {
+        if (fp32) MR_TRY(g->q32[j].alloc(ctx, (size_t)T + 1));   // [T]: k_tr_a's pad slot
+        else MR_TRY(g->q64[j].alloc(ctx, (size_t)T + 1));
+    }
+    v.T = T;
+    v.N = N;
+    v.anomaly = anomaly;
+    v.fp32 = fp32 ? 1 : 0;
+    v.cd = (float)(1.0 - d);
+    v.phi = g->phi;
+    v.v0 = 1.0 / (double)((int64_t)N + T);   // pagerank.py:118-119
+    v.nbp = g->lo_nbp;
+    v.w_tp = g->w_tp.p;
+    v.c_tp = g->c_tp.p;
+    v.kind = g->kind.p;
+    v.lenp = g->lo_lenp.p;
+    v.ppart = g->ppart.p;
+    v.scal = g->scal.p;
+    v.flag = g->flag.p;
+    v.mslot = g->mslot.p;
+    v.sp0 = g->spb[0].p;
+    v.su0 = g->sub[0].p;
+    v.su1 = g->sub[1].p;
+    v.q64 = g->q64[0].p;
+    v.q32 = g->q32[0].p;
+    v.u_o = g->u_o.p;
+    return MR_OK;
+}
+static void lo_mark_presetup(mr_graph* g, int anomaly, double d, bool fp32) {
+    g->pre_ok = true;
+    g->pre_anomaly = anomaly;
+    g->pre_d = d;
+    g->pre_phi = g->phi;
+    g->pre_fp32 = fp32;
+    g->pre_flags = 0;
+    g->pre_seed = kind_seed(0);
+    g->pre_hmask = kind_hmask(0);
+}
+// pagerank_setup of a layout-order graph (a call that did not take its presetup: a group rerun):
+// its kind class sizes, span counts and preference partials by position are kept on the graph
+static int lo_setup_one(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool fp32) {
+    std::vector<unsigned char> keep(sizeof(LDev), 0);
+    LDev& v = *reinterpret_cast<LDev*>(keep.data());
+    MR_TRY(lo_state(ctx, g, anomaly, d, fp32, v));
+    v.b_app = 0;
+    DBuf<LDev> dl;
+    MR_TRY(dl.upload(ctx, &v, 1));
+    hipStream_t st = ctx->stream;
+    hipLaunchKernelGGL(k_lo_total_b, dim3(1), dim3(1024), 0, st, dl.p);
+    const int64_t na = std::max<int64_t>({(int64_t)g->T, (int64_t)g->N + TR_PAD, MSLOT_WORDS, 8});
+    hipLaunchKernelGGL(k_lo_apply_b, dim3(cdiv(na, 256)), dim3(256), 0, st, dl.p, 1);
+    MR_TRY_HIP(ctx, hipGetLastError());
+    MR_TRY_HIP(ctx, hipStreamSynchronize(st));   // (the host descriptor leaves scope)
+    return MR_OK;
+}
+
+int mr_lo_prepare_batch(mr_ctx* ctx, mr_graph* const* gs, const mr_spans* const* sps, IxBuild* const* bs,
+                        const int* anomaly, int n, double d, int precision, std::vector<unsigned char>& keep) {
+    if (n <= 0) return MR_OK;
+    const bool fp32 = precision == MR_FP32;
+    hipStream_t st = ctx->stream;
+    keep.assign((size_t)n * sizeof(LDev), 0);
+    LDev* hv = reinterpret_cast<LDev*>(keep.data());
+    std::vector<DBuf<int64_t>> c64((size_t)n);
+    int32_t bcs = 0, bfl = 0, bap = 0;
+    int64_t st_words = 0;
+    for (int i = 0; i < n; ++i) {
+        mr_graph* g = gs[i];
+        const mr_spans* sp = sps[i];
+        const IxBuild& b = *bs[i];
+        const int32_t N = g->N, T = g->T, W = cdiv(T, WAVE);
+        const int64_t nnz = g->nnz_sr;
+        if (N <= 0 || T <= 0 || N > FX_NMAX || !TrLds(N, WV_SU_ALL).su_lds || nnz >= (1ll << 31))
+            return mr_fail(ctx, MR_ERR_STATE, "mr_lo_prepare_batch: graph outside the layout-order limits");
+        g->lo = true;
+        g->rs_is_sr = true;
+        g->pr_identity = true;
+        g->n_pr = T;
+        g->traces_nonempty = true;
+        g->cov_ready = true;
+        g->nhr = 0;
+        g->hmask.reset();
+        g->relabeled = false;
+        g->wide = false;
+        g->NA = N;
+        g->fused = true;
+        g->perm.reset();
+        g->rsp.reset();
+        g->n_wt = W;
+        g->wtile_nw = 0;
+        g->coff_h.clear();
+        g->n_tiles = 0;
+        g->n_pairs = 0;
+        g->tpos_ok = false;
+        g->lo_nbp = cdiv((int64_t)W * WAVE, 256);
+        MR_TRY(g->w_tp.alloc(ctx, (size_t)T));
+        MR_TRY(g->kind.alloc(ctx, (size_t)T));
+        MR_TRY(g->lo_lenp.alloc(ctx, (size_t)T));
+        MR_TRY(g->ppart.alloc(ctx, 2 * (size_t)g->lo_nbp));
+        MR_TRY(g->coff.alloc(ctx, (size_t)W + 1));
+        MR_TRY(c64[(size_t)i].alloc(ctx, (size_t)W + 1));
+        const int64_t nch = 2 * (int64_t)W + (nnz / WAVE + 2 * (int64_t)N) / 4 + 2;   // as tr_layout
+        MR_TRY(g->tids.alloc(ctx, (size_t)std::max<int64_t>(nch, 1) * WAVE * 4));
+        LDev& v = hv[i];
+        MR_TRY(lo_state(ctx, g, anomaly[i], d, fp32, v));
+        v.W = W;
+        v.n_cs = (int32_t)std::max<int64_t>(cdiv((int64_t)W, TS_TILE), 1);
+        v.st_off = st_words;
+        st_words += v.n_cs;
+        v.b_cs = bcs;
+        bcs += v.n_cs;
+        v.b_fill = bfl;
+        bfl += g->lo_nbp;
+        v.b_app = bap;
+        bap += cdiv(std::max<int64_t>({(int64_t)T, (int64_t)N + TR_PAD, MSLOT_WORDS, 8}), 256);
+        v.pinv = b.pinv.p;
+        v.lo_off = sp->lo_off.p;
+        v.lo16 = sp->lo16.p;
+        v.lo_len = sp->lo_len.p;
+        v.lo_kid = sp->lo_kid.p;
+        v.noc = b.node_of_code.p;
+        v.kcnt = b.kcnt;
+        v.c64 = c64[(size_t)i].p;
+        v.coff = g->coff.p;
+        v.tids = g->tids.p;
+        lo_mark_presetup(g, anomaly[i], d, fp32);
+    }
+    DBuf<LDev> dl;
+    MR_TRY(dl.upload(ctx, hv, (size_t)n));
+    unsigned long long* dst = nullptr;
+    uint64_t epoch = 0;
+    MR_TRY(mr_dl_status(ctx, st_words, &dst, &epoch));
+    hipLaunchKernelGGL(k_lo_cs_b, dim3(bcs), dim3(TS_T), 0, st, dl.p, n, dst, epoch);
+    hipLaunchKernelGGL(k_lo_fill_b, dim3(bfl), dim3(256), 0, st, dl.p, n);
+    hipLaunchKernelGGL(k_lo_total_b, dim3(n), dim3(1024), 0, st, dl.p);
+    hipLaunchKernelGGL(k_lo_apply_b, dim3(bap), dim3(256), 0, st, dl.p, n);
+    MR_TRY_HIP(ctx, hipGetLastError());
+    return MR_OK;   // (scratch returns to the stream-ordered pool)
 }
 
 int mr_pagerank_batch_impl(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly, int ng, double d, double alpha,

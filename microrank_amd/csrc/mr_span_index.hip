@@ -201,6 +201,108 @@ __global__ void k_ix_edge_runs(const uint64_t* key, const int32_t* head, const i
     atomicAdd(&truns[t], 1);
 }
 
+// ---------------------------------------------------------------- layout order (lo_index)
+// Traces sorted by distinct pod-op count, then code: key n << nbt | t
+__global__ void k_lo_keys(const int64_t* po_off, int32_t NT, int nbt, uint64_t* key) {
+    const int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < NT) key[t] = ((uint64_t)(po_off[t + 1] - po_off[t]) << nbt) | (uint32_t)t;
+}
+__global__ void k_lo_unpack(const uint64_t* key, int32_t NT, int nbt, const int32_t* tlen, int32_t* lo_tr, int32_t* lo_n,
+                            int32_t* lo_len) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= NT) return;
+    const uint64_t k = key[i];
+    const int32_t t = (int32_t)(k & ((1ull << nbt) - 1ull));
+    lo_tr[i] = t;
+    lo_n[i] = (int32_t)(k >> nbt);
+    lo_len[i] = tlen[t];
+}
+// each trace's entries into its layout slot: pod-op codes / span counts / first rows, its detector
+// scalars, and its service-op and join entry counts (the copies below); bad: a count or code past
+// the 16-bit packing (the table then keeps the general window path)
+__global__ void k_lo_copy(const int32_t* lo_tr, const int64_t* lo_off, int32_t NT, const int64_t* po_off,
+                          const int32_t* po_op, const int32_t* po_cnt, const int32_t* po_first, const long long* tts,
+                          const long long* tte, const long long* tmaxd, const int64_t* sv_off, const int64_t* ed_off,
+                          uint16_t* lo16, uint16_t* lo_cnt, int32_t* lo_first, long long* lo_ts, long long* lo_te,
+                          long long* lo_mx, int32_t* nsv, int32_t* ned, int32_t* bad) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= NT) return;
+    const int32_t t = lo_tr[i];
+    const int64_t a = po_off[t], n = po_off[t + 1] - a, o = lo_off[i];
+    bool big = false;
+    for (int64_t e = 0; e < n; ++e) {
+        const int32_t c = po_cnt[a + e];
+        big = big || c > 65535;
+        lo16[o + e] = (uint16_t)po_op[a + e];
+        lo_cnt[o + e] = (uint16_t)c;
+        lo_first[o + e] = po_first[a + e];
+    }
+    lo_ts[i] = tts[t];
+    lo_te[i] = tte[t];
+    lo_mx[i] = tmaxd[t];
+    nsv[i] = (int32_t)(sv_off[t + 1] - sv_off[t]);
+    ned[i] = (int32_t)(ed_off[t + 1] - ed_off[t]);
+    if (big) atomicOr(bad, 1);
+}
+__global__ void k_lo_copy2(const int32_t* lo_tr, int32_t NT, const int64_t* sv_off, const int32_t* sv_op,
+                           const int32_t* sv_cnt, const int64_t* ed_off, const int32_t* ed_eid, const int32_t* ed_cnt,
+                           const int64_t* lsv_off, const int64_t* le_off, uint32_t* lsv, uint32_t* le, int32_t* bad) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= NT) return;
+    const int32_t t = lo_tr[i];
+    bool big = false;
+    for (int64_t e = sv_off[t], o = lsv_off[i]; e < sv_off[t + 1]; ++e, ++o) {
+        const int32_t op = sv_op[e], c = sv_cnt[e];
+        big = big || op > 65535 || c > 65535;
+        lsv[o] = (uint32_t)(uint16_t)op | ((uint32_t)(uint16_t)c << 16);
+    }
+    for (int64_t e = ed_off[t], o = le_off[i]; e < ed_off[t + 1]; ++e, ++o) {
+        const int32_t id = ed_eid[e], c = ed_cnt[e];
+        big = big || id > 65535 || c > 65535;
+        le[o] = (uint32_t)(uint16_t)id | ((uint32_t)(uint16_t)c << 16);
+    }
+    if (big) atomicOr(bad, 1);
+}
+// the set hash of each trace's kind key (pagerank.py:54-66: op set, fp32(1/len_t), count; order-free)
+__device__ __forceinline__ uint64_t lo_mix(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__global__ void k_lo_hash(const int64_t* lo_off, const uint16_t* lo16, const int32_t* lo_len, int32_t NT, uint64_t seed,
+                          uint64_t* hkey, uint32_t* hval) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= NT) return;
+    const int64_t o = lo_off[i], n = lo_off[i + 1] - o;
+    uint64_t acc = 0;
+    for (int64_t e = 0; e < n; ++e) acc += lo_mix((uint64_t)lo16[o + e] ^ seed);
+    const float w = lo_len[i] > 0 ? (float)(1.0 / (double)lo_len[i]) : 0.0f;
+    hkey[i] = lo_mix(lo_mix(seed ^ (uint64_t)__float_as_uint(w) ^ ((uint64_t)n << 32)) + acc);
+    hval[i] = (uint32_t)i;
+}
+// classes = runs of equal hashes (sorted); the run's first member (smallest layout index: the
+// sort is stable) is its representative, and every member is compared with it exactly
+__global__ void k_lo_reps(const int32_t* head, const int64_t* hpos, const uint32_t* hval, int32_t NT, int32_t* rep) {
+    const int32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < NT && head[j]) rep[hpos[j]] = (int32_t)hval[j];
+}
+__global__ void k_lo_classes(const int32_t* head, const int64_t* hpos, const uint32_t* hval, const int32_t* rep,
+                             int32_t NT, const int64_t* lo_off, const uint16_t* lo16, const int32_t* lo_len,
+                             int32_t* lo_kid, int32_t* bad) {
+    const int32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= NT) return;
+    const int32_t k = (int32_t)hpos[j] + head[j] - 1, i = (int32_t)hval[j], r = rep[k];
+    lo_kid[i] = k;
+    if (r == i) return;
+    const int64_t a = lo_off[i], n = lo_off[i + 1] - a, b = lo_off[r];
+    const float wi = lo_len[i] > 0 ? (float)(1.0 / (double)lo_len[i]) : 0.0f;
+    const float wr = lo_len[r] > 0 ? (float)(1.0 / (double)lo_len[r]) : 0.0f;
+    bool eq = n == lo_off[r + 1] - b && __float_as_uint(wi) == __float_as_uint(wr);
+    for (int64_t e = 0; eq && e < n; ++e) eq = lo16[a + e] == lo16[b + e];
+    if (!eq) atomicOr(bad, 1);
+}
+
 // ---------------------------------------------------------------- window detector (uniform times)
 // (the per-block body: mr_detect_dev.h)
 __global__ void __launch_bounds__(DB) k_ix_detect(int32_t NT, DetIn d) {
@@ -332,6 +434,96 @@ static int trace_runs(mr_ctx* ctx, const mr_spans* s, const int32_t* code, int32
     MR_TRY_HIP(ctx, hipStreamSynchronize(st));   // scratch is freed on return
     *n_runs = R;
     return MR_OK;
+}
+
+// The table's layout order, u16 code lists and exact kind classes (mr_spans.lo_*): window graphs
+// of tables within the one-pass limits tile from them (mr_lo_launch_batch).  A hash collision
+// that the exact comparison finds retries with the next seed; after four the table keeps the
+// general window path (lo_ok false).
+static int lo_index(mr_ctx* ctx, mr_spans* s) {
+    hipStream_t st = ctx->stream;
+    const int32_t NT = s->n_traces;
+    s->lo_ok = false;
+    if (!mr_lo_fits(s) || s->n_po >= ((int64_t)1 << 31) || s->n_sv >= ((int64_t)1 << 31) ||
+        s->n_ed >= ((int64_t)1 << 31))
+        return MR_OK;
+    const int nbt = std::max(1, bits_for((uint64_t)std::max(NT - 1, 0)));
+    const int nbn = bits_for((uint64_t)s->n_podops);
+    DBuf<uint64_t> key;
+    DBuf<uint32_t> hval;
+    DBuf<int32_t> lo_n, nsv, ned, head, rep, bad;
+    DBuf<int64_t> hpos, tmp;
+    MR_TRY(key.alloc(ctx, (size_t)NT));
+    MR_TRY(hval.alloc(ctx, (size_t)NT));
+    MR_TRY(lo_n.alloc(ctx, (size_t)NT));
+    MR_TRY(nsv.alloc(ctx, (size_t)NT));
+    MR_TRY(ned.alloc(ctx, (size_t)NT));
+    MR_TRY(head.alloc(ctx, (size_t)NT));
+    MR_TRY(rep.alloc(ctx, (size_t)NT));
+    MR_TRY(hpos.alloc(ctx, (size_t)NT + 1));
+    MR_TRY(tmp.alloc(ctx, (size_t)scan_tmp_elems(NT)));
+    MR_TRY(bad.zero(ctx, 1));
+    MR_TRY(s->lo_tr.alloc(ctx, (size_t)NT));
+    MR_TRY(s->lo_len.alloc(ctx, (size_t)NT));
+    MR_TRY(s->lo_kid.alloc(ctx, (size_t)NT));
+    MR_TRY(s->lo_off.alloc(ctx, (size_t)NT + 1));
+    MR_TRY(s->lo16.alloc(ctx, (size_t)std::max<int64_t>(s->n_po, 1)));
+    MR_TRY(s->lo_cnt.alloc(ctx, (size_t)std::max<int64_t>(s->n_po, 1)));
+    MR_TRY(s->lo_first.alloc(ctx, (size_t)std::max<int64_t>(s->n_po, 1)));
+    MR_TRY(s->lo_ts.alloc(ctx, (size_t)NT));
+    MR_TRY(s->lo_te.alloc(ctx, (size_t)NT));
+    MR_TRY(s->lo_mx.alloc(ctx, (size_t)NT));
+    MR_TRY(s->lsv_off.alloc(ctx, (size_t)NT + 1));
+    MR_TRY(s->le_off.alloc(ctx, (size_t)NT + 1));
+    MR_TRY(s->lsv.alloc(ctx, (size_t)std::max<int64_t>(s->n_sv, 1)));
+    MR_TRY(s->le.alloc(ctx, (size_t)std::max<int64_t>(s->n_ed, 1)));
+    hipLaunchKernelGGL(k_lo_keys, dim3(cdiv(NT, XB)), dim3(XB), 0, st, s->po_off.p, NT, nbt, key.p);
+    {
+        SortScratch ws;
+        MR_TRY(mr_radix_sort(ctx, key.p, nullptr, NT, nbt + nbn, ws));
+        hipLaunchKernelGGL(k_lo_unpack, dim3(cdiv(NT, XB)), dim3(XB), 0, st, key.p, NT, nbt, s->tlen.p, s->lo_tr.p, lo_n.p,
+                           s->lo_len.p);
+        MR_TRY(mr_exclusive_scan_i32(ctx, lo_n.p, s->lo_off.p, NT, tmp.p));
+        hipLaunchKernelGGL(k_lo_copy, dim3(cdiv(NT, XB)), dim3(XB), 0, st, s->lo_tr.p, s->lo_off.p, NT, s->po_off.p,
+                           s->po_op.p, s->po_cnt.p, s->po_first.p, s->tts.p, s->tte.p, s->tmaxd.p, s->sv_off.p,
+                           s->ed_off.p, s->lo16.p, s->lo_cnt.p, s->lo_first.p, s->lo_ts.p, s->lo_te.p, s->lo_mx.p, nsv.p,
+                           ned.p, bad.p);
+        MR_TRY(mr_exclusive_scan_i32(ctx, nsv.p, s->lsv_off.p, NT, tmp.p));
+        MR_TRY(mr_exclusive_scan_i32(ctx, ned.p, s->le_off.p, NT, tmp.p));
+        hipLaunchKernelGGL(k_lo_copy2, dim3(cdiv(NT, XB)), dim3(XB), 0, st, s->lo_tr.p, NT, s->sv_off.p, s->sv_op.p,
+                           s->sv_cnt.p, s->ed_off.p, s->ed_eid.p, s->ed_cnt.p, s->lsv_off.p, s->le_off.p, s->lsv.p,
+                           s->le.p, bad.p);
+        MR_TRY_HIP(ctx, hipGetLastError());
+        int32_t hb = 0;
+        MR_TRY(bad.download(ctx, &hb, 1));
+        MR_TRY_HIP(ctx, hipStreamSynchronize(st));   // (the sort's scratch leaves scope)
+        if (hb) return MR_OK;   // (counts or codes past 16 bits: the general window path)
+    }
+    for (int attempt = 0; attempt < 4; ++attempt) {
+        const uint64_t seed = 0x51ed270b27a3c0deull + 0x9E3779B97F4A7C15ull * (uint64_t)attempt;
+        MR_TRY(bad.zero(ctx, 1));
+        hipLaunchKernelGGL(k_lo_hash, dim3(cdiv(NT, XB)), dim3(XB), 0, st, s->lo_off.p, s->lo16.p, s->lo_len.p, NT, seed,
+                           key.p, hval.p);
+        SortScratch ws;
+        MR_TRY(mr_radix_sort(ctx, key.p, hval.p, NT, 64, ws));
+        hipLaunchKernelGGL(k_ix_heads, dim3(cdiv(NT, XB)), dim3(XB), 0, st, key.p, (int64_t)NT, head.p);
+        MR_TRY(mr_exclusive_scan_i32(ctx, head.p, hpos.p, NT, tmp.p));
+        hipLaunchKernelGGL(k_lo_reps, dim3(cdiv(NT, XB)), dim3(XB), 0, st, head.p, hpos.p, hval.p, NT, rep.p);
+        hipLaunchKernelGGL(k_lo_classes, dim3(cdiv(NT, XB)), dim3(XB), 0, st, head.p, hpos.p, hval.p, rep.p, NT,
+                           s->lo_off.p, s->lo16.p, s->lo_len.p, s->lo_kid.p, bad.p);
+        MR_TRY_HIP(ctx, hipGetLastError());
+        int64_t nk = 0;
+        int32_t hb = 0;
+        MR_TRY_HIP(ctx, hipMemcpyAsync(&nk, hpos.p + NT, sizeof nk, hipMemcpyDeviceToHost, st));
+        MR_TRY(bad.download(ctx, &hb, 1));
+        MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+        if (hb == 0) {
+            s->lo_nk = (int32_t)nk;
+            s->lo_ok = true;
+            return MR_OK;
+        }
+    }
+    return MR_OK;   // (four colliding seeds: the general window path)
 }
 
 int mr_spans_index(mr_ctx* ctx, mr_spans* s) {
@@ -488,6 +680,7 @@ int mr_spans_index(mr_ctx* ctx, mr_spans* s) {
     MR_TRY_HIP(ctx, hipStreamSynchronize(st));
     s->uniform_times = s->has_times && hb == 0;
     s->indexed = true;
+    if (!getenv("MR_NO_LO")) MR_TRY(lo_index(ctx, s));   // (A/B and tests, read per table: the general window build)
     return MR_OK;
 }
 

@@ -616,42 +616,6 @@ def test_windows_batch_fast_paths_equal_general_paths(c3_window, monkeypatch):
         d.close()
 
 
-def test_windows_batch_second_pagerank_stream(c3_window, monkeypatch):
-    """MR_WIN_PR_STREAMS=2: odd window groups ranked on a second context (its own stream, pool and
-    scratch) give bitwise the results of one PageRank stream -- groups of one and two windows, two
-    calls on one context (the second reuses the first call's contexts)."""
-    import bench
-    from microrank_amd import _lib
-    from microrank_amd.online_rca import rank_windows
-    from microrank_amd.preprocess_data import DeviceSpans
-
-    ctx = _lib.default_context()
-    normal, abnormal, t0, t1 = c3_window
-    a3, ok = bench.slo_from_gpu(ctx, normal)
-    devs = [DeviceSpans(ctx, abnormal)]
-    wins = [(devs[0], t0, t1, a3, ok)]
-    for seed in (94, 95, 96, 97, 98):
-        _, nrm, ab = bench.make_window(seed, 500, 20_000)
-        s3, sok = bench.slo_from_gpu(ctx, nrm)
-        d = DeviceSpans(ctx, ab)
-        devs.append(d)
-        u0 = int(ab.tstart.min())
-        wins.append((d, u0, u0 + 5 * 60 * 10**9, s3, sok))
-    runs = {}
-    for group in ("1", "2"):
-        monkeypatch.setenv("MR_WIN_GROUP", group)
-        for ns in ("1", "2"):
-            monkeypatch.setenv("MR_WIN_PR_STREAMS", ns)
-            runs[(group, ns)] = rank_windows(ctx, wins) + rank_windows(ctx, wins[::-1])
-    base = runs[("1", "1")]
-    for key, got in runs.items():
-        for a, b in zip(base, got):
-            assert a[5] == b[5] == 0, key
-            assert a[2:] == b[2:] and list(a[0]) == list(b[0]) and a[1].tobytes() == b[1].tobytes(), key
-    for d in devs:
-        d.close()
-
-
 @pytest.mark.parametrize("name,minutes,device_append", [("stream", 7, True), ("stream", 3, True),
                                                          ("stream_gap", 7, True), ("stream", 7, False),
                                                          ("stream_gap", 3, False)])
@@ -919,3 +883,81 @@ def test_c2_windows_batch_groupings_agree(c2_batch, monkeypatch):
                 np.testing.assert_allclose(b[1], a[1], rtol=1e-12, atol=0, err_msg=f"{name} window {i}")
             else:
                 assert a[1].tobytes() == b[1].tobytes(), (name, i)
+
+
+def test_windows_batch_layout_order_equals_general_build(c3_window, monkeypatch):
+    """The layout-order window build (tables indexed with their trace layout and exact kind
+    classes: k_lo_sel_b, k_lo_fill_b, ...) against the general per-window build (MR_NO_LO_WIN):
+    four C3-shaped windows of three tables and an empty window -- statuses, abnormal / normal
+    counts and edges equal, top lists identical, DStar2 scores within 1e-12 (a tile's traces sum in
+    another rotation); and one-window chunks (the layout-order launches with n = 1) bitwise equal
+    to the default chunks of eight."""
+    import bench
+    from microrank_amd import _lib
+    from microrank_amd.online_rca import rank_windows
+    from microrank_amd.preprocess_data import DeviceSpans
+
+    ctx = _lib.default_context()
+    normal, abnormal, t0, t1 = c3_window
+    a3, ok = bench.slo_from_gpu(ctx, normal)
+    devs = [DeviceSpans(ctx, abnormal)]
+    wins = [(devs[0], t0, t1, a3, ok)]
+    for seed in (61, 62):
+        _, nrm, ab = bench.make_window(seed, 500, 20_000)
+        s3, sok = bench.slo_from_gpu(ctx, nrm)
+        d = DeviceSpans(ctx, ab)
+        devs.append(d)
+        u0 = int(ab.tstart.min())
+        wins.append((d, u0, u0 + 5 * 60 * 10**9, s3, sok))
+    wins.append((devs[0], 0, 1, a3, ok))   # empty window
+    runs = {}
+    for mode in ("lo", "general", "lo_chunk1"):
+        for k in ("MR_NO_LO_WIN", "MR_WIN_CHUNK"):
+            monkeypatch.delenv(k, raising=False)
+        if mode == "general":
+            monkeypatch.setenv("MR_NO_LO_WIN", "1")
+        if mode == "lo_chunk1":
+            monkeypatch.setenv("MR_WIN_CHUNK", "1")
+        runs[mode] = rank_windows(ctx, wins)
+    for a, b in zip(runs["lo"], runs["general"]):
+        assert a[5] == b[5]
+        assert a[2:] == b[2:] and list(a[0]) == list(b[0])
+        np.testing.assert_allclose(a[1], b[1], rtol=1e-12, atol=0)
+    assert runs["lo"][3][5] == _lib.MR_ERR_VALUE
+    for a, b in zip(runs["lo"], runs["lo_chunk1"]):
+        assert a[2:] == b[2:] and list(a[0]) == list(b[0]) and a[1].tobytes() == b[1].tobytes()
+    for d in devs:
+        d.close()
+
+
+def test_windows_batch_layout_order_rerun_sets_up_again(c3_window, monkeypatch):
+    """A PageRank group that mixes layout-order graphs with general-build ones (a table uploaded
+    without its layout: MR_NO_LO) and whose kind hashing collides (MR_KIND_TEST_COLLIDE) reruns
+    the whole group: the layout-order graphs' set-up runs again from their kept class sizes and
+    span counts (lo_setup_one), and every window ranks bitwise as without the collision; the
+    same window on either table ranks alike (1e-12)."""
+    import bench
+    from microrank_amd import _lib
+    from microrank_amd.online_rca import rank_windows
+    from microrank_amd.preprocess_data import DeviceSpans
+
+    ctx = _lib.default_context()
+    normal, abnormal, t0, t1 = c3_window
+    a3, ok = bench.slo_from_gpu(ctx, normal)
+    d_lo = DeviceSpans(ctx, abnormal)
+    monkeypatch.setenv("MR_NO_LO", "1")
+    d_gen = DeviceSpans(ctx, abnormal)
+    monkeypatch.delenv("MR_NO_LO")
+    wins = [(d_lo, t0, t1, a3, ok), (d_gen, t0, t1, a3, ok)] * 2
+    monkeypatch.setenv("MR_WIN_CHUNK", "1")
+    monkeypatch.setenv("MR_WIN_GROUP", "4")
+    base = rank_windows(ctx, wins)
+    monkeypatch.setenv("MR_KIND_TEST_COLLIDE", "1")
+    coll = rank_windows(ctx, wins)
+    for a, b in zip(base, coll):
+        assert a[5] == b[5] == 0
+        assert a[2:] == b[2:] and list(a[0]) == list(b[0]) and a[1].tobytes() == b[1].tobytes()
+    assert base[0][2:] == base[1][2:] and list(base[0][0]) == list(base[1][0])
+    np.testing.assert_allclose(base[0][1], base[1][1], rtol=1e-12, atol=0)
+    d_lo.close()
+    d_gen.close()
