@@ -1242,6 +1242,11 @@ def main():
                               "peak": HBM_PEAK_GBS, "unit": "GB/s",
                               "frac": round(bytes_w * n_win / elapsed / 1e9 / HBM_PEAK_GBS, 4),
                               "formula": "52 S + 2 (24 S + 4 nnz + 4 T) + 25 B_iter per graph (SURVEY 8(d))"}
+    if launches.value and avg_ms > 0:   # the same launches on the bytes they move: 2-B op ids, not SURVEY's 4-B
+        b16 = kbytes.value / launches.value - 2.0 * nnz_w * n_win * 25.0 / launches.value
+        out["roofline"]["u16_ids"] = {"bytes_per_launch": round(b16), "achieved": round(b16 / (avg_ms * 1e-3) / 1e9, 1),
+                                      "frac": round(b16 / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                      "what": "B_iter with 2 B per (trace, op) pair: k_tr_a reads u16 op ids"}
     if args.no_side:
         add_copy_frac(out, ctx)
         print(json.dumps(out), flush=True)

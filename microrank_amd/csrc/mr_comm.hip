@@ -221,11 +221,20 @@ __global__ void __launch_bounds__(PEER_T) k_peer_reduce(T* __restrict__ dst, int
 // its address, and a peer re-opening the new handle could be handed its cached mapping of the old
 // one -- its pushes and signals would land in freed memory (seen: a kind exchange after two region
 // replacements timed out on every rank).  Regions are a few MB; a context replaces one a handful
-// of times (sizes only grow).
+// of times (sizes only grow) plus once per peer timeout (mr_peer_check): a context that keeps timing
+// out keeps its regions until mr_comm_peer_destroy, which is collective like mr_comm_peer_enable(0)
+// (every rank frees its retired regions there; re-enabling maps fresh regions on every rank).
+// MR_PEER_RETIRE_MAX (default 64) bounds the list: past it the peer path turns off (the RCCL / host
+// collective carries on) instead of growing.
 static void peer_retire(mr_ctx* ctx) {
     if (ctx->peer_region || ctx->peer_dev || !ctx->peer_map.empty()) {
         if (ctx->peer_region) (void)hipStreamSynchronize(ctx->stream);
         ctx->peer_old.push_back(mr_ctx::PeerOld{ctx->peer_region, ctx->peer_dev, ctx->peer_map, ctx->rank});
+        static const size_t cap = [] {
+            const char* e = getenv("MR_PEER_RETIRE_MAX");
+            return (size_t)(e && atoi(e) > 0 ? atoi(e) : 64);
+        }();
+        if (ctx->peer_old.size() >= cap) ctx->peer_on = false;   // (the same count on every rank)
     }
     ctx->peer_map.clear();
     ctx->peer_region = nullptr;
@@ -263,8 +272,10 @@ static int peer_ensure(mr_ctx* ctx, int64_t words, int64_t xa = 0, int64_t xb = 
     peer_retire(ctx);
     const size_t bytes = ((size_t)PEER_FLAGS + 2 * (size_t)R * (size_t)words + (size_t)xa + (size_t)xb +
                           (size_t)R * (size_t)nbf) * sizeof(unsigned long long);
-    // (local failures from here on are agreed over the ranks below, never returned alone: every
-    // rank must reach the same collectives)
+    // (the region allocation and the mappings fail locally without returning alone: they are agreed
+    // over the ranks below, every rank reaching the same collectives.  The staging buffers and the
+    // handle gather are not: a rank failing THERE returns alone and its peers wait in the gather
+    // until the fallback collective's own timeout -- a device out of memory for a few hundred bytes)
     int32_t bad = 0;
     char why[160] = "";
     hipIpcMemHandle_t mine;
@@ -469,7 +480,9 @@ __global__ void __launch_bounds__(PEER_T) k_peer_bwait(const MrPeerX px, int32_t
         const int64_t w = px.bflags + (i / nb) * px.nbf + i % nb;
         while (__hip_atomic_load(reg + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < need) {
             __builtin_amdgcn_s_sleep(2);
-            if (__builtin_amdgcn_s_memrealtime() - t0 > px.timeout) {
+            // (a round of this call that already timed out: stop at once)
+            if (__builtin_amdgcn_s_memrealtime() - t0 > px.timeout ||
+                __hip_atomic_load(reg + px.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0ull) {
                 __hip_atomic_store(reg + px.err, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 return;
             }

@@ -269,24 +269,31 @@ extern "C" const char* mr_last_error(const mr_ctx* ctx) { return ctx ? ctx->err.
 
 // ---------------------------------------------------------------- measured copy peak
 // STREAM copy: every lane moves 4 x 16 B per round (all loads in flight before the stores),
-// grid-stride over the buffer
-__global__ void __launch_bounds__(256) k_copy16(const uint4* __restrict__ src, uint4* __restrict__ dst, int64_t n) {
+// grid-stride over the buffer; NT: non-temporal loads and stores (no L2 allocation)
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+template <bool NT>
+__global__ void __launch_bounds__(256) k_copy16(const u32x4* __restrict__ src, u32x4* __restrict__ dst, int64_t n) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    auto ld = [&](int64_t k) -> u32x4 { return NT ? __builtin_nontemporal_load(src + k) : src[k]; };
+    auto st = [&](int64_t k, u32x4 v) {
+        if (NT) __builtin_nontemporal_store(v, dst + k);
+        else dst[k] = v;
+    };
     for (; i + 3 * stride < n; i += 4 * stride) {
-        const uint4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
-        dst[i] = a;
-        dst[i + stride] = b;
-        dst[i + 2 * stride] = c;
-        dst[i + 3 * stride] = d;
+        const u32x4 a = ld(i), b = ld(i + stride), c = ld(i + 2 * stride), d = ld(i + 3 * stride);
+        st(i, a);
+        st(i + stride, b);
+        st(i + 2 * stride, c);
+        st(i + 3 * stride, d);
     }
-    for (; i < n; i += stride) dst[i] = src[i];
+    for (; i < n; i += stride) st(i, ld(i));
 }
 extern "C" int mr_copy_peak(mr_ctx* ctx, int64_t bytes, int reps, double* gbs) {
     if (!ctx || bytes < 16 || reps < 1 || !gbs) return mr_fail(ctx, MR_ERR_ARG, "mr_copy_peak: bad arguments");
     MR_TRY_HIP(ctx, hipSetDevice(ctx->device));
     const int64_t n = bytes / 16;
-    DBuf<uint4> a, b;
+    DBuf<u32x4> a, b;
     MR_TRY(a.alloc(ctx, (size_t)n));
     MR_TRY(b.alloc(ctx, (size_t)n));
     MR_TRY_HIP(ctx, hipMemsetAsync(a.p, 1, (size_t)n * 16, ctx->stream));
@@ -299,9 +306,10 @@ extern "C" int mr_copy_peak(mr_ctx* ctx, int64_t bytes, int reps, double* gbs) {
     MR_TRY_HIP(ctx, hipEventCreate(&e1));
     double best = 0.0;
     int rc = MR_OK;
-    for (int r = -1; r < reps && rc == MR_OK; ++r) {
+    for (int r = -2; r < 2 * reps && rc == MR_OK; ++r) {   // plain and non-temporal launches alternate
         (void)hipEventRecord(e0, ctx->stream);
-        hipLaunchKernelGGL(k_copy16, dim3(blocks), dim3(256), 0, ctx->stream, a.p, b.p, n);
+        if (r & 1) hipLaunchKernelGGL(k_copy16<true>, dim3(blocks), dim3(256), 0, ctx->stream, a.p, b.p, n);
+        else hipLaunchKernelGGL(k_copy16<false>, dim3(blocks), dim3(256), 0, ctx->stream, a.p, b.p, n);
         (void)hipEventRecord(e1, ctx->stream);
         if (hipEventSynchronize(e1) != hipSuccess) rc = mr_fail(ctx, MR_ERR_HIP, "mr_copy_peak: launch failed");
         float ms = 0.0f;

@@ -653,6 +653,21 @@ extern "C" int mr_rca_window(mr_ctx* ctx, const mr_spans* s, int64_t t0, int64_t
     MR_TRY_HIP(ctx, hipSetDevice(ctx->device));
     *n_out = 0;
     if (edges_traversed) *edges_traversed = 0;
+    // tables with a layout order: the window batch's build (one window), so a window ranks the
+    // same whether it comes alone or in a batch (the driver's window loop and its sweep, f3)
+    if (s->indexed && s->uniform_times && s->has_times && s->lo_ok && mr_lo_fits(s) && !getenv("MR_NO_LO_WIN") &&
+        !getenv("MR_NO_INDEX")) {
+        int32_t stw = MR_OK, na = 0, nn = 0;
+        int64_t ew = 0;
+        MR_TRY(mr_windows_batch(ctx, 1, &s, &t0, &t1, &a3, &a3_valid, method, top_max, precision, out_podop, out_score,
+                                n_out, &ew, &na, &nn, &stw));
+        if (stw == MR_ERR_VALUE) return mr_fail(ctx, MR_ERR_VALUE, "Current span list is empty");
+        if (stw != MR_OK) return stw;
+        if (edges_traversed) *edges_traversed = ew;
+        if (n_abnormal) *n_abnormal = na;
+        if (n_normal) *n_normal = nn;
+        return MR_OK;
+    }
     WinMarks mk(ctx->stream);
     mk.mark("start");
     WinRun w;

@@ -2178,8 +2178,27 @@ struct IxWinLoB {
     int32_t *ocnt[2], *ofinv[2], *ocov[2];   // (zeroed)
     uint32_t* gc[2];                 // (zeroed)
 };
+__device__ __forceinline__ int64_t rfl64_(int64_t v) {   // a wave-uniform int64 (lane 0's) into SGPRs
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)v);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)((uint64_t)v >> 32));
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+// the trace k (0..63) of the wave's tile whose entries [a_k, b_k) hold entry e (a_k ascending,
+// lane k holding a_k): one division when the tile's traces all have n entries (the layout sorts
+// by entry count: the usual case), else a binary search over the lanes' starts
+__device__ __forceinline__ int lo_trace_of(int64_t e, int64_t E0, int64_t n, int64_t a) {
+    if (n > 0) return (int)((uint32_t)(e - E0) / (uint32_t)n);
+    int lo = 0, hi = WAVE - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        const int64_t am = __shfl(a, mid, WAVE);
+        if (am <= e) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
 __global__ void __launch_bounds__(LB_T) k_lo_build_b(IxBatch<IxWinLoB> a, uint64_t epoch) {
-    extern __shared__ int32_t lh[];   // graph g: [g W, (g + 1) W): cnt | INT_MAX - first | cov | edges
+    // per graph g: [cnt | cov << 32] u64 x NP, then INT_MAX - first row x NP, then edge counts x nek
+    extern __shared__ __attribute__((aligned(16))) unsigned char lraw[];
     __shared__ int8_t side[LB_TILE];
     __shared__ int32_t sa[2][LB_T];
     __shared__ int32_t ex[2];
@@ -2188,27 +2207,45 @@ __global__ void __launch_bounds__(LB_T) k_lo_build_b(IxBatch<IxWinLoB> a, uint64
     const IxWinLoB& w = a.w[k];
     const int32_t blk = (int32_t)blockIdx.x - a.b0[k], nblk = a.b0[k + 1] - a.b0[k];
     const int tid = threadIdx.x, lane = tid & (WAVE - 1), wv = tid / WAVE;
-    const int32_t NP = w.NP, W = 3 * NP + w.nek;
-    for (int32_t x = tid; x < 2 * W; x += LB_T) lh[x] = 0;
+    const int32_t NP = w.NP, nek = w.nek;
+    const size_t gbytes = ((size_t)NP * 12 + (size_t)nek * 4 + 15) / 16 * 16;   // one graph's histograms
+    for (size_t x = (size_t)tid * 4; x < 2 * gbytes; x += (size_t)LB_T * 4) *(uint32_t*)(lraw + x) = 0u;
     __syncthreads();
     const int64_t base = (int64_t)blk * LB_TILE;
     int64_t nz0 = 0, nz1 = 0, rows = 0;
     int nab = 0, nno = 0;
-    for (int j = 0; j < LB_I; ++j) {   // consecutive lanes, consecutive traces: contiguous entries
+    for (int j = 0; j < LB_I; ++j) {   // wave tile j * 16 + wv: 64 consecutive traces of the layout
         const int64_t i = base + (int64_t)j * LB_T + tid;
+        const bool valid = i < w.NT;
+        int64_t pa = 0, pb = 0, ea = 0, eb = 0;
         int s_ = -1;
-        if (i < w.NT) {
+        if (valid) {
             const int32_t len = w.lo_len[i];
             const long long ts = w.lo_ts[i], te = w.lo_te[i], mx = w.lo_mx[i];
+            pa = w.lo_off[i];
+            pb = w.lo_off[i + 1];
+            ea = w.le_off[i];
+            eb = w.le_off[i + 1];
+            const int64_t va = w.lsv_off[i], vb = w.lsv_off[i + 1];
             const bool in = len > 0 && ts >= w.t0 && te <= w.t1;
             rows += in ? len : 0;
             int stt = 0;
             if (in && mx > 0) {   // grouped[grouped['duration'] > 0] (preprocess_data.py:117)
+                // expect: sequential in name order (T14), the entries' loads four at a time
                 double expect = 0.0;
-                for (int64_t e = w.lsv_off[i], e1 = w.lsv_off[i + 1]; e < e1; ++e) {
-                    const uint32_t v = w.lsv[e];
-                    const uint32_t op = v & 0xffffu;
-                    expect += w.a3v[op] ? (double)(v >> 16) * w.a3[op] : 0.0;   // :63-67 (T14)
+                for (int64_t e = va; e < vb; e += 4) {
+                    uint32_t v[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) v[q] = e + q < vb ? w.lsv[e + q] : 0u;
+                    double t[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const uint32_t op = v[q] & 0xffffu;
+                        t[q] = w.a3v[op] ? (double)(v[q] >> 16) * w.a3[op] : 0.0;   // anormaly_detector.py:63-67
+                    }
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        if (e + q < vb) expect += t[q];
                 }
                 stt = (double)mx / 1000.0 > expect ? 2 : 1;   // :58, :69
             }
@@ -2218,22 +2255,42 @@ __global__ void __launch_bounds__(LB_T) k_lo_build_b(IxBatch<IxWinLoB> a, uint64
             s_ = stt == 2 ? 0 : stt == 1 ? 1 : -1;
             if (s_ >= 0) {
                 atomicAdd(&w.kcnt[s_][w.lo_kid[i]], 1u);
-                int32_t* L = lh + s_ * W;
-                const int64_t e0 = w.lo_off[i], e1 = w.lo_off[i + 1];
-                if (s_ == 0) nz0 += e1 - e0; else nz1 += e1 - e0;
-                for (int64_t e = e0; e < e1; ++e) {
-                    const int32_t c = w.lo16[e];
-                    atomicAdd(&L[c], (int32_t)w.lo_cnt[e]);
-                    atomicMax(&L[NP + c], 0x7fffffff - w.lo_first[e]);
-                    atomicAdd(&L[2 * NP + c], 1);
-                }
-                for (int64_t e = w.le_off[i], e1e = w.le_off[i + 1]; e < e1e; ++e) {
-                    const uint32_t v = w.le[e];
-                    atomicAdd((uint32_t*)&L[3 * NP + (int32_t)(v & 0xffffu)], v >> 16);
-                }
+                if (s_ == 0) nz0 += pb - pa; else nz1 += pb - pa;
             }
         }
         side[j * LB_T + tid] = (int8_t)s_;
+        // the tile's pod-op and join entries, a lane per entry (coalesced), each to its trace's graph
+        const unsigned long long vm = __ballot(valid);
+        if (vm == 0ull) continue;   // (uniform: past the window's traces)
+        const int last = 63 - __builtin_clzll(vm);   // (valid lanes are a prefix)
+        const int64_t P0 = rfl64_(pa), P1 = rfl64_(__shfl(pb, last, WAVE));
+        const int64_t Q0 = rfl64_(ea), Q1 = rfl64_(__shfl(eb, last, WAVE));
+        const int64_t npo = P1 - P0 == (int64_t)(last + 1) * (rfl64_(pb) - P0) && last == WAVE - 1 ? rfl64_(pb) - P0 : 0;
+        if (!valid) pa = pb = P1, ea = eb = Q1;
+        // (every lane runs every round -- the shuffles read the other lanes' registers, which an
+        // inactive lane would not provide -- and a lane past the tile's entries skips the work)
+        for (int64_t eb0 = P0; eb0 < P1; eb0 += WAVE) {
+            const int64_t e = min(eb0 + lane, P1 - 1);
+            const int kt = lo_trace_of(e, P0, npo, pa);
+            const int sk = __shfl(s_, kt, WAVE);   // (all lanes: a disabled source lane reads as 0)
+            const int sd = eb0 + lane < P1 ? sk : -1;
+            const uint16_t c = w.lo16[e];
+            const uint16_t cn = w.lo_cnt[e];
+            const int32_t fr = w.lo_first[e];
+            if (sd >= 0) {
+                unsigned char* G = lraw + (size_t)sd * gbytes;
+                atomicAdd((unsigned long long*)G + c, (unsigned long long)cn | (1ull << 32));
+                atomicMax((int32_t*)(G + (size_t)NP * 8) + c, 0x7fffffff - fr);
+            }
+        }
+        for (int64_t eb0 = Q0; eb0 < Q1; eb0 += WAVE) {
+            const int64_t e = min(eb0 + lane, Q1 - 1);
+            const int kt = lo_trace_of(e, Q0, 0, ea);
+            const int sk = __shfl(s_, kt, WAVE);
+            const int sd = eb0 + lane < Q1 ? sk : -1;
+            const uint32_t v = w.le[e];
+            if (sd >= 0) atomicAdd((uint32_t*)(lraw + (size_t)sd * gbytes + (size_t)NP * 12) + (v & 0xffffu), v >> 16);
+        }
     }
     {   // the detector's counts and both graphs' entry totals: per wave, per block, one add each
         unsigned long long ab = (unsigned long long)nab, no = (unsigned long long)nno, rw = (unsigned long long)rows;
@@ -2300,14 +2357,19 @@ __global__ void __launch_bounds__(LB_T) k_lo_build_b(IxBatch<IxWinLoB> a, uint64
         else if (sd == 1) w.pinv[1][r1++] = ix;
     }
     // the block's histograms into the window's zeroed words
-    for (int32_t x = tid; x < 2 * W; x += LB_T) {
-        const int32_t v = lh[x];
-        if (!v) continue;
-        const int g = x >= W, jx = x - g * W;
-        if (jx < NP) atomicAdd(&w.ocnt[g][jx], v);
-        else if (jx < 2 * NP) atomicMax(&w.ofinv[g][jx - NP], v);
-        else if (jx < 3 * NP) atomicAdd(&w.ocov[g][jx - 2 * NP], v);
-        else atomicAdd(&w.gc[g][jx - 3 * NP], (uint32_t)v);
+    for (int g = 0; g < 2; ++g) {
+        const unsigned char* G = lraw + (size_t)g * gbytes;
+        for (int32_t c = tid; c < NP; c += LB_T) {
+            const unsigned long long v = ((const unsigned long long*)G)[c];
+            if (!v) continue;
+            atomicAdd(&w.ocnt[g][c], (int32_t)(v & 0xffffffffull));
+            atomicAdd(&w.ocov[g][c], (int32_t)(v >> 32));
+            atomicMax(&w.ofinv[g][c], ((const int32_t*)(G + (size_t)NP * 8))[c]);
+        }
+        for (int32_t x = tid; x < nek; x += LB_T) {
+            const uint32_t v = ((const uint32_t*)(G + (size_t)NP * 12))[x];
+            if (v) atomicAdd(&w.gc[g][x], v);
+        }
     }
 }
 
@@ -2407,7 +2469,7 @@ int mr_lo_launch_batch(mr_ctx* ctx, int n, const mr_spans* const* sps, mr_graph*
         L.NT = NT;
         L.NP = NP;
         L.nek = (int32_t)nek;
-        lds = std::max(lds, 2 * (3 * (size_t)NP + (size_t)nek) * sizeof(int32_t));
+        lds = std::max(lds, 2 * (((size_t)NP * 12 + (size_t)nek * 4 + 15) / 16 * 16));
         ac.b0[k] = bc;
         bc += (int32_t)cdiv(sp->n_xj, 256);
         ac.w[k] = IxWinCross{d.state, sp->xj_tc.p, sp->xj_tp.p, sp->xj_eid.p, sp->n_xj, xs};

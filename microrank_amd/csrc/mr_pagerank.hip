@@ -1514,8 +1514,9 @@ __global__ void k_pref_apply_b(const SDev* __restrict__ sd, int32_t ng) {
 // relabelled to node ids: node_of_code), w_t / span count / kind class size by position and the
 // preference partials, then the totals, then the preference and iteration state -- the work of
 // k_graph_consts .. k_tr_fill and k_reset_init .. k_pref_apply for these graphs, in four launches.
+constexpr int LO_NOC_MAX = 4096;   // (mr_lo_fits: tables of <= NS_PMAX pod-ops)
 struct LDev {
-    int32_t T, N, W, anomaly, fp32;
+    int32_t T, N, W, anomaly, fp32, rot, NP;
     int32_t b_cs, n_cs, b_fill, nbp, b_app;   // first block in each launch; partial blocks
     int64_t st_off;
     float cd;
@@ -1559,10 +1560,13 @@ __global__ void __launch_bounds__(TS_T) k_lo_cs_b(const LDev* __restrict__ ld, i
 // the block's 1/k and 1/len_t sums (pagerank.py:71-78) into ppart
 __global__ void __launch_bounds__(256) k_lo_fill_b(const LDev* __restrict__ ld, int32_t n) {
     __shared__ double red[256 / WAVE];
+    __shared__ uint16_t lnoc[LO_NOC_MAX];   // the code -> node id table (one LDS read per id)
     const LDev& G = ld[ld_graph(ld, n, (int32_t)blockIdx.x, 1)];
     const int32_t blk = (int32_t)blockIdx.x - G.b_fill;
     const int64_t i = (int64_t)blk * 256 + threadIdx.x;
     const int32_t T = G.T, N = G.N;
+    for (int32_t c = threadIdx.x; c < G.NP; c += 256) lnoc[c] = (uint16_t)G.noc[c];
+    __syncthreads();
     double a = 0.0, b = 0.0;
     if (i < (int64_t)G.W * WAVE) {
         const int32_t k = (int32_t)(i / WAVE), lane = (int32_t)(i % WAVE);
@@ -1571,7 +1575,7 @@ __global__ void __launch_bounds__(256) k_lo_fill_b(const LDev* __restrict__ ld, 
             const int32_t ix = G.pinv[i];
             e0 = G.lo_off[ix];
             len = G.lo_off[ix + 1] - e0;
-            rot = len ? ix % len : 0;
+            rot = len && G.rot ? (int64_t)((uint32_t)ix % (uint32_t)len) : 0;
             const int32_t L = G.lo_len[ix];
             const uint32_t kc = G.kcnt[G.lo_kid[ix]];
             G.w_tp[i] = L > 0 ? (float)(1.0 / (double)L) : 0.0f;
@@ -1588,7 +1592,7 @@ __global__ void __launch_bounds__(256) k_lo_fill_b(const LDev* __restrict__ ld, 
 #pragma unroll
             for (int q = 0; q < 4 * TF_CH; ++q) {
                 const int64_t e = 4 * c0 + q, jx = rot + e;
-                idv[q] = e < len ? (uint16_t)G.noc[G.lo16[e0 + (jx >= len ? jx - len : jx)]] : (uint16_t)(N + lane);
+                idv[q] = e < len ? lnoc[G.lo16[e0 + (jx >= len ? jx - len : jx)]] : (uint16_t)(N + lane);
             }
 #pragma unroll
             for (int u = 0; u < TF_CH; ++u)
@@ -1998,6 +2002,7 @@ __device__ __forceinline__ int32_t fx_graph(const GDev* gs, int32_t ng, int32_t 
 // ---------------------------------------------------------------- fused iteration: LDS budget and su modes
 constexpr size_t WV_LDS_MAX = 160 * 1024 - 512;
 constexpr int TR_AR_DEFAULT = 1;   // (tr_ar_want)
+constexpr int LO_ROT_DEFAULT = 1;  // (mr_lo_prepare_batch)
 // su modes of k_tr_a: global gathers only / every op's su in LDS / the n_hot most covered ops' su in
 // LDS (relabelled graphs, ops [0, n_hot)), the rest gathered
 enum { WV_SU_GLOBAL = 0, WV_SU_ALL = 1, WV_SU_HOT = 2 };
@@ -2759,7 +2764,10 @@ __global__ void __launch_bounds__(WAVE * FB_W) k_fx_b(const GDev* __restrict__ g
                 while (__hip_atomic_load(preg + px.bflags + (int64_t)r * px.nbf + bidx, __ATOMIC_RELAXED,
                                          __HIP_MEMORY_SCOPE_SYSTEM) < need) {
                     __builtin_amdgcn_s_sleep(2);
-                    if (__builtin_amdgcn_s_memrealtime() - t0 > px.timeout) {
+                    // a round that already timed out (this call's error word): stop at once instead
+                    // of spinning the full timeout again in every later iteration
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > px.timeout ||
+                        __hip_atomic_load(preg + px.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0ull) {
                         s_ok = 0;
                         __hip_atomic_store((GLB unsigned long long*)px.region + px.err, 1ull, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_SYSTEM);
@@ -4797,6 +4805,10 @@ int mr_lo_prepare_batch(mr_ctx* ctx, mr_graph* const* gs, const mr_spans* const*
     if (n <= 0) return MR_OK;
     const bool fp32 = precision == MR_FP32;
     hipStream_t st = ctx->stream;
+    // a trace's ids rotated by its layout index mod length (spreads a shared first op over a tile's
+    // id chunks) or kept in the layout's order (MR_LO_ROT=0; read per call)
+    const char* re = getenv("MR_LO_ROT");
+    const int lo_rot = re ? (atoi(re) != 0) : LO_ROT_DEFAULT;
     keep.assign((size_t)n * sizeof(LDev), 0);
     LDev* hv = reinterpret_cast<LDev*>(keep.data());
     std::vector<DBuf<int64_t>> c64((size_t)n);
@@ -4842,6 +4854,8 @@ int mr_lo_prepare_batch(mr_ctx* ctx, mr_graph* const* gs, const mr_spans* const*
         LDev& v = hv[i];
         MR_TRY(lo_state(ctx, g, anomaly[i], d, fp32, v));
         v.W = W;
+        v.rot = lo_rot;
+        v.NP = sp->n_podops;
         v.n_cs = (int32_t)std::max<int64_t>(cdiv((int64_t)W, TS_TILE), 1);
         v.st_off = st_words;
         st_words += v.n_cs;

@@ -224,18 +224,25 @@ __global__ void k_lo_copy(const int32_t* lo_tr, const int64_t* lo_off, int32_t N
                           const int32_t* po_op, const int32_t* po_cnt, const int32_t* po_first, const long long* tts,
                           const long long* tte, const long long* tmaxd, const int64_t* sv_off, const int64_t* ed_off,
                           uint16_t* lo16, uint16_t* lo_cnt, int32_t* lo_first, long long* lo_ts, long long* lo_te,
-                          long long* lo_mx, int32_t* nsv, int32_t* ned, int32_t* bad) {
+                          long long* lo_mx, int32_t* nsv, int32_t* ned, int32_t* bad, const int32_t* prank) {
     const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= NT) return;
     const int32_t t = lo_tr[i];
     const int64_t a = po_off[t], n = po_off[t + 1] - a, o = lo_off[i];
     bool big = false;
     for (int64_t e = 0; e < n; ++e) {
-        const int32_t c = po_cnt[a + e];
+        const int32_t c = po_cnt[a + e], op = po_op[a + e], fr = po_first[a + e];
         big = big || c > 65535;
-        lo16[o + e] = (uint16_t)po_op[a + e];
-        lo_cnt[o + e] = (uint16_t)c;
-        lo_first[o + e] = po_first[a + e];
+        int64_t j = e;   // prank: the trace's ops by table-wide popularity (insertion into place)
+        if (prank)
+            for (const int32_t key = prank[op]; j > 0 && prank[lo16[o + j - 1]] > key; --j) {
+                lo16[o + j] = lo16[o + j - 1];
+                lo_cnt[o + j] = lo_cnt[o + j - 1];
+                lo_first[o + j] = lo_first[o + j - 1];
+            }
+        lo16[o + j] = (uint16_t)op;
+        lo_cnt[o + j] = (uint16_t)c;
+        lo_first[o + j] = fr;
     }
     lo_ts[i] = tts[t];
     lo_te[i] = tte[t];
@@ -243,6 +250,16 @@ __global__ void k_lo_copy(const int32_t* lo_tr, const int64_t* lo_off, int32_t N
     nsv[i] = (int32_t)(sv_off[t + 1] - sv_off[t]);
     ned[i] = (int32_t)(ed_off[t + 1] - ed_off[t]);
     if (big) atomicOr(bad, 1);
+}
+__global__ void __launch_bounds__(256) k_lo_cov(const int32_t* po_op, int64_t n, int32_t NP, int32_t* cov) {
+    extern __shared__ int32_t lc[];   // (a popular op's adds stay in LDS: one global add per block and code)
+    for (int32_t c = threadIdx.x; c < NP; c += 256) lc[c] = 0;
+    __syncthreads();
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256)
+        atomicAdd(&lc[po_op[e]], 1);
+    __syncthreads();
+    for (int32_t c = threadIdx.x; c < NP; c += 256)
+        if (lc[c]) atomicAdd(&cov[c], lc[c]);
 }
 __global__ void k_lo_copy2(const int32_t* lo_tr, int32_t NT, const int64_t* sv_off, const int32_t* sv_op,
                            const int32_t* sv_cnt, const int64_t* ed_off, const int32_t* ed_eid, const int32_t* ed_cnt,
@@ -484,10 +501,32 @@ static int lo_index(mr_ctx* ctx, mr_spans* s) {
         hipLaunchKernelGGL(k_lo_unpack, dim3(cdiv(NT, XB)), dim3(XB), 0, st, key.p, NT, nbt, s->tlen.p, s->lo_tr.p, lo_n.p,
                            s->lo_len.p);
         MR_TRY(mr_exclusive_scan_i32(ctx, lo_n.p, s->lo_off.p, NT, tmp.p));
+        // each trace's ops in the order of their table-wide coverage (most covered first): a tile's
+        // lanes then hold the popular ops in the same id chunks -- one LDS broadcast per su read of
+        // such an op, and the accumulator replicas keep its adds apart (MR_LO_POP=0: code order)
+        DBuf<int32_t> prank;
+        std::vector<int32_t> rk;   // (alive until the stream has copied it: the sync below)
+        const char* pe = getenv("MR_LO_POP");   // (A/B, read per table)
+        if (!(pe && atoi(pe) == 0)) {
+            const int32_t NP = s->n_podops;
+            DBuf<int32_t> cov;
+            MR_TRY(cov.zero(ctx, (size_t)std::max(NP, 1)));
+            if (s->n_po)
+                hipLaunchKernelGGL(k_lo_cov, dim3(std::min(512, cdiv(s->n_po, XB))), dim3(XB), (size_t)NP * sizeof(int32_t),
+                                   st, s->po_op.p, s->n_po, NP, cov.p);
+            std::vector<int32_t> hc((size_t)std::max(NP, 1)), ord((size_t)NP);
+            rk.assign((size_t)std::max(NP, 1), 0);
+            MR_TRY(cov.download(ctx, hc.data(), (size_t)NP));
+            MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+            for (int32_t c = 0; c < NP; ++c) ord[(size_t)c] = c;
+            std::stable_sort(ord.begin(), ord.end(), [&](int32_t x, int32_t y) { return hc[(size_t)x] > hc[(size_t)y]; });
+            for (int32_t r = 0; r < NP; ++r) rk[(size_t)ord[(size_t)r]] = r;
+            MR_TRY(prank.upload(ctx, rk.data(), (size_t)std::max(NP, 1)));
+        }
         hipLaunchKernelGGL(k_lo_copy, dim3(cdiv(NT, XB)), dim3(XB), 0, st, s->lo_tr.p, s->lo_off.p, NT, s->po_off.p,
                            s->po_op.p, s->po_cnt.p, s->po_first.p, s->tts.p, s->tte.p, s->tmaxd.p, s->sv_off.p,
                            s->ed_off.p, s->lo16.p, s->lo_cnt.p, s->lo_first.p, s->lo_ts.p, s->lo_te.p, s->lo_mx.p, nsv.p,
-                           ned.p, bad.p);
+                           ned.p, bad.p, prank.p);
         MR_TRY(mr_exclusive_scan_i32(ctx, nsv.p, s->lsv_off.p, NT, tmp.p));
         MR_TRY(mr_exclusive_scan_i32(ctx, ned.p, s->le_off.p, NT, tmp.p));
         hipLaunchKernelGGL(k_lo_copy2, dim3(cdiv(NT, XB)), dim3(XB), 0, st, s->lo_tr.p, NT, s->sv_off.p, s->sv_op.p,

@@ -147,26 +147,51 @@ class _ColumnSnapshot:
     def __init__(self, s: pd.Series):
         arr = s.array
         self.pa = getattr(arr, "_pa_array", None)
-        self.np = None
+        self.np = self.mask = self.boxed = None
         if self.pa is None:
+            data, mask = _masked_parts(arr)
+            if data is not None:   # nullable (masked) columns, e.g. Int64 with pd.NA: values + mask
+                self.np, self.mask = data.copy(), mask.copy()
+                return
             a = getattr(arr, "_ndarray", None)
-            self.np = np.array(np.asarray(arr) if a is None else a, copy=True)
+            if a is None:   # another extension array: np.asarray boxes new objects per call
+                self.boxed = s.copy()
+            else:
+                self.np = np.array(a, copy=True)
 
     def matches(self, s: pd.Series) -> bool:
         arr = s.array
         pa_arr = getattr(arr, "_pa_array", None)
         if self.pa is not None or pa_arr is not None:
             return pa_arr is self.pa
+        if self.boxed is not None:   # compared by value (NA equal to NA), not by object identity
+            return s.dtype == self.boxed.dtype and bool(s.reset_index(drop=True).equals(self.boxed.reset_index(drop=True)))
+        data, mask = _masked_parts(arr)
+        if self.mask is not None or data is not None:
+            return self.mask is not None and data is not None and _same_values(data, self.np) and \
+                _same_values(mask, self.mask)
         a = getattr(arr, "_ndarray", None)
-        a = np.asarray(arr) if a is None else a
-        if a.dtype != self.np.dtype or a.shape != self.np.shape:
-            return False
-        if a.flags.c_contiguous and self.np.flags.c_contiguous:
-            # values, or an object column's pointers: memcmp (ctypes releases the GIL)
-            return a.nbytes == 0 or _memcmp(C.c_void_p(a.ctypes.data), C.c_void_p(self.np.ctypes.data),
-                                            C.c_size_t(a.nbytes)) == 0
-        return bool(np.array_equal(a, self.np)) if a.dtype != object else all(
-            u is v for u, v in zip(a.tolist(), self.np.tolist()))
+        return a is not None and _same_values(a, self.np)
+
+
+def _masked_parts(arr):
+    """(values, mask) of a pandas masked extension array (BaseMaskedArray: Int64, Float64,
+    boolean ...), else (None, None)."""
+    data, mask = getattr(arr, "_data", None), getattr(arr, "_mask", None)
+    if isinstance(data, np.ndarray) and isinstance(mask, np.ndarray):
+        return data, mask
+    return None, None
+
+
+def _same_values(a: np.ndarray, b: np.ndarray) -> bool:
+    """a equals the snapshot b: values, or an object column's pointers (the snapshot holds a
+    reference to every object, so equal pointers are the same immutable objects)."""
+    if a.dtype != b.dtype or a.shape != b.shape:
+        return False
+    if a.flags.c_contiguous and b.flags.c_contiguous:
+        # memcmp (ctypes releases the GIL)
+        return a.nbytes == 0 or _memcmp(C.c_void_p(a.ctypes.data), C.c_void_p(b.ctypes.data), C.c_size_t(a.nbytes)) == 0
+    return bool(np.array_equal(a, b)) if a.dtype != object else all(u is v for u, v in zip(a.tolist(), b.tolist()))
 
 
 class _FrameSnapshot:

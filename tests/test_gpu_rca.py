@@ -220,8 +220,11 @@ def test_driver_matches_reference(name, tmp_path, monkeypatch):
 
 @pytest.mark.parametrize("name", ["stream", "stream_gap"])
 def test_driver_sweep_equals_window_loop(name, tmp_path, monkeypatch):
-    """f3: the device sweep prints exactly what the window-by-window driver prints (same windows,
-    same counts, same rankings), and writes the same result.csv."""
+    """f3: the device sweep prints what the window-by-window driver prints (same windows, same
+    counts, same rankings and '%.8f' lines), and writes the same result.csv.  The sweep ranks
+    through the window batch's layout-order build, the loop through the drop-in per-window graphs
+    (get_pagerank_graph + trace_pagerank): a trace's entries are summed in another order, so the
+    full-repr scores (online_rca.py:202) and result.csv's agree to 1e-12, not bit for bit."""
     from microrank_amd import synth
 
     case = load_golden(f"{name}.json")
@@ -232,11 +235,28 @@ def test_driver_sweep_equals_window_loop(name, tmp_path, monkeypatch):
     out_a, err_a = _run_driver(adf, case)
     monkeypatch.chdir(tmp_path / "b")
     out_b, err_b = _run_driver(adf, case, sweep=False, monkeypatch=monkeypatch)
-    assert out_a == out_b and err_a == err_b
+    assert err_a == err_b
+    la, lb = out_a.splitlines(), out_b.splitlines()
+    assert len(la) == len(lb)
+    for a, b in zip(la, lb):
+        if a.startswith("[") and b.startswith("["):   # print(top_list, score_list): full repr
+            aa, bb = a.split("] [", 1), b.split("] [", 1)
+            assert aa[0] == bb[0]
+            xa = [float(v.split("(")[-1].rstrip(")]")) for v in aa[1].split(", ")]
+            xb = [float(v.split("(")[-1].rstrip(")]")) for v in bb[1].split(", ")]
+            np.testing.assert_allclose(xa, xb, rtol=1e-12, atol=0)
+        else:
+            assert a == b
     csv_a, csv_b = tmp_path / "a" / "result.csv", tmp_path / "b" / "result.csv"
     assert csv_a.exists() == csv_b.exists()
     if csv_a.exists():
-        assert csv_a.read_text() == csv_b.read_text()
+        ra, rb = csv_a.read_text().splitlines(), csv_b.read_text().splitlines()
+        assert len(ra) == len(rb)
+        for a, b in zip(ra, rb):
+            pa_, pb_ = a.split(","), b.split(",")
+            assert pa_[:-1] == pb_[:-1]
+            if pa_[-1] != "confidence":
+                assert math.isclose(float(pa_[-1]), float(pb_[-1]), rel_tol=1e-12)
 
 
 def test_detect_sweep_counts_equal_per_window_detector():

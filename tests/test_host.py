@@ -48,6 +48,34 @@ def test_fingerprint_is_exact_for_any_in_place_edit_and_invalidate():
     assert fp.matches(df.iloc[:0]) and not fp.matches(df)
 
 
+def test_fingerprint_nullable_and_extension_columns():
+    """nullable (masked) columns -- an Int64 duration holding pd.NA -- and other
+    extension arrays keep an exact, stable key: unchanged frames match on every lookup (no rebuild
+    per call), an in-place edit anywhere (value or NA-ness) does not."""
+    from microrank_amd.preprocess_data import _fingerprint
+
+    case = load_golden("c1.json")
+    _, adf = regen_window(case)
+    df = adf.copy()
+    n = len(df)
+    df["duration"] = df["duration"].astype("Int64")
+    df.loc[df.index[3], "duration"] = pd.NA
+    df["podName"] = df["podName"].astype("category")     # another extension array
+    fp = _fingerprint(df)
+    assert fp.matches(df) and fp.matches(df)
+    mid = df.index[n // 2 + 5]
+    df.loc[mid, "duration"] = int(df["duration"].iloc[n // 2 + 5]) + 1
+    assert not fp.matches(df)
+    fp = _fingerprint(df)
+    df.loc[mid, "duration"] = pd.NA                     # value -> NA
+    assert not fp.matches(df)
+    fp = _fingerprint(df)
+    assert fp.matches(df)
+    cats = list(df["podName"].cat.categories)
+    df.loc[mid, "podName"] = cats[0] if df.loc[mid, "podName"] != cats[0] else cats[-1]
+    assert not fp.matches(df)
+
+
 def test_fingerprint_arrow_columns_and_cost():
     """Arrow-backed columns (read_traces_csv) match by identity of their immutable arrays (an
     in-place edit replaces the array); a C2-sized frame (2.7M spans) is checked in a few tens
