@@ -2145,11 +2145,13 @@ int mr_ix_launch2_batch(mr_ctx* ctx, int n, const mr_spans* const* sps, uint8_t*
 // (pagerank.py:54-66's class size = the histogram of the graph's class ids).  No trace-major
 // incidence, no per-graph sort by length, no kind hashing: the prepare reads each position's
 // codes from the layout-ordered u16 lists (near-contiguous for a tile) and relabels them.
-constexpr int LB_T = 1024, LB_I = 8, LB_TILE = LB_T * LB_I;   // k_lo_build_b: threads, traces per thread / block
+constexpr int LB_T = 1024, LB_I = 2, LB_TILE = LB_T * LB_I;   // k_lo_build_b: threads, traces per thread / block
 constexpr int64_t LB_LDS_WORDS = 34816;   // its two graphs' histograms (136 KB beside its static LDS)
+constexpr int32_t LB_A3MAX = 4096;        // service-op thresholds in LDS (8 B each)
 bool mr_lo_fits(const mr_spans* sp) {
     return sp->indexed && sp->ekey.p && sp->n_podops <= NS_PMAX && sp->n_edge_keys <= NS_EMAX &&
-           2 * (3 * (int64_t)sp->n_podops + sp->n_edge_keys) <= LB_LDS_WORDS && sp->n_traces <= (1 << 24);
+           2 * (3 * (int64_t)sp->n_podops + sp->n_edge_keys) + 2 * (int64_t)sp->n_svcops <= LB_LDS_WORDS &&
+           sp->n_svcops <= LB_A3MAX && sp->n_traces <= (1 << 24);
 }
 // Per window, in its table's layout order: the detector (anormaly_detector.py:44-84 as
 // detect_block: a trace's expect summed sequentially over its service-ops in name order, T14),
@@ -2157,8 +2159,9 @@ bool mr_lo_fits(const mr_spans* sp) {
 // trace's position (its rank among the graph's traces in layout order: look-back scan) and kind
 // class count, and both graphs' per-pod-op span counts / first rows / coverage and per-edge-id
 // multiplicities (get_pagerank_graph's len_o, node order and children multisets,
-// preprocess_data.py:146-171) in LDS, flushed once per block into zeroed words (the first row as
-// INT_MAX - row under atomicMax).  One pass over everything a trace holds.
+// preprocess_data.py:146-171) in LDS, written once per block as a partial row (the first row as
+// INT_MAX - row, combined by max) that k_lo_reduce_b sums per window.  One pass over everything a
+// trace holds; each wave keeps four rounds of entry loads in flight.
 struct IxWinLoB {
     const int32_t *lo_tr, *lo_len, *lo_kid, *lo_first;
     const int64_t *lo_off, *lsv_off, *le_off;
@@ -2171,12 +2174,11 @@ struct IxWinLoB {
     uint8_t* state;                  // by trace code (k_ix_cross2_b reads it)
     unsigned long long* counts;      // detector counter shards (3 * CSH, zeroed)
     unsigned long long* st;          // look-back words: 2 chains x the window's tiles
-    int32_t NT, NP, nek, pad_;
+    int32_t NT, NP, nek, nsvc;
     int32_t* pinv[2];                // position -> layout index
     uint32_t* kcnt[2];               // kind class histograms (zeroed)
     int64_t* tot[2];                 // [T, nnz] (zeroed)
-    int32_t *ocnt[2], *ofinv[2], *ocov[2];   // (zeroed)
-    uint32_t* gc[2];                 // (zeroed)
+    uint32_t* rows;                  // partial rows [block][graph][cnt NP | cov NP | INT_MAX - first NP | edges nek]
 };
 __device__ __forceinline__ int64_t rfl64_(int64_t v) {   // a wave-uniform int64 (lane 0's) into SGPRs
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)v);
@@ -2185,7 +2187,8 @@ __device__ __forceinline__ int64_t rfl64_(int64_t v) {   // a wave-uniform int64
 }
 // the trace k (0..63) of the wave's tile whose entries [a_k, b_k) hold entry e (a_k ascending,
 // lane k holding a_k): one division when the tile's traces all have n entries (the layout sorts
-// by entry count: the usual case), else a binary search over the lanes' starts
+// by entry count: the usual case), else a binary search over the lanes' starts.  Every lane must
+// run it (the shuffles read other lanes' registers).
 __device__ __forceinline__ int lo_trace_of(int64_t e, int64_t E0, int64_t n, int64_t a) {
     if (n > 0) return (int)((uint32_t)(e - E0) / (uint32_t)n);
     int lo = 0, hi = WAVE - 1;
@@ -2196,8 +2199,10 @@ __device__ __forceinline__ int lo_trace_of(int64_t e, int64_t E0, int64_t n, int
     }
     return lo;
 }
-__global__ void __launch_bounds__(LB_T) k_lo_build_b(IxBatch<IxWinLoB> a, uint64_t epoch) {
-    // per graph g: [cnt | cov << 32] u64 x NP, then INT_MAX - first row x NP, then edge counts x nek
+constexpr int LB_R = 4;   // entry rounds per batch (their loads in flight together)
+__global__ void __launch_bounds__(LB_T, 8) k_lo_build_b(IxBatch<IxWinLoB> a, uint64_t epoch) {
+    // per graph g: [cnt | cov << 32] u64 x NP, then INT_MAX - first row x NP, then edge counts x
+    // nek; then the service-op thresholds (0 where a3v is false: adding +0.0 leaves expect as is)
     extern __shared__ __attribute__((aligned(16))) unsigned char lraw[];
     __shared__ int8_t side[LB_TILE];
     __shared__ int32_t sa[2][LB_T];
@@ -2209,7 +2214,9 @@ __global__ void __launch_bounds__(LB_T) k_lo_build_b(IxBatch<IxWinLoB> a, uint64
     const int tid = threadIdx.x, lane = tid & (WAVE - 1), wv = tid / WAVE;
     const int32_t NP = w.NP, nek = w.nek;
     const size_t gbytes = ((size_t)NP * 12 + (size_t)nek * 4 + 15) / 16 * 16;   // one graph's histograms
+    double* la3 = (double*)(lraw + 2 * gbytes);
     for (size_t x = (size_t)tid * 4; x < 2 * gbytes; x += (size_t)LB_T * 4) *(uint32_t*)(lraw + x) = 0u;
+    for (int32_t c = tid; c < w.nsvc; c += LB_T) la3[c] = w.a3v[c] ? w.a3[c] : 0.0;
     __syncthreads();
     const int64_t base = (int64_t)blk * LB_TILE;
     int64_t nz0 = 0, nz1 = 0, rows = 0;
@@ -2218,8 +2225,9 @@ __global__ void __launch_bounds__(LB_T) k_lo_build_b(IxBatch<IxWinLoB> a, uint64
         const int64_t i = base + (int64_t)j * LB_T + tid;
         const bool valid = i < w.NT;
         int64_t pa = 0, pb = 0, ea = 0, eb = 0;
-        int s_ = -1;
+        int s_ = -1, kid = -1;
         if (valid) {
+            kid = w.lo_kid[i];
             const int32_t len = w.lo_len[i];
             const long long ts = w.lo_ts[i], te = w.lo_te[i], mx = w.lo_mx[i];
             pa = w.lo_off[i];
@@ -2231,21 +2239,15 @@ __global__ void __launch_bounds__(LB_T) k_lo_build_b(IxBatch<IxWinLoB> a, uint64
             rows += in ? len : 0;
             int stt = 0;
             if (in && mx > 0) {   // grouped[grouped['duration'] > 0] (preprocess_data.py:117)
-                // expect: sequential in name order (T14), the entries' loads four at a time
+                // expect: sequential in name order (T14), the entries' loads eight at a time
                 double expect = 0.0;
-                for (int64_t e = va; e < vb; e += 4) {
-                    uint32_t v[4];
+                for (int64_t e = va; e < vb; e += 8) {
+                    uint32_t v[8];
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) v[q] = e + q < vb ? w.lsv[e + q] : 0u;
-                    double t[4];
+                    for (int q = 0; q < 8; ++q) v[q] = e + q < vb ? w.lsv[e + q] : 0u;
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const uint32_t op = v[q] & 0xffffu;
-                        t[q] = w.a3v[op] ? (double)(v[q] >> 16) * w.a3[op] : 0.0;   // anormaly_detector.py:63-67
-                    }
-#pragma unroll
-                    for (int q = 0; q < 4; ++q)
-                        if (e + q < vb) expect += t[q];
+                    for (int q = 0; q < 8; ++q)   // anormaly_detector.py:63-67
+                        if (e + q < vb) expect += (double)(v[q] >> 16) * la3[v[q] & 0xffffu];
                 }
                 stt = (double)mx / 1000.0 > expect ? 2 : 1;   // :58, :69
             }
@@ -2253,43 +2255,66 @@ __global__ void __launch_bounds__(LB_T) k_lo_build_b(IxBatch<IxWinLoB> a, uint64
             nab += stt == 2;
             nno += stt == 1;
             s_ = stt == 2 ? 0 : stt == 1 ? 1 : -1;
-            if (s_ >= 0) {
-                atomicAdd(&w.kcnt[s_][w.lo_kid[i]], 1u);
-                if (s_ == 0) nz0 += pb - pa; else nz1 += pb - pa;
-            }
+            if (s_ == 0) nz0 += pb - pa;
+            else if (s_ == 1) nz1 += pb - pa;
         }
         side[j * LB_T + tid] = (int8_t)s_;
+        {   // kind classes are runs of the layout: one add per (run, graph) of the wave
+            const int kp = __shfl_up(kid, 1, WAVE);
+            const bool hd = kid >= 0 && (lane == 0 || kp != kid);
+            const unsigned long long H = __ballot(hd), B0 = __ballot(s_ == 0), B1 = __ballot(s_ == 1);
+            if (hd) {
+                const unsigned long long above = lane == WAVE - 1 ? 0ull : H & (~0ull << (lane + 1));
+                const unsigned long long run = (above ? (above & (0ull - above)) - 1ull : ~0ull) & (~0ull << lane);
+                const uint32_t c0 = (uint32_t)__popcll(B0 & run), c1 = (uint32_t)__popcll(B1 & run);
+                if (c0) atomicAdd(&w.kcnt[0][kid], c0);
+                if (c1) atomicAdd(&w.kcnt[1][kid], c1);
+            }
+        }
         // the tile's pod-op and join entries, a lane per entry (coalesced), each to its trace's graph
         const unsigned long long vm = __ballot(valid);
         if (vm == 0ull) continue;   // (uniform: past the window's traces)
+        if (__ballot(s_ >= 0) == 0ull) continue;   // (no selected trace in the tile)
         const int last = 63 - __builtin_clzll(vm);   // (valid lanes are a prefix)
         const int64_t P0 = rfl64_(pa), P1 = rfl64_(__shfl(pb, last, WAVE));
         const int64_t Q0 = rfl64_(ea), Q1 = rfl64_(__shfl(eb, last, WAVE));
         const int64_t npo = P1 - P0 == (int64_t)(last + 1) * (rfl64_(pb) - P0) && last == WAVE - 1 ? rfl64_(pb) - P0 : 0;
         if (!valid) pa = pb = P1, ea = eb = Q1;
-        // (every lane runs every round -- the shuffles read the other lanes' registers, which an
-        // inactive lane would not provide -- and a lane past the tile's entries skips the work)
-        for (int64_t eb0 = P0; eb0 < P1; eb0 += WAVE) {
-            const int64_t e = min(eb0 + lane, P1 - 1);
-            const int kt = lo_trace_of(e, P0, npo, pa);
-            const int sk = __shfl(s_, kt, WAVE);   // (all lanes: a disabled source lane reads as 0)
-            const int sd = eb0 + lane < P1 ? sk : -1;
-            const uint16_t c = w.lo16[e];
-            const uint16_t cn = w.lo_cnt[e];
-            const int32_t fr = w.lo_first[e];
-            if (sd >= 0) {
-                unsigned char* G = lraw + (size_t)sd * gbytes;
-                atomicAdd((unsigned long long*)G + c, (unsigned long long)cn | (1ull << 32));
-                atomicMax((int32_t*)(G + (size_t)NP * 8) + c, 0x7fffffff - fr);
+        for (int64_t eb0 = P0; eb0 < P1; eb0 += LB_R * WAVE) {
+            int64_t e[LB_R];
+            uint16_t c[LB_R], cn[LB_R];
+            int32_t fr[LB_R];
+#pragma unroll
+            for (int r = 0; r < LB_R; ++r) {   // (clamped: every load in bounds)
+                e[r] = min(eb0 + r * WAVE + lane, P1 - 1);
+                c[r] = w.lo16[e[r]];
+                cn[r] = w.lo_cnt[e[r]];
+                fr[r] = w.lo_first[e[r]];
+            }
+#pragma unroll
+            for (int r = 0; r < LB_R; ++r) {
+                const int sk = __shfl(s_, lo_trace_of(e[r], P0, npo, pa), WAVE);   // (all lanes)
+                if (eb0 + r * WAVE + lane < P1 && sk >= 0) {
+                    unsigned char* G = lraw + (size_t)sk * gbytes;
+                    atomicAdd((unsigned long long*)G + c[r], (unsigned long long)cn[r] | (1ull << 32));
+                    atomicMax((int32_t*)(G + (size_t)NP * 8) + c[r], 0x7fffffff - fr[r]);
+                }
             }
         }
-        for (int64_t eb0 = Q0; eb0 < Q1; eb0 += WAVE) {
-            const int64_t e = min(eb0 + lane, Q1 - 1);
-            const int kt = lo_trace_of(e, Q0, 0, ea);
-            const int sk = __shfl(s_, kt, WAVE);
-            const int sd = eb0 + lane < Q1 ? sk : -1;
-            const uint32_t v = w.le[e];
-            if (sd >= 0) atomicAdd((uint32_t*)(lraw + (size_t)sd * gbytes + (size_t)NP * 12) + (v & 0xffffu), v >> 16);
+        for (int64_t eb0 = Q0; eb0 < Q1; eb0 += LB_R * WAVE) {
+            int64_t e[LB_R];
+            uint32_t v[LB_R];
+#pragma unroll
+            for (int r = 0; r < LB_R; ++r) {
+                e[r] = min(eb0 + r * WAVE + lane, Q1 - 1);
+                v[r] = w.le[e[r]];
+            }
+#pragma unroll
+            for (int r = 0; r < LB_R; ++r) {
+                const int sk = __shfl(s_, lo_trace_of(e[r], Q0, 0, ea), WAVE);
+                if (eb0 + r * WAVE + lane < Q1 && sk >= 0)
+                    atomicAdd((uint32_t*)(lraw + (size_t)sk * gbytes + (size_t)NP * 12) + (v[r] & 0xffffu), v[r] >> 16);
+            }
         }
     }
     {   // the detector's counts and both graphs' entry totals: per wave, per block, one add each
@@ -2356,21 +2381,59 @@ __global__ void __launch_bounds__(LB_T) k_lo_build_b(IxBatch<IxWinLoB> a, uint64
         if (sd == 0) w.pinv[0][r0++] = ix;
         else if (sd == 1) w.pinv[1][r1++] = ix;
     }
-    // the block's histograms into the window's zeroed words
+    // the block's histograms as its partial row (plain stores; k_lo_reduce_b combines the rows)
+    const size_t rw = 3 * (size_t)NP + (size_t)nek;
+    uint32_t* R = w.rows + (size_t)blk * 2 * rw;
     for (int g = 0; g < 2; ++g) {
         const unsigned char* G = lraw + (size_t)g * gbytes;
+        uint32_t* Rg = R + (size_t)g * rw;
         for (int32_t c = tid; c < NP; c += LB_T) {
             const unsigned long long v = ((const unsigned long long*)G)[c];
-            if (!v) continue;
-            atomicAdd(&w.ocnt[g][c], (int32_t)(v & 0xffffffffull));
-            atomicAdd(&w.ocov[g][c], (int32_t)(v >> 32));
-            atomicMax(&w.ofinv[g][c], ((const int32_t*)(G + (size_t)NP * 8))[c]);
+            Rg[c] = (uint32_t)v;
+            Rg[NP + c] = (uint32_t)(v >> 32);
+            Rg[2 * NP + c] = ((const uint32_t*)(G + (size_t)NP * 8))[c];
         }
-        for (int32_t x = tid; x < nek; x += LB_T) {
-            const uint32_t v = ((const uint32_t*)(G + (size_t)NP * 12))[x];
-            if (v) atomicAdd(&w.gc[g][x], v);
-        }
+        for (int32_t x = tid; x < nek; x += LB_T) Rg[3 * NP + x] = ((const uint32_t*)(G + (size_t)NP * 12))[x];
     }
+}
+// each window's partial rows, column by column: span counts, coverage and edge multiplicities
+// summed, INT_MAX - first row by max -- into the graph's words (overwritten; k_ix_cross2_b adds
+// the joins across traces after)
+struct IxLoRed {
+    const uint32_t* rows;
+    int32_t nblk, NP, nek, pad_;
+    int32_t *ocnt[2], *ofinv[2], *ocov[2];
+    uint32_t* gc[2];
+};
+__global__ void __launch_bounds__(256) k_lo_reduce_b(IxBatch<IxLoRed> a) {
+    const int k = ixb_pick(a.b0, a.n);
+    const IxLoRed& w = a.w[k];
+    const int64_t rw = 3 * (int64_t)w.NP + w.nek;
+    const int64_t col = (int64_t)((int32_t)blockIdx.x - a.b0[k]) * 256 + threadIdx.x;
+    if (col >= 2 * rw) return;
+    const int g = (int)(col / rw);
+    const int64_t c = col - (int64_t)g * rw;
+    const bool mx = c >= 2 * (int64_t)w.NP && c < 3 * (int64_t)w.NP;
+    const uint32_t* p = w.rows + col;
+    const size_t stride = 2 * (size_t)rw;
+    uint32_t acc = 0;
+    int32_t b = 0;
+    for (; b + 8 <= w.nblk; b += 8) {
+        uint32_t v[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = p[(size_t)(b + q) * stride];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc = mx ? max(acc, v[q]) : acc + v[q];
+    }
+    for (; b < w.nblk; ++b) {
+        const uint32_t v = p[(size_t)b * stride];
+        acc = mx ? max(acc, v) : acc + v;
+    }
+    const int32_t NP = w.NP;
+    if (c < NP) w.ocnt[g][c] = (int32_t)acc;
+    else if (c < 2 * (int64_t)NP) w.ocov[g][c - NP] = (int32_t)acc;
+    else if (c < 3 * (int64_t)NP) w.ofinv[g][c - 2 * NP] = (int32_t)acc;
+    else w.gc[g][c - 3 * NP] = acc;
 }
 
 // Per window (n <= IXW): k_lo_build_b, the rare joins across traces, the node order / P_ss / op
@@ -2388,10 +2451,13 @@ int mr_lo_launch_batch(mr_ctx* ctx, int n, const mr_spans* const* sps, mr_graph*
         if (!sps[k]->lo_ok || !mr_lo_fits(sps[k])) return MR_ERR_STATE;
     hipStream_t st = ctx->stream;
     IxBatch<IxWinLoB> ab{};
+    IxBatch<IxLoRed> ar{};
     IxBatch<IxWinCross> ac{};
     IxBatch<IxWinNodes> an{};
-    ab.n = ac.n = an.n = n;
-    int32_t bb = 0, bc = 0;
+    ab.n = ar.n = ac.n = an.n = n;
+    int32_t bb = 0, bc = 0, br = 0;
+    int64_t rwords = 0;
+    std::vector<int64_t> roff((size_t)n);
     size_t lds = 4;
     int64_t words = 0;
     std::vector<int64_t> woff((size_t)n);
@@ -2435,12 +2501,21 @@ int mr_lo_launch_batch(mr_ctx* ctx, int n, const mr_spans* const* sps, mr_graph*
             L.pinv[j] = B.pinv.p;
             L.kcnt[j] = B.kcnt;
             L.tot[j] = out + 5;
-            L.ocnt[j] = ocnt;
-            L.ofinv[j] = ofinv;
-            L.ocov[j] = ocov;
-            L.gc[j] = gc;
+            IxLoRed& R = ar.w[k];
+            R.ocnt[j] = ocnt;
+            R.ofinv[j] = ofinv;
+            R.ocov[j] = ocov;
+            R.gc[j] = gc;
         }
         const int32_t nt = (int32_t)std::max<int64_t>(cdiv((int64_t)NT, LB_TILE), 1);
+        const int64_t rw = 3 * (int64_t)NP + nek;
+        roff[(size_t)k] = rwords;
+        rwords += (int64_t)nt * 2 * rw;
+        ar.w[k].nblk = nt;
+        ar.w[k].NP = NP;
+        ar.w[k].nek = (int32_t)nek;
+        ar.b0[k] = br;
+        br += (int32_t)cdiv(2 * rw, 256);
         woff[(size_t)k] = words;
         words += 2 * (int64_t)nt;
         ab.b0[k] = bb;
@@ -2469,7 +2544,8 @@ int mr_lo_launch_batch(mr_ctx* ctx, int n, const mr_spans* const* sps, mr_graph*
         L.NT = NT;
         L.NP = NP;
         L.nek = (int32_t)nek;
-        lds = std::max(lds, 2 * (((size_t)NP * 12 + (size_t)nek * 4 + 15) / 16 * 16));
+        L.nsvc = sp->n_svcops;
+        lds = std::max(lds, 2 * (((size_t)NP * 12 + (size_t)nek * 4 + 15) / 16 * 16) + (size_t)sp->n_svcops * 8);
         ac.b0[k] = bc;
         bc += (int32_t)cdiv(sp->n_xj, 256);
         ac.w[k] = IxWinCross{d.state, sp->xj_tc.p, sp->xj_tp.p, sp->xj_eid.p, sp->n_xj, xs};
@@ -2478,14 +2554,22 @@ int mr_lo_launch_batch(mr_ctx* ctx, int n, const mr_spans* const* sps, mr_graph*
     }
     for (int k = n; k <= IXW; ++k) {   // (offsets past the last window: its end)
         ab.b0[k] = bb;
+        ar.b0[k] = br;
         ac.b0[k] = bc;
         an.b0[k] = 2 * n;
     }
     unsigned long long* dst = nullptr;
     uint64_t epoch = 0;
     MR_TRY(mr_dl_status(ctx, words, &dst, &epoch));
-    for (int k = 0; k < n; ++k) ab.w[k].st = dst + woff[(size_t)k];
+    DBuf<uint32_t> rows;   // (stream-ordered: freed back to this context's pool after the launches)
+    MR_TRY(rows.alloc(ctx, (size_t)std::max<int64_t>(rwords, 1)));
+    for (int k = 0; k < n; ++k) {
+        ab.w[k].st = dst + woff[(size_t)k];
+        ab.w[k].rows = rows.p + roff[(size_t)k];
+        ar.w[k].rows = rows.p + roff[(size_t)k];
+    }
     hipLaunchKernelGGL(k_lo_build_b, dim3(bb), dim3(LB_T), lds, st, ab, epoch);
+    hipLaunchKernelGGL(k_lo_reduce_b, dim3(br), dim3(256), 0, st, ar);
     if (bc) hipLaunchKernelGGL(k_ix_cross2_b, dim3(bc), dim3(256), 0, st, ac);
     hipLaunchKernelGGL(k_nodes_small2_b, dim3(2 * n), dim3(NS_T), 0, st, an);
     MR_TRY_HIP(ctx, hipGetLastError());

@@ -2001,7 +2001,6 @@ __device__ __forceinline__ int32_t fx_graph(const GDev* gs, int32_t ng, int32_t 
 
 // ---------------------------------------------------------------- fused iteration: LDS budget and su modes
 constexpr size_t WV_LDS_MAX = 160 * 1024 - 512;
-constexpr int TR_AR_DEFAULT = 1;   // (tr_ar_want)
 constexpr int LO_ROT_DEFAULT = 1;  // (mr_lo_prepare_batch)
 // su modes of k_tr_a: global gathers only / every op's su in LDS / the n_hot most covered ops' su in
 // LDS (relabelled graphs, ops [0, n_hot)), the rest gathered
@@ -2028,13 +2027,11 @@ struct TrLds {
     int32_t n_hot;    // WV_SU_HOT: su of ops [0, n_hot) in LDS
     // the accumulator first, then su (8-B strides: a 32-lane read group spreads over 32 bank
     // pairs, a 16-lane atomic group over 16)
-    // ar: accumulator replicas (k_tr_a's 512-thread window variant, TR_AR): op o of replica r at
-    // word o * ar + r, lane l adding into replica l mod ar
-    __host__ __device__ TrLds(int32_t N, int mode, int ar = 1) {
+    __host__ __device__ TrLds(int32_t N, int mode) {
         const size_t ns = (size_t)N + TR_PAD;
         su_lds = ns * 16 <= WV_LDS_MAX;
         const bool all = mode == WV_SU_ALL && su_lds;
-        const size_t accb = (ns * 8 * (size_t)ar + 15) / 16 * 16;
+        const size_t accb = (ns * 8 + 15) / 16 * 16;
         n_hot = 0;
         if (mode == WV_SU_HOT && accb < WV_LDS_MAX)
             n_hot = (int32_t)std::min<size_t>((size_t)N, (WV_LDS_MAX - accb) / 8 / 64 * 64);
@@ -2108,7 +2105,7 @@ __device__ __forceinline__ void tr_hot_sums(const GDev& G, const double* su_l, d
         hs[tid] = a;
     }
 }
-template <class Q, int NC, int EXT, int HN, int AR>
+template <class Q, int NC, int EXT, int HN>
 __device__ __forceinline__ int32_t tr_walk_short(const GDev& G, int32_t k, const int32_t ke, int32_t T, int32_t lane,
                                                  int cur, int nxt, double d, double Ms, double xsc, const double* su_l,
                                                  unsigned long long* lacc, double& rmax, TrHot<HN>& H, int32_t& c0,
@@ -2193,10 +2190,10 @@ __device__ __forceinline__ int32_t tr_walk_short(const GDev& G, int32_t k, const
         for (int j = 0; j < NC; ++j) {
             if (j + 1 < NC) rd(r.id[j + 1], sv[(j + 1) & 1]);
             const u32x2 w = r.id[j];
-            atomicAdd(&lacc[(w.x & 0xffffu) * AR], X);   // (lacc: this lane's replica)
-            atomicAdd(&lacc[(w.x >> 16) * AR], X);
-            atomicAdd(&lacc[(w.y & 0xffffu) * AR], X);
-            atomicAdd(&lacc[(w.y >> 16) * AR], X);
+            atomicAdd(&lacc[(w.x & 0xffffu)], X);
+            atomicAdd(&lacc[(w.x >> 16)], X);
+            atomicAdd(&lacc[(w.y & 0xffffu)], X);
+            atomicAdd(&lacc[(w.y >> 16)], X);
 #pragma unroll
             for (int i = 0; i < 4; ++i) acc += sv[j & 1][i];
         }
@@ -2249,7 +2246,7 @@ __device__ __forceinline__ int32_t tr_walk_short(const GDev& G, int32_t k, const
 // The wave's walk of k_tr_a over its run of wave tiles: per entry one
 // su read, one add into the lane's trace sum, one LDS u64 atomic of X_t; per tile r' of its traces
 // and their next q.  Returns the wave's largest r' (-inf when it owns no trace).
-template <class Q, int SUM, int NT, int EXT = 0, bool HOTT = false, int AR = 1>
+template <class Q, int SUM, int NT, int EXT = 0, bool HOTT = false>
 __device__ __forceinline__ double tr_walk(const GDev& G, int32_t lb, int cur, int nxt, int32_t N, int32_t NH, double d,
                                           double Ms, double xsc, const double* su_l, unsigned long long* lacc,
                                           const double* hs = nullptr) {
@@ -2276,12 +2273,11 @@ __device__ __forceinline__ double tr_walk(const GDev& G, int32_t lb, int cur, in
 #pragma unroll
     for (int h = 0; h < HN; ++h) H.acc[h] = 0ull;
     const int32_t k_first = k;
-    unsigned long long* const lacc_l = lacc + (lane & (AR - 1));   // this lane's accumulator replica
     if constexpr (SUL) {
         // one tier per chunk count (the run's tiles ascend in it): every count static, no branch
         // inside a tile, so each wait is for exactly the LDS reads and loads it consumes
         int32_t tc0 = 0, tn = -1, tq0 = 0, tnq = 0;   // the next tile's ranges, handed from tier to tier
-#define TR_TIER(NC_) if (NC_ <= (NT == 1024 || EXT ? TR_TIERS_EXT : MR_TR_TIERS512) && k < ke) k = tr_walk_short<Q, NC_, EXT, HN, AR>(G, k, ke, T, lane, cur, nxt, d, Ms, xsc, su_l, lacc_l, rmax, H, tc0, tn, tq0, tnq);
+#define TR_TIER(NC_) if (NC_ <= (NT == 1024 || EXT ? TR_TIERS_EXT : MR_TR_TIERS512) && k < ke) k = tr_walk_short<Q, NC_, EXT, HN>(G, k, ke, T, lane, cur, nxt, d, Ms, xsc, su_l, lacc, rmax, H, tc0, tn, tq0, tnq);
         TR_TIER(1) TR_TIER(2) TR_TIER(3) TR_TIER(4) TR_TIER(5) TR_TIER(6) TR_TIER(7) TR_TIER(8)
 #undef TR_TIER
     }
@@ -2347,7 +2343,7 @@ __device__ __forceinline__ double tr_walk(const GDev& G, int32_t lb, int cur, in
             if (SUL || HOT) lds_su(NXT, SN);                                                               \
             const int32_t o_[4] = {(int32_t)(CUR.x & 0xffffu), (int32_t)(CUR.x >> 16),                     \
                                    (int32_t)(CUR.y & 0xffffu), (int32_t)(CUR.y >> 16)};                    \
-            _Pragma("unroll") for (int j = 0; j < 4; ++j) atomicAdd(&lacc_l[o_[j] * AR], X);                 \
+            _Pragma("unroll") for (int j = 0; j < 4; ++j) atomicAdd(&lacc[o_[j]], X);                         \
             _Pragma("unroll") for (int j = 0; j < 4; ++j)                                                  \
                 acc += SUL ? SC[j] : HOT ? (o_[j] < NH ? SC[j] : GC[j]) : GC[j];                          \
             if (++c == ce) {                                                                               \
@@ -2387,7 +2383,7 @@ __device__ __forceinline__ double tr_walk(const GDev& G, int32_t lb, int cur, in
                 unsigned long long a = H.acc[h];
 #pragma unroll
                 for (int m = WAVE / 2; m >= 1; m >>= 1) a += (unsigned long long)__shfl_xor((long long)a, m, WAVE);
-                if (lane == 0) atomicAdd(&lacc[G.hop[h] * AR], a);
+                if (lane == 0) atomicAdd(&lacc[G.hop[h]], a);
             }
     return rmax;
 }
@@ -2535,15 +2531,7 @@ __device__ __forceinline__ void tr_last_finish(const GDev& G, int it, double d, 
     }
 }
 
-// op o's column of the block's partial row: its AR replicas (integers: the sum is order-free)
-template <int AR>
-__device__ __forceinline__ unsigned long long tr_acc_sum(const unsigned long long* lacc, int32_t o) {
-    unsigned long long v = 0ull;
-#pragma unroll
-    for (int r = 0; r < AR; ++r) v += lacc[(size_t)o * AR + r];
-    return v;
-}
-template <class Q, int SUM, int NT, int EXT, int AR = 1>
+template <class Q, int SUM, int NT, int EXT>
 __global__ void __launch_bounds__(NT) k_tr_a(const GDev* __restrict__ gs, int32_t ng, int32_t split, double d,
                                              double alpha, int it, int32_t unused) {
     constexpr bool SUL = SUM == WV_SU_ALL, HOT = SUM == WV_SU_HOT;
@@ -2556,7 +2544,7 @@ __global__ void __launch_bounds__(NT) k_tr_a(const GDev* __restrict__ gs, int32_
     const int cur = it & 1, nxt = cur ^ 1, k3 = it % 3;
     const int32_t N = G.NA;   // (wide graphs: the hot ops)
     const int32_t tid = (int32_t)threadIdx.x;
-    const TrLds L_(N, SUM, AR);
+    const TrLds L_(N, SUM);
     const int32_t NH = HOT ? G.n_hot : 0;   // <= L_.n_hot (the host sizes both alike), >= 64
     const GLB double* sug = gp(G.sub[cur]);   // ids >= N are pads (su 0)
     double* su_l = (double*)(lraw + L_.su);
@@ -2567,7 +2555,7 @@ __global__ void __launch_bounds__(NT) k_tr_a(const GDev* __restrict__ gs, int32_
     if (lb == 0 && tid < 2 * MSH) mslot[(size_t)2 * MSH * ((k3 + 2) % 3) + tid] = 0ull;
     if (SUL)
         for (int32_t o = tid; o < N + TR_PAD; o += NT) su_l[o] = o < N ? sug[o] : 0.0;
-    for (int32_t o = tid; o < (N + TR_PAD) * AR; o += NT) lacc[o] = 0ull;
+    for (int32_t o = tid; o < N + TR_PAD; o += NT) lacc[o] = 0ull;
     if (HOT)
         for (int32_t o = tid; o < NH; o += NT) su_l[o] = sug[o];
     __shared__ int s_ssv;   // the call-graph term chunks taken (G.ssv_pre)
@@ -2589,7 +2577,7 @@ __global__ void __launch_bounds__(NT) k_tr_a(const GDev* __restrict__ gs, int32_
         __syncthreads();
     }
     const double xsc = (G.dscale ? G.dscale[0] : G.fx_scale) / msh[1], Ms = msh[0];
-    const double rmax_w = tr_walk<Q, SUM, NT, EXT, HOTT, AR>(G, lb, cur, nxt, N, NH, d, Ms, xsc, su_l, lacc, hs);
+    const double rmax_w = tr_walk<Q, SUM, NT, EXT, HOTT>(G, lb, cur, nxt, N, NH, d, Ms, xsc, su_l, lacc, hs);
     // the call-graph terms of this block's share of the columns, by the waves done walking
     if (G.ssv_pre) tr_ssv_share(G, lb, cur, Ms, &s_ssv, tid & (WAVE - 1));
     __syncthreads();
@@ -2597,7 +2585,7 @@ __global__ void __launch_bounds__(NT) k_tr_a(const GDev* __restrict__ gs, int32_
     if constexpr (NT == 512) {   // (window-graph variant only: the large graphs' kernel stays as it is)
         if (G.lastfin) {
             for (int32_t o = tid; o < N; o += NT)   // write-through: the last block reads them with sc1 loads
-                __hip_atomic_store(prow + o, tr_acc_sum<AR>(lacc, o), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(prow + o, lacc[o], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const double rmax = block_max(rmax_w, red);
             if (tid == 0 && rmax >= 0.0) atomicMax((unsigned long long*)&Mnext[MSH + blockIdx.x % MSH], d2bits(rmax));
             tr_last_finish<NT>(G, it, d, Ms, Mnext);
@@ -2606,9 +2594,9 @@ __global__ void __launch_bounds__(NT) k_tr_a(const GDev* __restrict__ gs, int32_
     }
     if (G.row_wt)   // write-through (sc1): the boundary to k_fx_b has no dirty lines to write back
         for (int32_t o = tid; o < N; o += NT)
-            __hip_atomic_store(prow + o, tr_acc_sum<AR>(lacc, o), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(prow + o, lacc[o], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     else
-        for (int32_t o = tid; o < N; o += NT) prow[o] = tr_acc_sum<AR>(lacc, o);
+        for (int32_t o = tid; o < N; o += NT) prow[o] = lacc[o];
     const double rmax = block_max(rmax_w, red);
     if (tid == 0 && rmax >= 0.0)   // -inf: a block without traces (an empty shard's placeholder)
         atomicMax((unsigned long long*)&Mnext[MSH + blockIdx.x % MSH], d2bits(rmax));
@@ -3167,13 +3155,7 @@ void mr_prof_end(mr_ctx* ctx, double bytes, int64_t iters = 1);
 using TrA = void (*)(const GDev*, int32_t, int32_t, double, double, int, int32_t);
 // ext: some graph of the launch carries kind multiplicities (bit 0: mw_tp) or a cold side (bit 1:
 // wide graphs) -- only the short-tile walk of the su-in-LDS mode distinguishes them
-// ar > 1: the 512-thread su-in-LDS variant with accumulator replicas (TR_AR; no ext)
-static TrA tr_kernel(bool fp32, int mode, int NT, int ext = 0, int ar = 1) {
-    static const TrA tab_ar[2][4] = {
-        {k_tr_a<double, 1, 512, 0, 2>, k_tr_a<double, 1, 512, 0, 4>, k_tr_a<double, 1, 512, 0, 8>, k_tr_a<double, 1, 512, 0, 16>},
-        {k_tr_a<float, 1, 512, 0, 2>, k_tr_a<float, 1, 512, 0, 4>, k_tr_a<float, 1, 512, 0, 8>, k_tr_a<float, 1, 512, 0, 16>}};
-    if (ar > 1 && !ext && mode == WV_SU_ALL && NT == 512)
-        return tab_ar[fp32 ? 1 : 0][ar == 2 ? 0 : ar == 4 ? 1 : ar == 8 ? 2 : 3];
+static TrA tr_kernel(bool fp32, int mode, int NT, int ext = 0) {
     static const TrA tab[2][3][2] = {
         {{k_tr_a<double, 0, 512, 0>, k_tr_a<double, 0, 1024, 0>},
          {k_tr_a<double, 1, 512, 0>, k_tr_a<double, 1, 1024, 0>},
@@ -3206,17 +3188,7 @@ struct FxPlan {
     int NT = 1024;      // block size (16 waves; 512 when the graphs are small)
     int mode = WV_SU_ALL;   // su in LDS for every fused graph of the batch / hot ops / none
     bool sul = true;    // mode == WV_SU_ALL
-    int ar = 1;         // accumulator replicas (tr_kernel)
 };
-// k_tr_a's accumulator replicas for the 512-thread window variant: the LDS u64 adds of a 16-lane
-// group go to bank pairs (op * AR + lane mod AR) mod 16, so lanes of different replicas never
-// share a bank pair and the random-op bank conflicts (and the same-address adds of popular ops)
-// fall with AR.  MR_TR_AR (read per call): 1 / 2 / 4 / 8 / 16
-static int tr_ar_want() {
-    const char* e = getenv("MR_TR_AR");
-    const int v = e ? atoi(e) : TR_AR_DEFAULT;
-    return v >= 16 ? 16 : v >= 8 ? 8 : v >= 4 ? 4 : v >= 2 ? 2 : 1;
-}
 static FxPlan fx_plan(mr_graph* const* gs, int ng) {
     FxPlan P;
     int32_t nmax = 0;
@@ -3239,22 +3211,17 @@ static FxPlan fx_plan(mr_graph* const* gs, int ng) {
         for (int i = 0; i < ng; ++i)
             if (gs[i]->fused && !gs[i]->relabeled) P.mode = WV_SU_GLOBAL;
     if (P.mode == WV_SU_HOT && TrLds(nmax, WV_SU_HOT).n_hot < 64) P.mode = WV_SU_GLOBAL;
-    bool plain = P.NT == 512 && P.mode == WV_SU_ALL;   // (kind-compressed / wide graphs: no replicas)
-    for (int i = 0; i < ng; ++i)
-        if (gs[i]->fused) plain = plain && !gs[i]->mw_tp.p && !gs[i]->wide && !gs[i]->nhr;
-    if (plain)
-        for (P.ar = tr_ar_want(); P.ar > 1 && TrLds(nmax, WV_SU_ALL, P.ar).total > WV_LDS_MAX; P.ar >>= 1) {}
     return P;
 }
 static int32_t plan_n_hot(int32_t N, const FxPlan& P) {
     return P.mode == WV_SU_HOT ? TrLds(N, WV_SU_HOT).n_hot : 0;
 }
-static size_t plan_lds(int32_t N, const FxPlan& P) { return TrLds(N, P.mode, P.ar).total; }
+static size_t plan_lds(int32_t N, const FxPlan& P) { return TrLds(N, P.mode).total; }
 
 // resident blocks of the plan's kernel on the chip (occupancy by LDS image and VGPRs)
 static int64_t plan_resident(int32_t N, const FxPlan& P) {
     const size_t lds = plan_lds(N, P);
-    const TrA kfn = tr_kernel(false, P.mode, P.NT, 0, P.ar);
+    const TrA kfn = tr_kernel(false, P.mode, P.NT, 0);
     int n = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, (const void*)kfn, P.NT, lds) != hipSuccess || n < 1)
         n = std::max<int>(1, (int)(WV_LDS_MAX / std::max<size_t>(lds, 1)));
@@ -4505,7 +4472,7 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
     for (int i = 0; i < ng; ++i)   // the wide variant carries HOT_MAX_WIDE hot accumulators
         if ((any_ext & 2) && gs[i]->fused && gs[i]->nhr > HOT_MAX_WIDE)
             return mr_fail(ctx, MR_ERR_ARG, "pagerank batch: a hot-op layout of %d ops beside a wide graph", gs[i]->nhr);
-    const TrA tr_a = tr_kernel(fp32, plan.mode, plan.NT, any_ext, any_ext ? 1 : plan.ar);
+    const TrA tr_a = tr_kernel(fp32, plan.mode, plan.NT, any_ext);
     // a sharded graph with no collective backend is one whole shard: the split launches around the
     // (no-op) all-reduces would compute the same integers / sums in two halves
     const bool coll = sharded && mr_coll_ready(ctx);

@@ -202,47 +202,69 @@ __global__ void k_ix_edge_runs(const uint64_t* key, const int32_t* head, const i
 }
 
 // ---------------------------------------------------------------- layout order (lo_index)
-// Traces sorted by distinct pod-op count, then code: key n << nbt | t
-__global__ void k_lo_keys(const int64_t* po_off, int32_t NT, int nbt, uint64_t* key) {
-    const int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t < NT) key[t] = ((uint64_t)(po_off[t + 1] - po_off[t]) << nbt) | (uint32_t)t;
+// the set hash of each trace's kind key (pagerank.py:54-66: op set, fp32(1/len_t), count;
+// order-free), read from the trace's pod-op runs in code order
+__device__ __forceinline__ uint64_t lo_mix(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
 }
-__global__ void k_lo_unpack(const uint64_t* key, int32_t NT, int nbt, const int32_t* tlen, int32_t* lo_tr, int32_t* lo_n,
-                            int32_t* lo_len) {
+__device__ __forceinline__ float lo_w(int32_t len) { return len > 0 ? (float)(1.0 / (double)len) : 0.0f; }
+__global__ void k_lo_hash(const int64_t* po_off, const int32_t* po_op, const int32_t* tlen, int32_t NT, uint64_t seed,
+                          uint64_t* hkey, uint32_t* tr) {
+    const int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= NT) return;
+    const int64_t o = po_off[t], n = po_off[t + 1] - o;
+    uint64_t acc = 0;
+    for (int64_t e = 0; e < n; ++e) acc += lo_mix((uint64_t)po_op[o + e] ^ seed);
+    hkey[t] = lo_mix(lo_mix(seed ^ (uint64_t)__float_as_uint(lo_w(tlen[t])) ^ ((uint64_t)n << 32)) + acc);
+    tr[t] = (uint32_t)t;
+}
+// (sorted by hash, stably: trace codes ascending within a hash) key = count << nbt | hash rank
+__global__ void k_lo_keys(const uint32_t* tr_h, const int64_t* po_off, int32_t NT, int nbt, uint64_t* key) {
+    const int32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= NT) return;
+    const uint32_t t = tr_h[j];
+    key[j] = ((uint64_t)(po_off[t + 1] - po_off[t]) << nbt) | (uint32_t)j;
+}
+// layout index i: the trace, its entry count and span count; head: a new (count, hash) run
+__global__ void k_lo_unpack(const uint64_t* key, const uint32_t* tr_h, const uint64_t* hkey_h, int32_t NT, int nbt,
+                            const int32_t* tlen, int32_t* lo_tr, int32_t* lo_n, int32_t* lo_len, int32_t* head) {
     const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= NT) return;
-    const uint64_t k = key[i];
-    const int32_t t = (int32_t)(k & ((1ull << nbt) - 1ull));
+    const uint64_t m = (1ull << nbt) - 1ull, k = key[i];
+    const uint32_t j = (uint32_t)(k & m);
+    const int32_t t = (int32_t)tr_h[j];
     lo_tr[i] = t;
     lo_n[i] = (int32_t)(k >> nbt);
     lo_len[i] = tlen[t];
+    bool h = i == 0;
+    if (!h) {
+        const uint64_t kp = key[i - 1];
+        h = (kp >> nbt) != (k >> nbt) || hkey_h[(uint32_t)(kp & m)] != hkey_h[j];
+    }
+    head[i] = h ? 1 : 0;
 }
-// each trace's entries into its layout slot: pod-op codes / span counts / first rows, its detector
-// scalars, and its service-op and join entry counts (the copies below); bad: a count or code past
-// the 16-bit packing (the table then keeps the general window path)
+// each trace's entries into its layout slot (code order): pod-op codes / span counts / first rows,
+// its detector scalars, and its service-op and join entry counts (the copies below); bad: a count
+// or code past the 16-bit packing (the table then keeps the general window path)
 __global__ void k_lo_copy(const int32_t* lo_tr, const int64_t* lo_off, int32_t NT, const int64_t* po_off,
                           const int32_t* po_op, const int32_t* po_cnt, const int32_t* po_first, const long long* tts,
                           const long long* tte, const long long* tmaxd, const int64_t* sv_off, const int64_t* ed_off,
                           uint16_t* lo16, uint16_t* lo_cnt, int32_t* lo_first, long long* lo_ts, long long* lo_te,
-                          long long* lo_mx, int32_t* nsv, int32_t* ned, int32_t* bad, const int32_t* prank) {
+                          long long* lo_mx, int32_t* nsv, int32_t* ned, int32_t* bad) {
     const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= NT) return;
     const int32_t t = lo_tr[i];
     const int64_t a = po_off[t], n = po_off[t + 1] - a, o = lo_off[i];
     bool big = false;
     for (int64_t e = 0; e < n; ++e) {
-        const int32_t c = po_cnt[a + e], op = po_op[a + e], fr = po_first[a + e];
+        const int32_t c = po_cnt[a + e];
         big = big || c > 65535;
-        int64_t j = e;   // prank: the trace's ops by table-wide popularity (insertion into place)
-        if (prank)
-            for (const int32_t key = prank[op]; j > 0 && prank[lo16[o + j - 1]] > key; --j) {
-                lo16[o + j] = lo16[o + j - 1];
-                lo_cnt[o + j] = lo_cnt[o + j - 1];
-                lo_first[o + j] = lo_first[o + j - 1];
-            }
-        lo16[o + j] = (uint16_t)op;
-        lo_cnt[o + j] = (uint16_t)c;
-        lo_first[o + j] = fr;
+        lo16[o + e] = (uint16_t)po_op[a + e];
+        lo_cnt[o + e] = (uint16_t)c;
+        lo_first[o + e] = po_first[a + e];
     }
     lo_ts[i] = tts[t];
     lo_te[i] = tte[t];
@@ -250,16 +272,6 @@ __global__ void k_lo_copy(const int32_t* lo_tr, const int64_t* lo_off, int32_t N
     nsv[i] = (int32_t)(sv_off[t + 1] - sv_off[t]);
     ned[i] = (int32_t)(ed_off[t + 1] - ed_off[t]);
     if (big) atomicOr(bad, 1);
-}
-__global__ void __launch_bounds__(256) k_lo_cov(const int32_t* po_op, int64_t n, int32_t NP, int32_t* cov) {
-    extern __shared__ int32_t lc[];   // (a popular op's adds stay in LDS: one global add per block and code)
-    for (int32_t c = threadIdx.x; c < NP; c += 256) lc[c] = 0;
-    __syncthreads();
-    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256)
-        atomicAdd(&lc[po_op[e]], 1);
-    __syncthreads();
-    for (int32_t c = threadIdx.x; c < NP; c += 256)
-        if (lc[c]) atomicAdd(&cov[c], lc[c]);
 }
 __global__ void k_lo_copy2(const int32_t* lo_tr, int32_t NT, const int64_t* sv_off, const int32_t* sv_op,
                            const int32_t* sv_cnt, const int64_t* ed_off, const int32_t* ed_eid, const int32_t* ed_cnt,
@@ -280,42 +292,22 @@ __global__ void k_lo_copy2(const int32_t* lo_tr, int32_t NT, const int64_t* sv_o
     }
     if (big) atomicOr(bad, 1);
 }
-// the set hash of each trace's kind key (pagerank.py:54-66: op set, fp32(1/len_t), count; order-free)
-__device__ __forceinline__ uint64_t lo_mix(uint64_t z) {
-    z += 0x9E3779B97F4A7C15ull;
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    return z ^ (z >> 31);
+// classes = the (count, hash) runs of the layout: class id = the run's index; every member is
+// compared exactly with the run's first trace (its span-count weight and op list)
+__global__ void k_lo_reps(const int32_t* head, const int64_t* hpos, int32_t NT, int32_t* rep) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < NT && head[i]) rep[hpos[i]] = i;
 }
-__global__ void k_lo_hash(const int64_t* lo_off, const uint16_t* lo16, const int32_t* lo_len, int32_t NT, uint64_t seed,
-                          uint64_t* hkey, uint32_t* hval) {
+__global__ void k_lo_classes(const int32_t* head, const int64_t* hpos, const int32_t* rep, int32_t NT,
+                             const int64_t* lo_off, const uint16_t* lo16, const int32_t* lo_len, int32_t* lo_kid,
+                             int32_t* bad) {
     const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= NT) return;
-    const int64_t o = lo_off[i], n = lo_off[i + 1] - o;
-    uint64_t acc = 0;
-    for (int64_t e = 0; e < n; ++e) acc += lo_mix((uint64_t)lo16[o + e] ^ seed);
-    const float w = lo_len[i] > 0 ? (float)(1.0 / (double)lo_len[i]) : 0.0f;
-    hkey[i] = lo_mix(lo_mix(seed ^ (uint64_t)__float_as_uint(w) ^ ((uint64_t)n << 32)) + acc);
-    hval[i] = (uint32_t)i;
-}
-// classes = runs of equal hashes (sorted); the run's first member (smallest layout index: the
-// sort is stable) is its representative, and every member is compared with it exactly
-__global__ void k_lo_reps(const int32_t* head, const int64_t* hpos, const uint32_t* hval, int32_t NT, int32_t* rep) {
-    const int32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j < NT && head[j]) rep[hpos[j]] = (int32_t)hval[j];
-}
-__global__ void k_lo_classes(const int32_t* head, const int64_t* hpos, const uint32_t* hval, const int32_t* rep,
-                             int32_t NT, const int64_t* lo_off, const uint16_t* lo16, const int32_t* lo_len,
-                             int32_t* lo_kid, int32_t* bad) {
-    const int32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= NT) return;
-    const int32_t k = (int32_t)hpos[j] + head[j] - 1, i = (int32_t)hval[j], r = rep[k];
+    const int32_t k = (int32_t)hpos[i] + head[i] - 1, r = rep[k];
     lo_kid[i] = k;
     if (r == i) return;
     const int64_t a = lo_off[i], n = lo_off[i + 1] - a, b = lo_off[r];
-    const float wi = lo_len[i] > 0 ? (float)(1.0 / (double)lo_len[i]) : 0.0f;
-    const float wr = lo_len[r] > 0 ? (float)(1.0 / (double)lo_len[r]) : 0.0f;
-    bool eq = n == lo_off[r + 1] - b && __float_as_uint(wi) == __float_as_uint(wr);
+    bool eq = n == lo_off[r + 1] - b && __float_as_uint(lo_w(lo_len[i])) == __float_as_uint(lo_w(lo_len[r]));
     for (int64_t e = 0; eq && e < n; ++e) eq = lo16[a + e] == lo16[b + e];
     if (!eq) atomicOr(bad, 1);
 }
@@ -454,7 +446,9 @@ static int trace_runs(mr_ctx* ctx, const mr_spans* s, const int32_t* code, int32
 }
 
 // The table's layout order, u16 code lists and exact kind classes (mr_spans.lo_*): window graphs
-// of tables within the one-pass limits tile from them (mr_lo_launch_batch).  A hash collision
+// of tables within the one-pass limits tile from them (mr_lo_launch_batch).  Layout order: distinct
+// pod-op count, then kind hash, then code -- a kind class is a contiguous run of the layout (its id
+// the run's index), so a window counts a run's members with one add per wave.  A hash collision
 // that the exact comparison finds retries with the next seed; after four the table keeps the
 // general window path (lo_ok false).
 static int lo_index(mr_ctx* ctx, mr_spans* s) {
@@ -466,20 +460,21 @@ static int lo_index(mr_ctx* ctx, mr_spans* s) {
         return MR_OK;
     const int nbt = std::max(1, bits_for((uint64_t)std::max(NT - 1, 0)));
     const int nbn = bits_for((uint64_t)s->n_podops);
-    DBuf<uint64_t> key;
-    DBuf<uint32_t> hval;
+    DBuf<uint64_t> hkey, key;
+    DBuf<uint32_t> tr_h;
     DBuf<int32_t> lo_n, nsv, ned, head, rep, bad;
     DBuf<int64_t> hpos, tmp;
+    MR_TRY(hkey.alloc(ctx, (size_t)NT));
+    MR_TRY(rep.alloc(ctx, (size_t)NT));
     MR_TRY(key.alloc(ctx, (size_t)NT));
-    MR_TRY(hval.alloc(ctx, (size_t)NT));
+    MR_TRY(tr_h.alloc(ctx, (size_t)NT));
     MR_TRY(lo_n.alloc(ctx, (size_t)NT));
     MR_TRY(nsv.alloc(ctx, (size_t)NT));
     MR_TRY(ned.alloc(ctx, (size_t)NT));
     MR_TRY(head.alloc(ctx, (size_t)NT));
-    MR_TRY(rep.alloc(ctx, (size_t)NT));
     MR_TRY(hpos.alloc(ctx, (size_t)NT + 1));
     MR_TRY(tmp.alloc(ctx, (size_t)scan_tmp_elems(NT)));
-    MR_TRY(bad.zero(ctx, 1));
+    MR_TRY(bad.alloc(ctx, 1));
     MR_TRY(s->lo_tr.alloc(ctx, (size_t)NT));
     MR_TRY(s->lo_len.alloc(ctx, (size_t)NT));
     MR_TRY(s->lo_kid.alloc(ctx, (size_t)NT));
@@ -494,73 +489,50 @@ static int lo_index(mr_ctx* ctx, mr_spans* s) {
     MR_TRY(s->le_off.alloc(ctx, (size_t)NT + 1));
     MR_TRY(s->lsv.alloc(ctx, (size_t)std::max<int64_t>(s->n_sv, 1)));
     MR_TRY(s->le.alloc(ctx, (size_t)std::max<int64_t>(s->n_ed, 1)));
-    hipLaunchKernelGGL(k_lo_keys, dim3(cdiv(NT, XB)), dim3(XB), 0, st, s->po_off.p, NT, nbt, key.p);
-    {
+    const bool collide = getenv("MR_KIND_TEST_COLLIDE") != nullptr;   // (tests: every hash equal -> rerun)
+    for (int attempt = 0; attempt < 4; ++attempt) {
+        const uint64_t seed = 0x51ed270b27a3c0deull + 0x9E3779B97F4A7C15ull * (uint64_t)attempt;
+        MR_TRY(bad.zero(ctx, 1));
+        hipLaunchKernelGGL(k_lo_hash, dim3(cdiv(NT, XB)), dim3(XB), 0, st, s->po_off.p, s->po_op.p, s->tlen.p, NT, seed,
+                           hkey.p, tr_h.p);
+        if (collide && attempt == 0) MR_TRY_HIP(ctx, hipMemsetAsync(hkey.p, 0, (size_t)NT * 8, st));
         SortScratch ws;
+        MR_TRY(mr_radix_sort(ctx, hkey.p, tr_h.p, NT, 64, ws));   // (stable: codes ascending within a hash)
+        hipLaunchKernelGGL(k_lo_keys, dim3(cdiv(NT, XB)), dim3(XB), 0, st, tr_h.p, s->po_off.p, NT, nbt, key.p);
         MR_TRY(mr_radix_sort(ctx, key.p, nullptr, NT, nbt + nbn, ws));
-        hipLaunchKernelGGL(k_lo_unpack, dim3(cdiv(NT, XB)), dim3(XB), 0, st, key.p, NT, nbt, s->tlen.p, s->lo_tr.p, lo_n.p,
-                           s->lo_len.p);
+        hipLaunchKernelGGL(k_lo_unpack, dim3(cdiv(NT, XB)), dim3(XB), 0, st, key.p, tr_h.p, hkey.p, NT, nbt, s->tlen.p,
+                           s->lo_tr.p, lo_n.p, s->lo_len.p, head.p);
         MR_TRY(mr_exclusive_scan_i32(ctx, lo_n.p, s->lo_off.p, NT, tmp.p));
-        // each trace's ops in the order of their table-wide coverage (most covered first): a tile's
-        // lanes then hold the popular ops in the same id chunks -- one LDS broadcast per su read of
-        // such an op, and the accumulator replicas keep its adds apart (MR_LO_POP=0: code order)
-        DBuf<int32_t> prank;
-        std::vector<int32_t> rk;   // (alive until the stream has copied it: the sync below)
-        const char* pe = getenv("MR_LO_POP");   // (A/B, read per table)
-        if (!(pe && atoi(pe) == 0)) {
-            const int32_t NP = s->n_podops;
-            DBuf<int32_t> cov;
-            MR_TRY(cov.zero(ctx, (size_t)std::max(NP, 1)));
-            if (s->n_po)
-                hipLaunchKernelGGL(k_lo_cov, dim3(std::min(512, cdiv(s->n_po, XB))), dim3(XB), (size_t)NP * sizeof(int32_t),
-                                   st, s->po_op.p, s->n_po, NP, cov.p);
-            std::vector<int32_t> hc((size_t)std::max(NP, 1)), ord((size_t)NP);
-            rk.assign((size_t)std::max(NP, 1), 0);
-            MR_TRY(cov.download(ctx, hc.data(), (size_t)NP));
-            MR_TRY_HIP(ctx, hipStreamSynchronize(st));
-            for (int32_t c = 0; c < NP; ++c) ord[(size_t)c] = c;
-            std::stable_sort(ord.begin(), ord.end(), [&](int32_t x, int32_t y) { return hc[(size_t)x] > hc[(size_t)y]; });
-            for (int32_t r = 0; r < NP; ++r) rk[(size_t)ord[(size_t)r]] = r;
-            MR_TRY(prank.upload(ctx, rk.data(), (size_t)std::max(NP, 1)));
-        }
         hipLaunchKernelGGL(k_lo_copy, dim3(cdiv(NT, XB)), dim3(XB), 0, st, s->lo_tr.p, s->lo_off.p, NT, s->po_off.p,
                            s->po_op.p, s->po_cnt.p, s->po_first.p, s->tts.p, s->tte.p, s->tmaxd.p, s->sv_off.p,
                            s->ed_off.p, s->lo16.p, s->lo_cnt.p, s->lo_first.p, s->lo_ts.p, s->lo_te.p, s->lo_mx.p, nsv.p,
-                           ned.p, bad.p, prank.p);
+                           ned.p, bad.p);
+        int32_t hb = 0;
+        MR_TRY(bad.download(ctx, &hb, 1));
+        MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+        if (hb) return MR_OK;   // (counts past 16 bits: the general window path)
+        MR_TRY(mr_exclusive_scan_i32(ctx, head.p, hpos.p, NT, tmp.p));
+        hipLaunchKernelGGL(k_lo_reps, dim3(cdiv(NT, XB)), dim3(XB), 0, st, head.p, hpos.p, NT, rep.p);
+        hipLaunchKernelGGL(k_lo_classes, dim3(cdiv(NT, XB)), dim3(XB), 0, st, head.p, hpos.p, rep.p, NT, s->lo_off.p,
+                           s->lo16.p, s->lo_len.p, s->lo_kid.p, bad.p);
+        MR_TRY_HIP(ctx, hipGetLastError());
+        int64_t nk = 0;
+        MR_TRY_HIP(ctx, hipMemcpyAsync(&nk, hpos.p + NT, sizeof nk, hipMemcpyDeviceToHost, st));
+        MR_TRY(bad.download(ctx, &hb, 1));
+        MR_TRY_HIP(ctx, hipStreamSynchronize(st));   // (the sorts' scratch leaves scope)
+        if (hb) continue;   // (a collision: the next seed)
         MR_TRY(mr_exclusive_scan_i32(ctx, nsv.p, s->lsv_off.p, NT, tmp.p));
         MR_TRY(mr_exclusive_scan_i32(ctx, ned.p, s->le_off.p, NT, tmp.p));
         hipLaunchKernelGGL(k_lo_copy2, dim3(cdiv(NT, XB)), dim3(XB), 0, st, s->lo_tr.p, NT, s->sv_off.p, s->sv_op.p,
                            s->sv_cnt.p, s->ed_off.p, s->ed_eid.p, s->ed_cnt.p, s->lsv_off.p, s->le_off.p, s->lsv.p,
                            s->le.p, bad.p);
         MR_TRY_HIP(ctx, hipGetLastError());
-        int32_t hb = 0;
-        MR_TRY(bad.download(ctx, &hb, 1));
-        MR_TRY_HIP(ctx, hipStreamSynchronize(st));   // (the sort's scratch leaves scope)
-        if (hb) return MR_OK;   // (counts or codes past 16 bits: the general window path)
-    }
-    for (int attempt = 0; attempt < 4; ++attempt) {
-        const uint64_t seed = 0x51ed270b27a3c0deull + 0x9E3779B97F4A7C15ull * (uint64_t)attempt;
-        MR_TRY(bad.zero(ctx, 1));
-        hipLaunchKernelGGL(k_lo_hash, dim3(cdiv(NT, XB)), dim3(XB), 0, st, s->lo_off.p, s->lo16.p, s->lo_len.p, NT, seed,
-                           key.p, hval.p);
-        SortScratch ws;
-        MR_TRY(mr_radix_sort(ctx, key.p, hval.p, NT, 64, ws));
-        hipLaunchKernelGGL(k_ix_heads, dim3(cdiv(NT, XB)), dim3(XB), 0, st, key.p, (int64_t)NT, head.p);
-        MR_TRY(mr_exclusive_scan_i32(ctx, head.p, hpos.p, NT, tmp.p));
-        hipLaunchKernelGGL(k_lo_reps, dim3(cdiv(NT, XB)), dim3(XB), 0, st, head.p, hpos.p, hval.p, NT, rep.p);
-        hipLaunchKernelGGL(k_lo_classes, dim3(cdiv(NT, XB)), dim3(XB), 0, st, head.p, hpos.p, hval.p, rep.p, NT,
-                           s->lo_off.p, s->lo16.p, s->lo_len.p, s->lo_kid.p, bad.p);
-        MR_TRY_HIP(ctx, hipGetLastError());
-        int64_t nk = 0;
-        int32_t hb = 0;
-        MR_TRY_HIP(ctx, hipMemcpyAsync(&nk, hpos.p + NT, sizeof nk, hipMemcpyDeviceToHost, st));
         MR_TRY(bad.download(ctx, &hb, 1));
         MR_TRY_HIP(ctx, hipStreamSynchronize(st));
-        if (hb == 0) {
-            s->lo_nk = (int32_t)nk;
-            s->lo_ok = true;
-            return MR_OK;
-        }
+        if (hb) return MR_OK;   // (codes or counts past 16 bits)
+        s->lo_nk = (int32_t)nk;
+        s->lo_ok = true;
+        return MR_OK;
     }
     return MR_OK;   // (four colliding seeds: the general window path)
 }
