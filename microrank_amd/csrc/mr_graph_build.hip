@@ -2145,8 +2145,8 @@ int mr_ix_launch2_batch(mr_ctx* ctx, int n, const mr_spans* const* sps, uint8_t*
 // (pagerank.py:54-66's class size = the histogram of the graph's class ids).  No trace-major
 // incidence, no per-graph sort by length, no kind hashing: the prepare reads each position's
 // codes from the layout-ordered u16 lists (near-contiguous for a tile) and relabels them.
-constexpr int LB_T = 1024, LB_I = 2, LB_TILE = LB_T * LB_I;   // k_lo_build_b: threads, traces per thread / block
-constexpr int64_t LB_LDS_WORDS = 34816;   // its two graphs' histograms (136 KB beside its static LDS)
+constexpr int LB_T = 512;                  // k_lo_build_b threads (a block: a layout range of mr_spans.lo_bstart)
+constexpr int64_t LB_LDS_WORDS = 30720;   // its two graphs' histograms and the service-op thresholds (120 KB)
 constexpr int32_t LB_A3MAX = 4096;        // service-op thresholds in LDS (8 B each)
 bool mr_lo_fits(const mr_spans* sp) {
     return sp->indexed && sp->ekey.p && sp->n_podops <= NS_PMAX && sp->n_edge_keys <= NS_EMAX &&
@@ -2155,15 +2155,17 @@ bool mr_lo_fits(const mr_spans* sp) {
 }
 // Per window, in its table's layout order: the detector (anormaly_detector.py:44-84 as
 // detect_block: a trace's expect summed sequentially over its service-ops in name order, T14),
-// the selection of both graphs (T1 swap: state 2 -> graph 0, 1 -> graph 1) with each selected
-// trace's position (its rank among the graph's traces in layout order: look-back scan) and kind
-// class count, and both graphs' per-pod-op span counts / first rows / coverage and per-edge-id
-// multiplicities (get_pagerank_graph's len_o, node order and children multisets,
-// preprocess_data.py:146-171) in LDS, written once per block as a partial row (the first row as
-// INT_MAX - row, combined by max) that k_lo_reduce_b sums per window.  One pass over everything a
-// trace holds; each wave keeps four rounds of entry loads in flight.
+// the selection of both graphs (T1 swap: state 2 -> graph 0, 1 -> graph 1: a side byte per layout
+// index, k_lo_pos_b's input) and each class's count, and both graphs' per-pod-op span counts /
+// first rows / coverage and per-edge-id multiplicities (get_pagerank_graph's len_o, node order
+// and children multisets, preprocess_data.py:146-171) in LDS, written once per block as a partial
+// row (the first row as INT_MAX - row, combined by max) that k_lo_reduce_b combines per window.
+// A block is a layout range of at most LO_BT_MAX traces and LO_BE entries (mr_spans.lo_bstart):
+// a thread per trace for the detector, then every wave of the block over the range's entries (a
+// lane per entry, coalesced, four rounds of loads in flight), each entry's trace found from the
+// traces' starts in LDS.  No block waits for another.
 struct IxWinLoB {
-    const int32_t *lo_tr, *lo_len, *lo_kid, *lo_first;
+    const int32_t *lo_tr, *lo_len, *lo_kid, *lo_first, *bstart;
     const int64_t *lo_off, *lsv_off, *le_off;
     const uint16_t *lo16, *lo_cnt;
     const uint32_t *lsv, *le;
@@ -2172,214 +2174,156 @@ struct IxWinLoB {
     const uint8_t* a3v;
     int64_t t0, t1;
     uint8_t* state;                  // by trace code (k_ix_cross2_b reads it)
+    int8_t* side;                    // by layout index: 0 / 1 graph, -1 none
     unsigned long long* counts;      // detector counter shards (3 * CSH, zeroed)
-    unsigned long long* st;          // look-back words: 2 chains x the window's tiles
     int32_t NT, NP, nek, nsvc;
-    int32_t* pinv[2];                // position -> layout index
     uint32_t* kcnt[2];               // kind class histograms (zeroed)
     int64_t* tot[2];                 // [T, nnz] (zeroed)
     uint32_t* rows;                  // partial rows [block][graph][cnt NP | cov NP | INT_MAX - first NP | edges nek]
 };
-__device__ __forceinline__ int64_t rfl64_(int64_t v) {   // a wave-uniform int64 (lane 0's) into SGPRs
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)v);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)((uint64_t)v >> 32));
-    return (int64_t)(((uint64_t)hi << 32) | lo);
-}
-// the trace k (0..63) of the wave's tile whose entries [a_k, b_k) hold entry e (a_k ascending,
-// lane k holding a_k): one division when the tile's traces all have n entries (the layout sorts
-// by entry count: the usual case), else a binary search over the lanes' starts.  Every lane must
-// run it (the shuffles read other lanes' registers).
-__device__ __forceinline__ int lo_trace_of(int64_t e, int64_t E0, int64_t n, int64_t a) {
-    if (n > 0) return (int)((uint32_t)(e - E0) / (uint32_t)n);
-    int lo = 0, hi = WAVE - 1;
+constexpr int LB_R = 4;   // entry rounds per batch (their loads in flight together)
+// the block-relative trace whose entries [st[t], st[t+1]) hold entry e (st ascending, st[0] = 0,
+// st[nt] = the range's entries): a division when the range's traces all have n entries (the layout
+// sorts by entry count: the usual case), else a binary search in LDS
+__device__ __forceinline__ int32_t lo_trace_of(uint32_t e, uint32_t n, const uint32_t* st, int32_t nt) {
+    if (n > 0) return (int32_t)(e / n);
+    int32_t lo = 0, hi = nt - 1;
     while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        const int64_t am = __shfl(a, mid, WAVE);
-        if (am <= e) lo = mid; else hi = mid - 1;
+        const int32_t mid = (lo + hi + 1) >> 1;
+        if (st[mid] <= e) lo = mid; else hi = mid - 1;
     }
     return lo;
 }
-constexpr int LB_R = 4;   // entry rounds per batch (their loads in flight together)
-__global__ void __launch_bounds__(LB_T, 8) k_lo_build_b(IxBatch<IxWinLoB> a, uint64_t epoch) {
+__global__ void __launch_bounds__(LB_T, 6) k_lo_build_b(IxBatch<IxWinLoB> a) {
     // per graph g: [cnt | cov << 32] u64 x NP, then INT_MAX - first row x NP, then edge counts x
     // nek; then the service-op thresholds (0 where a3v is false: adding +0.0 leaves expect as is)
     extern __shared__ __attribute__((aligned(16))) unsigned char lraw[];
-    __shared__ int8_t side[LB_TILE];
-    __shared__ int32_t sa[2][LB_T];
-    __shared__ int32_t ex[2];
-    __shared__ unsigned long long bc[3][LB_T / WAVE], bz[2][LB_T / WAVE];
+    __shared__ uint32_t pst[LO_BT_MAX + 1], est[LO_BT_MAX + 1];   // the traces' first entries (relative)
+    __shared__ int8_t ss[LO_BT_MAX];
+    __shared__ unsigned long long bc[5][LB_T / WAVE];
     const int k = ixb_pick(a.b0, a.n);
     const IxWinLoB& w = a.w[k];
-    const int32_t blk = (int32_t)blockIdx.x - a.b0[k], nblk = a.b0[k + 1] - a.b0[k];
+    const int32_t blk = (int32_t)blockIdx.x - a.b0[k];
     const int tid = threadIdx.x, lane = tid & (WAVE - 1), wv = tid / WAVE;
     const int32_t NP = w.NP, nek = w.nek;
     const size_t gbytes = ((size_t)NP * 12 + (size_t)nek * 4 + 15) / 16 * 16;   // one graph's histograms
     double* la3 = (double*)(lraw + 2 * gbytes);
     for (size_t x = (size_t)tid * 4; x < 2 * gbytes; x += (size_t)LB_T * 4) *(uint32_t*)(lraw + x) = 0u;
     for (int32_t c = tid; c < w.nsvc; c += LB_T) la3[c] = w.a3v[c] ? w.a3[c] : 0.0;
+    const int32_t T0 = w.bstart[blk], nt = w.bstart[blk + 1] - T0;
+    const int64_t P0 = w.lo_off[T0], Q0 = w.le_off[T0];
+    const uint32_t np = (uint32_t)(w.lo_off[T0 + nt] - P0), nq = (uint32_t)(w.le_off[T0 + nt] - Q0);
+    if (tid == 0) {
+        pst[nt] = np;
+        est[nt] = nq;
+    }
     __syncthreads();
-    const int64_t base = (int64_t)blk * LB_TILE;
-    int64_t nz0 = 0, nz1 = 0, rows = 0;
-    int nab = 0, nno = 0;
-    for (int j = 0; j < LB_I; ++j) {   // wave tile j * 16 + wv: 64 consecutive traces of the layout
-        const int64_t i = base + (int64_t)j * LB_T + tid;
-        const bool valid = i < w.NT;
-        int64_t pa = 0, pb = 0, ea = 0, eb = 0;
-        int s_ = -1, kid = -1;
+    unsigned long long nab = 0, nno = 0, rows = 0, nz0 = 0, nz1 = 0;
+    for (int32_t t0 = 0; t0 < nt; t0 += LB_T) {   // a thread per trace: 64 consecutive traces per wave
+        const int32_t t = t0 + tid;
+        const bool valid = t < nt;
+        const int64_t i = (int64_t)T0 + (valid ? t : nt - 1);   // (clamped)
+        const int32_t kid0 = w.lo_kid[i], len = w.lo_len[i], tr = w.lo_tr[i];
+        const long long ts = w.lo_ts[i], te = w.lo_te[i], mx = w.lo_mx[i];
+        const int64_t pa = w.lo_off[i], pb = w.lo_off[i + 1], ea = w.le_off[i];
+        const int64_t va = w.lsv_off[i], vb = w.lsv_off[i + 1];
+        const bool in = valid && len > 0 && ts >= w.t0 && te <= w.t1;
+        rows += in ? (unsigned long long)len : 0ull;
+        int stt = 0;
+        if (in && mx > 0) {   // grouped[grouped['duration'] > 0] (preprocess_data.py:117)
+            // expect: sequential in name order (T14), the entries' loads eight at a time
+            double expect = 0.0;
+            for (int64_t e = va; e < vb; e += 8) {
+                uint32_t v[8];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) v[q] = e + q < vb ? w.lsv[e + q] : 0u;
+#pragma unroll
+                for (int q = 0; q < 8; ++q)   // anormaly_detector.py:63-67
+                    if (e + q < vb) expect += (double)(v[q] >> 16) * la3[v[q] & 0xffffu];
+            }
+            stt = (double)mx / 1000.0 > expect ? 2 : 1;   // :58, :69
+        }
+        const int s_ = valid ? (stt == 2 ? 0 : stt == 1 ? 1 : -1) : -1;
         if (valid) {
-            kid = w.lo_kid[i];
-            const int32_t len = w.lo_len[i];
-            const long long ts = w.lo_ts[i], te = w.lo_te[i], mx = w.lo_mx[i];
-            pa = w.lo_off[i];
-            pb = w.lo_off[i + 1];
-            ea = w.le_off[i];
-            eb = w.le_off[i + 1];
-            const int64_t va = w.lsv_off[i], vb = w.lsv_off[i + 1];
-            const bool in = len > 0 && ts >= w.t0 && te <= w.t1;
-            rows += in ? len : 0;
-            int stt = 0;
-            if (in && mx > 0) {   // grouped[grouped['duration'] > 0] (preprocess_data.py:117)
-                // expect: sequential in name order (T14), the entries' loads eight at a time
-                double expect = 0.0;
-                for (int64_t e = va; e < vb; e += 8) {
-                    uint32_t v[8];
-#pragma unroll
-                    for (int q = 0; q < 8; ++q) v[q] = e + q < vb ? w.lsv[e + q] : 0u;
-#pragma unroll
-                    for (int q = 0; q < 8; ++q)   // anormaly_detector.py:63-67
-                        if (e + q < vb) expect += (double)(v[q] >> 16) * la3[v[q] & 0xffffu];
-                }
-                stt = (double)mx / 1000.0 > expect ? 2 : 1;   // :58, :69
-            }
-            w.state[w.lo_tr[i]] = (uint8_t)stt;
-            nab += stt == 2;
-            nno += stt == 1;
-            s_ = stt == 2 ? 0 : stt == 1 ? 1 : -1;
-            if (s_ == 0) nz0 += pb - pa;
-            else if (s_ == 1) nz1 += pb - pa;
+            w.state[tr] = (uint8_t)stt;
+            w.side[i] = (int8_t)s_;
+            ss[t] = (int8_t)s_;
+            pst[t] = (uint32_t)(pa - P0);
+            est[t] = (uint32_t)(ea - Q0);
         }
-        side[j * LB_T + tid] = (int8_t)s_;
-        {   // kind classes are runs of the layout: one add per (run, graph) of the wave
-            const int kp = __shfl_up(kid, 1, WAVE);
-            const bool hd = kid >= 0 && (lane == 0 || kp != kid);
-            const unsigned long long H = __ballot(hd), B0 = __ballot(s_ == 0), B1 = __ballot(s_ == 1);
-            if (hd) {
-                const unsigned long long above = lane == WAVE - 1 ? 0ull : H & (~0ull << (lane + 1));
-                const unsigned long long run = (above ? (above & (0ull - above)) - 1ull : ~0ull) & (~0ull << lane);
-                const uint32_t c0 = (uint32_t)__popcll(B0 & run), c1 = (uint32_t)__popcll(B1 & run);
-                if (c0) atomicAdd(&w.kcnt[0][kid], c0);
-                if (c1) atomicAdd(&w.kcnt[1][kid], c1);
-            }
+        nab += stt == 2;
+        nno += stt == 1;
+        if (s_ == 0) nz0 += (unsigned long long)(pb - pa);
+        else if (s_ == 1) nz1 += (unsigned long long)(pb - pa);
+        // kind classes are runs of the layout: one add per (run, graph) of the wave
+        const int kid = valid ? kid0 : -1;
+        const int kp = __shfl_up(kid, 1, WAVE);
+        const bool hd = kid >= 0 && (lane == 0 || kp != kid);
+        const unsigned long long H = __ballot(hd), B0 = __ballot(s_ == 0), B1 = __ballot(s_ == 1);
+        if (hd) {
+            const unsigned long long above = lane == WAVE - 1 ? 0ull : H & (~0ull << (lane + 1));
+            const unsigned long long run = (above ? (above & (0ull - above)) - 1ull : ~0ull) & (~0ull << lane);
+            const uint32_t c0 = (uint32_t)__popcll(B0 & run), c1 = (uint32_t)__popcll(B1 & run);
+            if (c0) atomicAdd(&w.kcnt[0][kid], c0);
+            if (c1) atomicAdd(&w.kcnt[1][kid], c1);
         }
-        // the tile's pod-op and join entries, a lane per entry (coalesced), each to its trace's graph
-        const unsigned long long vm = __ballot(valid);
-        if (vm == 0ull) continue;   // (uniform: past the window's traces)
-        if (__ballot(s_ >= 0) == 0ull) continue;   // (no selected trace in the tile)
-        const int last = 63 - __builtin_clzll(vm);   // (valid lanes are a prefix)
-        const int64_t P0 = rfl64_(pa), P1 = rfl64_(__shfl(pb, last, WAVE));
-        const int64_t Q0 = rfl64_(ea), Q1 = rfl64_(__shfl(eb, last, WAVE));
-        const int64_t npo = P1 - P0 == (int64_t)(last + 1) * (rfl64_(pb) - P0) && last == WAVE - 1 ? rfl64_(pb) - P0 : 0;
-        if (!valid) pa = pb = P1, ea = eb = Q1;
-        for (int64_t eb0 = P0; eb0 < P1; eb0 += LB_R * WAVE) {
-            int64_t e[LB_R];
-            uint16_t c[LB_R], cn[LB_R];
-            int32_t fr[LB_R];
+    }
+    __syncthreads();
+    // the range's pod-op and join entries: every wave, a lane per entry, each to its trace's graph
+    const uint32_t n0 = nt ? pst[1 < nt ? 1 : nt] - pst[0] : 0u;
+    const uint32_t npo = n0 > 0 && np == (uint32_t)nt * n0 ? n0 : 0u;   // (uniform: every trace n0 entries)
+    constexpr int NW = LB_T / WAVE;
+    const uint32_t nmax = max(np, nq);
+    for (uint32_t b0 = (uint32_t)wv * (LB_R * WAVE); b0 < nmax; b0 += NW * LB_R * WAVE) {
+        uint32_t pc[LB_R], ev[LB_R];
+        int32_t fr[LB_R];
 #pragma unroll
-            for (int r = 0; r < LB_R; ++r) {   // (clamped: every load in bounds)
-                e[r] = min(eb0 + r * WAVE + lane, P1 - 1);
-                c[r] = w.lo16[e[r]];
-                cn[r] = w.lo_cnt[e[r]];
-                fr[r] = w.lo_first[e[r]];
+        for (int r = 0; r < LB_R; ++r) {   // (clamped: every load in bounds)
+            const uint32_t o = b0 + (uint32_t)(r * WAVE + lane);
+            if (b0 < np) {
+                const int64_t e = P0 + (int64_t)min(o, np - 1u);
+                pc[r] = (uint32_t)w.lo16[e] | ((uint32_t)w.lo_cnt[e] << 16);
+                fr[r] = w.lo_first[e];
             }
+            if (b0 < nq) ev[r] = w.le[Q0 + (int64_t)min(o, nq - 1u)];
+        }
 #pragma unroll
-            for (int r = 0; r < LB_R; ++r) {
-                const int sk = __shfl(s_, lo_trace_of(e[r], P0, npo, pa), WAVE);   // (all lanes)
-                if (eb0 + r * WAVE + lane < P1 && sk >= 0) {
-                    unsigned char* G = lraw + (size_t)sk * gbytes;
-                    atomicAdd((unsigned long long*)G + c[r], (unsigned long long)cn[r] | (1ull << 32));
-                    atomicMax((int32_t*)(G + (size_t)NP * 8) + c[r], 0x7fffffff - fr[r]);
+        for (int r = 0; r < LB_R; ++r) {
+            const uint32_t o = b0 + (uint32_t)(r * WAVE + lane);
+            if (o < np) {
+                const int sd = ss[lo_trace_of(o, npo, pst, nt)];
+                if (sd >= 0) {
+                    unsigned char* G = lraw + (size_t)sd * gbytes;
+                    const uint32_t c = pc[r] & 0xffffu;
+                    atomicAdd((unsigned long long*)G + c, (unsigned long long)(pc[r] >> 16) | (1ull << 32));
+                    atomicMax((int32_t*)(G + (size_t)NP * 8) + c, 0x7fffffff - fr[r]);
                 }
             }
-        }
-        for (int64_t eb0 = Q0; eb0 < Q1; eb0 += LB_R * WAVE) {
-            int64_t e[LB_R];
-            uint32_t v[LB_R];
-#pragma unroll
-            for (int r = 0; r < LB_R; ++r) {
-                e[r] = min(eb0 + r * WAVE + lane, Q1 - 1);
-                v[r] = w.le[e[r]];
-            }
-#pragma unroll
-            for (int r = 0; r < LB_R; ++r) {
-                const int sk = __shfl(s_, lo_trace_of(e[r], Q0, 0, ea), WAVE);
-                if (eb0 + r * WAVE + lane < Q1 && sk >= 0)
-                    atomicAdd((uint32_t*)(lraw + (size_t)sk * gbytes + (size_t)NP * 12) + (v[r] & 0xffffu), v[r] >> 16);
+            if (o < nq) {
+                const int sd = ss[lo_trace_of(o, 0u, est, nt)];
+                if (sd >= 0)
+                    atomicAdd((uint32_t*)(lraw + (size_t)sd * gbytes + (size_t)NP * 12) + (ev[r] & 0xffffu), ev[r] >> 16);
             }
         }
     }
     {   // the detector's counts and both graphs' entry totals: per wave, per block, one add each
-        unsigned long long ab = (unsigned long long)nab, no = (unsigned long long)nno, rw = (unsigned long long)rows;
-        unsigned long long z0 = (unsigned long long)nz0, z1 = (unsigned long long)nz1;
+        unsigned long long v[5] = {nab, nno, rows, nz0, nz1};
 #pragma unroll
-        for (int m = 32; m >= 1; m >>= 1) {
-            ab += __shfl_xor(ab, m, WAVE);
-            no += __shfl_xor(no, m, WAVE);
-            rw += __shfl_xor(rw, m, WAVE);
-            z0 += __shfl_xor(z0, m, WAVE);
-            z1 += __shfl_xor(z1, m, WAVE);
-        }
-        if (lane == 0) {
-            bc[0][wv] = ab;
-            bc[1][wv] = no;
-            bc[2][wv] = rw;
-            bz[0][wv] = z0;
-            bz[1][wv] = z1;
-        }
+        for (int m = 32; m >= 1; m >>= 1)
+#pragma unroll
+            for (int q = 0; q < 5; ++q) v[q] += __shfl_xor(v[q], m, WAVE);
+        if (lane == 0)
+#pragma unroll
+            for (int q = 0; q < 5; ++q) bc[q][wv] = v[q];
     }
     __syncthreads();
     if (tid < 5) {
         unsigned long long v = 0;
-        for (int q = 0; q < LB_T / WAVE; ++q) v += tid < 3 ? bc[tid][q] : bz[tid - 3][q];
+        for (int q = 0; q < NW; ++q) v += bc[tid][q];
         if (v) {
             if (tid < 3) atomicAdd(&w.counts[(size_t)(blk % CSH) * 3 + tid], v);
             else atomicAdd((unsigned long long*)&w.tot[tid - 3][1], v);
         }
-    }
-    // positions: thread tid owns the tile's traces [tid LB_I, (tid + 1) LB_I) for the scan
-    int32_t c0 = 0, c1 = 0;
-#pragma unroll
-    for (int q = 0; q < LB_I; ++q) {
-        const int sd = side[tid * LB_I + q];
-        c0 += sd == 0;
-        c1 += sd == 1;
-    }
-    sa[0][tid] = c0;
-    sa[1][tid] = c1;
-    __syncthreads();
-    for (int o = 1; o < LB_T; o <<= 1) {
-        const int32_t v0 = tid >= o ? sa[0][tid - o] : 0, v1 = tid >= o ? sa[1][tid - o] : 0;
-        __syncthreads();
-        sa[0][tid] += v0;
-        sa[1][tid] += v1;
-        __syncthreads();
-    }
-    if (tid < 2 * WAVE) {   // wave g: graph g's positions
-        const int g = tid / WAVE;
-        const int32_t agg = sa[g][LB_T - 1];
-        const int64_t e = dl_lookback_wave(w.st + (size_t)g * nblk, blk, agg, epoch);
-        if (lane == 0) {
-            ex[g] = (int32_t)e;
-            if (blk == nblk - 1) w.tot[g][0] = e + agg;
-        }
-    }
-    __syncthreads();
-    int32_t r0 = ex[0] + sa[0][tid] - c0, r1 = ex[1] + sa[1][tid] - c1;
-#pragma unroll
-    for (int q = 0; q < LB_I; ++q) {
-        const int sd = side[tid * LB_I + q];
-        const int32_t ix = (int32_t)(base + tid * LB_I + q);
-        if (sd == 0) w.pinv[0][r0++] = ix;
-        else if (sd == 1) w.pinv[1][r1++] = ix;
     }
     // the block's histograms as its partial row (plain stores; k_lo_reduce_b combines the rows)
     const size_t rw = 3 * (size_t)NP + (size_t)nek;
@@ -2394,6 +2338,72 @@ __global__ void __launch_bounds__(LB_T, 8) k_lo_build_b(IxBatch<IxWinLoB> a, uin
             Rg[2 * NP + c] = ((const uint32_t*)(G + (size_t)NP * 8))[c];
         }
         for (int32_t x = tid; x < nek; x += LB_T) Rg[3 * NP + x] = ((const uint32_t*)(G + (size_t)NP * 12))[x];
+    }
+}
+// positions: each selected trace's rank among its graph's traces in layout order (decoupled
+// look-back over the side bytes), pinv[position] = layout index, staged in LDS for coalesced
+// stores; the graph sizes tot[g][0]
+constexpr int LP_T = 256, LP_I = 16, LP_TILE = LP_T * LP_I;
+struct IxWinLoPos {
+    const int8_t* side;
+    int32_t NT, pad_;
+    unsigned long long* st;          // look-back words: 2 chains x the window's tiles
+    int32_t* pinv[2];
+    int64_t* tot[2];
+};
+__global__ void __launch_bounds__(LP_T) k_lo_pos_b(IxBatch<IxWinLoPos> a, uint64_t epoch) {
+    __shared__ int32_t sa[2][LP_T];
+    __shared__ int32_t ex[2];
+    __shared__ int32_t so[2][LP_TILE];
+    const int k = ixb_pick(a.b0, a.n);
+    const IxWinLoPos& w = a.w[k];
+    const int32_t blk = (int32_t)blockIdx.x - a.b0[k], nblk = a.b0[k + 1] - a.b0[k];
+    const int tid = threadIdx.x, lane = tid & (WAVE - 1);
+    const int64_t base = (int64_t)blk * LP_TILE + (int64_t)tid * LP_I;
+    int8_t sd[LP_I];
+    if (base + LP_I <= w.NT) {   // 16 side bytes: one load
+        const uint4 v = *(const uint4*)(w.side + base);
+        memcpy(sd, &v, 16);
+    } else {
+#pragma unroll
+        for (int q = 0; q < LP_I; ++q) sd[q] = base + q < w.NT ? w.side[base + q] : (int8_t)-1;
+    }
+    int32_t c0 = 0, c1 = 0;
+#pragma unroll
+    for (int q = 0; q < LP_I; ++q) {
+        c0 += sd[q] == 0;
+        c1 += sd[q] == 1;
+    }
+    sa[0][tid] = c0;
+    sa[1][tid] = c1;
+    __syncthreads();
+    for (int o = 1; o < LP_T; o <<= 1) {
+        const int32_t v0 = tid >= o ? sa[0][tid - o] : 0, v1 = tid >= o ? sa[1][tid - o] : 0;
+        __syncthreads();
+        sa[0][tid] += v0;
+        sa[1][tid] += v1;
+        __syncthreads();
+    }
+    if (tid < 2 * WAVE) {   // wave g: graph g's positions
+        const int g = tid / WAVE;
+        const int32_t agg = sa[g][LP_T - 1];
+        const int64_t e = dl_lookback_wave(w.st + (size_t)g * nblk, blk, agg, epoch);
+        if (lane == 0) {
+            ex[g] = (int32_t)e;
+            if (blk == nblk - 1) w.tot[g][0] = e + agg;
+        }
+    }
+    int32_t r0 = sa[0][tid] - c0, r1 = sa[1][tid] - c1;   // (block-relative)
+#pragma unroll
+    for (int q = 0; q < LP_I; ++q) {
+        const int32_t ix = (int32_t)(base + q);
+        if (sd[q] == 0) so[0][r0++] = ix;
+        else if (sd[q] == 1) so[1][r1++] = ix;
+    }
+    __syncthreads();
+    for (int g = 0; g < 2; ++g) {
+        const int32_t n = sa[g][LP_T - 1], e = ex[g];
+        for (int32_t x = tid; x < n; x += LP_T) w.pinv[g][e + x] = so[g][x];
     }
 }
 // each window's partial rows, column by column: span counts, coverage and edge multiplicities
@@ -2452,12 +2462,13 @@ int mr_lo_launch_batch(mr_ctx* ctx, int n, const mr_spans* const* sps, mr_graph*
     hipStream_t st = ctx->stream;
     IxBatch<IxWinLoB> ab{};
     IxBatch<IxLoRed> ar{};
+    IxBatch<IxWinLoPos> ap{};
     IxBatch<IxWinCross> ac{};
     IxBatch<IxWinNodes> an{};
-    ab.n = ar.n = ac.n = an.n = n;
-    int32_t bb = 0, bc = 0, br = 0;
-    int64_t rwords = 0;
-    std::vector<int64_t> roff((size_t)n);
+    ab.n = ar.n = ap.n = ac.n = an.n = n;
+    int32_t bb = 0, bc = 0, br = 0, bp = 0;
+    int64_t rwords = 0, sbytes = 0;
+    std::vector<int64_t> roff((size_t)n), soff((size_t)n);
     size_t lds = 4;
     int64_t words = 0;
     std::vector<int64_t> woff((size_t)n);
@@ -2498,7 +2509,8 @@ int mr_lo_launch_batch(mr_ctx* ctx, int n, const mr_spans* const* sps, mr_graph*
             int64_t* out = d_outs[k] + 8 * j;
             na.g[j] = NsArgs{gc, ocnt, ofinv, ocov, B.node_of_code.p, G->node_podop.p, G->len_o.p, G->nchild.p, G->cov.p,
                              G->ss_par.p, G->ss_off.p, out + 5, out + 6, nullptr, out, G->u_o.p, G->pw.p, 1};
-            L.pinv[j] = B.pinv.p;
+            ap.w[k].pinv[j] = B.pinv.p;
+            ap.w[k].tot[j] = out + 5;
             L.kcnt[j] = B.kcnt;
             L.tot[j] = out + 5;
             IxLoRed& R = ar.w[k];
@@ -2507,7 +2519,7 @@ int mr_lo_launch_batch(mr_ctx* ctx, int n, const mr_spans* const* sps, mr_graph*
             R.ocov[j] = ocov;
             R.gc[j] = gc;
         }
-        const int32_t nt = (int32_t)std::max<int64_t>(cdiv((int64_t)NT, LB_TILE), 1);
+        const int32_t nt = sp->lo_nblk;
         const int64_t rw = 3 * (int64_t)NP + nek;
         roff[(size_t)k] = rwords;
         rwords += (int64_t)nt * 2 * rw;
@@ -2516,11 +2528,18 @@ int mr_lo_launch_batch(mr_ctx* ctx, int n, const mr_spans* const* sps, mr_graph*
         ar.w[k].nek = (int32_t)nek;
         ar.b0[k] = br;
         br += (int32_t)cdiv(2 * rw, 256);
+        const int32_t npb = (int32_t)std::max<int64_t>(cdiv((int64_t)NT, LP_TILE), 1);
         woff[(size_t)k] = words;
-        words += 2 * (int64_t)nt;
+        words += 2 * (int64_t)npb;
+        ap.b0[k] = bp;
+        bp += npb;
+        ap.w[k].NT = NT;
+        soff[(size_t)k] = sbytes;
+        sbytes += ((int64_t)NT + 15) / 16 * 16;
         ab.b0[k] = bb;
         bb += nt;
         const DetIn& d = dets[k];
+        L.bstart = sp->lo_bstart.p;
         L.lo_tr = sp->lo_tr.p;
         L.lo_len = sp->lo_len.p;
         L.lo_kid = sp->lo_kid.p;
@@ -2555,6 +2574,7 @@ int mr_lo_launch_batch(mr_ctx* ctx, int n, const mr_spans* const* sps, mr_graph*
     for (int k = n; k <= IXW; ++k) {   // (offsets past the last window: its end)
         ab.b0[k] = bb;
         ar.b0[k] = br;
+        ap.b0[k] = bp;
         ac.b0[k] = bc;
         an.b0[k] = 2 * n;
     }
@@ -2562,13 +2582,18 @@ int mr_lo_launch_batch(mr_ctx* ctx, int n, const mr_spans* const* sps, mr_graph*
     uint64_t epoch = 0;
     MR_TRY(mr_dl_status(ctx, words, &dst, &epoch));
     DBuf<uint32_t> rows;   // (stream-ordered: freed back to this context's pool after the launches)
+    DBuf<int8_t> side;
     MR_TRY(rows.alloc(ctx, (size_t)std::max<int64_t>(rwords, 1)));
+    MR_TRY(side.alloc(ctx, (size_t)std::max<int64_t>(sbytes, 16)));
     for (int k = 0; k < n; ++k) {
-        ab.w[k].st = dst + woff[(size_t)k];
         ab.w[k].rows = rows.p + roff[(size_t)k];
         ar.w[k].rows = rows.p + roff[(size_t)k];
+        ab.w[k].side = side.p + soff[(size_t)k];
+        ap.w[k].side = side.p + soff[(size_t)k];
+        ap.w[k].st = dst + woff[(size_t)k];
     }
-    hipLaunchKernelGGL(k_lo_build_b, dim3(bb), dim3(LB_T), lds, st, ab, epoch);
+    hipLaunchKernelGGL(k_lo_build_b, dim3(bb), dim3(LB_T), lds, st, ab);
+    hipLaunchKernelGGL(k_lo_pos_b, dim3(bp), dim3(LP_T), 0, st, ap, epoch);
     hipLaunchKernelGGL(k_lo_reduce_b, dim3(br), dim3(256), 0, st, ar);
     if (bc) hipLaunchKernelGGL(k_ix_cross2_b, dim3(bc), dim3(256), 0, st, ac);
     hipLaunchKernelGGL(k_nodes_small2_b, dim3(2 * n), dim3(NS_T), 0, st, an);

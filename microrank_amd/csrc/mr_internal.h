@@ -377,6 +377,8 @@ struct mr_spans {
     DBuf<uint16_t> lo16, lo_cnt;         // [n_po] pod-op codes (ascending) and span counts, layout order
     DBuf<int32_t> lo_first;              // [n_po] first row of each pod-op entry
     DBuf<long long> lo_ts, lo_te, lo_mx; // [NT] trace-level start / end, max duration
+    DBuf<int32_t> lo_bstart;             // [lo_nblk+1] window-build blocks: layout ranges (LO_BT_MAX / LO_BE)
+    int32_t lo_nblk = 0;
     DBuf<int64_t> lsv_off, le_off;       // [NT+1] service-op entries / join entries of each trace
     DBuf<uint32_t> lsv, le;              // svcop | count << 16 (code order); dense edge id | count << 16
     // tables ingested from strings (mr_spans_ingest): the first row of each trace / pod-op /
@@ -521,6 +523,10 @@ int mr_ix_finish(mr_ctx* ctx, const mr_spans* sp, mr_graph* g, IxBuild& b, const
 // zw[k] mr_lo_zero_words(sps[k]) zeroed words.  MR_ERR_STATE: a window outside the limits (the
 // caller takes mr_ix_launch2_batch)
 bool mr_lo_fits(const mr_spans* sp);
+// a window-build block (k_lo_build_b) holds at most LO_BT_MAX traces and, past its first trace, at
+// most LO_BE pod-op entries: the layout's long traces spread over many blocks
+constexpr int32_t LO_BT_MAX = 1024;
+constexpr int64_t LO_BE = 12288;
 int64_t mr_lo_zero_words(const mr_spans* sp);
 int mr_lo_launch_batch(mr_ctx* ctx, int n, const mr_spans* const* sps, mr_graph* const* g0s, mr_graph* const* g1s,
                        IxBuild* const* b0s, IxBuild* const* b1s, int64_t* const* d_outs, const DetIn* dets,

@@ -530,6 +530,21 @@ static int lo_index(mr_ctx* ctx, mr_spans* s) {
         MR_TRY(bad.download(ctx, &hb, 1));
         MR_TRY_HIP(ctx, hipStreamSynchronize(st));
         if (hb) return MR_OK;   // (codes or counts past 16 bits)
+        {   // the window-build blocks: greedy cut of the layout by trace count and entries
+            std::vector<int64_t> off((size_t)NT + 1);
+            MR_TRY(s->lo_off.download(ctx, off.data(), (size_t)NT + 1));
+            MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+            std::vector<int32_t> bs;
+            bs.push_back(0);
+            for (int32_t i = 0; i < NT; ++i) {
+                const int32_t b0 = bs.back();
+                if (i > b0 && (i - b0 >= LO_BT_MAX || off[(size_t)i + 1] - off[(size_t)b0] > LO_BE)) bs.push_back(i);
+            }
+            bs.push_back(NT);
+            MR_TRY(s->lo_bstart.upload(ctx, bs.data(), bs.size()));
+            MR_TRY_HIP(ctx, hipStreamSynchronize(st));
+            s->lo_nblk = (int32_t)bs.size() - 1;
+        }
         s->lo_nk = (int32_t)nk;
         s->lo_ok = true;
         return MR_OK;

@@ -55,3 +55,15 @@ if has pmcenv; then
     echo "== [$e]"; python3 scripts/pmc_summary.py gpurun_out/pmce_${TAG}_$i k_tr_a | tee gpurun_out/pmce_${TAG}_$i.txt
   done
 fi
+# pmck: counter passes (PASSES: ';'-separated counter lists) over the kernels matching KRE in a
+# short c2 bench, one rocprofv3 run per pass
+if has pmck; then
+  IFS=';' read -ra PS <<< "${PASSES:-SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS}"
+  i=0
+  for pc in "${PS[@]}"; do
+    i=$((i+1))
+    timeout -s KILL 240 rocprofv3 --pmc $pc --kernel-include-regex "$KRE" -d gpurun_out/pmck_${TAG}_$i -o run --output-format csv -- \
+        python3 bench.py --no-traffic --no-cpu --no-side --c2-distinct 64 --steps 1 --warmup 0 > gpurun_out/pmck_${TAG}_$i.log 2>&1 || { echo "pmc pass $i failed"; tail -5 gpurun_out/pmck_${TAG}_$i.log; exit 1; }
+    echo "== pass $i"; python3 scripts/pmc_summary.py gpurun_out/pmck_${TAG}_$i "$KRE" | tee gpurun_out/pmck_${TAG}_$i.txt
+  done
+fi
