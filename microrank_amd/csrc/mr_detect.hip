@@ -744,6 +744,10 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
     const int64_t tper = std::max<int64_t>(1, tsum_tab / n_windows);
     int group_size = 16;
     while (group_size < 128 && (int64_t)group_size * 2 * tper <= WIN_GROUP_TRACES) group_size *= 2;
+    // at least two groups per call: the next group's builds overlap this one's PageRanks (round 5,
+    // C2 calls of 128 windows: group 128 / 64 -> 652-674 / 748-807 GTEPS; calls of 256: group 128
+    // and 64 within the spread, 981-1002 / 904-1000 GTEPS, `profiles/r05/r05f_groups_ab.txt`)
+    while (group_size > 16 && 2 * group_size > n_windows) group_size /= 2;
     if (const char* e = getenv("MR_WIN_GROUP")) group_size = std::max(1, atoi(e));
     const char* ce = getenv("MR_WIN_CHUNK");   // windows built together on one stream
     const int chunk_size = ce ? std::max(1, atoi(ce)) : group_size >= 64 && tper <= 65536 ? 8 : 4;
