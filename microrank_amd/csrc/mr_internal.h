@@ -318,6 +318,9 @@ struct mr_graph {
     // position (kind, lo_lenp) and the preference partials (ppart) stay for a re-set-up
     bool lo = false;
     DBuf<int32_t> lo_lenp;       // [T] span count by position
+    // [T] by position: the length of the run of identical traces (one kind class, adjacent in a
+    // wave tile) a position heads, 0 for the run's other positions (k_tr_a's walk merges the run)
+    DBuf<uint8_t> trun;
     int32_t lo_nbp = 0;          // preference partial blocks
 };
 

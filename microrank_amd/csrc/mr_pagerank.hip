@@ -1532,6 +1532,7 @@ struct LDev {
     float *w_tp, *c_tp;
     double* kind;
     int32_t* lenp;
+    uint8_t* trun;
     double *ppart, *scal;
     int32_t* flag;
     unsigned long long* mslot;
@@ -1568,14 +1569,27 @@ __global__ void __launch_bounds__(256) k_lo_fill_b(const LDev* __restrict__ ld, 
     for (int32_t c = threadIdx.x; c < G.NP; c += 256) lnoc[c] = (uint16_t)G.noc[c];
     __syncthreads();
     double a = 0.0, b = 0.0;
-    if (i < (int64_t)G.W * WAVE) {
+    if (i < (int64_t)G.W * WAVE) {   // (uniform per wave: a wave is one tile)
         const int32_t k = (int32_t)(i / WAVE), lane = (int32_t)(i % WAVE);
         int64_t e0 = 0, len = 0, rot = 0;
+        // runs of identical traces: adjacent positions of one kind class (the layout keeps a class
+        // contiguous); a run shares its head's rotation, so its members walk the same ids in the same
+        // order and k_tr_a lets the head walk for the run
+        const int32_t ix = i < T ? G.pinv[i] : -1;
+        const int32_t kid = i < T ? G.lo_kid[ix] : -1;
+        const int32_t kp = __shfl_up(kid, 1, WAVE);
+        const bool hd = lane == 0 || kid < 0 || kid != kp;
+        const unsigned long long hm = __ballot(hd);
+        const unsigned long long below = hm & (lane == WAVE - 1 ? ~0ull : (2ull << lane) - 1ull);
+        const int32_t ixh = __shfl(ix, 63 - __builtin_clzll(below), WAVE);
+        if (i < T && G.trun) {
+            const unsigned long long above = lane == WAVE - 1 ? 0ull : hm & (~0ull << (lane + 1));
+            G.trun[i] = hd ? (uint8_t)((above ? __builtin_ctzll(above) : WAVE) - lane) : (uint8_t)0;
+        }
         if (i < T) {
-            const int32_t ix = G.pinv[i];
             e0 = G.lo_off[ix];
             len = G.lo_off[ix + 1] - e0;
-            rot = len && G.rot ? (int64_t)((uint32_t)ix % (uint32_t)len) : 0;
+            rot = len && G.rot ? (int64_t)((uint32_t)ixh % (uint32_t)len) : 0;
             const int32_t L = G.lo_len[ix];
             const uint32_t kc = G.kcnt[G.lo_kid[ix]];
             G.w_tp[i] = L > 0 ? (float)(1.0 / (double)L) : 0.0f;
@@ -1717,6 +1731,7 @@ struct GDev {
     const float* w_tp;
     const double* mw_tp;        // kind-compressed graphs: w_t * multiplicity (position order), else null
     const uint8_t* hmask;       // register-accumulated hot ops: trace bits in position order (nhr > 0)
+    const uint8_t* trun;        // layout-order graphs: run lengths of identical traces by position (or null)
     const uint32_t* ctids;      // wide graphs: cold chunks of the short-tile walk ([chunk][lane] x 2 labels)
     const int32_t* ccoff;       // [n_wt+1] first cold chunk of a tile
     int32_t nhr;
@@ -2072,6 +2087,7 @@ struct TrTile {
     int32_t ccw;   // EXT & 2: lane j: ccoff[k + 1 + j] (the next tile's cold chunk range)
     int32_t cw;    // lane j: coff[k + 1 + j] (readlane 0 / 1: the next tile's chunk range)
     uint32_t hm;   // the trace's hot-op bits (nhr > 0)
+    uint32_t rl;   // the run of identical traces this lane heads (0: another lane's run; 1: its own)
 };
 // the hot ops of a trace: their su first in the lane's sum (the same order in both walks), X into
 // the lane's register accumulators (integers: order-free; flushed once per walk)
@@ -2129,6 +2145,7 @@ __device__ __forceinline__ int32_t tr_walk_short(const GDev& G, int32_t k, const
     const uint32_t cpad = (uint32_t)(G.N + lane);
     const bool hot = H.n > 0;
     const GLB uint8_t* hmk = hot ? gp(G.hmask) : (const GLB uint8_t*)coff;
+    const GLB uint8_t* trn = gp(G.trun);
     const int32_t cl = __builtin_amdgcn_readfirstlane(coff[ke]) - 1;   // the run's last chunk
     // the first tile's chunk ranges: handed over by the previous tier (n >= 0), else loaded
     if (n < 0) {
@@ -2162,7 +2179,8 @@ __device__ __forceinline__ int32_t tr_walk_short(const GDev& G, int32_t k, const
             r.ccw = ccoff[min(kq + 1 + lane, ke)];
         }
         r.cw = coff[min(kq + 1 + lane, ke)];
-        r.hm = hmk[hot ? p : 0];
+        r.hm = hot ? hmk[p] : 0u;   // (uniform)
+        r.rl = trn ? (uint32_t)trn[p] : 1u;
     };
     // tile kk from r: lane = position kk * 64 + lane
     auto run = [&](const R& r, int32_t kk, int32_t qq0, int32_t nqq) {
@@ -2176,26 +2194,32 @@ __device__ __forceinline__ int32_t tr_walk_short(const GDev& G, int32_t k, const
                 cg[2] = sug[nqq > 1 ? r.cid[1].x : cpad];
                 cg[3] = sug[nqq > 1 ? r.cid[1].y : cpad];
             }
-        const unsigned long long X = own ? (unsigned long long)__double2ull_rn((double)r.q * xsc) : 0ull;
+        // a run of rl identical traces (the same ops in the same order, the same q, c and w: the
+        // same sum and r') is walked by its head alone: its X times rl into the accumulators (integers:
+        // exactly the rl separate adds), its r' broadcast to the run below
+        const bool hd = r.rl != 0u;
+        const unsigned long long X = own ? (unsigned long long)__double2ull_rn((double)r.q * xsc) * (unsigned long long)r.rl : 0ull;
         double acc = H.n ? tr_hot_init(H, r.hm, X) : 0.0;
-        double sv[2][4];
-        auto rd = [&](const u32x2 w, double* s) {
-            s[0] = su_l[w.x & 0xffffu];
-            s[1] = su_l[w.x >> 16];
-            s[2] = su_l[w.y & 0xffffu];
-            s[3] = su_l[w.y >> 16];
-        };
-        rd(r.id[0], sv[0]);
+        if (hd) {
+            double sv[2][4];
+            auto rd = [&](const u32x2 w, double* s) {
+                s[0] = su_l[w.x & 0xffffu];
+                s[1] = su_l[w.x >> 16];
+                s[2] = su_l[w.y & 0xffffu];
+                s[3] = su_l[w.y >> 16];
+            };
+            rd(r.id[0], sv[0]);
 #pragma unroll
-        for (int j = 0; j < NC; ++j) {
-            if (j + 1 < NC) rd(r.id[j + 1], sv[(j + 1) & 1]);
-            const u32x2 w = r.id[j];
-            atomicAdd(&lacc[(w.x & 0xffffu)], X);
-            atomicAdd(&lacc[(w.x >> 16)], X);
-            atomicAdd(&lacc[(w.y & 0xffffu)], X);
-            atomicAdd(&lacc[(w.y >> 16)], X);
+            for (int j = 0; j < NC; ++j) {
+                if (j + 1 < NC) rd(r.id[j + 1], sv[(j + 1) & 1]);
+                const u32x2 w = r.id[j];
+                atomicAdd(&lacc[(w.x & 0xffffu)], X);
+                atomicAdd(&lacc[(w.x >> 16)], X);
+                atomicAdd(&lacc[(w.y & 0xffffu)], X);
+                atomicAdd(&lacc[(w.y >> 16)], X);
 #pragma unroll
-            for (int i = 0; i < 4; ++i) acc += sv[j & 1][i];
+                for (int i = 0; i < 4; ++i) acc += sv[j & 1][i];
+            }
         }
         double x = 0.0;   // the cold half, sequential in the trace's cold order (k_cold_trace's)
         if constexpr ((EXT & 2) != 0)
@@ -2204,7 +2228,11 @@ __device__ __forceinline__ int32_t tr_walk_short(const GDev& G, int32_t k, const
                 for (int i = 0; i < 4; ++i) x += cg[i];
                 if (nqq > 2) x = r.xo;   // (rare: > 4 cold entries in a trace of the tile: k_cold_trace's sum)
             }
-        const double rp = d * ((acc + x) / Ms) + (double)r.c;   // pagerank.py:125
+        double rp = d * ((acc + x) / Ms) + (double)r.c;   // pagerank.py:125
+        if (trn) {   // (uniform) the run's head's r'
+            const unsigned long long hb = __ballot(hd) & (lane == WAVE - 1 ? ~0ull : (2ull << lane) - 1ull);
+            rp = __shfl(rp, 63 - __builtin_clzll(hb), WAVE);
+        }
         if (own) rmax = nmax(rmax, rp);
         const double wq = kc ? r.mw : (double)r.w;
         qn[own ? p : T] = (Q)(wq * rp);   // q[T]: pad slot
@@ -4332,6 +4360,8 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
     // vs 44.6 us per iteration, C4 whole: within noise (two repeats each)
     const char* rwe = getenv("MR_TR_ROW_WT");
     const bool row_wt_on = !(rwe && atoi(rwe) == 0);
+    const char* mge = getenv("MR_TR_MERGE");   // (A/B and tests, read per call) 0: every lane walks its own trace
+    const bool merge_on = !(mge && atoi(mge) == 0);
     double bytes = 0.0;
     for (int i = 0; i < ng; ++i) {
         mr_graph* g = gs[i];
@@ -4349,6 +4379,7 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         v.w_tp = g->w_tp.p;
         v.mw_tp = g->mw_tp.p;
         v.hmask = g->nhr ? g->hmask.p : nullptr;
+        v.trun = g->lo && merge_on ? g->trun.p : nullptr;
         v.ctids = g->wide ? g->ctids.p : nullptr;
         v.ccoff = g->wide ? g->ccoff.p : nullptr;
         v.nhr = g->fused ? g->nhr : 0;
@@ -4772,8 +4803,9 @@ int mr_lo_prepare_batch(mr_ctx* ctx, mr_graph* const* gs, const mr_spans* const*
     if (n <= 0) return MR_OK;
     const bool fp32 = precision == MR_FP32;
     hipStream_t st = ctx->stream;
-    // a trace's ids rotated by its layout index mod length (spreads a shared first op over a tile's
-    // id chunks) or kept in the layout's order (MR_LO_ROT=0; read per call)
+    // a trace's ids rotated by its run head's layout index mod length (spreads a shared first op
+    // over a tile's id chunks; a run of identical traces keeps one order, k_lo_fill_b) or kept in the
+    // layout's order (MR_LO_ROT=0; read per call)
     const char* re = getenv("MR_LO_ROT");
     const int lo_rot = re ? (atoi(re) != 0) : LO_ROT_DEFAULT;
     keep.assign((size_t)n * sizeof(LDev), 0);
@@ -4813,6 +4845,7 @@ int mr_lo_prepare_batch(mr_ctx* ctx, mr_graph* const* gs, const mr_spans* const*
         MR_TRY(g->w_tp.alloc(ctx, (size_t)T));
         MR_TRY(g->kind.alloc(ctx, (size_t)T));
         MR_TRY(g->lo_lenp.alloc(ctx, (size_t)T));
+        MR_TRY(g->trun.alloc(ctx, (size_t)T));
         MR_TRY(g->ppart.alloc(ctx, 2 * (size_t)g->lo_nbp));
         MR_TRY(g->coff.alloc(ctx, (size_t)W + 1));
         MR_TRY(c64[(size_t)i].alloc(ctx, (size_t)W + 1));
@@ -4842,6 +4875,7 @@ int mr_lo_prepare_batch(mr_ctx* ctx, mr_graph* const* gs, const mr_spans* const*
         v.c64 = c64[(size_t)i].p;
         v.coff = g->coff.p;
         v.tids = g->tids.p;
+        v.trun = g->trun.p;
         lo_mark_presetup(g, anomaly[i], d, fp32);
     }
     DBuf<LDev> dl;

@@ -879,13 +879,16 @@ def test_c2_windows_batch_groupings_agree(c2_batch, monkeypatch):
     table) rank bitwise as the default -- build-side choices, the PageRank launches untouched; and
     PageRank groups of 4 and 2 windows (MR_WIN_GROUP) give the same top lists, counts and edges,
     scores within 1e-12 (a group's block budget sets each graph's fixed-point scale, so only the
-    rounding of the exact limb sums may move)."""
+    rounding of the exact limb sums may move).  k_tr_a without run merging (MR_TR_MERGE=0: every
+    lane walks its own trace instead of a run's head walking for its identical traces with X times
+    the run length) ranks bitwise as the default: the merge is exact."""
     from microrank_amd.online_rca import rank_windows
 
-    knobs = ("MR_WIN_GROUP", "MR_WIN_CHUNK", "MR_IX_EPT", "MR_DET_FUSE_MAX", "MR_NO_DET_FUSE")
+    knobs = ("MR_WIN_GROUP", "MR_WIN_CHUNK", "MR_IX_EPT", "MR_DET_FUSE_MAX", "MR_NO_DET_FUSE", "MR_TR_MERGE")
     ctx, _, wins = c2_batch
     variants = {"default": {}, "chunk1_ept16": {"MR_WIN_CHUNK": "1", "MR_IX_EPT": "16"},
                 "chunk2_fused": {"MR_WIN_CHUNK": "2", "MR_DET_FUSE_MAX": "100000000"},
+                "nomerge": {"MR_TR_MERGE": "0"},
                 "group4_chunk4": {"MR_WIN_GROUP": "4", "MR_WIN_CHUNK": "4"}, "group2": {"MR_WIN_GROUP": "2"}}
     runs = {}
     for name, env in variants.items():
