@@ -534,15 +534,25 @@ def isolated_group_roofline(ctx, group, prec, reps=3):
 
     lib = _lib.load()
     pr = "fp32" if prec == _lib.MR_FP32 else "fp64"
-    rank_windows(ctx, [w[:5] for w in group], precision=pr)
-    ctx.sync()
-    lib.mr_ctx_profile(ctx.h, 1)
-    for _ in range(reps):
+    # one group of the whole call (the library otherwise keeps groups to half a call, so that a
+    # call's builds overlap its PageRanks); MR_WIN_GROUP is read per call
+    old = os.environ.get("MR_WIN_GROUP")
+    os.environ["MR_WIN_GROUP"] = str(len(group))
+    try:
         rank_windows(ctx, [w[:5] for w in group], precision=pr)
-    ctx.sync()
-    launches, kms, kbytes = C.c_int64(), C.c_double(), C.c_double()
-    lib.mr_ctx_prof_read(ctx.h, C.byref(launches), C.byref(kms), C.byref(kbytes))
-    lib.mr_ctx_profile(ctx.h, 0)
+        ctx.sync()
+        lib.mr_ctx_profile(ctx.h, 1)
+        for _ in range(reps):
+            rank_windows(ctx, [w[:5] for w in group], precision=pr)
+        ctx.sync()
+        launches, kms, kbytes = C.c_int64(), C.c_double(), C.c_double()
+        lib.mr_ctx_prof_read(ctx.h, C.byref(launches), C.byref(kms), C.byref(kbytes))
+        lib.mr_ctx_profile(ctx.h, 0)
+    finally:
+        if old is None:
+            os.environ.pop("MR_WIN_GROUP", None)
+        else:
+            os.environ["MR_WIN_GROUP"] = old
     avg_ms = kms.value / max(launches.value, 1)
     achieved = (kbytes.value / max(launches.value, 1)) / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     return {"achieved": round(achieved, 1), "frac": round(achieved / HBM_PEAK_GBS, 4),
