@@ -2181,16 +2181,24 @@ struct IxWinLoB {
     int64_t* tot[2];                 // [T, nnz] (zeroed)
     uint32_t* rows;                  // partial rows [block][graph][cnt NP | cov NP | INT_MAX - first NP | edges nek]
 };
+// the build's first LDS region: both graphs' histograms, and before them (aliased) the detector's
+// products of a round -- at least 2048 of them
+__host__ __device__ __forceinline__ size_t lo_region0(size_t gbytes) {
+    return 2 * gbytes > (size_t)2048 * 8 ? 2 * gbytes : (size_t)2048 * 8;
+}
 constexpr int LB_R = 4;   // entry rounds per batch (their loads in flight together)
 // the block-relative trace whose entries [st[t], st[t+1]) hold entry e (st ascending, st[0] = 0,
 // st[nt] = the range's entries): a division when the range's traces all have n entries (the layout
 // sorts by entry count: the usual case), else a binary search in LDS
 __device__ __forceinline__ int32_t lo_trace_of(uint32_t e, uint32_t n, const uint32_t* st, int32_t nt) {
     if (n > 0) return (int32_t)(e / n);
-    int32_t lo = 0, hi = nt - 1;
-    while (lo < hi) {
-        const int32_t mid = (lo + hi + 1) >> 1;
-        if (st[mid] <= e) lo = mid; else hi = mid - 1;
+    // a fixed number of steps (LO_BT_MAX = 1024 traces): the searches of a batch's rounds are
+    // independent chains the compiler can interleave (a data-dependent loop would run them one by one)
+    int32_t lo = 0;
+#pragma unroll
+    for (int32_t step = LO_BT_MAX / 2; step >= 1; step >>= 1) {
+        const int32_t mid = lo + step;
+        lo = mid < nt && st[mid] <= e ? mid : lo;
     }
     return lo;
 }
@@ -2207,42 +2215,88 @@ __global__ void __launch_bounds__(LB_T, 6) k_lo_build_b(IxBatch<IxWinLoB> a) {
     const int tid = threadIdx.x, lane = tid & (WAVE - 1), wv = tid / WAVE;
     const int32_t NP = w.NP, nek = w.nek;
     const size_t gbytes = ((size_t)NP * 12 + (size_t)nek * 4 + 15) / 16 * 16;   // one graph's histograms
-    double* la3 = (double*)(lraw + 2 * gbytes);
-    for (size_t x = (size_t)tid * 4; x < 2 * gbytes; x += (size_t)LB_T * 4) *(uint32_t*)(lraw + x) = 0u;
+    const size_t reg0 = lo_region0(gbytes);   // the histograms; before them, the detector's products
+    double* la3 = (double*)(lraw + reg0);
+    double* prod = (double*)lraw;
+    const uint32_t cap = (uint32_t)(reg0 / 8 / LB_T * LB_T);   // products per round
     for (int32_t c = tid; c < w.nsvc; c += LB_T) la3[c] = w.a3v[c] ? w.a3[c] : 0.0;
     const int32_t T0 = w.bstart[blk], nt = w.bstart[blk + 1] - T0;
-    const int64_t P0 = w.lo_off[T0], Q0 = w.le_off[T0];
+    const int64_t P0 = w.lo_off[T0], Q0 = w.le_off[T0], V0 = w.lsv_off[T0];
     const uint32_t np = (uint32_t)(w.lo_off[T0 + nt] - P0), nq = (uint32_t)(w.le_off[T0 + nt] - Q0);
+    const uint32_t nv = (uint32_t)(w.lsv_off[T0 + nt] - V0);
     if (tid == 0) {
         pst[nt] = np;
         est[nt] = nq;
     }
-    __syncthreads();
-    unsigned long long nab = 0, nno = 0, rows = 0, nz0 = 0, nz1 = 0;
-    for (int32_t t0 = 0; t0 < nt; t0 += LB_T) {   // a thread per trace: 64 consecutive traces per wave
-        const int32_t t = t0 + tid;
+    // this thread's traces: slot s holds trace s * LB_T + tid of the range (64 consecutive per wave)
+    constexpr int NS = LO_BT_MAX / LB_T;
+    uint32_t va[NS], vb[NS];
+    bool act[NS];
+    double expect[NS];
+    long long mx[NS];
+    unsigned long long rows = 0;
+#pragma unroll
+    for (int q = 0; q < NS; ++q) {
+        const int32_t t = q * LB_T + tid;
         const bool valid = t < nt;
         const int64_t i = (int64_t)T0 + (valid ? t : nt - 1);   // (clamped)
-        const int32_t kid0 = w.lo_kid[i], len = w.lo_len[i], tr = w.lo_tr[i];
-        const long long ts = w.lo_ts[i], te = w.lo_te[i], mx = w.lo_mx[i];
-        const int64_t pa = w.lo_off[i], pb = w.lo_off[i + 1], ea = w.le_off[i];
-        const int64_t va = w.lsv_off[i], vb = w.lsv_off[i + 1];
+        const int32_t len = w.lo_len[i];
+        const long long ts = w.lo_ts[i], te = w.lo_te[i];
+        mx[q] = w.lo_mx[i];
+        va[q] = (uint32_t)(w.lsv_off[i] - V0);
+        vb[q] = (uint32_t)(w.lsv_off[i + 1] - V0);
         const bool in = valid && len > 0 && ts >= w.t0 && te <= w.t1;
         rows += in ? (unsigned long long)len : 0ull;
-        int stt = 0;
-        if (in && mx > 0) {   // grouped[grouped['duration'] > 0] (preprocess_data.py:117)
-            // expect: sequential in name order (T14), the entries' loads eight at a time
-            double expect = 0.0;
-            for (int64_t e = va; e < vb; e += 8) {
-                uint32_t v[8];
+        act[q] = in && mx[q] > 0;   // grouped[grouped['duration'] > 0] (preprocess_data.py:117)
+        expect[q] = 0.0;
+    }
+    __syncthreads();   // (the thresholds in LDS)
+    // the detector's expect (anormaly_detector.py:63-67), sequential in name order per trace (T14):
+    // the range's service-op products staged in LDS a round at a time (coalesced loads, every load of
+    // a round in flight), each lane then adding its own trace's products of the round in order --
+    // the same products, the same sequential sums as a lane walking its trace alone
+    for (uint32_t r0 = 0; r0 < nv; r0 += cap) {
+        const uint32_t rn = min(cap, nv - r0);
+        constexpr int LU = 8;
+        for (uint32_t x0 = 0; x0 < rn; x0 += LU * LB_T) {
+            uint32_t v[LU];
 #pragma unroll
-                for (int q = 0; q < 8; ++q) v[q] = e + q < vb ? w.lsv[e + q] : 0u;
-#pragma unroll
-                for (int q = 0; q < 8; ++q)   // anormaly_detector.py:63-67
-                    if (e + q < vb) expect += (double)(v[q] >> 16) * la3[v[q] & 0xffffu];
+            for (int u = 0; u < LU; ++u) {
+                const uint32_t x = x0 + (uint32_t)(u * LB_T + tid);
+                v[u] = w.lsv[V0 + (int64_t)(r0 + min(x, rn - 1))];
             }
-            stt = (double)mx / 1000.0 > expect ? 2 : 1;   // :58, :69
+#pragma unroll
+            for (int u = 0; u < LU; ++u) {
+                const uint32_t x = x0 + (uint32_t)(u * LB_T + tid);
+                if (x < rn) prod[x] = (double)(v[u] >> 16) * la3[v[u] & 0xffffu];
+            }
         }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < NS; ++q)
+            if (act[q]) {
+                const uint32_t lo = max(va[q], r0), hi = min(vb[q], r0 + rn);
+                for (uint32_t j = lo; j < hi; j += 8) {   // eight LDS reads in flight, then the adds in order
+                    double p8[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) p8[u] = prod[min(j + u, hi - 1) - r0];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u)
+                        if (j + u < hi) expect[q] += p8[u];
+                }
+            }
+        __syncthreads();
+    }
+    for (size_t x = (size_t)tid * 4; x < reg0; x += (size_t)LB_T * 4) *(uint32_t*)(lraw + x) = 0u;
+    unsigned long long nab = 0, nno = 0, nz0 = 0, nz1 = 0;
+#pragma unroll
+    for (int q = 0; q < NS; ++q) {
+        const int32_t t = q * LB_T + tid;
+        const bool valid = t < nt;
+        const int64_t i = (int64_t)T0 + (valid ? t : nt - 1);   // (clamped)
+        const int32_t kid0 = w.lo_kid[i], tr = w.lo_tr[i];
+        const int64_t pa = w.lo_off[i], pb = w.lo_off[i + 1], ea = w.le_off[i];
+        const int stt = act[q] ? ((double)mx[q] / 1000.0 > expect[q] ? 2 : 1) : 0;   // :58, :69
         const int s_ = valid ? (stt == 2 ? 0 : stt == 1 ? 1 : -1) : -1;
         if (valid) {
             w.state[tr] = (uint8_t)stt;
@@ -2306,6 +2360,7 @@ __global__ void __launch_bounds__(LB_T, 6) k_lo_build_b(IxBatch<IxWinLoB> a) {
             }
         }
     }
+    __syncthreads();
     {   // the detector's counts and both graphs' entry totals: per wave, per block, one add each
         unsigned long long v[5] = {nab, nno, rows, nz0, nz1};
 #pragma unroll
@@ -2339,6 +2394,7 @@ __global__ void __launch_bounds__(LB_T, 6) k_lo_build_b(IxBatch<IxWinLoB> a) {
         }
         for (int32_t x = tid; x < nek; x += LB_T) Rg[3 * NP + x] = ((const uint32_t*)(G + (size_t)NP * 12))[x];
     }
+    __syncthreads();
 }
 // positions: each selected trace's rank among its graph's traces in layout order (decoupled
 // look-back over the side bytes), pinv[position] = layout index, staged in LDS for coalesced
@@ -2564,7 +2620,7 @@ int mr_lo_launch_batch(mr_ctx* ctx, int n, const mr_spans* const* sps, mr_graph*
         L.NP = NP;
         L.nek = (int32_t)nek;
         L.nsvc = sp->n_svcops;
-        lds = std::max(lds, 2 * (((size_t)NP * 12 + (size_t)nek * 4 + 15) / 16 * 16) + (size_t)sp->n_svcops * 8);
+        lds = std::max(lds, lo_region0(((size_t)NP * 12 + (size_t)nek * 4 + 15) / 16 * 16) + (size_t)sp->n_svcops * 8);
         ac.b0[k] = bc;
         bc += (int32_t)cdiv(sp->n_xj, 256);
         ac.w[k] = IxWinCross{d.state, sp->xj_tc.p, sp->xj_tp.p, sp->xj_eid.p, sp->n_xj, xs};
