@@ -2088,6 +2088,7 @@ struct TrTile {
     int32_t cw;    // lane j: coff[k + 1 + j] (readlane 0 / 1: the next tile's chunk range)
     uint32_t hm;   // the trace's hot-op bits (nhr > 0)
     uint32_t rl;   // the run of identical traces this lane heads (0: another lane's run; 1: its own)
+    uint32_t rln;  // the next tile's rl (a tail loads nothing of its own: its loads need it a tile ahead)
 };
 // the hot ops of a trace: their su first in the lane's sum (the same order in both walks), X into
 // the lane's register accumulators (integers: order-free; flushed once per walk)
@@ -2126,7 +2127,6 @@ __device__ __forceinline__ int32_t tr_walk_short(const GDev& G, int32_t k, const
                                                  int cur, int nxt, double d, double Ms, double xsc, const double* su_l,
                                                  unsigned long long* lacc, double& rmax, TrHot<HN>& H, int32_t& c0,
                                                  int32_t& n, int32_t& q0, int32_t& nq) {
-    const GLB u32x2* ids = gp((const u32x2*)G.tids) + lane;
     const GLB int32_t* coff = gp(G.coff);
     const GLB Q* qc = gp((const Q*)G.q[cur]);
     GLB Q* qn = gpw((Q*)G.q[nxt]);
@@ -2161,14 +2161,24 @@ __device__ __forceinline__ int32_t tr_walk_short(const GDev& G, int32_t k, const
     if (n != NC) return k;
     using R = TrTile<Q, NC, EXT>;
     const GLB double* cacc = cx ? gp(G.cold_acc) : sug;
-    auto load = [&](R& r, int32_t kk, int32_t cc0, int32_t qq0, int32_t nqq) {
+    // run marks of tile kk's lanes (1 on graphs without runs)
+    auto rl_of = [&](int32_t kk) -> uint32_t {
+        return trn ? (uint32_t)trn[min(min(kk, ke - 1) * WAVE + lane, T - 1)] : 1u;
+    };
+    // a run's tail (rl 0) needs none of its own ids, q, c or w -- the head walks for it and its r'
+    // comes by shuffle -- so its loads go to one shared word each (one cache line per load, not
+    // its own): unconditional loads, no branch
+    const GLB u32x2* idb = gp((const u32x2*)G.tids);
+    auto load = [&](R& r, int32_t kk, int32_t cc0, int32_t qq0, int32_t nqq, uint32_t rl) {
         const int32_t kq = min(kk, ke - 1);
         const int32_t p = min(kq * WAVE + lane, T - 1);
+        const bool hd = rl != 0u;
+        const int32_t ph = hd ? p : 0;
 #pragma unroll
-        for (int j = 0; j < NC; ++j) r.id[j] = ids[(size_t)min(cc0 + j, cl) * WAVE];
-        r.q = qc[p];
-        r.c = c_tp[p];
-        r.w = w_tp[p];
+        for (int j = 0; j < NC; ++j) r.id[j] = idb[hd ? (size_t)min(cc0 + j, cl) * WAVE + lane : 0];
+        r.q = qc[ph];
+        r.c = c_tp[ph];
+        r.w = w_tp[ph];
         if constexpr ((EXT & 1) != 0) r.mw = mw_tp[kc ? p : 0];
         if constexpr ((EXT & 2) != 0) {
             if (cx) {   // (uniform; ctids exists only on wide graphs)
@@ -2180,7 +2190,8 @@ __device__ __forceinline__ int32_t tr_walk_short(const GDev& G, int32_t k, const
         }
         r.cw = coff[min(kq + 1 + lane, ke)];
         r.hm = hot ? hmk[p] : 0u;   // (uniform)
-        r.rl = trn ? (uint32_t)trn[p] : 1u;
+        r.rl = rl;
+        r.rln = rl_of(kk + 1);
     };
     // tile kk from r: lane = position kk * 64 + lane
     auto run = [&](const R& r, int32_t kk, int32_t qq0, int32_t nqq) {
@@ -2198,7 +2209,7 @@ __device__ __forceinline__ int32_t tr_walk_short(const GDev& G, int32_t k, const
         // same sum and r') is walked by its head alone: its X times rl into the accumulators (integers:
         // exactly the rl separate adds), its r' broadcast to the run below
         const bool hd = r.rl != 0u;
-        const unsigned long long X = own ? (unsigned long long)__double2ull_rn((double)r.q * xsc) * (unsigned long long)r.rl : 0ull;
+        const unsigned long long X = own && hd ? (unsigned long long)__double2ull_rn((double)r.q * xsc) * (unsigned long long)r.rl : 0ull;
         double acc = H.n ? tr_hot_init(H, r.hm, X) : 0.0;
         if (hd) {
             double sv[2][4];
@@ -2235,10 +2246,10 @@ __device__ __forceinline__ int32_t tr_walk_short(const GDev& G, int32_t k, const
         }
         if (own) rmax = nmax(rmax, rp);
         const double wq = kc ? r.mw : (double)r.w;
-        qn[own ? p : T] = (Q)(wq * rp);   // q[T]: pad slot
+        qn[own && hd ? p : T] = (Q)(wq * rp);   // q[T]: pad slot (a run's tails never read theirs)
     };
     R A, B;
-    load(A, k, c0, q0, nq);
+    load(A, k, c0, q0, nq, rl_of(k));
     int32_t nA = n, qA = q0, nqA = nq;
     for (;;) {
         // B = tile k + 1 (its ranges from A's offsets), then A's tile
@@ -2249,7 +2260,7 @@ __device__ __forceinline__ int32_t tr_walk_short(const GDev& G, int32_t k, const
             qB = __builtin_amdgcn_readfirstlane(A.ccw);
             nqB = __builtin_amdgcn_readlane(A.ccw, 1) - qB;
         }
-        load(B, k + 1, c0B, qB, nqB);
+        load(B, k + 1, c0B, qB, nqB, A.rln);
         run(A, k, qA, nqA);
         if (++k == ke || nB != NC) {
             c0 = c0B, n = nB, q0 = qB, nq = nqB;
@@ -2261,7 +2272,7 @@ __device__ __forceinline__ int32_t tr_walk_short(const GDev& G, int32_t k, const
             qA = __builtin_amdgcn_readfirstlane(B.ccw);
             nqA = __builtin_amdgcn_readlane(B.ccw, 1) - qA;
         }
-        load(A, k + 1, c0A, qA, nqA);
+        load(A, k + 1, c0A, qA, nqA, B.rln);
         run(B, k, qB, nqB);
         if (++k == ke || nA != NC) {
             c0 = c0A, n = nA, q0 = qA, nq = nqA;
