@@ -764,10 +764,15 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
     for (int g = 0; g < ngroups; ++g)
         for (int32_t i = gbeg[(size_t)g], e = gbeg[(size_t)g + 1]; i < e; i += chunk_size)
             chunks.emplace_back(i, std::min<int32_t>(e, i + chunk_size));
-    const int nthr = std::min<int>((int)chunks.size(), max_streams);
+    // a call of one chunk (one window: the single-window latency) runs inline: its build, PageRanks
+    // and spectrum on this context's stream from the calling thread -- no worker thread to start,
+    // no hand-offs between threads or streams.  MR_WIN_INLINE=0: worker threads anyway (read per call)
+    const char* ie = getenv("MR_WIN_INLINE");
+    const bool inl = chunks.size() == 1 && !(ie && atoi(ie) == 0);
+    const int nthr = inl ? 0 : std::min<int>((int)chunks.size(), max_streams);
     // (every group's PageRanks on this context's stream: a second PageRank stream for odd groups
     // measured within the spread, profiles/r04al/, and was removed)
-    MR_TRY(win_aux(ctx, nthr));
+    if (nthr) MR_TRY(win_aux(ctx, nthr));
     auto pr_ctx = [&](int) -> mr_ctx* { return ctx; };
     // the SLO vectors once per distinct (a3, a3_valid, length) of the batch (windows usually share
     // one pair), resident before any window's detector runs
@@ -800,7 +805,7 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
     std::vector<WinRun> w((size_t)n_windows);
     std::vector<WinChunk> cw(chunks.size());
     std::vector<hipEvent_t> gev((size_t)ngroups, nullptr);   // a group's PageRanks are done
-    std::vector<std::string> err((size_t)nthr);
+    std::vector<std::string> err((size_t)std::max(nthr, 1));
     // task queue: phase-1 tasks (chunk c -> c) first, phase-3 tasks (the spectra of spec[i] -> ~i)
     // appended per group
     std::mutex mu;
@@ -810,6 +815,66 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
     bool closed = false;
     std::vector<int> built((size_t)ngroups, 0);
     for (int32_t c = 0; c < (int32_t)chunks.size(); ++c) q.push_back(c);
+    // a task: chunk c (c >= 0: its detectors + graph builds) or the spectra of spec[~c], on context a
+    auto do_task = [&](int32_t task, mr_ctx* a, int k) {
+        if (task >= 0) {   // a chunk's detectors + graph builds
+            const int32_t i0 = chunks[(size_t)task].first, i1 = chunks[(size_t)task].second;
+            std::vector<WinIn> fast;
+            for (int32_t i = i0; i < i1; ++i) {
+                WinRun& r = w[(size_t)i];
+                const mr_spans* sp = spans[i];
+                if (sp->indexed && sp->uniform_times && sp->has_times && !no_index) {
+                    fast.push_back(WinIn{sp, t0[i], t1[i], d_a3[slo_of[(size_t)i]]->p, d_a3v[slo_of[(size_t)i]]->p, &r});
+                } else {   // (synchronised at its end: no event needed)
+                    r.rc = win_detect_build(a, sp, t0[i], t1[i], a3[i], a3_valid[i], r, nullptr, precision);
+                    if (r.rc != MR_OK && r.rc != MR_ERR_VALUE) err[(size_t)k] = a->err;
+                }
+            }
+            if (!fast.empty()) {
+                const int rc = win_chunk_build_async(a, fast.data(), (int)fast.size(), precision, cw[(size_t)task]);
+                if (rc != MR_OK) {
+                    err[(size_t)k] = a->err;
+                    for (WinIn& f : fast) f.w->rc = rc;
+                }
+            }
+            std::lock_guard<std::mutex> lk(mu);
+            built[(size_t)group_of[(size_t)i0]] += i1 - i0;
+            cv_done.notify_all();
+        } else {           // spectra of up to MR_WS_BATCH windows, after their group's PageRanks
+            WinPhase ph(3);   // (an event, not a host wait; one launch, a block per window)
+            const std::vector<int32_t>& ids = spec[(size_t)~task];
+            (void)hipStreamWaitEvent(a->stream, gev[(size_t)group_of[(size_t)ids[0]]], 0);
+            MrWsWin ws[MR_WS_BATCH];
+            int nb = 0;
+            std::vector<int32_t> general;
+            for (int32_t i : ids) {
+                const WinRun& r = w[(size_t)i];
+                if (spec_general || !mr_win_spectrum_fits(r.ga->N, r.gn->N, spans[i]->n_podops, K)) {
+                    general.push_back(i);
+                    continue;
+                }
+                ws[nb++] = MrWsWin{r.ga->node_podop.p, r.ga->cov.p, r.gn->node_podop.p, r.gn->cov.p, r.ga->weight.p,
+                                   r.gn->weight.p, slots.p + (size_t)i * MR_WS_SLOT, r.nn, r.na, r.ga->N,
+                                   r.gn->N, spans[i]->n_podops};
+            }
+            if (nb) {
+                const int rc = mr_win_spectrum_launch_n(a, ws, nb, method, K);
+                for (int32_t i : ids)
+                    if (std::find(general.begin(), general.end(), i) == general.end()) {
+                        w[(size_t)i].rc = rc;
+                        w[(size_t)i].slot = rc == MR_OK;
+                    }
+                if (rc != MR_OK) err[(size_t)k] = a->err;
+            }
+            for (int32_t i : general) {   // past the one-block limits: the general path (synchronous)
+                WinRun& r = w[(size_t)i];
+                r.rc = win_spectrum(a, spans[i], r, method, top_max,
+                                    out_podop ? out_podop + (size_t)i * K : nullptr,
+                                    out_score ? out_score + (size_t)i * K : nullptr, &n_out[i]);
+                if (r.rc != MR_OK) err[(size_t)k] = a->err;
+            }
+        }
+    };
     std::vector<std::thread> th;
     for (int k = 0; k < nthr; ++k)
         th.emplace_back([&, k] {
@@ -825,74 +890,31 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
                     task = q.front();
                     q.pop_front();
                 }
-                if (task >= 0) {   // a chunk's detectors + graph builds
-                    const int32_t i0 = chunks[(size_t)task].first, i1 = chunks[(size_t)task].second;
-                    std::vector<WinIn> fast;
-                    for (int32_t i = i0; i < i1; ++i) {
-                        WinRun& r = w[(size_t)i];
-                        const mr_spans* sp = spans[i];
-                        if (sp->indexed && sp->uniform_times && sp->has_times && !no_index) {
-                            fast.push_back(WinIn{sp, t0[i], t1[i], d_a3[slo_of[(size_t)i]]->p, d_a3v[slo_of[(size_t)i]]->p, &r});
-                        } else {   // (synchronised at its end: no event needed)
-                            r.rc = win_detect_build(a, sp, t0[i], t1[i], a3[i], a3_valid[i], r, nullptr, precision);
-                            if (r.rc != MR_OK && r.rc != MR_ERR_VALUE) err[(size_t)k] = a->err;
-                        }
-                    }
-                    if (!fast.empty()) {
-                        const int rc = win_chunk_build_async(a, fast.data(), (int)fast.size(), precision, cw[(size_t)task]);
-                        if (rc != MR_OK) {
-                            err[(size_t)k] = a->err;
-                            for (WinIn& f : fast) f.w->rc = rc;
-                        }
-                    }
-                    std::lock_guard<std::mutex> lk(mu);
-                    built[(size_t)group_of[(size_t)i0]] += i1 - i0;
-                    cv_done.notify_all();
-                } else {           // spectra of up to MR_WS_BATCH windows, after their group's PageRanks
-                    WinPhase ph(3);   // (an event, not a host wait; one launch, a block per window)
-                    const std::vector<int32_t>& ids = spec[(size_t)~task];
-                    (void)hipStreamWaitEvent(a->stream, gev[(size_t)group_of[(size_t)ids[0]]], 0);
-                    MrWsWin ws[MR_WS_BATCH];
-                    int nb = 0;
-                    std::vector<int32_t> general;
-                    for (int32_t i : ids) {
-                        const WinRun& r = w[(size_t)i];
-                        if (spec_general || !mr_win_spectrum_fits(r.ga->N, r.gn->N, spans[i]->n_podops, K)) {
-                            general.push_back(i);
-                            continue;
-                        }
-                        ws[nb++] = MrWsWin{r.ga->node_podop.p, r.ga->cov.p, r.gn->node_podop.p, r.gn->cov.p, r.ga->weight.p,
-                                           r.gn->weight.p, slots.p + (size_t)i * MR_WS_SLOT, r.nn, r.na, r.ga->N,
-                                           r.gn->N, spans[i]->n_podops};
-                    }
-                    if (nb) {
-                        const int rc = mr_win_spectrum_launch_n(a, ws, nb, method, K);
-                        for (int32_t i : ids)
-                            if (std::find(general.begin(), general.end(), i) == general.end()) {
-                                w[(size_t)i].rc = rc;
-                                w[(size_t)i].slot = rc == MR_OK;
-                            }
-                        if (rc != MR_OK) err[(size_t)k] = a->err;
-                    }
-                    for (int32_t i : general) {   // past the one-block limits: the general path (synchronous)
-                        WinRun& r = w[(size_t)i];
-                        r.rc = win_spectrum(a, spans[i], r, method, top_max,
-                                            out_podop ? out_podop + (size_t)i * K : nullptr,
-                                            out_score ? out_score + (size_t)i * K : nullptr, &n_out[i]);
-                        if (r.rc != MR_OK) err[(size_t)k] = a->err;
-                    }
-                }
+                do_task(task, a, k);
             }
         });
+    if (inl) {   // the one chunk, here
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            q.clear();
+        }
+        do_task(0, ctx, 0);
+    }
     int rc = MR_OK;
     // the previous call's graphs go back to their pools on a thread of their own (their streams
     // finished with them before that call returned; ~8 us of pool bookkeeping per graph had been
     // ~1 ms at the end of every 64-window call)
     std::vector<mr_graph*> dead;
     dead.swap(ctx->graveyard);
-    std::thread reaper([&dead] {
+    std::thread reaper;
+    if (inl && dead.size() <= 64) {   // (a few graphs: here, before this call's work)
         for (mr_graph* g : dead) delete g;
-    });
+        dead.clear();
+    } else {
+        reaper = std::thread([&dead] {
+            for (mr_graph* g : dead) delete g;
+        });
+    }
     // Each group's PageRanks are enqueued without their closing read-back (mr_pagerank_batch_async),
     // so the next group's go in behind them while they run: the PageRank stream no longer idles
     // while this thread waits for a group and then enqueues the next (measured: this thread had
@@ -993,6 +1015,16 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
         for (; rc == MR_OK && settled < (pr_sync ? g + 1 : g); ++settled) rc = settle(settled);
     }
     for (; rc == MR_OK && settled < ngroups; ++settled) rc = settle(settled);
+    while (inl && rc == MR_OK) {   // the spectra settle queued, here
+        int32_t task;
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            if (q.empty()) break;
+            task = q.front();
+            q.pop_front();
+        }
+        do_task(task, ctx, 0);
+    }
     if (rc != MR_OK) {   // (an error left groups in flight)
         (void)hipStreamSynchronize(ctx->stream);
     }
@@ -1005,7 +1037,7 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
     }
     std::unique_ptr<WinPhase> ph_tail(new WinPhase(7));
     for (auto& t : th) t.join();
-    reaper.join();
+    if (reaper.joinable()) reaper.join();
     for (int k = 0; k < nthr; ++k) (void)hipStreamSynchronize(ctx->aux[(size_t)k]->stream);
     // (an error may leave PageRank work queued on the main stream that still reads window graphs
     // whose blocks return to the worker pools below: drain it first)
