@@ -796,7 +796,7 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
     // the windows' spectrum results land in device slots, read back once at the end
     DBuf<unsigned char> slots;
     MR_TRY(slots.alloc(ctx, (size_t)n_windows * MR_WS_SLOT));
-    MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));   // uploads done before other streams read them
+    if (!inl) MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));   // uploads done before other streams read them
     static const bool no_index = getenv("MR_NO_INDEX") != nullptr;
     const bool spec_general = getenv("MR_NO_WIN_SPECTRUM_SMALL") != nullptr;   // (read per call: tests)
     const char* sbe = getenv("MR_WIN_SPEC_BATCH");   // windows per spectrum launch, 1..MR_WS_BATCH (A/B)

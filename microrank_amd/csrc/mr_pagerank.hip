@@ -3295,9 +3295,16 @@ static int tr_split(mr_ctx* ctx, mr_graph* g, const FxPlan& P, int64_t wsum, int
         if (force_nb <= 0 && wsum <= W && atoi(fe) > 0) force_nb = atoi(fe);
     if (force_nb > 0) {   // (at most 1023 wave tiles per block still)
         nb = std::max<int64_t>(force_nb, cdiv(W, 1023));
-    } else if (tr_budget() > 0.0 && wsum > W) {
-        const int64_t share = (int64_t)std::ceil((double)resident * tr_budget() * (double)W / (double)wsum);
-        nb = std::max<int64_t>({std::min(nb, share), cdiv(W, 1023), 1});
+    } else {
+        if (tr_budget() > 0.0 && wsum > W) {
+            const int64_t share = (int64_t)std::ceil((double)resident * tr_budget() * (double)W / (double)wsum);
+            nb = std::min(nb, share);
+        }
+        // at least two tiles per wave: a launch of few tiles (one window's graphs) otherwise runs a
+        // block per 8 tiles, each paying its LDS image and an N-word partial row for them (C2 single
+        // window: 365 blocks of one tile per wave 0.85 ms, ~180 blocks 0.78 ms; batches and whole
+        // graphs run many tiles per wave and do not reach the cap)
+        nb = std::max<int64_t>({std::min<int64_t>(nb, cdiv(W, 2 * NW)), cdiv(W, 1023), 1});
     }
     // on the device (k_tr_cut: no host round trip) unless a block's traces must be weighed by
     // their kinds' multiplicities (kind-compressed graphs) or the cut table exceeds its LDS
