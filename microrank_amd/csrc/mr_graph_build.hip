@@ -2323,11 +2323,56 @@ __global__ void __launch_bounds__(LB_T, 6) k_lo_build_b(IxBatch<IxWinLoB> a) {
         }
     }
     __syncthreads();
-    // the range's pod-op and join entries: every wave, a lane per entry, each to its trace's graph
+    // the range's pod-op and join entries, each to its trace's graph.  A range of short traces (the
+    // longest -- the layout sorts by count, so the last -- of <= LB_LANE pod-ops): a lane per trace
+    // walks its own entries, all loads out at once, no lookups, each trace's entries rotated by its
+    // index (a run of identical traces would otherwise add into the same word in the same round).
+    // Else every wave over the range's entries, a lane per entry, the entry's trace looked up.
+    constexpr int LB_LANE = 8;
+    const bool lanewise = nt > 0 && pst[nt] - pst[nt - 1] <= (uint32_t)LB_LANE;
+    if (lanewise) {
+#pragma unroll
+        for (int q = 0; q < NS; ++q) {
+            const int32_t t = q * LB_T + tid;
+            const int sd = t < nt ? (int)ss[t] : -1;
+            if (sd < 0) continue;
+            unsigned char* G = lraw + (size_t)sd * gbytes;
+            const uint32_t a0 = pst[t], n = pst[t + 1] - a0, rot = n ? (uint32_t)t % n : 0u;
+            uint32_t pc[LB_LANE];
+            int32_t fr[LB_LANE];
+#pragma unroll
+            for (int u = 0; u < LB_LANE; ++u) {
+                const uint32_t j = (uint32_t)u + rot;
+                const int64_t e = P0 + (int64_t)a0 + (u < (int)n ? (j >= n ? j - n : j) : 0u);
+                pc[u] = (uint32_t)w.lo16[e] | ((uint32_t)w.lo_cnt[e] << 16);
+                fr[u] = w.lo_first[e];
+            }
+#pragma unroll
+            for (int u = 0; u < LB_LANE; ++u)
+                if (u < (int)n) {
+                    const uint32_t c = pc[u] & 0xffffu;
+                    atomicAdd((unsigned long long*)G + c, (unsigned long long)(pc[u] >> 16) | (1ull << 32));
+                    atomicMax((int32_t*)(G + (size_t)NP * 8) + c, 0x7fffffff - fr[u]);
+                }
+            const uint32_t b0e = est[t], m = est[t + 1] - b0e, rte = m ? (uint32_t)t % m : 0u;
+            uint32_t* Ge = (uint32_t*)(G + (size_t)NP * 12);
+            for (uint32_t u0 = 0; u0 < m; u0 += LB_LANE) {
+                uint32_t ev[LB_LANE];
+#pragma unroll
+                for (int u = 0; u < LB_LANE; ++u) {
+                    const uint32_t j = u0 + (uint32_t)u, jr = j + rte;
+                    ev[u] = w.le[Q0 + (int64_t)b0e + (j < m ? (jr >= m ? jr - m : jr) : 0u)];
+                }
+#pragma unroll
+                for (int u = 0; u < LB_LANE; ++u)
+                    if (u0 + (uint32_t)u < m) atomicAdd(Ge + (ev[u] & 0xffffu), ev[u] >> 16);
+            }
+        }
+    }
     const uint32_t n0 = nt ? pst[1 < nt ? 1 : nt] - pst[0] : 0u;
     const uint32_t npo = n0 > 0 && np == (uint32_t)nt * n0 ? n0 : 0u;   // (uniform: every trace n0 entries)
     constexpr int NW = LB_T / WAVE;
-    const uint32_t nmax = max(np, nq);
+    const uint32_t nmax = lanewise ? 0u : max(np, nq);
     for (uint32_t b0 = (uint32_t)wv * (LB_R * WAVE); b0 < nmax; b0 += NW * LB_R * WAVE) {
         uint32_t pc[LB_R], ev[LB_R];
         int32_t fr[LB_R];

@@ -1,20 +1,21 @@
-"""W distinct C2 windows (1000 ops / 200k traces) per mr_windows_batch call, N calls: host wall
-time per call; under rocprofv3 --kernel-trace, `win1_trace.py --analyze` splits the trace per call
-(isolated kernel durations of one build chunk when W <= the chunk size).
-    python3 scripts/chunk_iso.py N W"""
+"""W distinct C2 windows (1000 ops / 200k traces; or OPS / TRACES) per mr_windows_batch call, N
+calls: host wall time per call; under rocprofv3 --kernel-trace, `call_timeline.py` /
+`win1_trace.py --analyze` split the trace per call (isolated kernel durations of one build chunk
+when W <= the chunk size).
+    python3 scripts/chunk_iso.py N W [OPS TRACES]"""
 import sys
 import time
 
 sys.path.insert(0, ".")
 
 
-def main(n, wn):
+def main(n, wn, ops=1000, traces=200_000):
     import bench
     from microrank_amd import _lib
     from microrank_amd.online_rca import rank_windows
     from microrank_amd.preprocess_data import DeviceSpans
 
-    normal, abn = bench.c2_windows(wn, 1000, 200_000, rank=0)
+    normal, abn = bench.c2_windows(wn, ops, traces, rank=0)
     ctx = _lib.default_context()
     s3, sok = bench.slo_from_gpu(ctx, normal)
     wins = []
@@ -38,4 +39,4 @@ def main(n, wn):
 
 
 if __name__ == "__main__":
-    main(int(sys.argv[1]), int(sys.argv[2]))
+    main(int(sys.argv[1]), int(sys.argv[2]), *[int(x) for x in sys.argv[3:5]])
