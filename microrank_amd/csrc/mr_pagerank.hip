@@ -3260,10 +3260,21 @@ static size_t plan_lds(int32_t N, const FxPlan& P) { return TrLds(N, P.mode).tot
 // resident blocks of the plan's kernel on the chip (occupancy by LDS image and VGPRs)
 static int64_t plan_resident(int32_t N, const FxPlan& P) {
     const size_t lds = plan_lds(N, P);
+    // (cached per (mode, block size, LDS bytes): a window group asks for each of its 256 graphs)
+    static std::mutex mu;
+    static std::map<std::tuple<int, int, size_t>, int> cache;
+    const auto key = std::make_tuple(P.mode, P.NT, lds);
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        auto it = cache.find(key);
+        if (it != cache.end()) return (int64_t)num_cus() * it->second;
+    }
     const TrA kfn = tr_kernel(false, P.mode, P.NT, 0);
     int n = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, (const void*)kfn, P.NT, lds) != hipSuccess || n < 1)
         n = std::max<int>(1, (int)(WV_LDS_MAX / std::max<size_t>(lds, 1)));
+    std::lock_guard<std::mutex> lk(mu);
+    cache[key] = n;
     return (int64_t)num_cus() * n;
 }
 
