@@ -2661,7 +2661,9 @@ static int fb_ops(int32_t N, bool many) {
     const char* e = getenv("MR_FB_OPS");
     const int force = e ? atoi(e) : 0;
     if (force == 16 || force == 32 || force == 64) return force;
-    return N <= 8192 ? (many ? 64 : 16) : 32;
+    // (> 8192 ops: 64 measured ahead of 32 -- C4 140.0 -> 137.8 us per iteration, its rank-0-of-8
+    // share 43.6 -> 41.5 us, C5 2.97 -> 2.94 ms; profiles/r05/r05q_fb_ops64_ab.txt)
+    return N <= 8192 ? (many ? 64 : 16) : 64;
 }
 constexpr int64_t FB_MANY_BLOCKS = 1024;   // 16-op blocks of a launch from which "many" holds
 constexpr int64_t LASTFIN_WORDS = 32768;   // k_tr_a's last-block finish: partial-row words it reads (256 KB)
