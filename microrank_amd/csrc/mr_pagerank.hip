@@ -939,6 +939,10 @@ __global__ void k_kind_verify(const int64_t* off, const ID* ops, const float* w_
 //   k_kind_final   per trace: kind = its record's class size; every member is checked against
 //                  the representative (ops and fp32(1/len_t), exactly): a hash collision raises
 //                  flag word 0 (retry with the next seed), never a miscount.
+// graphs of at least this many traces take the partition path (below: the LDS-aggregated global
+// table).  1M measured ahead of 2M for C4's rank-0-of-8 share (1.25M traces: step 1.50 -> 1.44 ms,
+// profiles/r05/r05r_kind_part_ab.txt); MR_KIND_PART_MIN overrides (read per call)
+constexpr int64_t KIND_PART_MIN_DEFAULT = (int64_t)1 << 20;
 constexpr int KP_MEAN = 1024;   // mean records per partition (at most)
 constexpr int KP_LDS = 4096;    // LDS table slots of a partition block
 constexpr int KP_B = 256;
@@ -3976,7 +3980,7 @@ static int pagerank_setup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool 
     uint64_t cap = 1;
     while (cap < 2ull * (uint64_t)T) cap <<= 1;
     const char* kpe = getenv("MR_KIND_PART_MIN");   // test knob (read per call): traces from which the partition path runs
-    const int64_t kp_min = kpe ? (int64_t)atoll(kpe) : (int64_t)(1 << 21);
+    const int64_t kp_min = kpe ? (int64_t)atoll(kpe) : KIND_PART_MIN_DEFAULT;
     const bool ktab = chk || (int64_t)T < kp_min;
     if (!ktab) cap = 0;
     const int32_t n_pr = g->n_pr;
@@ -4063,7 +4067,7 @@ static int pagerank_setup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool 
 // one rank, kinds through the hash table with u16 ids, pr_trace = operation_trace, k_tr_a layout.
 static bool setup_batchable(const mr_graph* g, uint32_t flags) {
     const char* kpe = getenv("MR_KIND_PART_MIN");
-    const int64_t kp_min = kpe ? (int64_t)atoll(kpe) : (int64_t)(1 << 21);
+    const int64_t kp_min = kpe ? (int64_t)atoll(kpe) : KIND_PART_MIN_DEFAULT;
     return g->T > 0 && (int64_t)g->T < kp_min && !g->kinds_given && !g->mult.p && g->rs_is_sr && g->rs16.p &&
            g->pr_identity && g->n_pr == g->T && g->fused && g->tperm.p && g->w_tp.p && !g->mw_tp.p &&
            !(flags & MR_PR_EXACT_SUMS) && g->T_all == 0;
@@ -4965,7 +4969,7 @@ static int kind_compressed_pagerank(mr_ctx* ctx, mr_graph* g, int anomaly, doubl
     uint64_t cap = 1;
     while (cap < 2ull * (uint64_t)T) cap <<= 1;
     const char* kpe = getenv("MR_KIND_PART_MIN");
-    const bool ktab = (int64_t)T < (kpe ? (int64_t)atoll(kpe) : (int64_t)(1 << 21));
+    const bool ktab = (int64_t)T < (kpe ? (int64_t)atoll(kpe) : KIND_PART_MIN_DEFAULT);
     if (!ktab) cap = 0;
     MR_TRY(g->kind.alloc(ctx, (size_t)T));
     MR_TRY(g->krep.alloc(ctx, (size_t)T));
