@@ -14,4 +14,5 @@ for c in c3 c4 c5; do
   cut -c1-300 gpurun_out/fin_$c.json
 done
 bash scripts/prof_bench.sh fin_c2s --no-cpu --no-side --steps 10 --warmup 2 > /dev/null || exit 1
+bash scripts/prof_bench.sh fin_c4s8 --config c4 --no-cpu --shard-of 8 --steps 10 --warmup 2 > /dev/null || exit 1
 echo done
