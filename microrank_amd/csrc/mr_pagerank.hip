@@ -1586,14 +1586,18 @@ __global__ void __launch_bounds__(256) k_lo_fill_b(const LDev* __restrict__ ld, 
         const unsigned long long hm = __ballot(hd);
         const unsigned long long below = hm & (lane == WAVE - 1 ? ~0ull : (2ull << lane) - 1ull);
         const int32_t ixh = __shfl(ix, 63 - __builtin_clzll(below), WAVE);
+        // only a tile of the 512-thread walk's short tiers merges (the general loop walks every
+        // lane): there its runs share the head's rotation and are marked; a longer tile keeps one
+        // rotation per trace (a shared rotation there would put a run's adds on one word at a time)
+        const bool mt = G.c64[k + 1] - G.c64[k] <= MR_TR_TIERS512;
         if (i < T && G.trun) {
             const unsigned long long above = lane == WAVE - 1 ? 0ull : hm & (~0ull << (lane + 1));
-            G.trun[i] = hd ? (uint8_t)((above ? __builtin_ctzll(above) : WAVE) - lane) : (uint8_t)0;
+            G.trun[i] = !mt ? (uint8_t)1 : hd ? (uint8_t)((above ? __builtin_ctzll(above) : WAVE) - lane) : (uint8_t)0;
         }
         if (i < T) {
             e0 = G.lo_off[ix];
             len = G.lo_off[ix + 1] - e0;
-            rot = len && G.rot ? (int64_t)((uint32_t)ixh % (uint32_t)len) : 0;
+            rot = len && G.rot ? (int64_t)((uint32_t)(mt ? ixh : ix) % (uint32_t)len) : 0;
             const int32_t L = G.lo_len[ix];
             const uint32_t kc = G.kcnt[G.lo_kid[ix]];
             G.w_tp[i] = L > 0 ? (float)(1.0 / (double)L) : 0.0f;
