@@ -577,7 +577,7 @@ def c4_leg_guarded(hg, world, rank, dist, line, limit_s=240.0):
     def expire():
         if line is not None:
             line["c4_sharded"] = {"error": f"timed out after {limit_s:.0f} s"}
-            print(json.dumps(line), flush=True)
+            emit(line)
         print(f"[bench] c4_sharded leg hung for {limit_s:.0f} s: exiting with status 3", file=sys.stderr, flush=True)
         os._exit(3)
 
@@ -935,7 +935,29 @@ def run_ingest(args):
                              "ms": round(dt_host * 1e3, 1)}}
 
 
+# The driver reads ONE JSON line from stdout, but libraries write there too (the gloo rendezvous'
+# "connected to N peer ranks", RCCL's version banner at communicator init): fd 1 is pointed at
+# stderr for the run and the line goes to the original stdout.
+_LINE_OUT = None
+
+
+def claim_stdout():
+    global _LINE_OUT
+    if _LINE_OUT is None:
+        sys.stdout.flush()
+        fd = os.dup(1)
+        os.dup2(2, 1)
+        _LINE_OUT = os.fdopen(fd, "w")
+
+
+def emit(obj):
+    out = _LINE_OUT if _LINE_OUT is not None else sys.stdout
+    out.write(json.dumps(obj) + "\n")
+    out.flush()
+
+
 def main():
+    claim_stdout()
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -1021,7 +1043,7 @@ def main():
         if args.config == "sweep" and "--steps" not in sys.argv:
             args.steps, args.warmup = 3, 1
         out = {"sweep": run_sweep, "stream": run_stream, "ingest": run_ingest, "dropin": run_dropin}[args.config](args)
-        print(json.dumps(out), flush=True)
+        emit(out)
         return
     if args.config in ("c4", "c5"):
         out = run_c4(args, world, rank, dist)
@@ -1031,7 +1053,7 @@ def main():
                 "fetch_bytes": round(traffic["fetch"]), "write_bytes": round(traffic["write"]),
                 "source": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950) / WRITE_SIZE, per iteration (A + B launches)"}
         if out is not None and not args.pmc_child:
-            print(json.dumps(out), flush=True)
+            emit(out)
         if dist is not None:
             dist.barrier()
             dist.destroy_process_group()
@@ -1259,7 +1281,7 @@ def main():
                                       "what": "B_iter with 2 B per (trace, op) pair: k_tr_a reads u16 op ids"}
     if args.no_side:
         add_copy_frac(out, ctx)
-        print(json.dumps(out), flush=True)
+        emit(out)
         if dist is not None:
             dist.barrier()
             dist.destroy_process_group()
@@ -1304,7 +1326,7 @@ def main():
             out["cpu_top_matches"] = bool(cres is not None and list(cres[0]) == list(top))
         except Exception as e:  # the baseline must never sink the GPU line
             out["cpu_baseline"] = {"value": None, "error": f"{type(e).__name__}: {e}"}
-    print(json.dumps(out), flush=True)
+    emit(out)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
