@@ -781,17 +781,44 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
     std::vector<std::unique_ptr<DBuf<double>>> d_a3;
     std::vector<std::unique_ptr<DBuf<uint8_t>>> d_a3v;
     std::vector<size_t> slo_of((size_t)n_windows);
+    std::vector<int32_t> slo_win;   // the first window of each distinct vector pair
+    size_t slo_bytes = 0;
     for (int32_t i = 0; i < n_windows; ++i) {
         const auto key = std::make_tuple(a3[i], a3_valid[i], spans[i]->n_svcops);
         auto it = slo_ix.find(key);
         if (it == slo_ix.end()) {
-            d_a3.emplace_back(new DBuf<double>());
-            d_a3v.emplace_back(new DBuf<uint8_t>());
-            MR_TRY(d_a3.back()->upload(ctx, a3[i], (size_t)std::max(spans[i]->n_svcops, 1)));
-            MR_TRY(d_a3v.back()->upload(ctx, a3_valid[i], (size_t)std::max(spans[i]->n_svcops, 1)));
-            it = slo_ix.emplace(key, d_a3.size() - 1).first;
+            it = slo_ix.emplace(key, slo_win.size()).first;
+            slo_win.push_back(i);
+            slo_bytes += (size_t)std::max(spans[i]->n_svcops, 1) * 9 + 16;
         }
         slo_of[(size_t)i] = it->second;
+    }
+    // staged through the context's pinned buffer when they fit: the copies go out asynchronously
+    // (a pageable copy blocks this thread while the runtime stages it)
+    if (slo_bytes <= MR_PIN_BYTES && !ctx->pin &&
+        hipHostMalloc((void**)&ctx->pin, MR_PIN_BYTES, hipHostMallocDefault) != hipSuccess)
+        ctx->pin = nullptr;
+    unsigned char* stage = slo_bytes <= MR_PIN_BYTES ? (unsigned char*)ctx->pin : nullptr;
+    for (int32_t i : slo_win) {
+        const size_t ns = (size_t)std::max(spans[i]->n_svcops, 1);
+        d_a3.emplace_back(new DBuf<double>());
+        d_a3v.emplace_back(new DBuf<uint8_t>());
+        if (!stage) {
+            MR_TRY(d_a3.back()->upload(ctx, a3[i], ns));
+            MR_TRY(d_a3v.back()->upload(ctx, a3_valid[i], ns));
+            continue;
+        }
+        MR_TRY(d_a3.back()->alloc(ctx, ns));
+        MR_TRY(d_a3v.back()->alloc(ctx, ns));
+        const size_t n_in = (size_t)spans[i]->n_svcops;   // (0: the buffers stay unread)
+        memcpy(stage, a3[i], n_in * sizeof(double));
+        memcpy(stage + n_in * sizeof(double), a3_valid[i], n_in);
+        if (n_in) {
+            MR_TRY_HIP(ctx, hipMemcpyAsync(d_a3.back()->p, stage, n_in * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+            MR_TRY_HIP(ctx, hipMemcpyAsync(d_a3v.back()->p, stage + n_in * sizeof(double), n_in, hipMemcpyHostToDevice,
+                                           ctx->stream));
+        }
+        stage += (n_in * 9 + 15) / 16 * 16;
     }
     // the windows' spectrum results land in device slots, read back once at the end
     DBuf<unsigned char> slots;
@@ -941,9 +968,26 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
         if (!gev[(size_t)g] && hipEventCreateWithFlags(&gev[(size_t)g], hipEventDisableTiming) != hipSuccess) return MR_ERR_HIP;
         return hipEventRecord(gev[(size_t)g], pr_ctx(g)->stream) == hipSuccess ? MR_OK : MR_ERR_HIP;
     };
+    // spectrum tasks of up to MR_WS_BATCH ranked windows of group g: task ~i = list spec[i]
+    auto queue_spectra = [&](int g) {   // (under mu)
+        const int32_t i0 = gbeg[(size_t)g], i1 = gbeg[(size_t)g + 1];
+        int32_t head = -1;
+        for (int32_t i = i0; i < i1; ++i) {
+            spec[(size_t)i].clear();
+            if (w[(size_t)i].rc != MR_OK || !w[(size_t)i].gn) continue;
+            if (head < 0 || (int)spec[(size_t)head].size() == spec_batch) {
+                if (head >= 0) q.push_back(~head);
+                head = i;
+            }
+            spec[(size_t)head].push_back(i);
+        }
+        if (head >= 0) q.push_back(~head);
+    };
     // group g's results are final: check its words (rerun on a collision) and queue its spectra
-    auto settle = [&](int g) -> int {
+    // (early: they went in behind the PageRanks already, again only after a rerun)
+    auto settle = [&](int g, bool early) -> int {
         int r = MR_OK;
+        bool reran = false;
         if (pend[(size_t)g]) {
             mr_ctx* pc = pr_ctx(g);
             bool rerun = false;
@@ -954,26 +998,21 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
                 r = mr_pagerank_batch(pc, ggs[(size_t)g].data(), gan[(size_t)g].data(), (int)ggs[(size_t)g].size(), 0.85,
                                       0.01, 25, precision, 0);
                 if (r == MR_OK) r = record(g);
+                reran = true;
             }
             if (r != MR_OK && pc != ctx) ctx->err = pc->err;
         }
-        const int32_t i0 = gbeg[(size_t)g], i1 = gbeg[(size_t)g + 1];
         std::lock_guard<std::mutex> lk(mu);
-        if (r == MR_OK) {   // spectrum tasks of up to MR_WS_BATCH ranked windows: task ~i = list spec[i]
-            int32_t head = -1;
-            for (int32_t i = i0; i < i1; ++i) {
-                if (w[(size_t)i].rc != MR_OK || !w[(size_t)i].gn) continue;
-                if (head < 0 || (int)spec[(size_t)head].size() == spec_batch) {
-                    if (head >= 0) q.push_back(~head);
-                    head = i;
-                }
-                spec[(size_t)head].push_back(i);
-            }
-            if (head >= 0) q.push_back(~head);
-        }
+        if (r == MR_OK && (!early || reran)) queue_spectra(g);
         cv_task.notify_all();
         return r;
     };
+    // a call of one chunk (inline, one group): its spectra go in behind its PageRanks before their
+    // words are read, so the host's wait for the words no longer sits between the two on the GPU
+    // (C2 one window: a ~20 us idle gap plus the spectrum's launch).  A collision rerun overwrites
+    // the slots with a second round of spectra.  MR_WIN_SPEC_EARLY=0: after the words (read per call)
+    const char* see = getenv("MR_WIN_SPEC_EARLY");
+    const bool spec_early = inl && !pr_sync && !(see && atoi(see) == 0);
     int settled = 0;   // groups whose spectra are queued
     for (int g = 0; g < ngroups && rc == MR_OK; ++g) {
         const int32_t i0 = gbeg[(size_t)g], i1 = gbeg[(size_t)g + 1];
@@ -1011,10 +1050,26 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
             if (rc != MR_OK && pc != ctx) ctx->err = pc->err;
         }
         if (rc == MR_OK) rc = record(g);
+        if (rc == MR_OK && spec_early) {
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                queue_spectra(g);
+            }
+            for (;;) {   // (inline: this thread is the only worker)
+                int32_t task;
+                {
+                    std::lock_guard<std::mutex> lk(mu);
+                    if (q.empty()) break;
+                    task = q.front();
+                    q.pop_front();
+                }
+                do_task(task, ctx, 0);
+            }
+        }
         // the previous group's words are in by now, or nearly: settle it (this one stays in flight)
-        for (; rc == MR_OK && settled < (pr_sync ? g + 1 : g); ++settled) rc = settle(settled);
+        for (; rc == MR_OK && settled < (pr_sync ? g + 1 : g); ++settled) rc = settle(settled, spec_early);
     }
-    for (; rc == MR_OK && settled < ngroups; ++settled) rc = settle(settled);
+    for (; rc == MR_OK && settled < ngroups; ++settled) rc = settle(settled, spec_early);
     while (inl && rc == MR_OK) {   // the spectra settle queued, here
         int32_t task;
         {
@@ -1039,6 +1094,14 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
     for (auto& t : th) t.join();
     if (reaper.joinable()) reaper.join();
     for (int k = 0; k < nthr; ++k) (void)hipStreamSynchronize(ctx->aux[(size_t)k]->stream);
+    // every device-slot spectrum in one read-back: queued on this stream into the pinned buffer
+    // when it fits (one window: ~30 us less than a synchronous pageable copy after the drain)
+    const size_t slot_bytes = (size_t)n_windows * MR_WS_SLOT;
+    bool slots_pinned = false;
+    if (rc == MR_OK && slot_bytes <= MR_PIN_BYTES) {
+        if (!ctx->pin && hipHostMalloc((void**)&ctx->pin, MR_PIN_BYTES, hipHostMallocDefault) != hipSuccess) ctx->pin = nullptr;
+        slots_pinned = ctx->pin && hipMemcpyAsync(ctx->pin, slots.p, slot_bytes, hipMemcpyDeviceToHost, ctx->stream) == hipSuccess;
+    }
     // (an error may leave PageRank work queued on the main stream that still reads window graphs
     // whose blocks return to the worker pools below: drain it first)
     (void)hipStreamSynchronize(ctx->stream);
@@ -1047,12 +1110,17 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
     MR_TRY(rc);
     for (auto& e : err)
         if (!e.empty()) return mr_fail(ctx, MR_ERR_HIP, "mr_windows_batch: %s", e.c_str());
-    {   // every device-slot spectrum in one read-back
-        std::vector<unsigned char> hs((size_t)n_windows * MR_WS_SLOT);
-        MR_TRY_HIP(ctx, hipMemcpy(hs.data(), slots.p, hs.size(), hipMemcpyDeviceToHost));
+    {
+        std::vector<unsigned char> hv;
+        const unsigned char* hs = (const unsigned char*)ctx->pin;
+        if (!slots_pinned) {
+            hv.resize(slot_bytes);
+            MR_TRY_HIP(ctx, hipMemcpy(hv.data(), slots.p, slot_bytes, hipMemcpyDeviceToHost));
+            hs = hv.data();
+        }
         for (int32_t i = 0; i < n_windows; ++i)
             if (w[(size_t)i].slot)
-                mr_win_spectrum_unpack(hs.data() + (size_t)i * MR_WS_SLOT, out_podop ? out_podop + (size_t)i * K : nullptr,
+                mr_win_spectrum_unpack(hs + (size_t)i * MR_WS_SLOT, out_podop ? out_podop + (size_t)i * K : nullptr,
                                        out_score ? out_score + (size_t)i * K : nullptr, &n_out[i]);
     }
     for (int32_t i = 0; i < n_windows; ++i) {

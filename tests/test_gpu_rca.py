@@ -984,3 +984,36 @@ def test_windows_batch_layout_order_rerun_sets_up_again(c3_window, monkeypatch):
     np.testing.assert_allclose(base[0][1], base[1][1], rtol=1e-12, atol=0)
     d_lo.close()
     d_gen.close()
+
+
+def test_single_window_early_spectrum_and_rerun(c3_window, monkeypatch):
+    """A call of one window runs inline and queues its spectrum behind its PageRanks before their
+    error words are read; a kind-hash collision (MR_KIND_TEST_COLLIDE, general build) reruns the
+    PageRanks and queues the spectrum again.  Every variant ranks bitwise as the spectrum queued
+    after the words (MR_WIN_SPEC_EARLY=0), on both table layouts."""
+    import bench
+    from microrank_amd import _lib
+    from microrank_amd.online_rca import rank_windows
+    from microrank_amd.preprocess_data import DeviceSpans
+
+    ctx = _lib.default_context()
+    normal, abnormal, t0, t1 = c3_window
+    a3, ok = bench.slo_from_gpu(ctx, normal)
+    d_lo = DeviceSpans(ctx, abnormal)
+    monkeypatch.setenv("MR_NO_LO", "1")
+    d_gen = DeviceSpans(ctx, abnormal)
+    monkeypatch.delenv("MR_NO_LO")
+    for d in (d_lo, d_gen):
+        one = [(d, t0, t1, a3, ok)]
+        monkeypatch.setenv("MR_WIN_SPEC_EARLY", "0")
+        base = rank_windows(ctx, one)[0]
+        monkeypatch.delenv("MR_WIN_SPEC_EARLY")
+        early = rank_windows(ctx, one)[0]
+        monkeypatch.setenv("MR_KIND_TEST_COLLIDE", "1")
+        coll = rank_windows(ctx, one)[0]
+        monkeypatch.delenv("MR_KIND_TEST_COLLIDE")
+        assert base[5] == 0 and len(base[0]) > 0
+        for r in (early, coll):
+            assert r[2:] == base[2:] and list(r[0]) == list(base[0]) and r[1].tobytes() == base[1].tobytes()
+    d_lo.close()
+    d_gen.close()
