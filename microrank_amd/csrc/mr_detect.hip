@@ -870,7 +870,8 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
         } else {           // spectra of up to MR_WS_BATCH windows, after their group's PageRanks
             WinPhase ph(3);   // (an event, not a host wait; one launch, a block per window)
             const std::vector<int32_t>& ids = spec[(size_t)~task];
-            (void)hipStreamWaitEvent(a->stream, gev[(size_t)group_of[(size_t)ids[0]]], 0);
+            if (a != pr_ctx(group_of[(size_t)ids[0]]))   // (the PageRanks' own stream: in order already)
+                (void)hipStreamWaitEvent(a->stream, gev[(size_t)group_of[(size_t)ids[0]]], 0);
             MrWsWin ws[MR_WS_BATCH];
             int nb = 0;
             std::vector<int32_t> general;
