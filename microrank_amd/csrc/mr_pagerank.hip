@@ -2485,7 +2485,13 @@ __device__ __forceinline__ void tr_ssv_share(const GDev& G, int32_t lb, int cur,
             bb = wave_sum(bb);
             if (lane == j) ssv = G.alpha * (bb / Ms);
         }
-        if (on) G.fx_ssv[o] = ssv;
+        if (on) {
+            if (G.lastfin)   // (write-through: the graph's last block reads it with sc1 loads)
+                __hip_atomic_store(gpw((unsigned long long*)G.fx_ssv) + o, (unsigned long long)__double_as_longlong(ssv),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else
+                G.fx_ssv[o] = ssv;
+        }
     }
 }
 
@@ -2541,7 +2547,10 @@ __device__ __forceinline__ void tr_last_finish(const GDev& G, int it, double d, 
         }
         double ssv = 0.0;
         bool big = false;
-        if (on) {
+        if (on && G.ssv_pre) {   // every block computed its share of the terms (tr_ssv_share): one load
+            ssv = __longlong_as_double((long long)__hip_atomic_load(gp((const unsigned long long*)G.fx_ssv) + o,
+                                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        } else if (on) {
             const int64_t e0 = ss_off[o], e1 = ss_off[o + 1];
             if (e1 - e0 <= 8) {
                 int32_t pp[8];
@@ -4395,6 +4404,8 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
     const bool lastfin_on = !(lfe && atoi(lfe) == 0);
     const char* sve = getenv("MR_TR_SSV");   // (A/B and tests, read per call) 0: k_fx_b computes the call-graph terms
     const bool ssv_on = !(sve && atoi(sve) == 0);
+    const char* lse = getenv("MR_TR_LFSSV");   // (A/B and tests, read per call)
+    const bool lfssv_on = !(lse && atoi(lse) == 0);
     // (A/B, read per call) 0: plain partial-row stores.  Write-through measured C4 rank 0 of 8: 43.1
     // vs 44.6 us per iteration, C4 whole: within noise (two repeats each)
     const char* rwe = getenv("MR_TR_ROW_WT");
@@ -4506,8 +4517,10 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
                     plan.mode == WV_SU_ALL && nfa >= 1 && g->N <= plan.NT && nfa * (int64_t)g->N <= LASTFIN_WORDS;
         v.n_fb = g->fused && !v.lastfin ? cdiv(g->N, v.fb_ops) : 0;
         // the call-graph terms in k_tr_a (large graphs: k_fx_b's chains of dependent loads leave its
-        // critical path); not for wide graphs (k_fx_b's columns past NA)
-        v.ssv_pre = ssv_on && v.n_fb > 0 && nfa >= 1 && !g->wide && g->N >= 2048;
+        // critical path; not for wide graphs: k_fx_b's columns past NA).  Last-block graphs: every
+        // block writes its share write-through and the last block reads the terms with one load per
+        // op instead of the ss_off -> ss_par -> pw / s_k chain (MR_TR_LFSSV=0: the chain; read per call)
+        v.ssv_pre = ssv_on && nfa >= 1 && !g->wide && ((v.n_fb > 0 && g->N >= 2048) || (v.lastfin && lfssv_on));
         v.row_wt = row_wt_on && g->N >= 2048;
         blocks_fb += v.n_fb;
         v.blk0 = blocks_a;

@@ -1017,3 +1017,30 @@ def test_single_window_early_spectrum_and_rerun(c3_window, monkeypatch):
             assert r[2:] == base[2:] and list(r[0]) == list(base[0]) and r[1].tobytes() == base[1].tobytes()
     d_lo.close()
     d_gen.close()
+
+
+def test_last_block_call_graph_terms_bitwise(c3_window, monkeypatch):
+    """Last-block graphs (one launch per iteration: C3-sized window graphs) take the call-graph
+    terms alpha (P_ss s_k)[o] / M_s(k) from every block's write-through share (tr_ssv_share) instead
+    of the last block's own ss_off -> ss_par -> pw chain: the same arithmetic, so a batch of four
+    windows and a window alone rank bitwise as with the chain (MR_TR_LFSSV=0)."""
+    import bench
+    from microrank_amd import _lib
+    from microrank_amd.online_rca import rank_windows
+    from microrank_amd.preprocess_data import DeviceSpans
+
+    ctx = _lib.default_context()
+    normal, abnormal, t0, t1 = c3_window
+    a3, ok = bench.slo_from_gpu(ctx, normal)
+    d = DeviceSpans(ctx, abnormal)
+    span = (t1 - t0) // 4
+    wins = [(d, t0 + k * span // 8, t1 - k * span // 8, a3, ok) for k in range(4)]
+    for batch in (wins, wins[:1]):
+        monkeypatch.setenv("MR_TR_LFSSV", "0")
+        base = rank_windows(ctx, batch)
+        monkeypatch.delenv("MR_TR_LFSSV")
+        got = rank_windows(ctx, batch)
+        for a, b in zip(base, got):
+            assert a[5] == 0 and len(a[0]) > 0
+            assert a[2:] == b[2:] and list(a[0]) == list(b[0]) and a[1].tobytes() == b[1].tobytes()
+    d.close()
