@@ -969,6 +969,10 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
         if (!gev[(size_t)g] && hipEventCreateWithFlags(&gev[(size_t)g], hipEventDisableTiming) != hipSuccess) return MR_ERR_HIP;
         return hipEventRecord(gev[(size_t)g], pr_ctx(g)->stream) == hipSuccess ? MR_OK : MR_ERR_HIP;
     };
+    // (early spectra: their slots' read-back is queued behind them too, before the words are read;
+    // a rerun's spectra clear this and the read-back is queued again at the end)
+    const size_t slot_bytes = (size_t)n_windows * MR_WS_SLOT;
+    bool slots_queued = false;
     // spectrum tasks of up to MR_WS_BATCH ranked windows of group g: task ~i = list spec[i]
     auto queue_spectra = [&](int g) {   // (under mu)
         const int32_t i0 = gbeg[(size_t)g], i1 = gbeg[(size_t)g + 1];
@@ -1005,6 +1009,7 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
         }
         std::lock_guard<std::mutex> lk(mu);
         if (r == MR_OK && (!early || reran)) queue_spectra(g);
+        if (reran) slots_queued = false;
         cv_task.notify_all();
         return r;
     };
@@ -1047,10 +1052,12 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
                 rc = mr_pagerank_batch(pc, gs.data(), anom.data(), (int)gs.size(), 0.85, 0.01, 25, precision, 0);
             else
                 rc = mr_pagerank_batch_async(pc, gs.data(), anom.data(), (int)gs.size(), 0.85, 0.01, 25, precision,
-                                             ctx->pin_flags + (size_t)8 * i0, &pend[(size_t)g]);
+                                             ctx->pin_flags + (size_t)8 * i0, &pend[(size_t)g], spec_early);
             if (rc != MR_OK && pc != ctx) ctx->err = pc->err;
         }
-        if (rc == MR_OK) rc = record(g);
+        // (early spectra: they follow on this stream, so no event between them and the iterations;
+        // the error words' copy and its event go in behind them)
+        if (rc == MR_OK && !spec_early) rc = record(g);
         if (rc == MR_OK && spec_early) {
             {
                 std::lock_guard<std::mutex> lk(mu);
@@ -1065,6 +1072,13 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
                     q.pop_front();
                 }
                 do_task(task, ctx, 0);
+            }
+            if (pend[(size_t)g]) rc = mr_pagerank_async_commit(pc, pend[(size_t)g]);
+            if (rc == MR_OK && slot_bytes <= MR_PIN_BYTES) {
+                if (!ctx->pin && hipHostMalloc((void**)&ctx->pin, MR_PIN_BYTES, hipHostMallocDefault) != hipSuccess)
+                    ctx->pin = nullptr;
+                slots_queued = ctx->pin && hipMemcpyAsync(ctx->pin, slots.p, slot_bytes, hipMemcpyDeviceToHost,
+                                                          ctx->stream) == hipSuccess;
             }
         }
         // the previous group's words are in by now, or nearly: settle it (this one stays in flight)
@@ -1097,9 +1111,8 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
     for (int k = 0; k < nthr; ++k) (void)hipStreamSynchronize(ctx->aux[(size_t)k]->stream);
     // every device-slot spectrum in one read-back: queued on this stream into the pinned buffer
     // when it fits (one window: ~30 us less than a synchronous pageable copy after the drain)
-    const size_t slot_bytes = (size_t)n_windows * MR_WS_SLOT;
-    bool slots_pinned = false;
-    if (rc == MR_OK && slot_bytes <= MR_PIN_BYTES) {
+    bool slots_pinned = slots_queued && rc == MR_OK;
+    if (rc == MR_OK && !slots_pinned && slot_bytes <= MR_PIN_BYTES) {
         if (!ctx->pin && hipHostMalloc((void**)&ctx->pin, MR_PIN_BYTES, hipHostMallocDefault) != hipSuccess) ctx->pin = nullptr;
         slots_pinned = ctx->pin && hipMemcpyAsync(ctx->pin, slots.p, slot_bytes, hipMemcpyDeviceToHost, ctx->stream) == hipSuccess;
     }

@@ -484,10 +484,13 @@ int mr_ix_launch2(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d_state, mr_gr
 // A PageRank batch enqueued without its closing read-back (mr_windows_batch keeps one group of
 // windows in flight while it enqueues the next): its kernels' descriptors and error words stay
 // alive in the handle; finish waits for it and reports a kind-hash collision (rerun with the
-// synchronous batch) or an error.  hflag: 4 * ng pinned words.
+// synchronous batch) or an error.  hflag: 4 * ng pinned words.  defer: the error words' copy and
+// the finish's event are left for mr_pagerank_async_commit (the caller enqueues work that needs no
+// words first -- a single window's spectrum -- so no event sits between it and the iterations)
 struct PrAsync;
 int mr_pagerank_batch_async(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly, int ng, double d, double alpha,
-                            int iters, int precision, int32_t* hflag, PrAsync** out);
+                            int iters, int precision, int32_t* hflag, PrAsync** out, bool defer = false);
+int mr_pagerank_async_commit(mr_ctx* ctx, PrAsync* a);
 int mr_pagerank_async_finish(mr_ctx* ctx, PrAsync* a, bool* rerun);
 void mr_pagerank_async_free(PrAsync* a);
 int mr_ix_launch2_batch(mr_ctx* ctx, int n, const mr_spans* const* sps, uint8_t* const* d_states, mr_graph* const* g0s,

@@ -4313,6 +4313,7 @@ struct PrAsync {   // (mr_internal.h) what an enqueued batch's kernels still rea
     int32_t* hflag = nullptr;   // pinned, 4 per graph
     std::vector<int> anomaly;
     int ng = 0;
+    bool defer = false;         // the words' copy waits for mr_pagerank_async_commit
     ~PrAsync() {
         if (ev) (void)hipEventDestroy(ev);
     }
@@ -4687,9 +4688,6 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         MR_TRY_HIP(ctx, hipMemcpyAsync(fl.p, gs[0]->flag.p, 4 * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
     }
     if (as) {   // enqueued only: the words go to the caller's pinned slot, the finish reads them
-        MR_TRY_HIP(ctx, hipMemcpyAsync(as->hflag, fl.p, (size_t)4 * ng * sizeof(int32_t), hipMemcpyDeviceToHost, st));
-        if (!as->ev) MR_TRY_HIP(ctx, hipEventCreateWithFlags(&as->ev, hipEventDisableTiming));
-        MR_TRY_HIP(ctx, hipEventRecord(as->ev, st));
         as->setup_h = std::move(setup_h);
         as->setup_d.swap(setup_d);
         as->hv = std::move(hv);
@@ -4697,7 +4695,7 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         as->fl.swap(fl);
         as->anomaly.assign(anomaly, anomaly + ng);
         as->ng = ng;
-        return MR_OK;
+        return as->defer ? MR_OK : mr_pagerank_async_commit(ctx, as);
     }
     // the only host round trip of the call: error words raised by the kernels (one pinned read)
     std::vector<int32_t> hflag((size_t)4 * ng, 0);
@@ -5094,10 +5092,18 @@ extern "C" int mr_pagerank_ex(mr_ctx* ctx, mr_graph* g, int anomaly, double d, d
     return rc;
 }
 
+int mr_pagerank_async_commit(mr_ctx* ctx, PrAsync* a) {
+    MR_TRY_HIP(ctx, hipMemcpyAsync(a->hflag, a->fl.p, (size_t)4 * a->ng * sizeof(int32_t), hipMemcpyDeviceToHost,
+                                   ctx->stream));
+    if (!a->ev) MR_TRY_HIP(ctx, hipEventCreateWithFlags(&a->ev, hipEventDisableTiming));
+    MR_TRY_HIP(ctx, hipEventRecord(a->ev, ctx->stream));
+    return MR_OK;
+}
 int mr_pagerank_batch_async(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly, int ng, double d, double alpha,
-                            int iters, int precision, int32_t* hflag, PrAsync** out) {
+                            int iters, int precision, int32_t* hflag, PrAsync** out, bool defer) {
     std::unique_ptr<PrAsync> a(new PrAsync());
     a->hflag = hflag;
+    a->defer = defer;
     bool collided = false;
     MR_TRY(pagerank_attempt(ctx, gs, anomaly, ng, d, alpha, iters, precision, 0, false, kind_seed(0), kind_hmask(0),
                             &collided, a.get()));
