@@ -145,10 +145,28 @@ def add_copy_frac(out, ctx):
         return
     r = out["roofline"]
     r["copy_peak"] = round(cp, 1)
-    for d in [r] + [r[k] for k in ("u16_ids", "isolated") if isinstance(r.get(k), dict)] + \
+    for d in [r] + [r[k] for k in ("u16_ids", "pmc_bytes", "isolated", "run_merged") if isinstance(r.get(k), dict)] + \
              ([out["window_roofline"]] if isinstance(out.get("window_roofline"), dict) else []):
         if isinstance(d.get("achieved"), (int, float)) and cp > 0:
             d["frac_vs_copy"] = round(d["achieved"] / cp, 4)
+    if isinstance(r.get("fracs"), dict) and cp > 0:
+        r["fracs"]["copy_peak_frac_of_spec"] = round(cp / HBM_PEAK_GBS, 4)
+
+
+def add_pmc_frac(out, traffic):
+    """roofline.pmc_bytes: the same launches on the HBM bytes the PMC counters saw (traffic per
+    iteration over the live per-iteration time), and roofline.fracs: the three fractions side by
+    side -- SURVEY 8(d) bytes (4-B op ids), the bytes the walk reads (2-B ids), PMC bytes."""
+    r = out["roofline"]
+    avg_us = r.get("avg_launch_us") or 0.0
+    if traffic is not None and avg_us > 0:
+        pb = traffic["fetch"] + traffic["write"]
+        r["pmc_bytes"] = {"bytes_per_launch": round(pb), "achieved": round(pb / (avg_us * 1e-6) / 1e9, 1),
+                          "frac": round(pb / (avg_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                          "what": "rocprofv3 FETCH_SIZE (x2) + WRITE_SIZE per iteration / the live iteration time"}
+    r["fracs"] = {"survey_bytes": r.get("frac"),
+                  "u16_bytes": r["u16_ids"]["frac"] if isinstance(r.get("u16_ids"), dict) else None,
+                  "pmc_bytes": r["pmc_bytes"]["frac"] if isinstance(r.get("pmc_bytes"), dict) else None}
 
 
 def kind_compressed_probe(ctx, dev, t0, t1, a3, ok, reps=5):
@@ -520,6 +538,44 @@ def c4_leg_run(hg, world, rank, dist, steps=10, warmup=2):
             "what": "iteration_us_max_rank: the slowest rank's HIP-event time of one iteration's launches (walk, "
                     "column sums, all-reduce, finish); iteration_frac: SURVEY B_iter of the whole graph / that "
                     "time / (N x 8 TB/s)"}
+
+
+def run_merged_leg(out, run_all, ctx, lib, steps, nnz_w):
+    """The run-merged walk (MR_TR_MERGE=1, read per call): runs of identical traces -- adjacent
+    positions of one kind class in the layout -- share one id rotation and k_tr_a walks each run
+    by its head (the run's adds as one integer add of r x X, the tails' r' by shuffle; bitwise the
+    per-trace walk).  That is SURVEY 8(f)4's kind compression inside the walk, so it is reported
+    here, under its own keys, and never in `value` / `roofline.frac`: the same windows, steps of
+    the same shape, this rank only."""
+    import ctypes as C
+
+    os.environ["MR_TR_MERGE"] = "1"
+    try:
+        run_all(1)   # (warm-up: the windows' graphs re-prepared with run rotations)
+        ctx.sync()
+        lib.mr_ctx_profile(ctx.h, 1)
+        ts = time.perf_counter()
+        edges, n_win, _ = run_all(steps)
+        ctx.sync()
+        el = time.perf_counter() - ts
+        launches, kms, kbytes = C.c_int64(), C.c_double(), C.c_double()
+        lib.mr_ctx_prof_read(ctx.h, C.byref(launches), C.byref(kms), C.byref(kbytes))
+        lib.mr_ctx_profile(ctx.h, 0)
+    finally:
+        os.environ.pop("MR_TR_MERGE", None)
+    avg_ms = kms.value / max(launches.value, 1)
+    bpl = kbytes.value / max(launches.value, 1)
+    ach = bpl / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+    b16 = bpl - 2.0 * nnz_w * n_win * 25.0 / max(launches.value, 1)
+    out["value_run_merged"] = round(edges / el / 1e9, 3)
+    out["windows_per_s_run_merged"] = round(n_win / el, 3)
+    out["roofline"]["run_merged"] = {
+        "achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4),
+        "u16_frac": round(b16 / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if avg_ms > 0 else None,
+        "avg_launch_us": round(avg_ms * 1e3, 3), "launches": launches.value, "ms_per_step": round(el / steps * 1e3, 3),
+        "what": f"MR_TR_MERGE=1, {steps} steps of the same windows: a run of identical traces walked by its head "
+                "(kind compression inside the walk, SURVEY 8(f)4) -- the bytes and edges are still counted per "
+                "trace, so these fractions credit avoided work; value_run_merged is its GTEPS"}
 
 
 def isolated_group_roofline(ctx, group, prec, reps=3):
@@ -1052,6 +1108,8 @@ def main():
             out["roofline"]["traffic_detail"] = {
                 "fetch_bytes": round(traffic["fetch"]), "write_bytes": round(traffic["write"]),
                 "source": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950) / WRITE_SIZE, per iteration (A + B launches)"}
+        if out is not None:
+            add_pmc_frac(out, traffic)
         if out is not None and not args.pmc_child:
             emit(out)
         if dist is not None:
@@ -1279,6 +1337,7 @@ def main():
         out["roofline"]["u16_ids"] = {"bytes_per_launch": round(b16), "achieved": round(b16 / (avg_ms * 1e-3) / 1e9, 1),
                                       "frac": round(b16 / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                                       "what": "B_iter with 2 B per (trace, op) pair: k_tr_a reads u16 op ids"}
+    add_pmc_frac(out, traffic)
     if args.no_side:
         add_copy_frac(out, ctx)
         emit(out)
@@ -1286,6 +1345,11 @@ def main():
             dist.barrier()
             dist.destroy_process_group()
         return
+    if batch:
+        try:   # kind compression inside the walk: its own leg, never the headline
+            run_merged_leg(out, run_all, ctx, load, min(args.steps, 5), nnz_w)
+        except Exception as e:  # a side metric never sinks the line
+            out["roofline"]["run_merged"] = {"error": f"{type(e).__name__}: {e}"}
     if batch and args.config == "c2" and len(wins[0]) >= 128:
         try:   # the same iteration kernel with nothing beside it: ONE 128-window group per call
             out["roofline"]["isolated"] = isolated_group_roofline(ctx, wins[0][:128], prec)

@@ -68,10 +68,10 @@ void*       mr_ctx_stream(mr_ctx* ctx);
 int         mr_ctx_profile(mr_ctx* ctx, int enable);
 int         mr_ctx_prof_read(mr_ctx* ctx, int64_t* launches, double* total_ms, double* total_bytes);
 /* the device's measured copy peak (the HBM roofline is also reported against a
- * measured STREAM-copy rate beside the 8 TB/s spec): a 16-B-per-lane copy kernel (plain and
- * non-temporal launches alternating) over two
- * buffers of `bytes` each on the context stream, one warm-up and `reps` timed launches; *gbs =
- * the best launch's (read + written) bytes / time in GB/s.  No reference counterpart (measurement) */
+ * measured STREAM-copy rate beside the 8 TB/s spec): 16-B-per-lane copy kernels (grid-stride
+ * and block-tile shapes, plain and non-temporal) over two buffers of `bytes` each on the context
+ * stream, per shape one warm-up and `reps` timed launches; *gbs = the best launch's (read +
+ * written) bytes / time in GB/s.  No reference counterpart (measurement) */
 int         mr_copy_peak(mr_ctx* ctx, int64_t bytes, int reps, double* gbs);
 
 /* ------------------------------------------------------------------ graph from index arrays

@@ -270,6 +270,9 @@ static int peer_ensure(mr_ctx* ctx, int64_t words, int64_t xa = 0, int64_t xb = 
     // (a first region already holds any fused graph's all-reduce: 2 x 16384 limbs + the r' slots)
     words = std::max<int64_t>(words, 2 * 16384 + PEER_MAXR + 1);
     peer_retire(ctx);
+    // the retired-region cap reached (peer_retire turned the path off, the same count on every
+    // rank): no fresh region -- the callers fall back to RCCL / the host collective on this code
+    if (!ctx->peer_on) return mr_fail(ctx, MR_ERR_STATE, "peer collectives: retired-region cap reached");
     const size_t bytes = ((size_t)PEER_FLAGS + 2 * (size_t)R * (size_t)words + (size_t)xa + (size_t)xb +
                           (size_t)R * (size_t)nbf) * sizeof(unsigned long long);
     // (the region allocation and the mappings fail locally without returning alone: they are agreed

@@ -268,27 +268,49 @@ extern "C" void mr_ctx_destroy(mr_ctx* ctx) {
 extern "C" const char* mr_last_error(const mr_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
 
 // ---------------------------------------------------------------- measured copy peak
-// STREAM copy: every lane moves 4 x 16 B per round (all loads in flight before the stores),
-// grid-stride over the buffer; NT: non-temporal loads and stores (no L2 allocation)
+// STREAM copy, 16 B per lane per access, in two shapes: grid-stride (every lane moves 4 x 16 B
+// per round, all loads in flight before the stores) and block tiles (a block copies U x 4 KB of
+// consecutive lines once, every load in flight before the stores: the float4-copy shape of
+// MI355X_MICROARCH.md's 6.29 TB/s row).  NT: non-temporal loads and stores (no L2 allocation).
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+template <bool NT>
+__device__ __forceinline__ u32x4 cp_ld(const u32x4* p) { return NT ? __builtin_nontemporal_load(p) : *p; }
+template <bool NT>
+__device__ __forceinline__ void cp_st(u32x4* p, u32x4 v) {
+    if (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
 template <bool NT>
 __global__ void __launch_bounds__(256) k_copy16(const u32x4* __restrict__ src, u32x4* __restrict__ dst, int64_t n) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    auto ld = [&](int64_t k) -> u32x4 { return NT ? __builtin_nontemporal_load(src + k) : src[k]; };
-    auto st = [&](int64_t k, u32x4 v) {
-        if (NT) __builtin_nontemporal_store(v, dst + k);
-        else dst[k] = v;
-    };
     for (; i + 3 * stride < n; i += 4 * stride) {
-        const u32x4 a = ld(i), b = ld(i + stride), c = ld(i + 2 * stride), d = ld(i + 3 * stride);
-        st(i, a);
-        st(i + stride, b);
-        st(i + 2 * stride, c);
-        st(i + 3 * stride, d);
+        const u32x4 a = cp_ld<NT>(src + i), b = cp_ld<NT>(src + i + stride), c = cp_ld<NT>(src + i + 2 * stride),
+                    d = cp_ld<NT>(src + i + 3 * stride);
+        cp_st<NT>(dst + i, a);
+        cp_st<NT>(dst + i + stride, b);
+        cp_st<NT>(dst + i + 2 * stride, c);
+        cp_st<NT>(dst + i + 3 * stride, d);
     }
-    for (; i < n; i += stride) st(i, ld(i));
+    for (; i < n; i += stride) cp_st<NT>(dst + i, cp_ld<NT>(src + i));
 }
+template <int U, bool NT>
+__global__ void __launch_bounds__(256) k_copy_tile(const u32x4* __restrict__ src, u32x4* __restrict__ dst, int64_t n) {
+    const int64_t base = (int64_t)blockIdx.x * (256 * U) + threadIdx.x;
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int64_t k = base + (int64_t)u * 256;
+        v[u] = cp_ld<NT>(src + (k < n ? k : n - 1));
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int64_t k = base + (int64_t)u * 256;
+        if (k < n) cp_st<NT>(dst + k, v[u]);
+    }
+}
+// The best rate of `reps` timed launches of each shape (after one untimed warm-up launch of each):
+// bytes read + written / launch time.
 extern "C" int mr_copy_peak(mr_ctx* ctx, int64_t bytes, int reps, double* gbs) {
     if (!ctx || bytes < 16 || reps < 1 || !gbs) return mr_fail(ctx, MR_ERR_ARG, "mr_copy_peak: bad arguments");
     MR_TRY_HIP(ctx, hipSetDevice(ctx->device));
@@ -300,22 +322,38 @@ extern "C" int mr_copy_peak(mr_ctx* ctx, int64_t bytes, int reps, double* gbs) {
     int dev = 0, cus = 256;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const int blocks = (int)std::min<int64_t>((int64_t)cus * 16, (n + 255) / 256);
-    hipEvent_t e0, e1;
+    const unsigned gs_blocks = (unsigned)std::min<int64_t>((int64_t)cus * 16, (n + 255) / 256);
+    auto launch = [&](int shape) {
+        hipStream_t st = ctx->stream;
+        switch (shape) {
+            case 0: hipLaunchKernelGGL(k_copy16<false>, dim3(gs_blocks), dim3(256), 0, st, a.p, b.p, n); break;
+            case 1: hipLaunchKernelGGL(k_copy16<true>, dim3(gs_blocks), dim3(256), 0, st, a.p, b.p, n); break;
+            case 2: hipLaunchKernelGGL((k_copy_tile<4, false>), dim3((unsigned)((n + 1023) / 1024)), dim3(256), 0, st, a.p, b.p, n); break;
+            case 3: hipLaunchKernelGGL((k_copy_tile<4, true>), dim3((unsigned)((n + 1023) / 1024)), dim3(256), 0, st, a.p, b.p, n); break;
+            case 4: hipLaunchKernelGGL((k_copy_tile<8, false>), dim3((unsigned)((n + 2047) / 2048)), dim3(256), 0, st, a.p, b.p, n); break;
+            default: hipLaunchKernelGGL((k_copy_tile<1, false>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a.p, b.p, n); break;
+        }
+    };
+    hipEvent_t e0 = nullptr, e1 = nullptr;
     MR_TRY_HIP(ctx, hipEventCreate(&e0));
-    MR_TRY_HIP(ctx, hipEventCreate(&e1));
+    if (hipEventCreate(&e1) != hipSuccess) {
+        (void)hipGetLastError();
+        (void)hipEventDestroy(e0);
+        return mr_fail(ctx, MR_ERR_HIP, "mr_copy_peak: hipEventCreate failed");
+    }
     double best = 0.0;
     int rc = MR_OK;
-    for (int r = -2; r < 2 * reps && rc == MR_OK; ++r) {   // plain and non-temporal launches alternate
-        (void)hipEventRecord(e0, ctx->stream);
-        if (r & 1) hipLaunchKernelGGL(k_copy16<true>, dim3(blocks), dim3(256), 0, ctx->stream, a.p, b.p, n);
-        else hipLaunchKernelGGL(k_copy16<false>, dim3(blocks), dim3(256), 0, ctx->stream, a.p, b.p, n);
-        (void)hipEventRecord(e1, ctx->stream);
-        if (hipEventSynchronize(e1) != hipSuccess) rc = mr_fail(ctx, MR_ERR_HIP, "mr_copy_peak: launch failed");
-        float ms = 0.0f;
-        if (rc == MR_OK && r >= 0 && hipEventElapsedTime(&ms, e0, e1) == hipSuccess && ms > 0.0f)
-            best = std::max(best, 2.0 * (double)n * 16.0 / (ms * 1e-3) / 1e9);
-    }
+    for (int shape = 0; shape < 6 && rc == MR_OK; ++shape)
+        for (int r = -1; r < reps && rc == MR_OK; ++r) {   // r = -1: the shape's warm-up launch
+            (void)hipEventRecord(e0, ctx->stream);
+            launch(shape);
+            (void)hipEventRecord(e1, ctx->stream);
+            if (hipEventSynchronize(e1) != hipSuccess || hipGetLastError() != hipSuccess)
+                rc = mr_fail(ctx, MR_ERR_HIP, "mr_copy_peak: launch failed");
+            float ms = 0.0f;
+            if (rc == MR_OK && r >= 0 && hipEventElapsedTime(&ms, e0, e1) == hipSuccess && ms > 0.0f)
+                best = std::max(best, 2.0 * (double)n * 16.0 / (ms * 1e-3) / 1e9);
+        }
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     MR_TRY(rc);

@@ -935,7 +935,11 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
     std::vector<mr_graph*> dead;
     dead.swap(ctx->graveyard);
     std::thread reaper;
-    if (inl && dead.size() <= 64) {   // (a few graphs: here, before this call's work)
+    // (a few graphs: here, on the calling thread.  The inline chunk's build is already enqueued
+    // above, so this runs after it was issued, not before; it is safe because the previous call
+    // drained these graphs' streams before it returned, and the blocks go back to stream-ordered
+    // pools)
+    if (inl && dead.size() <= 64) {
         for (mr_graph* g : dead) delete g;
         dead.clear();
     } else {

@@ -321,6 +321,8 @@ struct mr_graph {
     // [T] by position: the length of the run of identical traces (one kind class, adjacent in a
     // wave tile) a position heads, 0 for the run's other positions (k_tr_a's walk merges the run)
     DBuf<uint8_t> trun;
+    int lo_merged = 0;           // MR_TR_MERGE at prepare: 1 runs share a rotation and k_tr_a walks
+                                 // each by its head (trun); 2 the rotations only (tests); 0 neither
     int32_t lo_nbp = 0;          // preference partial blocks
 };
 

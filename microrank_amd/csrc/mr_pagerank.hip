@@ -1520,7 +1520,7 @@ __global__ void k_pref_apply_b(const SDev* __restrict__ sd, int32_t ng) {
 // k_graph_consts .. k_tr_fill and k_reset_init .. k_pref_apply for these graphs, in four launches.
 constexpr int LO_NOC_MAX = 4096;   // (mr_lo_fits: tables of <= NS_PMAX pod-ops)
 struct LDev {
-    int32_t T, N, W, anomaly, fp32, rot, NP;
+    int32_t T, N, W, anomaly, fp32, NP;
     int32_t b_cs, n_cs, b_fill, nbp, b_app;   // first block in each launch; partial blocks
     int64_t st_off;
     float cd;
@@ -1576,9 +1576,11 @@ __global__ void __launch_bounds__(256) k_lo_fill_b(const LDev* __restrict__ ld, 
     if (i < (int64_t)G.W * WAVE) {   // (uniform per wave: a wave is one tile)
         const int32_t k = (int32_t)(i / WAVE), lane = (int32_t)(i % WAVE);
         int64_t e0 = 0, len = 0, rot = 0;
-        // runs of identical traces: adjacent positions of one kind class (the layout keeps a class
-        // contiguous); a run shares its head's rotation, so its members walk the same ids in the same
-        // order and k_tr_a lets the head walk for the run
+        // every trace rotated by its own layout index mod length.  Run-merged graphs (MR_TR_MERGE=1,
+        // trun set; kind compression inside the walk, SURVEY 8(f)4 -- never the headline): runs of
+        // identical traces (adjacent positions of one kind class: the layout keeps a class
+        // contiguous) share their head's rotation instead, so its members walk the same ids in the
+        // same order and k_tr_a lets the head walk for the run
         const int32_t ix = i < T ? G.pinv[i] : -1;
         const int32_t kid = i < T ? G.lo_kid[ix] : -1;
         const int32_t kp = __shfl_up(kid, 1, WAVE);
@@ -1589,7 +1591,7 @@ __global__ void __launch_bounds__(256) k_lo_fill_b(const LDev* __restrict__ ld, 
         // only a tile of the 512-thread walk's short tiers merges (the general loop walks every
         // lane): there its runs share the head's rotation and are marked; a longer tile keeps one
         // rotation per trace (a shared rotation there would put a run's adds on one word at a time)
-        const bool mt = G.c64[k + 1] - G.c64[k] <= MR_TR_TIERS512;
+        const bool mt = G.trun && G.c64[k + 1] - G.c64[k] <= MR_TR_TIERS512;
         if (i < T && G.trun) {
             const unsigned long long above = lane == WAVE - 1 ? 0ull : hm & (~0ull << (lane + 1));
             G.trun[i] = !mt ? (uint8_t)1 : hd ? (uint8_t)((above ? __builtin_ctzll(above) : WAVE) - lane) : (uint8_t)0;
@@ -1597,7 +1599,7 @@ __global__ void __launch_bounds__(256) k_lo_fill_b(const LDev* __restrict__ ld, 
         if (i < T) {
             e0 = G.lo_off[ix];
             len = G.lo_off[ix + 1] - e0;
-            rot = len && G.rot ? (int64_t)((uint32_t)(mt ? ixh : ix) % (uint32_t)len) : 0;
+            rot = len ? (int64_t)((uint32_t)(mt ? ixh : ix) % (uint32_t)len) : 0;
             const int32_t L = G.lo_len[ix];
             const uint32_t kc = G.kcnt[G.lo_kid[ix]];
             G.w_tp[i] = L > 0 ? (float)(1.0 / (double)L) : 0.0f;
@@ -2024,7 +2026,6 @@ __device__ __forceinline__ int32_t fx_graph(const GDev* gs, int32_t ng, int32_t 
 
 // ---------------------------------------------------------------- fused iteration: LDS budget and su modes
 constexpr size_t WV_LDS_MAX = 160 * 1024 - 512;
-constexpr int LO_ROT_DEFAULT = 1;  // (mr_lo_prepare_batch)
 // su modes of k_tr_a: global gathers only / every op's su in LDS / the n_hot most covered ops' su in
 // LDS (relabelled graphs, ops [0, n_hot)), the rest gathered
 enum { WV_SU_GLOBAL = 0, WV_SU_ALL = 1, WV_SU_HOT = 2 };
@@ -2497,12 +2498,15 @@ __device__ __forceinline__ void tr_ssv_share(const GDev& G, int32_t lb, int cur,
 
 // The last k_tr_a block of a graph finishes the iteration itself (small graphs: window batches),
 // so an iteration is ONE launch instead of k_tr_a + k_fx_b.  Every block writes its partial row
-// write-through (sc1), waits for its stores, and takes a ticket from the graph's counter (an
-// agent-scope add, returned); the block whose ticket completes the iteration's count reads every
-// row with sc1 loads (MI355X_MICROARCH.md hand-off table, row 1: the last adder, told by the value
-// its add returned) and does k_fx_b's work for every op -- the same exact limb sums, the same
+// and its call-graph terms write-through (sc1), every wave waits for its stores (vmcnt(0)), and
+// behind a workgroup barrier one lane takes a ticket from the graph's counter (an agent-scope add,
+// returned); the block whose ticket completes the iteration's count is the consumer.  The launch
+// runs several workgroups per CU, so the hand-off table's sc1-only rows (MI355X_MICROARCH.md:
+// "hipMalloc; one per CU") do not apply: the consumer takes the guide's general form -- ONE agent
+// acquire on the adding lane, its own vmcnt(0) wait, a workgroup barrier, then the loads (kept sc1)
+// -- and reads every row and does k_fx_b's work for every op: the same exact limb sums, the same
 // call-graph term (a lane per op of <= 8 parents, a wave per op of more: wave_sum's butterfly) and
-// the same finish: bitwise k_fx_b's results.
+// the same finish: bitwise k_fx_b's results.  Only the finishing block pays the acquire.
 template <int NT>
 __device__ __forceinline__ void tr_last_finish(const GDev& G, int it, double d, double Ms,
                                             GLB unsigned long long* Mnext) {
@@ -2514,7 +2518,12 @@ __device__ __forceinline__ void tr_last_finish(const GDev& G, int it, double d, 
     if (tid == 0) {
         const unsigned long long t = __hip_atomic_fetch_add(gpw(G.mslot) + 6 * MSH + 1, 1ull, __ATOMIC_RELAXED,
                                                             __HIP_MEMORY_SCOPE_AGENT);
-        s_last = t + 1 == (unsigned long long)G.n_fa * (unsigned long long)(it + 1);
+        const bool last = t + 1 == (unsigned long long)G.n_fa * (unsigned long long)(it + 1);
+        if (last) {   // consumer: agent acquire (this CU's L1 invalidated), waited before the barrier
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        s_last = last;
     }
     __syncthreads();
     if (!s_last) return;
@@ -4314,6 +4323,7 @@ struct PrAsync {   // (mr_internal.h) what an enqueued batch's kernels still rea
     std::vector<int> anomaly;
     int ng = 0;
     bool defer = false;         // the words' copy waits for mr_pagerank_async_commit
+    bool committed = false;     // the words' copy and the event are enqueued
     ~PrAsync() {
         if (ev) (void)hipEventDestroy(ev);
     }
@@ -4411,8 +4421,6 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
     // vs 44.6 us per iteration, C4 whole: within noise (two repeats each)
     const char* rwe = getenv("MR_TR_ROW_WT");
     const bool row_wt_on = !(rwe && atoi(rwe) == 0);
-    const char* mge = getenv("MR_TR_MERGE");   // (A/B and tests, read per call) 0: every lane walks its own trace
-    const bool merge_on = !(mge && atoi(mge) == 0);
     double bytes = 0.0;
     for (int i = 0; i < ng; ++i) {
         mr_graph* g = gs[i];
@@ -4430,7 +4438,7 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         v.w_tp = g->w_tp.p;
         v.mw_tp = g->mw_tp.p;
         v.hmask = g->nhr ? g->hmask.p : nullptr;
-        v.trun = g->lo && merge_on ? g->trun.p : nullptr;
+        v.trun = g->lo && g->lo_merged == 1 ? g->trun.p : nullptr;   // (set at prepare: the ids' rotation follows it)
         v.ctids = g->wide ? g->ctids.p : nullptr;
         v.ccoff = g->wide ? g->ccoff.p : nullptr;
         v.nhr = g->fused ? g->nhr : 0;
@@ -4853,11 +4861,14 @@ int mr_lo_prepare_batch(mr_ctx* ctx, mr_graph* const* gs, const mr_spans* const*
     if (n <= 0) return MR_OK;
     const bool fp32 = precision == MR_FP32;
     hipStream_t st = ctx->stream;
-    // a trace's ids rotated by its run head's layout index mod length (spreads a shared first op
-    // over a tile's id chunks; a run of identical traces keeps one order, k_lo_fill_b) or kept in the
-    // layout's order (MR_LO_ROT=0; read per call)
-    const char* re = getenv("MR_LO_ROT");
-    const int lo_rot = re ? (atoi(re) != 0) : LO_ROT_DEFAULT;
+    // a trace's ids rotated by its layout index mod length (spreads a shared first op over a tile's
+    // id chunks, k_lo_fill_b).  MR_TR_MERGE=1 (read per call; the bench's run-merged side leg and
+    // tests): runs of identical traces share their head's rotation and k_tr_a walks each run by its
+    // head -- kind compression inside the walk, so never the default: the headline
+    // walks every trace.  MR_TR_MERGE=2 (tests): the run rotations without the merged walk, so every
+    // lane walks its own trace in its run head's order -- bitwise the merged walk
+    const char* mge = getenv("MR_TR_MERGE");
+    const int merge = mge ? std::min(std::max(atoi(mge), 0), 2) : 0;
     keep.assign((size_t)n * sizeof(LDev), 0);
     LDev* hv = reinterpret_cast<LDev*>(keep.data());
     std::vector<DBuf<int64_t>> c64((size_t)n);
@@ -4895,7 +4906,8 @@ int mr_lo_prepare_batch(mr_ctx* ctx, mr_graph* const* gs, const mr_spans* const*
         MR_TRY(g->w_tp.alloc(ctx, (size_t)T));
         MR_TRY(g->kind.alloc(ctx, (size_t)T));
         MR_TRY(g->lo_lenp.alloc(ctx, (size_t)T));
-        MR_TRY(g->trun.alloc(ctx, (size_t)T));
+        g->lo_merged = merge;
+        if (merge) MR_TRY(g->trun.alloc(ctx, (size_t)T));
         MR_TRY(g->ppart.alloc(ctx, 2 * (size_t)g->lo_nbp));
         MR_TRY(g->coff.alloc(ctx, (size_t)W + 1));
         MR_TRY(c64[(size_t)i].alloc(ctx, (size_t)W + 1));
@@ -4904,7 +4916,6 @@ int mr_lo_prepare_batch(mr_ctx* ctx, mr_graph* const* gs, const mr_spans* const*
         LDev& v = hv[i];
         MR_TRY(lo_state(ctx, g, anomaly[i], d, fp32, v));
         v.W = W;
-        v.rot = lo_rot;
         v.NP = sp->n_podops;
         v.n_cs = (int32_t)std::max<int64_t>(cdiv((int64_t)W, TS_TILE), 1);
         v.st_off = st_words;
@@ -4925,7 +4936,7 @@ int mr_lo_prepare_batch(mr_ctx* ctx, mr_graph* const* gs, const mr_spans* const*
         v.c64 = c64[(size_t)i].p;
         v.coff = g->coff.p;
         v.tids = g->tids.p;
-        v.trun = g->trun.p;
+        v.trun = merge ? g->trun.p : nullptr;
         lo_mark_presetup(g, anomaly[i], d, fp32);
     }
     DBuf<LDev> dl;
@@ -5097,6 +5108,7 @@ int mr_pagerank_async_commit(mr_ctx* ctx, PrAsync* a) {
                                    ctx->stream));
     if (!a->ev) MR_TRY_HIP(ctx, hipEventCreateWithFlags(&a->ev, hipEventDisableTiming));
     MR_TRY_HIP(ctx, hipEventRecord(a->ev, ctx->stream));
+    a->committed = true;
     return MR_OK;
 }
 int mr_pagerank_batch_async(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly, int ng, double d, double alpha,
@@ -5112,6 +5124,7 @@ int mr_pagerank_batch_async(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
 }
 int mr_pagerank_async_finish(mr_ctx* ctx, PrAsync* a, bool* rerun) {
     *rerun = false;
+    if (!a->committed) MR_TRY(mr_pagerank_async_commit(ctx, a));   // (a deferred batch nobody committed)
     MR_TRY_HIP(ctx, hipEventSynchronize(a->ev));
     for (int i = 0; i < a->ng; ++i) {
         const int32_t* w = a->hflag + 4 * i;

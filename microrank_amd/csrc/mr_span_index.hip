@@ -451,10 +451,14 @@ static int trace_runs(mr_ctx* ctx, const mr_spans* s, const int32_t* code, int32
 // the run's index), so a window counts a run's members with one add per wave.  A hash collision
 // that the exact comparison finds retries with the next seed; after four the table keeps the
 // general window path (lo_ok false).
-static int lo_index(mr_ctx* ctx, mr_spans* s) {
+static int lo_index_try(mr_ctx* ctx, mr_spans* s) {
     hipStream_t st = ctx->stream;
     const int32_t NT = s->n_traces;
     s->lo_ok = false;
+    if (getenv("MR_LO_TEST_FAIL")) {   // (tests, read per table: an allocation failing half-way)
+        MR_TRY(s->lo_tr.alloc(ctx, (size_t)std::max(NT, 1)));
+        return mr_fail(ctx, MR_ERR_HIP, "lo_index: forced failure (MR_LO_TEST_FAIL)");
+    }
     if (!mr_lo_fits(s) || s->n_po >= ((int64_t)1 << 31) || s->n_sv >= ((int64_t)1 << 31) ||
         s->n_ed >= ((int64_t)1 << 31))
         return MR_OK;
@@ -550,6 +554,40 @@ static int lo_index(mr_ctx* ctx, mr_spans* s) {
         return MR_OK;
     }
     return MR_OK;   // (four colliding seeds: the general window path)
+}
+static void lo_release(mr_spans* s) {
+    s->lo_ok = false;
+    s->lo_nk = 0;
+    s->lo_nblk = 0;
+    s->lo_tr.reset();
+    s->lo_len.reset();
+    s->lo_kid.reset();
+    s->lo_off.reset();
+    s->lo16.reset();
+    s->lo_cnt.reset();
+    s->lo_first.reset();
+    s->lo_ts.reset();
+    s->lo_te.reset();
+    s->lo_mx.reset();
+    s->lo_bstart.reset();
+    s->lsv_off.reset();
+    s->le_off.reset();
+    s->lsv.reset();
+    s->le.reset();
+}
+// Best effort: the layout order is a fast path of the window build.  A table it does not cover
+// (codes or counts past 16 bits, four colliding seeds) or an error on the way (an allocation, a
+// launch) leaves the table on the general window path with no lo_* buffers held; the index
+// itself stays valid and the call succeeds.
+static int lo_index(mr_ctx* ctx, mr_spans* s) {
+    const int rc = lo_index_try(ctx, s);
+    if (rc != MR_OK) {
+        (void)hipStreamSynchronize(ctx->stream);
+        (void)hipGetLastError();
+        ctx->err.clear();
+    }
+    if (rc != MR_OK || !s->lo_ok) lo_release(s);
+    return MR_OK;
 }
 
 int mr_spans_index(mr_ctx* ctx, mr_spans* s) {

@@ -879,16 +879,18 @@ def test_c2_windows_batch_groupings_agree(c2_batch, monkeypatch):
     table) rank bitwise as the default -- build-side choices, the PageRank launches untouched; and
     PageRank groups of 4 and 2 windows (MR_WIN_GROUP) give the same top lists, counts and edges,
     scores within 1e-12 (a group's block budget sets each graph's fixed-point scale, so only the
-    rounding of the exact limb sums may move).  k_tr_a without run merging (MR_TR_MERGE=0: every
-    lane walks its own trace instead of a run's head walking for its identical traces with X times
-    the run length) ranks bitwise as the default: the merge is exact."""
+    rounding of the exact limb sums may move).  The run-merged walk (MR_TR_MERGE=1: a run of
+    identical traces shares one id rotation and its head walks for it with X times the run length;
+    the bench's side leg, never the headline) ranks bitwise as every lane walking its own trace in
+    the same run rotations (MR_TR_MERGE=2): the merge is exact; against the default (a rotation per
+    trace: each trace's sum in another order) the scores agree to 1e-12."""
     from microrank_amd.online_rca import rank_windows
 
     knobs = ("MR_WIN_GROUP", "MR_WIN_CHUNK", "MR_IX_EPT", "MR_DET_FUSE_MAX", "MR_NO_DET_FUSE", "MR_TR_MERGE")
     ctx, _, wins = c2_batch
     variants = {"default": {}, "chunk1_ept16": {"MR_WIN_CHUNK": "1", "MR_IX_EPT": "16"},
                 "chunk2_fused": {"MR_WIN_CHUNK": "2", "MR_DET_FUSE_MAX": "100000000"},
-                "nomerge": {"MR_TR_MERGE": "0"},
+                "merge": {"MR_TR_MERGE": "1"}, "runrot": {"MR_TR_MERGE": "2"},
                 "group4_chunk4": {"MR_WIN_GROUP": "4", "MR_WIN_CHUNK": "4"}, "group2": {"MR_WIN_GROUP": "2"}}
     runs = {}
     for name, env in variants.items():
@@ -902,10 +904,12 @@ def test_c2_windows_batch_groupings_agree(c2_batch, monkeypatch):
         for i, (a, b) in enumerate(zip(base, got)):
             assert a[5] == b[5] == 0, (name, i)
             assert a[2:] == b[2:] and list(a[0]) == list(b[0]), (name, i)
-            if name.startswith("group"):
+            if name.startswith("group") or name in ("merge", "runrot"):
                 np.testing.assert_allclose(b[1], a[1], rtol=1e-12, atol=0, err_msg=f"{name} window {i}")
             else:
                 assert a[1].tobytes() == b[1].tobytes(), (name, i)
+    for i, (a, b) in enumerate(zip(runs["merge"], runs["runrot"])):
+        assert a[1].tobytes() == b[1].tobytes() and list(a[0]) == list(b[0]), ("merge == runrot", i)
 
 
 def test_windows_batch_layout_order_equals_general_build(c3_window, monkeypatch):
@@ -951,6 +955,32 @@ def test_windows_batch_layout_order_equals_general_build(c3_window, monkeypatch)
         assert a[2:] == b[2:] and list(a[0]) == list(b[0]) and a[1].tobytes() == b[1].tobytes()
     for d in devs:
         d.close()
+
+
+def test_layout_index_failure_keeps_general_path(c3_window, monkeypatch):
+    """The layout order is a best-effort fast path of the span index: a failure inside it
+    (MR_LO_TEST_FAIL: an error after an allocation, read per table) leaves the upload successful,
+    the context's error text clear, and the table on the general window build -- the window ranks
+    as on a table indexed with its layout (top list, counts and edges equal, scores 1e-12)."""
+    import bench
+    from microrank_amd import _lib
+    from microrank_amd.online_rca import rank_windows
+    from microrank_amd.preprocess_data import DeviceSpans
+
+    ctx = _lib.default_context()
+    normal, abnormal, t0, t1 = c3_window
+    a3, ok = bench.slo_from_gpu(ctx, normal)
+    good = DeviceSpans(ctx, abnormal)
+    monkeypatch.setenv("MR_LO_TEST_FAIL", "1")
+    bad = DeviceSpans(ctx, abnormal)
+    monkeypatch.delenv("MR_LO_TEST_FAIL")
+    assert (_lib.load().mr_last_error(ctx.h) or b"") == b""
+    a, b = rank_windows(ctx, [(good, t0, t1, a3, ok), (bad, t0, t1, a3, ok)])
+    assert a[5] == b[5] == 0
+    assert a[2:] == b[2:] and list(a[0]) == list(b[0])
+    np.testing.assert_allclose(b[1], a[1], rtol=1e-12, atol=0)
+    good.close()
+    bad.close()
 
 
 def test_windows_batch_layout_order_rerun_sets_up_again(c3_window, monkeypatch):
