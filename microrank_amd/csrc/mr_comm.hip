@@ -466,6 +466,10 @@ int mr_peer_fx_prepare(mr_ctx* ctx, int64_t words, int32_t nbf, MrPeerX* px) {
     px->seq = ctx->peer_seq;
     px->timeout = mr_peer_timeout_ticks();
     px->spin = 1;
+    // (tests, read per call) MR_PEER_TEST_MUTE=<rank>: that rank pushes its limbs but never stores
+    // its round flags -- every rank's wait then runs into the timeout (a peer that never arrives)
+    const char* me = getenv("MR_PEER_TEST_MUTE");
+    px->mute = me && atoi(me) == ctx->rank ? 1 : 0;
     return MR_OK;
 }
 void mr_peer_fx_round_done(mr_ctx* ctx, MrPeerX* px) {

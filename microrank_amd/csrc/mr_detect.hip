@@ -720,13 +720,10 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
     }
     const long long t_call = timing ? win_now() : 0;
     const int32_t K = std::max(0, top_max + 6);
-    // MR_WIN_STREAMS: auxiliary streams (and host threads) of a batch.  4 measured best (C2 2908 /
-    // C3 4850 windows/s vs 2705 / 4247 at 16): the windows' launches come from the host threads
-    // and more threads only contend for the runtime (the box runs 4 hardware queues per process)
-    static const int max_streams = [] {
-        const char* e = getenv("MR_WIN_STREAMS");
-        return e ? std::max(1, atoi(e)) : 4;
-    }();
+    // auxiliary streams (and host threads) of a batch: 4 measured best (C2 2908 / C3 4850
+    // windows/s vs 2705 / 4247 at 16): the windows' launches come from the host threads and more
+    // threads only contend for the runtime (the box runs 4 hardware queues per process)
+    constexpr int max_streams = 4;
     // Windows whose PageRanks share launches (a group): at most WIN_GROUP_TRACES traces per group,
     // 16..128 windows.  The iteration pair of a small-window group is latency-bound, so its cost per
     // window falls with the group (C3, 20k-trace windows, on one box: group 16 / 32 / 64 / 128 ->
@@ -766,9 +763,8 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
             chunks.emplace_back(i, std::min<int32_t>(e, i + chunk_size));
     // a call of one chunk (one window: the single-window latency) runs inline: its build, PageRanks
     // and spectrum on this context's stream from the calling thread -- no worker thread to start,
-    // no hand-offs between threads or streams.  MR_WIN_INLINE=0: worker threads anyway (read per call)
-    const char* ie = getenv("MR_WIN_INLINE");
-    const bool inl = chunks.size() == 1 && !(ie && atoi(ie) == 0);
+    // no hand-offs between threads or streams
+    const bool inl = chunks.size() == 1;
     const int nthr = inl ? 0 : std::min<int>((int)chunks.size(), max_streams);
     // (every group's PageRanks on this context's stream: a second PageRank stream for odd groups
     // measured within the spread, profiles/r04al/, and was removed)
@@ -826,8 +822,7 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
     if (!inl) MR_TRY_HIP(ctx, hipStreamSynchronize(ctx->stream));   // uploads done before other streams read them
     static const bool no_index = getenv("MR_NO_INDEX") != nullptr;
     const bool spec_general = getenv("MR_NO_WIN_SPECTRUM_SMALL") != nullptr;   // (read per call: tests)
-    const char* sbe = getenv("MR_WIN_SPEC_BATCH");   // windows per spectrum launch, 1..MR_WS_BATCH (A/B)
-    const int spec_batch = sbe ? std::min(MR_WS_BATCH, std::max(1, atoi(sbe))) : MR_WS_BATCH;
+    constexpr int spec_batch = MR_WS_BATCH;   // windows per spectrum launch
     ph_setup.reset();
     std::vector<WinRun> w((size_t)n_windows);
     std::vector<WinChunk> cw(chunks.size());
@@ -952,8 +947,7 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
     // while this thread waits for a group and then enqueues the next (measured: this thread had
     // spent 12 of a C2 call's 14.5 ms inside the synchronous batch).  A group's error words are
     // read one group later; only then are its spectra queued (a kind-hash collision reruns the
-    // group synchronously first).  MR_WIN_PR_SYNC=1: the synchronous batch per group.
-    const bool pr_sync = getenv("MR_WIN_PR_SYNC") != nullptr;   // (read per call)
+    // group synchronously first).
     {
         const size_t need = (size_t)8 * n_windows;   // 4 words per graph, 2 graphs per window
         if (ctx->pin_flags_n < need) {
@@ -1022,7 +1016,7 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
     // (C2 one window: a ~20 us idle gap plus the spectrum's launch).  A collision rerun overwrites
     // the slots with a second round of spectra.  MR_WIN_SPEC_EARLY=0: after the words (read per call)
     const char* see = getenv("MR_WIN_SPEC_EARLY");
-    const bool spec_early = inl && !pr_sync && !(see && atoi(see) == 0);
+    const bool spec_early = inl && !(see && atoi(see) == 0);
     int settled = 0;   // groups whose spectra are queued
     for (int g = 0; g < ngroups && rc == MR_OK; ++g) {
         const int32_t i0 = gbeg[(size_t)g], i1 = gbeg[(size_t)g + 1];
@@ -1052,11 +1046,8 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
         }
         if (!gs.empty()) {
             WinPhase ph(6);
-            if (pr_sync)
-                rc = mr_pagerank_batch(pc, gs.data(), anom.data(), (int)gs.size(), 0.85, 0.01, 25, precision, 0);
-            else
-                rc = mr_pagerank_batch_async(pc, gs.data(), anom.data(), (int)gs.size(), 0.85, 0.01, 25, precision,
-                                             ctx->pin_flags + (size_t)8 * i0, &pend[(size_t)g], spec_early);
+            rc = mr_pagerank_batch_async(pc, gs.data(), anom.data(), (int)gs.size(), 0.85, 0.01, 25, precision,
+                                         ctx->pin_flags + (size_t)8 * i0, &pend[(size_t)g], spec_early);
             if (rc != MR_OK && pc != ctx) ctx->err = pc->err;
         }
         // (early spectra: they follow on this stream, so no event between them and the iterations;
@@ -1086,7 +1077,7 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
             }
         }
         // the previous group's words are in by now, or nearly: settle it (this one stays in flight)
-        for (; rc == MR_OK && settled < (pr_sync ? g + 1 : g); ++settled) rc = settle(settled, spec_early);
+        for (; rc == MR_OK && settled < g; ++settled) rc = settle(settled, spec_early);
     }
     for (; rc == MR_OK && settled < ngroups; ++settled) rc = settle(settled, spec_early);
     while (inl && rc == MR_OK) {   // the spectra settle queued, here

@@ -1674,20 +1674,14 @@ static int ix_launch(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d_mask, mr_
                            b.dense ? (uint64_t*)nullptr : b.gk.p, b.gc.p, (int64_t)ecap);
     }
     if (NT) {
-        // more codes than one LDS histogram: op ranges of IX_HIST codes in blockIdx.y (MR_IX_RANGED=0:
-        // the global-atomic form, A/B)
-        static const bool no_ranged = getenv("MR_IX_RANGED") && atoi(getenv("MR_IX_RANGED")) == 0;
-        const int nrange = NP > IX_HIST && !no_ranged ? cdiv(NP, IX_HIST) : 1;
+        // more codes than one LDS histogram: op ranges of IX_HIST codes in blockIdx.y
+        const int nrange = NP > IX_HIST ? cdiv(NP, IX_HIST) : 1;
         const int use_lds = NP <= IX_HIST || nrange > 1;
         const int64_t NPL = std::min<int64_t>(NP, IX_HIST);
         // dense edge counts in LDS beside the pod-op histogram while both fit (else global adds)
         const int lds_ek = b.dense && (use_lds ? 3 * NPL : 0) + (int64_t)ecap <= IX_LDS_WORDS;
         const size_t lds = (use_lds ? 3 * (size_t)NPL * sizeof(int32_t) : 0) + (lds_ek ? ecap * sizeof(uint32_t) : 0);
-        // block cap 256 (one per CU); MR_IX_BLOCKS overrides it for measurements
-        static const int ix_cap = [] {
-            const char* e = getenv("MR_IX_BLOCKS");
-            return e ? std::max(1, atoi(e)) : 256;
-        }();
+        constexpr int ix_cap = 256;   // block cap: one per CU
         int nblk = std::max(1, std::min(ix_cap, cdiv(std::max(sp->n_po, sp->n_ed), IX_BT * IX_EPT)));
         if (nrange > 1) nblk = std::max(1, std::min(nblk, 2 * ix_cap / nrange));   // ~2 rounds of one block per CU
         // ranged: the entries grouped by range first (k_ix_rpart over nshare shares, 4 blocks per CU)
@@ -1734,8 +1728,7 @@ static int ix_launch(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d_mask, mr_
         hipLaunchKernelGGL(k_cross_join<true>, dim3(cdiv(sp->S, 256)), dim3(256), 0, st, sp->trace.p, sp->parent.p,
                            sp->podop.p, sp->S, d_mask, X.key.p, X.val.p, X.rec.p, X.n, ctx->rank,
                            (unsigned long long*)nullptr, b.gk.p, b.gc.p, ecap - 1);
-    static const bool no_small = getenv("MR_NO_NODES_SMALL") != nullptr;   // A/B knob
-    b.small = !sharded && !no_small && NP <= NS_PMAX;
+    b.small = !sharded && NP <= NS_PMAX;
     if (b.small) {
         // one launch for the node order and P_ss, the trace rows / op lists into upper-bound
         // buffers right behind it; the sizes (N, E, T, nnz) go to d_out
@@ -1872,10 +1865,7 @@ int mr_ix_launch2(mr_ctx* ctx, const mr_spans* sp, const uint8_t* d_state, mr_gr
                            NT, xs, dst, epoch, NP, nek);
     }
     if (NT) {
-        static const int ix_cap = [] {
-            const char* e = getenv("MR_IX_BLOCKS");
-            return e ? std::max(1, atoi(e)) : 256;
-        }();
+        constexpr int ix_cap = 256;   // block cap: one per CU
         const int nblk = std::max(1, std::min(ix_cap, cdiv(std::max(sp->n_po, sp->n_ed), IX_BT * IX_EPT)));
         const size_t lds = 2 * (3 * (size_t)NP + (size_t)nek) * sizeof(int32_t);
         hipLaunchKernelGGL(k_ix_stats2, dim3(nblk), dim3(IX_BT), lds, st, d_state, sp->n_po, sp->po_tr.p, sp->po_op.p,
@@ -2019,7 +2009,7 @@ __global__ void k_ix_traces2_b(IxBatch<IxWinTraces> a) {
 int mr_ix_launch2_batch(mr_ctx* ctx, int n, const mr_spans* const* sps, uint8_t* const* d_states, mr_graph* const* g0s,
                         mr_graph* const* g1s, IxBuild* const* b0s, IxBuild* const* b1s, int64_t* const* d_outs,
                         const DetIn* dets, bool fuse) {
-    if (n < 1 || n > IXW || getenv("MR_NO_IX2") != nullptr || getenv("MR_NO_IXB") != nullptr) return MR_ERR_STATE;
+    if (n < 1 || n > IXW || getenv("MR_NO_IX2") != nullptr) return MR_ERR_STATE;
     for (int k = 0; k < n; ++k) {
         const mr_spans* sp = sps[k];
         if (!sp->ekey.p || sp->n_podops > NS_PMAX || 2 * (3 * (int64_t)sp->n_podops + sp->n_edge_keys) > IX_LDS_WORDS)
@@ -2557,7 +2547,7 @@ int64_t mr_lo_zero_words(const mr_spans* sp) {
 int mr_lo_launch_batch(mr_ctx* ctx, int n, const mr_spans* const* sps, mr_graph* const* g0s, mr_graph* const* g1s,
                        IxBuild* const* b0s, IxBuild* const* b1s, int64_t* const* d_outs, const DetIn* dets,
                        uint32_t* const* zw) {
-    if (n < 1 || n > IXW || getenv("MR_NO_IX2") != nullptr || getenv("MR_NO_IXB") != nullptr) return MR_ERR_STATE;
+    if (n < 1 || n > IXW || getenv("MR_NO_IX2") != nullptr) return MR_ERR_STATE;
     for (int k = 0; k < n; ++k)
         if (!sps[k]->lo_ok || !mr_lo_fits(sps[k])) return MR_ERR_STATE;
     hipStream_t st = ctx->stream;

@@ -426,6 +426,7 @@ struct MrPeerX {
     unsigned long long* const* peers;   // device table of every rank's region (null: off)
     unsigned long long* region;         // this rank's region
     int32_t R, rank, nbf, spin;         // spin: mode-2 blocks wait themselves (0: k_peer_bwait did)
+    int32_t mute;                       // (tests: MR_PEER_TEST_MUTE) this rank never signals its rounds
     int64_t slots, W, bflags, err;      // word offsets in a region: slot area, words per slot, block flags, error word
     uint64_t seq;                       // the round (slot parity seq & 1, flags store seq + 1)
     unsigned long long timeout;         // s_memrealtime ticks

@@ -2892,7 +2892,7 @@ __global__ void __launch_bounds__(WAVE * FB_W) k_fx_b(const GDev* __restrict__ g
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (every wave: the r' word of wave 1 too)
         __syncthreads();
-        if ((int32_t)threadIdx.x < px.R) {
+        if ((int32_t)threadIdx.x < px.R && !px.mute) {
             __atomic_thread_fence(__ATOMIC_RELEASE);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __hip_atomic_store((GLB unsigned long long*)px.peers[threadIdx.x] + px.bflags + (int64_t)px.rank * px.nbf + bidx,
@@ -3309,18 +3309,11 @@ static int64_t plan_resident(int32_t N, const FxPlan& P) {
 // k_tr_a: blocks of one graph and the cut of its tiles into contiguous per-wave runs of about
 // equal cost (chunks + 2 per tile: a tile's q/r words weigh about two chunks).  Cached per
 // graph for the wave count; at most 1023 tiles (65472 traces) per block.
-// wsum: wave tiles of all fused graphs of the launch.  A graph of a batch gets its share of
-// MR_TR_BUDGET (default 1) x the resident blocks in proportion to its tiles: a small graph of a
-// batch then runs a few blocks with several tiles per wave instead of one block per tile set --
-// the per-block fixed cost (LDS image, the N-word partial row written here and re-read by
-// k_fx_b) falls with the block count while the batch still fills the chip.
-static double tr_budget() {
-    static const double v = [] {
-        const char* e = getenv("MR_TR_BUDGET");
-        return e ? std::max(0.0, atof(e)) : 1.0;
-    }();
-    return v;
-}
+// wsum: wave tiles of all fused graphs of the launch.  A graph of a batch gets its share of the
+// resident blocks in proportion to its tiles: a small graph of a batch then runs a few blocks with
+// several tiles per wave instead of one block per tile set -- the per-block fixed cost (LDS image,
+// the N-word partial row written here and re-read by k_fx_b) falls with the block count while the
+// batch still fills the chip.
 // a tile's fixed cost in chunks for the per-wave cut: its q / r words and r' (about two chunks),
 // plus the hot-op accumulators and mask sum on hot-op layouts (3: with 2 the waves of short hot
 // tiles became a tail, C4 188 us per iteration)
@@ -3335,8 +3328,8 @@ static int tr_split(mr_ctx* ctx, mr_graph* g, const FxPlan& P, int64_t wsum, int
     if (force_nb > 0) {   // (at most 1023 wave tiles per block still)
         nb = std::max<int64_t>(force_nb, cdiv(W, 1023));
     } else {
-        if (tr_budget() > 0.0 && wsum > W) {
-            const int64_t share = (int64_t)std::ceil((double)resident * tr_budget() * (double)W / (double)wsum);
+        if (wsum > W) {
+            const int64_t share = (int64_t)std::ceil((double)resident * (double)W / (double)wsum);
             nb = std::min(nb, share);
         }
         // at least two tiles per wave: a launch of few tiles (one window's graphs) otherwise runs a
@@ -4576,9 +4569,8 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
     bool fb_small = !any_wide;
     // (a large graph alone -- C4: 256 rows of 10k ops -- sums faster with 16-wave blocks: 137 -> 134 us)
     for (int i = 0; i < ng; ++i) fb_small = fb_small && hv[(size_t)i].n_fa <= FB_SMALL_ROWS && hv[(size_t)i].N <= 4096;
-    static const bool no_side = getenv("MR_WIDE_SERIAL") != nullptr;   // A/B knob: one stream
     hipStream_t sst = st;
-    if (any_wide && !no_side) {
+    if (any_wide) {
         if (!ctx->side) {
             MR_TRY_HIP(ctx, hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
             for (hipEvent_t& e : ctx->side_ev) MR_TRY_HIP(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));

@@ -470,3 +470,74 @@ def test_peer_regions_carry_over_graphs_of_different_sizes(mode):
             else:
                 assert wa.tobytes() == wb.tobytes(), f"graph {k} rank {r}: peer != host collective"
             assert b[r][1][k][0].tobytes() == b[0][1][k][0].tobytes(), "ranks disagree"
+
+
+# ------------------------------------------------------------ a peer that never arrives
+def _timeout_worker(rank, world, port, q, timeout_ms):
+    """A sharded ranking with the peer exchange, then the same with rank 1 never signalling its
+    rounds (MR_PEER_TEST_MUTE, read per call), then again unmuted: (rank, [ok times], fail time,
+    error text, weights bitwise equal before / after)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), MR_PEER_TIMEOUT_MS=str(timeout_ms))
+    import datetime
+    import time
+
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=90))
+    try:
+        from gpu_util import host_graph_from_oracle
+        from microrank_amd import _lib, shard
+        from microrank_amd.graph import DeviceGraph
+
+        ctx = _lib.Context(0)
+        shard.use_host(ctx)
+        shard.use_peer(ctx)
+        dg = DeviceGraph.upload(ctx, host_graph_from_oracle(_shard(_window_graph(), rank, world)))
+        times, ws = [], []
+        for _ in range(2):
+            dist.barrier()
+            ts = time.perf_counter()
+            ws.append(shard.sharded_pagerank(dg, True)[0])
+            times.append(time.perf_counter() - ts)
+        os.environ["MR_PEER_TEST_MUTE"] = "1"
+        dist.barrier()
+        ts = time.perf_counter()
+        err = None
+        try:
+            shard.sharded_pagerank(dg, True)
+        except Exception as e:   # the expected outcome
+            err = repr(e)
+        t_fail = time.perf_counter() - ts
+        os.environ.pop("MR_PEER_TEST_MUTE")
+        dist.barrier()
+        w_after = shard.sharded_pagerank(dg, True)[0]
+        dg.close()
+        ctx.close()
+        q.put((rank, times, t_fail, err, ws[0].tobytes() == w_after.tobytes()))
+    except Exception as e:
+        q.put((rank, None, None, f"setup: {e!r}", False))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_peer_timeout_reports_within_one_timeout():
+    """a rank whose rounds never arrive (two processes on one GPU, MR_PEER_TIMEOUT_MS
+    = 400 ms, rank 1 muted) makes EVERY rank's sharded ranking fail with the peer-timeout error
+    (agreed over the fallback collective), and the failure arrives within about one timeout -- the
+    bounded spins stop on the region's error word instead of timing out again in each of the 25
+    iterations (>= 10 s).  The context recovers: the next ranking (fresh regions) is bitwise the
+    one before."""
+    timeout_ms = 400
+    mpc = mp.get_context("spawn")
+    q = mpc.Queue()
+    port = _free_port()
+    procs = [mpc.Process(target=_timeout_worker, args=(r, 2, port, q, timeout_ms)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in procs], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, times, t_fail, err, same in res:
+        assert times is not None, f"rank {rank}: {err}"
+        assert err is not None and "peer timeout" in err, (rank, err)
+        assert t_fail < min(times) + 3 * timeout_ms / 1e3, (rank, t_fail, times)
+        assert same, f"rank {rank}: the ranking after the timeout differs"
