@@ -26,7 +26,10 @@ roofline: one power iteration (the k_tr_a + k_fx_b launch pair over a window gro
 algorithmic bytes (SURVEY §8(d) B_iter of every graph of the launch) over its live HIP-event
 duration on the library's stream; traffic = FETCH_SIZE (x2, gfx950) + WRITE_SIZE of the same
 launches per iteration from two rocprofv3 --pmc child runs made before this process touches the
-GPU (--no-traffic skips them).  --no-side: the timed steps only (no single-window latency, kind-
+GPU (--no-traffic skips them).  roofline.fracs puts the three fractions side by side: SURVEY
+bytes (4-B op ids), the bytes the walk reads (u16 ids), PMC bytes.  The timed walk visits every
+trace (no kind compression of any form); the run-merged walk -- SURVEY 8(f)4's compression
+inside k_tr_a -- is its own side leg (value_run_merged, roofline.run_merged).  --no-side: the timed steps only (no single-window latency, kind-
 compressed probe or c4_sharded leg), so a rocprofv3 kernel table of the command holds only the
 timed shape's launches (profiles/README.md).
 cpu_baseline: the C restatement (oracle/, OpenMP) of the same window on this host's cores.

@@ -511,8 +511,13 @@ __global__ void k_tr_coff(const int64_t* c64, int32_t n, int32_t* coff) {
 // weigh about two chunks), in one block on the device (no host round trip): cut[i] = first tile
 // whose cost prefix reaches total * i / nw.  A block (NW waves) must stay within 1023 tiles (65472
 // traces: the fixed-point budget); a cost cut that breaks it falls back to equal tile counts (the
-// host sizes the grid so those fit).  scale = {2^SC, 2^-SC}, SC = 64 - bits(most traces of a block).
+// host sizes the grid so those fit).  scale = {2^SC, 2^-SC} with SC = FX_SC = 48 for every graph: the
+// bound 64 - bits(1023 tiles x 64 traces) of any block, not of this cut's largest block, so a
+// trace's X (hence every exact limb sum) does not depend on how the graph's tiles are cut into
+// blocks -- a window ranks bitwise alike in any batch or group (quantisation 2^-48 of M_r per term,
+// far below the 1e-10 parity bar).
 constexpr int TC_T = 1024, TC_MAX = 16384;
+constexpr int FX_SC = 48;   // the fixed-point scale of X_t: 64 - bits(65472 traces of a block)
 __device__ __forceinline__ void tr_cut_body(const int32_t* coff, int32_t W, int32_t nw, int32_t NW, int32_t* cut,
                                             double* scale, double tw) {
     __shared__ int32_t lc[TC_MAX + 1];
@@ -543,7 +548,7 @@ __device__ __forceinline__ void tr_cut_body(const int32_t* coff, int32_t W, int3
     }
     for (int32_t i = threadIdx.x; i <= nw; i += TC_T) cut[i] = lc[i];
     if (threadIdx.x == 0) {
-        const int sc = __clzll((unsigned long long)max(mx, 1) * WAVE);   // 64 - bits(traces)
+        const int sc = FX_SC;
         scale[0] = __longlong_as_double((long long)(1023 + sc) << 52);
         scale[1] = __longlong_as_double((long long)(1023 - sc) << 52);
     }
@@ -4471,13 +4476,12 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         int64_t nfa = 0;
         if (g->fused) MR_TRY(fused_blocks(ctx, g, plan, wsum, &nfa));
         nfa = g->fused ? std::max<int64_t>(nfa, sharded ? 1 : 0) : 0;
-        // a row entry stays below 2^63; shards of one graph hold different trace counts, and their
-        // limbs are summed, so they share the scale of the largest block (2^15 traces)
-        // v1: a row entry stays below 2^63; v2: below 2^64 (traces per block < 2^(64-sc)).
-        // Shards of one graph hold different trace counts and their limbs are summed, so they
-        // share one scale, 2^48 (<= 65535 traces per block: wv_blocks / fx_blocks)
-        const int64_t tpb = g->fused ? g->wtile_msum : 0;
-        const int sc = sharded ? 48 : 64 - bits_for((uint64_t)std::max<int64_t>(tpb, 1));
+        // a row entry stays below 2^64 (traces per block <= 65535 < 2^(64-sc)); one scale for every
+        // graph and shard (FX_SC, see tr_cut_body): the limbs do not depend on the block cut, and the
+        // ranks of a sharded graph sum theirs.  A kind-compressed graph's block stands for its
+        // traces with multiplicity: below FX_SC when those exceed 65535
+        const int64_t msum = g->fused && !g->tile_mult_h.empty() ? g->wtile_msum : 0;
+        const int sc = std::min(FX_SC, 64 - bits_for((uint64_t)std::max<int64_t>(msum, 1)));
         v.alpha = alpha;
         v.fx_scale = std::ldexp(1.0, sc);
         v.fx_iscale = std::ldexp(1.0, -sc);
