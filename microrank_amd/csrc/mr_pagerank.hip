@@ -511,15 +511,14 @@ __global__ void k_tr_coff(const int64_t* c64, int32_t n, int32_t* coff) {
 // weigh about two chunks), in one block on the device (no host round trip): cut[i] = first tile
 // whose cost prefix reaches total * i / nw.  A block (NW waves) must stay within 1023 tiles (65472
 // traces: the fixed-point budget); a cost cut that breaks it falls back to equal tile counts (the
-// host sizes the grid so those fit).  scale = {2^SC, 2^-SC} with SC = FX_SC = 48 for every graph: the
-// bound 64 - bits(1023 tiles x 64 traces) of any block, not of this cut's largest block, so a
-// trace's X (hence every exact limb sum) does not depend on how the graph's tiles are cut into
-// blocks -- a window ranks bitwise alike in any batch or group (quantisation 2^-48 of M_r per term,
-// far below the 1e-10 parity bar).
+// host sizes the grid so those fit).  scale = {2^SC, 2^-SC}: SC = 64 - bits(most traces of a block)
+// (the finest scale whose row entries stay below 2^64), or scfix > 0: a scale that does not depend
+// on the cut -- window graphs (layout order) take 64 - bits(min(T, 65472)), so a trace's X, hence
+// every exact limb sum, is the same however a batch's group cuts the graph into blocks, and a window
+// ranks bitwise alike in any batch or group.
 constexpr int TC_T = 1024, TC_MAX = 16384;
-constexpr int FX_SC = 48;   // the fixed-point scale of X_t: 64 - bits(65472 traces of a block)
 __device__ __forceinline__ void tr_cut_body(const int32_t* coff, int32_t W, int32_t nw, int32_t NW, int32_t* cut,
-                                            double* scale, double tw) {
+                                            double* scale, double tw, int scfix) {
     __shared__ int32_t lc[TC_MAX + 1];
     __shared__ int32_t mx;
     if (threadIdx.x == 0) mx = 0;
@@ -548,14 +547,14 @@ __device__ __forceinline__ void tr_cut_body(const int32_t* coff, int32_t W, int3
     }
     for (int32_t i = threadIdx.x; i <= nw; i += TC_T) cut[i] = lc[i];
     if (threadIdx.x == 0) {
-        const int sc = FX_SC;
+        const int sc = scfix > 0 ? scfix : __clzll((unsigned long long)max(mx, 1) * WAVE);   // 64 - bits(traces)
         scale[0] = __longlong_as_double((long long)(1023 + sc) << 52);
         scale[1] = __longlong_as_double((long long)(1023 - sc) << 52);
     }
 }
 __global__ void __launch_bounds__(TC_T) k_tr_cut(const int32_t* coff, int32_t W, int32_t nw, int32_t NW, int32_t* cut,
-                                                 double* scale, double tw) {
-    tr_cut_body(coff, W, nw, NW, cut, scale, tw);
+                                                 double* scale, double tw, int scfix) {
+    tr_cut_body(coff, W, nw, NW, cut, scale, tw, scfix);
 }
 // the cuts of a batch's graphs in one launch (block g: graph g)
 struct CutArg {
@@ -564,6 +563,7 @@ struct CutArg {
     double* scale;
     int32_t W, nw, NW;
     float tw;   // a tile's fixed cost in chunks
+    int32_t scfix;   // > 0: the graph's cut-independent scale
 };
 constexpr int TC_BATCH = 64;
 struct CutBatch {
@@ -571,7 +571,7 @@ struct CutBatch {
 };
 __global__ void __launch_bounds__(TC_T) k_tr_cut_b(CutBatch b) {
     const CutArg& x = b.a[blockIdx.x];
-    tr_cut_body(x.coff, x.W, x.nw, x.NW, x.cut, x.scale, (double)x.tw);
+    tr_cut_body(x.coff, x.W, x.nw, x.NW, x.cut, x.scale, (double)x.tw, x.scfix);
 }
 // thread per (tile, lane): the lane's trace rotated by (trace mod len), then pads N + lane
 __device__ __forceinline__ void tr_fill_body(int32_t blk, const int32_t* tperm, const int64_t* off, const uint16_t* ids,
@@ -2159,7 +2159,10 @@ __device__ __forceinline__ int32_t tr_walk_short(const GDev& G, int32_t k, const
     const uint32_t cpad = (uint32_t)(G.N + lane);
     const bool hot = H.n > 0;
     const GLB uint8_t* hmk = hot ? gp(G.hmask) : (const GLB uint8_t*)coff;
-    const GLB uint8_t* trn = gp(G.trun);
+    // EXT & 4: run-merged graphs (trun).  Without it the run logic is compiled out: every lane walks
+    // its own trace (the headline walk)
+    constexpr bool RUNS = (EXT & 4) != 0;
+    const GLB uint8_t* trn = RUNS ? gp(G.trun) : nullptr;
     const int32_t cl = __builtin_amdgcn_readfirstlane(coff[ke]) - 1;   // the run's last chunk
     // the first tile's chunk ranges: handed over by the previous tier (n >= 0), else loaded
     if (n < 0) {
@@ -2177,6 +2180,7 @@ __device__ __forceinline__ int32_t tr_walk_short(const GDev& G, int32_t k, const
     const GLB double* cacc = cx ? gp(G.cold_acc) : sug;
     // run marks of tile kk's lanes (1 on graphs without runs)
     auto rl_of = [&](int32_t kk) -> uint32_t {
+        if constexpr (!RUNS) return 1u;
         return trn ? (uint32_t)trn[min(min(kk, ke - 1) * WAVE + lane, T - 1)] : 1u;
     };
     // a run's tail (rl 0) needs none of its own ids, q, c or w -- the head walks for it and its r'
@@ -2186,7 +2190,7 @@ __device__ __forceinline__ int32_t tr_walk_short(const GDev& G, int32_t k, const
     auto load = [&](R& r, int32_t kk, int32_t cc0, int32_t qq0, int32_t nqq, uint32_t rl) {
         const int32_t kq = min(kk, ke - 1);
         const int32_t p = min(kq * WAVE + lane, T - 1);
-        const bool hd = rl != 0u;
+        const bool hd = !RUNS || rl != 0u;
         const int32_t ph = hd ? p : 0;
 #pragma unroll
         for (int j = 0; j < NC; ++j) r.id[j] = idb[hd ? (size_t)min(cc0 + j, cl) * WAVE + lane : 0];
@@ -2222,8 +2226,9 @@ __device__ __forceinline__ int32_t tr_walk_short(const GDev& G, int32_t k, const
         // a run of rl identical traces (the same ops in the same order, the same q, c and w: the
         // same sum and r') is walked by its head alone: its X times rl into the accumulators (integers:
         // exactly the rl separate adds), its r' broadcast to the run below
-        const bool hd = r.rl != 0u;
-        const unsigned long long X = own && hd ? (unsigned long long)__double2ull_rn((double)r.q * xsc) * (unsigned long long)r.rl : 0ull;
+        const bool hd = !RUNS || r.rl != 0u;
+        const unsigned long long X0 = own && hd ? (unsigned long long)__double2ull_rn((double)r.q * xsc) : 0ull;
+        const unsigned long long X = RUNS ? X0 * (unsigned long long)r.rl : X0;
         double acc = H.n ? tr_hot_init(H, r.hm, X) : 0.0;
         if (hd) {
             double sv[2][4];
@@ -2254,7 +2259,7 @@ __device__ __forceinline__ int32_t tr_walk_short(const GDev& G, int32_t k, const
                 if (nqq > 2) x = r.xo;   // (rare: > 4 cold entries in a trace of the tile: k_cold_trace's sum)
             }
         double rp = d * ((acc + x) / Ms) + (double)r.c;   // pagerank.py:125
-        if (trn) {   // (uniform) the run's head's r'
+        if (RUNS && trn) {   // (uniform) the run's head's r'
             const unsigned long long hb = __ballot(hd) & (lane == WAVE - 1 ? ~0ull : (2ull << lane) - 1ull);
             rp = __shfl(rp, 63 - __builtin_clzll(hb), WAVE);
         }
@@ -2330,7 +2335,7 @@ __device__ __forceinline__ double tr_walk(const GDev& G, int32_t lb, int cur, in
         // one tier per chunk count (the run's tiles ascend in it): every count static, no branch
         // inside a tile, so each wait is for exactly the LDS reads and loads it consumes
         int32_t tc0 = 0, tn = -1, tq0 = 0, tnq = 0;   // the next tile's ranges, handed from tier to tier
-#define TR_TIER(NC_) if (NC_ <= (NT == 1024 || EXT ? TR_TIERS_EXT : MR_TR_TIERS512) && k < ke) k = tr_walk_short<Q, NC_, EXT, HN>(G, k, ke, T, lane, cur, nxt, d, Ms, xsc, su_l, lacc, rmax, H, tc0, tn, tq0, tnq);
+#define TR_TIER(NC_) if (NC_ <= (NT == 1024 || (EXT & 3) ? TR_TIERS_EXT : MR_TR_TIERS512) && k < ke) k = tr_walk_short<Q, NC_, EXT, HN>(G, k, ke, T, lane, cur, nxt, d, Ms, xsc, su_l, lacc, rmax, H, tc0, tn, tq0, tnq);
         TR_TIER(1) TR_TIER(2) TR_TIER(3) TR_TIER(4) TR_TIER(5) TR_TIER(6) TR_TIER(7) TR_TIER(8)
 #undef TR_TIER
     }
@@ -2601,8 +2606,11 @@ __device__ __forceinline__ void tr_last_finish(const GDev& G, int it, double d, 
     }
 }
 
+#ifndef MR_TR_WPE512
+#define MR_TR_WPE512 1   // (A/B builds) minimum waves per SIMD asked of the plain 512-thread k_tr_a
+#endif
 template <class Q, int SUM, int NT, int EXT>
-__global__ void __launch_bounds__(NT) k_tr_a(const GDev* __restrict__ gs, int32_t ng, int32_t split, double d,
+__global__ void __launch_bounds__(NT, NT == 512 && EXT == 0 && SUM != WV_SU_HOT ? MR_TR_WPE512 : 1) k_tr_a(const GDev* __restrict__ gs, int32_t ng, int32_t split, double d,
                                              double alpha, int it, int32_t unused) {
     constexpr bool SUL = SUM == WV_SU_ALL, HOT = SUM == WV_SU_HOT;
     constexpr int NW = NT / WAVE;
@@ -3235,11 +3243,14 @@ static TrA tr_kernel(bool fp32, int mode, int NT, int ext = 0) {
         {{k_tr_a<float, 0, 512, 0>, k_tr_a<float, 0, 1024, 0>},
          {k_tr_a<float, 1, 512, 0>, k_tr_a<float, 1, 1024, 0>},
          {k_tr_a<float, 2, 512, 0>, k_tr_a<float, 2, 1024, 0>}}};
-    static const TrA tab_ext[3][2][2] = {
+    static const TrA tab_ext[4][2][2] = {
         {{k_tr_a<double, 1, 512, 1>, k_tr_a<double, 1, 1024, 1>}, {k_tr_a<float, 1, 512, 1>, k_tr_a<float, 1, 1024, 1>}},
         {{k_tr_a<double, 1, 512, 2>, k_tr_a<double, 1, 1024, 2>}, {k_tr_a<float, 1, 512, 2>, k_tr_a<float, 1, 1024, 2>}},
-        {{k_tr_a<double, 1, 512, 3>, k_tr_a<double, 1, 1024, 3>}, {k_tr_a<float, 1, 512, 3>, k_tr_a<float, 1, 1024, 3>}}};
-    if (ext && mode == WV_SU_ALL) return tab_ext[ext - 1][fp32 ? 1 : 0][NT == 1024 ? 1 : 0];
+        {{k_tr_a<double, 1, 512, 3>, k_tr_a<double, 1, 1024, 3>}, {k_tr_a<float, 1, 512, 3>, k_tr_a<float, 1, 1024, 3>}},
+        {{k_tr_a<double, 1, 512, 4>, k_tr_a<double, 1, 1024, 4>}, {k_tr_a<float, 1, 512, 4>, k_tr_a<float, 1, 1024, 4>}}};
+    // ext 4: run-merged window graphs (trun; never beside multiplicities or cold sums)
+    if (ext == 4 && mode == WV_SU_ALL) return tab_ext[3][fp32 ? 1 : 0][NT == 1024 ? 1 : 0];
+    if ((ext & 3) && mode == WV_SU_ALL) return tab_ext[(ext & 3) - 1][fp32 ? 1 : 0][NT == 1024 ? 1 : 0];
     return tab[fp32 ? 1 : 0][mode][NT == 1024 ? 1 : 0];
 }
 static int num_cus() {
@@ -3323,6 +3334,12 @@ static int64_t plan_resident(int32_t N, const FxPlan& P) {
 // plus the hot-op accumulators and mask sum on hot-op layouts (3: with 2 the waves of short hot
 // tiles became a tail, C4 188 us per iteration)
 static double tr_tile_weight(const mr_graph* g) { return g->nhr ? 3.0 : 2.0; }
+// window graphs (layout order, ranked in batches whose groups cut them differently): the fixed-point
+// scale from the graph's trace count -- a bound for any block of any cut -- instead of the cut's
+// largest block (tr_cut_body); 0 for other graphs (the finest scale of their cut)
+static int32_t tr_scfix(const mr_graph* g) {
+    return g->lo ? 64 - bits_for((uint64_t)std::min<int64_t>(std::max<int32_t>(g->T, 1), 1023 * WAVE)) : 0;
+}
 static int tr_split(mr_ctx* ctx, mr_graph* g, const FxPlan& P, int64_t wsum, int64_t* nfa,
                     std::vector<CutArg>* defer = nullptr, int64_t force_nb = 0) {
     const int64_t W = g->n_wt, NW = P.NT / WAVE;
@@ -3352,10 +3369,10 @@ static int tr_split(mr_ctx* ctx, mr_graph* g, const FxPlan& P, int64_t wsum, int
             MR_TRY(g->dscale.alloc(ctx, 2));
             if (defer) {   // launched with the batch's other cuts (k_tr_cut_b)
                 defer->push_back(CutArg{g->coff.p, g->wtile.p, g->dscale.p, (int32_t)W, (int32_t)nw, (int32_t)NW,
-                                        (float)tr_tile_weight(g)});
+                                        (float)tr_tile_weight(g), tr_scfix(g)});
             } else {
                 hipLaunchKernelGGL(k_tr_cut, dim3(1), dim3(TC_T), 0, ctx->stream, g->coff.p, (int32_t)W, (int32_t)nw,
-                                   (int32_t)NW, g->wtile.p, g->dscale.p, tr_tile_weight(g));
+                                   (int32_t)NW, g->wtile.p, g->dscale.p, tr_tile_weight(g), tr_scfix(g));
                 MR_TRY_HIP(ctx, hipGetLastError());
             }
             g->wtile_nw = (int32_t)nw;
@@ -4476,12 +4493,12 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         int64_t nfa = 0;
         if (g->fused) MR_TRY(fused_blocks(ctx, g, plan, wsum, &nfa));
         nfa = g->fused ? std::max<int64_t>(nfa, sharded ? 1 : 0) : 0;
-        // a row entry stays below 2^64 (traces per block <= 65535 < 2^(64-sc)); one scale for every
-        // graph and shard (FX_SC, see tr_cut_body): the limbs do not depend on the block cut, and the
-        // ranks of a sharded graph sum theirs.  A kind-compressed graph's block stands for its
-        // traces with multiplicity: below FX_SC when those exceed 65535
-        const int64_t msum = g->fused && !g->tile_mult_h.empty() ? g->wtile_msum : 0;
-        const int sc = std::min(FX_SC, 64 - bits_for((uint64_t)std::max<int64_t>(msum, 1)));
+        // a row entry stays below 2^64 (traces per block < 2^(64-sc)).  Shards of one graph hold
+        // different trace counts and their limbs are summed, so they share one scale, 2^48 (<= 65535
+        // traces per block: wv_blocks / fx_blocks); window graphs take their cut-independent scale
+        // (tr_scfix); a graph cut on the device carries its scale there (dscale)
+        const int64_t tpb = g->fused ? g->wtile_msum : 0;
+        const int sc = sharded ? 48 : tr_scfix(g) > 0 ? tr_scfix(g) : 64 - bits_for((uint64_t)std::max<int64_t>(tpb, 1));
         v.alpha = alpha;
         v.fx_scale = std::ldexp(1.0, sc);
         v.fx_iscale = std::ldexp(1.0, -sc);
@@ -4555,9 +4572,11 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         if (gs[i]->fused && gs[i]->nhr && plan.mode != WV_SU_ALL)
             return mr_fail(ctx, MR_ERR_ARG, "pagerank batch: a hot-op layout (T >= MR_TR_HOT_MIN) with a graph of > %d ops",
                            (int)WIDE_NA);
-    int any_ext = 0;   // kind multiplicities (1) or cold sums (2) in some fused graph of the launch
+    int any_ext = 0;   // kind multiplicities (1), cold sums (2) or merged runs (4) in some fused graph of the launch
     for (int i = 0; i < ng; ++i)
-        if (gs[i]->fused) any_ext |= (hv[(size_t)i].mw_tp ? 1 : 0) | (hv[(size_t)i].cold_acc ? 2 : 0);
+        if (gs[i]->fused)
+            any_ext |= (hv[(size_t)i].mw_tp ? 1 : 0) | (hv[(size_t)i].cold_acc ? 2 : 0) | (hv[(size_t)i].trun ? 4 : 0);
+    if ((any_ext & 4) && (any_ext & 3)) any_ext &= 3;   // (not built: such a launch walks every trace)
     for (int i = 0; i < ng; ++i)   // the wide variant carries HOT_MAX_WIDE hot accumulators
         if ((any_ext & 2) && gs[i]->fused && gs[i]->nhr > HOT_MAX_WIDE)
             return mr_fail(ctx, MR_ERR_ARG, "pagerank batch: a hot-op layout of %d ops beside a wide graph", gs[i]->nhr);

@@ -430,9 +430,10 @@ class PagerankGraph:
                   "mr_graph_nodes")
         self.table, self.mask = table, mask.astype(bool)
         nodes = [table.podop_names[c] for c in self.node_podop]
-        traces = [table.trace_names[c] for c in self.trace_code]
-        self._dg = DeviceGraph(ctx, h, nodes, traces, self.N, self.T)
-        self.nodes, self.traces = nodes, traces
+        # the trace keys (sorted traceIDs, T of them) are built when something reads them: the
+        # driver's window body never does (trace_pagerank ranks the device graph)
+        self._dg = DeviceGraph(ctx, h, nodes, None, self.N, self.T)
+        self.nodes, self._traces = nodes, None
         self._lists = None
         self.operation_operation = GraphDicts(self, "operation_operation")
         self.operation_trace = GraphDicts(self, "operation_trace")
@@ -441,6 +442,17 @@ class PagerankGraph:
 
     def device_graph(self):
         return self._dg
+
+    @property
+    def traces(self):
+        if self._traces is None:
+            tb = self.table
+            names = tb.meta.get("trace_names_arr")
+            if names is None:
+                names = tb.meta["trace_names_arr"] = np.asarray(tb.trace_names, dtype=object)
+            self._traces = names[self.trace_code].tolist()
+            self._dg.traces = self._traces
+        return self._traces
 
     def as_tuple(self):
         return self.operation_operation, self.operation_trace, self.trace_operation, self.pr_trace
@@ -499,6 +511,8 @@ class GraphDicts(Mapping):
         return iter(self._keys())
 
     def __len__(self):
+        if self.kind in ("operation_trace", "pr_trace"):
+            return self.owner.T
         return len(self._keys())
 
     def __getitem__(self, k):
