@@ -18,7 +18,7 @@ import numpy as np
 
 from . import _lib
 from ._lib import ptr
-from .preprocess_data import get_operation_slo, get_service_operation_list, get_span, span_table
+from .preprocess_data import DETECT_READS, get_operation_slo, get_service_operation_list, get_span, span_table
 from .spans import to_ns
 
 
@@ -50,7 +50,7 @@ def slo_arrays(table, slo):
 def detect_states(data, start_time, end_time, slo, *, ctx=None):
     """(state per trace code, n_abnormal, n_normal, table) or None for an empty window."""
     ctx = ctx or _lib.default_context()
-    table, dev = span_table(data, ctx)
+    table, dev = span_table(data, ctx, DETECT_READS)
     a3, ok = slo_arrays(table, slo)
     state = np.zeros(table.n_traces, np.uint8)
     na, nn, nin = C.c_int32(), C.c_int32(), C.c_int64()

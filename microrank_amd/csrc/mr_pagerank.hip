@@ -2607,7 +2607,7 @@ __device__ __forceinline__ void tr_last_finish(const GDev& G, int it, double d, 
 }
 
 #ifndef MR_TR_WPE512
-#define MR_TR_WPE512 1   // (A/B builds) minimum waves per SIMD asked of the plain 512-thread k_tr_a
+#define MR_TR_WPE512 8   // minimum waves per SIMD asked of the plain 512-thread k_tr_a (A/B builds: 1)
 #endif
 template <class Q, int SUM, int NT, int EXT>
 __global__ void __launch_bounds__(NT, NT == 512 && EXT == 0 && SUM != WV_SU_HOT ? MR_TR_WPE512 : 1) k_tr_a(const GDev* __restrict__ gs, int32_t ng, int32_t split, double d,

@@ -206,16 +206,20 @@ class _FrameSnapshot:
         self.version = df.attrs.get("_mr_version", 0)
         self.parts = [_ColumnSnapshot(df[c]) for c in self.cols]
 
-    def matches(self, df: pd.DataFrame) -> bool:
+    def matches(self, df: pd.DataFrame, reads=None) -> bool:
+        """reads: the columns the caller's result depends on (None: all) -- only those are compared
+        word by word, so a call whose own columns are unchanged reuses the table even when another
+        column was edited (its result cannot see that column; the next call that reads it rebuilds)."""
         cols = tuple(c for c in _TABLE_COLUMNS if c in df.columns)
         if cols != self.cols or len(df) != self.n or df.attrs.get("_mr_version", 0) != self.version:
             return False
         if self.n == 0:
             return True
-        series = [df[c] for c in cols]
+        pick = [i for i, c in enumerate(cols) if reads is None or c in reads]
+        parts, series = [self.parts[i] for i in pick], [df[cols[i]] for i in pick]
         if self.n < 65536:
-            return all(p.matches(x) for p, x in zip(self.parts, series))
-        return all(_pool().map(lambda px: px[0].matches(px[1]), zip(self.parts, series)))
+            return all(p.matches(x) for p, x in zip(parts, series))
+        return all(list(_pool().map(lambda px: px[0].matches(px[1]), zip(parts, series))))
 
 
 _POOL = None
@@ -244,14 +248,21 @@ def invalidate(df: pd.DataFrame) -> None:
         _CACHE.pop(k, None)
 
 
-def span_table(df: pd.DataFrame, ctx=None):
+# the columns each drop-in call's result depends on (the cache compares only those, span_table)
+DETECT_READS = ("traceID", "serviceName", "operationName", "duration", "startTime", "endTime")
+GRAPH_READS = ("traceID", "spanID", "ParentSpanId", "serviceName", "operationName", "podName")
+
+
+def span_table(df: pd.DataFrame, ctx=None, reads=None):
     """(SpanTable, DeviceSpans) for a DataFrame, built once per (DataFrame, Context) and rebuilt
-    when any column it reads changed.  The device table belongs to the context that uploaded it
-    (mr_spans handles are per mr_ctx), so two contexts sharing a DataFrame get a handle each."""
+    when a column it reads changed -- of the columns in `reads` (the ones the caller's result
+    depends on; None: every column the table is built from).  The device table belongs to the
+    context that uploaded it (mr_spans handles are per mr_ctx), so two contexts sharing a DataFrame
+    get a handle each."""
     ctx = ctx or _lib.default_context()
     key = (id(df), id(ctx))
     hit = _CACHE.get(key)
-    if hit is not None and hit[0]() is df and hit[1]() is ctx and hit[2].matches(df):
+    if hit is not None and hit[0]() is df and hit[1]() is ctx and hit[2].matches(df, reads):
         return hit[3], hit[4]
     fp = _fingerprint(df)   # (taken before the build: the table is built from these values)
     arrays = None if _HOST_FACTORIZE else arrow_columns(df)
@@ -532,7 +543,7 @@ def get_pagerank_graph(trace_list, span_df: pd.DataFrame, *, ctx=None):
     """preprocess_data.py:146-171 on the GPU (K1).  Returns (operation_operation,
     operation_trace, trace_operation, pr_trace) as lazy mappings backed by the device graph."""
     ctx = ctx or _lib.default_context()
-    table, dev = span_table(span_df, ctx)
+    table, dev = span_table(span_df, ctx, GRAPH_READS)
     mask = np.zeros(table.n_traces, np.uint8)
     codes = trace_list.codes_for(table) if hasattr(trace_list, "codes_for") else None
     if codes is not None:   # a list system_anomaly_detect returned for this table: its codes

@@ -149,3 +149,22 @@ def test_oracle_phi_keyword(phi):
     got = orc.preference(g, k, True, phi)
     assert (got == base).all() == (phi == 0.5)
     assert (orc.preference(g, k, False) == orc.preference(g, k, False, phi)).all()
+
+
+def test_fingerprint_reads_subset():
+    """A call compares only the columns its result depends on: an edit of another column keeps
+    the cached table for that call and is caught by the next call that reads the edited column."""
+    from microrank_amd.preprocess_data import DETECT_READS, GRAPH_READS, _fingerprint
+
+    n = 70_000
+    df = pd.DataFrame({c: np.array([f"{c}{i % 977}" for i in range(n)], dtype=object) for c in
+                       ("traceID", "spanID", "ParentSpanId", "serviceName", "operationName", "podName")})
+    for c in ("duration", "startTime", "endTime"):
+        df[c] = np.arange(n, dtype=np.int64)
+    fp = _fingerprint(df)
+    assert fp.matches(df, DETECT_READS) and fp.matches(df, GRAPH_READS) and fp.matches(df)
+    df.loc[df.index[n // 2], "spanID"] = "edited"
+    assert fp.matches(df, DETECT_READS)
+    assert not fp.matches(df, GRAPH_READS) and not fp.matches(df)
+    df.loc[df.index[7], "duration"] = -1
+    assert not fp.matches(df, DETECT_READS)
