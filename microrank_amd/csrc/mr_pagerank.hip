@@ -23,6 +23,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <queue>
 
 #include "mr_internal.h"
 #include "mr_prim.h"
@@ -1790,6 +1791,8 @@ struct GDev {
     int32_t blk0f, n_fa, blk0fb, n_fb;   // fused path: k_tr_a / k_fx_b block ranges
     int32_t fb_ops;                      // k_fx_b ops per block
     int32_t lastfin;                     // k_tr_a's last block of the graph finishes the iteration (no k_fx_b)
+    int32_t lf_acq;                      // lastfin: the finishing block takes an agent acquire (else the launch
+                                         // runs one workgroup per CU and the sc1 hand-off of the guide's row 1 holds)
     int32_t ssv_pre;                     // k_tr_a's blocks compute the call-graph terms (fx_ssv) for k_fx_b
     int32_t row_wt;                      // k_tr_a's partial rows stored write-through (sc1)
 };
@@ -2508,15 +2511,21 @@ __device__ __forceinline__ void tr_ssv_share(const GDev& G, int32_t lb, int cur,
 
 // The last k_tr_a block of a graph finishes the iteration itself (small graphs: window batches),
 // so an iteration is ONE launch instead of k_tr_a + k_fx_b.  Every block writes its partial row
-// and its call-graph terms write-through (sc1), every wave waits for its stores (vmcnt(0)), and
-// behind a workgroup barrier one lane takes a ticket from the graph's counter (an agent-scope add,
-// returned); the block whose ticket completes the iteration's count is the consumer.  The launch
-// runs several workgroups per CU, so the hand-off table's sc1-only rows (MI355X_MICROARCH.md:
-// "hipMalloc; one per CU") do not apply: the consumer takes the guide's general form -- ONE agent
-// acquire on the adding lane, its own vmcnt(0) wait, a workgroup barrier, then the loads (kept sc1)
-// -- and reads every row and does k_fx_b's work for every op: the same exact limb sums, the same
-// call-graph term (a lane per op of <= 8 parents, a wave per op of more: wave_sum's butterfly) and
-// the same finish: bitwise k_fx_b's results.  Only the finishing block pays the acquire.
+// and its call-graph terms write-through (sc1, hipMalloc'd pool memory), every wave waits for its
+// stores (vmcnt(0)), and behind a workgroup barrier one lane takes a ticket from the graph's
+// counter (an agent-scope add, returned); the block whose ticket completes the iteration's count is
+// the consumer: it reads every row and does k_fx_b's work for every op -- the same exact limb sums,
+// the same call-graph term (a lane per op of <= 8 parents, a wave per op of more: wave_sum's
+// butterfly) and the same finish: bitwise k_fx_b's results.  Two forms of the hand-off
+// (MI355X_MICROARCH.md, inter-workgroup visibility):
+//  * a launch of at most one block per CU (<= num_cus blocks, the dynamic LDS padded past half a
+//    CU's 160 KB so no two blocks share a CU: single windows) is the hand-off table's row 1 in
+//    every cell -- one lane per storing workgroup adds to ONE unsharded counter, the last adder
+//    told by the returned value, the other waves behind a barrier it joins, hipMalloc, one
+//    workgroup per CU, 8-B sc1 stores and sc1 loads: no acquire (lf_acq 0);
+//  * any other launch (batches: several workgroups per CU) takes the guide's general consumer
+//    form: ONE agent acquire on the adding lane, its own vmcnt(0) wait, a workgroup barrier, then
+//    the loads (lf_acq 1).  Only the finishing block pays it.
 template <int NT>
 __device__ __forceinline__ void tr_last_finish(const GDev& G, int it, double d, double Ms,
                                             GLB unsigned long long* Mnext) {
@@ -2529,7 +2538,7 @@ __device__ __forceinline__ void tr_last_finish(const GDev& G, int it, double d, 
         const unsigned long long t = __hip_atomic_fetch_add(gpw(G.mslot) + 6 * MSH + 1, 1ull, __ATOMIC_RELAXED,
                                                             __HIP_MEMORY_SCOPE_AGENT);
         const bool last = t + 1 == (unsigned long long)G.n_fa * (unsigned long long)(it + 1);
-        if (last) {   // consumer: agent acquire (this CU's L1 invalidated), waited before the barrier
+        if (last && G.lf_acq) {   // consumer: agent acquire (this CU's L1 invalidated), waited before the barrier
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
@@ -2705,7 +2714,11 @@ static int fb_ops(int32_t N, bool many) {
     return N <= 8192 ? (many ? 64 : 16) : 64;
 }
 constexpr int64_t FB_MANY_BLOCKS = 1024;   // 16-op blocks of a launch from which "many" holds
-constexpr int64_t LASTFIN_WORDS = 32768;   // k_tr_a's last-block finish: partial-row words it reads (256 KB)
+constexpr int64_t LASTFIN_WORDS = 32768;
+#ifndef MR_LF_ONE_CU_LDS
+#define MR_LF_ONE_CU_LDS (80 * 1024 + 1024)   // (A/B builds: 0 = every last-block launch takes the acquire)
+#endif
+constexpr size_t LF_ONE_CU_LDS = MR_LF_ONE_CU_LDS;   // > half of a CU's 160 KB: one block per CU   // k_tr_a's last-block finish: partial-row words it reads (256 KB)
 // px.peers (sharded graphs on the peer path, one graph per launch): the exchange is fused in --
 // mode 1 pushes the block's limbs (and block 0 this rank's r' maximum) into every rank's slot for
 // this rank and stores the round number in the block's flag there; mode 2 block b waits for flag
@@ -3427,6 +3440,45 @@ static int tr_split(mr_ctx* ctx, mr_graph* g, const FxPlan& P, int64_t wsum, int
     return MR_OK;
 }
 
+// k_tr_a blocks of every graph of a batch launch: ONE resident set of blocks, split by the graphs'
+// wave tiles so that the largest per-block share is as small as it can be -- each graph first gets
+// floor(resident x its tiles / all tiles) blocks (at least one, at least its 1023-tile cap, at most
+// one per two tiles per wave), then the remaining blocks go one at a time to the graph whose blocks
+// carry the most tiles.  (Rounding each graph's share UP put 1152 blocks on the 1024 resident slots
+// of a C2 group -- 128 windows' 13k- and 187k-trace graphs, 7.5 and 0.5 blocks of share each: a
+// second round of blocks behind the first.)  Empty: the single-graph rule of tr_split.
+static std::vector<int64_t> batch_blocks(mr_graph* const* gs, int ng, const FxPlan& P, int64_t wsum) {
+    std::vector<int64_t> nb;
+    int nf = 0;
+    for (int i = 0; i < ng; ++i) nf += gs[i]->fused ? 1 : 0;
+    if (nf < 2 || wsum <= 0) return nb;
+    int64_t R = INT64_MAX;
+    for (int i = 0; i < ng; ++i)
+        if (gs[i]->fused) R = std::min(R, plan_resident(kern_n(gs[i]), P));
+    const int64_t NW = P.NT / WAVE;
+    nb.assign((size_t)ng, 0);
+    std::vector<int64_t> cap((size_t)ng, 0);
+    int64_t used = 0;
+    for (int i = 0; i < ng; ++i) {
+        if (!gs[i]->fused) continue;
+        const int64_t W = gs[i]->n_wt, lo = std::max<int64_t>(cdiv(W, 1023), 1);
+        cap[(size_t)i] = std::max<int64_t>(lo, cdiv(W, 2 * NW));
+        nb[(size_t)i] = std::min(cap[(size_t)i], std::max(lo, (int64_t)((double)R * (double)W / (double)wsum)));
+        used += nb[(size_t)i];
+    }
+    std::priority_queue<std::pair<double, int>> q;   // (tiles per block, graph)
+    for (int i = 0; i < ng; ++i)
+        if (gs[i]->fused && nb[(size_t)i] < cap[(size_t)i])
+            q.push({(double)gs[i]->n_wt / (double)nb[(size_t)i], i});
+    while (used < R && !q.empty()) {
+        const int i = q.top().second;
+        q.pop();
+        ++nb[(size_t)i];
+        ++used;
+        if (nb[(size_t)i] < cap[(size_t)i]) q.push({(double)gs[i]->n_wt / (double)nb[(size_t)i], i});
+    }
+    return nb;
+}
 static int fused_blocks(mr_ctx* ctx, mr_graph* g, const FxPlan& P, int64_t wsum, int64_t* nfa,
                         std::vector<CutArg>* defer = nullptr, int64_t force_nb = 0) {
     return tr_split(ctx, g, P, wsum, nfa, defer, force_nb);
@@ -4391,11 +4443,12 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
     for (int i = 0; i < ng; ++i)
         if (gs[i]->fused) wsum += gs[i]->n_wt;
     std::vector<CutArg> cuts;   // the graphs' per-wave cuts, launched together
+    const std::vector<int64_t> nbs = batch_blocks(gs, ng, plan, wsum);
     for (int i = 0; i < ng; ++i) {
         mr_graph* g = gs[i];
         if (g->fused) {   // the plan's blocks: partial rows and (k_tr_a) the per-wave cut
             int64_t nfa = 0;
-            MR_TRY(fused_blocks(ctx, g, plan, wsum, &nfa, &cuts));
+            MR_TRY(fused_blocks(ctx, g, plan, wsum, &nfa, &cuts, nbs.empty() ? 0 : nbs[(size_t)i]));
             MR_TRY(g->fx_part.alloc(ctx, (size_t)std::max<int64_t>(nfa, 1) * (size_t)kern_n(g)));
         }
     }
@@ -4491,7 +4544,7 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         // a shard without traces still runs one (empty) block: it clears the maxima slot and
         // writes a zero partial row, and the collectives after the launch need every rank
         int64_t nfa = 0;
-        if (g->fused) MR_TRY(fused_blocks(ctx, g, plan, wsum, &nfa));
+        if (g->fused) MR_TRY(fused_blocks(ctx, g, plan, wsum, &nfa, nullptr, nbs.empty() ? 0 : nbs[(size_t)i]));
         nfa = g->fused ? std::max<int64_t>(nfa, sharded ? 1 : 0) : 0;
         // a row entry stays below 2^64 (traces per block < 2^(64-sc)).  Shards of one graph hold
         // different trace counts and their limbs are summed, so they share one scale, 2^48 (<= 65535
@@ -4562,12 +4615,17 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         if (v.lds_su) lds = std::max(lds, ((size_t)g->N + VCAP) * sizeof(double));
         lds = std::max(lds, ((size_t)1 << g->tshift) * (fp32 ? sizeof(float) : sizeof(double)));
     }
-    DBuf<GDev> dv;
-    hm.mark("descr");
-    MR_TRY(dv.upload(ctx, hv.data(), hv.size()));
     const int32_t split_fa = ng == 2 ? hv[1].blk0f : 0, split_fb = ng == 2 ? hv[1].blk0fb : 0;
     for (int i = 0; i < ng; ++i)
         if (gs[i]->fused) lds_f = std::max(lds_f, plan_lds(kern_n(gs[i]), plan));
+    {   // last-block graphs: a launch that fits one block per CU runs so (LDS past half a CU), and its
+        // finishing blocks skip the acquire (tr_last_finish); else they take it
+        bool any_lf = false;
+        for (int i = 0; i < ng; ++i) any_lf = any_lf || hv[(size_t)i].lastfin;
+        const bool one_cu = LF_ONE_CU_LDS > 0 && any_lf && blocks_fa <= num_cus() && LF_ONE_CU_LDS <= WV_LDS_MAX;
+        if (one_cu) lds_f = std::max(lds_f, LF_ONE_CU_LDS);
+        for (int i = 0; i < ng; ++i) hv[(size_t)i].lf_acq = one_cu ? 0 : 1;
+    }
     for (int i = 0; i < ng; ++i)   // hot-op layouts need every op's su in LDS (a batch with a much wider graph)
         if (gs[i]->fused && gs[i]->nhr && plan.mode != WV_SU_ALL)
             return mr_fail(ctx, MR_ERR_ARG, "pagerank batch: a hot-op layout (T >= MR_TR_HOT_MIN) with a graph of > %d ops",
@@ -4581,6 +4639,9 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         if ((any_ext & 2) && gs[i]->fused && gs[i]->nhr > HOT_MAX_WIDE)
             return mr_fail(ctx, MR_ERR_ARG, "pagerank batch: a hot-op layout of %d ops beside a wide graph", gs[i]->nhr);
     const TrA tr_a = tr_kernel(fp32, plan.mode, plan.NT, any_ext);
+    DBuf<GDev> dv;
+    hm.mark("descr");
+    MR_TRY(dv.upload(ctx, hv.data(), hv.size()));
     // a sharded graph with no collective backend is one whole shard: the split launches around the
     // (no-op) all-reduces would compute the same integers / sums in two halves
     const bool coll = sharded && mr_coll_ready(ctx);
