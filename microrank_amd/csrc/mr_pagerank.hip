@@ -1791,6 +1791,8 @@ struct GDev {
     int32_t blk0f, n_fa, blk0fb, n_fb;   // fused path: k_tr_a / k_fx_b block ranges
     int32_t fb_ops;                      // k_fx_b ops per block
     int32_t lastfin;                     // k_tr_a's last block of the graph finishes the iteration (no k_fx_b)
+    int32_t pf;                          // k_tr_a(it) first finishes iteration it - 1 itself (no k_fx_b between)
+    int64_t pf_stride;                   // pf: words of one partial-row buffer (rows and terms double-buffered)
     int32_t lf_acq;                      // lastfin: the finishing block takes an agent acquire (else the launch
                                          // runs one workgroup per CU and the sc1 hand-off of the guide's row 1 holds)
     int32_t ssv_pre;                     // k_tr_a's blocks compute the call-graph terms (fx_ssv) for k_fx_b
@@ -2053,13 +2055,14 @@ enum { WV_SU_GLOBAL = 0, WV_SU_ALL = 1, WV_SU_HOT = 2 };
 // (sequential: deterministic), one LDS u64 atomic of the lane's X_t (integers: order-free).  The
 // block synchronises only to clear the accumulator and to write its partial row.
 struct TrLds {
-    size_t su, lacc, hs, total;
+    size_t su, lacc, hs, sp, total;
     bool su_lds;      // every op's su fits beside the accumulator (interleaved: 16 B per op)
     bool hot_ok;      // WV_SU_ALL: the hot-op mask sums (256 doubles) fit too
     int32_t n_hot;    // WV_SU_HOT: su of ops [0, n_hot) in LDS
     // the accumulator first, then su (8-B strides: a 32-lane read group spreads over 32 bank
     // pairs, a 16-lane atomic group over 16)
-    __host__ __device__ TrLds(int32_t N, int mode) {
+    // pf (every op's su in LDS only): s itself beside su (the launch finished the previous iteration)
+    __host__ __device__ TrLds(int32_t N, int mode, bool pf = false) {
         const size_t ns = (size_t)N + TR_PAD;
         su_lds = ns * 16 <= WV_LDS_MAX;
         const bool all = mode == WV_SU_ALL && su_lds;
@@ -2070,6 +2073,8 @@ struct TrLds {
         lacc = 0;
         su = accb;
         total = all ? 2 * accb : accb + (size_t)n_hot * 8;
+        sp = total;
+        if (pf && all) total += accb;
         hs = total;
         hot_ok = all && total + 256 * 8 <= WV_LDS_MAX;
         if (hot_ok) total += 256 * 8;
@@ -2455,7 +2460,10 @@ __device__ __forceinline__ double tr_walk(const GDev& G, int32_t lb, int cur, in
 // loads (ss_off -> ss_par -> pw, s_k) then run in the slack of the block's slowest wave, not in
 // k_fx_b's critical path.  The same arithmetic as k_fx_b (a lane per column of <= 8 parents with
 // wave_sum's butterfly value, a wave per column of more): fx_ssv[o], read there bitwise.
-__device__ __forceinline__ void tr_ssv_share(const GDev& G, int32_t lb, int cur, double Ms, int* ctr, int lane) {
+// (pf: s_k from the block's LDS copy spl -- this launch computed it -- and the terms into buffer
+// it & 1 of fx_ssv, read by the next launch's prologue or the final k_fx_b)
+__device__ __forceinline__ void tr_ssv_share(const GDev& G, int32_t lb, int cur, double Ms, int* ctr, int lane,
+                                             const double* spl = nullptr, int64_t ssv_off = 0) {
     const int32_t N = G.N;
     const int32_t oa = (int32_t)((int64_t)lb * N / G.n_fa), ob = (int32_t)((int64_t)(lb + 1) * N / G.n_fa);
     for (;;) {
@@ -2469,7 +2477,8 @@ __device__ __forceinline__ void tr_ssv_share(const GDev& G, int32_t lb, int cur,
         const GLB int64_t* ss_off = gp(G.ss_off);
         const GLB int32_t* ss_par = gp(G.ss_par);
         const GLB float* pw = gp(G.pw);
-        const GLB double* sp = gp(G.spb[cur]);
+        const GLB double* spg = gp(G.spb[cur]);
+        auto sp = [&](int32_t p) -> double { return spl ? spl[p] : spg[p]; };
         double ssv = 0.0;
         bool big = false;
         if (on) {
@@ -2480,7 +2489,7 @@ __device__ __forceinline__ void tr_ssv_share(const GDev& G, int32_t lb, int cur,
                 for (int k = 0; k < 8; ++k) pp[k] = e0 + k < e1 ? ss_par[e0 + k] : -1;
                 double t[8];
 #pragma unroll
-                for (int k = 0; k < 8; ++k) t[k] = pp[k] >= 0 ? (double)pw[pp[k]] * sp[pp[k]] : 0.0;
+                for (int k = 0; k < 8; ++k) t[k] = pp[k] >= 0 ? (double)pw[pp[k]] * sp(pp[k]) : 0.0;
                 const double bb = ((t[0] + t[4]) + (t[2] + t[6])) + ((t[1] + t[5]) + (t[3] + t[7]));
                 ssv = G.alpha * (bb / Ms);
             } else {
@@ -2494,7 +2503,7 @@ __device__ __forceinline__ void tr_ssv_share(const GDev& G, int32_t lb, int cur,
             double bb = 0.0;
             for (int64_t e = e0 + lane; e < e1; e += WAVE) {
                 const int32_t pp = ss_par[e];
-                bb += (double)pw[pp] * sp[pp];
+                bb += (double)pw[pp] * sp(pp);
             }
             bb = wave_sum(bb);
             if (lane == j) ssv = G.alpha * (bb / Ms);
@@ -2504,7 +2513,7 @@ __device__ __forceinline__ void tr_ssv_share(const GDev& G, int32_t lb, int cur,
                 __hip_atomic_store(gpw((unsigned long long*)G.fx_ssv) + o, (unsigned long long)__double_as_longlong(ssv),
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             else
-                G.fx_ssv[o] = ssv;
+                G.fx_ssv[ssv_off + o] = ssv;
         }
     }
 }
@@ -2631,17 +2640,59 @@ __global__ void __launch_bounds__(NT, NT == 512 && EXT == 0 && SUM != WV_SU_HOT 
     const int cur = it & 1, nxt = cur ^ 1, k3 = it % 3;
     const int32_t N = G.NA;   // (wide graphs: the hot ops)
     const int32_t tid = (int32_t)threadIdx.x;
-    const TrLds L_(N, SUM);
+    // pf (window batches, 512-thread variant): k_fx_b's finish of the previous iteration runs here,
+    // in every block of the graph (below), so an iteration is one launch
+    const bool pf = NT == 512 && SUL && EXT == 0 && G.pf;
+    const TrLds L_(N, SUM, pf);
     const int32_t NH = HOT ? G.n_hot : 0;   // <= L_.n_hot (the host sizes both alike), >= 64
     const GLB double* sug = gp(G.sub[cur]);   // ids >= N are pads (su 0)
     double* su_l = (double*)(lraw + L_.su);
+    double* sp_l = (double*)(lraw + L_.sp);   // (pf) s_it itself, for the call-graph terms
     unsigned long long* lacc = (unsigned long long*)(lraw + L_.lacc);
     GLB unsigned long long* mslot = gpw(G.mslot);
-    const GLB unsigned long long* Mcur = mslot + (size_t)2 * MSH * k3;
+    GLB unsigned long long* Mcur = mslot + (size_t)2 * MSH * k3;
     GLB unsigned long long* Mnext = mslot + (size_t)2 * MSH * ((k3 + 1) % 3);
     if (lb == 0 && tid < 2 * MSH) mslot[(size_t)2 * MSH * ((k3 + 2) % 3) + tid] = 0ull;
-    if (SUL)
+    double pf_max = -__builtin_huge_val();
+    if (pf && it > 0) {
+        // s_it[o] = d (S_o 2^-SC + alpha (P_ss s_{it-1})[o] / M_s(it-1)) from the previous launch's
+        // partial rows and call-graph terms (buffers (it - 1) & 1): k_fx_b's exact limb sums and its
+        // expression, so bitwise k_fx_b's values; every block of the graph computes all N of them
+        // (a few rows each) -- block 0 also publishes s_it and M_s(it) for the final k_fx_b
+        const int pb = (it - 1) & 1;
+        const GLB unsigned long long* rows = gp((const unsigned long long*)G.fx_part) + (size_t)pb * G.pf_stride;
+        const GLB double* ssvp = gp(G.fx_ssv) + (size_t)pb * N;
+        const GLB float* u_o = gp(G.u_o);
+        const double iscale = G.dscale ? G.dscale[1] : G.fx_iscale;
+        const int32_t nb = G.n_fa;
+        GLB double* spo = gpw(G.spb[cur]);
+        for (int32_t o = tid; o < N + TR_PAD; o += NT) {
+            if (o < N) {
+                unsigned long long lo = 0ull, hi = 0ull;
+                for (int32_t b = 0; b < nb; ++b) {
+                    const unsigned long long v = rows[(size_t)b * N + o];
+                    lo += v & 0xffffffffull;
+                    hi += v >> 32;
+                }
+                const double sum = ((double)hi * 4294967296.0 + (double)lo) * iscale;
+                const double v = d * (sum + ssvp[o]);   // pagerank.py:122-124
+                sp_l[o] = v;
+                su_l[o] = (double)u_o[o] * v;
+                pf_max = nmax(pf_max, v);
+                if (lb == 0) {
+                    spo[o] = v;
+                    atomicMax((unsigned long long*)&Mcur[o % MSH], d2bits(v));
+                }
+            } else {
+                su_l[o] = 0.0;
+                sp_l[o] = 0.0;
+            }
+        }
+    } else if (SUL) {
         for (int32_t o = tid; o < N + TR_PAD; o += NT) su_l[o] = o < N ? sug[o] : 0.0;
+        if (pf)
+            for (int32_t o = tid; o < N + TR_PAD; o += NT) sp_l[o] = o < N ? G.spb[cur][o] : 0.0;
+    }
     for (int32_t o = tid; o < N + TR_PAD; o += NT) lacc[o] = 0ull;
     if (HOT)
         for (int32_t o = tid; o < NH; o += NT) su_l[o] = sug[o];
@@ -2656,6 +2707,11 @@ __global__ void __launch_bounds__(NT, NT == 512 && EXT == 0 && SUM != WV_SU_HOT 
         }
     }
     __syncthreads();   // accumulator and maxima ready
+    if (pf && it > 0) {   // M_s(it): the maximum of the s_it just computed (block_max synchronises)
+        const double m = block_max(pf_max, red);
+        if (tid == 0) msh[0] = m;
+        __syncthreads();
+    }
     // hot ops (large graphs: the 1024-thread variant only) -- the mask sums of this iteration's su
     constexpr bool HOTT = SUL && NT == 1024;
     double* hs = (double*)(lraw + L_.hs);
@@ -2666,9 +2722,9 @@ __global__ void __launch_bounds__(NT, NT == 512 && EXT == 0 && SUM != WV_SU_HOT 
     const double xsc = (G.dscale ? G.dscale[0] : G.fx_scale) / msh[1], Ms = msh[0];
     const double rmax_w = tr_walk<Q, SUM, NT, EXT, HOTT>(G, lb, cur, nxt, N, NH, d, Ms, xsc, su_l, lacc, hs);
     // the call-graph terms of this block's share of the columns, by the waves done walking
-    if (G.ssv_pre) tr_ssv_share(G, lb, cur, Ms, &s_ssv, tid & (WAVE - 1));
+    if (G.ssv_pre) tr_ssv_share(G, lb, cur, Ms, &s_ssv, tid & (WAVE - 1), pf ? sp_l : nullptr, pf ? (int64_t)cur * N : 0);
     __syncthreads();
-    GLB unsigned long long* prow = gpw(G.fx_part) + (size_t)lb * N;
+    GLB unsigned long long* prow = gpw(G.fx_part) + (pf ? (size_t)cur * G.pf_stride : 0) + (size_t)lb * N;
     if constexpr (NT == 512) {   // (window-graph variant only: the large graphs' kernel stays as it is)
         if (G.lastfin) {
             for (int32_t o = tid; o < N; o += NT)   // write-through: the last block reads them with sc1 loads
@@ -2715,6 +2771,8 @@ static int fb_ops(int32_t N, bool many) {
 }
 constexpr int64_t FB_MANY_BLOCKS = 1024;   // 16-op blocks of a launch from which "many" holds
 constexpr int64_t LASTFIN_WORDS = 32768;
+constexpr int32_t PF_NMAX = 1024;   // pf launches: ops per graph (three N-word LDS arrays per block)
+constexpr int64_t PF_ROWS = 16;     // pf launches: partial rows per graph every block of it sums
 #ifndef MR_LF_ONE_CU_LDS
 #define MR_LF_ONE_CU_LDS (80 * 1024 + 1024)   // (A/B builds: 0 = every last-block launch takes the acquire)
 #endif
@@ -2750,8 +2808,8 @@ __global__ void __launch_bounds__(WAVE * FB_W) k_fx_b(const GDev* __restrict__ g
     int32_t nbl = 0;
     size_t rs = 1;
     if (on && mode != 2) {
-        if (o < G.NA) {
-            col = gp((const unsigned long long*)G.fx_part) + o;
+        if (o < G.NA) {   // (pf graphs: the final iteration's rows, buffer it & 1)
+            col = gp((const unsigned long long*)G.fx_part) + (G.pf ? (size_t)(it & 1) * G.pf_stride : 0) + o;
             nbl = nb;
             rs = (size_t)G.NA;
         } else {
@@ -2772,7 +2830,8 @@ __global__ void __launch_bounds__(WAVE * FB_W) k_fx_b(const GDev* __restrict__ g
     // thousands of parents costs one wave, not one thread).  (Not in mode 1: its sums only.)
     // ssv_pre: k_tr_a computed them (tr_ssv_share) -- one coalesced load
     if (mode != 1 && G.ssv_pre) {
-        if (threadIdx.x < (unsigned)OPB) lssv[threadIdx.x] = o0 + (int32_t)threadIdx.x < N ? G.fx_ssv[o0 + threadIdx.x] : 0.0;
+        if (threadIdx.x < (unsigned)OPB)
+            lssv[threadIdx.x] = o0 + (int32_t)threadIdx.x < N ? G.fx_ssv[(G.pf ? (size_t)(it & 1) * N : 0) + o0 + threadIdx.x] : 0.0;
     } else if (mode != 1) {
         const double Ms = wave_max(bits2d(G.mslot[(size_t)2 * MSH * k3c + lane]));
         const GLB double* sp_cur = gp(G.spb[it & 1]);
@@ -3284,6 +3343,7 @@ struct FxPlan {
     int NT = 1024;      // block size (16 waves; 512 when the graphs are small)
     int mode = WV_SU_ALL;   // su in LDS for every fused graph of the batch / hot ops / none
     bool sul = true;    // mode == WV_SU_ALL
+    bool pf = false;    // window batches: the next launch finishes an iteration (k_tr_a's pf prologue)
 };
 static FxPlan fx_plan(mr_graph* const* gs, int ng) {
     FxPlan P;
@@ -3312,7 +3372,7 @@ static FxPlan fx_plan(mr_graph* const* gs, int ng) {
 static int32_t plan_n_hot(int32_t N, const FxPlan& P) {
     return P.mode == WV_SU_HOT ? TrLds(N, WV_SU_HOT).n_hot : 0;
 }
-static size_t plan_lds(int32_t N, const FxPlan& P) { return TrLds(N, P.mode).total; }
+static size_t plan_lds(int32_t N, const FxPlan& P) { return TrLds(N, P.mode, P.pf).total; }
 
 // resident blocks of the plan's kernel on the chip (occupancy by LDS image and VGPRs)
 static int64_t plan_resident(int32_t N, const FxPlan& P) {
@@ -4413,7 +4473,7 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
     MR_TRY_HIP(ctx, hipSetDevice(ctx->device));
     hipStream_t st = ctx->stream;
     const bool fp32 = precision == MR_FP32;
-    const FxPlan plan = fx_plan(gs, ng);
+    FxPlan plan = fx_plan(gs, ng);
     std::vector<unsigned char> setup_h;   // (batched set-up descriptors: alive until the call's final sync)
     DBuf<SDev> setup_d;
     {   // set-up of every graph not set up ahead (mr_pagerank_presetup): batched when they allow it
@@ -4439,6 +4499,18 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         }
     }
     hm.mark("setup");
+    {   // window batches: the next launch's blocks finish an iteration (k_tr_a pf), no k_fx_b between
+        // launches -- every graph fused and plain (no multiplicities, cold sums, merged runs, hot
+        // ops or relabelling), N <= PF_NMAX (three N-word LDS arrays, four blocks per CU).
+        // MR_TR_PF=0 (read per call; A/B and tests): k_fx_b every iteration
+        const char* pe = getenv("MR_TR_PF");
+        plan.pf = !(pe && atoi(pe) == 0) && !sharded && ng >= 2 && plan.NT == 512 && plan.mode == WV_SU_ALL;
+        for (int i = 0; i < ng && plan.pf; ++i) {
+            const mr_graph* g = gs[i];
+            plan.pf = g->fused && !g->wide && !g->relabeled && !g->nhr && !g->mw_tp.p && kern_n(g) <= PF_NMAX &&
+                      !(g->lo && g->lo_merged == 1);
+        }
+    }
     int64_t wsum = 0;   // wave tiles of the launch's fused graphs (k_tr_a's block budget)
     for (int i = 0; i < ng; ++i)
         if (gs[i]->fused) wsum += gs[i]->n_wt;
@@ -4449,7 +4521,9 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         if (g->fused) {   // the plan's blocks: partial rows and (k_tr_a) the per-wave cut
             int64_t nfa = 0;
             MR_TRY(fused_blocks(ctx, g, plan, wsum, &nfa, &cuts, nbs.empty() ? 0 : nbs[(size_t)i]));
-            MR_TRY(g->fx_part.alloc(ctx, (size_t)std::max<int64_t>(nfa, 1) * (size_t)kern_n(g)));
+            // (pf: rows and call-graph terms double-buffered, iteration it & 1)
+            MR_TRY(g->fx_part.alloc(ctx, (size_t)(plan.pf ? 2 : 1) * std::max<int64_t>(nfa, 1) * (size_t)kern_n(g)));
+            if (plan.pf) MR_TRY(g->fx_ssv.alloc(ctx, 2 * (size_t)g->N));
         }
     }
     hm.mark("blocks");
@@ -4597,6 +4671,9 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         // block writes its share write-through and the last block reads the terms with one load per
         // op instead of the ss_off -> ss_par -> pw / s_k chain (MR_TR_LFSSV=0: the chain; read per call)
         v.ssv_pre = ssv_on && nfa >= 1 && !g->wide && ((v.n_fb > 0 && g->N >= 2048) || (v.lastfin && lfssv_on));
+        v.pf = plan.pf && !v.lastfin && nfa <= PF_ROWS;
+        v.pf_stride = nfa * (int64_t)kern_n(g);
+        if (v.pf) v.ssv_pre = 1;   // (the next launch's prologue reads the terms: one load per op)
         v.row_wt = row_wt_on && g->N >= 2048;
         blocks_fb += v.n_fb;
         v.blk0 = blocks_a;
@@ -4638,6 +4715,14 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
     for (int i = 0; i < ng; ++i)   // the wide variant carries HOT_MAX_WIDE hot accumulators
         if ((any_ext & 2) && gs[i]->fused && gs[i]->nhr > HOT_MAX_WIDE)
             return mr_fail(ctx, MR_ERR_ARG, "pagerank batch: a hot-op layout of %d ops beside a wide graph", gs[i]->nhr);
+    bool launch_pf = plan.pf;   // every graph finishes in-kernel: no k_fx_b before the last iteration
+    for (int i = 0; i < ng; ++i) launch_pf = launch_pf && (hv[(size_t)i].lastfin || hv[(size_t)i].pf);
+    launch_pf = launch_pf && any_ext == 0;
+    if (!launch_pf)
+        for (int i = 0; i < ng; ++i) {
+            if (hv[(size_t)i].pf) hv[(size_t)i].ssv_pre = ssv_on && !gs[i]->wide && gs[i]->N >= 2048;
+            hv[(size_t)i].pf = 0;
+        }
     const TrA tr_a = tr_kernel(fp32, plan.mode, plan.NT, any_ext);
     DBuf<GDev> dv;
     hm.mark("descr");
@@ -4719,7 +4804,9 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
                                        it, mode, p);
             };
             if (!coll) {
-                if (blocks_fb) fx_b(0, px_off);   // (none: every graph finished by its last k_tr_a block)
+                // (none: every graph finished by its last k_tr_a block; pf launches: the next k_tr_a
+                // finishes this iteration, k_fx_b only after the last one)
+                if (blocks_fb && (!launch_pf || it == iters - 1)) fx_b(0, px_off);
             } else if (px_on) {   // the exchange fused into k_fx_b: push in mode 1, per-block waits in mode 2
                 fx_b(1, px);
                 if (!px.spin) MR_TRY(mr_peer_fx_wait(ctx, px, blocks_fb));

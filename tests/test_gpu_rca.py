@@ -879,18 +879,20 @@ def test_c2_windows_batch_groupings_agree(c2_batch, monkeypatch):
     table) rank bitwise as the default -- build-side choices, the PageRank launches untouched; and
     PageRank groups of 4 and 2 windows (MR_WIN_GROUP) rank bitwise too: a group's block budget
     changes how a graph's tiles are cut into blocks, but the fixed-point scale of X_t is one
-    constant (FX_SC), so the exact limb sums -- and a window's scores -- do not depend on the batch.  The run-merged walk (MR_TR_MERGE=1: a run of
+    cut-independent constant (tr_scfix), so the exact limb sums -- and a window's scores -- do not depend on the batch.
+    k_fx_b every iteration (MR_TR_PF=0) instead of the next k_tr_a launch finishing the iteration in
+    its prologue ranks bitwise as the default: the same limb sums and expressions.  The run-merged walk (MR_TR_MERGE=1: a run of
     identical traces shares one id rotation and its head walks for it with X times the run length;
     the bench's side leg, never the headline) ranks bitwise as every lane walking its own trace in
     the same run rotations (MR_TR_MERGE=2): the merge is exact; against the default (a rotation per
     trace: each trace's sum in another order) the scores agree to 1e-12."""
     from microrank_amd.online_rca import rank_windows
 
-    knobs = ("MR_WIN_GROUP", "MR_WIN_CHUNK", "MR_IX_EPT", "MR_DET_FUSE_MAX", "MR_NO_DET_FUSE", "MR_TR_MERGE")
+    knobs = ("MR_WIN_GROUP", "MR_WIN_CHUNK", "MR_IX_EPT", "MR_DET_FUSE_MAX", "MR_NO_DET_FUSE", "MR_TR_MERGE", "MR_TR_PF")
     ctx, _, wins = c2_batch
     variants = {"default": {}, "chunk1_ept16": {"MR_WIN_CHUNK": "1", "MR_IX_EPT": "16"},
                 "chunk2_fused": {"MR_WIN_CHUNK": "2", "MR_DET_FUSE_MAX": "100000000"},
-                "merge": {"MR_TR_MERGE": "1"}, "runrot": {"MR_TR_MERGE": "2"},
+                "merge": {"MR_TR_MERGE": "1"}, "runrot": {"MR_TR_MERGE": "2"}, "nopf": {"MR_TR_PF": "0"},
                 "group4_chunk4": {"MR_WIN_GROUP": "4", "MR_WIN_CHUNK": "4"}, "group2": {"MR_WIN_GROUP": "2"}}
     runs = {}
     for name, env in variants.items():
