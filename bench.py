@@ -857,9 +857,24 @@ def run_dropin(args):
 
     import pandas as pd
 
+    from microrank_amd import online_rca as orca
     from microrank_amd import synth
     from microrank_amd.online_rca import _window_loop
     from microrank_amd.preprocess_data import get_operation_slo, get_service_operation_list
+
+    # the window body's calls (online_rca.py:167-201), each timed on the host: the phase table
+    phase_names = ("system_anomaly_detect", "get_pagerank_graph", "trace_pagerank",
+                   "calculate_spectrum_without_delay_list", "_write_result")
+    phase_ms = {}
+
+    def timed(name, fn):
+        def w(*a, **k):
+            ts = time.perf_counter()
+            try:
+                return fn(*a, **k)
+            finally:
+                phase_ms[name] = phase_ms.get(name, 0.0) + (time.perf_counter() - ts) * 1e3
+        return w
 
     sizes = {"C1": (40, 2000, 100), "C2": (args.ops, args.traces, 1234)}
     lines = {}
@@ -888,9 +903,26 @@ def run_dropin(args):
                     with contextlib.redirect_stdout(io.StringIO()):
                         _window_loop(adf, slo, op_list, start, one)
                 dt = (time.perf_counter() - ts) / n
+                # the phase table: the same windows again with each drop-in call timed
+                orig = {k: getattr(orca, k) for k in phase_names}
+                phase_ms.clear()
+                try:
+                    for k in phase_names:
+                        setattr(orca, k, timed(k, orig[k]))
+                    ts = time.perf_counter()
+                    for _ in range(n):
+                        with contextlib.redirect_stdout(io.StringIO()):
+                            _window_loop(adf, slo, op_list, start, one)
+                    dt_p = (time.perf_counter() - ts) / n
+                finally:
+                    for k in phase_names:
+                        setattr(orca, k, orig[k])
+                phases = {k: round(phase_ms.get(k, 0.0) / n, 3) for k in phase_names}
+                phases["other (loop, prints)"] = round(dt_p * 1e3 - sum(phases.values()), 3)
                 lines[name] = {"windows_per_s": round(1.0 / dt, 3), "ms_per_window": round(dt * 1e3, 3),
                                "first_window_ms": round(first_ms, 1), "ranked": ranked,
-                               "spans": int(len(adf)), "traces": int(adf["traceID"].nunique()), "ops": n_ops}
+                               "spans": int(len(adf)), "traces": int(adf["traceID"].nunique()), "ops": n_ops,
+                               "phase_ms_per_window": phases}
                 del ndf, adf
         finally:
             os.chdir(cwd)
@@ -1203,6 +1235,8 @@ def main():
         if dist is not None:
             dist.barrier()
 
+    step_times = []   # (batch mode) wall time of each step of the last run_all, ms
+
     def run_all(n):
         """n steps; (edges, windows, the first window's last result).  c2: a step is W windows;
         c3: a step is the rank's share of the batch."""
@@ -1212,7 +1246,9 @@ def main():
             pool = wins[0]
             per_step = share if share is not None else W   # c2: W windows, cycling the distinct ones
             res, first = [], None
+            step_times.clear()
             for _ in range(n):
+                ts_step = time.perf_counter()   # (each call returns its results: synchronous)
                 for c0 in range(0, per_step, W):   # c3: calls of <= W windows
                     idx = range(c0, min(per_step, c0 + W))
                     out = rank_windows(ctx, [pool[j % len(pool)][:5] for j in idx],
@@ -1223,6 +1259,7 @@ def main():
                         res.append(e_)
                         if j % len(pool) == 0:
                             first = (e_, codes, scores, na_, nn_)
+                step_times.append((time.perf_counter() - ts_step) * 1e3)
             return sum(res), len(res), first
 
         def one(ci):
@@ -1308,6 +1345,8 @@ def main():
                                    f"iteration's launches)") if batch
                                   else f"windows x{world} ranks x{W} streams"},
         "windows_per_s": round(win_all / elapsed, 3),
+        "step_ms": ({"min": round(min(step_times), 3), "median": round(sorted(step_times)[len(step_times) // 2], 3),
+                     "max": round(max(step_times), 3)} if step_times else None),
         "roofline": {"bound": "hbm", "kernel": ("one Jacobi iteration of a window group's graphs: the "
                                                 "k_tr_a (+ k_fx_b) launch(es) over the graphs of one group (c2: 256 graphs of 128 "
                                                 "windows; c3: 256 graphs of 128, one launch per iteration: the last "

@@ -695,7 +695,17 @@ static int win_aux(mr_ctx* ctx, int n) {
         mr_ctx* a = nullptr;
         const int rc = mr_ctx_create(ctx->device, ctx->flags, &a);
         if (rc != MR_OK) return mr_fail(ctx, rc, "mr_windows_batch: auxiliary context creation failed");
-        ctx->aux.push_back(a);   // (same stream priority as the PageRank stream: high priority measured C2 -4 %)
+        // MR_WIN_AUX_PRIO=low (A/B, read when the auxiliary contexts are made): their streams below
+        // the PageRank stream's priority (a high-priority PageRank stream measured C2 -4 % in round 4)
+        const char* pe = getenv("MR_WIN_AUX_PRIO");
+        int lo = 0, hi = 0;
+        hipStream_t s2 = nullptr;
+        if (pe && !strcmp(pe, "low") && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess && lo != hi &&
+            hipStreamCreateWithPriority(&s2, hipStreamNonBlocking, lo) == hipSuccess) {
+            (void)hipStreamDestroy(a->stream);
+            a->stream = s2;
+        }
+        ctx->aux.push_back(a);
     }
     return MR_OK;
 }
