@@ -695,16 +695,9 @@ static int win_aux(mr_ctx* ctx, int n) {
         mr_ctx* a = nullptr;
         const int rc = mr_ctx_create(ctx->device, ctx->flags, &a);
         if (rc != MR_OK) return mr_fail(ctx, rc, "mr_windows_batch: auxiliary context creation failed");
-        // MR_WIN_AUX_PRIO=low (A/B, read when the auxiliary contexts are made): their streams below
-        // the PageRank stream's priority (a high-priority PageRank stream measured C2 -4 % in round 4)
-        const char* pe = getenv("MR_WIN_AUX_PRIO");
-        int lo = 0, hi = 0;
-        hipStream_t s2 = nullptr;
-        if (pe && !strcmp(pe, "low") && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess && lo != hi &&
-            hipStreamCreateWithPriority(&s2, hipStreamNonBlocking, lo) == hipSuccess) {
-            (void)hipStreamDestroy(a->stream);
-            a->stream = s2;
-        }
+        // (the build streams at the PageRank stream's priority: a high-priority PageRank stream
+        // measured C2 -4 % in round 4, low-priority build streams within the spread in round 6,
+        // profiles/r06/r06h_serial_priority_ab.txt)
         ctx->aux.push_back(a);
     }
     return MR_OK;
@@ -1028,26 +1021,19 @@ extern "C" int mr_windows_batch(mr_ctx* ctx, int32_t n_windows, const mr_spans* 
     const char* see = getenv("MR_WIN_SPEC_EARLY");
     const bool spec_early = inl && !(see && atoi(see) == 0);
     int settled = 0;   // groups whose spectra are queued
-    // MR_WIN_SERIAL=1 (A/B, read per call): the first group's PageRanks wait for EVERY window's build,
-    // so no build runs beside an iteration
-    const char* sre = getenv("MR_WIN_SERIAL");
-    const bool serial = sre && atoi(sre) != 0 && ngroups > 1;
+    // (the next group's builds run beside a group's iterations: the iterations run ~20 % slower
+    // than alone, but a call that builds every window before the first iterations ranked 3.5 %
+    // fewer windows per second, profiles/r06/r06h_serial_priority_ab.txt)
     for (int g = 0; g < ngroups && rc == MR_OK; ++g) {
         const int32_t i0 = gbeg[(size_t)g], i1 = gbeg[(size_t)g + 1];
-        const int gw_last = serial && g == 0 ? ngroups - 1 : g;   // groups whose builds this one waits for
         {
             std::unique_lock<std::mutex> lk(mu);
             WinPhase ph(5);
-            cv_done.wait(lk, [&] {
-                for (int h = g; h <= gw_last; ++h)
-                    if (built[(size_t)h] != gbeg[(size_t)h + 1] - gbeg[(size_t)h]) return false;
-                return true;
-            });
+            cv_done.wait(lk, [&] { return built[(size_t)g] == i1 - i0; });
         }
         mr_ctx* pc = pr_ctx(g);
-        const int32_t iw1 = gbeg[(size_t)gw_last + 1];
         for (size_t c = 0; c < chunks.size(); ++c)   // the group's chunks' graphs are ready
-            if (chunks[c].first >= i0 && chunks[c].first < iw1 && cw[c].ev &&
+            if (chunks[c].first >= i0 && chunks[c].first < i1 && cw[c].ev &&
                 hipStreamWaitEvent(pc->stream, cw[c].ev, 0) != hipSuccess)
                 rc = mr_fail(ctx, MR_ERR_HIP, "mr_windows_batch: hipStreamWaitEvent failed");   // (threads joined below)
         if (rc != MR_OK) break;
