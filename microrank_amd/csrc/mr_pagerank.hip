@@ -3515,8 +3515,8 @@ static std::vector<int64_t> batch_blocks(mr_graph* const* gs, int ng, const FxPl
     int64_t R = INT64_MAX;
     for (int i = 0; i < ng; ++i)
         if (gs[i]->fused) R = std::min(R, plan_resident(kern_n(gs[i]), P));
-    if (const char* oe = getenv("MR_TR_OVERSUB"))   // (A/B, read per call) blocks per resident slot
-        R = (int64_t)((double)R * std::max(1.0, atof(oe)));
+    // (two or three blocks per resident slot measured 2-3 % faster per iteration inside the pipeline
+    // and within the wall-time spread, profiles/r06/r06i_oversub_ab.txt: one set kept)
     const int64_t NW = P.NT / WAVE;
     nb.assign((size_t)ng, 0);
     std::vector<int64_t> cap((size_t)ng, 0);
