@@ -27,10 +27,17 @@ if has prof; then
 fi
 for c in c3 c4 c5; do
   if has $c; then
-    timeout -k 10 600 python3 bench.py --config $c --no-cpu > ${O}_$c.json 2> ${O}_$c.err || { tail -5 ${O}_$c.err; exit 1; }
+    timeout -k 10 600 python3 bench.py --config $c > ${O}_$c.json 2> ${O}_$c.err || { tail -5 ${O}_$c.err; exit 1; }
     cut -c1-500 ${O}_$c.json
   fi
 done
+if has dropin; then
+  timeout -k 10 400 python3 bench.py --config dropin > ${O}_dropin.json 2> ${O}_dropin.err || { tail -5 ${O}_dropin.err; exit 1; }
+  cut -c1-400 ${O}_dropin.json
+fi
+if has pmc; then
+  bash scripts/pmc_c2.sh r06${TAG} k_tr_a > ${O}_pmc.txt 2>&1 || { tail -5 ${O}_pmc.txt; exit 1; }
+fi
 if has c4s8; then
   bash scripts/prof_bench.sh r06${TAG}_c4s8 --config c4 --no-cpu --shard-of 8 --steps 10 --warmup 2 > /dev/null || exit 1
 fi
