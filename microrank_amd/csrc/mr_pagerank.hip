@@ -18,6 +18,7 @@
 // sum_t w_t (r'_t / M_r) is evaluated as (sum_t w_t r'_t) / M_r.  Every float reduction has a
 // fixed order (no float atomics), so results are bitwise reproducible run to run.
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdlib>
@@ -4887,9 +4888,10 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         unsigned long long* barp = pbar.p;
         unsigned long long tmo = 200ull * 100000ull;   // 200 ms of s_memrealtime (100 MHz)
         void* args[] = {(void*)&dvp, (void*)&ngv, (void*)&splv, (void*)&dv_, (void*)&itv, (void*)&barp, (void*)&tmo};
+        const void* kp = fp32 ? (const void*)k_tr_p<float> : (const void*)k_tr_p<double>;
+        (void)hipFuncSetAttribute(kp, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_f);
         mr_prof_begin(ctx);
-        const hipError_t ce = hipLaunchCooperativeKernel(fp32 ? (const void*)k_tr_p<float> : (const void*)k_tr_p<double>,
-                                                         dim3((unsigned)blocks_fa), dim3(512), args, (unsigned)lds_f, st);
+        const hipError_t ce = hipLaunchCooperativeKernel(kp, dim3((unsigned)blocks_fa), dim3(512), args, (unsigned)lds_f, st);
         if (ce == hipSuccess) {
             mr_prof_end(ctx, bytes * (double)iters, iters);
             MR_DEBUG_CHECK(ctx, "k_tr_p");
@@ -4897,6 +4899,10 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
             (void)hipGetLastError();
             mr_prof_end(ctx, 0.0, 0);
             persist = false;
+            static std::atomic<bool> said{false};
+            if (!said.exchange(true))
+                fprintf(stderr, "[microrank] persistent iteration launch not admitted (%s, %lld blocks, %zu B LDS): a launch per iteration\n",
+                        hipGetErrorString(ce), (long long)blocks_fa, lds_f);
         }
     }
     for (int it = 0; it < iters && !persist; ++it) {
