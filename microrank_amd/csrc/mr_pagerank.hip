@@ -2872,7 +2872,7 @@ static int fb_ops(int32_t N, bool many) {
 constexpr int64_t FB_MANY_BLOCKS = 1024;   // 16-op blocks of a launch from which "many" holds
 constexpr int64_t LASTFIN_WORDS = 32768;
 constexpr int32_t PF_NMAX = 1024;   // pf launches: ops per graph (three N-word LDS arrays per block)
-constexpr int64_t PF_ROWS = 16;     // pf launches: partial rows per graph every block of it sums
+constexpr int64_t PF_ROWS = 32;     // pf launches: partial rows per graph every block of it sums (C3 windows: up to 19)
 #ifndef MR_LF_ONE_CU_LDS
 #define MR_LF_ONE_CU_LDS (80 * 1024 + 1024)   // (A/B builds: 0 = every last-block launch takes the acquire)
 #endif
