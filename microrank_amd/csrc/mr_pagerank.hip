@@ -18,7 +18,6 @@
 // sum_t w_t (r'_t / M_r) is evaluated as (sum_t w_t r'_t) / M_r.  Every float reduction has a
 // fixed order (no float atomics), so results are bitwise reproducible run to run.
 #include <algorithm>
-#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdlib>
@@ -2464,7 +2463,7 @@ __device__ __forceinline__ double tr_walk(const GDev& G, int32_t lb, int cur, in
 // (pf: s_k from the block's LDS copy spl -- this launch computed it -- and the terms into buffer
 // it & 1 of fx_ssv, read by the next launch's prologue or the final k_fx_b)
 __device__ __forceinline__ void tr_ssv_share(const GDev& G, int32_t lb, int cur, double Ms, int* ctr, int lane,
-                                             const double* spl = nullptr, int64_t ssv_off = 0, bool wt = false) {
+                                             const double* spl = nullptr, int64_t ssv_off = 0) {
     const int32_t N = G.N;
     const int32_t oa = (int32_t)((int64_t)lb * N / G.n_fa), ob = (int32_t)((int64_t)(lb + 1) * N / G.n_fa);
     for (;;) {
@@ -2510,8 +2509,8 @@ __device__ __forceinline__ void tr_ssv_share(const GDev& G, int32_t lb, int cur,
             if (lane == j) ssv = G.alpha * (bb / Ms);
         }
         if (on) {
-            if (G.lastfin || wt)   // (write-through: the graph's last block / the next iteration reads it with sc1 loads)
-                __hip_atomic_store(gpw((unsigned long long*)G.fx_ssv) + ssv_off + o, (unsigned long long)__double_as_longlong(ssv),
+            if (G.lastfin)   // (write-through: the graph's last block reads it with sc1 loads)
+                __hip_atomic_store(gpw((unsigned long long*)G.fx_ssv) + o, (unsigned long long)__double_as_longlong(ssv),
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             else
                 G.fx_ssv[ssv_off + o] = ssv;
@@ -2628,26 +2627,12 @@ __device__ __forceinline__ void tr_last_finish(const GDev& G, int it, double d, 
 #ifndef MR_TR_WPE512
 #define MR_TR_WPE512 8   // minimum waves per SIMD asked of the plain 512-thread k_tr_a (A/B builds: 1)
 #endif
-// sc1 (L1-bypassing) loads and write-through stores of the persistent launch's hand-offs
-template <class T>
-__device__ __forceinline__ T ld_sc1(const T* p) {
-    if constexpr (sizeof(T) == 8) {
-        const unsigned long long v = __hip_atomic_load(gp((const unsigned long long*)p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        T r;
-        __builtin_memcpy(&r, &v, 8);
-        return r;
-    } else {
-        return __hip_atomic_load(gp(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-// One iteration of k_tr_a for the block blockIdx.x (the kernel below; PER: one iteration of the
-// persistent launch k_tr_p -- every graph pf, its hand-offs through sc1 loads and write-through
-// stores across the grid barrier between iterations, never a last-block finish)
-template <class Q, int SUM, int NT, int EXT, bool PER>
-__device__ __forceinline__ void tr_a_body(const GDev* __restrict__ gs, int32_t ng, int32_t split, double d, int it,
-                                          unsigned char* lraw) {
+template <class Q, int SUM, int NT, int EXT>
+__global__ void __launch_bounds__(NT, NT == 512 && EXT == 0 && SUM != WV_SU_HOT ? MR_TR_WPE512 : 1) k_tr_a(const GDev* __restrict__ gs, int32_t ng, int32_t split, double d,
+                                             double alpha, int it, int32_t unused) {
     constexpr bool SUL = SUM == WV_SU_ALL, HOT = SUM == WV_SU_HOT;
     constexpr int NW = NT / WAVE;
+    extern __shared__ __attribute__((aligned(16))) unsigned char lraw[];
     __shared__ double red[NW];
     __shared__ double msh[2];
     const GDev& G = gs[fx_graph(gs, ng, split, 2)];
@@ -2657,7 +2642,7 @@ __device__ __forceinline__ void tr_a_body(const GDev* __restrict__ gs, int32_t n
     const int32_t tid = (int32_t)threadIdx.x;
     // pf (window batches, 512-thread variant): k_fx_b's finish of the previous iteration runs here,
     // in every block of the graph (below), so an iteration is one launch
-    const bool pf = PER || (NT == 512 && SUL && EXT == 0 && G.pf);
+    const bool pf = NT == 512 && SUL && EXT == 0 && G.pf;
     const TrLds L_(N, SUM, pf);
     const int32_t NH = HOT ? G.n_hot : 0;   // <= L_.n_hot (the host sizes both alike), >= 64
     const GLB double* sug = gp(G.sub[cur]);   // ids >= N are pads (su 0)
@@ -2667,10 +2652,7 @@ __device__ __forceinline__ void tr_a_body(const GDev* __restrict__ gs, int32_t n
     GLB unsigned long long* mslot = gpw(G.mslot);
     GLB unsigned long long* Mcur = mslot + (size_t)2 * MSH * k3;
     GLB unsigned long long* Mnext = mslot + (size_t)2 * MSH * ((k3 + 1) % 3);
-    if (lb == 0 && tid < 2 * MSH) {
-        if (PER) __hip_atomic_store(mslot + (size_t)2 * MSH * ((k3 + 2) % 3) + tid, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else mslot[(size_t)2 * MSH * ((k3 + 2) % 3) + tid] = 0ull;
-    }
+    if (lb == 0 && tid < 2 * MSH) mslot[(size_t)2 * MSH * ((k3 + 2) % 3) + tid] = 0ull;
     double pf_max = -__builtin_huge_val();
     if (pf && it > 0) {
         // s_it[o] = d (S_o 2^-SC + alpha (P_ss s_{it-1})[o] / M_s(it-1)) from the previous launch's
@@ -2688,13 +2670,12 @@ __device__ __forceinline__ void tr_a_body(const GDev* __restrict__ gs, int32_t n
             if (o < N) {
                 unsigned long long lo = 0ull, hi = 0ull;
                 for (int32_t b = 0; b < nb; ++b) {
-                    const unsigned long long v = PER ? ld_sc1((const unsigned long long*)rows + (size_t)b * N + o)
-                                                     : rows[(size_t)b * N + o];
+                    const unsigned long long v = rows[(size_t)b * N + o];
                     lo += v & 0xffffffffull;
                     hi += v >> 32;
                 }
                 const double sum = ((double)hi * 4294967296.0 + (double)lo) * iscale;
-                const double v = d * (sum + (PER ? ld_sc1((const double*)ssvp + o) : ssvp[o]));   // pagerank.py:122-124
+                const double v = d * (sum + ssvp[o]);   // pagerank.py:122-124
                 sp_l[o] = v;
                 su_l[o] = (double)u_o[o] * v;
                 pf_max = nmax(pf_max, v);
@@ -2717,8 +2698,8 @@ __device__ __forceinline__ void tr_a_body(const GDev* __restrict__ gs, int32_t n
         for (int32_t o = tid; o < NH; o += NT) su_l[o] = sug[o];
     __shared__ int s_ssv;   // the call-graph term chunks taken (G.ssv_pre)
     if (tid < WAVE) {
-        const double ms = wave_max(bits2d(PER ? ld_sc1((const unsigned long long*)Mcur + tid) : Mcur[tid]));
-        const double mr = wave_max(bits2d(PER ? ld_sc1((const unsigned long long*)Mcur + MSH + tid) : Mcur[MSH + tid]));
+        const double ms = wave_max(bits2d(Mcur[tid]));
+        const double mr = wave_max(bits2d(Mcur[MSH + tid]));
         if (tid == 0) {
             msh[0] = ms;
             msh[1] = mr;
@@ -2741,10 +2722,10 @@ __device__ __forceinline__ void tr_a_body(const GDev* __restrict__ gs, int32_t n
     const double xsc = (G.dscale ? G.dscale[0] : G.fx_scale) / msh[1], Ms = msh[0];
     const double rmax_w = tr_walk<Q, SUM, NT, EXT, HOTT>(G, lb, cur, nxt, N, NH, d, Ms, xsc, su_l, lacc, hs);
     // the call-graph terms of this block's share of the columns, by the waves done walking
-    if (G.ssv_pre) tr_ssv_share(G, lb, cur, Ms, &s_ssv, tid & (WAVE - 1), pf ? sp_l : nullptr, pf ? (int64_t)cur * N : 0, PER);
+    if (G.ssv_pre) tr_ssv_share(G, lb, cur, Ms, &s_ssv, tid & (WAVE - 1), pf ? sp_l : nullptr, pf ? (int64_t)cur * N : 0);
     __syncthreads();
     GLB unsigned long long* prow = gpw(G.fx_part) + (pf ? (size_t)cur * G.pf_stride : 0) + (size_t)lb * N;
-    if constexpr (NT == 512 && !PER) {   // (window-graph variant only: the large graphs' kernel stays as it is)
+    if constexpr (NT == 512) {   // (window-graph variant only: the large graphs' kernel stays as it is)
         if (G.lastfin) {
             for (int32_t o = tid; o < N; o += NT)   // write-through: the last block reads them with sc1 loads
                 __hip_atomic_store(prow + o, lacc[o], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2754,7 +2735,7 @@ __device__ __forceinline__ void tr_a_body(const GDev* __restrict__ gs, int32_t n
             return;
         }
     }
-    if (PER || G.row_wt)   // write-through (sc1): the boundary to k_fx_b has no dirty lines to write back
+    if (G.row_wt)   // write-through (sc1): the boundary to k_fx_b has no dirty lines to write back
         for (int32_t o = tid; o < N; o += NT)
             __hip_atomic_store(prow + o, lacc[o], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     else
@@ -2762,87 +2743,6 @@ __device__ __forceinline__ void tr_a_body(const GDev* __restrict__ gs, int32_t n
     const double rmax = block_max(rmax_w, red);
     if (tid == 0 && rmax >= 0.0)   // -inf: a block without traces (an empty shard's placeholder)
         atomicMax((unsigned long long*)&Mnext[MSH + blockIdx.x % MSH], d2bits(rmax));
-}
-template <class Q, int SUM, int NT, int EXT>
-__global__ void __launch_bounds__(NT, NT == 512 && EXT == 0 && SUM != WV_SU_HOT ? MR_TR_WPE512 : 1) k_tr_a(const GDev* __restrict__ gs, int32_t ng, int32_t split, double d,
-                                             double alpha, int it, int32_t unused) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char lraw[];
-    tr_a_body<Q, SUM, NT, EXT, false>(gs, ng, split, d, it, lraw);
-}
-
-// ---------------------------------------------------------------- persistent iteration (k_tr_p)
-// A launch of every iteration for a batch whose blocks fit one per CU (single windows: tens of
-// blocks; cooperative launch, the dynamic LDS past half a CU), the grid barrier between iterations
-// instead of a kernel boundary: iteration it is tr_a_body's pf form (the previous iteration
-// finished from the rows and terms in every block), its rows, terms and r' maxima handed to the
-// next through the hand-off table's row 1 of MI355X_MICROARCH.md in every cell -- write-through
-// (sc1) 8-B stores, each wave's vmcnt(0), a workgroup barrier, ONE lane per workgroup adding to ONE
-// unsharded agent counter, the consumer polling it with sc1 loads and its other waves behind a
-// workgroup barrier, sc1 loads of the bytes, hipMalloc'd memory, one workgroup per CU.  The spin
-// is bounded (`timeout` s_memrealtime ticks; then flag word 3 of every graph and an early exit of
-// every block -- no block waits on one that is not resident).  After the last iteration each block
-// finishes its share of the ops (k_fx_b's values) for the weights.  Bitwise the per-launch path.
-__device__ __forceinline__ bool tr_grid_sync(unsigned long long* bar, unsigned long long target, unsigned long long timeout,
-                                             int* s_ok) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave's write-through stores are out
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        GLB unsigned long long* b = gpw(bar);
-        __hip_atomic_fetch_add(b, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-        int ok = 1;
-        while (__hip_atomic_load(b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-            __builtin_amdgcn_s_sleep(1);
-            // (word 1: a block that timed out -- the others stop at once instead of waiting theirs)
-            if (__builtin_amdgcn_s_memrealtime() - t0 > timeout ||
-                __hip_atomic_load(b + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0ull) {
-                __hip_atomic_store(b + 1, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                ok = 0;
-                break;
-            }
-        }
-        *s_ok = ok;
-    }
-    __syncthreads();
-    return *s_ok != 0;
-}
-template <class Q>
-__global__ void __launch_bounds__(512, 1) k_tr_p(const GDev* __restrict__ gs, int32_t ng, int32_t split, double d,
-                                                 int iters, unsigned long long* bar, unsigned long long timeout) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char lraw[];
-    __shared__ int s_ok;
-    const unsigned long long nb = gridDim.x;
-    for (int it = 0; it < iters; ++it) {
-        tr_a_body<Q, WV_SU_ALL, 512, 0, true>(gs, ng, split, d, it, lraw);
-        if (!tr_grid_sync(bar, nb * (unsigned long long)(it + 1), timeout, &s_ok)) {
-            const GDev& G = gs[fx_graph(gs, ng, split, 2)];
-            if (threadIdx.x == 0) atomicOr(const_cast<int32_t*>(G.flag) + 3, 1);
-            return;
-        }
-    }
-    // the last iteration's finish for this block's share of the ops: s' into spb / sub and its
-    // maxima into the next slot (k_fx_b's mode-0 values)
-    const GDev& G = gs[fx_graph(gs, ng, split, 2)];
-    const int32_t lb = (int32_t)blockIdx.x - G.blk0f, N = G.N, nbg = G.n_fa;
-    const int pi = iters - 1, pb = pi & 1, nxt = pb ^ 1;
-    GLB unsigned long long* Mnext = gpw(G.mslot) + (size_t)2 * MSH * ((pi % 3 + 1) % 3);
-    const unsigned long long* rows = (const unsigned long long*)G.fx_part + (size_t)pb * G.pf_stride;
-    const double* ssvp = G.fx_ssv + (size_t)pb * N;
-    const double iscale = G.dscale ? G.dscale[1] : G.fx_iscale;
-    const int32_t oa = (int32_t)((int64_t)lb * N / nbg), ob = (int32_t)((int64_t)(lb + 1) * N / nbg);
-    for (int32_t o = oa + (int32_t)threadIdx.x; o < ob; o += 512) {
-        unsigned long long lo = 0ull, hi = 0ull;
-        for (int32_t b = 0; b < nbg; ++b) {
-            const unsigned long long v = ld_sc1(rows + (size_t)b * N + o);
-            lo += v & 0xffffffffull;
-            hi += v >> 32;
-        }
-        const double sum = ((double)hi * 4294967296.0 + (double)lo) * iscale;
-        const double v = d * (sum + ld_sc1(ssvp + o));   // pagerank.py:122-124
-        G.spb[nxt][o] = v;
-        G.sub[nxt][o] = (double)G.u_o[o] * v;
-        atomicMax((unsigned long long*)&Mnext[o % MSH], d2bits(v));
-    }
 }
 
 // Column sums of the partial rows: a block per chunk of FB_OPS consecutive ops (lane = op, so
@@ -4618,26 +4518,16 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         if (gs[i]->fused) wsum += gs[i]->n_wt;
     std::vector<CutArg> cuts;   // the graphs' per-wave cuts, launched together
     const std::vector<int64_t> nbs = batch_blocks(gs, ng, plan, wsum);
-    // ONE persistent launch for all iterations (k_tr_p) when every graph of the batch can be
-    // finished in the next iteration's prologue (plan.pf, <= PF_ROWS blocks each) and the whole
-    // launch fits one block per CU (single windows).  MR_TR_PERSIST=0 (read per call): a launch per
-    // iteration (A/B and tests)
-    const char* pse = getenv("MR_TR_PERSIST");
-    bool persist = !(pse && atoi(pse) == 0) && plan.pf && iters >= 1 && LF_ONE_CU_LDS > 0 && LF_ONE_CU_LDS <= WV_LDS_MAX;
-    int64_t persist_blocks = 0;
     for (int i = 0; i < ng; ++i) {
         mr_graph* g = gs[i];
         if (g->fused) {   // the plan's blocks: partial rows and (k_tr_a) the per-wave cut
             int64_t nfa = 0;
             MR_TRY(fused_blocks(ctx, g, plan, wsum, &nfa, &cuts, nbs.empty() ? 0 : nbs[(size_t)i]));
-            persist = persist && nfa >= 1 && nfa <= PF_ROWS;
-            persist_blocks += nfa;
             // (pf: rows and call-graph terms double-buffered, iteration it & 1)
             MR_TRY(g->fx_part.alloc(ctx, (size_t)(plan.pf ? 2 : 1) * std::max<int64_t>(nfa, 1) * (size_t)kern_n(g)));
             if (plan.pf) MR_TRY(g->fx_ssv.alloc(ctx, 2 * (size_t)g->N));
         }
     }
-    persist = persist && persist_blocks <= num_cus();
     hm.mark("blocks");
     for (size_t c0 = 0; c0 < cuts.size(); c0 += TC_BATCH) {
         CutBatch cb;
@@ -4775,7 +4665,7 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         // iteration); its sc1 row reads stay short: at most LASTFIN_WORDS row words
         // (ops <= threads: the finishing block takes every op in one round -- C3's 500-op windows;
         // C2's 1000-op windows measured -1.5 % with it, C3 +6.5 % windows/s, -7 % single window)
-        v.lastfin = !persist && lastfin_on && plan.NT == 512 && !sharded && g->fused && !g->wide && !g->relabeled &&
+        v.lastfin = lastfin_on && plan.NT == 512 && !sharded && g->fused && !g->wide && !g->relabeled &&
                     plan.mode == WV_SU_ALL && nfa >= 1 && g->N <= plan.NT && nfa * (int64_t)g->N <= LASTFIN_WORDS;
         v.n_fb = g->fused && !v.lastfin ? cdiv(g->N, v.fb_ops) : 0;
         // the call-graph terms in k_tr_a (large graphs: k_fx_b's chains of dependent loads leave its
@@ -4783,7 +4673,7 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         // block writes its share write-through and the last block reads the terms with one load per
         // op instead of the ss_off -> ss_par -> pw / s_k chain (MR_TR_LFSSV=0: the chain; read per call)
         v.ssv_pre = ssv_on && nfa >= 1 && !g->wide && ((v.n_fb > 0 && g->N >= 2048) || (v.lastfin && lfssv_on));
-        v.pf = persist || (plan.pf && !v.lastfin && nfa <= PF_ROWS);
+        v.pf = plan.pf && !v.lastfin && nfa <= PF_ROWS;
         v.pf_stride = nfa * (int64_t)kern_n(g);
         if (v.pf) v.ssv_pre = 1;   // (the next launch's prologue reads the terms: one load per op)
         v.row_wt = row_wt_on && g->N >= 2048;
@@ -4811,7 +4701,7 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         // finishing blocks skip the acquire (tr_last_finish); else they take it
         bool any_lf = false;
         for (int i = 0; i < ng; ++i) any_lf = any_lf || hv[(size_t)i].lastfin;
-        const bool one_cu = persist || (LF_ONE_CU_LDS > 0 && any_lf && blocks_fa <= num_cus() && LF_ONE_CU_LDS <= WV_LDS_MAX);
+        const bool one_cu = LF_ONE_CU_LDS > 0 && any_lf && blocks_fa <= num_cus() && LF_ONE_CU_LDS <= WV_LDS_MAX;
         if (one_cu) lds_f = std::max(lds_f, LF_ONE_CU_LDS);
         for (int i = 0; i < ng; ++i) hv[(size_t)i].lf_acq = one_cu ? 0 : 1;
     }
@@ -4830,7 +4720,6 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
     bool launch_pf = plan.pf;   // every graph finishes in-kernel: no k_fx_b before the last iteration
     for (int i = 0; i < ng; ++i) launch_pf = launch_pf && (hv[(size_t)i].lastfin || hv[(size_t)i].pf);
     launch_pf = launch_pf && any_ext == 0;
-    if (persist && !launch_pf) return mr_fail(ctx, MR_ERR_STATE, "pagerank batch: persistent launch without pf graphs");
     if (!launch_pf)
         for (int i = 0; i < ng; ++i) {
             if (hv[(size_t)i].pf) hv[(size_t)i].ssv_pre = ssv_on && !gs[i]->wide && gs[i]->N >= 2048;
@@ -4878,34 +4767,7 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         }
     }
     hm.mark("pre-loop");
-    DBuf<unsigned long long> pbar;   // (persistent launch) grid barrier counter, timeout word
-    if (persist) {
-        MR_TRY(pbar.zero(ctx, 2));
-        const GDev* dvp = dv.p;
-        int32_t ngv = ng, splv = split_fa;
-        double dv_ = d;
-        int itv = iters;
-        unsigned long long* barp = pbar.p;
-        unsigned long long tmo = 200ull * 100000ull;   // 200 ms of s_memrealtime (100 MHz)
-        void* args[] = {(void*)&dvp, (void*)&ngv, (void*)&splv, (void*)&dv_, (void*)&itv, (void*)&barp, (void*)&tmo};
-        const void* kp = fp32 ? (const void*)k_tr_p<float> : (const void*)k_tr_p<double>;
-        (void)hipFuncSetAttribute(kp, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_f);
-        mr_prof_begin(ctx);
-        const hipError_t ce = hipLaunchCooperativeKernel(kp, dim3((unsigned)blocks_fa), dim3(512), args, (unsigned)lds_f, st);
-        if (ce == hipSuccess) {
-            mr_prof_end(ctx, bytes * (double)iters, iters);
-            MR_DEBUG_CHECK(ctx, "k_tr_p");
-        } else {   // (not admitted: a launch per iteration, the same pf graphs)
-            (void)hipGetLastError();
-            mr_prof_end(ctx, 0.0, 0);
-            persist = false;
-            static std::atomic<bool> said{false};
-            if (!said.exchange(true))
-                fprintf(stderr, "[microrank] persistent iteration launch not admitted (%s, %lld blocks, %zu B LDS): a launch per iteration\n",
-                        hipGetErrorString(ce), (long long)blocks_fa, lds_f);
-        }
-    }
-    for (int it = 0; it < iters && !persist; ++it) {
+    for (int it = 0; it < iters; ++it) {
         mr_prof_begin(ctx);
         if (any_wide && sst != st) {
             MR_TRY_HIP(ctx, hipEventRecord(ctx->side_ev[0], st));   // this iteration's su and q are ready
@@ -5024,7 +4886,6 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
             return MR_OK;
         }
         if (hflag[(size_t)4 * i + 2] & 1) return mr_fail(ctx, MR_ERR_STATE, "trace kinds: a partition exceeded its table");
-        if (hflag[(size_t)4 * i + 3] & 1) return mr_fail(ctx, MR_ERR_STATE, "persistent iteration: grid barrier timed out");
         if (anomaly[i] && (hflag[(size_t)4 * i + 1] & 1)) return mr_fail(ctx, MR_ERR_ZERODIV, "float division by zero");
     }
     return MR_OK;
@@ -5437,7 +5298,6 @@ int mr_pagerank_async_finish(mr_ctx* ctx, PrAsync* a, bool* rerun) {
             return MR_OK;
         }
         if (w[2] & 1) return mr_fail(ctx, MR_ERR_STATE, "trace kinds: a partition exceeded its table");
-        if (w[3] & 1) return mr_fail(ctx, MR_ERR_STATE, "persistent iteration: grid barrier timed out");
         if (a->anomaly[(size_t)i] && (w[1] & 1)) return mr_fail(ctx, MR_ERR_ZERODIV, "float division by zero");
     }
     return MR_OK;

@@ -959,49 +959,6 @@ def test_windows_batch_layout_order_equals_general_build(c3_window, monkeypatch)
         d.close()
 
 
-def test_single_window_persistent_launch_bitwise(c3_window, monkeypatch):
-    """One C3-shaped window per call runs its 25 iterations as ONE persistent launch (k_tr_p: a
-    grid barrier between iterations, every graph finished in the next iteration's prologue) -- it
-    ranks bitwise as a launch per iteration with the graphs' last blocks finishing them
-    (MR_TR_PERSIST=0: one block per CU, no acquire), with the next launch's prologue finishing them
-    (MR_TR_LASTFIN=0), with k_fx_b every iteration (MR_TR_PF=0 too), and inside a call of 16 windows
-    (last-block finish behind the agent acquire: several blocks per CU): the same exact limb sums
-    and expressions everywhere, and the window graphs' fixed-point scale does not depend on the
-    block cut."""
-    import bench
-    from microrank_amd import _lib
-    from microrank_amd.online_rca import rank_windows
-    from microrank_amd.preprocess_data import DeviceSpans
-
-    ctx = _lib.default_context()
-    normal, abnormal, t0, t1 = c3_window
-    a3, ok = bench.slo_from_gpu(ctx, normal)
-    dev = DeviceSpans(ctx, abnormal)
-    win = (dev, t0, t1, a3, ok)
-    runs = {}
-    for name, env in (("persist", {}), ("lastfin", {"MR_TR_PERSIST": "0"}),
-                      ("pf", {"MR_TR_PERSIST": "0", "MR_TR_LASTFIN": "0"}),
-                      ("k_fx_b", {"MR_TR_PERSIST": "0", "MR_TR_PF": "0", "MR_TR_LASTFIN": "0"})):
-        for k in ("MR_TR_PERSIST", "MR_TR_PF", "MR_TR_LASTFIN"):
-            monkeypatch.delenv(k, raising=False)
-        for k, v in env.items():
-            monkeypatch.setenv(k, v)
-        runs[name] = rank_windows(ctx, [win])[0]
-        runs[name + "_fp32"] = rank_windows(ctx, [win], precision="fp32")[0]
-    for k in ("MR_TR_PERSIST", "MR_TR_PF", "MR_TR_LASTFIN"):
-        monkeypatch.delenv(k, raising=False)
-    batch = rank_windows(ctx, [win] * 16)
-    runs["batch"] = batch[0]
-    assert all(b[1].tobytes() == batch[0][1].tobytes() for b in batch)
-    base = runs["persist"]
-    assert base[5] == 0 and len(base[0]) == 11
-    for name, got in runs.items():
-        ref = runs["persist_fp32"] if name.endswith("_fp32") else base
-        assert got[5] == 0 and got[2:] == ref[2:] and list(got[0]) == list(ref[0]), name
-        assert got[1].tobytes() == ref[1].tobytes(), name
-    dev.close()
-
-
 def test_layout_index_failure_keeps_general_path(c3_window, monkeypatch):
     """The layout order is a best-effort fast path of the span index: a failure inside it
     (MR_LO_TEST_FAIL: an error after an allocation, read per table) leaves the upload successful,
