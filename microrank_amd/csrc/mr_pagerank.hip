@@ -4741,7 +4741,11 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
     // (a large graph alone -- C4: 256 rows of 10k ops -- sums faster with 16-wave blocks: 137 -> 134 us)
     for (int i = 0; i < ng; ++i) fb_small = fb_small && hv[(size_t)i].n_fa <= FB_SMALL_ROWS && hv[(size_t)i].N <= 4096;
     hipStream_t sst = st;
+#ifdef MR_AB_WIDE_SERIAL   // (A/B builds: k_cold_ops on the main stream)
+    if (false) {
+#else
     if (any_wide) {
+#endif
         if (!ctx->side) {
             MR_TRY_HIP(ctx, hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
             for (hipEvent_t& e : ctx->side_ev) MR_TRY_HIP(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
