@@ -304,6 +304,7 @@ struct mr_graph {
     DBuf<unsigned long long> mslot;  // [6] bits of (M_s, M_r) for iterations k%3
     DBuf<double> spb[2];         // [N] unnormalised s' (double-buffered)
     DBuf<double> sub[2];         // [N] u_o * s'[o]
+    DBuf<float> suf[2];          // fp32 wide graphs: the same, as floats (k_tr_a's warm gathers)
     DBuf<double> sn;             // [N] final normalised s
     DBuf<double> scal;           // [8] M_s, M_r, sums
     DBuf<double> ppart;          // preference-sum block partials

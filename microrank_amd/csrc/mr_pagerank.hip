@@ -24,6 +24,7 @@
 #include <cstring>
 #include <memory>
 #include <queue>
+#include <type_traits>
 
 #include "mr_internal.h"
 #include "mr_prim.h"
@@ -622,6 +623,10 @@ __global__ void k_tr_fill(const int32_t* tperm, const int64_t* off, const uint16
 #define MR_TR_TIERS512 4   // short-tile tiers of the 512-thread k_tr_a (window graphs: occupancy)
 #endif
 constexpr int TR_TIERS_EXT = 8;   // short-tile tiers of the EXT (kind-compressed / wide) variants
+#ifndef MR_TR_TIERS_W32
+#define MR_TR_TIERS_W32 5   // ... of the fp32 wide variant (EXT & 8: its pipelined cold registers; 6 spilled)
+#endif
+constexpr int TR_TIERS_W32 = MR_TR_TIERS_W32;
 #ifndef MR_HOT_MAX
 #define MR_HOT_MAX 8
 #endif
@@ -1705,7 +1710,8 @@ __global__ void k_iter_init(const float* w_t, const double* mw, const float* u_o
 __global__ void k_pr_reset_init(int32_t T, int64_t cap, int32_t N, float* pref, float* c_t, unsigned long long* hk,
                                 KCnt* cr, int32_t* flag, double* scal, const float* w_t, const double* mw,
                                 const float* u_o, int64_t T_all, double* sp0, double* su0, double* su1, double* q64,
-                                float* q32, int fp32, unsigned long long* mslot, const int32_t* perm) {
+                                float* q32, int fp32, unsigned long long* mslot, const int32_t* perm, int su32,
+                                float* suf0, float* suf1) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < T) {
         pref[i] = 0.0f;
@@ -1720,9 +1726,12 @@ __global__ void k_pr_reset_init(int32_t T, int64_t cap, int32_t N, float* pref, 
     const double v0 = 1.0 / (double)((int64_t)N + T_all);      // pagerank.py:118-119
     if (i < N) {
         sp0[i] = v0;
-        su0[i] = (double)u_o[perm ? perm[i] : i] * v0;
+        const double su = (double)u_o[perm ? perm[i] : i] * v0;
+        su0[i] = su32 ? (double)(float)su : su;   // (fp32 wide graphs: k_tr_a's float copies are exact)
+        if (su32) suf0[i] = (float)su;
     }
     if (i >= N && i < N + TR_PAD) su0[i] = su1[i] = 0.0;
+    if (su32 && i >= N && i < N + TR_PAD) suf0[i] = suf1[i] = 0.0f;
     if (i < T) {
         const double q = (mw ? mw[i] : (double)w_t[i]) * v0;
         if (fp32) q32[i] = (float)q; else q64[i] = q;
@@ -1767,6 +1776,7 @@ struct GDev {
     const int32_t* ss_par;
     void* q[2];
     double* sub[2];
+    float* suf[2];                 // su32 graphs: the same su as floats (k_tr_a EXT & 8 gathers these)
     double* spb[2];
     double* part;
     unsigned long long* mslot;
@@ -1782,6 +1792,8 @@ struct GDev {
     // wide fused graphs: k_tr_a's ops [0, NA) (NA = N otherwise); ops [NA, N) in ranges of
     // cold_rw ops whose rows (cold_part, blocks cold_rowbase[r] .. [r+1]) carry scale cx_scale
     int32_t NA, cold_rw;
+    int32_t ns_warm;               // k_tr_a EXT & 8: labels [NA, ns_warm) have their su in LDS (else NA)
+    int32_t su32;                  // fp32 wide graphs: su rounded to float where k_fx_b makes it
     const double* cold_acc;        // [T] per position: the cold half of the trace's su sum
     const unsigned long long* cold_part;
     const int32_t* cold_rowbase;
@@ -2062,17 +2074,26 @@ struct TrLds {
     // the accumulator first, then su (8-B strides: a 32-lane read group spreads over 32 bank
     // pairs, a 16-lane atomic group over 16)
     // pf (every op's su in LDS only): s itself beside su (the launch finished the previous iteration)
-    __host__ __device__ TrLds(int32_t N, int mode, bool pf = false) {
+    // w32 (fp32 wide graphs, k_tr_a EXT & 8): su as 4-B floats -- the hot ops, their 64 pad slots,
+    // then n_warm "warm" cold labels (NA + j at slot NA + 64 + j) in the space the floats free
+    int32_t n_warm;
+    __host__ __device__ TrLds(int32_t N, int mode, bool pf = false, bool w32 = false) {
         const size_t ns = (size_t)N + TR_PAD;
         su_lds = ns * 16 <= WV_LDS_MAX;
         const bool all = mode == WV_SU_ALL && su_lds;
         const size_t accb = (ns * 8 + 15) / 16 * 16;
         n_hot = 0;
+        n_warm = 0;
         if (mode == WV_SU_HOT && accb < WV_LDS_MAX)
             n_hot = (int32_t)std::min<size_t>((size_t)N, (WV_LDS_MAX - accb) / 8 / 64 * 64);
         lacc = 0;
         su = accb;
         total = all ? 2 * accb : accb + (size_t)n_hot * 8;
+        if (all && w32 && !pf) {   // (the hot-op mask sums keep their 2 KB)
+            const size_t fl = (WV_LDS_MAX - accb - 256 * 8 - 16) / 4;
+            n_warm = fl > ns ? (int32_t)((fl - ns) / 64 * 64) : 0;
+            total = accb + ((ns + (size_t)n_warm) * 4 + 15) / 16 * 16;
+        }
         sp = total;
         if (pf && all) total += accb;
         hs = total;
@@ -2097,6 +2118,10 @@ __device__ __forceinline__ double uni_d(double v) {   // a block-uniform double 
 // by length, so a wave's run is a sequence of short-tile tiers (NC = 1, 2, .., 8, each a code copy
 // with every count static) and a suffix of longer tiles the general loop takes.  Same per-lane sums
 // in the same order as the general loop: bitwise equal results.
+// su in k_tr_a's LDS: doubles, or 4-B floats on fp32 wide graphs (EXT & 8: every su value of such
+// a graph is rounded to float where it is made, so the float copy is exact)
+template <class Q, int EXT>
+using TrSu = std::conditional_t<((EXT & 8) != 0) && std::is_same<Q, float>::value, float, double>;
 template <class Q, int NC, int EXT>
 struct TrTile {
     u32x2 id[NC];
@@ -2111,6 +2136,9 @@ struct TrTile {
     uint32_t hm;   // the trace's hot-op bits (nhr > 0)
     uint32_t rl;   // the run of identical traces this lane heads (0: another lane's run; 1: its own)
     uint32_t rln;  // the next tile's rl (a tail loads nothing of its own: its loads need it a tile ahead)
+    u32x2 cidn[2]; // EXT & 8: the NEXT tile's first two cold chunks (its gathers go out a tile early)
+    float cf[4];   // EXT & 8: this tile's non-warm cold su, gathered while the previous tile walked
+    float xw;      // EXT & 8: this tile's warm cold su (LDS), summed at the previous tile's end
 };
 // the hot ops of a trace: their su first in the lane's sum (the same order in both walks), X into
 // the lane's register accumulators (integers: order-free; flushed once per walk)
@@ -2136,7 +2164,8 @@ __device__ __forceinline__ double tr_hot_init(TrHot<HN>& H, uint32_t hm, unsigne
     return H.hs[hm];
 }
 // hs[m] for m = tid < 256 (su of every op in LDS; the caller synchronises before and after)
-__device__ __forceinline__ void tr_hot_sums(const GDev& G, const double* su_l, double* hs, int32_t tid) {
+template <class SU>
+__device__ __forceinline__ void tr_hot_sums(const GDev& G, const SU* su_l, double* hs, int32_t tid) {
     if (tid < 256) {
         double a = 0.0;
         for (int h = 0; h < G.nhr; ++h)
@@ -2146,7 +2175,7 @@ __device__ __forceinline__ void tr_hot_sums(const GDev& G, const double* su_l, d
 }
 template <class Q, int NC, int EXT, int HN>
 __device__ __forceinline__ int32_t tr_walk_short(const GDev& G, int32_t k, const int32_t ke, int32_t T, int32_t lane,
-                                                 int cur, int nxt, double d, double Ms, double xsc, const double* su_l,
+                                                 int cur, int nxt, double d, double Ms, double xsc, const TrSu<Q, EXT>* su_l,
                                                  unsigned long long* lacc, double& rmax, TrHot<HN>& H, int32_t& c0,
                                                  int32_t& n, int32_t& q0, int32_t& nq) {
     const GLB int32_t* coff = gp(G.coff);
@@ -2165,6 +2194,13 @@ __device__ __forceinline__ int32_t tr_walk_short(const GDev& G, int32_t k, const
     const GLB int32_t* ccoff = cx ? gp(G.ccoff) : coff;
     const int32_t ccl = max(__builtin_amdgcn_readfirstlane(ccoff[ke]) - 1, 0);
     const uint32_t cpad = (uint32_t)(G.N + lane);
+    // EXT & 8: cold labels below ns_warm ("warm") read their su from LDS slot label + TR_PAD; the
+    // other labels from global memory.  Both reads issue for every slot: the LDS one of a non-warm
+    // label reads the lane's zero pad slot NA + lane, the global one of a warm label the lane's zero
+    // pad N + lane (one coalesced line per wave) -- the sum of the two is the label's su exactly
+    constexpr bool W32 = (EXT & 8) != 0;
+    const uint32_t nsw = W32 ? (uint32_t)G.ns_warm : 0u, lzero = W32 ? (uint32_t)(G.NA + lane) : 0u;
+    const GLB float* sugf = W32 ? gp((const float*)G.suf[cur]) : nullptr;
     const bool hot = H.n > 0;
     const GLB uint8_t* hmk = hot ? gp(G.hmask) : (const GLB uint8_t*)coff;
     // EXT & 4: run-merged graphs (trun).  Without it the run logic is compiled out: every lane walks
@@ -2195,7 +2231,7 @@ __device__ __forceinline__ int32_t tr_walk_short(const GDev& G, int32_t k, const
     // comes by shuffle -- so its loads go to one shared word each (one cache line per load, not
     // its own): unconditional loads, no branch
     const GLB u32x2* idb = gp((const u32x2*)G.tids);
-    auto load = [&](R& r, int32_t kk, int32_t cc0, int32_t qq0, int32_t nqq, uint32_t rl) {
+    auto load = [&](R& r, int32_t kk, int32_t cc0, int32_t qq0, int32_t nqq, uint32_t rl, int32_t qn1 = 0) {
         const int32_t kq = min(kk, ke - 1);
         const int32_t p = min(kq * WAVE + lane, T - 1);
         const bool hd = !RUNS || rl != 0u;
@@ -2208,8 +2244,13 @@ __device__ __forceinline__ int32_t tr_walk_short(const GDev& G, int32_t k, const
         if constexpr ((EXT & 1) != 0) r.mw = mw_tp[kc ? p : 0];
         if constexpr ((EXT & 2) != 0) {
             if (cx) {   // (uniform; ctids exists only on wide graphs)
-                r.cid[0] = cids[(size_t)min(qq0, ccl) * WAVE];
-                r.cid[1] = cids[(size_t)min(qq0 + 1, ccl) * WAVE];
+                if constexpr (W32) {   // tile kk + 1's labels (its first cold chunk qn1)
+                    r.cidn[0] = cids[(size_t)min(qn1, ccl) * WAVE];
+                    r.cidn[1] = cids[(size_t)min(qn1 + 1, ccl) * WAVE];
+                } else {
+                    r.cid[0] = cids[(size_t)min(qq0, ccl) * WAVE];
+                    r.cid[1] = cids[(size_t)min(qq0 + 1, ccl) * WAVE];
+                }
             }
             r.xo = cacc[nqq > 2 ? p : 0];   // (unconditional: a branch here costs ~50 VGPRs)
             r.ccw = ccoff[min(kq + 1 + lane, ke)];
@@ -2220,16 +2261,48 @@ __device__ __forceinline__ int32_t tr_walk_short(const GDev& G, int32_t k, const
         r.rln = rl_of(kk + 1);
     };
     // tile kk from r: lane = position kk * 64 + lane
-    auto run = [&](const R& r, int32_t kk, int32_t qq0, int32_t nqq) {
+    // EXT & 8: a tile's cold labels (l4: pads past its cold chunk count), their non-warm su gathered
+    // into dst.cf (global; warm labels read the lane's zero pad) and their warm su summed into
+    // dst.xw (LDS; non-warm labels read the lane's zero pad slot)
+    auto labels = [&](const u32x2 (&cid)[2], int32_t nqq, uint32_t (&l4)[4]) {
+        l4[0] = nqq > 0 ? cid[0].x : cpad;
+        l4[1] = nqq > 0 ? cid[0].y : cpad;
+        l4[2] = nqq > 1 ? cid[1].x : cpad;
+        l4[3] = nqq > 1 ? cid[1].y : cpad;
+    };
+    auto gissue = [&](R& dst, const u32x2 (&cid)[2], int32_t nqq) {
+        uint32_t l4[4];
+        labels(cid, nqq, l4);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dst.cf[i] = sugf[l4[i] < nsw ? cpad : l4[i]];
+    };
+    auto wsum = [&](R& dst, const u32x2 (&cid)[2], int32_t nqq) {
+        uint32_t l4[4];
+        labels(cid, nqq, l4);
+        float a = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a += (float)su_l[l4[i] < nsw ? l4[i] + (uint32_t)TR_PAD : lzero];
+        dst.xw = a;
+    };
+    // W32: nx = the next tile's register set (its gathers issued here from r.cidn, its warm sum at
+    // the end), nqn = the next tile's cold chunk count
+    auto run = [&](const R& r, int32_t kk, int32_t qq0, int32_t nqq, R* nx = nullptr, int32_t nqn = 0) {
         const int32_t p = kk * WAVE + lane;
         const bool own = p < T;
         double cg[4] = {0.0, 0.0, 0.0, 0.0};
-        if constexpr ((EXT & 2) != 0)
+        if constexpr (W32)
+            if (cx) gissue(*nx, r.cidn, nqn);
+        if constexpr ((EXT & 2) != 0 && !W32)
             if (cx) {   // the first two cold chunks' su (pads past the tile's chunk count: N + lane, 0)
-                cg[0] = sug[nqq > 0 ? r.cid[0].x : cpad];
-                cg[1] = sug[nqq > 0 ? r.cid[0].y : cpad];
-                cg[2] = sug[nqq > 1 ? r.cid[1].x : cpad];
-                cg[3] = sug[nqq > 1 ? r.cid[1].y : cpad];
+#ifdef MR_AB_NOGATHER   // (A/B timing builds only: every gather at the lane's pad -- wrong sums)
+                const uint32_t z = (r.cid[0].x ^ r.cid[1].y) & 0u;
+                cg[0] = sug[cpad + z]; cg[1] = sug[cpad + z]; cg[2] = sug[cpad + z]; cg[3] = sug[cpad + z];
+#else
+                const uint32_t l4[4] = {nqq > 0 ? r.cid[0].x : cpad, nqq > 0 ? r.cid[0].y : cpad,
+                                        nqq > 1 ? r.cid[1].x : cpad, nqq > 1 ? r.cid[1].y : cpad};
+#pragma unroll
+                for (int i = 0; i < 4; ++i) cg[i] = sug[l4[i]];
+#endif
             }
         // a run of rl identical traces (the same ops in the same order, the same q, c and w: the
         // same sum and r') is walked by its head alone: its X times rl into the accumulators (integers:
@@ -2263,7 +2336,11 @@ __device__ __forceinline__ int32_t tr_walk_short(const GDev& G, int32_t k, const
         if constexpr ((EXT & 2) != 0)
             if (cx) {
 #pragma unroll
-                for (int i = 0; i < 4; ++i) x += cg[i];
+                for (int i = 0; i < 4; ++i) x += W32 ? (double)r.cf[i] : cg[i];
+                if constexpr (W32) {
+                    x += (double)r.xw;   // (the warm part after the global one: a fixed order)
+                    wsum(*nx, r.cidn, nqn);   // the next tile's warm sum (its labels still in r)
+                }
                 if (nqq > 2) x = r.xo;   // (rare: > 4 cold entries in a trace of the tile: k_cold_trace's sum)
             }
         double rp = d * ((acc + x) / Ms) + (double)r.c;   // pagerank.py:125
@@ -2276,6 +2353,48 @@ __device__ __forceinline__ int32_t tr_walk_short(const GDev& G, int32_t k, const
         qn[own && hd ? p : T] = (Q)(wq * rp);   // q[T]: pad slot (a run's tails never read theirs)
     };
     R A, B;
+    if constexpr (W32) {
+        // the tier's first tile: its cold labels and gathers here (later tiles' go out a tile early),
+        // the next tile's cold range from lanes 1 and 2 of the cold offsets
+        const int32_t u3 = ccoff[min(k + lane, ke)];
+        const int32_t q1 = __builtin_amdgcn_readlane(u3, 1), nq1 = __builtin_amdgcn_readlane(u3, 2) - q1;
+        u32x2 c0v[2];
+        c0v[0] = cids[(size_t)min(q0, ccl) * WAVE];
+        c0v[1] = cids[(size_t)min(q0 + 1, ccl) * WAVE];
+        if (cx) {
+            gissue(A, c0v, nq);
+            wsum(A, c0v, nq);
+        }
+        load(A, k, c0, q0, nq, rl_of(k), q1);
+        int32_t nqA1 = nq1;   // tile k + 1's cold chunk count
+        for (;;) {
+            const int32_t c0B = __builtin_amdgcn_readfirstlane(A.cw);
+            const int32_t nB = __builtin_amdgcn_readlane(A.cw, 1) - c0B;
+            const int32_t qB = __builtin_amdgcn_readfirstlane(A.ccw);
+            const int32_t nqB = __builtin_amdgcn_readlane(A.ccw, 1) - qB;
+            const int32_t qB1 = __builtin_amdgcn_readlane(A.ccw, 1), nqB1 = __builtin_amdgcn_readlane(A.ccw, 2) - qB1;
+            load(B, k + 1, c0B, qB, nqB, A.rln, qB1);
+            run(A, k, q0, nq, &B, nqA1);
+            if (++k == ke || nB != NC) {
+                c0 = c0B, n = nB, q0 = qB, nq = nqB;
+                break;
+            }
+            const int32_t c0A = __builtin_amdgcn_readfirstlane(B.cw);
+            const int32_t nA2 = __builtin_amdgcn_readlane(B.cw, 1) - c0A;
+            const int32_t qA2 = __builtin_amdgcn_readfirstlane(B.ccw);
+            const int32_t nqA2 = __builtin_amdgcn_readlane(B.ccw, 1) - qA2;
+            const int32_t qA1 = __builtin_amdgcn_readlane(B.ccw, 1);
+            nqA1 = __builtin_amdgcn_readlane(B.ccw, 2) - qA1;
+            load(A, k + 1, c0A, qA2, nqA2, B.rln, qA1);
+            run(B, k, qB, nqB, &A, nqB1);
+            if (++k == ke || nA2 != NC) {
+                c0 = c0A, n = nA2, q0 = qA2, nq = nqA2;
+                break;
+            }
+            q0 = qA2, nq = nqA2;
+        }
+        return k;
+    }
     load(A, k, c0, q0, nq, rl_of(k));
     int32_t nA = n, qA = q0, nqA = nq;
     for (;;) {
@@ -2314,7 +2433,7 @@ __device__ __forceinline__ int32_t tr_walk_short(const GDev& G, int32_t k, const
 // and their next q.  Returns the wave's largest r' (-inf when it owns no trace).
 template <class Q, int SUM, int NT, int EXT = 0, bool HOTT = false>
 __device__ __forceinline__ double tr_walk(const GDev& G, int32_t lb, int cur, int nxt, int32_t N, int32_t NH, double d,
-                                          double Ms, double xsc, const double* su_l, unsigned long long* lacc,
+                                          double Ms, double xsc, const TrSu<Q, EXT>* su_l, unsigned long long* lacc,
                                           const double* hs = nullptr) {
     constexpr bool SUL = SUM == WV_SU_ALL, HOT = SUM == WV_SU_HOT;
     constexpr int NW = NT / WAVE;
@@ -2343,7 +2462,7 @@ __device__ __forceinline__ double tr_walk(const GDev& G, int32_t lb, int cur, in
         // one tier per chunk count (the run's tiles ascend in it): every count static, no branch
         // inside a tile, so each wait is for exactly the LDS reads and loads it consumes
         int32_t tc0 = 0, tn = -1, tq0 = 0, tnq = 0;   // the next tile's ranges, handed from tier to tier
-#define TR_TIER(NC_) if (NC_ <= (NT == 1024 || (EXT & 3) ? TR_TIERS_EXT : MR_TR_TIERS512) && k < ke) k = tr_walk_short<Q, NC_, EXT, HN>(G, k, ke, T, lane, cur, nxt, d, Ms, xsc, su_l, lacc, rmax, H, tc0, tn, tq0, tnq);
+#define TR_TIER(NC_) if (NC_ <= ((EXT & 8) ? TR_TIERS_W32 : NT == 1024 || (EXT & 3) ? TR_TIERS_EXT : MR_TR_TIERS512) && k < ke) k = tr_walk_short<Q, NC_, EXT, HN>(G, k, ke, T, lane, cur, nxt, d, Ms, xsc, su_l, lacc, rmax, H, tc0, tn, tq0, tnq);
         TR_TIER(1) TR_TIER(2) TR_TIER(3) TR_TIER(4) TR_TIER(5) TR_TIER(6) TR_TIER(7) TR_TIER(8)
 #undef TR_TIER
     }
@@ -2643,10 +2762,12 @@ __global__ void __launch_bounds__(NT, NT == 512 && EXT == 0 && SUM != WV_SU_HOT 
     // pf (window batches, 512-thread variant): k_fx_b's finish of the previous iteration runs here,
     // in every block of the graph (below), so an iteration is one launch
     const bool pf = NT == 512 && SUL && EXT == 0 && G.pf;
-    const TrLds L_(N, SUM, pf);
+    constexpr bool W32 = (EXT & 8) != 0;   // (fp32 wide graphs: float su, warm labels in LDS)
+    using SU = TrSu<Q, EXT>;
+    const TrLds L_(N, SUM, pf, W32);
     const int32_t NH = HOT ? G.n_hot : 0;   // <= L_.n_hot (the host sizes both alike), >= 64
     const GLB double* sug = gp(G.sub[cur]);   // ids >= N are pads (su 0)
-    double* su_l = (double*)(lraw + L_.su);
+    SU* su_l = (SU*)(lraw + L_.su);
     double* sp_l = (double*)(lraw + L_.sp);   // (pf) s_it itself, for the call-graph terms
     unsigned long long* lacc = (unsigned long long*)(lraw + L_.lacc);
     GLB unsigned long long* mslot = gpw(G.mslot);
@@ -2688,6 +2809,10 @@ __global__ void __launch_bounds__(NT, NT == 512 && EXT == 0 && SUM != WV_SU_HOT 
                 sp_l[o] = 0.0;
             }
         }
+    } else if (W32) {   // hot ops, 64 zero pads, then the warm labels N .. ns_warm - 1
+        const int32_t nw = G.ns_warm - N;
+        for (int32_t o = tid; o < N + TR_PAD + nw; o += NT)
+            su_l[o] = (SU)(o < N ? sug[o] : o < N + TR_PAD ? 0.0 : sug[o - TR_PAD]);
     } else if (SUL) {
         for (int32_t o = tid; o < N + TR_PAD; o += NT) su_l[o] = o < N ? sug[o] : 0.0;
         if (pf)
@@ -3014,7 +3139,14 @@ __global__ void __launch_bounds__(WAVE * FB_W) k_fx_b(const GDev* __restrict__ g
     const double sum = ((double)hi * 4294967296.0 + (double)lo) * (o < G.NA ? (G.dscale ? G.dscale[1] : G.fx_iscale) : G.cx_iscale);
     const double v = d * (sum + ssv);      // pagerank.py:122-124
     G.spb[nxt][op] = v;
-    G.sub[nxt][o] = (double)uo * v;   // su in the kernel's labels
+    const double su = (double)uo * v;
+    if (G.su32) {   // (fp32 wide graphs: rounded to float, kept both ways)
+        const float f = (float)su;
+        G.sub[nxt][o] = (double)f;
+        G.suf[nxt][o] = f;
+    } else {
+        G.sub[nxt][o] = su;   // su in the kernel's labels
+    }
     atomicMax(&Mnext[op % MSH], d2bits(v));
 }
 
@@ -3320,6 +3452,8 @@ static TrA tr_kernel(bool fp32, int mode, int NT, int ext = 0) {
         {{k_tr_a<double, 1, 512, 2>, k_tr_a<double, 1, 1024, 2>}, {k_tr_a<float, 1, 512, 2>, k_tr_a<float, 1, 1024, 2>}},
         {{k_tr_a<double, 1, 512, 3>, k_tr_a<double, 1, 1024, 3>}, {k_tr_a<float, 1, 512, 3>, k_tr_a<float, 1, 1024, 3>}},
         {{k_tr_a<double, 1, 512, 4>, k_tr_a<double, 1, 1024, 4>}, {k_tr_a<float, 1, 512, 4>, k_tr_a<float, 1, 1024, 4>}}};
+    // ext 10: fp32 wide graphs with float su and warm labels in LDS
+    if (ext == 10 && fp32 && mode == WV_SU_ALL) return NT == 1024 ? k_tr_a<float, 1, 1024, 10> : k_tr_a<float, 1, 512, 10>;
     // ext 4: run-merged window graphs (trun; never beside multiplicities or cold sums)
     if (ext == 4 && mode == WV_SU_ALL) return tab_ext[3][fp32 ? 1 : 0][NT == 1024 ? 1 : 0];
     if ((ext & 3) && mode == WV_SU_ALL) return tab_ext[(ext & 3) - 1][fp32 ? 1 : 0][NT == 1024 ? 1 : 0];
@@ -3344,6 +3478,7 @@ struct FxPlan {
     int mode = WV_SU_ALL;   // su in LDS for every fused graph of the batch / hot ops / none
     bool sul = true;    // mode == WV_SU_ALL
     bool pf = false;    // window batches: the next launch finishes an iteration (k_tr_a's pf prologue)
+    bool w32 = false;   // fp32 wide graphs only: float su and warm labels in LDS (k_tr_a EXT & 8)
 };
 static FxPlan fx_plan(mr_graph* const* gs, int ng) {
     FxPlan P;
@@ -3372,7 +3507,7 @@ static FxPlan fx_plan(mr_graph* const* gs, int ng) {
 static int32_t plan_n_hot(int32_t N, const FxPlan& P) {
     return P.mode == WV_SU_HOT ? TrLds(N, WV_SU_HOT).n_hot : 0;
 }
-static size_t plan_lds(int32_t N, const FxPlan& P) { return TrLds(N, P.mode, P.pf).total; }
+static size_t plan_lds(int32_t N, const FxPlan& P) { return TrLds(N, P.mode, P.pf, P.w32).total; }
 
 // resident blocks of the plan's kernel on the chip (occupancy by LDS image and VGPRs)
 static int64_t plan_resident(int32_t N, const FxPlan& P) {
@@ -3816,7 +3951,7 @@ static int wide_prepare(mr_ctx* ctx, mr_graph* g) {
         MR_TRY(ccnt.download(ctx, cn.data(), cn.size()));
         MR_TRY_HIP(ctx, hipStreamSynchronize(st));
         for (int32_t k = 0; k < W; ++k)
-            if (co[(size_t)k + 1] - co[(size_t)k] > TR_TIERS_EXT || cn[(size_t)k] > 2) tl.push_back(k);
+            if (co[(size_t)k + 1] - co[(size_t)k] > std::min(TR_TIERS_EXT, TR_TIERS_W32) || cn[(size_t)k] > 2) tl.push_back(k);
         g->n_ctl = (int32_t)tl.size();
         MR_TRY(g->ctl.alloc(ctx, std::max<size_t>(tl.size(), 1)));
         if (!tl.empty()) MR_TRY(g->ctl.upload(ctx, tl.data(), tl.size()));
@@ -4153,6 +4288,10 @@ static int pagerank_setup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool 
     MR_TRY(g->spb[1].alloc(ctx, (size_t)N));
     MR_TRY(g->sub[0].alloc(ctx, (size_t)N + TR_PAD));   // [N, N + TR_PAD) = 0: the fused walks' pad slots
     MR_TRY(g->sub[1].alloc(ctx, (size_t)N + TR_PAD));
+    if (fp32 && g->wide) {
+        MR_TRY(g->suf[0].alloc(ctx, (size_t)N + TR_PAD));
+        MR_TRY(g->suf[1].alloc(ctx, (size_t)N + TR_PAD));
+    }
     MR_TRY(g->weight.alloc(ctx, (size_t)N));
     const bool tr = g->fused;
     if (tr) MR_TRY(g->c_tp.alloc(ctx, (size_t)std::max(T, 1)));
@@ -4169,7 +4308,8 @@ static int pagerank_setup(mr_ctx* ctx, mr_graph* g, int anomaly, double d, bool 
                        dim3(256), 0, st, T, (int64_t)cap, N, g->pref.p, g->c_t.p, g->ht_key.p, g->ht_cr.p,
                        g->flag.p, g->scal.p, tr ? g->w_tp.p : g->w_t.p, tr ? g->mw_tp.p : nullptr, g->u_o.p,
                        g->T_all > 0 ? g->T_all : (int64_t)T, g->spb[0].p, g->sub[0].p, g->sub[1].p, g->q64[0].p,
-                       g->q32[0].p, (int)fp32, g->mslot.p, g->relabeled ? (const int32_t*)g->perm.p : nullptr);
+                       g->q32[0].p, (int)fp32, g->mslot.p, g->relabeled ? (const int32_t*)g->perm.p : nullptr,
+                       (int)(fp32 && g->wide), g->suf[0].p, g->suf[1].p);
     MR_DEBUG_CHECK(ctx, "k_pr_reset_init");
     // ---- kinds (a kind-compressed graph carries its class sizes: kinds_given)
     if (!g->kinds_given) MR_TRY(graph_kinds(ctx, g, chk, ktab, cap, seed, hmask));
@@ -4513,6 +4653,20 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
                       !(g->lo && g->lo_merged == 1);
         }
     }
+    {   // fp32 wide graphs: su as floats in k_tr_a's LDS, the freed half holding the next ~10k
+        // ("warm") labels' su, so their cold entries read LDS instead of L2 (k_tr_a EXT & 8);
+        // every fused graph of the launch wide and plain (no multiplicities)
+#ifndef MR_AB_NO_W32
+        plan.w32 = fp32 && plan.mode == WV_SU_ALL && !plan.pf;
+#endif
+        bool anyf = false;
+        for (int i = 0; i < ng && plan.w32; ++i)
+            if (gs[i]->fused) {
+                anyf = true;
+                plan.w32 = gs[i]->wide && !gs[i]->mw_tp.p && !gs[i]->trun.p;
+            }
+        plan.w32 = plan.w32 && anyf;
+    }
     int64_t wsum = 0;   // wave tiles of the launch's fused graphs (k_tr_a's block budget)
     for (int i = 0; i < ng; ++i)
         if (gs[i]->fused) wsum += gs[i]->n_wt;
@@ -4603,6 +4757,7 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         for (int j = 0; j < 2; ++j) {
             v.q[j] = fp32 ? (void*)g->q32[j].p : (void*)g->q64[j].p;
             v.sub[j] = g->sub[j].p;
+            v.suf[j] = g->suf[j].p;
             v.spb[j] = g->spb[j].p;
         }
         v.part = g->part.p;
@@ -4635,6 +4790,8 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
         v.N = g->N;
         v.NA = kern_n(g);
         v.cold_rw = g->cold_rw;
+        v.ns_warm = plan.w32 ? v.NA + std::min(TrLds(v.NA, WV_SU_ALL, false, true).n_warm, g->N - v.NA) : v.NA;
+        v.su32 = fp32 && g->wide;
         v.cold_acc = g->wide ? g->cold_acc.p : nullptr;
         v.cold_part = (const unsigned long long*)g->cold_part.p;
         v.cold_rowbase = g->cold_rowbase.p;
@@ -4725,7 +4882,7 @@ static int pagerank_attempt(mr_ctx* ctx, mr_graph* const* gs, const int* anomaly
             if (hv[(size_t)i].pf) hv[(size_t)i].ssv_pre = ssv_on && !gs[i]->wide && gs[i]->N >= 2048;
             hv[(size_t)i].pf = 0;
         }
-    const TrA tr_a = tr_kernel(fp32, plan.mode, plan.NT, any_ext);
+    const TrA tr_a = tr_kernel(fp32, plan.mode, plan.NT, any_ext == 2 && plan.w32 ? 10 : any_ext);
     DBuf<GDev> dv;
     hm.mark("descr");
     MR_TRY(dv.upload(ctx, hv.data(), hv.size()));
