@@ -213,7 +213,10 @@ __global__ void k_relabel_ids(const uint16_t* ids, int64_t n, const int32_t* inv
 // ids, su and accumulator in LDS); the other ("cold") entries of each trace are summed per
 // position by k_cold_trace and accumulated per op range by k_cold_ops (LDS accumulator of one
 // range, (position, op) pairs grouped by range, position order within a range).
-constexpr int32_t WIDE_NA = 10000;      // (WIDE_NA + TR_PAD) * 16 B + the hot-op sums <= k_tr_a's LDS
+#ifndef MR_WIDE_NA
+#define MR_WIDE_NA 10000
+#endif
+constexpr int32_t WIDE_NA = MR_WIDE_NA;   // (WIDE_NA + TR_PAD) * 16 B + the hot-op sums <= k_tr_a's LDS
 constexpr int32_t WIDE_RW_MAX = 19456;  // ops per cold range: k_cold_ops' accumulator <= 152 KB
 constexpr int WIDE_CB = 256;            // k_cold_ops blocks over all ranges (one per CU: LDS-bound)
 constexpr int WIDE_CT = 1024;           // k_cold_ops block size
@@ -1034,14 +1037,13 @@ __global__ void k_kind_rscatter(const KRec* rin, const int32_t* nrec, int32_t T,
 //   k_kp1_scatter the tile's records to their buckets through LDS cursors, each with its slot;
 //   k_kp2         a block per bucket: counts its fine partitions (the next pb - b1 bits) in LDS,
 //                 writes their starts, and scatters the bucket's records into partition order
-//                 inside the bucket's range, recording every slot's final position (rpos).
+//                 inside the bucket's range, each beside its block-order slot (eslot).
 // The order inside a partition depends on LDS atomics; k_kind_part's merge (sums, minimum) does
 // not: the same classes and representatives.
 constexpr int KP1_B = 8;    // coarse bits (1024 buckets over tiles of 16384 measured slower at C4: 584 vs 553 us)
 constexpr int KT = 4096;    // slots per level-1 tile
 constexpr int KT_T = 256;   // threads of a level-1 block
 constexpr int KP2_T = 1024;
-constexpr size_t KG_TWO_MAX = (size_t)1 << 25;   // record slots up to which the two-pass grouping runs
 __device__ __forceinline__ int32_t kbits(uint64_t h, int n) { return n ? (int32_t)(h >> (64 - n)) : 0; }
 // (the three loops take KP_BATCH records per thread per round: loads first, then the LDS atomics
 // and stores -- one round's loads in flight together instead of one dependent chain per record)
@@ -1100,7 +1102,7 @@ __global__ void __launch_bounds__(KT_T) k_kp1_scatter(const KRec* __restrict__ r
 }
 __global__ void __launch_bounds__(KP2_T) k_kp2(const KRec* __restrict__ in, const uint32_t* __restrict__ islot,
                                                const int64_t* __restrict__ off, int pb, int b1, int32_t ntile,
-                                               KRec* __restrict__ out, int32_t* __restrict__ rpos,
+                                               KRec* __restrict__ out, uint32_t* __restrict__ eslot,
                                                int64_t* __restrict__ pstart) {
     extern __shared__ int64_t kp2[];   // [KP2_T] scan partials, then [nf] 32-bit counts / cursors (from B0)
     const int nf = 1 << (pb - b1), b = (int)blockIdx.x, tid = (int)threadIdx.x;
@@ -1159,11 +1161,15 @@ __global__ void __launch_bounds__(KP2_T) k_kp2(const KRec* __restrict__ in, cons
             if (i0 + (int64_t)j * KP2_T >= B1) continue;
             const int64_t pos = B0 + (int64_t)atomicAdd(&cur[(uint64_t)kbits(v[j].h, pb) & fm], 1u);
             out[pos] = v[j];
-            rpos[sl[j]] = (int32_t)pos;
+            eslot[pos] = sl[j];   // (beside the record, in partition order: k_kind_part writes back through it)
         }
     }
 }
-__global__ void __launch_bounds__(KP_B) k_kind_part(const int64_t* pstart, KRec* e, int32_t* flag) {
+// eslot (two-pass grouping): each record's slot in the block-order records `back`, where the class
+// (count, first trace) is written -- k_kind_final then reads it at rec_of[t] (a block's own range)
+// instead of through a per-record position (a random read per trace); null: into e itself
+__global__ void __launch_bounds__(KP_B) k_kind_part(const int64_t* pstart, KRec* e, int32_t* flag,
+                                                    const uint32_t* eslot, KRec* back) {
     __shared__ unsigned long long tkey[KP_LDS];
     __shared__ uint32_t tcnt[KP_LDS];
     __shared__ int32_t trep[KP_LDS];
@@ -1214,7 +1220,7 @@ __global__ void __launch_bounds__(KP_B) k_kind_part(const int64_t* pstart, KRec*
             int s = (int)(h & (KP_LDS - 1));
             for (int probe = 0; probe < KP_LDS && tkey[s] != h; ++probe) s = (s + 1) & (KP_LDS - 1);
             if (tkey[s] != h) continue;   // (overflowed: flagged above)
-            *(uint2*)&e[i].c = make_uint2(tcnt[s], (uint32_t)trep[s]);   // (c, r): one 8-B store
+            *(uint2*)&(eslot ? back[eslot[i]] : e[i]).c = make_uint2(tcnt[s], (uint32_t)trep[s]);   // (c, r): one 8-B store
         }
     }
 }
@@ -1223,7 +1229,7 @@ __global__ void k_kind_final(const int32_t* rec_of, const int32_t* rpos, const K
                              const ID* ops, const float* w_t, int32_t T, double* kind, int32_t* flag, int32_t* krep) {
     const int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= T) return;
-    const int32_t pos = rpos[rec_of[t]];
+    const int32_t pos = rpos ? rpos[rec_of[t]] : rec_of[t];   // (null: e holds the classes in slot order)
     const uint2 cr = *(const uint2*)&e[pos].c;
     kind[t] = (double)cr.x;
     const int32_t r = (int32_t)cr.y;
@@ -4493,22 +4499,25 @@ static int graph_kinds(mr_ctx* ctx, mr_graph* g, bool chk, bool ktab, uint64_t c
         const size_t R = (size_t)nb * KB;
         DBuf<KRec> rec, e;
         DBuf<int32_t> nrec, rec_of, rpos, hist;
+        DBuf<uint32_t> eslot;
         DBuf<int64_t> pstart, tmp;
         DBuf<unsigned long long> cur;
         MR_TRY(rec.alloc(ctx, R));
-        MR_TRY(rpos.alloc(ctx, R));
         MR_TRY(e.alloc(ctx, (size_t)T));
         MR_TRY(nrec.alloc(ctx, (size_t)nb));
         MR_TRY(rec_of.alloc(ctx, (size_t)T));
         MR_TRY(pstart.alloc(ctx, (size_t)P + 1));
-        // The two-pass grouping (k_kp1_*, k_kp2) up to KG_TWO_MAX record slots, the per-record cursor
-        // scatter above it: the two-pass form ends in one random 4-B write per record (rpos), which
-        // the MALL absorbs at C4's 10M records (+4.3 % C4 GTEPS, profiles/r04q) but not at C5's 100M
-        // (93.6 vs 92.0 ms per step).  MR_KIND_GROUP (A/B, read per call): "two" / "cursor" forces one.
+        // The two-pass grouping (k_kp1_*, k_kp2; no device atomic per record) at every size: its
+        // records carry their block-order slot (eslot), k_kind_part writes each class back there and
+        // k_kind_final reads it in block order -- one random 8-B write per record, where the
+        // per-record cursor scatter (k_kind_rscatter: a returning atomic and a random 16-B write per
+        // record, then a random read per trace; 7.4 ms of C5's 100M records) took three.
+        // MR_KIND_GROUP=cursor (A/B, read per call) forces the cursor form.
         const char* kge = getenv("MR_KIND_GROUP");
-        const bool cursor = kge ? !strcmp(kge, "cursor") : R > KG_TWO_MAX;
+        const bool cursor = kge && !strcmp(kge, "cursor");
         auto krec = u16 ? k_kind_rec<2> : walk ? k_kind_rec<0> : k_kind_rec<4>;
         if (cursor) {
+            MR_TRY(rpos.alloc(ctx, R));
             MR_TRY(hist.zero(ctx, (size_t)P));
             MR_TRY(cur.alloc(ctx, (size_t)P));
             MR_TRY(tmp.alloc(ctx, (size_t)scan_tmp_elems(P)));
@@ -4538,16 +4547,21 @@ static int graph_kinds(mr_ctx* ctx, mr_graph* g, bool chk, bool ktab, uint64_t c
             hipLaunchKernelGGL(k_kp1_scatter, dim3(ntile), dim3(KT_T), 0, st, rec.p, nrec.p, (int64_t)R, b1, ntile,
                                toff.p, r1.p, s1.p);
             const size_t lds2 = (size_t)KP2_T * sizeof(int64_t) + (size_t)nf * sizeof(uint32_t);
-            hipLaunchKernelGGL(k_kp2, dim3(nbk), dim3(KP2_T), lds2, st, r1.p, s1.p, toff.p, pb, b1, ntile, e.p, rpos.p,
+            MR_TRY(eslot.alloc(ctx, (size_t)T));
+            hipLaunchKernelGGL(k_kp2, dim3(nbk), dim3(KP2_T), lds2, st, r1.p, s1.p, toff.p, pb, b1, ntile, e.p, eslot.p,
                                pstart.p);
             MR_TRY_HIP(ctx, hipStreamSynchronize(st));   // (the level-1 buffers leave scope)
         }
-        hipLaunchKernelGGL(k_kind_part, dim3((uint32_t)P), dim3(KP_B), 0, st, pstart.p, e.p, g->flag.p);
+        hipLaunchKernelGGL(k_kind_part, dim3((uint32_t)P), dim3(KP_B), 0, st, pstart.p, e.p, g->flag.p,
+                           cursor ? nullptr : eslot.p, rec.p);
+        // the classes: through rpos into e (cursor form) or in block order in rec (two-pass form)
+        const int32_t* rp = cursor ? rpos.p : nullptr;
+        const KRec* cls = cursor ? e.p : rec.p;
         if (u16)
-            hipLaunchKernelGGL(k_kind_final<uint16_t>, dim3(cdiv(T, 256)), dim3(256), 0, st, rec_of.p, rpos.p, e.p, koff,
+            hipLaunchKernelGGL(k_kind_final<uint16_t>, dim3(cdiv(T, 256)), dim3(256), 0, st, rec_of.p, rp, cls, koff,
                                (const uint16_t*)g->rs16.p, g->w_t.p, T, g->kind.p, g->flag.p, g->krep.p);
         else
-            hipLaunchKernelGGL(k_kind_final<int32_t>, dim3(cdiv(T, 256)), dim3(256), 0, st, rec_of.p, rpos.p, e.p, koff,
+            hipLaunchKernelGGL(k_kind_final<int32_t>, dim3(cdiv(T, 256)), dim3(256), 0, st, rec_of.p, rp, cls, koff,
                                kops, g->w_t.p, T, g->kind.p, g->flag.p, g->krep.p);
         MR_DEBUG_CHECK(ctx, "k_kind_part");
     }
