@@ -3658,6 +3658,9 @@ static std::vector<int64_t> batch_blocks(mr_graph* const* gs, int ng, const FxPl
         if (gs[i]->fused) R = std::min(R, plan_resident(kern_n(gs[i]), P));
     // (two or three blocks per resident slot measured 2-3 % faster per iteration inside the pipeline
     // and within the wall-time spread, profiles/r06/r06i_oversub_ab.txt: one set kept)
+#ifdef MR_AB_RFRAC   // (A/B builds: a fraction of the resident slots, leaving room for the builds' blocks)
+    R = std::max<int64_t>(1, (int64_t)((double)R * MR_AB_RFRAC));
+#endif
     const int64_t NW = P.NT / WAVE;
     nb.assign((size_t)ng, 0);
     std::vector<int64_t> cap((size_t)ng, 0);
