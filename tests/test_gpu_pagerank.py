@@ -123,9 +123,9 @@ def test_kinds_partition_and_table_paths(c2, part_min, monkeypatch):
     dg.pagerank(True)
     w2, _ = dg.fetch()
     assert w2.tobytes() == w.tobytes()
-    # the partition path's two ways of grouping records by partition (two passes of its bits, the
-    # default at this size; a device cursor per partition, the default past 32M records): the same
-    # classes and representatives
+    # the partition path's two ways of grouping records by partition (two passes of its bits with
+    # the classes written back to each record's slot, the default; a device cursor per partition,
+    # MR_KIND_GROUP=cursor): the same classes and representatives
     monkeypatch.setenv("MR_KIND_PART_MIN", "0")
     for grouping in ("two", "cursor"):
         monkeypatch.setenv("MR_KIND_GROUP", grouping)
