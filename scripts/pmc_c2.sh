@@ -1,6 +1,7 @@
 #!/bin/bash
 # PMC passes over the C2 window-group iteration kernel (one rocprofv3 run per counter group, <= 8 SQ
 # each): scripts/pmc_c2.sh TAG [kernel-pattern] [extra env assignments...]   (GPU box)
+#   BARGS: the bench arguments (default the C2 line on 16 distinct windows; C3: "--config c3 --steps 1 --warmup 1")
 TAG=${1:-c2}; PAT=${2:-k_tr_a}; shift 2
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
@@ -12,7 +13,7 @@ for ctr in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONF
            "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))
   timeout -s KILL 240 rocprofv3 --pmc $ctr -d gpurun_out/pmc_${TAG}_$i -o run --output-format csv -- \
-      python3 bench.py --c2-distinct 16 --steps 1 --warmup 1 --no-cpu --no-traffic --no-side \
+      python3 bench.py ${BARGS:---c2-distinct 16 --steps 1 --warmup 1} --no-cpu --no-traffic --no-side \
       > gpurun_out/pmc_${TAG}_$i.log 2>&1
   rc=$?
   echo "pass $i rc=$rc"
