@@ -698,6 +698,21 @@ static int win_aux(mr_ctx* ctx, int n) {
         // (the build streams at the PageRank stream's priority: a high-priority PageRank stream
         // measured C2 -4 % in round 4, low-priority build streams within the spread in round 6,
         // profiles/r06/r06h_serial_priority_ab.txt)
+#ifdef MR_AB_CUMASK   // (A/B builds: the build streams on the CUs with i % 4 < MR_AB_CUMASK only)
+        {
+            int ncu = 0;
+            if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device) == hipSuccess && ncu > 0) {
+                std::vector<uint32_t> m((size_t)(ncu + 31) / 32, 0u);
+                for (int i = 0; i < ncu; ++i)
+                    if (i % 4 < MR_AB_CUMASK) m[(size_t)i / 32] |= 1u << (i % 32);
+                hipStream_t s2 = nullptr;
+                if (hipExtStreamCreateWithCUMask(&s2, (uint32_t)m.size(), m.data()) == hipSuccess) {
+                    (void)hipStreamDestroy(a->stream);
+                    a->stream = s2;
+                }
+            }
+        }
+#endif
         ctx->aux.push_back(a);
     }
     return MR_OK;
