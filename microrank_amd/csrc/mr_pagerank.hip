@@ -3648,6 +3648,9 @@ static int tr_split(mr_ctx* ctx, mr_graph* g, const FxPlan& P, int64_t wsum, int
 // carry the most tiles.  (Rounding each graph's share UP put 1152 blocks on the 1024 resident slots
 // of a C2 group -- 128 windows' 13k- and 187k-trace graphs, 7.5 and 0.5 blocks of share each: a
 // second round of blocks behind the first.)  Empty: the single-graph rule of tr_split.
+#ifndef MR_TR_TPW
+#define MR_TR_TPW 2   // batch launches: at least this many wave tiles per wave of a graph's blocks
+#endif
 static std::vector<int64_t> batch_blocks(mr_graph* const* gs, int ng, const FxPlan& P, int64_t wsum) {
     std::vector<int64_t> nb;
     int nf = 0;
@@ -3668,7 +3671,7 @@ static std::vector<int64_t> batch_blocks(mr_graph* const* gs, int ng, const FxPl
     for (int i = 0; i < ng; ++i) {
         if (!gs[i]->fused) continue;
         const int64_t W = gs[i]->n_wt, lo = std::max<int64_t>(cdiv(W, 1023), 1);
-        cap[(size_t)i] = std::max<int64_t>(lo, cdiv(W, 2 * NW));
+        cap[(size_t)i] = std::max<int64_t>(lo, cdiv(W, (int64_t)MR_TR_TPW * NW));
         nb[(size_t)i] = std::min(cap[(size_t)i], std::max(lo, (int64_t)((double)R * (double)W / (double)wsum)));
         used += nb[(size_t)i];
     }
